@@ -1,0 +1,168 @@
+/*
+ * mythril_hip.h — C-ABI of libmythril_hip, the MI355X constraint sieve for Mythril's LASER engine.
+ *
+ * The sieve evaluates path-constraint "tapes" (flattened z3 QF_BV/Bool terms, see §Tape IR) against
+ * millions of candidate assignments resident in HBM and reports, per tape, the smallest satisfying
+ * assignment index (a witness) and/or the number of satisfying assignments.  It replaces, for the
+ * SAT-by-witness case only, the z3 round trip behind
+ *     mythril/support/model.py:15-62            get_model(constraints, minimize=(), maximize=(), ...)
+ *     mythril/laser/smt/model.py:45-59          Model.eval(expression, model_completion=True)
+ *     mythril/laser/smt/solver/solver.py:47-64  BaseSolver.check / BaseSolver.model
+ * (reference = terasum/mythril v0.22.9).  Every entry point below is what a Python ctypes binding in
+ * the reference would bind.  Conventions:
+ *   - C linkage, plain pointers and sizes, no exceptions cross the ABI, the library never aborts;
+ *   - every function returns int32: MH_OK (0) or a negative MH_E_* code; mh_last_error() gives text;
+ *   - the caller owns host buffers; the library owns device memory behind opaque handles;
+ *   - entry points are re-entrant per handle (one ctx per thread / per GPU).
+ */
+#ifndef MYTHRIL_HIP_H
+#define MYTHRIL_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MH_VERSION_MAJOR 0
+#define MH_VERSION_MINOR 1
+#define MH_VERSION_PATCH 0
+
+/* ---- error codes ------------------------------------------------------------------------------ */
+enum {
+    MH_OK = 0,
+    MH_E_INVALID = -1,      /* bad argument / malformed tape                                     */
+    MH_E_UNSUPPORTED = -2,  /* tape uses a feature the device path does not cover (fall back to z3) */
+    MH_E_DEVICE = -3,       /* HIP runtime error                                                 */
+    MH_E_NOMEM = -4,        /* host or device allocation failed                                  */
+    MH_E_NODEVICE = -5      /* no gfx950 device visible                                          */
+};
+
+/* ---- Tape IR ----------------------------------------------------------------------------------
+ * A tape is a topologically ordered list of nodes (each node's operands are earlier nodes of the
+ * same tape, by tape-local index); the last node is the root.  Sort: width == 0 means Bool, width
+ * in 1..512 means a bit-vector of that many bits.  Node semantics are SMT-LIB QF_BV (as z3's
+ * model_completion evaluator implements them), plus three EVM-word helpers (MH_OP_EVM_*) and the
+ * Keccak-256 hash.  The op -> reference-construction map is in DESIGN.md §Tape IR.             */
+enum mh_op {
+    MH_OP_CONST = 0,   /* imm0 = const-pool index                   (symbol_factory.BitVecVal)   */
+    MH_OP_VAR = 1,     /* imm0 = assignment column; low `width` bits (symbol_factory.BitVecSym)  */
+    MH_OP_TRUE = 2,    /* Bool true                                  (symbol_factory.Bool)       */
+    MH_OP_FALSE = 3,   /* Bool false                                                            */
+    MH_OP_BVADD = 10, MH_OP_BVSUB = 11, MH_OP_BVMUL = 12,
+    MH_OP_BVUDIV = 13, MH_OP_BVUREM = 14, MH_OP_BVSDIV = 15, MH_OP_BVSREM = 16, MH_OP_BVSMOD = 17,
+    MH_OP_BVNEG = 18, MH_OP_BVNOT = 19,
+    MH_OP_BVAND = 20, MH_OP_BVOR = 21, MH_OP_BVXOR = 22,
+    MH_OP_BVSHL = 23, MH_OP_BVLSHR = 24, MH_OP_BVASHR = 25,    /* a = value, b = shift amount    */
+    MH_OP_EQ = 30,                                               /* bv or Bool operands -> Bool   */
+    MH_OP_BVULT = 31, MH_OP_BVULE = 32, MH_OP_BVUGT = 33, MH_OP_BVUGE = 34,
+    MH_OP_BVSLT = 35, MH_OP_BVSLE = 36, MH_OP_BVSGT = 37, MH_OP_BVSGE = 38,
+    MH_OP_AND = 40, MH_OP_OR = 41, MH_OP_XOR = 42, MH_OP_NOT = 43,
+    MH_OP_ITE = 45,                                              /* a = Bool cond, b = then, c = else */
+    MH_OP_EXTRACT = 50,                                          /* imm0 = hi, imm1 = lo          */
+    MH_OP_CONCAT = 51,                                           /* a = high part, b = low part   */
+    MH_OP_ZEXT = 52, MH_OP_SEXT = 53,                            /* imm0 = extra bits             */
+    MH_OP_KECCAK = 60,        /* Keccak-256 of the big-endian bytes of a (width % 8 == 0) -> 256 */
+    MH_OP_BVADD_NOOVFL_U = 61,  /* z3.BVAddNoOverflow(a, b, False) -> Bool                        */
+    MH_OP_BVMUL_NOOVFL_U = 62,  /* z3.BVMulNoOverflow(a, b, False) -> Bool                        */
+    MH_OP_BVSUB_NOUDFL_U = 63,  /* z3.BVSubNoUnderflow(a, b, False) -> Bool  (b <=u a)            */
+    MH_OP_EVM_EXP = 70,       /* a ** b mod 2^width                                               */
+    MH_OP_EVM_SIGNEXTEND = 71,/* a = byte index k, b = x (yellow-paper SIGNEXTEND)                 */
+    MH_OP_EVM_BYTE = 72       /* a = byte index i, b = x (yellow-paper BYTE)                       */
+};
+
+typedef struct mh_node {
+    uint8_t op;      /* enum mh_op                                   */
+    uint8_t flags;   /* reserved, must be 0                          */
+    uint16_t width;  /* 0 = Bool, else bit-vector width 1..512       */
+    uint32_t a, b, c;        /* operand node indices (tape-local)    */
+    uint32_t imm0, imm1;     /* op immediates                        */
+} mh_node;                   /* 24 bytes, little-endian              */
+
+/* Evaluation modes for mh_run*. */
+enum {
+    MH_MODE_FIRST_HIT = 0,   /* per tape: smallest satisfying assignment index (early exit allowed) */
+    MH_MODE_COUNT_ALL = 1    /* per tape: number of satisfying assignments AND smallest index;       */
+                             /*           every (tape, assignment) pair is evaluated (throughput)    */
+};
+#define MH_NO_HIT 0xFFFFFFFFFFFFFFFFull
+
+typedef struct mh_ctx mh_ctx;           /* one device + one stream                                */
+typedef struct mh_tapeset mh_tapeset;   /* compiled tapes + const pool, resident on the device    */
+typedef struct mh_assign mh_assign;     /* assignments, SoA u32 limbs, resident on the device     */
+
+/* Per-tape compile statistics returned by mh_tapes_info. */
+typedef struct mh_tape_info {
+    uint32_t n_nodes;        /* IR nodes                                                          */
+    uint32_t n_insns;        /* device instructions after legalisation                            */
+    uint32_t n_regs;         /* peak registers used (of MH_NUM_REGS)                              */
+    uint32_t features;       /* bit 0: division family, bit 1: keccak, bit 2: EVM_EXP             */
+    uint64_t alg_ops;        /* algorithmic u32 ALU ops per evaluation (op-cost table) */
+} mh_tape_info;
+
+/* ---- library / device ------------------------------------------------------------------------ */
+int32_t mh_version(uint32_t* major, uint32_t* minor, uint32_t* patch);
+const char* mh_last_error(void);                       /* thread-local; never NULL               */
+int32_t mh_device_count(int32_t* n);                   /* gfx950 devices visible                 */
+
+int32_t mh_ctx_create(int32_t device, mh_ctx** out);
+int32_t mh_ctx_destroy(mh_ctx* ctx);
+/* Launch on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own.   */
+int32_t mh_ctx_set_stream(mh_ctx* ctx, void* hip_stream);
+int32_t mh_ctx_synchronize(mh_ctx* ctx);
+
+/* ---- tapes ----------------------------------------------------------------------------------- */
+/* nodes: all tapes concatenated; tape_offsets[n_tapes+1] delimit them (node indices).
+ * consts: n_consts x 8 u32 limbs (little-endian limb order, 256-bit entries).
+ * n_vars: number of assignment columns the tapes may reference.                                 */
+int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape_offsets,
+                         uint32_t n_tapes, const uint32_t* consts, uint32_t n_consts,
+                         uint32_t n_vars, mh_tapeset** out);
+int32_t mh_tapes_destroy(mh_tapeset* ts);
+int32_t mh_tapes_info(const mh_tapeset* ts, mh_tape_info* info /* [n_tapes] */, uint32_t n_tapes);
+
+/* ---- assignments ----------------------------------------------------------------------------- */
+/* Layout in HBM: column v, limb k (0 = least significant) of assignment i is word
+ * ((v * 8 + k) * capacity + i).  Every column is a 256-bit word.                                 */
+int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_assign** out);
+int32_t mh_assign_destroy(mh_assign* as);
+/* host_soa has the same layout with `count` in place of capacity; fills [first, first+count).   */
+int32_t mh_assign_upload(mh_assign* as, const uint32_t* host_soa, uint64_t first, uint64_t count);
+int32_t mh_assign_download(const mh_assign* as, uint32_t* host_soa, uint64_t first, uint64_t count);
+/* Fill all `capacity` rows from the counter-based generator: row i of this buffer gets the value
+ * mh_gen_word(seed, v, global_base + i) (see mh_gen_limb).                                       */
+int32_t mh_assign_generate(mh_assign* as, uint64_t seed, uint64_t global_base);
+/* Host reference of the generator (same bits as the device kernel).                             */
+uint32_t mh_gen_limb(uint64_t seed, uint32_t var, uint64_t index, uint32_t limb);
+
+/* ---- evaluation ------------------------------------------------------------------------------ */
+/* Evaluate tapes [tape_first, tape_first+tape_count) over assignment rows [row_first,
+ * row_first+row_count) of `as`.  Results are indexed by tape - tape_first and hold GLOBAL indices
+ * (index_base + row).  Host-pointer form: blocks until done.                                      */
+int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+               const mh_assign* as, uint64_t row_first, uint64_t row_count, uint64_t index_base,
+               uint32_t mode, uint64_t* first_hit /* [tape_count] or NULL */,
+               uint64_t* hit_count /* [tape_count] or NULL */);
+/* Device-pointer form: enqueues on the ctx stream and returns.  d_first_hit / d_hit_count are
+ * device buffers of tape_count u64; they are NOT reset (callers initialise them to MH_NO_HIT / 0
+ * with mh_results_reset), so several launches can accumulate into them.                          */
+int32_t mh_results_reset(mh_ctx* ctx, uint64_t* d_first_hit, uint64_t* d_hit_count, uint32_t n);
+int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+                     const mh_assign* as, uint64_t row_first, uint64_t row_count,
+                     uint64_t index_base, uint32_t mode, uint64_t* d_first_hit,
+                     uint64_t* d_hit_count);
+/* Parity path: the root value of tape `tape` for rows [row_first, row_first+row_count):
+ * out[(k * row_count) + r] = limb k of the root value (Bool roots: 0/1 in limb 0).  Roots wider
+ * than 256 bits are MH_E_UNSUPPORTED.  Blocks until done.                                         */
+int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const mh_assign* as,
+                       uint64_t row_first, uint64_t row_count, uint32_t* out /* [8*row_count] */);
+
+/* ---- measurement ----------------------------------------------------------------------------- */
+/* Integer VALU micro-benchmark: returns sustained u32 lane-ops/s for v_add_co/v_addc chains
+ * (kind 0), v_mad_u64_u32 (kind 1), and v_xor/v_and (kind 2).                                    */
+int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MYTHRIL_HIP_H */

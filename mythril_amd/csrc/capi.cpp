@@ -1,0 +1,430 @@
+// C-ABI of libmythril_hip (include/mythril_hip.h): handles, error reporting, device buffers,
+// launch orchestration.  No exception crosses the ABI and nothing here aborts the process:
+// every failure is an MH_E_* code plus a thread-local message, so the Python front end can fall
+// back to z3 (SURVEY.md §5 "fail closed").
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mythril_hip.h"
+#include "compile.h"
+#include "dev_isa.h"
+#include "kernels.h"
+
+struct mh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t* scratch = nullptr;  // microbench sink
+};
+
+struct mh_tapeset {
+    mh_ctx* ctx = nullptr;
+    uint32_t n_tapes = 0;
+    uint32_t n_vars = 0;
+    uint2* d_insns = nullptr;
+    mh_dev_tape* d_tapes = nullptr;
+    uint32_t* d_consts = nullptr;
+    std::vector<mh_tape_info> info;
+};
+
+struct mh_assign {
+    mh_ctx* ctx = nullptr;
+    uint32_t n_vars = 0;
+    uint64_t capacity = 0;
+    uint32_t* d = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int32_t set_err(int32_t code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define MH_HIP(call)                                                                      \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return set_err(MH_E_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+int32_t use_device(const mh_ctx* ctx) {
+    MH_HIP(hipSetDevice(ctx->device));
+    return MH_OK;
+}
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+uint32_t union_features(const mh_tapeset* ts, uint32_t first, uint32_t count) {
+    uint32_t f = 0;
+    for (uint32_t t = first; t < first + count; ++t) f |= ts->info[t].features;
+    return f;
+}
+
+int32_t check_run_args(const mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first,
+                       uint32_t tape_count, const mh_assign* as, uint64_t row_first,
+                       uint64_t row_count, uint32_t mode) {
+    if (!ctx || !ts || !as) return set_err(MH_E_INVALID, "null handle");
+    if (ts->ctx != ctx || as->ctx != ctx) return set_err(MH_E_INVALID, "handles of another ctx");
+    if ((uint64_t)tape_first + tape_count > ts->n_tapes)
+        return set_err(MH_E_INVALID, "tape range out of bounds");
+    if (row_first > as->capacity || row_count > as->capacity - row_first)
+        return set_err(MH_E_INVALID, "row range out of bounds");
+    if (as->n_vars < ts->n_vars)
+        return set_err(MH_E_INVALID, "assignment buffer has fewer columns than the tapes use");
+    if (mode != MH_MODE_FIRST_HIT && mode != MH_MODE_COUNT_ALL)
+        return set_err(MH_E_INVALID, "bad mode");
+    return MH_OK;
+}
+
+mh::KParams make_params(const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+                        const mh_assign* as, uint64_t row_first, uint64_t row_count,
+                        uint64_t index_base, uint32_t mode) {
+    mh::KParams p{};
+    p.insns = ts->d_insns;
+    p.tapes = ts->d_tapes;
+    p.consts = ts->d_consts;
+    p.assign = as->d;
+    p.capacity = as->capacity;
+    p.n_pre = ts->n_vars <= MH_MAX_PRELOAD ? ts->n_vars : 0;
+    p.tape_first = tape_first;
+    p.tape_count = tape_count;
+    p.row_first = row_first;
+    p.row_count = row_count;
+    p.index_base = index_base;
+    p.mode = mode;
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mh_version(uint32_t* major, uint32_t* minor, uint32_t* patch) {
+    if (major) *major = MH_VERSION_MAJOR;
+    if (minor) *minor = MH_VERSION_MINOR;
+    if (patch) *patch = MH_VERSION_PATCH;
+    return MH_OK;
+}
+
+const char* mh_last_error(void) { return g_err.c_str(); }
+
+int32_t mh_device_count(int32_t* n) {
+    if (!n) return set_err(MH_E_INVALID, "null out pointer");
+    *n = 0;
+    int total = 0;
+    if (hipGetDeviceCount(&total) != hipSuccess) {
+        (void)hipGetLastError();
+        return MH_OK;
+    }
+    for (int d = 0; d < total; ++d) *n += is_gfx950(d) ? 1 : 0;
+    return MH_OK;
+}
+
+int32_t mh_ctx_create(int32_t device, mh_ctx** out) {
+    if (!out) return set_err(MH_E_INVALID, "null out pointer");
+    *out = nullptr;
+    int total = 0;
+    if (hipGetDeviceCount(&total) != hipSuccess || device < 0 || device >= total) {
+        (void)hipGetLastError();
+        return set_err(MH_E_NODEVICE, "no HIP device " + std::to_string(device));
+    }
+    if (!is_gfx950(device)) return set_err(MH_E_NODEVICE, "device is not gfx950 (MI355X)");
+    mh_ctx* c = new (std::nothrow) mh_ctx();
+    if (!c) return set_err(MH_E_NOMEM, "ctx allocation");
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->scratch, 64);
+    if (e != hipSuccess) {
+        delete c;
+        return set_err(MH_E_DEVICE, std::string("ctx init: ") + hipGetErrorString(e));
+    }
+    c->own_stream = true;
+    *out = c;
+    return MH_OK;
+}
+
+int32_t mh_ctx_destroy(mh_ctx* ctx) {
+    if (!ctx) return MH_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    delete ctx;
+    return MH_OK;
+}
+
+int32_t mh_ctx_set_stream(mh_ctx* ctx, void* hip_stream) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    if (int32_t r = use_device(ctx)) return r;
+    if (ctx->own_stream && ctx->stream) {
+        MH_HIP(hipStreamSynchronize(ctx->stream));
+        MH_HIP(hipStreamDestroy(ctx->stream));
+    }
+    if (hip_stream) {
+        ctx->stream = (hipStream_t)hip_stream;
+        ctx->own_stream = false;
+    } else {
+        MH_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->own_stream = true;
+    }
+    return MH_OK;
+}
+
+int32_t mh_ctx_synchronize(mh_ctx* ctx) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    if (int32_t r = use_device(ctx)) return r;
+    MH_HIP(hipStreamSynchronize(ctx->stream));
+    return MH_OK;
+}
+
+int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape_offsets,
+                         uint32_t n_tapes, const uint32_t* consts, uint32_t n_consts,
+                         uint32_t n_vars, mh_tapeset** out) {
+    if (!ctx || !out || (!nodes && n_tapes) || !tape_offsets || (!consts && n_consts))
+        return set_err(MH_E_INVALID, "null argument");
+    *out = nullptr;
+    std::vector<uint32_t> words, dconsts;
+    std::unordered_map<std::string, uint32_t> dindex;
+    std::vector<mh_dev_tape> heads(n_tapes);
+    std::vector<mh_tape_info> info(n_tapes);
+    try {
+        for (uint32_t t = 0; t < n_tapes; ++t) {
+            const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
+            if (e <= b) return set_err(MH_E_INVALID, "tape " + std::to_string(t) + " is empty");
+            mh::CompiledTape ct;
+            std::string err;
+            const uint32_t first_insn = (uint32_t)(words.size() / 2);
+            int32_t r = mh::compile_tape(nodes + b, (size_t)(e - b), consts, n_consts, n_vars,
+                                         dconsts, dindex, words, ct, err);
+            if (r != MH_OK) return set_err(r, "tape " + std::to_string(t) + ": " + err);
+            heads[t] = mh_dev_tape{first_insn, ct.n_insns, ct.root_reg, ct.root_bool};
+            info[t] = mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops};
+        }
+    } catch (const std::bad_alloc&) {
+        return set_err(MH_E_NOMEM, "host allocation during compile");
+    }
+    if (dconsts.empty()) dconsts.assign(8, 0);
+    if (words.empty()) words.assign(2, 0);
+    if (int32_t r = use_device(ctx)) return r;
+    mh_tapeset* ts = new (std::nothrow) mh_tapeset();
+    if (!ts) return set_err(MH_E_NOMEM, "tapeset allocation");
+    ts->ctx = ctx;
+    ts->n_tapes = n_tapes;
+    ts->n_vars = n_vars;
+    ts->info = std::move(info);
+    hipError_t e = hipMalloc(&ts->d_insns, words.size() * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&ts->d_tapes, std::max<size_t>(1, n_tapes) * sizeof(mh_dev_tape));
+    if (e == hipSuccess) e = hipMalloc(&ts->d_consts, dconsts.size() * sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipMemcpy(ts->d_insns, words.data(), words.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && n_tapes)
+        e = hipMemcpy(ts->d_tapes, heads.data(), n_tapes * sizeof(mh_dev_tape), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(ts->d_consts, dconsts.data(), dconsts.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        mh_tapes_destroy(ts);
+        return set_err(MH_E_DEVICE, std::string("tapeset upload: ") + hipGetErrorString(e));
+    }
+    *out = ts;
+    return MH_OK;
+}
+
+int32_t mh_tapes_destroy(mh_tapeset* ts) {
+    if (!ts) return MH_OK;
+    (void)hipSetDevice(ts->ctx->device);
+    if (ts->d_insns) (void)hipFree(ts->d_insns);
+    if (ts->d_tapes) (void)hipFree(ts->d_tapes);
+    if (ts->d_consts) (void)hipFree(ts->d_consts);
+    delete ts;
+    return MH_OK;
+}
+
+int32_t mh_tapes_info(const mh_tapeset* ts, mh_tape_info* info, uint32_t n_tapes) {
+    if (!ts || !info) return set_err(MH_E_INVALID, "null argument");
+    if (n_tapes > ts->n_tapes) return set_err(MH_E_INVALID, "n_tapes exceeds the tape set");
+    std::copy(ts->info.begin(), ts->info.begin() + n_tapes, info);
+    return MH_OK;
+}
+
+int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_assign** out) {
+    if (!ctx || !out) return set_err(MH_E_INVALID, "null argument");
+    *out = nullptr;
+    if (n_vars == 0 || capacity == 0) return set_err(MH_E_INVALID, "empty assignment buffer");
+    if (int32_t r = use_device(ctx)) return r;
+    mh_assign* as = new (std::nothrow) mh_assign();
+    if (!as) return set_err(MH_E_NOMEM, "assign allocation");
+    as->ctx = ctx;
+    as->n_vars = n_vars;
+    as->capacity = capacity;
+    hipError_t e = hipMalloc(&as->d, (size_t)n_vars * 8 * capacity * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        delete as;
+        return set_err(MH_E_NOMEM, std::string("assignment buffer: ") + hipGetErrorString(e));
+    }
+    *out = as;
+    return MH_OK;
+}
+
+int32_t mh_assign_destroy(mh_assign* as) {
+    if (!as) return MH_OK;
+    (void)hipSetDevice(as->ctx->device);
+    if (as->d) (void)hipFree(as->d);
+    delete as;
+    return MH_OK;
+}
+
+int32_t mh_assign_upload(mh_assign* as, const uint32_t* host_soa, uint64_t first, uint64_t count) {
+    if (!as || (!host_soa && count)) return set_err(MH_E_INVALID, "null argument");
+    if (first > as->capacity || count > as->capacity - first)
+        return set_err(MH_E_INVALID, "row range out of bounds");
+    if (int32_t r = use_device(as->ctx)) return r;
+    for (uint64_t col = 0; col < (uint64_t)as->n_vars * 8; ++col) {
+        MH_HIP(hipMemcpyAsync(as->d + col * as->capacity + first, host_soa + col * count,
+                              count * sizeof(uint32_t), hipMemcpyHostToDevice, as->ctx->stream));
+    }
+    MH_HIP(hipStreamSynchronize(as->ctx->stream));
+    return MH_OK;
+}
+
+int32_t mh_assign_download(const mh_assign* as, uint32_t* host_soa, uint64_t first,
+                           uint64_t count) {
+    if (!as || (!host_soa && count)) return set_err(MH_E_INVALID, "null argument");
+    if (first > as->capacity || count > as->capacity - first)
+        return set_err(MH_E_INVALID, "row range out of bounds");
+    if (int32_t r = use_device(as->ctx)) return r;
+    for (uint64_t col = 0; col < (uint64_t)as->n_vars * 8; ++col) {
+        MH_HIP(hipMemcpyAsync(host_soa + col * count, as->d + col * as->capacity + first,
+                              count * sizeof(uint32_t), hipMemcpyDeviceToHost, as->ctx->stream));
+    }
+    MH_HIP(hipStreamSynchronize(as->ctx->stream));
+    return MH_OK;
+}
+
+int32_t mh_assign_generate(mh_assign* as, uint64_t seed, uint64_t global_base) {
+    if (!as) return set_err(MH_E_INVALID, "null handle");
+    if (int32_t r = use_device(as->ctx)) return r;
+    MH_HIP(mh::launch_generate(as->d, as->capacity, as->n_vars, seed, global_base,
+                               as->ctx->stream));
+    return MH_OK;
+}
+
+uint32_t mh_gen_limb(uint64_t seed, uint32_t var, uint64_t index, uint32_t limb) {
+    const uint64_t key = splitmix64(seed ^ (((uint64_t)var * 8 + limb) * 0xD1B54A32D192ED03ull));
+    return (uint32_t)splitmix64(key ^ index);
+}
+
+int32_t mh_results_reset(mh_ctx* ctx, uint64_t* d_first_hit, uint64_t* d_hit_count, uint32_t n) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    if (int32_t r = use_device(ctx)) return r;
+    if (d_first_hit) MH_HIP(hipMemsetAsync(d_first_hit, 0xFF, n * sizeof(uint64_t), ctx->stream));
+    if (d_hit_count) MH_HIP(hipMemsetAsync(d_hit_count, 0, n * sizeof(uint64_t), ctx->stream));
+    return MH_OK;
+}
+
+int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+                     const mh_assign* as, uint64_t row_first, uint64_t row_count,
+                     uint64_t index_base, uint32_t mode, uint64_t* d_first_hit,
+                     uint64_t* d_hit_count) {
+    if (int32_t r = check_run_args(ctx, ts, tape_first, tape_count, as, row_first, row_count, mode))
+        return r;
+    if (int32_t r = use_device(ctx)) return r;
+    mh::KParams p = make_params(ts, tape_first, tape_count, as, row_first, row_count, index_base,
+                                mode);
+    p.first_hit = reinterpret_cast<unsigned long long*>(d_first_hit);
+    p.hit_count = reinterpret_cast<unsigned long long*>(d_hit_count);
+    MH_HIP(mh::launch_sieve(p, union_features(ts, tape_first, tape_count), ctx->stream));
+    return MH_OK;
+}
+
+int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+               const mh_assign* as, uint64_t row_first, uint64_t row_count, uint64_t index_base,
+               uint32_t mode, uint64_t* first_hit, uint64_t* hit_count) {
+    if (int32_t r = check_run_args(ctx, ts, tape_first, tape_count, as, row_first, row_count, mode))
+        return r;
+    if (int32_t r = use_device(ctx)) return r;
+    uint64_t* d = nullptr;
+    const size_t n = std::max<uint32_t>(tape_count, 1);
+    MH_HIP(hipMalloc(&d, 2 * n * sizeof(uint64_t)));
+    int32_t r = mh_results_reset(ctx, d, d + n, (uint32_t)n);
+    if (r == MH_OK)
+        r = mh_run_async(ctx, ts, tape_first, tape_count, as, row_first, row_count, index_base,
+                         mode, d, d + n);
+    hipError_t e = hipSuccess;
+    if (r == MH_OK) e = hipStreamSynchronize(ctx->stream);
+    if (r == MH_OK && e == hipSuccess && first_hit && tape_count)
+        e = hipMemcpy(first_hit, d, tape_count * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (r == MH_OK && e == hipSuccess && hit_count && tape_count)
+        e = hipMemcpy(hit_count, d + n, tape_count * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (r != MH_OK) return r;
+    if (e != hipSuccess) return set_err(MH_E_DEVICE, std::string("mh_run: ") + hipGetErrorString(e));
+    return MH_OK;
+}
+
+int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const mh_assign* as,
+                       uint64_t row_first, uint64_t row_count, uint32_t* out) {
+    if (int32_t r = check_run_args(ctx, ts, tape, 1, as, row_first, row_count, MH_MODE_COUNT_ALL))
+        return r;
+    if (!out && row_count) return set_err(MH_E_INVALID, "null out");
+    if (row_count == 0) return MH_OK;
+    if (int32_t r = use_device(ctx)) return r;
+    uint32_t* d = nullptr;
+    MH_HIP(hipMalloc(&d, 8 * row_count * sizeof(uint32_t)));
+    mh::KParams p = make_params(ts, tape, 1, as, row_first, row_count, 0, MH_MODE_COUNT_ALL);
+    hipError_t e = mh::launch_values(p, tape, d, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpy(out, d, 8 * row_count * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess)
+        return set_err(MH_E_DEVICE, std::string("mh_eval_values: ") + hipGetErrorString(e));
+    return MH_OK;
+}
+
+int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s) {
+    if (!ctx || !ops_per_s || kind > 2) return set_err(MH_E_INVALID, "bad argument");
+    if (int32_t r = use_device(ctx)) return r;
+    const uint32_t blocks = 256 * 8, iters = 4096;
+    hipEvent_t e0, e1;
+    MH_HIP(hipEventCreate(&e0));
+    MH_HIP(hipEventCreate(&e1));
+    MH_HIP(mh::launch_microbench(kind, 64, blocks, ctx->scratch, ctx->stream));  // warm-up
+    MH_HIP(hipEventRecord(e0, ctx->stream));
+    MH_HIP(mh::launch_microbench(kind, iters, blocks, ctx->scratch, ctx->stream));
+    MH_HIP(hipEventRecord(e1, ctx->stream));
+    MH_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    MH_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    // ops per lane per iteration: kind 0 = 16 (two 8-limb chains), 1 = 8 mads, 2 = 16 (xor+add)
+    const double per_iter = kind == 0 ? 16.0 : kind == 1 ? 8.0 : 16.0;
+    const double lanes = (double)blocks * 256.0;
+    *ops_per_s = lanes * iters * per_iter / (ms * 1e-3);
+    return MH_OK;
+}
+
+}  // extern "C"

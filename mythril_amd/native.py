@@ -1,0 +1,296 @@
+"""ctypes binding of libmythril_hip (include/mythril_hip.h).
+
+The reference reaches its native solver (z3) in-process through ctypes as well
+(z3-solver's ``z3core``); this module is the analogous binding for the sieve.  The
+library is loaded from the package directory (built in-tree by ``__graft_entry__.build()``
+or ``make -C mythril_amd/csrc``); a missing library raises ``NativeUnavailable`` — there is
+no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from .tape import NODE_DTYPE, TapeSet
+
+LIB_NAME = "libmythril_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+MH_OK = 0
+MH_E_INVALID = -1
+MH_E_UNSUPPORTED = -2
+MH_E_DEVICE = -3
+MH_E_NOMEM = -4
+MH_E_NODEVICE = -5
+
+MODE_FIRST_HIT = 0
+MODE_COUNT_ALL = 1
+NO_HIT = 0xFFFFFFFFFFFFFFFF
+
+# every symbol include/mythril_hip.h declares: name -> (restype, argtypes)
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_vp = C.c_void_p
+SIGNATURES = {
+    "mh_version": (C.c_int32, [_u32p, _u32p, _u32p]),
+    "mh_last_error": (C.c_char_p, []),
+    "mh_device_count": (C.c_int32, [C.POINTER(C.c_int32)]),
+    "mh_ctx_create": (C.c_int32, [C.c_int32, C.POINTER(_vp)]),
+    "mh_ctx_destroy": (C.c_int32, [_vp]),
+    "mh_ctx_set_stream": (C.c_int32, [_vp, _vp]),
+    "mh_ctx_synchronize": (C.c_int32, [_vp]),
+    "mh_tapes_compile": (C.c_int32, [_vp, _vp, _u64p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
+                                     C.POINTER(_vp)]),
+    "mh_tapes_destroy": (C.c_int32, [_vp]),
+    "mh_tapes_info": (C.c_int32, [_vp, _vp, C.c_uint32]),
+    "mh_assign_create": (C.c_int32, [_vp, C.c_uint32, C.c_uint64, C.POINTER(_vp)]),
+    "mh_assign_destroy": (C.c_int32, [_vp]),
+    "mh_assign_upload": (C.c_int32, [_vp, _u32p, C.c_uint64, C.c_uint64]),
+    "mh_assign_download": (C.c_int32, [_vp, _u32p, C.c_uint64, C.c_uint64]),
+    "mh_assign_generate": (C.c_int32, [_vp, C.c_uint64, C.c_uint64]),
+    "mh_gen_limb": (C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]),
+    "mh_results_reset": (C.c_int32, [_vp, _vp, _vp, C.c_uint32]),
+    "mh_run": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
+                           C.c_uint64, C.c_uint32, _u64p, _u64p]),
+    "mh_run_async": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
+                                 C.c_uint64, C.c_uint32, _vp, _vp]),
+    "mh_eval_values": (C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint64, C.c_uint64, _u32p]),
+    "mh_microbench_valu": (C.c_int32, [_vp, C.c_uint32, C.POINTER(C.c_double)]),
+}
+
+
+class NativeUnavailable(RuntimeError):
+    """libmythril_hip.so is missing or cannot be loaded."""
+
+
+class SieveError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("mythril_hip error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Unsupported(SieveError):
+    """The tape uses something the device path does not cover: fall back to z3."""
+
+
+class TapeInfo(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint32),
+        ("n_insns", C.c_uint32),
+        ("n_regs", C.c_uint32),
+        ("features", C.c_uint32),
+        ("alg_ops", C.c_uint64),
+    ]
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeUnavailable(
+            "%s not built; run `python -c 'import __graft_entry__ as g; g.build()'`" % path)
+    try:
+        lib = C.CDLL(path)
+    except OSError as e:  # pragma: no cover - depends on the ROCm runtime
+        raise NativeUnavailable("cannot load %s: %s" % (path, e)) from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(code: int) -> None:
+    if code != MH_OK:
+        msg = load().mh_last_error().decode(errors="replace")
+        if code == MH_E_UNSUPPORTED:
+            raise Unsupported(code, msg)
+        raise SieveError(code, msg)
+
+
+def _ptr(a: np.ndarray, t=C.c_uint32):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def version() -> Tuple[int, int, int]:
+    a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    _check(load().mh_version(C.byref(a), C.byref(b), C.byref(c)))
+    return a.value, b.value, c.value
+
+
+def device_count() -> int:
+    n = C.c_int32()
+    _check(load().mh_device_count(C.byref(n)))
+    return n.value
+
+
+def gen_limb(seed: int, var: int, index: int, limb: int) -> int:
+    return int(load().mh_gen_limb(seed, var, index, limb))
+
+
+class Context:
+    """One GPU + one stream (mh_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        _check(self.lib.mh_ctx_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def set_stream(self, stream_ptr: Optional[int]) -> None:
+        _check(self.lib.mh_ctx_set_stream(self.h, C.c_void_p(stream_ptr or 0)))
+
+    def synchronize(self) -> None:
+        _check(self.lib.mh_ctx_synchronize(self.h))
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.mh_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compile(self, tapeset: TapeSet) -> "CompiledTapes":
+        return CompiledTapes(self, tapeset)
+
+    def assignments(self, n_vars: int, capacity: int) -> "Assignments":
+        return Assignments(self, n_vars, capacity)
+
+    def microbench(self, kind: int) -> float:
+        v = C.c_double()
+        _check(self.lib.mh_microbench_valu(self.h, kind, C.byref(v)))
+        return v.value
+
+
+class CompiledTapes:
+    """mh_tapeset: tapes lowered to device code, resident in HBM."""
+
+    def __init__(self, ctx: Context, tapeset: TapeSet):
+        self.ctx = ctx
+        nodes, offs, consts = tapeset.flatten()
+        nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        consts = np.ascontiguousarray(consts, dtype=np.uint32)
+        h = C.c_void_p()
+        _check(ctx.lib.mh_tapes_compile(
+            ctx.h, nodes.ctypes.data_as(C.c_void_p), _ptr(offs, C.c_uint64), len(tapeset.tapes),
+            _ptr(consts), len(tapeset.pool.values), tapeset.n_vars, C.byref(h)))
+        self.h = h
+        self.n_tapes = len(tapeset.tapes)
+        self.n_vars = tapeset.n_vars
+
+    def info(self):
+        arr = (TapeInfo * max(self.n_tapes, 1))()
+        _check(self.ctx.lib.mh_tapes_info(self.h, C.cast(arr, C.c_void_p), self.n_tapes))
+        return [dict(n_nodes=x.n_nodes, n_insns=x.n_insns, n_regs=x.n_regs,
+                     features=x.features, alg_ops=x.alg_ops) for x in arr[: self.n_tapes]]
+
+    def close(self) -> None:
+        if self.h:
+            self.ctx.lib.mh_tapes_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Assignments:
+    """mh_assign: candidate assignments, SoA u32 limbs in HBM."""
+
+    def __init__(self, ctx: Context, n_vars: int, capacity: int):
+        self.ctx = ctx
+        self.n_vars = n_vars
+        self.capacity = capacity
+        h = C.c_void_p()
+        _check(ctx.lib.mh_assign_create(ctx.h, n_vars, capacity, C.byref(h)))
+        self.h = h
+
+    def upload(self, soa: np.ndarray, first: int = 0) -> None:
+        """soa: u32 array shaped [n_vars, 8, count] (limb 0 least significant)."""
+        soa = np.ascontiguousarray(soa, dtype=np.uint32)
+        assert soa.shape[:2] == (self.n_vars, 8)
+        _check(self.ctx.lib.mh_assign_upload(self.h, _ptr(soa), first, soa.shape[2]))
+
+    def download(self, first: int, count: int) -> np.ndarray:
+        out = np.zeros((self.n_vars, 8, count), dtype=np.uint32)
+        _check(self.ctx.lib.mh_assign_download(self.h, _ptr(out), first, count))
+        return out
+
+    def generate(self, seed: int, global_base: int = 0) -> None:
+        _check(self.ctx.lib.mh_assign_generate(self.h, seed, global_base))
+
+    def close(self) -> None:
+        if self.h:
+            self.ctx.lib.mh_assign_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run(ctx: Context, tapes: CompiledTapes, assign: Assignments, *, tape_first: int = 0,
+        tape_count: Optional[int] = None, row_first: int = 0, row_count: Optional[int] = None,
+        index_base: int = 0, mode: int = MODE_COUNT_ALL):
+    """Blocking run; returns (first_hit[u64], hit_count[u64]) per tape."""
+    tc = tapes.n_tapes - tape_first if tape_count is None else tape_count
+    rc = assign.capacity - row_first if row_count is None else row_count
+    fh = np.zeros(max(tc, 1), dtype=np.uint64)
+    hc = np.zeros(max(tc, 1), dtype=np.uint64)
+    _check(ctx.lib.mh_run(ctx.h, tapes.h, tape_first, tc, assign.h, row_first, rc, index_base,
+                          mode, _ptr(fh, C.c_uint64), _ptr(hc, C.c_uint64)))
+    return fh[:tc], hc[:tc]
+
+
+def run_async(ctx: Context, tapes: CompiledTapes, assign: Assignments, d_first_hit: int,
+              d_hit_count: int, *, tape_first: int = 0, tape_count: Optional[int] = None,
+              row_first: int = 0, row_count: Optional[int] = None, index_base: int = 0,
+              mode: int = MODE_COUNT_ALL) -> None:
+    """Enqueue on the ctx stream; results accumulate into caller device buffers (u64)."""
+    tc = tapes.n_tapes - tape_first if tape_count is None else tape_count
+    rc = assign.capacity - row_first if row_count is None else row_count
+    _check(ctx.lib.mh_run_async(ctx.h, tapes.h, tape_first, tc, assign.h, row_first, rc,
+                                index_base, mode, C.c_void_p(d_first_hit),
+                                C.c_void_p(d_hit_count)))
+
+
+def results_reset(ctx: Context, d_first_hit: int, d_hit_count: int, n: int) -> None:
+    _check(ctx.lib.mh_results_reset(ctx.h, C.c_void_p(d_first_hit), C.c_void_p(d_hit_count), n))
+
+
+def eval_values(ctx: Context, tapes: CompiledTapes, tape: int, assign: Assignments,
+                row_first: int = 0, row_count: Optional[int] = None) -> np.ndarray:
+    """Root value of `tape` per row: u32 [8, rows] (limb-major)."""
+    rc = assign.capacity - row_first if row_count is None else row_count
+    out = np.zeros((8, max(rc, 1)), dtype=np.uint32)
+    _check(ctx.lib.mh_eval_values(ctx.h, tapes.h, tape, assign.h, row_first, rc, _ptr(out)))
+    return out[:, :rc]
+
+
+def limbs_to_ints(arr: np.ndarray) -> Sequence[int]:
+    """[8, n] u32 limbs -> Python ints."""
+    out = []
+    for j in range(arr.shape[1]):
+        v = 0
+        for k in range(8):
+            v |= int(arr[k, j]) << (32 * k)
+        out.append(v)
+    return out

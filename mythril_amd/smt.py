@@ -1,0 +1,505 @@
+"""Term-construction front end that mirrors ``mythril.laser.smt`` and emits tape nodes.
+
+The reference builds path constraints through thin wrappers over z3
+(mythril/laser/smt/__init__.py, bitvec.py, bitvec_helper.py, bool.py, array.py).
+This module offers the same names, argument meaning and operator semantics, but
+the terms it builds are sieve tape nodes instead of z3 ASTs, so the parity tests
+read like the reference's own tests and a z3-free box can still build tapes.
+Operator quirks of the reference are kept on purpose:
+
+* ``BitVec.__truediv__`` is *signed* division (bitvec.py:96-103, z3 ``/``);
+* ``<``, ``>``, ``<=``, ``>=`` are *signed* comparisons (bitvec.py:138-180);
+* ``>>`` is the *arithmetic* shift (bitvec.py:237-243, z3 ``>>``); ``LShR`` is logical;
+* ``==`` / ``!=`` between different widths zero-pads the narrower side with a
+  ``Concat`` (bitvec.py:16-22,183-216);
+* ``UGE``/``ULE`` are ``Or(UGT, ==)``/``Or(ULT, ==)`` (bitvec_helper.py:53-80);
+* ``If`` turns Python ints into 256-bit values (bitvec_helper.py:26-40).
+
+No simplification is applied: z3's ``simplify`` rewrites are not restated (their
+normal forms vary by z3 version), so a tape built here is the term
+*as constructed*, which evaluates to the same value as its simplified form.
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence, Union
+
+from .tape import BOOL, Op, Tape, TapeBuilder, TapeError, TapeSet
+
+
+class Context:
+    """One hash-consed term store feeding one TapeSet (the analogue of a z3 context)."""
+
+    def __init__(self, tapeset: Optional[TapeSet] = None):
+        self.tapeset = tapeset if tapeset is not None else TapeSet()
+        self.b: TapeBuilder = self.tapeset.builder()
+
+    def tape(self, *constraints: "Bool") -> Tape:
+        """The conjunction of ``constraints`` as one tape (what get_model would hand to z3)."""
+        root = And(*constraints, ctx=self) if len(constraints) != 1 else constraints[0]
+        if isinstance(root, BitVec) and not isinstance(root, Bool):
+            return self.b.finish(root.node)
+        return self.b.finish(_as_bool(root, self).node)
+
+    def add_tape(self, *constraints) -> int:
+        return self.tapeset.add(self.tape(*constraints))
+
+
+_tls = threading.local()
+
+
+def context() -> Context:
+    ctx = getattr(_tls, "ctx", None)
+    if ctx is None:
+        ctx = _tls.ctx = Context()
+    return ctx
+
+
+def set_context(ctx: Context) -> Context:
+    _tls.ctx = ctx
+    return ctx
+
+
+class Expression:
+    """Base of BitVec and Bool (mythril/laser/smt/expression.py:10-58)."""
+
+    def __init__(self, node: int, ctx: Context, annotations=None):
+        self.node = node
+        self.ctx = ctx
+        self.annotations = set(annotations or ())
+
+    def annotate(self, annotation) -> None:
+        self.annotations.add(annotation)
+
+    def size(self) -> int:
+        return self.ctx.b.width(self.node)
+
+    def __hash__(self) -> int:
+        return hash((id(self.ctx), self.node))
+
+    def _const_value(self) -> Optional[int]:
+        op, _, _, _, _, imm0, _ = self.ctx.b.nodes[self.node]
+        if op == Op.CONST:
+            return self.ctx.b.pool.values[imm0]
+        if op == Op.TRUE:
+            return 1
+        if op == Op.FALSE:
+            return 0
+        return None
+
+
+def _b(ctx: Context) -> TapeBuilder:
+    return ctx.b
+
+
+class BitVec(Expression):
+    """Bit-vector term (mythril/laser/smt/bitvec.py:25-253)."""
+
+    @property
+    def symbolic(self) -> bool:
+        return self._const_value() is None
+
+    @property
+    def value(self) -> Optional[int]:
+        return self._const_value()
+
+    def _other(self, other: Union[int, "BitVec"]) -> "BitVec":
+        if isinstance(other, BitVec):
+            return other
+        return BitVec(_b(self.ctx).const(int(other), self.size()), self.ctx)
+
+    def _bin(self, op: Op, other) -> "BitVec":
+        o = self._other(other)
+        return BitVec(_b(self.ctx).op(op, self.node, o.node), self.ctx,
+                      self.annotations | o.annotations)
+
+    def _cmp(self, op: Op, other) -> "Bool":
+        o = self._other(other)
+        return Bool(_b(self.ctx).op(op, self.node, o.node), self.ctx,
+                    self.annotations | o.annotations)
+
+    def __add__(self, other):
+        return self._bin(Op.BVADD, other)
+
+    def __radd__(self, other):
+        return self._other(other)._bin(Op.BVADD, self)
+
+    def __sub__(self, other):
+        return self._bin(Op.BVSUB, other)
+
+    def __rsub__(self, other):
+        return self._other(other)._bin(Op.BVSUB, self)
+
+    def __mul__(self, other):
+        return self._bin(Op.BVMUL, other)
+
+    def __truediv__(self, other):  # signed, as z3 '/'
+        return self._bin(Op.BVSDIV, other)
+
+    def __and__(self, other):
+        return self._bin(Op.BVAND, other)
+
+    def __or__(self, other):
+        return self._bin(Op.BVOR, other)
+
+    def __xor__(self, other):
+        return self._bin(Op.BVXOR, other)
+
+    def __invert__(self):
+        return BitVec(_b(self.ctx).op(Op.BVNOT, self.node), self.ctx, self.annotations)
+
+    def __neg__(self):
+        return BitVec(_b(self.ctx).op(Op.BVNEG, self.node), self.ctx, self.annotations)
+
+    def __lt__(self, other):
+        return self._cmp(Op.BVSLT, other)
+
+    def __gt__(self, other):
+        return self._cmp(Op.BVSGT, other)
+
+    def __le__(self, other):
+        return self._cmp(Op.BVSLE, other)
+
+    def __ge__(self, other):
+        return self._cmp(Op.BVSGE, other)
+
+    def __lshift__(self, other):
+        return self._bin(Op.BVSHL, other)
+
+    def __rshift__(self, other):  # arithmetic, as z3 '>>'
+        return self._bin(Op.BVASHR, other)
+
+    def _padded(self, other: "BitVec"):
+        a, b = self, other
+        if a.size() == b.size():
+            return a, b
+        if a.size() < b.size():
+            a, b = b, a
+        pad = BitVec(_b(self.ctx).const(0, a.size() - b.size()), self.ctx)
+        return a, Concat(pad, b)
+
+    def __eq__(self, other):  # type: ignore[override]
+        if not isinstance(other, BitVec):
+            return self._cmp(Op.EQ, other)
+        a, b = self._padded(other)
+        return Bool(_b(self.ctx).op(Op.EQ, a.node, b.node), self.ctx,
+                    self.annotations | other.annotations)
+
+    def __ne__(self, other):  # type: ignore[override]
+        return Not(self.__eq__(other))
+
+    def __hash__(self) -> int:
+        return Expression.__hash__(self)
+
+
+class Bool(Expression):
+    """Boolean term (mythril/laser/smt/bool.py:14-84)."""
+
+    @property
+    def value(self) -> Optional[bool]:
+        v = self._const_value()
+        return None if v is None else bool(v)
+
+    @property
+    def is_true(self) -> bool:
+        return self.value is True
+
+    @property
+    def is_false(self) -> bool:
+        return self.value is False
+
+    def __eq__(self, other):  # type: ignore[override]
+        o = _as_bool(other, self.ctx)
+        return Bool(_b(self.ctx).op(Op.EQ, self.node, o.node), self.ctx,
+                    self.annotations | o.annotations)
+
+    def __ne__(self, other):  # type: ignore[override]
+        return Not(self.__eq__(other))
+
+    def __bool__(self) -> bool:
+        # concrete-only truth value, as bool.py:73-81
+        v = self.value
+        return bool(v) if v is not None else False
+
+    def __hash__(self) -> int:
+        return Expression.__hash__(self)
+
+
+def _as_bool(x, ctx: Context) -> Bool:
+    if isinstance(x, Bool):
+        return x
+    if isinstance(x, bool):
+        return Bool(_b(ctx).true() if x else _b(ctx).false(), ctx)
+    raise TapeError("expected a Bool, got %r" % (x,))
+
+
+class _SymbolFactory:
+    """mythril/laser/smt/__init__.py:83-154 (_SmtSymbolFactory)."""
+
+    @staticmethod
+    def Bool(value: bool, annotations=None) -> Bool:
+        ctx = context()
+        return Bool(_b(ctx).true() if value else _b(ctx).false(), ctx, annotations)
+
+    @staticmethod
+    def BoolSym(name: str, annotations=None) -> Bool:
+        ctx = context()
+        v = _b(ctx).var(name, 1)
+        one = _b(ctx).const(1, 1)
+        return Bool(_b(ctx).op(Op.EQ, v, one), ctx, annotations)
+
+    @staticmethod
+    def BitVecVal(value: int, size: int, annotations=None) -> BitVec:
+        ctx = context()
+        return BitVec(_b(ctx).const(int(value), size), ctx, annotations)
+
+    @staticmethod
+    def BitVecSym(name: str, size: int, annotations=None) -> BitVec:
+        ctx = context()
+        return BitVec(_b(ctx).var(name, size), ctx, annotations)
+
+
+symbol_factory = _SymbolFactory()
+
+
+def _ctx_of(args) -> Context:
+    for a in args:
+        if isinstance(a, Expression):
+            return a.ctx
+    return context()
+
+
+def And(*args, ctx: Optional[Context] = None) -> Bool:
+    """n-ary And folded left (bool.py:87-93)."""
+    ctx = ctx or _ctx_of(args)
+    bs = [_as_bool(a, ctx) for a in args]
+    if not bs:
+        return Bool(_b(ctx).true(), ctx)
+    acc = bs[0]
+    for x in bs[1:]:
+        acc = Bool(_b(ctx).op(Op.AND, acc.node, x.node), ctx, acc.annotations | x.annotations)
+    return acc
+
+
+def Or(*args, ctx: Optional[Context] = None) -> Bool:
+    """n-ary Or folded left (bool.py:103-115)."""
+    ctx = ctx or _ctx_of(args)
+    bs = [_as_bool(a, ctx) for a in args]
+    if not bs:
+        return Bool(_b(ctx).false(), ctx)
+    acc = bs[0]
+    for x in bs[1:]:
+        acc = Bool(_b(ctx).op(Op.OR, acc.node, x.node), ctx, acc.annotations | x.annotations)
+    return acc
+
+
+def Xor(a: Bool, b: Bool) -> Bool:
+    """bool.py:96-100."""
+    ctx = _ctx_of((a, b))
+    a, b = _as_bool(a, ctx), _as_bool(b, ctx)
+    return Bool(_b(ctx).op(Op.XOR, a.node, b.node), ctx, a.annotations | b.annotations)
+
+
+def Not(a: Bool) -> Bool:
+    """bool.py:118-124."""
+    ctx = _ctx_of((a,))
+    a = _as_bool(a, ctx)
+    return Bool(_b(ctx).op(Op.NOT, a.node), ctx, a.annotations)
+
+
+def is_true(a: Bool) -> bool:
+    return a.value is True
+
+
+def is_false(a: Bool) -> bool:
+    return a.value is False
+
+
+def simplify(e):
+    """Identity: z3 rewriting is not restated (see module docstring)."""
+    return e
+
+
+def If(a: Union[Bool, bool], b: Union[BitVec, int], c: Union[BitVec, int]) -> BitVec:
+    """bitvec_helper.py:26-40; also accepts Bool branches (z3.If is sort-polymorphic)."""
+    ctx = _ctx_of((a, b, c))
+    a = _as_bool(a, ctx)
+    if not isinstance(b, Expression):
+        b = BitVec(_b(ctx).const(int(b), 256), ctx)
+    if not isinstance(c, Expression):
+        c = BitVec(_b(ctx).const(int(c), 256), ctx)
+    cls = Bool if isinstance(b, Bool) else BitVec
+    return cls(_b(ctx).op(Op.ITE, a.node, b.node, c.node), ctx,
+               a.annotations | b.annotations | c.annotations)
+
+
+def _cmp(op: Op, a: BitVec, b: BitVec) -> Bool:
+    return a._cmp(op, b)
+
+
+def UGT(a: BitVec, b: BitVec) -> Bool:
+    return _cmp(Op.BVUGT, a, b)
+
+
+def UGE(a: BitVec, b: BitVec) -> Bool:
+    return Or(UGT(a, b), a == b)
+
+
+def ULT(a: BitVec, b: BitVec) -> Bool:
+    return _cmp(Op.BVULT, a, b)
+
+
+def ULE(a: BitVec, b: BitVec) -> Bool:
+    return Or(ULT(a, b), a == b)
+
+
+def Concat(*args) -> BitVec:
+    """bitvec_helper.py:83-116 (z3.Concat, first argument most significant)."""
+    if len(args) == 1 and isinstance(args[0], (list, tuple)):
+        args = tuple(args[0])
+    ctx = _ctx_of(args)
+    acc = args[0]
+    for x in args[1:]:
+        acc = BitVec(_b(ctx).op(Op.CONCAT, acc.node, x.node), ctx,
+                     acc.annotations | x.annotations)
+    return acc
+
+
+def Extract(high: int, low: int, bv: BitVec) -> BitVec:
+    """bitvec_helper.py:119-128."""
+    return BitVec(_b(bv.ctx).op(Op.EXTRACT, bv.node, imm0=high, imm1=low), bv.ctx,
+                  bv.annotations)
+
+
+def ZeroExt(n: int, bv: BitVec) -> BitVec:
+    return BitVec(_b(bv.ctx).op(Op.ZEXT, bv.node, imm0=n), bv.ctx, bv.annotations)
+
+
+def SignExt(n: int, bv: BitVec) -> BitVec:
+    return BitVec(_b(bv.ctx).op(Op.SEXT, bv.node, imm0=n), bv.ctx, bv.annotations)
+
+
+def URem(a: BitVec, b: BitVec) -> BitVec:
+    return a._bin(Op.BVUREM, b)
+
+
+def SRem(a: BitVec, b: BitVec) -> BitVec:
+    return a._bin(Op.BVSREM, b)
+
+
+def SMod(a: BitVec, b: BitVec) -> BitVec:
+    return a._bin(Op.BVSMOD, b)
+
+
+def UDiv(a: BitVec, b: BitVec) -> BitVec:
+    return a._bin(Op.BVUDIV, b)
+
+
+def LShR(a: BitVec, b: BitVec) -> BitVec:
+    return a._bin(Op.BVLSHR, b)
+
+
+def Sum(*args: BitVec) -> BitVec:
+    """bitvec_helper.py:164-175 (z3.Sum folds bvadd)."""
+    acc = args[0]
+    for x in args[1:]:
+        acc = acc + x
+    return acc
+
+
+def _bv256(x, ctx: Context) -> BitVec:
+    return x if isinstance(x, BitVec) else BitVec(_b(ctx).const(int(x), 256), ctx)
+
+
+def BVAddNoOverflow(a, b, signed: bool) -> Bool:
+    """bitvec_helper.py:178-191 (z3.BVAddNoOverflow)."""
+    ctx = _ctx_of((a, b))
+    a, b = _bv256(a, ctx), _bv256(b, ctx)
+    if not signed:
+        return a._cmp(Op.BVADD_NOOVFL_U, b)
+    # signed: overflow iff sign(a) == sign(b) != sign(a + b)
+    w = a.size()
+    sa, sb, ss = (Extract(w - 1, w - 1, x) for x in (a, b, a + b))
+    return Not(And(sa == sb, Not(sa == ss)))
+
+
+def BVMulNoOverflow(a, b, signed: bool) -> Bool:
+    """bitvec_helper.py:194-207 (z3.BVMulNoOverflow); the signed form is not on the device path."""
+    ctx = _ctx_of((a, b))
+    a, b = _bv256(a, ctx), _bv256(b, ctx)
+    if signed:
+        raise TapeError("signed BVMulNoOverflow is not supported by the sieve")
+    return a._cmp(Op.BVMUL_NOOVFL_U, b)
+
+
+def BVSubNoUnderflow(a, b, signed: bool) -> Bool:
+    """bitvec_helper.py:210-227 (z3.BVSubNoUnderflow)."""
+    ctx = _ctx_of((a, b))
+    a, b = _bv256(a, ctx), _bv256(b, ctx)
+    if signed:
+        # signed underflow of a - b: sign(a) != sign(b) and sign(a - b) != sign(a)
+        w = a.size()
+        sa, sb, sd = (Extract(w - 1, w - 1, x) for x in (a, b, a - b))
+        return Not(And(Not(sa == sb), Not(sd == sa)))
+    return a._cmp(Op.BVSUB_NOUDFL_U, b)
+
+
+def Keccak256(data: BitVec) -> BitVec:
+    """Concrete Keccak-256 of ``data``'s big-endian bytes: the value the reference computes for a
+    concrete input (keccak_function_manager.py:43-57, find_concrete_keccak), here evaluated per
+    candidate assignment on the device."""
+    return BitVec(_b(data.ctx).op(Op.KECCAK, data.node), data.ctx, data.annotations)
+
+
+class BaseArray:
+    """Select/Store arrays lowered to ite chains (mythril/laser/smt/array.py:16-63).
+
+    ``select(store(A, k, v), i) = ite(i == k, v, select(A, i))`` and ``select(K(c), i) = c``.
+    A free ``Array`` base (uninterpreted contents) has no device lowering yet.
+    """
+
+    def __init__(self, domain: int, value_range: int):
+        self.domain = domain
+        self.range = value_range
+        self.stores: List[tuple] = []
+        self.default: Optional[int] = None
+        self.name: Optional[str] = None
+
+    def __getitem__(self, item: BitVec) -> BitVec:
+        if isinstance(item, slice):
+            raise ValueError("Instance of BaseArray, does not support getitem with slices")
+        ctx = item.ctx
+        if self.default is None:
+            raise TapeError("reads of free array %r are not supported by the sieve" % self.name)
+        acc = BitVec(_b(ctx).const(self.default, self.range), ctx)
+        for k, v in self.stores:
+            acc = If(item == k, v, acc)
+        return acc
+
+    def __setitem__(self, key: BitVec, value) -> None:
+        if isinstance(value, Bool):
+            value = If(value, 1, 0)
+        if not isinstance(value, BitVec):
+            value = symbol_factory.BitVecVal(int(value), self.range)
+        self.stores.append((key, value))
+
+
+class Array(BaseArray):
+    def __init__(self, name: str, domain: int, value_range: int):
+        super().__init__(domain, value_range)
+        self.name = name
+
+
+class K(BaseArray):
+    def __init__(self, domain: int, value_range: int, value: int):
+        super().__init__(domain, value_range)
+        self.default = int(value) & ((1 << value_range) - 1)
+
+
+__all__ = [
+    "Context", "context", "set_context", "Expression", "BitVec", "Bool", "symbol_factory",
+    "And", "Or", "Xor", "Not", "is_true", "is_false", "simplify", "If", "UGT", "UGE", "ULT",
+    "ULE", "Concat", "Extract", "ZeroExt", "SignExt", "URem", "SRem", "SMod", "UDiv", "LShR",
+    "Sum", "BVAddNoOverflow", "BVMulNoOverflow", "BVSubNoUnderflow", "Keccak256", "BaseArray",
+    "Array", "K", "BOOL",
+]

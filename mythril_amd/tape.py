@@ -1,0 +1,352 @@
+"""Tape IR: flattened z3 QF_BV / Bool terms as the sieve consumes them.
+
+A *tape* is one path-constraint term (normally the conjunction handed to
+``get_model``, mythril/support/model.py:15-62) flattened into a topologically
+ordered node list; every node names its operands by tape-local index and the
+last node is the root.  The node layout is ``mh_node`` of include/mythril_hip.h
+(24 bytes).  Terms are hash-consed while a tape is built, so the DAG sharing z3
+keeps (calldata concat chains, keccak conditions repeated across constraints) is
+kept instead of being unrolled into a tree.
+
+Sorts: ``width == 0`` is Bool, ``1..512`` a bit-vector.  The node kinds and the
+reference construction that produces each one are tabulated in DESIGN.md
+(§Tape IR) and in SURVEY.md §2.1.
+"""
+from __future__ import annotations
+
+import enum
+from dataclasses import dataclass, field
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+BOOL = 0
+MAX_WIDTH = 512
+
+
+class Op(enum.IntEnum):
+    CONST = 0
+    VAR = 1
+    TRUE = 2
+    FALSE = 3
+    BVADD = 10
+    BVSUB = 11
+    BVMUL = 12
+    BVUDIV = 13
+    BVUREM = 14
+    BVSDIV = 15
+    BVSREM = 16
+    BVSMOD = 17
+    BVNEG = 18
+    BVNOT = 19
+    BVAND = 20
+    BVOR = 21
+    BVXOR = 22
+    BVSHL = 23
+    BVLSHR = 24
+    BVASHR = 25
+    EQ = 30
+    BVULT = 31
+    BVULE = 32
+    BVUGT = 33
+    BVUGE = 34
+    BVSLT = 35
+    BVSLE = 36
+    BVSGT = 37
+    BVSGE = 38
+    AND = 40
+    OR = 41
+    XOR = 42
+    NOT = 43
+    ITE = 45
+    EXTRACT = 50
+    CONCAT = 51
+    ZEXT = 52
+    SEXT = 53
+    KECCAK = 60
+    BVADD_NOOVFL_U = 61
+    BVMUL_NOOVFL_U = 62
+    BVSUB_NOUDFL_U = 63
+    EVM_EXP = 70
+    EVM_SIGNEXTEND = 71
+    EVM_BYTE = 72
+
+
+NODE_DTYPE = np.dtype(
+    [
+        ("op", "u1"),
+        ("flags", "u1"),
+        ("width", "<u2"),
+        ("a", "<u4"),
+        ("b", "<u4"),
+        ("c", "<u4"),
+        ("imm0", "<u4"),
+        ("imm1", "<u4"),
+    ]
+)
+assert NODE_DTYPE.itemsize == 24
+
+# operand arity per op (number of node operands a, b, c used)
+ARITY = {
+    Op.CONST: 0, Op.VAR: 0, Op.TRUE: 0, Op.FALSE: 0,
+    Op.BVNEG: 1, Op.BVNOT: 1, Op.NOT: 1, Op.EXTRACT: 1, Op.ZEXT: 1, Op.SEXT: 1, Op.KECCAK: 1,
+    Op.ITE: 3,
+}
+for _op in Op:
+    ARITY.setdefault(_op, 2)
+
+BV_BINARY = {
+    Op.BVADD, Op.BVSUB, Op.BVMUL, Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD,
+    Op.BVAND, Op.BVOR, Op.BVXOR, Op.BVSHL, Op.BVLSHR, Op.BVASHR, Op.EVM_EXP,
+    Op.EVM_SIGNEXTEND, Op.EVM_BYTE,
+}
+BV_COMPARE = {
+    Op.BVULT, Op.BVULE, Op.BVUGT, Op.BVUGE, Op.BVSLT, Op.BVSLE, Op.BVSGT, Op.BVSGE,
+    Op.BVADD_NOOVFL_U, Op.BVMUL_NOOVFL_U, Op.BVSUB_NOUDFL_U,
+}
+BOOL_BINARY = {Op.AND, Op.OR, Op.XOR}
+
+
+class TapeError(ValueError):
+    pass
+
+
+@dataclass
+class ConstPool:
+    """Shared 256-bit constant pool of a tape set (8 little-endian u32 limbs per entry)."""
+
+    values: List[int] = field(default_factory=list)
+    index: Dict[int, int] = field(default_factory=dict)
+
+    def add(self, value: int) -> int:
+        if value < 0 or value >= 1 << 256:
+            raise TapeError("constant pool entries are 256-bit: %r" % value)
+        i = self.index.get(value)
+        if i is None:
+            i = len(self.values)
+            self.values.append(value)
+            self.index[value] = i
+        return i
+
+    def to_array(self) -> np.ndarray:
+        arr = np.zeros((max(len(self.values), 1), 8), dtype=np.uint32)
+        for i, v in enumerate(self.values):
+            for k in range(8):
+                arr[i, k] = (v >> (32 * k)) & 0xFFFFFFFF
+        return arr
+
+
+class TapeBuilder:
+    """Builds one tape; nodes are hash-consed (structurally equal terms share one node)."""
+
+    def __init__(self, pool: ConstPool, var_index: Dict[str, int]):
+        self.pool = pool
+        self.var_index = var_index
+        self.nodes: List[Tuple[int, int, int, int, int, int, int]] = []
+        self.widths: List[int] = []
+        self._memo: Dict[tuple, int] = {}
+
+    # -- node creation ------------------------------------------------------------------------
+    def _add(self, op: Op, width: int, a=0, b=0, c=0, imm0=0, imm1=0) -> int:
+        key = (int(op), width, a, b, c, imm0, imm1)
+        got = self._memo.get(key)
+        if got is not None:
+            return got
+        idx = len(self.nodes)
+        self.nodes.append(key)
+        self.widths.append(width)
+        self._memo[key] = idx
+        return idx
+
+    def width(self, n: int) -> int:
+        return self.widths[n]
+
+    def const(self, value: int, width: int) -> int:
+        if not 1 <= width <= 256:
+            raise TapeError("constants are 1..256 bits wide (use concat for wider): %d" % width)
+        value &= (1 << width) - 1
+        return self._add(Op.CONST, width, imm0=self.pool.add(value))
+
+    def var(self, name: str, width: int = 256) -> int:
+        if not 1 <= width <= 256:
+            raise TapeError("variables are 1..256 bits wide: %d" % width)
+        if name not in self.var_index:
+            self.var_index[name] = len(self.var_index)
+        return self._add(Op.VAR, width, imm0=self.var_index[name])
+
+    def true(self) -> int:
+        return self._add(Op.TRUE, BOOL)
+
+    def false(self) -> int:
+        return self._add(Op.FALSE, BOOL)
+
+    def op(self, op: Op, *args: int, imm0: int = 0, imm1: int = 0) -> int:
+        op = Op(op)
+        ws = [self.widths[x] for x in args]
+        if len(args) != ARITY[op]:
+            raise TapeError("%s takes %d operands" % (op.name, ARITY[op]))
+        if op in BV_BINARY:
+            if ws[0] == BOOL or ws[0] != ws[1]:
+                raise TapeError("%s needs equal bit-vector widths, got %s" % (op.name, ws))
+            w = ws[0]
+        elif op in BV_COMPARE:
+            if ws[0] == BOOL or ws[0] != ws[1]:
+                raise TapeError("%s needs equal bit-vector widths, got %s" % (op.name, ws))
+            w = BOOL
+        elif op in (Op.BVNEG, Op.BVNOT):
+            if ws[0] == BOOL:
+                raise TapeError("%s needs a bit-vector" % op.name)
+            w = ws[0]
+        elif op == Op.EQ:
+            if ws[0] != ws[1]:
+                raise TapeError("EQ needs equal sorts, got %s" % ws)
+            w = BOOL
+        elif op in BOOL_BINARY or op == Op.NOT:
+            if any(x != BOOL for x in ws):
+                raise TapeError("%s needs Bool operands" % op.name)
+            w = BOOL
+        elif op == Op.ITE:
+            if ws[0] != BOOL or ws[1] != ws[2]:
+                raise TapeError("ITE needs (Bool, s, s), got %s" % ws)
+            w = ws[1]
+        elif op == Op.EXTRACT:
+            hi, lo = imm0, imm1
+            if ws[0] == BOOL or not (0 <= lo <= hi < ws[0]):
+                raise TapeError("bad extract [%d:%d] of width %d" % (hi, lo, ws[0]))
+            w = hi - lo + 1
+        elif op == Op.CONCAT:
+            if BOOL in ws:
+                raise TapeError("CONCAT needs bit-vectors")
+            w = ws[0] + ws[1]
+        elif op in (Op.ZEXT, Op.SEXT):
+            if ws[0] == BOOL:
+                raise TapeError("%s needs a bit-vector" % op.name)
+            w = ws[0] + imm0
+        elif op == Op.KECCAK:
+            if ws[0] == BOOL or ws[0] % 8:
+                raise TapeError("KECCAK input must be a whole number of bytes, got %d" % ws[0])
+            w = 256
+        else:
+            raise TapeError("op %s is not built with op()" % op.name)
+        if w > MAX_WIDTH:
+            raise TapeError("width %d exceeds %d" % (w, MAX_WIDTH))
+        a, b, c = (list(args) + [0, 0, 0])[:3]
+        return self._add(op, w, a, b, c, imm0, imm1)
+
+    def finish(self, root: int) -> "Tape":
+        """Return the tape of the sub-DAG reachable from ``root`` (root last, topological)."""
+        order: List[int] = []
+        seen = set()
+        stack = [(root, False)]
+        while stack:
+            n, done = stack.pop()
+            if done:
+                order.append(n)
+                continue
+            if n in seen:
+                continue
+            seen.add(n)
+            stack.append((n, True))
+            op = Op(self.nodes[n][0])
+            k = ARITY[op]
+            for child in reversed(self.nodes[n][2 : 2 + k]):
+                if child not in seen:
+                    stack.append((child, False))
+        remap = {old: new for new, old in enumerate(order)}
+        arr = np.zeros(len(order), dtype=NODE_DTYPE)
+        for new, old in enumerate(order):
+            op, w, a, b, c, i0, i1 = self.nodes[old]
+            k = ARITY[Op(op)]
+            opnds = [a, b, c]
+            for j in range(k):
+                opnds[j] = remap[opnds[j]]
+            for j in range(k, 3):
+                opnds[j] = 0
+            arr[new] = (op, 0, w, opnds[0], opnds[1], opnds[2], i0, i1)
+        return Tape(arr)
+
+
+@dataclass
+class Tape:
+    nodes: np.ndarray  # NODE_DTYPE, root last
+
+    @property
+    def root_width(self) -> int:
+        return int(self.nodes[-1]["width"])
+
+    def __len__(self) -> int:
+        return len(self.nodes)
+
+
+class TapeSet:
+    """A batch of tapes sharing one constant pool and one assignment schema (variable columns)."""
+
+    def __init__(self, var_names: Sequence[str] = ()):
+        self.pool = ConstPool()
+        self.var_index: Dict[str, int] = {}
+        for n in var_names:
+            self.var_index.setdefault(n, len(self.var_index))
+        self.tapes: List[Tape] = []
+
+    def builder(self) -> TapeBuilder:
+        return TapeBuilder(self.pool, self.var_index)
+
+    def add(self, tape: Tape) -> int:
+        self.tapes.append(tape)
+        return len(self.tapes) - 1
+
+    @property
+    def n_vars(self) -> int:
+        return len(self.var_index)
+
+    @property
+    def var_names(self) -> List[str]:
+        return [n for n, _ in sorted(self.var_index.items(), key=lambda kv: kv[1])]
+
+    def flatten(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(nodes, tape_offsets[n+1] as u64, consts[n_consts, 8] as u32) for mh_tapes_compile."""
+        offs = np.zeros(len(self.tapes) + 1, dtype=np.uint64)
+        for i, t in enumerate(self.tapes):
+            offs[i + 1] = offs[i] + len(t.nodes)
+        nodes = (
+            np.concatenate([t.nodes for t in self.tapes])
+            if self.tapes
+            else np.zeros(0, dtype=NODE_DTYPE)
+        )
+        return nodes, offs, self.pool.to_array()
+
+    def save(self, path: str) -> None:
+        nodes, offs, consts = self.flatten()
+        np.savez_compressed(
+            path,
+            nodes=nodes.view(np.uint8),
+            offsets=offs,
+            consts=consts,
+            var_names=np.array(self.var_names, dtype=object).astype(str),
+        )
+
+    @classmethod
+    def load(cls, path: str) -> "TapeSet":
+        z = np.load(path, allow_pickle=False)
+        ts = cls([str(x) for x in z["var_names"]])
+        consts = z["consts"]
+        for row in consts:
+            v = limbs_to_int(row)
+            ts.pool.index.setdefault(v, len(ts.pool.values))
+            ts.pool.values.append(v)
+        nodes = z["nodes"].view(NODE_DTYPE)
+        offs = z["offsets"]
+        for i in range(len(offs) - 1):
+            ts.tapes.append(Tape(nodes[int(offs[i]) : int(offs[i + 1])].copy()))
+        return ts
+
+
+def limbs_to_int(limbs: Sequence[int]) -> int:
+    v = 0
+    for k, x in enumerate(limbs):
+        v |= int(x) << (32 * k)
+    return v
+
+
+def int_to_limbs(v: int, n: int = 8) -> List[int]:
+    return [(v >> (32 * k)) & 0xFFFFFFFF for k in range(n)]
