@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Sieve throughput on BASELINE.json config 5.
+
+One step = every tape of the synthetic tape set (10^4 seeded random 256-bit constraint tapes,
+mythril_amd/synth_spec.json) evaluated against this rank's shard of candidate assignments,
+resident in HBM (2^23 rows per GPU by default, i.e. 2^26 over 8 GPUs), in throughput mode: every
+(tape, assignment) pair is evaluated to its Bool (MH_MODE_COUNT_ALL), per-tape hit counts and
+smallest witnesses are reduced in LDS and flushed by atomics.  With N ranks the rows are sharded
+(weak scaling) and the only exchange is one all-reduce (MIN of witness index, SUM of counts) of
+2 x 8 B per tape over RCCL.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+NOMINAL_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # u32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
+PMC_SUMMARY = os.path.join(HERE, "profiles", "pmc_summary.json")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(ts, seed, seconds: float):
+    """Oracle port (oracle/tape_eval.c, OpenMP on all host cores) on a bounded sample."""
+    from oracle import ctape
+
+    return ctape.benchmark(ts, seed, seconds)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tapes", type=int, default=None, help="default: spec n_tapes (10^4)")
+    ap.add_argument("--rows-per-gpu", type=int, default=1 << 23)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from mythril_amd import native, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    stream = torch.cuda.current_stream(dev)
+
+    spec = synth.load_spec()
+    t0 = time.time()
+    ts = synth.generate(args.tapes)
+    n_tapes = len(ts.tapes)
+    ctx = native.Context(local_rank)
+    ctx.set_stream(stream.cuda_stream)
+    ct = ctx.compile(ts)
+    info = ct.info()
+    alg_ops_per_row = sum(int(i["alg_ops"]) for i in info)
+    rows = args.rows_per_gpu
+    seed = spec["assignment_seed"]
+    assign = ctx.assignments(ts.n_vars, rows)
+    assign.generate(seed, rank * rows)
+    fh = torch.empty(n_tapes, dtype=torch.int64, device=dev)
+    hc = torch.empty(n_tapes, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    log("[rank %d] setup %.1fs: %d tapes, %d insns, %d rows, %.0f alg-ops/row"
+        % (rank, time.time() - t0, n_tapes, sum(i["n_insns"] for i in info), rows,
+           alg_ops_per_row))
+
+    kernel_ms = []
+
+    def step(timed: bool):
+        native.results_reset(ctx, fh.data_ptr(), hc.data_ptr(), n_tapes)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        native.run_async(ctx, ct, assign, fh.data_ptr(), hc.data_ptr(), index_base=rank * rows,
+                         mode=native.MODE_COUNT_ALL)
+        e1.record(stream)
+        if world > 1:
+            f = torch.where(fh < 0, torch.full_like(fh, torch.iinfo(torch.int64).max), fh)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hc, op=dist.ReduceOp.SUM)
+        if timed:
+            kernel_ms.append((e0, e1))
+
+    for i in range(args.warmup):
+        step(False)
+        torch.cuda.synchronize(dev)
+        log("[rank %d] warmup %d done" % (rank, i))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(True)
+        if rank == 0:
+            torch.cuda.synchronize(dev)
+            log("[rank 0] step %d done" % i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kms = float(np.mean([a.elapsed_time(b) for a, b in kernel_ms]))
+    ms_per_step = elapsed * 1e3 / args.steps
+    evals_per_step = n_tapes * rows * world
+    value = evals_per_step / (ms_per_step / 1e3)
+    hits = int((hc > 0).sum().item())
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    achieved = alg_ops_per_row * rows / (kms / 1e3) / 1e12
+    try:
+        peak_measured = ctx.microbench(0) / 1e12
+    except Exception as e:  # pragma: no cover
+        log("microbench failed: %s" % e)
+        peak_measured = None
+    traffic = None
+    if os.path.exists(PMC_SUMMARY):
+        pmc = json.load(open(PMC_SUMMARY))
+        if pmc.get("tapes") == n_tapes and pmc.get("rows_per_gpu") == rows:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    line = {
+        "metric": "constraint-evals/sec",
+        "value": value,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded config-5 tapes, counter-based PRNG assignments)",
+        "config": {
+            "workload": "synthetic config 5: %d random 256-bit constraint tapes x %d "
+                        "assignments per GPU (2^26 total at 8 GPUs), throughput mode"
+                        % (n_tapes, rows),
+            "tapes": n_tapes,
+            "rows_per_gpu": rows,
+            "vars": ts.n_vars,
+            "mode": "count_all",
+            "parallelism": "dp%d (row shards, all-reduce of per-tape results)" % world,
+        },
+        "per_gpu": value / world,
+        "kernel_ms": kms,
+        "tapes_with_witness": hits,
+        "roofline": {
+            "bound": "valu",
+            "achieved": achieved,
+            "peak": NOMINAL_PEAK_TOPS,
+            "unit": "T u32-ops/s",
+            "frac": achieved / NOMINAL_PEAK_TOPS,
+            "traffic": traffic,
+            "peak_measured_add_chain": peak_measured,
+            "alg_ops_per_eval": alg_ops_per_row / n_tapes,
+        },
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(ts, seed, args.cpu_seconds)
+        except Exception as e:  # pragma: no cover
+            log("cpu baseline failed: %s" % e)
+            line["cpu_baseline"] = None
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

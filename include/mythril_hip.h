@@ -107,7 +107,8 @@ int32_t mh_device_count(int32_t* n);                   /* gfx950 devices visible
 
 int32_t mh_ctx_create(int32_t device, mh_ctx** out);
 int32_t mh_ctx_destroy(mh_ctx* ctx);
-/* Launch on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own.   */
+/* Launch on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream; 0/NULL is the
+ * null stream).  The ctx starts on a stream of its own.                                          */
 int32_t mh_ctx_set_stream(mh_ctx* ctx, void* hip_stream);
 int32_t mh_ctx_synchronize(mh_ctx* ctx);
 

@@ -183,13 +183,8 @@ int32_t mh_ctx_set_stream(mh_ctx* ctx, void* hip_stream) {
         MH_HIP(hipStreamSynchronize(ctx->stream));
         MH_HIP(hipStreamDestroy(ctx->stream));
     }
-    if (hip_stream) {
-        ctx->stream = (hipStream_t)hip_stream;
-        ctx->own_stream = false;
-    } else {
-        MH_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-        ctx->own_stream = true;
-    }
+    ctx->stream = (hipStream_t)hip_stream;  // NULL = the device's null stream
+    ctx->own_stream = false;
     return MH_OK;
 }
 
@@ -420,8 +415,9 @@ int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s) {
     MH_HIP(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    // ops per lane per iteration: kind 0 = 16 (two 8-limb chains), 1 = 8 mads, 2 = 16 (xor+add)
-    const double per_iter = kind == 0 ? 16.0 : kind == 1 ? 8.0 : 16.0;
+    // u32 ops per lane per iteration: kind 0 = 32 (4 x 8-limb add chains), 1 = 8 mads,
+    // 2 = 64 (32 xor + 32 add)
+    const double per_iter = kind == 0 ? 32.0 : kind == 1 ? 8.0 : 64.0;
     const double lanes = (double)blocks * 256.0;
     *ops_per_s = lanes * iters * per_iter / (ms * 1e-3);
     return MH_OK;

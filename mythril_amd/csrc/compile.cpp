@@ -62,8 +62,9 @@ struct Piece {
 // most significant piece first).
 struct Val {
     int vreg = -1;
+    int remat = -1;  // constant node re-materialised at every use (keeps pressure low)
     std::vector<Piece> pieces;
-    bool wide() const { return vreg < 0; }
+    bool wide() const { return !pieces.empty(); }
 };
 
 struct Lowering {
@@ -127,9 +128,25 @@ struct Lowering {
         return false;
     }
 
+    std::vector<Val>* vals_ = nullptr;
+
+    // register holding narrow value k (constants are re-loaded at each use)
+    int vreg_of(uint32_t k) {
+        const Val& v = (*vals_)[k];
+        if (v.wide()) return -1;
+        if (v.remat >= 0) {
+            const mh_node& c = t[(size_t)v.remat];
+            if (c.op == MH_OP_TRUE) return emit(D_TRUE, -1, -1, -1, 1);
+            if (c.op == MH_OP_FALSE) return emit(D_FALSE, -1, -1, -1, 1);
+            return load_const(consts + 8ull * c.imm0, c.width);
+        }
+        return v.vreg;
+    }
+
     // pieces of a value (a narrow value is one piece)
-    std::vector<Piece> pieces_of(const Val& v, uint32_t width) {
-        if (!v.wide()) return {Piece{v.vreg, width}};
+    std::vector<Piece> pieces_of(uint32_t k, uint32_t width) {
+        const Val& v = (*vals_)[k];
+        if (!v.wide()) return {Piece{vreg_of(k), width}};
         return v.pieces;
     }
 
@@ -155,23 +172,65 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
         }
     }
     vals.assign(n, Val());
+    vals_ = &vals;
+    // evaluation order: post-order DFS from the root, operands with the larger Sethi-Ullman
+    // register need first (the input order is only required to be topological)
+    std::vector<uint32_t> need(n, 1);
+    auto arity = [&](const mh_node& nd) -> int {
+        return (nd.op <= MH_OP_FALSE) ? 0 : (nd.op == MH_OP_ITE) ? 3
+               : (nd.op == MH_OP_BVNEG || nd.op == MH_OP_BVNOT || nd.op == MH_OP_NOT ||
+                  nd.op == MH_OP_EXTRACT || nd.op == MH_OP_ZEXT || nd.op == MH_OP_SEXT ||
+                  nd.op == MH_OP_KECCAK) ? 1 : 2;
+    };
+    auto children = [&](size_t i, uint32_t* ch) -> int {
+        const mh_node& nd = t[i];
+        const int ar = arity(nd);
+        const uint32_t ops[3] = {nd.a, nd.b, nd.c};
+        for (int k = 0; k < ar; ++k) ch[k] = ops[k];
+        std::stable_sort(ch, ch + ar, [&](uint32_t x, uint32_t y) { return need[x] > need[y]; });
+        return ar;
+    };
     for (size_t i = 0; i < n; ++i) {
-        if (!live[i]) continue;
+        const mh_node& nd = t[i];
+        if (nd.op == MH_OP_VAR && pinned) { need[i] = 0; continue; }
+        uint32_t ch[3];
+        const int ar = children(i, ch);
+        uint32_t m = 1;
+        for (int k = 0; k < ar; ++k) m = std::max<uint32_t>(m, need[ch[k]] + (uint32_t)k);
+        need[i] = m;
+    }
+    std::vector<uint32_t> order;
+    order.reserve(n);
+    {
+        std::vector<char> seen(n, 0);
+        std::vector<std::pair<uint32_t, bool>> st;
+        st.push_back({(uint32_t)(n - 1), false});
+        while (!st.empty()) {
+            auto [x, done] = st.back();
+            st.pop_back();
+            if (done) { order.push_back(x); continue; }
+            if (seen[x]) continue;
+            seen[x] = 1;
+            st.push_back({x, true});
+            uint32_t ch[3];
+            const int ar = children(x, ch);
+            for (int k = ar - 1; k >= 0; --k)
+                if (!seen[ch[k]]) st.push_back({ch[k], false});
+        }
+    }
+    for (const uint32_t i : order) {
         const mh_node& nd = t[i];
         const uint32_t w = nd.width;
-        if (w > 512) return fail("width > 512");
+        if (w > 1088) return fail("width > 1088");
         auto V = [&](uint32_t k) -> const Val& { return vals[k]; };
         auto W = [&](uint32_t k) -> uint32_t { return t[k].width; };
-        auto narrow = [&](uint32_t k) -> int {
-            if (vals[k].wide()) return -1;
-            return vals[k].vreg;
-        };
+        auto narrow = [&](uint32_t k) -> int { return vreg_of(k); };
         Val out;
         switch (nd.op) {
             case MH_OP_CONST: {
                 if (nd.imm0 >= n_consts) return fail("const index out of range");
                 if (w == 0 || w > 256) return fail("const width");
-                out.vreg = load_const(consts + 8ull * nd.imm0, w);
+                out.remat = (int)i;
                 break;
             }
             case MH_OP_VAR: {
@@ -187,8 +246,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 out.vreg = r;
                 break;
             }
-            case MH_OP_TRUE: out.vreg = emit(D_TRUE, -1, -1, -1, 1); break;
-            case MH_OP_FALSE: out.vreg = emit(D_FALSE, -1, -1, -1, 1); break;
+            case MH_OP_TRUE: case MH_OP_FALSE: out.remat = (int)i; break;
             case MH_OP_BVADD: case MH_OP_BVSUB: case MH_OP_BVMUL: case MH_OP_BVAND:
             case MH_OP_BVOR: case MH_OP_BVXOR: case MH_OP_BVUDIV: case MH_OP_BVUREM:
             case MH_OP_BVSDIV: case MH_OP_BVSREM: case MH_OP_BVSMOD: case MH_OP_EVM_EXP:
@@ -336,8 +394,8 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 if (w <= 256) {
                     out.vreg = emit(D_CONCAT, narrow(nd.a), narrow(nd.b), -1, w, wb);
                 } else {
-                    out.pieces = pieces_of(V(nd.a), wa);
-                    auto pb = pieces_of(V(nd.b), wb);
+                    out.pieces = pieces_of(nd.a, wa);
+                    auto pb = pieces_of(nd.b, wb);
                     out.pieces.insert(out.pieces.end(), pb.begin(), pb.end());
                 }
                 break;
@@ -347,6 +405,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 if (wa == 0 || wa + nd.imm0 != w) return fail("bad zero_extend");
                 if (w <= 256) {
                     out.vreg = V(nd.a).vreg;  // canonical values: zero extension is free
+                    out.remat = V(nd.a).remat;
                 } else {
                     int z = zero_reg();
                     uint32_t left = nd.imm0;
@@ -355,7 +414,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                         out.pieces.push_back(Piece{z, take});
                         left -= take;
                     }
-                    auto pa = pieces_of(V(nd.a), wa);
+                    auto pa = pieces_of(nd.a, wa);
                     out.pieces.insert(out.pieces.end(), pa.begin(), pa.end());
                 }
                 break;
@@ -369,7 +428,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             case MH_OP_KECCAK: {
                 const uint32_t wa = W(nd.a);
                 if (wa == 0 || wa % 8 || w != 256) return fail("bad keccak input");
-                auto ps = pieces_of(V(nd.a), wa);
+                auto ps = pieces_of(nd.a, wa);
                 // merge into byte-aligned chunks of <= 256 bits
                 std::vector<Piece> chunks;
                 int cur = -1;
@@ -413,7 +472,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
     }
     const Val& rv = vals[n - 1];
     if (rv.wide()) return fail("root wider than 256 bits");
-    *root_reg = (uint32_t)rv.vreg;
+    *root_reg = (uint32_t)vreg_of((uint32_t)(n - 1));
     *root_bool = t[n - 1].width == 0;
     return true;
 }

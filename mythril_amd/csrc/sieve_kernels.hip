@@ -363,48 +363,50 @@ __global__ void __launch_bounds__(kBlock) generate_kernel(u32* assign, u64 capac
     }
 }
 
-// Integer VALU throughput probe: 8 independent dependency chains per lane.
+// Integer VALU throughput probe: independent dependency chains per lane (enough ILP that the
+// measured rate is issue-bound, not latency-bound).
 __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters, u32* sink) {
-    u32 s[8];
+    u32 s[4][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s[k] = threadIdx.x * 2654435761u + k;
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[j][k] = threadIdx.x * 2654435761u + 8 * j + k;
     const u32 y = blockIdx.x | 1u;
-    if (kind == 0) {
+    if (kind == 0) {  // 4 independent 256-bit add-with-carry chains: 32 ops / iteration
         for (u32 i = 0; i < iters; ++i) {
-            u64 c = 0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {  // 8-limb carry chain: 8 ops
-                c = (u64)s[k] + (s[(k + 3) & 7] ^ y) + c;
-                s[k] = (u32)c;
-                c >>= 32;
-            }
-            u64 c2 = 0;
+            for (int j = 0; j < 4; ++j) {
+                u64 c = y;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                c2 = (u64)s[k] + y + c2;
-                s[k] = (u32)c2;
-                c2 >>= 32;
+                for (int k = 0; k < 8; ++k) {
+                    c = (u64)s[j][k] + s[(j + 1) & 3][k] + (c >> 32);
+                    s[j][k] = (u32)c;
+                }
             }
         }
-    } else if (kind == 1) {
+    } else if (kind == 1) {  // v_mad_u64_u32: 8 independent chains, 8 mads / iteration
         u64 acc[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = s[k];
+        for (int k = 0; k < 8; ++k) acc[k] = s[0][k];
         for (u32 i = 0; i < iters; ++i) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc[k] = (u64)(u32)acc[k] * (y + k) + (acc[k] >> 32);
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s[k] = (u32)acc[k] ^ (u32)(acc[k] >> 32);
-    } else {
+        for (int k = 0; k < 8; ++k) s[0][k] = (u32)acc[k] ^ (u32)(acc[k] >> 32);
+    } else {  // xor/add mix: 32 independent ops / iteration
         for (u32 i = 0; i < iters; ++i) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) s[k] = (s[k] ^ y) + s[(k + 1) & 7];
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s[j][k] = (s[j][k] ^ y) + k;
         }
     }
     u32 r = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) r ^= s[k];
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r ^= s[j][k];
     if (r == 0x12345678u) sink[0] = r;
 }
 

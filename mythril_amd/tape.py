@@ -21,7 +21,7 @@ from typing import Dict, List, Sequence, Tuple
 import numpy as np
 
 BOOL = 0
-MAX_WIDTH = 512
+MAX_WIDTH = 1088  # 136 bytes: one Keccak block
 
 
 class Op(enum.IntEnum):
