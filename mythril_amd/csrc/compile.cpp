@@ -48,9 +48,10 @@ struct VInsn {
     uint8_t op;
     int d, a, b, c;   // virtual registers (-1 = none)
     uint32_t width;   // 1..256
-    uint32_t aux;     // 15-bit immediate
-    uint32_t w1raw;   // full second word (LOADC, KECCAK); used when raw == true
+    uint32_t aux;     // 21-bit immediate (constant index for D_LOADC / constant operands)
+    uint32_t w1raw;   // full second word (D_KECCAK); used when raw == true
     bool raw;
+    uint8_t flags;    // F_ACONST / F_BCONST
 };
 
 struct Piece {
@@ -91,9 +92,38 @@ struct Lowering {
 
     int emit(uint8_t op, int a = -1, int b = -1, int c = -1, uint32_t width = 256,
              uint32_t aux = 0) {
-        VInsn v{op, fresh(), a, b, c, width, aux, 0, false};
+        VInsn v{op, fresh(), a, b, c, width, aux, 0, false, 0};
         code.push_back(v);
         return v.d;
+    }
+
+    bool is_const_node(uint32_t k) const {
+        const Val& v = (*vals_)[k];
+        return !v.wide() && v.remat >= 0 && t[(size_t)v.remat].op == MH_OP_CONST;
+    }
+
+    uint32_t const_of(uint32_t k) {
+        const mh_node& c = t[(size_t)(*vals_)[k].remat];
+        return const_index(consts + 8ull * c.imm0, c.width);
+    }
+
+    // Binary op on IR nodes na, nb; a constant operand is folded into the instruction (read by
+    // the scalar unit from the constant pool) instead of being loaded into a register.
+    int emit_bin(uint8_t op, uint32_t na, uint32_t nb, uint32_t width, bool commutative) {
+        if ((MH_CONST_OPERAND_OK >> op) & 1) {
+            const bool ca = is_const_node(na), cb = is_const_node(nb);
+            if (cb || (ca && commutative)) {
+                const uint32_t kc = cb ? nb : na, kr = cb ? na : nb;
+                const int r = vreg_of(kr);
+                if (r < 0) return -1;
+                VInsn v{op, fresh(), r, -1, -1, width, const_of(kc), 0, false, F_BCONST};
+                code.push_back(v);
+                return v.d;
+            }
+        }
+        const int a = vreg_of(na), b = vreg_of(nb);
+        if (a < 0 || b < 0) return -1;
+        return emit(op, a, b, -1, width);
     }
 
     uint32_t const_index(const uint32_t* limbs, uint32_t width) {
@@ -113,7 +143,7 @@ struct Lowering {
     }
 
     int load_const(const uint32_t* limbs, uint32_t width) {
-        VInsn v{D_LOADC, fresh(), -1, -1, -1, width, 0, const_index(limbs, width), true};
+        VInsn v{D_LOADC, fresh(), -1, -1, -1, width, const_index(limbs, width), 0, false, 0};
         code.push_back(v);
         return v.d;
     }
@@ -251,8 +281,8 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             case MH_OP_BVOR: case MH_OP_BVXOR: case MH_OP_BVUDIV: case MH_OP_BVUREM:
             case MH_OP_BVSDIV: case MH_OP_BVSREM: case MH_OP_BVSMOD: case MH_OP_EVM_EXP:
             case MH_OP_EVM_SIGNEXTEND: case MH_OP_EVM_BYTE: {
-                int a = narrow(nd.a), b = narrow(nd.b);
-                if (a < 0 || b < 0 || w == 0 || w > 256 || W(nd.a) != w || W(nd.b) != w)
+                if (V(nd.a).wide() || V(nd.b).wide() || w == 0 || w > 256 || W(nd.a) != w ||
+                    W(nd.b) != w)
                     return fail("bit-vector op wider than 256 bits");
                 uint8_t op = 0;
                 switch (nd.op) {
@@ -273,12 +303,14 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 }
                 if ((op == D_SIGNEXT || op == D_BYTE) && w != 256)
                     return fail("EVM word ops are 256-bit");
-                out.vreg = emit(op, a, b, -1, w);
+                const bool comm = op == D_ADD || op == D_MUL || op == D_AND || op == D_OR ||
+                                  op == D_XOR;
+                out.vreg = emit_bin(op, nd.a, nd.b, w, comm);
                 break;
             }
             case MH_OP_BVSHL: case MH_OP_BVLSHR: case MH_OP_BVASHR: {
-                int a = narrow(nd.a), b = narrow(nd.b);
-                if (a < 0 || b < 0 || w == 0 || w > 256) return fail("shift wider than 256");
+                if (V(nd.a).wide() || V(nd.b).wide() || w == 0 || w > 256)
+                    return fail("shift wider than 256");
                 const mh_node& sn = t[nd.b];
                 if (sn.op == MH_OP_CONST) {  // uniform shift amount
                     const uint32_t* lim = consts + 8ull * sn.imm0;
@@ -290,11 +322,11 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                     if (s > 511) s = 511;
                     uint8_t op = nd.op == MH_OP_BVSHL ? D_SHLI : nd.op == MH_OP_BVLSHR ? D_LSHRI
                                                                                         : D_ASHRI;
-                    out.vreg = emit(op, a, -1, -1, w, s);
+                    out.vreg = emit(op, narrow(nd.a), -1, -1, w, s);
                 } else {
                     uint8_t op = nd.op == MH_OP_BVSHL ? D_SHL : nd.op == MH_OP_BVLSHR ? D_LSHR
                                                                                        : D_ASHR;
-                    out.vreg = emit(op, a, b, -1, w);
+                    out.vreg = emit_bin(op, nd.a, nd.b, w, false);
                 }
                 break;
             }
@@ -307,17 +339,16 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             case MH_OP_EQ: {
                 uint32_t wa = W(nd.a);
                 if (wa != W(nd.b)) return fail("EQ sort mismatch");
-                int a = narrow(nd.a), b = narrow(nd.b);
-                if (a < 0 || b < 0) return fail("EQ wider than 256 bits");
-                out.vreg = emit(wa == 0 ? D_BEQ : D_EQ, a, b, -1, wa == 0 ? 1 : wa);
+                if (V(nd.a).wide() || V(nd.b).wide()) return fail("EQ wider than 256 bits");
+                if (wa == 0) out.vreg = emit(D_BEQ, narrow(nd.a), narrow(nd.b), -1, 1);
+                else out.vreg = emit_bin(D_EQ, nd.a, nd.b, wa, true);
                 break;
             }
             case MH_OP_BVULT: case MH_OP_BVULE: case MH_OP_BVUGT: case MH_OP_BVUGE:
             case MH_OP_BVSLT: case MH_OP_BVSLE: case MH_OP_BVSGT: case MH_OP_BVSGE:
             case MH_OP_BVADD_NOOVFL_U: case MH_OP_BVMUL_NOOVFL_U: case MH_OP_BVSUB_NOUDFL_U: {
                 uint32_t wa = W(nd.a);
-                int a = narrow(nd.a), b = narrow(nd.b);
-                if (a < 0 || b < 0 || wa == 0 || wa > 256 || W(nd.b) != wa)
+                if (V(nd.a).wide() || V(nd.b).wide() || wa == 0 || wa > 256 || W(nd.b) != wa)
                     return fail("compare wider than 256 bits");
                 uint8_t op = 0;
                 bool swap = false;
@@ -334,7 +365,9 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                     case MH_OP_BVMUL_NOOVFL_U: op = D_UMUL_NOOVFL; break;
                     case MH_OP_BVSUB_NOUDFL_U: op = D_ULE; swap = true; break;  // b <= a
                 }
-                out.vreg = swap ? emit(op, b, a, -1, wa) : emit(op, a, b, -1, wa);
+                out.vreg = swap ? emit_bin(op, nd.b, nd.a, wa, false)
+                                : emit_bin(op, nd.a, nd.b, wa, op == D_UADD_NOOVFL ||
+                                                               op == D_UMUL_NOOVFL);
                 break;
             }
             case MH_OP_AND: case MH_OP_OR: case MH_OP_XOR: {
@@ -455,7 +488,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 features |= F_KECCAK;
                 VInsn v{D_KECCAK, fresh(), chunks[0].vreg,
                         chunks.size() > 1 ? chunks[1].vreg : -1,
-                        chunks.size() > 2 ? chunks[2].vreg : -1, 256, 0, 0, true};
+                        chunks.size() > 2 ? chunks[2].vreg : -1, 256, 0, 0, true, 0};
                 uint32_t w1 = 0;
                 for (size_t k = 0; k < chunks.size(); ++k)
                     w1 |= (chunks[k].bits / 8) << (8 + 6 * k);
@@ -468,6 +501,8 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             default:
                 return fail("unknown op " + std::to_string(nd.op));
         }
+        if (!out.wide() && out.vreg < 0 && out.remat < 0)
+            return fail("operand wider than 256 bits");
         vals[i] = std::move(out);
     }
     const Val& rv = vals[n - 1];
@@ -560,12 +595,15 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
         auto P = [&](int r) -> uint32_t { return r < 0 ? 0u : (uint32_t)phys[r]; };
         const uint32_t w0 = (uint32_t)v.op | (P(v.d) << 8) | (P(v.a) << 16) | (P(v.b) << 24);
         uint32_t w1;
-        if (v.op == D_LOADC) {
-            w1 = v.w1raw;
-        } else if (v.op == D_KECCAK) {
+        if (v.op == D_KECCAK) {
             w1 = v.w1raw | P(v.c);
         } else {
-            w1 = P(v.c) | ((v.width & 0x1FF) << 8) | ((v.aux & 0x7FFF) << 17);
+            const uint32_t aux = (v.op == D_ITE || v.op == D_BITE) ? P(v.c) : v.aux;
+            if (aux > MH_AUX_MAX) {
+                err = "immediate / constant index exceeds 21 bits";
+                return MH_E_UNSUPPORTED;
+            }
+            w1 = (uint32_t)v.flags | ((v.width & 0x1FF) << 2) | (aux << 11);
         }
         words.push_back(w0);
         words.push_back(w1);

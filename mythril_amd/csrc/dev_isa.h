@@ -5,50 +5,74 @@
 //
 // Encoding: two u32 words per instruction.
 //   w0 = op | d << 8 | a << 16 | b << 24
-//   w1 = c | width << 8 | aux << 17        (width 1..256; aux 15 bits)
-//   D_LOADC uses all of w1 as the constant-pool index.
-// Op ranges select the operand class the interpreter reads/writes:
-//   [1,32)   bv x bv -> bv        reads R[a], R[b]; writes 8 limbs of R[d]
-//   [32,48)  bv -> bv             reads R[a]
-//   [48,64)  bv x bv -> Bool      writes limb 0 of R[d] (0/1); Bool registers only use limb 0
-//   [64,80)  Bool ops             read/write limb 0
-//   [80,96)  others (ite, loads, keccak)
+//   w1 = flags | width << 2 | aux << 11      (flags bit 0: operand a is constant aux,
+//                                              bit 1: operand b is constant aux; width 1..256)
+//   D_ITE: aux = c (else register).  D_LOADC: aux = constant index.
+//   D_KECCAK: w1 = c | n0 << 8 | n1 << 14 | n2 << 20 | npieces << 26 (n_i = bytes of piece i).
+// Constant operands are read by the scalar unit straight from the constant pool: no register,
+// no load instruction, no register-file traffic for them.
 #pragma once
 #include <stdint.h>
 
 #ifndef MH_NUM_REGS
-#define MH_NUM_REGS 16
+#define MH_NUM_REGS 12
 #endif
 #define MH_MAX_PRELOAD 4   // assignment columns kept resident in R0..R3 for the whole launch
 
 enum mh_dop : uint8_t {
     D_NOP = 0,
     // bv x bv -> bv
-    D_ADD = 1, D_SUB, D_MUL, D_AND, D_OR, D_XOR, D_SHL, D_LSHR, D_ASHR,
+    D_ADD, D_SUB, D_MUL, D_AND, D_OR, D_XOR, D_SHL, D_LSHR, D_ASHR,
     D_UDIV, D_UREM, D_SDIV, D_SREM, D_SMOD, D_EXP, D_SIGNEXT, D_BYTE,
     D_CONCAT,                       // a = high, b = low, aux = width of b
     // bv -> bv
-    D_NEG = 32, D_NOT, D_MOV, D_SHLI, D_LSHRI, D_ASHRI, D_EXTRACT, D_SEXT,
-    // bv x bv -> Bool
-    D_EQ = 48, D_ULT, D_ULE, D_SLT, D_SLE, D_UADD_NOOVFL, D_UMUL_NOOVFL,
+    D_NEG, D_NOT, D_MOV, D_SHLI, D_LSHRI, D_ASHRI, D_EXTRACT, D_SEXT,
+    // bv x bv -> Bool (0/1 in limb 0)
+    D_EQ, D_ULT, D_ULE, D_SLT, D_SLE, D_UADD_NOOVFL, D_UMUL_NOOVFL,
     // Bool
-    D_BAND = 64, D_BOR, D_BXOR, D_BEQ, D_BNOT, D_TRUE, D_FALSE,
+    D_BAND, D_BOR, D_BXOR, D_BEQ, D_BNOT, D_TRUE, D_FALSE,
     // others
-    D_ITE = 80,                     // a = Bool cond, b = then, c = else (bv)
-    D_BITE,                         // Bool-valued ite
-    D_LOADC,                        // w1 = const index
+    D_ITE,                          // a = Bool cond, b = then, aux = else register
+    D_BITE,                         // Bool-valued ite, aux = else register
+    D_LOADC,                        // aux = constant index
     D_LOADVAR,                      // aux = column
-    D_KECCAK                        // message = concat of up to 3 byte-aligned pieces a,b,c;
-                                    // w1: c | n0 << 8 | n1 << 14 | n2 << 20 | npieces << 26
-                                    //     (n_i = bytes of piece i, 1..32)
+    D_KECCAK,                       // message = concat of up to 3 byte-aligned pieces a, b, c
+    D_NUM_OPS
 };
 
-enum { D_CLASS_VVV = 0, D_CLASS_VV = 1, D_CLASS_VVB = 2, D_CLASS_BOOL = 3, D_CLASS_MISC = 4 };
+static_assert(D_NUM_OPS <= 64, "operand masks are 64-bit");
 
-static inline int mh_dop_class(uint32_t op) {
-    return op < 32 ? D_CLASS_VVV : op < 48 ? D_CLASS_VV : op < 64 ? D_CLASS_VVB
-         : op < 80 ? D_CLASS_BOOL : D_CLASS_MISC;
-}
+#define MH_BIT(op) (1ull << (op))
+// ops that read operand a / operand b as a full 8-limb value
+#define MH_READS_A                                                                             \
+    (MH_BIT(D_ADD) | MH_BIT(D_SUB) | MH_BIT(D_MUL) | MH_BIT(D_AND) | MH_BIT(D_OR) |          \
+     MH_BIT(D_XOR) | MH_BIT(D_SHL) | MH_BIT(D_LSHR) | MH_BIT(D_ASHR) | MH_BIT(D_UDIV) |      \
+     MH_BIT(D_UREM) | MH_BIT(D_SDIV) | MH_BIT(D_SREM) | MH_BIT(D_SMOD) | MH_BIT(D_EXP) |     \
+     MH_BIT(D_SIGNEXT) | MH_BIT(D_BYTE) | MH_BIT(D_CONCAT) | MH_BIT(D_NEG) | MH_BIT(D_NOT) | \
+     MH_BIT(D_MOV) | MH_BIT(D_SHLI) | MH_BIT(D_LSHRI) | MH_BIT(D_ASHRI) | MH_BIT(D_EXTRACT) | \
+     MH_BIT(D_SEXT) | MH_BIT(D_EQ) | MH_BIT(D_ULT) | MH_BIT(D_ULE) | MH_BIT(D_SLT) |         \
+     MH_BIT(D_SLE) | MH_BIT(D_UADD_NOOVFL) | MH_BIT(D_UMUL_NOOVFL) | MH_BIT(D_KECCAK))
+#define MH_READS_B                                                                             \
+    (MH_BIT(D_ADD) | MH_BIT(D_SUB) | MH_BIT(D_MUL) | MH_BIT(D_AND) | MH_BIT(D_OR) |          \
+     MH_BIT(D_XOR) | MH_BIT(D_SHL) | MH_BIT(D_LSHR) | MH_BIT(D_ASHR) | MH_BIT(D_UDIV) |      \
+     MH_BIT(D_UREM) | MH_BIT(D_SDIV) | MH_BIT(D_SREM) | MH_BIT(D_SMOD) | MH_BIT(D_EXP) |     \
+     MH_BIT(D_SIGNEXT) | MH_BIT(D_BYTE) | MH_BIT(D_CONCAT) | MH_BIT(D_EQ) | MH_BIT(D_ULT) |  \
+     MH_BIT(D_ULE) | MH_BIT(D_SLT) | MH_BIT(D_SLE) | MH_BIT(D_UADD_NOOVFL) |                 \
+     MH_BIT(D_UMUL_NOOVFL) | MH_BIT(D_ITE) | MH_BIT(D_KECCAK))
+// ops whose operands are Bools (limb 0 only)
+#define MH_BOOL_IN                                                                             \
+    (MH_BIT(D_BAND) | MH_BIT(D_BOR) | MH_BIT(D_BXOR) | MH_BIT(D_BEQ) | MH_BIT(D_BNOT) |      \
+     MH_BIT(D_ITE) | MH_BIT(D_BITE))
+// ops that may take a constant operand (flags) — binary ops without other uses of aux
+#define MH_CONST_OPERAND_OK                                                                    \
+    (MH_BIT(D_ADD) | MH_BIT(D_SUB) | MH_BIT(D_MUL) | MH_BIT(D_AND) | MH_BIT(D_OR) |          \
+     MH_BIT(D_XOR) | MH_BIT(D_SHL) | MH_BIT(D_LSHR) | MH_BIT(D_ASHR) | MH_BIT(D_UDIV) |      \
+     MH_BIT(D_UREM) | MH_BIT(D_SDIV) | MH_BIT(D_SREM) | MH_BIT(D_SMOD) | MH_BIT(D_EXP) |     \
+     MH_BIT(D_SIGNEXT) | MH_BIT(D_BYTE) | MH_BIT(D_EQ) | MH_BIT(D_ULT) | MH_BIT(D_ULE) |     \
+     MH_BIT(D_SLT) | MH_BIT(D_SLE) | MH_BIT(D_UADD_NOOVFL) | MH_BIT(D_UMUL_NOOVFL))
+
+enum { F_ACONST = 1, F_BCONST = 2 };
+#define MH_AUX_MAX ((1u << 21) - 1)
 
 // Feature bits (mh_tape_info.features) — select the kernel variant.
 enum { F_DIV = 1, F_KECCAK = 2, F_EVM = 4 };

@@ -101,21 +101,50 @@ __device__ __forceinline__ TapeHead tape_head(const KParams& p, u32 t) {
     return TapeHead{tp[0], tp[1], tp[2], tp[3]};
 }
 
-// One instruction = one read of R[a], R[b] (and R[c] for ite/keccak), one compute, one write
-// of R[d]: a single definition of the register-file vectors per step keeps the compiler from
+// Instruction stream: lane j of the wave holds instruction (64*chunk + j) of the current tape
+// in two VGPRs (one coalesced 512-B load per 64 instructions, prefetched one tape ahead); the
+// interpreter extracts instruction i with v_readlane into SGPRs, so fetching costs no memory
+// round trip per instruction.
+struct InsnCache {
+    u32 w0, w1;
+};
+
+__device__ __forceinline__ InsnCache load_insns(const KParams& p, u32 insn_off, u32 n, u32 first) {
+    const u32 lane = threadIdx.x & 63u;
+    const u32 j = first + lane;
+    InsnCache c{0u, 0u};
+    if (j < n) {
+        const uint2 v = p.insns[insn_off + j];
+        c.w0 = v.x;
+        c.w1 = v.y;
+    }
+    return c;
+}
+
+__device__ __forceinline__ void load_const(const KParams& p, u32 idx, u32* z) {
+    const cu32_ptr cp = (cu32_ptr)p.consts + 8ull * idx;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) z[k] = cp[k];
+}
+
+// One instruction = operand reads (register file or scalar constant), one compute, one write of
+// R[d]: a single definition of the register-file vectors per step keeps the compiler from
 // materialising copies of the whole file on every control-flow merge.
 template <int NR, int FEAT>
-__device__ __forceinline__ void exec_tape(RegFile<NR>& R, const KParams& p, cu32_ptr ip,
-                                          u32 n, u64 lrow) {
+__device__ __forceinline__ void exec_tape(RegFile<NR>& R, const KParams& p, InsnCache ic,
+                                          u32 insn_off, u32 n, u64 lrow) {
     for (u32 i = 0; i < n; ++i) {
-        const u32 w0 = ip[2 * i], w1 = ip[2 * i + 1];
+        if ((i & 63u) == 0 && i) ic = load_insns(p, insn_off, n, i);  // tapes > 64 insns
+        const u32 w0 = __builtin_amdgcn_readlane(ic.w0, i & 63u);
+        const u32 w1 = __builtin_amdgcn_readlane(ic.w1, i & 63u);
         const u32 op = w0 & 0xFFu, d = (w0 >> 8) & 0xFFu, a = (w0 >> 16) & 0xFFu, b = w0 >> 24;
-        const u32 c = w1 & 0xFFu, w = (w1 >> 8) & 0x1FFu, aux = w1 >> 17;
+        const u32 w = (w1 >> 2) & 0x1FFu, aux = w1 >> 11;
         u32 x[8], y[8], z[8];
+        // unconditional register reads (no control-flow merge of operand values); a constant
+        // operand b overwrites y from the scalar constant pool
         R.read(a, x);
         R.read(b, y);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) z[k] = 0;
+        if (((MH_CONST_OPERAND_OK >> op) & 1u) && (w1 & F_BCONST)) load_const(p, aux, y);
         switch (op) {
             // ---- bv x bv -> bv
             case D_ADD: add256(x, y, z); mask_w(z, w); break;
@@ -208,18 +237,18 @@ __device__ __forceinline__ void exec_tape(RegFile<NR>& R, const KParams& p, cu32
                 z[0] = hi == 0;
                 break;
             }
-            // ---- Bool
+            // ---- Bool (limb 0)
             case D_BAND: z[0] = x[0] & y[0] & 1u; break;
             case D_BOR: z[0] = (x[0] | y[0]) & 1u; break;
             case D_BXOR: z[0] = (x[0] ^ y[0]) & 1u; break;
             case D_BEQ: z[0] = ((x[0] ^ y[0]) & 1u) ^ 1u; break;
             case D_BNOT: z[0] = (x[0] & 1u) ^ 1u; break;
             case D_TRUE: z[0] = 1u; break;
-            case D_FALSE: break;
+            case D_FALSE: z[0] = 0u; break;
             // ---- others
-            case D_ITE: {  // x = cond, y = then, R[c] = else
+            case D_ITE: {  // x[0] = cond, y = then, R[aux] = else
                 u32 e[8];
-                R.read(c, e);
+                R.read(aux, e);
                 const bool cnd = (x[0] & 1u) != 0;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) z[k] = cnd ? y[k] : e[k];
@@ -227,15 +256,10 @@ __device__ __forceinline__ void exec_tape(RegFile<NR>& R, const KParams& p, cu32
             }
             case D_BITE: {
                 const bool cnd = (x[0] & 1u) != 0;
-                z[0] = cnd ? (y[0] & 1u) : (R.read0(c) & 1u);
+                z[0] = cnd ? (y[0] & 1u) : (R.read0(aux) & 1u);
                 break;
             }
-            case D_LOADC: {
-                const cu32_ptr cp = (cu32_ptr)p.consts + 8ull * w1;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = cp[k];
-                break;
-            }
+            case D_LOADC: load_const(p, aux, z); break;
             case D_LOADVAR:
 #pragma unroll
                 for (int k = 0; k < 8; ++k) z[k] = p.assign[((u64)aux * 8 + k) * p.capacity + lrow];
@@ -245,7 +269,7 @@ __device__ __forceinline__ void exec_tape(RegFile<NR>& R, const KParams& p, cu32
                     const u32 np = (w1 >> 26) & 3u;
                     const u32 n0 = (w1 >> 8) & 63u, n1 = (w1 >> 14) & 63u, n2 = (w1 >> 20) & 63u;
                     u32 P2[8];
-                    R.read(c, P2);
+                    R.read(w1 & 0xFFu, P2);
                     keccak_pieces(x, y, P2, n0, np > 1 ? n1 : 0u, np > 2 ? n2 : 0u, z);
                 }
                 break;
@@ -292,17 +316,25 @@ __global__ void __launch_bounds__(kBlock) sieve_kernel(const KParams p) {
             s_cnt[tid] = 0;
         }
         __syncthreads();
+        TapeHead th = tape_head(p, cb);
+        InsnCache ic = load_insns(p, th.insn_off, th.n_insns, 0);
         for (u32 j = 0; j < nt; ++j) {
             const u32 t = cb + j;
+            // prefetch the next tape's header and first 64 instructions
+            const TapeHead th_next = tape_head(p, j + 1 < nt ? t + 1 : t);
+            const InsnCache ic_next = load_insns(p, th_next.insn_off, th_next.n_insns, 0);
             if (p.mode == MH_MODE_FIRST_HIT) {
                 // early exit: a smaller witness is already known for this tape
                 const u64 km = s_min[j];
                 const u64 known = ((u64)__builtin_amdgcn_readfirstlane((u32)(km >> 32)) << 32) |
                                   __builtin_amdgcn_readfirstlane((u32)km);
-                if (known < wave_first) continue;
+                if (known < wave_first) {
+                    th = th_next;
+                    ic = ic_next;
+                    continue;
+                }
             }
-            const TapeHead th = tape_head(p, t);
-            exec_tape<NR, FEAT>(R, p, (cu32_ptr)p.insns + 2ull * th.insn_off, th.n_insns, lrow);
+            exec_tape<NR, FEAT>(R, p, ic, th.insn_off, th.n_insns, lrow);
             u32 res;
             if (th.root_bool) {
                 res = R.read0(th.root_reg) & 1u;
@@ -316,6 +348,8 @@ __global__ void __launch_bounds__(kBlock) sieve_kernel(const KParams p) {
                 atomicAdd(&s_cnt[j], (unsigned long long)__builtin_popcountll(mask));
                 atomicMin(&s_min[j], (unsigned long long)(wave_first + __builtin_ctzll(mask)));
             }
+            th = th_next;
+            ic = ic_next;
         }
         __syncthreads();
         if (tid < nt) {
@@ -335,8 +369,8 @@ __global__ void __launch_bounds__(kBlock) values_kernel(const KParams p, u32 tap
     const u64 lrow = p.row_first + (valid ? r : 0);
     preload<NR>(R, p, lrow);
     const TapeHead th = tape_head(p, tape);
-    exec_tape<NR, F_DIV | F_KECCAK | F_EVM>(R, p, (cu32_ptr)p.insns + 2ull * th.insn_off,
-                                            th.n_insns, lrow);
+    exec_tape<NR, F_DIV | F_KECCAK | F_EVM>(R, p, load_insns(p, th.insn_off, th.n_insns, 0),
+                                            th.insn_off, th.n_insns, lrow);
     u32 x[8];
     R.read(th.root_reg, x);
     if (th.root_bool) {

@@ -52,26 +52,39 @@ MH_FN bool any_lane(bool p) {
 #endif
 }
 
+// add / subtract with carry: v_add_co_u32 / v_addc_co_u32 (v_sub_co / v_subb_co) on gfx950
+MH_FN u32 addc32(u32 x, u32 y, u32 cin, u32* cout) {
+#if defined(__clang__)
+    return __builtin_addc(x, y, cin, cout);
+#else
+    const u64 t = (u64)x + y + cin;
+    *cout = (u32)(t >> 32);
+    return (u32)t;
+#endif
+}
+
+MH_FN u32 subc32(u32 x, u32 y, u32 bin, u32* bout) {
+#if defined(__clang__)
+    return __builtin_subc(x, y, bin, bout);
+#else
+    const u64 t = (u64)x - y - bin;
+    *bout = (u32)(t >> 63);
+    return (u32)t;
+#endif
+}
+
 // ---- basic ops ---------------------------------------------------------------------------------
 MH_FN u32 add256(const u32* x, const u32* y, u32* z) {  // returns carry out
-    u64 c = 0;
+    u32 c = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        c = (u64)x[k] + y[k] + c;
-        z[k] = (u32)c;
-        c >>= 32;
-    }
-    return (u32)c;
+    for (int k = 0; k < 8; ++k) z[k] = addc32(x[k], y[k], c, &c);
+    return c;
 }
 
 MH_FN u32 sub256(const u32* x, const u32* y, u32* z) {  // returns borrow out
     u32 br = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        u64 t = (u64)x[k] - y[k] - br;
-        z[k] = (u32)t;
-        br = (u32)(t >> 63);
-    }
+    for (int k = 0; k < 8; ++k) z[k] = subc32(x[k], y[k], br, &br);
     return br;
 }
 
@@ -83,10 +96,7 @@ MH_FN void neg256(const u32* x, u32* z) {
 MH_FN bool ult256(const u32* x, const u32* y) {
     u32 br = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        u64 t = (u64)x[k] - y[k] - br;
-        br = (u32)(t >> 63);
-    }
+    for (int k = 0; k < 8; ++k) (void)subc32(x[k], y[k], br, &br);
     return br != 0;
 }
 
@@ -136,12 +146,14 @@ MH_FN void mul_lo256(const u32* x, const u32* y, u32* z) {
     u32 r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        u64 carry = 0;
+        u32 carry = 0;
 #pragma unroll
         for (int j = 0; j < 8 - i; ++j) {
-            u64 t = (u64)x[i] * y[j] + r[i + j] + carry;
-            r[i + j] = (u32)t;
-            carry = t >> 32;
+            // t = x*y + carry (v_mad_u64_u32), r += lo(t), carry = hi(t) + c
+            const u64 t = (u64)x[i] * y[j] + carry;
+            u32 c;
+            r[i + j] = addc32(r[i + j], (u32)t, 0u, &c);
+            carry = (u32)(t >> 32) + c;
         }
     }
 #pragma unroll

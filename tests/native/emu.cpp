@@ -54,10 +54,11 @@ static void exec(u32 R[MH_NUM_REGS][8], const u32* ip, u32 n, const u32* consts,
     for (u32 i = 0; i < n; ++i) {
         const u32 w0 = ip[2 * i], w1 = ip[2 * i + 1];
         const u32 op = w0 & 0xFFu, d = (w0 >> 8) & 0xFFu, a = (w0 >> 16) & 0xFFu, b = w0 >> 24;
-        const u32 c = w1 & 0xFFu, w = (w1 >> 8) & 0x1FFu, aux = w1 >> 17;
+        const u32 flags = ((MH_CONST_OPERAND_OK >> op) & 1u) ? (w1 & 3u) : 0u;
+        const u32 w = (w1 >> 2) & 0x1FFu, aux = w1 >> 11;
         u32 x[8], y[8], z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        memcpy(x, R[a], 32);
-        memcpy(y, R[b], 32);
+        memcpy(x, (flags & F_ACONST) ? consts + 8ull * aux : R[a], 32);
+        memcpy(y, (flags & F_BCONST) ? consts + 8ull * aux : R[b], 32);
         switch (op) {
             case D_ADD: add256(x, y, z); mask_w(z, w); break;
             case D_SUB: sub256(x, y, z); mask_w(z, w); break;
@@ -116,21 +117,21 @@ static void exec(u32 R[MH_NUM_REGS][8], const u32* ip, u32 n, const u32* consts,
             case D_BEQ: z[0] = ((x[0] ^ y[0]) & 1u) ^ 1u; break;
             case D_BNOT: z[0] = (x[0] & 1u) ^ 1u; break;
             case D_TRUE: z[0] = 1u; break;
-            case D_FALSE: break;
+            case D_FALSE: z[0] = 0u; break;
             case D_ITE: {
                 const bool cnd = (x[0] & 1u) != 0;
-                for (int k = 0; k < 8; ++k) z[k] = cnd ? y[k] : R[c][k];
+                for (int k = 0; k < 8; ++k) z[k] = cnd ? y[k] : R[aux][k];
                 break;
             }
-            case D_BITE: z[0] = (x[0] & 1u) ? (y[0] & 1u) : (R[c][0] & 1u); break;
-            case D_LOADC: memcpy(z, consts + 8ull * w1, 32); break;
+            case D_BITE: z[0] = (x[0] & 1u) ? (y[0] & 1u) : (R[aux][0] & 1u); break;
+            case D_LOADC: memcpy(z, consts + 8ull * aux, 32); break;
             case D_LOADVAR:
                 for (int k = 0; k < 8; ++k) z[k] = assign[((u64)aux * 8 + k) * cap + row];
                 break;
             case D_KECCAK: {
                 const u32 np = (w1 >> 26) & 3u;
                 const u32 n0 = (w1 >> 8) & 63u, n1 = (w1 >> 14) & 63u, n2 = (w1 >> 20) & 63u;
-                keccak_msg(x, y, R[c], n0, np > 1 ? n1 : 0u, np > 2 ? n2 : 0u, z);
+                keccak_msg(x, y, R[w1 & 0xFFu], n0, np > 1 ? n1 : 0u, np > 2 ? n2 : 0u, z);
                 break;
             }
             default: break;
