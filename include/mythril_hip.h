@@ -162,6 +162,12 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
 /* Integer VALU micro-benchmark: returns sustained u32 lane-ops/s for v_add_co/v_addc chains
  * (kind 0), v_mad_u64_u32 (kind 1), and v_xor/v_and (kind 2).                                    */
 int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s);
+/* Kernel timing on the ctx stream.  While enabled, every sieve launch (mh_run / mh_run_async) is
+ * bracketed by HIP events recorded on the ctx stream itself, so the measured span is exactly the
+ * launch's device time whatever stream the caller uses.  mh_ctx_kernel_time synchronises, returns
+ * the summed milliseconds and the number of launches since the previous call, and resets both.   */
+int32_t mh_ctx_enable_timing(mh_ctx* ctx, int32_t enable);
+int32_t mh_ctx_kernel_time(mh_ctx* ctx, double* total_ms, uint64_t* launches);
 
 #ifdef __cplusplus
 }

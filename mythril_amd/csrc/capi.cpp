@@ -22,6 +22,8 @@ struct mh_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     uint32_t* scratch = nullptr;  // microbench sink
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> spans;  // one per timed sieve launch
 };
 
 struct mh_tapeset {
@@ -170,6 +172,10 @@ int32_t mh_ctx_destroy(mh_ctx* ctx) {
     if (!ctx) return MH_OK;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& sp : ctx->spans) {
+        (void)hipEventDestroy(sp.first);
+        (void)hipEventDestroy(sp.second);
+    }
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     delete ctx;
@@ -350,7 +356,15 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
                                 mode);
     p.first_hit = reinterpret_cast<unsigned long long*>(d_first_hit);
     p.hit_count = reinterpret_cast<unsigned long long*>(d_hit_count);
+    std::pair<hipEvent_t, hipEvent_t> sp{nullptr, nullptr};
+    if (ctx->timing) {
+        MH_HIP(hipEventCreate(&sp.first));
+        MH_HIP(hipEventCreate(&sp.second));
+        ctx->spans.push_back(sp);
+        MH_HIP(hipEventRecord(sp.first, ctx->stream));
+    }
     MH_HIP(mh::launch_sieve(p, union_features(ts, tape_first, tape_count), ctx->stream));
+    if (ctx->timing) MH_HIP(hipEventRecord(sp.second, ctx->stream));
     return MH_OK;
 }
 
@@ -420,6 +434,33 @@ int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s) {
     const double per_iter = kind == 0 ? 32.0 : kind == 1 ? 8.0 : 64.0;
     const double lanes = (double)blocks * 256.0;
     *ops_per_s = lanes * iters * per_iter / (ms * 1e-3);
+    return MH_OK;
+}
+
+int32_t mh_ctx_enable_timing(mh_ctx* ctx, int32_t enable) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    ctx->timing = enable != 0;
+    return MH_OK;
+}
+
+int32_t mh_ctx_kernel_time(mh_ctx* ctx, double* total_ms, uint64_t* launches) {
+    if (!ctx || !total_ms || !launches) return set_err(MH_E_INVALID, "null argument");
+    if (int32_t r = use_device(ctx)) return r;
+    double sum = 0.0;
+    hipError_t err = hipSuccess;
+    for (auto& sp : ctx->spans) {
+        float ms = 0.f;
+        if (err == hipSuccess) err = hipEventSynchronize(sp.second);
+        if (err == hipSuccess) err = hipEventElapsedTime(&ms, sp.first, sp.second);
+        sum += ms;
+        (void)hipEventDestroy(sp.first);
+        (void)hipEventDestroy(sp.second);
+    }
+    *launches = ctx->spans.size();
+    ctx->spans.clear();
+    *total_ms = sum;
+    if (err != hipSuccess)
+        return set_err(MH_E_DEVICE, std::string("kernel timing: ") + hipGetErrorString(err));
     return MH_OK;
 }
 

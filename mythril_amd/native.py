@@ -59,6 +59,8 @@ SIGNATURES = {
                                  C.c_uint64, C.c_uint32, _vp, _vp]),
     "mh_eval_values": (C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint64, C.c_uint64, _u32p]),
     "mh_microbench_valu": (C.c_int32, [_vp, C.c_uint32, C.POINTER(C.c_double)]),
+    "mh_ctx_enable_timing": (C.c_int32, [_vp, C.c_int32]),
+    "mh_ctx_kernel_time": (C.c_int32, [_vp, C.POINTER(C.c_double), _u64p]),
 }
 
 
@@ -168,6 +170,15 @@ class Context:
 
     def assignments(self, n_vars: int, capacity: int) -> "Assignments":
         return Assignments(self, n_vars, capacity)
+
+    def enable_timing(self, on: bool = True) -> None:
+        _check(self.lib.mh_ctx_enable_timing(self.h, 1 if on else 0))
+
+    def kernel_time(self) -> Tuple[float, int]:
+        """(summed ms, launches) of the sieve launches timed since the last call."""
+        ms, n = C.c_double(), C.c_uint64()
+        _check(self.lib.mh_ctx_kernel_time(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
 
     def microbench(self, kind: int) -> float:
         v = C.c_double()
