@@ -195,10 +195,18 @@ __device__ __forceinline__ void exec_tape(RegFile<NR>& R, const KParams& p, Insn
                 if (aux < w) {
                     shl256(x, aux, z);
                     mask_w(z, w);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) z[k] = 0;
                 }
                 break;
             case D_LSHRI:
-                if (aux < w) shr256(x, aux, z, 0u);
+                if (aux < w) {
+                    shr256(x, aux, z, 0u);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) z[k] = 0;
+                }
                 break;
             case D_ASHRI: bvashr_v(x, aux, z, w); break;
             case D_EXTRACT: shr256(x, aux, z, 0u); mask_w(z, w); break;

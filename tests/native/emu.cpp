@@ -56,7 +56,9 @@ static void exec(u32 R[MH_NUM_REGS][8], const u32* ip, u32 n, const u32* consts,
         const u32 op = w0 & 0xFFu, d = (w0 >> 8) & 0xFFu, a = (w0 >> 16) & 0xFFu, b = w0 >> 24;
         const u32 flags = ((MH_CONST_OPERAND_OK >> op) & 1u) ? (w1 & 3u) : 0u;
         const u32 w = (w1 >> 2) & 0x1FFu, aux = w1 >> 11;
-        u32 x[8], y[8], z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        // z starts as garbage, as in the kernel: a handler that leaves limbs unwritten is a bug
+        u32 x[8], y[8], z[8];
+        for (int k = 0; k < 8; ++k) z[k] = 0xA5A5A5A5u ^ (u32)k;
         memcpy(x, (flags & F_ACONST) ? consts + 8ull * aux : R[a], 32);
         memcpy(y, (flags & F_BCONST) ? consts + 8ull * aux : R[b], 32);
         switch (op) {
@@ -83,8 +85,8 @@ static void exec(u32 R[MH_NUM_REGS][8], const u32* ip, u32 n, const u32* consts,
             case D_BYTE: evm_byte(x, y, z); break;
             case D_NEG: neg256(x, z); mask_w(z, w); break;
             case D_NOT: for (int k = 0; k < 8; ++k) z[k] = ~x[k]; mask_w(z, w); break;
-            case D_SHLI: if (aux < w) { shl256(x, aux, z); mask_w(z, w); } break;
-            case D_LSHRI: if (aux < w) shr256(x, aux, z, 0u); break;
+            case D_SHLI: if (aux < w) { shl256(x, aux, z); mask_w(z, w); } else memset(z, 0, 32); break;
+            case D_LSHRI: if (aux < w) shr256(x, aux, z, 0u); else memset(z, 0, 32); break;
             case D_ASHRI: bvashr_v(x, aux, z, w); break;
             case D_EXTRACT: shr256(x, aux, z, 0u); mask_w(z, w); break;
             case D_SEXT: sext_to256(x, aux, z); mask_w(z, w); break;
