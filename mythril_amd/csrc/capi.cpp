@@ -34,6 +34,11 @@ struct mh_tapeset {
     mh_dev_tape* d_tapes = nullptr;
     uint32_t* d_consts = nullptr;
     std::vector<mh_tape_info> info;
+    // tapes bucketed by kernel variant (kernels.h variant_of): ascending tape ids per bucket,
+    // concatenated in d_ids; bucket v is [bucket_off[v], bucket_off[v+1])
+    uint32_t* d_ids = nullptr;
+    std::vector<uint32_t> ids;
+    uint32_t bucket_off[mh::kNumVariants + 1] = {};
 };
 
 struct mh_assign {
@@ -78,12 +83,6 @@ uint64_t splitmix64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-uint32_t union_features(const mh_tapeset* ts, uint32_t first, uint32_t count) {
-    uint32_t f = 0;
-    for (uint32_t t = first; t < first + count; ++t) f |= ts->info[t].features;
-    return f;
-}
-
 int32_t check_run_args(const mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first,
                        uint32_t tape_count, const mh_assign* as, uint64_t row_first,
                        uint64_t row_count, uint32_t mode) {
@@ -100,9 +99,9 @@ int32_t check_run_args(const mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_fi
     return MH_OK;
 }
 
-mh::KParams make_params(const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
-                        const mh_assign* as, uint64_t row_first, uint64_t row_count,
-                        uint64_t index_base, uint32_t mode) {
+mh::KParams make_params(const mh_tapeset* ts, uint32_t tape_first, const mh_assign* as,
+                        uint64_t row_first, uint64_t row_count, uint64_t index_base,
+                        uint32_t mode) {
     mh::KParams p{};
     p.insns = ts->d_insns;
     p.tapes = ts->d_tapes;
@@ -110,8 +109,7 @@ mh::KParams make_params(const mh_tapeset* ts, uint32_t tape_first, uint32_t tape
     p.assign = as->d;
     p.capacity = as->capacity;
     p.n_pre = ts->n_vars <= MH_MAX_PRELOAD ? ts->n_vars : 0;
-    p.tape_first = tape_first;
-    p.tape_count = tape_count;
+    p.result_base = tape_first;
     p.row_first = row_first;
     p.row_count = row_count;
     p.index_base = index_base;
@@ -211,19 +209,35 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     std::unordered_map<std::string, uint32_t> dindex;
     std::vector<mh_dev_tape> heads(n_tapes);
     std::vector<mh_tape_info> info(n_tapes);
+    std::vector<uint32_t> ids, bucket_off(mh::kNumVariants + 1, 0);
     try {
+        std::vector<std::vector<uint32_t>> tw(n_tapes);
         for (uint32_t t = 0; t < n_tapes; ++t) {
             const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
             if (e <= b) return set_err(MH_E_INVALID, "tape " + std::to_string(t) + " is empty");
             mh::CompiledTape ct;
             std::string err;
-            const uint32_t first_insn = (uint32_t)(words.size() / 2);
             int32_t r = mh::compile_tape(nodes + b, (size_t)(e - b), consts, n_consts, n_vars,
-                                         dconsts, dindex, words, ct, err);
+                                         dconsts, dindex, tw[t], ct, err);
             if (r != MH_OK) return set_err(r, "tape " + std::to_string(t) + ": " + err);
-            heads[t] = mh_dev_tape{first_insn, ct.n_insns, ct.root_reg, ct.root_bool};
+            heads[t] = mh_dev_tape{0, ct.n_insns, ct.root_bool, ct.n_regs};
             info[t] = mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops};
         }
+        // bucket by kernel variant; instruction words laid out bucket by bucket (ascending tape
+        // id inside a bucket) so that any run of consecutive bucket entries is one contiguous
+        // range of words, which the kernel stages into LDS with one coalesced copy
+        std::vector<std::vector<uint32_t>> bucket(mh::kNumVariants);
+        for (uint32_t t = 0; t < n_tapes; ++t)
+            bucket[mh::variant_of(info[t].n_regs, info[t].features)].push_back(t);
+        for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+            bucket_off[v] = (uint32_t)ids.size();
+            for (uint32_t t : bucket[v]) {
+                heads[t].insn_off = (uint32_t)(words.size() / 2);
+                words.insert(words.end(), tw[t].begin(), tw[t].end());
+                ids.push_back(t);
+            }
+        }
+        bucket_off[mh::kNumVariants] = (uint32_t)ids.size();
     } catch (const std::bad_alloc&) {
         return set_err(MH_E_NOMEM, "host allocation during compile");
     }
@@ -235,8 +249,15 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     ts->ctx = ctx;
     ts->n_tapes = n_tapes;
     ts->n_vars = n_vars;
+    ts->ids = std::move(ids);
+    for (uint32_t v = 0; v <= mh::kNumVariants; ++v) ts->bucket_off[v] = bucket_off[v];
     ts->info = std::move(info);
     hipError_t e = hipMalloc(&ts->d_insns, words.size() * sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipMalloc(&ts->d_ids, std::max<size_t>(1, ts->ids.size()) * sizeof(uint32_t));
+    if (e == hipSuccess && !ts->ids.empty())
+        e = hipMemcpy(ts->d_ids, ts->ids.data(), ts->ids.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&ts->d_tapes, std::max<size_t>(1, n_tapes) * sizeof(mh_dev_tape));
     if (e == hipSuccess) e = hipMalloc(&ts->d_consts, dconsts.size() * sizeof(uint32_t));
     if (e == hipSuccess)
@@ -259,6 +280,7 @@ int32_t mh_tapes_destroy(mh_tapeset* ts) {
     if (ts->d_insns) (void)hipFree(ts->d_insns);
     if (ts->d_tapes) (void)hipFree(ts->d_tapes);
     if (ts->d_consts) (void)hipFree(ts->d_consts);
+    if (ts->d_ids) (void)hipFree(ts->d_ids);
     delete ts;
     return MH_OK;
 }
@@ -352,8 +374,7 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
     if (int32_t r = check_run_args(ctx, ts, tape_first, tape_count, as, row_first, row_count, mode))
         return r;
     if (int32_t r = use_device(ctx)) return r;
-    mh::KParams p = make_params(ts, tape_first, tape_count, as, row_first, row_count, index_base,
-                                mode);
+    mh::KParams p = make_params(ts, tape_first, as, row_first, row_count, index_base, mode);
     p.first_hit = reinterpret_cast<unsigned long long*>(d_first_hit);
     p.hit_count = reinterpret_cast<unsigned long long*>(d_hit_count);
     std::pair<hipEvent_t, hipEvent_t> sp{nullptr, nullptr};
@@ -363,7 +384,17 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
         ctx->spans.push_back(sp);
         MH_HIP(hipEventRecord(sp.first, ctx->stream));
     }
-    MH_HIP(mh::launch_sieve(p, union_features(ts, tape_first, tape_count), ctx->stream));
+    // one launch per kernel-variant bucket, over the bucket's tapes inside the requested range
+    for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+        const uint32_t* b = ts->ids.data() + ts->bucket_off[v];
+        const uint32_t* e = ts->ids.data() + ts->bucket_off[v + 1];
+        const uint32_t* lo = std::lower_bound(b, e, tape_first);
+        const uint32_t* hi = std::lower_bound(lo, e, tape_first + tape_count);
+        if (hi == lo) continue;
+        p.tape_ids = ts->d_ids + (lo - ts->ids.data());
+        p.n_ids = (uint32_t)(hi - lo);
+        MH_HIP(mh::launch_sieve(p, v, ctx->stream));
+    }
     if (ctx->timing) MH_HIP(hipEventRecord(sp.second, ctx->stream));
     return MH_OK;
 }
@@ -400,10 +431,21 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
     if (!out && row_count) return set_err(MH_E_INVALID, "null out");
     if (row_count == 0) return MH_OK;
     if (int32_t r = use_device(ctx)) return r;
+    // the production sieve kernel in values mode, over a one-tape list
     uint32_t* d = nullptr;
-    MH_HIP(hipMalloc(&d, 8 * row_count * sizeof(uint32_t)));
-    mh::KParams p = make_params(ts, tape, 1, as, row_first, row_count, 0, MH_MODE_COUNT_ALL);
-    hipError_t e = mh::launch_values(p, tape, d, ctx->stream);
+    MH_HIP(hipMalloc(&d, (8 * row_count + 8) * sizeof(uint32_t)));
+    uint32_t* d_id = d + 8 * row_count;  // [0]: tape id, [2..5]: first_hit / hit_count
+    mh::KParams p = make_params(ts, tape, as, row_first, row_count, 0, MH_MODE_COUNT_ALL);
+    p.tape_ids = d_id;
+    p.n_ids = 1;
+    p.first_hit = reinterpret_cast<unsigned long long*>(d_id + 2);
+    p.hit_count = reinterpret_cast<unsigned long long*>(d_id + 4);
+    p.values_out = d;
+    const uint32_t ids[8] = {tape, 0, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0, 0, 0};
+    hipError_t e = hipMemcpy(d_id, ids, sizeof(ids), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = mh::launch_sieve(p, mh::variant_of(ts->info[tape].n_regs, ts->info[tape].features),
+                             ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpy(out, d, 8 * row_count * sizeof(uint32_t), hipMemcpyDeviceToHost);

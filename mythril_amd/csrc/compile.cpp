@@ -1,11 +1,23 @@
-// Tape compiler: mh_node IR (include/mythril_hip.h) -> device register code (dev_isa.h).
+// Tape compiler: mh_node IR (include/mythril_hip.h) -> device code (dev_isa.h, ISA v4).
 //
-// Per tape: reachability from the root, legalisation (values wider than 256 bits exist only as
-// Concat/ZeroExt chains feeding Keccak, kept as lists of byte-aligned pieces), lowering to
-// device ops with virtual registers, then linear-scan allocation onto MH_NUM_REGS registers.
-// Assignment columns 0..3 are pinned in R0..R3 when the tape set has at most 4 columns.
-// Anything the device path does not cover returns MH_E_UNSUPPORTED so the caller falls back
-// to z3, as get_model's contract requires.
+// Per tape:
+//  1. reachability from the root and legalisation: values wider than 256 bits exist only as
+//     Concat/ZeroExt chains feeding Keccak, kept as lists of byte-aligned pieces;
+//  2. lowering, in a Sethi-Ullman post-order, to device ops on SSA virtual registers: the asm-core
+//     ops (add/sub/logic/compares/selects/immediate shifts, with explicit AND masks where a
+//     narrow result could overflow its width) and the complex ops run in C++ (mul, division,
+//     variable shifts, narrow signed compares, keccak, EVM helpers); a constant second operand
+//     becomes an inline constant (the *_C forms);
+//  3. the accumulator pass: each instruction's first operand is the previous result (kept in X)
+//     whenever possible, through operand swaps and mirrored ops (a - b = rsub(b, a), a < b =
+//     b > a); a result is written back to the register file only if something reads it again
+//     from there;
+//  4. linear-scan allocation of the written-back values onto at most MH_NR_MAX registers
+//     (assignment columns 0..3 pinned in R0..R3), which fixes the kernel variant (NR) and hence
+//     the accumulator index NRX used in the encoding;
+//  5. slot layout: inline constants, 64-slot windows closed by D_WINDOW, D_END.
+// Anything the device path does not cover returns MH_E_UNSUPPORTED so the caller falls back to
+// z3, as get_model's contract requires.
 #include "compile.h"
 
 #include <algorithm>
@@ -44,14 +56,51 @@ uint64_t op_cost(const mh_node& n, const std::vector<mh_node>& t) {
     }
 }
 
+// ops whose y may be an inline constant: asm pairs (given as the *_R form) and binary complex ops
+bool y_const_ok(uint8_t op) {
+    if (op >= D_ADD_R && op <= D_SGE_C) return ((op - D_ADD_R) & 1) == 0;
+    switch (op) {
+        case D_MUL_R: case D_UDIV: case D_UREM: case D_SDIV: case D_SREM: case D_SMOD:
+        case D_UADD_NOOVFL: case D_UMUL_NOOVFL: case D_EXP: case D_SIGNEXT: case D_BYTE:
+            return true;
+        default:
+            return false;
+    }
+}
+
+bool commutes(uint8_t op) {
+    switch (op) {
+        case D_ADD_R: case D_AND_R: case D_OR_R: case D_XOR_R: case D_EQ_R: case D_MUL_R:
+        case D_UADD_NOOVFL: case D_UMUL_NOOVFL: case D_BAND: case D_BOR: case D_BXOR: case D_BEQ:
+            return true;
+        default:
+            return false;
+    }
+}
+
+uint8_t mirror(uint8_t op) {  // op(a, b) == mirror(op)(b, a), or 0
+    switch (op) {
+        case D_SUB_R: return D_RSUB_R;
+        case D_RSUB_R: return D_SUB_R;
+        case D_ULT_R: return D_UGT_R;
+        case D_UGT_R: return D_ULT_R;
+        case D_ULE_R: return D_UGE_R;
+        case D_UGE_R: return D_ULE_R;
+        case D_SLT_R: return D_SGT_R;
+        case D_SGT_R: return D_SLT_R;
+        case D_SLE_R: return D_SGE_R;
+        case D_SGE_R: return D_SLE_R;
+        default: return 0;
+    }
+}
+
 struct VInsn {
-    uint8_t op;
+    uint8_t op;       // device op (the *_R form for asm pairs); D_ITE here = generic select
     int d, a, b, c;   // virtual registers (-1 = none)
     uint32_t width;   // 1..256
-    uint32_t aux;     // 21-bit immediate (constant index for D_LOADC / constant operands)
-    uint32_t w1raw;   // full second word (D_KECCAK); used when raw == true
-    bool raw;
-    uint8_t flags;    // F_ACONST / F_BCONST
+    uint32_t aux;     // immediate (shift amount, SEXT source width, LOADVAR column)
+    int cidx;         // inline constant y (pool index), -1 = none
+    uint32_t w1raw;   // D_KECCAK second word (lengths)
 };
 
 struct Piece {
@@ -68,89 +117,39 @@ struct Val {
     bool wide() const { return !pieces.empty(); }
 };
 
+uint32_t lane_mask(int k, uint32_t w) {
+    const int rem = (int)w - 32 * k;
+    return rem >= 32 ? 0xFFFFFFFFu : rem <= 0 ? 0u : ((1u << rem) - 1u);
+}
+
 struct Lowering {
     const std::vector<mh_node>& t;
     const uint32_t* consts;
     uint32_t n_consts;
     uint32_t n_vars;
     bool pinned;
-    std::vector<uint32_t>& dconsts;           // device const pool (8 limbs each)
-    std::unordered_map<std::string, uint32_t>& dconst_index;
+    std::vector<uint32_t>& pool;  // deduplicated 256-bit constants (8 limbs each)
+    std::unordered_map<std::string, uint32_t>& pool_index;
     std::vector<VInsn> code;
     int n_vregs = 0;
     uint32_t features = 0;
     std::string err;
+    std::vector<Val>* vals_ = nullptr;
 
     Lowering(const std::vector<mh_node>& tape, const uint32_t* c, uint32_t nc, uint32_t nv,
-             std::vector<uint32_t>& dc, std::unordered_map<std::string, uint32_t>& di)
+             std::vector<uint32_t>& pl, std::unordered_map<std::string, uint32_t>& pi)
         : t(tape), consts(c), n_consts(nc), n_vars(nv), pinned(nv <= MH_MAX_PRELOAD),
-          dconsts(dc), dconst_index(di) {
+          pool(pl), pool_index(pi) {
         if (pinned) n_vregs = (int)nv;  // vregs 0..nv-1 are the pinned columns
     }
 
     int fresh() { return n_vregs++; }
 
     int emit(uint8_t op, int a = -1, int b = -1, int c = -1, uint32_t width = 256,
-             uint32_t aux = 0) {
-        VInsn v{op, fresh(), a, b, c, width, aux, 0, false, 0};
+             uint32_t aux = 0, int cidx = -1) {
+        VInsn v{op, fresh(), a, b, c, width, aux, cidx, 0};
         code.push_back(v);
         return v.d;
-    }
-
-    bool is_const_node(uint32_t k) const {
-        const Val& v = (*vals_)[k];
-        return !v.wide() && v.remat >= 0 && t[(size_t)v.remat].op == MH_OP_CONST;
-    }
-
-    uint32_t const_of(uint32_t k) {
-        const mh_node& c = t[(size_t)(*vals_)[k].remat];
-        return const_index(consts + 8ull * c.imm0, c.width);
-    }
-
-    // Binary op on IR nodes na, nb; a constant operand is folded into the instruction (read by
-    // the scalar unit from the constant pool) instead of being loaded into a register.
-    int emit_bin(uint8_t op, uint32_t na, uint32_t nb, uint32_t width, bool commutative) {
-        if ((MH_CONST_OPERAND_OK >> op) & 1) {
-            const bool ca = is_const_node(na), cb = is_const_node(nb);
-            if (cb || (ca && commutative)) {
-                const uint32_t kc = cb ? nb : na, kr = cb ? na : nb;
-                const int r = vreg_of(kr);
-                if (r < 0) return -1;
-                VInsn v{op, fresh(), r, -1, -1, width, const_of(kc), 0, false, F_BCONST};
-                code.push_back(v);
-                return v.d;
-            }
-        }
-        const int a = vreg_of(na), b = vreg_of(nb);
-        if (a < 0 || b < 0) return -1;
-        return emit(op, a, b, -1, width);
-    }
-
-    uint32_t const_index(const uint32_t* limbs, uint32_t width) {
-        uint32_t m[8];
-        for (int k = 0; k < 8; ++k) {
-            int rem = (int)width - 32 * k;
-            uint32_t mask = rem >= 32 ? 0xFFFFFFFFu : rem <= 0 ? 0u : ((1u << rem) - 1u);
-            m[k] = limbs[k] & mask;
-        }
-        std::string key(reinterpret_cast<const char*>(m), sizeof(m));
-        auto it = dconst_index.find(key);
-        if (it != dconst_index.end()) return it->second;
-        uint32_t idx = (uint32_t)(dconsts.size() / 8);
-        dconsts.insert(dconsts.end(), m, m + 8);
-        dconst_index.emplace(key, idx);
-        return idx;
-    }
-
-    int load_const(const uint32_t* limbs, uint32_t width) {
-        VInsn v{D_LOADC, fresh(), -1, -1, -1, width, const_index(limbs, width), 0, false, 0};
-        code.push_back(v);
-        return v.d;
-    }
-
-    int zero_reg() {
-        static const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        return load_const(z, 256);
     }
 
     bool fail(const std::string& m) {
@@ -158,9 +157,90 @@ struct Lowering {
         return false;
     }
 
-    std::vector<Val>* vals_ = nullptr;
+    uint32_t const_index(const uint32_t* limbs, uint32_t width) {
+        uint32_t m[8];
+        for (int k = 0; k < 8; ++k) m[k] = limbs[k] & lane_mask(k, width);
+        std::string key(reinterpret_cast<const char*>(m), sizeof(m));
+        auto it = pool_index.find(key);
+        if (it != pool_index.end()) return it->second;
+        uint32_t idx = (uint32_t)(pool.size() / 8);
+        pool.insert(pool.end(), m, m + 8);
+        pool_index.emplace(key, idx);
+        return idx;
+    }
 
-    // register holding narrow value k (constants are re-loaded at each use)
+    int mask_const(uint32_t w) {
+        static const uint32_t ones[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
+        return (int)const_index(ones, w);
+    }
+
+    int zero_const() {
+        static const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return (int)const_index(z, 256);
+    }
+
+    // r & (2^w - 1) when w < 256 (keeps narrow values canonical)
+    int masked(int r, uint32_t w) {
+        if (w >= 256 || r < 0) return r;
+        return emit(D_AND_R, r, -1, -1, w, 0, mask_const(w));
+    }
+
+    int bit_const(uint32_t b) {  // 2^b, b < 256
+        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        m[b >> 5] = 1u << (b & 31);
+        return (int)const_index(m, 256);
+    }
+
+    // sign extension of a canonical wa-bit value to 256 bits: (x ^ 2^(wa-1)) - 2^(wa-1)
+    int sext256(int r, uint32_t wa) {
+        if (wa >= 256 || r < 0) return r;
+        const int m = bit_const(wa - 1);
+        return emit(D_SUB_R, emit(D_XOR_R, r, -1, -1, 256, 0, m), -1, -1, 256, 0, m);
+    }
+
+    // arithmetic shift right by a uniform s at width w:
+    // ((x ^ 2^(w-1)) >> s') - 2^(w-1-s'), s' = min(s, w-1), then masked to w
+    int ashr_imm(int r, uint32_t s, uint32_t w) {
+        const uint32_t sp = s < w - 1 ? s : w - 1;
+        int u = emit(D_XOR_R, r, -1, -1, 256, 0, bit_const(w - 1));
+        if (sp) u = emit(D_LSHRI, u, -1, -1, 256, sp);
+        u = emit(D_SUB_R, u, -1, -1, 256, 0, bit_const(w - 1 - sp));
+        return masked(u, w);
+    }
+
+    // signed compare at width w < 256 as the unsigned compare of the biased values
+    // x ^ 2^(w-1) (a constant operand is biased on the host)
+    int emit_scmp(uint8_t uop, uint32_t na, uint32_t nb, uint32_t w) {
+        auto biased_const = [&](uint32_t k) {
+            const mh_node& c = t[(size_t)(*vals_)[k].remat];
+            uint32_t m[8];
+            for (int i = 0; i < 8; ++i) m[i] = consts[8ull * c.imm0 + i] & lane_mask(i, w);
+            m[(w - 1) >> 5] ^= 1u << ((w - 1) & 31);
+            return (int)const_index(m, 256);
+        };
+        auto bias = [&](uint32_t k) {
+            const int r = vreg_of(k);
+            return r < 0 ? -1 : emit(D_XOR_R, r, -1, -1, 256, 0, bit_const(w - 1));
+        };
+        if (is_const_node(nb)) return emit(uop, bias(na), -1, -1, 256, 0, biased_const(nb));
+        if (is_const_node(na))
+            return emit(mirror(uop), bias(nb), -1, -1, 256, 0, biased_const(na));
+        const int a = bias(na), b = bias(nb);
+        if (a < 0 || b < 0) return -1;
+        return emit(uop, a, b, -1, 256);
+    }
+
+    bool is_const_node(uint32_t k) const {
+        const Val& v = (*vals_)[k];
+        return !v.wide() && v.remat >= 0 && t[(size_t)v.remat].op == MH_OP_CONST;
+    }
+
+    int const_of(uint32_t k) {
+        const mh_node& c = t[(size_t)(*vals_)[k].remat];
+        return (int)const_index(consts + 8ull * c.imm0, c.width);
+    }
+
+    // register holding narrow value k (constants are re-materialised at each use)
     int vreg_of(uint32_t k) {
         const Val& v = (*vals_)[k];
         if (v.wide()) return -1;
@@ -168,33 +248,77 @@ struct Lowering {
             const mh_node& c = t[(size_t)v.remat];
             if (c.op == MH_OP_TRUE) return emit(D_TRUE, -1, -1, -1, 1);
             if (c.op == MH_OP_FALSE) return emit(D_FALSE, -1, -1, -1, 1);
-            return load_const(consts + 8ull * c.imm0, c.width);
+            return emit(D_LOADC, -1, -1, -1, 256, 0,
+                        (int)const_index(consts + 8ull * c.imm0, c.width));
         }
         return v.vreg;
     }
 
-    // pieces of a value (a narrow value is one piece)
+    // Binary op on IR nodes na, nb: a constant operand becomes the inline constant y (swapping
+    // through commutativity or the mirrored op when the constant is the first operand).
+    int emit_bin(uint8_t op, uint32_t na, uint32_t nb, uint32_t width) {
+        if (y_const_ok(op)) {
+            const bool ca = is_const_node(na), cb = is_const_node(nb);
+            if (cb || (ca && (commutes(op) || mirror(op)))) {
+                uint8_t o = op;
+                uint32_t kc = nb, kr = na;
+                if (!cb) {
+                    kc = na;
+                    kr = nb;
+                    if (!commutes(op)) o = mirror(op);
+                }
+                const int r = vreg_of(kr);
+                if (r < 0) return -1;
+                return emit(o, r, -1, -1, width, 0, const_of(kc));
+            }
+        }
+        const int a = vreg_of(na), b = vreg_of(nb);
+        if (a < 0 || b < 0) return -1;
+        return emit(op, a, b, -1, width);
+    }
+
+    // logical shift left by a uniform amount s (0 < s < 256), result mod 2^256
+    int shl_imm(int r, uint32_t s) {
+        return emit((s & 31) ? D_SHLI : D_SHLQ, r, -1, -1, 256, s);
+    }
+
+    // bits [lo, lo + w) of a wa-bit canonical value
+    int extract(int r, uint32_t lo, uint32_t w, uint32_t wa) {
+        if (lo) r = emit(D_LSHRI, r, -1, -1, 256, lo);
+        if (lo + w < wa) r = masked(r, w);
+        return r;
+    }
+
+    // (hi << wb) | lo for canonical parts, wb + width(hi) <= 256
+    int concat(int hi, int lo, uint32_t wb) { return emit(D_OR_R, shl_imm(hi, wb), lo, -1); }
+
     std::vector<Piece> pieces_of(uint32_t k, uint32_t width) {
         const Val& v = (*vals_)[k];
         if (!v.wide()) return {Piece{vreg_of(k), width}};
         return v.pieces;
     }
 
-    bool lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_bool);
+    bool lower(std::vector<Val>& vals);
 };
 
-bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_bool) {
+int arity(const mh_node& nd) {
+    if (nd.op <= MH_OP_FALSE) return 0;
+    if (nd.op == MH_OP_ITE) return 3;
+    if (nd.op == MH_OP_BVNEG || nd.op == MH_OP_BVNOT || nd.op == MH_OP_NOT ||
+        nd.op == MH_OP_EXTRACT || nd.op == MH_OP_ZEXT || nd.op == MH_OP_SEXT ||
+        nd.op == MH_OP_KECCAK)
+        return 1;
+    return 2;
+}
+
+bool Lowering::lower(std::vector<Val>& vals) {
     const size_t n = t.size();
     // operand validation (every node) and reachability from the root
     std::vector<char> live(n, 0);
     live[n - 1] = 1;
     for (size_t i = n; i-- > 0;) {
         const mh_node& nd = t[i];
-        int ar = (nd.op <= MH_OP_FALSE) ? 0
-                 : (nd.op == MH_OP_ITE) ? 3
-                 : (nd.op == MH_OP_BVNEG || nd.op == MH_OP_BVNOT || nd.op == MH_OP_NOT ||
-                    nd.op == MH_OP_EXTRACT || nd.op == MH_OP_ZEXT || nd.op == MH_OP_SEXT ||
-                    nd.op == MH_OP_KECCAK) ? 1 : 2;
+        const int ar = arity(nd);
         const uint32_t ops[3] = {nd.a, nd.b, nd.c};
         for (int k = 0; k < ar; ++k) {
             if (ops[k] >= i) return fail("operand index not before node " + std::to_string(i));
@@ -206,12 +330,6 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
     // evaluation order: post-order DFS from the root, operands with the larger Sethi-Ullman
     // register need first (the input order is only required to be topological)
     std::vector<uint32_t> need(n, 1);
-    auto arity = [&](const mh_node& nd) -> int {
-        return (nd.op <= MH_OP_FALSE) ? 0 : (nd.op == MH_OP_ITE) ? 3
-               : (nd.op == MH_OP_BVNEG || nd.op == MH_OP_BVNOT || nd.op == MH_OP_NOT ||
-                  nd.op == MH_OP_EXTRACT || nd.op == MH_OP_ZEXT || nd.op == MH_OP_SEXT ||
-                  nd.op == MH_OP_KECCAK) ? 1 : 2;
-    };
     auto children = [&](size_t i, uint32_t* ch) -> int {
         const mh_node& nd = t[i];
         const int ar = arity(nd);
@@ -222,7 +340,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
     };
     for (size_t i = 0; i < n; ++i) {
         const mh_node& nd = t[i];
-        if (nd.op == MH_OP_VAR && pinned) { need[i] = 0; continue; }
+        if ((nd.op == MH_OP_VAR && pinned) || nd.op == MH_OP_CONST) { need[i] = 0; continue; }
         uint32_t ch[3];
         const int ar = children(i, ch);
         uint32_t m = 1;
@@ -266,14 +384,9 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             case MH_OP_VAR: {
                 if (nd.imm0 >= n_vars) return fail("var column out of range");
                 if (w == 0 || w > 256) return fail("var width");
-                int r;
-                if (pinned) {
-                    r = (int)nd.imm0;
-                } else {
-                    r = emit(D_LOADVAR, -1, -1, -1, 256, nd.imm0);
-                }
-                if (w < 256) r = emit(D_EXTRACT, r, -1, -1, w, 0);
-                out.vreg = r;
+                if (!pinned) features |= F_CPLX;
+                int r = pinned ? (int)nd.imm0 : emit(D_LOADVAR, -1, -1, -1, 256, nd.imm0);
+                out.vreg = masked(r, w);  // a w-bit variable is the low w bits of its column
                 break;
             }
             case MH_OP_TRUE: case MH_OP_FALSE: out.remat = (int)i; break;
@@ -285,13 +398,14 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                     W(nd.b) != w)
                     return fail("bit-vector op wider than 256 bits");
                 uint8_t op = 0;
+                bool mask = false;
                 switch (nd.op) {
-                    case MH_OP_BVADD: op = D_ADD; break;
-                    case MH_OP_BVSUB: op = D_SUB; break;
-                    case MH_OP_BVMUL: op = D_MUL; break;
-                    case MH_OP_BVAND: op = D_AND; break;
-                    case MH_OP_BVOR: op = D_OR; break;
-                    case MH_OP_BVXOR: op = D_XOR; break;
+                    case MH_OP_BVADD: op = D_ADD_R; mask = true; break;
+                    case MH_OP_BVSUB: op = D_SUB_R; mask = true; break;
+                    case MH_OP_BVMUL: op = D_MUL_R; mask = true; break;
+                    case MH_OP_BVAND: op = D_AND_R; break;
+                    case MH_OP_BVOR: op = D_OR_R; break;
+                    case MH_OP_BVXOR: op = D_XOR_R; break;
                     case MH_OP_BVUDIV: op = D_UDIV; features |= F_DIV; break;
                     case MH_OP_BVUREM: op = D_UREM; features |= F_DIV; break;
                     case MH_OP_BVSDIV: op = D_SDIV; features |= F_DIV; break;
@@ -303,9 +417,8 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 }
                 if ((op == D_SIGNEXT || op == D_BYTE) && w != 256)
                     return fail("EVM word ops are 256-bit");
-                const bool comm = op == D_ADD || op == D_MUL || op == D_AND || op == D_OR ||
-                                  op == D_XOR;
-                out.vreg = emit_bin(op, nd.a, nd.b, w, comm);
+                int r = emit_bin(op, nd.a, nd.b, w);
+                out.vreg = mask ? masked(r, w) : r;
                 break;
             }
             case MH_OP_BVSHL: case MH_OP_BVLSHR: case MH_OP_BVASHR: {
@@ -315,66 +428,82 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 if (sn.op == MH_OP_CONST) {  // uniform shift amount
                     const uint32_t* lim = consts + 8ull * sn.imm0;
                     uint32_t hi = 0;
-                    for (int k = 1; k < 8; ++k) hi |= lim[k];
-                    uint32_t s = lim[0];
-                    if (sn.width < 32) s &= (1u << sn.width) - 1u;
-                    else if (hi && sn.width > 32) s = 511;
-                    if (s > 511) s = 511;
-                    uint8_t op = nd.op == MH_OP_BVSHL ? D_SHLI : nd.op == MH_OP_BVLSHR ? D_LSHRI
-                                                                                        : D_ASHRI;
-                    out.vreg = emit(op, narrow(nd.a), -1, -1, w, s);
-                } else {
-                    uint8_t op = nd.op == MH_OP_BVSHL ? D_SHL : nd.op == MH_OP_BVLSHR ? D_LSHR
-                                                                                       : D_ASHR;
-                    out.vreg = emit_bin(op, nd.a, nd.b, w, false);
+                    for (int k = 1; k < 8; ++k) hi |= lim[k] & lane_mask(k, sn.width);
+                    uint32_t s = lim[0] & lane_mask(0, sn.width);
+                    if (hi || s > 511) s = 511;
+                    const int a = narrow(nd.a);
+                    if (nd.op == MH_OP_BVASHR) {
+                        out.vreg = s ? ashr_imm(a, s, w) : a;
+                    } else if (s >= w) {
+                        out.vreg = emit(D_LOADC, -1, -1, -1, 256, 0, zero_const());
+                    } else if (s == 0) {
+                        out.vreg = a;
+                    } else if (nd.op == MH_OP_BVLSHR) {
+                        out.vreg = emit(D_LSHRI, a, -1, -1, 256, s);
+                    } else {
+                        out.vreg = masked(shl_imm(a, s), w);
+                    }
+                } else {  // per-lane amount: 256-bit shifts of canonical / sign-extended values
+                    const int a = narrow(nd.a), b = narrow(nd.b);
+                    if (nd.op == MH_OP_BVSHL)
+                        out.vreg = masked(emit(D_SHL_V, a, b, -1, 256), w);
+                    else if (nd.op == MH_OP_BVLSHR)
+                        out.vreg = emit(D_LSHR_V, a, b, -1, 256);
+                    else
+                        out.vreg = masked(emit(D_ASHR_V, sext256(a, w), b, -1, 256), w);
                 }
                 break;
             }
-            case MH_OP_BVNEG: case MH_OP_BVNOT: {
-                int a = narrow(nd.a);
+            case MH_OP_BVNEG: {
+                const int a = narrow(nd.a);
                 if (a < 0 || w == 0 || w > 256) return fail("unary op wider than 256");
-                out.vreg = emit(nd.op == MH_OP_BVNEG ? D_NEG : D_NOT, a, -1, -1, w);
+                out.vreg = masked(emit(D_RSUB_R, a, -1, -1, w, 0, zero_const()), w);  // 0 - a
+                break;
+            }
+            case MH_OP_BVNOT: {
+                const int a = narrow(nd.a);
+                if (a < 0 || w == 0 || w > 256) return fail("unary op wider than 256");
+                out.vreg = emit(D_XOR_R, a, -1, -1, w, 0, mask_const(w));  // a ^ (2^w - 1)
                 break;
             }
             case MH_OP_EQ: {
-                uint32_t wa = W(nd.a);
+                const uint32_t wa = W(nd.a);
                 if (wa != W(nd.b)) return fail("EQ sort mismatch");
                 if (V(nd.a).wide() || V(nd.b).wide()) return fail("EQ wider than 256 bits");
                 if (wa == 0) out.vreg = emit(D_BEQ, narrow(nd.a), narrow(nd.b), -1, 1);
-                else out.vreg = emit_bin(D_EQ, nd.a, nd.b, wa, true);
+                else out.vreg = emit_bin(D_EQ_R, nd.a, nd.b, wa);
                 break;
             }
             case MH_OP_BVULT: case MH_OP_BVULE: case MH_OP_BVUGT: case MH_OP_BVUGE:
             case MH_OP_BVSLT: case MH_OP_BVSLE: case MH_OP_BVSGT: case MH_OP_BVSGE:
             case MH_OP_BVADD_NOOVFL_U: case MH_OP_BVMUL_NOOVFL_U: case MH_OP_BVSUB_NOUDFL_U: {
-                uint32_t wa = W(nd.a);
+                const uint32_t wa = W(nd.a);
                 if (V(nd.a).wide() || V(nd.b).wide() || wa == 0 || wa > 256 || W(nd.b) != wa)
                     return fail("compare wider than 256 bits");
+                const bool full = wa == 256;
                 uint8_t op = 0;
-                bool swap = false;
                 switch (nd.op) {
-                    case MH_OP_BVULT: op = D_ULT; break;
-                    case MH_OP_BVULE: op = D_ULE; break;
-                    case MH_OP_BVUGT: op = D_ULT; swap = true; break;
-                    case MH_OP_BVUGE: op = D_ULE; swap = true; break;
-                    case MH_OP_BVSLT: op = D_SLT; break;
-                    case MH_OP_BVSLE: op = D_SLE; break;
-                    case MH_OP_BVSGT: op = D_SLT; swap = true; break;
-                    case MH_OP_BVSGE: op = D_SLE; swap = true; break;
-                    case MH_OP_BVADD_NOOVFL_U: op = D_UADD_NOOVFL; break;
-                    case MH_OP_BVMUL_NOOVFL_U: op = D_UMUL_NOOVFL; break;
-                    case MH_OP_BVSUB_NOUDFL_U: op = D_ULE; swap = true; break;  // b <= a
+                    case MH_OP_BVULT: op = D_ULT_R; break;
+                    case MH_OP_BVULE: op = D_ULE_R; break;
+                    case MH_OP_BVUGT: op = D_UGT_R; break;
+                    case MH_OP_BVUGE: op = D_UGE_R; break;
+                    case MH_OP_BVSLT: op = full ? D_SLT_R : D_ULT_R; break;
+                    case MH_OP_BVSLE: op = full ? D_SLE_R : D_ULE_R; break;
+                    case MH_OP_BVSGT: op = full ? D_SGT_R : D_UGT_R; break;
+                    case MH_OP_BVSGE: op = full ? D_SGE_R : D_UGE_R; break;
+                    case MH_OP_BVADD_NOOVFL_U: op = D_UADD_NOOVFL; features |= F_CPLX; break;
+                    case MH_OP_BVMUL_NOOVFL_U: op = D_UMUL_NOOVFL; features |= F_CPLX; break;
+                    case MH_OP_BVSUB_NOUDFL_U: op = D_UGE_R; break;  // b <= a
                 }
-                out.vreg = swap ? emit_bin(op, nd.b, nd.a, wa, false)
-                                : emit_bin(op, nd.a, nd.b, wa, op == D_UADD_NOOVFL ||
-                                                               op == D_UMUL_NOOVFL);
+                const bool narrow_signed = !full && (nd.op == MH_OP_BVSLT || nd.op == MH_OP_BVSLE ||
+                                                     nd.op == MH_OP_BVSGT || nd.op == MH_OP_BVSGE);
+                out.vreg = narrow_signed ? emit_scmp(op, nd.a, nd.b, wa) : emit_bin(op, nd.a, nd.b, wa);
                 break;
             }
             case MH_OP_AND: case MH_OP_OR: case MH_OP_XOR: {
-                int a = narrow(nd.a), b = narrow(nd.b);
                 if (W(nd.a) != 0 || W(nd.b) != 0) return fail("Bool op on bit-vectors");
-                uint8_t op = nd.op == MH_OP_AND ? D_BAND : nd.op == MH_OP_OR ? D_BOR : D_BXOR;
-                out.vreg = emit(op, a, b, -1, 1);
+                const uint8_t op = nd.op == MH_OP_AND ? D_BAND : nd.op == MH_OP_OR ? D_BOR : D_BXOR;
+                out.vreg = emit(op, narrow(nd.a), narrow(nd.b), -1, 1);
                 break;
             }
             case MH_OP_NOT: {
@@ -384,17 +513,19 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             }
             case MH_OP_ITE: {
                 if (W(nd.a) != 0) return fail("ITE condition must be Bool");
-                int c = narrow(nd.a), a = narrow(nd.b), b = narrow(nd.c);
-                if (a < 0 || b < 0 || W(nd.b) != W(nd.c)) return fail("ITE wider than 256");
-                if (w == 0) out.vreg = emit(D_BITE, c, a, b, 1);
-                else out.vreg = emit(D_ITE, c, a, b, w);
+                if (V(nd.b).wide() || V(nd.c).wide() || W(nd.b) != W(nd.c))
+                    return fail("ITE wider than 256");
+                const int c = narrow(nd.a), a = narrow(nd.b), b = narrow(nd.c);
+                if (a < 0 || b < 0 || c < 0) return fail("ITE wider than 256");
+                // generic select (cond, then, else); the accumulator pass picks the form
+                out.vreg = emit(w == 0 ? D_BITE : D_ITE, c, a, b, w == 0 ? 1 : w);
                 break;
             }
             case MH_OP_EXTRACT: {
                 const uint32_t hi = nd.imm0, lo = nd.imm1, wa = W(nd.a);
                 if (wa == 0 || lo > hi || hi >= wa || hi - lo + 1 != w) return fail("bad extract");
                 if (!V(nd.a).wide()) {
-                    out.vreg = emit(D_EXTRACT, narrow(nd.a), -1, -1, w, lo);
+                    out.vreg = extract(narrow(nd.a), lo, w, wa);
                     break;
                 }
                 if (w > 256) return fail("extract result wider than 256");
@@ -402,21 +533,14 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 const auto& ps = V(nd.a).pieces;
                 uint32_t top = wa;  // bit just above the current piece
                 int acc = -1;
-                uint32_t accw = 0;
                 for (const Piece& p : ps) {
                     const uint32_t plo = top - p.bits, phi = top - 1;
                     top = plo;
                     if (phi < lo || plo > hi) continue;
                     const uint32_t elo = std::max(lo, plo) - plo, ehi = std::min(hi, phi) - plo;
-                    int part = (elo == 0 && ehi + 1 == p.bits)
-                                   ? p.vreg
-                                   : emit(D_EXTRACT, p.vreg, -1, -1, ehi - elo + 1, elo);
                     const uint32_t pw = ehi - elo + 1;
-                    if (acc < 0) { acc = part; accw = pw; }
-                    else {
-                        acc = emit(D_CONCAT, acc, part, -1, accw + pw, pw);
-                        accw += pw;
-                    }
+                    const int part = extract(p.vreg, elo, pw, p.bits);
+                    acc = acc < 0 ? part : concat(acc, part, pw);
                 }
                 out.vreg = acc;
                 break;
@@ -425,7 +549,11 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 const uint32_t wa = W(nd.a), wb = W(nd.b);
                 if (wa == 0 || wb == 0 || wa + wb != w) return fail("bad concat");
                 if (w <= 256) {
-                    out.vreg = emit(D_CONCAT, narrow(nd.a), narrow(nd.b), -1, w, wb);
+                    const int hi = narrow(nd.a);
+                    if (is_const_node(nd.b))
+                        out.vreg = emit(D_OR_R, shl_imm(hi, wb), -1, -1, 256, 0, const_of(nd.b));
+                    else
+                        out.vreg = concat(hi, narrow(nd.b), wb);
                 } else {
                     out.pieces = pieces_of(nd.a, wa);
                     auto pb = pieces_of(nd.b, wb);
@@ -440,10 +568,10 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                     out.vreg = V(nd.a).vreg;  // canonical values: zero extension is free
                     out.remat = V(nd.a).remat;
                 } else {
-                    int z = zero_reg();
+                    const int z = emit(D_LOADC, -1, -1, -1, 256, 0, zero_const());
                     uint32_t left = nd.imm0;
                     while (left) {
-                        uint32_t take = left > 256 ? 256 : left;
+                        const uint32_t take = left > 256 ? 256 : left;
                         out.pieces.push_back(Piece{z, take});
                         left -= take;
                     }
@@ -455,7 +583,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             case MH_OP_SEXT: {
                 const uint32_t wa = W(nd.a);
                 if (wa == 0 || wa + nd.imm0 != w || w > 256) return fail("sign_extend > 256");
-                out.vreg = emit(D_SEXT, narrow(nd.a), -1, -1, w, wa);
+                out.vreg = nd.imm0 ? masked(sext256(narrow(nd.a), wa), w) : narrow(nd.a);
                 break;
             }
             case MH_OP_KECCAK: {
@@ -468,7 +596,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 uint32_t curw = 0;
                 for (const Piece& p : ps) {
                     if (cur >= 0 && curw + p.bits <= 256) {
-                        cur = emit(D_CONCAT, cur, p.vreg, -1, curw + p.bits, p.bits);
+                        cur = concat(cur, p.vreg, p.bits);
                         curw += p.bits;
                     } else {
                         if (cur >= 0) {
@@ -486,14 +614,13 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
                 for (auto& ch : chunks) total += ch.bits / 8;
                 if (total > 135) return fail("multi-block keccak");
                 features |= F_KECCAK;
-                VInsn v{D_KECCAK, fresh(), chunks[0].vreg,
-                        chunks.size() > 1 ? chunks[1].vreg : -1,
-                        chunks.size() > 2 ? chunks[2].vreg : -1, 256, 0, 0, true, 0};
-                uint32_t w1 = 0;
+                uint32_t w1 = D_KECCAK;
                 for (size_t k = 0; k < chunks.size(); ++k)
                     w1 |= (chunks[k].bits / 8) << (8 + 6 * k);
                 w1 |= (uint32_t)chunks.size() << 26;
-                v.w1raw = w1;  // c is filled at encode time
+                VInsn v{D_KECCAK, fresh(), chunks[0].vreg,
+                        chunks.size() > 1 ? chunks[1].vreg : -1,
+                        chunks.size() > 2 ? chunks[2].vreg : -1, 256, 0, -1, w1};
                 code.push_back(v);
                 out.vreg = v.d;
                 break;
@@ -505,10 +632,7 @@ bool Lowering::lower(std::vector<Val>& vals, uint32_t* root_reg, uint32_t* root_
             return fail("operand wider than 256 bits");
         vals[i] = std::move(out);
     }
-    const Val& rv = vals[n - 1];
-    if (rv.wide()) return fail("root wider than 256 bits");
-    *root_reg = (uint32_t)vreg_of((uint32_t)(n - 1));
-    *root_bool = t[n - 1].width == 0;
+    if (vals[n - 1].wide()) return fail("root wider than 256 bits");
     return true;
 }
 
@@ -525,89 +649,154 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
     std::vector<mh_node> t(nodes, nodes + n_nodes);
     Lowering L(t, consts, n_consts, n_vars, dconsts, dconst_index);
     std::vector<Val> vals;
-    uint32_t root_v = 0, root_bool = 0;
-    if (!L.lower(vals, &root_v, &root_bool)) {
+    if (!L.lower(vals)) {
         err = L.err;
         return MH_E_UNSUPPORTED;
     }
     out.alg_ops = 0;
     out.n_nodes = (uint32_t)n_nodes;
     for (size_t i = 0; i < n_nodes; ++i) out.alg_ops += op_cost(t[i], t);
+
+    std::vector<VInsn>& code = L.code;
+    const int n_pinned = L.pinned ? (int)n_vars : 0;
+    // root: X after the last instruction must hold it
+    const int root_v = L.vreg_of((uint32_t)(n_nodes - 1));
+    if (root_v < 0) {
+        err = "root wider than 256 bits";
+        return MH_E_UNSUPPORTED;
+    }
+    if (code.empty() || code.back().d != root_v) L.emit(D_NOP, root_v);
     out.features = L.features;
 
-    // ---- linear-scan register allocation ----
-    const int nv = L.n_vregs;
-    const int n_pinned = L.pinned ? (int)n_vars : 0;
-    std::vector<int> last_use(nv, -1);
-    auto use = [&](int r, int i) { if (r >= 0) last_use[r] = std::max(last_use[r], i); };
-    for (int i = 0; i < (int)L.code.size(); ++i) {
-        use(L.code[i].a, i);
-        use(L.code[i].b, i);
-        use(L.code[i].c, i);
+    // ---- accumulator pass: which operand each instruction finds in X ----
+    std::vector<char> lda(code.size(), 0);
+    int acc = -1;
+    for (size_t i = 0; i < code.size(); ++i) {
+        VInsn& v = code[i];
+        int prim = v.a;  // operand that goes through X
+        switch (v.op) {
+            case D_LOADC: case D_LOADVAR: case D_TRUE: case D_FALSE:
+                prim = -1;
+                break;
+            case D_ITE: {  // generic select from lowering: a = cond, b = then, c = else
+                const int cnd = v.a, thn = v.b;
+                if (acc == cnd && thn != cnd) {
+                    v.op = D_ITEC;  // X = cond, R[b] = then
+                } else {
+                    v.op = D_ITE;  // X = then, R[b] = cond
+                    v.a = thn;
+                    v.b = cnd;
+                }
+                prim = v.a;
+                break;
+            }
+            case D_BITE:  // X = cond, R[b] = then, R[c] = else
+                break;
+            default:
+                if (v.cidx < 0 && v.b >= 0 && acc == v.b && acc != v.a) {
+                    if (commutes(v.op)) {
+                        std::swap(v.a, v.b);
+                    } else if (uint8_t mo = mirror(v.op)) {
+                        v.op = mo;
+                        std::swap(v.a, v.b);
+                    }
+                }
+                prim = v.a;
+                break;
+        }
+        if (prim >= 0 && acc != prim) lda[i] = 1;
+        acc = v.d;
     }
-    use((int)root_v, (int)L.code.size());  // root stays live to the end
+    // register uses: loads of the first operand (LDA), y operands, the third operand
+    const int nv = L.n_vregs;
+    std::vector<int> last_use(nv, -1);
+    std::vector<char> needs_reg(nv, 0);
+    for (int r = 0; r < n_pinned; ++r) needs_reg[r] = 1;
+    auto reg_use = [&](int r, int i) {
+        if (r < 0) return;
+        last_use[r] = std::max(last_use[r], i);
+        needs_reg[r] = 1;
+    };
+    for (int i = 0; i < (int)code.size(); ++i) {
+        const VInsn& v = code[i];
+        if (lda[i]) reg_use(v.a, i);
+        if (v.cidx < 0) reg_use(v.b, i);
+        reg_use(v.c, i);
+    }
+    // ---- linear-scan allocation of the written-back values ----
     std::vector<int> phys(nv, -1);
     for (int r = 0; r < n_pinned; ++r) phys[r] = r;
     std::vector<int> free_regs;
-    for (int r = MH_NUM_REGS - 1; r >= n_pinned; --r) free_regs.push_back(r);
-    int peak = n_pinned;
-    std::vector<int> in_use_count(MH_NUM_REGS, 0);
-    int used = n_pinned;
-    for (int i = 0; i < (int)L.code.size(); ++i) {
-        VInsn& v = L.code[i];
-        // release operands whose last use is this instruction (the kernel reads operands
-        // before writing the destination, so d may reuse an operand's register)
-        int ops[3] = {v.a, v.b, v.c};
+    for (int r = MH_NR_MAX - 1; r >= n_pinned; --r) free_regs.push_back(r);
+    std::vector<char> wb(code.size(), 0);
+    int peak = n_pinned;  // highest register index used + 1
+    for (int i = 0; i < (int)code.size(); ++i) {
+        const VInsn& v = code[i];
+        const int ops[3] = {lda[i] ? v.a : -1, v.cidx >= 0 ? -1 : v.b, v.c};
         for (int k = 0; k < 3; ++k) {
-            int r = ops[k];
-            if (r < n_pinned || r < 0) continue;
+            const int r = ops[k];
+            if (r < n_pinned) continue;
             bool dup = false;
             for (int j = 0; j < k; ++j) dup |= ops[j] == r;
-            if (!dup && last_use[r] == i) {
-                free_regs.push_back(phys[r]);
-                --used;
-            }
+            if (!dup && last_use[r] == i) free_regs.push_back(phys[r]);
         }
-        if (last_use[v.d] < 0) {
-            // dead result (only possible for unused keccak chunks etc.) — still needs a slot
-            last_use[v.d] = i;
-        }
+        if (!needs_reg[v.d]) continue;
         if (free_regs.empty()) {
-            err = "register pressure exceeds " + std::to_string(MH_NUM_REGS) + " registers";
+            err = "register pressure exceeds " + std::to_string(MH_NR_MAX) + " registers";
             return MH_E_UNSUPPORTED;
         }
-        phys[v.d] = free_regs.back();
-        free_regs.pop_back();
-        ++used;
-        peak = std::max(peak, used);
-        if (last_use[v.d] == i) {  // dead immediately
-            free_regs.push_back(phys[v.d]);
-            --used;
-        }
+        // lowest free register keeps small tapes in the small-register kernel
+        auto it = std::min_element(free_regs.begin(), free_regs.end());
+        phys[v.d] = *it;
+        free_regs.erase(it);
+        peak = std::max(peak, phys[v.d] + 1);
+        wb[i] = 1;
     }
-    out.n_regs = (uint32_t)peak;
-    out.n_insns = (uint32_t)L.code.size();
-    out.root_reg = (uint32_t)phys[root_v];
-    out.root_bool = root_bool;
+    const uint32_t nrx = peak <= MH_NR_SMALL ? MH_NR_SMALL : MH_NR_MAX;
+    out.n_regs = (uint32_t)std::max(peak, 1);
+    out.root_bool = t.back().width == 0;
 
-    // ---- encode ----
-    for (const VInsn& v : L.code) {
-        auto P = [&](int r) -> uint32_t { return r < 0 ? 0u : (uint32_t)phys[r]; };
-        const uint32_t w0 = (uint32_t)v.op | (P(v.d) << 8) | (P(v.a) << 16) | (P(v.b) << 24);
+    // ---- encode + slot layout ----
+    std::vector<uint32_t> slots;  // pairs (w0, w1)
+    auto put = [&](uint32_t w0, uint32_t w1) {
+        slots.push_back(w0);
+        slots.push_back(w1);
+    };
+    auto pos = [&]() { return (uint32_t)(slots.size() / 2); };
+    for (size_t i = 0; i < code.size(); ++i) {
+        const VInsn& v = code[i];
+        auto P = [&](int r) -> uint32_t { return (r < 0 || phys[r] < 0) ? 0u : (uint32_t)phys[r]; };
+        const uint32_t a = lda[i] ? P(v.a) : nrx;
+        const uint32_t d = wb[i] ? P(v.d) : nrx;
+        const uint32_t b = v.cidx >= 0 ? 0u : P(v.b);
+        const uint32_t c = P(v.c);
+        uint32_t op = v.op;
         uint32_t w1;
         if (v.op == D_KECCAK) {
-            w1 = v.w1raw | P(v.c);
+            w1 = v.w1raw;
         } else {
-            const uint32_t aux = (v.op == D_ITE || v.op == D_BITE) ? P(v.c) : v.aux;
-            if (aux > MH_AUX_MAX) {
-                err = "immediate / constant index exceeds 21 bits";
+            if (v.aux > MH_AUX_MAX) {
+                err = "immediate exceeds 14 bits";
                 return MH_E_UNSUPPORTED;
             }
-            w1 = (uint32_t)v.flags | ((v.width & 0x1FF) << 2) | (aux << 11);
+            if (v.cidx >= 0 && op < D_FIRST_COMPLEX && op != D_LOADC) op += 1;  // *_C form
+            w1 = op | ((v.width & 0x1FFu) << 8) | (v.aux << 17);
+            if (v.cidx >= 0 && op >= D_FIRST_COMPLEX) w1 |= F_YC;
         }
-        words.push_back(w0);
-        words.push_back(w1);
+        const uint32_t len = v.cidx >= 0 ? 5u : 1u;
+        if (pos() % MH_WINDOW + len > MH_WINDOW - 1) {  // keep the last slot for D_WINDOW
+            put(0, D_WINDOW);
+            while (pos() % MH_WINDOW) put(0, 0);
+        }
+        put(a | (b << 8) | (d << 16) | (c << 24), w1);
+        if (v.cidx >= 0) {
+            const uint32_t* lim = dconsts.data() + 8ull * (uint32_t)v.cidx;
+            for (int k = 0; k < 4; ++k) put(lim[2 * k], lim[2 * k + 1]);
+        }
     }
+    put(0, D_END);
+    out.n_insns = pos();
+    words.insert(words.end(), slots.begin(), slots.end());
     return MH_OK;
 }
 

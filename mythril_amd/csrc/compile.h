@@ -15,7 +15,6 @@ struct CompiledTape {
     uint32_t n_nodes = 0;
     uint32_t n_insns = 0;
     uint32_t n_regs = 0;
-    uint32_t root_reg = 0;
     uint32_t root_bool = 0;
     uint32_t features = 0;
     uint64_t alg_ops = 0;

@@ -1,86 +1,88 @@
 // Device instruction set of the sieve interpreter (internal; the public IR is mh_node in
-// include/mythril_hip.h).  mh_tapes_compile() lowers each IR tape to this form: a register
-// machine over MH_NUM_REGS registers of 8 x u32 limbs (least significant limb first), with
-// assignment columns pinned in the first registers.
+// include/mythril_hip.h).  mh_tapes_compile() lowers each IR tape to this form.
 //
-// Encoding: two u32 words per instruction.
-//   w0 = op | d << 8 | a << 16 | b << 24
-//   w1 = flags | width << 2 | aux << 11      (flags bit 0: operand a is constant aux,
-//                                              bit 1: operand b is constant aux; width 1..256)
-//   D_ITE: aux = c (else register).  D_LOADC: aux = constant index.
-//   D_KECCAK: w1 = c | n0 << 8 | n1 << 14 | n2 << 20 | npieces << 26 (n_i = bytes of piece i).
-// Constant operands are read by the scalar unit straight from the constant pool: no register,
-// no load instruction, no register-file traffic for them.
+// Machine model.  A register file R[0..NRX] of 256-bit values held in VGPRs as 8 "limb planes"
+// (plane k = limb k of every register, NRX+1 consecutive VGPRs), indexed by a wave-uniform
+// register number through the GPR-index mode (s_set_gpr_idx_on).  The LAST register of every
+// plane, R[NRX], is the ACCUMULATOR X.  Every instruction computes
+//     X = f(R[a'], y, ...)        then      R[d'] = X
+// where a' = NRX means "X itself" (the previous result, no load) and d' = NRX means "no write-back"
+// (the copy X -> X is harmless), so operand load and write-back need no branch: the host picks
+// the indices.  y is R[b] (the *_R forms) or a 256-bit constant stored INLINE in the instruction
+// stream (the *_C forms: the 4 slots after the instruction hold limbs 0..7), read with v_readlane
+// like the instruction itself, so no instruction waits on memory.  Assignment columns 0..3 are
+// pinned in R0..R3.  NRX depends on the kernel variant (kernels.h) and is fixed at compile time.
+//
+// Encoding: a slot is two u32 words (w0, w1); an instruction is one slot (+4 constant slots).
+//   w0 = a' | b << 8 | d' << 16 | c << 24       (c: ITE else register, KECCAK third piece)
+//   w1 = op | width << 8 | aux << 17 | F_YC << 31
+//        width 1..256 (9 bits); aux 14 bits: shift amount, SEXT source width, LOADVAR column
+//        F_YC (complex ops only): y is the inline constant rather than R[b]
+//   D_KECCAK: w1 = op | n0 << 8 | n1 << 14 | n2 << 20 | npieces << 26
+//             (message = X (n0 bytes) | R[b] (n1) | R[c] (n2), big-endian bytes)
+// Ops below D_FIRST_COMPLEX run in the hand-written assembly core (asm_core.inc, threaded
+// code: one computed jump per instruction); the others in C++ (exec.h).  Narrow signed
+// compares, sign extension and arithmetic shifts are lowered by the host onto asm ops
+// (x ^ 2^(w-1) biasing), so only division, the overflow predicates, keccak and the EVM helpers
+// need the C++ path.  Tapes are cut into
+// windows of 64 slots (what one wave holds in two VGPRs); D_WINDOW ends a window that is not the
+// tape's last, D_END ends the tape.  No instruction straddles a window.
+// Bool values are 0/1 in limb 0 (other limbs undefined).  Values narrower than 256 bits are kept
+// canonical (zero above the width); the host inserts AND_C masks where an op could overflow.
 #pragma once
 #include <stdint.h>
 
-#ifndef MH_NUM_REGS
-#define MH_NUM_REGS 12
-#endif
 #define MH_MAX_PRELOAD 4   // assignment columns kept resident in R0..R3 for the whole launch
+#define MH_NR_SMALL 7      // register-file sizes of the kernel variants (tapes bucketed by need);
+#define MH_NR_MAX 15       // the accumulator is register NR, so planes are NR+1 VGPRs (even:
+                           // VGPR tuples are even-aligned on gfx950)
+#define MH_WINDOW 64       // instruction slots per window
 
 enum mh_dop : uint8_t {
-    D_NOP = 0,
-    // bv x bv -> bv
-    D_ADD, D_SUB, D_MUL, D_AND, D_OR, D_XOR, D_SHL, D_LSHR, D_ASHR,
-    D_UDIV, D_UREM, D_SDIV, D_SREM, D_SMOD, D_EXP, D_SIGNEXT, D_BYTE,
-    D_CONCAT,                       // a = high, b = low, aux = width of b
-    // bv -> bv
-    D_NEG, D_NOT, D_MOV, D_SHLI, D_LSHRI, D_ASHRI, D_EXTRACT, D_SEXT,
-    // bv x bv -> Bool (0/1 in limb 0)
-    D_EQ, D_ULT, D_ULE, D_SLT, D_SLE, D_UADD_NOOVFL, D_UMUL_NOOVFL,
-    // Bool
-    D_BAND, D_BOR, D_BXOR, D_BEQ, D_BNOT, D_TRUE, D_FALSE,
-    // others
-    D_ITE,                          // a = Bool cond, b = then, aux = else register
-    D_BITE,                         // Bool-valued ite, aux = else register
-    D_LOADC,                        // aux = constant index
-    D_LOADVAR,                      // aux = column
-    D_KECCAK,                       // message = concat of up to 3 byte-aligned pieces a, b, c
+    // ---- assembly core (threaded dispatch)
+    D_EXIT = 0,  // leave the asm core (never emitted; table slot for every op >= D_FIRST_COMPLEX)
+    D_NOP,       // X = R[a'], R[d'] = X   (loads, copies, root)
+    D_ADD_R, D_ADD_C, D_SUB_R, D_SUB_C, D_RSUB_R, D_RSUB_C,  // mod 2^256 (host masks)
+    D_AND_R, D_AND_C, D_OR_R, D_OR_C, D_XOR_R, D_XOR_C,
+    D_EQ_R, D_EQ_C, D_ULT_R, D_ULT_C, D_UGT_R, D_UGT_C, D_ULE_R, D_ULE_C, D_UGE_R, D_UGE_C,
+    D_SLT_R, D_SLT_C, D_SGT_R, D_SGT_C, D_SLE_R, D_SLE_C, D_SGE_R, D_SGE_C,  // 256-bit signed
+    D_BAND, D_BOR, D_BXOR, D_BEQ, D_BNOT, D_TRUE, D_FALSE,   // y0 = R[b] limb 0
+    D_ITE,    // X = R[a'] (then), cond = R[b] limb 0, else = R[c]
+    D_ITEC,   // cond = R[a'] limb 0, then = R[b], else = R[c]
+    D_BITE,   // Bool select: cond = R[a'], then = R[b] limb 0, else = R[c] limb 0
+    D_LOADC,  // X = inline constant
+    D_LSHRI,  // X = R[a'] >> aux          (aux < 256)
+    D_SHLI,   // X = R[a'] << aux mod 2^256 (aux % 32 != 0)
+    D_SHLQ,   // X = R[a'] << aux mod 2^256 (aux % 32 == 0)
+    D_MUL_R, D_MUL_C,  // X = R[a'] * y mod 2^256 (host masks)
+    D_SHL_V, D_LSHR_V, D_ASHR_V,  // 256-bit shifts by y (per lane; >= 256 saturates to 0 / fill)
+    D_NUM_ASM,
+    // ---- C++ (exec.h); y = R[b] or the inline constant (F_YC)
+    D_FIRST_COMPLEX = 64,
+    D_UDIV = D_FIRST_COMPLEX, D_UREM, D_SDIV, D_SREM, D_SMOD,  // width-w semantics
+    D_UADD_NOOVFL, D_UMUL_NOOVFL,    // z3 BVAddNoOverflow / BVMulNoOverflow (unsigned) -> Bool
+    D_EXP, D_SIGNEXT, D_BYTE,        // EVM word ops (256-bit)
+    D_KECCAK,
+    D_LOADVAR,                     // X = assignment column aux (columns beyond the pinned ones)
+    D_END,                         // end of tape: X holds the root
+    D_WINDOW,                      // end of a 64-slot window: continue with the next one
     D_NUM_OPS
 };
 
-static_assert(D_NUM_OPS <= 64, "operand masks are 64-bit");
+static_assert(D_NUM_ASM <= D_FIRST_COMPLEX, "asm opcode space");
+static_assert(D_NUM_OPS <= 128, "opcode space");
 
-#define MH_BIT(op) (1ull << (op))
-// ops that read operand a / operand b as a full 8-limb value
-#define MH_READS_A                                                                             \
-    (MH_BIT(D_ADD) | MH_BIT(D_SUB) | MH_BIT(D_MUL) | MH_BIT(D_AND) | MH_BIT(D_OR) |          \
-     MH_BIT(D_XOR) | MH_BIT(D_SHL) | MH_BIT(D_LSHR) | MH_BIT(D_ASHR) | MH_BIT(D_UDIV) |      \
-     MH_BIT(D_UREM) | MH_BIT(D_SDIV) | MH_BIT(D_SREM) | MH_BIT(D_SMOD) | MH_BIT(D_EXP) |     \
-     MH_BIT(D_SIGNEXT) | MH_BIT(D_BYTE) | MH_BIT(D_CONCAT) | MH_BIT(D_NEG) | MH_BIT(D_NOT) | \
-     MH_BIT(D_MOV) | MH_BIT(D_SHLI) | MH_BIT(D_LSHRI) | MH_BIT(D_ASHRI) | MH_BIT(D_EXTRACT) | \
-     MH_BIT(D_SEXT) | MH_BIT(D_EQ) | MH_BIT(D_ULT) | MH_BIT(D_ULE) | MH_BIT(D_SLT) |         \
-     MH_BIT(D_SLE) | MH_BIT(D_UADD_NOOVFL) | MH_BIT(D_UMUL_NOOVFL) | MH_BIT(D_KECCAK))
-#define MH_READS_B                                                                             \
-    (MH_BIT(D_ADD) | MH_BIT(D_SUB) | MH_BIT(D_MUL) | MH_BIT(D_AND) | MH_BIT(D_OR) |          \
-     MH_BIT(D_XOR) | MH_BIT(D_SHL) | MH_BIT(D_LSHR) | MH_BIT(D_ASHR) | MH_BIT(D_UDIV) |      \
-     MH_BIT(D_UREM) | MH_BIT(D_SDIV) | MH_BIT(D_SREM) | MH_BIT(D_SMOD) | MH_BIT(D_EXP) |     \
-     MH_BIT(D_SIGNEXT) | MH_BIT(D_BYTE) | MH_BIT(D_CONCAT) | MH_BIT(D_EQ) | MH_BIT(D_ULT) |  \
-     MH_BIT(D_ULE) | MH_BIT(D_SLT) | MH_BIT(D_SLE) | MH_BIT(D_UADD_NOOVFL) |                 \
-     MH_BIT(D_UMUL_NOOVFL) | MH_BIT(D_ITE) | MH_BIT(D_KECCAK))
-// ops whose operands are Bools (limb 0 only)
-#define MH_BOOL_IN                                                                             \
-    (MH_BIT(D_BAND) | MH_BIT(D_BOR) | MH_BIT(D_BXOR) | MH_BIT(D_BEQ) | MH_BIT(D_BNOT) |      \
-     MH_BIT(D_ITE) | MH_BIT(D_BITE))
-// ops that may take a constant operand (flags) — binary ops without other uses of aux
-#define MH_CONST_OPERAND_OK                                                                    \
-    (MH_BIT(D_ADD) | MH_BIT(D_SUB) | MH_BIT(D_MUL) | MH_BIT(D_AND) | MH_BIT(D_OR) |          \
-     MH_BIT(D_XOR) | MH_BIT(D_SHL) | MH_BIT(D_LSHR) | MH_BIT(D_ASHR) | MH_BIT(D_UDIV) |      \
-     MH_BIT(D_UREM) | MH_BIT(D_SDIV) | MH_BIT(D_SREM) | MH_BIT(D_SMOD) | MH_BIT(D_EXP) |     \
-     MH_BIT(D_SIGNEXT) | MH_BIT(D_BYTE) | MH_BIT(D_EQ) | MH_BIT(D_ULT) | MH_BIT(D_ULE) |     \
-     MH_BIT(D_SLT) | MH_BIT(D_SLE) | MH_BIT(D_UADD_NOOVFL) | MH_BIT(D_UMUL_NOOVFL))
+enum { F_YC = 1u << 31 };
+#define MH_AUX_MAX ((1u << 14) - 1)
 
-enum { F_ACONST = 1, F_BCONST = 2 };
-#define MH_AUX_MAX ((1u << 21) - 1)
-
-// Feature bits (mh_tape_info.features) — select the kernel variant.
-enum { F_DIV = 1, F_KECCAK = 2, F_EVM = 4 };
+// Feature bits (mh_tape_info.features) — select the kernel variant.  A tape with none of them
+// runs entirely in the asm core (a kernel without the C++ path: fewer VGPRs, more waves).
+enum { F_DIV = 1, F_KECCAK = 2, F_EVM = 4, F_CPLX = 8 /* other C++ ops */ };
 
 // Per-tape header in the device tape table.
 struct mh_dev_tape {
-    uint32_t insn_off;   // first instruction (in instructions, not words)
-    uint32_t n_insns;
-    uint32_t root_reg;
-    uint32_t root_bool;  // 1 if the root is Bool
+    uint32_t insn_off;   // first slot of the tape in the slot array
+    uint32_t n_insns;    // slots (windows are MH_WINDOW slots apart)
+    uint32_t root_bool;  // 1 if the root (X at D_END) is Bool
+    uint32_t n_regs;     // registers the tape uses (pinned columns included, X excluded)
 };

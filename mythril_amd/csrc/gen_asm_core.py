@@ -1,0 +1,503 @@
+#!/usr/bin/env python3
+"""Generate asm_core.inc: the threaded-code interpreter core of the sieve kernel (gfx950).
+
+One inline-asm statement per register-file size NR runs the asm-core ops of dev_isa.h back to
+back with ONE computed jump per instruction (s_setpc_b64 into a table of 256-byte handler
+slots), instead of the binary-search branch tree a C++ switch compiles to: on CDNA every taken
+branch stalls the wave on instruction fetch, and that stall, not the arithmetic, bounded the C++
+interpreter (rocprofv3: 11.6 branches and ~260 parked cycles per interpreted instruction).
+
+Register model (dev_isa.h): plane k of the register file is VGPRs [k*(NR+1), (k+1)*(NR+1)),
+R[r] limb k is v[k*(NR+1) + r], the accumulator X is R[NR]; operands are read and written through
+the GPR-index mode, so a' = NR (X itself) and d' = NR (no write-back) need no branch.  Scratch
+S0..S16 follows the planes (S0..S7 doubles as y).  Constants ride in the instruction stream and
+arrive by v_readlane, like the instructions.  The statement returns with ip at the first
+instruction it does not handle (a complex op, D_WINDOW, D_END); the C++ driver
+(sieve_kernels.hip) executes that one and re-enters.
+
+Hazards (CDNA3/4 manually-inserted wait states): no VALU-written SGPR is used as a readlane lane
+select or a VMEM operand inside the core; VCC is only used as carry/mask (no alias mixing); the
+statement opens with s_nop so the VGPRs the compiler wrote just before are safe to readlane.
+Every handler ends with s_set_gpr_idx_off before the next dispatch.
+
+    python3 gen_asm_core.py > asm_core.inc      (run by the Makefile)
+"""
+import sys
+
+SLOT = 256          # bytes per handler slot
+NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
+
+# opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
+OPS = ["EXIT", "NOP",
+       "ADD_R", "ADD_C", "SUB_R", "SUB_C", "RSUB_R", "RSUB_C",
+       "AND_R", "AND_C", "OR_R", "OR_C", "XOR_R", "XOR_C",
+       "EQ_R", "EQ_C", "ULT_R", "ULT_C", "UGT_R", "UGT_C", "ULE_R", "ULE_C", "UGE_R", "UGE_C",
+       "SLT_R", "SLT_C", "SGT_R", "SGT_C", "SLE_R", "SLE_C", "SGE_R", "SGE_C",
+       "BAND", "BOR", "BXOR", "BEQ", "BNOT", "TRUE", "FALSE",
+       "ITE", "ITEC", "BITE", "LOADC", "LSHRI", "SHLI", "SHLQ",
+       "MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V"]
+OPNUM = {n: i for i, n in enumerate(OPS)}
+# handlers longer than a slot live after the table (one extra jump)
+OUT_OF_LINE = {"MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V"}
+
+# scalar registers the core owns (declared clobbered)
+S_TAB, S_TAB_HI = "s40", "s41"   # handler table base
+S_W0, S_W1 = "s42", "s43"        # current instruction words
+S_T = "s44"                      # temp
+S_PC, S_PC_HI = "s46", "s47"     # jump target
+S_B, S_D, S_C = "s48", "s49", "s50"  # register operands (low byte = index)
+S_L = "s51"                      # readlane lane
+S_Q, S_R = "s52", "s53"          # shift: limb part, bit part
+S_K = ["s%d" % (54 + k) for k in range(8)]  # inline constant limbs
+SGPR_CLOBBERS = ["s%d" % i for i in range(40, 64)]
+
+
+class Core:
+    def __init__(self, nr: int):
+        self.nr = nr
+        self.nr1 = nr + 1
+        self.sb = 8 * self.nr1  # scratch base
+
+    def P(self, k, r=0):
+        return "v%d" % (k * self.nr1 + r)
+
+    def X(self, k):
+        return self.P(k, self.nr)
+
+    def S(self, j):
+        assert 0 <= j <= 23
+        return "v%d" % (self.sb + j)
+
+    def Y(self, k):
+        return self.S(k)
+
+    # ---- building blocks
+    def dispatch(self, adv):
+        out = []
+        if adv:
+            out.append("s_add_u32 %[ip], %[ip], {}".format(adv))
+        out += [
+            "v_readlane_b32 {}, %[ic0], %[ip]".format(S_W0),
+            "v_readlane_b32 {}, %[ic1], %[ip]".format(S_W1),
+            "s_and_b32 {}, {}, 0x7f".format(S_T, S_W1),
+            "s_lshl_b32 {}, {}, 8".format(S_T, S_T),
+            "s_add_u32 {}, {}, {}".format(S_PC, S_TAB, S_T),
+            "s_addc_u32 {}, {}, 0".format(S_PC_HI, S_TAB_HI),
+            "s_setpc_b64 s[46:47]",
+        ]
+        return out
+
+    def idx_on(self, sreg, modes):
+        return ["s_set_gpr_idx_on {}, gpr_idx({})".format(sreg, ",".join(modes))]
+
+    def idx_off(self):
+        return ["s_set_gpr_idx_off"]
+
+    def field(self, dst, shift):
+        return ["s_lshr_b32 {}, {}, {}".format(dst, S_W0, shift)]
+
+    def y_reg(self, limbs=8):  # Y <- R[b]
+        out = self.field(S_B, 8) + self.idx_on(S_B, ["SRC0"])
+        out += ["v_mov_b32 {}, {}".format(self.Y(k), self.P(k)) for k in range(limbs)]
+        return out + self.idx_off()
+
+    def consts(self, to_y=(), flip7=False):  # S_K <- inline constant; Y[k] <- S_K[k] for k in to_y
+        out = []
+        for i in range(4):
+            out.append("s_add_u32 {}, %[ip], {}".format(S_L, i + 1))
+            out.append("v_readlane_b32 {}, %[ic0], {}".format(S_K[2 * i], S_L))
+            out.append("v_readlane_b32 {}, %[ic1], {}".format(S_K[2 * i + 1], S_L))
+        if flip7:
+            out.append("s_xor_b32 {}, {}, 0x80000000".format(S_K[7], S_K[7]))
+        out += ["v_mov_b32 {}, {}".format(self.Y(k), S_K[k]) for k in to_y]
+        return out
+
+    def wb(self, limbs=8):  # R[d'] <- X
+        out = self.field(S_D, 16) + self.idx_on(S_D, ["DST"])
+        out += ["v_mov_b32 {}, {}".format(self.P(k), self.X(k)) for k in range(limbs)]
+        return out + self.idx_off()
+
+    def bool_out(self, true_if_vcc=True):
+        a, b = ("0", "1") if true_if_vcc else ("1", "0")
+        return ["v_cndmask_b32_e64 {}, {}, {}, vcc".format(self.X(0), a, b)]
+
+    # ---- handlers: list of instruction lines, ending in a dispatch (or the exit branch)
+    def handler(self, name):
+        X, P, Y, S = self.X, self.P, self.Y, self.S
+        a_src0 = self.idx_on(S_W0, ["SRC0"])
+        a_src1 = self.idx_on(S_W0, ["SRC1"])
+        off = self.idx_off()
+        if name == "EXIT":
+            return ["s_branch L_out_%="]
+        if name == "NOP":
+            body = a_src0 + ["v_mov_b32 {}, {}".format(X(k), P(k)) for k in range(8)] + off
+            return body + self.wb() + self.dispatch(1)
+        arith = {"ADD": ("v_add_co_u32", "v_addc_co_u32"), "SUB": ("v_sub_co_u32", "v_subb_co_u32"),
+                 "RSUB": ("v_subrev_co_u32", "v_subbrev_co_u32")}
+        if name in ("ADD_R", "SUB_R", "RSUB_R"):
+            first, rest = arith[name[:-2]]
+            body = self.y_reg() + a_src0
+            body.append("{} {}, vcc, {}, {}".format(first, X(0), P(0), Y(0)))
+            body += ["{} {}, vcc, {}, {}, vcc".format(rest, X(k), P(k), Y(k)) for k in range(1, 8)]
+            return body + off + self.wb() + self.dispatch(1)
+        if name in ("ADD_C", "SUB_C", "RSUB_C"):
+            # y is SGPR src0 for limb 0; VGPR for the carry chain (one scalar operand per VALU)
+            first, rest = {"ADD_C": ("v_add_co_u32", "v_addc_co_u32"),
+                           "SUB_C": ("v_subrev_co_u32", "v_subbrev_co_u32"),  # R - c
+                           "RSUB_C": ("v_sub_co_u32", "v_subb_co_u32")}[name]  # c - R
+            body = self.consts(to_y=range(1, 8)) + a_src1
+            body.append("{} {}, vcc, {}, {}".format(first, X(0), S_K[0], P(0)))
+            body += ["{} {}, vcc, {}, {}, vcc".format(rest, X(k), Y(k), P(k)) for k in range(1, 8)]
+            return body + off + self.wb() + self.dispatch(5)
+        logic = {"AND": "v_and_b32", "OR": "v_or_b32", "XOR": "v_xor_b32"}
+        if name in ("AND_R", "OR_R", "XOR_R"):
+            ins = logic[name[:-2]]
+            body = self.y_reg() + a_src0
+            body += ["{} {}, {}, {}".format(ins, X(k), P(k), Y(k)) for k in range(8)]
+            return body + off + self.wb() + self.dispatch(1)
+        if name in ("AND_C", "OR_C", "XOR_C"):
+            ins = logic[name[:-2]]
+            body = self.consts() + a_src1
+            body += ["{} {}, {}, {}".format(ins, X(k), S_K[k], P(k)) for k in range(8)]
+            return body + off + self.wb() + self.dispatch(5)
+        if name in ("EQ_R", "EQ_C"):
+            if name == "EQ_R":
+                body = self.y_reg() + a_src0
+                body += ["v_xor_b32 {}, {}, {}".format(S(8 + k), P(k), Y(k)) for k in range(8)]
+            else:
+                body = self.consts() + a_src1
+                body += ["v_xor_b32 {}, {}, {}".format(S(8 + k), S_K[k], P(k)) for k in range(8)]
+            body += off
+            body += ["v_or3_b32 {0}, {0}, {1}, {2}".format(S(8), S(9), S(10)),
+                     "v_or3_b32 {0}, {0}, {1}, {2}".format(S(8), S(11), S(12)),
+                     "v_or3_b32 {0}, {0}, {1}, {2}".format(S(8), S(13), S(14)),
+                     "v_or_b32 {0}, {0}, {1}".format(S(8), S(15)),
+                     "v_cmp_eq_u32 vcc, 0, {}".format(S(8))]
+            body += self.bool_out(True) + self.wb(1)
+            return body + self.dispatch(1 if name == "EQ_R" else 5)
+        cmp_kind = name[:-2]
+        if cmp_kind in ("ULT", "UGT", "ULE", "UGE", "SLT", "SGT", "SLE", "SGE"):
+            signed = cmp_kind[0] == "S"
+            # borrow chain: R - y (lt) or y - R (gt); le = not gt, ge = not lt
+            r_minus_y = cmp_kind[1:] in ("LT", "GE")
+            truth = cmp_kind[1:] in ("LT", "GT")
+            reg = name.endswith("_R")
+            t8 = S(8)
+            body = []
+            if reg:
+                body += self.y_reg()
+                if signed:
+                    body += a_src1 + ["v_xor_b32 {}, 0x80000000, {}".format(S(9), P(7))] + off
+                    body += ["v_xor_b32 {0}, 0x80000000, {0}".format(Y(7))]
+                body += a_src0
+                if r_minus_y:  # P - Y
+                    body.append("v_sub_co_u32 {}, vcc, {}, {}".format(t8, P(0), Y(0)))
+                    body += ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(t8, P(k), Y(k))
+                             for k in range(1, 7)]
+                    if signed:
+                        body += off + ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(t8, S(9), Y(7))]
+                    else:
+                        body += ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(t8, P(7), Y(7))] + off
+                else:  # Y - P
+                    body.append("v_subrev_co_u32 {}, vcc, {}, {}".format(t8, P(0), Y(0)))
+                    body += ["v_subbrev_co_u32 {}, vcc, {}, {}, vcc".format(t8, P(k), Y(k))
+                             for k in range(1, 7)]
+                    if signed:
+                        body += off + ["v_subbrev_co_u32 {}, vcc, {}, {}, vcc".format(t8, S(9), Y(7))]
+                    else:
+                        body += ["v_subbrev_co_u32 {}, vcc, {}, {}, vcc".format(t8, P(7), Y(7))] + off
+            else:
+                body += self.consts(to_y=range(1, 8), flip7=signed)
+                if signed:
+                    body += a_src1 + ["v_xor_b32 {}, 0x80000000, {}".format(S(9), P(7))] + off
+                body += a_src1
+                if r_minus_y:  # P - c
+                    body.append("v_subrev_co_u32 {}, vcc, {}, {}".format(t8, S_K[0], P(0)))
+                    body += ["v_subbrev_co_u32 {}, vcc, {}, {}, vcc".format(t8, Y(k), P(k))
+                             for k in range(1, 7)]
+                    if signed:
+                        body += off + ["v_subbrev_co_u32 {}, vcc, {}, {}, vcc".format(t8, Y(7), S(9))]
+                    else:
+                        body += ["v_subbrev_co_u32 {}, vcc, {}, {}, vcc".format(t8, Y(7), P(7))] + off
+                else:  # c - P
+                    body.append("v_sub_co_u32 {}, vcc, {}, {}".format(t8, S_K[0], P(0)))
+                    body += ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(t8, Y(k), P(k))
+                             for k in range(1, 7)]
+                    if signed:
+                        body += off + ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(t8, Y(7), S(9))]
+                    else:
+                        body += ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(t8, Y(7), P(7))] + off
+            body += self.bool_out(truth) + self.wb(1)
+            return body + self.dispatch(1 if reg else 5)
+        if name in ("BAND", "BOR", "BXOR", "BEQ"):
+            ins = {"BAND": "v_and_b32", "BOR": "v_or_b32", "BXOR": "v_xor_b32",
+                   "BEQ": "v_xor_b32"}[name]
+            body = self.y_reg(1) + a_src0 + ["{} {}, {}, {}".format(ins, X(0), P(0), Y(0))] + off
+            if name == "BEQ":
+                body.append("v_not_b32 {0}, {0}".format(X(0)))
+            body.append("v_and_b32 {0}, 1, {0}".format(X(0)))
+            return body + self.wb(1) + self.dispatch(1)
+        if name == "BNOT":
+            body = a_src0 + ["v_not_b32 {}, {}".format(X(0), P(0))] + off
+            body.append("v_and_b32 {0}, 1, {0}".format(X(0)))
+            return body + self.wb(1) + self.dispatch(1)
+        if name in ("TRUE", "FALSE"):
+            body = ["v_mov_b32 {}, {}".format(X(0), 1 if name == "TRUE" else 0)]
+            return body + self.wb(1) + self.dispatch(1)
+        if name in ("ITE", "ITEC", "BITE"):
+            limbs = 1 if name == "BITE" else 8
+            body = self.field(S_B, 8) + self.field(S_C, 24)
+            cond_reg = S_B if name == "ITE" else S_W0
+            then_reg = S_W0 if name == "ITE" else S_B
+            body += self.idx_on(cond_reg, ["SRC1"]) + ["v_and_b32 {}, 1, {}".format(S(16), P(0))]
+            body += off + ["v_cmp_ne_u32 vcc, 0, {}".format(S(16))]
+            body += self.idx_on(S_C, ["SRC0"])
+            body += ["v_mov_b32 {}, {}".format(Y(k), P(k)) for k in range(limbs)] + off
+            body += self.idx_on(then_reg, ["SRC1"])
+            body += ["v_cndmask_b32 {}, {}, {}, vcc".format(X(k), Y(k), P(k)) for k in range(limbs)]
+            body += off
+            if name == "BITE":
+                body.append("v_and_b32 {0}, 1, {0}".format(X(0)))
+            return body + self.wb(limbs) + self.dispatch(1)
+        if name == "LOADC":
+            body = self.consts() + ["v_mov_b32 {}, {}".format(X(k), S_K[k]) for k in range(8)]
+            return body + self.wb() + self.dispatch(5)
+        if name in ("LSHRI", "SHLI", "SHLQ"):
+            body = ["s_lshr_b32 {}, {}, 17".format(S_L, S_W1),
+                    "s_lshr_b32 {}, {}, 5".format(S_Q, S_L),
+                    "s_and_b32 {}, {}, 31".format(S_R, S_L)]
+            if name == "LSHRI":  # S0..7 = x, S8..16 = 0; X_k = alignbit(S[k+q+1], S[k+q], r)
+                body += a_src0 + ["v_mov_b32 {}, {}".format(S(k), P(k)) for k in range(8)] + off
+                body += ["v_mov_b32 {}, 0".format(S(j)) for j in range(8, 17)]
+                body += self.idx_on(S_Q, ["SRC0", "SRC1"])
+                body += ["v_alignbit_b32 {}, {}, {}, {}".format(X(k), S(k + 1), S(k), S_R)
+                         for k in range(8)]
+            else:  # S0..8 = 0, S9..16 = x; idx = 8 - q
+                body += ["v_mov_b32 {}, 0".format(S(j)) for j in range(0, 9)]
+                body += a_src0 + ["v_mov_b32 {}, {}".format(S(9 + k), P(k)) for k in range(8)] + off
+                body += ["s_sub_u32 {}, 8, {}".format(S_Q, S_Q)]
+                if name == "SHLI":  # X_k = alignbit(S[9+k-q], S[8+k-q], 32 - r)
+                    body += ["s_sub_u32 {}, 32, {}".format(S_R, S_R)]
+                    body += self.idx_on(S_Q, ["SRC0", "SRC1"])
+                    body += ["v_alignbit_b32 {}, {}, {}, {}".format(X(k), S(k + 1), S(k), S_R)
+                             for k in range(8)]
+                else:  # X_k = S[9+k-q]
+                    body += self.idx_on(S_Q, ["SRC0"])
+                    body += ["v_mov_b32 {}, {}".format(X(k), S(k + 1)) for k in range(8)]
+            body += off
+            return body + self.wb() + self.dispatch(1)
+        if name in ("MUL_R", "MUL_C"):
+            # product scanning: column k of x*y accumulated in (c1:c0) = S16:S17 by
+            # v_mad_u64_u32 (carry-out to VCC folded into c2 = S18); x copied to S8..S15 so the
+            # result can go straight to X even when x is X
+            reg = name == "MUL_R"
+            body = self.y_reg() if reg else self.consts()
+            yv = (lambda j: Y(j)) if reg else (lambda j: S_K[j])
+            body += a_src0 + ["v_mov_b32 {}, {}".format(S(8 + k), P(k)) for k in range(8)] + off
+            acc = "v[{}:{}]".format(self.sb + 16, self.sb + 17)
+            c0, c1, c2 = S(16), S(17), S(18)
+            body.append("v_mad_u64_u32 {}, vcc, {}, {}, 0".format(acc, S(8), yv(0)))
+            body += ["v_mov_b32 {}, {}".format(X(0), c0), "v_mov_b32 {}, 0".format(c2)]
+            for k in range(1, 8):
+                # shift the column accumulator: (c2:c1:c0) >>= 32
+                body += ["v_mov_b32 {}, {}".format(c0, c1), "v_mov_b32 {}, {}".format(c1, c2)]
+                if k < 7:
+                    body.append("v_mov_b32 {}, 0".format(c2))
+                for i in range(k + 1):
+                    body.append("v_mad_u64_u32 {0}, vcc, {1}, {2}, {0}".format(acc, S(8 + i), yv(k - i)))
+                    if k < 7:
+                        body.append("v_addc_co_u32 {0}, vcc, 0, {0}, vcc".format(c2))
+                body.append("v_mov_b32 {}, {}".format(X(k), c0))
+            return body + self.wb() + self.dispatch(1 if reg else 5)
+        if name in ("LSHR_V", "ASHR_V", "SHL_V"):
+            # per-lane amount s = y (>= 256 saturates); t = x in S8..S15; 3-stage limb select
+            # network on bits 7..5 of s, then v_alignbit by the bit part
+            right = name != "SHL_V"
+            body = self.y_reg()
+            body += a_src0 + ["v_mov_b32 {}, {}".format(S(8 + k), P(k)) for k in range(8)] + off
+            big = "s[62:63]"
+            body += ["v_or3_b32 {}, {}, {}, {}".format(S(16), Y(1), Y(2), Y(3)),
+                     "v_or3_b32 {0}, {0}, {1}, {2}".format(S(16), Y(4), Y(5)),
+                     "v_or3_b32 {0}, {0}, {1}, {2}".format(S(16), Y(6), Y(7)),
+                     "v_cmp_ne_u32_e64 {}, 0, {}".format(big, S(16)),
+                     "v_cmp_lt_u32_e32 vcc, 0xff, {}".format(Y(0)),
+                     "s_or_b64 {0}, {0}, vcc".format(big),
+                     "v_lshrrev_b32 {}, 5, {}".format(S(18), Y(0)),   # q (limbs)
+                     "v_and_b32 {}, 31, {}".format(S(19), Y(0))]      # r (bits)
+            fill = "0"
+            if name == "ASHR_V":
+                body.append("v_ashrrev_i32 {}, 31, {}".format(S(17), S(15)))
+                fill = S(17)
+            t = [S(8 + k) for k in range(8)]
+            for st in (4, 2, 1):
+                body += ["v_and_b32 {}, {}, {}".format(S(20), st, S(18)),
+                         "v_cmp_ne_u32_e32 vcc, 0, {}".format(S(20))]
+                if right:
+                    for k in range(8):
+                        src = t[k + st] if k + st < 8 else fill
+                        body.append("v_cndmask_b32_e64 {0}, {0}, {1}, vcc".format(t[k], src))
+                else:
+                    for k in range(7, -1, -1):
+                        src = t[k - st] if k - st >= 0 else "0"
+                        body.append("v_cndmask_b32_e64 {0}, {0}, {1}, vcc".format(t[k], src))
+            if right:
+                for k in range(8):
+                    hi = t[k + 1] if k < 7 else fill
+                    body.append("v_alignbit_b32 {}, {}, {}, {}".format(X(k), hi, t[k], S(19)))
+                fillv = fill
+            else:
+                body += ["v_sub_u32 {}, 32, {}".format(S(20), S(19)),
+                         "v_cmp_eq_u32_e32 vcc, 0, {}".format(S(19))]
+                for k in range(8):
+                    lo = t[k - 1] if k > 0 else "0"
+                    body.append("v_alignbit_b32 {}, {}, {}, {}".format(X(k), t[k], lo, S(20)))
+                    body.append("v_cndmask_b32_e64 {0}, {0}, {1}, vcc".format(X(k), t[k]))
+                fillv = "0"
+            body += ["v_cndmask_b32_e64 {0}, {0}, {1}, {2}".format(X(k), fillv, big) for k in range(8)]
+            return body + self.wb() + self.dispatch(1)
+        raise KeyError(name)
+
+    def fetch_text(self):
+        """Operands of a complex op into S0..7 (x = R[a']), S8..15 (y = R[b] or the inline
+        constant), S16..23 (R[c])."""
+        S, P = self.S, self.P
+        out = ["s_nop 1"]
+        out += ["s_set_gpr_idx_on %[w0], gpr_idx(SRC0)"]
+        out += ["v_mov_b32 {}, {}".format(S(k), P(k)) for k in range(8)] + ["s_set_gpr_idx_off"]
+        out += ["s_lshr_b32 {}, %[w0], 24".format(S_C), "s_set_gpr_idx_on {}, gpr_idx(SRC0)".format(S_C)]
+        out += ["v_mov_b32 {}, {}".format(S(16 + k), P(k)) for k in range(8)]
+        out += ["s_set_gpr_idx_off", "s_bitcmp1_b32 %[w1], 31", "s_cbranch_scc1 L_yc_%="]
+        out += ["s_lshr_b32 {}, %[w0], 8".format(S_B), "s_set_gpr_idx_on {}, gpr_idx(SRC0)".format(S_B)]
+        out += ["v_mov_b32 {}, {}".format(S(8 + k), P(k)) for k in range(8)]
+        out += ["s_set_gpr_idx_off", "s_branch L_done_%=", "L_yc_%=:"]
+        for i in range(4):
+            out.append("s_add_u32 {}, %[ip], {}".format(S_L, i + 1))
+            out.append("v_readlane_b32 {}, %[ic0], {}".format(S_K[2 * i], S_L))
+            out.append("v_readlane_b32 {}, %[ic1], {}".format(S_K[2 * i + 1], S_L))
+        out += ["v_mov_b32 {}, {}".format(S(8 + k), S_K[k]) for k in range(8)]
+        out += ["L_done_%=:"]
+        return out
+
+    def commit_text(self):
+        """X = z (S0..7), then R[d'] = X."""
+        S, X = self.S, self.X
+        out = ["v_mov_b32 {}, {}".format(X(k), S(k)) for k in range(8)]
+        out += ["s_lshr_b32 {}, %[w0], 16".format(S_D)]
+        out += ["s_set_gpr_idx_on {}, gpr_idx(DST)".format(S_D)]
+        out += ["v_mov_b32 {}, {}".format(self.P(k), X(k)) for k in range(8)]
+        out += ["s_set_gpr_idx_off"]
+        return out
+
+    def asm_text(self):
+        lines = ["s_nop 1",
+                 "s_getpc_b64 s[40:41]",
+                 "L_pc_%=:",
+                 "s_add_u32 {0}, {0}, (L_tab_%= - L_pc_%=)".format(S_TAB),
+                 "s_addc_u32 {0}, {0}, 0".format(S_TAB_HI)]
+        lines += self.dispatch(0)
+        lines += [".p2align 8", "L_tab_%=:"]
+        bodies = []
+        for i in range(NSLOTS):
+            lines.append(".org L_tab_%= + {}".format(i * SLOT))
+            name = OPS[i] if i < len(OPS) else "EXIT"
+            h = self.handler(name)
+            if name in OUT_OF_LINE:  # too long for a slot: jump to a body after the table
+                lines.append("s_branch L_body_{}_%=".format(name))
+                bodies += ["L_body_{}_%=:".format(name)] + h
+            else:
+                lines += h
+        lines += [".org L_tab_%= + {}".format(NSLOTS * SLOT)] + bodies + ["L_out_%=:"]
+        return lines
+
+
+N_SCRATCH = 24  # S0..S23, declared clobbered by the core (fetch outputs use all 24)
+
+
+def check_registers(core, lines, n_scratch):
+    """Every register the asm names must be a plane register, a declared scratch VGPR or a
+    declared SGPR clobber: anything else could hold a live compiler value (an address...)."""
+    import re
+    hi_plane = 8 * core.nr1
+    ok_v = set(range(hi_plane)) | set(range(core.sb, core.sb + n_scratch))
+    ok_s = {int(x[1:]) for x in SGPR_CLOBBERS}
+    for line in lines:
+        for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", line):
+            for r in range(int(a), int(b) + 1):
+                assert r in ok_v, (line, r)
+        for r in re.findall(r"\bv(\d+)\b", line):
+            assert int(r) in ok_v, (line, r)
+        for a, b in re.findall(r"\bs\[(\d+):(\d+)\]", line):
+            for r in range(int(a), int(b) + 1):
+                assert r in ok_s, (line, r)
+        for r in re.findall(r"\bs(\d+)\b", line):
+            assert int(r) in ok_s, (line, r)
+
+
+def emit(out):
+    w = out.write
+    w("// GENERATED by gen_asm_core.py -- do not edit.  Threaded-code asm core of the sieve\n")
+    w("// interpreter (see the generator's docstring and dev_isa.h for the machine model).\n")
+    w("#pragma once\n\n")
+    for name, num in OPNUM.items():
+        w("static_assert(D_{} == {}, \"asm core opcode numbering\");\n".format(name, num))
+    w("static_assert(D_NUM_ASM == {}, \"asm core covers every asm op\");\n\n".format(len(OPS)))
+    w("template <int NR> struct AsmCore;\n\n")
+    for nr in (7, 15):
+        c = Core(nr)
+        nr1 = nr + 1
+        w("template <> struct AsmCore<{}> {{\n".format(nr))
+        w("    typedef u32 plane_t __attribute__((ext_vector_type({})));\n".format(nr1))
+        w("    // runs asm-core instructions from slot ip of the window (ic0, ic1); returns the\n")
+        w("    // slot of the first instruction it does not handle\n")
+        w("    __device__ __forceinline__ static u32 run(plane_t& p0, plane_t& p1, plane_t& p2,\n")
+        w("                                              plane_t& p3, plane_t& p4, plane_t& p5,\n")
+        w("                                              plane_t& p6, plane_t& p7, u32 ic0, u32 ic1,\n")
+        w("                                              u32 ip) {\n")
+        w("        asm volatile(\n")
+        for line in c.asm_text():
+            w("            \"{}\\n\"\n".format(line))
+        cons = []
+        for k in range(8):
+            cons.append("\"+{{v[{}:{}]}}\"(p{})".format(k * nr1, k * nr1 + nr, k))
+        w("            : {}, [ip] \"+s\"(ip)\n".format(", ".join(cons)))
+        w("            : [ic0] \"v\"(ic0), [ic1] \"v\"(ic1)\n")
+        check_registers(c, c.asm_text(), N_SCRATCH)
+        check_registers(c, c.fetch_text(), N_SCRATCH)
+        check_registers(c, c.commit_text(), N_SCRATCH)
+        clob = ["\"v{}\"".format(c.sb + j) for j in range(N_SCRATCH)] + \
+               ["\"{}\"".format(s) for s in SGPR_CLOBBERS] + ["\"vcc\"", "\"scc\"", "\"m0\""]
+        w("            : {});\n".format(", ".join(clob)))
+        w("        return ip;\n")
+        w("    }\n")
+        sb = c.sb
+        vec = "typedef u32 v8_t __attribute__((ext_vector_type(8)));\n"
+        w("    " + vec)
+        w("    // operands of the complex op at slot ip: x = R[a'], y = R[b] / inline const, c = R[c]\n")
+        w("    __device__ __forceinline__ static void fetch(plane_t& p0, plane_t& p1, plane_t& p2,\n")
+        w("            plane_t& p3, plane_t& p4, plane_t& p5, plane_t& p6, plane_t& p7, u32 ic0,\n")
+        w("            u32 ic1, u32 ip, u32 w0, u32 w1, v8_t& x, v8_t& y, v8_t& c) {\n")
+        w("        asm volatile(\n")
+        for line in c.fetch_text():
+            w("            \"{}\\n\"\n".format(line))
+        w("            : {}, \"={{v[{}:{}]}}\"(x), \"={{v[{}:{}]}}\"(y), \"={{v[{}:{}]}}\"(c)\n".format(
+            ", ".join(cons), sb, sb + 7, sb + 8, sb + 15, sb + 16, sb + 23))
+        w("            : [ic0] \"v\"(ic0), [ic1] \"v\"(ic1), [ip] \"s\"(ip), [w0] \"s\"(w0), [w1] \"s\"(w1)\n")
+        w("            : {});\n".format(", ".join("\"{}\"".format(x) for x in
+                                          [S_B, S_C, S_L] + S_K + ["scc", "m0"])))
+        w("    }\n")
+        w("    // X = z, then R[d'] = X\n")
+        w("    __device__ __forceinline__ static void commit(plane_t& p0, plane_t& p1, plane_t& p2,\n")
+        w("            plane_t& p3, plane_t& p4, plane_t& p5, plane_t& p6, plane_t& p7, u32 w0,\n")
+        w("            v8_t z) {\n")
+        w("        asm volatile(\n")
+        for line in c.commit_text():
+            w("            \"{}\\n\"\n".format(line))
+        w("            : {}\n".format(", ".join(cons)))
+        w("            : [w0] \"s\"(w0), \"{{v[{}:{}]}}\"(z)\n".format(sb, sb + 7))
+        w("            : \"{}\", \"scc\", \"m0\");\n".format(S_D))
+        w("    }\n")
+        w("};\n\n")
+
+
+if __name__ == "__main__":
+    emit(sys.stdout)

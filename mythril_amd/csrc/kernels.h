@@ -13,17 +13,29 @@ struct KParams {
     const mh_dev_tape* tapes;    // per-tape headers
     const uint32_t* consts;      // device constant pool, 8 limbs per entry
     const uint32_t* assign;      // SoA assignment buffer
+    const uint32_t* tape_ids;    // the tapes this launch evaluates (one kernel-variant bucket)
     uint64_t capacity;           // rows allocated per column
     uint32_t n_pre;              // columns preloaded into R0..R(n_pre-1)
-    uint32_t tape_first, tape_count;
+    uint32_t n_ids;              // entries of tape_ids
+    uint32_t result_base;        // results are indexed by tape id - result_base
+    uint32_t pad;
     uint64_t row_first, row_count, index_base;
     uint32_t mode;
-    unsigned long long* first_hit;  // [tape_count]
-    unsigned long long* hit_count;  // [tape_count]
+    unsigned long long* first_hit;  // [tapes of the run]
+    unsigned long long* hit_count;  // [tapes of the run]
+    uint32_t* values_out;           // parity path: [n_ids][8][row_count] root values, or null
 };
 
-hipError_t launch_sieve(const KParams& p, uint32_t feat, hipStream_t stream);
-hipError_t launch_values(const KParams& p, uint32_t tape, uint32_t* out, hipStream_t stream);
+// Kernel variants: register-file size class x feature set.
+enum { V_NR_SMALL = 0, V_NR_MAX = 1 };
+inline uint32_t variant_of(uint32_t n_regs, uint32_t features) {
+    const uint32_t nr = n_regs <= MH_NR_SMALL ? V_NR_SMALL : V_NR_MAX;
+    const uint32_t fc = (features & (F_KECCAK | F_EVM)) ? 2u : (features & (F_DIV | F_CPLX)) ? 1u : 0u;
+    return nr * 3 + fc;  // 0..5
+}
+constexpr uint32_t kNumVariants = 6;
+
+hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream);
 hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars, uint64_t seed,
                            uint64_t base, hipStream_t stream);
 hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uint32_t* sink,

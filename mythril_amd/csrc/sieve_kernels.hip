@@ -2,31 +2,48 @@
 // micro-benchmark.
 //
 // Mapping: one lane = one candidate assignment (row); a 256-thread workgroup = 256 consecutive
-// rows; every wave walks the whole tape batch, so the tape stream (instruction words, constants)
-// is wave-uniform and comes through the scalar unit (s_load), while the per-lane 256-bit values
-// live in VGPRs.  The register file is 8 "limb planes", each an ext_vector of MH_NUM_REGS u32,
-// indexed by the wave-uniform register number (s_set_gpr_idx_on / v_mov), so no per-lane
-// scratch is touched.  Assignment columns 0..3 are loaded once per launch into R0..R3 and stay
-// resident for every tape: HBM traffic is 32 B x columns per row per launch, independent of the
-// number of tapes.  Results are reduced per workgroup in LDS (64-tape chunks) and flushed with
-// one atomic per tape per workgroup.
+// rows; every wave walks the launch's whole tape list, so the tape stream (instruction words,
+// constants) is wave-uniform: instructions arrive 64 at a time in two VGPRs (lane j = instruction
+// j, one coalesced 512-B load) and are extracted with v_readlane into SGPRs; constant operands
+// come through the scalar unit (s_load).  Per-lane 256-bit values live in VGPRs: the accumulator
+// X in 8 fixed registers and the register file as 8 "limb planes", each an ext_vector of NR u32
+// indexed by the wave-uniform register number (s_set_gpr_idx_on / v_mov, no scratch).
+// Assignment columns 0..3 are loaded once per launch into R0..R3 and stay resident for every
+// tape: HBM traffic is 32 B x columns per row per launch, independent of the number of tapes.
+// Tapes are processed in chunks of up to 64 whose instruction words (contiguous in HBM, see
+// mh_tapes_compile) are first staged into LDS by the whole workgroup with one coalesced copy, so
+// instruction fetch never waits on L2.  Per-tape results are reduced per workgroup in LDS and
+// flushed with one atomic per tape per workgroup.
+//
+// Kernel variants (kernels.h variant_of): NR in {7, 15} x {asm only, + C++ division/overflow
+// predicates, + keccak/EVM};
+// mh_run launches one variant per non-empty bucket of tapes, so a tape set's simple tapes run
+// with the register budget (and occupancy) they need rather than the worst tape's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "dev_isa.h"
+#include "exec.h"
 #include "kernels.h"
 #include "u256_ops.h"
 
 using namespace mh;
 
+#ifndef MH_ASM_CORE
+#define MH_ASM_CORE 1  // 0: every op through the C++ step() (reference / A-B builds)
+#endif
+
 namespace {
+
+#include "asm_core.inc"
 
 constexpr int kBlock = 256;
 constexpr int kChunk = 64;  // tapes per LDS result chunk
 
+// Register file: 8 limb planes of NR+1 VGPRs; R[NR] is the accumulator X (dev_isa.h).
 template <int NR>
 struct RegFile {
-    typedef u32 plane_t __attribute__((ext_vector_type(NR)));
+    typedef u32 plane_t __attribute__((ext_vector_type(NR + 1)));
     plane_t p0, p1, p2, p3, p4, p5, p6, p7;
 
     __device__ __forceinline__ void read(u32 r, u32* x) const {
@@ -38,7 +55,36 @@ struct RegFile {
         p4[r] = x[4]; p5[r] = x[5]; p6[r] = x[6]; p7[r] = x[7];
     }
     __device__ __forceinline__ u32 read0(u32 r) const { return p0[r]; }
-    __device__ __forceinline__ void write0(u32 r, u32 v) { p0[r] = v; }
+};
+
+// Instruction window: lane j of the wave holds slot (window base + j) of the tape in two VGPRs.
+struct InsnCache {
+    u32 w0, w1;
+};
+
+// The machine interface of exec.h's step() on the device (the complex ops).
+template <int NR>
+struct DevMachine {
+    RegFile<NR> R;
+    const KParams* p;
+    u64 lrow;
+    InsnCache ic;
+
+    __device__ __forceinline__ u32 nrx() const { return NR; }
+    __device__ __forceinline__ void read(u32 r, u32* v) const { R.read(r, v); }
+    __device__ __forceinline__ u32 read0(u32 r) const { return R.read0(r); }
+    __device__ __forceinline__ void write(u32 r, const u32* v) { R.write(r, v); }
+    __device__ __forceinline__ void iconst(u32 slot, u32* v) const {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[2 * k] = __builtin_amdgcn_readlane(ic.w0, slot + k);
+            v[2 * k + 1] = __builtin_amdgcn_readlane(ic.w1, slot + k);
+        }
+    }
+    __device__ __forceinline__ void var(u32 col, u32* v) const {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p->assign[((u64)col * 8 + k) * p->capacity + lrow];
+    }
 };
 
 __device__ __forceinline__ u64 splitmix64(u64 x) {
@@ -49,346 +95,193 @@ __device__ __forceinline__ u64 splitmix64(u64 x) {
     return z ^ (z >> 31);
 }
 
-// Keccak-256 of up to three byte-aligned pieces (big-endian byte order within each piece).
-__device__ __forceinline__ void keccak_pieces(const u32* P0, const u32* P1, const u32* P2,
-                                              u32 n0, u32 n1, u32 n2, u32* z) {
-    typedef u32 v32_t __attribute__((ext_vector_type(32)));
-    v32_t pv;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { pv[k] = P0[k]; pv[8 + k] = P1[k]; pv[16 + k] = P2[k]; }
-    const u32 len = n0 + n1 + n2;
-    u64 st[25];
-#pragma unroll
-    for (int i = 0; i < 25; ++i) st[i] = 0;
-#pragma unroll
-    for (int wd = 0; wd < 34; ++wd) {
-        u32 word = 0;
-#pragma unroll
-        for (int bi = 0; bi < 4; ++bi) {
-            const u32 m = 4u * wd + bi;
-            u32 byte = 0;
-            if (m < len) {  // wave-uniform
-                const u32 p = m < n0 ? 0u : (m < n0 + n1 ? 1u : 2u);
-                const u32 off = p == 0 ? 0u : (p == 1 ? n0 : n0 + n1);
-                const u32 np = p == 0 ? n0 : (p == 1 ? n1 : n2);
-                const u32 e = np - 1u - (m - off);  // little-endian byte index in the piece
-                const u32 limb = pv[p * 8u + (e >> 2)];
-                byte = (limb >> (8u * (e & 3u))) & 0xFFu;
+// Run one tape from its first window ic: on return X (= R[NR]) holds the root.  The asm core
+// runs the simple ops; each complex op, window change and the end come back here.  LDS holds the
+// tape's slots (or global memory when the tape alone exceeds the LDS chunk).
+template <int NR, int FEAT>
+__device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, InsnCache ic,
+                                          u32 n) {
+    u32 win = 0, ip = 0;
+    for (;;) {
+#if MH_ASM_CORE
+        ip = AsmCore<NR>::run(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6, m.R.p7,
+                              ic.w0, ic.w1, ip);
+#endif
+        const u32 w0 = __builtin_amdgcn_readlane(ic.w0, ip);
+        const u32 w1 = __builtin_amdgcn_readlane(ic.w1, ip);
+        const u32 op = w1 & 0xFFu;
+        if (op == D_END) break;
+        if (op == D_WINDOW) {
+            win += MH_WINDOW;
+            const u32 j = win + (threadIdx.x & 63u);
+            ic.w0 = ic.w1 = 0u;
+            if (j < n) {
+                const uint2 v = src[j];
+                ic.w0 = v.x;
+                ic.w1 = v.y;
             }
-            if (m == len) byte |= 0x01u;
-            if (m == 135u) byte |= 0x80u;
-            word |= byte << (8 * bi);
+            ip = 0;
+            continue;
         }
-        st[wd >> 1] |= (u64)word << (32 * (wd & 1));
-    }
-    keccak_f1600(st);
+#if MH_ASM_CORE
+        if constexpr (FEAT == 0) {
+            break;  // asm-only variant: the host never buckets a complex op here
+        } else {
+            // complex op: operands out of the register file by asm, the op in C++, the result
+            // back by asm -- the C++ code never touches the planes, so they stay in their VGPRs
+            typedef typename AsmCore<NR>::v8_t v8_t;
+            v8_t xv, yv, cv;
+            AsmCore<NR>::fetch(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6, m.R.p7,
+                               ic.w0, ic.w1, ip, w0, w1, xv, yv, cv);
+            u32 x[8], y[8], c3[8], z[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int i = 7 - k;  // u32 word i of the output bytes
-        const u32 wv = (i & 1) ? (u32)(st[i >> 1] >> 32) : (u32)st[i >> 1];
-        z[k] = bswap32(wv);
+            for (int k = 0; k < 8; ++k) { x[k] = xv[k]; y[k] = yv[k]; c3[k] = cv[k]; }
+            complex_op<FEAT>(m, w1, x, y, c3, z);
+            v8_t zv;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) zv[k] = z[k];
+            AsmCore<NR>::commit(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6, m.R.p7,
+                                w0, zv);
+            ip += (w1 & F_YC) ? 5u : 1u;
+        }
+#else
+        m.ic = ic;
+        ip += step<FEAT, true>(m, w0, w1, ip);
+#endif
     }
 }
 
-typedef const __attribute__((address_space(4))) u32* cu32_ptr;  // scalar-cache path
-
-struct TapeHead {
-    u32 insn_off, n_insns, root_reg, root_bool;
-};
-
-__device__ __forceinline__ TapeHead tape_head(const KParams& p, u32 t) {
-    const cu32_ptr tp = (cu32_ptr)p.tapes + 4ull * t;
-    return TapeHead{tp[0], tp[1], tp[2], tp[3]};
+template <int NR>
+__device__ __forceinline__ void preload(DevMachine<NR>& m, const KParams& p) {
+#pragma unroll
+    for (u32 v = 0; v < MH_MAX_PRELOAD; ++v) {
+        if (v < p.n_pre) {
+            u32 x[8];
+            m.var(v, x);
+            m.R.write(v, x);
+        }
+    }
 }
 
-// Instruction stream: lane j of the wave holds instruction (64*chunk + j) of the current tape
-// in two VGPRs (one coalesced 512-B load per 64 instructions, prefetched one tape ahead); the
-// interpreter extracts instruction i with v_readlane into SGPRs, so fetching costs no memory
-// round trip per instruction.
-struct InsnCache {
-    u32 w0, w1;
-};
+// LDS-staged instruction chunk: up to kChunk tapes whose instruction words fit in kLdsInsns.
+constexpr u32 kLdsInsns = 2048;  // 16 KB
 
-__device__ __forceinline__ InsnCache load_insns(const KParams& p, u32 insn_off, u32 n, u32 first) {
-    const u32 lane = threadIdx.x & 63u;
-    const u32 j = first + lane;
+__device__ __forceinline__ InsnCache lds_insns(const uint2* s_insn, u32 off, u32 n, u32 first) {
+    const u32 j = first + (threadIdx.x & 63u);
     InsnCache c{0u, 0u};
     if (j < n) {
-        const uint2 v = p.insns[insn_off + j];
+        const uint2 v = s_insn[off + j];
         c.w0 = v.x;
         c.w1 = v.y;
     }
     return c;
 }
 
-__device__ __forceinline__ void load_const(const KParams& p, u32 idx, u32* z) {
-    const cu32_ptr cp = (cu32_ptr)p.consts + 8ull * idx;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) z[k] = cp[k];
-}
-
-// One instruction = operand reads (register file or scalar constant), one compute, one write of
-// R[d]: a single definition of the register-file vectors per step keeps the compiler from
-// materialising copies of the whole file on every control-flow merge.
-template <int NR, int FEAT>
-__device__ __forceinline__ void exec_tape(RegFile<NR>& R, const KParams& p, InsnCache ic,
-                                          u32 insn_off, u32 n, u64 lrow) {
-    for (u32 i = 0; i < n; ++i) {
-        if ((i & 63u) == 0 && i) ic = load_insns(p, insn_off, n, i);  // tapes > 64 insns
-        const u32 w0 = __builtin_amdgcn_readlane(ic.w0, i & 63u);
-        const u32 w1 = __builtin_amdgcn_readlane(ic.w1, i & 63u);
-        const u32 op = w0 & 0xFFu, d = (w0 >> 8) & 0xFFu, a = (w0 >> 16) & 0xFFu, b = w0 >> 24;
-        const u32 w = (w1 >> 2) & 0x1FFu, aux = w1 >> 11;
-        u32 x[8], y[8], z[8];
-        // unconditional register reads (no control-flow merge of operand values); a constant
-        // operand b overwrites y from the scalar constant pool
-        R.read(a, x);
-        R.read(b, y);
-        if (((MH_CONST_OPERAND_OK >> op) & 1u) && (w1 & F_BCONST)) load_const(p, aux, y);
-        switch (op) {
-            // ---- bv x bv -> bv
-            case D_ADD: add256(x, y, z); mask_w(z, w); break;
-            case D_SUB: sub256(x, y, z); mask_w(z, w); break;
-            case D_MUL: mul_lo256(x, y, z); mask_w(z, w); break;
-            case D_AND:
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = x[k] & y[k];
-                break;
-            case D_OR:
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = x[k] | y[k];
-                break;
-            case D_XOR:
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = x[k] ^ y[k];
-                break;
-            case D_SHL: bvshl_v(x, shift_amount(y), z, w); break;
-            case D_LSHR: bvlshr_v(x, shift_amount(y), z, w); break;
-            case D_ASHR: bvashr_v(x, shift_amount(y), z, w); break;
-            case D_CONCAT: {
-                u32 t[8];
-                shl256(x, aux, t);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = t[k] | y[k];
-                break;
-            }
-            case D_UDIV: case D_UREM: case D_SDIV: case D_SREM: case D_SMOD:
-                if constexpr ((FEAT & F_DIV) != 0) divmod_family(op - D_UDIV, x, y, z, w);
-                break;
-            case D_EXP:
-                if constexpr ((FEAT & F_EVM) != 0) evm_exp(x, y, z, w);
-                break;
-            case D_SIGNEXT:
-                if constexpr ((FEAT & F_EVM) != 0) evm_signextend(x, y, z);
-                break;
-            case D_BYTE:
-                if constexpr ((FEAT & F_EVM) != 0) evm_byte(x, y, z);
-                break;
-            // ---- bv -> bv
-            case D_NEG: neg256(x, z); mask_w(z, w); break;
-            case D_NOT:
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = ~x[k];
-                mask_w(z, w);
-                break;
-            case D_SHLI:
-                if (aux < w) {
-                    shl256(x, aux, z);
-                    mask_w(z, w);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) z[k] = 0;
-                }
-                break;
-            case D_LSHRI:
-                if (aux < w) {
-                    shr256(x, aux, z, 0u);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) z[k] = 0;
-                }
-                break;
-            case D_ASHRI: bvashr_v(x, aux, z, w); break;
-            case D_EXTRACT: shr256(x, aux, z, 0u); mask_w(z, w); break;
-            case D_SEXT: sext_to256(x, aux, z); mask_w(z, w); break;
-            case D_MOV:
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = x[k];
-                break;
-            // ---- bv x bv -> Bool (0/1 in limb 0)
-            case D_EQ: z[0] = eq256(x, y); break;
-            case D_ULT: z[0] = ult256(x, y); break;
-            case D_ULE: z[0] = !ult256(y, x); break;
-            case D_SLT: z[0] = slt_w(x, y, w); break;
-            case D_SLE: z[0] = !slt_w(y, x, w); break;
-            case D_UADD_NOOVFL: {
-                u32 t[8];
-                const u32 cy = add256(x, y, t);
-                u32 hi = 0;
-                if (w < 256) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) hi |= t[k] & ~width_mask(k, w);
-                }
-                z[0] = !(cy || hi);
-                break;
-            }
-            case D_UMUL_NOOVFL: {
-                u32 t[16];
-                mul_full256(x, y, t);
-                u32 hi = 0;
-#pragma unroll
-                for (int k = 8; k < 16; ++k) hi |= t[k];
-                if (w < 256) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) hi |= t[k] & ~width_mask(k, w);
-                }
-                z[0] = hi == 0;
-                break;
-            }
-            // ---- Bool (limb 0)
-            case D_BAND: z[0] = x[0] & y[0] & 1u; break;
-            case D_BOR: z[0] = (x[0] | y[0]) & 1u; break;
-            case D_BXOR: z[0] = (x[0] ^ y[0]) & 1u; break;
-            case D_BEQ: z[0] = ((x[0] ^ y[0]) & 1u) ^ 1u; break;
-            case D_BNOT: z[0] = (x[0] & 1u) ^ 1u; break;
-            case D_TRUE: z[0] = 1u; break;
-            case D_FALSE: z[0] = 0u; break;
-            // ---- others
-            case D_ITE: {  // x[0] = cond, y = then, R[aux] = else
-                u32 e[8];
-                R.read(aux, e);
-                const bool cnd = (x[0] & 1u) != 0;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = cnd ? y[k] : e[k];
-                break;
-            }
-            case D_BITE: {
-                const bool cnd = (x[0] & 1u) != 0;
-                z[0] = cnd ? (y[0] & 1u) : (R.read0(aux) & 1u);
-                break;
-            }
-            case D_LOADC: load_const(p, aux, z); break;
-            case D_LOADVAR:
-#pragma unroll
-                for (int k = 0; k < 8; ++k) z[k] = p.assign[((u64)aux * 8 + k) * p.capacity + lrow];
-                break;
-            case D_KECCAK:
-                if constexpr ((FEAT & F_KECCAK) != 0) {
-                    const u32 np = (w1 >> 26) & 3u;
-                    const u32 n0 = (w1 >> 8) & 63u, n1 = (w1 >> 14) & 63u, n2 = (w1 >> 20) & 63u;
-                    u32 P2[8];
-                    R.read(w1 & 0xFFu, P2);
-                    keccak_pieces(x, y, P2, n0, np > 1 ? n1 : 0u, np > 2 ? n2 : 0u, z);
-                }
-                break;
-            default:
-                break;
-        }
-        R.write(d, z);
-    }
-}
-
-template <int NR>
-__device__ __forceinline__ void preload(RegFile<NR>& R, const KParams& p, u64 lrow) {
-#pragma unroll
-    for (u32 v = 0; v < MH_MAX_PRELOAD; ++v) {
-        if (v < p.n_pre) {
-            u32 x[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) x[k] = p.assign[((u64)v * 8 + k) * p.capacity + lrow];
-            R.write(v, x);
-        }
-    }
-}
-
 template <int NR, int FEAT>
 __global__ void __launch_bounds__(kBlock) sieve_kernel(const KParams p) {
+    __shared__ uint2 s_insn[kLdsInsns];
+    __shared__ u32 s_off[kChunk], s_n[kChunk], s_rb[kChunk], s_tid[kChunk];
+    __shared__ u32 s_meta[4];  // tapes in chunk, first word index, words, streaming flag
     __shared__ unsigned long long s_min[kChunk];
     __shared__ unsigned long long s_cnt[kChunk];
-    RegFile<NR> R;
     const u32 tid = threadIdx.x;
     const u64 row = p.row_first + (u64)blockIdx.x * kBlock + tid;
-    const u64 row_end = p.row_first + p.row_count;
-    const bool valid = row < row_end;
-    const u64 lrow = valid ? row : p.row_first;
-    preload<NR>(R, p, lrow);
+    const bool valid = row < p.row_first + p.row_count;
+    DevMachine<NR> m;
+    m.p = &p;
+    m.lrow = valid ? row : p.row_first;
+    preload<NR>(m, p);
     const u64 block_first = p.index_base + p.row_first + (u64)blockIdx.x * kBlock;
     const u64 wave_first = block_first + (tid & ~63u);
-    const u32 t_end = p.tape_first + p.tape_count;
-    for (u32 cb = p.tape_first; cb < t_end; cb += kChunk) {
-        const u32 nt = (t_end - cb) < (u32)kChunk ? (t_end - cb) : (u32)kChunk;
-        __syncthreads();
+    for (u32 cb = 0; cb < p.n_ids;) {
+        __syncthreads();  // previous chunk's LDS fully consumed
         if (tid < (u32)kChunk) {
-            s_min[tid] = (p.mode == MH_MODE_FIRST_HIT && tid < nt && p.first_hit)
-                             ? p.first_hit[cb - p.tape_first + tid] : ~0ull;
+            // chunk formation by wave 0: the bucket's tapes are contiguous in the word array,
+            // so the chunk is the longest prefix of the next kChunk tapes within kLdsInsns
+            const u32 i = cb + tid;
+            const bool in = i < p.n_ids;
+            const u32 t = in ? p.tape_ids[i] : 0u;
+            const mh_dev_tape h = p.tapes[t];
+            const u32 base = __builtin_amdgcn_readfirstlane(h.insn_off);
+            const u32 end = h.insn_off + h.n_insns - base;
+            const unsigned long long fit = __builtin_amdgcn_ballot_w64(in && end <= kLdsInsns);
+            u32 nt = (u32)__builtin_popcountll(fit);
+            const u32 stream = nt == 0 ? 1u : 0u;  // a single tape larger than the LDS chunk
+            nt = stream ? 1u : nt;
+            s_off[tid] = stream ? h.insn_off : h.insn_off - base;
+            s_n[tid] = h.n_insns;
+            s_rb[tid] = h.root_bool;
+            s_tid[tid] = t;
+            s_min[tid] = (p.mode == MH_MODE_FIRST_HIT && in && p.first_hit)
+                             ? p.first_hit[t - p.result_base] : ~0ull;
             s_cnt[tid] = 0;
+            if (tid == nt - 1) {
+                s_meta[0] = nt;
+                s_meta[1] = base;
+                s_meta[2] = stream ? 0u : end;
+                s_meta[3] = stream;
+            }
         }
         __syncthreads();
-        TapeHead th = tape_head(p, cb);
-        InsnCache ic = load_insns(p, th.insn_off, th.n_insns, 0);
+        const u32 nt = __builtin_amdgcn_readfirstlane(s_meta[0]);
+        const u32 wbase = __builtin_amdgcn_readfirstlane(s_meta[1]);
+        const u32 nwords = __builtin_amdgcn_readfirstlane(s_meta[2]);
+        const bool stream = __builtin_amdgcn_readfirstlane(s_meta[3]) != 0;
+        for (u32 k = tid; k < nwords; k += kBlock) s_insn[k] = p.insns[wbase + k];
+        __syncthreads();
+        u32 off = __builtin_amdgcn_readfirstlane(s_off[0]);
+        u32 n = __builtin_amdgcn_readfirstlane(s_n[0]);
+        InsnCache ic = stream ? lds_insns(p.insns, off, n, 0) : lds_insns(s_insn, off, n, 0);
         for (u32 j = 0; j < nt; ++j) {
-            const u32 t = cb + j;
-            // prefetch the next tape's header and first 64 instructions
-            const TapeHead th_next = tape_head(p, j + 1 < nt ? t + 1 : t);
-            const InsnCache ic_next = load_insns(p, th_next.insn_off, th_next.n_insns, 0);
+            const u32 jn = j + 1 < nt ? j + 1 : j;
+            const u32 off_next = __builtin_amdgcn_readfirstlane(s_off[jn]);
+            const u32 n_next = __builtin_amdgcn_readfirstlane(s_n[jn]);
+            InsnCache ic_next{0u, 0u};
+            if (!stream) ic_next = lds_insns(s_insn, off_next, n_next, 0);
+            bool skip = false;
             if (p.mode == MH_MODE_FIRST_HIT) {
                 // early exit: a smaller witness is already known for this tape
                 const u64 km = s_min[j];
                 const u64 known = ((u64)__builtin_amdgcn_readfirstlane((u32)(km >> 32)) << 32) |
                                   __builtin_amdgcn_readfirstlane((u32)km);
-                if (known < wave_first) {
-                    th = th_next;
-                    ic = ic_next;
-                    continue;
+                skip = known < wave_first;
+            }
+            if (!skip) {
+                exec_tape<NR, FEAT>(m, stream ? p.insns + off : s_insn + off, ic, n);
+                u32 X[8];
+                m.R.read(NR, X);
+                const u32 rb = __builtin_amdgcn_readfirstlane(s_rb[j]);
+                if (p.values_out) {  // parity path: the root value of (tape, row)
+                    if (rb) {
+                        X[0] &= 1u;
+#pragma unroll
+                        for (int k = 1; k < 8; ++k) X[k] = 0;
+                    }
+                    if (valid) {
+                        const u64 r = row - p.row_first;
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            p.values_out[((u64)(cb + j) * 8 + k) * p.row_count + r] = X[k];
+                    }
+                }
+                const u32 res = rb ? (X[0] & 1u) : (is_zero256(X) ? 0u : 1u);
+                const unsigned long long mask = __builtin_amdgcn_ballot_w64(valid && res);
+                if (mask && (tid & 63u) == 0) {
+                    atomicAdd(&s_cnt[j], (unsigned long long)__builtin_popcountll(mask));
+                    atomicMin(&s_min[j], (unsigned long long)(wave_first + __builtin_ctzll(mask)));
                 }
             }
-            exec_tape<NR, FEAT>(R, p, ic, th.insn_off, th.n_insns, lrow);
-            u32 res;
-            if (th.root_bool) {
-                res = R.read0(th.root_reg) & 1u;
-            } else {
-                u32 x[8];
-                R.read(th.root_reg, x);
-                res = is_zero256(x) ? 0u : 1u;
-            }
-            const unsigned long long mask = __builtin_amdgcn_ballot_w64(valid && res);
-            if (mask && (tid & 63u) == 0) {
-                atomicAdd(&s_cnt[j], (unsigned long long)__builtin_popcountll(mask));
-                atomicMin(&s_min[j], (unsigned long long)(wave_first + __builtin_ctzll(mask)));
-            }
-            th = th_next;
+            off = off_next;
+            n = n_next;
             ic = ic_next;
         }
         __syncthreads();
         if (tid < nt) {
-            const u32 ti = cb - p.tape_first + tid;
+            const u32 ti = s_tid[tid] - p.result_base;
             if (s_cnt[tid] && p.hit_count) atomicAdd(&p.hit_count[ti], s_cnt[tid]);
             if (s_min[tid] != ~0ull && p.first_hit) atomicMin(&p.first_hit[ti], s_min[tid]);
         }
-    }
-}
-
-// Root value of one tape per row (parity path).
-template <int NR>
-__global__ void __launch_bounds__(kBlock) values_kernel(const KParams p, u32 tape, u32* out) {
-    RegFile<NR> R;
-    const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = r < p.row_count;
-    const u64 lrow = p.row_first + (valid ? r : 0);
-    preload<NR>(R, p, lrow);
-    const TapeHead th = tape_head(p, tape);
-    exec_tape<NR, F_DIV | F_KECCAK | F_EVM>(R, p, load_insns(p, th.insn_off, th.n_insns, 0),
-                                            th.insn_off, th.n_insns, lrow);
-    u32 x[8];
-    R.read(th.root_reg, x);
-    if (th.root_bool) {
-        x[0] &= 1u;
-#pragma unroll
-        for (int k = 1; k < 8; ++k) x[k] = 0;
-    }
-    if (valid) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) out[(u64)k * p.row_count + r] = x[k];
+        cb += nt;
     }
 }
 
@@ -405,8 +298,9 @@ __global__ void __launch_bounds__(kBlock) generate_kernel(u32* assign, u64 capac
     }
 }
 
-// Integer VALU throughput probe: independent dependency chains per lane (enough ILP that the
-// measured rate is issue-bound, not latency-bound).
+// Integer VALU throughput probe.  kind 0: v_add_co/v_addc 256-bit carry chains (4 independent
+// chains, 32 VALU per iteration); kind 1: v_mad_u64_u32 (8 independent chains); kind 2:
+// v_xor + v_add (64 VALU per iteration).  Reported as u32 lane-ops/s = VALU lane-instructions/s.
 __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters, u32* sink) {
     u32 s[4][8];
 #pragma unroll
@@ -414,19 +308,16 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters,
 #pragma unroll
         for (int k = 0; k < 8; ++k) s[j][k] = threadIdx.x * 2654435761u + 8 * j + k;
     const u32 y = blockIdx.x | 1u;
-    if (kind == 0) {  // 4 independent 256-bit add-with-carry chains: 32 ops / iteration
+    if (kind == 0) {
         for (u32 i = 0; i < iters; ++i) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                u64 c = y;
+                u32 c = 0;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    c = (u64)s[j][k] + s[(j + 1) & 3][k] + (c >> 32);
-                    s[j][k] = (u32)c;
-                }
+                for (int k = 0; k < 8; ++k) s[j][k] = addc32(s[j][k], s[(j + 1) & 3][k], c, &c);
             }
         }
-    } else if (kind == 1) {  // v_mad_u64_u32: 8 independent chains, 8 mads / iteration
+    } else if (kind == 1) {
         u64 acc[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[k] = s[0][k];
@@ -436,7 +327,7 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters,
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) s[0][k] = (u32)acc[k] ^ (u32)(acc[k] >> 32);
-    } else {  // xor/add mix: 32 independent ops / iteration
+    } else {
         for (u32 i = 0; i < iters; ++i) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -452,30 +343,29 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters,
     if (r == 0x12345678u) sink[0] = r;
 }
 
+template <int NR, int FEAT>
+hipError_t launch_variant(const KParams& p, hipStream_t stream) {
+    const u64 blocks = (p.row_count + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                       p);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 namespace mh {
 
-hipError_t launch_sieve(const KParams& p, uint32_t feat, hipStream_t stream) {
-    const u64 blocks = (p.row_count + kBlock - 1) / kBlock;
-    if (blocks == 0 || p.tape_count == 0) return hipSuccess;
-    dim3 grid((unsigned)blocks), block(kBlock);
-    if (feat & (F_KECCAK | F_EVM))
-        hipLaunchKernelGGL((sieve_kernel<MH_NUM_REGS, F_DIV | F_KECCAK | F_EVM>), grid, block, 0,
-                           stream, p);
-    else if (feat & F_DIV)
-        hipLaunchKernelGGL((sieve_kernel<MH_NUM_REGS, F_DIV>), grid, block, 0, stream, p);
-    else
-        hipLaunchKernelGGL((sieve_kernel<MH_NUM_REGS, 0>), grid, block, 0, stream, p);
-    return hipGetLastError();
-}
-
-hipError_t launch_values(const KParams& p, uint32_t tape, uint32_t* out, hipStream_t stream) {
-    const u64 blocks = (p.row_count + kBlock - 1) / kBlock;
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((values_kernel<MH_NUM_REGS>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                       stream, p, tape, out);
-    return hipGetLastError();
+hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream) {
+    if (p.row_count == 0 || p.n_ids == 0) return hipSuccess;
+    constexpr int kCplx = F_DIV | F_CPLX, kAll = F_DIV | F_CPLX | F_KECCAK | F_EVM;
+    switch (variant) {
+        case 0: return launch_variant<MH_NR_SMALL, 0>(p, stream);
+        case 1: return launch_variant<MH_NR_SMALL, kCplx>(p, stream);
+        case 2: return launch_variant<MH_NR_SMALL, kAll>(p, stream);
+        case 3: return launch_variant<MH_NR_MAX, 0>(p, stream);
+        case 4: return launch_variant<MH_NR_MAX, kCplx>(p, stream);
+        default: return launch_variant<MH_NR_MAX, kAll>(p, stream);
+    }
 }
 
 hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars, uint64_t seed,

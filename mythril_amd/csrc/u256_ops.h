@@ -220,6 +220,36 @@ MH_FN void shr256(const u32* x, u32 s, u32* z, u32 fill) {  // fill = 0 or 0xfff
     }
 }
 
+// Shifts by a WAVE-UNIFORM amount s < 256 (tape immediates): the limb offset q is uniform, so
+// the limb move is an indexed register read (s_set_gpr_idx / v_movrels, no select network) and
+// the bit part one v_alignbit per limb.
+MH_FN void shr256_u(const u32* x, u32 s, u32* z, u32 fill) {
+    u32 t[17];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = x[k];
+#pragma unroll
+    for (int k = 8; k < 17; ++k) t[k] = fill;
+    const u32 q = s >> 5, r = s & 31;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) z[k] = alignbit(t[k + q + 1], t[k + q], r);
+}
+
+MH_FN void shl256_u(const u32* x, u32 s, u32* z) {
+    u32 t[17];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) t[k] = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[9 + k] = x[k];
+    const u32 q = s >> 5, r = s & 31;
+    if (r == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) z[k] = t[9 + k - q];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) z[k] = alignbit(t[9 + k - q], t[8 + k - q], 32u - r);
+    }
+}
+
 // shift amount as a 256-bit value, saturated to 256 (any high limb set => >= 256)
 MH_FN u32 shift_amount(const u32* y) {
     u32 hi = 0;

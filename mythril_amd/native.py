@@ -17,7 +17,8 @@ import numpy as np
 from .tape import NODE_DTYPE, TapeSet
 
 LIB_NAME = "libmythril_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("MYTHRIL_HIP_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 MH_OK = 0
 MH_E_INVALID = -1
