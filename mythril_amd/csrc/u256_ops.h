@@ -376,7 +376,33 @@ MH_FN u32 knuth_step(u32* u, const u32* v, double vinv) {
     return qh;
 }
 
+// 1/d to ~2^-52 relative: hardware reciprocal + one Newton step on the device.  Only feeds an
+// estimate that udivrem256 corrects exactly, so host and device may round differently.
+MH_FN double recip_f64(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(d);
+    const double e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
+#else
+    return 1.0 / d;
+#endif
+}
+
+// 256-bit value as a double (relative error < 2^-50: Horner over the limbs with fma)
+MH_FN double to_f64(const u32* x) {
+    double d = (double)x[7];
+#pragma unroll
+    for (int k = 6; k >= 0; --k) d = __builtin_fma(d, 4294967296.0, (double)x[k]);
+    return d;
+}
+
 // q = x / y, r = x % y (256-bit unsigned, SMT-LIB: y == 0 gives q = 2^256 - 1, r = x)
+//
+// Fast path: when every lane's quotient is below 2^47 (the common case: random operands give
+// 0- or 1-digit quotients), q is estimated as x/y in f64 (relative error ~2^-49, so the
+// truncated estimate is the quotient or off by one), then made exact with one 9-limb product,
+// one subtraction and a +-1 correction.  Otherwise (some lane has a long quotient): Knuth
+// algorithm D on 32-bit digits with f64 digit estimates.
 MH_FN void udivrem256(const u32* x, const u32* y, u32* q, u32* r) {
     // s = leading zeros of y (normalisation shift)
     u32 s = 0;
@@ -395,6 +421,55 @@ MH_FN void udivrem256(const u32* x, const u32* y, u32* q, u32* r) {
         for (int k = 0; k < 8; ++k) { q[k] = 0; r[k] = x[k]; }
         return;
     }
+    {
+        const double qd = to_f64(x) * recip_f64(to_f64(y));
+        const bool est_ok = qd < 140737488355328.0;  // 2^47 (false for y == 0: inf / NaN)
+        if (!any_lane(nz && !est_ok)) {
+            const u64 qi = est_ok ? (u64)qd : 0ull;
+            const u32 q0 = (u32)qi, q1 = (u32)(qi >> 32);
+            // p = qi * y, 9 limbs (qi <= quotient + 1, so p < x + y < 2^257)
+            u32 p[9];
+            u64 c = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const u64 t = (u64)q0 * y[k] + c;
+                p[k] = (u32)t;
+                c = t >> 32;
+            }
+            p[8] = (u32)c;
+            c = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {  // + (q1 * y) << 32
+                const u64 t = (u64)q1 * y[k] + p[k + 1] + c;
+                p[k + 1] = (u32)t;
+                c = t >> 32;
+            }
+            // rr = x - p over 9 limbs; a borrow means the estimate was one too large
+            u32 rr[9], br = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rr[k] = subc32(x[k], p[k], br, &br);
+            rr[8] = subc32(0u, p[8], br, &br);
+            const bool neg = br != 0;
+            // neg: rr += y (and q - 1); then rr >= y: rr -= y (and q + 1)
+            u32 ca = 0, t9[9];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t9[k] = addc32(rr[k], neg ? y[k] : 0u, ca, &ca);
+            t9[8] = rr[8] + (neg ? ca : 0u);
+            u32 d9[9], bd = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d9[k] = subc32(t9[k], y[k], bd, &bd);
+            d9[8] = subc32(t9[8], 0u, bd, &bd);
+            const bool ge = bd == 0;  // t9 >= y
+            const u64 qf = qi - (neg ? 1ull : 0ull) + (ge ? 1ull : 0ull);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const u32 rk = ge ? d9[k] : t9[k];
+                q[k] = nz ? (k == 0 ? (u32)qf : k == 1 ? (u32)(qf >> 32) : 0u) : 0xFFFFFFFFu;
+                r[k] = nz ? rk : x[k];
+            }
+            return;
+        }
+    }
     u32 v[8];
     shl256(y, s, v);
     // u = x << s as 512 bits (u[16]), built from two 256-bit shifts
@@ -409,7 +484,7 @@ MH_FN void udivrem256(const u32* x, const u32* y, u32* q, u32* r) {
         for (int k = 0; k < 8; ++k) u[8 + k] = s ? hi[k] : 0u;
     }
     u[16] = 0;
-    const double vinv = 1.0 / (double)(v[7] ? v[7] : 1u);
+    const double vinv = recip_f64((double)(v[7] ? v[7] : 1u));
     const u32 jmax = s >> 5;  // quotient digits above jmax are zero
     u32 qd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define MH_KSTEP(J) \
