@@ -58,9 +58,8 @@ uint64_t op_cost(const mh_node& n, const std::vector<mh_node>& t) {
 
 // ops whose y may be an inline constant: asm pairs (given as the *_R form) and binary complex ops
 bool y_const_ok(uint8_t op) {
-    if (op >= D_ADD_R && op <= D_SGE_C) return ((op - D_ADD_R) & 1) == 0;
+    if (mh_pair_form(op)) return mh_pair_form(op) == 1;
     switch (op) {
-        case D_MUL_R: case D_UDIV: case D_UREM: case D_SDIV: case D_SREM: case D_SMOD:
         case D_UADD_NOOVFL: case D_UMUL_NOOVFL: case D_EXP: case D_SIGNEXT: case D_BYTE:
             return true;
         default:
@@ -206,6 +205,27 @@ struct Lowering {
         if (sp) u = emit(D_LSHRI, u, -1, -1, 256, sp);
         u = emit(D_SUB_R, u, -1, -1, 256, 0, bit_const(w - 1 - sp));
         return masked(u, w);
+    }
+
+    // op(sext256(a), sext256(b)) for a binary op on signed operands of width w < 256 (a
+    // constant operand is sign-extended on the host and becomes the inline constant)
+    int emit_sext_bin(uint8_t op, uint32_t na, uint32_t nb, uint32_t w) {
+        auto sext_const = [&](uint32_t k) {
+            const mh_node& c = t[(size_t)(*vals_)[k].remat];
+            uint32_t m[8];
+            for (int i = 0; i < 8; ++i) m[i] = consts[8ull * c.imm0 + i] & lane_mask(i, w);
+            if ((m[(w - 1) >> 5] >> ((w - 1) & 31)) & 1u)
+                for (int i = 0; i < 8; ++i) m[i] |= ~lane_mask(i, w);
+            return (int)const_index(m, 256);
+        };
+        auto sx = [&](uint32_t k) {
+            const int r = vreg_of(k);
+            return r < 0 ? -1 : sext256(r, w);
+        };
+        if (is_const_node(nb)) return emit(op, sx(na), -1, -1, 256, 0, sext_const(nb));
+        const int a = sx(na), b = sx(nb);
+        if (a < 0 || b < 0) return -1;
+        return emit(op, a, b, -1, 256);
     }
 
     // signed compare at width w < 256 as the unsigned compare of the biased values
@@ -406,17 +426,23 @@ bool Lowering::lower(std::vector<Val>& vals) {
                     case MH_OP_BVAND: op = D_AND_R; break;
                     case MH_OP_BVOR: op = D_OR_R; break;
                     case MH_OP_BVXOR: op = D_XOR_R; break;
-                    case MH_OP_BVUDIV: op = D_UDIV; features |= F_DIV; break;
-                    case MH_OP_BVUREM: op = D_UREM; features |= F_DIV; break;
-                    case MH_OP_BVSDIV: op = D_SDIV; features |= F_DIV; break;
-                    case MH_OP_BVSREM: op = D_SREM; features |= F_DIV; break;
-                    case MH_OP_BVSMOD: op = D_SMOD; features |= F_DIV; break;
+                    case MH_OP_BVUDIV: op = D_UDIV_R; mask = true; features |= F_DIV; break;
+                    case MH_OP_BVUREM: op = D_UREM_R; features |= F_DIV; break;
+                    case MH_OP_BVSDIV: op = D_SDIV_R; features |= F_DIV; break;
+                    case MH_OP_BVSREM: op = D_SREM_R; features |= F_DIV; break;
+                    case MH_OP_BVSMOD: op = D_SMOD_R; features |= F_DIV; break;
                     case MH_OP_EVM_EXP: op = D_EXP; features |= F_EVM; break;
                     case MH_OP_EVM_SIGNEXTEND: op = D_SIGNEXT; features |= F_EVM; break;
                     case MH_OP_EVM_BYTE: op = D_BYTE; features |= F_EVM; break;
                 }
                 if ((op == D_SIGNEXT || op == D_BYTE) && w != 256)
                     return fail("EVM word ops are 256-bit");
+                if (w < 256 && (op == D_SDIV_R || op == D_SREM_R || op == D_SMOD_R)) {
+                    // signed division at width w = 256-bit signed division of the sign-extended
+                    // operands, masked (all SMT-LIB sign cases agree mod 2^w)
+                    out.vreg = masked(emit_sext_bin(op, nd.a, nd.b, w), w);
+                    break;
+                }
                 int r = emit_bin(op, nd.a, nd.b, w);
                 out.vreg = mask ? masked(r, w) : r;
                 break;
@@ -752,7 +778,7 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
         peak = std::max(peak, phys[v.d] + 1);
         wb[i] = 1;
     }
-    const uint32_t nrx = peak <= MH_NR_SMALL ? MH_NR_SMALL : MH_NR_MAX;
+    const uint32_t nrx = mh_nrx_of((uint32_t)peak);
     out.n_regs = (uint32_t)std::max(peak, 1);
     out.root_bool = t.back().width == 0;
 

@@ -34,6 +34,7 @@
 
 #define MH_MAX_PRELOAD 4   // assignment columns kept resident in R0..R3 for the whole launch
 #define MH_NR_SMALL 7      // register-file sizes of the kernel variants (tapes bucketed by need);
+#define MH_NR_MID 9
 #define MH_NR_MAX 15       // the accumulator is register NR, so planes are NR+1 VGPRs (even:
                            // VGPR tuples are even-aligned on gfx950)
 #define MH_WINDOW 64       // instruction slots per window
@@ -56,11 +57,15 @@ enum mh_dop : uint8_t {
     D_SHLQ,   // X = R[a'] << aux mod 2^256 (aux % 32 == 0)
     D_MUL_R, D_MUL_C,  // X = R[a'] * y mod 2^256 (host masks)
     D_SHL_V, D_LSHR_V, D_ASHR_V,  // 256-bit shifts by y (per lane; >= 256 saturates to 0 / fill)
+    // 256-bit division family, SMT-LIB semantics (x / 0 = 2^256 - 1, x % 0 = x, signed forms by
+    // the bvsdiv/bvsrem/bvsmod sign rules); narrower widths are sign-extended / masked by the host
+    D_UDIV_R, D_UDIV_C, D_UREM_R, D_UREM_C, D_SDIV_R, D_SDIV_C, D_SREM_R, D_SREM_C,
+    D_SMOD_R, D_SMOD_C,
     D_NUM_ASM,
     // ---- C++ (exec.h); y = R[b] or the inline constant (F_YC)
     D_FIRST_COMPLEX = 64,
-    D_UDIV = D_FIRST_COMPLEX, D_UREM, D_SDIV, D_SREM, D_SMOD,  // width-w semantics
-    D_UADD_NOOVFL, D_UMUL_NOOVFL,    // z3 BVAddNoOverflow / BVMulNoOverflow (unsigned) -> Bool
+    D_UADD_NOOVFL = D_FIRST_COMPLEX,  // z3 BVAddNoOverflow (unsigned) -> Bool
+    D_UMUL_NOOVFL,                    // z3 BVMulNoOverflow (unsigned) -> Bool
     D_EXP, D_SIGNEXT, D_BYTE,        // EVM word ops (256-bit)
     D_KECCAK,
     D_LOADVAR,                     // X = assignment column aux (columns beyond the pinned ones)
@@ -70,13 +75,27 @@ enum mh_dop : uint8_t {
 };
 
 static_assert(D_NUM_ASM <= D_FIRST_COMPLEX, "asm opcode space");
+
+// *_R / *_C pairs (y from a register / inline constant): 1 = R form, 2 = C form, 0 = neither
+static inline int mh_pair_form(unsigned op) {
+    if (op >= D_ADD_R && op <= D_SGE_C) return 1 + ((op - D_ADD_R) & 1);
+    if (op == D_MUL_R || op == D_MUL_C) return 1 + (op - D_MUL_R);
+    if (op >= D_UDIV_R && op <= D_SMOD_C) return 1 + ((op - D_UDIV_R) & 1);
+    return 0;
+}
+
+// accumulator index (last register of the planes) of the kernel variant a tape needs
+static inline unsigned mh_nrx_of(unsigned n_regs) {
+    return n_regs <= MH_NR_SMALL ? MH_NR_SMALL : n_regs <= MH_NR_MID ? MH_NR_MID : MH_NR_MAX;
+}
 static_assert(D_NUM_OPS <= 128, "opcode space");
 
 enum { F_YC = 1u << 31 };
 #define MH_AUX_MAX ((1u << 14) - 1)
 
-// Feature bits (mh_tape_info.features) — select the kernel variant.  A tape with none of them
-// runs entirely in the asm core (a kernel without the C++ path: fewer VGPRs, more waves).
+// Feature bits (mh_tape_info.features) — select the kernel variant.  A tape without F_CPLX,
+// F_KECCAK or F_EVM runs entirely in the asm core (a kernel without the C++ path: fewer VGPRs,
+// more waves).  F_DIV is informational (division runs in the asm core).
 enum { F_DIV = 1, F_KECCAK = 2, F_EVM = 4, F_CPLX = 8 /* other C++ ops */ };
 
 // Per-tape header in the device tape table.

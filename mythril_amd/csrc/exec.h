@@ -77,9 +77,6 @@ MH_FN void complex_op(const E& env, u32 w1, const u32* x, const u32* y, const u3
     const u32 op = w1 & 0xFFu, w = (w1 >> 8) & 0x1FFu, aux = (w1 >> 17) & MH_AUX_MAX;
     copy8(z, x);
     switch (op) {
-        case D_UDIV: case D_UREM: case D_SDIV: case D_SREM: case D_SMOD:
-            if constexpr ((FEAT & F_DIV) != 0) divmod_family(op - D_UDIV, x, y, z, w);
-            break;
         case D_UADD_NOOVFL: {
             u32 t[8];
             const u32 cy = add256(x, y, t);
@@ -129,15 +126,12 @@ MH_FN void complex_op(const E& env, u32 w1, const u32* x, const u32* y, const u3
 }
 
 // True for the asm-core ops whose y is the inline constant (the *_C forms and D_LOADC).
-MH_FN bool asm_op_yconst(u32 op) {
-    return (op >= D_ADD_R && op <= D_SGE_C && ((op - D_ADD_R) & 1u)) || op == D_LOADC ||
-           op == D_MUL_C;
-}
+MH_FN bool asm_op_yconst(u32 op) { return mh_pair_form(op) == 2 || op == D_LOADC; }
 
 // asm-core ops that read y = R[b] in full
 MH_FN bool asm_op_yreg(u32 op) {
-    return (op >= D_ADD_R && op <= D_SGE_C && !((op - D_ADD_R) & 1u)) || op == D_ITEC ||
-           op == D_MUL_R || op == D_SHL_V || op == D_LSHR_V || op == D_ASHR_V;
+    return mh_pair_form(op) == 1 || op == D_ITEC || op == D_SHL_V || op == D_LSHR_V ||
+           op == D_ASHR_V;
 }
 
 // One instruction at slot ip (words w0, w1): X = f(R[a'], y, ...), R[d'] = X.  Returns the slots
@@ -237,6 +231,10 @@ MH_FN u32 step(M& m, u32 w0, u32 w1, u32 ip) {
         case D_SHL_V: if constexpr (SIMPLE) bvshl_v(x, shift_amount(y), z, 256); break;
         case D_LSHR_V: if constexpr (SIMPLE) bvlshr_v(x, shift_amount(y), z, 256); break;
         case D_ASHR_V: if constexpr (SIMPLE) bvashr_v(x, shift_amount(y), z, 256); break;
+        case D_UDIV_R: case D_UDIV_C: case D_UREM_R: case D_UREM_C: case D_SDIV_R: case D_SDIV_C:
+        case D_SREM_R: case D_SREM_C: case D_SMOD_R: case D_SMOD_C:
+            if constexpr (SIMPLE) divmod_family((op - D_UDIV_R) >> 1, x, y, z, 256);
+            break;
         default:
             if (op >= D_FIRST_COMPLEX) {
                 u32 c3[8];

@@ -35,7 +35,11 @@ OPS = ["EXIT", "NOP",
        "SLT_R", "SLT_C", "SGT_R", "SGT_C", "SLE_R", "SLE_C", "SGE_R", "SGE_C",
        "BAND", "BOR", "BXOR", "BEQ", "BNOT", "TRUE", "FALSE",
        "ITE", "ITEC", "BITE", "LOADC", "LSHRI", "SHLI", "SHLQ",
-       "MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V"]
+       "MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V",
+       "UDIV_R", "UDIV_C", "UREM_R", "UREM_C", "SDIV_R", "SDIV_C", "SREM_R", "SREM_C",
+       "SMOD_R", "SMOD_C"]
+DIV_KIND = {"UDIV_R": 0, "UDIV_C": 0, "UREM_R": 1, "UREM_C": 1, "SDIV_R": 2, "SDIV_C": 2,
+            "SREM_R": 3, "SREM_C": 3, "SMOD_R": 4, "SMOD_C": 4}
 OPNUM = {n: i for i, n in enumerate(OPS)}
 # handlers longer than a slot live after the table (one extra jump)
 OUT_OF_LINE = {"MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V"}
@@ -49,7 +53,10 @@ S_B, S_D, S_C = "s48", "s49", "s50"  # register operands (low byte = index)
 S_L = "s51"                      # readlane lane
 S_Q, S_R = "s52", "s53"          # shift: limb part, bit part
 S_K = ["s%d" % (54 + k) for k in range(8)]  # inline constant limbs
-SGPR_CLOBBERS = ["s%d" % i for i in range(40, 64)]
+S_KIND, S_ADV = "s70", "s71"   # division: kind (0 udiv .. 4 smod), slot advance
+S_F64N = (68, 69)                # f64 constant pair (2^32, thresholds)
+S_F64 = ("s68", "s69")
+SGPR_CLOBBERS = ["s%d" % i for i in range(40, 72)]
 
 
 class Core:
@@ -65,7 +72,7 @@ class Core:
         return self.P(k, self.nr)
 
     def S(self, j):
-        assert 0 <= j <= 23
+        assert 0 <= j <= 31
         return "v%d" % (self.sb + j)
 
     def Y(self, k):
@@ -355,7 +362,168 @@ class Core:
                 fillv = "0"
             body += ["v_cndmask_b32_e64 {0}, {0}, {1}, {2}".format(X(k), fillv, big) for k in range(8)]
             return body + self.wb() + self.dispatch(1)
+        if name in DIV_KIND:
+            # y into Y, the kind and the slot advance into SGPRs, then the shared body
+            reg = name.endswith("_R")
+            body = self.y_reg() if reg else self.consts(to_y=range(8))
+            body += ["s_mov_b32 {}, {}".format(S_KIND, DIV_KIND[name]),
+                     "s_mov_b32 {}, {}".format(S_ADV, 1 if reg else 5),
+                     "s_branch L_div_%="]
+            return body
         raise KeyError(name)
+
+    def to_f64(self, dst, limbs, tmp):
+        """dst (f64 pair) = the 256-bit value limbs[0..7] (Horner with fma, rel. error < 2^-50)."""
+        out = ["s_mov_b32 {}, 0".format(S_F64[0]), "s_mov_b32 {}, 0x41f00000".format(S_F64[1]),
+               "v_cvt_f64_u32 {}, {}".format(dst, limbs[7])]
+        for k in range(6, -1, -1):
+            out += ["v_cvt_f64_u32 {}, {}".format(tmp, limbs[k]),
+                    "v_fma_f64 {0}, {0}, s[{1}:{2}], {3}".format(dst, S_F64N[0], S_F64N[1], tmp)]
+        return out
+
+    def div_body(self):
+        """256-bit division by f64 digit estimates over 32-bit digits, no normalisation shifts.
+        Step j (7..0, entered at the highest j any lane needs): c = trunc(R / (y 2^(32j))) from
+        f64 (relative error ~2^-48, so c is the digit or off by one), R -= c*y*2^(32j) (8 mads),
+        then one add-back if R went negative, one subtract if R >= y 2^(32j).  Lanes with y = 0
+        keep R = |x| and get q = 2^256 - 1 (SMT-LIB); signed kinds divide |x| by |y| and fix the
+        signs by the bvsdiv / bvsrem / bvsmod rules.  Y = S0..7 = y, R = S8..15."""
+        X, S = self.X, self.S
+        Y = [S(k) for k in range(8)]
+        R = [S(8 + k) for k in range(8)]
+        FY, FR, FC, FT = ("v[{}:{}]".format(self.sb + i, self.sb + i + 1) for i in (16, 18, 20, 22))
+        CARRY = "v[{}:{}]".format(self.sb + 24, self.sb + 25)   # {carry, 0}
+        MAD = "v[{}:{}]".format(self.sb + 26, self.sb + 27)     # {lo, hi}
+        C, T1, SX, SY = S(28), S(29), S(30), S(31)
+        YNZ, DUMMY, MSK, TM = "s[62:63]", "s[64:65]", "s[66:67]", "s[44:45]"
+        out = ["L_div_%=:"]
+        out += self.idx_on(S_W0, ["SRC0"]) + ["v_mov_b32 {}, {}".format(R[k], self.P(k)) for k in range(8)]
+        out += self.idx_off()
+        # signed kinds: |x|, |y| as (v ^ m) - m with m = sign mask
+        out += ["s_cmp_lt_u32 {}, 2".format(S_KIND), "s_cbranch_scc1 L_div_uns_%="]
+        for v, m in ((R, SX), (Y, SY)):
+            out.append("v_ashrrev_i32 {}, 31, {}".format(m, v[7]))
+            out += ["v_xor_b32 {0}, {0}, {1}".format(v[k], m) for k in range(8)]
+            out.append("v_sub_co_u32 {0}, vcc, {0}, {1}".format(v[0], m))
+            out += ["v_subb_co_u32 {0}, vcc, {0}, {1}, vcc".format(v[k], m) for k in range(1, 8)]
+        out.append("L_div_uns_%=:")
+        out += ["v_mov_b32 {}, 0".format(X(k)) for k in range(8)]
+        # y != 0 lanes; skip everything when no such lane has R >= y
+        out += ["v_or3_b32 {}, {}, {}, {}".format(T1, Y[0], Y[1], Y[2]),
+                "v_or3_b32 {0}, {0}, {1}, {2}".format(T1, Y[3], Y[4]),
+                "v_or3_b32 {0}, {0}, {1}, {2}".format(T1, Y[5], Y[6]),
+                "v_or_b32 {0}, {0}, {1}".format(T1, Y[7]),
+                "v_cmp_ne_u32_e64 {}, 0, {}".format(YNZ, T1),
+                "v_sub_co_u32 {}, vcc, {}, {}".format(T1, R[0], Y[0])]
+        out += ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(T1, R[k], Y[k]) for k in range(1, 8)]
+        out += ["s_andn2_b64 {}, {}, vcc".format(MSK, YNZ),
+                "s_cmp_eq_u64 {}, 0".format(MSK), "s_cbranch_scc1 L_div_done_%="]
+        # 1/yd, qd = R/y for the start digit
+        out += self.to_f64(FY, Y, FT)
+        out += ["v_rcp_f64 {}, {}".format(FC, FY),
+                "s_nop 1",  # trans result -> non-trans VALU use needs a wait state (CDNA3/4)
+                "v_fma_f64 {}, -{}, {}, 1.0".format(FT, FY, FC),
+                "v_fma_f64 {}, {}, {}, {}".format(FY, FC, FT, FC)]
+        out += self.to_f64(FR, R, FT)
+        out.append("v_mul_f64 {}, {}, {}".format(FC, FR, FY))
+        for j in range(7, 0, -1):  # start at the highest j with qd >= 2^(32j - 1) in some lane
+            hi = (1023 + 32 * j - 1) << 20
+            out += ["s_mov_b32 {}, 0".format(S_F64[0]), "s_mov_b32 {}, 0x{:x}".format(S_F64[1], hi),
+                    "v_cmp_le_f64_e32 vcc, s[{}:{}], {}".format(S_F64N[0], S_F64N[1], FC),
+                    "s_and_b64 {}, vcc, {}".format(TM, MSK),
+                    "s_cmp_lg_u64 {}, 0".format(TM),
+                    "s_cbranch_scc1 L_step{}_%=".format(j)]
+        out.append("s_branch L_step0_%=")
+        for j in range(7, -1, -1):
+            out.append("L_step{}_%=:".format(j))
+            out += self.to_f64(FR, R, FT)
+            out.append("v_mul_f64 {}, {}, {}".format(FC, FR, FY))
+            if j:  # * 2^-32j as an f64 constant (v_ldexp_f64 with an SGPR exponent left FC unscaled on gfx950)
+                out += ["s_mov_b32 {}, 0".format(S_F64[0]),
+                        "s_mov_b32 {}, 0x{:x}".format(S_F64[1], (1023 - 32 * j) << 20),
+                        "v_mul_f64 {0}, {0}, s[{1}:{2}]".format(FC, S_F64N[0], S_F64N[1])]
+            # clamp to 2^32 - 1 before the conversion (the estimate may exceed the digit range
+            # by the last ulp; NaN from y = 0 lanes becomes the clamp and is zeroed below)
+            out += ["s_mov_b32 {}, 0xffe00000".format(S_F64[0]),
+                    "s_mov_b32 {}, 0x41efffff".format(S_F64[1]),
+                    "v_min_f64 {0}, {0}, s[{1}:{2}]".format(FC, S_F64N[0], S_F64N[1]),
+                    "v_cvt_u32_f64 {}, {}".format(C, FC),
+                    "v_cndmask_b32_e64 {0}, 0, {0}, {1}".format(C, YNZ)]
+            # R[j..] -= c * y  (the product's limbs above limb 7 only feed the borrow)
+            out += ["v_mov_b32 {}, 0".format(S(24)), "v_mov_b32 {}, 0".format(S(25))]
+            for k in range(8):
+                out.append("v_mad_u64_u32 {}, {}, {}, {}, {}".format(MAD, DUMMY, C, Y[k], CARRY))
+                out.append("v_mov_b32 {}, {}".format(S(24), S(27)))
+                limb = j + k
+                if limb <= 7:
+                    ins = "v_sub_co_u32 {0}, vcc, {0}, {1}" if k == 0 else "v_subb_co_u32 {0}, vcc, {0}, {1}, vcc"
+                    out.append(ins.format(R[limb], S(26)))
+                else:
+                    out.append("v_subb_co_u32 {}, vcc, 0, {}, vcc".format(T1, S(26)))
+            out.append("v_subb_co_u32 {}, vcc, 0, {}, vcc".format(T1, S(24)))  # limb j + 8 > 7
+            # negative: add y << 32j back, c - 1
+            out += ["s_mov_b64 {}, vcc".format(MSK), "s_cmp_eq_u64 {}, 0".format(MSK),
+                    "s_cbranch_scc1 L_noneg{}_%=".format(j)]
+            for k in range(8 - j):
+                out.append("v_cndmask_b32_e64 {}, 0, {}, {}".format(T1, Y[k], MSK))
+                ins = "v_add_co_u32 {0}, vcc, {0}, {1}" if k == 0 else "v_addc_co_u32 {0}, vcc, {0}, {1}, vcc"
+                out.append(ins.format(R[j + k], T1))
+            out += ["v_cndmask_b32_e64 {}, 0, 1, {}".format(T1, MSK),
+                    "v_sub_u32 {0}, {0}, {1}".format(C, T1),
+                    "L_noneg{}_%=:".format(j)]
+            # R >= y << 32j (y = 0 lanes excluded): subtract once more, c + 1
+            out.append("v_sub_co_u32 {}, vcc, {}, {}".format(T1, R[j], Y[0]))
+            out += ["v_subb_co_u32 {}, vcc, {}, {}, vcc".format(T1, R[j + k], Y[k]) for k in range(1, 8 - j)]
+            out += ["v_subb_co_u32 {}, vcc, 0, {}, vcc".format(T1, Y[k]) for k in range(8 - j, 8)]
+            out += ["s_andn2_b64 {}, {}, vcc".format(MSK, YNZ), "s_cmp_eq_u64 {}, 0".format(MSK),
+                    "s_cbranch_scc1 L_noge{}_%=".format(j)]
+            for k in range(8 - j):
+                out.append("v_cndmask_b32_e64 {}, 0, {}, {}".format(T1, Y[k], MSK))
+                ins = "v_sub_co_u32 {0}, vcc, {0}, {1}" if k == 0 else "v_subb_co_u32 {0}, vcc, {0}, {1}, vcc"
+                out.append(ins.format(R[j + k], T1))
+            out += ["v_cndmask_b32_e64 {}, 0, 1, {}".format(T1, MSK),
+                    "v_add_u32 {0}, {0}, {1}".format(C, T1),
+                    "L_noge{}_%=:".format(j),
+                    "v_mov_b32 {}, {}".format(X(j), C)]
+        out.append("L_div_done_%=:")
+        # y = 0: q = 2^256 - 1 (R already holds |x|)
+        out += ["v_cndmask_b32_e64 {0}, -1, {0}, {1}".format(X(k), YNZ) for k in range(8)]
+
+        def cneg(dst, src, m):  # dst = (src ^ m) - m
+            o = ["v_xor_b32 {}, {}, {}".format(dst[k], src[k], m) for k in range(8)]
+            o.append("v_sub_co_u32 {0}, vcc, {0}, {1}".format(dst[0], m))
+            o += ["v_subb_co_u32 {0}, vcc, {0}, {1}, vcc".format(dst[k], m) for k in range(1, 8)]
+            return o
+        XS = [X(k) for k in range(8)]
+        out += ["s_cmp_eq_u32 {}, 0".format(S_KIND), "s_cbranch_scc1 L_div_wb_%=",
+                "s_cmp_eq_u32 {}, 2".format(S_KIND), "s_cbranch_scc1 L_div_sdiv_%=",
+                "s_cmp_eq_u32 {}, 4".format(S_KIND), "s_cbranch_scc1 L_div_smod_%=",
+                "s_cmp_eq_u32 {}, 3".format(S_KIND), "s_cbranch_scc1 L_div_srem_%="]
+        # UREM
+        out += ["v_mov_b32 {}, {}".format(X(k), R[k]) for k in range(8)] + ["s_branch L_div_wb_%="]
+        out.append("L_div_sdiv_%=:")  # q negated when the signs differ
+        out += ["v_xor_b32 {}, {}, {}".format(T1, SX, SY)] + cneg(XS, XS, T1) + ["s_branch L_div_wb_%="]
+        out.append("L_div_srem_%=:")  # r takes the sign of x
+        out += cneg(XS, R, SX) + ["s_branch L_div_wb_%="]
+        out.append("L_div_smod_%=:")  # u = |x| % |y|: (x<0 ? -u : u) + (signs differ && u ? +-|y| : 0)
+        out += cneg(XS, R, SX)
+        out += ["v_or3_b32 {}, {}, {}, {}".format(T1, R[0], R[1], R[2]),
+                "v_or3_b32 {0}, {0}, {1}, {2}".format(T1, R[3], R[4]),
+                "v_or3_b32 {0}, {0}, {1}, {2}".format(T1, R[5], R[6]),
+                "v_or_b32 {0}, {0}, {1}".format(T1, R[7]),
+                "v_cmp_ne_u32_e64 {}, 0, {}".format(MSK, T1),
+                "v_xor_b32 {}, {}, {}".format(T1, SX, SY),
+                "v_cmp_ne_u32_e32 vcc, 0, {}".format(T1),
+                "s_and_b64 {0}, {0}, vcc".format(MSK)]
+        out += cneg(Y, Y, SY)  # t = +-|y| (the original y)
+        for k in range(8):
+            out.append("v_cndmask_b32_e64 {}, 0, {}, {}".format(T1, Y[k], MSK))
+            ins = "v_add_co_u32 {0}, vcc, {0}, {1}" if k == 0 else "v_addc_co_u32 {0}, vcc, {0}, {1}, vcc"
+            out.append(ins.format(X(k), T1))
+        out.append("L_div_wb_%=:")
+        out += self.wb()
+        out += ["s_add_u32 %[ip], %[ip], {}".format(S_ADV)] + self.dispatch(0)
+        return out
 
     def fetch_text(self):
         """Operands of a complex op into S0..7 (x = R[a']), S8..15 (y = R[b] or the inline
@@ -406,11 +574,12 @@ class Core:
                 bodies += ["L_body_{}_%=:".format(name)] + h
             else:
                 lines += h
-        lines += [".org L_tab_%= + {}".format(NSLOTS * SLOT)] + bodies + ["L_out_%=:"]
+        lines += [".org L_tab_%= + {}".format(NSLOTS * SLOT)] + bodies + self.div_body()
+        lines += ["L_out_%=:"]
         return lines
 
 
-N_SCRATCH = 24  # S0..S23, declared clobbered by the core (fetch outputs use all 24)
+N_SCRATCH = 32  # S0..S31, declared clobbered by the core (division uses all 32)
 
 
 def check_registers(core, lines, n_scratch):
@@ -442,7 +611,7 @@ def emit(out):
         w("static_assert(D_{} == {}, \"asm core opcode numbering\");\n".format(name, num))
     w("static_assert(D_NUM_ASM == {}, \"asm core covers every asm op\");\n\n".format(len(OPS)))
     w("template <int NR> struct AsmCore;\n\n")
-    for nr in (7, 15):
+    for nr in (7, 9, 15):
         c = Core(nr)
         nr1 = nr + 1
         w("template <> struct AsmCore<{}> {{\n".format(nr))

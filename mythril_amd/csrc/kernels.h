@@ -26,14 +26,16 @@ struct KParams {
     uint32_t* values_out;           // parity path: [n_ids][8][row_count] root values, or null
 };
 
-// Kernel variants: register-file size class x feature set.
-enum { V_NR_SMALL = 0, V_NR_MAX = 1 };
-inline uint32_t variant_of(uint32_t n_regs, uint32_t features) {
-    const uint32_t nr = n_regs <= MH_NR_SMALL ? V_NR_SMALL : V_NR_MAX;
-    const uint32_t fc = (features & (F_KECCAK | F_EVM)) ? 2u : (features & (F_DIV | F_CPLX)) ? 1u : 0u;
-    return nr * 3 + fc;  // 0..5
+// Kernel variants: register-file size class (NR 7 / 9 / 15) x feature set (asm only / + C++
+// complex ops / + keccak and EVM helpers).
+inline uint32_t nr_class(uint32_t n_regs) {
+    return n_regs <= MH_NR_SMALL ? 0u : n_regs <= MH_NR_MID ? 1u : 2u;
 }
-constexpr uint32_t kNumVariants = 6;
+inline uint32_t variant_of(uint32_t n_regs, uint32_t features) {
+    const uint32_t fc = (features & (F_KECCAK | F_EVM)) ? 2u : (features & F_CPLX) ? 1u : 0u;
+    return nr_class(n_regs) * 3 + fc;  // 0..8
+}
+constexpr uint32_t kNumVariants = 9;
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream);
 hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars, uint64_t seed,

@@ -62,7 +62,7 @@ extern "C" int32_t emu_eval(const mh_node* nodes, const uint64_t* offs, uint32_t
     if (n_regs_out) *n_regs_out = sel.n_regs;
     const uint32_t n_pre = n_vars <= MH_MAX_PRELOAD ? n_vars : 0;
     const u32* ip = words.data() + 2ull * sel_off;
-    const u32 nrx = sel.n_regs <= MH_NR_SMALL ? MH_NR_SMALL : MH_NR_MAX;
+    const u32 nrx = mh_nrx_of(sel.n_regs);
     for (uint64_t row = 0; row < rows; ++row) {
         HostMachine m;
         memset(m.R, 0xCD, sizeof(m.R));  // poison: reads of never-written registers show up
