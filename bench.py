@@ -135,11 +135,12 @@ def main() -> None:
     except Exception as e:  # pragma: no cover
         log("microbench failed: %s" % e)
         peak_measured = None
-    traffic = None
+    traffic = valu_busy = None
     if os.path.exists(PMC_SUMMARY):
         pmc = json.load(open(PMC_SUMMARY))
         if pmc.get("tapes") == n_tapes and pmc.get("rows_per_gpu") == rows:
             traffic = pmc.get("hbm_bytes_per_launch")
+            valu_busy = pmc.get("valu_busy")
     line = {
         "metric": "constraint-evals/sec",
         "value": value,
@@ -173,6 +174,8 @@ def main() -> None:
             "unit": "T u32-ops/s",
             "frac": achieved / NOMINAL_PEAK_TOPS,
             "traffic": traffic,
+            "traffic_unit": "bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, profiles/)",
+            "valu_busy_pmc": valu_busy,
             "peak_measured_add_chain": peak_measured,
             "alg_ops_per_eval": alg_ops_per_row / n_tapes,
         },

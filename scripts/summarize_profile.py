@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Summarise one scripts/profile.sh run (gpurun_out/prof_<tag>) into profiles/<tag>/.
+
+Writes
+  profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the bench
+  profiles/<tag>/pmc_counters.json  per sieve-kernel PMC sums, one entry per pass
+  profiles/<tag>/summary.json       derived figures (below)
+  profiles/pmc_summary.json         the same derived figures, read by bench.py for `traffic`
+
+Derived figures, per sieve launch group (one mh_run = one launch of each kernel variant the tape
+set needs; the variants run back to back on one stream):
+  hbm_bytes_per_launch  FETCH_SIZE + WRITE_SIZE (rocprofv3 reports KiB) summed over the variants.
+                        Not doubled: the MI355X guide's x2 correction is calibrated for 16 B/lane
+                        streaming vector reads; this kernel's reads are 4 B/lane column loads plus
+                        scalar-cache fills of the tape program, an uncalibrated width.
+  valu_busy             SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the share
+                        of SIMD issue cycles spent on vector instructions (a wave64 VALU op holds
+                        its SIMD's vector issue for 4 cycles, MI355X_MICROARCH.md constants table).
+  salu_per_valu         scalar instructions per vector instruction (interpreter dispatch overhead).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load_pass(d: str, name: str):
+    path = os.path.join(d, name, name + "_counter_collection.csv")
+    if not os.path.exists(path):
+        return None
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    dispatches = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        if "sieve_kernel" not in k:
+            continue
+        short = k.split("sieve_kernel")[1].split("(")[0]
+        agg[short][r["Counter_Name"]] += float(r["Counter_Value"])
+        dispatches[short].add(r["Dispatch_Id"])
+    return {k: dict(v, dispatches=len(dispatches[k])) for k, v in agg.items()}
+
+
+def main(tag: str) -> None:
+    src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(dst, "kernel_stats.csv"))
+    bench_line = open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1]
+    with open(os.path.join(dst, "bench_trace.json"), "w") as f:
+        f.write(bench_line + "\n")
+    bench = json.loads(bench_line)
+    passes = {p: load_pass(src, p) for p in ("sq1", "sq2", "tcc1", "tcc2")}
+    json.dump(passes, open(os.path.join(dst, "pmc_counters.json"), "w"), indent=1)
+
+    pmc_out = open(os.path.join(src, "sq1.out")).read() if os.path.exists(
+        os.path.join(src, "sq1.out")) else ""
+    pmc_bench = None
+    for line in pmc_out.splitlines():
+        if line.startswith("{"):
+            pmc_bench = json.loads(line)
+    per_kernel = {}
+    for k in (passes["sq1"] or {}):
+        sq1, sq2 = passes["sq1"][k], (passes["sq2"] or {}).get(k, {})
+        n = max(sq1["dispatches"], 1)
+        gui = sq2.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+        fetch = (passes["tcc1"] or {}).get(k, {}).get("FETCH_SIZE", 0.0) * 1024
+        write = (passes["tcc2"] or {}).get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+        per_kernel[k] = {
+            "dispatches": n,
+            "valu_insts_per_launch": sq1["SQ_INSTS_VALU"] / n,
+            "salu_per_valu": sq1["SQ_INSTS_SALU"] / max(sq1["SQ_INSTS_VALU"], 1),
+            "valu_busy": (sq1["SQ_INSTS_VALU"] * 4 / (1024 * gui)) if gui else None,
+            "fetch_bytes_per_launch": fetch / n,
+            "write_bytes_per_launch": write / n,
+        }
+    tot_valu = sum(v["valu_insts_per_launch"] for v in per_kernel.values())
+    tot_gui = sum((passes["sq2"] or {}).get(k, {}).get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+                  / per_kernel[k]["dispatches"] for k in per_kernel)
+    summary = {
+        "tag": tag,
+        "tapes": (pmc_bench or bench)["config"]["tapes"],
+        "rows_per_gpu": (pmc_bench or bench)["config"]["rows_per_gpu"],
+        "hbm_bytes_per_launch": sum(v["fetch_bytes_per_launch"] + v["write_bytes_per_launch"]
+                                    for v in per_kernel.values()),
+        "valu_busy": tot_valu * 4 / (1024 * tot_gui) if tot_gui else None,
+        "effective_clock_ghz": None,
+        "per_kernel": per_kernel,
+        "bench_under_trace": {"value": bench["value"], "kernel_ms": bench["kernel_ms"]},
+    }
+    if pmc_bench and tot_gui:
+        summary["effective_clock_ghz"] = tot_gui / (pmc_bench["kernel_ms"] * 1e-3) / 1e9
+    json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    json.dump(summary, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
