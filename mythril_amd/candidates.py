@@ -1,0 +1,466 @@
+"""Candidate generation for one query: what the sieve's assignment rows should try.
+
+Uniform random 256-bit values almost never satisfy a path condition (a 4-byte selector check
+alone has p = 2^-32, SURVEY.md §7 "hard parts"), so rows are drawn from a *guide* harvested from
+the query's own terms:
+
+* **sets of alternatives** — every conjunct of the path condition is inverted toward the
+  columns it reads: ``t == K`` through ``concat`` / ``extract`` / ``zero_extend`` / ``ite`` /
+  ``+ c`` / ``- c`` / ``xor c`` / ``* odd c`` / ``not`` gives partial assignments (column ->
+  value) that make the conjunct true; ``Or`` gives alternatives (``sender`` in ACTORS,
+  transaction/symbolic.py:22-67); ordered comparisons against constants give boundary values.
+  An equality between two symbolic terms is tried with the query's constants of that width (an
+  address argument equal to ``Extract(159, 0, sender)``).  The parent path condition's witness
+  (the query minus its newest constraint, svm.py:257-262) is the first set;
+* **per-column pools** — the values the inversions produced for that column, boundary values of
+  comparisons, and 0, 1, 2^w - 1, 2^(w-1).
+
+The device generator (``mh_assign_generate_guided``, restated in oracle/guided_gen.py) draws
+each column from {small, uniform, pool} and then applies one alternative of each set with the
+set's probability, from a counter-based RNG, so any row range regenerates independently.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .lower import Schema
+from .tape import BOOL, Op, TapeBuilder
+
+Alt = Dict[str, int]          # column name -> value
+Copy = Tuple[str, str, int, int, int]  # (dst column, src column, dst_lo, src_lo, nbits)
+MAX_ALTS = 16                 # alternatives kept per inversion
+MAX_SETS = 1024
+MAX_POOL = 64                 # values per column pool
+MAX_EQ_CONSTS = 24            # constants tried against a symbolic-symbolic equality
+PROB_DEFAULT = 208            # of 256: a set is applied to ~81 % of rows
+PROB_PARENT = 192
+COPY_FLAG = 0x80000000        # entry_col bit: the entry copies bits of another column
+PROB_HINT = 64                # soft hints (conditions of ite branches)
+
+
+def _mask(w: int) -> int:
+    return (1 << w) - 1
+
+
+def _merge(xs: List[Alt], ys: List[Alt]) -> List[Alt]:
+    out = []
+    for x in xs:
+        for y in ys:
+            if any(k in x and x[k] != v for k, v in y.items()):
+                continue
+            z = dict(x)
+            z.update(y)
+            out.append(z)
+            if len(out) >= MAX_ALTS:
+                return out
+    return out
+
+
+@dataclass
+class Guide:
+    """Host form of mh_guide (include/mythril_hip.h)."""
+
+    columns: List[str]
+    widths: List[int]
+    pools: List[List[int]]
+    sets: List[Tuple[int, List[Alt]]] = field(default_factory=list)  # (prob/256, alternatives)
+    copy_sets: List[Tuple[int, List[List[Copy]]]] = field(default_factory=list)
+
+    def arrays(self):
+        """numpy arrays in mh_guide order."""
+        col_index = {c: i for i, c in enumerate(self.columns)}
+        width = np.array(self.widths, dtype=np.uint16)
+        pool_off = np.zeros(len(self.columns) + 1, dtype=np.uint32)
+        pool_vals: List[int] = []
+        for i, p in enumerate(self.pools):
+            pool_vals += p
+            pool_off[i + 1] = len(pool_vals)
+        n_sets = len(self.sets) + len(self.copy_sets)
+        set_off = np.zeros(n_sets + 1, dtype=np.uint32)
+        set_prob = np.zeros(max(n_sets, 1), dtype=np.uint8)
+        alt_off: List[int] = [0]
+        e_col: List[int] = []
+        e_val: List[int] = []
+        j = 0
+        for prob, alts in self.sets:
+            set_prob[j] = prob
+            for alt in alts:
+                for name, v in sorted(alt.items(), key=lambda kv: col_index[kv[0]]):
+                    e_col.append(col_index[name])
+                    e_val.append(v)
+                alt_off.append(len(e_col))
+            j += 1
+            set_off[j] = len(alt_off) - 1
+        for prob, alts in self.copy_sets:
+            set_prob[j] = prob
+            for alt in alts:
+                for dst, src, dlo, slo, nb in alt:
+                    e_col.append(col_index[dst] | COPY_FLAG)
+                    e_val.append(col_index[src] | dlo << 32 | slo << 64 | nb << 96)
+                alt_off.append(len(e_col))
+            j += 1
+            set_off[j] = len(alt_off) - 1
+        return dict(
+            width=width, pool_off=pool_off, pool=_limbs(pool_vals), set_off=set_off,
+            set_prob=set_prob, alt_off=np.array(alt_off, dtype=np.uint32),
+            entry_col=np.array(e_col or [0], dtype=np.uint32), entry_val=_limbs(e_val))
+
+
+def _limbs(vals: Sequence[int]) -> np.ndarray:
+    arr = np.zeros((max(len(vals), 1), 8), dtype=np.uint32)
+    for i, v in enumerate(vals):
+        for k in range(8):
+            arr[i, k] = (v >> (32 * k)) & 0xFFFFFFFF
+    return arr
+
+
+class Harvester:
+    def __init__(self, b: TapeBuilder, schema: Schema, columns: Sequence[str]):
+        self.b = b
+        self.schema = schema
+        self.columns = list(columns)
+        self.col_of_var = {}
+        for name in self.columns:
+            self.col_of_var[b.var_index[name]] = name
+        self.pools: Dict[str, List[int]] = {c: [] for c in self.columns}
+        self.sets: List[Tuple[int, List[Alt]]] = []
+        self._inv_memo: Dict[Tuple[int, int, int], Optional[List[Alt]]] = {}
+        self._consts_by_width: Dict[int, List[int]] = {}
+        self.hints: List[Tuple[int, List[Alt]]] = []
+        self.copy_sets: List[List[List[Copy]]] = []
+        self._hint_keys = set()
+
+    # -- inversion -------------------------------------------------------------------------
+    def invert_bits(self, n: int, value: int, mask: int, depth: int = 0) -> Optional[List[Alt]]:
+        """Partial assignments making (term n) & mask == value & mask; None = don't know."""
+        key = (n, value, mask)
+        if key in self._inv_memo:
+            return self._inv_memo[key]
+        r = self._invert_bits(n, value & mask, mask, depth) if depth < 64 else None
+        self._inv_memo[key] = r
+        return r
+
+    def _invert_bits(self, n: int, value: int, mask: int, depth: int) -> Optional[List[Alt]]:
+        b = self.b
+        op, w, a, bb, c, i0, i1 = b.nodes[n]
+        full = mask == _mask(w)
+        cv = b.const_value(n)
+        if cv is not None:
+            return [{}] if (cv & mask) == value else []
+        if op == Op.VAR:
+            name = self.col_of_var.get(i0)
+            return None if name is None else [{name: value}]
+        if op == Op.CONCAT:
+            wb = b.widths[bb]
+            m_hi, m_lo = mask >> wb, mask & _mask(wb)
+            parts = []
+            for child, m, v in ((a, m_hi, value >> wb), (bb, m_lo, value & _mask(wb))):
+                if m == 0:
+                    continue
+                r = self.invert_bits(child, v, m, depth + 1)
+                if r is None:
+                    r = [{}]
+                parts.append(r)
+            acc: List[Alt] = [{}]
+            for p in parts:
+                acc = _merge(acc, p)
+            return acc
+        if op == Op.EXTRACT:
+            return self.invert_bits(a, value << i1, mask << i1, depth + 1)
+        if op in (Op.ZEXT, Op.SEXT):
+            wa = b.widths[a]
+            if op == Op.ZEXT and (value >> wa) != 0:
+                return []
+            return self.invert_bits(a, value & _mask(wa), mask & _mask(wa), depth + 1)
+        if op == Op.ITE:
+            # the branch's requirement is exact; the condition's is usually a range (calldata
+            # bytes: `i < calldatasize`), so it is kept as a soft hint of its own, not merged
+            out: List[Alt] = []
+            for branch, truth in ((bb, True), (c, False)):
+                r = self.invert_bits(branch, value, mask, depth + 1)
+                if not r:
+                    continue
+                cond = self.invert_bool(a, truth, depth + 1)
+                if cond and cond != [{}]:
+                    self._hint(cond)
+                out += r
+            return out[:MAX_ALTS]
+        if not full:
+            return None
+        m = _mask(w)
+        if op in (Op.BVADD, Op.BVSUB, Op.BVXOR, Op.BVMUL):
+            ka, kb = b.const_value(a), b.const_value(bb)
+            if kb is not None:
+                x, k = a, kb
+            elif ka is not None:
+                x, k = bb, ka
+            else:
+                return None
+            if op == Op.BVADD:
+                t = value - k
+            elif op == Op.BVSUB:
+                t = value + k if x == a else k - value
+            elif op == Op.BVXOR:
+                t = value ^ k
+            else:
+                if k % 2 == 0:
+                    return None
+                t = value * pow(k, -1, 1 << w)
+            return self.invert_bits(x, t & m, m, depth + 1)
+        if op == Op.BVNOT:
+            return self.invert_bits(a, ~value & m, m, depth + 1)
+        if op == Op.BVNEG:
+            return self.invert_bits(a, -value & m, m, depth + 1)
+        return None
+
+    def invert_bool(self, n: int, truth: bool, depth: int = 0) -> Optional[List[Alt]]:
+        """Partial assignments making Bool node n == truth; None = don't know."""
+        if depth > 64:
+            return None
+        b = self.b
+        op, w, a, bb, c, i0, i1 = b.nodes[n]
+        cv = b.const_value(n)
+        if cv is not None:
+            return [{}] if bool(cv) == truth else []
+        if op == Op.NOT:
+            return self.invert_bool(a, not truth, depth + 1)
+        if op in (Op.AND, Op.OR):
+            conj = (op == Op.AND) == truth
+            x, y = self.invert_bool(a, truth, depth + 1), self.invert_bool(bb, truth, depth + 1)
+            if conj:
+                return _merge(x if x is not None else [{}], y if y is not None else [{}])
+            out = (x or []) + (y or [])
+            return out[:MAX_ALTS] if (x is not None or y is not None) else None
+        if op == Op.EQ:
+            if b.widths[a] == BOOL:
+                return None
+            ka, kb = b.const_value(a), b.const_value(bb)
+            t, k = (a, kb) if kb is not None else (bb, ka)
+            if k is None:
+                return None
+            if truth:
+                return self.invert_bits(t, k, _mask(b.widths[t]))
+            return [{}]  # t != K: almost every value satisfies it
+        if op in (Op.BVADD_NOOVFL_U, Op.BVMUL_NOOVFL_U, Op.BVSUB_NOUDFL_U):
+            wt = b.widths[a]
+            if op == Op.BVSUB_NOUDFL_U:  # b <=u a
+                pairs = [(0, 0), (1, 0)] if truth else [(0, 1), (1, 2)]
+            elif truth:
+                pairs = [(0, 0), (1, 1)]
+            else:  # overflow: a = 2^w - 1 with b >= 2 (add: b >= 1)
+                pairs = [(_mask(wt), 2), (_mask(wt), _mask(wt))]
+            out = []
+            for va, vb in pairs:
+                ra = self.invert_bits(a, va, _mask(wt))
+                rb = self.invert_bits(bb, vb, _mask(wt))
+                if ra is None and rb is None:
+                    continue
+                out += _merge(ra if ra is not None else [{}], rb if rb is not None else [{}])
+            return out[:MAX_ALTS] if out else None
+        if op in (Op.BVULT, Op.BVULE, Op.BVUGT, Op.BVUGE, Op.BVSLT, Op.BVSLE, Op.BVSGT,
+                  Op.BVSGE):
+            ka, kb = b.const_value(a), b.const_value(bb)
+            if ka is None and kb is None:
+                return None
+            wt = b.widths[a]
+            t = bb if ka is not None else a
+            k = ka if ka is not None else kb
+            out = []
+            for v in self._boundary(Op(op), k, t == a, truth, wt):
+                r = self.invert_bits(t, v, _mask(wt))
+                if r:
+                    out += r
+            return out[:MAX_ALTS]
+        return None
+
+    @staticmethod
+    def _boundary(op: Op, k: int, var_left: bool, truth: bool, w: int) -> List[int]:
+        """Values of the symbolic side that make `op` come out `truth` near the constant k."""
+        m = _mask(w)
+        # normalise to "var < k" style: which side of k satisfies?
+        less = op in (Op.BVULT, Op.BVULE, Op.BVSLT, Op.BVSLE)
+        strict = op in (Op.BVULT, Op.BVUGT, Op.BVSLT, Op.BVSGT)
+        want_below = less == var_left  # var < k (or <=) when the var is on the left of '<'
+        if not truth:
+            want_below, strict = not want_below, not strict
+        if want_below:
+            vals = [k - 1, k >> 1, 0] if strict else [k, k - 1, 0]
+        else:
+            vals = [k + 1, k + 2, (k << 1) + 1] if strict else [k, k + 1]
+        return [v & m for v in vals]
+
+    def segments(self, n: int, depth: int = 0) -> Optional[List[Tuple[int, int, str, int]]]:
+        """Bits of term n that are bits of a column: [(lo, nbits, column, column_lo)], through
+        concat / extract / zero_extend and the value branch of ite(c, x, const); None if the
+        term computes."""
+        if depth > 64:
+            return None
+        b = self.b
+        op, w, a, bb, c, i0, i1 = b.nodes[n]
+        if b.const_value(n) is not None:
+            return []
+        if op == Op.VAR:
+            name = self.col_of_var.get(i0)
+            return None if name is None else [(0, w, name, 0)]
+        if op == Op.CONCAT:
+            hi, lo = self.segments(a, depth + 1), self.segments(bb, depth + 1)
+            if hi is None or lo is None:
+                return None
+            wb = b.widths[bb]
+            return lo + [(x + wb, n_, col, cl) for x, n_, col, cl in hi]
+        if op == Op.EXTRACT:
+            inner = self.segments(a, depth + 1)
+            if inner is None:
+                return None
+            out = []
+            for x, n_, col, cl in inner:
+                s0, s1 = max(x, i1), min(x + n_, i0 + 1)
+                if s0 < s1:
+                    out.append((s0 - i1, s1 - s0, col, cl + (s0 - x)))
+            return out
+        if op == Op.ZEXT:
+            return self.segments(a, depth + 1)
+        if op == Op.ITE:
+            if b.const_value(c) is not None:
+                return self.segments(bb, depth + 1)
+            if b.const_value(bb) is not None:
+                return self.segments(c, depth + 1)
+        return None
+
+    def copy_alternatives(self, x: int, y: int) -> List[List[Copy]]:
+        """For x == y over column bits: copy y's bits into x's columns, or x's into y's."""
+        sx, sy = self.segments(x), self.segments(y)
+        if not sx or not sy:
+            return []
+        alts = []
+        for dst_side, src_side in ((sx, sy), (sy, sx)):
+            copies: List[Copy] = []
+            for dlo, dn, dcol, dcl in dst_side:
+                for slo, sn, scol, scl in src_side:
+                    s0, s1 = max(dlo, slo), min(dlo + dn, slo + sn)
+                    if s0 < s1 and dcol != scol:
+                        copies.append((dcol, scol, dcl + (s0 - dlo), scl + (s0 - slo), s1 - s0))
+            if copies:
+                alts.append(copies[:256])
+        return alts
+
+    def _hint(self, alts: List[Alt]) -> None:
+        key = tuple(tuple(sorted(a.items())) for a in alts)
+        if key not in self._hint_keys and len(self._hint_keys) < MAX_SETS // 4:
+            self._hint_keys.add(key)
+            self.hints.append((PROB_HINT, [a for a in alts if a][:MAX_ALTS]))
+
+    # -- driver ----------------------------------------------------------------------------
+    def _conjuncts(self, root: int) -> List[int]:
+        out, stack = [], [root]
+        while stack:
+            n = stack.pop()
+            op = self.b.nodes[n][0]
+            if op == Op.AND:
+                stack += [self.b.nodes[n][3], self.b.nodes[n][2]]
+            else:
+                out.append(n)
+        return out
+
+    def _consts_of_width(self, w: int) -> List[int]:
+        got = self._consts_by_width.get(w)
+        if got is None:
+            vals = sorted({v & _mask(w) for v in self.query_consts},
+                          key=lambda v: (-(v.bit_length() > 8), -v.bit_length(), v))
+            got = self._consts_by_width[w] = vals[:MAX_EQ_CONSTS]
+        return got
+
+    def harvest(self, root: int, parent: Optional[Alt] = None) -> Guide:
+        b = self.b
+        self.query_consts = set()
+        seen, stack = set(), [root]
+        while stack:  # the constants of this query (the pool is shared by all queries)
+            n = stack.pop()
+            if n in seen:
+                continue
+            seen.add(n)
+            op, _, a, bb, c, i0, _ = b.nodes[n]
+            if op == Op.CONST:
+                self.query_consts.add(b.pool.values[i0])
+            from .tape import ARITY
+
+            stack += [a, bb, c][:ARITY[Op(op)]]
+        if parent:
+            alt = {k: v for k, v in parent.items() if k in self.pools}
+            if alt:
+                self.sets.append((PROB_PARENT, [alt]))
+        seen_eq = set()
+        for conj in self._conjuncts(root):
+            alts = self.invert_bool(conj, True)
+            if alts and alts != [{}]:
+                self.sets.append((PROB_DEFAULT, [a for a in alts if a][:MAX_ALTS]))
+            # symbolic == symbolic anywhere below this conjunct: try the query's constants
+            for n in self._eq_nodes(conj):
+                if n in seen_eq:
+                    continue
+                seen_eq.add(n)
+                _, _, x, y, _, _, _ = b.nodes[n]
+                w = b.widths[x]
+                if w == BOOL or b.const_value(x) is not None or b.const_value(y) is not None:
+                    continue
+                calts = self.copy_alternatives(x, y)
+                if calts:
+                    if len(self.copy_sets) < MAX_SETS // 4:
+                        self.copy_sets.append(calts)
+                    continue
+                for k in self._consts_of_width(w):
+                    rx = self.invert_bits(x, k, _mask(w))
+                    ry = self.invert_bits(y, k, _mask(w))
+                    if rx and ry:
+                        both = _merge(rx, ry)
+                        if both and both != [{}]:
+                            self.sets.append((PROB_DEFAULT // 2, both[:MAX_ALTS]))
+                if len(self.sets) >= MAX_SETS:
+                    break
+            if len(self.sets) >= MAX_SETS:
+                break
+        # hints first: the exact requirements of the conjuncts (later sets) override them
+        self.sets = self.sets[:1] + self.hints + self.sets[1:] if parent else \
+            self.hints + self.sets
+        for _, alts in self.sets:
+            for alt in alts:
+                for name, v in alt.items():
+                    p = self.pools[name]
+                    if v not in p and len(p) < MAX_POOL:
+                        p.append(v)
+        widths = [self.schema.columns[c].width for c in self.columns]
+        for name, w in zip(self.columns, widths):
+            p = self.pools[name]
+            for v in (0, 1, _mask(w), 1 << (w - 1)):
+                if v not in p and len(p) < MAX_POOL:
+                    p.append(v)
+        # copies go last (their sources are final by then); the two directions of one
+        # equality are the two alternatives of one set
+        copy_sets = [(PROB_DEFAULT, alts) for alts in self.copy_sets]
+        return Guide(self.columns, widths, [self.pools[c] for c in self.columns],
+                     self.sets[:MAX_SETS], copy_sets[:MAX_SETS // 4])
+
+    def _eq_nodes(self, root: int) -> List[int]:
+        out, seen, stack = [], set(), [root]
+        b = self.b
+        while stack:
+            n = stack.pop()
+            if n in seen:
+                continue
+            seen.add(n)
+            op, w, a, bb, c, _, _ = b.nodes[n]
+            if op == Op.EQ:
+                out.append(n)
+            if w == BOOL and op in (Op.AND, Op.OR, Op.NOT, Op.XOR, Op.EQ, Op.ITE):
+                from .tape import ARITY
+
+                stack += [a, bb, c][:ARITY[Op(op)]]
+        return out
+
+
+def build_guide(b: TapeBuilder, root: int, schema: Schema, columns: Sequence[str],
+                parent: Optional[Alt] = None) -> Guide:
+    return Harvester(b, schema, columns).harvest(root, parent)

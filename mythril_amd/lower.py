@@ -1,0 +1,343 @@
+"""Lowering of arrays and uninterpreted functions into per-candidate tables.
+
+LASER's path conditions read free arrays (``{tx}_calldata``, ``Storage``, ``balance``:
+mythril/laser/ethereum/state/calldata.py:207-232, account.py:18-82, world_state.py:33-34) and
+apply keccak uninterpreted functions (mythril/laser/ethereum/keccak_function_manager.py:59-149).
+The device evaluates bit-vector terms only, so a query is lowered, once per ``get_model`` call,
+into a term over scalar *columns* whose every assignment denotes one complete z3-style model:
+
+* a free array ``A`` becomes a finite map over the constant keys the query reads (one *cell*
+  column per key) plus one *else* column: ``select(A, c)`` for a harvested constant ``c`` is
+  cell ``A[c]``; a symbolic index becomes ``ite(i == c1, A[c1], ite(i == c2, A[c2], ... A[*]))``.
+  That is exactly the shape of a z3 array model (``Store(...Store(K(else), c1, v1)..., ck, vk)``),
+  so a satisfying assignment is a model of the original query; ``store`` chains become ``ite``
+  over their keys and ``K(v)`` becomes ``v`` (array.py:16-63).
+* a keccak function ``keccak256_N`` becomes ``ite(x == c_i, k_i, H(x))`` over the concrete pairs
+  ``keccak256_N(c_i) == k_i`` the query states (keccak_function_manager.py:92-97,145-148), with
+  ``H(x) = base + ((keccak256(x) >> 139) << 6)``: a function of the argument (so congruence
+  holds), injective up to keccak collisions in 117 bits (so the inverse condition
+  ``keccak256_N-1(keccak256_N(x)) == x`` holds, lowered to ``x``), a multiple of 64, and inside
+  ``[base, base + 2^123)``, where ``base`` is the interval's lower bound harvested from the
+  query, rounded up to a multiple of 64 — the interval of ``_create_condition`` (:121-149) is
+  ``PART = (2^256-1) // 10^40 > 2^123 + 64`` wide, so the interval and ``mod 64`` conditions hold
+  by construction.  The hash runs on the device's Keccak-f[1600].
+* any other uninterpreted function is tabled like an array (cells over constant arguments plus
+  one else column).
+
+Anything else array- or function-sorted (array equality, ``ite`` over arrays, an inverse applied
+to something other than its forward function) raises ``LoweringUnsupported``: the query goes to
+z3 unchanged.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+from .tape import BOOL, F_ARRAY, Op, TapeBuilder, TapeError
+
+KECCAK_SHIFT = 139   # keep 117 bits of the hash ...
+KECCAK_ALIGN = 6     # ... as multiples of 64: H - base < 2^123 < PART
+ORDERED = {Op.BVULT, Op.BVULE, Op.BVUGT, Op.BVUGE, Op.BVSLT, Op.BVSLE, Op.BVSGT, Op.BVSGE}
+
+
+class LoweringUnsupported(TapeError):
+    """The query uses an array/function construct the sieve does not model: ask z3."""
+
+
+@dataclass
+class Column:
+    """One scalar column of the candidate assignments of a query."""
+
+    name: str             # VAR name in the tape set
+    width: int
+    kind: str             # "var" | "cell" | "else" | "ufcell" | "ufelse"
+    symbol: str           # variable / array / function name
+    key: Optional[int] = None
+
+
+@dataclass
+class KeccakMap:
+    base: int                                            # aligned lower bound of the interval
+    pairs: Dict[int, int] = field(default_factory=dict)  # concrete argument -> hash
+
+
+@dataclass
+class Schema:
+    """What one query's columns mean: enough to rebuild a model from a witness row."""
+
+    cells: Dict[str, Dict[int, str]] = field(default_factory=dict)   # array -> key -> column
+    uf_cells: Dict[str, Dict[int, str]] = field(default_factory=dict)
+    keccak: Dict[str, KeccakMap] = field(default_factory=dict)
+    columns: Dict[str, Column] = field(default_factory=dict)         # column name -> Column
+
+
+def cell_name(arr: str, key: int) -> str:
+    return "%s[%#x]" % (arr, key)
+
+
+def else_name(arr: str) -> str:
+    return "%s[*]" % arr
+
+
+def is_keccak(name: str) -> bool:
+    return name.startswith("keccak256_") and not name.endswith("-1")
+
+
+def _walk(b: TapeBuilder, roots: Iterable[int]) -> List[int]:
+    """Every node reachable from roots (array chains included), children before parents."""
+    order, seen = [], set()
+    stack = [(r, False) for r in roots]
+    while stack:
+        n, done = stack.pop()
+        if done:
+            order.append(n)
+            continue
+        if n in seen:
+            continue
+        seen.add(n)
+        stack.append((n, True))
+        op, _, a, bb, c, _, _ = b.nodes[n]
+        k = _arity(op)
+        for ch in (a, bb, c)[:k][::-1]:
+            if ch not in seen:
+                stack.append((ch, False))
+    return order
+
+
+def _arity(op: int) -> int:
+    from .tape import ARITY
+
+    return ARITY[Op(op)]
+
+
+class Lowering:
+    """Harvest a query's constant keys, then rewrite its terms onto scalar columns.
+
+    With ``frozen`` (the schema of a solved query) nothing is harvested: constant keys outside
+    the schema read the else column, i.e. the value the model gives every other key — the
+    behaviour ``Model.eval`` needs (mythril/laser/smt/model.py:45-59)."""
+
+    def __init__(self, b: TapeBuilder, frozen: Optional[Schema] = None):
+        self.b = b
+        self.frozen = frozen is not None
+        self.schema = frozen if frozen is not None else Schema()
+        self.memo: Dict[int, int] = {}
+        self.sym = b.symbols
+
+    # -- pass 1: harvest ------------------------------------------------------------------
+    def harvest(self, roots: Sequence[int]) -> None:
+        if self.frozen:
+            return
+        b = self.b
+        bounds: Dict[str, List[int]] = {}
+        for n in _walk(b, roots):
+            op, w, a, bb, c, i0, i1 = b.nodes[n]
+            if op == Op.SELECT:
+                base = self._array_base(a)
+                if base is not None:
+                    name = self.sym.array_names[b.nodes[base][5]]
+                    key = b.const_value(bb)
+                    cells = self.schema.cells.setdefault(name, {})
+                    if key is not None:
+                        cells.setdefault(key, cell_name(name, key))
+            elif op == Op.UF:
+                fname = self.sym.function_names[i0]
+                if is_keccak(fname):
+                    self.schema.keccak.setdefault(fname, KeccakMap(0))
+                elif not fname.endswith("-1"):
+                    cells = self.schema.uf_cells.setdefault(fname, {})
+                    key = b.const_value(a)
+                    if key is not None:
+                        cells.setdefault(key, cell_name(fname, key))
+            elif op == Op.EQ or op in ORDERED:
+                for x, y in ((a, bb), (bb, a)):
+                    f = self._keccak_app(x)
+                    kv = b.const_value(y)
+                    if f is None or kv is None:
+                        continue
+                    if op == Op.EQ:
+                        arg = b.const_value(b.nodes[x][2])
+                        if arg is not None:  # keccak256_N(c) == k: a concrete pair
+                            self.schema.keccak.setdefault(f, KeccakMap(0)).pairs[arg] = kv
+                    else:
+                        bounds.setdefault(f, []).append(kv)
+        for f, km in self.schema.keccak.items():
+            lo = min(bounds.get(f, [0]))
+            km.base = (lo + 63) & ~63
+
+    def _keccak_app(self, n: int) -> Optional[str]:
+        op, _, _, _, _, i0, _ = self.b.nodes[n]
+        if op != Op.UF:
+            return None
+        name = self.sym.function_names[i0]
+        return name if is_keccak(name) else None
+
+    def _array_base(self, arr: int) -> Optional[int]:
+        """The ARRAY node under a store chain, None for a K(...) base."""
+        b = self.b
+        while True:
+            op = b.nodes[arr][0]
+            if op == Op.STORE:
+                arr = b.nodes[arr][2]
+            elif op == Op.ARRAY:
+                return arr
+            elif op == Op.CONST_ARRAY:
+                return None
+            else:
+                raise LoweringUnsupported("array term %s is not a store chain" % Op(op).name)
+
+    # -- pass 2: rewrite -------------------------------------------------------------------
+    def _column(self, name: str, width: int, kind: str, symbol: str,
+                key: Optional[int] = None) -> int:
+        if name not in self.schema.columns:
+            if self.frozen and kind != "var":
+                raise LoweringUnsupported("column %s is not in the frozen schema" % name)
+            self.schema.columns[name] = Column(name, width, kind, symbol, key)
+        return self.b.var(name, width)
+
+    def _deps(self, n: int) -> List[int]:
+        b = self.b
+        op, _, a, bb, c, i0, _ = b.nodes[n]
+        if op == Op.SELECT:
+            deps = [bb]
+            arr = a
+            while b.nodes[arr][0] == Op.STORE:
+                deps += [b.nodes[arr][3], b.nodes[arr][4]]
+                arr = b.nodes[arr][2]
+            if b.nodes[arr][0] == Op.CONST_ARRAY:
+                deps.append(b.nodes[arr][2])
+            elif b.nodes[arr][0] != Op.ARRAY:
+                raise LoweringUnsupported("array term %s is not a store chain"
+                                          % Op(b.nodes[arr][0]).name)
+            return deps
+        if op == Op.UF:
+            fname = self.sym.function_names[i0]
+            if fname.endswith("-1"):
+                inner = b.nodes[a]
+                if inner[0] != Op.UF or self.sym.function_names[inner[5]] != fname[:-2]:
+                    raise LoweringUnsupported("%s applied to something other than %s(...)"
+                                              % (fname, fname[:-2]))
+                return [inner[2]]
+            return [a]
+        if b.flags[n] & F_ARRAY:
+            raise LoweringUnsupported("array-sorted term used as a value")
+        k = _arity(op)
+        for ch in (a, bb, c)[:k]:
+            if b.flags[ch] & F_ARRAY:
+                raise LoweringUnsupported("%s over arrays" % Op(op).name)
+        return [a, bb, c][:k]
+
+    def lower(self, root: int) -> int:
+        """The column-only equivalent of node `root` (memoised across calls)."""
+        memo = self.memo
+        if root in memo:
+            return memo[root]
+        stack = [(root, False)]
+        while stack:
+            n, ready = stack.pop()
+            if n in memo:
+                continue
+            if not ready:
+                stack.append((n, True))
+                for d in self._deps(n):
+                    if d not in memo:
+                        stack.append((d, False))
+                continue
+            memo[n] = self._rewrite(n)
+        return memo[root]
+
+    def _rewrite(self, n: int) -> int:
+        b, memo = self.b, self.memo
+        op, w, a, bb, c, i0, i1 = b.nodes[n]
+        if op == Op.VAR:
+            name = self._var_name(i0)
+            self._column(name, w, "var", name)
+            return n
+        if op == Op.SELECT:
+            return self._select(a, memo[bb], bb)
+        if op == Op.UF:
+            return self._apply(n)
+        k = _arity(op)
+        if k == 0:
+            return n
+        args = [memo[x] for x in (a, bb, c)[:k]]
+        if args == [a, bb, c][:k]:
+            return n
+        return b.op(Op(op), *args, imm0=i0, imm1=i1)
+
+    def _var_name(self, col: int) -> str:
+        names = getattr(self, "_names", None)
+        if names is None or len(names) != len(self.b.var_index):
+            names = self._names = {v: k for k, v in self.b.var_index.items()}
+        return names[col]
+
+    def _select(self, arr: int, idx: int, idx_orig: int) -> int:
+        b = self.b
+        op = b.nodes[arr][0]
+        if op == Op.STORE:
+            key, val = self.memo[b.nodes[arr][3]], self.memo[b.nodes[arr][4]]
+            rest = self._select(b.nodes[arr][2], idx, idx_orig)
+            return b.op(Op.ITE, b.op(Op.EQ, idx, key), val, rest)
+        if op == Op.CONST_ARRAY:
+            return self.memo[b.nodes[arr][2]]
+        name = self.sym.array_names[b.nodes[arr][5]]
+        rng = b.widths[arr]
+        return self._table(name, rng, idx, self.schema.cells.get(name, {}), "cell", "else")
+
+    def _table(self, name: str, rng: int, idx: int, cells: Dict[int, str], kcell: str,
+               kelse: str) -> int:
+        b = self.b
+        key = b.const_value(idx)
+        if key is not None and key in cells:
+            return self._column(cells[key], rng, kcell, name, key)
+        acc = self._column(else_name(name), rng, kelse, name)
+        if key is not None:  # a constant key outside the table reads the else value
+            return acc
+        for ck in sorted(cells, reverse=True):
+            cell = self._column(cells[ck], rng, kcell, name, ck)
+            kn = b.const(ck, b.widths[idx])
+            acc = b.op(Op.ITE, b.op(Op.EQ, idx, kn), cell, acc)
+        return acc
+
+    def _apply(self, n: int) -> int:
+        b = self.b
+        _, w, a, _, _, i0, _ = b.nodes[n]
+        fname = self.sym.function_names[i0]
+        if fname.endswith("-1"):
+            return self.memo[b.nodes[a][2]]
+        x = self.memo[a]
+        if is_keccak(fname):
+            km = self.schema.keccak.get(fname)
+            if km is None:
+                if not self.frozen:
+                    raise LoweringUnsupported("keccak function %s not harvested" % fname)
+                km = KeccakMap(0)
+            h = b.op(Op.KECCAK, x)
+            h = b.op(Op.BVLSHR, h, b.const(KECCAK_SHIFT, 256))
+            h = b.op(Op.BVSHL, h, b.const(KECCAK_ALIGN, 256))
+            acc = b.op(Op.BVADD, h, b.const(km.base, 256)) if km.base else h
+            if w != 256:
+                raise LoweringUnsupported("keccak function %s has range %d" % (fname, w))
+            for arg in sorted(km.pairs, reverse=True):
+                acc = b.op(Op.ITE, b.op(Op.EQ, x, b.const(arg, b.widths[x])),
+                           b.const(km.pairs[arg], 256), acc)
+            return acc
+        cells = self.schema.uf_cells.get(fname, {})
+        return self._table(fname, w, x, cells, "ufcell", "ufelse")
+
+
+def lower_query(b: TapeBuilder, roots: Sequence[int],
+                frozen: Optional[Schema] = None) -> Tuple[int, Schema]:
+    """Lower the conjunction of Bool `roots`: (root node of the column-only term, schema)."""
+    L = Lowering(b, frozen)
+    L.harvest(roots)
+    low = [L.lower(r) for r in roots]
+    for r in low:
+        if b.widths[r] != BOOL:
+            raise TapeError("constraints must be Bool")
+    if not low:
+        return b.true(), L.schema
+    acc = low[0]
+    for x in low[1:]:
+        acc = b.op(Op.AND, acc, x)
+    return acc, L.schema

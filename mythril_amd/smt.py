@@ -34,12 +34,23 @@ class Context:
         self.tapeset = tapeset if tapeset is not None else TapeSet()
         self.b: TapeBuilder = self.tapeset.builder()
 
+    def query(self, *constraints: "Bool"):
+        """The conjunction of ``constraints`` as one device tape plus the schema of its columns
+        (arrays and uninterpreted functions lowered, mythril_amd/lower.py)."""
+        from .lower import lower_query
+
+        roots = [_as_bool(c, self).node for c in constraints]
+        root, schema = lower_query(self.b, roots)
+        return self.b.finish(root), schema
+
     def tape(self, *constraints: "Bool") -> Tape:
         """The conjunction of ``constraints`` as one tape (what get_model would hand to z3)."""
-        root = And(*constraints, ctx=self) if len(constraints) != 1 else constraints[0]
-        if isinstance(root, BitVec) and not isinstance(root, Bool):
-            return self.b.finish(root.node)
-        return self.b.finish(_as_bool(root, self).node)
+        if len(constraints) == 1 and isinstance(constraints[0], BitVec) \
+                and not isinstance(constraints[0], Bool):
+            from .lower import Lowering
+
+            return self.b.finish(Lowering(self.b).lower(constraints[0].node))
+        return self.query(*constraints)[0]
 
     def add_tape(self, *constraints) -> int:
         return self.tapeset.add(self.tape(*constraints))
@@ -78,14 +89,7 @@ class Expression:
         return hash((id(self.ctx), self.node))
 
     def _const_value(self) -> Optional[int]:
-        op, _, _, _, _, imm0, _ = self.ctx.b.nodes[self.node]
-        if op == Op.CONST:
-            return self.ctx.b.pool.values[imm0]
-        if op == Op.TRUE:
-            return 1
-        if op == Op.FALSE:
-            return 0
-        return None
+        return self.ctx.b.const_value(self.node)
 
 
 def _b(ctx: Context) -> TapeBuilder:
@@ -452,48 +456,69 @@ def Keccak256(data: BitVec) -> BitVec:
 
 
 class BaseArray:
-    """Select/Store arrays lowered to ite chains (mythril/laser/smt/array.py:16-63).
+    """Symbolic arrays (mythril/laser/smt/array.py:16-63).
 
-    ``select(store(A, k, v), i) = ite(i == k, v, select(A, i))`` and ``select(K(c), i) = c``.
-    A free ``Array`` base (uninterpreted contents) has no device lowering yet.
+    ``raw`` of the reference is a z3 array term that ``__setitem__`` replaces by a ``Store``;
+    here ``node`` is the array-sorted term node and is replaced the same way.  Reads build
+    ``select`` terms; lower.py turns them into per-candidate array tables (a finite map over
+    the constant keys the query reads, plus one else-value), so free arrays such as
+    ``{tx}_calldata`` and ``Storage`` need no device support of their own.
     """
 
-    def __init__(self, domain: int, value_range: int):
-        self.domain = domain
-        self.range = value_range
-        self.stores: List[tuple] = []
-        self.default: Optional[int] = None
-        self.name: Optional[str] = None
+    ctx: Context
+    node: int
+    domain: int
+    range: int
 
     def __getitem__(self, item: BitVec) -> BitVec:
         if isinstance(item, slice):
             raise ValueError("Instance of BaseArray, does not support getitem with slices")
-        ctx = item.ctx
-        if self.default is None:
-            raise TapeError("reads of free array %r are not supported by the sieve" % self.name)
-        acc = BitVec(_b(ctx).const(self.default, self.range), ctx)
-        for k, v in self.stores:
-            acc = If(item == k, v, acc)
-        return acc
+        return BitVec(_b(self.ctx).select(self.node, item.node), self.ctx)
 
     def __setitem__(self, key: BitVec, value) -> None:
         if isinstance(value, Bool):
             value = If(value, 1, 0)
         if not isinstance(value, BitVec):
-            value = symbol_factory.BitVecVal(int(value), self.range)
-        self.stores.append((key, value))
+            value = BitVec(_b(self.ctx).const(int(value), self.range), self.ctx)
+        if not isinstance(key, BitVec):
+            key = BitVec(_b(self.ctx).const(int(key), self.domain), self.ctx)
+        self.node = _b(self.ctx).store(self.node, key.node, value.node)
 
 
 class Array(BaseArray):
+    """array.py:35-47 (z3.Array(name, BitVecSort(domain), BitVecSort(value_range)))."""
+
     def __init__(self, name: str, domain: int, value_range: int):
-        super().__init__(domain, value_range)
+        self.ctx = context()
         self.name = name
+        self.domain = domain
+        self.range = value_range
+        self.node = _b(self.ctx).array(name, domain, value_range)
 
 
 class K(BaseArray):
+    """array.py:50-63 (z3.K(BitVecSort(domain), BitVecVal(value, value_range)))."""
+
     def __init__(self, domain: int, value_range: int, value: int):
-        super().__init__(domain, value_range)
-        self.default = int(value) & ((1 << value_range) - 1)
+        self.ctx = context()
+        self.domain = domain
+        self.range = value_range
+        self.value = int(value) & ((1 << value_range) - 1)
+        default = _b(self.ctx).const(self.value, value_range)
+        self.node = _b(self.ctx).const_array(domain, default)
+
+
+class Function:
+    """An uninterpreted function (mythril/laser/smt/function.py:7-25)."""
+
+    def __init__(self, name: str, domain: int, value_range: int):
+        self.name = name
+        self.domain = domain
+        self.range = value_range
+
+    def __call__(self, item: BitVec) -> BitVec:
+        return BitVec(_b(item.ctx).apply(self.name, self.domain, self.range, item.node),
+                      item.ctx, item.annotations)
 
 
 __all__ = [
@@ -501,5 +526,5 @@ __all__ = [
     "And", "Or", "Xor", "Not", "is_true", "is_false", "simplify", "If", "UGT", "UGE", "ULT",
     "ULE", "Concat", "Extract", "ZeroExt", "SignExt", "URem", "SRem", "SMod", "UDiv", "LShR",
     "Sum", "BVAddNoOverflow", "BVMulNoOverflow", "BVSubNoUnderflow", "Keccak256", "BaseArray",
-    "Array", "K", "BOOL",
+    "Array", "K", "Function", "BOOL",
 ]

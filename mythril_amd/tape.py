@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import enum
 from dataclasses import dataclass, field
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -70,6 +70,13 @@ class Op(enum.IntEnum):
     EVM_EXP = 70
     EVM_SIGNEXTEND = 71
     EVM_BYTE = 72
+    # host-only term kinds: built by the term layer (smt.py, smtlib.py) and removed by
+    # lower.py before a tape reaches mh_tapes_compile (which rejects them)
+    ARRAY = 80        # free array symbol: imm0 = array id, imm1 = domain width, width = range
+    CONST_ARRAY = 81  # K(domain, v): a = default value node, imm1 = domain width
+    STORE = 82        # store(a, b = key, c = value)
+    SELECT = 83       # select(a = array, b = index) -> range-width bit-vector
+    UF = 84           # uninterpreted function application: imm0 = function id, a = argument
 
 
 NODE_DTYPE = np.dtype(
@@ -86,11 +93,14 @@ NODE_DTYPE = np.dtype(
 )
 assert NODE_DTYPE.itemsize == 24
 
+HOST_ONLY = {Op.ARRAY, Op.CONST_ARRAY, Op.STORE, Op.SELECT, Op.UF}
+F_ARRAY = 1  # mh_node.flags bit of host-only array-sorted nodes (never sent to the device)
+
 # operand arity per op (number of node operands a, b, c used)
 ARITY = {
     Op.CONST: 0, Op.VAR: 0, Op.TRUE: 0, Op.FALSE: 0,
     Op.BVNEG: 1, Op.BVNOT: 1, Op.NOT: 1, Op.EXTRACT: 1, Op.ZEXT: 1, Op.SEXT: 1, Op.KECCAK: 1,
-    Op.ITE: 3,
+    Op.ITE: 3, Op.ARRAY: 0, Op.CONST_ARRAY: 1, Op.STORE: 3, Op.UF: 1,
 }
 for _op in Op:
     ARITY.setdefault(_op, 2)
@@ -139,15 +149,18 @@ class ConstPool:
 class TapeBuilder:
     """Builds one tape; nodes are hash-consed (structurally equal terms share one node)."""
 
-    def __init__(self, pool: ConstPool, var_index: Dict[str, int]):
+    def __init__(self, pool: ConstPool, var_index: Dict[str, int],
+                 symbols: "Optional[Symbols]" = None):
         self.pool = pool
         self.var_index = var_index
+        self.symbols = symbols if symbols is not None else Symbols()
         self.nodes: List[Tuple[int, int, int, int, int, int, int]] = []
         self.widths: List[int] = []
+        self.flags: List[int] = []
         self._memo: Dict[tuple, int] = {}
 
     # -- node creation ------------------------------------------------------------------------
-    def _add(self, op: Op, width: int, a=0, b=0, c=0, imm0=0, imm1=0) -> int:
+    def _add(self, op: Op, width: int, a=0, b=0, c=0, imm0=0, imm1=0, flags=0) -> int:
         key = (int(op), width, a, b, c, imm0, imm1)
         got = self._memo.get(key)
         if got is not None:
@@ -155,21 +168,99 @@ class TapeBuilder:
         idx = len(self.nodes)
         self.nodes.append(key)
         self.widths.append(width)
+        self.flags.append(flags)
         self._memo[key] = idx
         return idx
 
     def width(self, n: int) -> int:
         return self.widths[n]
 
+    def is_array(self, n: int) -> bool:
+        return bool(self.flags[n] & F_ARRAY)
+
+    def const_value(self, n: int) -> Optional[int]:
+        """The value of a constant node, else None.  CONST / TRUE / FALSE, and the bit-layout
+        ops CONCAT / EXTRACT / ZEXT / SEXT over constants, which z3's ``simplify`` folds before
+        ``BitVec.symbolic`` / ``.value`` look (mythril/laser/smt/bitvec.py:44-60); arithmetic is
+        not folded here."""
+        op, w, a, b, _, imm0, imm1 = self.nodes[n]
+        if op == Op.CONST:
+            return self.pool.values[imm0]
+        if op == Op.TRUE:
+            return 1
+        if op == Op.FALSE:
+            return 0
+        if op == Op.CONCAT:
+            hi, lo = self.const_value(a), self.const_value(b)
+            if hi is None or lo is None:
+                return None
+            return (hi << self.widths[b]) | lo
+        if op in (Op.EXTRACT, Op.ZEXT, Op.SEXT):
+            x = self.const_value(a)
+            if x is None:
+                return None
+            if op == Op.EXTRACT:
+                return (x >> imm1) & ((1 << (imm0 - imm1 + 1)) - 1)
+            if op == Op.SEXT and x >> (self.widths[a] - 1) & 1:
+                return (x | (((1 << imm0) - 1) << self.widths[a]))
+            return x
+        return None
+
+    # -- host-only term kinds (arrays, uninterpreted functions) -------------------------------
+    def array(self, name: str, domain: int, value_range: int) -> int:
+        """Free array symbol (mythril/laser/smt/array.py:35-47, z3.Array)."""
+        aid = self.symbols.array_id(name, domain, value_range)
+        return self._add(Op.ARRAY, value_range, imm0=aid, imm1=domain, flags=F_ARRAY)
+
+    def const_array(self, domain: int, default: int) -> int:
+        """K(domain, default) (array.py:50-63, z3.K); `default` is a bit-vector node."""
+        if self.is_array(default) or self.widths[default] == BOOL:
+            raise TapeError("K needs a bit-vector default")
+        return self._add(Op.CONST_ARRAY, self.widths[default], a=default, imm1=domain,
+                         flags=F_ARRAY)
+
+    def store(self, arr: int, key: int, value: int) -> int:
+        """z3.Store (array.py:27-32)."""
+        dom, rng = self._array_sort(arr)
+        if self.widths[key] != dom or self.widths[value] != rng:
+            raise TapeError("store sort mismatch: key %d/%d, value %d/%d"
+                            % (self.widths[key], dom, self.widths[value], rng))
+        return self._add(Op.STORE, rng, a=arr, b=key, c=value, imm1=dom, flags=F_ARRAY)
+
+    def select(self, arr: int, index: int) -> int:
+        """z3.Select (array.py:19-25)."""
+        dom, rng = self._array_sort(arr)
+        if self.widths[index] != dom or self.is_array(index):
+            raise TapeError("select index is %d bits, array domain %d"
+                            % (self.widths[index], dom))
+        return self._add(Op.SELECT, rng, a=arr, b=index)
+
+    def apply(self, name: str, domain: int, value_range: int, arg: int) -> int:
+        """Uninterpreted function application (mythril/laser/smt/function.py:7-25)."""
+        if self.widths[arg] != domain or self.is_array(arg):
+            raise TapeError("%s takes %d bits, got %d" % (name, domain, self.widths[arg]))
+        fid = self.symbols.function_id(name, domain, value_range)
+        return self._add(Op.UF, value_range, a=arg, imm0=fid)
+
+    def _array_sort(self, arr: int) -> Tuple[int, int]:
+        if not self.is_array(arr):
+            raise TapeError("node %d is not an array" % arr)
+        return self.nodes[arr][6], self.widths[arr]
+
     def const(self, value: int, width: int) -> int:
-        if not 1 <= width <= 256:
-            raise TapeError("constants are 1..256 bits wide (use concat for wider): %d" % width)
+        """A constant; wider than 256 bits it is a CONCAT of pool entries (the pool is 256-bit)."""
+        if not 1 <= width <= MAX_WIDTH:
+            raise TapeError("constants are 1..%d bits wide: %d" % (MAX_WIDTH, width))
         value &= (1 << width) - 1
+        if width > 256:
+            lo = self.const(value & ((1 << 256) - 1), 256)
+            return self.op(Op.CONCAT, self.const(value >> 256, width - 256), lo)
         return self._add(Op.CONST, width, imm0=self.pool.add(value))
 
     def var(self, name: str, width: int = 256) -> int:
         if not 1 <= width <= 256:
             raise TapeError("variables are 1..256 bits wide: %d" % width)
+        self.symbols.check_var(name, width)
         if name not in self.var_index:
             self.var_index[name] = len(self.var_index)
         return self._add(Op.VAR, width, imm0=self.var_index[name])
@@ -182,6 +273,11 @@ class TapeBuilder:
 
     def op(self, op: Op, *args: int, imm0: int = 0, imm1: int = 0) -> int:
         op = Op(op)
+        if op in HOST_ONLY:
+            raise TapeError("%s is built with array()/const_array()/store()/select()/apply()"
+                            % op.name)
+        if any(self.flags[x] & F_ARRAY for x in args):
+            raise TapeError("%s does not take array operands" % op.name)
         ws = [self.widths[x] for x in args]
         if len(args) != ARITY[op]:
             raise TapeError("%s takes %d operands" % (op.name, ARITY[op]))
@@ -262,8 +358,43 @@ class TapeBuilder:
                 opnds[j] = remap[opnds[j]]
             for j in range(k, 3):
                 opnds[j] = 0
-            arr[new] = (op, 0, w, opnds[0], opnds[1], opnds[2], i0, i1)
+            arr[new] = (op, self.flags[old], w, opnds[0], opnds[1], opnds[2], i0, i1)
         return Tape(arr)
+
+
+class Symbols:
+    """Declared arrays and uninterpreted functions of a tape set (name -> id and sort), plus the
+    sorts of scalar variables, so one name always denotes one symbol of one sort (as in z3)."""
+
+    def __init__(self):
+        self.arrays: Dict[str, Tuple[int, int, int]] = {}     # name -> (id, domain, range)
+        self.functions: Dict[str, Tuple[int, int, int]] = {}  # name -> (id, domain, range)
+        self.array_names: List[str] = []
+        self.function_names: List[str] = []
+        self.var_widths: Dict[str, int] = {}
+
+    def array_id(self, name: str, domain: int, value_range: int) -> int:
+        got = self.arrays.get(name)
+        if got is None:
+            got = self.arrays[name] = (len(self.array_names), domain, value_range)
+            self.array_names.append(name)
+        elif got[1:] != (domain, value_range):
+            raise TapeError("array %r redeclared with another sort" % name)
+        return got[0]
+
+    def function_id(self, name: str, domain: int, value_range: int) -> int:
+        got = self.functions.get(name)
+        if got is None:
+            got = self.functions[name] = (len(self.function_names), domain, value_range)
+            self.function_names.append(name)
+        elif got[1:] != (domain, value_range):
+            raise TapeError("function %r redeclared with another sort" % name)
+        return got[0]
+
+    def check_var(self, name: str, width: int) -> None:
+        got = self.var_widths.setdefault(name, width)
+        if got != width:
+            raise TapeError("variable %r is %d bits, used as %d" % (name, got, width))
 
 
 @dataclass
@@ -287,11 +418,16 @@ class TapeSet:
         for n in var_names:
             self.var_index.setdefault(n, len(self.var_index))
         self.tapes: List[Tape] = []
+        self.symbols = Symbols()
 
     def builder(self) -> TapeBuilder:
-        return TapeBuilder(self.pool, self.var_index)
+        return TapeBuilder(self.pool, self.var_index, self.symbols)
 
     def add(self, tape: Tape) -> int:
+        host = [Op(int(o)).name for o in set(tape.nodes["op"].tolist()) if int(o) in HOST_ONLY]
+        if host:
+            raise TapeError("tape still holds host-only terms %s: lower it first "
+                            "(mythril_amd.lower)" % sorted(host))
         self.tapes.append(tape)
         return len(self.tapes) - 1
 

@@ -147,13 +147,16 @@ def evm_byte(i: int, x: int, w: int) -> int:
 Value = Union[int, bool]
 
 
-def evaluate(nodes, consts: Sequence[int], assignment: Sequence[int], all_values: bool = False):
+def evaluate(nodes, consts: Sequence[int], assignment: Sequence[int], all_values: bool = False,
+             extra=None):
     """Evaluate one tape.
 
     nodes: structured array / sequence of records with fields op, width, a, b, c, imm0, imm1
     consts: the tape set's constant pool (Python ints)
     assignment: per-variable 256-bit values (Python ints), indexed by column
     Returns the root value (int for bit-vectors, bool for Bool); with all_values, every node's.
+    extra(op, node, vals): value of an op this module does not know (oracle/term_eval.py uses it
+    for arrays and uninterpreted functions).
     """
     vals: List[Value] = []
     for nd in nodes:
@@ -256,6 +259,8 @@ def evaluate(nodes, consts: Sequence[int], assignment: Sequence[int], all_values
         elif op == KECCAK:
             wa = int(nodes[a]["width"])
             v = int.from_bytes(keccak256(vals[a].to_bytes(wa // 8, "big")), "big")
+        elif extra is not None:
+            v = extra(op, nd, vals)
         else:
             raise ValueError("unknown op %d" % op)
         vals.append(v)

@@ -1,0 +1,140 @@
+"""Builders of LASER-shaped path conditions with the mythril_amd.smt term API (test helpers).
+
+Each builder follows the reference construction it names, so the queries the tests hand to the
+lowering / sieve have the shapes ``myth analyze`` produces:
+
+* calldata reads: ``If(i < calldatasize, calldata[i], 0)`` per byte, words as ``Concat`` of 32
+  bytes (mythril/laser/ethereum/state/calldata.py:48-54, 219-232; ``<`` is signed, bitvec.py);
+* the function-selector check of a Solidity dispatcher (JUMPI on
+  ``Extract(255, 224, calldataload(0)) == selector``, instructions.py:1543-1619);
+* ``sender in ACTORS`` (transaction/symbolic.py:22-67, 87-104);
+* ``UGE(balance[sender], value)`` (transaction_models.py:129-133, world_state.py:33-34);
+* storage reads of a free ``Storage`` array (account.py:18-82);
+* keccak UF applications with the manager's interval / mod-64 / inverse / concrete-pair
+  conditions (keccak_function_manager.py:83-149) — concrete hashes from the oracle's Keccak-256;
+* the integer-overflow module's ``BVAddNoOverflow``/``BVMulNoOverflow`` (integer.py:141-157).
+"""
+from __future__ import annotations
+
+from mythril_amd import smt
+from mythril_amd.smt import (And, Array, BitVec, Concat, Extract, Function, If, K, Not, Or, ULE,
+                             ULT, UGE, URem, symbol_factory)
+from oracle.keccak import keccak256
+
+CREATOR = 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE
+ATTACKER = 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF
+SOMEGUY = 0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA
+
+TOTAL_PARTS = 10 ** 40
+PART = (2 ** 256 - 1) // TOTAL_PARTS
+INTERVAL_DIFFERENCE = 10 ** 30
+
+
+class Calldata:
+    """SymbolicCalldata (calldata.py:207-255)."""
+
+    def __init__(self, tx_id: str):
+        self.size = symbol_factory.BitVecSym("%s_calldatasize" % tx_id, 256)
+        self.data = Array("%s_calldata" % tx_id, 256, 8)
+
+    def load(self, i) -> BitVec:
+        item = symbol_factory.BitVecVal(i, 256) if isinstance(i, int) else i
+        return If(item < self.size, self.data[item], symbol_factory.BitVecVal(0, 8))
+
+    def word(self, offset: int) -> BitVec:
+        return Concat([self.load(offset + k) for k in range(32)])
+
+
+def selector_is(cd: Calldata, selector: int) -> smt.Bool:
+    return Extract(255, 224, cd.word(0)) == symbol_factory.BitVecVal(selector, 32)
+
+
+def sender_is_actor(sender: BitVec) -> smt.Bool:
+    return Or(*[sender == symbol_factory.BitVecVal(a, 256) for a in (CREATOR, ATTACKER, SOMEGUY)])
+
+
+class KeccakManager:
+    """keccak_function_manager.py:24-149 restated over the test term API."""
+
+    def __init__(self):
+        self.store = {}
+        self.hooks = {}
+        self.counter = TOTAL_PARTS - 34534
+        self.concrete = []  # (data term, hash term)
+
+    def functions(self, length: int):
+        if length not in self.store:
+            self.store[length] = (Function("keccak256_%d" % length, length, 256),
+                                  Function("keccak256_%d-1" % length, 256, length))
+        return self.store[length]
+
+    def create(self, data: BitVec):
+        length = data.size()
+        f, inv = self.functions(length)
+        if data.value is not None:
+            h = int.from_bytes(keccak256(data.value.to_bytes(length // 8, "big")), "big")
+            hv = symbol_factory.BitVecVal(h, 256)
+            self.concrete.append((data, hv))
+            return hv, And(f(data) == hv, inv(f(data)) == data)
+        if length not in self.hooks:
+            self.hooks[length] = self.counter
+            self.counter -= INTERVAL_DIFFERENCE
+        lo = self.hooks[length] * PART
+        hi = lo + PART
+        cond = And(inv(f(data)) == data,
+                   ULE(symbol_factory.BitVecVal(lo, 256), f(data)),
+                   ULT(f(data), symbol_factory.BitVecVal(hi, 256)),
+                   URem(f(data), symbol_factory.BitVecVal(64, 256)) == 0)
+        conc = symbol_factory.Bool(False)
+        for key, hv in self.concrete:
+            if key.size() == length:
+                conc = Or(conc, And(f(data) == hv, key == data))
+        return f(data), And(inv(f(data)) == data, Or(cond, conc))
+
+
+def mapping_slot(km: KeccakManager, key: BitVec, slot: int):
+    """keccak256(key . slot): the storage slot of mapping[key] (Solidity layout)."""
+    return km.create(Concat(key, symbol_factory.BitVecVal(slot, 256)))
+
+
+def queries():
+    """A list of (name, [constraints]) LASER-shaped feasibility queries, most of them SAT."""
+    out = []
+    ctx = smt.Context()
+    smt.set_context(ctx)
+    cd = Calldata("1")
+    sender = symbol_factory.BitVecSym("sender_1", 256)
+    value = symbol_factory.BitVecSym("call_value1", 256)
+    balance = Array("balance", 256, 256)
+    storage = Array("Storage0x901d12ebe1b195e5aa8748e62bd7734ae19b51f", 256, 256)
+    out.append(("selector", [selector_is(cd, 0x9FA299CC), sender_is_actor(sender)]))
+    out.append(("selector_size", [selector_is(cd, 0x13AF4035),
+                                  UGE(cd.size, symbol_factory.BitVecVal(36, 256)),
+                                  ULT(cd.size, symbol_factory.BitVecVal(5000, 256))]))
+    out.append(("owner_check", [sender_is_actor(sender), storage[symbol_factory.BitVecVal(0, 256)]
+                                == sender, Not(sender == symbol_factory.BitVecVal(CREATOR, 256))]))
+    out.append(("balance", [sender_is_actor(sender), UGE(balance[sender], value),
+                            Not(value == symbol_factory.BitVecVal(0, 256))]))
+    arg = Extract(159, 0, cd.word(4))
+    out.append(("address_arg", [selector_is(cd, 0x9FA299CC),
+                                arg == Extract(159, 0, sender)]))
+    x = cd.word(4)
+    y = cd.word(36)
+    out.append(("overflow", [selector_is(cd, 0xA9059CBB),
+                             Not(smt.BVAddNoOverflow(x, y, False))]))
+    out.append(("mul_overflow", [Not(smt.BVMulNoOverflow(x, symbol_factory.BitVecVal(3, 256),
+                                                          False))]))
+    km = KeccakManager()
+    h_c, cond_c = mapping_slot(km, symbol_factory.BitVecVal(CREATOR, 256), 1)
+    h_s, cond_s = mapping_slot(km, sender, 1)
+    out.append(("keccak_mapping", [cond_c, cond_s, sender_is_actor(sender),
+                                   storage[h_s] == symbol_factory.BitVecVal(7, 256)]))
+    out.append(("keccak_alias", [cond_c, cond_s, h_s == h_c]))
+    st = K(256, 256, 0)
+    st[symbol_factory.BitVecVal(0, 256)] = sender
+    st[cd.word(4)] = value
+    out.append(("k_storage", [st[symbol_factory.BitVecVal(0, 256)] == symbol_factory.BitVecVal(
+        ATTACKER, 256), sender_is_actor(sender)]))
+    out.append(("unsat_actor", [sender_is_actor(sender), sender == symbol_factory.BitVecVal(5,
+                                                                                            256)]))
+    return ctx, out

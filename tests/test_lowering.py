@@ -1,0 +1,146 @@
+"""Lowering of arrays / uninterpreted functions (mythril_amd/lower.py) against the term oracle.
+
+The property that makes a sieve witness a model: for every candidate row, the lowered
+(column-only) tape evaluates to the same Bool as the ORIGINAL query (arrays, stores, keccak UFs
+and their inverses) evaluated by oracle/term_eval.py under the model the row denotes — array
+tables from the cell/else columns, ``keccak256_N`` as the concrete pairs plus
+``H(x) = base + ((keccak(x) >> 139) << 6)``, ``keccak256_N-1`` as the true inverse of the values
+the forward function produced.  Shapes come from tests/laser_like.py (LASER's constructions).
+"""
+import random
+
+import pytest
+
+from mythril_amd.candidates import build_guide
+from mythril_amd.lower import KECCAK_ALIGN, KECCAK_SHIFT, LoweringUnsupported, lower_query
+from mythril_amd.smt import And
+from mythril_amd.tape import HOST_ONLY, Op
+from oracle import smt_eval as E
+from oracle.guided_gen import generate_row
+from oracle.keccak import keccak256
+from oracle.term_eval import evaluate_term
+from tests.laser_like import PART, queries
+
+
+def model_of(schema, row):
+    """The z3-style model a row of columns denotes (restated from lower.py's docstring)."""
+    cols = schema.columns
+    vars_ = {c.name: row[c.name] for c in cols.values() if c.kind == "var"}
+    arrays = {}
+    for arr, cells in schema.cells.items():
+        tab = {k: row[n] for k, n in cells.items()}
+        arrays[arr] = (tab, row.get("%s[*]" % arr, 0))
+    funcs = {}
+    for f, km in schema.keccak.items():
+        inv = {}
+
+        def fwd(x, km=km, inv=inv, width=None):
+            if x in km.pairs:
+                y = km.pairs[x]
+            else:
+                nbytes = fwd.width // 8
+                h = int.from_bytes(keccak256(x.to_bytes(nbytes, "big")), "big")
+                y = (km.base + ((h >> KECCAK_SHIFT) << KECCAK_ALIGN)) % (1 << 256)
+            inv[y] = x
+            return y
+
+        fwd.width = int(f.split("_")[1])
+        funcs[f] = fwd
+        funcs[f + "-1"] = (lambda y, inv=inv: inv.get(y, 0))
+    for f, cells in schema.uf_cells.items():
+        tab = {k: row[n] for k, n in cells.items()}
+        dflt = row.get("%s[*]" % f, 0)
+        funcs[f] = (lambda x, tab=tab, dflt=dflt: tab.get(x, dflt))
+    return vars_, arrays, funcs
+
+
+def candidate_values(ctx, width, rng):
+    pool = ctx.b.pool.values
+    m = (1 << width) - 1
+    pick = rng.random()
+    if pick < 0.2:
+        return rng.randrange(0, 256) & m
+    if pick < 0.4:
+        return rng.getrandbits(width)
+    v = rng.choice(pool)
+    if width == 8:
+        return (v >> (8 * rng.randrange(0, 32))) & 0xFF
+    return (v + rng.choice((0, 0, 1, -1))) & m
+
+
+@pytest.mark.parametrize("qi", range(11))
+def test_lowered_tape_matches_term_semantics(qi):
+    ctx, qs = queries()
+    name, cs = qs[qi]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    tape = ctx.b.finish(root)
+    assert not any(int(o) in HOST_ONLY for o in tape.nodes["op"]), name
+    orig = ctx.b.finish(And(*cs).node)
+    var_names = [n for n, _ in sorted(ctx.b.var_index.items(), key=lambda kv: kv[1])]
+    rng = random.Random(1234 + qi)
+    cols = list(schema.columns)
+    guide = build_guide(ctx.b, root, schema, cols).arrays()
+    outcomes = []
+    for trial in range(160):
+        if trial % 2:  # rows of the guided generator (oracle restatement), mostly SAT
+            row = dict(zip(cols, generate_row(99 + qi, trial, guide)))
+        else:
+            row = {c.name: candidate_values(ctx, c.width, rng) for c in schema.columns.values()}
+        assign = [row.get(n, 0) for n in var_names]
+        low = E.evaluate(tape.nodes, ctx.b.pool.values, assign)
+        vars_, arrays, funcs = model_of(schema, row)
+        want = evaluate_term(orig.nodes, ctx.b.pool.values, var_names,
+                             ctx.b.symbols.array_names, ctx.b.symbols.function_names,
+                             vars_, arrays, funcs)
+        assert bool(low) == bool(want), (name, trial, row)
+        outcomes.append(bool(low))
+    if name == "unsat_actor":
+        assert not any(outcomes)
+    else:  # the harvested guide finds witnesses of every SAT shape
+        assert sum(outcomes) >= 5, (name, sum(outcomes))
+
+
+def test_keccak_base_is_inside_the_interval():
+    ctx, qs = queries()
+    cs = dict(qs)["keccak_mapping"]
+    _, schema = ctx.query(*cs)
+    km = schema.keccak["keccak256_512"]
+    lo = (10 ** 40 - 34534) * PART
+    assert km.base % 64 == 0 and lo <= km.base < lo + 64
+    assert km.base + (1 << 123) < lo + PART
+    assert len(km.pairs) == 1
+
+
+def test_calldata_cells_and_else_columns():
+    ctx, qs = queries()
+    _, schema = ctx.query(*dict(qs)["selector_size"])
+    cells = schema.cells["1_calldata"]
+    assert sorted(cells) == list(range(32))  # word(0): 32 constant offsets
+    kinds = {c.kind for c in schema.columns.values()}
+    assert kinds == {"var", "cell"}
+
+
+def test_symbolic_index_reads_else_and_cells():
+    from mythril_amd import smt
+    from mythril_amd.smt import Array, symbol_factory
+
+    ctx = smt.set_context(smt.Context())
+    a = Array("A", 256, 256)
+    i = symbol_factory.BitVecSym("i", 256)
+    c1 = a[symbol_factory.BitVecVal(3, 256)] == symbol_factory.BitVecVal(9, 256)
+    c2 = a[i] == symbol_factory.BitVecVal(5, 256)
+    tape, schema = ctx.query(c1, c2)
+    assert set(schema.columns) == {"A[0x3]", "A[*]", "i"}
+    ops = [Op(int(o)) for o in tape.nodes["op"]]
+    assert Op.ITE in ops
+
+
+def test_inverse_of_something_else_is_unsupported():
+    from mythril_amd import smt
+    from mythril_amd.smt import Function, symbol_factory
+
+    ctx = smt.set_context(smt.Context())
+    inv = Function("keccak256_256-1", 256, 256)
+    y = symbol_factory.BitVecSym("y", 256)
+    with pytest.raises(LoweringUnsupported):
+        ctx.query(inv(y) == y)
