@@ -136,6 +136,36 @@ int32_t mh_assign_generate(mh_assign* as, uint64_t seed, uint64_t global_base);
 /* Host reference of the generator (same bits as the device kernel).                             */
 uint32_t mh_gen_limb(uint64_t seed, uint32_t var, uint64_t index, uint32_t limb);
 
+/* Guided candidates for one query (mythril_amd/candidates.py harvests the guide from the query's
+ * terms; SURVEY.md §8f "candidate generation").  Row r in [first, first+count) gets global index
+ * g = global_base + r and, for column v < n_cols (width w_v, value pool P_v):
+ *     m0 = mh_gen_limb(seed ^ 0x6A09E667F3BCC909, v, g, 0), m1 = the same with limb 1;
+ *     (m0 & 0xff) <  64               -> (m0 >> 8) & 0xff                        small
+ *     (m0 & 0xff) < 128 or P_v empty  -> limbs mh_gen_limb(seed, v, g, k)        uniform
+ *     otherwise                       -> P_v[m1 % |P_v|]                         pool
+ * masked to w_v bits.  Then, for each set j in order, with s = mh_gen_limb(seed ^
+ * 0xBB67AE8584CAA73B, j, g, 0): if (s & 0xff) < set_prob[j] and the set has alternatives,
+ * alternative set_off[j] + (s >> 8) % n_alt is applied: each of its entries writes its value
+ * (masked) into column entry_col, or, when entry_col has bit 31 set (MH_GUIDE_COPY), copies bits
+ * [src_lo, src_lo + nbits) of column src into bits [dst_lo, dst_lo + nbits) of the destination,
+ * with entry_val limbs = {src, dst_lo, src_lo, nbits, 0, 0, 0, 0}.  Later sets override earlier
+ * ones.  Columns n_cols.. of the buffer are left untouched.                                     */
+#define MH_GUIDE_COPY 0x80000000u
+typedef struct mh_guide {
+    uint32_t n_cols;             /* columns generated (<= the buffer's n_vars)                   */
+    const uint16_t* col_width;   /* [n_cols] 1..256                                              */
+    const uint32_t* pool_off;    /* [n_cols + 1] value ranges of `pool`                          */
+    const uint32_t* pool;        /* [pool_off[n_cols]] x 8 limbs                                 */
+    uint32_t n_sets;
+    const uint8_t* set_prob;     /* [n_sets] probability in 1/256                                */
+    const uint32_t* set_off;     /* [n_sets + 1] alternative ranges                              */
+    const uint32_t* alt_off;     /* [set_off[n_sets] + 1] entry ranges                           */
+    const uint32_t* entry_col;   /* [alt_off[set_off[n_sets]]] column, or MH_GUIDE_COPY | dst    */
+    const uint32_t* entry_val;   /* x 8 limbs                                                    */
+} mh_guide;
+int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_base,
+                                  uint64_t first, uint64_t count, const mh_guide* guide);
+
 /* ---- evaluation ------------------------------------------------------------------------------ */
 /* Evaluate tapes [tape_first, tape_first+tape_count) over assignment rows [row_first,
  * row_first+row_count) of `as`.  Results are indexed by tape - tape_first and hold GLOBAL indices

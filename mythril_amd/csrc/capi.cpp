@@ -46,6 +46,9 @@ struct mh_assign {
     uint32_t n_vars = 0;
     uint64_t capacity = 0;
     uint32_t* d = nullptr;
+    uint32_t* d_guide = nullptr;   // packed mh_guide (grow-only)
+    size_t guide_words = 0;
+    std::vector<uint32_t> h_guide; // host staging of the packed guide
 };
 
 namespace {
@@ -315,6 +318,7 @@ int32_t mh_assign_destroy(mh_assign* as) {
     if (!as) return MH_OK;
     (void)hipSetDevice(as->ctx->device);
     if (as->d) (void)hipFree(as->d);
+    if (as->d_guide) (void)hipFree(as->d_guide);
     delete as;
     return MH_OK;
 }
@@ -351,6 +355,96 @@ int32_t mh_assign_generate(mh_assign* as, uint64_t seed, uint64_t global_base) {
     if (int32_t r = use_device(as->ctx)) return r;
     MH_HIP(mh::launch_generate(as->d, as->capacity, as->n_vars, seed, global_base,
                                as->ctx->stream));
+    return MH_OK;
+}
+
+int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_base,
+                                  uint64_t first, uint64_t count, const mh_guide* g) {
+    if (!as || !g) return set_err(MH_E_INVALID, "null argument");
+    if (first > as->capacity || count > as->capacity - first)
+        return set_err(MH_E_INVALID, "row range out of bounds");
+    if (g->n_cols > as->n_vars) return set_err(MH_E_INVALID, "guide has more columns than the buffer");
+    if (g->n_cols && (!g->col_width || !g->pool_off))
+        return set_err(MH_E_INVALID, "guide: null column arrays");
+    if (g->n_sets && (!g->set_prob || !g->set_off || !g->alt_off))
+        return set_err(MH_E_INVALID, "guide: null set arrays");
+    // validate every offset and entry on the host: the kernel trusts them
+    const uint32_t nc = g->n_cols, ns = g->n_sets;
+    if (nc && g->pool_off[0] != 0) return set_err(MH_E_INVALID, "guide: pool_off[0] != 0");
+    for (uint32_t v = 0; v < nc; ++v) {
+        if (g->col_width[v] < 1 || g->col_width[v] > 256)
+            return set_err(MH_E_INVALID, "guide: column width outside 1..256");
+        if (g->pool_off[v + 1] < g->pool_off[v])
+            return set_err(MH_E_INVALID, "guide: pool_off not monotone");
+    }
+    const uint32_t n_pool = nc ? g->pool_off[nc] : 0;
+    if (n_pool && !g->pool) return set_err(MH_E_INVALID, "guide: null pool");
+    const uint32_t n_alts = ns ? g->set_off[ns] : 0;
+    if (ns && g->set_off[0] != 0) return set_err(MH_E_INVALID, "guide: set_off[0] != 0");
+    for (uint32_t j = 0; j < ns; ++j)
+        if (g->set_off[j + 1] < g->set_off[j])
+            return set_err(MH_E_INVALID, "guide: set_off not monotone");
+    if (ns && g->alt_off[0] != 0) return set_err(MH_E_INVALID, "guide: alt_off[0] != 0");
+    for (uint32_t a = 0; a < n_alts; ++a)
+        if (g->alt_off[a + 1] < g->alt_off[a])
+            return set_err(MH_E_INVALID, "guide: alt_off not monotone");
+    const uint32_t n_ent = ns ? g->alt_off[n_alts] : 0;
+    if (n_ent && (!g->entry_col || !g->entry_val))
+        return set_err(MH_E_INVALID, "guide: null entry arrays");
+    for (uint32_t e = 0; e < n_ent; ++e) {
+        const uint32_t c = g->entry_col[e];
+        const uint32_t dst = c & ~MH_GUIDE_COPY;
+        if (dst >= nc) return set_err(MH_E_INVALID, "guide: entry column out of range");
+        if (c & MH_GUIDE_COPY) {
+            const uint32_t* ev = g->entry_val + (size_t)e * 8;
+            if (ev[0] >= nc || ev[3] < 1 || ev[3] > 256 || ev[1] >= 256 || ev[2] >= 256)
+                return set_err(MH_E_INVALID, "guide: malformed copy entry");
+        }
+    }
+    if (int32_t r = use_device(as->ctx)) return r;
+    // pack: width | pool_off | pool | set_prob | set_off | alt_off | entry_col | entry_val
+    const size_t o_width = 0, o_poff = o_width + nc, o_pool = o_poff + nc + 1,
+                 o_prob = o_pool + (size_t)n_pool * 8, o_soff = o_prob + ns,
+                 o_aoff = o_soff + ns + 1, o_ecol = o_aoff + n_alts + 1,
+                 o_eval = o_ecol + n_ent, words = o_eval + (size_t)n_ent * 8;
+    std::vector<uint32_t>& h = as->h_guide;
+    h.assign(words, 0);
+    for (uint32_t v = 0; v < nc; ++v) h[o_width + v] = g->col_width[v];
+    if (nc) std::copy(g->pool_off, g->pool_off + nc + 1, h.begin() + o_poff);
+    if (n_pool) std::copy(g->pool, g->pool + (size_t)n_pool * 8, h.begin() + o_pool);
+    for (uint32_t j = 0; j < ns; ++j) h[o_prob + j] = g->set_prob[j];
+    if (ns) {
+        std::copy(g->set_off, g->set_off + ns + 1, h.begin() + o_soff);
+        std::copy(g->alt_off, g->alt_off + n_alts + 1, h.begin() + o_aoff);
+    }
+    if (n_ent) {
+        std::copy(g->entry_col, g->entry_col + n_ent, h.begin() + o_ecol);
+        std::copy(g->entry_val, g->entry_val + (size_t)n_ent * 8, h.begin() + o_eval);
+    }
+    if (words > as->guide_words) {
+        if (as->d_guide) MH_HIP(hipFree(as->d_guide));
+        as->d_guide = nullptr;
+        as->guide_words = 0;
+        MH_HIP(hipMalloc(&as->d_guide, words * sizeof(uint32_t)));
+        as->guide_words = words;
+    }
+    MH_HIP(hipMemcpyAsync(as->d_guide, h.data(), words * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          as->ctx->stream));
+    mh::KGuide k;
+    k.n_cols = nc;
+    k.n_sets = ns;
+    k.width = as->d_guide + o_width;
+    k.pool_off = as->d_guide + o_poff;
+    k.pool = as->d_guide + o_pool;
+    k.set_prob = as->d_guide + o_prob;
+    k.set_off = as->d_guide + o_soff;
+    k.alt_off = as->d_guide + o_aoff;
+    k.entry_col = as->d_guide + o_ecol;
+    k.entry_val = as->d_guide + o_eval;
+    MH_HIP(mh::launch_generate_guided(as->d, as->capacity, first, count, seed, global_base, k,
+                                      as->ctx->stream));
+    // the staging vector is reused by the next call: finish the copy first
+    MH_HIP(hipStreamSynchronize(as->ctx->stream));
     return MH_OK;
 }
 

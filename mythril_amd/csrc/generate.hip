@@ -1,0 +1,143 @@
+// Guided candidate generator (mh_assign_generate_guided): one thread per assignment row, SoA
+// writes (column v limb k of row r at word (v*8 + k)*capacity + r), so a wave's 64 lanes store
+// 256 contiguous bytes per limb.  The semantics are stated in include/mythril_hip.h and restated
+// bit for bit in oracle/guided_gen.py; the harvest that fills the guide is
+// mythril_amd/candidates.py.  Off the hot path: written once per query, before the sieve reads it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace {
+
+using u32 = uint32_t;
+using u64 = uint64_t;
+
+constexpr int kBlock = 256;
+constexpr u64 kSaltMode = 0x6A09E667F3BCC909ull;
+constexpr u64 kSaltSet = 0xBB67AE8584CAA73Bull;
+constexpr u32 kCopy = 0x80000000u;
+
+__device__ __forceinline__ u64 splitmix64(u64 x) {
+    x += 0x9E3779B97F4A7C15ull;
+    u64 z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// mh_gen_limb on the device
+__device__ __forceinline__ u32 gen_limb(u64 seed, u32 var, u64 index, u32 limb) {
+    const u64 key = splitmix64(seed ^ (((u64)var * 8 + limb) * 0xD1B54A32D192ED03ull));
+    return (u32)splitmix64(key ^ index);
+}
+
+__device__ __forceinline__ u32 limb_mask(u32 width, u32 k) {
+    const u32 lo = 32 * k;
+    if (width >= lo + 32) return 0xFFFFFFFFu;
+    if (width <= lo) return 0u;
+    return (1u << (width - lo)) - 1u;
+}
+
+// bits [lo, lo + n) of an 8-limb value, as a (right-aligned) 8-limb value
+__device__ void extract_bits(const u32* v, u32 lo, u32 n, u32* out) {
+    const u32 q = lo >> 5, r = lo & 31;
+#pragma unroll
+    for (u32 k = 0; k < 8; ++k) {
+        const u32 a = (q + k < 8) ? v[q + k] : 0u;
+        const u32 b = (q + k + 1 < 8) ? v[q + k + 1] : 0u;
+        out[k] = r ? ((a >> r) | (b << (32 - r))) : a;
+    }
+#pragma unroll
+    for (u32 k = 0; k < 8; ++k) out[k] &= limb_mask(n, k);
+}
+
+__global__ void __launch_bounds__(kBlock)
+    guided_kernel(u32* assign, u64 capacity, u64 first, u64 count, u64 seed, u64 base,
+                  mh::KGuide g) {
+    const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= count) return;
+    const u64 row = first + i;
+    const u64 gidx = base + row;
+    for (u32 v = 0; v < g.n_cols; ++v) {
+        const u32 w = g.width[v];
+        const u32 m0 = gen_limb(seed ^ kSaltMode, v, gidx, 0);
+        const u32 mode = m0 & 0xFFu;
+        const u32 plo = g.pool_off[v], phi = g.pool_off[v + 1];
+        u32 val[8];
+        if (mode < 64) {
+            val[0] = (m0 >> 8) & 0xFFu;
+#pragma unroll
+            for (u32 k = 1; k < 8; ++k) val[k] = 0;
+        } else if (mode < 128 || phi == plo) {
+#pragma unroll
+            for (u32 k = 0; k < 8; ++k) val[k] = gen_limb(seed, v, gidx, k);
+        } else {
+            const u32 m1 = gen_limb(seed ^ kSaltMode, v, gidx, 1);
+            const u32* src = g.pool + (u64)(plo + m1 % (phi - plo)) * 8;
+#pragma unroll
+            for (u32 k = 0; k < 8; ++k) val[k] = src[k];
+        }
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k)
+            assign[((u64)v * 8 + k) * capacity + row] = val[k] & limb_mask(w, k);
+    }
+    for (u32 j = 0; j < g.n_sets; ++j) {
+        const u32 s = gen_limb(seed ^ kSaltSet, j, gidx, 0);
+        const u32 a0 = g.set_off[j], n_alt = g.set_off[j + 1] - a0;
+        if ((s & 0xFFu) >= g.set_prob[j] || n_alt == 0) continue;
+        const u32 alt = a0 + (s >> 8) % n_alt;
+        for (u32 e = g.alt_off[alt]; e < g.alt_off[alt + 1]; ++e) {
+            const u32 c = g.entry_col[e];
+            const u32* ev = g.entry_val + (u64)e * 8;
+            if (c & kCopy) {
+                const u32 dst = c & ~kCopy, src = ev[0], dlo = ev[1], slo = ev[2], nb = ev[3];
+                u32 sv[8], bits[8], dv[8], m[8], one[8];
+#pragma unroll
+                for (u32 k = 0; k < 8; ++k) {
+                    sv[k] = assign[((u64)src * 8 + k) * capacity + row];
+                    dv[k] = assign[((u64)dst * 8 + k) * capacity + row];
+                }
+                extract_bits(sv, slo, nb, bits);
+                // shift bits and an nb-wide mask left by dlo
+#pragma unroll
+                for (u32 k = 0; k < 8; ++k) one[k] = limb_mask(nb, k);
+                const u32 q = dlo >> 5, r = dlo & 31;
+#pragma unroll
+                for (int k = 7; k >= 0; --k) {
+                    const int s0 = k - (int)q, s1 = k - (int)q - 1;
+                    const u32 ba = s0 >= 0 ? bits[s0] : 0u, bb = s1 >= 0 ? bits[s1] : 0u;
+                    const u32 ma = s0 >= 0 ? one[s0] : 0u, mb = s1 >= 0 ? one[s1] : 0u;
+                    sv[k] = r ? ((ba << r) | (bb >> (32 - r))) : ba;
+                    m[k] = r ? ((ma << r) | (mb >> (32 - r))) : ma;
+                }
+                const u32 w = g.width[dst];
+#pragma unroll
+                for (u32 k = 0; k < 8; ++k)
+                    assign[((u64)dst * 8 + k) * capacity + row] =
+                        ((dv[k] & ~m[k]) | (sv[k] & m[k])) & limb_mask(w, k);
+            } else {
+                const u32 w = g.width[c];
+#pragma unroll
+                for (u32 k = 0; k < 8; ++k)
+                    assign[((u64)c * 8 + k) * capacity + row] = ev[k] & limb_mask(w, k);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+namespace mh {
+
+hipError_t launch_generate_guided(uint32_t* assign, uint64_t capacity, uint64_t first,
+                                  uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
+                                  hipStream_t stream) {
+    const u64 blocks = (count + kBlock - 1) / kBlock;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(guided_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, assign,
+                       capacity, first, count, seed, base, g);
+    return hipGetLastError();
+}
+
+}  // namespace mh

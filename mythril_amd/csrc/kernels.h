@@ -40,6 +40,21 @@ constexpr uint32_t kNumVariants = 9;
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream);
 hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars, uint64_t seed,
                            uint64_t base, hipStream_t stream);
+// Device form of mh_guide (pointers into one device buffer owned by the mh_assign).
+struct KGuide {
+    uint32_t n_cols, n_sets;
+    const uint32_t* width;      // [n_cols]
+    const uint32_t* pool_off;   // [n_cols + 1]
+    const uint32_t* pool;       // x 8 limbs
+    const uint32_t* set_prob;   // [n_sets]
+    const uint32_t* set_off;    // [n_sets + 1]
+    const uint32_t* alt_off;    // [n_alts + 1]
+    const uint32_t* entry_col;  // [n_entries]
+    const uint32_t* entry_val;  // x 8 limbs
+};
+hipError_t launch_generate_guided(uint32_t* assign, uint64_t capacity, uint64_t first,
+                                  uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
+                                  hipStream_t stream);
 hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uint32_t* sink,
                              hipStream_t stream);
 

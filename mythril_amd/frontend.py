@@ -1,0 +1,179 @@
+"""Solver front end: ``get_model`` with the reference's signature and semantics, sieve first.
+
+Mirrors mythril/support/model.py:15-62 line for line in behaviour —
+
+* ``lru_cache(maxsize=2**23)`` keyed on (constraints, minimize, maximize,
+  enforce_execution_time); UNSAT raises, so it is never cached;
+* time budget: ``min(args.solver_timeout, time_handler.time_remaining() - 500)``, and
+  ``UnsatError`` when it is not positive (only with ``enforce_execution_time``);
+* a Python ``False`` among the constraints raises ``UnsatError``; Python bools are dropped;
+* ``args.solver_log``: the query is written as SMT-LIB2 to ``<dir>/<abs(hash(...))>.smt2``
+  before solving (smtlib.py prints it);
+* sat -> a ``Model``; unknown / unsat -> ``UnsatError``
+
+— with one change: when there is nothing to optimise (``minimize == maximize == ()``, the
+feasibility case of ``Constraints.is_possible`` and the detection modules), the
+query first goes to the sieve (sieve.py).  A witness comes back as a sieve ``Model``, re-verified
+by the configured verifier (z3 when the reference runs around this module, plugin.py).  A miss,
+an unsupported term, a device error or a failed verification hands the query, unchanged, to the
+fallback solver — the reference's own ``get_model`` when installed by the plugin.  With no
+fallback configured a miss is reported the way the reference reports a z3 ``unknown``:
+``UnsatError``.  Queries with objectives always go to the fallback (transaction sequences in
+reports must stay z3 Optimize output, analysis/solver.py:48-96).
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from functools import lru_cache
+from pathlib import Path
+from typing import Callable, Optional
+
+from .support import SolverStatistics, UnsatError, args, time_handler
+
+log = logging.getLogger(__name__)
+
+_tls = threading.local()
+_config = {
+    "fallback": None,   # callable(constraints, minimize, maximize, enforce_execution_time)
+    "verify": None,     # callable(constraints, model) -> bool (z3 re-verification)
+    "to_terms": None,   # callable(constraints) -> (smt.Context, [Bool]) for foreign terms
+    "sieve_kwargs": {},
+    "enabled": True,
+}
+
+
+def configure(*, fallback: Optional[Callable] = None, verify: Optional[Callable] = None,
+              to_terms: Optional[Callable] = None, enabled: Optional[bool] = None,
+              **sieve_kwargs) -> None:
+    """Set the fallback solver, the witness verifier, the term importer and sieve options."""
+    if fallback is not None:
+        _config["fallback"] = fallback
+    if verify is not None:
+        _config["verify"] = verify
+    if to_terms is not None:
+        _config["to_terms"] = to_terms
+    if enabled is not None:
+        _config["enabled"] = enabled
+    if sieve_kwargs:
+        _config["sieve_kwargs"] = dict(sieve_kwargs)
+        close_sieve()
+    get_model.cache_clear()
+
+
+def reset() -> None:
+    """Back to defaults (tests, plugin stop)."""
+    _config.update(fallback=None, verify=None, to_terms=None, sieve_kwargs={}, enabled=True)
+    close_sieve()
+    get_model.cache_clear()
+
+
+def sieve():
+    """This thread's sieve (device context + buffers), created on first use."""
+    s = getattr(_tls, "sieve", None)
+    if s is None:
+        from .sieve import Sieve
+
+        s = _tls.sieve = Sieve(**_config["sieve_kwargs"])
+    return s
+
+
+def close_sieve() -> None:
+    s = getattr(_tls, "sieve", None)
+    if s is not None:
+        s.close()
+        _tls.sieve = None
+
+
+def _log_query(constraints, minimize, maximize) -> None:
+    from .smtlib import to_smtlib
+
+    Path(args.solver_log).mkdir(parents=True, exist_ok=True)
+    key = tuple(list(constraints) + list(minimize) + list(maximize)
+                + [len(constraints), len(minimize), len(maximize)])
+    with open(args.solver_log + "/%d.smt2" % abs(hash(key)), "w") as f:
+        f.write(to_smtlib(constraints, minimize, maximize))
+
+
+def _terms(constraints):
+    """(smt.Context, [Bool]) for the constraints: ours as they are, foreign ones imported."""
+    from . import smt
+
+    if all(isinstance(c, smt.Bool) for c in constraints):
+        ctx = constraints[0].ctx if constraints else smt.context()
+        if any(c.ctx is not ctx for c in constraints):
+            raise ValueError("constraints from different term contexts")
+        return ctx, list(constraints)
+    conv = _config["to_terms"]
+    if conv is None:
+        raise TypeError("no importer for constraints of type %s"
+                        % type(constraints[0]).__name__)
+    return conv(constraints)
+
+
+def sieve_model(constraints):
+    """The sieve's answer for a feasibility query: a Model, or None (ask the fallback)."""
+    from .model import Model
+
+    stats = SolverStatistics()
+    try:
+        ctx, terms = _terms(constraints)
+        s = sieve()
+        key = tuple(t.node for t in terms)
+        w = s.solve(ctx.b, [t.node for t in terms], key=key)
+    except Exception as e:  # fail closed: any problem means "ask the fallback"
+        from .lower import LoweringUnsupported
+        from .native import Unsupported
+
+        if isinstance(e, (LoweringUnsupported, Unsupported)):
+            stats.sieve_unsupported += 1
+        else:
+            stats.sieve_errors += 1
+            log.debug("sieve error: %s", e)
+        return None
+    if w is None:
+        stats.sieve_misses += 1
+        return None
+    m = Model(s, ctx, w.schema, w.values, w.index)
+    verify = _config["verify"]
+    if verify is not None and not verify(constraints, m):
+        stats.sieve_rejected += 1
+        return None
+    stats.sieve_hits += 1
+    return m
+
+
+@lru_cache(maxsize=2 ** 23)
+def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True):
+    """support/model.py:15-62 with the sieve in front of the solver (module docstring)."""
+    timeout = args.solver_timeout
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+        if timeout <= 0:
+            raise UnsatError
+    for constraint in constraints:
+        if type(constraint) == bool and not constraint:
+            raise UnsatError
+    constraints = [c for c in constraints if type(c) != bool]
+    if args.solver_log:
+        _log_query(constraints, minimize, maximize)
+    stats = SolverStatistics()
+    if _config["enabled"] and not minimize and not maximize:
+        t0 = time.perf_counter()
+        m = sieve_model(constraints)
+        if stats.enabled:
+            stats.sieve_time += time.perf_counter() - t0
+        if m is not None:
+            return m
+    fallback = _config["fallback"]
+    if fallback is None:
+        log.debug("sieve found no witness and no fallback solver is configured")
+        raise UnsatError
+    t0 = time.perf_counter()
+    try:
+        return fallback(tuple(constraints), minimize, maximize, enforce_execution_time)
+    finally:
+        if stats.enabled:
+            stats.query_count += 1
+            stats.solver_time += time.perf_counter() - t0

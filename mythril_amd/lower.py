@@ -190,8 +190,8 @@ class Lowering:
     def _column(self, name: str, width: int, kind: str, symbol: str,
                 key: Optional[int] = None) -> int:
         if name not in self.schema.columns:
-            if self.frozen and kind != "var":
-                raise LoweringUnsupported("column %s is not in the frozen schema" % name)
+            # frozen (Model.eval): no new cells are ever made (constant keys outside the table
+            # read the else column); a new else / variable column reads 0 (model completion)
             self.schema.columns[name] = Column(name, width, kind, symbol, key)
         return self.b.var(name, width)
 
@@ -261,9 +261,72 @@ class Lowering:
         if k == 0:
             return n
         args = [memo[x] for x in (a, bb, c)[:k]]
+        if op == Op.EQ and b.widths[args[0]] > 256:
+            return self.eq(args[0], args[1])
         if args == [a, bb, c][:k]:
             return n
         return b.op(Op(op), *args, imm0=i0, imm1=i1)
+
+    # -- wide equalities: the device compares at most 256 bits ---------------------------------
+    def _pieces(self, n: int) -> List[int]:
+        """Leaves of the CONCAT tree of n, most significant first (ZEXT = zeros ++ x)."""
+        b = self.b
+        out, stack = [], [n]
+        while stack:
+            x = stack.pop()
+            op, w, a, bb, _, i0, _ = b.nodes[x]
+            if op == Op.CONCAT:
+                stack += [bb, a]
+            elif op == Op.ZEXT:
+                stack += [a, b.const(0, i0) if i0 <= 256 else self._zeros(i0)]
+            elif w > 256 and b.const_value(x) is None:
+                raise LoweringUnsupported("%d-bit %s operand of a wide equality"
+                                          % (w, Op(op).name))
+            else:
+                out.append(x)
+        return out
+
+    def _zeros(self, w: int) -> int:
+        return self.b.const(0, w)
+
+    def _slice(self, piece: int, hi: int, lo: int) -> int:
+        """Bits [lo, hi) of a <= 256-bit piece (constants sliced on the host)."""
+        b = self.b
+        w = b.widths[piece]
+        if lo == 0 and hi == w:
+            return piece
+        cv = b.const_value(piece)
+        if cv is not None:
+            return b.const((cv >> lo) & ((1 << (hi - lo)) - 1), hi - lo)
+        return b.op(Op.EXTRACT, piece, imm0=hi - 1, imm1=lo)
+
+    def eq(self, x: int, y: int) -> int:
+        """x == y for bit-vectors of any width: an AND of <= 256-bit equalities over the common
+        refinement of the two sides' concat boundaries."""
+        b = self.b
+        w = b.widths[x]
+        if w <= 256:
+            return b.op(Op.EQ, x, y)
+        sides = []
+        for t in (x, y):
+            pos, segs = w, []
+            for p in self._pieces(t):
+                pw = b.widths[p]
+                segs.append((pos - pw, pos, p))
+                pos -= pw
+            sides.append(segs)
+        cuts = sorted({lo for s in sides for lo, _, _ in s} | {w})
+        acc = None
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            parts = []
+            for segs in sides:
+                for plo, phi, p in segs:
+                    if plo <= lo and hi <= phi:
+                        parts.append(self._slice(p, hi - plo, lo - plo))
+                        break
+            e = b.op(Op.EQ, parts[0], parts[1])
+            acc = e if acc is None else b.op(Op.AND, acc, e)
+        return acc
 
     def _var_name(self, col: int) -> str:
         names = getattr(self, "_names", None)
@@ -277,7 +340,7 @@ class Lowering:
         if op == Op.STORE:
             key, val = self.memo[b.nodes[arr][3]], self.memo[b.nodes[arr][4]]
             rest = self._select(b.nodes[arr][2], idx, idx_orig)
-            return b.op(Op.ITE, b.op(Op.EQ, idx, key), val, rest)
+            return b.op(Op.ITE, self.eq(idx, key), val, rest)
         if op == Op.CONST_ARRAY:
             return self.memo[b.nodes[arr][2]]
         name = self.sym.array_names[b.nodes[arr][5]]
@@ -296,7 +359,7 @@ class Lowering:
         for ck in sorted(cells, reverse=True):
             cell = self._column(cells[ck], rng, kcell, name, ck)
             kn = b.const(ck, b.widths[idx])
-            acc = b.op(Op.ITE, b.op(Op.EQ, idx, kn), cell, acc)
+            acc = b.op(Op.ITE, self.eq(idx, kn), cell, acc)
         return acc
 
     def _apply(self, n: int) -> int:
@@ -319,7 +382,7 @@ class Lowering:
             if w != 256:
                 raise LoweringUnsupported("keccak function %s has range %d" % (fname, w))
             for arg in sorted(km.pairs, reverse=True):
-                acc = b.op(Op.ITE, b.op(Op.EQ, x, b.const(arg, b.widths[x])),
+                acc = b.op(Op.ITE, self.eq(x, b.const(arg, b.widths[x])),
                            b.const(km.pairs[arg], 256), acc)
             return acc
         cells = self.schema.uf_cells.get(fname, {})

@@ -53,6 +53,8 @@ SIGNATURES = {
     "mh_assign_download": (C.c_int32, [_vp, _u32p, C.c_uint64, C.c_uint64]),
     "mh_assign_generate": (C.c_int32, [_vp, C.c_uint64, C.c_uint64]),
     "mh_gen_limb": (C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]),
+    "mh_assign_generate_guided": (C.c_int32, [_vp, C.c_uint64, C.c_uint64, C.c_uint64,
+                                              C.c_uint64, _vp]),
     "mh_results_reset": (C.c_int32, [_vp, _vp, _vp, C.c_uint32]),
     "mh_run": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
                            C.c_uint64, C.c_uint32, _u64p, _u64p]),
@@ -86,6 +88,23 @@ class TapeInfo(C.Structure):
         ("n_regs", C.c_uint32),
         ("features", C.c_uint32),
         ("alg_ops", C.c_uint64),
+    ]
+
+
+class Guide(C.Structure):
+    """mh_guide (include/mythril_hip.h)."""
+
+    _fields_ = [
+        ("n_cols", C.c_uint32),
+        ("col_width", C.POINTER(C.c_uint16)),
+        ("pool_off", _u32p),
+        ("pool", _u32p),
+        ("n_sets", C.c_uint32),
+        ("set_prob", C.POINTER(C.c_uint8)),
+        ("set_off", _u32p),
+        ("alt_off", _u32p),
+        ("entry_col", _u32p),
+        ("entry_val", _u32p),
     ]
 
 
@@ -246,6 +265,20 @@ class Assignments:
 
     def generate(self, seed: int, global_base: int = 0) -> None:
         _check(self.ctx.lib.mh_assign_generate(self.h, seed, global_base))
+
+    def generate_guided(self, seed: int, arrays: dict, global_base: int = 0, first: int = 0,
+                        count: Optional[int] = None) -> None:
+        """Rows [first, first+count) from a guide (mythril_amd.candidates.Guide.arrays())."""
+        count = self.capacity - first if count is None else count
+        a = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
+        n_cols = len(a["width"])
+        n_sets = len(a["set_off"]) - 1
+        g = Guide(n_cols, a["width"].ctypes.data_as(C.POINTER(C.c_uint16)), _ptr(a["pool_off"]),
+                  _ptr(a["pool"]), n_sets, a["set_prob"].ctypes.data_as(C.POINTER(C.c_uint8)),
+                  _ptr(a["set_off"]), _ptr(a["alt_off"]), _ptr(a["entry_col"]),
+                  _ptr(a["entry_val"]))
+        _check(self.ctx.lib.mh_assign_generate_guided(self.h, seed, global_base, first, count,
+                                                      C.byref(g)))
 
     def close(self) -> None:
         if self.h:

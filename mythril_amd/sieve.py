@@ -1,0 +1,228 @@
+"""The sieve engine behind ``get_model``: one path condition -> a witness, or nothing.
+
+For one query (the tuple of Bool constraints ``Constraints.is_possible`` hands to ``get_model``,
+mythril/laser/ethereum/state/constraints.py:25-35, support/model.py:15-62):
+
+1. lower arrays / keccak UFs onto scalar columns (lower.py) — ``LoweringUnsupported`` -> None;
+2. harvest a candidate guide from the lowered term and the parent query's witness
+   (candidates.py);
+3. compile the conjunction as one device tape over the query's own columns (mh_tapes_compile);
+4. per round: fill ``rows`` assignment rows on the device from the guide
+   (mh_assign_generate_guided), run the tape over them in MH_MODE_FIRST_HIT (the kernel stops
+   at the first satisfying lane of each wave), read back the smallest satisfying row;
+5. on a hit, download that one row: the witness (column name -> value).
+
+Everything on the device path raises on failure; the caller (frontend.get_model) treats any
+exception as "no answer from the sieve" and asks the fallback solver, so the reference's
+behaviour is kept on every error (SURVEY.md §5 "fail closed").
+"""
+from __future__ import annotations
+
+import time
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import native
+from .candidates import build_guide
+from .lower import Schema, lower_query
+from .tape import Op, TapeBuilder, TapeSet
+
+
+@dataclass
+class Witness:
+    schema: Schema
+    values: Dict[str, int]             # column name -> value
+    index: int = 0                     # global candidate index that satisfied the query
+    rounds: int = 0
+
+
+@dataclass
+class SieveStats:
+    queries: int = 0
+    hits: int = 0
+    misses: int = 0
+    unsupported: int = 0
+    errors: int = 0
+    rounds: int = 0
+    rows: int = 0
+    host_s: float = 0.0
+    device_s: float = 0.0
+    extra: Dict[str, int] = field(default_factory=dict)
+
+
+def local_tape(b: TapeBuilder, root: int, columns: Sequence[str]) -> np.ndarray:
+    """The tape of `root` with VAR columns renumbered to the query's own column order."""
+    tape = b.finish(root)
+    nodes = tape.nodes.copy()
+    local = {b.var_index[c]: i for i, c in enumerate(columns)}
+    is_var = nodes["op"] == int(Op.VAR)
+    if is_var.any():
+        nodes["imm0"][is_var] = [local[int(x)] for x in nodes["imm0"][is_var]]
+    return nodes
+
+
+# ops whose recomputation is cheap enough to duplicate instead of keeping a value live
+_HEAVY = {Op.BVMUL, Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD, Op.KECCAK,
+          Op.EVM_EXP, Op.BVMUL_NOOVFL_U}
+
+
+def rematerialize(nodes: np.ndarray, max_size: int) -> np.ndarray:
+    """Duplicate cheap shared sub-terms (at most `max_size` nodes, no multiply / divide /
+    keccak) at every use instead of keeping their values live.  A path condition reads the same
+    calldata bytes in several overlapping words (calldata.py:48-54: word(0) and word(4) share 28
+    byte terms), which otherwise holds more values live than the device register file has; the
+    copies cost a few cheap instructions each."""
+    from .tape import ARITY
+
+    n = len(nodes)
+    ops = nodes["op"].astype(int)
+    opnds = np.stack([nodes["a"], nodes["b"], nodes["c"]], axis=1).astype(int)
+    ar = [ARITY[Op(o)] for o in ops]
+    uses = np.zeros(n, dtype=int)
+    size = np.zeros(n, dtype=int)
+    cheap = np.zeros(n, dtype=bool)
+    for i in range(n):
+        kids = opnds[i, :ar[i]]
+        for k in kids:
+            uses[k] += 1
+        size[i] = 1 + sum(int(size[k]) for k in kids)
+        cheap[i] = (Op(ops[i]) not in _HEAVY and size[i] <= max_size
+                    and all(cheap[k] for k in kids) and nodes["width"][i] <= 256)
+    dup = cheap & (uses > 1)
+    out: List[tuple] = []
+    remap = {}
+
+    def copy(k: int, deep: bool) -> int:
+        # inside a duplicated sub-term every cheap node is copied too, so copies share nothing
+        kids = [copy(int(x), True) if cheap[x] and (deep or dup[x]) else remap[int(x)]
+                for x in opnds[k, :ar[k]]]
+        rec = list(nodes[k].tolist())
+        for j, x in enumerate(kids):
+            rec[3 + j] = x
+        out.append(tuple(rec))
+        return len(out) - 1
+
+    for i in range(n):
+        if dup[i] and i != n - 1:
+            continue
+        remap[i] = copy(i, False)
+    return np.array(out, dtype=nodes.dtype)
+
+
+class Sieve:
+    """A device context plus reusable buffers; one per thread (handles are not shared)."""
+
+    def __init__(self, device: int = 0, rows: int = 1 << 16, max_rounds: int = 4,
+                 seed: int = 0x5EED5EED, budget_s: float = 0.25):
+        self.ctx = native.Context(device)
+        self.rows = rows
+        self.max_rounds = max_rounds
+        self.seed = seed
+        self.budget_s = budget_s
+        self.assign: Optional[native.Assignments] = None
+        self.stats = SieveStats()
+        self.witnesses: "OrderedDict[tuple, Dict[str, int]]" = OrderedDict()
+        self.max_witnesses = 1 << 14
+
+    def close(self) -> None:
+        if self.assign is not None:
+            self.assign.close()
+            self.assign = None
+        self.ctx.close()
+
+    def _buffer(self, n_cols: int) -> native.Assignments:
+        if self.assign is None or self.assign.n_vars < n_cols:
+            if self.assign is not None:
+                self.assign.close()
+            cap = max(n_cols, 64)
+            cap = 1 << (cap - 1).bit_length()
+            self.assign = self.ctx.assignments(cap, self.rows)
+        return self.assign
+
+    def remember(self, key: tuple, w: Witness) -> None:
+        self.witnesses[key] = w.values
+        self.witnesses.move_to_end(key)
+        while len(self.witnesses) > self.max_witnesses:
+            self.witnesses.popitem(last=False)
+
+    def compile(self, ts: TapeSet, nodes: np.ndarray) -> native.CompiledTapes:
+        """Compile one query tape; on register pressure, retry with cheap sub-terms duplicated
+        at their uses (rematerialize), widening what counts as cheap."""
+        try:
+            return self.ctx.compile(ts)
+        except native.Unsupported as e:
+            if "register pressure" not in str(e):
+                raise
+            last = e
+        from .tape import Tape
+
+        for size in (8, 32, 256):
+            ts.tapes[-1] = Tape(rematerialize(nodes, size))
+            try:
+                ct = self.ctx.compile(ts)
+                self.stats.extra["remat_%d" % size] = self.stats.extra.get("remat_%d" % size,
+                                                                           0) + 1
+                return ct
+            except native.Unsupported as e:
+                if "register pressure" not in str(e):
+                    raise
+                last = e
+        raise last
+
+    def solve(self, b: TapeBuilder, roots: Sequence[int], key: Optional[tuple] = None,
+              pool=None) -> Optional[Witness]:
+        """A witness of the conjunction of Bool nodes `roots` of builder `b`, or None."""
+        t0 = time.perf_counter()
+        self.stats.queries += 1
+        root, schema = lower_query(b, roots)
+        columns = list(schema.columns)
+        if not columns:  # ground query: one row decides it
+            columns = ["__ground__"]
+            b.var("__ground__", 1)
+            from .lower import Column
+
+            schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
+        parent = self.witnesses.get(key[:-1]) if key else None
+        guide = build_guide(b, root, schema, columns, parent).arrays()
+        ts = TapeSet(columns)
+        ts.pool = pool if pool is not None else b.pool
+        from .tape import Tape
+
+        nodes = local_tape(b, root, columns)
+        ts.tapes.append(Tape(nodes))
+        t1 = time.perf_counter()
+        self.stats.host_s += t1 - t0
+        ct = self.compile(ts, nodes)
+        try:
+            assign = self._buffer(len(columns))
+            for rnd in range(self.max_rounds):
+                base = (self.stats.queries << 24) + rnd * self.rows
+                assign.generate_guided(self.seed, guide, global_base=base, count=self.rows)
+                fh, _ = native.run(self.ctx, ct, assign, mode=native.MODE_FIRST_HIT,
+                                   index_base=base, row_count=self.rows)
+                self.stats.rounds += 1
+                self.stats.rows += self.rows
+                hit = int(fh[0])
+                if hit != native.NO_HIT:
+                    row = hit - base
+                    vals = assign.download(row, 1)
+                    values = {c: _limbs(vals[i, :, 0]) for i, c in enumerate(columns)}
+                    w = Witness(schema, values, hit, rnd + 1)
+                    if key:
+                        self.remember(key, w)
+                    self.stats.hits += 1
+                    return w
+                if time.perf_counter() - t1 > self.budget_s:
+                    break
+            self.stats.misses += 1
+            return None
+        finally:
+            ct.close()
+            self.stats.device_s += time.perf_counter() - t1
+
+
+def _limbs(col: np.ndarray) -> int:
+    return sum(int(x) << (32 * k) for k, x in enumerate(col))

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Run the sieve on the LASER-shaped queries of tests/laser_like.py and report, per query: hit
+or miss, rounds, witness index, host / device seconds, and any exception (the front end swallows
+them to fall back; this script shows them).  One JSON line per query.
+
+    python scripts/sieve_queries.py [rows_per_round]
+"""
+import json
+import os
+import sys
+import time
+import traceback
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+from mythril_amd.sieve import Sieve  # noqa: E402
+from tests.laser_like import queries  # noqa: E402
+
+
+def main():
+    rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
+    s = Sieve(rows=rows)
+    ctx, qs = queries()
+    for name, cs in qs:
+        t0 = time.perf_counter()
+        rec = {"query": name, "constraints": len(cs)}
+        try:
+            w = s.solve(ctx.b, [c.node for c in cs])
+            rec.update(hit=w is not None, rounds=getattr(w, "rounds", None),
+                       index=getattr(w, "index", None),
+                       columns=len(w.schema.columns) if w else None)
+        except Exception as e:
+            rec.update(error="%s: %s" % (type(e).__name__, e),
+                       trace=traceback.format_exc().splitlines()[-4:])
+        rec["ms"] = (time.perf_counter() - t0) * 1e3
+        print(json.dumps(rec), flush=True)
+    st = s.stats
+    print(json.dumps({"queries": st.queries, "hits": st.hits, "misses": st.misses,
+                      "rounds": st.rounds, "host_s": st.host_s, "device_s": st.device_s}))
+    s.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,124 @@
+"""The sieve front end on an MI355X: guided generator parity, witnesses of LASER-shaped queries,
+Model.eval on the device.  Every witness is checked by the ORACLE: the original query (arrays,
+keccak UFs, inverses) evaluated by oracle/term_eval.py under the model the witness row denotes.
+
+Run on the GPU box:  python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+"""
+import numpy as np
+import pytest
+
+from mythril_amd import frontend, native
+from mythril_amd.candidates import build_guide
+from mythril_amd.lower import lower_query
+from mythril_amd.smt import And
+from mythril_amd.support import SolverStatistics, UnsatError
+from oracle.guided_gen import generate_row
+from oracle.term_eval import evaluate_term
+from tests.laser_like import queries
+from tests.test_lowering import model_of
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _reset():
+    frontend.reset()
+    yield
+    frontend.reset()
+
+
+def _oracle_holds(ctx, cs, schema, values):
+    names = [n for n, _ in sorted(ctx.b.var_index.items(), key=lambda kv: kv[1])]
+    vars_, arrays, funcs = model_of(schema, values)
+    tape = ctx.b.finish(And(*cs).node)
+    return bool(evaluate_term(tape.nodes, ctx.b.pool.values, names, ctx.b.symbols.array_names,
+                              ctx.b.symbols.function_names, vars_, arrays, funcs))
+
+
+@pytest.mark.parametrize("qi", [0, 4, 5, 7, 9])
+def test_guided_generator_matches_oracle(gpu_ctx, qi):
+    ctx, qs = queries()
+    _, cs = qs[qi]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    cols = list(schema.columns)
+    arrays = build_guide(ctx.b, root, schema, cols).arrays()
+    rows, seed, base = 512, 0xC0FFEE + qi, 1 << 20
+    a = gpu_ctx.assignments(len(cols) + 3, rows)  # wider buffer: extra columns untouched
+    a.generate(1, 0)
+    before = a.download(0, rows)
+    a.generate_guided(seed, arrays, global_base=base, first=0, count=rows)
+    got = a.download(0, rows)
+    assert np.array_equal(got[len(cols):], before[len(cols):])
+    for r in list(range(0, rows, 37)) + [rows - 1]:
+        want = generate_row(seed, base + r, arrays)
+        for v, wv in enumerate(want):
+            gv = sum(int(got[v, k, r]) << (32 * k) for k in range(8))
+            assert gv == wv, (qi, r, cols[v])
+
+
+def test_guided_generator_rejects_malformed_guides(gpu_ctx):
+    ctx, qs = queries()
+    _, cs = qs[0]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    cols = list(schema.columns)
+    arrays = build_guide(ctx.b, root, schema, cols).arrays()
+    a = gpu_ctx.assignments(len(cols), 64)
+    bad = dict(arrays, entry_col=arrays["entry_col"].copy())
+    bad["entry_col"][0] = len(cols) + 5
+    with pytest.raises(native.SieveError):
+        a.generate_guided(1, bad)
+    narrow = gpu_ctx.assignments(1, 64)
+    with pytest.raises(native.SieveError):
+        narrow.generate_guided(1, arrays)
+    with pytest.raises(native.SieveError):
+        a.generate_guided(1, arrays, first=60, count=10)
+
+
+@pytest.mark.parametrize("qi", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+def test_sieve_witnesses_are_models(gpu_ctx, qi):
+    ctx, qs = queries()
+    name, cs = qs[qi]
+    m = frontend.get_model(tuple(cs))  # no fallback: a miss would raise UnsatError
+    assert _oracle_holds(ctx, cs, m.schema, m.values), name
+    for c in cs:  # Model.eval on the device agrees
+        assert m.eval(c, model_completion=True) is True, name
+
+
+def test_unsat_query_goes_to_the_fallback(gpu_ctx):
+    ctx, qs = queries()
+    cs = dict(qs)["unsat_actor"]
+    with pytest.raises(UnsatError):
+        frontend.get_model(tuple(cs))
+    frontend.configure(fallback=lambda *a: "z3 says")
+    assert frontend.get_model(tuple(cs)) == "z3 says"
+    assert SolverStatistics().sieve_misses >= 2
+
+
+def test_model_eval_values(gpu_ctx):
+    from tests.laser_like import Calldata
+
+    ctx, qs = queries()
+    cs = dict(qs)["selector_size"]
+    m = frontend.get_model(tuple(cs))
+    cd = Calldata("1")
+    word = m.eval(cd.word(0), model_completion=True)
+    assert word.as_long() >> 224 == 0x13AF4035
+    size = m.eval(cd.size, model_completion=True)
+    assert 36 <= size < 5000
+    # a symbol outside the model: unevaluated without completion, 0 with it
+    from mythril_amd.smt import symbol_factory
+
+    y = symbol_factory.BitVecSym("not_in_query", 256)
+    assert m.eval(y + 1) is not None and not isinstance(m.eval(y + 1), int)
+    assert m.eval(y + 1, model_completion=True) == 1
+
+
+def test_parent_witness_is_reused(gpu_ctx):
+    ctx, qs = queries()
+    cs = dict(qs)["selector_size"]
+    s = frontend.sieve()
+    frontend.get_model(tuple(cs[:2]))
+    rounds_before = s.stats.rounds
+    m = frontend.get_model(tuple(cs))
+    assert s.stats.rounds - rounds_before == 1  # found in the first round
+    assert _oracle_holds(ctx, cs, m.schema, m.values)

@@ -1,0 +1,80 @@
+"""Host side of the sieve engine (mythril_amd/sieve.py), checked with the oracle and the
+test-only host emulator of the device ISA (tests/native/emu.cpp, the product tape compiler).
+
+* every LASER-shaped query of tests/laser_like.py compiles for the device (with
+  rematerialisation where overlapping calldata words exceed the register file) and the compiled
+  code agrees with the oracle on guided candidate rows;
+* ``rematerialize`` preserves the value of a tape and lowers its register need.
+"""
+import numpy as np
+import pytest
+
+from mythril_amd.candidates import build_guide
+from mythril_amd.lower import lower_query
+from mythril_amd.sieve import local_tape, rematerialize
+from mythril_amd.tape import Tape, TapeSet
+from oracle import smt_eval as E
+from oracle.guided_gen import generate_row
+from tests.emu import EmuError
+from tests.laser_like import queries
+
+
+def _soa(rows, n_cols):
+    soa = np.zeros((n_cols, 8, len(rows)), dtype=np.uint32)
+    for j, row in enumerate(rows):
+        for i, v in enumerate(row):
+            for k in range(8):
+                soa[i, k, j] = (v >> (32 * k)) & 0xFFFFFFFF
+    return soa
+
+
+@pytest.mark.parametrize("qi", range(11))
+def test_queries_compile_and_match_oracle(emu, qi):
+    ctx, qs = queries()
+    name, cs = qs[qi]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    cols = list(schema.columns)
+    guide = build_guide(ctx.b, root, schema, cols).arrays()
+    nodes = local_tape(ctx.b, root, cols)
+    ts = TapeSet(cols)
+    ts.pool = ctx.b.pool
+    rows = [generate_row(11 + qi, r, guide) for r in range(96)]
+    soa = _soa(rows, len(cols))
+    got = None
+    for size in (0, 8, 32, 256):  # the retry ladder of Sieve.compile
+        ts.tapes[:] = [Tape(nodes if size == 0 else rematerialize(nodes, size))]
+        try:
+            got, nregs = emu.eval(ts, 0, soa)
+            break
+        except EmuError as e:
+            assert "register pressure" in str(e), (name, str(e))
+    assert got is not None, name
+    for j, row in enumerate(rows):
+        want = E.evaluate(nodes, ctx.b.pool.values, row)
+        assert bool(got[j]) == bool(want), (name, j)
+        # the rematerialised tape is the same function
+        assert bool(E.evaluate(ts.tapes[0].nodes, ctx.b.pool.values, row)) == bool(want)
+
+
+def test_rematerialize_removes_sharing_of_cheap_terms():
+    ctx, qs = queries()
+    cs = dict(qs)["address_arg"]
+    root, _ = lower_query(ctx.b, [c.node for c in cs])
+    nodes = local_tape(ctx.b, root, list(ctx.b.var_index))
+    r = rematerialize(nodes, 8)
+    # reachable part of r: every cheap node has one user
+    from mythril_amd.tape import ARITY, Op
+
+    n = len(r)
+    reach = np.zeros(n, dtype=bool)
+    reach[-1] = True
+    uses = np.zeros(n, dtype=int)
+    for i in range(n - 1, -1, -1):
+        if not reach[i]:
+            continue
+        for x in [r["a"][i], r["b"][i], r["c"][i]][:ARITY[Op(int(r["op"][i]))]]:
+            reach[x] = True
+            uses[x] += 1
+    shared_ites = [i for i in range(n) if reach[i] and int(r["op"][i]) == Op.ITE
+                   and uses[i] > 1]
+    assert not shared_ites
