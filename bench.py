@@ -54,7 +54,7 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    from mythril_amd import native, synth
+    from mythril_amd import native, shard, synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -74,10 +74,10 @@ def main() -> None:
     ct = ctx.compile(ts)
     info = ct.info()
     alg_ops_per_row = sum(int(i["alg_ops"]) for i in info)
-    rows = args.rows_per_gpu
+    index_base, rows = shard.shard_range(rank, world, args.rows_per_gpu)
     seed = spec["assignment_seed"]
     assign = ctx.assignments(ts.n_vars, rows)
-    assign.generate(seed, rank * rows)
+    assign.generate(seed, index_base)
     fh = torch.empty(n_tapes, dtype=torch.int64, device=dev)
     hc = torch.empty(n_tapes, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
@@ -87,12 +87,10 @@ def main() -> None:
 
     def step(timed: bool):
         native.results_reset(ctx, fh.data_ptr(), hc.data_ptr(), n_tapes)
-        native.run_async(ctx, ct, assign, fh.data_ptr(), hc.data_ptr(), index_base=rank * rows,
+        native.run_async(ctx, ct, assign, fh.data_ptr(), hc.data_ptr(), index_base=index_base,
                          mode=native.MODE_COUNT_ALL)
-        if world > 1:
-            f = torch.where(fh < 0, torch.full_like(fh, torch.iinfo(torch.int64).max), fh)
-            dist.all_reduce(f, op=dist.ReduceOp.MIN)
-            dist.all_reduce(hc, op=dist.ReduceOp.SUM)
+        if world > 1:  # the one exchange: MIN of first witnesses, SUM of counts (RCCL)
+            shard.allreduce_results(fh, hc)
 
     for i in range(args.warmup):
         step(False)

@@ -1,0 +1,34 @@
+"""Multi-GPU sharding of a sieve sweep: one process per GPU, rows split by rank.
+
+Assignments are regenerated per rank from the counter-based generator (row i of rank r is global
+candidate index r * rows_per_rank + i), so no input moves between GPUs.  The one exchange per
+step is the per-tape result: the smallest satisfying global index (MIN; MH_NO_HIT = all ones is
+mapped to INT64_MAX for the reduction) and the number of satisfying rows (SUM), 16 B per tape,
+over RCCL ("nccl" backend) on the GPUs or gloo on the CPU.  The minimum over shards is the global
+minimum, so results are identical for any number of ranks.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+INT64_MAX = (1 << 63) - 1
+
+
+def shard_range(rank: int, world: int, rows_per_rank: int) -> Tuple[int, int]:
+    """(global index of this rank's first row, rows) — weak scaling: every rank sweeps
+    rows_per_rank candidates."""
+    if not 0 <= rank < world:
+        raise ValueError("rank %d outside world of %d" % (rank, world))
+    return rank * rows_per_rank, rows_per_rank
+
+
+def allreduce_results(first_hit, hit_count, group=None) -> None:
+    """In place over all ranks: first_hit = MIN (NO_HIT stays NO_HIT), hit_count = SUM.
+    first_hit / hit_count are int64 tensors holding the u64 results (NO_HIT reads -1)."""
+    import torch
+    import torch.distributed as dist
+
+    f = torch.where(first_hit == -1, torch.full_like(first_hit, INT64_MAX), first_hit)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hit_count, op=dist.ReduceOp.SUM, group=group)
+    first_hit.copy_(torch.where(f == INT64_MAX, torch.full_like(f, -1), f))

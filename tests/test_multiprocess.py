@@ -1,0 +1,100 @@
+"""The N > 1 path on the CPU: world_size 2 over gloo.
+
+Each rank evaluates its shard of candidate rows (mythril_amd.shard.shard_range: the
+counter-based generator gives rank r the global rows [r*R, (r+1)*R)) — here with the ORACLE,
+since the container has no GPU — and the product reduction (shard.allreduce_results: MIN of the
+first witness, SUM of the counts) must reproduce the single-process answer over all 2R rows.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from mythril_amd import shard
+from mythril_amd.tape import Op, TapeSet
+from oracle import smt_eval
+
+ROWS = 48
+TAPES = 12
+SEED = 0x5EED
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _tapes():
+    """Tapes with satisfaction rates from ~1/2 down to 0 over the generated rows."""
+    ts = TapeSet(["a", "b", "c", "d"])
+    for t in range(TAPES):
+        b = ts.builder()
+        x, y = b.var("a"), b.var("b")
+        if t % 3 == 0:
+            root = b.op(Op.BVULT, x, y)
+        elif t % 3 == 1:
+            lo = b.op(Op.EXTRACT, x, imm0=2 + t // 3, imm1=0)  # p = 2^-(3 + t/3)
+            root = b.op(Op.EQ, lo, b.const(t, 3 + t // 3))
+        else:
+            root = b.op(Op.EQ, b.op(Op.BVXOR, x, y), b.const(t, 256))  # never in 96 rows
+        ts.add(b.finish(root))
+    return ts
+
+
+def _shard_results(ts, base, rows):
+    fh = [-1] * len(ts.tapes)
+    hc = [0] * len(ts.tapes)
+    for r in range(rows):
+        a = smt_eval.gen_assignment(SEED, ts.n_vars, base + r)
+        for t, tape in enumerate(ts.tapes):
+            if smt_eval.evaluate(tape.nodes, ts.pool.values, a):
+                hc[t] += 1
+                if fh[t] < 0:
+                    fh[t] = base + r
+    return fh, hc
+
+
+def _worker(rank, world, port, out):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ts = _tapes()
+        base, rows = shard.shard_range(rank, world, ROWS)
+        fh, hc = _shard_results(ts, base, rows)
+        fh_t = torch.tensor(fh, dtype=torch.int64)
+        hc_t = torch.tensor(hc, dtype=torch.int64)
+        shard.allreduce_results(fh_t, hc_t)
+        out[rank] = (fh_t.tolist(), hc_t.tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_reduction_matches_single_process():
+    world = 2
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+        results = dict(out)
+    ts = _tapes()
+    want = _shard_results(ts, 0, ROWS * world)
+    assert any(x >= ROWS for x in want[0])  # some first witnesses lie in rank 1's shard
+    assert any(x < 0 for x in want[0]) and any(0 <= x < ROWS for x in want[0])
+    assert results[0] == results[1]
+    assert tuple(results[0][0]) == tuple(want[0])
+    assert tuple(results[0][1]) == tuple(want[1])
+
+
+def test_shard_range():
+    assert shard.shard_range(0, 4, 100) == (0, 100)
+    assert shard.shard_range(3, 4, 100) == (300, 100)
+    with pytest.raises(ValueError):
+        shard.shard_range(4, 4, 100)
