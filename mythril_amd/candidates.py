@@ -170,6 +170,13 @@ class Harvester:
             return acc
         if op == Op.EXTRACT:
             return self.invert_bits(a, value << i1, mask << i1, depth + 1)
+        if op == Op.BVAND:  # x & m == value on `mask`: only the bits of m are free
+            for x, m in ((a, b.const_value(bb)), (bb, b.const_value(a))):
+                if m is not None:
+                    if value & ~m & mask:
+                        return []
+                    return self.invert_bits(x, value & m, mask & m, depth + 1)
+            return None
         if op in (Op.ZEXT, Op.SEXT):
             wa = b.widths[a]
             if op == Op.ZEXT and (value >> wa) != 0:
@@ -323,6 +330,16 @@ class Harvester:
             return out
         if op == Op.ZEXT:
             return self.segments(a, depth + 1)
+        if op == Op.BVAND:  # x & (2^k - 1): the low k bits of x (ABI decoding of addresses)
+            for x, m in ((a, b.const_value(bb)), (bb, b.const_value(a))):
+                if m is not None and m & (m + 1) == 0:
+                    inner = self.segments(x, depth + 1)
+                    if inner is None:
+                        return None
+                    k = m.bit_length()
+                    return [(lo, min(n_, k - lo), col, cl) for lo, n_, col, cl in inner
+                            if lo < k]
+            return None
         if op == Op.ITE:
             if b.const_value(c) is not None:
                 return self.segments(bb, depth + 1)
@@ -406,6 +423,10 @@ class Harvester:
                 w = b.widths[x]
                 if w == BOOL or b.const_value(x) is not None or b.const_value(y) is not None:
                     continue
+                x, y = self.strip_common(x, y)
+                if x == y:  # t == t (keccak inverse conditions after lowering): always true
+                    continue
+                w = b.widths[x]
                 calts = self.copy_alternatives(x, y)
                 if calts:
                     if len(self.copy_sets) < MAX_SETS // 4:
@@ -443,10 +464,14 @@ class Harvester:
         return Guide(self.columns, widths, [self.pools[c] for c in self.columns],
                      self.sets[:MAX_SETS], copy_sets[:MAX_SETS // 4])
 
-    def _eq_nodes(self, root: int) -> List[int]:
+    def _eq_nodes(self, root: int, limit: int = 4096) -> List[int]:
+        """Equalities anywhere under a conjunct (also inside ite conditions of bit-vector terms:
+        store-chain reads lower to ite(key == stored_key, ...))."""
+        from .tape import ARITY
+
         out, seen, stack = [], set(), [root]
         b = self.b
-        while stack:
+        while stack and len(seen) < limit:
             n = stack.pop()
             if n in seen:
                 continue
@@ -454,11 +479,35 @@ class Harvester:
             op, w, a, bb, c, _, _ = b.nodes[n]
             if op == Op.EQ:
                 out.append(n)
-            if w == BOOL and op in (Op.AND, Op.OR, Op.NOT, Op.XOR, Op.EQ, Op.ITE):
-                from .tape import ARITY
-
-                stack += [a, bb, c][:ARITY[Op(op)]]
+            stack += [a, bb, c][:ARITY[Op(op)]]
         return out
+
+    def strip_common(self, x: int, y: int) -> Tuple[int, int]:
+        """Peel wrappers both sides share (same op, same constant operand, or the same other
+        concat half) so that f(x') == f(y') is tried as x' == y' — the keccak interval map
+        H(x) = base + ((keccak(x) >> 139) << 6) of lower.py included (a heuristic for
+        candidate generation only: the witness is checked on the device)."""
+        b = self.b
+        for _ in range(64):
+            ox, oy = b.nodes[x], b.nodes[y]
+            if ox[0] != oy[0] or ox[1] != oy[1]:
+                break
+            op = Op(ox[0])
+            if op in (Op.KECCAK, Op.BVNOT, Op.BVNEG) or (op in (Op.ZEXT, Op.SEXT)
+                                                          and ox[5] == oy[5]):
+                x, y = ox[2], oy[2]
+                continue
+            if op in (Op.BVADD, Op.BVSUB, Op.BVXOR, Op.BVSHL, Op.BVLSHR, Op.BVMUL, Op.CONCAT):
+                if ox[3] == oy[3] or (b.const_value(ox[3]) is not None
+                                      and b.const_value(ox[3]) == b.const_value(oy[3])):
+                    x, y = ox[2], oy[2]
+                    continue
+                if ox[2] == oy[2] or (b.const_value(ox[2]) is not None
+                                      and b.const_value(ox[2]) == b.const_value(oy[2])):
+                    x, y = ox[3], oy[3]
+                    continue
+            break
+        return x, y
 
 
 def build_guide(b: TapeBuilder, root: int, schema: Schema, columns: Sequence[str],

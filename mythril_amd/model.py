@@ -96,7 +96,7 @@ class Model:
         nodes = local_tape(b, root, columns)
         ts.tapes.append(Tape(nodes))
         dev = self.sieve.ctx
-        ct = self.sieve.compile(ts, nodes)
+        ct = self.sieve.compile(ts)
         try:
             assign = dev.assignments(len(columns), 1)
             try:

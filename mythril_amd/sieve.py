@@ -148,33 +148,92 @@ class Sieve:
         while len(self.witnesses) > self.max_witnesses:
             self.witnesses.popitem(last=False)
 
-    def compile(self, ts: TapeSet, nodes: np.ndarray) -> native.CompiledTapes:
-        """Compile one query tape; on register pressure, retry with cheap sub-terms duplicated
-        at their uses (rematerialize), widening what counts as cheap."""
-        try:
-            return self.ctx.compile(ts)
-        except native.Unsupported as e:
-            if "register pressure" not in str(e):
-                raise
-            last = e
+    def compile(self, ts: TapeSet) -> native.CompiledTapes:
+        """Compile a query's tapes; a tape that runs out of registers is retried with cheap
+        sub-terms duplicated at their uses (rematerialize), widening what counts as cheap."""
+        import re
+
         from .tape import Tape
 
-        for size in (8, 32, 256):
-            ts.tapes[-1] = Tape(rematerialize(nodes, size))
+        orig = [t.nodes for t in ts.tapes]
+        level = [0] * len(orig)
+        sizes = (0, 8, 32, 256)
+        while True:
             try:
-                ct = self.ctx.compile(ts)
-                self.stats.extra["remat_%d" % size] = self.stats.extra.get("remat_%d" % size,
-                                                                           0) + 1
-                return ct
+                return self.ctx.compile(ts)
             except native.Unsupported as e:
-                if "register pressure" not in str(e):
+                m = re.search(r"tape (\d+): register pressure", str(e))
+                if not m:
                     raise
-                last = e
-        raise last
+                t = int(m.group(1))
+                level[t] += 1
+                if level[t] >= len(sizes):
+                    raise
+                ts.tapes[t] = Tape(rematerialize(orig[t], sizes[level[t]]))
+                k = "remat_%d" % sizes[level[t]]
+                self.stats.extra[k] = self.stats.extra.get(k, 0) + 1
+
+    @staticmethod
+    def buckets(b: TapeBuilder, root: int) -> List[Tuple[List[int], set]]:
+        """Variable-disjoint groups of the conjuncts of `root` (the DependenceMap of
+        laser/smt/solver/independence_solver.py:38-83, over lowered columns): [(conjunct nodes,
+        column var indices)].  Groups share no column, so each can take its witness from a
+        different candidate row."""
+        from .tape import ARITY
+
+        conj, stack = [], [root]
+        while stack:
+            n = stack.pop()
+            if b.nodes[n][0] == Op.AND:
+                stack += [b.nodes[n][3], b.nodes[n][2]]
+            else:
+                conj.append(n)
+        cols: Dict[int, frozenset] = {}
+        order, seen, st = [], set(), [(c, False) for c in conj]
+        while st:
+            n, done = st.pop()
+            if done:
+                order.append(n)
+                continue
+            if n in seen:
+                continue
+            seen.add(n)
+            st.append((n, True))
+            op, _, a, bb, c, _, _ = b.nodes[n]
+            st += [(x, False) for x in (a, bb, c)[:ARITY[Op(op)]] if x not in seen]
+        for n in order:
+            op, _, a, bb, c, i0, _ = b.nodes[n]
+            if op == Op.VAR:
+                cols[n] = frozenset((i0,))
+            else:
+                kids = (a, bb, c)[:ARITY[Op(op)]]
+                cols[n] = frozenset().union(*(cols[x] for x in kids)) if kids else frozenset()
+        parent: Dict[int, int] = {}
+
+        def find(x):
+            while parent.setdefault(x, x) != x:
+                parent[x] = parent[parent[x]]
+                x = parent[x]
+            return x
+
+        for cn in conj:
+            vs = list(cols[cn])
+            for v in vs[1:]:
+                parent[find(v)] = find(vs[0])
+        groups: Dict[object, Tuple[List[int], set]] = {}
+        for cn in conj:
+            vs = cols[cn]
+            key = find(next(iter(vs))) if vs else ("ground", cn)
+            g = groups.setdefault(key, ([], set()))
+            g[0].append(cn)
+            g[1].update(vs)
+        return list(groups.values())
 
     def solve(self, b: TapeBuilder, roots: Sequence[int], key: Optional[tuple] = None,
               pool=None) -> Optional[Witness]:
         """A witness of the conjunction of Bool nodes `roots` of builder `b`, or None."""
+        from .tape import Tape
+
         t0 = time.perf_counter()
         self.stats.queries += 1
         root, schema = lower_query(b, roots)
@@ -187,17 +246,28 @@ class Sieve:
             schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
         parent = self.witnesses.get(key[:-1]) if key else None
         guide = build_guide(b, root, schema, columns, parent).arrays()
+        groups = self.buckets(b, root)
         ts = TapeSet(columns)
         ts.pool = pool if pool is not None else b.pool
-        from .tape import Tape
-
-        nodes = local_tape(b, root, columns)
-        ts.tapes.append(Tape(nodes))
+        names = {b.var_index[c]: c for c in columns}
+        group_cols = []
+        for conj, vs in groups:
+            acc = conj[0]
+            for x in conj[1:]:
+                acc = b.op(Op.AND, acc, x)
+            ts.tapes.append(Tape(local_tape(b, acc, columns)))
+            group_cols.append([names[v] for v in vs])
+        if len(groups) > 1:
+            self.stats.extra["bucketed"] = self.stats.extra.get("bucketed", 0) + 1
         t1 = time.perf_counter()
         self.stats.host_s += t1 - t0
-        ct = self.compile(ts, nodes)
+        ct = self.compile(ts)
         try:
             assign = self._buffer(len(columns))
+            col_index = {c: i for i, c in enumerate(columns)}
+            values: Dict[str, int] = {}
+            solved = [False] * len(groups)
+            first_index = None
             for rnd in range(self.max_rounds):
                 base = (self.stats.queries << 24) + rnd * self.rows
                 assign.generate_guided(self.seed, guide, global_base=base, count=self.rows)
@@ -205,12 +275,22 @@ class Sieve:
                                    index_base=base, row_count=self.rows)
                 self.stats.rounds += 1
                 self.stats.rows += self.rows
-                hit = int(fh[0])
-                if hit != native.NO_HIT:
+                rows_read: Dict[int, np.ndarray] = {}
+                for g, hit in enumerate(fh.tolist()):
+                    if solved[g] or hit == native.NO_HIT:
+                        continue
                     row = hit - base
-                    vals = assign.download(row, 1)
-                    values = {c: _limbs(vals[i, :, 0]) for i, c in enumerate(columns)}
-                    w = Witness(schema, values, hit, rnd + 1)
+                    if row not in rows_read:
+                        rows_read[row] = assign.download(row, 1)
+                    vals = rows_read[row]
+                    for c in group_cols[g]:
+                        values[c] = _limbs(vals[col_index[c], :, 0])
+                    solved[g] = True
+                    first_index = hit if first_index is None else min(first_index, hit)
+                if all(solved):
+                    for c in columns:  # columns no conjunct reads: any value is a model
+                        values.setdefault(c, 0)
+                    w = Witness(schema, values, first_index, rnd + 1)
                     if key:
                         self.remember(key, w)
                     self.stats.hits += 1

@@ -97,6 +97,41 @@ def mapping_slot(km: KeccakManager, key: BitVec, slot: int):
     return km.create(Concat(key, symbol_factory.BitVecVal(slot, 256)))
 
 
+def killbilly():
+    """The path condition at ``selfdestruct`` in the 3-transaction KillBilly sequence of
+    README.md:54-76 (killerize(addr); activatekillability(); commencekilling()): three
+    calldata arrays and dispatcher checks, senders in ACTORS, non-payable functions, and the
+    created contract's storage (K(0), account.py:26-29) carrying
+    approved_killers[addr] = 1 (mapping slot keccak(addr . 1)) from tx 1 to tx 2 and
+    is_killable = 1 (slot 0) from tx 2 to tx 3, with the keccak manager's conditions."""
+    km = KeccakManager()
+    zero = symbol_factory.BitVecVal(0, 256)
+    one = symbol_factory.BitVecVal(1, 256)
+    storage = K(256, 256, 0)
+    cs = []
+    txs = []
+    for t, sel in ((1, 0x9FA299CC), (2, 0x84057065), (3, 0x7C11DA20)):
+        cd = Calldata(str(t))
+        sender = symbol_factory.BitVecSym("sender_%d" % t, 256)
+        value = symbol_factory.BitVecSym("call_value%d" % t, 256)
+        cs += [sender_is_actor(sender), selector_is(cd, sel), value == zero,
+               ULT(cd.size, symbol_factory.BitVecVal(5000, 256))]
+        txs.append((cd, sender))
+    cd1, _ = txs[0]
+    cs.append(UGE(cd1.size, symbol_factory.BitVecVal(36, 256)))
+    addr = cd1.word(4) & symbol_factory.BitVecVal((1 << 160) - 1, 256)
+    slot_a, cond_a = mapping_slot(km, addr, 1)
+    storage[slot_a] = one                                   # tx 1: approved_killers[addr] = 1
+    _, sender2 = txs[1]
+    slot_s, cond_s = mapping_slot(km, sender2, 1)
+    cs += [cond_a, cond_s, storage[slot_s] == one]          # tx 2: require(approved[msg.sender])
+    storage[zero] = one                                     # tx 2: is_killable = 1
+    _, sender3 = txs[2]
+    cs += [Not(storage[zero] == zero),                      # tx 3: require(is_killable)
+           sender3 == symbol_factory.BitVecVal(ATTACKER, 256)]
+    return cs
+
+
 def queries():
     """A list of (name, [constraints]) LASER-shaped feasibility queries, most of them SAT."""
     out = []
@@ -135,6 +170,7 @@ def queries():
     st[cd.word(4)] = value
     out.append(("k_storage", [st[symbol_factory.BitVecVal(0, 256)] == symbol_factory.BitVecVal(
         ATTACKER, 256), sender_is_actor(sender)]))
+    out.append(("killbilly", killbilly()))
     out.append(("unsat_actor", [sender_is_actor(sender), sender == symbol_factory.BitVecVal(5,
                                                                                             256)]))
     return ctx, out

@@ -74,7 +74,7 @@ def test_guided_generator_rejects_malformed_guides(gpu_ctx):
         a.generate_guided(1, arrays, first=60, count=10)
 
 
-@pytest.mark.parametrize("qi", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("qi", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_sieve_witnesses_are_models(gpu_ctx, qi):
     ctx, qs = queries()
     name, cs = qs[qi]

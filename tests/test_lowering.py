@@ -68,7 +68,7 @@ def candidate_values(ctx, width, rng):
     return (v + rng.choice((0, 0, 1, -1))) & m
 
 
-@pytest.mark.parametrize("qi", range(11))
+@pytest.mark.parametrize("qi", range(12))
 def test_lowered_tape_matches_term_semantics(qi):
     ctx, qs = queries()
     name, cs = qs[qi]
@@ -97,7 +97,8 @@ def test_lowered_tape_matches_term_semantics(qi):
     if name == "unsat_actor":
         assert not any(outcomes)
     else:  # the harvested guide finds witnesses of every SAT shape
-        assert sum(outcomes) >= 5, (name, sum(outcomes))
+        # (whole rows; the device also solves variable-disjoint groups separately)
+        assert sum(outcomes) >= (1 if name == "killbilly" else 5), (name, sum(outcomes))
 
 
 def test_keccak_base_is_inside_the_interval():

@@ -28,7 +28,7 @@ def _soa(rows, n_cols):
     return soa
 
 
-@pytest.mark.parametrize("qi", range(11))
+@pytest.mark.parametrize("qi", range(12))
 def test_queries_compile_and_match_oracle(emu, qi):
     ctx, qs = queries()
     name, cs = qs[qi]
@@ -78,3 +78,21 @@ def test_rematerialize_removes_sharing_of_cheap_terms():
     shared_ites = [i for i in range(n) if reach[i] and int(r["op"][i]) == Op.ITE
                    and uses[i] > 1]
     assert not shared_ites
+
+
+def test_buckets_split_variable_disjoint_conjuncts():
+    from mythril_amd.sieve import Sieve
+
+    ctx, qs = queries()
+    sizes = {}
+    for name, cs in qs:
+        root, schema = lower_query(ctx.b, [c.node for c in cs])
+        groups = Sieve.buckets(ctx.b, root)
+        cols = [v for _, vs in groups for v in vs]
+        assert len(cols) == len(set(cols)), name  # disjoint
+        names = {ctx.b.var_index[c] for c in schema.columns}
+        assert set(cols) == names, name  # every column of the query is in some group
+        sizes[name] = sum(1 for _, vs in groups if vs)  # ground conjuncts form groups too
+    assert sizes["selector"] == 2        # calldata bytes + size  |  sender in ACTORS
+    assert sizes["owner_check"] == 1     # Storage[0] == sender ties them
+    assert sizes["keccak_alias"] == 1

@@ -74,7 +74,7 @@ def test_reads_z3_style_text():
     assert not _eval(q.ctx, q.constraints, dict(good, call_value1=0), arrays, funcs)
 
 
-@pytest.mark.parametrize("qi", range(11))
+@pytest.mark.parametrize("qi", range(12))
 def test_roundtrip_preserves_laser_queries(qi):
     ctx, qs = queries()
     name, cs = qs[qi]
