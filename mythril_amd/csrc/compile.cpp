@@ -21,6 +21,7 @@
 #include "compile.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -91,6 +92,31 @@ uint8_t mirror(uint8_t op) {  // op(a, b) == mirror(op)(b, a), or 0
         case D_SGE_R: return D_SLE_R;
         default: return 0;
     }
+}
+
+// Diagnostic switch: MH_XFORM_MASK (env, default all) enables X forms per group --
+// 1 add/sub R, 2 add/sub C, 4 logic R, 8 logic C, 16 eq, 32 compares R, 64 compares C,
+// 128 immediate shifts, 256 mul, 512 loadc.
+bool xform_enabled(uint32_t op) {
+    static const uint32_t mask = [] {
+        const char* e = std::getenv("MH_XFORM_MASK");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : ~0u;
+    }();
+    uint32_t g = 0;
+    switch (op) {
+        case D_ADD_R: case D_SUB_R: case D_RSUB_R: g = 1; break;
+        case D_ADD_C: case D_SUB_C: case D_RSUB_C: g = 2; break;
+        case D_AND_R: case D_OR_R: case D_XOR_R: g = 4; break;
+        case D_AND_C: case D_OR_C: case D_XOR_C: g = 8; break;
+        case D_EQ_R: case D_EQ_C: g = 16; break;
+        case D_LSHRI: case D_SHLI: case D_SHLQ: g = 128; break;
+        case D_MUL_R: case D_MUL_C: g = 256; break;
+        case D_LOADC: g = 512; break;
+        default:
+            if (op >= D_ULT_R && op <= D_SGE_C) g = ((op - D_ULT_R) & 1) ? 64 : 32;
+            break;
+    }
+    return (mask & g) != 0;
 }
 
 struct VInsn {
@@ -806,6 +832,10 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
                 return MH_E_UNSUPPORTED;
             }
             if (v.cidx >= 0 && op < D_FIRST_COMPLEX && op != D_LOADC) op += 1;  // *_C form
+            // first operand already in X and no write-back: the X form (a' = d' = X)
+            if (op < D_FIRST_COMPLEX && a == nrx && d == nrx && mh_xform(op) &&
+                xform_enabled(op))
+                op = mh_xform(op);
             w1 = op | ((v.width & 0x1FFu) << 8) | (v.aux << 17);
             if (v.cidx >= 0 && op >= D_FIRST_COMPLEX) w1 |= F_YC;
         }

@@ -61,9 +61,18 @@ enum mh_dop : uint8_t {
     // the bvsdiv/bvsrem/bvsmod sign rules); narrower widths are sign-extended / masked by the host
     D_UDIV_R, D_UDIV_C, D_UREM_R, D_UREM_C, D_SDIV_R, D_SDIV_C, D_SREM_R, D_SREM_C,
     D_SMOD_R, D_SMOD_C,
+    // X forms: the first operand is already in the accumulator and the result stays there
+    // (a' = d' = X).  Same semantics as the base op; the handlers read y = R[b] directly through
+    // the SRC1 index instead of copying it, and skip the write-back (mh_xform / mh_base_op).
+    D_ADD_RX, D_ADD_CX, D_SUB_RX, D_SUB_CX, D_RSUB_RX, D_RSUB_CX,
+    D_AND_RX, D_AND_CX, D_OR_RX, D_OR_CX, D_XOR_RX, D_XOR_CX,
+    D_EQ_RX, D_EQ_CX, D_ULT_RX, D_ULT_CX, D_UGT_RX, D_UGT_CX, D_ULE_RX, D_ULE_CX,
+    D_UGE_RX, D_UGE_CX, D_SLT_RX, D_SLT_CX, D_SGT_RX, D_SGT_CX, D_SLE_RX, D_SLE_CX,
+    D_SGE_RX, D_SGE_CX,
+    D_LSHRI_X, D_SHLI_X, D_SHLQ_X, D_MUL_RX, D_MUL_CX, D_LOADC_X,
     D_NUM_ASM,
     // ---- C++ (exec.h); y = R[b] or the inline constant (F_YC)
-    D_FIRST_COMPLEX = 64,
+    D_FIRST_COMPLEX = 112,
     D_UADD_NOOVFL = D_FIRST_COMPLEX,  // z3 BVAddNoOverflow (unsigned) -> Bool
     D_UMUL_NOOVFL,                    // z3 BVMulNoOverflow (unsigned) -> Bool
     D_EXP, D_SIGNEXT, D_BYTE,        // EVM word ops (256-bit)
@@ -76,8 +85,37 @@ enum mh_dop : uint8_t {
 
 static_assert(D_NUM_ASM <= D_FIRST_COMPLEX, "asm opcode space");
 
+// the base op of an X form (identity for every other op)
+static inline unsigned mh_base_op(unsigned op) {
+    if (op >= D_ADD_RX && op <= D_SGE_CX) return D_ADD_R + (op - D_ADD_RX);
+    switch (op) {
+        case D_LSHRI_X: return D_LSHRI;
+        case D_SHLI_X: return D_SHLI;
+        case D_SHLQ_X: return D_SHLQ;
+        case D_MUL_RX: return D_MUL_R;
+        case D_MUL_CX: return D_MUL_C;
+        case D_LOADC_X: return D_LOADC;
+        default: return op;
+    }
+}
+
+// the X form of a (final, R- or C-form) asm op, or 0 when it has none
+static inline unsigned mh_xform(unsigned op) {
+    if (op >= D_ADD_R && op <= D_SGE_C) return D_ADD_RX + (op - D_ADD_R);
+    switch (op) {
+        case D_LSHRI: return D_LSHRI_X;
+        case D_SHLI: return D_SHLI_X;
+        case D_SHLQ: return D_SHLQ_X;
+        case D_MUL_R: return D_MUL_RX;
+        case D_MUL_C: return D_MUL_CX;
+        case D_LOADC: return D_LOADC_X;
+        default: return 0;
+    }
+}
+
 // *_R / *_C pairs (y from a register / inline constant): 1 = R form, 2 = C form, 0 = neither
 static inline int mh_pair_form(unsigned op) {
+    op = mh_base_op(op);
     if (op >= D_ADD_R && op <= D_SGE_C) return 1 + ((op - D_ADD_R) & 1);
     if (op == D_MUL_R || op == D_MUL_C) return 1 + (op - D_MUL_R);
     if (op >= D_UDIV_R && op <= D_SMOD_C) return 1 + ((op - D_UDIV_R) & 1);

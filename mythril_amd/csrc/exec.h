@@ -141,7 +141,7 @@ MH_FN bool asm_op_yreg(u32 op) {
 template <int FEAT, bool SIMPLE, class M>
 MH_FN u32 step(M& m, u32 w0, u32 w1, u32 ip) {
     const u32 a = w0 & 0xFFu, b = (w0 >> 8) & 0xFFu, d = (w0 >> 16) & 0xFFu, c = w0 >> 24;
-    const u32 op = w1 & 0xFFu, w = (w1 >> 8) & 0x1FFu, aux = (w1 >> 17) & MH_AUX_MAX;
+    const u32 op = mh_base_op(w1 & 0xFFu), aux = (w1 >> 17) & MH_AUX_MAX;
     u32 x[8], y[8], z[8];
     m.read(a, x);
     u32 len = 1;

@@ -37,12 +37,19 @@ OPS = ["EXIT", "NOP",
        "ITE", "ITEC", "BITE", "LOADC", "LSHRI", "SHLI", "SHLQ",
        "MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V",
        "UDIV_R", "UDIV_C", "UREM_R", "UREM_C", "SDIV_R", "SDIV_C", "SREM_R", "SREM_C",
-       "SMOD_R", "SMOD_C"]
+       "SMOD_R", "SMOD_C",
+       # X forms (dev_isa.h): a' = d' = X
+       "ADD_RX", "ADD_CX", "SUB_RX", "SUB_CX", "RSUB_RX", "RSUB_CX",
+       "AND_RX", "AND_CX", "OR_RX", "OR_CX", "XOR_RX", "XOR_CX",
+       "EQ_RX", "EQ_CX", "ULT_RX", "ULT_CX", "UGT_RX", "UGT_CX", "ULE_RX", "ULE_CX",
+       "UGE_RX", "UGE_CX", "SLT_RX", "SLT_CX", "SGT_RX", "SGT_CX", "SLE_RX", "SLE_CX",
+       "SGE_RX", "SGE_CX",
+       "LSHRI_X", "SHLI_X", "SHLQ_X", "MUL_RX", "MUL_CX", "LOADC_X"]
 DIV_KIND = {"UDIV_R": 0, "UDIV_C": 0, "UREM_R": 1, "UREM_C": 1, "SDIV_R": 2, "SDIV_C": 2,
             "SREM_R": 3, "SREM_C": 3, "SMOD_R": 4, "SMOD_C": 4}
 OPNUM = {n: i for i, n in enumerate(OPS)}
 # handlers longer than a slot live after the table (one extra jump)
-OUT_OF_LINE = {"MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V"}
+OUT_OF_LINE = {"MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V", "MUL_RX", "MUL_CX"}
 
 # scalar registers the core owns (declared clobbered)
 S_TAB, S_TAB_HI = "s40", "s41"   # handler table base
@@ -64,6 +71,7 @@ class Core:
         self.nr = nr
         self.nr1 = nr + 1
         self.sb = 8 * self.nr1  # scratch base
+        self.no_wb = False
 
     def P(self, k, r=0):
         return "v%d" % (k * self.nr1 + r)
@@ -119,7 +127,9 @@ class Core:
         out += ["v_mov_b32 {}, {}".format(self.Y(k), S_K[k]) for k in to_y]
         return out
 
-    def wb(self, limbs=8):  # R[d'] <- X
+    def wb(self, limbs=8):  # R[d'] <- X (nothing in an X form)
+        if self.no_wb:
+            return []
         out = self.field(S_D, 16) + self.idx_on(S_D, ["DST"])
         out += ["v_mov_b32 {}, {}".format(self.P(k), self.X(k)) for k in range(limbs)]
         return out + self.idx_off()
@@ -128,8 +138,23 @@ class Core:
         a, b = ("0", "1") if true_if_vcc else ("1", "0")
         return ["v_cndmask_b32_e64 {}, {}, {}, vcc".format(self.X(0), a, b)]
 
+    # ---- X forms: a' = d' = X (dev_isa.h).  The base handler verbatim minus its write-back
+    # (R[d'] <- X is X <- X when d' = X): the operand reads keep the base forms' GPR-index
+    # patterns (a' = NR reads X through the same indexed src0/src1 as any register).  Forms that
+    # read the first operand from X as a plain VGPR beside an indexed operand faulted on gfx950
+    # under full occupancy (illegal memory accesses, bisected on MI355X), so none are used.
+    def handler_x(self, name):
+        base = name[:-2] if name.endswith("_X") else name[:-1]
+        self.no_wb = True
+        try:
+            return self.handler(base)
+        finally:
+            self.no_wb = False
+
     # ---- handlers: list of instruction lines, ending in a dispatch (or the exit branch)
     def handler(self, name):
+        if name.endswith("X") and name != "EXIT":
+            return self.handler_x(name)
         X, P, Y, S = self.X, self.P, self.Y, self.S
         a_src0 = self.idx_on(S_W0, ["SRC0"])
         a_src1 = self.idx_on(S_W0, ["SRC1"])

@@ -98,3 +98,28 @@ extern "C" int32_t emu_eval(const mh_node* nodes, const uint64_t* offs, uint32_t
     }
     return MH_OK;
 }
+
+// Compile every tape and return the concatenated slot words (test-only: instruction-mix
+// analysis, scripts/isa_mix.py).  *n_words_out is set to the number of u32 words needed; the
+// words are copied when it fits in cap.
+extern "C" int32_t emu_compile_words(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
+                                     const uint32_t* consts, uint32_t n_consts, uint32_t n_vars,
+                                     uint32_t* out, uint64_t cap, uint64_t* n_words_out,
+                                     uint32_t* nrx_out, char* err, int errlen) {
+    std::vector<uint32_t> dconsts, words;
+    std::unordered_map<std::string, uint32_t> dindex;
+    for (uint32_t t = 0; t < n_tapes; ++t) {
+        CompiledTape ct;
+        std::string e;
+        int32_t r = compile_tape(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts,
+                                 n_consts, n_vars, dconsts, dindex, words, ct, e);
+        if (r != MH_OK) {
+            snprintf(err, errlen, "tape %u: %s", t, e.c_str());
+            return r;
+        }
+        if (nrx_out) nrx_out[t] = mh_nrx_of(ct.n_regs);
+    }
+    *n_words_out = words.size();
+    if (words.size() <= cap) memcpy(out, words.data(), words.size() * 4);
+    return MH_OK;
+}

@@ -1,0 +1,84 @@
+"""Static checks of the generated threaded-code asm core (mythril_amd/csrc/gen_asm_core.py).
+
+* every handler fits its 256-byte dispatch slot (assembled with llvm-mc for gfx950);
+* the GPR-index mode is balanced: never left on across a jump or at a handler's end (a stale
+  index would redirect the next handler's plain VGPR operands);
+* every register the core names is a plane register, a declared scratch VGPR or a declared SGPR
+  clobber (checked by the generator itself, exercised here for all three register-file sizes);
+* the opcode table of the generator matches dev_isa.h.
+"""
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mythril_amd",
+                    "csrc")
+sys.path.insert(0, CSRC)
+
+import gen_asm_core as G  # noqa: E402
+
+LLVM_MC = "/opt/rocm/lib/llvm/bin/llvm-mc"
+
+
+def _asm_lines(lines):
+    out = []
+    for ln in lines:
+        ln = (ln.replace("%[ip]", "s39").replace("%[ic0]", "v200").replace("%[ic1]", "v201")
+              .replace("%=", "0"))
+        if ln.endswith(":"):
+            continue
+        if ln.startswith(("s_branch L_", "s_cbranch")):
+            ln = ln.split()[0] + " 0"
+        out.append(ln)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not installed")
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_handlers_fit_their_slots(nr):
+    core = G.Core(nr)
+    for name in G.OPS:
+        if name in G.OUT_OF_LINE:
+            continue
+        src = "\n".join(_asm_lines(core.handler(name))) + "\n"
+        p = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "-show-encoding"],
+                           input=src, capture_output=True, text=True)
+        assert p.returncode == 0, (name, p.stderr[:400])
+        size = sum(len(re.findall(r"0x[0-9a-f]{2}", m))
+                   for m in re.findall(r"encoding: \[(.*?)\]", p.stdout))
+        assert 0 < size <= G.SLOT, (nr, name, size)
+
+
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_gpr_index_mode_is_balanced(nr):
+    core = G.Core(nr)
+    bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
+    for name, lines in bodies:
+        on = False
+        for ln in lines:
+            if ln.startswith("s_set_gpr_idx_on"):
+                assert not on, (name, "nested")
+                on = True
+            elif ln.startswith("s_set_gpr_idx_off"):
+                on = False
+            elif ln.startswith(("s_setpc", "s_branch", "s_cbranch")):
+                assert not on, (name, ln)
+        assert not on, name
+
+
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_registers_are_declared(nr):
+    core = G.Core(nr)
+    G.check_registers(core, core.asm_text(), G.N_SCRATCH)
+
+
+def test_opcode_table_matches_isa_header():
+    src = open(os.path.join(CSRC, "dev_isa.h")).read()
+    body = src[src.index("enum mh_dop"):src.index("D_NUM_ASM")]
+    body = "\n".join(line.split("//")[0] for line in body.splitlines())
+    names = re.findall(r"\b(D_[A-Z0-9_]+)", body)
+    assert [n[2:] for n in names] == G.OPS
