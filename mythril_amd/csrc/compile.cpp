@@ -19,6 +19,7 @@
 // Anything the device path does not cover returns MH_E_UNSUPPORTED so the caller falls back to
 // z3, as get_model's contract requires.
 #include "compile.h"
+#include "exec.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -688,6 +689,135 @@ bool Lowering::lower(std::vector<Val>& vals) {
     return true;
 }
 
+// Host machine for exec.h's step() over one instruction: x = R[0], y = R[1], third operand R[2],
+// result in R[3] (the accumulator).  Folding runs the device's own instruction semantics, so a
+// folded value is bit-identical to what the kernel would have computed in every lane.
+struct FoldMachine {
+    u32 R[4][8];
+    u32 nrx() const { return 3; }
+    void read(u32 r, u32* v) const { std::memcpy(v, R[r], 32); }
+    u32 read0(u32 r) const { return R[r][0]; }
+    void write(u32 r, const u32* v) { std::memcpy(R[r], v, 32); }
+    void iconst(u32, u32* v) const { std::memcpy(v, R[1], 32); }
+    void var(u32, u32* v) const { std::memset(v, 0, 32); }  // never reached: LOADVAR is not folded
+};
+
+bool bool_result(uint8_t op) {
+    switch (op) {
+        case D_EQ_R: case D_BAND: case D_BOR: case D_BXOR: case D_BEQ: case D_BNOT:
+        case D_TRUE: case D_FALSE: case D_BITE: case D_UADD_NOOVFL: case D_UMUL_NOOVFL:
+            return true;
+        default:
+            return op >= D_ULT_R && op <= D_SGE_C;
+    }
+}
+
+// Constant folding and dead-code elimination on the lowered SSA code (before the accumulator
+// pass).  An instruction whose operands are all known constants becomes a LOADC (TRUE / FALSE
+// for a Bool) of its value; a select with a known condition becomes its chosen operand; a known
+// y operand of an op with a *_C form becomes the inline constant (a known x of a commutative or
+// mirrored op likewise, by swapping).  This is what z3's simplify does to mythril's constraints
+// before any solver sees them (laser/smt/bitvec.py, `simplify` calls); nodes whose value does not
+// depend on the assignment are not counted as per-evaluation work (compile_tape's alg_ops).
+// Returns the root's register after aliasing; recomputes the feature bits.
+int fold_constants(Lowering& L, int root_v) {
+    std::vector<VInsn>& code = L.code;
+    const int nv = L.n_vregs;
+    std::vector<char> known(nv, 0);
+    std::vector<u32> val((size_t)nv * 8, 0u);
+    std::vector<int> rep(nv);
+    for (int r = 0; r < nv; ++r) rep[r] = r;
+    auto R = [&](int r) { return r < 0 ? r : rep[r]; };
+    auto K = [&](int r) { return r >= 0 && known[r]; };
+    for (VInsn& v : code) {
+        v.a = R(v.a);
+        v.b = R(v.b);
+        v.c = R(v.c);
+        const uint8_t op = v.op;
+        if (op == D_LOADC) {
+            known[v.d] = 1;
+            std::memcpy(&val[(size_t)v.d * 8], L.pool.data() + 8ull * (uint32_t)v.cidx, 32);
+            continue;
+        }
+        if (op == D_TRUE || op == D_FALSE) {
+            known[v.d] = 1;
+            val[(size_t)v.d * 8] = op == D_TRUE ? 1u : 0u;
+            continue;
+        }
+        if (op == D_LOADVAR || op == D_KECCAK) continue;
+        if (op == D_ITE || op == D_BITE) {  // (cond a, then b, else c)
+            if (K(v.a)) rep[v.d] = (val[(size_t)v.a * 8] & 1u) ? v.b : v.c;
+            continue;
+        }
+        const bool ka = v.a < 0 || K(v.a);
+        const bool kb = v.cidx >= 0 || v.b < 0 || K(v.b);
+        const bool kc = v.c < 0 || K(v.c);
+        if (ka && kb && kc && v.aux <= MH_AUX_MAX) {
+            FoldMachine m;
+            std::memset(m.R, 0, sizeof(m.R));
+            if (v.a >= 0) std::memcpy(m.R[0], &val[(size_t)v.a * 8], 32);
+            if (v.cidx >= 0)
+                std::memcpy(m.R[1], L.pool.data() + 8ull * (uint32_t)v.cidx, 32);
+            else if (v.b >= 0)
+                std::memcpy(m.R[1], &val[(size_t)v.b * 8], 32);
+            if (v.c >= 0) std::memcpy(m.R[2], &val[(size_t)v.c * 8], 32);
+            const u32 w1 = op | ((v.width & 0x1FFu) << 8) | (v.aux << 17);
+            step<F_CPLX | F_KECCAK | F_EVM | F_DIV, true>(m, 0u | 1u << 8 | 3u << 16 | 2u << 24,
+                                                           w1, 0u);
+            u32* z = &val[(size_t)v.d * 8];
+            std::memcpy(z, m.R[3], 32);
+            known[v.d] = 1;
+            if (bool_result(op)) {
+                z[0] &= 1u;
+                for (int k = 1; k < 8; ++k) z[k] = 0;
+                v = VInsn{z[0] ? (uint8_t)D_TRUE : (uint8_t)D_FALSE, v.d, -1, -1, -1, 1, 0, -1, 0};
+            } else {
+                v = VInsn{D_LOADC, v.d, -1, -1, -1, 256, 0, (int)L.const_index(z, 256), 0};
+            }
+            continue;
+        }
+        // a known operand of a pair op becomes the inline constant
+        if (v.cidx < 0 && v.b >= 0 && y_const_ok(op) && op < D_FIRST_COMPLEX) {
+            if (K(v.b)) {
+                v.cidx = (int)L.const_index(&val[(size_t)v.b * 8], 256);
+                v.b = -1;
+            } else if (K(v.a) && (commutes(op) || mirror(op))) {
+                if (!commutes(op)) v.op = mirror(op);
+                v.cidx = (int)L.const_index(&val[(size_t)v.a * 8], 256);
+                v.a = v.b;
+                v.b = -1;
+            }
+        }
+    }
+    root_v = R(root_v);
+    // dead code: everything the root does not read (every op is pure)
+    std::vector<char> used(nv, 0);
+    used[root_v] = 1;
+    std::vector<char> keep(code.size(), 0);
+    for (size_t i = code.size(); i-- > 0;) {
+        const VInsn& v = code[i];
+        if (!used[v.d]) continue;
+        keep[i] = 1;
+        for (int r : {v.a, v.b, v.c})
+            if (r >= 0) used[r] = 1;
+    }
+    std::vector<VInsn> live;
+    live.reserve(code.size());
+    uint32_t feats = 0;
+    for (size_t i = 0; i < code.size(); ++i) {
+        if (!keep[i]) continue;
+        const uint8_t op = code[i].op;
+        if (op >= D_UDIV_R && op <= D_SMOD_C) feats |= F_DIV;
+        else if (op == D_KECCAK) feats |= F_KECCAK;
+        else if (op == D_EXP || op == D_SIGNEXT || op == D_BYTE) feats |= F_EVM;
+        else if (op >= D_FIRST_COMPLEX) feats |= F_CPLX;
+        live.push_back(code[i]);
+    }
+    code.swap(live);
+    L.features = feats;
+    return root_v;
+}
+
 }  // namespace
 
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
@@ -705,18 +835,29 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
         err = L.err;
         return MH_E_UNSUPPORTED;
     }
+    // algorithmic work per evaluation: the nodes whose value depends on the assignment (the
+    // others are folded to constants on the host, fold_constants)
     out.alg_ops = 0;
     out.n_nodes = (uint32_t)n_nodes;
-    for (size_t i = 0; i < n_nodes; ++i) out.alg_ops += op_cost(t[i], t);
+    std::vector<char> dep(n_nodes, 0);
+    for (size_t i = 0; i < n_nodes; ++i) {
+        const mh_node& nd = t[i];
+        if (nd.op == MH_OP_VAR) { dep[i] = 1; continue; }
+        const int ar = arity(nd);
+        const uint32_t ops[3] = {nd.a, nd.b, nd.c};
+        for (int k = 0; k < ar; ++k) dep[i] |= dep[ops[k]];
+        if (dep[i]) out.alg_ops += op_cost(nd, t);
+    }
 
     std::vector<VInsn>& code = L.code;
     const int n_pinned = L.pinned ? (int)n_vars : 0;
     // root: X after the last instruction must hold it
-    const int root_v = L.vreg_of((uint32_t)(n_nodes - 1));
+    int root_v = L.vreg_of((uint32_t)(n_nodes - 1));
     if (root_v < 0) {
         err = "root wider than 256 bits";
         return MH_E_UNSUPPORTED;
     }
+    if (!std::getenv("MH_NO_FOLD")) root_v = fold_constants(L, root_v);
     if (code.empty() || code.back().d != root_v) L.emit(D_NOP, root_v);
     out.features = L.features;
 

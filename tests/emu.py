@@ -46,3 +46,26 @@ class Emulator:
                 v |= int(out[k, j]) << (32 * k)
             vals.append(v)
         return vals, nregs.value
+
+    def n_slots(self, ts: TapeSet) -> int:
+        """Instruction slots the compiler emits for the whole tape set (emu_compile_words)."""
+        f = self.lib.emu_compile_words
+        f.restype = C.c_int32
+        f.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                      C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_char_p,
+                      C.c_int]
+        nodes, offs, consts = ts.flatten()
+        nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        consts = np.ascontiguousarray(consts, dtype=np.uint32)
+        cap = 1 << 20
+        out = np.zeros(cap, dtype=np.uint32)
+        nw = C.c_uint64()
+        nrx = np.zeros(max(len(ts.tapes), 1), dtype=np.uint32)
+        err = C.create_string_buffer(256)
+        r = f(nodes.ctypes.data, offs.ctypes.data, len(ts.tapes), consts.ctypes.data,
+              len(ts.pool.values), ts.n_vars, out.ctypes.data, C.c_uint64(cap), C.byref(nw),
+              nrx.ctypes.data, err, 256)
+        if r != 0:
+            raise EmuError(r, err.value.decode())
+        return int(nw.value) // 2

@@ -227,3 +227,35 @@ def final_storage(pre: Dict[int, int], pairs, values) -> Dict[int, int]:
     for kt, vt in pairs:
         st[int(values[kt])] = int(values[vt])
     return {k: v for k, v in st.items() if v != 0}
+
+
+def lift_constants(ts):
+    """The same tapes with every constant leaf turned into an assignment column holding that
+    constant (one row), so the compiler cannot fold them: the device evaluates every op of a
+    VMTest on registers.  Returns (lifted tapeset, soa [n_cols, 8, 1] u32)."""
+    import numpy as np
+
+    from mythril_amd.tape import Op, Tape, TapeSet
+
+    cols = {}
+    out = TapeSet()
+    for t in ts.tapes:
+        nodes = t.nodes.copy()
+        for i in range(len(nodes)):
+            if int(nodes[i]["op"]) == int(Op.CONST):
+                w = int(nodes[i]["width"])
+                v = ts.pool.values[int(nodes[i]["imm0"])] & ((1 << w) - 1)
+                name = "k%d_%x" % (w, v)
+                if name not in cols:
+                    cols[name] = v
+                    out.var_index[name] = len(out.var_index)
+                nodes[i]["op"] = int(Op.VAR)
+                nodes[i]["imm0"] = out.var_index[name]
+                nodes[i]["imm1"] = 0
+        out.tapes.append(Tape(nodes))
+    soa = np.zeros((max(out.n_vars, 1), 8, 1), dtype=np.uint32)
+    for name, v in cols.items():
+        c = out.var_index[name]
+        for k in range(8):
+            soa[c, k, 0] = (v >> (32 * k)) & 0xFFFFFFFF
+    return out, soa

@@ -57,6 +57,7 @@ def test_handlers_fit_their_slots(nr):
 def test_gpr_index_mode_is_balanced(nr):
     core = G.Core(nr)
     bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
+
     for name, lines in bodies:
         on = False
         for ln in lines:
@@ -82,3 +83,36 @@ def test_opcode_table_matches_isa_header():
     body = "\n".join(line.split("//")[0] for line in body.splitlines())
     names = re.findall(r"\b(D_[A-Z0-9_]+)", body)
     assert [n[2:] for n in names] == G.OPS
+
+
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_indexed_slots_hold_vgprs(nr):
+    """While the GPR-index mode is on, every operand slot it enables (SRC0/SRC1/SRC2/DST) holds
+    a VGPR: the index is defined for VGPR operands only, and an SGPR or constant in an enabled
+    slot is a pattern no handler relies on (memory faults on MI355X were traced to such
+    mixtures)."""
+    core = G.Core(nr)
+    bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
+    bodies += [("fetch", core.fetch_text()), ("commit", core.commit_text())]
+    vgpr = re.compile(r"^v(\d+|\[\d+:\d+\])$")
+    for name, lines in bodies:
+        modes = None
+        for ln in lines:
+            if ln.startswith("s_set_gpr_idx_on"):
+                modes = set(re.search(r"gpr_idx\((.*)\)", ln).group(1).split(","))
+                continue
+            if ln.startswith("s_set_gpr_idx_off"):
+                modes = None
+                continue
+            if modes is None or not ln.startswith("v_"):
+                continue
+            mnem, _, rest = ln.partition(" ")
+            ops = [o.strip() for o in rest.split(",")]
+            dst, srcs = ops[0], ops[1:]
+            if srcs and srcs[0] in ("vcc", "s[62:63]", "s[64:65]") and "_co_" in mnem:
+                srcs = srcs[1:]  # carry-out destination
+            if "DST" in modes:
+                assert vgpr.match(dst), (name, ln)
+            for slot, op in zip(("SRC0", "SRC1", "SRC2"), srcs):
+                if slot in modes:
+                    assert vgpr.match(op.lstrip("-")), (name, ln)

@@ -11,7 +11,7 @@ import pytest
 from mythril_amd.tape import Op, TapeSet
 from oracle import smt_eval
 from tests.emu import EmuError
-from tests.evm_translate import Unsupported, final_storage, vmtest_tapes
+from tests.evm_translate import Unsupported, final_storage, lift_constants, vmtest_tapes
 from tests.fuzz import TapeFuzzer, assignment_soa, soa_row
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -48,6 +48,63 @@ def test_vmtests_through_compiler(emu, mode):
             assert final_storage(pre, pairs, vals) == expected, vec["name"]
         checked += 1
     assert checked >= 300
+
+
+@pytest.mark.parametrize("mode", ["laser", "evm"])
+def test_vmtests_lifted_through_compiler(emu, mode):
+    """The VMTests with every constant lifted into an assignment column: nothing folds, every
+    op runs as device code (the folded variant above checks the host folding)."""
+    checked = 0
+    for vec in VMTESTS:
+        try:
+            ts, pairs, expected, pre = vmtest_tapes(vec, mode)
+        except Unsupported:
+            continue
+        lts, soa = lift_constants(ts)
+        vals = []
+        for i, t in enumerate(ts.tapes):
+            want = int(smt_eval.evaluate(t.nodes, ts.pool.values, []))
+            try:
+                got, _ = emu.eval(lts, i, soa)
+            except EmuError as e:
+                assert mode == "evm" and e.code == -2, (vec["name"], str(e))
+                got = [want]
+            assert got[0] == want, (vec["name"], i)
+            vals.append(got[0])
+        if not (mode == "laser" and vec["name"] in LASER_DIVERGENT):
+            assert final_storage(pre, pairs, vals) == expected, vec["name"]
+        checked += 1
+    assert checked >= 300
+
+
+def test_constant_folding(emu):
+    """Constant-only subtrees fold on the host to the value the device computes; a select with
+    a constant condition becomes its chosen operand; results match the oracle either way."""
+    import random as _r
+
+    rng = _r.Random(77)
+    ts = TapeSet()
+    b = ts.builder()
+    x = b.var("x")
+    k1 = b.const(rng.getrandbits(256), 256)
+    k2 = b.const(rng.getrandbits(256), 256)
+    kk = b.op(Op.BVMUL, b.op(Op.BVADD, k1, k2), b.op(Op.BVUDIV, k1, b.const(7, 256)))
+    kx = b.op(Op.EXTRACT, kk, imm0=159, imm1=32)
+    sel = b.op(Op.ITE, b.op(Op.BVULT, k1, k2), b.op(Op.BVXOR, x, kk), b.op(Op.BVSUB, x, kk))
+    ts.add(b.finish(b.op(Op.BVADD, sel, b.op(Op.ZEXT, kx, imm0=128))))
+    ts.add(b.finish(b.op(Op.AND, b.op(Op.BVULT, x, kk), b.op(Op.EQ, k1, k1))))
+    soa = assignment_soa(rng, ts.n_vars, 16)
+    for i, t in enumerate(ts.tapes):
+        got, _ = emu.eval(ts, i, soa)
+        for r in range(soa.shape[2]):
+            assert got[r] == int(smt_eval.evaluate(t.nodes, ts.pool.values, soa_row(soa, r)))
+    folded = emu.n_slots(ts)
+    os.environ["MH_NO_FOLD"] = "1"
+    try:
+        unfolded = emu.n_slots(ts)
+    finally:
+        del os.environ["MH_NO_FOLD"]
+    assert folded < unfolded, (folded, unfolded)
 
 
 @pytest.mark.parametrize("seed", range(12))

@@ -12,7 +12,7 @@ import pytest
 from mythril_amd import native, synth
 from mythril_amd.tape import Op, TapeSet
 from oracle import smt_eval
-from tests.evm_translate import Unsupported, final_storage, vmtest_tapes
+from tests.evm_translate import Unsupported, final_storage, lift_constants, vmtest_tapes
 from tests.fuzz import TapeFuzzer, assignment_soa, soa_row
 
 pytestmark = pytest.mark.gpu
@@ -74,6 +74,33 @@ def test_vmtests_on_gpu(gpu_ctx, mode):
     assert checked >= 300
 
 
+@pytest.mark.parametrize("mode", ["laser", "evm"])
+def test_vmtests_lifted_on_gpu(gpu_ctx, mode):
+    """The VMTests known answers with every constant lifted into an assignment column, so no op
+    folds on the host: the kernel's own handlers compute every operation of every vector."""
+    checked = 0
+    for vec in VMTESTS:
+        try:
+            ts, pairs, expected, pre = vmtest_tapes(vec, mode)
+        except Unsupported:
+            continue
+        if mode == "evm" and any(max(int(x) for x in t.nodes["width"]) > 256 for t in ts.tapes):
+            continue  # EVM-exact ADDMOD/MULMOD use 512-bit arithmetic: oracle-only vectors
+        lts, soa = lift_constants(ts)
+        ct = gpu_ctx.compile(lts)
+        a = upload(gpu_ctx, soa)
+        vals = []
+        for i, t in enumerate(ts.tapes):
+            got = native.limbs_to_ints(native.eval_values(gpu_ctx, ct, i, a))[0]
+            want = int(smt_eval.evaluate(t.nodes, ts.pool.values, []))
+            assert got == want, (vec["name"], i)
+            vals.append(got)
+        if not (mode == "laser" and vec["name"] in LASER_DIVERGENT):
+            assert final_storage(pre, pairs, vals) == expected, vec["name"]
+        checked += 1
+    assert checked >= 300
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_fuzz_tapes_on_gpu(gpu_ctx, seed):
     rng = random.Random(5000 + seed)
@@ -89,6 +116,39 @@ def test_fuzz_tapes_on_gpu(gpu_ctx, seed):
         for r in range(soa.shape[2]):
             want = int(smt_eval.evaluate(t.nodes, ts.pool.values, soa_row(soa, r)))
             assert got[r] == want, (seed, i, r)
+
+
+def test_immediate_shifts_on_gpu(gpu_ctx):
+    """Every constant amount 1..255 of bvshl / bvlshr, with the operand in a register (a column)
+    and in the accumulator (a sum), result kept in X or written back (used twice): the
+    limb-specialised shift bodies of the asm core against the oracle."""
+    rng = random.Random(31)
+    ts = TapeSet()
+    b = ts.builder()
+    x, y = b.var("x"), b.var("y")
+    s_sum = b.op(Op.BVADD, x, y)
+    for s in range(1, 256):
+        k = b.const(s, 256)
+        for op in (Op.BVSHL, Op.BVLSHR):
+            ts.add(b.finish(b.op(op, x, k)))
+            ts.add(b.finish(b.op(op, s_sum, k)))
+            t = b.op(op, s_sum, k)
+            ts.add(b.finish(b.op(Op.BVADD, b.op(Op.BVXOR, t, y), t)))
+    vals = [0, 1, (1 << 256) - 1, 1 << 255, (1 << 255) - 1] + [rng.getrandbits(256)
+                                                               for _ in range(27)]
+    soa = np.zeros((2, 8, len(vals)), dtype=np.uint32)
+    for r, v in enumerate(vals):
+        w = vals[(r * 7 + 3) % len(vals)]
+        for k in range(8):
+            soa[0, k, r] = (v >> (32 * k)) & 0xFFFFFFFF
+            soa[1, k, r] = (w >> (32 * k)) & 0xFFFFFFFF
+    ct = gpu_ctx.compile(ts)
+    a = upload(gpu_ctx, soa)
+    for i, t in enumerate(ts.tapes):
+        got = native.limbs_to_ints(native.eval_values(gpu_ctx, ct, i, a))
+        for r in range(len(vals)):
+            want = int(smt_eval.evaluate(t.nodes, ts.pool.values, soa_row(soa, r)))
+            assert got[r] == want, (i, r)
 
 
 def test_division_edges_on_gpu(gpu_ctx):
