@@ -97,7 +97,7 @@ uint8_t mirror(uint8_t op) {  // op(a, b) == mirror(op)(b, a), or 0
 
 // Diagnostic switch: MH_XFORM_MASK (env, default all) enables X forms per group --
 // 1 add/sub R, 2 add/sub C, 4 logic R, 8 logic C, 16 eq, 32 compares R, 64 compares C,
-// 128 immediate shifts, 256 mul, 512 loadc.
+// 256 mul, 512 loadc.
 bool xform_enabled(uint32_t op) {
     static const uint32_t mask = [] {
         const char* e = std::getenv("MH_XFORM_MASK");
@@ -110,7 +110,6 @@ bool xform_enabled(uint32_t op) {
         case D_AND_R: case D_OR_R: case D_XOR_R: g = 4; break;
         case D_AND_C: case D_OR_C: case D_XOR_C: g = 8; break;
         case D_EQ_R: case D_EQ_C: g = 16; break;
-        case D_LSHRI: case D_SHLI: case D_SHLQ: g = 128; break;
         case D_MUL_R: case D_MUL_C: g = 256; break;
         case D_LOADC: g = 512; break;
         default:
@@ -229,7 +228,7 @@ struct Lowering {
     int ashr_imm(int r, uint32_t s, uint32_t w) {
         const uint32_t sp = s < w - 1 ? s : w - 1;
         int u = emit(D_XOR_R, r, -1, -1, 256, 0, bit_const(w - 1));
-        if (sp) u = emit(D_LSHRI, u, -1, -1, 256, sp);
+        if (sp) u = shr_imm(u, sp);
         u = emit(D_SUB_R, u, -1, -1, 256, 0, bit_const(w - 1 - sp));
         return masked(u, w);
     }
@@ -324,14 +323,22 @@ struct Lowering {
         return emit(op, a, b, -1, width);
     }
 
-    // logical shift left by a uniform amount s (0 < s < 256), result mod 2^256
+    // logical shift left by a uniform amount s (0 < s < 256), result mod 2^256: the limb-count
+    // op D_SHL0 + p with the alignbit field (dev_isa.h)
     int shl_imm(int r, uint32_t s) {
-        return emit((s & 31) ? D_SHLI : D_SHLQ, r, -1, -1, 256, s);
+        const uint32_t q = s >> 5, b = s & 31;
+        if (b) return emit((uint8_t)(D_SHL0 + q), r, -1, -1, 256, 32 - b);
+        return emit((uint8_t)(D_SHL0 + q - 1), r, -1, -1, 256, 0);
+    }
+
+    // logical shift right by a uniform amount s (0 < s < 256)
+    int shr_imm(int r, uint32_t s) {
+        return emit((uint8_t)(D_SHR0 + (s >> 5)), r, -1, -1, 256, s & 31);
     }
 
     // bits [lo, lo + w) of a wa-bit canonical value
     int extract(int r, uint32_t lo, uint32_t w, uint32_t wa) {
-        if (lo) r = emit(D_LSHRI, r, -1, -1, 256, lo);
+        if (lo) r = shr_imm(r, lo);
         if (lo + w < wa) r = masked(r, w);
         return r;
     }
@@ -492,7 +499,7 @@ bool Lowering::lower(std::vector<Val>& vals) {
                     } else if (s == 0) {
                         out.vreg = a;
                     } else if (nd.op == MH_OP_BVLSHR) {
-                        out.vreg = emit(D_LSHRI, a, -1, -1, 256, s);
+                        out.vreg = shr_imm(a, s);
                     } else {
                         out.vreg = masked(shl_imm(a, s), w);
                     }

@@ -52,9 +52,6 @@ enum mh_dop : uint8_t {
     D_ITEC,   // cond = R[a'] limb 0, then = R[b], else = R[c]
     D_BITE,   // Bool select: cond = R[a'], then = R[b] limb 0, else = R[c] limb 0
     D_LOADC,  // X = inline constant
-    D_LSHRI,  // X = R[a'] >> aux          (aux < 256)
-    D_SHLI,   // X = R[a'] << aux mod 2^256 (aux % 32 != 0)
-    D_SHLQ,   // X = R[a'] << aux mod 2^256 (aux % 32 == 0)
     D_MUL_R, D_MUL_C,  // X = R[a'] * y mod 2^256 (host masks)
     D_SHL_V, D_LSHR_V, D_ASHR_V,  // 256-bit shifts by y (per lane; >= 256 saturates to 0 / fill)
     // 256-bit division family, SMT-LIB semantics (x / 0 = 2^256 - 1, x % 0 = x, signed forms by
@@ -69,7 +66,13 @@ enum mh_dop : uint8_t {
     D_EQ_RX, D_EQ_CX, D_ULT_RX, D_ULT_CX, D_UGT_RX, D_UGT_CX, D_ULE_RX, D_ULE_CX,
     D_UGE_RX, D_UGE_CX, D_SLT_RX, D_SLT_CX, D_SGT_RX, D_SGT_CX, D_SLE_RX, D_SLE_CX,
     D_SGE_RX, D_SGE_CX,
-    D_LSHRI_X, D_SHLI_X, D_SHLQ_X, D_MUL_RX, D_MUL_CX, D_LOADC_X,
+    D_MUL_RX, D_MUL_CX, D_LOADC_X,
+    // immediate shifts, one op per limb count (the limb offsets are static in the handler; the
+    // result is always written back, d' = X being the harmless X -> X):
+    //   D_SHR0 + q: X = R[a'] >> (32 q + aux)                        aux < 32
+    //   D_SHL0 + p: X = R[a'] << (aux ? 32 p + 32 - aux : 32 (p + 1)) mod 2^256, aux < 32
+    D_SHR0, D_SHR1, D_SHR2, D_SHR3, D_SHR4, D_SHR5, D_SHR6, D_SHR7,
+    D_SHL0, D_SHL1, D_SHL2, D_SHL3, D_SHL4, D_SHL5, D_SHL6, D_SHL7,
     D_NUM_ASM,
     // ---- C++ (exec.h); y = R[b] or the inline constant (F_YC)
     D_FIRST_COMPLEX = 112,
@@ -89,9 +92,6 @@ static_assert(D_NUM_ASM <= D_FIRST_COMPLEX, "asm opcode space");
 static inline unsigned mh_base_op(unsigned op) {
     if (op >= D_ADD_RX && op <= D_SGE_CX) return D_ADD_R + (op - D_ADD_RX);
     switch (op) {
-        case D_LSHRI_X: return D_LSHRI;
-        case D_SHLI_X: return D_SHLI;
-        case D_SHLQ_X: return D_SHLQ;
         case D_MUL_RX: return D_MUL_R;
         case D_MUL_CX: return D_MUL_C;
         case D_LOADC_X: return D_LOADC;
@@ -103,9 +103,6 @@ static inline unsigned mh_base_op(unsigned op) {
 static inline unsigned mh_xform(unsigned op) {
     if (op >= D_ADD_R && op <= D_SGE_C) return D_ADD_RX + (op - D_ADD_R);
     switch (op) {
-        case D_LSHRI: return D_LSHRI_X;
-        case D_SHLI: return D_SHLI_X;
-        case D_SHLQ: return D_SHLQ_X;
         case D_MUL_R: return D_MUL_RX;
         case D_MUL_C: return D_MUL_CX;
         case D_LOADC: return D_LOADC_X;

@@ -225,8 +225,19 @@ MH_FN u32 step(M& m, u32 w0, u32 w1, u32 ip) {
             if constexpr (SIMPLE) z[0] = (x[0] & 1u) ? (y[0] & 1u) : (m.read0(c) & 1u);
             break;
         case D_LOADC: if constexpr (SIMPLE) copy8(z, y); break;
-        case D_LSHRI: if constexpr (SIMPLE) shr256_u(x, aux, z, 0u); break;
-        case D_SHLI: case D_SHLQ: if constexpr (SIMPLE) shl256_u(x, aux, z); break;
+        case D_SHR0: case D_SHR1: case D_SHR2: case D_SHR3: case D_SHR4: case D_SHR5:
+        case D_SHR6: case D_SHR7:
+            if constexpr (SIMPLE) shr256_u(x, 32u * (op - D_SHR0) + (aux & 31u), z, 0u);
+            break;
+        case D_SHL0: case D_SHL1: case D_SHL2: case D_SHL3: case D_SHL4: case D_SHL5:
+        case D_SHL6: case D_SHL7:
+            if constexpr (SIMPLE) {
+                const u32 p = op - D_SHL0, f = aux & 31u;
+                const u32 s = f ? 32u * p + 32u - f : 32u * (p + 1u);
+                if (s >= 256u) zero8(z);
+                else shl256_u(x, s, z);
+            }
+            break;
         case D_MUL_R: case D_MUL_C: if constexpr (SIMPLE) mul_lo256(x, y, z); break;
         case D_SHL_V: if constexpr (SIMPLE) bvshl_v(x, shift_amount(y), z, 256); break;
         case D_LSHR_V: if constexpr (SIMPLE) bvlshr_v(x, shift_amount(y), z, 256); break;

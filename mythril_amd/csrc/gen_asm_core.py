@@ -20,6 +20,13 @@ select or a VMEM operand inside the core; VCC is only used as carry/mask (no ali
 statement opens with s_nop so the VGPRs the compiler wrote just before are safe to readlane.
 Every handler ends with s_set_gpr_idx_off before the next dispatch.
 
+GPR-index rule (measured on MI355X, tests/test_asm_core.py checks the static half): an index taken
+from the instruction word (S_W0 / S_B / S_D) enables ONE operand slot, and every enabled slot
+holds a VGPR.  Handlers that read two indexed sources at static limb offsets under an S_W0 index
+(SRC0|SRC1), or that put a constant in an enabled slot, returned wrong values, memory faults or
+hangs -- but only at >= 2 waves per SIMD (1024+ workgroups), never in small parity runs, so any
+new handler is also checked at full occupancy (scripts/diag_modes.py against a known-good build).
+
     python3 gen_asm_core.py > asm_core.inc      (run by the Makefile)
 """
 import sys
@@ -34,7 +41,7 @@ OPS = ["EXIT", "NOP",
        "EQ_R", "EQ_C", "ULT_R", "ULT_C", "UGT_R", "UGT_C", "ULE_R", "ULE_C", "UGE_R", "UGE_C",
        "SLT_R", "SLT_C", "SGT_R", "SGT_C", "SLE_R", "SLE_C", "SGE_R", "SGE_C",
        "BAND", "BOR", "BXOR", "BEQ", "BNOT", "TRUE", "FALSE",
-       "ITE", "ITEC", "BITE", "LOADC", "LSHRI", "SHLI", "SHLQ",
+       "ITE", "ITEC", "BITE", "LOADC",
        "MUL_R", "MUL_C", "SHL_V", "LSHR_V", "ASHR_V",
        "UDIV_R", "UDIV_C", "UREM_R", "UREM_C", "SDIV_R", "SDIV_C", "SREM_R", "SREM_C",
        "SMOD_R", "SMOD_C",
@@ -44,7 +51,8 @@ OPS = ["EXIT", "NOP",
        "EQ_RX", "EQ_CX", "ULT_RX", "ULT_CX", "UGT_RX", "UGT_CX", "ULE_RX", "ULE_CX",
        "UGE_RX", "UGE_CX", "SLT_RX", "SLT_CX", "SGT_RX", "SGT_CX", "SLE_RX", "SLE_CX",
        "SGE_RX", "SGE_CX",
-       "LSHRI_X", "SHLI_X", "SHLQ_X", "MUL_RX", "MUL_CX", "LOADC_X"]
+       "MUL_RX", "MUL_CX", "LOADC_X"] + \
+      ["SHR%d" % q for q in range(8)] + ["SHL%d" % q for q in range(8)]
 DIV_KIND = {"UDIV_R": 0, "UDIV_C": 0, "UREM_R": 1, "UREM_C": 1, "SDIV_R": 2, "SDIV_C": 2,
             "SREM_R": 3, "SREM_C": 3, "SMOD_R": 4, "SMOD_C": 4}
 OPNUM = {n: i for i, n in enumerate(OPS)}
@@ -294,29 +302,26 @@ class Core:
         if name == "LOADC":
             body = self.consts() + ["v_mov_b32 {}, {}".format(X(k), S_K[k]) for k in range(8)]
             return body + self.wb() + self.dispatch(5)
-        if name in ("LSHRI", "SHLI", "SHLQ"):
-            body = ["s_lshr_b32 {}, {}, 17".format(S_L, S_W1),
-                    "s_lshr_b32 {}, {}, 5".format(S_Q, S_L),
-                    "s_and_b32 {}, {}, 31".format(S_R, S_L)]
-            if name == "LSHRI":  # S0..7 = x, S8..16 = 0; X_k = alignbit(S[k+q+1], S[k+q], r)
-                body += a_src0 + ["v_mov_b32 {}, {}".format(S(k), P(k)) for k in range(8)] + off
-                body += ["v_mov_b32 {}, 0".format(S(j)) for j in range(8, 17)]
-                body += self.idx_on(S_Q, ["SRC0", "SRC1"])
-                body += ["v_alignbit_b32 {}, {}, {}, {}".format(X(k), S(k + 1), S(k), S_R)
-                         for k in range(8)]
-            else:  # S0..8 = 0, S9..16 = x; idx = 8 - q
-                body += ["v_mov_b32 {}, 0".format(S(j)) for j in range(0, 9)]
-                body += a_src0 + ["v_mov_b32 {}, {}".format(S(9 + k), P(k)) for k in range(8)] + off
-                body += ["s_sub_u32 {}, 8, {}".format(S_Q, S_Q)]
-                if name == "SHLI":  # X_k = alignbit(S[9+k-q], S[8+k-q], 32 - r)
-                    body += ["s_sub_u32 {}, 32, {}".format(S_R, S_R)]
-                    body += self.idx_on(S_Q, ["SRC0", "SRC1"])
-                    body += ["v_alignbit_b32 {}, {}, {}, {}".format(X(k), S(k + 1), S(k), S_R)
-                             for k in range(8)]
-                else:  # X_k = S[9+k-q]
-                    body += self.idx_on(S_Q, ["SRC0"])
-                    body += ["v_mov_b32 {}, {}".format(X(k), S(k + 1)) for k in range(8)]
-            body += off
+        if name[:3] in ("SHR", "SHL") and name[3:].isdigit():
+            # immediate shift by q limbs + the alignbit field aux (dev_isa.h D_SHR0 / D_SHL0):
+            # the limbs that reach the result are copied out of R[a'] under the SRC0 index (the
+            # same single-mode pattern as every other handler), then combined with static limb
+            # offsets, no index
+            q = int(name[3:])
+            body = ["s_lshr_b32 {}, {}, 17".format(S_R, S_W1)]
+            body += a_src0
+            if name.startswith("SHR"):  # S(j) = limb j for j >= q, S(8) = 0
+                body += ["v_mov_b32 {}, {}".format(S(j), P(j)) for j in range(q, 8)] + off
+                body.append("v_mov_b32 {}, 0".format(S(8)))
+                for k in range(0, 8 - q):
+                    body.append("v_alignbit_b32 {}, {}, {}, {}".format(X(k), S(k + q + 1), S(k + q), S_R))
+                body += ["v_mov_b32 {}, 0".format(X(k)) for k in range(8 - q, 8)]
+            else:  # S(j + 1) = limb j for j <= 7 - q, S(0) = 0
+                body += ["v_mov_b32 {}, {}".format(S(j + 1), P(j)) for j in range(0, 8 - q)] + off
+                body.append("v_mov_b32 {}, 0".format(S(0)))
+                for k in range(q, 8):  # X(k) = alignbit(limb(k - q), limb(k - q - 1), field)
+                    body.append("v_alignbit_b32 {}, {}, {}, {}".format(X(k), S(k - q + 1), S(k - q), S_R))
+                body += ["v_mov_b32 {}, 0".format(X(k)) for k in range(0, q)]
             return body + self.wb() + self.dispatch(1)
         if name in ("MUL_R", "MUL_C"):
             # product scanning: column k of x*y accumulated in (c1:c0) = S16:S17 by
