@@ -255,6 +255,18 @@ def test_full_size_properties(gpu_ctx):
     for t in rng.sample(list(hit_tapes), min(300, len(hit_tapes))):
         w = smt_eval.gen_assignment(seed, ts.n_vars, int(fh[t]))
         assert smt_eval.evaluate(ts.tapes[t].nodes, ts.pool.values, w), t
+    # exact counts and first hits of a tape sample at full occupancy (1024 workgroups), by the
+    # C oracle over every row: asm-core defects that only show with >= 2 waves per SIMD
+    from mythril_amd.tape import TapeSet as _TS
+    from oracle import ctape
+
+    pick = sorted(rng.sample(range(len(ts.tapes)), 32))
+    sub = _TS(ts.var_names)
+    sub.pool = ts.pool
+    sub.tapes = [ts.tapes[t] for t in pick]
+    cnt, first = ctape.count(sub, seed, 0, rows, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(hc[pick], cnt), "hit counts differ from the C oracle"
+    assert np.array_equal(fh[pick], first), "first hits differ from the C oracle"
     # a no-hit tape really has no witness in a sampled prefix
     for t in rng.sample([i for i in range(len(ts.tapes)) if fh[i] == native.NO_HIT],
                         min(20, int((fh == native.NO_HIT).sum()))):
