@@ -324,27 +324,35 @@ class Core:
                 body += ["v_mov_b32 {}, 0".format(X(k)) for k in range(0, q)]
             return body + self.wb() + self.dispatch(1)
         if name in ("MUL_R", "MUL_C"):
-            # product scanning: column k of x*y accumulated in (c1:c0) = S16:S17 by
-            # v_mad_u64_u32 (carry-out to VCC folded into c2 = S18); x copied to S8..S15 so the
-            # result can go straight to X even when x is X
+            # product scanning: column k of x*y accumulated by v_mad_u64_u32 into a 64-bit pair
+            # that alternates between A = S16:S17 and B = S18:S19; the carry-outs of column k
+            # (VCC) are counted straight into the OTHER pair's high word, which the column's first
+            # v_addc initialises, so the next column starts as (carries : this column's high word)
+            # with one move.  x is copied to S8..S15 so the result can go straight to X even
+            # when x is X.
             reg = name == "MUL_R"
             body = self.y_reg() if reg else self.consts()
             yv = (lambda j: Y(j)) if reg else (lambda j: S_K[j])
             body += a_src0 + ["v_mov_b32 {}, {}".format(S(8 + k), P(k)) for k in range(8)] + off
-            acc = "v[{}:{}]".format(self.sb + 16, self.sb + 17)
-            c0, c1, c2 = S(16), S(17), S(18)
-            body.append("v_mad_u64_u32 {}, vcc, {}, {}, 0".format(acc, S(8), yv(0)))
-            body += ["v_mov_b32 {}, {}".format(X(0), c0), "v_mov_b32 {}, 0".format(c2)]
-            for k in range(1, 8):
-                # shift the column accumulator: (c2:c1:c0) >>= 32
-                body += ["v_mov_b32 {}, {}".format(c0, c1), "v_mov_b32 {}, {}".format(c1, c2)]
-                if k < 7:
-                    body.append("v_mov_b32 {}, 0".format(c2))
+            pair = ["v[{}:{}]".format(self.sb + 16, self.sb + 17),
+                    "v[{}:{}]".format(self.sb + 18, self.sb + 19)]
+            lo, hi = [S(16), S(18)], [S(17), S(19)]
+            for k in range(8):
+                cur, nxt = k & 1, 1 - (k & 1)
                 for i in range(k + 1):
-                    body.append("v_mad_u64_u32 {0}, vcc, {1}, {2}, {0}".format(acc, S(8 + i), yv(k - i)))
-                    if k < 7:
-                        body.append("v_addc_co_u32 {0}, vcc, 0, {0}, vcc".format(c2))
-                body.append("v_mov_b32 {}, {}".format(X(k), c0))
+                    addend = "0" if k == 0 else pair[cur]
+                    body.append("v_mad_u64_u32 {}, vcc, {}, {}, {}".format(
+                        pair[cur], S(8 + i), yv(k - i), addend))
+                    if 0 < k < 7:
+                        if i == 0:
+                            body.append("v_addc_co_u32 {}, vcc, 0, 0, vcc".format(hi[nxt]))
+                        else:
+                            body.append("v_addc_co_u32 {0}, vcc, 0, {0}, vcc".format(hi[nxt]))
+                body.append("v_mov_b32 {}, {}".format(X(k), lo[cur]))
+                if k < 7:
+                    body.append("v_mov_b32 {}, {}".format(lo[nxt], hi[cur]))
+                if k == 0:
+                    body.append("v_mov_b32 {}, 0".format(hi[nxt]))
             return body + self.wb() + self.dispatch(1 if reg else 5)
         if name in ("LSHR_V", "ASHR_V", "SHL_V"):
             # per-lane amount s = y (>= 256 saturates); t = x in S8..S15; 3-stage limb select
