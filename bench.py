@@ -46,10 +46,16 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tapes", type=int, default=None, help="default: spec n_tapes (10^4)")
-    ap.add_argument("--rows-per-gpu", type=int, default=1 << 23)
+    ap.add_argument("--rows-per-gpu", type=int, default=None,
+                    help="default 2^23 (plain), 2^20 (keccak variant)")
+    ap.add_argument("--variant", choices=["plain", "keccak"], default="plain",
+                    help="keccak: SURVEY §8d's keccak variant (one keccak256 of a 512-bit "
+                         "input per tape); the headline line is the plain config 5")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.rows_per_gpu is None:
+        args.rows_per_gpu = 1 << 20 if args.variant == "keccak" else 1 << 23
 
     import torch
     import torch.distributed as dist
@@ -67,7 +73,7 @@ def main() -> None:
 
     spec = synth.load_spec()
     t0 = time.time()
-    ts = synth.generate(args.tapes)
+    ts = synth.generate(args.tapes, keccak=args.variant == "keccak")
     n_tapes = len(ts.tapes)
     ctx = native.Context(local_rank)
     ctx.set_stream(stream.cuda_stream)
@@ -153,9 +159,11 @@ def main() -> None:
         "dtype": "u32",
         "data": "synthetic (seeded config-5 tapes, counter-based PRNG assignments)",
         "config": {
-            "workload": "synthetic config 5: %d random 256-bit constraint tapes x %d "
-                        "assignments per GPU (2^26 total at 8 GPUs), throughput mode"
-                        % (n_tapes, rows),
+            "workload": "synthetic config 5%s: %d random 256-bit constraint tapes x %d "
+                        "assignments per GPU, throughput mode"
+                        % (" (keccak variant: + one keccak256 of 512 bits per tape)"
+                           if args.variant == "keccak" else "", n_tapes, rows),
+            "variant": args.variant,
             "tapes": n_tapes,
             "rows_per_gpu": rows,
             "vars": ts.n_vars,

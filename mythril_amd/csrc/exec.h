@@ -22,6 +22,33 @@ namespace mh {
 // 136-byte block.  Every byte position is wave-uniform: piece boundaries come from the tape.
 MH_FN void keccak_pieces(const u32* P0, const u32* P1, const u32* P2, u32 n0, u32 n1, u32 n2,
                          u32* z) {
+    if (n0 == 32u && n2 == 0u && (n1 == 0u || n1 == 32u)) {  // wave-uniform
+        // the shapes LASER produces (keccak of one word; of word . word, the mapping slot):
+        // whole big-endian words, so every state word is a byte-swapped limb at a static place
+        u64 st[25];
+#pragma unroll
+        for (int i = 0; i < 25; ++i) st[i] = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            st[t] = (u64)bswap32(P0[7 - 2 * t]) | ((u64)bswap32(P0[6 - 2 * t]) << 32);
+        if (n1 == 32u) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                st[4 + t] = (u64)bswap32(P1[7 - 2 * t]) | ((u64)bswap32(P1[6 - 2 * t]) << 32);
+            st[8] = 0x01ull;
+        } else {
+            st[4] = 0x01ull;
+        }
+        st[16] |= 0x8000000000000000ull;  // byte 135 of the 136-byte block
+        keccak_f1600(st);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = 7 - k;
+            const u32 wv = (i & 1) ? (u32)(st[i >> 1] >> 32) : (u32)st[i >> 1];
+            z[k] = bswap32(wv);
+        }
+        return;
+    }
     u32 pv[24];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { pv[k] = P0[k]; pv[8 + k] = P1[k]; pv[16 + k] = P2[k]; }

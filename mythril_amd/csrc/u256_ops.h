@@ -7,7 +7,8 @@
 // flow would serialise the wave.
 //
 // The functions are __host__ __device__ so tests/native/emu.cpp can run the same code on the
-// host CPU (unit test of the limb algorithms only; the product library has no host evaluator).
+// host CPU: the test emulator, and the tape compiler's constant folding (compile.cpp), which
+// evaluates constant-only instructions with the device's own semantics.
 #pragma once
 #include <stdint.h>
 
@@ -676,16 +677,29 @@ MH_FN void evm_byte(const u32* ii, const u32* x, u32* z) {
 // ---- Keccak-f[1600] ----------------------------------------------------------------------------
 MH_FN u64 rotl64(u64 x, int n) { return n ? ((x << n) | (x >> (64 - n))) : x; }
 
+// Keccak-f[1600] round constants.  On the device a __constant__ table read with a wave-uniform
+// index (scalar loads); a local array indexed by the loop counter lived in scratch memory.
+#define MH_KECCAK_RC                                                                              \
+    {0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull, \
+     0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull, \
+     0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull, \
+     0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull, \
+     0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull, \
+     0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull}
+#if defined(__HIPCC__)
+__constant__ static const u64 kKeccakRCDev[24] = MH_KECCAK_RC;
+#endif
+static const u64 kKeccakRCHost[24] = MH_KECCAK_RC;
+
+MH_FN u64 keccak_rc(int round) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return kKeccakRCDev[round];
+#else
+    return kKeccakRCHost[round];
+#endif
+}
+
 MH_FN void keccak_f1600(u64* a) {
-    const u64 RC[24] = {
-        0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull,
-        0x8000000080008000ull, 0x000000000000808Bull, 0x0000000080000001ull,
-        0x8000000080008081ull, 0x8000000000008009ull, 0x000000000000008Aull,
-        0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
-        0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull,
-        0x8000000000008003ull, 0x8000000000008002ull, 0x8000000000000080ull,
-        0x000000000000800Aull, 0x800000008000000Aull, 0x8000000080008081ull,
-        0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
 #pragma unroll 1
     for (int round = 0; round < 24; ++round) {
         u64 c[5], d[5];
@@ -713,7 +727,7 @@ MH_FN void keccak_f1600(u64* a) {
             a[y + 3] = b3 ^ (~b4 & b0);
             a[y + 4] = b4 ^ (~b0 & b1);
         }
-        a[0] ^= RC[round];
+        a[0] ^= keccak_rc(round);
     }
 }
 

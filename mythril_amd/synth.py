@@ -56,7 +56,10 @@ def _weighted(rng: SplitMix64, items: List[tuple]) -> str:
     return items[-1][0]
 
 
-def gen_tape(ts: TapeSet, tape_id: int, spec: Optional[Dict] = None) -> int:
+def gen_tape(ts: TapeSet, tape_id: int, spec: Optional[Dict] = None, keccak: bool = False) -> int:
+    """One config-5 tape.  keccak=True is SURVEY §8d's keccak variant: the same program plus one
+    keccak256 of a 512-bit (word . word) input, the mapping-slot shape of
+    keccak_function_manager.py, compared against a pool constant and conjoined at the root."""
     spec = spec or load_spec()
     rng = SplitMix64(spec["seed_base"] + tape_id)
     b = ts.builder()
@@ -140,6 +143,11 @@ def gen_tape(ts: TapeSet, tape_id: int, spec: Optional[Dict] = None) -> int:
             y, x = pop(), pop()
             stack.append(b.op(op, x, y))
             done += 1
+    if keccak:  # drawn after the main program, so the plain variant's tapes are unchanged
+        key = pop()
+        slot = var_nodes[rng.below(len(var_nodes))]
+        h = b.op(Op.KECCAK, b.op(Op.CONCAT, key, slot))
+        bools.append(compare(h, leaf()))
     # every remaining value feeds a comparison so the whole program is live
     while stack:
         bools.append(compare(stack.pop(), leaf()))
@@ -151,11 +159,11 @@ def gen_tape(ts: TapeSet, tape_id: int, spec: Optional[Dict] = None) -> int:
     return ts.add(b.finish(root))
 
 
-def generate(n_tapes: Optional[int] = None, first: int = 0, spec: Optional[Dict] = None
-             ) -> TapeSet:
+def generate(n_tapes: Optional[int] = None, first: int = 0, spec: Optional[Dict] = None,
+             keccak: bool = False) -> TapeSet:
     spec = spec or load_spec()
     n = spec["n_tapes"] if n_tapes is None else n_tapes
     ts = TapeSet(spec["vars"])
     for t in range(first, first + n):
-        gen_tape(ts, t, spec)
+        gen_tape(ts, t, spec, keccak=keccak)
     return ts

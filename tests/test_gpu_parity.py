@@ -297,3 +297,19 @@ def test_unsupported_and_invalid(gpu_ctx):
     a = gpu_ctx.assignments(4, 16)
     with pytest.raises(native.SieveError):
         native.run(gpu_ctx, ct, a, row_first=10, row_count=10)
+
+
+def test_keccak_variant_counts_on_gpu(gpu_ctx):
+    """SURVEY §8d's keccak variant (one keccak256 of a 512-bit input per tape): exact per-tape
+    counts and first hits against the C oracle, at a size that fills the chip."""
+    from oracle import ctape
+
+    ts = synth.generate(48, keccak=True)
+    seed, rows = synth.load_spec()["assignment_seed"], 1 << 16
+    ct = gpu_ctx.compile(ts)
+    a = gpu_ctx.assignments(ts.n_vars, rows)
+    a.generate(seed, 0)
+    fh, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    cnt, first = ctape.count(ts, seed, 0, rows, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(hc, cnt)
+    assert np.array_equal(fh, first)
