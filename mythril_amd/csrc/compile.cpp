@@ -672,15 +672,40 @@ bool Lowering::lower(std::vector<Val>& vals) {
                 if (chunks.size() > 3) return fail("keccak input of more than 3 chunks");
                 uint32_t total = 0;
                 for (auto& ch : chunks) total += ch.bits / 8;
-                if (total > 135) return fail("multi-block keccak");
+                if (total == 0 || total > 96) return fail("keccak input longer than 96 bytes");
                 features |= F_KECCAK;
-                uint32_t w1 = D_KECCAK;
-                for (size_t k = 0; k < chunks.size(); ++k)
-                    w1 |= (chunks[k].bits / 8) << (8 + 6 * k);
-                w1 |= (uint32_t)chunks.size() << 26;
-                VInsn v{D_KECCAK, fresh(), chunks[0].vreg,
-                        chunks.size() > 1 ? chunks[1].vreg : -1,
-                        chunks.size() > 2 ? chunks[2].vreg : -1, 256, 0, -1, w1};
+                // re-cut the message (big-endian bytes of the chunks, in order) into LEFT-aligned
+                // 32-byte words and put the 0x01 pad byte in place, so the device absorbs whole
+                // words at static state positions (exec.h keccak_words)
+                const uint32_t nw = (total + 31) / 32;
+                std::vector<int> words;
+                for (uint32_t i = 0; i < nw; ++i) {
+                    int word = -1;
+                    uint32_t o = 0;
+                    for (const Piece& ch : chunks) {
+                        const uint32_t nb = ch.bits / 8;
+                        if (o < 32 * i + 32 && o + nb > 32 * i) {
+                            const int sh = (int)(32 * i + 32) - (int)(o + nb);  // bytes left
+                            int part = ch.vreg;
+                            if (sh > 0) part = shl_imm(part, 8u * (uint32_t)sh);
+                            else if (sh < 0) part = shr_imm(part, 8u * (uint32_t)(-sh));
+                            word = word < 0 ? part : emit(D_OR_R, word, part, -1);
+                        }
+                        o += nb;
+                    }
+                    words.push_back(word);
+                }
+                const uint32_t rem = total % 32;
+                if (rem) {  // pad byte right after the message, inside the last word
+                    uint32_t pad[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    const uint32_t bit = 8 * (31 - rem);
+                    pad[bit >> 5] = 1u << (bit & 31);
+                    words.back() = emit(D_OR_R, words.back(), -1, -1, 256, 0,
+                                        (int)const_index(pad, 256));
+                }
+                const uint32_t w1 = D_KECCAK | (nw << 8) | ((rem ? 0u : 1u) << 10);
+                VInsn v{D_KECCAK, fresh(), words[0], nw > 1 ? words[1] : -1,
+                        nw > 2 ? words[2] : -1, 256, 0, -1, w1};
                 code.push_back(v);
                 out.vreg = v.d;
                 break;

@@ -18,8 +18,8 @@
 //   w1 = op | width << 8 | aux << 17 | F_YC << 31
 //        width 1..256 (9 bits); aux 14 bits: shift amount, SEXT source width, LOADVAR column
 //        F_YC (complex ops only): y is the inline constant rather than R[b]
-//   D_KECCAK: w1 = op | n0 << 8 | n1 << 14 | n2 << 20 | npieces << 26
-//             (message = X (n0 bytes) | R[b] (n1) | R[c] (n2), big-endian bytes)
+//   D_KECCAK: w1 = op | nw << 8 | full << 10: message = nw (1..3) left-aligned 32-byte words
+//             X, R[b], R[c] (big-endian bytes, 0x01 pad already in place unless full = 1)
 // Ops below D_FIRST_COMPLEX run in the hand-written assembly core (asm_core.inc, threaded
 // code: one computed jump per instruction); the others in C++ (exec.h).  Narrow signed
 // compares, sign extension and arithmetic shifts are lowered by the host onto asm ops

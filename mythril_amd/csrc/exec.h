@@ -18,65 +18,29 @@
 
 namespace mh {
 
-// Keccak-256 of up to three byte-aligned pieces (big-endian byte order within each piece), one
-// 136-byte block.  Every byte position is wave-uniform: piece boundaries come from the tape.
-MH_FN void keccak_pieces(const u32* P0, const u32* P1, const u32* P2, u32 n0, u32 n1, u32 n2,
-                         u32* z) {
-    if (n0 == 32u && n2 == 0u && (n1 == 0u || n1 == 32u)) {  // wave-uniform
-        // the shapes LASER produces (keccak of one word; of word . word, the mapping slot):
-        // whole big-endian words, so every state word is a byte-swapped limb at a static place
-        u64 st[25];
+// Keccak-256 of a message of nw (1..3) LEFT-aligned 32-byte words W0, W1, W2 (big-endian byte
+// order, the host has already cut the message into words and placed the 0x01 pad byte when the
+// message ends inside a word; full = the message ends on a word boundary, so the pad starts the
+// next word).  One 136-byte block; every state position is static, so no byte gathering.
+MH_FN void keccak_absorb_word(u64* st, const u32* W) {
 #pragma unroll
-        for (int i = 0; i < 25; ++i) st[i] = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-            st[t] = (u64)bswap32(P0[7 - 2 * t]) | ((u64)bswap32(P0[6 - 2 * t]) << 32);
-        if (n1 == 32u) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                st[4 + t] = (u64)bswap32(P1[7 - 2 * t]) | ((u64)bswap32(P1[6 - 2 * t]) << 32);
-            st[8] = 0x01ull;
-        } else {
-            st[4] = 0x01ull;
-        }
-        st[16] |= 0x8000000000000000ull;  // byte 135 of the 136-byte block
-        keccak_f1600(st);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int i = 7 - k;
-            const u32 wv = (i & 1) ? (u32)(st[i >> 1] >> 32) : (u32)st[i >> 1];
-            z[k] = bswap32(wv);
-        }
-        return;
-    }
-    u32 pv[24];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { pv[k] = P0[k]; pv[8 + k] = P1[k]; pv[16 + k] = P2[k]; }
-    const u32 len = n0 + n1 + n2;
+    for (int t = 0; t < 4; ++t)
+        st[t] = (u64)bswap32(W[7 - 2 * t]) | ((u64)bswap32(W[6 - 2 * t]) << 32);
+}
+
+MH_FN void keccak_words(const u32* W0, const u32* W1, const u32* W2, u32 nw, u32 full, u32* z) {
     u64 st[25];
 #pragma unroll
     for (int i = 0; i < 25; ++i) st[i] = 0;
-#pragma unroll
-    for (int wd = 0; wd < 34; ++wd) {
-        u32 word = 0;
-#pragma unroll
-        for (int bi = 0; bi < 4; ++bi) {
-            const u32 m = 4u * wd + bi;
-            u32 byte = 0;
-            if (m < len) {  // wave-uniform
-                const u32 p = m < n0 ? 0u : (m < n0 + n1 ? 1u : 2u);
-                const u32 off = p == 0 ? 0u : (p == 1 ? n0 : n0 + n1);
-                const u32 np = p == 0 ? n0 : (p == 1 ? n1 : n2);
-                const u32 e = np - 1u - (m - off);  // little-endian byte index in the piece
-                const u32 limb = pv[p * 8u + (e >> 2)];
-                byte = (limb >> (8u * (e & 3u))) & 0xFFu;
-            }
-            if (m == len) byte |= 0x01u;
-            if (m == 135u) byte |= 0x80u;
-            word |= byte << (8 * bi);
-        }
-        st[wd >> 1] |= (u64)word << (32 * (wd & 1));
+    keccak_absorb_word(st, W0);
+    if (nw >= 2u) keccak_absorb_word(st + 4, W1);  // wave-uniform
+    if (nw >= 3u) keccak_absorb_word(st + 8, W2);
+    if (full) {
+        if (nw == 1u) st[4] |= 0x01ull;
+        else if (nw == 2u) st[8] |= 0x01ull;
+        else st[12] |= 0x01ull;
     }
+    st[16] |= 0x8000000000000000ull;  // byte 135 of the 136-byte block
     keccak_f1600(st);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -139,11 +103,9 @@ MH_FN void complex_op(const E& env, u32 w1, const u32* x, const u32* y, const u3
             break;
         case D_KECCAK:
             if constexpr ((FEAT & F_KECCAK) != 0) {
-                const u32 np = (w1 >> 26) & 3u;
-                const u32 n0 = (w1 >> 8) & 63u, n1 = (w1 >> 14) & 63u, n2 = (w1 >> 20) & 63u;
-                u32 P2[8];
-                copy8(P2, c3);
-                keccak_pieces(x, y, P2, n0, np > 1 ? n1 : 0u, np > 2 ? n2 : 0u, z);
+                u32 W2[8];
+                copy8(W2, c3);
+                keccak_words(x, y, W2, (w1 >> 8) & 3u, (w1 >> 10) & 1u, z);
             }
             break;
         case D_LOADVAR: env.var(aux, z); break;

@@ -27,15 +27,17 @@ struct KParams {
 };
 
 // Kernel variants: register-file size class (NR 7 / 9 / 15) x feature set (asm only / + C++
-// complex ops / + keccak and EVM helpers).
+// complex ops / + keccak / + keccak and the EVM helpers).  Keccak tapes get a kernel without the
+// EVM helpers' register footprint.
 inline uint32_t nr_class(uint32_t n_regs) {
     return n_regs <= MH_NR_SMALL ? 0u : n_regs <= MH_NR_MID ? 1u : 2u;
 }
 inline uint32_t variant_of(uint32_t n_regs, uint32_t features) {
-    const uint32_t fc = (features & (F_KECCAK | F_EVM)) ? 2u : (features & F_CPLX) ? 1u : 0u;
-    return nr_class(n_regs) * 3 + fc;  // 0..8
+    const uint32_t fc = (features & F_EVM) ? 3u : (features & F_KECCAK) ? 2u
+                        : (features & F_CPLX) ? 1u : 0u;
+    return nr_class(n_regs) * 4 + fc;  // 0..11
 }
-constexpr uint32_t kNumVariants = 9;
+constexpr uint32_t kNumVariants = 12;
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream);
 hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars, uint64_t seed,

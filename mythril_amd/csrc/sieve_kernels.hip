@@ -16,7 +16,7 @@
 // flushed with one atomic per tape per workgroup.
 //
 // Kernel variants (kernels.h variant_of): NR in {7, 9, 15} x {asm only, + C++ overflow
-// predicates / unpinned columns, + keccak/EVM};
+// predicates / unpinned columns, + keccak, + keccak/EVM};
 // mh_run launches one variant per non-empty bucket of tapes, so a tape set's simple tapes run
 // with the register budget (and occupancy) they need rather than the worst tape's.
 #include <hip/hip_runtime.h>
@@ -357,16 +357,19 @@ namespace mh {
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream) {
     if (p.row_count == 0 || p.n_ids == 0) return hipSuccess;
-    constexpr int kCplx = F_CPLX, kAll = F_CPLX | F_KECCAK | F_EVM;
+    constexpr int kCplx = F_CPLX, kKec = F_CPLX | F_KECCAK, kAll = F_CPLX | F_KECCAK | F_EVM;
     switch (variant) {
         case 0: return launch_variant<MH_NR_SMALL, 0>(p, stream);
         case 1: return launch_variant<MH_NR_SMALL, kCplx>(p, stream);
-        case 2: return launch_variant<MH_NR_SMALL, kAll>(p, stream);
-        case 3: return launch_variant<MH_NR_MID, 0>(p, stream);
-        case 4: return launch_variant<MH_NR_MID, kCplx>(p, stream);
-        case 5: return launch_variant<MH_NR_MID, kAll>(p, stream);
-        case 6: return launch_variant<MH_NR_MAX, 0>(p, stream);
-        case 7: return launch_variant<MH_NR_MAX, kCplx>(p, stream);
+        case 2: return launch_variant<MH_NR_SMALL, kKec>(p, stream);
+        case 3: return launch_variant<MH_NR_SMALL, kAll>(p, stream);
+        case 4: return launch_variant<MH_NR_MID, 0>(p, stream);
+        case 5: return launch_variant<MH_NR_MID, kCplx>(p, stream);
+        case 6: return launch_variant<MH_NR_MID, kKec>(p, stream);
+        case 7: return launch_variant<MH_NR_MID, kAll>(p, stream);
+        case 8: return launch_variant<MH_NR_MAX, 0>(p, stream);
+        case 9: return launch_variant<MH_NR_MAX, kCplx>(p, stream);
+        case 10: return launch_variant<MH_NR_MAX, kKec>(p, stream);
         default: return launch_variant<MH_NR_MAX, kAll>(p, stream);
     }
 }

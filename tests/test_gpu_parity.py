@@ -313,3 +313,35 @@ def test_keccak_variant_counts_on_gpu(gpu_ctx):
     cnt, first = ctape.count(ts, seed, 0, rows, threads=min(16, os.cpu_count() or 1))
     assert np.array_equal(hc, cnt)
     assert np.array_equal(fh, first)
+
+
+def test_keccak_message_cuts_on_gpu(gpu_ctx):
+    """Keccak of 1..96-byte messages cut from byte pieces of several widths, on the device."""
+    from oracle.keccak import keccak256
+
+    rng = random.Random(404)
+    splits = [[1], [5], [20], [31], [32], [7, 26], [32, 1], [20, 32], [31, 31], [32, 32],
+              [12, 32, 8], [32, 32, 1], [30, 3, 32], [32, 32, 31], [32, 32, 32], [8, 8, 8]]
+    ts = TapeSet()
+    b = ts.builder()
+    xs = [b.var("x%d" % i) for i in range(3)]
+    for parts in splits:
+        node = None
+        for i, nb in enumerate(parts):
+            p = xs[i] if nb == 32 else b.op(Op.EXTRACT, xs[i], imm0=8 * nb - 1, imm1=0)
+            node = p if node is None else b.op(Op.CONCAT, node, p)
+        ts.add(b.finish(b.op(Op.KECCAK, node)))
+    rows = [[rng.getrandbits(256) for _ in range(3)] for _ in range(63)] + [[0, 0, 0]]
+    soa = np.zeros((3, 8, len(rows)), dtype=np.uint32)
+    for r, vals in enumerate(rows):
+        for v in range(3):
+            for k in range(8):
+                soa[v, k, r] = (vals[v] >> (32 * k)) & 0xFFFFFFFF
+    ct = gpu_ctx.compile(ts)
+    a = upload(gpu_ctx, soa)
+    for t, parts in enumerate(splits):
+        got = native.limbs_to_ints(native.eval_values(gpu_ctx, ct, t, a))
+        for r, vals in enumerate(rows):
+            msg = b"".join((vals[i] & ((1 << (8 * nb)) - 1)).to_bytes(nb, "big")
+                           for i, nb in enumerate(parts))
+            assert got[r] == int.from_bytes(keccak256(msg), "big"), (parts, r)
