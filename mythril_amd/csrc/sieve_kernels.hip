@@ -38,6 +38,14 @@ namespace {
 #include "asm_core.inc"
 
 constexpr int kBlock = 256;
+#ifndef MH_SIEVE_BLOCK
+#define MH_SIEVE_BLOCK 256
+#endif
+// sieve workgroup size.  A/B on MI355X (config 5): 512 rows per workgroup cut the PMC traffic per
+// launch from 9.4 to 5.5 GB (each staged tape chunk read once per 8 waves, half the result
+// flushes) but ran 7 % slower (1.92e10 vs 2.07e10 evals/s: longer barriers around the LDS
+// staging); the kernel is VALU-bound at ~2 GB/s of HBM, so 256 stays.
+constexpr int kSieveBlock = MH_SIEVE_BLOCK;
 constexpr int kChunk = 64;  // tapes per LDS result chunk
 
 // Register file: 8 limb planes of NR+1 VGPRs; R[NR] is the accumulator X (dev_isa.h).
@@ -178,20 +186,20 @@ __device__ __forceinline__ InsnCache lds_insns(const uint2* s_insn, u32 off, u32
 }
 
 template <int NR, int FEAT>
-__global__ void __launch_bounds__(kBlock) sieve_kernel(const KParams p) {
+__global__ void __launch_bounds__(kSieveBlock) sieve_kernel(const KParams p) {
     __shared__ uint2 s_insn[kLdsInsns];
     __shared__ u32 s_off[kChunk], s_n[kChunk], s_rb[kChunk], s_tid[kChunk];
     __shared__ u32 s_meta[4];  // tapes in chunk, first word index, words, streaming flag
     __shared__ unsigned long long s_min[kChunk];
     __shared__ unsigned long long s_cnt[kChunk];
     const u32 tid = threadIdx.x;
-    const u64 row = p.row_first + (u64)blockIdx.x * kBlock + tid;
+    const u64 row = p.row_first + (u64)blockIdx.x * kSieveBlock + tid;
     const bool valid = row < p.row_first + p.row_count;
     DevMachine<NR> m;
     m.p = &p;
     m.lrow = valid ? row : p.row_first;
     preload<NR>(m, p);
-    const u64 block_first = p.index_base + p.row_first + (u64)blockIdx.x * kBlock;
+    const u64 block_first = p.index_base + p.row_first + (u64)blockIdx.x * kSieveBlock;
     const u64 wave_first = block_first + (tid & ~63u);
     for (u32 cb = 0; cb < p.n_ids;) {
         __syncthreads();  // previous chunk's LDS fully consumed
@@ -227,7 +235,7 @@ __global__ void __launch_bounds__(kBlock) sieve_kernel(const KParams p) {
         const u32 wbase = __builtin_amdgcn_readfirstlane(s_meta[1]);
         const u32 nwords = __builtin_amdgcn_readfirstlane(s_meta[2]);
         const bool stream = __builtin_amdgcn_readfirstlane(s_meta[3]) != 0;
-        for (u32 k = tid; k < nwords; k += kBlock) s_insn[k] = p.insns[wbase + k];
+        for (u32 k = tid; k < nwords; k += kSieveBlock) s_insn[k] = p.insns[wbase + k];
         __syncthreads();
         u32 off = __builtin_amdgcn_readfirstlane(s_off[0]);
         u32 n = __builtin_amdgcn_readfirstlane(s_n[0]);
@@ -345,8 +353,8 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters,
 
 template <int NR, int FEAT>
 hipError_t launch_variant(const KParams& p, hipStream_t stream) {
-    const u64 blocks = (p.row_count + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+    const u64 blocks = (p.row_count + kSieveBlock - 1) / kSieveBlock;
+    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0, stream,
                        p);
     return hipGetLastError();
 }
