@@ -29,9 +29,13 @@ new handler is also checked at full occupancy (scripts/diag_modes.py against a k
 
     python3 gen_asm_core.py > asm_core.inc      (run by the Makefile)
 """
+import os
 import sys
 
 SLOT = 256          # bytes per handler slot
+# inline constants by one s_load_dwordx8 from the tape's global copy instead of 8 v_readlane
+# (MH_GEN_SMEM=0 restores the readlane form, for A/B builds)
+SMEM_CONSTS = os.environ.get("MH_GEN_SMEM", "1") != "0"
 NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
@@ -67,7 +71,8 @@ S_PC, S_PC_HI = "s46", "s47"     # jump target
 S_B, S_D, S_C = "s48", "s49", "s50"  # register operands (low byte = index)
 S_L = "s51"                      # readlane lane
 S_Q, S_R = "s52", "s53"          # shift: limb part, bit part
-S_K = ["s%d" % (54 + k) for k in range(8)]  # inline constant limbs
+S_K = ["s%d" % (56 + k) for k in range(8)]  # inline constant limbs (s_load_dwordx8 needs s[4n])
+S_LANE2 = "s[54:55]"             # lane masks: shift saturation, division y != 0
 S_KIND, S_ADV = "s70", "s71"   # division: kind (0 udiv .. 4 smod), slot advance
 S_F64N = (68, 69)                # f64 constant pair (2^32, thresholds)
 S_F64 = ("s68", "s69")
@@ -126,10 +131,16 @@ class Core:
 
     def consts(self, to_y=(), flip7=False):  # S_K <- inline constant; Y[k] <- S_K[k] for k in to_y
         out = []
-        for i in range(4):
-            out.append("s_add_u32 {}, %[ip], {}".format(S_L, i + 1))
-            out.append("v_readlane_b32 {}, %[ic0], {}".format(S_K[2 * i], S_L))
-            out.append("v_readlane_b32 {}, %[ic1], {}".format(S_K[2 * i + 1], S_L))
+        if SMEM_CONSTS:  # one scalar load of the 4 constant slots after ip (window base gwin)
+            out += ["s_lshl_b32 {}, %[ip], 3".format(S_T),
+                    "s_add_u32 {0}, {0}, 8".format(S_T),
+                    "s_load_dwordx8 s[{}:{}], %[gwin], {}".format(S_K[0][1:], S_K[7][1:], S_T),
+                    "s_waitcnt lgkmcnt(0)"]
+        else:
+            for i in range(4):
+                out.append("s_add_u32 {}, %[ip], {}".format(S_L, i + 1))
+                out.append("v_readlane_b32 {}, %[ic0], {}".format(S_K[2 * i], S_L))
+                out.append("v_readlane_b32 {}, %[ic1], {}".format(S_K[2 * i + 1], S_L))
         if flip7:
             out.append("s_xor_b32 {}, {}, 0x80000000".format(S_K[7], S_K[7]))
         out += ["v_mov_b32 {}, {}".format(self.Y(k), S_K[k]) for k in to_y]
@@ -360,7 +371,7 @@ class Core:
             right = name != "SHL_V"
             body = self.y_reg()
             body += a_src0 + ["v_mov_b32 {}, {}".format(S(8 + k), P(k)) for k in range(8)] + off
-            big = "s[62:63]"
+            big = S_LANE2
             body += ["v_or3_b32 {}, {}, {}, {}".format(S(16), Y(1), Y(2), Y(3)),
                      "v_or3_b32 {0}, {0}, {1}, {2}".format(S(16), Y(4), Y(5)),
                      "v_or3_b32 {0}, {0}, {1}, {2}".format(S(16), Y(6), Y(7)),
@@ -433,7 +444,7 @@ class Core:
         CARRY = "v[{}:{}]".format(self.sb + 24, self.sb + 25)   # {carry, 0}
         MAD = "v[{}:{}]".format(self.sb + 26, self.sb + 27)     # {lo, hi}
         C, T1, SX, SY = S(28), S(29), S(30), S(31)
-        YNZ, DUMMY, MSK, TM = "s[62:63]", "s[64:65]", "s[66:67]", "s[44:45]"
+        YNZ, DUMMY, MSK, TM = S_LANE2, "s[64:65]", "s[66:67]", "s[44:45]"
         out = ["L_div_%=:"]
         out += self.idx_on(S_W0, ["SRC0"]) + ["v_mov_b32 {}, {}".format(R[k], self.P(k)) for k in range(8)]
         out += self.idx_off()
@@ -659,7 +670,7 @@ def emit(out):
         w("    __device__ __forceinline__ static u32 run(plane_t& p0, plane_t& p1, plane_t& p2,\n")
         w("                                              plane_t& p3, plane_t& p4, plane_t& p5,\n")
         w("                                              plane_t& p6, plane_t& p7, u32 ic0, u32 ic1,\n")
-        w("                                              u32 ip) {\n")
+        w("                                              u32 ip, const void* gwin) {\n")
         w("        asm volatile(\n")
         for line in c.asm_text():
             w("            \"{}\\n\"\n".format(line))
@@ -667,7 +678,7 @@ def emit(out):
         for k in range(8):
             cons.append("\"+{{v[{}:{}]}}\"(p{})".format(k * nr1, k * nr1 + nr, k))
         w("            : {}, [ip] \"+s\"(ip)\n".format(", ".join(cons)))
-        w("            : [ic0] \"v\"(ic0), [ic1] \"v\"(ic1)\n")
+        w("            : [ic0] \"v\"(ic0), [ic1] \"v\"(ic1), [gwin] \"s\"(gwin)\n")
         check_registers(c, c.asm_text(), N_SCRATCH)
         check_registers(c, c.fetch_text(), N_SCRATCH)
         check_registers(c, c.commit_text(), N_SCRATCH)

@@ -108,12 +108,12 @@ __device__ __forceinline__ u64 splitmix64(u64 x) {
 // tape's slots (or global memory when the tape alone exceeds the LDS chunk).
 template <int NR, int FEAT>
 __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, InsnCache ic,
-                                          u32 n) {
+                                          u32 n, const uint2* gsrc) {
     u32 win = 0, ip = 0;
     for (;;) {
 #if MH_ASM_CORE
         ip = AsmCore<NR>::run(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6, m.R.p7,
-                              ic.w0, ic.w1, ip);
+                              ic.w0, ic.w1, ip, gsrc + win);
 #endif
         const u32 w0 = __builtin_amdgcn_readlane(ic.w0, ip);
         const u32 w1 = __builtin_amdgcn_readlane(ic.w1, ip);
@@ -255,7 +255,8 @@ __global__ void __launch_bounds__(kSieveBlock) sieve_kernel(const KParams p) {
                 skip = known < wave_first;
             }
             if (!skip) {
-                exec_tape<NR, FEAT>(m, stream ? p.insns + off : s_insn + off, ic, n);
+                exec_tape<NR, FEAT>(m, stream ? p.insns + off : s_insn + off, ic, n,
+                                    p.insns + (stream ? off : wbase + off));
                 u32 X[8];
                 m.R.read(NR, X);
                 const u32 rb = __builtin_amdgcn_readfirstlane(s_rb[j]);

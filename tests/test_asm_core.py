@@ -28,6 +28,7 @@ def _asm_lines(lines):
     out = []
     for ln in lines:
         ln = (ln.replace("%[ip]", "s39").replace("%[ic0]", "v200").replace("%[ic1]", "v201")
+              .replace("%[gwin]", "s[80:81]")
               .replace("%=", "0"))
         if ln.endswith(":"):
             continue
