@@ -36,6 +36,8 @@ SLOT = 256          # bytes per handler slot
 # inline constants by one s_load_dwordx8 from the tape's global copy instead of 8 v_readlane
 # (MH_GEN_SMEM=0 restores the readlane form, for A/B builds)
 SMEM_CONSTS = os.environ.get("MH_GEN_SMEM", "1") != "0"
+# instruction words likewise by s_load_dwordx2 in the dispatch (MH_GEN_SMEM_INSN=0: v_readlane)
+SMEM_INSNS = os.environ.get("MH_GEN_SMEM_INSN", "1") != "0"
 NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
@@ -104,9 +106,14 @@ class Core:
         out = []
         if adv:
             out.append("s_add_u32 %[ip], %[ip], {}".format(adv))
+        if SMEM_INSNS:  # the instruction words by one scalar load (no VALU in the dispatch)
+            out += ["s_lshl_b32 {}, %[ip], 3".format(S_T),
+                    "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_W0[1:], S_W1[1:], S_T),
+                    "s_waitcnt lgkmcnt(0)"]
+        else:
+            out += ["v_readlane_b32 {}, %[ic0], %[ip]".format(S_W0),
+                    "v_readlane_b32 {}, %[ic1], %[ip]".format(S_W1)]
         out += [
-            "v_readlane_b32 {}, %[ic0], %[ip]".format(S_W0),
-            "v_readlane_b32 {}, %[ic1], %[ip]".format(S_W1),
             "s_and_b32 {}, {}, 0x7f".format(S_T, S_W1),
             "s_lshl_b32 {}, {}, 8".format(S_T, S_T),
             "s_add_u32 {}, {}, {}".format(S_PC, S_TAB, S_T),
