@@ -38,6 +38,9 @@ SLOT = 256          # bytes per handler slot
 SMEM_CONSTS = os.environ.get("MH_GEN_SMEM", "1") != "0"
 # instruction words likewise by s_load_dwordx2 in the dispatch (MH_GEN_SMEM_INSN=0: v_readlane)
 SMEM_INSNS = os.environ.get("MH_GEN_SMEM_INSN", "1") != "0"
+# and the next instruction's words loaded at the top of the handler (after its constants), so the
+# scalar-cache latency overlaps the handler's VALU body (MH_GEN_PREFETCH=0: load in the dispatch)
+PREFETCH = SMEM_INSNS and os.environ.get("MH_GEN_PREFETCH", "1") != "0"
 NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
@@ -78,6 +81,9 @@ S_LANE2 = "s[54:55]"             # lane masks: shift saturation, division y != 0
 S_KIND, S_ADV = "s70", "s71"   # division: kind (0 udiv .. 4 smod), slot advance
 S_F64N = (68, 69)                # f64 constant pair (2^32, thresholds)
 S_F64 = ("s68", "s69")
+S_NW0, S_NW1 = "s64", "s65"      # prefetched next instruction words
+S_NT = "s66"                     # prefetch address temp
+DISPATCH_MARK = "@@dispatch_words"   # replaced per handler (prefetched or loaded in the dispatch)
 SGPR_CLOBBERS = ["s%d" % i for i in range(40, 72)]
 
 
@@ -107,9 +113,7 @@ class Core:
         if adv:
             out.append("s_add_u32 %[ip], %[ip], {}".format(adv))
         if SMEM_INSNS:  # the instruction words by one scalar load (no VALU in the dispatch)
-            out += ["s_lshl_b32 {}, %[ip], 3".format(S_T),
-                    "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_W0[1:], S_W1[1:], S_T),
-                    "s_waitcnt lgkmcnt(0)"]
+            out.append(DISPATCH_MARK)
         else:
             out += ["v_readlane_b32 {}, %[ic0], %[ip]".format(S_W0),
                     "v_readlane_b32 {}, %[ic1], %[ip]".format(S_W1)]
@@ -120,6 +124,49 @@ class Core:
             "s_addc_u32 {}, {}, 0".format(S_PC_HI, S_TAB_HI),
             "s_setpc_b64 s[46:47]",
         ]
+        return out
+
+    @staticmethod
+    def load_words():
+        return ["s_lshl_b32 {}, %[ip], 3".format(S_T),
+                "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_W0[1:], S_W1[1:], S_T),
+                "s_waitcnt lgkmcnt(0)"]
+
+    def resolve(self, lines):
+        """Replace the dispatch marks of one handler.  A handler with a single static advance
+        prefetches the next instruction's words right after its constants' load (or at its top):
+        the next slot always exists (every tape ends in D_END, and this op is not the end), so
+        the address is the one the dispatch would load.  Other handlers (the division body's
+        register advance, entry) load in the dispatch."""
+        import re
+        marks = [i for i, l in enumerate(lines) if l == DISPATCH_MARK]
+        if not marks:
+            return lines
+        advs = set()
+        for i in marks:
+            m = re.match(r"s_add_u32 %\[ip\], %\[ip\], (\d+)$", lines[i - 1]) if i else None
+            advs.add(int(m.group(1)) if m else None)
+        if not PREFETCH or len(advs) != 1 or None in advs:
+            out = []
+            for l in lines:
+                out += self.load_words() if l == DISPATCH_MARK else [l]
+            return out
+        adv = advs.pop()
+        pre = ["s_lshl_b32 {}, %[ip], 3".format(S_NT),
+               "s_add_u32 {0}, {0}, {1}".format(S_NT, 8 * adv),
+               "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_NW0[1:], S_NW1[1:], S_NT)]
+        at = 0
+        for i, l in enumerate(lines):  # after the constants' wait, if the handler loads any
+            if l.startswith("s_load_dwordx8"):
+                at = i + 2
+                assert lines[i + 1] == "s_waitcnt lgkmcnt(0)", lines[i + 1]
+                break
+        assert at < marks[0]
+        out = lines[:at] + pre
+        for l in lines[at:]:
+            out += ["s_waitcnt lgkmcnt(0)",
+                    "s_mov_b64 s[{}:{}], s[{}:{}]".format(S_W0[1:], S_W1[1:], S_NW0[1:], S_NW1[1:])] \
+                if l == DISPATCH_MARK else [l]
         return out
 
     def idx_on(self, sreg, modes):
@@ -179,6 +226,9 @@ class Core:
 
     # ---- handlers: list of instruction lines, ending in a dispatch (or the exit branch)
     def handler(self, name):
+        return self.resolve(self.handler_raw(name))
+
+    def handler_raw(self, name):
         if name.endswith("X") and name != "EXIT":
             return self.handler_x(name)
         X, P, Y, S = self.X, self.P, self.Y, self.S
@@ -618,7 +668,7 @@ class Core:
                  "L_pc_%=:",
                  "s_add_u32 {0}, {0}, (L_tab_%= - L_pc_%=)".format(S_TAB),
                  "s_addc_u32 {0}, {0}, 0".format(S_TAB_HI)]
-        lines += self.dispatch(0)
+        lines += self.resolve(self.dispatch(0))
         lines += [".p2align 8", "L_tab_%=:"]
         bodies = []
         for i in range(NSLOTS):
@@ -630,7 +680,7 @@ class Core:
                 bodies += ["L_body_{}_%=:".format(name)] + h
             else:
                 lines += h
-        lines += [".org L_tab_%= + {}".format(NSLOTS * SLOT)] + bodies + self.div_body()
+        lines += [".org L_tab_%= + {}".format(NSLOTS * SLOT)] + bodies + self.resolve(self.div_body())
         lines += ["L_out_%=:"]
         return lines
 
