@@ -46,6 +46,9 @@ constexpr int kBlock = 256;
 // flushes) but ran 7 % slower (1.92e10 vs 2.07e10 evals/s: longer barriers around the LDS
 // staging); the kernel is VALU-bound at ~2 GB/s of HBM, so 256 stays.
 constexpr int kSieveBlock = MH_SIEVE_BLOCK;
+#ifndef MH_SIEVE_WAVES9
+#define MH_SIEVE_WAVES9 4  // 0: the NR 9 asm-only variant at its natural register allocation
+#endif
 constexpr int kChunk = 64;  // tapes per LDS result chunk
 
 // Register file: 8 limb planes of NR+1 VGPRs; R[NR] is the accumulator X (dev_isa.h).
@@ -186,7 +189,7 @@ __device__ __forceinline__ InsnCache lds_insns(const uint2* s_insn, u32 off, u32
 }
 
 template <int NR, int FEAT>
-__global__ void __launch_bounds__(kSieveBlock) sieve_kernel(const KParams p) {
+__device__ __forceinline__ void sieve_body(const KParams& p) {
     __shared__ uint2 s_insn[kLdsInsns];
     __shared__ u32 s_off[kChunk], s_n[kChunk], s_rb[kChunk], s_tid[kChunk];
     __shared__ u32 s_meta[4];  // tapes in chunk, first word index, words, streaming flag
@@ -353,10 +356,27 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters,
 }
 
 template <int NR, int FEAT>
+__global__ void __launch_bounds__(kSieveBlock) sieve_kernel(const KParams p) {
+    sieve_body<NR, FEAT>(p);
+}
+
+// The NR 9 asm-only variant held at four waves per SIMD (<= 128 VGPRs): its natural allocation is
+// 136, i.e. three waves, and occupancy decides this latency-bound interpreter's issue rate.
+template <int NR, int FEAT>
+__global__ void __launch_bounds__(kSieveBlock) __attribute__((amdgpu_waves_per_eu(MH_SIEVE_WAVES9, 8)))
+sieve_kernel_occ(const KParams p) {
+    sieve_body<NR, FEAT>(p);
+}
+
+template <int NR, int FEAT>
 hipError_t launch_variant(const KParams& p, hipStream_t stream) {
     const u64 blocks = (p.row_count + kSieveBlock - 1) / kSieveBlock;
-    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0, stream,
-                       p);
+    if constexpr (NR == 9 && FEAT == 0 && MH_SIEVE_WAVES9 > 0)
+        hipLaunchKernelGGL((sieve_kernel_occ<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0,
+                           stream, p);
+    else
+        hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0,
+                           stream, p);
     return hipGetLastError();
 }
 
