@@ -47,7 +47,7 @@ constexpr int kBlock = 256;
 // staging); the kernel is VALU-bound at ~2 GB/s of HBM, so 256 stays.
 constexpr int kSieveBlock = MH_SIEVE_BLOCK;
 #ifndef MH_SIEVE_WAVES9
-#define MH_SIEVE_WAVES9 4  // 0: the NR 9 asm-only variant at its natural register allocation
+#define MH_SIEVE_WAVES9 1  // 0: every sieve variant at its natural register allocation
 #endif
 constexpr int kChunk = 64;  // tapes per LDS result chunk
 
@@ -355,28 +355,26 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters,
     if (r == 0x12345678u) sink[0] = r;
 }
 
-template <int NR, int FEAT>
-__global__ void __launch_bounds__(kSieveBlock) sieve_kernel(const KParams p) {
-    sieve_body<NR, FEAT>(p);
+// Minimum waves per SIMD a variant is compiled for (amdgpu_waves_per_eu; 1 = the natural register
+// allocation).  Occupancy decides this latency-bound interpreter's issue rate, so variants whose
+// natural allocation lands just above a wave boundary are held below it, at the price of a few
+// spilled values outside the asm core: NR 9 asm-only 136 -> 128 VGPRs (four waves, was three);
+// NR 9 keccak / keccak+EVM 256 + 2 AGPRs -> 256 (two waves, was one).
+constexpr int sieve_min_waves(int nr, int feat) {
+    return MH_SIEVE_WAVES9 == 0 ? 1 : nr == 9 && feat == 0 ? 4 : nr == 9 && feat >= 8 ? 2 : 1;
 }
 
-// The NR 9 asm-only variant held at four waves per SIMD (<= 128 VGPRs): its natural allocation is
-// 136, i.e. three waves, and occupancy decides this latency-bound interpreter's issue rate.
 template <int NR, int FEAT>
-__global__ void __launch_bounds__(kSieveBlock) __attribute__((amdgpu_waves_per_eu(MH_SIEVE_WAVES9, 8)))
-sieve_kernel_occ(const KParams p) {
+__global__ void __launch_bounds__(kSieveBlock)
+__attribute__((amdgpu_waves_per_eu(sieve_min_waves(NR, FEAT), 8))) sieve_kernel(const KParams p) {
     sieve_body<NR, FEAT>(p);
 }
 
 template <int NR, int FEAT>
 hipError_t launch_variant(const KParams& p, hipStream_t stream) {
     const u64 blocks = (p.row_count + kSieveBlock - 1) / kSieveBlock;
-    if constexpr (NR == 9 && FEAT == 0 && MH_SIEVE_WAVES9 > 0)
-        hipLaunchKernelGGL((sieve_kernel_occ<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0,
-                           stream, p);
-    else
-        hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0,
-                           stream, p);
+    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0, stream,
+                       p);
     return hipGetLastError();
 }
 

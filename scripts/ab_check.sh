@@ -19,5 +19,5 @@ for m in ('count', 'first'):
     print(m, 'identical' if np.array_equal(a, b) else 'DIFFER (%d entries)' % int((a != b).sum()))
     if not np.array_equal(a, b): sys.exit(1)
 " > $OUT/compare.log 2>&1 && \
-MYTHRIL_HIP_LIB=$PWD/$A timeout -k 10 300 python -u bench.py --no-cpu-baseline > $OUT/bench_a.json 2> $OUT/bench_a.log && \
-MYTHRIL_HIP_LIB=$PWD/$B timeout -k 10 300 python -u bench.py --no-cpu-baseline > $OUT/bench_b.json 2> $OUT/bench_b.log
+MYTHRIL_HIP_LIB=$PWD/$A timeout -k 10 300 python -u bench.py --no-cpu-baseline $BENCH_ARGS > $OUT/bench_a.json 2> $OUT/bench_a.log && \
+MYTHRIL_HIP_LIB=$PWD/$B timeout -k 10 300 python -u bench.py --no-cpu-baseline $BENCH_ARGS > $OUT/bench_b.json 2> $OUT/bench_b.log

@@ -117,3 +117,38 @@ def test_indexed_slots_hold_vgprs(nr):
             for slot, op in zip(("SRC0", "SRC1", "SRC2"), srcs):
                 if slot in modes:
                     assert vgpr.match(op.lstrip("-")), (name, ln)
+
+
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_next_instruction_prefetch(nr):
+    """Every dispatch that takes prefetched words (s_mov from S_NW) is preceded, in straight-line
+    code from the handler's top, by exactly one load of S_NW at the address the dispatch's own ip
+    advance gives; nothing in between writes S_NW / S_NT or leaves the handler; every other
+    dispatch loads its words itself.  No unresolved dispatch mark reaches the asm text."""
+    core = G.Core(nr)
+    nw = "s[{}:{}]".format(G.S_NW0[1:], G.S_NW1[1:])
+    take = "s_mov_b64 s[{}:{}], {}".format(G.S_W0[1:], G.S_W1[1:], nw)
+    assert G.DISPATCH_MARK not in core.asm_text()
+    n_pre = 0
+    for name in G.OPS:
+        lines = core.handler(name)
+        takes = [i for i, ln in enumerate(lines) if ln == take]
+        loads = [i for i, ln in enumerate(lines) if ln.startswith("s_load_dwordx2 " + nw)]
+        if not takes:
+            assert not loads, name
+            continue
+        n_pre += 1
+        assert len(loads) == 1 and loads[0] < takes[0], name
+        head = lines[:loads[0]]
+        assert not any(ln.endswith(":") for ln in head), (name, "label before the prefetch")
+        adv = {int(m.group(1)) for m in (re.match(r"s_add_u32 %\[ip\], %\[ip\], (\d+)$", ln)
+                                          for ln in lines) if m}
+        assert len(adv) == 1, (name, adv)
+        assert lines[loads[0] - 1] == "s_add_u32 {0}, {0}, {1}".format(G.S_NT, 8 * adv.pop()), name
+        for ln in lines[loads[0] + 1:takes[-1]]:
+            dst = ln.split(" ", 1)[1].split(",")[0] if " " in ln else ""
+            assert dst not in (G.S_NW0, G.S_NW1, G.S_NT, nw), (name, ln)
+            assert not ln.startswith(("s_setpc", "s_branch L_out")), (name, ln)
+        for i in takes:
+            assert lines[i - 1] == "s_waitcnt lgkmcnt(0)", name
+    assert n_pre > len(G.OPS) // 2
