@@ -246,6 +246,9 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     }
     if (dconsts.empty()) dconsts.assign(8, 0);
     if (words.empty()) words.assign(2, 0);
+    // the asm core's scalar prefetch reads the 8 slots from the next instruction on (its words and
+    // its inline constants): zero slots after the last tape keep those loads inside the buffer
+    words.resize(words.size() + 2 * 8, 0u);
     if (int32_t r = use_device(ctx)) return r;
     mh_tapeset* ts = new (std::nothrow) mh_tapeset();
     if (!ts) return set_err(MH_E_NOMEM, "tapeset allocation");

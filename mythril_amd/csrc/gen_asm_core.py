@@ -41,6 +41,10 @@ SMEM_INSNS = os.environ.get("MH_GEN_SMEM_INSN", "1") != "0"
 # and the next instruction's words loaded at the top of the handler (after its constants), so the
 # scalar-cache latency overlaps the handler's VALU body (MH_GEN_PREFETCH=0: load in the dispatch)
 PREFETCH = SMEM_INSNS and os.environ.get("MH_GEN_PREFETCH", "1") != "0"
+# the prefetch covers 8 slots from the next instruction (s_load_dwordx16): its words AND its inline
+# constants, so a constant-operand handler copies them from the bank instead of loading
+# (MH_GEN_PREFETCH_CONSTS=0: constants by their own s_load_dwordx8)
+PREFETCH_CONSTS = PREFETCH and SMEM_CONSTS and os.environ.get("MH_GEN_PREFETCH_CONSTS", "1") != "0"
 NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
@@ -81,10 +85,12 @@ S_LANE2 = "s[54:55]"             # lane masks: shift saturation, division y != 0
 S_KIND, S_ADV = "s70", "s71"   # division: kind (0 udiv .. 4 smod), slot advance
 S_F64N = (68, 69)                # f64 constant pair (2^32, thresholds)
 S_F64 = ("s68", "s69")
-S_NW0, S_NW1 = "s64", "s65"      # prefetched next instruction words
+# prefetched next instruction words (+ with PREFETCH_CONSTS, its constant slots: bank s[72:87])
+S_NW0, S_NW1 = ("s72", "s73") if PREFETCH_CONSTS else ("s64", "s65")
+S_BANK = "s[72:87]"
 S_NT = "s66"                     # prefetch address temp
 DISPATCH_MARK = "@@dispatch_words"   # replaced per handler (prefetched or loaded in the dispatch)
-SGPR_CLOBBERS = ["s%d" % i for i in range(40, 72)]
+SGPR_CLOBBERS = ["s%d" % i for i in range(40, 88 if PREFETCH_CONSTS else 72)]
 
 
 class Core:
@@ -128,6 +134,11 @@ class Core:
 
     @staticmethod
     def load_words():
+        if PREFETCH_CONSTS:  # every handler entry finds slots ip..ip+7 in the bank
+            return ["s_lshl_b32 {}, %[ip], 3".format(S_T),
+                    "s_load_dwordx16 {}, %[gwin], {}".format(S_BANK, S_T),
+                    "s_waitcnt lgkmcnt(0)",
+                    "s_mov_b64 s[{}:{}], s[{}:{}]".format(S_W0[1:], S_W1[1:], S_NW0[1:], S_NW1[1:])]
         return ["s_lshl_b32 {}, %[ip], 3".format(S_T),
                 "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_W0[1:], S_W1[1:], S_T),
                 "s_waitcnt lgkmcnt(0)"]
@@ -154,12 +165,17 @@ class Core:
         adv = advs.pop()
         pre = ["s_lshl_b32 {}, %[ip], 3".format(S_NT),
                "s_add_u32 {0}, {0}, {1}".format(S_NT, 8 * adv),
-               "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_NW0[1:], S_NW1[1:], S_NT)]
+               ("s_load_dwordx16 {}, %[gwin], {}".format(S_BANK, S_NT) if PREFETCH_CONSTS else
+                "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_NW0[1:], S_NW1[1:], S_NT))]
         at = 0
-        for i, l in enumerate(lines):  # after the constants' wait, if the handler loads any
+        for i, l in enumerate(lines):  # after the constants' wait / copy, if the handler has any
             if l.startswith("s_load_dwordx8"):
                 at = i + 2
                 assert lines[i + 1] == "s_waitcnt lgkmcnt(0)", lines[i + 1]
+                break
+            if l.startswith("s_mov_b64 s[56:57]"):
+                at = i + 4
+                assert all(x.startswith("s_mov_b64 s[") for x in lines[i:at]), lines[i:at]
                 break
         assert at < marks[0]
         out = lines[:at] + pre
@@ -185,7 +201,10 @@ class Core:
 
     def consts(self, to_y=(), flip7=False):  # S_K <- inline constant; Y[k] <- S_K[k] for k in to_y
         out = []
-        if SMEM_CONSTS:  # one scalar load of the 4 constant slots after ip (window base gwin)
+        if PREFETCH_CONSTS:  # the 4 constant slots after ip arrived with this op's words
+            out += ["s_mov_b64 s[{}:{}], s[{}:{}]".format(56 + 2 * i, 57 + 2 * i, 74 + 2 * i,
+                                                          75 + 2 * i) for i in range(4)]
+        elif SMEM_CONSTS:  # one scalar load of the 4 constant slots after ip (window base gwin)
             out += ["s_lshl_b32 {}, %[ip], 3".format(S_T),
                     "s_add_u32 {0}, {0}, 8".format(S_T),
                     "s_load_dwordx8 s[{}:{}], %[gwin], {}".format(S_K[0][1:], S_K[7][1:], S_T),

@@ -124,7 +124,9 @@ def test_next_instruction_prefetch(nr):
     """Every dispatch that takes prefetched words (s_mov from S_NW) is preceded, in straight-line
     code from the handler's top, by exactly one load of S_NW at the address the dispatch's own ip
     advance gives; nothing in between writes S_NW / S_NT or leaves the handler; every other
-    dispatch loads its words itself.  No unresolved dispatch mark reaches the asm text."""
+    dispatch loads its words itself.  With PREFETCH_CONSTS the load fills the bank (the next
+    instruction's words and its constant slots) and no handler reads the bank's constants after
+    issuing it.  No unresolved dispatch mark reaches the asm text."""
     core = G.Core(nr)
     nw = "s[{}:{}]".format(G.S_NW0[1:], G.S_NW1[1:])
     take = "s_mov_b64 s[{}:{}], {}".format(G.S_W0[1:], G.S_W1[1:], nw)
@@ -133,7 +135,9 @@ def test_next_instruction_prefetch(nr):
     for name in G.OPS:
         lines = core.handler(name)
         takes = [i for i, ln in enumerate(lines) if ln == take]
-        loads = [i for i, ln in enumerate(lines) if ln.startswith("s_load_dwordx2 " + nw)]
+        loads = [i for i, ln in enumerate(lines)
+                 if ln.startswith(("s_load_dwordx2 " + nw, "s_load_dwordx16 " + G.S_BANK))
+                 and G.S_NT in ln]
         if not takes:
             assert not loads, name
             continue
@@ -147,7 +151,9 @@ def test_next_instruction_prefetch(nr):
         assert lines[loads[0] - 1] == "s_add_u32 {0}, {0}, {1}".format(G.S_NT, 8 * adv.pop()), name
         for ln in lines[loads[0] + 1:takes[-1]]:
             dst = ln.split(" ", 1)[1].split(",")[0] if " " in ln else ""
-            assert dst not in (G.S_NW0, G.S_NW1, G.S_NT, nw), (name, ln)
+            assert dst not in (G.S_NW0, G.S_NW1, G.S_NT, nw, G.S_BANK), (name, ln)
+            if G.PREFETCH_CONSTS:  # the constants were copied out of the bank before the load
+                assert not any("s[%d:" % r in ln for r in (74, 76, 78, 80)), (name, ln)
             assert not ln.startswith(("s_setpc", "s_branch L_out")), (name, ln)
         for i in takes:
             assert lines[i - 1] == "s_waitcnt lgkmcnt(0)", name
