@@ -163,8 +163,7 @@ class Core:
                 out += self.load_words() if l == DISPATCH_MARK else [l]
             return out
         adv = advs.pop()
-        pre = ["s_lshl_b32 {}, %[ip], 3".format(S_NT),
-               "s_add_u32 {0}, {0}, {1}".format(S_NT, 8 * adv),
+        pre = ["s_lshl3_add_u32 {}, %[ip], {}".format(S_NT, 8 * adv),  # (ip << 3) + 8 adv
                ("s_load_dwordx16 {}, %[gwin], {}".format(S_BANK, S_NT) if PREFETCH_CONSTS else
                 "s_load_dwordx2 s[{}:{}], %[gwin], {}".format(S_NW0[1:], S_NW1[1:], S_NT))]
         at = 0

@@ -148,7 +148,7 @@ def test_next_instruction_prefetch(nr):
         adv = {int(m.group(1)) for m in (re.match(r"s_add_u32 %\[ip\], %\[ip\], (\d+)$", ln)
                                           for ln in lines) if m}
         assert len(adv) == 1, (name, adv)
-        assert lines[loads[0] - 1] == "s_add_u32 {0}, {0}, {1}".format(G.S_NT, 8 * adv.pop()), name
+        assert lines[loads[0] - 1] == "s_lshl3_add_u32 {}, %[ip], {}".format(G.S_NT, 8 * adv.pop()), name
         for ln in lines[loads[0] + 1:takes[-1]]:
             dst = ln.split(" ", 1)[1].split(",")[0] if " " in ln else ""
             assert dst not in (G.S_NW0, G.S_NW1, G.S_NT, nw, G.S_BANK), (name, ln)
