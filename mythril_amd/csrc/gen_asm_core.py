@@ -358,14 +358,14 @@ class Core:
         if name in ("BAND", "BOR", "BXOR", "BEQ"):
             ins = {"BAND": "v_and_b32", "BOR": "v_or_b32", "BXOR": "v_xor_b32",
                    "BEQ": "v_xor_b32"}[name]
+            # Bool operands are 0/1 in limb 0 (dev_isa.h), so and/or/xor need no mask and
+            # BEQ is 1 ^ a ^ b
             body = self.y_reg(1) + a_src0 + ["{} {}, {}, {}".format(ins, X(0), P(0), Y(0))] + off
             if name == "BEQ":
-                body.append("v_not_b32 {0}, {0}".format(X(0)))
-            body.append("v_and_b32 {0}, 1, {0}".format(X(0)))
+                body.append("v_xor_b32 {0}, 1, {0}".format(X(0)))
             return body + self.wb(1) + self.dispatch(1)
         if name == "BNOT":
-            body = a_src0 + ["v_not_b32 {}, {}".format(X(0), P(0))] + off
-            body.append("v_and_b32 {0}, 1, {0}".format(X(0)))
+            body = a_src1 + ["v_xor_b32 {}, 1, {}".format(X(0), P(0))] + off  # R[a'] in src1
             return body + self.wb(1) + self.dispatch(1)
         if name in ("TRUE", "FALSE"):
             body = ["v_mov_b32 {}, {}".format(X(0), 1 if name == "TRUE" else 0)]
