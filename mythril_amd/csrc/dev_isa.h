@@ -110,6 +110,13 @@ static inline unsigned mh_xform(unsigned op) {
     }
 }
 
+// ops whose result is a Bool (0/1 in limb 0)
+static inline bool mh_produces_bool(unsigned op) {
+    op = mh_base_op(op);
+    return (op >= D_EQ_R && op <= D_SGE_C) || (op >= D_BAND && op <= D_FALSE) || op == D_BITE ||
+           op == D_UADD_NOOVFL || op == D_UMUL_NOOVFL;
+}
+
 // *_R / *_C pairs (y from a register / inline constant): 1 = R form, 2 = C form, 0 = neither
 static inline int mh_pair_form(unsigned op) {
     op = mh_base_op(op);

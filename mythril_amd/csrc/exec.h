@@ -185,11 +185,14 @@ MH_FN u32 step(M& m, u32 w0, u32 w1, u32 ip) {
         case D_SGT_R: case D_SGT_C: if constexpr (SIMPLE) z[0] = slt_w(y, x, 256); break;
         case D_SLE_R: case D_SLE_C: if constexpr (SIMPLE) z[0] = !slt_w(y, x, 256); break;
         case D_SGE_R: case D_SGE_C: if constexpr (SIMPLE) z[0] = !slt_w(x, y, 256); break;
-        case D_BAND: if constexpr (SIMPLE) z[0] = x[0] & y[0] & 1u; break;
-        case D_BOR: if constexpr (SIMPLE) z[0] = (x[0] | y[0]) & 1u; break;
-        case D_BXOR: if constexpr (SIMPLE) z[0] = (x[0] ^ y[0]) & 1u; break;
-        case D_BEQ: if constexpr (SIMPLE) z[0] = ((x[0] ^ y[0]) & 1u) ^ 1u; break;
-        case D_BNOT: if constexpr (SIMPLE) z[0] = (x[0] & 1u) ^ 1u; break;
+        // Bool operands are canonical 0/1 in limb 0 (dev_isa.h), so, exactly like the asm core,
+        // no mask: a producer that left other bits set would show here as a non-0/1 result,
+        // which the host emulator rejects (tests/native/emu.cpp, mh_produces_bool)
+        case D_BAND: if constexpr (SIMPLE) z[0] = x[0] & y[0]; break;
+        case D_BOR: if constexpr (SIMPLE) z[0] = x[0] | y[0]; break;
+        case D_BXOR: if constexpr (SIMPLE) z[0] = x[0] ^ y[0]; break;
+        case D_BEQ: if constexpr (SIMPLE) z[0] = x[0] ^ y[0] ^ 1u; break;
+        case D_BNOT: if constexpr (SIMPLE) z[0] = x[0] ^ 1u; break;
         case D_TRUE: if constexpr (SIMPLE) z[0] = 1u; break;
         case D_FALSE: if constexpr (SIMPLE) z[0] = 0u; break;
         case D_ITE:

@@ -8,8 +8,14 @@ Mirrors mythril/support/model.py:15-62 line for line in behaviour —
   ``UnsatError`` when it is not positive (only with ``enforce_execution_time``);
 * a Python ``False`` among the constraints raises ``UnsatError``; Python bools are dropped;
 * ``args.solver_log``: the query is written as SMT-LIB2 to ``<dir>/<abs(hash(...))>.smt2``
-  before solving (smtlib.py prints it);
+  (smtlib.py prints this package's terms; foreign terms go through the configured
+  ``log_writer``, z3's own ``Optimize.sexpr()`` under the plugin).  A query answered by the
+  fallback is logged by the fallback itself (the reference's get_model writes the file), so no
+  query is written twice and a writer error never escapes ``get_model``;
 * sat -> a ``Model``; unknown / unsat -> ``UnsatError``
+* ``SolverStatistics``: ``query_count`` / ``solver_time`` stay z3's own counters — the
+  reference's ``stat_smt_query`` on ``BaseSolver.check`` (laser/smt/solver/solver.py:47)
+  already counts every fallback query, so the front end adds only the ``sieve_*`` counters
 
 — with one change: when there is nothing to optimise (``minimize == maximize == ()``, the
 feasibility case of ``Constraints.is_possible`` and the detection modules), the
@@ -39,6 +45,8 @@ _config = {
     "fallback": None,   # callable(constraints, minimize, maximize, enforce_execution_time)
     "verify": None,     # callable(constraints, model) -> bool (z3 re-verification)
     "to_terms": None,   # callable(constraints) -> (smt.Context, [Bool]) for foreign terms
+    "log_writer": None,  # callable(constraints, minimize, maximize) -> SMT-LIB2 text (foreign)
+    "fallback_logs": False,  # the fallback writes --solver-log files itself (the reference's)
     "sieve_kwargs": {},
     "enabled": True,
 }
@@ -46,10 +54,15 @@ _config = {
 
 def configure(*, fallback: Optional[Callable] = None, verify: Optional[Callable] = None,
               to_terms: Optional[Callable] = None, enabled: Optional[bool] = None,
+              log_writer: Optional[Callable] = None, fallback_logs: Optional[bool] = None,
               **sieve_kwargs) -> None:
     """Set the fallback solver, the witness verifier, the term importer and sieve options."""
     if fallback is not None:
         _config["fallback"] = fallback
+    if log_writer is not None:
+        _config["log_writer"] = log_writer
+    if fallback_logs is not None:
+        _config["fallback_logs"] = fallback_logs
     if verify is not None:
         _config["verify"] = verify
     if to_terms is not None:
@@ -64,7 +77,8 @@ def configure(*, fallback: Optional[Callable] = None, verify: Optional[Callable]
 
 def reset() -> None:
     """Back to defaults (tests, plugin stop)."""
-    _config.update(fallback=None, verify=None, to_terms=None, sieve_kwargs={}, enabled=True)
+    _config.update(fallback=None, verify=None, to_terms=None, log_writer=None,
+                   fallback_logs=False, sieve_kwargs={}, enabled=True)
     close_sieve()
     get_model.cache_clear()
 
@@ -79,6 +93,14 @@ def sieve():
     return s
 
 
+def forget_witnesses() -> None:
+    """Drop the sieve's parent-witness table (its keys are node ids of a term context the
+    importer has just replaced)."""
+    s = getattr(_tls, "sieve", None)
+    if s is not None:
+        s.witnesses.clear()
+
+
 def close_sieve() -> None:
     s = getattr(_tls, "sieve", None)
     if s is not None:
@@ -87,13 +109,30 @@ def close_sieve() -> None:
 
 
 def _log_query(constraints, minimize, maximize) -> None:
-    from .smtlib import to_smtlib
+    """support/model.py:44-55: one ``.smt2`` file per query, named by the hash of the query.
+    This package's terms print through smtlib.to_smtlib; foreign (z3) terms through the
+    configured ``log_writer``.  Never raises: a query that cannot be printed is skipped (the
+    reference only logs what z3 can print, and a log must not change the answer)."""
+    from . import smt
 
-    Path(args.solver_log).mkdir(parents=True, exist_ok=True)
-    key = tuple(list(constraints) + list(minimize) + list(maximize)
-                + [len(constraints), len(minimize), len(maximize)])
-    with open(args.solver_log + "/%d.smt2" % abs(hash(key)), "w") as f:
-        f.write(to_smtlib(constraints, minimize, maximize))
+    try:
+        if all(isinstance(c, smt.Bool) for c in constraints) and \
+                all(isinstance(e, smt.BitVec) for e in tuple(minimize) + tuple(maximize)):
+            from .smtlib import to_smtlib
+
+            text = to_smtlib(constraints, minimize, maximize)
+        elif _config["log_writer"] is not None:
+            text = _config["log_writer"](constraints, minimize, maximize)
+        else:
+            log.debug("--solver-log: no writer for %s terms", type(constraints[0]).__name__)
+            return
+        Path(args.solver_log).mkdir(parents=True, exist_ok=True)
+        key = tuple(list(constraints) + list(minimize) + list(maximize)
+                    + [len(constraints), len(minimize), len(maximize)])
+        with open(args.solver_log + "/%d.smt2" % abs(hash(key)), "w") as f:
+            f.write(text)
+    except Exception as e:  # noqa: BLE001 - logging is best effort
+        log.debug("--solver-log write failed: %s", e)
 
 
 def _terms(constraints):
@@ -112,16 +151,20 @@ def _terms(constraints):
     return conv(constraints)
 
 
-def sieve_model(constraints):
-    """The sieve's answer for a feasibility query: a Model, or None (ask the fallback)."""
+def sieve_model(constraints, timeout_ms: Optional[float] = None):
+    """The sieve's answer for a feasibility query: a Model, or None (ask the fallback).
+    ``timeout_ms`` is get_model's budget (support/model.py:26-31): the sieve's own rounds and the
+    verifier both stop inside it."""
     from .model import Model
 
     stats = SolverStatistics()
+    t0 = time.perf_counter()
     try:
         ctx, terms = _terms(constraints)
         s = sieve()
         key = tuple(t.node for t in terms)
-        w = s.solve(ctx.b, [t.node for t in terms], key=key)
+        budget = None if timeout_ms is None else max(timeout_ms, 0.0) / 1000.0
+        w = s.solve(ctx.b, [t.node for t in terms], key=key, budget_s=budget)
     except Exception as e:  # fail closed: any problem means "ask the fallback"
         from .lower import LoweringUnsupported
         from .native import Unsupported
@@ -137,9 +180,17 @@ def sieve_model(constraints):
         return None
     m = Model(s, ctx, w.schema, w.values, w.index)
     verify = _config["verify"]
-    if verify is not None and not verify(constraints, m):
-        stats.sieve_rejected += 1
-        return None
+    if verify is not None:
+        left = None if timeout_ms is None else timeout_ms - 1000.0 * (time.perf_counter() - t0)
+        try:
+            ok = left is None or left > 0
+            ok = ok and verify(constraints, m, timeout_ms=left)
+        except Exception as e:  # noqa: BLE001 - a failing verifier rejects
+            log.debug("sieve witness verifier error: %s", e)
+            ok = False
+        if not ok:
+            stats.sieve_rejected += 1
+            return None
     stats.sieve_hits += 1
     return m
 
@@ -156,24 +207,21 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         if type(constraint) == bool and not constraint:
             raise UnsatError
     constraints = [c for c in constraints if type(c) != bool]
-    if args.solver_log:
-        _log_query(constraints, minimize, maximize)
     stats = SolverStatistics()
+    fallback = _config["fallback"]
     if _config["enabled"] and not minimize and not maximize:
         t0 = time.perf_counter()
-        m = sieve_model(constraints)
+        m = sieve_model(constraints, timeout)
         if stats.enabled:
             stats.sieve_time += time.perf_counter() - t0
         if m is not None:
+            if args.solver_log:
+                _log_query(constraints, minimize, maximize)
             return m
-    fallback = _config["fallback"]
+    if args.solver_log and (fallback is None or not _config["fallback_logs"]):
+        _log_query(constraints, minimize, maximize)
     if fallback is None:
         log.debug("sieve found no witness and no fallback solver is configured")
         raise UnsatError
-    t0 = time.perf_counter()
-    try:
-        return fallback(tuple(constraints), minimize, maximize, enforce_execution_time)
-    finally:
-        if stats.enabled:
-            stats.query_count += 1
-            stats.solver_time += time.perf_counter() - t0
+    # the fallback (the reference's get_model) counts itself through stat_smt_query
+    return fallback(tuple(constraints), minimize, maximize, enforce_execution_time)

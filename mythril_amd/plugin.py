@@ -96,12 +96,38 @@ def _reference_modules() -> List[object]:
     return out
 
 
-def z3_verifier(constraints, model) -> bool:
+def z3_log_writer(constraints, minimize, maximize) -> str:
+    """``--solver-log`` text of reference (z3-backed) terms exactly as support/model.py:37-55
+    writes it: an ``Optimize`` with the constraints and objectives, printed by ``sexpr()``."""
+    import z3
+
+    s = z3.Optimize()
+    for c in constraints:
+        s.add(getattr(c, "raw", c))
+    for e in minimize:
+        s.minimize(getattr(e, "raw", e))
+    for e in maximize:
+        s.maximize(getattr(e, "raw", e))
+    return s.sexpr()
+
+
+def z3_verifier(constraints, model, timeout_ms=None) -> bool:
     """Re-verify a sieve witness with z3: the constraints plus the witness as equalities on every
-    scalar column must be SAT.  Runs only where z3 is importable."""
+    scalar column must be SAT.  Runs only where z3 is importable.
+
+    The check runs under get_model's own budget (``timeout_ms`` = what is left of
+    ``min(args.solver_timeout, time_remaining - 500)``, support/model.py:26-31): array else-values
+    and keccak / UF interpretations stay free, so the check is a real solver call, and ``unknown``
+    (timeout) counts as a rejection — the query then goes to the fallback unchanged."""
     import z3  # noqa: F401
 
+    from .support import args
+
     s = z3.Solver()
+    budget = args.solver_timeout if timeout_ms is None else min(args.solver_timeout, timeout_ms)
+    if budget <= 0:
+        return False
+    s.set("timeout", max(1, int(budget)))
     s.add([getattr(c, "raw", c) for c in constraints])
     arrays = model.ctx.b.symbols.arrays
     for col in model.schema.columns.values():
@@ -134,14 +160,18 @@ class SievePlugin(LaserPlugin):
         kwargs = dict(self.sieve_kwargs)
         conf = {}
         if original is not None:
+            # the reference's get_model, unwrapped from its lru_cache (the front end has its
+            # own); it writes its own --solver-log file and counts itself in SolverStatistics
             conf["fallback"] = getattr(original, "__wrapped__", original)
+            conf["fallback_logs"] = True
         try:
             import z3  # noqa: F401
 
             from .smtlib import Z3Importer
 
             conf["verify"] = z3_verifier
-            conf["to_terms"] = Z3Importer()
+            conf["log_writer"] = z3_log_writer
+            conf["to_terms"] = Z3Importer(on_reset=frontend.forget_witnesses)
         except Exception:
             pass
         frontend.configure(**conf, **kwargs)
@@ -170,11 +200,21 @@ class SievePluginBuilder(MythrilLaserPlugin):
     plugin_type = "Laser Plugin"
     plugin_version = "0.1.0"
     plugin_description = "MI355X constraint sieve: feasibility witnesses before z3"
-    plugin_default_enabled = False
+    # the reference's CLI loads only default-enabled entry-point plugins
+    # (plugin/loader.py:73-80, cli.py:39), so a drop-in must be default-enabled; the
+    # environment variable MYTHRIL_AMD_SIEVE=0 turns it off without uninstalling
+    plugin_default_enabled = True
 
     def __init__(self, **kwargs):
         super().__init__(**kwargs)
-        self.enabled = True
+        self.enabled = enabled_by_env()
 
     def __call__(self, *args, **kwargs) -> SievePlugin:
         return SievePlugin(**kwargs)
+
+
+def enabled_by_env() -> bool:
+    import os
+
+    return os.environ.get("MYTHRIL_AMD_SIEVE", "1").strip().lower() not in ("0", "off", "false",
+                                                                            "no")

@@ -230,12 +230,18 @@ class Sieve:
         return list(groups.values())
 
     def solve(self, b: TapeBuilder, roots: Sequence[int], key: Optional[tuple] = None,
-              pool=None) -> Optional[Witness]:
-        """A witness of the conjunction of Bool nodes `roots` of builder `b`, or None."""
+              pool=None, budget_s: Optional[float] = None) -> Optional[Witness]:
+        """A witness of the conjunction of Bool nodes `roots` of builder `b`, or None.
+        ``budget_s`` (get_model's remaining solver budget) caps this query's rounds below the
+        sieve's own ``self.budget_s``; no round starts once it is spent."""
         from .tape import Tape
 
         t0 = time.perf_counter()
+        budget = self.budget_s if budget_s is None else min(self.budget_s, budget_s)
         self.stats.queries += 1
+        if budget <= 0:
+            self.stats.misses += 1
+            return None
         root, schema = lower_query(b, roots)
         columns = list(schema.columns)
         if not columns:  # ground query: one row decides it
@@ -295,7 +301,7 @@ class Sieve:
                         self.remember(key, w)
                     self.stats.hits += 1
                     return w
-                if time.perf_counter() - t1 > self.budget_s:
+                if time.perf_counter() - t0 > budget:
                     break
             self.stats.misses += 1
             return None

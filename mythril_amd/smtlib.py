@@ -169,31 +169,59 @@ class Reader:
         raise SmtlibError("unsupported command %r" % (head,))
 
     def term(self, t: Sexp, env: Dict[str, int]) -> int:
-        # explicit stack: LASER terms nest deeply (calldata concat chains, folded Ands)
-        return self._term(t, env, 0)
-
-    def _term(self, t: Sexp, env: Dict[str, int], depth: int) -> int:
-        if depth > 20000:
-            raise SmtlibError("term too deep")
-        b = self.b
-        if isinstance(t, str):
-            return self._atom(t, env)
-        if not t:
-            raise SmtlibError("empty application")
-        head = t[0]
-        if head == "let":
-            env2 = dict(env)
-            for name, val in t[1]:
-                env2[name] = self._term(val, env, depth + 1)  # parallel let
-            return self._term(t[2], env2, depth + 1)
-        if isinstance(head, list):
-            return self._indexed(head, t[1:], env, depth)
-        if head == "_":  # (_ bvN w)
-            if isinstance(t[1], str) and t[1].startswith("bv"):
-                return b.const(int(t[1][2:]), int(t[2]))
-            raise SmtlibError("unsupported indexed term %r" % (t,))
-        args_ = [self._term(x, env, depth + 1) for x in t[1:]]
-        return self._apply(head, args_)
+        """The node of term `t`.  An explicit work stack, not recursion: LASER terms nest
+        thousands deep (store chains of every SSTORE, ite chains of symbolic-index reads, folded
+        Ands), far past Python's recursion limit."""
+        vals: List[int] = []
+        work: list = [(0, t, env)]
+        steps = 0
+        while work:
+            item = work.pop()
+            kind = item[0]
+            steps += 1
+            if kind == 0:  # evaluate item[1] in env item[2]
+                _, t, env = item
+                if isinstance(t, str):
+                    vals.append(self._atom(t, env))
+                    continue
+                if not t:
+                    raise SmtlibError("empty application")
+                head = t[0]
+                if head == "let":  # parallel let: every binding in the outer env
+                    binds = t[1]
+                    work.append((1, t[2], env, [name for name, _ in binds]))
+                    work += [(0, val, env) for _, val in reversed(binds)]
+                    continue
+                if isinstance(head, list):
+                    if len(t) != 2:
+                        raise SmtlibError("indexed application takes 1 argument: %r" % (head,))
+                    work.append((3, head))
+                    work.append((0, t[1], env))
+                    continue
+                if head == "_":  # (_ bvN w)
+                    if isinstance(t[1], str) and t[1].startswith("bv"):
+                        vals.append(self.b.const(int(t[1][2:]), int(t[2])))
+                        continue
+                    raise SmtlibError("unsupported indexed term %r" % (t,))
+                work.append((2, head, len(t) - 1))
+                work += [(0, x, env) for x in reversed(t[1:])]
+            elif kind == 1:  # let body, bindings on the value stack
+                _, body, env, names = item
+                k = len(names)
+                bound = vals[len(vals) - k:] if k else []
+                del vals[len(vals) - k:]
+                env2 = dict(env)
+                env2.update(zip(names, bound))
+                work.append((0, body, env2))
+            elif kind == 2:  # application of a named operator
+                _, head, n = item
+                a = vals[len(vals) - n:] if n else []
+                del vals[len(vals) - n:]
+                vals.append(self._apply(head, a))
+            else:  # indexed operator / (as const ..) over the value on top
+                vals.append(self._indexed(item[1], vals.pop()))
+        assert len(vals) == 1
+        return vals[0]
 
     def _atom(self, t: str, env: Dict[str, int]) -> int:
         b = self.b
@@ -222,16 +250,14 @@ class Reader:
             return b.var(t, sort.width)
         return b.array(t, sort.domain, sort.width)
 
-    def _indexed(self, head: list, rest, env, depth) -> int:
+    def _indexed(self, head: list, x: int) -> int:
         b = self.b
         if head[0] == "as" and head[1] == "const":
             s = _sort(head[2])
-            v = self._term(rest[0], env, depth + 1)
-            return b.const_array(s.domain, v)
+            return b.const_array(s.domain, x)
         if head[0] != "_":
             raise SmtlibError("unsupported application head %r" % (head,))
         name, idx = head[1], [int(x) for x in head[2:]]
-        x = self._term(rest[0], env, depth + 1)
         w = b.widths[x]
         if name == "extract":
             return b.op(Op.EXTRACT, x, imm0=idx[0], imm1=idx[1])
@@ -463,30 +489,65 @@ def to_smtlib(constraints: Sequence, minimize: Sequence = (), maximize: Sequence
 
 
 # -- z3 import -------------------------------------------------------------------------------
+def _z3_sexpr(raw) -> str:
+    import z3  # only on a box where the reference runs
+
+    s = z3.Solver()
+    s.add(raw)
+    return s.sexpr()
+
+
 class Z3Importer:
     """z3-backed reference terms -> sieve terms, memoised per z3 AST id (callable as the
-    front end's ``to_terms``)."""
+    front end's ``to_terms``).
 
-    def __init__(self, ctx: Optional[smt.Context] = None):
+    Memory stays bounded over a long ``myth analyze`` run: the memo is an LRU of at most
+    ``max_memo`` ASTs, and once the reader's term store holds more than ``max_nodes`` nodes the
+    importer starts over with a fresh context (between two queries, never inside one) and calls
+    ``on_reset`` — the front end drops every cache keyed by the old context's node ids then (the
+    sieve's parent-witness table).  ``sexpr_of`` prints one reference term as SMT-LIB2 (z3's
+    ``Solver.sexpr()`` by default)."""
+
+    def __init__(self, ctx: Optional[smt.Context] = None, max_memo: int = 1 << 16,
+                 max_nodes: int = 1 << 21, sexpr_of=None, on_reset=None):
+        from collections import OrderedDict
+
         self.reader = Reader(ctx)
-        self.memo: Dict[int, Tuple[object, int]] = {}
+        self.memo: "OrderedDict[int, Tuple[object, int]]" = OrderedDict()
+        self.max_memo = max_memo
+        self.max_nodes = max_nodes
+        self.sexpr_of = sexpr_of or _z3_sexpr
+        self.on_reset = on_reset
+        self.resets = 0
+
+    def reset(self) -> None:
+        self.reader = Reader()
+        self.memo.clear()
+        self.resets += 1
+        if self.on_reset is not None:
+            self.on_reset()
+
+    def n_nodes(self) -> int:
+        return len(self.reader.b.nodes)
 
     def __call__(self, constraints):
-        import z3  # only on a box where the reference runs
-
+        if self.n_nodes() > self.max_nodes:
+            self.reset()
         out = []
         for c in constraints:
             raw = getattr(c, "raw", c)
             key = raw.get_id()
             got = self.memo.get(key)
             if got is None or got[0] is not raw:
-                s = z3.Solver()
-                s.add(raw)
                 q = Query(self.reader.ctx)
-                for cmd in read_sexps(s.sexpr()):
+                for cmd in read_sexps(self.sexpr_of(raw)):
                     self.reader.command(cmd, q)
                 node = q.constraints[-1].node if len(q.constraints) == 1 else \
                     smt.And(*q.constraints).node
                 got = self.memo[key] = (raw, node)
+                while len(self.memo) > self.max_memo:
+                    self.memo.popitem(last=False)
+            else:
+                self.memo.move_to_end(key)
             out.append(smt.Bool(got[1], self.reader.ctx))
         return self.reader.ctx, out

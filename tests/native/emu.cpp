@@ -87,6 +87,12 @@ extern "C" int32_t emu_eval(const mh_node* nodes, const uint64_t* offs, uint32_t
                 continue;
             }
             s += step<F_DIV | F_KECCAK | F_EVM, true>(m, w0, w1, s);
+            if (mh_produces_bool(op) && m.R[nrx][0] > 1u) {
+                // the device's Bool handlers assume canonical operands (dev_isa.h): a
+                // producer that breaks it must fail here, not only on the GPU
+                snprintf(err, errlen, "non-canonical Bool from op %u at slot %u", op, s);
+                return MH_E_INVALID;
+            }
         }
         u32 res[8];
         memcpy(res, m.R[nrx], 32);

@@ -146,3 +146,167 @@ def test_constraints_mirror_is_possible():
 
     assert is_possible([x == 1])
     assert not is_possible([x == 1, x == 2])
+
+
+# -- boundary defects of round 1 (VERDICT "What's weak" 7) -------------------------------------
+def _stat_smt_query(func):
+    """laser/smt/solver/solver_statistics.py:8-26 restated: the reference counts every z3
+    check itself, on BaseSolver.check."""
+    stats = SolverStatistics()
+
+    def wrapper(*a, **k):
+        if not stats.enabled:
+            return func(*a, **k)
+        stats.query_count += 1
+        return func(*a, **k)
+    return wrapper
+
+
+def test_fallback_queries_are_counted_once():
+    """The reference's get_model counts itself through stat_smt_query; the front end must not
+    count the same query again (solver.py:47)."""
+    stats = SolverStatistics()
+    old = (stats.enabled, stats.query_count)
+    stats.enabled = True
+    stats.query_count = 0
+    check = _stat_smt_query(lambda cs: "m")
+    frontend.configure(fallback=lambda cs, mn, mx, enf: check(cs), enabled=False)
+    try:
+        x = _x()
+        for k in range(5):
+            frontend.get_model((x == k,))
+        assert stats.query_count == 5
+    finally:
+        stats.enabled, stats.query_count = old
+
+
+class ForeignBool:
+    """A z3-backed reference Bool: no ``.ctx``, not an smt.Bool (z3 is absent here)."""
+
+    def __init__(self, k):
+        self.k = k
+
+    def __hash__(self):
+        return hash(("foreign", self.k))
+
+    def __eq__(self, other):
+        return isinstance(other, ForeignBool) and other.k == self.k
+
+
+def test_solver_log_with_foreign_terms_does_not_escape(tmp_path):
+    """--solver-log with reference terms: round 1 raised AttributeError out of get_model
+    (smtlib.to_smtlib read items[0].ctx).  Now the query is answered and logged by the writer
+    the plugin configures, or skipped when there is none."""
+    old = args.solver_log
+    args.solver_log = str(tmp_path / "log")
+    try:
+        frontend.configure(fallback=lambda *a: "z3")
+        assert frontend.get_model((ForeignBool(1),)) == "z3"
+        assert not (tmp_path / "log").exists() or not list((tmp_path / "log").iterdir())
+        frontend.configure(log_writer=lambda cs, mn, mx: "(assert foreign)\n(check-sat)\n")
+        assert frontend.get_model((ForeignBool(2),)) == "z3"
+        files = list((tmp_path / "log").iterdir())
+        assert len(files) == 1 and files[0].read_text().startswith("(assert foreign)")
+        # the reference's own get_model as fallback writes its file itself: not written twice
+        frontend.configure(fallback_logs=True)
+        assert frontend.get_model((ForeignBool(3),)) == "z3"
+        assert len(list((tmp_path / "log").iterdir())) == 1
+    finally:
+        args.solver_log = old
+
+
+class _FakeSieve:
+    def __init__(self, witness=None):
+        self.budgets = []
+        self.witness = witness
+        self.witnesses = {}
+
+    def solve(self, b, roots, key=None, budget_s=None):
+        self.budgets.append(budget_s)
+        return self.witness
+
+
+def test_sieve_budget_follows_the_solver_timeout(monkeypatch):
+    """The sieve runs inside get_model's own budget (support/model.py:26-31)."""
+    fake = _FakeSieve()
+    monkeypatch.setattr(frontend, "sieve", lambda: fake)
+    old = args.solver_timeout
+    args.solver_timeout = 1234
+    try:
+        frontend.configure(fallback=lambda *a: "z3")
+        x = _x()
+        assert frontend.get_model((x == 1,)) == "z3"
+        assert fake.budgets == [pytest.approx(1.234)]
+        t0 = (time_handler._start_time, time_handler._execution_time)
+        time_handler.start_execution(1)  # 1000 ms left -> budget min(1234, 1000 - 500)
+        try:
+            assert frontend.get_model((x == 2,)) == "z3"
+        finally:
+            time_handler._start_time, time_handler._execution_time = t0
+        assert fake.budgets[1] <= 0.5
+    finally:
+        args.solver_timeout = old
+
+
+def test_verifier_gets_the_budget_and_errors_reject(monkeypatch):
+    from mythril_amd.lower import Schema
+    from mythril_amd.sieve import Witness
+
+    fake = _FakeSieve(Witness(Schema(), {}, 0, 1))
+    monkeypatch.setattr(frontend, "sieve", lambda: fake)
+    seen = []
+
+    def verify(cs, m, timeout_ms=None):
+        seen.append(timeout_ms)
+        return True
+
+    old = args.solver_timeout
+    args.solver_timeout = 2000
+    try:
+        frontend.configure(fallback=lambda *a: "z3", verify=verify)
+        x = _x()
+        m = frontend.get_model((x == 1,))
+        assert m != "z3" and 0 < seen[0] <= 2000
+        before = SolverStatistics().sieve_rejected
+
+        def boom(cs, m, timeout_ms=None):
+            raise RuntimeError("z3 exploded")
+
+        frontend.configure(verify=boom)
+        assert frontend.get_model((x == 5,)) == "z3"
+        assert SolverStatistics().sieve_rejected == before + 1
+    finally:
+        args.solver_timeout = old
+
+
+def test_plugin_is_default_enabled_and_env_switch(monkeypatch):
+    """Only default-enabled entry-point plugins are loaded by the CLI (plugin/loader.py:73-80)."""
+    assert plugin.SievePluginBuilder.plugin_default_enabled is True
+    monkeypatch.setenv("MYTHRIL_AMD_SIEVE", "0")
+    assert plugin.SievePluginBuilder().enabled is False
+    monkeypatch.setenv("MYTHRIL_AMD_SIEVE", "1")
+    assert plugin.SievePluginBuilder().enabled is True
+
+
+def test_setup_declares_the_entry_point():
+    """plugin/discovery.py:17-21: pkg_resources.iter_entry_points("mythril.plugins")."""
+    import importlib
+    import os
+    import runpy
+
+    import setuptools
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    captured = {}
+    orig = setuptools.setup
+    setuptools.setup = lambda **kw: captured.update(kw)
+    try:
+        runpy.run_path(os.path.join(root, "setup.py"), run_name="setup")
+    finally:
+        setuptools.setup = orig
+    (line,) = captured["entry_points"]["mythril.plugins"]
+    name, target = [x.strip() for x in line.split("=")]
+    assert name == plugin.SievePluginBuilder.plugin_name
+    mod, cls = target.split(":")
+    assert getattr(importlib.import_module(mod), cls) is plugin.SievePluginBuilder
+    assert "libmythril_hip.so" in captured["package_data"]["mythril_amd"]

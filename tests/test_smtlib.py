@@ -130,3 +130,67 @@ def test_solver_log_written_by_front_end(tmp_path):
     assert len(files) == 1
     q = smtlib.parse(files[0].read_text())
     assert len(q.constraints) == 1
+
+
+def test_deep_store_and_ite_chains_parse():
+    """LASER terms nest thousands deep (a store per SSTORE, an ite per symbolic-index read);
+    the reader must not recurse (round 1 hit Python's recursion limit near depth 1000)."""
+    depth = 5000
+    arr = "s0"
+    text = ["(declare-fun s0 () (Array (_ BitVec 256) (_ BitVec 256)))",
+            "(declare-fun k () (_ BitVec 256))"]
+    t = arr
+    for i in range(depth):
+        t = "(store %s (_ bv%d 256) (_ bv%d 256))" % (t, i, i + 1)
+    e = "(select %s k)" % t
+    for i in range(depth):
+        e = "(ite (= k (_ bv%d 256)) (bvadd %s (_ bv1 256)) k)" % (i, e)
+    text.append("(assert (= %s (_ bv7 256)))" % e)
+    q = smtlib.parse("\n".join(text))
+    assert len(q.constraints) == 1
+    # a deep let chain (z3's a!N bindings)
+    lets = "(declare-fun x () (_ BitVec 8))\n(assert " + "".join(
+        "(let ((a!%d (bvadd %s #x01))) " % (i, "x" if i == 0 else "a!%d" % (i - 1))
+        for i in range(3000)) + "(= a!2999 #x00)" + ")" * 3000 + ")"
+    q2 = smtlib.parse(lets)
+    # x + 3000 == 0 (mod 256)  <=>  x == 256 - 3000 % 256
+    want = (256 - 3000 % 256) % 256
+    assert _eval(q2.ctx, q2.constraints, {"x": want}, {}, {})
+    assert not _eval(q2.ctx, q2.constraints, {"x": want + 1}, {}, {})
+
+
+class _FakeZ3Term:
+    """A z3 AST stand-in: an id and the text z3's Solver.sexpr() would print for it."""
+
+    _next = 0
+
+    def __init__(self, text):
+        _FakeZ3Term._next += 1
+        self.id = _FakeZ3Term._next
+        self.text = text
+
+    def get_id(self):
+        return self.id
+
+
+def test_importer_memory_is_bounded():
+    """A long run replays millions of is_possible queries: the importer's memo and term store
+    must stay bounded (ADVICE: Z3Importer.memo / reader.ctx grew without bound)."""
+    resets = []
+    imp = smtlib.Z3Importer(max_memo=64, max_nodes=5000, sexpr_of=lambda raw: raw.text,
+                            on_reset=lambda: resets.append(1))
+    decl = "(declare-fun x () (_ BitVec 256))\n"
+    peak = 0
+    for i in range(2000):
+        raw = _FakeZ3Term(decl + "(assert (bvult (bvmul x (_ bv%d 256)) (_ bv%d 256)))" % (i, i))
+        ctx, terms = imp([raw])
+        assert len(terms) == 1 and terms[0].ctx is ctx
+        peak = max(peak, imp.n_nodes())
+        assert len(imp.memo) <= 64
+    assert resets and imp.resets == len(resets)
+    assert peak <= 5000 + 10  # one query past the threshold at most
+    # memo hit: the same AST object is not re-read
+    raw = _FakeZ3Term(decl + "(assert (= x (_ bv1 256)))")
+    n0 = imp([raw])[1][0].node
+    before = imp.n_nodes()
+    assert imp([raw])[1][0].node == n0 and imp.n_nodes() == before
