@@ -189,8 +189,16 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
                        uint64_t row_first, uint64_t row_count, uint32_t* out /* [8*row_count] */);
 
 /* ---- measurement ----------------------------------------------------------------------------- */
-/* Integer VALU micro-benchmark: returns sustained u32 lane-ops/s for v_add_co/v_addc chains
- * (kind 0), v_mad_u64_u32 (kind 1), and v_xor/v_and (kind 2).                                    */
+/* Integer VALU issue-rate micro-benchmark (no reference counterpart: it settles the roofline peak
+ * of SURVEY.md §8d).  Runs 32 wave-instructions of one kind per loop iteration, written in asm,
+ * at `waves_per_simd` (1..8) waves on every SIMD of the chip, and returns the sustained lane-ops/s
+ * (wave-instructions/s x 64).  Kinds: 0 v_add_co/v_addc 256-bit carry chains; 1 v_mad_u64_u32;
+ * 2 v_add_u32; 3 v_xor_b32; 4 v_alignbit_b32; 5 v_cndmask_b32; 6 v_or3_b32; 7 v_readlane_b32;
+ * 8 v_mov_b32; 9 v_add_co_u32 (carry-out only); 10 v_sub_co/v_subb through VCC.              */
+#define MH_MB_NUM_KINDS 11
+int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
+                            double* lane_ops_per_s);
+/* Round-1 form: kinds 0..2 of mh_microbench_issue at 8 waves per SIMD.                           */
 int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s);
 /* Kernel timing on the ctx stream.  While enabled, every sieve launch (mh_run / mh_run_async) is
  * bracketed by HIP events recorded on the ctx stream itself, so the measured span is exactly the

@@ -552,10 +552,14 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
     return MH_OK;
 }
 
-int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s) {
-    if (!ctx || !ops_per_s || kind > 2) return set_err(MH_E_INVALID, "bad argument");
+int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
+                            double* lane_ops_per_s) {
+    if (!ctx || !lane_ops_per_s || kind >= MH_MB_NUM_KINDS || waves_per_simd == 0 ||
+        waves_per_simd > 8)
+        return set_err(MH_E_INVALID, "bad argument");
     if (int32_t r = use_device(ctx)) return r;
-    const uint32_t blocks = 256 * 8, iters = 4096;
+    // 256 CUs x 4 SIMDs; a 256-thread workgroup is 4 waves, one per SIMD of its CU
+    const uint32_t blocks = 256u * waves_per_simd, iters = 8192;
     hipEvent_t e0, e1;
     MH_HIP(hipEventCreate(&e0));
     MH_HIP(hipEventCreate(&e1));
@@ -568,12 +572,17 @@ int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s) {
     MH_HIP(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    // u32 ops per lane per iteration: kind 0 = 32 (4 x 8-limb add chains), 1 = 8 mads,
-    // 2 = 64 (32 xor + 32 add)
-    const double per_iter = kind == 0 ? 32.0 : kind == 1 ? 8.0 : 64.0;
+    // 32 wave-instructions of the measured kind per iteration (kind 7: 32 readlanes + 1 SALU)
     const double lanes = (double)blocks * 256.0;
-    *ops_per_s = lanes * iters * per_iter / (ms * 1e-3);
+    *lane_ops_per_s = lanes * iters * 32.0 / (ms * 1e-3);
     return MH_OK;
+}
+
+int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s) {
+    // round-1 entry point: kind 0 add/addc chains, 1 v_mad_u64_u32, 2 v_add_u32 (no carry),
+    // each at 8 waves per SIMD
+    if (kind > 2) return set_err(MH_E_INVALID, "bad argument");
+    return mh_microbench_issue(ctx, kind, 8, ops_per_s);
 }
 
 int32_t mh_ctx_enable_timing(mh_ctx* ctx, int32_t enable) {

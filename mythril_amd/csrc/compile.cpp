@@ -119,14 +119,7 @@ bool xform_enabled(uint32_t op) {
     return (mask & g) != 0;
 }
 
-struct VInsn {
-    uint8_t op;       // device op (the *_R form for asm pairs); D_ITE here = generic select
-    int d, a, b, c;   // virtual registers (-1 = none)
-    uint32_t width;   // 1..256
-    uint32_t aux;     // immediate (shift amount, SEXT source width, LOADVAR column)
-    int cidx;         // inline constant y (pool index), -1 = none
-    uint32_t w1raw;   // D_KECCAK second word (lengths)
-};
+typedef SsaInsn VInsn;
 
 struct Piece {
     int vreg;
@@ -852,10 +845,10 @@ int fold_constants(Lowering& L, int root_v) {
 
 }  // namespace
 
-int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
-                     uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
-                     std::unordered_map<std::string, uint32_t>& dconst_index,
-                     std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
+int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
+                       uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
+                       std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,
+                       std::string& err) {
     if (n_nodes == 0) {
         err = "empty tape";
         return MH_E_INVALID;
@@ -869,8 +862,7 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
     }
     // algorithmic work per evaluation: the nodes whose value depends on the assignment (the
     // others are folded to constants on the host, fold_constants)
-    out.alg_ops = 0;
-    out.n_nodes = (uint32_t)n_nodes;
+    st.alg_ops = 0;
     std::vector<char> dep(n_nodes, 0);
     for (size_t i = 0; i < n_nodes; ++i) {
         const mh_node& nd = t[i];
@@ -878,11 +870,8 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
         const int ar = arity(nd);
         const uint32_t ops[3] = {nd.a, nd.b, nd.c};
         for (int k = 0; k < ar; ++k) dep[i] |= dep[ops[k]];
-        if (dep[i]) out.alg_ops += op_cost(nd, t);
+        if (dep[i]) st.alg_ops += op_cost(nd, t);
     }
-
-    std::vector<VInsn>& code = L.code;
-    const int n_pinned = L.pinned ? (int)n_vars : 0;
     // root: X after the last instruction must hold it
     int root_v = L.vreg_of((uint32_t)(n_nodes - 1));
     if (root_v < 0) {
@@ -890,8 +879,31 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
         return MH_E_UNSUPPORTED;
     }
     if (!std::getenv("MH_NO_FOLD")) root_v = fold_constants(L, root_v);
-    if (code.empty() || code.back().d != root_v) L.emit(D_NOP, root_v);
-    out.features = L.features;
+    st.code.swap(L.code);
+    st.root = root_v;
+    st.n_vregs = L.n_vregs;
+    st.n_pinned = L.pinned ? (int)n_vars : 0;
+    st.features = L.features;
+    st.root_bool = t.back().width == 0;
+    return MH_OK;
+}
+
+int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
+                     uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
+                     std::unordered_map<std::string, uint32_t>& dconst_index,
+                     std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
+    SsaTape st;
+    if (int32_t r = lower_tape_ssa(nodes, n_nodes, consts, n_consts, n_vars, dconsts,
+                                   dconst_index, st, err))
+        return r;
+    out.alg_ops = st.alg_ops;
+    out.n_nodes = (uint32_t)n_nodes;
+    std::vector<VInsn>& code = st.code;
+    const int n_pinned = st.n_pinned;
+    int root_v = st.root;
+    if (code.empty() || code.back().d != root_v)
+        code.push_back(VInsn{D_NOP, st.n_vregs++, root_v, -1, -1, 256, 0, -1, 0});
+    out.features = st.features;
 
     // ---- accumulator pass: which operand each instruction finds in X ----
     std::vector<char> lda(code.size(), 0);
@@ -933,7 +945,7 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
         acc = v.d;
     }
     // register uses: loads of the first operand (LDA), y operands, the third operand
-    const int nv = L.n_vregs;
+    const int nv = st.n_vregs;
     std::vector<int> last_use(nv, -1);
     std::vector<char> needs_reg(nv, 0);
     for (int r = 0; r < n_pinned; ++r) needs_reg[r] = 1;
@@ -979,7 +991,7 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
     }
     const uint32_t nrx = mh_nrx_of((uint32_t)peak);
     out.n_regs = (uint32_t)std::max(peak, 1);
-    out.root_bool = t.back().width == 0;
+    out.root_bool = st.root_bool;
 
     // ---- encode + slot layout ----
     std::vector<uint32_t> slots;  // pairs (w0, w1)

@@ -20,6 +20,36 @@ struct CompiledTape {
     uint64_t alg_ops = 0;
 };
 
+// One instruction of a lowered tape in SSA form (before the interpreter's accumulator pass and
+// register allocation): device op (dev_isa.h; the *_R form of an asm pair, the inline constant
+// in `cidx`), destination and operand virtual registers (-1 = none).  D_ITE here is the generic
+// select (a = cond, b = then, c = else).  Shared by the interpreter's encoder (compile.cpp) and
+// the native-code JIT (jit.cpp).
+struct SsaInsn {
+    uint8_t op;
+    int d, a, b, c;
+    uint32_t width;   // 1..256
+    uint32_t aux;     // immediate (shift amount, SEXT source width, LOADVAR column)
+    int cidx;         // inline constant y (index into the 8-limb constant pool), -1 = none
+    uint32_t w1raw;   // D_KECCAK second word (lengths)
+};
+
+struct SsaTape {
+    std::vector<SsaInsn> code;
+    int root = -1;        // the root's virtual register
+    int n_vregs = 0;      // virtual registers 0..n_pinned-1 are the pinned assignment columns
+    int n_pinned = 0;
+    uint32_t features = 0;
+    bool root_bool = false;
+    uint64_t alg_ops = 0;
+};
+
+// Lower one tape to SSA, fold constants and drop dead code (compile_tape's first half).
+int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
+                       uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
+                       std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& out,
+                       std::string& err);
+
 // Lower one tape.  Appends its instruction words (2 per instruction) to `words` and any new
 // constants to the shared device pool `dconsts` (8 limbs each, deduplicated via dconst_index).
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,

@@ -310,50 +310,84 @@ __global__ void __launch_bounds__(kBlock) generate_kernel(u32* assign, u64 capac
     }
 }
 
-// Integer VALU throughput probe.  kind 0: v_add_co/v_addc 256-bit carry chains (4 independent
-// chains, 32 VALU per iteration); kind 1: v_mad_u64_u32 (8 independent chains); kind 2:
-// v_xor + v_add (64 VALU per iteration).  Reported as u32 lane-ops/s = VALU lane-instructions/s.
-__global__ void __launch_bounds__(kBlock) microbench_kernel(u32 kind, u32 iters, u32* sink) {
-    u32 s[4][8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s[j][k] = threadIdx.x * 2654435761u + 8 * j + k;
+// Integer VALU issue-rate probe: 32 wave-instructions of ONE kind per loop iteration, written in
+// asm so the compiler can neither fuse nor drop them (round 1's C++ kind 2 could compile
+// xor + add into one v_xad_u32).  Eight independent accumulators per lane (dependency distance
+// 8), the launch's occupancy set by `blocks` (256 threads = 4 waves each).  Kinds (dev_isa.h
+// mh_mb_kind): 0 v_add_co/v_addc 256-bit carry chains (4 chains, each its own SGPR carry pair);
+// 1 v_mad_u64_u32; 2 v_add_u32; 3 v_xor_b32; 4 v_alignbit_b32; 5 v_cndmask_b32 (SGPR mask);
+// 6 v_or3_b32; 7 v_readlane_b32 (VALU -> SGPR); 8 v_mov_b32; 9 v_add_co_u32 with a VCC carry-out
+// but no carry-in (independent); 10 v_sub_co_u32 chains through VCC (one chain, dependent).
+#define MB8(op) op op op op op op op op
+template <int KIND>
+__global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink) {
+    u32 a0 = threadIdx.x * 2654435761u, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+        a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     const u32 y = blockIdx.x | 1u;
-    if (kind == 0) {
-        for (u32 i = 0; i < iters; ++i) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                u32 c = 0;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s[j][k] = addc32(s[j][k], s[(j + 1) & 3][k], c, &c);
-            }
-        }
-    } else if (kind == 1) {
-        u64 acc[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = s[0][k];
-        for (u32 i = 0; i < iters; ++i) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc[k] = (u64)(u32)acc[k] * (y + k) + (acc[k] >> 32);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s[0][k] = (u32)acc[k] ^ (u32)(acc[k] >> 32);
-    } else {
-        for (u32 i = 0; i < iters; ++i) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s[j][k] = (s[j][k] ^ y) + k;
+    for (u32 i = 0; i < iters; ++i) {
+        if constexpr (KIND == 0) {
+            // 4 independent 8-limb chains = 32 instructions
+            asm volatile(
+                MB8("v_add_co_u32 %0, s[20:21], %0, %8\n v_addc_co_u32 %1, s[20:21], %1, %8, s[20:21]\n"
+                    "v_addc_co_u32 %2, s[20:21], %2, %8, s[20:21]\n v_addc_co_u32 %3, s[20:21], %3, %8, s[20:21]\n")
+                : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                : "v"(y) : "s20", "s21");
+        } else if constexpr (KIND == 1) {
+            u64 m0 = ((u64)a1 << 32) | a0, m1 = ((u64)a3 << 32) | a2, m2 = ((u64)a5 << 32) | a4,
+                m3 = ((u64)a7 << 32) | a6;
+            asm volatile(MB8("v_mad_u64_u32 %0, s[20:21], %4, %5, %0\n v_mad_u64_u32 %1, s[22:23], %4, %5, %1\n"
+                             "v_mad_u64_u32 %2, s[24:25], %4, %5, %2\n v_mad_u64_u32 %3, s[26:27], %4, %5, %3\n")
+                         : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3) : "v"(y ^ 0x9E3779B9u), "v"(y)
+                         : "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+            a0 = (u32)m0; a1 = (u32)(m0 >> 32); a2 = (u32)m1; a3 = (u32)(m1 >> 32);
+            a4 = (u32)m2; a5 = (u32)(m2 >> 32); a6 = (u32)m3; a7 = (u32)(m3 >> 32);
+        } else if constexpr (KIND == 7) {
+            u32 acc = 0;
+            asm volatile(MB8("v_readlane_b32 s20, %1, 1\n v_readlane_b32 s21, %1, 2\n"
+                             "v_readlane_b32 s22, %1, 3\n v_readlane_b32 s23, %1, 4\n")
+                         "s_add_u32 %0, s20, s23\n"
+                         : "+s"(acc) : "v"(a0) : "s20", "s21", "s22", "s23");
+            a1 += acc;
+        } else if constexpr (KIND == 10) {
+            asm volatile(MB8("v_sub_co_u32 %0, vcc, %0, %8\n v_subb_co_u32 %1, vcc, %1, %8, vcc\n"
+                             "v_subb_co_u32 %2, vcc, %2, %8, vcc\n v_subb_co_u32 %3, vcc, %3, %8, vcc\n")
+                         : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                         : "v"(y) : "vcc");
+        } else {
+#define MB_ONE(ins) asm volatile(MB8(ins " %0, %0, %8\n " ins " %1, %1, %8\n " ins " %2, %2, %8\n " ins " %3, %3, %8\n") \
+    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(y))
+            if constexpr (KIND == 2) MB_ONE("v_add_u32");
+            if constexpr (KIND == 3) MB_ONE("v_xor_b32");
+            if constexpr (KIND == 4)
+                asm volatile(MB8("v_alignbit_b32 %0, %0, %1, 7\n v_alignbit_b32 %1, %1, %2, 9\n"
+                                 "v_alignbit_b32 %2, %2, %3, 11\n v_alignbit_b32 %3, %3, %4, 13\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+            if constexpr (KIND == 5)
+                asm volatile("s_mov_b64 s[20:21], 0x5555\n"
+                             MB8("v_cndmask_b32_e64 %0, %0, %8, s[20:21]\n v_cndmask_b32_e64 %1, %1, %8, s[20:21]\n"
+                                 "v_cndmask_b32_e64 %2, %2, %8, s[20:21]\n v_cndmask_b32_e64 %3, %3, %8, s[20:21]\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y) : "s20", "s21");
+            if constexpr (KIND == 6)
+                asm volatile(MB8("v_or3_b32 %0, %0, %8, %4\n v_or3_b32 %1, %1, %8, %5\n"
+                                 "v_or3_b32 %2, %2, %8, %6\n v_or3_b32 %3, %3, %8, %7\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y));
+            if constexpr (KIND == 8)
+                asm volatile(MB8("v_mov_b32 %0, %4\n v_mov_b32 %1, %5\n v_mov_b32 %2, %6\n v_mov_b32 %3, %7\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+            if constexpr (KIND == 9)
+                asm volatile(MB8("v_add_co_u32 %0, vcc, %0, %8\n v_add_co_u32 %1, vcc, %1, %8\n"
+                                 "v_add_co_u32 %2, vcc, %2, %8\n v_add_co_u32 %3, vcc, %3, %8\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y) : "vcc");
+#undef MB_ONE
         }
     }
-    u32 r = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r ^= s[j][k];
+    const u32 r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
     if (r == 0x12345678u) sink[0] = r;
 }
+#undef MB8
 
 // Minimum waves per SIMD a variant is compiled for (amdgpu_waves_per_eu; 1 = the natural register
 // allocation).  Occupancy decides this latency-bound interpreter's issue rate, so variants whose
@@ -412,8 +446,14 @@ hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars,
 
 hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uint32_t* sink,
                              hipStream_t stream) {
-    hipLaunchKernelGGL(microbench_kernel, dim3(blocks), dim3(kBlock), 0, stream, kind, iters,
-                       sink);
+    switch (kind) {
+#define MB_CASE(k) \
+    case k: hipLaunchKernelGGL(microbench_kernel<k>, dim3(blocks), dim3(kBlock), 0, stream, iters, sink); break;
+        MB_CASE(0) MB_CASE(1) MB_CASE(2) MB_CASE(3) MB_CASE(4) MB_CASE(5) MB_CASE(6) MB_CASE(7)
+        MB_CASE(8) MB_CASE(9) MB_CASE(10)
+#undef MB_CASE
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -62,9 +62,15 @@ SIGNATURES = {
                                  C.c_uint64, C.c_uint32, _vp, _vp]),
     "mh_eval_values": (C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint64, C.c_uint64, _u32p]),
     "mh_microbench_valu": (C.c_int32, [_vp, C.c_uint32, C.POINTER(C.c_double)]),
+    "mh_microbench_issue": (C.c_int32, [_vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]),
     "mh_ctx_enable_timing": (C.c_int32, [_vp, C.c_int32]),
     "mh_ctx_kernel_time": (C.c_int32, [_vp, C.POINTER(C.c_double), _u64p]),
 }
+
+
+# mh_microbench_issue kinds (include/mythril_hip.h)
+MB_KINDS = ("add_co_chain", "mad_u64_u32", "add_u32", "xor_b32", "alignbit_b32", "cndmask_b32",
+            "or3_b32", "readlane_b32", "mov_b32", "add_co_nocarryin", "sub_co_vcc_chain")
 
 
 class NativeUnavailable(RuntimeError):
@@ -200,9 +206,10 @@ class Context:
         _check(self.lib.mh_ctx_kernel_time(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
-    def microbench(self, kind: int) -> float:
+    def microbench(self, kind: int, waves_per_simd: int = 8) -> float:
+        """Sustained lane-ops/s of one instruction kind (mh_microbench_issue; MB_KINDS)."""
         v = C.c_double()
-        _check(self.lib.mh_microbench_valu(self.h, kind, C.byref(v)))
+        _check(self.lib.mh_microbench_issue(self.h, kind, waves_per_simd, C.byref(v)))
         return v.value
 
 

@@ -100,3 +100,14 @@ def benchmark(ts, seed: int, seconds: float = 15.0, tapes: int = 100):
         "sample": "oracle/tape_eval.c (OpenMP, %d threads): first %d synthetic tapes x %d "
                   "generated rows, %.1f s" % (th, tapes, rows, dt),
     }
+
+
+def eval_pairs(ts, seed: int, tapes, rows):
+    """[bool]: tape tapes[i] evaluated (C oracle) on generated row rows[i] — re-checks witness
+    indices reported by the device."""
+    from . import smt_eval
+
+    out = []
+    for t, r in zip(tapes, rows):
+        out.append(evaluate(ts, int(t), smt_eval.gen_assignment(seed, ts.n_vars, int(r))) != 0)
+    return out

@@ -285,6 +285,96 @@ def test_full_size_properties(gpu_ctx):
     assert np.array_equal(np.sum(parts_c, axis=0), hc)
 
 
+EIP145 = json.load(open(os.path.join(HERE, "golden", "eip145.json")))
+_SHIFT_OP = {"shl": Op.BVSHL, "shr": Op.BVLSHR, "sar": Op.BVASHR}
+
+
+@pytest.mark.parametrize("op", ["shl", "shr", "sar"])
+def test_eip145_on_gpu(gpu_ctx, op):
+    """The EIP-145 SHL/SHR/SAR vectors (tests/instructions/{shl,shr,sar}_test.py of the
+    reference, instructions.py:528-552) through the kernel, three ways: folded on the host (both
+    operands constant), value and shift both assignment columns (the per-lane variable-shift
+    handlers), and value a column with the shift constant (the limb-specialised immediate
+    shifts)."""
+    vecs = EIP145[op]
+    vals = [int(v["value"], 16) for v in vecs]
+    shifts = [int(v["shift"], 16) for v in vecs]
+    want = [int(v["expected"], 16) for v in vecs]
+    # folded
+    ts = TapeSet()
+    b = ts.builder()
+    for v, sh in zip(vals, shifts):
+        ts.add(b.finish(b.op(_SHIFT_OP[op], b.const(v, 256), b.const(sh, 256))))
+    ct = gpu_ctx.compile(ts)
+    a = gpu_ctx.assignments(1, 1)
+    a.upload(np.zeros((1, 8, 1), dtype=np.uint32))
+    for i in range(len(vecs)):
+        assert native.limbs_to_ints(native.eval_values(gpu_ctx, ct, i, a))[0] == want[i], (op, i)
+    # lifted: one tape, one row per vector
+    ts = TapeSet()
+    b = ts.builder()
+    ts.add(b.finish(b.op(_SHIFT_OP[op], b.var("value"), b.var("shift"))))
+    soa = np.zeros((2, 8, len(vecs)), dtype=np.uint32)
+    for r, (v, sh) in enumerate(zip(vals, shifts)):
+        for k in range(8):
+            soa[0, k, r] = (v >> (32 * k)) & 0xFFFFFFFF
+            soa[1, k, r] = (sh >> (32 * k)) & 0xFFFFFFFF
+    ct = gpu_ctx.compile(ts)
+    a = upload(gpu_ctx, soa)
+    assert native.limbs_to_ints(native.eval_values(gpu_ctx, ct, 0, a)) == want, op
+    # shift constant, value a column: one tape per vector, evaluated on its own row
+    ts = TapeSet()
+    b = ts.builder()
+    for sh in shifts:
+        ts.add(b.finish(b.op(_SHIFT_OP[op], b.var("value"), b.const(sh, 256))))
+    soa1 = np.ascontiguousarray(soa[:1])
+    ct = gpu_ctx.compile(ts)
+    a = upload(gpu_ctx, soa1)
+    for i in range(len(vecs)):
+        got = native.limbs_to_ints(native.eval_values(gpu_ctx, ct, i, a))
+        assert got[i] == want[i], (op, i)
+
+
+def test_bench_config_pinned(gpu_ctx):
+    """bench.py's own workload at full size (all 10^4 config-5 tapes x 2^23 rows, one GPU's
+    shard): exact per-tape counts and first hits of a 32-tape sample against the C oracle over
+    all 2^23 rows, every reported witness of every tape re-checked by the oracle, first-hit mode
+    equal to count mode, and the count of tapes with a witness recorded for the bench line."""
+    from oracle import ctape
+
+    ts = synth.generate()
+    seed, rows = synth.load_spec()["assignment_seed"], 1 << 23
+    ct = gpu_ctx.compile(ts)
+    a = gpu_ctx.assignments(ts.n_vars, rows)
+    a.generate(seed, 0)
+    fh, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    fh1, _ = native.run(gpu_ctx, ct, a, mode=native.MODE_FIRST_HIT)
+    assert np.array_equal(fh, fh1)
+    hit = np.nonzero(fh != native.NO_HIT)[0]
+    assert np.array_equal(hit, np.nonzero(hc > 0)[0])
+    # every witness of every tape: the oracle evaluates that (tape, row) to true
+    w_rows = [int(fh[t]) for t in hit]
+    ok = ctape.eval_pairs(ts, seed, [int(t) for t in hit], w_rows)
+    assert all(ok), [int(t) for t, g in zip(hit, ok) if not g][:10]
+    rng = random.Random(23)
+    pick = sorted(rng.sample(range(len(ts.tapes)), 32))
+    sub = TapeSet(ts.var_names)
+    sub.pool = ts.pool
+    sub.tapes = [ts.tapes[t] for t in pick]
+    cnt, first = ctape.count(sub, seed, 0, rows, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(hc[pick], cnt), "hit counts differ from the C oracle"
+    assert np.array_equal(fh[pick], first), "first hits differ from the C oracle"
+    print("bench config: %d tapes with a witness, %d total hits" % (len(hit), int(hc.sum())))
+
+
+def test_microbench_issue(gpu_ctx):
+    """mh_microbench_issue runs every kind and reports a plausible rate (below 2x the nominal
+    2-cycle wave64 issue rate of 78.6 T lane-ops/s)."""
+    for kind in range(len(native.MB_KINDS)):
+        r = gpu_ctx.microbench(kind, 4)
+        assert 1e11 < r < 2 * 78.7e12, (native.MB_KINDS[kind], r)
+
+
 def test_unsupported_and_invalid(gpu_ctx):
     ts = TapeSet()
     b = ts.builder()
