@@ -51,6 +51,10 @@ def main() -> None:
     ap.add_argument("--variant", choices=["plain", "keccak"], default="plain",
                     help="keccak: SURVEY §8d's keccak variant (one keccak256 of a 512-bit "
                          "input per tape); the headline line is the plain config 5")
+    ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
+                    help="jit: per-tape native gfx950 code (mh_tapes_jit), the interpreter only "
+                         "for tapes the JIT does not cover; interp: the threaded-code interpreter")
+    ap.add_argument("--max-vgpr", type=int, default=0, help="JIT register budget (0: default)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -79,6 +83,10 @@ def main() -> None:
     ctx.set_stream(stream.cuda_stream)
     ct = ctx.compile(ts)
     info = ct.info()
+    jit_info = None
+    if args.engine == "jit":
+        jit_info = ct.jit(max_vgpr=args.max_vgpr)
+        log("[rank %d] jit: %s" % (rank, jit_info))
     alg_ops_per_row = sum(int(i["alg_ops"]) for i in info)
     index_base, rows = shard.shard_range(rank, world, args.rows_per_gpu)
     seed = spec["assignment_seed"]
@@ -168,11 +176,13 @@ def main() -> None:
             "rows_per_gpu": rows,
             "vars": ts.n_vars,
             "mode": "count_all",
+            "engine": args.engine,
             "parallelism": "dp%d (row shards, all-reduce of per-tape results)" % world,
         },
         "per_gpu": value / world,
         "kernel_ms": kms,
         "tapes_with_witness": hits,
+        "jit": jit_info,
         "roofline": {
             "bound": "valu",
             "achieved": achieved,

@@ -189,6 +189,37 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
                        uint64_t row_first, uint64_t row_count, uint32_t* out /* [8*row_count] */);
 
 /* ---- measurement ----------------------------------------------------------------------------- */
+/* ---- native-code path (no reference counterpart: replaces the interpreter for throughput runs)
+ * mh_tapes_jit compiles every tape of the set that the JIT covers (the asm-core op set plus the
+ * division family, at most 4 assignment columns) to straight-line gfx950 machine code -- one
+ * code object per slice of tape groups, assembled in-process by comgr and loaded with
+ * hipModuleLoadData (src/jit.cpp).  Afterwards mh_run / mh_run_async over the whole tape set run
+ * the jitted tapes through that code and the rest through the interpreter; results are
+ * identical.  flags: MH_JIT_VALUES also builds the values kernel behind mh_jit_eval_all.
+ * max_vgpr: register budget per wave (occupancy = 512 / max_vgpr waves per SIMD), 0 = default
+ * 128.  Cost: a few seconds per thousand tapes, once per tape set, outside any timed region.      */
+#define MH_JIT_VALUES 1u
+typedef struct mh_jit_info {
+    uint32_t n_jitted;         /* tapes on the native path                                        */
+    uint32_t n_groups;         /* tape groups (grid rows of the JIT kernels)                      */
+    uint32_t n_modules;        /* code objects                                                    */
+    uint32_t max_vgpr;         /* VGPRs per wave of the JIT kernels                               */
+    uint64_t code_bytes;       /* machine code, all code objects                                  */
+    uint64_t valu_static;      /* static VALU instructions over the jitted tapes (division calls
+                                  not expanded)                                                   */
+    uint64_t valu_wide_static; /* ... of them in the 4-cycle class (VOP3, carry / compare writes) */
+    double build_ms;           /* emission + assembly + load                                      */
+} mh_jit_info;
+int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr);
+int32_t mh_tapes_jit_info(const mh_tapeset* ts, mh_jit_info* out);
+/* 1 if tape t runs on the native path.                                                           */
+int32_t mh_tapes_jitted(const mh_tapeset* ts, uint8_t* out /* [n_tapes] */, uint32_t n_tapes);
+/* Parity path of the native code: root values of every jitted tape over rows
+ * [row_first, row_first + row_count), out = [n_tapes][8][row_count] u32 (slots of tapes not on
+ * the native path are left untouched).  Needs mh_tapes_jit(ts, MH_JIT_VALUES, ...).              */
+int32_t mh_jit_eval_all(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as,
+                        uint64_t row_first, uint64_t row_count, uint32_t* out);
+
 /* Integer VALU issue-rate micro-benchmark (no reference counterpart: it settles the roofline peak
  * of SURVEY.md §8d).  Runs 32 wave-instructions of one kind per loop iteration, written in asm,
  * at `waves_per_simd` (1..8) waves on every SIMD of the chip, and returns the sustained lane-ops/s

@@ -5,16 +5,20 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
 #include "../../include/mythril_hip.h"
 #include "compile.h"
 #include "dev_isa.h"
+#include "jit.h"
 #include "kernels.h"
 
 struct mh_ctx {
@@ -39,6 +43,24 @@ struct mh_tapeset {
     uint32_t* d_ids = nullptr;
     std::vector<uint32_t> ids;
     uint32_t bucket_off[mh::kNumVariants + 1] = {};
+    // host copy of the IR, for mh_tapes_jit
+    std::vector<mh_node> h_nodes;
+    std::vector<uint64_t> h_offs;
+    std::vector<uint32_t> h_consts;
+    // native-code path (mh_tapes_jit): one module per slice of tape groups; the interpreter's
+    // buckets restricted to the tapes the JIT does not take
+    struct JitMod {
+        hipModule_t mod = nullptr, vmod = nullptr;
+        hipFunction_t fn = nullptr, vfn = nullptr;
+        uint32_t n_groups = 0;
+    };
+    std::vector<JitMod> jit;
+    std::vector<uint8_t> jitted;
+    bool has_jit = false;
+    uint32_t* d_ids_rest = nullptr;
+    std::vector<uint32_t> ids_rest;
+    uint32_t bucket_off_rest[mh::kNumVariants + 1] = {};
+    mh_jit_info jinfo{};
 };
 
 struct mh_assign {
@@ -118,6 +140,46 @@ mh::KParams make_params(const mh_tapeset* ts, uint32_t tape_first, const mh_assi
     p.index_base = index_base;
     p.mode = mode;
     return p;
+}
+
+// Rows per workgroup of the JIT kernels: 4 waves, each over a contiguous run of 64-row chunks.
+uint32_t jit_rows_per_wg(uint64_t row_count) {
+    uint64_t r = 256;
+    while (r < 16384 && r * 2048 < row_count) r *= 2;  // >= ~2048 row blocks before growing
+    return (uint32_t)r;
+}
+
+int32_t launch_jit(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as, uint64_t row_first,
+                   uint64_t row_count, uint64_t index_base, uint32_t mode, uint64_t* d_first_hit,
+                   uint64_t* d_hit_count, uint32_t* d_values) {
+    mh::jit::KernArgs a{};
+    a.assign = (uint64_t)(uintptr_t)as->d;
+    a.capacity = as->capacity;
+    a.row_first = row_first;
+    a.row_count = row_count;
+    a.index_base = index_base;
+    a.first_hit = (uint64_t)(uintptr_t)d_first_hit;
+    a.hit_count = (uint64_t)(uintptr_t)d_hit_count;
+    a.rows_per_wg = jit_rows_per_wg(row_count);
+    a.n_rowblocks = (uint32_t)((row_count + a.rows_per_wg - 1) / a.rows_per_wg);
+    a.values_out = (uint64_t)(uintptr_t)d_values;
+    a.mode = mode;
+    if (as->capacity >= (1ull << 30) || row_first + row_count > (1ull << 31))
+        return set_err(MH_E_UNSUPPORTED, "JIT kernels address < 2^30 rows per column");
+    for (const auto& j : ts->jit) {
+        hipFunction_t fn = d_values ? j.vfn : j.fn;
+        if (!fn || !j.n_groups) continue;
+        for (uint32_t g0 = 0; g0 < j.n_groups; g0 += 65535) {
+            a.group_first = g0;
+            const uint32_t gy = std::min<uint32_t>(65535, j.n_groups - g0);
+            size_t sz = sizeof(a);
+            void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                           HIP_LAUNCH_PARAM_END};
+            MH_HIP(hipModuleLaunchKernel(fn, a.n_rowblocks, gy, 1, 256, 1, 1, 0, ctx->stream,
+                                         nullptr, cfg));
+        }
+    }
+    return MH_OK;
 }
 
 }  // namespace
@@ -255,6 +317,14 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     ts->ctx = ctx;
     ts->n_tapes = n_tapes;
     ts->n_vars = n_vars;
+    try {
+        ts->h_nodes.assign(nodes, nodes + (n_tapes ? tape_offsets[n_tapes] : 0));
+        ts->h_offs.assign(tape_offsets, tape_offsets + n_tapes + 1);
+        ts->h_consts.assign(consts, consts + (size_t)n_consts * 8);
+    } catch (const std::bad_alloc&) {
+        delete ts;
+        return set_err(MH_E_NOMEM, "host copy of the tapes");
+    }
     ts->ids = std::move(ids);
     for (uint32_t v = 0; v <= mh::kNumVariants; ++v) ts->bucket_off[v] = bucket_off[v];
     ts->info = std::move(info);
@@ -287,6 +357,11 @@ int32_t mh_tapes_destroy(mh_tapeset* ts) {
     if (ts->d_tapes) (void)hipFree(ts->d_tapes);
     if (ts->d_consts) (void)hipFree(ts->d_consts);
     if (ts->d_ids) (void)hipFree(ts->d_ids);
+    if (ts->d_ids_rest) (void)hipFree(ts->d_ids_rest);
+    for (auto& j : ts->jit) {
+        if (j.mod) (void)hipModuleUnload(j.mod);
+        if (j.vmod) (void)hipModuleUnload(j.vmod);
+    }
     delete ts;
     return MH_OK;
 }
@@ -481,14 +556,24 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
         ctx->spans.push_back(sp);
         MH_HIP(hipEventRecord(sp.first, ctx->stream));
     }
+    // the native code takes the jitted tapes of a whole-set run; the interpreter the rest
+    const bool use_jit = ts->has_jit && tape_first == 0 && tape_count == ts->n_tapes;
+    if (use_jit && row_count) {
+        if (int32_t r = launch_jit(ctx, ts, as, row_first, row_count, index_base, mode,
+                                   d_first_hit, d_hit_count, nullptr))
+            return r;
+    }
+    const std::vector<uint32_t>& ids = use_jit ? ts->ids_rest : ts->ids;
+    const uint32_t* boff = use_jit ? ts->bucket_off_rest : ts->bucket_off;
+    uint32_t* d_ids = use_jit ? ts->d_ids_rest : ts->d_ids;
     // one launch per kernel-variant bucket, over the bucket's tapes inside the requested range
     for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
-        const uint32_t* b = ts->ids.data() + ts->bucket_off[v];
-        const uint32_t* e = ts->ids.data() + ts->bucket_off[v + 1];
+        const uint32_t* b = ids.data() + boff[v];
+        const uint32_t* e = ids.data() + boff[v + 1];
         const uint32_t* lo = std::lower_bound(b, e, tape_first);
         const uint32_t* hi = std::lower_bound(lo, e, tape_first + tape_count);
         if (hi == lo) continue;
-        p.tape_ids = ts->d_ids + (lo - ts->ids.data());
+        p.tape_ids = d_ids + (lo - ids.data());
         p.n_ids = (uint32_t)(hi - lo);
         MH_HIP(mh::launch_sieve(p, v, ctx->stream));
     }
@@ -549,6 +634,130 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
     (void)hipFree(d);
     if (e != hipSuccess)
         return set_err(MH_E_DEVICE, std::string("mh_eval_values: ") + hipGetErrorString(e));
+    return MH_OK;
+}
+
+int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
+    if (!ts) return set_err(MH_E_INVALID, "null tapeset");
+    if (ts->has_jit) return set_err(MH_E_INVALID, "tapeset already has native code");
+    if (int32_t r = use_device(ts->ctx)) return r;
+    const auto t0 = std::chrono::steady_clock::now();
+    mh::jit::Options opt;
+    opt.max_vgpr = max_vgpr ? max_vgpr : 128;
+    if (opt.max_vgpr > 512 || opt.max_vgpr < 96) return set_err(MH_E_INVALID, "max_vgpr outside 96..512");
+    uint32_t threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("MH_JIT_THREADS")) threads = (uint32_t)std::max(1, atoi(e));
+    std::vector<mh::jit::Built> built;
+    mh::jit::BuildStats stats;
+    std::string err;
+    bool ok;
+    try {
+        ok = mh::jit::build_tapeset(ts->h_nodes.data(), ts->h_offs.data(), ts->n_tapes,
+                                    ts->h_consts.data(), (uint32_t)(ts->h_consts.size() / 8),
+                                    ts->n_vars, (flags & MH_JIT_VALUES) != 0, opt, threads, built,
+                                    stats, err);
+    } catch (const std::bad_alloc&) {
+        return set_err(MH_E_NOMEM, "host allocation during JIT build");
+    }
+    if (!ok) return set_err(MH_E_UNSUPPORTED, "JIT: " + err);
+    std::vector<mh_tapeset::JitMod> mods;
+    auto unload = [&]() {
+        for (auto& j : mods) {
+            if (j.mod) (void)hipModuleUnload(j.mod);
+            if (j.vmod) (void)hipModuleUnload(j.vmod);
+        }
+    };
+    uint32_t maxv = 0;
+    for (const auto& b : built) {
+        if (b.hsaco.empty()) continue;
+        mh_tapeset::JitMod j;
+        j.n_groups = b.n_groups;
+        hipError_t e = hipModuleLoadData(&j.mod, b.hsaco.data());
+        if (e == hipSuccess) e = hipModuleGetFunction(&j.fn, j.mod, "mh_jit");
+        if (e == hipSuccess && !b.hsaco_values.empty()) {
+            e = hipModuleLoadData(&j.vmod, b.hsaco_values.data());
+            if (e == hipSuccess) e = hipModuleGetFunction(&j.vfn, j.vmod, "mh_jit");
+        }
+        mods.push_back(j);
+        if (e != hipSuccess) {
+            unload();
+            return set_err(MH_E_DEVICE, std::string("JIT module load: ") + hipGetErrorString(e));
+        }
+        maxv = std::max(maxv, b.max_vgpr);
+    }
+    // the interpreter's buckets without the jitted tapes
+    std::vector<uint32_t> rest;
+    uint32_t boff[mh::kNumVariants + 1];
+    for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+        boff[v] = (uint32_t)rest.size();
+        for (uint32_t i = ts->bucket_off[v]; i < ts->bucket_off[v + 1]; ++i)
+            if (!stats.jitted[ts->ids[i]]) rest.push_back(ts->ids[i]);
+    }
+    boff[mh::kNumVariants] = (uint32_t)rest.size();
+    uint32_t* d_rest = nullptr;
+    hipError_t e = hipMalloc(&d_rest, std::max<size_t>(1, rest.size()) * sizeof(uint32_t));
+    if (e == hipSuccess && !rest.empty())
+        e = hipMemcpy(d_rest, rest.data(), rest.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (d_rest) (void)hipFree(d_rest);
+        unload();
+        return set_err(MH_E_DEVICE, std::string("JIT bucket upload: ") + hipGetErrorString(e));
+    }
+    ts->jit = std::move(mods);
+    ts->jitted = stats.jitted;
+    ts->ids_rest = std::move(rest);
+    std::copy(boff, boff + mh::kNumVariants + 1, ts->bucket_off_rest);
+    ts->d_ids_rest = d_rest;
+    ts->has_jit = true;
+    mh_jit_info& ji = ts->jinfo;
+    ji = mh_jit_info{};
+    for (uint8_t x : stats.jitted) ji.n_jitted += x;
+    for (const auto& j : ts->jit) ji.n_groups += j.n_groups;
+    ji.n_modules = (uint32_t)ts->jit.size();
+    ji.max_vgpr = maxv;
+    ji.code_bytes = stats.code_bytes;
+    ji.valu_static = stats.valu_static;
+    ji.valu_wide_static = stats.valu_wide_static;
+    ji.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return MH_OK;
+}
+
+int32_t mh_tapes_jit_info(const mh_tapeset* ts, mh_jit_info* out) {
+    if (!ts || !out) return set_err(MH_E_INVALID, "null argument");
+    *out = ts->jinfo;
+    return MH_OK;
+}
+
+int32_t mh_tapes_jitted(const mh_tapeset* ts, uint8_t* out, uint32_t n_tapes) {
+    if (!ts || (!out && n_tapes)) return set_err(MH_E_INVALID, "null argument");
+    if (n_tapes > ts->n_tapes) return set_err(MH_E_INVALID, "n_tapes exceeds the tape set");
+    for (uint32_t t = 0; t < n_tapes; ++t) out[t] = ts->has_jit ? ts->jitted[t] : 0;
+    return MH_OK;
+}
+
+int32_t mh_jit_eval_all(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as,
+                        uint64_t row_first, uint64_t row_count, uint32_t* out) {
+    if (int32_t r = check_run_args(ctx, ts, 0, ts ? ts->n_tapes : 0, as, row_first, row_count,
+                                   MH_MODE_COUNT_ALL))
+        return r;
+    if (!ts->has_jit) return set_err(MH_E_INVALID, "no native code (mh_tapes_jit first)");
+    for (const auto& j : ts->jit)
+        if (j.n_groups && !j.vfn) return set_err(MH_E_INVALID, "built without MH_JIT_VALUES");
+    if (!out && row_count) return set_err(MH_E_INVALID, "null out");
+    if (row_count == 0) return MH_OK;
+    if (int32_t r = use_device(ctx)) return r;
+    const size_t n = (size_t)ts->n_tapes * 8 * row_count;
+    uint32_t* d = nullptr;
+    MH_HIP(hipMalloc(&d, n * sizeof(uint32_t)));
+    hipError_t e = hipMemcpy(d, out, n * sizeof(uint32_t), hipMemcpyHostToDevice);
+    int32_t r = MH_OK;
+    if (e == hipSuccess)
+        r = launch_jit(ctx, ts, as, row_first, row_count, 0, MH_MODE_COUNT_ALL, nullptr, nullptr, d);
+    if (e == hipSuccess && r == MH_OK) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess && r == MH_OK) e = hipMemcpy(out, d, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (r != MH_OK) return r;
+    if (e != hipSuccess) return set_err(MH_E_DEVICE, std::string("mh_jit_eval_all: ") + hipGetErrorString(e));
     return MH_OK;
 }
 

@@ -1,0 +1,1665 @@
+// Native-code emitter of the sieve JIT (see jit.h for the design).
+//
+// Per tape (SSA from compile.cpp lower_tape_ssa, constants folded):
+//   1. last use of every virtual register, and the limbs each value must provide (demanded
+//      limbs, a backward pass: a consumer that reads limb k of its result asks its operands for
+//      the limbs limb k depends on -- carries reach up, shifts move, masks cut);
+//   2. forward emission: a value is 8 limbs, each a constant (no code) or one VGPR; every op
+//      computes only its demanded limbs, with limb-level constant folding and renaming
+//      (x + (c << 128) copies nothing below limb 4, x & 0xff..ff is x, a shift by 64 is a rename);
+//      Bool values are lane masks in SGPR pairs; registers are reference counted and freed at
+//      the last use;
+//   3. the root's mask goes to s[S_RES:S_RES+1] (values mode also reports the root's limbs).
+// Encoding rules of gfx950 honoured here: a VOP2/VOPC (e32) src1 must be a VGPR; a VOP2 that
+// reads VCC implicitly (addc/subb/cndmask e32) takes no literal or SGPR in src0; VOP3 takes no
+// literal and at most one SGPR (a carry-in or mask pair counts).  Constants that break a rule are
+// first moved into a VGPR (v_mov, a 2-cycle instruction) or staged in an SGPR (s_mov).
+#include "jit.h"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <climits>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace mh {
+namespace jit {
+
+namespace {
+
+struct Fail {
+    std::string why;
+};
+
+[[noreturn]] void fail(const std::string& w) { throw Fail{w}; }
+
+enum LK : uint8_t { L_UNDEF, L_CONST, L_VGPR };
+struct Limb {
+    uint8_t k = L_UNDEF;
+    uint32_t v = 0;
+    static Limb C(uint32_t x) { Limb l; l.k = L_CONST; l.v = x; return l; }
+    static Limb R(uint32_t r) { Limb l; l.k = L_VGPR; l.v = r; return l; }
+    bool is_c() const { return k == L_CONST; }
+    bool is_r() const { return k == L_VGPR; }
+    bool is_c(uint32_t x) const { return k == L_CONST && v == x; }
+};
+
+struct Val {
+    bool is_bool = false;
+    int bconst = -1;  // Bool: 0/1 when known, -1 = lane mask in SGPR pair `pair`
+    int pair = -1;
+    Limb l[8];
+    bool defined = false;
+};
+
+int top_bit(uint32_t m) { return m ? 31 - __builtin_clz(m) : -1; }
+uint32_t prefix_mask(uint32_t m) { int t = top_bit(m); return t < 0 ? 0u : ((2u << t) - 1u); }
+
+class Emitter {
+public:
+    Emitter(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
+            const Options& opt)
+        : st_(st), pool_(pool), n_vars_(n_vars), opt_(opt) {}
+
+    TapeCode run();
+
+private:
+    const SsaTape& st_;
+    const std::vector<uint32_t>& pool_;
+    uint32_t n_vars_;
+    Options opt_;
+    std::vector<MI> code_;
+    std::vector<Val> vals_;
+    std::vector<int> last_;
+    std::vector<uint8_t> dem_;
+    int vref_[512] = {};
+    uint32_t vbase_ = 0, vmax_ = 0, vhigh_ = 0;
+    int pref_[N_BOOL_PAIRS] = {};
+    uint32_t kstage_ = 0;
+    uint32_t n_valu_ = 0, n_wide_ = 0, n_salu_ = 0;
+    bool calls_div_ = false;
+
+    // ---- emission
+    void emit(uint16_t op, std::initializer_list<Opnd> ops, bool e64 = false) {
+        MI m;
+        m.op = op;
+        m.e64 = e64 ? 1 : 0;
+        int i = 0;
+        for (const Opnd& o : ops) m.o[i++] = o;
+        code_.push_back(m);
+        if (op <= M_V_CMP_LE_F64) {
+            ++n_valu_;
+            const bool wide = e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
+                              op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO ||
+                              op == M_V_OR3 || op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 ||
+                              (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) || op >= M_V_CVT_F64_U32;
+            if (wide) ++n_wide_;
+        } else if (op <= M_S_CMP_LT_U32) {
+            ++n_salu_;
+        }
+    }
+
+    // ---- VGPRs (reference counted; columns and fixed registers are never freed)
+    uint32_t valloc() {
+        for (uint32_t r = vbase_; r < vmax_; ++r)
+            if (vref_[r] == 0) {
+                vref_[r] = 1;
+                vhigh_ = std::max(vhigh_, r + 1);
+                return r;
+            }
+        fail("VGPR pressure");
+    }
+    uint32_t valloc_pair() {
+        for (uint32_t r = (vbase_ + 1) & ~1u; r + 1 < vmax_; r += 2)
+            if (vref_[r] == 0 && vref_[r + 1] == 0) {
+                vref_[r] = vref_[r + 1] = 1;
+                vhigh_ = std::max(vhigh_, r + 2);
+                return r;
+            }
+        fail("VGPR pressure (pair)");
+    }
+    void vretain(uint32_t r) { if (r >= vbase_) ++vref_[r]; }
+    void vrelease(uint32_t r) {
+        if (r < vbase_) return;
+        if (vref_[r] <= 0) fail("internal: VGPR refcount");
+        --vref_[r];
+    }
+
+    // ---- Bool pairs
+    int palloc() {
+        for (int i = 0; i < (int)N_BOOL_PAIRS; ++i)
+            if (pref_[i] == 0) {
+                pref_[i] = 1;
+                return i;
+            }
+        fail("SGPR pressure (Bool masks)");
+    }
+    static Opnd P(int i) { return S(S_BOOL0 + 2 * (uint32_t)i, 2); }
+
+    // ---- values
+    void retain(const Val& v) {
+        if (v.is_bool) {
+            if (v.bconst < 0) ++pref_[v.pair];
+            return;
+        }
+        for (const Limb& l : v.l)
+            if (l.is_r()) vretain(l.v);
+    }
+    void release(const Val& v) {
+        if (v.is_bool) {
+            if (v.bconst < 0) {
+                if (pref_[v.pair] <= 0) fail("internal: pair refcount");
+                --pref_[v.pair];
+            }
+            return;
+        }
+        for (const Limb& l : v.l)
+            if (l.is_r()) vrelease(l.v);
+    }
+    const Val& val(int r) const {
+        if (r < 0 || r >= (int)vals_.size() || !vals_[r].defined) fail("internal: undefined vreg");
+        return vals_[r];
+    }
+    Val const_val(int cidx) const {
+        Val v;
+        v.defined = true;
+        for (int k = 0; k < 8; ++k) v.l[k] = Limb::C(pool_[8ull * (uint32_t)cidx + k]);
+        return v;
+    }
+    static Val bool_const(bool b) {
+        Val v;
+        v.defined = true;
+        v.is_bool = true;
+        v.bconst = b ? 1 : 0;
+        return v;
+    }
+    Val bool_mask(int pair) {
+        Val v;
+        v.defined = true;
+        v.is_bool = true;
+        v.pair = pair;
+        return v;
+    }
+    // a Bool as a mask pair (constants materialised in a fresh pair; caller releases)
+    int mask_of(const Val& b, std::vector<int>& tmp_pairs) {
+        if (b.bconst < 0) return b.pair;
+        const int p = palloc();
+        tmp_pairs.push_back(p);
+        emit(M_S_MOV_B64, {P(p), IMM(b.bconst ? 0xFFFFFFFFu : 0u)});
+        return p;
+    }
+
+    static Opnd src(const Limb& l) {
+        if (l.k == L_UNDEF) fail("internal: read of an undemanded limb");
+        return l.is_c() ? IMM(l.v) : V(l.v);
+    }
+    // a VGPR holding limb l (constants moved into a temporary, released by the caller)
+    uint32_t vgpr_of(const Limb& l, std::vector<uint32_t>& tmp) {
+        if (l.k == L_UNDEF) fail("internal: read of an undemanded limb");
+        if (l.is_r()) return l.v;
+        const uint32_t t = valloc();
+        tmp.push_back(t);
+        emit(M_V_MOV, {V(t), IMM(l.v)});
+        return t;
+    }
+    // VGPR or inline constant
+    Opnd vi_of(const Limb& l, std::vector<uint32_t>& tmp) {
+        if (l.is_c() && is_inline(l.v)) return IMM(l.v);
+        return V(vgpr_of(l, tmp));
+    }
+    // SGPR-staged constant (one per VOP3 at most)
+    Opnd staged(uint32_t x) {
+        if (is_inline(x)) return IMM(x);
+        const uint32_t s = S_KSTAGE + (kstage_++ % N_KSTAGE);
+        emit(M_S_MOV_B32, {S(s), IMM(x)});
+        return S(s);
+    }
+    void free_tmp(std::vector<uint32_t>& tmp) {
+        for (uint32_t r : tmp) vrelease(r);
+        tmp.clear();
+    }
+    void free_tmp_pairs(std::vector<int>& tp) {
+        for (int p : tp) --pref_[p];
+        tp.clear();
+    }
+
+    // ---- building blocks
+    int chain(bool sub, const Limb* a, const Limb* b, int top, Limb* res, uint32_t junk,
+              std::vector<uint32_t>& tmp);
+    void op_addsub(int d, const Val& A, const Val& B, bool sub);
+    void op_logic(int d, const Val& A, const Val& B, int kind);
+    Val op_eq(const Val& A, const Val& B);
+    Val op_ult(const Val& A, const Val& B, bool signed_, bool negate);
+    void op_ite(int d, const Val& C, const Val& T, const Val& E);
+    Val op_bite(const Val& C, const Val& T, const Val& E);
+    Val op_bool2(uint8_t op, const Val& A, const Val& B);
+    void op_shr(int d, const Val& A, uint32_t s);
+    void op_shl(int d, const Val& A, uint32_t s);
+    void op_vshift(int d, const Val& A, const Val& B, uint8_t op);
+    void op_mul(int d, const Val& A, const Val& B);
+    void op_div(int d, const Val& A, const Val& B, uint32_t kind);
+    void demand();
+    Val& out(int d) {
+        Val& v = vals_[d];
+        v = Val();
+        v.defined = true;
+        return v;
+    }
+};
+
+// Carry / borrow chain over limbs 0..top: res[k] = a[k] +- b[k] +- carry (res == nullptr: the
+// limbs go to `junk`, only the final carry matters).  Returns the final carry state: 0 / 1 when
+// known at compile time, 2 when it is in VCC.
+int Emitter::chain(bool sub, const Limb* a, const Limb* b, int top, Limb* res, uint32_t junk,
+                   std::vector<uint32_t>& tmp) {
+    int cs = 0;
+    for (int k = 0; k <= top; ++k) {
+        const Limb x = a[k], y = b[k];
+        if (x.k == L_UNDEF || y.k == L_UNDEF) fail("internal: chain over an undemanded limb");
+        if (cs != 2 && x.is_c() && y.is_c()) {
+            const uint64_t xv = x.v, yv = y.v;
+            if (sub) {
+                if (res) res[k] = Limb::C((uint32_t)(xv - yv - (uint64_t)cs));
+                cs = xv < yv + (uint64_t)cs ? 1 : 0;
+            } else {
+                const uint64_t r = xv + yv + (uint64_t)cs;
+                if (res) res[k] = Limb::C((uint32_t)r);
+                cs = (int)(r >> 32);
+            }
+            continue;
+        }
+        if (cs == 0 && y.is_c(0)) {  // x +- 0, no carry: x
+            if (res) { res[k] = x; if (x.is_r()) vretain(x.v); }
+            continue;
+        }
+        if (cs == 0 && !sub && x.is_c(0)) {
+            if (res) { res[k] = y; if (y.is_r()) vretain(y.v); }
+            continue;
+        }
+        const uint32_t dst = res ? valloc() : junk;
+        if (cs == 1) {
+            emit(M_S_MOV_B64, {VCC(), IMM(0xFFFFFFFFu)});
+            cs = 2;
+        }
+        if (cs == 0) {  // first instruction of the chain: carry-out only
+            if (!sub) {
+                if (y.is_r()) emit(M_V_ADD_CO, {V(dst), VCC(), src(x), V(y.v)});
+                else if (x.is_r()) emit(M_V_ADD_CO, {V(dst), VCC(), src(y), V(x.v)});
+                else emit(M_V_ADD_CO, {V(dst), VCC(), src(x), V(vgpr_of(y, tmp))});
+            } else {
+                if (y.is_r()) emit(M_V_SUB_CO, {V(dst), VCC(), src(x), V(y.v)});        // x - y
+                else if (x.is_r()) emit(M_V_SUBREV_CO, {V(dst), VCC(), src(y), V(x.v)});  // x - y
+                else emit(M_V_SUB_CO, {V(dst), VCC(), src(x), V(vgpr_of(y, tmp))});
+            }
+        } else {  // carry-in in VCC
+            if (!sub) {
+                Limb p = x, q = y;
+                if (!q.is_r() && p.is_r()) std::swap(p, q);
+                if (!q.is_r() && !p.is_r() && is_inline(p.v) && is_inline(q.v)) {
+                    emit(M_V_ADDC_CO, {V(dst), VCC(), IMM(p.v), IMM(q.v), VCC()}, true);
+                } else {
+                    const uint32_t qr = vgpr_of(q, tmp);
+                    emit(M_V_ADDC_CO, {V(dst), VCC(), vi_of(p, tmp), V(qr), VCC()});
+                }
+            } else {
+                if (y.is_r()) {
+                    emit(M_V_SUBB_CO, {V(dst), VCC(), vi_of(x, tmp), V(y.v), VCC()});
+                } else if (x.is_r()) {
+                    emit(M_V_SUBBREV_CO, {V(dst), VCC(), vi_of(y, tmp), V(x.v), VCC()});
+                } else if (is_inline(x.v) && is_inline(y.v)) {
+                    emit(M_V_SUBB_CO, {V(dst), VCC(), IMM(x.v), IMM(y.v), VCC()}, true);
+                } else {
+                    emit(M_V_SUBB_CO, {V(dst), VCC(), vi_of(x, tmp), V(vgpr_of(y, tmp)), VCC()});
+                }
+            }
+        }
+        cs = 2;
+        if (res) res[k] = Limb::R(dst);
+    }
+    return cs;
+}
+
+void Emitter::op_addsub(int d, const Val& A, const Val& B, bool sub) {
+    const int top = top_bit(dem_[d]);
+    Val& R = out(d);
+    if (top < 0) return;
+    std::vector<uint32_t> tmp;
+    chain(sub, A.l, B.l, top, R.l, 0, tmp);
+    free_tmp(tmp);
+}
+
+// kind 0 and, 1 or, 2 xor
+void Emitter::op_logic(int d, const Val& A, const Val& B, int kind) {
+    const uint32_t dm = dem_[d];
+    Val& R = out(d);
+    for (int k = 0; k < 8; ++k) {
+        if (!((dm >> k) & 1)) continue;
+        Limb x = A.l[k], y = B.l[k];
+        if (x.is_c() && !y.is_c()) std::swap(x, y);  // constant (if any) in y
+        if (y.is_c() && ((kind == 0 && y.v == 0) || (kind == 1 && y.v == ~0u))) {
+            R.l[k] = Limb::C(y.v);  // the constant decides (the other limb was not demanded)
+            continue;
+        }
+        if (x.k == L_UNDEF || y.k == L_UNDEF) fail("internal: logic over an undemanded limb");
+        auto alias = [&](const Limb& l) { R.l[k] = l; if (l.is_r()) vretain(l.v); };
+        if (x.is_c() && y.is_c()) {
+            R.l[k] = Limb::C(kind == 0 ? (x.v & y.v) : kind == 1 ? (x.v | y.v) : (x.v ^ y.v));
+            continue;
+        }
+        if (y.is_c()) {
+            const uint32_t c = y.v;
+            if (kind == 0 && c == 0) { R.l[k] = Limb::C(0); continue; }
+            if (kind == 0 && c == ~0u) { alias(x); continue; }
+            if (kind == 1 && c == 0) { alias(x); continue; }
+            if (kind == 1 && c == ~0u) { R.l[k] = Limb::C(~0u); continue; }
+            if (kind == 2 && c == 0) { alias(x); continue; }
+            const uint32_t dst = valloc();
+            if (kind == 2 && c == ~0u) emit(M_V_NOT, {V(dst), V(x.v)});
+            else emit(kind == 0 ? M_V_AND : kind == 1 ? M_V_OR : M_V_XOR, {V(dst), IMM(c), V(x.v)});
+            R.l[k] = Limb::R(dst);
+            continue;
+        }
+        if (x.v == y.v) {  // same register
+            if (kind == 2) R.l[k] = Limb::C(0);
+            else alias(x);
+            continue;
+        }
+        const uint32_t dst = valloc();
+        emit(kind == 0 ? M_V_AND : kind == 1 ? M_V_OR : M_V_XOR, {V(dst), V(x.v), V(y.v)});
+        R.l[k] = Limb::R(dst);
+    }
+}
+
+Val Emitter::op_eq(const Val& A, const Val& B) {
+    int p = -1;
+    for (int k = 0; k < 8; ++k) {
+        Limb x = A.l[k], y = B.l[k];
+        if (x.is_c() && y.is_c()) {
+            if (x.v != y.v) {
+                if (p >= 0) --pref_[p];
+                return bool_const(false);
+            }
+            continue;
+        }
+        if (x.is_r() && y.is_r() && x.v == y.v) continue;
+        if (!y.is_r()) std::swap(x, y);
+        emit(M_V_CMP_EQ, {VCC(), src(x), V(y.v)});
+        if (p < 0) {
+            p = palloc();
+            emit(M_S_MOV_B64, {P(p), VCC()});
+        } else {
+            emit(M_S_AND_B64, {P(p), P(p), VCC()});
+        }
+    }
+    if (p < 0) return bool_const(true);
+    return bool_mask(p);
+}
+
+// A < B (unsigned, or signed 256-bit), optionally negated (>=)
+Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
+    std::vector<uint32_t> tmp;
+    Limb a[8], b[8];
+    for (int k = 0; k < 8; ++k) { a[k] = A.l[k]; b[k] = B.l[k]; }
+    if (signed_) {  // bias the sign bit: signed order = unsigned order of x ^ 2^255
+        for (Limb* l : {&a[7], &b[7]}) {
+            if (l->is_c()) {
+                l->v ^= 0x80000000u;
+            } else {
+                const uint32_t t = valloc();
+                tmp.push_back(t);
+                emit(M_V_XOR, {V(t), IMM(0x80000000u), V(l->v)});
+                *l = Limb::R(t);
+            }
+        }
+    }
+    int top = 7;
+    while (top > 0 && a[top].is_c(0) && b[top].is_c(0)) --top;
+    const uint32_t junk = valloc();
+    tmp.push_back(junk);
+    const int cs = chain(true, a, b, top, nullptr, junk, tmp);
+    free_tmp(tmp);
+    if (cs != 2) return bool_const((cs == 1) != negate);
+    const int p = palloc();
+    emit(negate ? M_S_NOT_B64 : M_S_MOV_B64, {P(p), VCC()});
+    return bool_mask(p);
+}
+
+void Emitter::op_ite(int d, const Val& C, const Val& T, const Val& E) {
+    if (C.bconst >= 0) {
+        Val v = C.bconst ? T : E;
+        retain(v);
+        vals_[d] = v;
+        return;
+    }
+    const uint32_t dm = dem_[d];
+    Val& R = out(d);
+    std::vector<uint32_t> tmp;
+    for (int k = 0; k < 8; ++k) {
+        if (!((dm >> k) & 1)) continue;
+        const Limb t = T.l[k], e = E.l[k];
+        if (t.k == L_UNDEF || e.k == L_UNDEF) fail("internal: ite over an undemanded limb");
+        if (t.k == e.k && t.v == e.v) {
+            R.l[k] = t;
+            if (t.is_r()) vretain(t.v);
+            continue;
+        }
+        const uint32_t dst = valloc();
+        emit(M_V_CNDMASK, {V(dst), vi_of(e, tmp), vi_of(t, tmp), P(C.pair)}, true);
+        R.l[k] = Limb::R(dst);
+    }
+    free_tmp(tmp);
+}
+
+Val Emitter::op_bite(const Val& C, const Val& T, const Val& E) {
+    if (C.bconst >= 0) {
+        Val v = C.bconst ? T : E;
+        retain(v);
+        return v;
+    }
+    if (T.bconst >= 0 && E.bconst >= 0) {
+        if (T.bconst == E.bconst) return bool_const(T.bconst != 0);
+        const int p = palloc();
+        emit(T.bconst ? M_S_MOV_B64 : M_S_NOT_B64, {P(p), P(C.pair)});
+        return bool_mask(p);
+    }
+    std::vector<int> tp;
+    const int t = mask_of(T, tp), e = mask_of(E, tp);
+    const int p = palloc();
+    const int q = palloc();
+    emit(M_S_AND_B64, {P(p), P(C.pair), P(t)});
+    emit(M_S_ANDN2_B64, {P(q), P(e), P(C.pair)});
+    emit(M_S_OR_B64, {P(p), P(p), P(q)});
+    --pref_[q];
+    free_tmp_pairs(tp);
+    return bool_mask(p);
+}
+
+Val Emitter::op_bool2(uint8_t op, const Val& A, const Val& B) {
+    const Val* a = &A;
+    const Val* b = &B;
+    if (a->bconst >= 0 && b->bconst >= 0) {
+        const bool x = a->bconst, y = b->bconst;
+        switch (op) {
+            case D_BAND: return bool_const(x && y);
+            case D_BOR: return bool_const(x || y);
+            case D_BXOR: return bool_const(x != y);
+            default: return bool_const(x == y);  // D_BEQ
+        }
+    }
+    if (a->bconst >= 0) std::swap(a, b);  // constant (if any) in b
+    if (b->bconst >= 0) {
+        const bool y = b->bconst;
+        const bool same = (op == D_BAND && y) || (op == D_BOR && !y) || (op == D_BXOR && !y) ||
+                          (op == D_BEQ && y);
+        if (same) { retain(*a); return *a; }
+        if (op == D_BAND) return bool_const(false);
+        if (op == D_BOR) return bool_const(true);
+        const int p = palloc();  // xor 1 / eq 0: not
+        emit(M_S_NOT_B64, {P(p), P(a->pair)});
+        return bool_mask(p);
+    }
+    const int p = palloc();
+    const uint16_t m = op == D_BAND ? M_S_AND_B64 : op == D_BOR ? M_S_OR_B64 :
+                       op == D_BXOR ? M_S_XOR_B64 : M_S_XNOR_B64;
+    emit(m, {P(p), P(a->pair), P(b->pair)});
+    return bool_mask(p);
+}
+
+// logical right shift by a constant s (0 < s < 256)
+void Emitter::op_shr(int d, const Val& A, uint32_t s) {
+    const uint32_t q = s >> 5, bsh = s & 31, dm = dem_[d];
+    Val& R = out(d);
+    std::vector<uint32_t> tmp;
+    for (int k = 0; k < 8; ++k) {
+        if (!((dm >> k) & 1)) continue;
+        const int i = k + (int)q;
+        const Limb lo = i < 8 ? A.l[i] : Limb::C(0);
+        const Limb hi = i + 1 < 8 ? A.l[i + 1] : Limb::C(0);
+        if (bsh == 0) {
+            R.l[k] = lo;
+            if (lo.is_r()) vretain(lo.v);
+            continue;
+        }
+        if (lo.k == L_UNDEF || hi.k == L_UNDEF) fail("internal: shift of an undemanded limb");
+        if (lo.is_c() && hi.is_c()) {
+            R.l[k] = Limb::C((uint32_t)((((uint64_t)hi.v << 32) | lo.v) >> bsh));
+            continue;
+        }
+        const uint32_t dst = valloc();
+        if (hi.is_c(0)) emit(M_V_LSHRREV, {V(dst), IMM(bsh), V(lo.v)});
+        else if (lo.is_c(0)) emit(M_V_LSHLREV, {V(dst), IMM(32 - bsh), V(hi.v)});
+        else emit(M_V_ALIGNBIT, {V(dst), vi_of(hi, tmp), vi_of(lo, tmp), IMM(bsh)});
+        R.l[k] = Limb::R(dst);
+    }
+    free_tmp(tmp);
+}
+
+// left shift by a constant s (0 < s < 256), mod 2^256
+void Emitter::op_shl(int d, const Val& A, uint32_t s) {
+    const uint32_t q = s >> 5, bsh = s & 31, dm = dem_[d];
+    Val& R = out(d);
+    std::vector<uint32_t> tmp;
+    for (int k = 0; k < 8; ++k) {
+        if (!((dm >> k) & 1)) continue;
+        const int i = k - (int)q;
+        const Limb hi = i >= 0 ? A.l[i] : Limb::C(0);       // supplies the high bits
+        const Limb lo = i - 1 >= 0 ? A.l[i - 1] : Limb::C(0);
+        if (bsh == 0) {
+            R.l[k] = hi;
+            if (hi.is_r()) vretain(hi.v);
+            continue;
+        }
+        if (lo.k == L_UNDEF || hi.k == L_UNDEF) fail("internal: shift of an undemanded limb");
+        if (lo.is_c() && hi.is_c()) {
+            R.l[k] = Limb::C((uint32_t)((((uint64_t)hi.v << 32) | lo.v) >> (32 - bsh)));
+            continue;
+        }
+        const uint32_t dst = valloc();
+        if (lo.is_c(0)) emit(M_V_LSHLREV, {V(dst), IMM(bsh), V(hi.v)});
+        else if (hi.is_c(0)) emit(M_V_LSHRREV, {V(dst), IMM(32 - bsh), V(lo.v)});
+        else emit(M_V_ALIGNBIT, {V(dst), vi_of(hi, tmp), vi_of(lo, tmp), IMM(32 - bsh)});
+        R.l[k] = Limb::R(dst);
+    }
+    free_tmp(tmp);
+}
+
+// per-lane shift amount B (>= 256 saturates: 0 / sign fill): limb-select network + alignbit
+void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
+    const bool right = op != D_SHL_V, arith = op == D_ASHR_V;
+    bool bconst = true;
+    for (int k = 0; k < 8; ++k) bconst &= B.l[k].is_c();
+    if (bconst) {  // uniform amount after folding: the constant-shift forms
+        uint32_t hi = 0;
+        for (int k = 1; k < 8; ++k) hi |= B.l[k].v;
+        const uint32_t s = hi || B.l[0].v > 255u ? 256u : B.l[0].v;
+        if (s == 0) { retain(A); vals_[d] = A; return; }
+        if (!arith && s >= 256) {
+            Val& R = out(d);
+            for (int k = 0; k < 8; ++k) R.l[k] = Limb::C(0);
+            return;
+        }
+        if (!arith) {
+            if (right) op_shr(d, A, s); else op_shl(d, A, s);
+            return;
+        }
+    }
+    std::vector<uint32_t> tmp;
+    std::vector<int> tp;
+    // amount: q = y0 >> 5 (limbs, bits 7..5), r = y0 & 31; big = y >= 256
+    const uint32_t y0 = vgpr_of(B.l[0], tmp);
+    const int big = palloc();
+    tp.push_back(big);
+    emit(M_V_CMP_LT, {VCC(), IMM(0xFFu), V(y0)});  // 255 < y0
+    emit(M_S_MOV_B64, {P(big), VCC()});
+    uint32_t orr = ~0u;
+    for (int k = 1; k < 8; ++k) {
+        const Limb l = B.l[k];
+        if (l.is_c()) {
+            if (l.v) { emit(M_S_MOV_B64, {P(big), IMM(0xFFFFFFFFu)}); }
+            continue;
+        }
+        if (orr == ~0u) {
+            orr = valloc();
+            tmp.push_back(orr);
+            emit(M_V_MOV, {V(orr), V(l.v)});
+        } else {
+            emit(M_V_OR, {V(orr), V(l.v), V(orr)});
+        }
+    }
+    if (orr != ~0u) {
+        emit(M_V_CMP_NE, {VCC(), IMM(0), V(orr)});
+        emit(M_S_OR_B64, {P(big), P(big), VCC()});
+    }
+    const uint32_t qv = valloc(), rv = valloc(), tv = valloc();
+    tmp.push_back(qv); tmp.push_back(rv); tmp.push_back(tv);
+    emit(M_V_LSHRREV, {V(qv), IMM(5), V(y0)});
+    emit(M_V_AND, {V(rv), IMM(31), V(y0)});
+    uint32_t t[8];
+    for (int k = 0; k < 8; ++k) {
+        t[k] = valloc();
+        tmp.push_back(t[k]);
+        emit(M_V_MOV, {V(t[k]), src(A.l[k])});
+    }
+    Opnd fill = IMM(0);
+    if (arith) {
+        const uint32_t f = valloc();
+        tmp.push_back(f);
+        emit(M_V_ASHRREV, {V(f), IMM(31), V(t[7])});
+        fill = V(f);
+    }
+    for (uint32_t st : {4u, 2u, 1u}) {
+        emit(M_V_AND, {V(tv), IMM(st), V(qv)});
+        emit(M_V_CMP_NE, {VCC(), IMM(0), V(tv)});
+        if (right) {
+            for (int k = 0; k < 8; ++k) {
+                const Opnd s2 = k + (int)st < 8 ? V(t[k + st]) : fill;
+                emit(M_V_CNDMASK, {V(t[k]), V(t[k]), s2, VCC()}, s2.k != O_V);
+            }
+        } else {
+            for (int k = 7; k >= 0; --k) {
+                const Opnd s2 = k - (int)st >= 0 ? V(t[k - st]) : IMM(0);
+                emit(M_V_CNDMASK, {V(t[k]), V(t[k]), s2, VCC()}, s2.k != O_V);
+            }
+        }
+    }
+    Val& R = out(d);
+    uint32_t o[8];
+    for (int k = 0; k < 8; ++k) o[k] = valloc();
+    if (right) {
+        for (int k = 0; k < 8; ++k)
+            emit(M_V_ALIGNBIT, {V(o[k]), k < 7 ? V(t[k + 1]) : fill, V(t[k]), V(rv)});
+    } else {
+        emit(M_V_SUB_U32, {V(tv), IMM(32), V(rv)});
+        emit(M_V_CMP_EQ, {VCC(), IMM(0), V(rv)});
+        for (int k = 0; k < 8; ++k) {
+            emit(M_V_ALIGNBIT, {V(o[k]), V(t[k]), k > 0 ? V(t[k - 1]) : IMM(0), V(tv)});
+            emit(M_V_CNDMASK, {V(o[k]), V(o[k]), V(t[k]), VCC()});
+        }
+    }
+    for (int k = 0; k < 8; ++k) {
+        emit(M_V_CNDMASK, {V(o[k]), V(o[k]), right ? fill : IMM(0), P(big)}, true);
+        R.l[k] = Limb::R(o[k]);
+    }
+    free_tmp(tmp);
+    free_tmp_pairs(tp);
+}
+
+// x * y mod 2^256, product scanning over the demanded columns: column k accumulates its terms
+// with v_mad_u64_u32 into a 64-bit pair; carries out of the pair (only where the column can
+// exceed 2^64) are counted into the next column's high word.
+void Emitter::op_mul(int d, const Val& A, const Val& B) {
+    const int top = top_bit(dem_[d]);
+    Val& R = out(d);
+    if (top < 0) return;
+    std::vector<uint32_t> tmp;
+    typedef unsigned __int128 u128;
+    const u128 M32 = 0xFFFFFFFFull;
+    auto maxv = [&](const Limb& l) -> u128 { return l.is_c() ? (u128)l.v : M32; };
+    int init = -1;          // VGPR pair (lo = carry-in, hi = carried overflows) of this column
+    u128 init_max = 0;
+    for (int k = 0; k <= top; ++k) {
+        std::vector<std::pair<int, int>> terms;
+        u128 colmax = init_max;
+        for (int i = 0; i <= k; ++i) {
+            const Limb x = A.l[i], y = B.l[k - i];
+            if (x.k == L_UNDEF || y.k == L_UNDEF) fail("internal: mul over an undemanded limb");
+            if (x.is_c(0) || y.is_c(0)) continue;
+            terms.push_back({i, k - i});
+            colmax += maxv(x) * maxv(y);
+        }
+        if (terms.empty()) {
+            if (init < 0) { R.l[k] = Limb::C(0); continue; }
+            // the column is its carry-in: limb = init.lo, the next carry-in = (init.hi, 0)
+            R.l[k] = Limb::R((uint32_t)init);
+            if (k < top) {
+                const uint32_t np = valloc_pair();
+                emit(M_V_MOV, {V(np), V((uint32_t)init + 1)});
+                emit(M_V_MOV, {V(np + 1), IMM(0)});
+                vrelease((uint32_t)init + 1);
+                init = (int)np;
+                init_max >>= 32;
+            } else {
+                vrelease((uint32_t)init + 1);
+            }
+            continue;
+        }
+        const bool count = k < top && colmax >> 64;
+        const uint32_t acc = valloc_pair();
+        uint32_t np = 0;
+        if (k < top) np = valloc_pair();
+        bool first = true;
+        for (auto [i, j] : terms) {
+            Limb x = A.l[i], y = B.l[j];
+            if (x.is_c() && !y.is_c()) std::swap(x, y);
+            Opnd s0, s1;
+            if (x.is_c() && y.is_c()) {
+                s0 = staged(x.v);
+                s1 = V(vgpr_of(y, tmp));
+            } else if (y.is_c()) {
+                s0 = staged(y.v);
+                s1 = V(x.v);
+            } else {
+                s0 = V(x.v);
+                s1 = V(y.v);
+            }
+            const Opnd s2 = first ? (init >= 0 ? V((uint32_t)init, 2) : IMM(0)) : V(acc, 2);
+            emit(M_V_MAD_U64_U32, {V(acc, 2), count ? VCC() : S(S_DIV_DUMMY, 2), s0, s1, s2});
+            if (count) {
+                if (first) emit(M_V_ADDC_CO, {V(np + 1), VCC(), IMM(0), IMM(0), VCC()}, true);
+                else emit(M_V_ADDC_CO, {V(np + 1), VCC(), IMM(0), V(np + 1), VCC()});
+            }
+            first = false;
+        }
+        if (init >= 0) {
+            vrelease((uint32_t)init);
+            vrelease((uint32_t)init + 1);
+        }
+        R.l[k] = Limb::R(acc);
+        if (k < top) {
+            if (!count) emit(M_V_MOV, {V(np + 1), IMM(0)});
+            emit(M_V_MOV, {V(np), V(acc + 1)});
+            init = (int)np;
+            init_max = colmax >> 32;
+        }
+        vrelease(acc + 1);
+    }
+    free_tmp(tmp);
+}
+
+void Emitter::op_div(int d, const Val& A, const Val& B, uint32_t kind) {
+    calls_div_ = true;
+    for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DR + k), src(A.l[k])});
+    for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DY + k), src(B.l[k])});
+    emit(M_S_MOV_B32, {S(S_DIV_KIND), IMM(kind)});
+    emit(M_CALL_DIV, {IMM((uint32_t)code_.size())});
+    Val& R = out(d);
+    const uint32_t dm = dem_[d];
+    for (int k = 0; k < 8; ++k) {
+        if (!((dm >> k) & 1)) continue;
+        const uint32_t r = valloc();
+        emit(M_V_MOV, {V(r), V(R_DQ + k)});
+        R.l[k] = Limb::R(r);
+    }
+}
+
+void Emitter::demand() {
+    const auto& code = st_.code;
+    const int nv = st_.n_vregs;
+    dem_.assign(nv, 0);
+    if (st_.root >= 0) dem_[st_.root] = 0xFF;
+    auto D = [&](int r, uint32_t m) { if (r >= 0) dem_[r] |= (uint8_t)m; };
+    for (size_t i = code.size(); i-- > 0;) {
+        const SsaInsn& v = code[i];
+        const uint32_t dd = dem_[v.d];
+        const uint8_t op = v.op;
+        switch (op) {
+            case D_NOP: D(v.a, dd); break;
+            case D_ADD_R: case D_SUB_R: case D_RSUB_R: case D_MUL_R:
+                D(v.a, prefix_mask(dd));
+                D(v.b, prefix_mask(dd));
+                break;
+            case D_AND_R: case D_OR_R: case D_XOR_R: {
+                uint32_t ma = dd;
+                if (v.cidx >= 0) {
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t c = pool_[8ull * (uint32_t)v.cidx + k];
+                        if ((op == D_AND_R && c == 0) || (op == D_OR_R && c == ~0u))
+                            ma &= ~(1u << k);
+                    }
+                }
+                D(v.a, ma);
+                D(v.b, dd);
+                break;
+            }
+            case D_ITE: D(v.b, dd); D(v.c, dd); break;
+            case D_SHL_V: case D_LSHR_V: case D_ASHR_V:
+                D(v.a, 0xFF);
+                D(v.b, 0xFF);
+                break;
+            default:
+                if (op >= D_SHR0 && op <= D_SHR7) {
+                    const uint32_t s = 32u * (op - D_SHR0) + (v.aux & 31u);
+                    const uint32_t q = s >> 5, bsh = s & 31;
+                    uint32_t m = 0;
+                    for (int k = 0; k < 8; ++k)
+                        if ((dd >> k) & 1) {
+                            if (k + q < 8) m |= 1u << (k + q);
+                            if (bsh && k + q + 1 < 8) m |= 1u << (k + q + 1);
+                        }
+                    D(v.a, m);
+                } else if (op >= D_SHL0 && op <= D_SHL7) {
+                    const uint32_t p = op - D_SHL0, f = v.aux & 31u;
+                    const uint32_t s = f ? 32u * p + 32u - f : 32u * (p + 1u);
+                    if (s < 256) {
+                        const int q = (int)(s >> 5), bsh = (int)(s & 31);
+                        uint32_t m = 0;
+                        for (int k = 0; k < 8; ++k)
+                            if ((dd >> k) & 1) {
+                                if (k - q >= 0) m |= 1u << (k - q);
+                                if (bsh && k - q - 1 >= 0) m |= 1u << (k - q - 1);
+                            }
+                        D(v.a, m);
+                    }
+                } else if ((op >= D_EQ_R && op <= D_SGE_C) ||
+                           (op >= D_UDIV_R && op <= D_SMOD_C)) {
+                    D(v.a, 0xFF);
+                    D(v.b, 0xFF);
+                } else {  // Bool ops, constants
+                    D(v.a, 0);
+                }
+                break;
+        }
+    }
+}
+
+TapeCode Emitter::run() {
+    TapeCode tc;
+    tc.alg_ops = st_.alg_ops;
+    try {
+        const auto& code = st_.code;
+        const int nv = st_.n_vregs;
+        if (st_.n_pinned != (int)n_vars_ || n_vars_ > 4) fail("assignment columns not pinned");
+        bool has_div = false;
+        for (const SsaInsn& v : code) {
+            if (v.op >= D_FIRST_COMPLEX) fail("complex op (interpreter only)");
+            if (v.op >= D_UDIV_R && v.op <= D_SMOD_C) has_div = true;
+        }
+        vbase_ = has_div ? R_TEMP0 : R_TEMP_NODIV;
+        vmax_ = std::min<uint32_t>(opt_.max_vgpr, 512);
+        if (vmax_ <= vbase_ + 16) fail("VGPR budget too small");
+        vhigh_ = R_COL0 + 8 * n_vars_;
+        vals_.assign(nv, Val());
+        for (int c = 0; c < st_.n_pinned; ++c) {
+            Val& v = vals_[c];
+            v.defined = true;
+            for (int k = 0; k < 8; ++k) v.l[k] = Limb::R(R_COL0 + 8u * (uint32_t)c + k);
+        }
+        last_.assign(nv, -1);
+        for (int i = 0; i < (int)code.size(); ++i)
+            for (int r : {code[i].a, code[i].b, code[i].c})
+                if (r >= 0) last_[r] = i;
+        if (st_.root >= 0) last_[st_.root] = INT_MAX;
+        demand();
+        for (int i = 0; i < (int)code.size(); ++i) {
+            const SsaInsn& v = code[i];
+            const uint8_t op = v.op;
+            auto Y = [&]() -> Val { return v.cidx >= 0 ? const_val(v.cidx) : val(v.b); };
+            switch (op) {
+                case D_NOP: {
+                    const Val& a = val(v.a);
+                    retain(a);
+                    vals_[v.d] = a;
+                    break;
+                }
+                case D_LOADC: vals_[v.d] = const_val(v.cidx); break;
+                case D_TRUE: vals_[v.d] = bool_const(true); break;
+                case D_FALSE: vals_[v.d] = bool_const(false); break;
+                case D_ADD_R: op_addsub(v.d, val(v.a), Y(), false); break;
+                case D_SUB_R: op_addsub(v.d, val(v.a), Y(), true); break;
+                case D_RSUB_R: op_addsub(v.d, Y(), val(v.a), true); break;
+                case D_AND_R: op_logic(v.d, val(v.a), Y(), 0); break;
+                case D_OR_R: op_logic(v.d, val(v.a), Y(), 1); break;
+                case D_XOR_R: op_logic(v.d, val(v.a), Y(), 2); break;
+                case D_EQ_R: vals_[v.d] = op_eq(val(v.a), Y()); break;
+                case D_ULT_R: vals_[v.d] = op_ult(val(v.a), Y(), false, false); break;
+                case D_UGE_R: vals_[v.d] = op_ult(val(v.a), Y(), false, true); break;
+                case D_UGT_R: vals_[v.d] = op_ult(Y(), val(v.a), false, false); break;
+                case D_ULE_R: vals_[v.d] = op_ult(Y(), val(v.a), false, true); break;
+                case D_SLT_R: vals_[v.d] = op_ult(val(v.a), Y(), true, false); break;
+                case D_SGE_R: vals_[v.d] = op_ult(val(v.a), Y(), true, true); break;
+                case D_SGT_R: vals_[v.d] = op_ult(Y(), val(v.a), true, false); break;
+                case D_SLE_R: vals_[v.d] = op_ult(Y(), val(v.a), true, true); break;
+                case D_BAND: case D_BOR: case D_BXOR: case D_BEQ:
+                    vals_[v.d] = op_bool2(op, val(v.a), val(v.b));
+                    break;
+                case D_BNOT: {
+                    const Val& a = val(v.a);
+                    if (a.bconst >= 0) {
+                        vals_[v.d] = bool_const(!a.bconst);
+                    } else {
+                        const int p = palloc();
+                        emit(M_S_NOT_B64, {P(p), P(a.pair)});
+                        vals_[v.d] = bool_mask(p);
+                    }
+                    break;
+                }
+                case D_ITE: op_ite(v.d, val(v.a), val(v.b), val(v.c)); break;
+                case D_BITE: vals_[v.d] = op_bite(val(v.a), val(v.b), val(v.c)); break;
+                case D_MUL_R: op_mul(v.d, val(v.a), Y()); break;
+                case D_SHL_V: case D_LSHR_V: case D_ASHR_V:
+                    op_vshift(v.d, val(v.a), val(v.b), op);
+                    break;
+                case D_UDIV_R: case D_UREM_R: case D_SDIV_R: case D_SREM_R: case D_SMOD_R:
+                    op_div(v.d, val(v.a), Y(), (uint32_t)(op - D_UDIV_R) >> 1);
+                    break;
+                default:
+                    if (op >= D_SHR0 && op <= D_SHR7) {
+                        const uint32_t s = 32u * (op - D_SHR0) + (v.aux & 31u);
+                        if (s == 0) { const Val& a = val(v.a); retain(a); vals_[v.d] = a; }
+                        else op_shr(v.d, val(v.a), s);
+                    } else if (op >= D_SHL0 && op <= D_SHL7) {
+                        const uint32_t p = op - D_SHL0, f = v.aux & 31u;
+                        const uint32_t s = f ? 32u * p + 32u - f : 32u * (p + 1u);
+                        if (s >= 256) {
+                            Val& R = out(v.d);
+                            for (int k = 0; k < 8; ++k) R.l[k] = Limb::C(0);
+                        } else {
+                            op_shl(v.d, val(v.a), s);
+                        }
+                    } else {
+                        fail("op " + std::to_string(op) + " not in the JIT");
+                    }
+                    break;
+            }
+            vals_[v.d].defined = true;
+            // operands whose last use this was
+            int seen[3] = {-1, -1, -1};
+            int ns = 0;
+            for (int r : {v.a, v.b, v.c}) {
+                if (r < 0 || last_[r] != i) continue;
+                bool dup = false;
+                for (int j = 0; j < ns; ++j) dup |= seen[j] == r;
+                if (dup) continue;
+                seen[ns++] = r;
+                release(vals_[r]);
+            }
+        }
+        // root
+        const Val& root = val(st_.root);
+        tc.root_bool = root.is_bool;
+        if (root.is_bool) {
+            if (root.bconst >= 0) emit(M_S_MOV_B64, {S(S_RES, 2), IMM(root.bconst ? ~0u : 0u)});
+            else emit(M_S_MOV_B64, {S(S_RES, 2), P(root.pair)});
+            for (int k = 0; k < 8; ++k) { tc.root_limbs[k] = ~0u; tc.root_const[k] = 0; }
+        } else {
+            // hit = value != 0
+            uint32_t acc = ~0u, cacc = 0;
+            for (int k = 0; k < 8; ++k) {
+                const Limb l = root.l[k];
+                if (l.is_c()) { cacc |= l.v; tc.root_limbs[k] = ~0u; tc.root_const[k] = l.v; continue; }
+                tc.root_limbs[k] = l.v;
+                tc.root_const[k] = 0;
+                if (acc == ~0u) { acc = valloc(); emit(M_V_MOV, {V(acc), V(l.v)}); }
+                else emit(M_V_OR, {V(acc), V(l.v), V(acc)});
+            }
+            if (cacc) emit(M_S_MOV_B64, {S(S_RES, 2), IMM(~0u)});
+            else if (acc == ~0u) emit(M_S_MOV_B64, {S(S_RES, 2), IMM(0)});
+            else {
+                emit(M_V_CMP_NE, {VCC(), IMM(0), V(acc)});
+                emit(M_S_MOV_B64, {S(S_RES, 2), VCC()});
+            }
+        }
+        tc.ok = true;
+    } catch (const Fail& f) {
+        tc.ok = false;
+        tc.why = f.why;
+        code_.clear();
+    }
+    tc.code.swap(code_);
+    tc.max_vgpr = vhigh_;
+    tc.calls_div = calls_div_;
+    tc.n_valu = n_valu_;
+    tc.n_valu_wide = n_wide_;
+    tc.n_salu = n_salu_;
+    return tc;
+}
+
+// ---- printer ---------------------------------------------------------------------------
+struct OpInfo {
+    const char* name;
+};
+const char* op_name(uint16_t op) {
+    switch (op) {
+        case M_V_MOV: return "v_mov_b32";
+        case M_V_ADD_U32: return "v_add_u32";
+        case M_V_SUB_U32: return "v_sub_u32";
+        case M_V_SUBREV_U32: return "v_subrev_u32";
+        case M_V_ADD_CO: return "v_add_co_u32";
+        case M_V_ADDC_CO: return "v_addc_co_u32";
+        case M_V_SUB_CO: return "v_sub_co_u32";
+        case M_V_SUBB_CO: return "v_subb_co_u32";
+        case M_V_SUBREV_CO: return "v_subrev_co_u32";
+        case M_V_SUBBREV_CO: return "v_subbrev_co_u32";
+        case M_V_AND: return "v_and_b32";
+        case M_V_OR: return "v_or_b32";
+        case M_V_XOR: return "v_xor_b32";
+        case M_V_NOT: return "v_not_b32";
+        case M_V_OR3: return "v_or3_b32";
+        case M_V_ALIGNBIT: return "v_alignbit_b32";
+        case M_V_LSHLREV: return "v_lshlrev_b32";
+        case M_V_LSHRREV: return "v_lshrrev_b32";
+        case M_V_ASHRREV: return "v_ashrrev_i32";
+        case M_V_CNDMASK: return "v_cndmask_b32";
+        case M_V_CMP_EQ: return "v_cmp_eq_u32";
+        case M_V_CMP_NE: return "v_cmp_ne_u32";
+        case M_V_CMP_LT: return "v_cmp_lt_u32";
+        case M_V_CMP_LE: return "v_cmp_le_u32";
+        case M_V_CMP_GT: return "v_cmp_gt_u32";
+        case M_V_CMP_GE: return "v_cmp_ge_u32";
+        case M_V_MAD_U64_U32: return "v_mad_u64_u32";
+        case M_V_CVT_F64_U32: return "v_cvt_f64_u32";
+        case M_V_FMA_F64: return "v_fma_f64";
+        case M_V_RCP_F64: return "v_rcp_f64";
+        case M_V_MUL_F64: return "v_mul_f64";
+        case M_V_MIN_F64: return "v_min_f64";
+        case M_V_CVT_U32_F64: return "v_cvt_u32_f64";
+        case M_V_CMP_LE_F64: return "v_cmp_le_f64";
+        case M_S_MOV_B32: return "s_mov_b32";
+        case M_S_MOV_B64: return "s_mov_b64";
+        case M_S_AND_B64: return "s_and_b64";
+        case M_S_OR_B64: return "s_or_b64";
+        case M_S_XOR_B64: return "s_xor_b64";
+        case M_S_XNOR_B64: return "s_xnor_b64";
+        case M_S_ANDN2_B64: return "s_andn2_b64";
+        case M_S_NOT_B64: return "s_not_b64";
+        case M_S_CMP_EQ_U64: return "s_cmp_eq_u64";
+        case M_S_CMP_LG_U64: return "s_cmp_lg_u64";
+        case M_S_CMP_EQ_U32: return "s_cmp_eq_u32";
+        case M_S_CMP_LT_U32: return "s_cmp_lt_u32";
+        case M_S_CBRANCH_SCC0: return "s_cbranch_scc0";
+        case M_S_CBRANCH_SCC1: return "s_cbranch_scc1";
+        case M_S_BRANCH: return "s_branch";
+        case M_S_NOP: return "s_nop";
+        default: return "?";
+    }
+}
+
+std::string opnd_str(const Opnd& o, const std::string& prefix) {
+    char b[64];
+    switch (o.k) {
+        case O_V:
+            if (o.n == 1) snprintf(b, sizeof b, "%sv%u", o.neg ? "-" : "", o.v);
+            else snprintf(b, sizeof b, "%sv[%u:%u]", o.neg ? "-" : "", o.v, o.v + o.n - 1);
+            return b;
+        case O_S:
+            if (o.n == 1) snprintf(b, sizeof b, "s%u", o.v);
+            else snprintf(b, sizeof b, "s[%u:%u]", o.v, o.v + o.n - 1);
+            return b;
+        case O_VCC: return "vcc";
+        case O_EXEC: return "exec";
+        case O_IMM:
+            if (o.v <= 64u) snprintf(b, sizeof b, "%u", o.v);
+            else if (o.v >= 0xFFFFFFF0u) snprintf(b, sizeof b, "%d", (int32_t)o.v);
+            else snprintf(b, sizeof b, "0x%x", o.v);
+            return b;
+        case O_LABEL: return prefix + "_L" + std::to_string(o.v);
+        case O_FONE: return "1.0";
+        default: return "";
+    }
+}
+
+}  // namespace
+
+// ---- the division subroutine ---------------------------------------------------------------
+// 256-bit division by f64 digit estimates over 32-bit digits, no normalisation shifts (the
+// round-1 interpreter's algorithm, gen_asm_core.py div_body, over fixed registers).  Step j
+// (7..0, entered at the highest j any lane needs): c = trunc(R / (y 2^(32j))) from f64 (relative
+// error ~2^-48, so c is the digit or off by one), R -= c*y*2^(32j) (8 mads), then one add-back if
+// R went negative, one subtract if R >= y 2^(32j).  Lanes with y = 0 keep R = |x| and get
+// q = 2^256 - 1 (SMT-LIB); signed kinds divide |x| by |y| and fix the signs by the bvsdiv /
+// bvsrem / bvsmod rules.
+std::vector<MI> div_routine() {
+    std::vector<MI> o;
+    auto E = [&](uint16_t op, std::initializer_list<Opnd> ops, bool e64 = false) {
+        MI m;
+        m.op = op;
+        m.e64 = e64 ? 1 : 0;
+        int i = 0;
+        for (const Opnd& x : ops) m.o[i++] = x;
+        o.push_back(m);
+    };
+    auto L = [&](uint32_t id) { E(M_LABEL, {LBL(id)}); };
+    auto Yr = [](int k) { return V(R_DY + k); };
+    auto Rr = [](int k) { return V(R_DR + k); };
+    auto Xr = [](int k) { return V(R_DQ + k); };
+    const Opnd FY = V(R_FY, 2), FR = V(R_FR, 2), FC = V(R_FC, 2), FT = V(R_FT, 2);
+    const Opnd CARRY = V(R_CARRY, 2), MAD = V(R_MAD, 2);
+    const Opnd C = V(R_C), T1 = V(R_T1), SX = V(R_SX), SY = V(R_SY);
+    const Opnd YNZ = S(S_DIV_YNZ, 2), DUMMY = S(S_DIV_DUMMY, 2), MSK = S(S_DIV_MSK, 2),
+               TM = S(S_DIV_TM, 2), K64 = S(S_DIV_F64K, 2), KIND = S(S_DIV_KIND);
+    const Opnd K64LO = S(S_DIV_F64K), K64HI = S(S_DIV_F64K + 1);
+    enum : uint32_t { L_UNS = 1, L_DONE, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
+                      L_SDIV, L_SREM, L_SMOD };
+    auto to_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
+        E(M_S_MOV_B32, {K64LO, IMM(0)});
+        E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});
+        E(M_V_CVT_F64_U32, {dst, limb(7)});
+        for (int k = 6; k >= 0; --k) {
+            E(M_V_CVT_F64_U32, {FT, limb(k)});
+            E(M_V_FMA_F64, {dst, dst, K64, FT});
+        }
+    };
+    auto Rl = [](int k) { return V(R_DR + k); };
+    auto Yl = [](int k) { return V(R_DY + k); };
+    // signed kinds: |x|, |y| as (v ^ m) - m with m = sign mask
+    E(M_S_CMP_LT_U32, {KIND, IMM(2)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_UNS)});
+    for (int w = 0; w < 2; ++w) {
+        const uint32_t base = w == 0 ? R_DR : R_DY;
+        const Opnd m = w == 0 ? SX : SY;
+        E(M_V_ASHRREV, {m, IMM(31), V(base + 7)});
+        for (int k = 0; k < 8; ++k) E(M_V_XOR, {V(base + k), V(base + k), m});
+        E(M_V_SUB_CO, {V(base), VCC(), V(base), m});
+        for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {V(base + k), VCC(), V(base + k), m, VCC()});
+    }
+    L(L_UNS);
+    for (int k = 0; k < 8; ++k) E(M_V_MOV, {Xr(k), IMM(0)});
+    E(M_V_OR3, {T1, Yr(0), Yr(1), Yr(2)});
+    E(M_V_OR3, {T1, T1, Yr(3), Yr(4)});
+    E(M_V_OR3, {T1, T1, Yr(5), Yr(6)});
+    E(M_V_OR, {T1, T1, Yr(7)});
+    E(M_V_CMP_NE, {YNZ, IMM(0), T1}, true);
+    E(M_V_SUB_CO, {T1, VCC(), Rr(0), Yr(0)});
+    for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {T1, VCC(), Rr(k), Yr(k), VCC()});
+    E(M_S_ANDN2_B64, {MSK, YNZ, VCC()});
+    E(M_S_CMP_EQ_U64, {MSK, IMM(0)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_DONE)});
+    // 1/yd, qd = R/y for the start digit
+    to_f64(FY, Yl);
+    E(M_V_RCP_F64, {FC, FY});
+    E(M_S_NOP, {IMM(1)});  // trans result -> non-trans VALU use needs a wait state
+    E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
+    E(M_V_FMA_F64, {FY, FC, FT, FC});
+    to_f64(FR, Rl);
+    E(M_V_MUL_F64, {FC, FR, FY});
+    for (int j = 7; j >= 1; --j) {  // start at the highest j with qd >= 2^(32j - 1) in some lane
+        const uint32_t hi = (uint32_t)(1023 + 32 * j - 1) << 20;
+        E(M_S_MOV_B32, {K64LO, IMM(0)});
+        E(M_S_MOV_B32, {K64HI, IMM(hi)});
+        E(M_V_CMP_LE_F64, {VCC(), K64, FC});
+        E(M_S_AND_B64, {TM, VCC(), MSK});
+        E(M_S_CMP_LG_U64, {TM, IMM(0)});
+        E(M_S_CBRANCH_SCC1, {LBL(L_STEP0 + j)});
+    }
+    E(M_S_BRANCH, {LBL(L_STEP0)});
+    for (int j = 7; j >= 0; --j) {
+        L(L_STEP0 + j);
+        to_f64(FR, Rl);
+        E(M_V_MUL_F64, {FC, FR, FY});
+        if (j) {
+            E(M_S_MOV_B32, {K64LO, IMM(0)});
+            E(M_S_MOV_B32, {K64HI, IMM((uint32_t)(1023 - 32 * j) << 20)});
+            E(M_V_MUL_F64, {FC, FC, K64});
+        }
+        // clamp to 2^32 - 1 (NaN from y = 0 lanes becomes the clamp and is zeroed below)
+        E(M_S_MOV_B32, {K64LO, IMM(0xffe00000u)});
+        E(M_S_MOV_B32, {K64HI, IMM(0x41efffffu)});
+        E(M_V_MIN_F64, {FC, FC, K64});
+        E(M_V_CVT_U32_F64, {C, FC});
+        E(M_V_CNDMASK, {C, IMM(0), C, YNZ}, true);
+        // R[j..] -= c * y (the product's limbs above limb 7 only feed the borrow)
+        E(M_V_MOV, {V(R_CARRY), IMM(0)});
+        E(M_V_MOV, {V(R_CARRY + 1), IMM(0)});
+        for (int k = 0; k < 8; ++k) {
+            E(M_V_MAD_U64_U32, {MAD, DUMMY, C, Yr(k), CARRY});
+            E(M_V_MOV, {V(R_CARRY), V(R_MAD + 1)});
+            const int limb = j + k;
+            if (limb <= 7) {
+                if (k == 0) E(M_V_SUB_CO, {Rr(limb), VCC(), Rr(limb), V(R_MAD)});
+                else E(M_V_SUBB_CO, {Rr(limb), VCC(), Rr(limb), V(R_MAD), VCC()});
+            } else {
+                E(M_V_SUBB_CO, {T1, VCC(), IMM(0), V(R_MAD), VCC()});
+            }
+        }
+        E(M_V_SUBB_CO, {T1, VCC(), IMM(0), V(R_CARRY), VCC()});  // limb j + 8 > 7
+        // negative: add y << 32j back, c - 1
+        E(M_S_MOV_B64, {MSK, VCC()});
+        E(M_S_CMP_EQ_U64, {MSK, IMM(0)});
+        E(M_S_CBRANCH_SCC1, {LBL(L_NONEG0 + j)});
+        for (int k = 0; k < 8 - j; ++k) {
+            E(M_V_CNDMASK, {T1, IMM(0), Yr(k), MSK}, true);
+            if (k == 0) E(M_V_ADD_CO, {Rr(j + k), VCC(), Rr(j + k), T1});
+            else E(M_V_ADDC_CO, {Rr(j + k), VCC(), Rr(j + k), T1, VCC()});
+        }
+        E(M_V_CNDMASK, {T1, IMM(0), IMM(1), MSK}, true);
+        E(M_V_SUB_U32, {C, C, T1});
+        L(L_NONEG0 + j);
+        // R >= y << 32j (y = 0 lanes excluded): subtract once more, c + 1
+        E(M_V_SUB_CO, {T1, VCC(), Rr(j), Yr(0)});
+        for (int k = 1; k < 8 - j; ++k) E(M_V_SUBB_CO, {T1, VCC(), Rr(j + k), Yr(k), VCC()});
+        for (int k = 8 - j; k < 8; ++k) E(M_V_SUBB_CO, {T1, VCC(), IMM(0), Yr(k), VCC()});
+        E(M_S_ANDN2_B64, {MSK, YNZ, VCC()});
+        E(M_S_CMP_EQ_U64, {MSK, IMM(0)});
+        E(M_S_CBRANCH_SCC1, {LBL(L_NOGE0 + j)});
+        for (int k = 0; k < 8 - j; ++k) {
+            E(M_V_CNDMASK, {T1, IMM(0), Yr(k), MSK}, true);
+            if (k == 0) E(M_V_SUB_CO, {Rr(j + k), VCC(), Rr(j + k), T1});
+            else E(M_V_SUBB_CO, {Rr(j + k), VCC(), Rr(j + k), T1, VCC()});
+        }
+        E(M_V_CNDMASK, {T1, IMM(0), IMM(1), MSK}, true);
+        E(M_V_ADD_U32, {C, C, T1});
+        L(L_NOGE0 + j);
+        E(M_V_MOV, {Xr(j), C});
+    }
+    L(L_DONE);
+    // y = 0: q = 2^256 - 1 (R already holds |x|)
+    for (int k = 0; k < 8; ++k) E(M_V_CNDMASK, {Xr(k), IMM(0xFFFFFFFFu), Xr(k), YNZ}, true);
+    auto cneg = [&](uint32_t dst, uint32_t srcb, Opnd m) {  // dst = (src ^ m) - m
+        for (int k = 0; k < 8; ++k) E(M_V_XOR, {V(dst + k), V(srcb + k), m});
+        E(M_V_SUB_CO, {V(dst), VCC(), V(dst), m});
+        for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {V(dst + k), VCC(), V(dst + k), m, VCC()});
+    };
+    E(M_S_CMP_EQ_U32, {KIND, IMM(0)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_WB)});
+    E(M_S_CMP_EQ_U32, {KIND, IMM(2)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_SDIV)});
+    E(M_S_CMP_EQ_U32, {KIND, IMM(4)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_SMOD)});
+    E(M_S_CMP_EQ_U32, {KIND, IMM(3)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_SREM)});
+    for (int k = 0; k < 8; ++k) E(M_V_MOV, {Xr(k), Rr(k)});  // UREM
+    E(M_S_BRANCH, {LBL(L_WB)});
+    L(L_SDIV);  // q negated when the signs differ
+    E(M_V_XOR, {T1, SX, SY});
+    cneg(R_DQ, R_DQ, T1);
+    E(M_S_BRANCH, {LBL(L_WB)});
+    L(L_SREM);  // r takes the sign of x
+    cneg(R_DQ, R_DR, SX);
+    E(M_S_BRANCH, {LBL(L_WB)});
+    L(L_SMOD);  // u = |x| % |y|: (x<0 ? -u : u) + (signs differ && u ? +-|y| : 0)
+    cneg(R_DQ, R_DR, SX);
+    E(M_V_OR3, {T1, Rr(0), Rr(1), Rr(2)});
+    E(M_V_OR3, {T1, T1, Rr(3), Rr(4)});
+    E(M_V_OR3, {T1, T1, Rr(5), Rr(6)});
+    E(M_V_OR, {T1, T1, Rr(7)});
+    E(M_V_CMP_NE, {MSK, IMM(0), T1}, true);
+    E(M_V_XOR, {T1, SX, SY});
+    E(M_V_CMP_NE, {VCC(), IMM(0), T1});
+    E(M_S_AND_B64, {MSK, MSK, VCC()});
+    cneg(R_DY, R_DY, SY);  // t = +-|y| (the original y)
+    for (int k = 0; k < 8; ++k) {
+        E(M_V_CNDMASK, {T1, IMM(0), Yr(k), MSK}, true);
+        if (k == 0) E(M_V_ADD_CO, {Xr(k), VCC(), Xr(k), T1});
+        else E(M_V_ADDC_CO, {Xr(k), VCC(), Xr(k), T1, VCC()});
+    }
+    L(L_WB);
+    E(M_RET, {});
+    return o;
+}
+
+std::string print(const MI& m, const std::string& prefix) {
+    if (m.op == M_LABEL) return prefix + "_L" + std::to_string(m.o[0].v) + ":";
+    if (m.op == M_CALL_DIV) {
+        const std::string l = prefix + "_c" + std::to_string(m.o[0].v);
+        char b[512];
+        snprintf(b, sizeof b,
+                 "s_getpc_b64 s[%u:%u]\n%s:\n"
+                 "s_add_u32 s%u, s%u, mh_div - %s\n"
+                 "s_addc_u32 s%u, s%u, 0\n"
+                 "s_swappc_b64 s[%u:%u], s[%u:%u]",
+                 S_DIV_TGT, S_DIV_TGT + 1, l.c_str(), S_DIV_TGT, S_DIV_TGT, l.c_str(),
+                 S_DIV_TGT + 1, S_DIV_TGT + 1, S_DIV_RA, S_DIV_RA + 1, S_DIV_TGT, S_DIV_TGT + 1);
+        return b;
+    }
+    if (m.op == M_RET) {
+        char b[64];
+        snprintf(b, sizeof b, "s_setpc_b64 s[%u:%u]", S_DIV_RA, S_DIV_RA + 1);
+        return b;
+    }
+    std::string s = op_name(m.op);
+    if (m.e64) s += "_e64";
+    if (m.op == M_S_NOP) return s + " " + std::to_string(m.o[0].v);
+    bool first = true;
+    for (const Opnd& o : m.o) {
+        if (o.k == O_NONE) break;
+        s += first ? " " : ", ";
+        s += opnd_str(o, prefix);
+        first = false;
+    }
+    return s;
+}
+
+void print_list(const std::vector<MI>& code, const std::string& prefix, std::string& out) {
+    for (const MI& m : code) {
+        out += print(m, prefix);
+        out += '\n';
+    }
+}
+
+uint32_t code_bytes(const TapeCode& tc) {
+    uint32_t b = 0;
+    for (const MI& m : tc.code) {
+        if (m.op == M_LABEL) continue;
+        if (m.op == M_CALL_DIV) { b += 24; continue; }
+        bool lit = false;
+        for (const Opnd& o : m.o) lit |= o.k == O_IMM && !is_inline(o.v);
+        const bool vop3 = m.e64 || m.op == M_V_OR3 || m.op == M_V_ALIGNBIT ||
+                          m.op == M_V_MAD_U64_U32 || m.op == M_V_FMA_F64 || m.op == M_V_MUL_F64 ||
+                          m.op == M_V_MIN_F64;
+        b += (vop3 || lit) ? 8 : 4;
+    }
+    return b;
+}
+
+namespace {
+
+void line(std::string& out, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+void line(std::string& out, const char* fmt, ...) {
+    char b[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof b, fmt, ap);
+    va_end(ap);
+    out += b;
+    out += '\n';
+}
+
+}  // namespace
+
+// Kernel `mh_jit` (register map in jit.h):
+//   s[0:1] kernarg pointer, s2 = workgroup id x (row block), s3 = workgroup id y (tape group);
+//   kernel arguments in s4..s23 (KernArgs); s24 = this wave's first row (buffer-local),
+//   s25 = its end, s26 = current 64-row chunk, s27 = column stride in bytes, s[28:29] load
+//   address, s[30:31] valid-lane mask, s[32:33] the tape's root mask, s34/s35 scratch,
+//   s[36:37] jump-table address, s38 = group index.
+//   v0 = workitem id, v1 = lane, v2 = row offset in bytes, v3 = per-tape hit counts (lane t =
+//   the group's tape t), v4 = per-tape first hit + 1 (0 = none), v5..v7 atomics / stores,
+//   v[8:39] the assignment columns, v[40:79] the division subroutine, v80.. tape temporaries.
+Module build_module(const std::vector<const TapeCode*>& codes,
+                    const std::vector<uint32_t>& tape_ids, uint32_t n_vars, bool values,
+                    uint32_t group_bytes) {
+    Module m;
+    std::string& o = m.text;
+    // groups: consecutive tapes up to group_bytes of code (and at most 64: one lane per tape)
+    uint32_t cur = 0, first = 0;
+    for (uint32_t i = 0; i < codes.size(); ++i) {
+        const uint32_t b = code_bytes(*codes[i]) + 96;
+        if (i > first && (cur + b > group_bytes || i - first >= 64)) {
+            m.group_first.push_back(first);
+            m.group_count.push_back(i - first);
+            first = i;
+            cur = 0;
+        }
+        cur += b;
+    }
+    if (first < codes.size()) {
+        m.group_first.push_back(first);
+        m.group_count.push_back((uint32_t)codes.size() - first);
+    }
+    uint32_t maxv = R_COL0 + 8 * n_vars;
+    bool any_div = false;
+    for (const TapeCode* tc : codes) {
+        maxv = std::max(maxv, tc->max_vgpr);
+        any_div |= tc->calls_div;
+    }
+    if (any_div) maxv = std::max<uint32_t>(maxv, R_TEMP0);
+    maxv = std::max<uint32_t>(maxv, 8);
+    maxv = (maxv + 7) & ~7u;
+    m.max_vgpr = maxv;
+    m.n_sgpr = S_NEXT_FREE;
+
+    line(o, ".amdgcn_target \"amdgcn-amd-amdhsa--gfx950\"");
+    line(o, ".amdhsa_code_object_version 5");
+    line(o, ".text");
+    line(o, ".globl mh_jit");
+    line(o, ".p2align 8");
+    line(o, ".type mh_jit,@function");
+    line(o, "mh_jit:");
+    line(o, "s_load_dwordx16 s[4:19], s[0:1], 0x0");
+    line(o, "s_load_dwordx4 s[20:23], s[0:1], 0x40");
+    line(o, "v_and_b32 v1, 63, v0");
+    line(o, "v_lshrrev_b32 v2, 6, v0");
+    line(o, "v_readfirstlane_b32 s24, v2");
+    line(o, "s_waitcnt lgkmcnt(0)");
+    line(o, "s_lshr_b32 s25, s19, 2");        // rows per wave
+    line(o, "s_mul_i32 s26, s2, s19");        // row block * rows per workgroup
+    line(o, "s_mul_i32 s27, s24, s25");       // wave * rows per wave
+    line(o, "s_add_u32 s24, s8, s26");
+    line(o, "s_add_u32 s24, s24, s27");       // first row of this wave
+    line(o, "s_add_u32 s25, s24, s25");
+    line(o, "s_add_u32 s26, s8, s10");        // row_first + row_count
+    line(o, "s_min_u32 s25, s25, s26");
+    line(o, "s_cmp_ge_u32 s24, s25");
+    line(o, "s_cbranch_scc1 mh_done");
+    line(o, "s_lshl_b32 s27, s6, 2");         // column stride (bytes)
+    line(o, "v_mov_b32 v3, 0");
+    line(o, "v_mov_b32 v4, 0");
+    line(o, "s_add_u32 s38, s3, s22");        // group
+    line(o, "s_getpc_b64 s[36:37]");
+    line(o, "mh_pc:");
+    line(o, "s_add_u32 s36, s36, mh_tab - mh_pc");
+    line(o, "s_addc_u32 s37, s37, 0");
+    line(o, "s_lshl_b32 s34, s38, 2");
+    line(o, "s_load_dword s35, s[36:37], s34");
+    line(o, "s_waitcnt lgkmcnt(0)");
+    line(o, "s_add_u32 s36, s36, s35");
+    line(o, "s_addc_u32 s37, s37, 0");
+    line(o, "s_setpc_b64 s[36:37]");
+    line(o, "mh_done:");
+    line(o, "s_endpgm");
+    line(o, ".p2align 2");
+    line(o, "mh_tab:");
+    for (size_t g = 0; g < m.group_first.size(); ++g) line(o, ".long mh_g%zu - mh_tab", g);
+    for (size_t g = 0; g < m.group_first.size(); ++g) {
+        const uint32_t g0 = m.group_first[g], gn = m.group_count[g];
+        line(o, ".p2align 6");
+        line(o, "mh_g%zu:", g);
+        line(o, "s_mov_b32 s26, s24");
+        line(o, "mh_g%zu_chunk:", g);
+        // rows of this chunk, validity, clamped load offsets
+        line(o, "v_add_u32 v2, s26, v1");
+        line(o, "v_cmp_gt_u32 vcc, s25, v2");
+        line(o, "s_mov_b64 s[30:31], vcc");
+        line(o, "s_sub_u32 s34, s25, 1");
+        line(o, "v_min_u32 v2, s34, v2");
+        line(o, "v_lshlrev_b32 v2, 2, v2");
+        line(o, "s_mov_b64 s[28:29], s[4:5]");
+        for (uint32_t j = 0; j < 8 * n_vars; ++j) {
+            if (j) {
+                line(o, "s_add_u32 s28, s28, s27");
+                line(o, "s_addc_u32 s29, s29, 0");
+            }
+            line(o, "global_load_dword v%u, v2, s[28:29]", R_COL0 + j);
+        }
+        line(o, "s_waitcnt vmcnt(0)");
+        for (uint32_t t = 0; t < gn; ++t) {
+            const TapeCode& tc = *codes[g0 + t];
+            char pre[64];
+            snprintf(pre, sizeof pre, "mh_g%zut%u", g, t);
+            print_list(tc.code, pre, o);
+            if (values) {
+                const uint32_t id = tape_ids[g0 + t];
+                line(o, "s_mov_b64 exec, s[30:31]");
+                line(o, "s_nop 1");
+                line(o, "s_sub_u32 s34, s26, s8");
+                line(o, "v_add_u32 v5, s34, v1");
+                line(o, "v_lshlrev_b32 v5, 2, v5");
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t mult = ((uint64_t)id * 8 + (uint64_t)k) * 4ull;
+                    if (mult >> 32) { line(o, "s_endpgm"); break; }
+                    line(o, "s_mul_i32 s34, s10, 0x%x", (uint32_t)mult);
+                    line(o, "s_mul_hi_u32 s35, s10, 0x%x", (uint32_t)mult);
+                    line(o, "s_add_u32 s28, s20, s34");
+                    line(o, "s_addc_u32 s29, s21, s35");
+                    if (tc.root_bool) {
+                        if (k == 0) line(o, "v_cndmask_b32_e64 v6, 0, 1, s[32:33]");
+                        else line(o, "v_mov_b32 v6, 0");
+                        line(o, "global_store_dword v5, v6, s[28:29]");
+                    } else if (tc.root_limbs[k] != ~0u) {
+                        line(o, "global_store_dword v5, v%u, s[28:29]", tc.root_limbs[k]);
+                    } else {
+                        line(o, "v_mov_b32 v6, 0x%x", tc.root_const[k]);
+                        line(o, "global_store_dword v5, v6, s[28:29]");
+                    }
+                }
+                line(o, "s_mov_b64 exec, -1");
+                continue;
+            }
+            line(o, "s_and_b64 s[32:33], s[32:33], s[30:31]");
+            line(o, "s_bcnt1_i32_b64 s34, s[32:33]");
+            line(o, "v_readlane_b32 s35, v3, %u", t);
+            line(o, "s_add_u32 s35, s35, s34");
+            line(o, "v_writelane_b32 v3, s35, %u", t);
+            line(o, "s_nop 4");
+            line(o, "s_cmp_eq_u64 s[32:33], 0");
+            line(o, "s_cbranch_scc1 %s_nf", pre);
+            line(o, "v_readlane_b32 s35, v4, %u", t);
+            line(o, "s_cmp_lg_u32 s35, 0");
+            line(o, "s_cbranch_scc1 %s_nf", pre);
+            line(o, "s_ff1_i32_b64 s34, s[32:33]");
+            line(o, "s_add_u32 s34, s34, s26");
+            line(o, "s_add_u32 s34, s34, 1");
+            line(o, "v_writelane_b32 v4, s34, %u", t);
+            line(o, "s_nop 4");
+            line(o, "%s_nf:", pre);
+        }
+        line(o, "s_add_u32 s26, s26, 64");
+        line(o, "s_cmp_lt_u32 s26, s25");
+        line(o, "s_cbranch_scc1 mh_g%zu_chunk", g);
+        if (!values) {
+            line(o, "s_nop 4");
+            for (uint32_t t = 0; t < gn; ++t) {
+                const uint32_t id = tape_ids[g0 + t];
+                line(o, "v_readlane_b32 s34, v3, %u", t);
+                line(o, "s_cmp_eq_u32 s34, 0");
+                line(o, "s_cbranch_scc1 mh_g%zue%u_nc", g, t);
+                line(o, "s_mov_b64 exec, 1");
+                line(o, "s_nop 1");
+                line(o, "v_mov_b32 v6, s34");
+                line(o, "v_mov_b32 v7, 0");
+                line(o, "v_mov_b32 v5, 0x%x", id * 8u);
+                line(o, "global_atomic_add_x2 v5, v[6:7], s[16:17]");
+                line(o, "s_mov_b64 exec, -1");
+                line(o, "mh_g%zue%u_nc:", g, t);
+                line(o, "v_readlane_b32 s34, v4, %u", t);
+                line(o, "s_cmp_eq_u32 s34, 0");
+                line(o, "s_cbranch_scc1 mh_g%zue%u_nf", g, t);
+                line(o, "s_sub_u32 s34, s34, 1");
+                line(o, "s_add_u32 s34, s34, s12");
+                line(o, "s_addc_u32 s35, s13, 0");
+                line(o, "s_mov_b64 exec, 1");
+                line(o, "s_nop 1");
+                line(o, "v_mov_b32 v6, s34");
+                line(o, "v_mov_b32 v7, s35");
+                line(o, "v_mov_b32 v5, 0x%x", id * 8u);
+                line(o, "global_atomic_umin_x2 v5, v[6:7], s[14:15]");
+                line(o, "s_mov_b64 exec, -1");
+                line(o, "mh_g%zue%u_nf:", g, t);
+            }
+        }
+        line(o, "s_endpgm");
+    }
+    if (any_div) {
+        line(o, ".p2align 6");
+        line(o, "mh_div:");
+        print_list(div_routine(), "mh_dv", o);
+    }
+    line(o, ".Lmh_jit_end:");
+    line(o, ".size mh_jit, .Lmh_jit_end-mh_jit");
+    // kernel descriptor
+    line(o, ".rodata");
+    line(o, ".p2align 6");
+    line(o, ".amdhsa_kernel mh_jit");
+    line(o, "  .amdhsa_group_segment_fixed_size 0");
+    line(o, "  .amdhsa_private_segment_fixed_size 0");
+    line(o, "  .amdhsa_kernarg_size %u", (uint32_t)sizeof(KernArgs));
+    line(o, "  .amdhsa_user_sgpr_count 2");
+    line(o, "  .amdhsa_user_sgpr_kernarg_segment_ptr 1");
+    line(o, "  .amdhsa_system_sgpr_workgroup_id_x 1");
+    line(o, "  .amdhsa_system_sgpr_workgroup_id_y 1");
+    line(o, "  .amdhsa_system_vgpr_workitem_id 0");
+    line(o, "  .amdhsa_next_free_vgpr %u", maxv);
+    line(o, "  .amdhsa_next_free_sgpr %u", (uint32_t)S_NEXT_FREE);
+    line(o, "  .amdhsa_accum_offset %u", (maxv + 3) & ~3u);
+    line(o, "  .amdhsa_reserve_vcc 1");
+    line(o, "  .amdhsa_ieee_mode 1");
+    line(o, "  .amdhsa_dx10_clamp 1");
+    line(o, ".end_amdhsa_kernel");
+    line(o, ".amdgpu_metadata");
+    line(o, "---");
+    line(o, "amdhsa.kernels:");
+    line(o, "  - .args:");
+    line(o, "      - .offset: 0");
+    line(o, "        .size: %u", (uint32_t)sizeof(KernArgs));
+    line(o, "        .value_kind: by_value");
+    line(o, "    .group_segment_fixed_size: 0");
+    line(o, "    .kernarg_segment_align: 8");
+    line(o, "    .kernarg_segment_size: %u", (uint32_t)sizeof(KernArgs));
+    line(o, "    .max_flat_workgroup_size: 256");
+    line(o, "    .name: mh_jit");
+    line(o, "    .private_segment_fixed_size: 0");
+    line(o, "    .sgpr_count: %u", (uint32_t)S_NEXT_FREE + 6);
+    line(o, "    .sgpr_spill_count: 0");
+    line(o, "    .symbol: mh_jit.kd");
+    line(o, "    .vgpr_count: %u", maxv);
+    line(o, "    .vgpr_spill_count: 0");
+    line(o, "    .agpr_count: 0");
+    line(o, "    .wavefront_size: 64");
+    line(o, "amdhsa.target: amdgcn-amd-amdhsa--gfx950");
+    line(o, "amdhsa.version:");
+    line(o, "  - 1");
+    line(o, "  - 2");
+    line(o, "...");
+    line(o, ".end_amdgpu_metadata");
+    return m;
+}
+
+bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
+                   const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, bool values,
+                   const Options& opt, uint32_t threads, std::vector<Built>& out,
+                   BuildStats& stats, std::string& err) {
+    threads = std::max<uint32_t>(1, std::min<uint32_t>(threads, (n_tapes + 63) / 64));
+    out.assign(threads, Built());
+    stats.jitted.assign(n_tapes, 0);
+    stats.why.assign(n_tapes, std::string());
+    std::vector<uint64_t> bytes(threads, 0), valu(threads, 0), wide(threads, 0);
+    auto work = [&](uint32_t s) {
+        const uint32_t lo = (uint32_t)((uint64_t)n_tapes * s / threads);
+        const uint32_t hi = (uint32_t)((uint64_t)n_tapes * (s + 1) / threads);
+        Built& b = out[s];
+        std::vector<uint32_t> pool;
+        std::unordered_map<std::string, uint32_t> index;
+        std::vector<TapeCode> codes;
+        codes.reserve(hi - lo);
+        std::vector<uint32_t> ids;
+        for (uint32_t t = lo; t < hi; ++t) {
+            SsaTape st;
+            std::string e;
+            if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts, n_consts,
+                               n_vars, pool, index, st, e) != MH_OK) {
+                stats.why[t] = "lowering: " + e;
+                continue;
+            }
+            TapeCode tc = emit_tape(st, pool, n_vars, opt);
+            if (tc.ok && code_bytes(tc) > 96 * 1024) {
+                tc.ok = false;
+                tc.why = "tape code larger than 96 KB";
+            }
+            if (!tc.ok) {
+                stats.why[t] = tc.why;
+                continue;
+            }
+            stats.jitted[t] = 1;
+            bytes[s] += code_bytes(tc);
+            valu[s] += tc.n_valu;
+            wide[s] += tc.n_valu_wide;
+            codes.push_back(std::move(tc));
+            ids.push_back(t);
+        }
+        b.tape_ids = ids;
+        if (codes.empty()) return;
+        std::vector<const TapeCode*> ptrs;
+        for (const TapeCode& c : codes) ptrs.push_back(&c);
+        Module m = build_module(ptrs, ids, n_vars, false);
+        b.n_groups = (uint32_t)m.group_first.size();
+        b.max_vgpr = m.max_vgpr;
+        std::string log;
+        if (!assemble(m.text, b.hsaco, log)) {
+            b.err = "assemble: " + log.substr(0, 2000);
+            return;
+        }
+        if (values) {
+            Module mv = build_module(ptrs, ids, n_vars, true);
+            if (!assemble(mv.text, b.hsaco_values, log)) b.err = "assemble (values): " + log.substr(0, 2000);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t s = 1; s < threads; ++s) pool.emplace_back(work, s);
+    work(0);
+    for (auto& th : pool) th.join();
+    for (uint32_t s = 0; s < threads; ++s) {
+        if (!out[s].err.empty()) {
+            err = out[s].err;
+            return false;
+        }
+        stats.code_bytes += bytes[s];
+        stats.valu_static += valu[s];
+        stats.valu_wide_static += wide[s];
+    }
+    return true;
+}
+
+TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
+                   const Options& opt) {
+    Emitter e(st, pool, n_vars, opt);
+    return e.run();
+}
+
+}  // namespace jit
+}  // namespace mh

@@ -1,0 +1,187 @@
+// Native-code path for throughput launches (no reference counterpart: it replaces the
+// interpreter's per-instruction dispatch for mh_run over a resident tape set).
+//
+// Each tape is compiled from its SSA form (compile.h lower_tape_ssa) into straight-line gfx950
+// machine code with fixed registers: every 256-bit value is 8 limbs, each limb either a
+// compile-time constant (no register, no instruction) or one VGPR; Bool values are 64-bit lane
+// masks in SGPR pairs (compares leave their result in VCC, the conjunction at the root is
+// s_and_b64).  Only the limbs a consumer demands are computed (an AND with a 160-bit mask never
+// computes the top three limbs of its operand), shifts by constants are register renaming plus
+// at most one v_alignbit per limb, and the division family runs in one shared subroutine.
+//
+// The machine code of a whole tape set is one code object: a single kernel whose workgroups
+// are a 2-D grid (x = block of rows, y = group of tapes).  A group is a run of consecutive tapes
+// whose code fits the instruction cache; each wave loads its rows' assignment columns into VGPRs
+// once per 64-row chunk and runs every tape of its group over them, so the tape code is fetched
+// from the instruction cache rather than decoded per instruction as the interpreter does.
+//
+// Text is assembled in-process by comgr (jit_comgr.cpp) and loaded with hipModuleLoadData
+// (capi.cpp).  The instruction list (MI) is also what the test-only host emulator runs
+// (tests/native/jit_emu.cpp), so the emitted code is checked against the oracle without a GPU.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "compile.h"
+
+namespace mh {
+namespace jit {
+
+// ---- machine instructions ---------------------------------------------------------------
+enum OKind : uint8_t { O_NONE, O_V, O_S, O_VCC, O_IMM, O_LABEL, O_EXEC, O_FONE /* f64 1.0 */ };
+
+struct Opnd {
+    uint8_t k = O_NONE;
+    uint8_t n = 1;        // registers in the range (1, 2 = pair)
+    uint8_t neg = 0;      // f64 source negation modifier
+    uint32_t v = 0;       // register number / immediate bits / label id
+};
+
+inline Opnd V(uint32_t r, uint8_t n = 1) { Opnd o; o.k = O_V; o.v = r; o.n = n; return o; }
+inline Opnd S(uint32_t r, uint8_t n = 1) { Opnd o; o.k = O_S; o.v = r; o.n = n; return o; }
+inline Opnd VCC() { Opnd o; o.k = O_VCC; o.n = 2; return o; }
+inline Opnd EXEC() { Opnd o; o.k = O_EXEC; o.n = 2; return o; }
+inline Opnd IMM(uint32_t x) { Opnd o; o.k = O_IMM; o.v = x; return o; }
+inline Opnd LBL(uint32_t id) { Opnd o; o.k = O_LABEL; o.v = id; return o; }
+inline Opnd FONE() { Opnd o; o.k = O_FONE; return o; }
+inline Opnd NEG(Opnd o) { o.neg = 1; return o; }
+
+// inline constants of 32-bit integer operands (no literal dword, no constant-bus use)
+inline bool is_inline(uint32_t x) { return x <= 64u || x >= 0xFFFFFFF0u; }
+
+enum Op : uint16_t {
+    // VALU (e64 flag selects the VOP3 encoding where both exist)
+    M_V_MOV, M_V_ADD_U32, M_V_SUB_U32, M_V_SUBREV_U32,
+    M_V_ADD_CO, M_V_ADDC_CO, M_V_SUB_CO, M_V_SUBB_CO, M_V_SUBREV_CO, M_V_SUBBREV_CO,
+    M_V_AND, M_V_OR, M_V_XOR, M_V_NOT, M_V_OR3,
+    M_V_ALIGNBIT, M_V_LSHLREV, M_V_LSHRREV, M_V_ASHRREV,
+    M_V_CNDMASK,   // d = mask ? src1 : src0
+    M_V_CMP_EQ, M_V_CMP_NE, M_V_CMP_LT, M_V_CMP_LE, M_V_CMP_GT, M_V_CMP_GE,  // u32
+    M_V_MAD_U64_U32,
+    M_V_CVT_F64_U32, M_V_FMA_F64, M_V_RCP_F64, M_V_MUL_F64, M_V_MIN_F64, M_V_CVT_U32_F64,
+    M_V_CMP_LE_F64,
+    // SALU
+    M_S_MOV_B32, M_S_MOV_B64, M_S_AND_B64, M_S_OR_B64, M_S_XOR_B64, M_S_XNOR_B64,
+    M_S_ANDN2_B64, M_S_NOT_B64, M_S_CMP_EQ_U64, M_S_CMP_LG_U64, M_S_CMP_EQ_U32,
+    M_S_CMP_LT_U32,
+    // control
+    M_S_CBRANCH_SCC0, M_S_CBRANCH_SCC1, M_S_BRANCH, M_LABEL, M_S_NOP,
+    M_CALL_DIV,    // s_getpc / s_add / s_swappc into the division subroutine
+    M_RET,         // s_setpc_b64 of the return address (end of the subroutine)
+    M_NUM_OPS
+};
+
+struct MI {
+    uint16_t op;
+    uint8_t e64 = 0;
+    Opnd o[5];
+};
+
+// ---- register map of the generated kernel (documented in jit.cpp) ----------------------
+enum : uint32_t {
+    R_COL0 = 8,          // assignment column v limb k is v[R_COL0 + 8 v + k]
+    R_DIV0 = 40,         // division subroutine registers v[40..79]
+    R_DY = 40, R_DR = 48, R_DQ = 56, R_FY = 64, R_FR = 66, R_FC = 68, R_FT = 70,
+    R_CARRY = 72, R_MAD = 74, R_C = 76, R_T1 = 77, R_SX = 78, R_SY = 79,
+    R_TEMP0 = 80,        // first free VGPR of a tape that can call the division subroutine
+    R_TEMP_NODIV = 40,   // ... and of one that cannot
+    // SGPRs
+    S_RES = 32,          // the tape's root mask
+    S_BOOL0 = 40, N_BOOL_PAIRS = 16,   // Bool lane masks s[40:71]
+    S_KSTAGE = 72, N_KSTAGE = 4,       // constant staging s72..s75
+    S_DIV_RA = 76, S_DIV_TGT = 78, S_DIV_KIND = 80, S_DIV_YNZ = 82, S_DIV_DUMMY = 84,
+    S_DIV_MSK = 86, S_DIV_TM = 88, S_DIV_F64K = 90,
+    S_NEXT_FREE = 92,
+};
+
+struct TapeCode {
+    bool ok = false;
+    std::string why;            // reason the tape stays on the interpreter
+    std::vector<MI> code;       // body: root mask in s[S_RES:S_RES+1] (or the root value)
+    uint32_t max_vgpr = 0;      // highest VGPR used + 1
+    bool calls_div = false;
+    bool root_bool = true;
+    uint32_t root_limbs[8];     // values mode: VGPR of each root limb, or ~0u (then constant)
+    uint32_t root_const[8];
+    uint32_t n_valu = 0, n_valu_wide = 0, n_salu = 0;  // static counts (wide = 4-cycle class)
+    uint64_t alg_ops = 0;
+};
+
+struct Options {
+    uint32_t max_vgpr = 128;    // VGPR budget of the kernel (occupancy: 512 / max_vgpr waves)
+};
+
+// Emit one tape (SSA after folding) with constants from `pool` (8 limbs per entry).
+TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
+                   const Options& opt);
+
+// The division subroutine (x in v[R_DR..], y in v[R_DY..], kind in S_DIV_KIND: 0 udiv, 1 urem,
+// 2 sdiv, 3 srem, 4 smod; result in v[R_DQ..]).
+std::vector<MI> div_routine();
+
+// Assembly text of one instruction / a list (labels get `prefix`).
+std::string print(const MI& m, const std::string& prefix);
+void print_list(const std::vector<MI>& code, const std::string& prefix, std::string& out);
+
+// The whole code object source for tapes `codes` (only the ok ones are included), grouped by
+// instruction bytes; tape_ids[i] is the result slot of codes[i].
+struct Module {
+    std::string text;
+    std::vector<uint32_t> group_first;   // index into the jitted list of each group's first tape
+    std::vector<uint32_t> group_count;
+    uint32_t max_vgpr = 0;
+    uint32_t n_sgpr = 0;
+};
+// values = true: every tape stores its root value (8 limbs per row, the parity path) instead of
+// counting hits.
+Module build_module(const std::vector<const TapeCode*>& codes,
+                    const std::vector<uint32_t>& tape_ids, uint32_t n_vars, bool values,
+                    uint32_t group_bytes = 40 * 1024);
+
+// Estimated machine-code bytes of a tape body.
+uint32_t code_bytes(const TapeCode& tc);
+
+// comgr: assemble + link `text` into a gfx950 code object (jit_comgr.cpp).
+bool assemble(const std::string& text, std::vector<char>& hsaco, std::string& log);
+
+// A whole tape set to code objects: tapes are lowered and emitted, cut into `threads` contiguous
+// slices, and each slice becomes one code object (count kernel, and the values kernel when
+// asked), built and assembled on its own thread.  No HIP calls: capi.cpp loads the results.
+struct Built {
+    std::vector<char> hsaco, hsaco_values;
+    uint32_t n_groups = 0;
+    uint32_t max_vgpr = 0;
+    std::vector<uint32_t> tape_ids;    // jitted tapes of this slice
+    std::string err;
+};
+struct BuildStats {
+    std::vector<uint8_t> jitted;       // per tape
+    std::vector<std::string> why;      // per tape: reason when not jitted
+    uint64_t code_bytes = 0, valu_static = 0, valu_wide_static = 0;
+};
+bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
+                   const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, bool values,
+                   const Options& opt, uint32_t threads, std::vector<Built>& out,
+                   BuildStats& stats, std::string& err);
+
+// Kernel arguments (the kernarg layout build_module's prologue reads).
+struct KernArgs {
+    uint64_t assign;       // 0x00
+    uint64_t capacity;     // 0x08
+    uint64_t row_first;    // 0x10
+    uint64_t row_count;    // 0x18
+    uint64_t index_base;   // 0x20
+    uint64_t first_hit;    // 0x28 (u64 per tape id, already offset by -result_base)
+    uint64_t hit_count;    // 0x30
+    uint32_t n_rowblocks;  // 0x38
+    uint32_t rows_per_wg;  // 0x3c (multiple of 256)
+    uint64_t values_out;   // 0x40 (0: count mode)
+    uint32_t group_first;  // 0x48
+    uint32_t mode;         // 0x4c (0 count all, 1 first hit)
+};
+static_assert(sizeof(KernArgs) == 0x50, "kernarg layout");
+
+}  // namespace jit
+}  // namespace mh

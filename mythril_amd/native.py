@@ -63,6 +63,10 @@ SIGNATURES = {
     "mh_eval_values": (C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint64, C.c_uint64, _u32p]),
     "mh_microbench_valu": (C.c_int32, [_vp, C.c_uint32, C.POINTER(C.c_double)]),
     "mh_microbench_issue": (C.c_int32, [_vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]),
+    "mh_tapes_jit": (C.c_int32, [_vp, C.c_uint32, C.c_uint32]),
+    "mh_tapes_jit_info": (C.c_int32, [_vp, _vp]),
+    "mh_tapes_jitted": (C.c_int32, [_vp, C.POINTER(C.c_uint8), C.c_uint32]),
+    "mh_jit_eval_all": (C.c_int32, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _u32p]),
     "mh_ctx_enable_timing": (C.c_int32, [_vp, C.c_int32]),
     "mh_ctx_kernel_time": (C.c_int32, [_vp, C.POINTER(C.c_double), _u64p]),
 }
@@ -95,6 +99,24 @@ class TapeInfo(C.Structure):
         ("features", C.c_uint32),
         ("alg_ops", C.c_uint64),
     ]
+
+
+class JitInfo(C.Structure):
+    """mh_jit_info (include/mythril_hip.h)."""
+
+    _fields_ = [
+        ("n_jitted", C.c_uint32),
+        ("n_groups", C.c_uint32),
+        ("n_modules", C.c_uint32),
+        ("max_vgpr", C.c_uint32),
+        ("code_bytes", C.c_uint64),
+        ("valu_static", C.c_uint64),
+        ("valu_wide_static", C.c_uint64),
+        ("build_ms", C.c_double),
+    ]
+
+
+JIT_VALUES = 1
 
 
 class Guide(C.Structure):
@@ -229,6 +251,32 @@ class CompiledTapes:
         self.h = h
         self.n_tapes = len(tapeset.tapes)
         self.n_vars = tapeset.n_vars
+
+    def jit(self, values: bool = False, max_vgpr: int = 0) -> dict:
+        """Compile the tapes the JIT covers to native gfx950 code (mh_tapes_jit); later runs
+        over the whole set use it.  Returns mh_tapes_jit_info as a dict."""
+        _check(self.ctx.lib.mh_tapes_jit(self.h, JIT_VALUES if values else 0, max_vgpr))
+        return self.jit_info()
+
+    def jit_info(self) -> dict:
+        ji = JitInfo()
+        _check(self.ctx.lib.mh_tapes_jit_info(self.h, C.byref(ji)))
+        return {f: getattr(ji, f) for f, _ in JitInfo._fields_}
+
+    def jitted(self) -> np.ndarray:
+        out = np.zeros(max(self.n_tapes, 1), dtype=np.uint8)
+        _check(self.ctx.lib.mh_tapes_jitted(self.h, out.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                            self.n_tapes))
+        return out[: self.n_tapes]
+
+    def jit_values(self, assign: "Assignments", row_first: int = 0,
+                   row_count: Optional[int] = None) -> np.ndarray:
+        """Root values of every jitted tape by the native code: u32 [n_tapes, 8, rows]."""
+        rc = assign.capacity - row_first if row_count is None else row_count
+        out = np.zeros((self.n_tapes, 8, max(rc, 1)), dtype=np.uint32)
+        _check(self.ctx.lib.mh_jit_eval_all(self.ctx.h, self.h, assign.h, row_first, rc,
+                                            _ptr(out)))
+        return out[:, :, :rc]
 
     def info(self):
         arr = (TapeInfo * max(self.n_tapes, 1))()

@@ -20,12 +20,16 @@ CSRC = os.path.join(ROOT, "mythril_amd", "csrc")
 
 def build_emulator() -> str:
     """Build the test-only host emulator (tests/native/emu.cpp + the tape compiler)."""
-    srcs = [os.path.join(EMU_DIR, "emu.cpp"), os.path.join(CSRC, "compile.cpp")]
+    srcs = [os.path.join(EMU_DIR, "emu.cpp"), os.path.join(EMU_DIR, "jit_emu.cpp"),
+            os.path.join(CSRC, "compile.cpp"), os.path.join(CSRC, "jit.cpp"),
+            os.path.join(CSRC, "jit_comgr.cpp")]
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     if os.path.exists(EMU_LIB) and all(os.path.getmtime(EMU_LIB) >= os.path.getmtime(d)
                                        for d in deps):
         return EMU_LIB
-    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + CSRC, "-o", EMU_LIB] + srcs
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + CSRC, "-I/opt/rocm/include",
+           "-o", EMU_LIB] + srcs + ["-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib",
+                                    "-lamd_comgr"]
     subprocess.run(cmd, check=True, capture_output=True)
     return EMU_LIB
 

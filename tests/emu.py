@@ -69,3 +69,73 @@ class Emulator:
         if r != 0:
             raise EmuError(r, err.value.decode())
         return int(nw.value) // 2
+
+
+class JitResult:
+    def __init__(self, info, values, why):
+        self.ok = bool(info[0])
+        self.max_vgpr, self.n_valu, self.n_valu_wide, self.n_salu = (int(x) for x in info[1:5])
+        self.calls_div, self.root_bool, self.code_bytes = bool(info[5]), bool(info[6]), int(info[7])
+        self.values = values
+        self.why = why
+
+
+def _jit_fn(lib, name, restype, argtypes):
+    f = getattr(lib, name)
+    f.restype = restype
+    f.argtypes = argtypes
+    return f
+
+
+def jit_eval(emu: "Emulator", ts: TapeSet, tape: int, soa: np.ndarray, max_vgpr: int = 128):
+    """The JIT's machine code for one tape, run by the host wave emulator
+    (tests/native/jit_emu.cpp) over rows of `soa` ([n_vars, 8, rows] u32).  Returns a
+    JitResult whose .values are root ints per row (None when the tape is not jitted)."""
+    f = _jit_fn(emu.lib, "emu_jit_eval", C.c_int32,
+                [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                 C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p,
+                 C.c_char_p, C.c_int])
+    nodes, offs, consts = ts.flatten()
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32)
+    rows = soa.shape[2] if soa.size else 1
+    if soa.size == 0:
+        soa = np.zeros((max(ts.n_vars, 1), 8, 1), dtype=np.uint32)
+    soa = np.ascontiguousarray(soa, dtype=np.uint32)
+    out = np.zeros((8, rows), dtype=np.uint32)
+    info = np.zeros(8, dtype=np.uint32)
+    err = C.create_string_buffer(512)
+    r = f(nodes.ctypes.data, offs.ctypes.data, len(ts.tapes), consts.ctypes.data,
+          len(ts.pool.values), ts.n_vars, tape, soa.ctypes.data, rows, out.ctypes.data, max_vgpr,
+          info.ctypes.data, err, 512)
+    if r != 0:
+        raise EmuError(r, err.value.decode())
+    if not info[0]:
+        return JitResult(info, None, err.value.decode())
+    vals = [sum(int(out[k, j]) << (32 * k) for k in range(8)) for j in range(rows)]
+    return JitResult(info, vals, "")
+
+
+def jit_module(emu: "Emulator", ts: TapeSet, values: bool = False, max_vgpr: int = 128,
+               assemble: bool = True):
+    """(module text, code object bytes, tapes jitted) for a whole tape set."""
+    f = _jit_fn(emu.lib, "emu_jit_module", C.c_int64,
+                [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                 C.c_uint32, C.c_uint32, C.c_int32, C.c_char_p, C.c_uint64,
+                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_char_p, C.c_int])
+    nodes, offs, consts = ts.flatten()
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32)
+    cap = 64 << 20
+    text = C.create_string_buffer(cap)
+    hs = C.c_uint64()
+    nj = C.c_uint32()
+    err = C.create_string_buffer(8192)
+    n = f(nodes.ctypes.data, offs.ctypes.data, len(ts.tapes), consts.ctypes.data,
+          len(ts.pool.values), ts.n_vars, int(values), max_vgpr, int(assemble), text, cap,
+          C.byref(hs), C.byref(nj), err, 8192)
+    if n < 0:
+        raise EmuError(int(n), err.value.decode())
+    return text.value.decode(), int(hs.value), int(nj.value)

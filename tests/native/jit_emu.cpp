@@ -1,0 +1,396 @@
+// TEST-ONLY host emulator of the JIT's machine code (mythril_amd/csrc/jit.h MI lists).
+//
+// Executes the instruction list the JIT emits for one tape (and the shared division subroutine)
+// on a host model of one gfx950 wave: 64 lanes of VGPRs, SGPRs, VCC, SCC.  Every instruction
+// kind the emitter uses has its ISA semantics restated here (carry chains, v_mad_u64_u32,
+// v_alignbit, v_cndmask, compares, the f64 digit estimates of the division), so
+// tests/test_jit.py checks the emitted code -- register allocation, limb specialisation,
+// encodings -- against the oracle without a GPU.  Registers nobody wrote are poisoned.
+// (v_rcp_f64 is modelled as an exact reciprocal; the division corrects its digit estimates by
+// +-1, so its results do not depend on the last bit of the estimate.)
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "compile.h"
+#include "jit.h"
+
+using namespace mh;
+using namespace mh::jit;
+
+namespace {
+
+struct Wave {
+    uint32_t v[512][64];
+    uint32_t s[128];
+    uint64_t vcc = 0;
+    bool scc = false;
+
+    uint32_t r32(const Opnd& o, int l) const {
+        switch (o.k) {
+            case O_V: return v[o.v][l];
+            case O_S: return s[o.v];
+            case O_IMM: return o.v;
+            case O_VCC: return (uint32_t)vcc;
+            default: return 0;
+        }
+    }
+    uint64_t mask(const Opnd& o) const {
+        switch (o.k) {
+            case O_VCC: return vcc;
+            case O_S: return (uint64_t)s[o.v] | ((uint64_t)s[o.v + 1] << 32);
+            case O_IMM: return (uint64_t)(int64_t)(int32_t)o.v;
+            case O_EXEC: return ~0ull;
+            default: return 0;
+        }
+    }
+    void set_mask(const Opnd& o, uint64_t m) {
+        if (o.k == O_VCC) vcc = m;
+        else if (o.k == O_S) { s[o.v] = (uint32_t)m; s[o.v + 1] = (uint32_t)(m >> 32); }
+    }
+    uint64_t r64(const Opnd& o, int l) const {
+        if (o.k == O_V) return (uint64_t)v[o.v][l] | ((uint64_t)v[o.v + 1][l] << 32);
+        if (o.k == O_S) return (uint64_t)s[o.v] | ((uint64_t)s[o.v + 1] << 32);
+        if (o.k == O_IMM) return (uint64_t)(int64_t)(int32_t)o.v;
+        return 0;
+    }
+    double f64(const Opnd& o, int l) const {
+        double d;
+        if (o.k == O_FONE) d = 1.0;
+        else {
+            const uint64_t b = r64(o, l);
+            memcpy(&d, &b, 8);
+        }
+        return o.neg ? -d : d;
+    }
+    void wf64(const Opnd& o, int l, double d) {
+        uint64_t b;
+        memcpy(&b, &d, 8);
+        v[o.v][l] = (uint32_t)b;
+        v[o.v + 1][l] = (uint32_t)(b >> 32);
+    }
+};
+
+struct Err {
+    std::string m;
+};
+
+void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int depth = 0) {
+    std::unordered_map<uint32_t, size_t> lab;
+    for (size_t i = 0; i < code.size(); ++i)
+        if (code[i].op == M_LABEL) lab[code[i].o[0].v] = i;
+    size_t pc = 0, steps = 0;
+    while (pc < code.size()) {
+        if (++steps > 10000000) throw Err{"emulator: runaway"};
+        const MI& m = code[pc++];
+        const Opnd* o = m.o;
+        auto each = [&](auto f) { for (int l = 0; l < 64; ++l) f(l); };
+        auto carry_op = [&](auto f) {  // d = f(l, &carry); sdst = o[1]
+            uint64_t cm = 0;
+            uint32_t res[64];
+            for (int l = 0; l < 64; ++l) {
+                bool c = false;
+                res[l] = f(l, &c);
+                if (c) cm |= 1ull << l;
+            }
+            for (int l = 0; l < 64; ++l) w.v[o[0].v][l] = res[l];
+            w.set_mask(o[1], cm);
+        };
+        auto bit = [&](const Opnd& mo, int l) { return (w.mask(mo) >> l) & 1ull; };
+        switch (m.op) {
+            case M_V_MOV: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l); }); break;
+            case M_V_ADD_U32: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) + w.r32(o[2], l); }); break;
+            case M_V_SUB_U32: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) - w.r32(o[2], l); }); break;
+            case M_V_SUBREV_U32: each([&](int l) { w.v[o[0].v][l] = w.r32(o[2], l) - w.r32(o[1], l); }); break;
+            case M_V_ADD_CO:
+                carry_op([&](int l, bool* c) {
+                    const uint64_t r = (uint64_t)w.r32(o[2], l) + w.r32(o[3], l);
+                    *c = r >> 32;
+                    return (uint32_t)r;
+                });
+                break;
+            case M_V_ADDC_CO: {
+                const uint64_t cin = w.mask(o[4]);
+                carry_op([&](int l, bool* c) {
+                    const uint64_t r = (uint64_t)w.r32(o[2], l) + w.r32(o[3], l) + ((cin >> l) & 1);
+                    *c = r >> 32;
+                    return (uint32_t)r;
+                });
+                break;
+            }
+            case M_V_SUB_CO: case M_V_SUBREV_CO: {
+                const bool rev = m.op == M_V_SUBREV_CO;
+                carry_op([&](int l, bool* c) {
+                    const uint64_t a = w.r32(o[rev ? 3 : 2], l), b = w.r32(o[rev ? 2 : 3], l);
+                    *c = a < b;
+                    return (uint32_t)(a - b);
+                });
+                break;
+            }
+            case M_V_SUBB_CO: case M_V_SUBBREV_CO: {
+                const bool rev = m.op == M_V_SUBBREV_CO;
+                const uint64_t bin = w.mask(o[4]);
+                carry_op([&](int l, bool* c) {
+                    const uint64_t a = w.r32(o[rev ? 3 : 2], l), b = w.r32(o[rev ? 2 : 3], l);
+                    const uint64_t bb = b + ((bin >> l) & 1);
+                    *c = a < bb;
+                    return (uint32_t)(a - bb);
+                });
+                break;
+            }
+            case M_V_AND: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) & w.r32(o[2], l); }); break;
+            case M_V_OR: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) | w.r32(o[2], l); }); break;
+            case M_V_XOR: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) ^ w.r32(o[2], l); }); break;
+            case M_V_NOT: each([&](int l) { w.v[o[0].v][l] = ~w.r32(o[1], l); }); break;
+            case M_V_OR3:
+                each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) | w.r32(o[2], l) | w.r32(o[3], l); });
+                break;
+            case M_V_ALIGNBIT:
+                each([&](int l) {
+                    const uint64_t x = ((uint64_t)w.r32(o[1], l) << 32) | w.r32(o[2], l);
+                    w.v[o[0].v][l] = (uint32_t)(x >> (w.r32(o[3], l) & 31));
+                });
+                break;
+            case M_V_LSHLREV: each([&](int l) { w.v[o[0].v][l] = w.r32(o[2], l) << (w.r32(o[1], l) & 31); }); break;
+            case M_V_LSHRREV: each([&](int l) { w.v[o[0].v][l] = w.r32(o[2], l) >> (w.r32(o[1], l) & 31); }); break;
+            case M_V_ASHRREV:
+                each([&](int l) { w.v[o[0].v][l] = (uint32_t)((int32_t)w.r32(o[2], l) >> (w.r32(o[1], l) & 31)); });
+                break;
+            case M_V_CNDMASK: {
+                uint32_t res[64];
+                for (int l = 0; l < 64; ++l) res[l] = bit(o[3], l) ? w.r32(o[2], l) : w.r32(o[1], l);
+                for (int l = 0; l < 64; ++l) w.v[o[0].v][l] = res[l];
+                break;
+            }
+            case M_V_CMP_EQ: case M_V_CMP_NE: case M_V_CMP_LT: case M_V_CMP_LE: case M_V_CMP_GT:
+            case M_V_CMP_GE: {
+                uint64_t cm = 0;
+                for (int l = 0; l < 64; ++l) {
+                    const uint32_t a = w.r32(o[1], l), b = w.r32(o[2], l);
+                    bool r = false;
+                    switch (m.op) {
+                        case M_V_CMP_EQ: r = a == b; break;
+                        case M_V_CMP_NE: r = a != b; break;
+                        case M_V_CMP_LT: r = a < b; break;
+                        case M_V_CMP_LE: r = a <= b; break;
+                        case M_V_CMP_GT: r = a > b; break;
+                        default: r = a >= b; break;
+                    }
+                    if (r) cm |= 1ull << l;
+                }
+                w.set_mask(o[0], cm);
+                break;
+            }
+            case M_V_MAD_U64_U32: {
+                uint64_t cm = 0;
+                uint64_t res[64];
+                for (int l = 0; l < 64; ++l) {
+                    const unsigned __int128 r = (unsigned __int128)((uint64_t)w.r32(o[2], l) * w.r32(o[3], l)) +
+                                                w.r64(o[4], l);
+                    res[l] = (uint64_t)r;
+                    if (r >> 64) cm |= 1ull << l;
+                }
+                for (int l = 0; l < 64; ++l) {
+                    w.v[o[0].v][l] = (uint32_t)res[l];
+                    w.v[o[0].v + 1][l] = (uint32_t)(res[l] >> 32);
+                }
+                w.set_mask(o[1], cm);
+                break;
+            }
+            case M_V_CVT_F64_U32: each([&](int l) { w.wf64(o[0], l, (double)w.r32(o[1], l)); }); break;
+            case M_V_FMA_F64:
+                each([&](int l) { w.wf64(o[0], l, fma(w.f64(o[1], l), w.f64(o[2], l), w.f64(o[3], l))); });
+                break;
+            case M_V_RCP_F64: each([&](int l) { w.wf64(o[0], l, 1.0 / w.f64(o[1], l)); }); break;
+            case M_V_MUL_F64: each([&](int l) { w.wf64(o[0], l, w.f64(o[1], l) * w.f64(o[2], l)); }); break;
+            case M_V_MIN_F64: each([&](int l) { w.wf64(o[0], l, fmin(w.f64(o[1], l), w.f64(o[2], l))); }); break;
+            case M_V_CVT_U32_F64:
+                each([&](int l) {
+                    const double d = w.f64(o[1], l);
+                    uint32_t r;
+                    if (isnan(d) || d <= 0) r = 0;
+                    else if (d >= 4294967295.0) r = 0xFFFFFFFFu;
+                    else r = (uint32_t)d;
+                    w.v[o[0].v][l] = r;
+                });
+                break;
+            case M_V_CMP_LE_F64: {
+                uint64_t cm = 0;
+                for (int l = 0; l < 64; ++l)
+                    if (w.f64(o[1], l) <= w.f64(o[2], l)) cm |= 1ull << l;
+                w.set_mask(o[0], cm);
+                break;
+            }
+            case M_S_MOV_B32: w.s[o[0].v] = w.r32(o[1], 0); break;
+            case M_S_MOV_B64: w.set_mask(o[0], w.mask(o[1])); break;
+            case M_S_AND_B64: case M_S_OR_B64: case M_S_XOR_B64: case M_S_XNOR_B64:
+            case M_S_ANDN2_B64: {
+                const uint64_t a = w.mask(o[1]), b = w.mask(o[2]);
+                uint64_t r = m.op == M_S_AND_B64 ? a & b : m.op == M_S_OR_B64 ? a | b :
+                             m.op == M_S_XOR_B64 ? a ^ b : m.op == M_S_XNOR_B64 ? ~(a ^ b) : a & ~b;
+                w.set_mask(o[0], r);
+                w.scc = r != 0;
+                break;
+            }
+            case M_S_NOT_B64: {
+                const uint64_t r = ~w.mask(o[1]);
+                w.set_mask(o[0], r);
+                w.scc = r != 0;
+                break;
+            }
+            case M_S_CMP_EQ_U64: w.scc = w.mask(o[0]) == w.mask(o[1]); break;
+            case M_S_CMP_LG_U64: w.scc = w.mask(o[0]) != w.mask(o[1]); break;
+            case M_S_CMP_EQ_U32: w.scc = w.r32(o[0], 0) == w.r32(o[1], 0); break;
+            case M_S_CMP_LT_U32: w.scc = w.r32(o[0], 0) < w.r32(o[1], 0); break;
+            case M_S_CBRANCH_SCC0: case M_S_CBRANCH_SCC1: case M_S_BRANCH: {
+                const bool take = m.op == M_S_BRANCH || (m.op == M_S_CBRANCH_SCC1) == w.scc;
+                if (take) {
+                    auto it = lab.find(o[0].v);
+                    if (it == lab.end()) throw Err{"emulator: missing label"};
+                    pc = it->second;
+                }
+                break;
+            }
+            case M_LABEL: case M_S_NOP: break;
+            case M_CALL_DIV:
+                if (depth) throw Err{"emulator: nested call"};
+                run(w, div, div, depth + 1);
+                break;
+            case M_RET: return;
+            default: throw Err{"emulator: unknown op " + std::to_string(m.op)};
+        }
+    }
+}
+
+bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
+                    const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, uint32_t tape,
+                    uint32_t max_vgpr, std::vector<uint32_t>& pool, TapeCode& tc, std::string& e) {
+    std::unordered_map<std::string, uint32_t> index;
+    SsaTape st;
+    std::string err;
+    if (tape >= n_tapes) { e = "tape index"; return false; }
+    if (lower_tape_ssa(nodes + offs[tape], (size_t)(offs[tape + 1] - offs[tape]), consts,
+                       n_consts, n_vars, pool, index, st, err) != MH_OK) {
+        e = "lowering: " + err;
+        return false;
+    }
+    Options opt;
+    opt.max_vgpr = max_vgpr;
+    tc = emit_tape(st, pool, n_vars, opt);
+    return true;
+}
+
+}  // namespace
+
+// info[0] = 1 if jitted, [1] max_vgpr, [2] n_valu, [3] n_valu_wide, [4] n_salu, [5] calls_div,
+// [6] root_bool, [7] code bytes.  Returns 0 (evaluated or not jittable: see info[0] / err),
+// < 0 on an emulator / lowering error.
+extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
+                                const uint32_t* consts, uint32_t n_consts, uint32_t n_vars,
+                                uint32_t tape, const uint32_t* assign, uint64_t rows,
+                                uint32_t* out, uint32_t max_vgpr, uint32_t* info, char* err,
+                                int errlen) {
+    std::vector<uint32_t> pool;
+    TapeCode tc;
+    std::string e;
+    if (!lower_and_emit(nodes, offs, n_tapes, consts, n_consts, n_vars, tape, max_vgpr, pool, tc,
+                        e)) {
+        snprintf(err, errlen, "%s", e.c_str());
+        return -1;
+    }
+    info[0] = tc.ok;
+    info[1] = tc.max_vgpr;
+    info[2] = tc.n_valu;
+    info[3] = tc.n_valu_wide;
+    info[4] = tc.n_salu;
+    info[5] = tc.calls_div;
+    info[6] = tc.root_bool;
+    info[7] = code_bytes(tc);
+    if (!tc.ok) {
+        snprintf(err, errlen, "%s", tc.why.c_str());
+        return 0;
+    }
+    static const std::vector<MI> div = div_routine();
+    static Wave w;
+    try {
+        for (uint64_t base = 0; base < rows; base += 64) {
+            for (int r = 0; r < 512; ++r)
+                for (int l = 0; l < 64; ++l) w.v[r][l] = 0xDEAD0000u + (uint32_t)r;
+            for (int r = 0; r < 128; ++r) w.s[r] = 0xBEEF0000u + (uint32_t)r;
+            w.vcc = 0x5555AAAA5555AAAAull;
+            for (uint32_t c = 0; c < n_vars; ++c)
+                for (int k = 0; k < 8; ++k)
+                    for (int l = 0; l < 64; ++l) {
+                        const uint64_t row = base + (uint64_t)l < rows ? base + (uint64_t)l : 0;
+                        w.v[R_COL0 + 8 * c + k][l] = assign[((uint64_t)c * 8 + k) * rows + row];
+                    }
+            run(w, tc.code, div);
+            const uint64_t res = (uint64_t)w.s[S_RES] | ((uint64_t)w.s[S_RES + 1] << 32);
+            for (int l = 0; l < 64 && base + (uint64_t)l < rows; ++l) {
+                const uint64_t row = base + (uint64_t)l;
+                for (int k = 0; k < 8; ++k) {
+                    uint32_t x;
+                    if (tc.root_bool) x = k == 0 ? (uint32_t)((res >> l) & 1) : 0u;
+                    else x = tc.root_limbs[k] != ~0u ? w.v[tc.root_limbs[k]][l] : tc.root_const[k];
+                    out[(uint64_t)k * rows + row] = x;
+                }
+            }
+        }
+    } catch (const Err& x) {
+        snprintf(err, errlen, "%s", x.m.c_str());
+        return -2;
+    }
+    return 0;
+}
+
+// The module source of a whole tape set (values / count mode); assemble != 0 also runs comgr.
+// Returns the text length (and the code object size in *hsaco_size), < 0 on error.
+extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
+                                  const uint32_t* consts, uint32_t n_consts, uint32_t n_vars,
+                                  uint32_t values, uint32_t max_vgpr, int32_t assemble_it,
+                                  char* text, uint64_t cap, uint64_t* hsaco_size,
+                                  uint32_t* n_jitted, char* err, int errlen) {
+    std::vector<uint32_t> pool;
+    std::unordered_map<std::string, uint32_t> index;
+    std::vector<TapeCode> codes(n_tapes);
+    std::vector<const TapeCode*> ok;
+    std::vector<uint32_t> ids;
+    Options opt;
+    opt.max_vgpr = max_vgpr;
+    for (uint32_t t = 0; t < n_tapes; ++t) {
+        SsaTape st;
+        std::string e;
+        if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts, n_consts,
+                           n_vars, pool, index, st, e) != MH_OK)
+            continue;
+        codes[t] = emit_tape(st, pool, n_vars, opt);
+        if (codes[t].ok) {
+            ok.push_back(&codes[t]);
+            ids.push_back(t);
+        }
+    }
+    *n_jitted = (uint32_t)ok.size();
+    Module m = build_module(ok, ids, n_vars, values != 0);
+    if (text && cap) {
+        const size_t n = std::min<size_t>(cap - 1, m.text.size());
+        memcpy(text, m.text.data(), n);
+        text[n] = 0;
+    }
+    *hsaco_size = 0;
+    if (assemble_it) {
+        std::vector<char> bin;
+        std::string log;
+        if (!assemble(m.text, bin, log)) {
+            snprintf(err, errlen, "%s", log.substr(0, (size_t)errlen - 1).c_str());
+            return -1;
+        }
+        *hsaco_size = bin.size();
+    }
+    return (int64_t)m.text.size();
+}

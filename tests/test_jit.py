@@ -1,0 +1,191 @@
+"""The native-code JIT (mythril_amd/csrc/jit.cpp), checked on the host: the machine code it
+emits for a tape runs on the test-only wave emulator (tests/native/jit_emu.cpp) and must give
+the oracle's value on every row, bit for bit; whole tape sets assemble with comgr.  The GPU runs
+the same code in tests/test_gpu_jit.py."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from mythril_amd import synth
+from mythril_amd.tape import Op, TapeSet
+from oracle import smt_eval
+from tests.emu import jit_eval, jit_module
+from tests.evm_translate import Unsupported, lift_constants, vmtest_tapes
+from tests.fuzz import TapeFuzzer, assignment_soa, soa_row
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+VMTESTS = json.load(open(os.path.join(HERE, "golden", "vmtests.json")))
+EIP145 = json.load(open(os.path.join(HERE, "golden", "eip145.json")))
+
+
+def soa_of(rows_vals, n_vars):
+    soa = np.zeros((n_vars, 8, len(rows_vals)), dtype=np.uint32)
+    for r, vals in enumerate(rows_vals):
+        for v in range(n_vars):
+            for k in range(8):
+                soa[v, k, r] = (vals[v] >> (32 * k)) & 0xFFFFFFFF
+    return soa
+
+
+def check_tapes(emu, ts, soa, require_all=True, max_vgpr=128):
+    jitted = 0
+    for i, t in enumerate(ts.tapes):
+        res = jit_eval(emu, ts, i, soa, max_vgpr)
+        if not res.ok:
+            assert not require_all, (i, res.why)
+            continue
+        jitted += 1
+        for r in range(soa.shape[2]):
+            want = int(smt_eval.evaluate(t.nodes, ts.pool.values, soa_row(soa, r)))
+            assert res.values[r] == want, (i, r, hex(res.values[r]), hex(want))
+    return jitted
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_tapes_jit(emu, seed):
+    """Random tapes over every op the JIT covers, narrow and wide, Bool and bit-vector roots."""
+    rng = random.Random(9000 + seed)
+    ts = TapeSet()
+    fz = TapeFuzzer(rng, ts, n_vars=3, max_depth=4, allow_keccak=False)
+    for _ in range(24):
+        fz.tape()
+    soa = assignment_soa(rng, ts.n_vars, 70)
+    n = check_tapes(emu, ts, soa, require_all=False)
+    assert n >= 12
+
+
+def test_synthetic_tapes_jit(emu):
+    """Config-5 tapes (the bench's), every one through the JIT, on generated rows."""
+    ts = synth.generate(60)
+    seed = synth.load_spec()["assignment_seed"]
+    rows = [smt_eval.gen_assignment(seed, ts.n_vars, r) for r in range(100)]
+    # plus edge rows: zeros, ones, all-ones, sign bits
+    rows += [[0] * 4, [1] * 4, [(1 << 256) - 1] * 4, [1 << 255] * 4, [(1 << 255) - 1, 0, 1, 2]]
+    n = check_tapes(emu, ts, soa_of(rows, ts.n_vars), require_all=False)
+    assert n >= 55
+
+
+def test_division_edges_jit(emu):
+    rng = random.Random(8)
+    for w in (8, 64, 160, 255, 256):
+        ts = TapeSet()
+        b = ts.builder()
+        x = b.op(Op.EXTRACT, b.var("x"), imm0=w - 1, imm1=0) if w < 256 else b.var("x")
+        y = b.op(Op.EXTRACT, b.var("y"), imm0=w - 1, imm1=0) if w < 256 else b.var("y")
+        for op in (Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD):
+            ts.add(b.finish(b.op(op, x, y)))
+            ts.add(b.finish(b.op(op, x, b.const(rng.getrandbits(w) | 1, w))))
+        m = (1 << w) - 1
+        vals = [0, 1, 2, 3, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1]
+        vals += [rng.getrandbits(w) for _ in range(6)] + [rng.getrandbits(min(w, 40))
+                                                          for _ in range(6)]
+        pairs = [(p, q) for p in vals for q in vals]
+        check_tapes(emu, ts, soa_of(pairs, 2))
+
+
+def test_immediate_and_variable_shifts_jit(emu):
+    rng = random.Random(31)
+    ts = TapeSet()
+    b = ts.builder()
+    x, y = b.var("x"), b.var("y")
+    s_sum = b.op(Op.BVADD, x, y)
+    for s in list(range(1, 256, 7)) + [32, 64, 96, 128, 224, 255]:
+        k = b.const(s, 256)
+        for op in (Op.BVSHL, Op.BVLSHR, Op.BVASHR):
+            ts.add(b.finish(b.op(op, x, k)))
+            ts.add(b.finish(b.op(op, s_sum, k)))
+    for op in (Op.BVSHL, Op.BVLSHR, Op.BVASHR):
+        ts.add(b.finish(b.op(op, x, y)))
+        ts.add(b.finish(b.op(op, x, b.op(Op.BVAND, y, b.const(0x1FF, 256)))))
+    vals = [0, 1, (1 << 256) - 1, 1 << 255, (1 << 255) - 1] + [rng.getrandbits(256)
+                                                               for _ in range(20)]
+    amts = [0, 1, 31, 32, 33, 255, 256, 257, 1 << 200] + [rng.getrandbits(9) for _ in range(16)]
+    rows = [[v, amts[(i * 7 + 3) % len(amts)]] for i, v in enumerate(vals * 2)]
+    check_tapes(emu, ts, soa_of(rows, 2))
+
+
+def test_mul_shapes_jit(emu):
+    """Multiplication with constant / narrow operands (sparse product columns) and full 256."""
+    rng = random.Random(77)
+    ts = TapeSet()
+    b = ts.builder()
+    x, y = b.var("x"), b.var("y")
+    consts = [1, 2, 0xFFFFFFFF, 1 << 32, (1 << 64) - 1, 1 << 255, (1 << 256) - 1,
+              0xDEADBEEF << 96, rng.getrandbits(256)]
+    for c in consts:
+        ts.add(b.finish(b.op(Op.BVMUL, x, b.const(c, 256))))
+    ts.add(b.finish(b.op(Op.BVMUL, x, y)))
+    ts.add(b.finish(b.op(Op.BVMUL, x, x)))
+    for w in (8, 32, 160):
+        xe = b.op(Op.ZEXT, b.op(Op.EXTRACT, x, imm0=w - 1, imm1=0), imm0=256 - w)
+        ye = b.op(Op.ZEXT, b.op(Op.EXTRACT, y, imm0=w - 1, imm1=0), imm0=256 - w)
+        ts.add(b.finish(b.op(Op.BVMUL, xe, ye)))
+        ts.add(b.finish(b.op(Op.BVMUL, xe, y)))
+    vals = [0, 1, (1 << 256) - 1, 1 << 255] + [rng.getrandbits(256) for _ in range(20)]
+    rows = [[v, vals[(i * 5 + 1) % len(vals)]] for i, v in enumerate(vals)]
+    check_tapes(emu, ts, soa_of(rows, 2))
+
+
+@pytest.mark.parametrize("op", ["shl", "shr", "sar"])
+def test_eip145_jit(emu, op):
+    """EIP-145 vectors (reference tests/instructions/*_test.py) through the JIT's code."""
+    sop = {"shl": Op.BVSHL, "shr": Op.BVLSHR, "sar": Op.BVASHR}[op]
+    ts = TapeSet()
+    b = ts.builder()
+    ts.add(b.finish(b.op(sop, b.var("value"), b.var("shift"))))
+    rows = [[int(v["value"], 16), int(v["shift"], 16)] for v in EIP145[op]]
+    res = jit_eval(emu, ts, 0, soa_of(rows, 2))
+    assert res.ok
+    assert res.values == [int(v["expected"], 16) for v in EIP145[op]]
+
+
+def test_vmtests_lifted_jit(emu):
+    """The reference's VMTests known answers with every constant lifted into a column: each op
+    of each vector runs as JIT code (vectors with > 4 columns or 512-bit arithmetic excepted)."""
+    checked = 0
+    for vec in VMTESTS:
+        try:
+            ts, pairs, expected, pre = vmtest_tapes(vec, "laser")
+        except Unsupported:
+            continue
+        lts, soa = lift_constants(ts)
+        if lts.n_vars > 4:
+            continue
+        for i, t in enumerate(ts.tapes):
+            res = jit_eval(emu, lts, i, soa)
+            if not res.ok:
+                continue
+            want = int(smt_eval.evaluate(t.nodes, ts.pool.values, []))
+            assert res.values[0] == want, (vec["name"], i)
+            checked += 1
+    assert checked >= 100
+
+
+def test_module_assembles(emu):
+    """A tape set's whole code object (count and values kernels) assembles and links with comgr
+    for gfx950."""
+    ts = synth.generate(120)
+    for values in (False, True):
+        text, nbytes, nj = jit_module(emu, ts, values=values)
+        assert nj >= 110
+        assert nbytes > 1000
+        assert ".amdhsa_kernel mh_jit" in text
+
+
+def test_jit_coverage_and_static_cost(emu):
+    """How much of config 5 the JIT takes, and its static instruction counts (informational
+    bounds: every tape fits the 128-VGPR budget; far fewer VALU per op than the interpreter)."""
+    ts = synth.generate(200)
+    soa = np.zeros((4, 8, 1), dtype=np.uint32)
+    ok, valu, nodes = 0, 0, 0
+    for i, t in enumerate(ts.tapes):
+        r = jit_eval(emu, ts, i, soa)
+        if r.ok:
+            ok += 1
+            valu += r.n_valu
+            nodes += len(t.nodes)
+    assert ok >= 195, ok
+    print("jitted %d/200, %.1f static VALU per tape node" % (ok, valu / max(nodes, 1)))
