@@ -53,6 +53,9 @@ struct mh_tapeset {
         hipModule_t mod = nullptr, vmod = nullptr;
         hipFunction_t fn = nullptr, vfn = nullptr;
         uint32_t n_groups = 0;
+        // the code object images stay alive as long as the modules: the HIP runtime may read
+        // an image after hipModuleLoadData returns (lazy loading)
+        std::vector<char> image, vimage;
     };
     std::vector<JitMod> jit;
     std::vector<uint8_t> jitted;
@@ -661,6 +664,7 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
     }
     if (!ok) return set_err(MH_E_UNSUPPORTED, "JIT: " + err);
     std::vector<mh_tapeset::JitMod> mods;
+    mods.reserve(built.size());
     auto unload = [&]() {
         for (auto& j : mods) {
             if (j.mod) (void)hipModuleUnload(j.mod);
@@ -668,17 +672,19 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
         }
     };
     uint32_t maxv = 0;
-    for (const auto& b : built) {
+    for (auto& b : built) {
         if (b.hsaco.empty()) continue;
-        mh_tapeset::JitMod j;
+        mods.emplace_back();
+        mh_tapeset::JitMod& j = mods.back();
         j.n_groups = b.n_groups;
-        hipError_t e = hipModuleLoadData(&j.mod, b.hsaco.data());
+        j.image.swap(b.hsaco);
+        j.vimage.swap(b.hsaco_values);
+        hipError_t e = hipModuleLoadData(&j.mod, j.image.data());
         if (e == hipSuccess) e = hipModuleGetFunction(&j.fn, j.mod, "mh_jit");
-        if (e == hipSuccess && !b.hsaco_values.empty()) {
-            e = hipModuleLoadData(&j.vmod, b.hsaco_values.data());
+        if (e == hipSuccess && !j.vimage.empty()) {
+            e = hipModuleLoadData(&j.vmod, j.vimage.data());
             if (e == hipSuccess) e = hipModuleGetFunction(&j.vfn, j.vmod, "mh_jit");
         }
-        mods.push_back(j);
         if (e != hipSuccess) {
             unload();
             return set_err(MH_E_DEVICE, std::string("JIT module load: ") + hipGetErrorString(e));

@@ -1385,6 +1385,9 @@ Module build_module(const std::vector<const TapeCode*>& codes,
     line(o, "s_load_dwordx4 s[20:23], s[0:1], 0x40");
     line(o, "v_and_b32 v1, 63, v0");
     line(o, "v_lshrrev_b32 v2, 6, v0");
+    // a VALU write of a VGPR -> v_readfirstlane / v_readlane of it needs a wait state (CDNA3/4
+    // manually inserted wait states); without it the wave reads a stale wave index
+    line(o, "s_nop 1");
     line(o, "v_readfirstlane_b32 s24, v2");
     line(o, "s_waitcnt lgkmcnt(0)");
     line(o, "s_lshr_b32 s25, s19, 2");        // rows per wave

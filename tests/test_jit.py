@@ -189,3 +189,45 @@ def test_jit_coverage_and_static_cost(emu):
             nodes += len(t.nodes)
     assert ok >= 195, ok
     print("jitted %d/200, %.1f static VALU per tape node" % (ok, valu / max(nodes, 1)))
+
+
+def _hazards(text):
+    """Pairs of adjacent instructions in the module text that break a manually inserted wait
+    state of CDNA3/4 the JIT must honour: a VALU write of vN directly followed by
+    v_readlane / v_readfirstlane of vN; v_rcp_f64 directly followed by a use of its result;
+    a VALU write of an SGPR directly followed by a global_* instruction using that SGPR."""
+    import re
+    bad = []
+    prev = None
+    for ln in text.splitlines():
+        ln = ln.strip()
+        if not ln or ln.endswith(":") or ln.startswith("."):
+            continue
+        ins = ln.split()[0]
+        if prev is not None and not ins.startswith("s_nop"):
+            p_ins, p_ops = prev
+            dst = p_ops[0] if p_ops else ""
+            if ins in ("v_readlane_b32", "v_readfirstlane_b32") and p_ins.startswith("v_"):
+                src = ln.split()[2].rstrip(",")
+                if re.fullmatch(r"v\d+", dst) and dst == src:
+                    bad.append((prev, ln))
+            if p_ins == "v_rcp_f64":
+                bad.append((prev, ln))
+            if ins.startswith("global_") and p_ins.startswith("v_") and dst.startswith("s"):
+                if dst.split("[")[0] in ln or dst in ln:
+                    bad.append((prev, ln))
+        if ins.startswith("s_nop"):
+            prev = None
+        else:
+            ops = [x.strip(",") for x in ln.split()[1:]]
+            prev = (ins, ops)
+    return bad
+
+
+def test_module_wait_states(emu):
+    """The generated text honours the wait states above (the round-2 bring-up hit the first:
+    a stale wave index read by v_readfirstlane right after the VALU that wrote it)."""
+    ts = synth.generate(60)
+    for values in (False, True):
+        text, _, _ = jit_module(emu, ts, values=values, assemble=False)
+        assert _hazards(text) == []
