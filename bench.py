@@ -147,12 +147,14 @@ def main() -> None:
     except Exception as e:  # pragma: no cover
         log("microbench failed: %s" % e)
         peak_measured = None
-    traffic = valu_busy = None
+    traffic = valu_busy = exec_ops = None
     if os.path.exists(PMC_SUMMARY):
         pmc = json.load(open(PMC_SUMMARY))
-        if pmc.get("tapes") == n_tapes and pmc.get("rows_per_gpu") == rows:
+        if pmc.get("tapes") == n_tapes and pmc.get("rows_per_gpu") == rows and \
+                pmc.get("engine", "interp") == args.engine:
             traffic = pmc.get("hbm_bytes_per_launch")
             valu_busy = pmc.get("valu_busy")
+            exec_ops = pmc.get("exec_lane_ops_per_launch")
     line = {
         "metric": "constraint-evals/sec",
         "value": value,
@@ -192,6 +194,8 @@ def main() -> None:
             "traffic": traffic,
             "traffic_unit": "bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, profiles/)",
             "valu_busy_pmc": valu_busy,
+            "frac_exec": (exec_ops / (kms / 1e3) / 1e12 / NOMINAL_PEAK_TOPS) if exec_ops else None,
+            "exec_lane_ops_per_eval": (exec_ops / (n_tapes * rows)) if exec_ops else None,
             "peak_measured_add_chain": peak_measured,
             "alg_ops_per_eval": alg_ops_per_row / n_tapes,
         },

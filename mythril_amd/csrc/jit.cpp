@@ -84,6 +84,10 @@ private:
     uint32_t kstage_ = 0;
     uint32_t n_valu_ = 0, n_wide_ = 0, n_salu_ = 0;
     bool calls_div_ = false;
+    int cur_op_ = -1;  // SSA op being emitted (diagnostic attribution)
+public:
+    static uint64_t op_valu[256], op_wide[256], op_count[256];
+private:
 
     // ---- emission
     void emit(uint16_t op, std::initializer_list<Opnd> ops, bool e64 = false) {
@@ -98,8 +102,10 @@ private:
             const bool wide = e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
                               op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO ||
                               op == M_V_OR3 || op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 ||
+                              op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
                               (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) || op >= M_V_CVT_F64_U32;
             if (wide) ++n_wide_;
+            if (cur_op_ >= 0) { ++op_valu[cur_op_]; op_wide[cur_op_] += wide; }
         } else if (op <= M_S_CMP_LT_U32) {
             ++n_salu_;
         }
@@ -235,6 +241,7 @@ private:
     void op_addsub(int d, const Val& A, const Val& B, bool sub);
     void op_logic(int d, const Val& A, const Val& B, int kind);
     Val op_eq(const Val& A, const Val& B);
+    void and_all_zero(const std::vector<uint32_t>& regs, int* p, std::vector<uint32_t>& tmp);
     Val op_ult(const Val& A, const Val& B, bool signed_, bool negate);
     void op_ite(int d, const Val& C, const Val& T, const Val& E);
     Val op_bite(const Val& C, const Val& T, const Val& E);
@@ -243,7 +250,8 @@ private:
     void op_shl(int d, const Val& A, uint32_t s);
     void op_vshift(int d, const Val& A, const Val& B, uint8_t op);
     void op_mul(int d, const Val& A, const Val& B);
-    void op_div(int d, const Val& A, const Val& B, uint32_t kind);
+    void op_div(int d, int a, int b, int cidx, uint32_t kind, int cur);
+    void rescue_div_regs(int cur);
     void demand();
     Val& out(int d) {
         Val& v = vals_[d];
@@ -376,8 +384,29 @@ void Emitter::op_logic(int d, const Val& A, const Val& B, int kind) {
     }
 }
 
+// a lane mask "all of these VGPR limbs are zero" folded into the pair *p (allocated on first
+// use): v_or (2-cycle) reduction, one compare
+void Emitter::and_all_zero(const std::vector<uint32_t>& regs, int* p, std::vector<uint32_t>& tmp) {
+    if (regs.empty()) return;
+    uint32_t acc = regs[0];
+    if (regs.size() > 1) {
+        acc = valloc();
+        tmp.push_back(acc);
+        emit(M_V_OR, {V(acc), V(regs[0]), V(regs[1])});
+        for (size_t i = 2; i < regs.size(); ++i) emit(M_V_OR, {V(acc), V(regs[i]), V(acc)});
+    }
+    emit(M_V_CMP_EQ, {VCC(), IMM(0), V(acc)});
+    if (*p < 0) {
+        *p = palloc();
+        emit(M_S_MOV_B64, {P(*p), VCC()});
+    } else {
+        emit(M_S_AND_B64, {P(*p), P(*p), VCC()});
+    }
+}
+
 Val Emitter::op_eq(const Val& A, const Val& B) {
     int p = -1;
+    std::vector<uint32_t> zero_regs, tmp;  // VGPR limbs compared against a known zero
     for (int k = 0; k < 8; ++k) {
         Limb x = A.l[k], y = B.l[k];
         if (x.is_c() && y.is_c()) {
@@ -389,6 +418,10 @@ Val Emitter::op_eq(const Val& A, const Val& B) {
         }
         if (x.is_r() && y.is_r() && x.v == y.v) continue;
         if (!y.is_r()) std::swap(x, y);
+        if (x.is_c(0)) {
+            zero_regs.push_back(y.v);
+            continue;
+        }
         emit(M_V_CMP_EQ, {VCC(), src(x), V(y.v)});
         if (p < 0) {
             p = palloc();
@@ -397,11 +430,17 @@ Val Emitter::op_eq(const Val& A, const Val& B) {
             emit(M_S_AND_B64, {P(p), P(p), VCC()});
         }
     }
+    and_all_zero(zero_regs, &p, tmp);
+    free_tmp(tmp);
     if (p < 0) return bool_const(true);
     return bool_mask(p);
 }
 
-// A < B (unsigned, or signed 256-bit), optionally negated (>=)
+// A < B (unsigned, or signed 256-bit), optionally negated (>=).  Limbs where both sides are
+// equal constants at the top do not take part; a run of top limbs known zero on one side only
+// is an OR-reduction of the other side's limbs plus the compare of the limbs below:
+//   A < B  =  A[hi] == 0 && A[lo] < B[lo]   (B zero in hi)
+//          =  B[hi] != 0 || A[lo] < B[lo]   (A zero in hi)
 Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
     std::vector<uint32_t> tmp;
     Limb a[8], b[8];
@@ -419,14 +458,62 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
         }
     }
     int top = 7;
-    while (top > 0 && a[top].is_c(0) && b[top].is_c(0)) --top;
+    while (top > 0 && a[top].is_c() && b[top].is_c() && a[top].v == b[top].v) --top;
+    // top run where exactly one side is known zero
+    int hi_side = 0;  // 1: b zero on [m+1, top], 2: a zero there
+    int m = top;
+    if (b[top].is_c(0) && !a[top].is_c()) {
+        hi_side = 1;
+        while (m > 0 && b[m].is_c(0)) --m;
+    } else if (a[top].is_c(0) && !b[top].is_c()) {
+        hi_side = 2;
+        while (m > 0 && a[m].is_c(0)) --m;
+    }
+    if (hi_side && m == top) hi_side = 0;
+    int p = -1;  // the high-run mask (A[hi] == 0 / B[hi] == 0)
+    if (hi_side) {
+        std::vector<uint32_t> regs;
+        const Limb* o = hi_side == 1 ? a : b;  // the side that is not zero there
+        for (int k = m + 1; k <= top; ++k) {
+            if (o[k].is_c()) {
+                if (o[k].v) {  // decided by a known nonzero limb
+                    free_tmp(tmp);
+                    if (p >= 0) --pref_[p];
+                    return bool_const((hi_side == 2) != negate);
+                }
+                continue;
+            }
+            regs.push_back(o[k].v);
+        }
+        and_all_zero(regs, &p, tmp);
+    }
     const uint32_t junk = valloc();
     tmp.push_back(junk);
-    const int cs = chain(true, a, b, top, nullptr, junk, tmp);
+    const int cs = chain(true, a, b, m, nullptr, junk, tmp);
     free_tmp(tmp);
-    if (cs != 2) return bool_const((cs == 1) != negate);
-    const int p = palloc();
-    emit(negate ? M_S_NOT_B64 : M_S_MOV_B64, {P(p), VCC()});
+    // combine: lo = borrow (A[lo] < B[lo]); result = hi_side 1: p && lo; 2: !p || lo
+    if (p < 0) {
+        if (cs != 2) return bool_const((cs == 1) != negate);
+        const int q = palloc();
+        emit(negate ? M_S_NOT_B64 : M_S_MOV_B64, {P(q), VCC()});
+        return bool_mask(q);
+    }
+    // p holds "the other side's high run is zero"
+    if (cs != 2) {
+        const bool lo = cs == 1;
+        if (hi_side == 1) {  // p && lo
+            if (!lo) { --pref_[p]; return bool_const(negate); }
+            if (negate) emit(M_S_NOT_B64, {P(p), P(p)});
+            return bool_mask(p);
+        }
+        // !p || lo
+        if (lo) { --pref_[p]; return bool_const(!negate); }
+        if (!negate) emit(M_S_NOT_B64, {P(p), P(p)});
+        return bool_mask(p);
+    }
+    if (hi_side == 1) emit(M_S_AND_B64, {P(p), P(p), VCC()});
+    else emit(M_S_ORN2_B64, {P(p), VCC(), P(p)});  // lo || !p
+    if (negate) emit(M_S_NOT_B64, {P(p), P(p)});
     return bool_mask(p);
 }
 
@@ -620,31 +707,44 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
     tmp.push_back(qv); tmp.push_back(rv); tmp.push_back(tv);
     emit(M_V_LSHRREV, {V(qv), IMM(5), V(y0)});
     emit(M_V_AND, {V(rv), IMM(31), V(y0)});
+    // the network's first stage reads the operand's limbs (VGPRs or inline constants) and
+    // writes fresh registers t[k]; later stages update t in place
+    Opnd cur[8];
+    for (int k = 0; k < 8; ++k) cur[k] = vi_of(A.l[k], tmp);
     uint32_t t[8];
     for (int k = 0; k < 8; ++k) {
         t[k] = valloc();
         tmp.push_back(t[k]);
-        emit(M_V_MOV, {V(t[k]), src(A.l[k])});
     }
     Opnd fill = IMM(0);
     if (arith) {
         const uint32_t f = valloc();
         tmp.push_back(f);
-        emit(M_V_ASHRREV, {V(f), IMM(31), V(t[7])});
+        if (cur[7].k == O_V) emit(M_V_ASHRREV, {V(f), IMM(31), cur[7]});
+        else emit(M_V_MOV, {V(f), IMM((cur[7].v >> 31) ? ~0u : 0u)});
         fill = V(f);
     }
+    // lane masks go to an SGPR pair for the e64 v_cndmask: the e32 form with its implicit VCC
+    // mask issues at ~23 cycles on gfx950 (profiles/r02e/valu_peak.json), the e64 form at ~4.6
+    const int sel = palloc();
+    tp.push_back(sel);
     for (uint32_t st : {4u, 2u, 1u}) {
         emit(M_V_AND, {V(tv), IMM(st), V(qv)});
         emit(M_V_CMP_NE, {VCC(), IMM(0), V(tv)});
+        emit(M_S_MOV_B64, {P(sel), VCC()});
+        const bool first = st == 4;
+        auto in = [&](int k) { return first ? cur[k] : V(t[k]); };
         if (right) {
             for (int k = 0; k < 8; ++k) {
-                const Opnd s2 = k + (int)st < 8 ? V(t[k + st]) : fill;
-                emit(M_V_CNDMASK, {V(t[k]), V(t[k]), s2, VCC()}, s2.k != O_V);
+                const Opnd s2 = k + (int)st < 8 ? in(k + (int)st) : fill;
+                const Opnd s1 = in(k);
+                emit(M_V_CNDMASK, {V(t[k]), s1, s2, P(sel)}, true);
             }
         } else {
             for (int k = 7; k >= 0; --k) {
-                const Opnd s2 = k - (int)st >= 0 ? V(t[k - st]) : IMM(0);
-                emit(M_V_CNDMASK, {V(t[k]), V(t[k]), s2, VCC()}, s2.k != O_V);
+                const Opnd s2 = k - (int)st >= 0 ? in(k - (int)st) : IMM(0);
+                const Opnd s1 = in(k);
+                emit(M_V_CNDMASK, {V(t[k]), s1, s2, P(sel)}, true);
             }
         }
     }
@@ -657,9 +757,10 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
     } else {
         emit(M_V_SUB_U32, {V(tv), IMM(32), V(rv)});
         emit(M_V_CMP_EQ, {VCC(), IMM(0), V(rv)});
+        emit(M_S_MOV_B64, {P(sel), VCC()});
         for (int k = 0; k < 8; ++k) {
             emit(M_V_ALIGNBIT, {V(o[k]), V(t[k]), k > 0 ? V(t[k - 1]) : IMM(0), V(tv)});
-            emit(M_V_CNDMASK, {V(o[k]), V(o[k]), V(t[k]), VCC()});
+            emit(M_V_CNDMASK, {V(o[k]), V(o[k]), V(t[k]), P(sel)}, true);
         }
     }
     for (int k = 0; k < 8; ++k) {
@@ -752,20 +853,51 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
     free_tmp(tmp);
 }
 
-void Emitter::op_div(int d, const Val& A, const Val& B, uint32_t kind) {
+// The result stays where the subroutine leaves it (the quotient / signed remainders in DQ, the
+// unsigned remainder in DR) until the next call: limbs of live values that sit in the
+// subroutine's registers are moved out just before it (rescue_div_regs).
+void Emitter::rescue_div_regs(int cur) {
+    std::vector<std::pair<uint32_t, uint32_t>> moved;  // (div register, new register)
+    for (size_t r = 0; r < vals_.size(); ++r) {
+        Val& v = vals_[r];
+        if (!v.defined || v.is_bool || last_[r] <= cur) continue;
+        for (Limb& l : v.l) {
+            if (!l.is_r() || l.v < R_DIV0 || l.v >= R_TEMP0) continue;
+            uint32_t nr = ~0u;
+            for (auto& m : moved)
+                if (m.first == l.v) nr = m.second;
+            if (nr == ~0u) {
+                nr = valloc();
+                emit(M_V_MOV, {V(nr), V(l.v)});
+                moved.push_back({l.v, nr});
+            } else {
+                vretain(nr);
+            }
+            l.v = nr;
+        }
+    }
+}
+
+void Emitter::op_div(int d, int a, int b, int cidx, uint32_t kind, int cur) {
     calls_div_ = true;
-    for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DR + k), src(A.l[k])});
+    // values still live after this call move out of the subroutine's registers first; then y
+    // before x, so an operand sitting in R (a previous remainder read for the last time here)
+    // is read before R is overwritten
+    rescue_div_regs(cur);
+    const Val& A = val(a);
+    const Val B = cidx >= 0 ? const_val(cidx) : val(b);
+    // bvsdiv / bvsrem / bvsmod of operands whose sign bits are known clear are bvudiv / bvurem
+    // (every SMT-LIB sign rule reduces to the unsigned form for non-negative x and y)
+    if (kind >= 2 && A.l[7].is_c() && !(A.l[7].v >> 31) && B.l[7].is_c() && !(B.l[7].v >> 31))
+        kind = kind == 2 ? 0u : 1u;
     for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DY + k), src(B.l[k])});
+    for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DR + k), src(A.l[k])});
     emit(M_S_MOV_B32, {S(S_DIV_KIND), IMM(kind)});
     emit(M_CALL_DIV, {IMM((uint32_t)code_.size())});
     Val& R = out(d);
-    const uint32_t dm = dem_[d];
-    for (int k = 0; k < 8; ++k) {
-        if (!((dm >> k) & 1)) continue;
-        const uint32_t r = valloc();
-        emit(M_V_MOV, {V(r), V(R_DQ + k)});
-        R.l[k] = Limb::R(r);
-    }
+    const uint32_t dm = dem_[d], base = kind == 1 ? R_DR : R_DQ;
+    for (int k = 0; k < 8; ++k)
+        if ((dm >> k) & 1) R.l[k] = Limb::R(base + k);
 }
 
 void Emitter::demand() {
@@ -838,6 +970,8 @@ void Emitter::demand() {
     }
 }
 
+uint64_t Emitter::op_valu[256], Emitter::op_wide[256], Emitter::op_count[256];
+
 TapeCode Emitter::run() {
     TapeCode tc;
     tc.alg_ops = st_.alg_ops;
@@ -869,6 +1003,8 @@ TapeCode Emitter::run() {
         for (int i = 0; i < (int)code.size(); ++i) {
             const SsaInsn& v = code[i];
             const uint8_t op = v.op;
+            cur_op_ = op;
+            ++op_count[op];
             auto Y = [&]() -> Val { return v.cidx >= 0 ? const_val(v.cidx) : val(v.b); };
             switch (op) {
                 case D_NOP: {
@@ -916,7 +1052,7 @@ TapeCode Emitter::run() {
                     op_vshift(v.d, val(v.a), val(v.b), op);
                     break;
                 case D_UDIV_R: case D_UREM_R: case D_SDIV_R: case D_SREM_R: case D_SMOD_R:
-                    op_div(v.d, val(v.a), Y(), (uint32_t)(op - D_UDIV_R) >> 1);
+                    op_div(v.d, v.a, v.b, v.cidx, (uint32_t)(op - D_UDIV_R) >> 1, i);
                     break;
                 default:
                     if (op >= D_SHR0 && op <= D_SHR7) {
@@ -1037,6 +1173,7 @@ const char* op_name(uint16_t op) {
         case M_S_XOR_B64: return "s_xor_b64";
         case M_S_XNOR_B64: return "s_xnor_b64";
         case M_S_ANDN2_B64: return "s_andn2_b64";
+        case M_S_ORN2_B64: return "s_orn2_b64";
         case M_S_NOT_B64: return "s_not_b64";
         case M_S_CMP_EQ_U64: return "s_cmp_eq_u64";
         case M_S_CMP_LG_U64: return "s_cmp_lg_u64";
@@ -1105,7 +1242,7 @@ std::vector<MI> div_routine() {
                TM = S(S_DIV_TM, 2), K64 = S(S_DIV_F64K, 2), KIND = S(S_DIV_KIND);
     const Opnd K64LO = S(S_DIV_F64K), K64HI = S(S_DIV_F64K + 1);
     enum : uint32_t { L_UNS = 1, L_DONE, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
-                      L_SDIV, L_SREM, L_SMOD };
+                      L_SDIV, L_SREM, L_SMOD, L_NARROW = 50, L_NNEG0 = 60, L_NGE0 = 70 };
     auto to_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
         E(M_S_MOV_B32, {K64LO, IMM(0)});
         E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});
@@ -1130,16 +1267,20 @@ std::vector<MI> div_routine() {
     }
     L(L_UNS);
     for (int k = 0; k < 8; ++k) E(M_V_MOV, {Xr(k), IMM(0)});
-    E(M_V_OR3, {T1, Yr(0), Yr(1), Yr(2)});
-    E(M_V_OR3, {T1, T1, Yr(3), Yr(4)});
-    E(M_V_OR3, {T1, T1, Yr(5), Yr(6)});
-    E(M_V_OR, {T1, T1, Yr(7)});
+    E(M_V_OR3, {T1, Yr(1), Yr(2), Yr(3)});
+    E(M_V_OR3, {T1, T1, Yr(4), Yr(5)});
+    E(M_V_OR3, {T1, T1, Yr(6), Yr(7)});
+    E(M_V_CMP_NE, {TM, IMM(0), T1}, true);  // lanes with y >= 2^32
+    E(M_V_OR, {T1, T1, Yr(0)});
     E(M_V_CMP_NE, {YNZ, IMM(0), T1}, true);
     E(M_V_SUB_CO, {T1, VCC(), Rr(0), Yr(0)});
     for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {T1, VCC(), Rr(k), Yr(k), VCC()});
     E(M_S_ANDN2_B64, {MSK, YNZ, VCC()});
     E(M_S_CMP_EQ_U64, {MSK, IMM(0)});
     E(M_S_CBRANCH_SCC1, {LBL(L_DONE)});
+    // every lane's divisor below 2^32: digit-by-digit 64/32 division (L_NARROW)
+    E(M_S_CMP_EQ_U64, {TM, IMM(0)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_NARROW)});
     // 1/yd, qd = R/y for the start digit
     to_f64(FY, Yl);
     E(M_V_RCP_F64, {FC, FY});
@@ -1148,6 +1289,13 @@ std::vector<MI> div_routine() {
     E(M_V_FMA_F64, {FY, FC, FT, FC});
     to_f64(FR, Rl);
     E(M_V_MUL_F64, {FC, FR, FY});
+    // common case first: every active lane's quotient estimate below 2^31 -> the last step only
+    E(M_S_MOV_B32, {K64LO, IMM(0)});
+    E(M_S_MOV_B32, {K64HI, IMM((uint32_t)(1023 + 31) << 20)});
+    E(M_V_CMP_LE_F64, {VCC(), K64, FC});
+    E(M_S_AND_B64, {TM, VCC(), MSK});
+    E(M_S_CMP_EQ_U64, {TM, IMM(0)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_STEP0)});
     for (int j = 7; j >= 1; --j) {  // start at the highest j with qd >= 2^(32j - 1) in some lane
         const uint32_t hi = (uint32_t)(1023 + 32 * j - 1) << 20;
         E(M_S_MOV_B32, {K64LO, IMM(0)});
@@ -1158,10 +1306,10 @@ std::vector<MI> div_routine() {
         E(M_S_CBRANCH_SCC1, {LBL(L_STEP0 + j)});
     }
     E(M_S_BRANCH, {LBL(L_STEP0)});
+    // FC = R * (1/y) is valid on entry to every step: computed above for the first step the
+    // dispatch picks, recomputed at the end of each step for the next one
     for (int j = 7; j >= 0; --j) {
         L(L_STEP0 + j);
-        to_f64(FR, Rl);
-        E(M_V_MUL_F64, {FC, FR, FY});
         if (j) {
             E(M_S_MOV_B32, {K64LO, IMM(0)});
             E(M_S_MOV_B32, {K64HI, IMM((uint32_t)(1023 - 32 * j) << 20)});
@@ -1216,25 +1364,82 @@ std::vector<MI> div_routine() {
         E(M_V_ADD_U32, {C, C, T1});
         L(L_NOGE0 + j);
         E(M_V_MOV, {Xr(j), C});
+        if (j) {  // the next step's estimate from the reduced remainder
+            to_f64(FR, Rl);
+            E(M_V_MUL_F64, {FC, FR, FY});
+        }
     }
+    E(M_S_BRANCH, {LBL(L_DONE)});
+    // ---- narrow divisor (d = y0 < 2^32 in every lane, y = 0 lanes masked by YNZ): for
+    // k = 7..0, q_k = floor((r 2^32 + R[k]) / d) from an f64 estimate (the 64-bit numerator and
+    // the refined reciprocal round to 2^-52 relative, so the estimate is the digit or off by
+    // one), R[k] = the low word of the exact difference, corrected by one add-back / subtract;
+    // it is the next digit's r
+    L(L_NARROW);
+    E(M_V_CVT_F64_U32, {FY, Yr(0)});
+    E(M_V_RCP_F64, {FC, FY});
+    E(M_S_NOP, {IMM(1)});
+    E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
+    E(M_V_FMA_F64, {FY, FC, FT, FC});          // FY = 1/d
+    // y = 0 lanes: 1/d := 0, so their digit estimates are 0, nothing is subtracted and R keeps
+    // |x| (the SMT-LIB x % 0 = x); their quotient is fixed to 2^256 - 1 at the end
+    E(M_V_CNDMASK, {V(R_FY), IMM(0), V(R_FY), YNZ}, true);
+    E(M_V_CNDMASK, {V(R_FY + 1), IMM(0), V(R_FY + 1), YNZ}, true);
+    E(M_S_MOV_B32, {K64LO, IMM(0)});
+    E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});  // 2^32
+    E(M_V_MOV, {C, IMM(0)});                    // running remainder r < d
+    for (int k = 7; k >= 0; --k) {
+        E(M_V_CVT_F64_U32, {FR, C});
+        E(M_V_CVT_F64_U32, {FT, Rr(k)});
+        E(M_V_FMA_F64, {FR, FR, K64, FT});      // r 2^32 + R[k]
+        E(M_V_MUL_F64, {FC, FR, FY});
+        E(M_S_MOV_B32, {K64LO, IMM(0xffe00000u)});
+        E(M_S_MOV_B32, {K64HI, IMM(0x41efffffu)});
+        E(M_V_MIN_F64, {FC, FC, K64});
+        E(M_S_MOV_B32, {K64LO, IMM(0)});
+        E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});
+        E(M_V_CVT_U32_F64, {Xr(k), FC});          // digit estimate
+        E(M_V_MAD_U64_U32, {MAD, DUMMY, Xr(k), Yr(0), IMM(0)});
+        E(M_V_SUB_CO, {Rr(k), VCC(), Rr(k), V(R_MAD)});        // low word of the difference
+        E(M_V_SUBB_CO, {T1, VCC(), C, V(R_MAD + 1), VCC()});    // borrow: estimate one too high
+        E(M_S_MOV_B64, {TM, VCC()});
+        E(M_S_CMP_EQ_U64, {TM, IMM(0)});
+        E(M_S_CBRANCH_SCC1, {LBL(L_NNEG0 + k)});
+        E(M_V_CNDMASK, {T1, IMM(0), Yr(0), TM}, true);
+        E(M_V_CNDMASK, {C, IMM(0), IMM(1), TM}, true);
+        E(M_V_ADD_U32, {Rr(k), Rr(k), T1});
+        E(M_V_SUB_U32, {Xr(k), Xr(k), C});
+        L(L_NNEG0 + k);
+        E(M_V_CMP_GE, {VCC(), Rr(k), Yr(0)});              // one too low: r >= d
+        E(M_S_AND_B64, {TM, VCC(), YNZ});
+        E(M_S_CMP_EQ_U64, {TM, IMM(0)});
+        E(M_S_CBRANCH_SCC1, {LBL(L_NGE0 + k)});
+        E(M_V_CNDMASK, {T1, IMM(0), Yr(0), TM}, true);
+        E(M_V_CNDMASK, {C, IMM(0), IMM(1), TM}, true);
+        E(M_V_SUB_U32, {Rr(k), Rr(k), T1});
+        E(M_V_ADD_U32, {Xr(k), Xr(k), C});
+        L(L_NGE0 + k);
+        E(M_V_MOV, {C, Rr(k)});                  // r
+    }
+    // R[0] is the remainder; R[1..7] hold the intermediate remainders: zero them (y != 0 lanes)
+    for (int k = 1; k < 8; ++k) E(M_V_CNDMASK, {Rr(k), Rr(k), IMM(0), YNZ}, true);
     L(L_DONE);
-    // y = 0: q = 2^256 - 1 (R already holds |x|)
-    for (int k = 0; k < 8; ++k) E(M_V_CNDMASK, {Xr(k), IMM(0xFFFFFFFFu), Xr(k), YNZ}, true);
     auto cneg = [&](uint32_t dst, uint32_t srcb, Opnd m) {  // dst = (src ^ m) - m
         for (int k = 0; k < 8; ++k) E(M_V_XOR, {V(dst + k), V(srcb + k), m});
         E(M_V_SUB_CO, {V(dst), VCC(), V(dst), m});
         for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {V(dst + k), VCC(), V(dst + k), m, VCC()});
     };
-    E(M_S_CMP_EQ_U32, {KIND, IMM(0)});
+    // UREM: the remainder stays in R (the caller reads it there); x % 0 = x needs no fix-up
+    E(M_S_CMP_EQ_U32, {KIND, IMM(1)});
     E(M_S_CBRANCH_SCC1, {LBL(L_WB)});
-    E(M_S_CMP_EQ_U32, {KIND, IMM(2)});
-    E(M_S_CBRANCH_SCC1, {LBL(L_SDIV)});
     E(M_S_CMP_EQ_U32, {KIND, IMM(4)});
     E(M_S_CBRANCH_SCC1, {LBL(L_SMOD)});
     E(M_S_CMP_EQ_U32, {KIND, IMM(3)});
     E(M_S_CBRANCH_SCC1, {LBL(L_SREM)});
-    for (int k = 0; k < 8; ++k) E(M_V_MOV, {Xr(k), Rr(k)});  // UREM
-    E(M_S_BRANCH, {LBL(L_WB)});
+    // y = 0: q = 2^256 - 1 (R already holds |x|)
+    for (int k = 0; k < 8; ++k) E(M_V_CNDMASK, {Xr(k), IMM(0xFFFFFFFFu), Xr(k), YNZ}, true);
+    E(M_S_CMP_EQ_U32, {KIND, IMM(0)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_WB)});
     L(L_SDIV);  // q negated when the signs differ
     E(M_V_XOR, {T1, SX, SY});
     cneg(R_DQ, R_DQ, T1);
@@ -1261,6 +1466,15 @@ std::vector<MI> div_routine() {
     L(L_WB);
     E(M_RET, {});
     return o;
+}
+
+void op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, bool reset) {
+    for (int i = 0; i < 256; ++i) {
+        valu[i] = Emitter::op_valu[i];
+        wide[i] = Emitter::op_wide[i];
+        count[i] = Emitter::op_count[i];
+        if (reset) Emitter::op_valu[i] = Emitter::op_wide[i] = Emitter::op_count[i] = 0;
+    }
 }
 
 std::string print(const MI& m, const std::string& prefix) {

@@ -64,7 +64,7 @@ enum Op : uint16_t {
     M_V_CMP_LE_F64,
     // SALU
     M_S_MOV_B32, M_S_MOV_B64, M_S_AND_B64, M_S_OR_B64, M_S_XOR_B64, M_S_XNOR_B64,
-    M_S_ANDN2_B64, M_S_NOT_B64, M_S_CMP_EQ_U64, M_S_CMP_LG_U64, M_S_CMP_EQ_U32,
+    M_S_ANDN2_B64, M_S_ORN2_B64, M_S_NOT_B64, M_S_CMP_EQ_U64, M_S_CMP_LG_U64, M_S_CMP_EQ_U32,
     M_S_CMP_LT_U32,
     // control
     M_S_CBRANCH_SCC0, M_S_CBRANCH_SCC1, M_S_BRANCH, M_LABEL, M_S_NOP,
@@ -139,6 +139,10 @@ struct Module {
 Module build_module(const std::vector<const TapeCode*>& codes,
                     const std::vector<uint32_t>& tape_ids, uint32_t n_vars, bool values,
                     uint32_t group_bytes = 40 * 1024);
+
+// Diagnostics: static VALU (and 4-cycle VALU) emitted per SSA op kind since the last reset
+// (not thread safe; tests / scripts only).
+void op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, bool reset);
 
 // Estimated machine-code bytes of a tape body.
 uint32_t code_bytes(const TapeCode& tc);

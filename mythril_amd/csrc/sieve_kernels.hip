@@ -381,6 +381,35 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink
                                  "v_add_co_u32 %2, vcc, %2, %8\n v_add_co_u32 %3, vcc, %3, %8\n")
                              : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
                              : "v"(y) : "vcc");
+            if constexpr (KIND == 11)  // v_cndmask_b32_e32: mask in VCC (implicit)
+                asm volatile("s_mov_b64 vcc, 0x5555\n"
+                             MB8("v_cndmask_b32 %0, %0, %8, vcc\n v_cndmask_b32 %1, %1, %8, vcc\n"
+                                 "v_cndmask_b32 %2, %2, %8, vcc\n v_cndmask_b32 %3, %3, %8, vcc\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y) : "vcc");
+            if constexpr (KIND == 12)  // v_cmp_eq_u32_e32 (VCC written), results folded by s_and
+                asm volatile(MB8("v_cmp_eq_u32 vcc, %0, %8\n v_cmp_eq_u32 vcc, %1, %8\n"
+                                 "v_cmp_eq_u32 vcc, %2, %8\n v_cmp_eq_u32 vcc, %3, %8\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y) : "vcc");
+            if constexpr (KIND == 13)  // VOP2 with a 32-bit literal (8-byte instruction)
+                asm volatile(MB8("v_xor_b32 %0, 0x12345678, %0\n v_xor_b32 %1, 0x2345678a, %1\n"
+                                 "v_xor_b32 %2, 0x345678ab, %2\n v_xor_b32 %3, 0x45678abc, %3\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+            if constexpr (KIND == 14) MB_ONE("v_lshlrev_b32");
+            if constexpr (KIND == 15)  // VOP3 without an SGPR write or constant
+                asm volatile(MB8("v_add3_u32 %0, %0, %8, %4\n v_add3_u32 %1, %1, %8, %5\n"
+                                 "v_add3_u32 %2, %2, %8, %6\n v_add3_u32 %3, %3, %8, %7\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y));
+            if constexpr (KIND == 16) {  // v_fma_f64 (4 independent pairs)
+                double d0 = a0, d1 = a1, d2 = a2, d3 = a3;
+                const double e = 1.0000001;
+                asm volatile(MB8("v_fma_f64 %0, %0, %4, %4\n v_fma_f64 %1, %1, %4, %4\n"
+                                 "v_fma_f64 %2, %2, %4, %4\n v_fma_f64 %3, %3, %4, %4\n")
+                             : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "v"(e));
+                a0 = (u32)d0 ^ (u32)d1 ^ (u32)d2 ^ (u32)d3;
+            }
 #undef MB_ONE
         }
     }
@@ -450,7 +479,8 @@ hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uin
 #define MB_CASE(k) \
     case k: hipLaunchKernelGGL(microbench_kernel<k>, dim3(blocks), dim3(kBlock), 0, stream, iters, sink); break;
         MB_CASE(0) MB_CASE(1) MB_CASE(2) MB_CASE(3) MB_CASE(4) MB_CASE(5) MB_CASE(6) MB_CASE(7)
-        MB_CASE(8) MB_CASE(9) MB_CASE(10)
+        MB_CASE(8) MB_CASE(9) MB_CASE(10) MB_CASE(11) MB_CASE(12) MB_CASE(13) MB_CASE(14)
+        MB_CASE(15) MB_CASE(16)
 #undef MB_CASE
         default: return hipErrorInvalidValue;
     }

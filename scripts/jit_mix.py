@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Executed instruction mix of the JIT's code on config-5 tapes, from the host wave emulator
+(tests/native/jit_emu.cpp runs the very instruction lists the GPU runs, on the same generated
+rows): VALU per wave-evaluation, split into 2-cycle and 4-cycle issue classes (the measured
+issue costs of profiles/r02a/valu_peak.json) and into tape body vs the division subroutine.
+With a measured evals/s it gives the cycle-weighted VALU issue busy of the native kernel.
+
+    python scripts/jit_mix.py [n_tapes] [evals_per_s]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from mythril_amd import synth  # noqa: E402
+from oracle import smt_eval  # noqa: E402
+from tests.conftest import build_emulator  # noqa: E402
+from tests.emu import Emulator, jit_eval  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    evals = float(sys.argv[2]) if len(sys.argv) > 2 else None
+    emu = Emulator(build_emulator())
+    ts = synth.generate(n)
+    seed = synth.load_spec()["assignment_seed"]
+    rows = 128
+    soa = np.zeros((4, 8, rows), dtype=np.uint32)
+    for r in range(rows):
+        a = smt_eval.gen_assignment(seed, 4, r)
+        for v in range(4):
+            for k in range(8):
+                soa[v, k, r] = (a[v] >> (32 * k)) & 0xFFFFFFFF
+    tot = dict(valu=0, wide=0, salu=0, div_valu=0, div_wide=0, f64=0)
+    m = 0
+    for i in range(n):
+        res = jit_eval(emu, ts, i, soa)
+        if not res.ok:
+            continue
+        m += 1
+        for k in tot:
+            tot[k] += res.dyn[k]
+    per = {k: v / m for k, v in tot.items()}
+    narrow = per["valu"] - per["wide"]
+    # issue cycles per wave-evaluation at the measured costs (8 waves / SIMD,
+    # profiles/r02e/valu_peak.json): 2-cycle class 2.56, VOP3 / carry / compare / shift 4.5,
+    # f64 6.1 (counted inside the wide class)
+    cyc = 2.56 * narrow + 4.5 * (per["wide"] - per["f64"]) + 6.1 * per["f64"]
+    out = {"tapes": m, "per_wave_eval": per, "issue_cycles_per_wave_eval": cyc,
+           "valu_lane_ops_per_eval": per["valu"]}
+    if evals:
+        wave_evals = evals / 64.0
+        out["issue_busy"] = wave_evals * cyc / (1024 * 2.4e9)
+        out["exec_lane_ops_per_s"] = evals * per["valu"]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -78,6 +78,9 @@ class JitResult:
         self.calls_div, self.root_bool, self.code_bytes = bool(info[5]), bool(info[6]), int(info[7])
         self.values = values
         self.why = why
+        # executed per 64-row chunk (wave): VALU, 4-cycle VALU, SALU, division VALU / 4-cycle
+        self.dyn = dict(zip(("valu", "wide", "salu", "div_valu", "div_wide", "f64"),
+                            (int(x) for x in info[8:14])))
 
 
 def _jit_fn(lib, name, restype, argtypes):
@@ -104,7 +107,7 @@ def jit_eval(emu: "Emulator", ts: TapeSet, tape: int, soa: np.ndarray, max_vgpr:
         soa = np.zeros((max(ts.n_vars, 1), 8, 1), dtype=np.uint32)
     soa = np.ascontiguousarray(soa, dtype=np.uint32)
     out = np.zeros((8, rows), dtype=np.uint32)
-    info = np.zeros(8, dtype=np.uint32)
+    info = np.zeros(16, dtype=np.uint32)
     err = C.create_string_buffer(512)
     r = f(nodes.ctypes.data, offs.ctypes.data, len(ts.tapes), consts.ctypes.data,
           len(ts.pool.values), ts.n_vars, tape, soa.ctypes.data, rows, out.ctypes.data, max_vgpr,

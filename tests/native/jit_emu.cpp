@@ -81,6 +81,22 @@ struct Err {
     std::string m;
 };
 
+// executed-instruction counters (per wave): VALU, of them 4-cycle class, SALU, and the part
+// inside the division subroutine
+struct Counts {
+    uint64_t valu = 0, wide = 0, salu = 0, div_valu = 0, div_wide = 0, f64 = 0;
+} g_counts;
+uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
+
+bool is_wide(const MI& m) {
+    const uint16_t op = m.op;
+    return m.e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
+           op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO || op == M_V_OR3 ||
+           op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 || (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) ||
+           op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
+           op >= M_V_CVT_F64_U32;
+}
+
 void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int depth = 0) {
     std::unordered_map<uint32_t, size_t> lab;
     for (size_t i = 0; i < code.size(); ++i)
@@ -90,6 +106,15 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
         if (++steps > 10000000) throw Err{"emulator: runaway"};
         const MI& m = code[pc++];
         const Opnd* o = m.o;
+        if (m.op <= M_V_CMP_LE_F64) {
+            const bool wd = is_wide(m);
+            ++g_counts.valu;
+            g_counts.wide += wd;
+            g_counts.f64 += m.op >= M_V_CVT_F64_U32;
+            if (depth) { ++g_counts.div_valu; g_counts.div_wide += wd; }
+        } else if (m.op <= M_S_CMP_LT_U32) {
+            ++g_counts.salu;
+        }
         auto each = [&](auto f) { for (int l = 0; l < 64; ++l) f(l); };
         auto carry_op = [&](auto f) {  // d = f(l, &carry); sdst = o[1]
             uint64_t cm = 0;
@@ -230,10 +255,11 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
             case M_S_MOV_B32: w.s[o[0].v] = w.r32(o[1], 0); break;
             case M_S_MOV_B64: w.set_mask(o[0], w.mask(o[1])); break;
             case M_S_AND_B64: case M_S_OR_B64: case M_S_XOR_B64: case M_S_XNOR_B64:
-            case M_S_ANDN2_B64: {
+            case M_S_ANDN2_B64: case M_S_ORN2_B64: {
                 const uint64_t a = w.mask(o[1]), b = w.mask(o[2]);
                 uint64_t r = m.op == M_S_AND_B64 ? a & b : m.op == M_S_OR_B64 ? a | b :
-                             m.op == M_S_XOR_B64 ? a ^ b : m.op == M_S_XNOR_B64 ? ~(a ^ b) : a & ~b;
+                             m.op == M_S_XOR_B64 ? a ^ b : m.op == M_S_XNOR_B64 ? ~(a ^ b) :
+                             m.op == M_S_ANDN2_B64 ? a & ~b : a | ~b;
                 w.set_mask(o[0], r);
                 w.scc = r != 0;
                 break;
@@ -258,10 +284,14 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 break;
             }
             case M_LABEL: case M_S_NOP: break;
-            case M_CALL_DIV:
+            case M_CALL_DIV: {
                 if (depth) throw Err{"emulator: nested call"};
+                const uint64_t before = g_counts.div_valu;
                 run(w, div, div, depth + 1);
+                const uint64_t n = (g_counts.div_valu - before) / 32;
+                ++g_div_hist[n < 31 ? n : 31];
                 break;
+            }
             case M_RET: return;
             default: throw Err{"emulator: unknown op " + std::to_string(m.op)};
         }
@@ -289,7 +319,8 @@ bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes
 }  // namespace
 
 // info[0] = 1 if jitted, [1] max_vgpr, [2] n_valu, [3] n_valu_wide, [4] n_salu, [5] calls_div,
-// [6] root_bool, [7] code bytes.  Returns 0 (evaluated or not jittable: see info[0] / err),
+// [6] root_bool, [7] code bytes; executed per 64-row chunk: [8] VALU, [9] 4-cycle VALU, [10] SALU,
+// [11] VALU inside the division subroutine, [12] 4-cycle VALU inside it.  Returns 0 (evaluated or not jittable: see info[0] / err),
 // < 0 on an emulator / lowering error.
 extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                                 const uint32_t* consts, uint32_t n_consts, uint32_t n_vars,
@@ -318,6 +349,8 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
     }
     static const std::vector<MI> div = div_routine();
     static Wave w;
+    g_counts = Counts();
+    uint64_t chunks = 0;
     try {
         for (uint64_t base = 0; base < rows; base += 64) {
             for (int r = 0; r < 512; ++r)
@@ -331,6 +364,7 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
                         w.v[R_COL0 + 8 * c + k][l] = assign[((uint64_t)c * 8 + k) * rows + row];
                     }
             run(w, tc.code, div);
+            ++chunks;
             const uint64_t res = (uint64_t)w.s[S_RES] | ((uint64_t)w.s[S_RES + 1] << 32);
             for (int l = 0; l < 64 && base + (uint64_t)l < rows; ++l) {
                 const uint64_t row = base + (uint64_t)l;
@@ -346,6 +380,13 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
         snprintf(err, errlen, "%s", x.m.c_str());
         return -2;
     }
+    // dynamic counts per 64-row chunk (one wave evaluation of the tape)
+    info[8] = (uint32_t)(g_counts.valu / chunks);
+    info[9] = (uint32_t)(g_counts.wide / chunks);
+    info[10] = (uint32_t)(g_counts.salu / chunks);
+    info[11] = (uint32_t)(g_counts.div_valu / chunks);
+    info[12] = (uint32_t)(g_counts.div_wide / chunks);
+    info[13] = (uint32_t)(g_counts.f64 / chunks);
     return 0;
 }
 
@@ -393,4 +434,15 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
         *hsaco_size = bin.size();
     }
     return (int64_t)m.text.size();
+}
+
+extern "C" void emu_jit_op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, int reset) {
+    op_stats(valu, wide, count, reset != 0);
+}
+
+extern "C" void emu_jit_div_hist(uint64_t* out, int reset) {
+    for (int i = 0; i < 32; ++i) {
+        out[i] = g_div_hist[i];
+        if (reset) g_div_hist[i] = 0;
+    }
 }
