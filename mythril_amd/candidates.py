@@ -110,11 +110,10 @@ class Guide:
 
 
 def _limbs(vals: Sequence[int]) -> np.ndarray:
-    arr = np.zeros((max(len(vals), 1), 8), dtype=np.uint32)
-    for i, v in enumerate(vals):
-        for k in range(8):
-            arr[i, k] = (v >> (32 * k)) & 0xFFFFFFFF
-    return arr
+    if not vals:
+        return np.zeros((1, 8), dtype=np.uint32)
+    buf = b"".join((v & ((1 << 256) - 1)).to_bytes(32, "little") for v in vals)
+    return np.frombuffer(buf, dtype="<u4").reshape(len(vals), 8).astype(np.uint32)
 
 
 class Harvester:
@@ -404,7 +403,7 @@ class Harvester:
                 self.query_consts.add(b.pool.values[i0])
             from .tape import ARITY
 
-            stack += [a, bb, c][:ARITY[Op(op)]]
+            stack += [a, bb, c][:ARITY[op]]
         if parent:
             alt = {k: v for k, v in parent.items() if k in self.pools}
             if alt:
@@ -479,7 +478,7 @@ class Harvester:
             op, w, a, bb, c, _, _ = b.nodes[n]
             if op == Op.EQ:
                 out.append(n)
-            stack += [a, bb, c][:ARITY[Op(op)]]
+            stack += [a, bb, c][:ARITY[op]]
         return out
 
     def strip_common(self, x: int, y: int) -> Tuple[int, int]:

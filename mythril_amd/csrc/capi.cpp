@@ -28,7 +28,44 @@ struct mh_ctx {
     uint32_t* scratch = nullptr;  // microbench sink
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> spans;  // one per timed sieve launch
+    // per-query latency path (mh_run / mh_eval_values / mh_assign_download): grow-only device
+    // result buffer and pinned host staging, so a query allocates nothing
+    void* d_buf = nullptr;
+    size_t d_buf_bytes = 0;
+    void* h_buf = nullptr;
+    size_t h_buf_bytes = 0;
 };
+
+namespace {
+hipError_t ctx_dbuf(mh_ctx* c, size_t bytes, void** out) {
+    if (bytes > c->d_buf_bytes) {
+        if (c->d_buf) (void)hipFree(c->d_buf);
+        c->d_buf = nullptr;
+        c->d_buf_bytes = 0;
+        size_t n = 1 << 16;
+        while (n < bytes) n <<= 1;
+        hipError_t e = hipMalloc(&c->d_buf, n);
+        if (e != hipSuccess) return e;
+        c->d_buf_bytes = n;
+    }
+    *out = c->d_buf;
+    return hipSuccess;
+}
+hipError_t ctx_hbuf(mh_ctx* c, size_t bytes, void** out) {
+    if (bytes > c->h_buf_bytes) {
+        if (c->h_buf) (void)hipHostFree(c->h_buf);
+        c->h_buf = nullptr;
+        c->h_buf_bytes = 0;
+        size_t n = 1 << 16;
+        while (n < bytes) n <<= 1;
+        hipError_t e = hipHostMalloc(&c->h_buf, n, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        c->h_buf_bytes = n;
+    }
+    *out = c->h_buf;
+    return hipSuccess;
+}
+}  // namespace
 
 struct mh_tapeset {
     mh_ctx* ctx = nullptr;
@@ -73,7 +110,11 @@ struct mh_assign {
     uint32_t* d = nullptr;
     uint32_t* d_guide = nullptr;   // packed mh_guide (grow-only)
     size_t guide_words = 0;
-    std::vector<uint32_t> h_guide; // host staging of the packed guide
+    std::vector<uint32_t> h_guide; // host packing of the guide
+    uint32_t* h_pinned = nullptr;  // pinned staging of the packed guide (grow-only)
+    size_t pinned_words = 0;
+    hipEvent_t staged = nullptr;   // recorded after the staging copy; reuse waits on it
+    bool staged_pending = false;
 };
 
 namespace {
@@ -244,6 +285,8 @@ int32_t mh_ctx_destroy(mh_ctx* ctx) {
     }
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->d_buf) (void)hipFree(ctx->d_buf);
+    if (ctx->h_buf) (void)hipHostFree(ctx->h_buf);
     delete ctx;
     return MH_OK;
 }
@@ -398,6 +441,9 @@ int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_ass
 int32_t mh_assign_destroy(mh_assign* as) {
     if (!as) return MH_OK;
     (void)hipSetDevice(as->ctx->device);
+    if (as->staged_pending) (void)hipEventSynchronize(as->staged);
+    if (as->staged) (void)hipEventDestroy(as->staged);
+    if (as->h_pinned) (void)hipHostFree(as->h_pinned);
     if (as->d) (void)hipFree(as->d);
     if (as->d_guide) (void)hipFree(as->d_guide);
     delete as;
@@ -423,10 +469,12 @@ int32_t mh_assign_download(const mh_assign* as, uint32_t* host_soa, uint64_t fir
     if (first > as->capacity || count > as->capacity - first)
         return set_err(MH_E_INVALID, "row range out of bounds");
     if (int32_t r = use_device(as->ctx)) return r;
-    for (uint64_t col = 0; col < (uint64_t)as->n_vars * 8; ++col) {
-        MH_HIP(hipMemcpyAsync(host_soa + col * count, as->d + col * as->capacity + first,
-                              count * sizeof(uint32_t), hipMemcpyDeviceToHost, as->ctx->stream));
-    }
+    if (count == 0) return MH_OK;
+    // one strided copy of every column-limb's [first, first + count) slice (a query reads one
+    // witness row: one call instead of one per column-limb)
+    MH_HIP(hipMemcpy2DAsync(host_soa, count * sizeof(uint32_t), as->d + first,
+                            as->capacity * sizeof(uint32_t), count * sizeof(uint32_t),
+                            (size_t)as->n_vars * 8, hipMemcpyDeviceToHost, as->ctx->stream));
     MH_HIP(hipStreamSynchronize(as->ctx->stream));
     return MH_OK;
 }
@@ -509,8 +557,25 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
         MH_HIP(hipMalloc(&as->d_guide, words * sizeof(uint32_t)));
         as->guide_words = words;
     }
-    MH_HIP(hipMemcpyAsync(as->d_guide, h.data(), words * sizeof(uint32_t), hipMemcpyHostToDevice,
-                          as->ctx->stream));
+    // pinned staging: the async copy needs no stream sync; the next call's packing waits on
+    // the event of this copy before it overwrites the staging buffer
+    if (as->staged_pending) {
+        MH_HIP(hipEventSynchronize(as->staged));
+        as->staged_pending = false;
+    }
+    if (words > as->pinned_words) {
+        if (as->h_pinned) MH_HIP(hipHostFree(as->h_pinned));
+        as->h_pinned = nullptr;
+        as->pinned_words = 0;
+        MH_HIP(hipHostMalloc(&as->h_pinned, words * sizeof(uint32_t), hipHostMallocDefault));
+        as->pinned_words = words;
+    }
+    if (!as->staged) MH_HIP(hipEventCreateWithFlags(&as->staged, hipEventDisableTiming));
+    std::memcpy(as->h_pinned, h.data(), words * sizeof(uint32_t));
+    MH_HIP(hipMemcpyAsync(as->d_guide, as->h_pinned, words * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, as->ctx->stream));
+    MH_HIP(hipEventRecord(as->staged, as->ctx->stream));
+    as->staged_pending = true;
     mh::KGuide k;
     k.n_cols = nc;
     k.n_sets = ns;
@@ -524,8 +589,6 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
     k.entry_val = as->d_guide + o_eval;
     MH_HIP(mh::launch_generate_guided(as->d, as->capacity, first, count, seed, global_base, k,
                                       as->ctx->stream));
-    // the staging vector is reused by the next call: finish the copy first
-    MH_HIP(hipStreamSynchronize(as->ctx->stream));
     return MH_OK;
 }
 
@@ -590,20 +653,25 @@ int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t 
     if (int32_t r = check_run_args(ctx, ts, tape_first, tape_count, as, row_first, row_count, mode))
         return r;
     if (int32_t r = use_device(ctx)) return r;
-    uint64_t* d = nullptr;
     const size_t n = std::max<uint32_t>(tape_count, 1);
-    MH_HIP(hipMalloc(&d, 2 * n * sizeof(uint64_t)));
+    void* dv = nullptr;
+    void* hv = nullptr;
+    MH_HIP(ctx_dbuf(ctx, 2 * n * sizeof(uint64_t), &dv));
+    MH_HIP(ctx_hbuf(ctx, 2 * n * sizeof(uint64_t), &hv));
+    uint64_t* d = static_cast<uint64_t*>(dv);
+    uint64_t* h = static_cast<uint64_t*>(hv);
     int32_t r = mh_results_reset(ctx, d, d + n, (uint32_t)n);
     if (r == MH_OK)
         r = mh_run_async(ctx, ts, tape_first, tape_count, as, row_first, row_count, index_base,
                          mode, d, d + n);
     hipError_t e = hipSuccess;
-    if (r == MH_OK) e = hipStreamSynchronize(ctx->stream);
+    if (r == MH_OK)  // both result arrays in one copy into pinned memory
+        e = hipMemcpyAsync(h, d, 2 * n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (r == MH_OK && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (r == MH_OK && e == hipSuccess && first_hit && tape_count)
-        e = hipMemcpy(first_hit, d, tape_count * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        std::memcpy(first_hit, h, tape_count * sizeof(uint64_t));
     if (r == MH_OK && e == hipSuccess && hit_count && tape_count)
-        e = hipMemcpy(hit_count, d + n, tape_count * sizeof(uint64_t), hipMemcpyDeviceToHost);
-    (void)hipFree(d);
+        std::memcpy(hit_count, h + n, tape_count * sizeof(uint64_t));
     if (r != MH_OK) return r;
     if (e != hipSuccess) return set_err(MH_E_DEVICE, std::string("mh_run: ") + hipGetErrorString(e));
     return MH_OK;

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -279,7 +280,9 @@ struct Lowering {
         return (int)const_index(consts + 8ull * c.imm0, c.width);
     }
 
-    // register holding narrow value k (constants are re-materialised at each use)
+    // register holding narrow value k (constants, and assignment columns that are not pinned in
+    // registers, are re-materialised at each use: a column load costs less than keeping a value
+    // live, and a query over many columns would otherwise exceed the register file)
     int vreg_of(uint32_t k) {
         const Val& v = (*vals_)[k];
         if (v.wide()) return -1;
@@ -287,6 +290,8 @@ struct Lowering {
             const mh_node& c = t[(size_t)v.remat];
             if (c.op == MH_OP_TRUE) return emit(D_TRUE, -1, -1, -1, 1);
             if (c.op == MH_OP_FALSE) return emit(D_FALSE, -1, -1, -1, 1);
+            if (c.op == MH_OP_VAR)
+                return masked(emit(D_LOADVAR, -1, -1, -1, 256, c.imm0), c.width);
             return emit(D_LOADC, -1, -1, -1, 256, 0,
                         (int)const_index(consts + 8ull * c.imm0, c.width));
         }
@@ -431,9 +436,12 @@ bool Lowering::lower(std::vector<Val>& vals) {
             case MH_OP_VAR: {
                 if (nd.imm0 >= n_vars) return fail("var column out of range");
                 if (w == 0 || w > 256) return fail("var width");
-                if (!pinned) features |= F_CPLX;
-                int r = pinned ? (int)nd.imm0 : emit(D_LOADVAR, -1, -1, -1, 256, nd.imm0);
-                out.vreg = masked(r, w);  // a w-bit variable is the low w bits of its column
+                if (!pinned) {
+                    features |= F_CPLX;
+                    out.remat = (int)i;  // loaded at each use (vreg_of)
+                    break;
+                }
+                out.vreg = masked((int)nd.imm0, w);  // a w-bit variable: low w bits of its column
                 break;
             }
             case MH_OP_TRUE: case MH_OP_FALSE: out.remat = (int)i; break;
@@ -888,10 +896,92 @@ int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* con
     return MH_OK;
 }
 
+namespace {
+
+// Cheap shared sub-terms (at most max_size nodes, no multiply / divide / keccak / exp) duplicated
+// at every use instead of kept live: a path condition reads the same calldata bytes in several
+// overlapping words (calldata.py:48-54: word(0) and word(4) share 28 byte terms), which otherwise
+// holds more values live than the register file has; the copies cost a few cheap instructions.
+std::vector<mh_node> rematerialize(const mh_node* t, size_t n, uint32_t max_size) {
+    std::vector<uint32_t> uses(n, 0), size(n, 0);
+    std::vector<char> cheap(n, 0), dup(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const mh_node& nd = t[i];
+        const int ar = arity(nd);
+        const uint32_t ops[3] = {nd.a, nd.b, nd.c};
+        uint64_t sz = 1;
+        bool ok = nd.width <= 256;
+        for (int k = 0; k < ar; ++k) {
+            ++uses[ops[k]];
+            sz += size[ops[k]];
+            ok = ok && cheap[ops[k]];
+        }
+        size[i] = (uint32_t)std::min<uint64_t>(sz, 1u << 30);
+        switch (nd.op) {
+            case MH_OP_BVMUL: case MH_OP_BVUDIV: case MH_OP_BVUREM: case MH_OP_BVSDIV:
+            case MH_OP_BVSREM: case MH_OP_BVSMOD: case MH_OP_KECCAK: case MH_OP_EVM_EXP:
+            case MH_OP_BVMUL_NOOVFL_U:
+                ok = false;
+                break;
+            default:
+                break;
+        }
+        cheap[i] = ok && size[i] <= max_size;
+    }
+    for (size_t i = 0; i < n; ++i) dup[i] = cheap[i] && uses[i] > 1;
+    std::vector<mh_node> out;
+    std::vector<uint32_t> remap(n, 0);
+    // inside a duplicated sub-term every cheap node is copied too, so copies share nothing
+    std::function<uint32_t(uint32_t, bool)> copy = [&](uint32_t k, bool deep) -> uint32_t {
+        mh_node nd = t[k];
+        const int ar = arity(nd);
+        uint32_t* ops[3] = {&nd.a, &nd.b, &nd.c};
+        for (int j = 0; j < ar; ++j) {
+            const uint32_t x = *ops[j];
+            *ops[j] = (cheap[x] && (deep || dup[x])) ? copy(x, true) : remap[x];
+        }
+        out.push_back(nd);
+        return (uint32_t)(out.size() - 1);
+    };
+    for (size_t i = 0; i < n; ++i) {
+        if (dup[i] && i != n - 1) continue;
+        remap[i] = copy((uint32_t)i, false);
+    }
+    return out;
+}
+
+int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
+                          uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
+                          std::unordered_map<std::string, uint32_t>& dconst_index,
+                          std::vector<uint32_t>& words, CompiledTape& out, std::string& err);
+
+}  // namespace
+
+// A tape that runs out of registers is retried with cheap shared sub-terms duplicated at their
+// uses, widening what counts as cheap (8, 32, 256 nodes).
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                      uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                      std::unordered_map<std::string, uint32_t>& dconst_index,
                      std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
+    int32_t r = compile_tape_once(nodes, n_nodes, consts, n_consts, n_vars, dconsts, dconst_index,
+                                  words, out, err);
+    for (uint32_t sz : {8u, 32u, 256u}) {
+        if (r != MH_E_UNSUPPORTED || err.find("register pressure") == std::string::npos) break;
+        std::vector<mh_node> t2 = rematerialize(nodes, n_nodes, sz);
+        err.clear();
+        r = compile_tape_once(t2.data(), t2.size(), consts, n_consts, n_vars, dconsts,
+                              dconst_index, words, out, err);
+        out.n_nodes = (uint32_t)n_nodes;
+    }
+    return r;
+}
+
+namespace {
+
+int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
+                          uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
+                          std::unordered_map<std::string, uint32_t>& dconst_index,
+                          std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
     SsaTape st;
     if (int32_t r = lower_tape_ssa(nodes, n_nodes, consts, n_consts, n_vars, dconsts,
                                    dconst_index, st, err))
@@ -1040,5 +1130,7 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
     words.insert(words.end(), slots.begin(), slots.end());
     return MH_OK;
 }
+
+}  // namespace
 
 }  // namespace mh

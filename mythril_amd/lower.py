@@ -33,7 +33,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
-from .tape import BOOL, F_ARRAY, Op, TapeBuilder, TapeError
+from .tape import ARITY, BOOL, F_ARRAY, Op, TapeBuilder, TapeError
 
 KECCAK_SHIFT = 139   # keep 117 bits of the hash ...
 KECCAK_ALIGN = 6     # ... as multiples of 64: H - base < 2^123 < PART
@@ -105,9 +105,7 @@ def _walk(b: TapeBuilder, roots: Iterable[int]) -> List[int]:
 
 
 def _arity(op: int) -> int:
-    from .tape import ARITY
-
-    return ARITY[Op(op)]
+    return ARITY[op]  # Op is an IntEnum: the int keys the table directly
 
 
 class Lowering:

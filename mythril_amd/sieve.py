@@ -51,6 +51,11 @@ class SieveStats:
     host_s: float = 0.0
     device_s: float = 0.0
     extra: Dict[str, int] = field(default_factory=dict)
+    # seconds per stage: lower, guide, tapes, compile, generate, run, download
+    stage_s: Dict[str, float] = field(default_factory=dict)
+
+    def add(self, stage: str, dt: float) -> None:
+        self.stage_s[stage] = self.stage_s.get(stage, 0.0) + dt
 
 
 def local_tape(b: TapeBuilder, root: int, columns: Sequence[str]) -> np.ndarray:
@@ -116,9 +121,13 @@ class Sieve:
     """A device context plus reusable buffers; one per thread (handles are not shared)."""
 
     def __init__(self, device: int = 0, rows: int = 1 << 16, max_rounds: int = 4,
-                 seed: int = 0x5EED5EED, budget_s: float = 0.25):
+                 seed: int = 0x5EED5EED, budget_s: float = 0.25, first_rows: int = 256):
         self.ctx = native.Context(device)
         self.rows = rows
+        # the harvested guide usually solves a LASER query in its first rows (round 1 found every
+        # SAT witness of tests/laser_like.py within the first 16 rows): a small first round
+        # answers those at a fraction of the latency, the full-size rounds follow
+        self.first_rows = min(first_rows, rows)
         self.max_rounds = max_rounds
         self.seed = seed
         self.budget_s = budget_s
@@ -242,7 +251,10 @@ class Sieve:
         if budget <= 0:
             self.stats.misses += 1
             return None
+        st = self.stats
         root, schema = lower_query(b, roots)
+        t_l = time.perf_counter()
+        st.add("lower", t_l - t0)
         columns = list(schema.columns)
         if not columns:  # ground query: one row decides it
             columns = ["__ground__"]
@@ -252,6 +264,8 @@ class Sieve:
             schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
         parent = self.witnesses.get(key[:-1]) if key else None
         guide = build_guide(b, root, schema, columns, parent).arrays()
+        t_g = time.perf_counter()
+        st.add("guide", t_g - t_l)
         groups = self.buckets(b, root)
         ts = TapeSet(columns)
         ts.pool = pool if pool is not None else b.pool
@@ -266,28 +280,41 @@ class Sieve:
         if len(groups) > 1:
             self.stats.extra["bucketed"] = self.stats.extra.get("bucketed", 0) + 1
         t1 = time.perf_counter()
+        st.add("tapes", t1 - t_g)
         self.stats.host_s += t1 - t0
         ct = self.compile(ts)
+        t_c = time.perf_counter()
+        st.add("compile", t_c - t1)
         try:
             assign = self._buffer(len(columns))
             col_index = {c: i for i, c in enumerate(columns)}
             values: Dict[str, int] = {}
             solved = [False] * len(groups)
             first_index = None
+            offset = 0
             for rnd in range(self.max_rounds):
-                base = (self.stats.queries << 24) + rnd * self.rows
-                assign.generate_guided(self.seed, guide, global_base=base, count=self.rows)
+                n = self.first_rows if rnd == 0 else self.rows
+                base = (self.stats.queries << 24) + offset
+                offset += n
+                ta = time.perf_counter()
+                assign.generate_guided(self.seed, guide, global_base=base, count=n)
+                tb = time.perf_counter()
                 fh, _ = native.run(self.ctx, ct, assign, mode=native.MODE_FIRST_HIT,
-                                   index_base=base, row_count=self.rows)
+                                   index_base=base, row_count=n)
+                tr = time.perf_counter()
+                st.add("generate", tb - ta)
+                st.add("run", tr - tb)
                 self.stats.rounds += 1
-                self.stats.rows += self.rows
+                self.stats.rows += n
                 rows_read: Dict[int, np.ndarray] = {}
                 for g, hit in enumerate(fh.tolist()):
                     if solved[g] or hit == native.NO_HIT:
                         continue
                     row = hit - base
                     if row not in rows_read:
+                        td = time.perf_counter()
                         rows_read[row] = assign.download(row, 1)
+                        st.add("download", time.perf_counter() - td)
                     vals = rows_read[row]
                     for c in group_cols[g]:
                         values[c] = _limbs(vals[col_index[c], :, 0])

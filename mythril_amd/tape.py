@@ -179,10 +179,18 @@ class TapeBuilder:
         return bool(self.flags[n] & F_ARRAY)
 
     def const_value(self, n: int) -> Optional[int]:
-        """The value of a constant node, else None.  CONST / TRUE / FALSE, and the bit-layout
-        ops CONCAT / EXTRACT / ZEXT / SEXT over constants, which z3's ``simplify`` folds before
+        """The value of a constant node, else None (memoised: nodes are immutable).  CONST / TRUE /
+        FALSE, and the bit-layout ops CONCAT / EXTRACT / ZEXT / SEXT over constants, which z3's ``simplify`` folds before
         ``BitVec.symbolic`` / ``.value`` look (mythril/laser/smt/bitvec.py:44-60); arithmetic is
         not folded here."""
+        cv = self.__dict__.setdefault("_cv", {})
+        if n in cv:
+            return cv[n]
+        r = self._const_value(n)
+        cv[n] = r
+        return r
+
+    def _const_value(self, n: int) -> Optional[int]:
         op, w, a, b, _, imm0, imm1 = self.nodes[n]
         if op == Op.CONST:
             return self.pool.values[imm0]

@@ -1,0 +1,7 @@
+#!/bin/bash
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02f
+mkdir -p $O
+T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+timeout -k 10 600 $T tests/test_gpu_frontend.py tests/test_gpu_parity.py -k "not bench_config" > $O/pytest_front_parity.txt 2>&1 && \
+timeout -k 10 300 python -u scripts/sieve_queries.py > $O/sieve_queries.jsonl 2> $O/sieve_queries.txt
