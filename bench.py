@@ -94,6 +94,12 @@ def main() -> None:
     assign.generate(seed, index_base)
     fh = torch.empty(n_tapes, dtype=torch.int64, device=dev)
     hc = torch.empty(n_tapes, dtype=torch.int64, device=dev)
+    if world > 1:
+        # the library's own RCCL communicator (mh_comm_init): rank 0's id reaches the others
+        # through torch.distributed; the per-step exchange then never leaves the C-ABI
+        box = [native.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        ctx.comm_init(box[0], rank, world)
     torch.cuda.synchronize(dev)
     log("[rank %d] setup %.1fs: %d tapes, %d insns, %d rows, %.0f alg-ops/row"
         % (rank, time.time() - t0, n_tapes, sum(i["n_insns"] for i in info), rows,
@@ -104,7 +110,7 @@ def main() -> None:
         native.run_async(ctx, ct, assign, fh.data_ptr(), hc.data_ptr(), index_base=index_base,
                          mode=native.MODE_COUNT_ALL)
         if world > 1:  # the one exchange: MIN of first witnesses, SUM of counts (RCCL)
-            shard.allreduce_results(fh, hc)
+            ctx.comm_allreduce(fh.data_ptr(), hc.data_ptr(), n_tapes)
 
     for i in range(args.warmup):
         step(False)

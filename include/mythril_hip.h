@@ -106,6 +106,9 @@ const char* mh_last_error(void);                       /* thread-local; never NU
 int32_t mh_device_count(int32_t* n);                   /* gfx950 devices visible                 */
 
 int32_t mh_ctx_create(int32_t device, mh_ctx** out);
+/* Releases the handle.  Tape sets and assignment buffers created from it keep it alive: its
+ * device memory, stream and communicator are freed when the last of them is destroyed (so the
+ * destroy order of handles never matters).  Destroying a ctx twice is MH_E_INVALID.             */
 int32_t mh_ctx_destroy(mh_ctx* ctx);
 /* Launch on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream; 0/NULL is the
  * null stream).  The ctx starts on a stream of its own.                                          */
@@ -219,6 +222,19 @@ int32_t mh_tapes_jitted(const mh_tapeset* ts, uint8_t* out /* [n_tapes] */, uint
  * the native path are left untouched).  Needs mh_tapes_jit(ts, MH_JIT_VALUES, ...).              */
 int32_t mh_jit_eval_all(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as,
                         uint64_t row_first, uint64_t row_count, uint32_t* out);
+
+/* ---- multi-GPU (no reference counterpart): rows shard across GPUs, one process
+ * per GPU, one RCCL communicator per handle.  The only exchange is one all-reduce per batch:
+ * MIN of the per-tape smallest witness index (MH_NO_HIT = UINT64_MAX is MIN's identity) and SUM
+ * of the hit counts, in place in device buffers, on the ctx stream, so the result is identical
+ * for any number of GPUs.  Rank 0 creates the id (mh_comm_unique_id) and the caller distributes
+ * it (torch.distributed, a file, ...).  RCCL is dlopen'ed on first use.                          */
+#define MH_COMM_ID_BYTES 128
+int32_t mh_comm_unique_id(uint8_t* out /* [MH_COMM_ID_BYTES] */);
+int32_t mh_comm_init(mh_ctx* ctx, const uint8_t* unique_id, int32_t rank, int32_t world);
+int32_t mh_comm_allreduce_results(mh_ctx* ctx, uint64_t* d_first_hit, uint64_t* d_hit_count,
+                                  uint32_t n);
+int32_t mh_comm_destroy(mh_ctx* ctx);
 
 /* Integer VALU issue-rate micro-benchmark (no reference counterpart: it settles the roofline peak
  * of SURVEY.md §8d).  Runs 32 wave-instructions of one kind per loop iteration, written in asm,

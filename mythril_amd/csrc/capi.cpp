@@ -2,7 +2,9 @@
 // launch orchestration.  No exception crosses the ABI and nothing here aborts the process:
 // every failure is an MH_E_* code plus a thread-local message, so the Python front end can fall
 // back to z3 (SURVEY.md §5 "fail closed").
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -34,7 +36,56 @@ struct mh_ctx {
     size_t d_buf_bytes = 0;
     void* h_buf = nullptr;
     size_t h_buf_bytes = 0;
+    // multi-GPU: one RCCL communicator per handle (mh_comm_init)
+    ncclComm_t comm = nullptr;
+    int32_t rank = 0, world = 1;
+    // device blocks of destroyed tape sets, by power-of-two size class: a query's tape set
+    // reuses them instead of calling hipMalloc (a new size class costs milliseconds)
+    std::unordered_map<size_t, std::vector<void*>> pool;
+    std::unordered_map<void*, size_t> pool_class;
+    size_t pool_bytes = 0;
+    // tape sets and assignment buffers hold the context: mh_ctx_destroy before them only marks
+    // it released, and the last child's destroy frees it
+    int32_t children = 0;
+    bool released = false;
 };
+
+namespace {
+// RCCL is opened on first use (dlopen), not linked: a process that never shards never loads it.
+// The ROCm install's copy comes first, opened by path with its own symbol scope (DEEPBIND): it
+// binds to the same libamdhip64.so.7 this library runs on, whereas a Python wheel's bundled
+// librccl (torch's) binds to the wheel's own HIP runtime -- on the box that copy fails with
+// "no ROCm-capable device" when this library initialised HIP first.
+struct Rccl {
+    void* h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+const Rccl* rccl() {
+    static Rccl r;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        for (const char* name : {"/opt/rocm/lib/librccl.so.1", "librccl.so.1"}) {
+            r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+            if (r.h) break;
+        }
+        if (r.h) {
+            r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.h, "ncclGetUniqueId");
+            r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(r.h, "ncclCommInitRank");
+            r.all_reduce = (decltype(r.all_reduce))dlsym(r.h, "ncclAllReduce");
+            r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.h, "ncclCommDestroy");
+            r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
+        }
+    }
+    if (!r.get_unique_id || !r.comm_init_rank || !r.all_reduce || !r.comm_destroy) return nullptr;
+    return &r;
+}
+}  // namespace
 
 namespace {
 hipError_t ctx_dbuf(mh_ctx* c, size_t bytes, void** out) {
@@ -50,6 +101,43 @@ hipError_t ctx_dbuf(mh_ctx* c, size_t bytes, void** out) {
     }
     *out = c->d_buf;
     return hipSuccess;
+}
+size_t pool_size_class(size_t bytes) {
+    size_t n = 4096;
+    while (n < bytes) n <<= 1;
+    return n;
+}
+template <class T>
+hipError_t pool_alloc(mh_ctx* c, T** out, size_t bytes) {
+    const size_t k = pool_size_class(bytes);
+    auto& fl = c->pool[k];
+    if (!fl.empty()) {
+        *out = static_cast<T*>(fl.back());
+        fl.pop_back();
+        c->pool_bytes -= k;
+        return hipSuccess;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, k);
+    if (e != hipSuccess) return e;
+    c->pool_class[p] = k;
+    *out = static_cast<T*>(p);
+    return hipSuccess;
+}
+void pool_free(mh_ctx* c, void* p) {
+    if (!p) return;
+    auto it = c->pool_class.find(p);
+    if (it == c->pool_class.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    if (c->pool_bytes + it->second > (256u << 20)) {  // keep at most 256 MiB cached
+        (void)hipFree(p);
+        c->pool_class.erase(it);
+        return;
+    }
+    c->pool[it->second].push_back(p);
+    c->pool_bytes += it->second;
 }
 hipError_t ctx_hbuf(mh_ctx* c, size_t bytes, void** out) {
     if (bytes > c->h_buf_bytes) {
@@ -275,8 +363,8 @@ int32_t mh_ctx_create(int32_t device, mh_ctx** out) {
     return MH_OK;
 }
 
-int32_t mh_ctx_destroy(mh_ctx* ctx) {
-    if (!ctx) return MH_OK;
+namespace {
+void ctx_free(mh_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto& sp : ctx->spans) {
@@ -287,7 +375,24 @@ int32_t mh_ctx_destroy(mh_ctx* ctx) {
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->d_buf) (void)hipFree(ctx->d_buf);
     if (ctx->h_buf) (void)hipHostFree(ctx->h_buf);
+    if (ctx->comm && rccl()) (void)rccl()->comm_destroy(ctx->comm);
+    for (auto& kv : ctx->pool_class) (void)hipFree(kv.first);
     delete ctx;
+}
+// a child (tape set / assignment buffer) of `ctx` is gone
+void ctx_unref(mh_ctx* ctx) {
+    if (--ctx->children == 0 && ctx->released) ctx_free(ctx);
+}
+}  // namespace
+
+int32_t mh_ctx_destroy(mh_ctx* ctx) {
+    if (!ctx) return MH_OK;
+    if (ctx->released) return set_err(MH_E_INVALID, "context already destroyed");
+    if (ctx->children > 0) {
+        ctx->released = true;
+        return MH_OK;
+    }
+    ctx_free(ctx);
     return MH_OK;
 }
 
@@ -361,6 +466,7 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     mh_tapeset* ts = new (std::nothrow) mh_tapeset();
     if (!ts) return set_err(MH_E_NOMEM, "tapeset allocation");
     ts->ctx = ctx;
+    ++ctx->children;
     ts->n_tapes = n_tapes;
     ts->n_vars = n_vars;
     try {
@@ -368,20 +474,21 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
         ts->h_offs.assign(tape_offsets, tape_offsets + n_tapes + 1);
         ts->h_consts.assign(consts, consts + (size_t)n_consts * 8);
     } catch (const std::bad_alloc&) {
-        delete ts;
+        mh_tapes_destroy(ts);
         return set_err(MH_E_NOMEM, "host copy of the tapes");
     }
     ts->ids = std::move(ids);
     for (uint32_t v = 0; v <= mh::kNumVariants; ++v) ts->bucket_off[v] = bucket_off[v];
     ts->info = std::move(info);
-    hipError_t e = hipMalloc(&ts->d_insns, words.size() * sizeof(uint32_t));
+    hipError_t e = pool_alloc(ctx, &ts->d_insns, words.size() * sizeof(uint32_t));
     if (e == hipSuccess)
-        e = hipMalloc(&ts->d_ids, std::max<size_t>(1, ts->ids.size()) * sizeof(uint32_t));
+        e = pool_alloc(ctx, &ts->d_ids, std::max<size_t>(1, ts->ids.size()) * sizeof(uint32_t));
     if (e == hipSuccess && !ts->ids.empty())
         e = hipMemcpy(ts->d_ids, ts->ids.data(), ts->ids.size() * sizeof(uint32_t),
                       hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&ts->d_tapes, std::max<size_t>(1, n_tapes) * sizeof(mh_dev_tape));
-    if (e == hipSuccess) e = hipMalloc(&ts->d_consts, dconsts.size() * sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = pool_alloc(ctx, &ts->d_tapes, std::max<size_t>(1, n_tapes) * sizeof(mh_dev_tape));
+    if (e == hipSuccess) e = pool_alloc(ctx, &ts->d_consts, dconsts.size() * sizeof(uint32_t));
     if (e == hipSuccess)
         e = hipMemcpy(ts->d_insns, words.data(), words.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess && n_tapes)
@@ -399,16 +506,20 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
 int32_t mh_tapes_destroy(mh_tapeset* ts) {
     if (!ts) return MH_OK;
     (void)hipSetDevice(ts->ctx->device);
-    if (ts->d_insns) (void)hipFree(ts->d_insns);
-    if (ts->d_tapes) (void)hipFree(ts->d_tapes);
-    if (ts->d_consts) (void)hipFree(ts->d_consts);
-    if (ts->d_ids) (void)hipFree(ts->d_ids);
+    // kernels of this set may still run on the ctx stream: finish them before the blocks go back
+    if (ts->ctx->stream) (void)hipStreamSynchronize(ts->ctx->stream);
+    pool_free(ts->ctx, ts->d_insns);
+    pool_free(ts->ctx, ts->d_tapes);
+    pool_free(ts->ctx, ts->d_consts);
+    pool_free(ts->ctx, ts->d_ids);
     if (ts->d_ids_rest) (void)hipFree(ts->d_ids_rest);
     for (auto& j : ts->jit) {
         if (j.mod) (void)hipModuleUnload(j.mod);
         if (j.vmod) (void)hipModuleUnload(j.vmod);
     }
+    mh_ctx* ctx = ts->ctx;
     delete ts;
+    ctx_unref(ctx);
     return MH_OK;
 }
 
@@ -427,11 +538,12 @@ int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_ass
     mh_assign* as = new (std::nothrow) mh_assign();
     if (!as) return set_err(MH_E_NOMEM, "assign allocation");
     as->ctx = ctx;
+    ++ctx->children;
     as->n_vars = n_vars;
     as->capacity = capacity;
     hipError_t e = hipMalloc(&as->d, (size_t)n_vars * 8 * capacity * sizeof(uint32_t));
     if (e != hipSuccess) {
-        delete as;
+        mh_assign_destroy(as);
         return set_err(MH_E_NOMEM, std::string("assignment buffer: ") + hipGetErrorString(e));
     }
     *out = as;
@@ -446,7 +558,9 @@ int32_t mh_assign_destroy(mh_assign* as) {
     if (as->h_pinned) (void)hipHostFree(as->h_pinned);
     if (as->d) (void)hipFree(as->d);
     if (as->d_guide) (void)hipFree(as->d_guide);
+    mh_ctx* ctx = as->ctx;
     delete as;
+    ctx_unref(ctx);
     return MH_OK;
 }
 
@@ -832,6 +946,68 @@ int32_t mh_jit_eval_all(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as,
     (void)hipFree(d);
     if (r != MH_OK) return r;
     if (e != hipSuccess) return set_err(MH_E_DEVICE, std::string("mh_jit_eval_all: ") + hipGetErrorString(e));
+    return MH_OK;
+}
+
+int32_t mh_comm_unique_id(uint8_t* out) {
+    if (!out) return set_err(MH_E_INVALID, "null out");
+    const Rccl* r = rccl();
+    if (!r) return set_err(MH_E_UNSUPPORTED, "RCCL (librccl.so) not loadable");
+    ncclUniqueId id;
+    const ncclResult_t e = r->get_unique_id(&id);
+    if (e != ncclSuccess)
+        return set_err(MH_E_DEVICE, std::string("ncclGetUniqueId: ") +
+                                        (r->error_string ? r->error_string(e) : "error"));
+    static_assert(sizeof(id) == MH_COMM_ID_BYTES, "RCCL unique id size");
+    std::memcpy(out, &id, sizeof(id));
+    return MH_OK;
+}
+
+int32_t mh_comm_init(mh_ctx* ctx, const uint8_t* unique_id, int32_t rank, int32_t world) {
+    if (!ctx || !unique_id) return set_err(MH_E_INVALID, "null argument");
+    if (world < 1 || rank < 0 || rank >= world) return set_err(MH_E_INVALID, "bad rank / world");
+    if (ctx->comm) return set_err(MH_E_INVALID, "ctx already has a communicator");
+    const Rccl* r = rccl();
+    if (!r) return set_err(MH_E_UNSUPPORTED, "RCCL (librccl.so) not loadable");
+    if (int32_t rc = use_device(ctx)) return rc;
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    const ncclResult_t e = r->comm_init_rank(&ctx->comm, world, id, rank);
+    if (e != ncclSuccess) {
+        ctx->comm = nullptr;
+        return set_err(MH_E_DEVICE, std::string("ncclCommInitRank: ") +
+                                        (r->error_string ? r->error_string(e) : "error"));
+    }
+    ctx->rank = rank;
+    ctx->world = world;
+    return MH_OK;
+}
+
+int32_t mh_comm_allreduce_results(mh_ctx* ctx, uint64_t* d_first_hit, uint64_t* d_hit_count,
+                                  uint32_t n) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    if (!ctx->comm) return set_err(MH_E_INVALID, "no communicator (mh_comm_init)");
+    const Rccl* r = rccl();
+    if (int32_t rc = use_device(ctx)) return rc;
+    // the one exchange of a sharded run: smallest witness index (NO_HIT = UINT64_MAX is the
+    // identity of MIN) and summed hit counts, in place on the ctx stream
+    ncclResult_t e = ncclSuccess;
+    if (d_first_hit && n)
+        e = r->all_reduce(d_first_hit, d_first_hit, n, ncclUint64, ncclMin, ctx->comm, ctx->stream);
+    if (e == ncclSuccess && d_hit_count && n)
+        e = r->all_reduce(d_hit_count, d_hit_count, n, ncclUint64, ncclSum, ctx->comm, ctx->stream);
+    if (e != ncclSuccess)
+        return set_err(MH_E_DEVICE, std::string("ncclAllReduce: ") +
+                                        (r->error_string ? r->error_string(e) : "error"));
+    return MH_OK;
+}
+
+int32_t mh_comm_destroy(mh_ctx* ctx) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    if (ctx->comm && rccl()) (void)rccl()->comm_destroy(ctx->comm);
+    ctx->comm = nullptr;
+    ctx->rank = 0;
+    ctx->world = 1;
     return MH_OK;
 }
 

@@ -94,6 +94,7 @@ private:
         MI m;
         m.op = op;
         m.e64 = e64 ? 1 : 0;
+        m.tag = cur_op_ >= 0 ? (uint8_t)cur_op_ : 0xFF;
         int i = 0;
         for (const Opnd& o : ops) m.o[i++] = o;
         code_.push_back(m);

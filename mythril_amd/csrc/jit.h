@@ -76,6 +76,7 @@ enum Op : uint16_t {
 struct MI {
     uint16_t op;
     uint8_t e64 = 0;
+    uint8_t tag = 0xFF;   // SSA op kind that emitted it (diagnostics; 0xFF = none)
     Opnd o[5];
 };
 

@@ -5,6 +5,11 @@ The reference reaches its native solver (z3) in-process through ctypes as well
 library is loaded from the package directory (built in-tree by ``__graft_entry__.build()``
 or ``make -C mythril_amd/csrc``); a missing library raises ``NativeUnavailable`` — there is
 no CPU fallback on the product path.
+
+One HIP runtime per process: torch ships its own ``libamdhip64`` (same SONAME as ROCm's).  A
+process that also uses torch on the GPU (bench.py, the GPU tests) imports torch and initialises
+CUDA before this library loads, so both bind to torch's copy; the library's RCCL (mh_comm_*) is
+ROCm's, opened with RTLD_DEEPBIND and bound to that same runtime.
 """
 from __future__ import annotations
 
@@ -67,6 +72,10 @@ SIGNATURES = {
     "mh_tapes_jit_info": (C.c_int32, [_vp, _vp]),
     "mh_tapes_jitted": (C.c_int32, [_vp, C.POINTER(C.c_uint8), C.c_uint32]),
     "mh_jit_eval_all": (C.c_int32, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _u32p]),
+    "mh_comm_unique_id": (C.c_int32, [_vp]),
+    "mh_comm_init": (C.c_int32, [_vp, _vp, C.c_int32, C.c_int32]),
+    "mh_comm_allreduce_results": (C.c_int32, [_vp, _vp, _vp, C.c_uint32]),
+    "mh_comm_destroy": (C.c_int32, [_vp]),
     "mh_ctx_enable_timing": (C.c_int32, [_vp, C.c_int32]),
     "mh_ctx_kernel_time": (C.c_int32, [_vp, C.POINTER(C.c_double), _u64p]),
 }
@@ -183,6 +192,16 @@ def device_count() -> int:
     return n.value
 
 
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 creates it; every rank passes it to Context.comm_init)."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    _check(load().mh_comm_unique_id(C.cast(buf, C.c_void_p)))
+    return bytes(buf)
+
+
 def gen_limb(seed: int, var: int, index: int, limb: int) -> int:
     return int(load().mh_gen_limb(seed, var, index, limb))
 
@@ -228,6 +247,19 @@ class Context:
         ms, n = C.c_double(), C.c_uint64()
         _check(self.lib.mh_ctx_kernel_time(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def comm_init(self, unique_id: bytes, rank: int, world: int) -> None:
+        """One RCCL communicator for this ctx (mh_comm_init)."""
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(unique_id)
+        _check(self.lib.mh_comm_init(self.h, C.cast(buf, C.c_void_p), rank, world))
+
+    def comm_allreduce(self, d_first_hit: int, d_hit_count: int, n: int) -> None:
+        """MIN of first witnesses, SUM of counts over the ranks, in place (device buffers)."""
+        _check(self.lib.mh_comm_allreduce_results(self.h, C.c_void_p(d_first_hit),
+                                                  C.c_void_p(d_hit_count), n))
+
+    def comm_destroy(self) -> None:
+        _check(self.lib.mh_comm_destroy(self.h))
 
     def microbench(self, kind: int, waves_per_simd: int = 8) -> float:
         """Sustained lane-ops/s of one instruction kind (mh_microbench_issue; MB_KINDS)."""

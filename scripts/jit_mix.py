@@ -36,6 +36,12 @@ def main():
             for k in range(8):
                 soa[v, k, r] = (a[v] >> (32 * k)) & 0xFFFFFFFF
     tot = dict(valu=0, wide=0, salu=0, div_valu=0, div_wide=0, f64=0)
+    import ctypes as C
+    tagf = emu.lib.emu_jit_tag_valu
+    tagf.restype = None
+    tagf.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    tags = (C.c_uint64 * 512)()
+    tagf(tags, 1)
     m = 0
     for i in range(n):
         res = jit_eval(emu, ts, i, soa)
@@ -45,13 +51,37 @@ def main():
         for k in tot:
             tot[k] += res.dyn[k]
     per = {k: v / m for k, v in tot.items()}
+    tagf(tags, 1)
+    chunks = m * (rows // 64)
+    import re
+    src = open(os.path.join(ROOT, "mythril_amd", "csrc", "dev_isa.h")).read()
+    body = src[src.index("enum mh_dop"):]
+    body = body[body.index("{") + 1:body.index("};")]
+    body = re.sub(r"//[^\n]*", "", body)
+    names, nxt = {}, 0
+    for ent in [e.strip() for e in body.split(",") if e.strip()]:
+        if "=" in ent:
+            nm, val = [x.strip() for x in ent.split("=")]
+            nxt = int(val, 0) if val[0].isdigit() else {v: k for k, v in names.items()}[val]
+        else:
+            nm = ent
+        names[nxt] = nm
+        nxt += 1
+    by_op = {}
+    for t in range(256):
+        for base, suffix in ((0, ""), (256, "/div")):
+            v = tags[base + t]
+            if v:
+                name = names.get(t, "other") if t != 255 else "other"
+                by_op[name + suffix] = round(v / chunks, 2)
+    by_op = dict(sorted(by_op.items(), key=lambda kv: -kv[1]))
     narrow = per["valu"] - per["wide"]
     # issue cycles per wave-evaluation at the measured costs (8 waves / SIMD,
     # profiles/r02e/valu_peak.json): 2-cycle class 2.56, VOP3 / carry / compare / shift 4.5,
     # f64 6.1 (counted inside the wide class)
     cyc = 2.56 * narrow + 4.5 * (per["wide"] - per["f64"]) + 6.1 * per["f64"]
     out = {"tapes": m, "per_wave_eval": per, "issue_cycles_per_wave_eval": cyc,
-           "valu_lane_ops_per_eval": per["valu"]}
+           "valu_lane_ops_per_eval": per["valu"], "valu_per_wave_eval_by_op": by_op}
     if evals:
         wave_evals = evals / 64.0
         out["issue_busy"] = wave_evals * cyc / (1024 * 2.4e9)

@@ -38,6 +38,7 @@ def main():
             rec.update(error="%s: %s" % (type(e).__name__, e),
                        trace=traceback.format_exc().splitlines()[-4:])
         rec["ms"] = (time.perf_counter() - t0) * 1e3
+        rec["extra"] = dict(s.stats.extra)
         rec["stages_ms"] = {k: round((v - before.get(k, 0.0)) * 1e3, 3)
                             for k, v in s.stats.stage_s.items() if v - before.get(k, 0.0) > 0}
         print(json.dumps(rec), flush=True)

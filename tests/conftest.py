@@ -43,6 +43,14 @@ def emu():
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
+    # torch's HIP runtime first, as bench.py does: libmythril_hip then binds to the same
+    # libamdhip64 (one runtime per process)
+    try:
+        import torch
+
+        torch.cuda.init()
+    except Exception:
+        pass
     from mythril_amd import native
 
     if native.device_count() < 1:

@@ -87,6 +87,9 @@ struct Counts {
     uint64_t valu = 0, wide = 0, salu = 0, div_valu = 0, div_wide = 0, f64 = 0;
 } g_counts;
 uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
+// executed VALU by the SSA op kind that emitted it: [tag] body, [256 + tag] inside the division
+// subroutine called by that op (tag 255 = prologue / untagged)
+uint64_t g_tag_valu[512];
 
 bool is_wide(const MI& m) {
     const uint16_t op = m.op;
@@ -97,7 +100,8 @@ bool is_wide(const MI& m) {
            op >= M_V_CVT_F64_U32;
 }
 
-void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int depth = 0) {
+void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int depth = 0,
+         uint8_t caller_tag = 0xFF) {
     std::unordered_map<uint32_t, size_t> lab;
     for (size_t i = 0; i < code.size(); ++i)
         if (code[i].op == M_LABEL) lab[code[i].o[0].v] = i;
@@ -112,6 +116,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
             g_counts.wide += wd;
             g_counts.f64 += m.op >= M_V_CVT_F64_U32;
             if (depth) { ++g_counts.div_valu; g_counts.div_wide += wd; }
+            ++g_tag_valu[depth ? 256 + caller_tag : m.tag];
         } else if (m.op <= M_S_CMP_LT_U32) {
             ++g_counts.salu;
         }
@@ -287,7 +292,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
             case M_CALL_DIV: {
                 if (depth) throw Err{"emulator: nested call"};
                 const uint64_t before = g_counts.div_valu;
-                run(w, div, div, depth + 1);
+                run(w, div, div, depth + 1, m.tag);
                 const uint64_t n = (g_counts.div_valu - before) / 32;
                 ++g_div_hist[n < 31 ? n : 31];
                 break;
@@ -438,6 +443,13 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
 
 extern "C" void emu_jit_op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, int reset) {
     op_stats(valu, wide, count, reset != 0);
+}
+
+extern "C" void emu_jit_tag_valu(uint64_t* out, int reset) {
+    for (int i = 0; i < 512; ++i) {
+        out[i] = g_tag_valu[i];
+        if (reset) g_tag_valu[i] = 0;
+    }
 }
 
 extern "C" void emu_jit_div_hist(uint64_t* out, int reset) {

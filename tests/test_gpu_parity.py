@@ -435,3 +435,31 @@ def test_keccak_message_cuts_on_gpu(gpu_ctx):
             msg = b"".join((vals[i] & ((1 << (8 * nb)) - 1)).to_bytes(nb, "big")
                            for i, nb in enumerate(parts))
             assert got[r] == int.from_bytes(keccak256(msg), "big"), (parts, r)
+
+
+def test_comm_library_path(gpu_ctx):
+    """The library's RCCL exchange (mh_comm_init / mh_comm_allreduce_results) on a one-rank
+    communicator: the all-reduce is the identity and the run's results are unchanged (the 8-GPU
+    path is the same call with world = 8)."""
+    import torch
+
+    ts = synth.generate(16)
+    seed, rows = synth.load_spec()["assignment_seed"], 4096
+    ctx = native.Context(0)
+    try:
+        ctx.comm_init(native.comm_unique_id(), 0, 1)
+        ct = ctx.compile(ts)
+        a = ctx.assignments(ts.n_vars, rows)
+        a.generate(seed, 0)
+        fh0, hc0 = native.run(ctx, ct, a, mode=native.MODE_COUNT_ALL)
+        fh = torch.empty(len(ts.tapes), dtype=torch.int64, device="cuda")
+        hc = torch.empty(len(ts.tapes), dtype=torch.int64, device="cuda")
+        native.results_reset(ctx, fh.data_ptr(), hc.data_ptr(), len(ts.tapes))
+        native.run_async(ctx, ct, a, fh.data_ptr(), hc.data_ptr(), mode=native.MODE_COUNT_ALL)
+        ctx.comm_allreduce(fh.data_ptr(), hc.data_ptr(), len(ts.tapes))
+        ctx.synchronize()
+        assert np.array_equal(fh.cpu().numpy().view(np.uint64), fh0)
+        assert np.array_equal(hc.cpu().numpy().view(np.uint64), hc0)
+        ctx.comm_destroy()
+    finally:
+        ctx.close()
