@@ -46,6 +46,20 @@ def _mask(w: int) -> int:
 
 
 def _merge(xs: List[Alt], ys: List[Alt]) -> List[Alt]:
+    if len(ys) == 1 and not ys[0]:
+        return xs[:MAX_ALTS]
+    if len(xs) == 1 and not xs[0]:
+        return ys[:MAX_ALTS]
+    if len(xs) == 1 and len(ys) == 1:  # the common case (bytes of one word): one pair
+        x, y = xs[0], ys[0]
+        if len(y) < len(x):
+            x, y = y, x
+        for k, v in x.items():
+            if k in y and y[k] != v:
+                return []
+        z = dict(y)
+        z.update(x)
+        return [z]
     out = []
     for x in xs:
         for y in ys:
@@ -152,20 +166,18 @@ class Harvester:
         if op == Op.VAR:
             name = self.col_of_var.get(i0)
             return None if name is None else [{name: value}]
-        if op == Op.CONCAT:
-            wb = b.widths[bb]
-            m_hi, m_lo = mask >> wb, mask & _mask(wb)
-            parts = []
-            for child, m, v in ((a, m_hi, value >> wb), (bb, m_lo, value & _mask(wb))):
+        if op == Op.CONCAT:  # every leaf of the concat tree inverted on its own bit range
+            acc: List[Alt] = [{}]
+            for child, lo, wc in self._concat_leaves(n):
+                m = (mask >> lo) & _mask(wc)
                 if m == 0:
                     continue
-                r = self.invert_bits(child, v, m, depth + 1)
-                if r is None:
-                    r = [{}]
-                parts.append(r)
-            acc: List[Alt] = [{}]
-            for p in parts:
-                acc = _merge(acc, p)
+                r = self.invert_bits(child, (value >> lo) & m, m, depth + 1)
+                if r is None or r == [{}]:
+                    continue
+                acc = _merge(acc, r)
+                if not acc:
+                    return acc
             return acc
         if op == Op.EXTRACT:
             return self.invert_bits(a, value << i1, mask << i1, depth + 1)
@@ -221,6 +233,25 @@ class Harvester:
         if op == Op.BVNEG:
             return self.invert_bits(a, -value & m, m, depth + 1)
         return None
+
+    def _concat_leaves(self, n: int) -> List[Tuple[int, int, int]]:
+        """(leaf node, bit offset, width) of the maximal concat tree rooted at n, low bits first
+        (memoised on the builder: nodes are immutable)."""
+        b = self.b
+        memo = b.__dict__.setdefault("_concat_leaves", {})
+        got = memo.get(n)
+        if got is None:
+            got, stack = [], [(n, 0)]
+            while stack:
+                x, lo = stack.pop()
+                node = b.nodes[x]
+                if node[0] == Op.CONCAT:
+                    stack.append((node[2], lo + b.widths[node[3]]))
+                    stack.append((node[3], lo))
+                else:
+                    got.append((x, lo, b.widths[x]))
+            memo[n] = got
+        return got
 
     def invert_bool(self, n: int, truth: bool, depth: int = 0) -> Optional[List[Alt]]:
         """Partial assignments making Bool node n == truth; None = don't know."""
@@ -390,20 +421,24 @@ class Harvester:
         return got
 
     def harvest(self, root: int, parent: Optional[Alt] = None) -> Guide:
+        from .tape import ARITY
+
         b = self.b
-        self.query_consts = set()
+        nodes, pool_values = b.nodes, b.pool.values
+        self.query_consts = qc = set()
         seen, stack = set(), [root]
         while stack:  # the constants of this query (the pool is shared by all queries)
             n = stack.pop()
             if n in seen:
                 continue
             seen.add(n)
-            op, _, a, bb, c, i0, _ = b.nodes[n]
+            node = nodes[n]
+            op = node[0]
             if op == Op.CONST:
-                self.query_consts.add(b.pool.values[i0])
-            from .tape import ARITY
-
-            stack += [a, bb, c][:ARITY[op]]
+                qc.add(pool_values[node[5]])
+            k = ARITY[op]
+            if k:
+                stack += node[2:2 + k]
         if parent:
             alt = {k: v for k, v in parent.items() if k in self.pools}
             if alt:
@@ -475,10 +510,13 @@ class Harvester:
             if n in seen:
                 continue
             seen.add(n)
-            op, w, a, bb, c, _, _ = b.nodes[n]
+            node = b.nodes[n]
+            op = node[0]
             if op == Op.EQ:
                 out.append(n)
-            stack += [a, bb, c][:ARITY[op]]
+            k = ARITY[op]
+            if k:
+                stack += node[2:2 + k]
         return out
 
     def strip_common(self, x: int, y: int) -> Tuple[int, int]:

@@ -48,6 +48,12 @@ struct mh_ctx {
     // it released, and the last child's destroy frees it
     int32_t children = 0;
     bool released = false;
+    // pinned staging of tape-set uploads (one async copy per compile; the next compile waits on
+    // the event before it refills the buffer)
+    void* h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+    hipEvent_t stage_ev = nullptr;
+    bool stage_pending = false;
 };
 
 namespace {
@@ -102,8 +108,10 @@ hipError_t ctx_dbuf(mh_ctx* c, size_t bytes, void** out) {
     *out = c->d_buf;
     return hipSuccess;
 }
+// smallest class 256 KiB: a query's whole tape set fits one block, so after the first query every
+// compile reuses a block (a hipMalloc of a size the process has not seen costs milliseconds)
 size_t pool_size_class(size_t bytes) {
-    size_t n = 4096;
+    size_t n = 256u << 10;
     while (n < bytes) n <<= 1;
     return n;
 }
@@ -159,6 +167,7 @@ struct mh_tapeset {
     mh_ctx* ctx = nullptr;
     uint32_t n_tapes = 0;
     uint32_t n_vars = 0;
+    void* d_block = nullptr;  // one pool block: insns | ids | tapes | consts
     uint2* d_insns = nullptr;
     mh_dev_tape* d_tapes = nullptr;
     uint32_t* d_consts = nullptr;
@@ -339,6 +348,10 @@ int32_t mh_device_count(int32_t* n) {
     return MH_OK;
 }
 
+namespace {
+void ctx_free(mh_ctx* ctx);
+}
+
 int32_t mh_ctx_create(int32_t device, mh_ctx** out) {
     if (!out) return set_err(MH_E_INVALID, "null out pointer");
     *out = nullptr;
@@ -353,12 +366,30 @@ int32_t mh_ctx_create(int32_t device, mh_ctx** out) {
     c->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    c->own_stream = c->stream != nullptr;
     if (e == hipSuccess) e = hipMalloc(&c->scratch, 64);
+    if (e == hipSuccess) {
+        // one block of the smallest class ready for the first query, and the pinned upload
+        // staging; one round trip through them initialises the runtime's copy path for sizes a
+        // query's first large tape set would otherwise pay for (~30 ms once per process)
+        void* blk = nullptr;
+        const size_t warm = 256u << 10;
+        e = pool_alloc(c, (char**)&blk, warm);
+        if (e == hipSuccess) e = hipHostMalloc(&c->h_stage, 1u << 20, hipHostMallocDefault);
+        if (e == hipSuccess) {
+            c->h_stage_bytes = 1u << 20;
+            std::memset(c->h_stage, 0, warm);
+            e = hipMemcpyAsync(blk, c->h_stage, warm, hipMemcpyHostToDevice, c->stream);
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->h_stage, blk, warm, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (blk) pool_free(c, blk);
+    }
     if (e != hipSuccess) {
-        delete c;
+        ctx_free(c);
         return set_err(MH_E_DEVICE, std::string("ctx init: ") + hipGetErrorString(e));
     }
-    c->own_stream = true;
     *out = c;
     return MH_OK;
 }
@@ -375,6 +406,8 @@ void ctx_free(mh_ctx* ctx) {
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->d_buf) (void)hipFree(ctx->d_buf);
     if (ctx->h_buf) (void)hipHostFree(ctx->h_buf);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
     if (ctx->comm && rccl()) (void)rccl()->comm_destroy(ctx->comm);
     for (auto& kv : ctx->pool_class) (void)hipFree(kv.first);
     delete ctx;
@@ -418,6 +451,9 @@ int32_t mh_ctx_synchronize(mh_ctx* ctx) {
 int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape_offsets,
                          uint32_t n_tapes, const uint32_t* consts, uint32_t n_consts,
                          uint32_t n_vars, mh_tapeset** out) {
+    static const bool trace = std::getenv("MH_TRACE_COMPILE") != nullptr;
+    auto tnow = [] { return std::chrono::steady_clock::now(); };
+    const auto t_start = tnow();
     if (!ctx || !out || (!nodes && n_tapes) || !tape_offsets || (!consts && n_consts))
         return set_err(MH_E_INVALID, "null argument");
     *out = nullptr;
@@ -457,6 +493,7 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     } catch (const std::bad_alloc&) {
         return set_err(MH_E_NOMEM, "host allocation during compile");
     }
+    const auto t_compiled = tnow();
     if (dconsts.empty()) dconsts.assign(8, 0);
     if (words.empty()) words.assign(2, 0);
     // the asm core's scalar prefetch reads the 8 slots from the next instruction on (its words and
@@ -480,24 +517,54 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     ts->ids = std::move(ids);
     for (uint32_t v = 0; v <= mh::kNumVariants; ++v) ts->bucket_off[v] = bucket_off[v];
     ts->info = std::move(info);
-    hipError_t e = pool_alloc(ctx, &ts->d_insns, words.size() * sizeof(uint32_t));
-    if (e == hipSuccess)
-        e = pool_alloc(ctx, &ts->d_ids, std::max<size_t>(1, ts->ids.size()) * sizeof(uint32_t));
-    if (e == hipSuccess && !ts->ids.empty())
-        e = hipMemcpy(ts->d_ids, ts->ids.data(), ts->ids.size() * sizeof(uint32_t),
-                      hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = pool_alloc(ctx, &ts->d_tapes, std::max<size_t>(1, n_tapes) * sizeof(mh_dev_tape));
-    if (e == hipSuccess) e = pool_alloc(ctx, &ts->d_consts, dconsts.size() * sizeof(uint32_t));
-    if (e == hipSuccess)
-        e = hipMemcpy(ts->d_insns, words.data(), words.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess && n_tapes)
-        e = hipMemcpy(ts->d_tapes, heads.data(), n_tapes * sizeof(mh_dev_tape), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(ts->d_consts, dconsts.data(), dconsts.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    // one device block and one async copy from pinned staging (a query compiles a tape set per
+    // call: four synchronous pageable copies cost more than the kernels they feed)
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b_insns = words.size() * sizeof(uint32_t),
+                 b_ids = std::max<size_t>(1, ts->ids.size()) * sizeof(uint32_t),
+                 b_tapes = std::max<size_t>(1, n_tapes) * sizeof(mh_dev_tape),
+                 b_consts = dconsts.size() * sizeof(uint32_t);
+    const size_t o_ids = al(b_insns), o_tapes = o_ids + al(b_ids), o_consts = o_tapes + al(b_tapes),
+                 total = o_consts + al(b_consts);
+    hipError_t e = pool_alloc(ctx, (char**)&ts->d_block, total);
+    if (e == hipSuccess && ctx->stage_pending) {
+        e = hipEventSynchronize(ctx->stage_ev);
+        ctx->stage_pending = false;
+    }
+    if (e == hipSuccess && total > ctx->h_stage_bytes) {
+        if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+        ctx->h_stage = nullptr;
+        ctx->h_stage_bytes = 0;
+        e = hipHostMalloc(&ctx->h_stage, std::max<size_t>(total, 1 << 20), hipHostMallocDefault);
+        if (e == hipSuccess) ctx->h_stage_bytes = std::max<size_t>(total, 1 << 20);
+    }
+    if (e == hipSuccess && !ctx->stage_ev)
+        e = hipEventCreateWithFlags(&ctx->stage_ev, hipEventDisableTiming);
+    if (e == hipSuccess) {
+        char* h = (char*)ctx->h_stage;
+        std::memcpy(h, words.data(), b_insns);
+        if (!ts->ids.empty()) std::memcpy(h + o_ids, ts->ids.data(), ts->ids.size() * sizeof(uint32_t));
+        if (n_tapes) std::memcpy(h + o_tapes, heads.data(), n_tapes * sizeof(mh_dev_tape));
+        std::memcpy(h + o_consts, dconsts.data(), b_consts);
+        char* d = (char*)ts->d_block;
+        ts->d_insns = (uint2*)d;
+        ts->d_ids = (uint32_t*)(d + o_ids);
+        ts->d_tapes = (mh_dev_tape*)(d + o_tapes);
+        ts->d_consts = (uint32_t*)(d + o_consts);
+        e = hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess) e = hipEventRecord(ctx->stage_ev, ctx->stream);
+        if (e == hipSuccess) ctx->stage_pending = true;
+    }
     if (e != hipSuccess) {
         mh_tapes_destroy(ts);
         return set_err(MH_E_DEVICE, std::string("tapeset upload: ") + hipGetErrorString(e));
+    }
+    if (trace) {
+        auto us = [](auto a, auto b) {
+            return std::chrono::duration<double, std::micro>(b - a).count();
+        };
+        fprintf(stderr, "mh_tapes_compile: %u tapes, %zu words, compile %.1f us, upload %.1f us\n",
+                n_tapes, words.size(), us(t_start, t_compiled), us(t_compiled, tnow()));
     }
     *out = ts;
     return MH_OK;
@@ -508,10 +575,7 @@ int32_t mh_tapes_destroy(mh_tapeset* ts) {
     (void)hipSetDevice(ts->ctx->device);
     // kernels of this set may still run on the ctx stream: finish them before the blocks go back
     if (ts->ctx->stream) (void)hipStreamSynchronize(ts->ctx->stream);
-    pool_free(ts->ctx, ts->d_insns);
-    pool_free(ts->ctx, ts->d_tapes);
-    pool_free(ts->ctx, ts->d_consts);
-    pool_free(ts->ctx, ts->d_ids);
+    pool_free(ts->ctx, ts->d_block);
     if (ts->d_ids_rest) (void)hipFree(ts->d_ids_rest);
     for (auto& j : ts->jit) {
         if (j.mod) (void)hipModuleUnload(j.mod);

@@ -272,16 +272,22 @@ class CompiledTapes:
     """mh_tapeset: tapes lowered to device code, resident in HBM."""
 
     def __init__(self, ctx: Context, tapeset: TapeSet):
+        import time
+
         self.ctx = ctx
+        t0 = time.perf_counter()
         nodes, offs, consts = tapeset.flatten()
         nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         consts = np.ascontiguousarray(consts, dtype=np.uint32)
         h = C.c_void_p()
+        t1 = time.perf_counter()
         _check(ctx.lib.mh_tapes_compile(
             ctx.h, nodes.ctypes.data_as(C.c_void_p), _ptr(offs, C.c_uint64), len(tapeset.tapes),
             _ptr(consts), len(tapeset.pool.values), tapeset.n_vars, C.byref(h)))
         self.h = h
+        # host flatten / native compile+upload seconds (per-stage latency reports)
+        self.timing = (t1 - t0, time.perf_counter() - t1)
         self.n_tapes = len(tapeset.tapes)
         self.n_vars = tapeset.n_vars
 

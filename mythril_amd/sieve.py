@@ -209,13 +209,13 @@ class Sieve:
             seen.add(n)
             st.append((n, True))
             op, _, a, bb, c, _, _ = b.nodes[n]
-            st += [(x, False) for x in (a, bb, c)[:ARITY[Op(op)]] if x not in seen]
+            st += [(x, False) for x in (a, bb, c)[:ARITY[op]] if x not in seen]
         for n in order:
             op, _, a, bb, c, i0, _ = b.nodes[n]
             if op == Op.VAR:
                 cols[n] = frozenset((i0,))
             else:
-                kids = (a, bb, c)[:ARITY[Op(op)]]
+                kids = (a, bb, c)[:ARITY[op]]
                 cols[n] = frozenset().union(*(cols[x] for x in kids)) if kids else frozenset()
         parent: Dict[int, int] = {}
 
@@ -285,6 +285,9 @@ class Sieve:
         ct = self.compile(ts)
         t_c = time.perf_counter()
         st.add("compile", t_c - t1)
+        ft, nt = getattr(ct, "timing", (0.0, 0.0))
+        st.add("compile_flatten", ft)
+        st.add("compile_native", nt)
         try:
             assign = self._buffer(len(columns))
             col_index = {c: i for i, c in enumerate(columns)}

@@ -139,11 +139,21 @@ class ConstPool:
         return i
 
     def to_array(self) -> np.ndarray:
-        arr = np.zeros((max(len(self.values), 1), 8), dtype=np.uint32)
-        for i, v in enumerate(self.values):
-            for k in range(8):
-                arr[i, k] = (v >> (32 * k)) & 0xFFFFFFFF
-        return arr
+        """[n, 8] u32 limbs of every value (incremental: a pool shared by a process's queries
+        only converts the values added since the last call)."""
+        n = len(self.values)
+        arr = self.__dict__.get("_arr")
+        done = 0 if arr is None else self.__dict__["_arr_n"]
+        if arr is None or arr.shape[0] < max(n, 1):
+            grown = np.zeros((max(n, 1, 2 * done), 8), dtype=np.uint32)
+            if arr is not None:
+                grown[:done] = arr[:done]
+            arr = self._arr = grown
+        if n > done:
+            buf = b"".join(v.to_bytes(32, "little") for v in self.values[done:n])
+            arr[done:n] = np.frombuffer(buf, dtype="<u4").reshape(n - done, 8)
+        self._arr_n = n
+        return arr[:max(n, 1)]
 
 
 class TapeBuilder:
@@ -280,7 +290,8 @@ class TapeBuilder:
         return self._add(Op.FALSE, BOOL)
 
     def op(self, op: Op, *args: int, imm0: int = 0, imm1: int = 0) -> int:
-        op = Op(op)
+        if op.__class__ is not Op:
+            op = Op(op)
         if op in HOST_ONLY:
             raise TapeError("%s is built with array()/const_array()/store()/select()/apply()"
                             % op.name)
@@ -351,23 +362,19 @@ class TapeBuilder:
                 continue
             seen.add(n)
             stack.append((n, True))
-            op = Op(self.nodes[n][0])
-            k = ARITY[op]
-            for child in reversed(self.nodes[n][2 : 2 + k]):
+            node = self.nodes[n]
+            for child in reversed(node[2 : 2 + ARITY[node[0]]]):
                 if child not in seen:
                     stack.append((child, False))
         remap = {old: new for new, old in enumerate(order)}
-        arr = np.zeros(len(order), dtype=NODE_DTYPE)
-        for new, old in enumerate(order):
+        rows = []
+        flags = self.flags
+        for old in order:
             op, w, a, b, c, i0, i1 = self.nodes[old]
-            k = ARITY[Op(op)]
-            opnds = [a, b, c]
-            for j in range(k):
-                opnds[j] = remap[opnds[j]]
-            for j in range(k, 3):
-                opnds[j] = 0
-            arr[new] = (op, self.flags[old], w, opnds[0], opnds[1], opnds[2], i0, i1)
-        return Tape(arr)
+            k = ARITY[op]
+            rows.append((op, flags[old], w, remap[a] if k > 0 else 0, remap[b] if k > 1 else 0,
+                         remap[c] if k > 2 else 0, i0, i1))
+        return Tape(np.array(rows, dtype=NODE_DTYPE))
 
 
 class Symbols:
