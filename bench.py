@@ -154,13 +154,16 @@ def main() -> None:
         log("microbench failed: %s" % e)
         peak_measured = None
     traffic = valu_busy = exec_ops = None
-    if os.path.exists(PMC_SUMMARY):
-        pmc = json.load(open(PMC_SUMMARY))
-        if pmc.get("tapes") == n_tapes and pmc.get("rows_per_gpu") == rows and \
-                pmc.get("engine", "interp") == args.engine:
-            traffic = pmc.get("hbm_bytes_per_launch")
-            valu_busy = pmc.get("valu_busy")
-            exec_ops = pmc.get("exec_lane_ops_per_launch")
+    pmc_tag = None
+    if os.path.exists(PMC_SUMMARY):  # the committed PMC profile of this exact workload
+        for pmc in json.load(open(PMC_SUMMARY)).get("entries", []):
+            if pmc.get("tapes") == n_tapes and pmc.get("rows_per_gpu") == rows and \
+                    pmc.get("engine", "interp") == args.engine and \
+                    pmc.get("variant", "plain") == args.variant:
+                traffic = pmc.get("hbm_bytes_per_launch")
+                valu_busy = pmc.get("valu_busy")
+                exec_ops = pmc.get("exec_lane_ops_per_launch")
+                pmc_tag = pmc.get("tag")
     line = {
         "metric": "constraint-evals/sec",
         "value": value,
@@ -199,11 +202,19 @@ def main() -> None:
             "frac": achieved / NOMINAL_PEAK_TOPS,
             "traffic": traffic,
             "traffic_unit": "bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, profiles/)",
+            "pmc_profile": pmc_tag,
             "valu_busy_pmc": valu_busy,
             "frac_exec": (exec_ops / (kms / 1e3) / 1e12 / NOMINAL_PEAK_TOPS) if exec_ops else None,
             "exec_lane_ops_per_eval": (exec_ops / (n_tapes * rows)) if exec_ops else None,
             "peak_measured_add_chain": peak_measured,
             "alg_ops_per_eval": alg_ops_per_row / n_tapes,
+            "note": "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (a wave64 VALU op issues over "
+                    "2 cycles; valu_busy_pmc and frac_exec use the same peak). frac prices the "
+                    "SURVEY 8d op-cost table (division family 1100 ops) and exceeds 1 when the "
+                    "kernel does less than the table (JIT: ~130 VALU per division call, demanded "
+                    "limbs, folded constants); frac_exec = executed VALU lane-ops (PMC) / time / "
+                    "peak. Carry, compare, shift, VOP3 and mad ops issue at 4 cycles "
+                    "(profiles/r02e/valu_peak.json): DESIGN.md 5 for the issue-bound argument.",
         },
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -5,7 +5,8 @@ Writes
   profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the bench
   profiles/<tag>/pmc_counters.json  per sieve-kernel PMC sums, one entry per pass
   profiles/<tag>/summary.json       derived figures (below)
-  profiles/pmc_summary.json         the same derived figures, read by bench.py for `traffic`
+  profiles/pmc_summary.json         {"entries": [...]}: the derived figures of the latest profile of
+                                    each (variant, engine, tapes, rows) workload, read by bench.py
 
 Derived figures, per sieve launch group (one mh_run = one launch of each kernel variant the tape
 set needs; the variants run back to back on one stream):
@@ -98,6 +99,7 @@ def main(tag: str) -> None:
         "hbm_bytes_per_launch": sum(v["fetch_bytes_per_launch"] + v["write_bytes_per_launch"]
                                     for v in per_kernel.values()),
         "engine": (pmc_bench or bench)["config"].get("engine", "interp"),
+        "variant": (pmc_bench or bench)["config"].get("variant", "plain"),
         "exec_lane_ops_per_launch": tot_valu * 64,
         "valu_busy": tot_valu * 2 / (1024 * tot_gui) if tot_gui else None,
         "effective_clock_ghz": None,
@@ -107,7 +109,14 @@ def main(tag: str) -> None:
     if pmc_bench and tot_gui:
         summary["effective_clock_ghz"] = tot_gui / (pmc_bench["kernel_ms"] * 1e-3) / 1e9
     json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
-    json.dump(summary, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    entries = []
+    if os.path.exists(path):
+        old = json.load(open(path))
+        entries = old.get("entries", []) if "entries" in old else []
+    key = lambda e: (e.get("variant", "plain"), e.get("engine"), e["tapes"], e["rows_per_gpu"])
+    entries = [e for e in entries if key(e) != key(summary)] + [summary]
+    json.dump({"entries": entries}, open(path, "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
 
