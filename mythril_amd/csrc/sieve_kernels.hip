@@ -1,18 +1,18 @@
-// Sieve kernels for gfx950: the tape interpreter, the assignment generator and a VALU
-// micro-benchmark.
+// Sieve kernels for gfx950: the tape interpreter, the assignment generator and VALU
+// micro-benchmarks.  (Throughput runs over a whole tape set use the per-tape native code of
+// jit.cpp instead; the interpreter serves queries and the tapes the native code does not cover.)
 //
 // Mapping: one lane = one candidate assignment (row); a 256-thread workgroup = 256 consecutive
 // rows; every wave walks the launch's whole tape list, so the tape stream (instruction words,
-// constants) is wave-uniform: instructions arrive 64 at a time in two VGPRs (lane j = instruction
-// j, one coalesced 512-B load) and are extracted with v_readlane into SGPRs; constant operands
-// come through the scalar unit (s_load).  Per-lane 256-bit values live in VGPRs: the accumulator
-// X in 8 fixed registers and the register file as 8 "limb planes", each an ext_vector of NR u32
-// indexed by the wave-uniform register number (s_set_gpr_idx_on / v_mov, no scratch).
-// Assignment columns 0..3 are loaded once per launch into R0..R3 and stay resident for every
-// tape: HBM traffic is 32 B x columns per row per launch, independent of the number of tapes.
-// Tapes are processed in chunks of up to 64 whose instruction words (contiguous in HBM, see
-// mh_tapes_compile) are first staged into LDS by the whole workgroup with one coalesced copy, so
-// instruction fetch never waits on L2.  Per-tape results are reduced per workgroup in LDS and
+// constants) is wave-uniform.  The asm core (asm_core.inc, gen_asm_core.py) takes each
+// instruction's two words, and the next instruction's words plus inline constants, by scalar loads
+// (s_load_dwordx16 into an SGPR bank) from the tape's global copy, issued one handler ahead, and
+// dispatches with one s_setpc_b64 into 256-byte handler slots; the C++ driver below keeps a
+// 64-instruction window in two VGPRs (lane j = instruction j, read with v_readlane) for the
+// complex ops it executes itself.  Per-lane 256-bit values live in VGPRs: the accumulator X and
+// the register file as 8 "limb planes" indexed by the wave-uniform register number
+// (s_set_gpr_idx_on, no scratch).  Assignment columns 0..3 are loaded once per launch into
+// R0..R3 and stay resident for every tape.  Per-tape results are reduced per workgroup in LDS and
 // flushed with one atomic per tape per workgroup.
 //
 // Kernel variants (kernels.h variant_of): NR in {7, 9, 15} x {asm only, + C++ overflow

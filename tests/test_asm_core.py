@@ -158,3 +158,44 @@ def test_next_instruction_prefetch(nr):
         for i in takes:
             assert lines[i - 1] == "s_waitcnt lgkmcnt(0)", name
     assert n_pre > len(G.OPS) // 2
+
+
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_indexed_operands_stay_in_the_register_file(nr):
+    """Every operand the GPR-index mode relocates lands inside the wave's register-file planes
+    for every index the host can encode (register operands are 0..NR, dev_isa.h), so an indexed
+    access can never reach the scratch VGPRs, the driver's values or past the wave's allocation
+    (a co-resident wave's registers).  This rules out an out-of-range index as the cause of the
+    full-occupancy faults of the two-source indexed handlers."""
+    core = G.Core(nr)
+    planes = 8 * (nr + 1)
+    bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
+    bodies += [("fetch", core.fetch_text()), ("commit", core.commit_text())]
+    vreg = re.compile(r"^v(?:(\d+)|\[(\d+):(\d+)\])$")
+    checked = 0
+    for name, lines in bodies:
+        modes = None
+        for ln in lines:
+            if ln.startswith("s_set_gpr_idx_on"):
+                modes = set(re.search(r"gpr_idx\((.*)\)", ln).group(1).split(","))
+                continue
+            if ln.startswith("s_set_gpr_idx_off"):
+                modes = None
+                continue
+            if modes is None or not ln.startswith("v_"):
+                continue
+            mnem, _, rest = ln.partition(" ")
+            ops = [o.strip().lstrip("-") for o in rest.split(",")]
+            dst, srcs = ops[0], ops[1:]
+            if srcs and srcs[0] in ("vcc", "s[62:63]", "s[64:65]") and "_co_" in mnem:
+                srcs = srcs[1:]
+            slots = [("DST", dst)] + list(zip(("SRC0", "SRC1", "SRC2"), srcs))
+            for slot, op in slots:
+                if slot not in modes:
+                    continue
+                m = vreg.match(op)
+                assert m, (name, ln)
+                hi = int(m.group(1) or m.group(3))
+                assert hi + nr < planes, (name, ln, "index reaches v%d" % (hi + nr))
+                checked += 1
+    assert checked > 100
