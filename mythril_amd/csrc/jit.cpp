@@ -1242,7 +1242,7 @@ std::vector<MI> div_routine() {
     const Opnd YNZ = S(S_DIV_YNZ, 2), DUMMY = S(S_DIV_DUMMY, 2), MSK = S(S_DIV_MSK, 2),
                TM = S(S_DIV_TM, 2), K64 = S(S_DIV_F64K, 2), KIND = S(S_DIV_KIND);
     const Opnd K64LO = S(S_DIV_F64K), K64HI = S(S_DIV_F64K + 1);
-    enum : uint32_t { L_UNS = 1, L_DONE, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
+    enum : uint32_t { L_UNS = 1, L_DONE, L_TOP3, L_CONV, L_ZQ, L_NOZQ, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
                       L_SDIV, L_SREM, L_SMOD, L_NARROW = 50, L_NNEG0 = 60, L_NGE0 = 70 };
     auto to_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
         E(M_S_MOV_B32, {K64LO, IMM(0)});
@@ -1267,7 +1267,15 @@ std::vector<MI> div_routine() {
         for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {V(base + k), VCC(), V(base + k), m, VCC()});
     }
     L(L_UNS);
+    // the quotient registers start at 0 for the kinds that return the quotient (the digit steps
+    // write only the digits they compute); remainder kinds leave them as they are
+    E(M_S_CMP_EQ_U32, {KIND, IMM(0)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_ZQ)});
+    E(M_S_CMP_EQ_U32, {KIND, IMM(2)});
+    E(M_S_CBRANCH_SCC0, {LBL(L_NOZQ)});
+    L(L_ZQ);
     for (int k = 0; k < 8; ++k) E(M_V_MOV, {Xr(k), IMM(0)});
+    L(L_NOZQ);
     E(M_V_OR3, {T1, Yr(1), Yr(2), Yr(3)});
     E(M_V_OR3, {T1, T1, Yr(4), Yr(5)});
     E(M_V_OR3, {T1, T1, Yr(6), Yr(7)});
@@ -1282,13 +1290,43 @@ std::vector<MI> div_routine() {
     // every lane's divisor below 2^32: digit-by-digit 64/32 division (L_NARROW)
     E(M_S_CMP_EQ_U64, {TM, IMM(0)});
     E(M_S_CBRANCH_SCC1, {LBL(L_NARROW)});
-    // 1/yd, qd = R/y for the start digit
+    // 1/yd, qd = R/y for the start digit.  When every lane that needs a digit has y >= 2^224,
+    // y's and R's top three limbs give both to 2^-64 relative (R >= y there; lower limbs of R
+    // only shift the estimate by < 2^-64, which the +-1 corrections absorb): 6 f64 ops per
+    // conversion instead of 15
+    auto recip = [&]() {
+        E(M_V_RCP_F64, {FC, FY});
+        E(M_S_NOP, {IMM(1)});  // trans result -> non-trans VALU use needs a wait state
+        E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
+        E(M_V_FMA_F64, {FY, FC, FT, FC});
+    };
+    auto top3_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
+        E(M_S_MOV_B32, {K64LO, IMM(0)});
+        E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});  // 2^32
+        E(M_V_CVT_F64_U32, {dst, limb(7)});
+        for (int k = 6; k >= 5; --k) {
+            E(M_V_CVT_F64_U32, {FT, limb(k)});
+            E(M_V_FMA_F64, {dst, dst, K64, FT});
+        }
+        E(M_S_MOV_B32, {K64HI, IMM((uint32_t)(1023 + 160) << 20)});  // 2^160
+        E(M_V_MUL_F64, {dst, dst, K64});
+    };
+    E(M_V_CMP_NE, {VCC(), IMM(0), Yr(7)});
+    E(M_S_ANDN2_B64, {TM, MSK, VCC()});
+    E(M_S_CBRANCH_SCC0, {LBL(L_TOP3)});
     to_f64(FY, Yl);
-    E(M_V_RCP_F64, {FC, FY});
-    E(M_S_NOP, {IMM(1)});  // trans result -> non-trans VALU use needs a wait state
-    E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
-    E(M_V_FMA_F64, {FY, FC, FT, FC});
+    recip();
     to_f64(FR, Rl);
+    E(M_S_BRANCH, {LBL(L_CONV)});
+    L(L_TOP3);
+    top3_f64(FY, Yl);
+    recip();
+    // lanes outside MSK (x < y, or y = 0) may have y < 2^224, where the top limbs say nothing:
+    // 1/y := 0 there, so every digit estimate is 0 and R keeps x, as their results need
+    E(M_V_CNDMASK, {V(R_FY), IMM(0), V(R_FY), MSK}, true);
+    E(M_V_CNDMASK, {V(R_FY + 1), IMM(0), V(R_FY + 1), MSK}, true);
+    top3_f64(FR, Rl);
+    L(L_CONV);
     E(M_V_MUL_F64, {FC, FR, FY});
     // common case first: every active lane's quotient estimate below 2^31 -> the last step only
     E(M_S_MOV_B32, {K64LO, IMM(0)});

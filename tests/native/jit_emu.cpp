@@ -90,6 +90,7 @@ uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
 // executed VALU by the SSA op kind that emitted it: [tag] body, [256 + tag] inside the division
 // subroutine called by that op (tag 255 = prologue / untagged)
 uint64_t g_tag_valu[512];
+uint64_t g_div_label[128];  // division subroutine: executions of each label (path statistics)
 
 bool is_wide(const MI& m) {
     const uint16_t op = m.op;
@@ -288,7 +289,10 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 }
                 break;
             }
-            case M_LABEL: case M_S_NOP: break;
+            case M_LABEL:
+                if (depth && o[0].v < 128) ++g_div_label[o[0].v];
+                break;
+            case M_S_NOP: break;
             case M_CALL_DIV: {
                 if (depth) throw Err{"emulator: nested call"};
                 const uint64_t before = g_counts.div_valu;
@@ -443,6 +447,13 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
 
 extern "C" void emu_jit_op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, int reset) {
     op_stats(valu, wide, count, reset != 0);
+}
+
+extern "C" void emu_jit_div_labels(uint64_t* out, int reset) {
+    for (int i = 0; i < 128; ++i) {
+        out[i] = g_div_label[i];
+        if (reset) g_div_label[i] = 0;
+    }
 }
 
 extern "C" void emu_jit_tag_valu(uint64_t* out, int reset) {

@@ -86,6 +86,49 @@ def test_division_edges_jit(emu):
         check_tapes(emu, ts, soa_of(pairs, 2))
 
 
+def division_wave_rows(seed):
+    """64-row waves shaped for the division subroutine's uniform paths: (a) every divisor
+    >= 2^224 (the top-three-limb estimate), x above and below y; (b) the same with lanes whose
+    small divisor exceeds x and lanes with y = 0, which sit outside the digit mask; (c) every
+    divisor below 2^32 (the narrow path); (d) negative operands for the signed kinds."""
+    rng = random.Random(seed)
+    M = (1 << 256) - 1
+    rows = []
+    for _ in range(64):  # (a)
+        y = rng.getrandbits(256) | (1 << (224 + rng.randrange(32)))
+        x = rng.choice([rng.getrandbits(256), y + rng.getrandbits(200), y - 1, y, y * 3 & M,
+                        rng.getrandbits(255)])
+        rows.append([x & M, y])
+    for i in range(64):  # (b)
+        if i % 3 == 0:
+            y = rng.getrandbits(256) | (1 << 255 >> rng.randrange(32))
+            rows.append([(y + rng.getrandbits(100)) & M, y])
+        elif i % 3 == 1:
+            y = rng.getrandbits(rng.choice([8, 40, 100, 200])) + 2
+            rows.append([rng.randrange(y), y])
+        else:
+            rows.append([rng.choice([0, 1, rng.getrandbits(256)]), 0])
+    for _ in range(64):  # (c)
+        rows.append([rng.getrandbits(256), rng.getrandbits(rng.choice([1, 8, 31, 32])) + 1])
+    for _ in range(64):  # (d)
+        y = rng.getrandbits(256) | (1 << 255)
+        rows.append([rng.getrandbits(256), y if rng.random() < 0.5 else (-y) & M])
+    return rows
+
+
+def test_division_uniform_paths_jit(emu):
+    ts = TapeSet()
+    b = ts.builder()
+    x, y = b.var("x"), b.var("y")
+    for op in (Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD):
+        ts.add(b.finish(b.op(op, x, y)))
+        # a quotient and a remainder of one tape share a call site
+        ts.add(b.finish(b.op(Op.BVXOR, b.op(op, x, y), b.op(Op.BVUREM, y, b.op(Op.BVADD, x,
+                                                                              b.const(1, 256))))))
+    for seed in range(3):
+        check_tapes(emu, ts, soa_of(division_wave_rows(seed), 2))
+
+
 def test_immediate_and_variable_shifts_jit(emu):
     rng = random.Random(31)
     ts = TapeSet()
