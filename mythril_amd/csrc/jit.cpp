@@ -84,6 +84,7 @@ private:
     uint32_t kstage_ = 0;
     uint32_t n_valu_ = 0, n_wide_ = 0, n_salu_ = 0;
     bool calls_div_ = false;
+    bool uses_lds_ = false;
     int cur_op_ = -1;  // SSA op being emitted (diagnostic attribution)
 public:
     static uint64_t op_valu[256], op_wide[256], op_count[256];
@@ -103,6 +104,7 @@ private:
             const bool wide = e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
                               op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO ||
                               op == M_V_OR3 || op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 ||
+                              op == M_V_LSHL_ADD ||
                               op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
                               (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) || op >= M_V_CVT_F64_U32;
             if (wide) ++n_wide_;
@@ -677,9 +679,17 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
             return;
         }
     }
+    // Through the lane's LDS window (R_LDS): the operand's limbs go to words [D, D+8) between
+    // zero words, and result limb k is the funnel of window words (base + k + 1, base + k) by
+    // the bit part of the amount, base = D + q for right shifts (q = amount >> 5) and
+    // D - q' for left shifts (q' = ceil(amount / 32), bit part (-amount) & 31, a right funnel);
+    // amounts >= 256 read the zero words (q = q' = 8, bit part 0).  Arithmetic right shifts are
+    // logical ones of x ^ s, xor s (s = the sign mask).  This replaces a three-stage select
+    // network of 24 v_cndmask (4-cycle VALU) with 4 LDS writes and <= 5 LDS reads.
+    uses_lds_ = true;
     std::vector<uint32_t> tmp;
     std::vector<int> tp;
-    // amount: q = y0 >> 5 (limbs, bits 7..5), r = y0 & 31; big = y >= 256
+    const uint32_t dm = dem_[d];
     const uint32_t y0 = vgpr_of(B.l[0], tmp);
     const int big = palloc();
     tp.push_back(big);
@@ -704,70 +714,85 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
         emit(M_V_CMP_NE, {VCC(), IMM(0), V(orr)});
         emit(M_S_OR_B64, {P(big), P(big), VCC()});
     }
-    const uint32_t qv = valloc(), rv = valloc(), tv = valloc();
-    tmp.push_back(qv); tmp.push_back(rv); tmp.push_back(tv);
-    emit(M_V_LSHRREV, {V(qv), IMM(5), V(y0)});
-    emit(M_V_AND, {V(rv), IMM(31), V(y0)});
-    // the network's first stage reads the operand's limbs (VGPRs or inline constants) and
-    // writes fresh registers t[k]; later stages update t in place
-    Opnd cur[8];
-    for (int k = 0; k < 8; ++k) cur[k] = vi_of(A.l[k], tmp);
-    uint32_t t[8];
-    for (int k = 0; k < 8; ++k) {
-        t[k] = valloc();
-        tmp.push_back(t[k]);
-    }
-    Opnd fill = IMM(0);
+    free_tmp(tmp);  // the amount's temporaries (y0 stays live in B or is re-read below)
+    // operand limbs into VGPRs (ASHR: x ^ s), two at a time, each pair's temporaries freed as
+    // soon as it is in LDS (register pressure: the network's eight temporaries are gone)
+    uint32_t sgn = ~0u;
     if (arith) {
-        const uint32_t f = valloc();
-        tmp.push_back(f);
-        if (cur[7].k == O_V) emit(M_V_ASHRREV, {V(f), IMM(31), cur[7]});
-        else emit(M_V_MOV, {V(f), IMM((cur[7].v >> 31) ? ~0u : 0u)});
-        fill = V(f);
+        sgn = valloc();
+        const Opnd c7 = vi_of(A.l[7], tmp);
+        if (c7.k == O_V) emit(M_V_ASHRREV, {V(sgn), IMM(31), c7});
+        else emit(M_V_MOV, {V(sgn), IMM((c7.v >> 31) ? ~0u : 0u)});
+        free_tmp(tmp);
     }
-    // lane masks go to an SGPR pair for the e64 v_cndmask: the e32 form with its implicit VCC
-    // mask issues at ~23 cycles on gfx950 (profiles/r02e/valu_peak.json), the e64 form at ~4.6
-    const int sel = palloc();
-    tp.push_back(sel);
-    for (uint32_t st : {4u, 2u, 1u}) {
-        emit(M_V_AND, {V(tv), IMM(st), V(qv)});
-        emit(M_V_CMP_NE, {VCC(), IMM(0), V(tv)});
-        emit(M_S_MOV_B64, {P(sel), VCC()});
-        const bool first = st == 4;
-        auto in = [&](int k) { return first ? cur[k] : V(t[k]); };
-        if (right) {
-            for (int k = 0; k < 8; ++k) {
-                const Opnd s2 = k + (int)st < 8 ? in(k + (int)st) : fill;
-                const Opnd s1 = in(k);
-                emit(M_V_CNDMASK, {V(t[k]), s1, s2, P(sel)}, true);
-            }
-        } else {
-            for (int k = 7; k >= 0; --k) {
-                const Opnd s2 = k - (int)st >= 0 ? in(k - (int)st) : IMM(0);
-                const Opnd s1 = in(k);
-                emit(M_V_CNDMASK, {V(t[k]), s1, s2, P(sel)}, true);
+    for (int i = 0; i < 4; ++i) {
+        uint32_t src[2];
+        for (int h = 0; h < 2; ++h) {
+            const Limb& l = A.l[2 * i + h];
+            if (arith) {
+                src[h] = valloc();
+                const Opnd x = vi_of(l, tmp);
+                tmp.push_back(src[h]);
+                emit(M_V_XOR, {V(src[h]), x, V(sgn)});
+            } else {
+                src[h] = vgpr_of(l, tmp);
             }
         }
+        emit(M_DS_WRITE2ST64, {V(R_LDS), V(src[0]), V(src[1]), IMM(LDS_D + 2 * i),
+                               IMM(LDS_D + 2 * i + 1)});
+        free_tmp(tmp);
     }
-    Val& R = out(d);
-    uint32_t o[8];
-    for (int k = 0; k < 8; ++k) o[k] = valloc();
+    const uint32_t y0r = vgpr_of(B.l[0], tmp);
+    const uint32_t qv = valloc(), rv = valloc(), av = valloc();
+    tmp.push_back(qv); tmp.push_back(rv); tmp.push_back(av);
     if (right) {
-        for (int k = 0; k < 8; ++k)
-            emit(M_V_ALIGNBIT, {V(o[k]), k < 7 ? V(t[k + 1]) : fill, V(t[k]), V(rv)});
+        emit(M_V_LSHRREV, {V(qv), IMM(5), V(y0r)});
+        emit(M_V_AND, {V(rv), IMM(31), V(y0r)});
     } else {
-        emit(M_V_SUB_U32, {V(tv), IMM(32), V(rv)});
-        emit(M_V_CMP_EQ, {VCC(), IMM(0), V(rv)});
-        emit(M_S_MOV_B64, {P(sel), VCC()});
-        for (int k = 0; k < 8; ++k) {
-            emit(M_V_ALIGNBIT, {V(o[k]), V(t[k]), k > 0 ? V(t[k - 1]) : IMM(0), V(tv)});
-            emit(M_V_CNDMASK, {V(o[k]), V(o[k]), V(t[k]), P(sel)}, true);
+        emit(M_V_ADD_U32, {V(qv), IMM(31), V(y0r)});
+        emit(M_V_LSHRREV, {V(qv), IMM(5), V(qv)});
+        emit(M_V_SUB_U32, {V(rv), IMM(0), V(y0r)});
+        emit(M_V_AND, {V(rv), IMM(31), V(rv)});
+    }
+    emit(M_V_CNDMASK, {V(qv), V(qv), IMM(8), P(big)}, true);
+    emit(M_V_CNDMASK, {V(rv), V(rv), IMM(0), P(big)}, true);
+    // base word: D + q (right) or D - q' = 8 - q' (left); the reads add their word offsets
+    if (!right) emit(M_V_SUB_U32, {V(qv), IMM(LDS_D), V(qv)});
+    emit(M_V_LSHL_ADD, {V(av), V(qv), IMM(8), V(R_LDS)});
+    const uint32_t off0 = right ? LDS_D : 0u;
+    // window words k, k+1 of every demanded result limb k, two per read
+    uint32_t need = 0;
+    for (int k = 0; k < 8; ++k)
+        if ((dm >> k) & 1) need |= 3u << k;
+    std::vector<int> words;
+    for (int j = 0; j < 9; ++j)
+        if ((need >> j) & 1) words.push_back(j);
+    uint32_t w[9];
+    for (size_t i = 0; i < words.size(); i += 2) {
+        if (i + 1 < words.size()) {
+            const uint32_t pr = valloc_pair();
+            tmp.push_back(pr); tmp.push_back(pr + 1);
+            emit(M_DS_READ2ST64, {V(pr, 2), V(av), IMM(off0 + words[i]),
+                                  IMM(off0 + words[i + 1])});
+            w[words[i]] = pr;
+            w[words[i + 1]] = pr + 1;
+        } else {
+            const uint32_t r1 = valloc();
+            tmp.push_back(r1);
+            emit(M_DS_READ_B32, {V(r1), V(av), IMM((off0 + words[i]) * 256u)});
+            w[words[i]] = r1;
         }
     }
+    emit(M_S_WAITCNT_LGKM, {IMM(0)});
+    Val& R = out(d);
     for (int k = 0; k < 8; ++k) {
-        emit(M_V_CNDMASK, {V(o[k]), V(o[k]), right ? fill : IMM(0), P(big)}, true);
-        R.l[k] = Limb::R(o[k]);
+        if (!((dm >> k) & 1)) continue;
+        const uint32_t o = valloc();
+        emit(M_V_ALIGNBIT, {V(o), V(w[k + 1]), V(w[k]), V(rv)});
+        if (arith) emit(M_V_XOR, {V(o), V(o), V(sgn)});
+        R.l[k] = Limb::R(o);
     }
+    if (arith) vrelease(sgn);
     free_tmp(tmp);
     free_tmp_pairs(tp);
 }
@@ -1121,6 +1146,7 @@ TapeCode Emitter::run() {
     tc.code.swap(code_);
     tc.max_vgpr = vhigh_;
     tc.calls_div = calls_div_;
+    tc.uses_lds = uses_lds_;
     tc.n_valu = n_valu_;
     tc.n_valu_wide = n_wide_;
     tc.n_salu = n_salu_;
@@ -1160,6 +1186,7 @@ const char* op_name(uint16_t op) {
         case M_V_CMP_GT: return "v_cmp_gt_u32";
         case M_V_CMP_GE: return "v_cmp_ge_u32";
         case M_V_MAD_U64_U32: return "v_mad_u64_u32";
+        case M_V_LSHL_ADD: return "v_lshl_add_u32";
         case M_V_CVT_F64_U32: return "v_cvt_f64_u32";
         case M_V_FMA_F64: return "v_fma_f64";
         case M_V_RCP_F64: return "v_rcp_f64";
@@ -1535,6 +1562,22 @@ std::string print(const MI& m, const std::string& prefix) {
         snprintf(b, sizeof b, "s_setpc_b64 s[%u:%u]", S_DIV_RA, S_DIV_RA + 1);
         return b;
     }
+    if (m.op == M_DS_WRITE2ST64 || m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32 ||
+        m.op == M_S_WAITCNT_LGKM) {
+        char b[128];
+        const Opnd* o = m.o;
+        if (m.op == M_DS_WRITE2ST64)
+            snprintf(b, sizeof b, "ds_write2st64_b32 v%u, v%u, v%u offset0:%u offset1:%u", o[0].v,
+                     o[1].v, o[2].v, o[3].v, o[4].v);
+        else if (m.op == M_DS_READ2ST64)
+            snprintf(b, sizeof b, "ds_read2st64_b32 v[%u:%u], v%u offset0:%u offset1:%u", o[0].v,
+                     o[0].v + 1, o[1].v, o[2].v, o[3].v);
+        else if (m.op == M_DS_READ_B32)
+            snprintf(b, sizeof b, "ds_read_b32 v%u, v%u offset:%u", o[0].v, o[1].v, o[2].v);
+        else
+            snprintf(b, sizeof b, "s_waitcnt lgkmcnt(%u)", o[0].v);
+        return b;
+    }
     std::string s = op_name(m.op);
     if (m.e64) s += "_e64";
     if (m.op == M_S_NOP) return s + " " + std::to_string(m.o[0].v);
@@ -1564,7 +1607,8 @@ uint32_t code_bytes(const TapeCode& tc) {
         for (const Opnd& o : m.o) lit |= o.k == O_IMM && !is_inline(o.v);
         const bool vop3 = m.e64 || m.op == M_V_OR3 || m.op == M_V_ALIGNBIT ||
                           m.op == M_V_MAD_U64_U32 || m.op == M_V_FMA_F64 || m.op == M_V_MUL_F64 ||
-                          m.op == M_V_MIN_F64;
+                          m.op == M_V_MIN_F64 || m.op == M_V_LSHL_ADD || m.op == M_DS_WRITE2ST64 ||
+                          m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32;
         b += (vop3 || lit) ? 8 : 4;
     }
     return b;
@@ -1616,10 +1660,11 @@ Module build_module(const std::vector<const TapeCode*>& codes,
         m.group_count.push_back((uint32_t)codes.size() - first);
     }
     uint32_t maxv = R_COL0 + 8 * n_vars;
-    bool any_div = false;
+    bool any_div = false, any_lds = false;
     for (const TapeCode* tc : codes) {
         maxv = std::max(maxv, tc->max_vgpr);
         any_div |= tc->calls_div;
+        any_lds |= tc->uses_lds;
     }
     if (any_div) maxv = std::max<uint32_t>(maxv, R_TEMP0);
     maxv = std::max<uint32_t>(maxv, 8);
@@ -1642,6 +1687,22 @@ Module build_module(const std::vector<const TapeCode*>& codes,
     // manually inserted wait states); without it the wave reads a stale wave index
     line(o, "s_nop 1");
     line(o, "v_readfirstlane_b32 s24, v2");
+    if (any_lds) {
+        // this lane's shift window (R_LDS) and its zero words [0, D) and [D + 8, LDS_WORDS)
+        line(o, "v_mul_u32_u24 v%u, 0x%x, v2", R_LDS, LDS_WAVE_BYTES);
+        line(o, "v_lshl_add_u32 v%u, v1, 2, v%u", R_LDS, R_LDS);
+        line(o, "v_mov_b32 v5, 0");
+        for (uint32_t w = 0; w < LDS_WORDS; ++w) {
+            if (w >= LDS_D && w < LDS_D + 8) continue;
+            const uint32_t w2 = w + 1;
+            if (w2 < LDS_WORDS && !(w2 >= LDS_D && w2 < LDS_D + 8)) {
+                line(o, "ds_write2st64_b32 v%u, v5, v5 offset0:%u offset1:%u", R_LDS, w, w2);
+                ++w;
+            } else {
+                line(o, "ds_write_b32 v%u, v5 offset:%u", R_LDS, w * 256);
+            }
+        }
+    }
     line(o, "s_waitcnt lgkmcnt(0)");
     line(o, "s_lshr_b32 s25, s19, 2");        // rows per wave
     line(o, "s_mul_i32 s26, s2, s19");        // row block * rows per workgroup
@@ -1792,7 +1853,7 @@ Module build_module(const std::vector<const TapeCode*>& codes,
     line(o, ".rodata");
     line(o, ".p2align 6");
     line(o, ".amdhsa_kernel mh_jit");
-    line(o, "  .amdhsa_group_segment_fixed_size 0");
+    line(o, "  .amdhsa_group_segment_fixed_size %u", any_lds ? (uint32_t)LDS_WG_BYTES : 0u);
     line(o, "  .amdhsa_private_segment_fixed_size 0");
     line(o, "  .amdhsa_kernarg_size %u", (uint32_t)sizeof(KernArgs));
     line(o, "  .amdhsa_user_sgpr_count 2");
@@ -1814,7 +1875,7 @@ Module build_module(const std::vector<const TapeCode*>& codes,
     line(o, "      - .offset: 0");
     line(o, "        .size: %u", (uint32_t)sizeof(KernArgs));
     line(o, "        .value_kind: by_value");
-    line(o, "    .group_segment_fixed_size: 0");
+    line(o, "    .group_segment_fixed_size: %u", any_lds ? (uint32_t)LDS_WG_BYTES : 0u);
     line(o, "    .kernarg_segment_align: 8");
     line(o, "    .kernarg_segment_size: %u", (uint32_t)sizeof(KernArgs));
     line(o, "    .max_flat_workgroup_size: 256");

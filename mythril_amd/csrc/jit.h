@@ -60,6 +60,7 @@ enum Op : uint16_t {
     M_V_CNDMASK,   // d = mask ? src1 : src0
     M_V_CMP_EQ, M_V_CMP_NE, M_V_CMP_LT, M_V_CMP_LE, M_V_CMP_GT, M_V_CMP_GE,  // u32
     M_V_MAD_U64_U32,
+    M_V_LSHL_ADD,    // d = (s0 << s1) + s2
     M_V_CVT_F64_U32, M_V_FMA_F64, M_V_RCP_F64, M_V_MUL_F64, M_V_MIN_F64, M_V_CVT_U32_F64,
     M_V_CMP_LE_F64,
     // SALU
@@ -70,6 +71,11 @@ enum Op : uint16_t {
     M_S_CBRANCH_SCC0, M_S_CBRANCH_SCC1, M_S_BRANCH, M_LABEL, M_S_NOP,
     M_CALL_DIV,    // s_getpc / s_add / s_swappc into the division subroutine
     M_RET,         // s_setpc_b64 of the return address (end of the subroutine)
+    // LDS (the variable-shift window, see R_LDS)
+    M_DS_WRITE2ST64,  // addr, data0, data1, IMM offset0, IMM offset1 (units of 256 B)
+    M_DS_READ2ST64,   // dst pair, addr, IMM offset0, IMM offset1 (units of 256 B)
+    M_DS_READ_B32,    // dst, addr, IMM offset (bytes)
+    M_S_WAITCNT_LGKM, // IMM count
     M_NUM_OPS
 };
 
@@ -82,6 +88,7 @@ struct MI {
 
 // ---- register map of the generated kernel (documented in jit.cpp) ----------------------
 enum : uint32_t {
+    R_LDS = 7,           // this lane's LDS byte address of word 0 of its shift window
     R_COL0 = 8,          // assignment column v limb k is v[R_COL0 + 8 v + k]
     R_DIV0 = 40,         // division subroutine registers v[40..79]
     R_DY = 40, R_DR = 48, R_DQ = 56, R_FY = 64, R_FR = 66, R_FC = 68, R_FT = 70,
@@ -97,12 +104,22 @@ enum : uint32_t {
     S_NEXT_FREE = 92,
 };
 
+// Variable shifts go through LDS: each lane owns a window of LDS_WORDS 32-bit words, word w of
+// lane l of wave i at byte i * LDS_WAVE_BYTES + w * 256 + 4 l (consecutive lanes, consecutive
+// banks).  Words [0, LDS_D) and [LDS_D + 8, LDS_WORDS) stay zero (written once by the kernel
+// prologue); a shift writes its operand's 8 limbs at [LDS_D, LDS_D + 8) and reads 9 words from
+// a per-lane base moved by the limb part of the amount.
+enum : uint32_t {
+    LDS_D = 8, LDS_WORDS = 25, LDS_WAVE_BYTES = LDS_WORDS * 256, LDS_WG_BYTES = 4 * LDS_WAVE_BYTES,
+};
+
 struct TapeCode {
     bool ok = false;
     std::string why;            // reason the tape stays on the interpreter
     std::vector<MI> code;       // body: root mask in s[S_RES:S_RES+1] (or the root value)
     uint32_t max_vgpr = 0;      // highest VGPR used + 1
     bool calls_div = false;
+    bool uses_lds = false;      // variable shifts (the kernel then reserves LDS_WG_BYTES)
     bool root_bool = true;
     uint32_t root_limbs[8];     // values mode: VGPR of each root limb, or ~0u (then constant)
     uint32_t root_const[8];

@@ -28,6 +28,7 @@ namespace {
 
 struct Wave {
     uint32_t v[512][64];
+    uint32_t lds[16384];  // this wave's LDS (64 KiB, byte-addressed by the DS ops)
     uint32_t s[128];
     uint64_t vcc = 0;
     bool scc = false;
@@ -96,7 +97,8 @@ bool is_wide(const MI& m) {
     const uint16_t op = m.op;
     return m.e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
            op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO || op == M_V_OR3 ||
-           op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 || (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) ||
+           op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 || op == M_V_LSHL_ADD ||
+           (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) ||
            op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
            op >= M_V_CVT_F64_U32;
 }
@@ -234,6 +236,11 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 w.set_mask(o[1], cm);
                 break;
             }
+            case M_V_LSHL_ADD:
+                each([&](int l) {
+                    w.v[o[0].v][l] = (w.r32(o[1], l) << (w.r32(o[2], l) & 31)) + w.r32(o[3], l);
+                });
+                break;
             case M_V_CVT_F64_U32: each([&](int l) { w.wf64(o[0], l, (double)w.r32(o[1], l)); }); break;
             case M_V_FMA_F64:
                 each([&](int l) { w.wf64(o[0], l, fma(w.f64(o[1], l), w.f64(o[2], l), w.f64(o[3], l))); });
@@ -302,6 +309,27 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 break;
             }
             case M_RET: return;
+            case M_DS_WRITE2ST64: case M_DS_READ2ST64: case M_DS_READ_B32: {
+                auto word = [&](uint32_t byte) -> uint32_t& {
+                    if ((byte & 3) || byte / 4 >= 16384) throw Err{"emulator: LDS address"};
+                    return w.lds[byte / 4];
+                };
+                for (int l = 0; l < 64; ++l) {
+                    if (m.op == M_DS_WRITE2ST64) {
+                        const uint32_t a = w.v[o[0].v][l];
+                        word(a + o[3].v * 256) = w.v[o[1].v][l];
+                        word(a + o[4].v * 256) = w.v[o[2].v][l];
+                    } else if (m.op == M_DS_READ2ST64) {
+                        const uint32_t a = w.v[o[1].v][l];
+                        w.v[o[0].v][l] = word(a + o[2].v * 256);
+                        w.v[o[0].v + 1][l] = word(a + o[3].v * 256);
+                    } else {
+                        w.v[o[0].v][l] = word(w.v[o[1].v][l] + o[2].v);
+                    }
+                }
+                break;
+            }
+            case M_S_WAITCNT_LGKM: break;
             default: throw Err{"emulator: unknown op " + std::to_string(m.op)};
         }
     }
@@ -366,6 +394,12 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
                 for (int l = 0; l < 64; ++l) w.v[r][l] = 0xDEAD0000u + (uint32_t)r;
             for (int r = 0; r < 128; ++r) w.s[r] = 0xBEEF0000u + (uint32_t)r;
             w.vcc = 0x5555AAAA5555AAAAull;
+            // the kernel prologue's shift windows: lane l of wave 0, zero words outside [D, D+8)
+            for (int l = 0; l < 64; ++l) w.v[R_LDS][l] = 4u * (uint32_t)l;
+            for (uint32_t i = 0; i < 16384; ++i) w.lds[i] = 0xBAD0000u + i;
+            for (uint32_t wd = 0; wd < LDS_WORDS; ++wd)
+                if (wd < LDS_D || wd >= LDS_D + 8)
+                    for (int l = 0; l < 64; ++l) w.lds[wd * 64 + l] = 0;
             for (uint32_t c = 0; c < n_vars; ++c)
                 for (int k = 0; k < 8; ++k)
                     for (int l = 0; l < 64; ++l) {
