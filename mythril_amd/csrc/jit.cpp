@@ -85,6 +85,7 @@ private:
     uint32_t n_valu_ = 0, n_wide_ = 0, n_salu_ = 0;
     bool calls_div_ = false;
     bool uses_lds_ = false;
+    bool calls_kec_ = false;
     int cur_op_ = -1;  // SSA op being emitted (diagnostic attribution)
 public:
     static uint64_t op_valu[256], op_wide[256], op_count[256];
@@ -104,7 +105,7 @@ private:
             const bool wide = e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
                               op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO ||
                               op == M_V_OR3 || op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 ||
-                              op == M_V_LSHL_ADD ||
+                              op == M_V_LSHL_ADD || op == M_V_PERM || op == M_V_BFI ||
                               op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
                               (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) || op >= M_V_CVT_F64_U32;
             if (wide) ++n_wide_;
@@ -254,7 +255,8 @@ private:
     void op_vshift(int d, const Val& A, const Val& B, uint8_t op);
     void op_mul(int d, const Val& A, const Val& B);
     void op_div(int d, int a, int b, int cidx, uint32_t kind, int cur);
-    void rescue_div_regs(int cur);
+    void rescue_div_regs(int cur, uint32_t end = R_TEMP0);
+    void op_keccak(const SsaInsn& v, int cur);
     void demand();
     Val& out(int d) {
         Val& v = vals_[d];
@@ -882,13 +884,13 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
 // The result stays where the subroutine leaves it (the quotient / signed remainders in DQ, the
 // unsigned remainder in DR) until the next call: limbs of live values that sit in the
 // subroutine's registers are moved out just before it (rescue_div_regs).
-void Emitter::rescue_div_regs(int cur) {
+void Emitter::rescue_div_regs(int cur, uint32_t end) {
     std::vector<std::pair<uint32_t, uint32_t>> moved;  // (div register, new register)
     for (size_t r = 0; r < vals_.size(); ++r) {
         Val& v = vals_[r];
         if (!v.defined || v.is_bool || last_[r] <= cur) continue;
         for (Limb& l : v.l) {
-            if (!l.is_r() || l.v < R_DIV0 || l.v >= R_TEMP0) continue;
+            if (!l.is_r() || l.v < R_DIV0 || l.v >= end) continue;
             uint32_t nr = ~0u;
             for (auto& m : moved)
                 if (m.first == l.v) nr = m.second;
@@ -924,6 +926,62 @@ void Emitter::op_div(int d, int a, int b, int cidx, uint32_t kind, int cur) {
     const uint32_t dm = dem_[d], base = kind == 1 ? R_DR : R_DQ;
     for (int k = 0; k < 8; ++k)
         if ((dm >> k) & 1) R.l[k] = Limb::R(base + k);
+}
+
+// KECCAK (exec.h keccak_words): the caller absorbs the message words straight into the
+// subroutine's state registers (byte-swapped by v_perm_b32; constants swapped on the host),
+// zeroes the rest, sets the pad bits, calls the permutation and byte-swaps the first 8 output
+// words out of wherever the subroutine's renaming leaves them.
+void Emitter::op_keccak(const SsaInsn& v, int cur) {
+    calls_kec_ = true;
+    rescue_div_regs(cur, R_TEMP_KEC);
+    const uint32_t nw = (v.w1raw >> 8) & 3u, full = (v.w1raw >> 10) & 1u;
+    if (nw < 1 || nw > 3) fail("keccak: bad word count");
+    const int ops[3] = {v.a, v.b, v.c};
+    // message limbs; a dying operand inside the state registers is copied out first (the
+    // absorb overwrites those registers)
+    Limb src[3][8];
+    std::vector<uint32_t> tmp;
+    for (uint32_t i = 0; i < nw; ++i) {
+        const Val& W = val(ops[i]);
+        for (int k = 0; k < 8; ++k) {
+            src[i][k] = W.l[k];
+            if (src[i][k].k == L_UNDEF) fail("internal: keccak over an undemanded limb");
+            if (src[i][k].is_r() && src[i][k].v >= R_KEC0 && src[i][k].v < R_TEMP_KEC) {
+                const uint32_t r = valloc();
+                tmp.push_back(r);
+                emit(M_V_MOV, {V(r), V(src[i][k].v)});
+                src[i][k] = Limb::R(r);
+            }
+        }
+    }
+    emit(M_S_MOV_B32, {S(S_PERM_SEL), IMM(0x00010203u)});  // byte swap
+    for (uint32_t i = 0; i < nw; ++i)
+        for (int t = 0; t < 4; ++t)
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t dst = R_KEC0 + 2 * (4 * i + t) + h;
+                const Limb& l = src[i][h ? 6 - 2 * t : 7 - 2 * t];
+                if (l.is_c()) emit(M_V_MOV, {V(dst), IMM(__builtin_bswap32(l.v))});
+                else emit(M_V_PERM, {V(dst), IMM(0), V(l.v), S(S_PERM_SEL)});
+            }
+    free_tmp(tmp);
+    for (uint32_t lane = 4 * nw; lane < 25; ++lane)
+        for (uint32_t h = 0; h < 2; ++h) {
+            uint32_t x = 0;
+            if (full && lane == 4 * nw && h == 0) x = 1u;         // pad byte 0x01
+            if (lane == 16 && h == 1) x = 0x80000000u;            // byte 135: 0x80
+            emit(M_V_MOV, {V(R_KEC0 + 2 * lane + h), IMM(x)});
+        }
+    emit(M_CALL_KEC, {IMM((uint32_t)code_.size())});
+    const KecCode& kc = kec_routine();
+    Val& R = out(v.d);
+    const uint32_t dm = dem_[v.d];
+    for (int k = 0; k < 8; ++k) {
+        if (!((dm >> k) & 1)) continue;
+        const uint32_t r = valloc();
+        emit(M_V_PERM, {V(r), IMM(0), V(kc.out[7 - k]), S(S_PERM_SEL)});
+        R.l[k] = Limb::R(r);
+    }
 }
 
 void Emitter::demand() {
@@ -988,6 +1046,10 @@ void Emitter::demand() {
                            (op >= D_UDIV_R && op <= D_SMOD_C)) {
                     D(v.a, 0xFF);
                     D(v.b, 0xFF);
+                } else if (op == D_KECCAK) {
+                    D(v.a, 0xFF);
+                    D(v.b, 0xFF);
+                    D(v.c, 0xFF);
                 } else {  // Bool ops, constants
                     D(v.a, 0);
                 }
@@ -1005,13 +1067,15 @@ TapeCode Emitter::run() {
         const auto& code = st_.code;
         const int nv = st_.n_vregs;
         if (st_.n_pinned != (int)n_vars_ || n_vars_ > 4) fail("assignment columns not pinned");
-        bool has_div = false;
+        bool has_div = false, has_kec = false;
         for (const SsaInsn& v : code) {
+            if (v.op == D_KECCAK) { has_kec = true; continue; }
             if (v.op >= D_FIRST_COMPLEX) fail("complex op (interpreter only)");
             if (v.op >= D_UDIV_R && v.op <= D_SMOD_C) has_div = true;
         }
-        vbase_ = has_div ? R_TEMP0 : R_TEMP_NODIV;
-        vmax_ = std::min<uint32_t>(opt_.max_vgpr, 512);
+        vbase_ = has_kec ? R_TEMP_KEC : has_div ? R_TEMP0 : R_TEMP_NODIV;
+        vmax_ = std::min<uint32_t>(has_kec ? std::max(opt_.max_vgpr, opt_.max_vgpr_keccak)
+                                           : opt_.max_vgpr, 512);
         if (vmax_ <= vbase_ + 16) fail("VGPR budget too small");
         vhigh_ = R_COL0 + 8 * n_vars_;
         vals_.assign(nv, Val());
@@ -1080,6 +1144,7 @@ TapeCode Emitter::run() {
                 case D_UDIV_R: case D_UREM_R: case D_SDIV_R: case D_SREM_R: case D_SMOD_R:
                     op_div(v.d, v.a, v.b, v.cidx, (uint32_t)(op - D_UDIV_R) >> 1, i);
                     break;
+                case D_KECCAK: op_keccak(v, i); break;
                 default:
                     if (op >= D_SHR0 && op <= D_SHR7) {
                         const uint32_t s = 32u * (op - D_SHR0) + (v.aux & 31u);
@@ -1147,6 +1212,7 @@ TapeCode Emitter::run() {
     tc.max_vgpr = vhigh_;
     tc.calls_div = calls_div_;
     tc.uses_lds = uses_lds_;
+    tc.calls_kec = calls_kec_;
     tc.n_valu = n_valu_;
     tc.n_valu_wide = n_wide_;
     tc.n_salu = n_salu_;
@@ -1187,6 +1253,8 @@ const char* op_name(uint16_t op) {
         case M_V_CMP_GE: return "v_cmp_ge_u32";
         case M_V_MAD_U64_U32: return "v_mad_u64_u32";
         case M_V_LSHL_ADD: return "v_lshl_add_u32";
+        case M_V_PERM: return "v_perm_b32";
+        case M_V_BFI: return "v_bfi_b32";
         case M_V_CVT_F64_U32: return "v_cvt_f64_u32";
         case M_V_FMA_F64: return "v_fma_f64";
         case M_V_RCP_F64: return "v_rcp_f64";
@@ -1534,6 +1602,133 @@ std::vector<MI> div_routine() {
     return o;
 }
 
+// ---- the Keccak-f[1600] subroutine ---------------------------------------------------------
+// 24 rounds fully unrolled, each lane's halves renamed instead of moved: theta's column parities
+// and rho's rotations (two v_alignbit per 64-bit lane) and chi's new rows go to free registers and
+// the old ones are freed, so pi costs nothing and the state never moves; the final lane ->
+// register map is fixed at build time (KecCode::out).  chi = b0 ^ (~b1 & b2) as
+// v_bfi_b32(b1, b0, b0 ^ b2).  Per round: 152 two-cycle-class VALU (xor), 108 four-cycle (alignbit,
+// bfi).  Restates keccak_f1600 (u256_ops.h).
+namespace {
+const uint64_t kKeccakRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+// rho + pi along the pi cycle from lane 1: (destination lane, rotation of the lane moved there)
+const int kRhoPi[24][2] = {{10, 1}, {7, 3},   {11, 6},  {17, 10}, {18, 15}, {3, 21},
+                           {5, 28}, {16, 36}, {8, 45},  {21, 55}, {24, 2},  {4, 14},
+                           {15, 27}, {23, 41}, {19, 56}, {13, 8},  {12, 25}, {2, 43},
+                           {20, 62}, {14, 18}, {22, 39}, {9, 61},  {6, 20},  {1, 44}};
+}  // namespace
+
+const KecCode& kec_routine() {
+    static const KecCode kc = [] {
+        KecCode k;
+        std::vector<MI>& o = k.code;
+        auto E = [&](uint16_t op, std::initializer_list<Opnd> ops) {
+            MI m;
+            m.op = op;
+            int i = 0;
+            for (const Opnd& x : ops) m.o[i++] = x;
+            o.push_back(m);
+        };
+        uint32_t map[25][2];
+        for (uint32_t i = 0; i < 25; ++i) {
+            map[i][0] = R_KEC0 + 2 * i;
+            map[i][1] = R_KEC0 + 2 * i + 1;
+        }
+        std::vector<uint32_t> spare;
+        for (uint32_t r = R_KEC0 + N_KEC_REGS; r-- > R_KEC0 + 50;) spare.push_back(r);
+        auto take = [&]() {
+            const uint32_t r = spare.back();
+            spare.pop_back();
+            return r;
+        };
+        auto give = [&](uint32_t r) { spare.push_back(r); };
+        // rotl64 of (lo, hi) by r (1..63, not 32) into two fresh registers
+        auto rotl = [&](uint32_t lo, uint32_t hi, int r, uint32_t* out) {
+            if (r > 32) { std::swap(lo, hi); r -= 32; }
+            out[0] = take();
+            out[1] = take();
+            E(M_V_ALIGNBIT, {V(out[0]), V(lo), V(hi), IMM((uint32_t)(32 - r))});
+            E(M_V_ALIGNBIT, {V(out[1]), V(hi), V(lo), IMM((uint32_t)(32 - r))});
+        };
+        for (int round = 0; round < 24; ++round) {
+            // theta
+            uint32_t c[5][2];
+            for (int x = 0; x < 5; ++x)
+                for (int h = 0; h < 2; ++h) {
+                    c[x][h] = take();
+                    E(M_V_XOR, {V(c[x][h]), V(map[x][h]), V(map[x + 5][h])});
+                    for (int y = 2; y < 5; ++y)
+                        E(M_V_XOR, {V(c[x][h]), V(map[x + 5 * y][h]), V(c[x][h])});
+                }
+            for (int x = 0; x < 5; ++x) {
+                uint32_t d[2];
+                rotl(c[(x + 1) % 5][0], c[(x + 1) % 5][1], 1, d);
+                for (int h = 0; h < 2; ++h) {
+                    E(M_V_XOR, {V(d[h]), V(c[(x + 4) % 5][h]), V(d[h])});
+                    for (int y = 0; y < 5; ++y)
+                        E(M_V_XOR, {V(map[x + 5 * y][h]), V(d[h]), V(map[x + 5 * y][h])});
+                }
+                give(d[0]);
+                give(d[1]);
+            }
+            for (int x = 0; x < 5; ++x) { give(c[x][0]); give(c[x][1]); }
+            // rho + pi
+            uint32_t cur[2] = {map[1][0], map[1][1]};
+            for (int step = 0; step < 24; ++step) {
+                const int dst = kRhoPi[step][0];
+                const uint32_t t[2] = {map[dst][0], map[dst][1]};
+                uint32_t nv[2];
+                rotl(cur[0], cur[1], kRhoPi[step][1], nv);
+                map[dst][0] = nv[0];
+                map[dst][1] = nv[1];
+                give(cur[0]);
+                give(cur[1]);
+                cur[0] = t[0];
+                cur[1] = t[1];
+                // the last step's t is lane 1's original registers, freed by the first step
+            }
+            // chi
+            for (int y = 0; y < 25; y += 5) {
+                uint32_t nrow[5][2];
+                for (int x = 0; x < 5; ++x)
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t b0 = map[y + x][h], b1 = map[y + (x + 1) % 5][h],
+                                       b2 = map[y + (x + 2) % 5][h];
+                        const uint32_t t = take();
+                        E(M_V_XOR, {V(t), V(b0), V(b2)});
+                        nrow[x][h] = take();
+                        E(M_V_BFI, {V(nrow[x][h]), V(b1), V(b0), V(t)});
+                        give(t);
+                    }
+                for (int x = 0; x < 5; ++x)
+                    for (int h = 0; h < 2; ++h) {
+                        give(map[y + x][h]);
+                        map[y + x][h] = nrow[x][h];
+                    }
+            }
+            // iota
+            const uint64_t rc = kKeccakRC[round];
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t w = (uint32_t)(rc >> (32 * h));
+                if (w) E(M_V_XOR, {V(map[0][h]), IMM(w), V(map[0][h])});
+            }
+        }
+        for (int i = 0; i < 4; ++i) {
+            k.out[2 * i] = map[i][0];
+            k.out[2 * i + 1] = map[i][1];
+        }
+        E(M_RET, {});
+        return k;
+    }();
+    return kc;
+}
+
 void op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, bool reset) {
     for (int i = 0; i < 256; ++i) {
         valu[i] = Emitter::op_valu[i];
@@ -1545,15 +1740,16 @@ void op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, bool reset) {
 
 std::string print(const MI& m, const std::string& prefix) {
     if (m.op == M_LABEL) return prefix + "_L" + std::to_string(m.o[0].v) + ":";
-    if (m.op == M_CALL_DIV) {
+    if (m.op == M_CALL_DIV || m.op == M_CALL_KEC) {
         const std::string l = prefix + "_c" + std::to_string(m.o[0].v);
+        const char* tgt = m.op == M_CALL_DIV ? "mh_div" : "mh_kec";
         char b[512];
         snprintf(b, sizeof b,
                  "s_getpc_b64 s[%u:%u]\n%s:\n"
-                 "s_add_u32 s%u, s%u, mh_div - %s\n"
+                 "s_add_u32 s%u, s%u, %s - %s\n"
                  "s_addc_u32 s%u, s%u, 0\n"
                  "s_swappc_b64 s[%u:%u], s[%u:%u]",
-                 S_DIV_TGT, S_DIV_TGT + 1, l.c_str(), S_DIV_TGT, S_DIV_TGT, l.c_str(),
+                 S_DIV_TGT, S_DIV_TGT + 1, l.c_str(), S_DIV_TGT, S_DIV_TGT, tgt, l.c_str(),
                  S_DIV_TGT + 1, S_DIV_TGT + 1, S_DIV_RA, S_DIV_RA + 1, S_DIV_TGT, S_DIV_TGT + 1);
         return b;
     }
@@ -1602,12 +1798,13 @@ uint32_t code_bytes(const TapeCode& tc) {
     uint32_t b = 0;
     for (const MI& m : tc.code) {
         if (m.op == M_LABEL) continue;
-        if (m.op == M_CALL_DIV) { b += 24; continue; }
+        if (m.op == M_CALL_DIV || m.op == M_CALL_KEC) { b += 24; continue; }
         bool lit = false;
         for (const Opnd& o : m.o) lit |= o.k == O_IMM && !is_inline(o.v);
         const bool vop3 = m.e64 || m.op == M_V_OR3 || m.op == M_V_ALIGNBIT ||
                           m.op == M_V_MAD_U64_U32 || m.op == M_V_FMA_F64 || m.op == M_V_MUL_F64 ||
-                          m.op == M_V_MIN_F64 || m.op == M_V_LSHL_ADD || m.op == M_DS_WRITE2ST64 ||
+                          m.op == M_V_MIN_F64 || m.op == M_V_LSHL_ADD || m.op == M_V_PERM ||
+                          m.op == M_V_BFI || m.op == M_DS_WRITE2ST64 ||
                           m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32;
         b += (vop3 || lit) ? 8 : 4;
     }
@@ -1660,12 +1857,14 @@ Module build_module(const std::vector<const TapeCode*>& codes,
         m.group_count.push_back((uint32_t)codes.size() - first);
     }
     uint32_t maxv = R_COL0 + 8 * n_vars;
-    bool any_div = false, any_lds = false;
+    bool any_div = false, any_lds = false, any_kec = false;
     for (const TapeCode* tc : codes) {
         maxv = std::max(maxv, tc->max_vgpr);
         any_div |= tc->calls_div;
         any_lds |= tc->uses_lds;
+        any_kec |= tc->calls_kec;
     }
+    if (any_kec) maxv = std::max<uint32_t>(maxv, R_TEMP_KEC);
     if (any_div) maxv = std::max<uint32_t>(maxv, R_TEMP0);
     maxv = std::max<uint32_t>(maxv, 8);
     maxv = (maxv + 7) & ~7u;
@@ -1846,6 +2045,11 @@ Module build_module(const std::vector<const TapeCode*>& codes,
         line(o, ".p2align 6");
         line(o, "mh_div:");
         print_list(div_routine(), "mh_dv", o);
+    }
+    if (any_kec) {
+        line(o, ".p2align 6");
+        line(o, "mh_kec:");
+        print_list(kec_routine().code, "mh_kc", o);
     }
     line(o, ".Lmh_jit_end:");
     line(o, ".size mh_jit, .Lmh_jit_end-mh_jit");

@@ -61,6 +61,8 @@ enum Op : uint16_t {
     M_V_CMP_EQ, M_V_CMP_NE, M_V_CMP_LT, M_V_CMP_LE, M_V_CMP_GT, M_V_CMP_GE,  // u32
     M_V_MAD_U64_U32,
     M_V_LSHL_ADD,    // d = (s0 << s1) + s2
+    M_V_PERM,        // v_perm_b32 d, s0, s1, sel (byte select from {s0, s1})
+    M_V_BFI,         // d = (s0 & s1) | (~s0 & s2)
     M_V_CVT_F64_U32, M_V_FMA_F64, M_V_RCP_F64, M_V_MUL_F64, M_V_MIN_F64, M_V_CVT_U32_F64,
     M_V_CMP_LE_F64,
     // SALU
@@ -71,6 +73,7 @@ enum Op : uint16_t {
     M_S_CBRANCH_SCC0, M_S_CBRANCH_SCC1, M_S_BRANCH, M_LABEL, M_S_NOP,
     M_CALL_DIV,    // s_getpc / s_add / s_swappc into the division subroutine
     M_RET,         // s_setpc_b64 of the return address (end of the subroutine)
+    M_CALL_KEC,    // the same into the Keccak-f[1600] subroutine
     // LDS (the variable-shift window, see R_LDS)
     M_DS_WRITE2ST64,  // addr, data0, data1, IMM offset0, IMM offset1 (units of 256 B)
     M_DS_READ2ST64,   // dst pair, addr, IMM offset0, IMM offset1 (units of 256 B)
@@ -95,13 +98,17 @@ enum : uint32_t {
     R_CARRY = 72, R_MAD = 74, R_C = 76, R_T1 = 77, R_SX = 78, R_SY = 79,
     R_TEMP0 = 80,        // first free VGPR of a tape that can call the division subroutine
     R_TEMP_NODIV = 40,   // ... and of one that cannot
+    R_KEC0 = 40,         // Keccak-f[1600] subroutine: lane i of the state in v[40 + 2i] (low
+    N_KEC_REGS = 62,     // half), v[41 + 2i] (high) on entry; 12 spare registers up to v101
+    R_TEMP_KEC = 102,    // first free VGPR of a tape that hashes
     // SGPRs
     S_RES = 32,          // the tape's root mask
     S_BOOL0 = 40, N_BOOL_PAIRS = 16,   // Bool lane masks s[40:71]
     S_KSTAGE = 72, N_KSTAGE = 4,       // constant staging s72..s75
     S_DIV_RA = 76, S_DIV_TGT = 78, S_DIV_KIND = 80, S_DIV_YNZ = 82, S_DIV_DUMMY = 84,
     S_DIV_MSK = 86, S_DIV_TM = 88, S_DIV_F64K = 90,
-    S_NEXT_FREE = 92,
+    S_PERM_SEL = 92,     // v_perm_b32 byte-swap selector
+    S_NEXT_FREE = 93,
 };
 
 // Variable shifts go through LDS: each lane owns a window of LDS_WORDS 32-bit words, word w of
@@ -120,6 +127,7 @@ struct TapeCode {
     uint32_t max_vgpr = 0;      // highest VGPR used + 1
     bool calls_div = false;
     bool uses_lds = false;      // variable shifts (the kernel then reserves LDS_WG_BYTES)
+    bool calls_kec = false;
     bool root_bool = true;
     uint32_t root_limbs[8];     // values mode: VGPR of each root limb, or ~0u (then constant)
     uint32_t root_const[8];
@@ -129,6 +137,7 @@ struct TapeCode {
 
 struct Options {
     uint32_t max_vgpr = 128;    // VGPR budget of the kernel (occupancy: 512 / max_vgpr waves)
+    uint32_t max_vgpr_keccak = 168;  // ... of tapes that hash (the state holds 62 VGPRs)
 };
 
 // Emit one tape (SSA after folding) with constants from `pool` (8 limbs per entry).
@@ -138,6 +147,14 @@ TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_
 // The division subroutine (x in v[R_DR..], y in v[R_DY..], kind in S_DIV_KIND: 0 udiv, 1 urem,
 // 2 sdiv, 3 srem, 4 smod; result in v[R_DQ..]).
 std::vector<MI> div_routine();
+
+// The Keccak-f[1600] subroutine (fully unrolled, registers renamed from round to round): state
+// on entry as R_KEC0 says; on return lane i half h is in v[out[2 i + h]] for the first 4 lanes.
+struct KecCode {
+    std::vector<MI> code;
+    uint32_t out[8];
+};
+const KecCode& kec_routine();
 
 // Assembly text of one instruction / a list (labels get `prefix`).
 std::string print(const MI& m, const std::string& prefix);

@@ -98,6 +98,7 @@ bool is_wide(const MI& m) {
     return m.e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
            op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO || op == M_V_OR3 ||
            op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 || op == M_V_LSHL_ADD ||
+           op == M_V_PERM || op == M_V_BFI ||
            (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) ||
            op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
            op >= M_V_CVT_F64_U32;
@@ -241,6 +242,29 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                     w.v[o[0].v][l] = (w.r32(o[1], l) << (w.r32(o[2], l) & 31)) + w.r32(o[3], l);
                 });
                 break;
+            case M_V_PERM:
+                each([&](int l) {
+                    const uint64_t src = ((uint64_t)w.r32(o[1], l) << 32) | w.r32(o[2], l);
+                    const uint32_t sel = w.r32(o[3], l);
+                    uint32_t r = 0;
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t s8 = (sel >> (8 * b)) & 0xFF;
+                        uint32_t byte;
+                        if (s8 < 8) byte = (uint32_t)(src >> (8 * s8)) & 0xFF;
+                        else if (s8 == 12) byte = 0;
+                        else if (s8 > 12) byte = 0xFF;
+                        else throw Err{"emulator: v_perm sign-extension selector"};
+                        r |= byte << (8 * b);
+                    }
+                    w.v[o[0].v][l] = r;
+                });
+                break;
+            case M_V_BFI:
+                each([&](int l) {
+                    const uint32_t m = w.r32(o[1], l);
+                    w.v[o[0].v][l] = (m & w.r32(o[2], l)) | (~m & w.r32(o[3], l));
+                });
+                break;
             case M_V_CVT_F64_U32: each([&](int l) { w.wf64(o[0], l, (double)w.r32(o[1], l)); }); break;
             case M_V_FMA_F64:
                 each([&](int l) { w.wf64(o[0], l, fma(w.f64(o[1], l), w.f64(o[2], l), w.f64(o[3], l))); });
@@ -308,6 +332,10 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 ++g_div_hist[n < 31 ? n : 31];
                 break;
             }
+            case M_CALL_KEC:
+                if (depth) throw Err{"emulator: nested call"};
+                run(w, kec_routine().code, div, depth + 1, m.tag);
+                break;
             case M_RET: return;
             case M_DS_WRITE2ST64: case M_DS_READ2ST64: case M_DS_READ_B32: {
                 auto word = [&](uint32_t byte) -> uint32_t& {

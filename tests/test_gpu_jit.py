@@ -112,6 +112,49 @@ def test_jit_synthetic_values(gpu_ctx):
     assert n == 64
 
 
+def test_jit_keccak_values(gpu_ctx):
+    """Keccak-256 in the native code: messages of 1..96 bytes from several pieces (constant
+    pieces swapped on the host) and the keccak variant's tapes, root values against the oracle."""
+    rng = random.Random(405)
+    splits = [[1], [20], [31], [32], [7, 26], [32, 1], [31, 31], [32, 32], [12, 32, 8],
+              [32, 32, 31], [32, 32, 32]]
+    ts = TapeSet()
+    b = ts.builder()
+    xs = [b.var("x%d" % i) for i in range(3)]
+    for parts in splits:
+        node = None
+        for i, nb in enumerate(parts):
+            p = xs[i] if nb == 32 else b.op(Op.EXTRACT, xs[i], imm0=8 * nb - 1, imm1=0)
+            node = p if node is None else b.op(Op.CONCAT, node, p)
+        ts.add(b.finish(b.op(Op.KECCAK, node)))
+    k = b.const(0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE, 256)
+    ts.add(b.finish(b.op(Op.KECCAK, b.op(Op.CONCAT, k, xs[1]))))
+    rows = [[rng.getrandbits(256) for _ in range(3)] for _ in range(130)] + [[0, 0, 0]]
+    n, info = jit_values_match(gpu_ctx, ts, soa_of(rows, 3))
+    assert n == len(ts.tapes)
+    kv = synth.generate(32, keccak=True)
+    seed = synth.load_spec()["assignment_seed"]
+    rows = [smt_eval.gen_assignment(seed, kv.n_vars, r) for r in range(128)]
+    n, _ = jit_values_match(gpu_ctx, kv, soa_of(rows, kv.n_vars))
+    assert n >= 30
+
+
+def test_jit_keccak_variant_counts(gpu_ctx):
+    """The keccak variant through the native code: counts and first hits equal the
+    interpreter's (its C++ Keccak) on 2^16 rows."""
+    ts = synth.generate(160, keccak=True)
+    seed, rows = synth.load_spec()["assignment_seed"], 1 << 16
+    a = gpu_ctx.assignments(ts.n_vars, rows)
+    a.generate(seed, 0)
+    ref = gpu_ctx.compile(ts)
+    fh0, hc0 = native.run(gpu_ctx, ref, a, mode=native.MODE_COUNT_ALL)
+    ct = gpu_ctx.compile(ts)
+    info = ct.jit()
+    assert info["n_jitted"] >= 150
+    fh, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    assert np.array_equal(hc, hc0) and np.array_equal(fh, fh0)
+
+
 def test_jit_counts_match_interpreter_and_oracle(gpu_ctx):
     """Counts and first hits, native vs interpreter (same tape set, same rows) and vs the C
     oracle, at a size that fills the chip (several groups, many row blocks)."""

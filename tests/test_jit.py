@@ -129,6 +129,39 @@ def test_division_uniform_paths_jit(emu):
         check_tapes(emu, ts, soa_of(division_wave_rows(seed), 2))
 
 
+def test_keccak_message_cuts_jit(emu):
+    """Keccak-256 in the native code (the mh_kec subroutine, absorb and byte swaps at the call
+    site) for messages of 1..96 bytes cut from several pieces, plus constant pieces: every value
+    equals the oracle's (which the reference's known answers pin, tests/test_oracle.py)."""
+    rng = random.Random(405)
+    splits = [[1], [5], [20], [31], [32], [7, 26], [32, 1], [20, 32], [31, 31], [32, 32],
+              [12, 32, 8], [32, 32, 1], [30, 3, 32], [32, 32, 31], [32, 32, 32], [8, 8, 8]]
+    ts = TapeSet()
+    b = ts.builder()
+    xs = [b.var("x%d" % i) for i in range(3)]
+    for parts in splits:
+        node = None
+        for i, nb in enumerate(parts):
+            p = xs[i] if nb == 32 else b.op(Op.EXTRACT, xs[i], imm0=8 * nb - 1, imm1=0)
+            node = p if node is None else b.op(Op.CONCAT, node, p)
+        ts.add(b.finish(b.op(Op.KECCAK, node)))
+    # constant words mixed in (swapped on the host) and a hash feeding arithmetic
+    k = b.const(0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE, 256)
+    ts.add(b.finish(b.op(Op.KECCAK, b.op(Op.CONCAT, xs[0], k))))
+    ts.add(b.finish(b.op(Op.KECCAK, b.op(Op.CONCAT, k, xs[1]))))
+    h = b.op(Op.KECCAK, b.op(Op.CONCAT, xs[0], xs[1]))
+    ts.add(b.finish(b.op(Op.BVADD, b.op(Op.BVLSHR, h, b.const(139, 256)), xs[2])))
+    rows = [[rng.getrandbits(256) for _ in range(3)] for _ in range(70)] + [[0, 0, 0]]
+    assert check_tapes(emu, ts, soa_of(rows, 3)) == len(ts.tapes)
+
+
+def test_keccak_variant_tapes_jit(emu):
+    """SURVEY §8d's keccak variant (config 5 plus one keccak256 of 512 bits per tape)."""
+    ts = synth.generate(24, keccak=True)
+    soa = assignment_soa(random.Random(406), ts.n_vars, 64)
+    assert check_tapes(emu, ts, soa, require_all=False) >= 22
+
+
 def test_immediate_and_variable_shifts_jit(emu):
     rng = random.Random(31)
     ts = TapeSet()
