@@ -1261,6 +1261,7 @@ const char* op_name(uint16_t op) {
         case M_V_MUL_F64: return "v_mul_f64";
         case M_V_MIN_F64: return "v_min_f64";
         case M_V_CVT_U32_F64: return "v_cvt_u32_f64";
+        case M_V_FRACT_F64: return "v_fract_f64";
         case M_V_CMP_LE_F64: return "v_cmp_le_f64";
         case M_S_MOV_B32: return "s_mov_b32";
         case M_S_MOV_B64: return "s_mov_b64";
@@ -1455,6 +1456,14 @@ std::vector<MI> div_routine() {
         E(M_V_MIN_F64, {FC, FC, K64});
         E(M_V_CVT_U32_F64, {C, FC});
         E(M_V_CNDMASK, {C, IMM(0), C, YNZ}, true);
+        // the estimate is within 2^-19 of R / (y 2^32j), so c is one too small only in lanes
+        // whose estimate has a fraction above 1 - 2^-18: without such a lane the "R >= y" test
+        // below (a 9-instruction borrow chain) is skipped
+        E(M_V_FRACT_F64, {FT, FC});
+        E(M_S_MOV_B32, {K64LO, IMM(0)});
+        E(M_S_MOV_B32, {K64HI, IMM(0x3feffff8u)});  // 1 - 2^-18
+        E(M_V_CMP_LE_F64, {VCC(), K64, FT});
+        E(M_S_AND_B64, {TM, VCC(), YNZ});
         // R[j..] -= c * y (the product's limbs above limb 7 only feed the borrow)
         E(M_V_MOV, {V(R_CARRY), IMM(0)});
         E(M_V_MOV, {V(R_CARRY + 1), IMM(0)});
@@ -1483,6 +1492,8 @@ std::vector<MI> div_routine() {
         E(M_V_SUB_U32, {C, C, T1});
         L(L_NONEG0 + j);
         // R >= y << 32j (y = 0 lanes excluded): subtract once more, c + 1
+        E(M_S_CMP_EQ_U64, {TM, IMM(0)});
+        E(M_S_CBRANCH_SCC1, {LBL(L_NOGE0 + j)});
         E(M_V_SUB_CO, {T1, VCC(), Rr(j), Yr(0)});
         for (int k = 1; k < 8 - j; ++k) E(M_V_SUBB_CO, {T1, VCC(), Rr(j + k), Yr(k), VCC()});
         for (int k = 8 - j; k < 8; ++k) E(M_V_SUBB_CO, {T1, VCC(), IMM(0), Yr(k), VCC()});

@@ -64,6 +64,7 @@ enum Op : uint16_t {
     M_V_PERM,        // v_perm_b32 d, s0, s1, sel (byte select from {s0, s1})
     M_V_BFI,         // d = (s0 & s1) | (~s0 & s2)
     M_V_CVT_F64_U32, M_V_FMA_F64, M_V_RCP_F64, M_V_MUL_F64, M_V_MIN_F64, M_V_CVT_U32_F64,
+    M_V_FRACT_F64,
     M_V_CMP_LE_F64,
     // SALU
     M_S_MOV_B32, M_S_MOV_B64, M_S_AND_B64, M_S_OR_B64, M_S_XOR_B64, M_S_XNOR_B64,

@@ -282,6 +282,15 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                     w.v[o[0].v][l] = r;
                 });
                 break;
+            case M_V_FRACT_F64:
+                each([&](int l) {
+                    const double x = w.f64(o[1], l);
+                    double r;
+                    if (!isfinite(x)) r = NAN;
+                    else r = fmin(x - floor(x), 0.99999999999999989);
+                    w.wf64(o[0], l, r);
+                });
+                break;
             case M_V_CMP_LE_F64: {
                 uint64_t cm = 0;
                 for (int l = 0; l < 64; ++l)

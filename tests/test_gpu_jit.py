@@ -112,6 +112,22 @@ def test_jit_synthetic_values(gpu_ctx):
     assert n == 64
 
 
+def test_jit_division_digit_boundaries(gpu_ctx):
+    """Quotient digits on an integer boundary (x = q y + {-1, 0, 1}) and the uniform paths of
+    the division subroutine (tests/test_jit.py division_wave_rows), where the hardware's
+    reciprocal decides whether a digit estimate lands one off and a correction must run."""
+    from tests.test_jit import division_wave_rows
+
+    ts = TapeSet()
+    b = ts.builder()
+    x, y = b.var("x"), b.var("y")
+    for op in (Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD):
+        ts.add(b.finish(b.op(op, x, y)))
+    for seed in range(4):
+        n, _ = jit_values_match(gpu_ctx, ts, soa_of(division_wave_rows(seed), 2))
+        assert n == len(ts.tapes)
+
+
 def test_jit_keccak_values(gpu_ctx):
     """Keccak-256 in the native code: messages of 1..96 bytes from several pieces (constant
     pieces swapped on the host) and the keccak variant's tapes, root values against the oracle."""

@@ -463,3 +463,24 @@ def test_comm_library_path(gpu_ctx):
         ctx.comm_destroy()
     finally:
         ctx.close()
+
+
+def test_handles_outlive_their_context(gpu_ctx):
+    """Tape sets and assignment buffers keep their context alive: destroying the context first
+    and the children afterwards (Python's garbage collector picks any order) is safe, and the
+    device pool of a context is reused by its next tape sets."""
+    ts = synth.generate(8)
+    ctx = native.Context(0)
+    a = ctx.assignments(ts.n_vars, 1024)
+    a.generate(1, 0)
+    cts = [ctx.compile(ts) for _ in range(3)]
+    fh, hc = native.run(ctx, cts[0], a, mode=native.MODE_COUNT_ALL)
+    for ct in cts[1:]:
+        ct.close()
+    ct = ctx.compile(ts)  # a block from the pool
+    fh2, hc2 = native.run(ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    assert np.array_equal(fh, fh2) and np.array_equal(hc, hc2)
+    ctx.close()           # released, not freed: three children remain
+    ct.close()
+    cts[0].close()
+    a.close()             # the last child frees the context

@@ -113,6 +113,11 @@ def division_wave_rows(seed):
     for _ in range(64):  # (d)
         y = rng.getrandbits(256) | (1 << 255)
         rows.append([rng.getrandbits(256), y if rng.random() < 0.5 else (-y) & M])
+    for i in range(128):  # (e) x = q y + {-1, 0, 1}: quotient digits on an integer boundary
+        y = rng.getrandbits(rng.choice([40, 100, 200, 230, 255]))  | 1
+        q = rng.getrandbits(min(32, 256 - y.bit_length()) if i % 2 else 256 - y.bit_length())
+        x = q * y + rng.choice([-1, 0, 0, 1])
+        rows.append([x & M, y])
     return rows
 
 
