@@ -101,8 +101,8 @@ class Guide:
         j = 0
         for prob, alts in self.sets:
             set_prob[j] = prob
-            for alt in alts:
-                for name, v in sorted(alt.items(), key=lambda kv: col_index[kv[0]]):
+            for alt in alts:  # an alternative's entries write distinct columns: any order
+                for name, v in alt.items():
                     e_col.append(col_index[name])
                     e_val.append(v)
                 alt_off.append(len(e_col))
