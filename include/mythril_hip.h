@@ -198,10 +198,14 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
  * code object per slice of tape groups, assembled in-process by comgr and loaded with
  * hipModuleLoadData (src/jit.cpp).  Afterwards mh_run / mh_run_async over the whole tape set run
  * the jitted tapes through that code and the rest through the interpreter; results are
- * identical.  flags: MH_JIT_VALUES also builds the values kernel behind mh_jit_eval_all.
+ * identical.  flags: MH_JIT_VALUES also builds the values kernel behind mh_jit_eval_all;
+ * MH_JIT_FULL_EVAL turns off short-circuit evaluation of root conjunctions (by default a wave
+ * leaves a tape once no row of its 64 satisfies the conjuncts evaluated so far -- the results
+ * are the same either way; the environment variable MH_JIT_SC=0 does the same).
  * max_vgpr: register budget per wave (occupancy = 512 / max_vgpr waves per SIMD), 0 = default
  * 128.  Cost: a few seconds per thousand tapes, once per tape set, outside any timed region.      */
 #define MH_JIT_VALUES 1u
+#define MH_JIT_FULL_EVAL 2u
 typedef struct mh_jit_info {
     uint32_t n_jitted;         /* tapes on the native path                                        */
     uint32_t n_groups;         /* tape groups (grid rows of the JIT kernels)                      */

@@ -893,6 +893,8 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
     const auto t0 = std::chrono::steady_clock::now();
     mh::jit::Options opt;
     opt.max_vgpr = max_vgpr ? max_vgpr : 128;
+    opt.short_circuit = (flags & MH_JIT_FULL_EVAL) == 0;
+    if (const char* e = std::getenv("MH_JIT_SC")) opt.short_circuit = opt.short_circuit && atoi(e) != 0;
     if (opt.max_vgpr > 512 || opt.max_vgpr < 96) return set_err(MH_E_INVALID, "max_vgpr outside 96..512");
     uint32_t threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     if (const char* e = std::getenv("MH_JIT_THREADS")) threads = (uint32_t)std::max(1, atoi(e));

@@ -853,6 +853,57 @@ int fold_constants(Lowering& L, int root_v) {
 
 }  // namespace
 
+void sample_bools(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_rows,
+                  uint64_t seed, const std::vector<int>& want,
+                  std::vector<std::vector<uint8_t>>& out) {
+    out.assign(want.size(), std::vector<uint8_t>(n_rows, 0));
+    std::vector<u32> val((size_t)st.n_vregs * 8, 0u);
+    uint64_t s = seed;
+    auto next = [&]() {
+        s += 0x9E3779B97F4A7C15ull;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    for (uint32_t r = 0; r < n_rows; ++r) {
+        for (int c = 0; c < st.n_pinned; ++c)
+            for (int k = 0; k < 8; k += 2) {
+                const uint64_t x = next();
+                val[(size_t)c * 8 + k] = (u32)x;
+                val[(size_t)c * 8 + k + 1] = (u32)(x >> 32);
+            }
+        for (const SsaInsn& v : st.code) {
+            FoldMachine m;
+            std::memset(m.R, 0, sizeof(m.R));
+            auto ld = [&](int slot, int reg) {
+                if (reg >= 0) std::memcpy(m.R[slot], &val[(size_t)reg * 8], 32);
+            };
+            if (v.op == D_ITE) {  // SSA select (a = cond, b = then, c = else) -> step's D_ITE
+                ld(0, v.b);
+                ld(1, v.a);
+                ld(2, v.c);
+            } else {
+                ld(0, v.a);
+                if (v.cidx >= 0) std::memcpy(m.R[1], pool.data() + 8ull * (uint32_t)v.cidx, 32);
+                else ld(1, v.b);
+                ld(2, v.c);
+            }
+            if (v.op == D_LOADC) std::memcpy(m.R[3], pool.data() + 8ull * (uint32_t)v.cidx, 32);
+            else if (v.op == D_LOADVAR) std::memset(m.R[3], 0, 32);
+            else {
+                const u32 w1 = v.op == D_KECCAK ? v.w1raw
+                                                : (v.op | ((v.width & 0x1FFu) << 8) | (v.aux << 17));
+                step<F_CPLX | F_KECCAK | F_EVM | F_DIV, true>(m, 0u | 1u << 8 | 3u << 16 | 2u << 24,
+                                                               w1, 0u);
+            }
+            std::memcpy(&val[(size_t)v.d * 8], m.R[3], 32);
+        }
+        for (size_t i = 0; i < want.size(); ++i)
+            out[i][r] = want[i] >= 0 ? (uint8_t)(val[(size_t)want[i] * 8] & 1u) : 0;
+    }
+}
+
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,

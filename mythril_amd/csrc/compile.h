@@ -50,6 +50,14 @@ int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* con
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& out,
                        std::string& err);
 
+// Bool values of the SSA registers `want` on n_rows sample rows (each pinned column a uniform
+// 256-bit value from a splitmix64 stream seeded by `seed`), by the device's own instruction
+// semantics (exec.h step).  out[i][r] = value of want[i] on row r.  For ordering conjuncts
+// (jit.cpp schedule_conjuncts); never part of a result.
+void sample_bools(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_rows,
+                  uint64_t seed, const std::vector<int>& want,
+                  std::vector<std::vector<uint8_t>>& out);
+
 // Lower one tape.  Appends its instruction words (2 per instruction) to `words` and any new
 // constants to the shared device pool `dconsts` (8 limbs each, deduplicated via dconst_index).
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,

@@ -58,14 +58,16 @@ struct Val {
     bool defined = false;
 };
 
+enum : uint32_t { LBL_SC_SKIP = 0xFFF0, LBL_SC_END = 0xFFF1 };  // tape-local labels
+
 int top_bit(uint32_t m) { return m ? 31 - __builtin_clz(m) : -1; }
 uint32_t prefix_mask(uint32_t m) { int t = top_bit(m); return t < 0 ? 0u : ((2u << t) - 1u); }
 
 class Emitter {
 public:
     Emitter(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
-            const Options& opt)
-        : st_(st), pool_(pool), n_vars_(n_vars), opt_(opt) {}
+            const Options& opt, const std::vector<uint8_t>* check = nullptr)
+        : st_(st), pool_(pool), n_vars_(n_vars), opt_(opt), check_(check) {}
 
     TapeCode run();
 
@@ -74,6 +76,8 @@ private:
     const std::vector<uint32_t>& pool_;
     uint32_t n_vars_;
     Options opt_;
+    const std::vector<uint8_t>* check_;  // short-circuit test after these vregs (or null)
+    bool sc_used_ = false;
     std::vector<MI> code_;
     std::vector<Val> vals_;
     std::vector<int> last_;
@@ -258,6 +262,7 @@ private:
     void rescue_div_regs(int cur, uint32_t end = R_TEMP0);
     void op_keccak(const SsaInsn& v, int cur);
     void demand();
+    void sc_check(const Val& v);
     Val& out(int d) {
         Val& v = vals_[d];
         v = Val();
@@ -1060,6 +1065,193 @@ void Emitter::demand() {
 
 uint64_t Emitter::op_valu[256], Emitter::op_wide[256], Emitter::op_count[256];
 
+// Short-circuit test after a conjunct (or partial conjunction): leave the tape when no valid lane
+// of the wave is still true.  s_and_b64 sets SCC = (result != 0).
+void Emitter::sc_check(const Val& v) {
+    if (!v.is_bool || v.bconst == 1) return;
+    sc_used_ = true;
+    if (v.bconst == 0) {
+        emit(M_S_BRANCH, {LBL(LBL_SC_SKIP)});
+        return;
+    }
+    emit(M_S_AND_B64, {S(S_SCRATCH, 2), P(v.pair), S(S_VALID, 2)});
+    emit(M_S_CBRANCH_SCC0, {LBL(LBL_SC_SKIP)});
+}
+
+namespace {
+
+// Rough VALU cost of an SSA op in the native code (jit_mix.json's per-op averages), for ordering
+// conjuncts only.
+double sc_cost(const SsaInsn& v) {
+    const uint8_t op = v.op;
+    if (op == D_MUL_R) return 60;
+    if (op >= D_UDIV_R && op <= D_SMOD_C) return 130;
+    if (op == D_SHL_V || op == D_LSHR_V || op == D_ASHR_V) return 35;
+    if (op == D_KECCAK) return 7000;
+    if (op == D_ADD_R || op == D_SUB_R || op == D_RSUB_R) return 10;
+    if (op >= D_EQ_R && op <= D_SGE_C) return 9;
+    if (op == D_AND_R || op == D_OR_R || op == D_XOR_R || op == D_ITE) return 6;
+    if ((op >= D_SHR0 && op <= D_SHR7) || (op >= D_SHL0 && op <= D_SHL7)) return 4;
+    if (op >= D_BAND && op <= D_BITE) return 1;
+    return 0.5;
+}
+
+}  // namespace
+
+// Order the conjuncts of a root AND chain for short-circuit evaluation.  Each conjunct needs the
+// SSA instructions of its operand cone that are not computed yet; conjuncts are taken greedily by
+// (cost of that remainder) / (probability the conjunct ends the evaluation), the classic order
+// for filters.  The probability is measured on sample rows (sample_bools: uniform columns, by
+// the device's semantics), per 64-row wave and conditioned on the conjuncts already placed;
+// without samples, static guesses: an equality rarely holds (0.02), its negation nearly always
+// (0.98), anything else half the time.  The order only moves work, never changes a result.  The
+// chain's ANDs are rebuilt in that order (the last one defines the root), each operand cone is
+// emitted just before the AND that consumes it, in the original relative order.
+bool schedule_impl(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t sample_rows,
+                   SsaTape& out, std::vector<uint8_t>& check) {
+    const auto& code = st.code;
+    const int n = (int)code.size();
+    if (st.root < 0 || !st.root_bool || n == 0) return false;
+    std::vector<int> def(st.n_vregs, -1), uses(st.n_vregs, 0);
+    for (int i = 0; i < n; ++i) {
+        if (code[i].d < 0 || code[i].d >= st.n_vregs) return false;
+        def[code[i].d] = i;
+        for (int r : {code[i].a, code[i].b, code[i].c})
+            if (r >= 0 && r < st.n_vregs) ++uses[r];
+    }
+    if (def[st.root] < 0 || code[def[st.root]].op != D_BAND) return false;
+    // the chain: BANDs reachable from the root through single-use BANDs
+    std::vector<char> chain(n, 0);
+    std::vector<int> conj, stack{st.root};
+    while (!stack.empty()) {
+        const int r = stack.back();
+        stack.pop_back();
+        const int i = r >= 0 ? def[r] : -1;
+        if (i >= 0 && code[i].op == D_BAND && (r == st.root || uses[r] == 1)) {
+            chain[i] = 1;
+            stack.push_back(code[i].b);
+            stack.push_back(code[i].a);
+        } else if (std::find(conj.begin(), conj.end(), r) == conj.end()) {
+            conj.push_back(r);
+        }
+    }
+    if (conj.size() < 2) return false;
+    for (int r : conj)
+        if (r < st.n_pinned || def[r] < 0) return false;
+    // operand cone of each conjunct (chain ANDs excluded), in instruction order
+    std::vector<std::vector<int>> cone(conj.size());
+    for (size_t k = 0; k < conj.size(); ++k) {
+        std::vector<char> seen(n, 0);
+        std::vector<int> st2{def[conj[k]]};
+        seen[def[conj[k]]] = 1;
+        while (!st2.empty()) {
+            const int i = st2.back();
+            st2.pop_back();
+            cone[k].push_back(i);
+            for (int r : {code[i].a, code[i].b, code[i].c}) {
+                if (r < 0 || def[r] < 0 || seen[def[r]]) continue;
+                if (chain[def[r]]) return false;  // a chain AND used inside a conjunct
+                seen[def[r]] = 1;
+                st2.push_back(def[r]);
+            }
+        }
+        std::sort(cone[k].begin(), cone[k].end());
+    }
+    auto reject_p = [&](int r) -> double {
+        const SsaInsn& v = code[def[r]];
+        double pass = 0.5;
+        if (v.op == D_EQ_R) pass = 0.02;
+        else if (v.op == D_FALSE) pass = 0.0;
+        else if (v.op == D_TRUE) pass = 1.0;
+        else if (v.op == D_BNOT && v.a >= 0 && def[v.a] >= 0 && code[def[v.a]].op == D_EQ_R)
+            pass = 0.98;
+        return std::max(1.0 - pass, 0.02);
+    };
+    // measured rejection: each conjunct on sample rows, conditioned on the rows that passed the
+    // conjuncts already placed (correlated conjuncts), counted in waves of 64 rows as the device
+    // leaves a tape per wave; the static guess when no sample row is left
+    std::vector<std::vector<uint8_t>> bits;
+    if (sample_rows) sample_bools(st, pool, sample_rows, 0x5A4D91C3E7B2F601ull, conj, bits);
+    std::vector<uint8_t> alive(sample_rows, 1);
+    uint32_t n_alive = sample_rows;
+    std::vector<char> done(n, 0), taken(conj.size(), 0);
+    std::vector<int> order;
+    for (size_t step = 0; step < conj.size(); ++step) {
+        int best = -1;
+        double best_s = 0;
+        for (size_t k = 0; k < conj.size(); ++k) {
+            if (taken[k]) continue;
+            double c = 0;
+            for (int i : cone[k])
+                if (!done[i]) c += sc_cost(code[i]);
+            double rej = reject_p(conj[k]);
+            if (n_alive) {
+                uint32_t fails = 0;
+                for (uint32_t r = 0; r < sample_rows; ++r) fails += alive[r] && !bits[k][r];
+                rej = (fails + 0.5) / (n_alive + 1.0);
+                {  // a wave leaves only when all its rows fail: the fraction of the sample's
+                   // 64-row waves still alive that this conjunct would end, the row rate as
+                   // the tie-breaker when it ends none
+                    uint32_t wa = 0, wk = 0;
+                    for (uint32_t w0 = 0; w0 + 64 <= sample_rows; w0 += 64) {
+                        bool al = false, st = false;
+                        for (uint32_t r = w0; r < w0 + 64; ++r) {
+                            al |= alive[r] != 0;
+                            st |= alive[r] && bits[k][r];
+                        }
+                        wa += al;
+                        wk += al && !st;
+                    }
+                    if (wa) rej = (wk + rej) / (wa + 1.0);
+                }
+            }
+            const double sc = c / rej;
+            if (best < 0 || sc < best_s) { best = (int)k; best_s = sc; }
+        }
+        taken[best] = 1;
+        order.push_back(best);
+        for (int i : cone[best]) done[i] = 1;
+        if (n_alive)
+            for (uint32_t r = 0; r < sample_rows; ++r)
+                if (alive[r] && !bits[best][r]) { alive[r] = 0; --n_alive; }
+    }
+    // every instruction is either in the chain or in some cone (dead code was dropped)
+    for (int i = 0; i < n; ++i)
+        if (!chain[i] && !done[i]) return false;
+    std::vector<int> chain_d;
+    for (int i = 0; i < n; ++i)
+        if (chain[i] && code[i].d != st.root) chain_d.push_back(code[i].d);
+    if (chain_d.size() + 2 < conj.size()) return false;
+    out = st;
+    out.code.clear();
+    check.assign(st.n_vregs, 0);
+    std::fill(done.begin(), done.end(), 0);
+    int acc = -1;
+    size_t next_d = 0;
+    for (size_t s = 0; s < order.size(); ++s) {
+        const int k = order[s];
+        for (int i : cone[k])
+            if (!done[i]) { out.code.push_back(code[i]); done[i] = 1; }
+        if (acc < 0) {
+            acc = conj[k];
+            check[acc] = 1;
+            continue;
+        }
+        SsaInsn a{};
+        a.op = D_BAND;
+        a.d = s + 1 == order.size() ? st.root : chain_d[next_d++];
+        a.a = acc;
+        a.b = conj[k];
+        a.c = -1;
+        a.width = 1;
+        a.cidx = -1;
+        out.code.push_back(a);
+        acc = a.d;
+        if (acc != st.root) check[acc] = 1;
+    }
+    return true;
+}
+
 TapeCode Emitter::run() {
     TapeCode tc;
     tc.alg_ops = st_.alg_ops;
@@ -1176,6 +1368,7 @@ TapeCode Emitter::run() {
                 seen[ns++] = r;
                 release(vals_[r]);
             }
+            if (check_ && (*check_)[v.d]) sc_check(vals_[v.d]);
         }
         // root
         const Val& root = val(st_.root);
@@ -1183,6 +1376,12 @@ TapeCode Emitter::run() {
         if (root.is_bool) {
             if (root.bconst >= 0) emit(M_S_MOV_B64, {S(S_RES, 2), IMM(root.bconst ? ~0u : 0u)});
             else emit(M_S_MOV_B64, {S(S_RES, 2), P(root.pair)});
+            if (sc_used_) {  // a wave with no valid lane left: root mask 0
+                emit(M_S_BRANCH, {LBL(LBL_SC_END)});
+                emit(M_LABEL, {LBL(LBL_SC_SKIP)});
+                emit(M_S_MOV_B64, {S(S_RES, 2), IMM(0)});
+                emit(M_LABEL, {LBL(LBL_SC_END)});
+            }
             for (int k = 0; k < 8; ++k) { tc.root_limbs[k] = ~0u; tc.root_const[k] = 0; }
         } else {
             // hit = value != 0
@@ -1309,6 +1508,11 @@ std::string opnd_str(const Opnd& o, const std::string& prefix) {
 }
 
 }  // namespace
+
+bool schedule_conjuncts(const SsaTape& st, const std::vector<uint32_t>& pool,
+                        uint32_t sample_rows, SsaTape& out, std::vector<uint8_t>& check) {
+    return schedule_impl(st, pool, sample_rows, out, check);
+}
 
 // ---- the division subroutine ---------------------------------------------------------------
 // 256-bit division by f64 digit estimates over 32-bit digits, no normalisation shifts (the
@@ -2189,6 +2393,15 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
 
 TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
                    const Options& opt) {
+    if (opt.short_circuit) {
+        SsaTape sc;
+        std::vector<uint8_t> check;
+        if (schedule_conjuncts(st, pool, opt.sample_rows, sc, check)) {
+            Emitter e(sc, pool, n_vars, opt, &check);
+            TapeCode tc = e.run();
+            if (tc.ok) return tc;  // else (register pressure of the new order): source order
+        }
+    }
     Emitter e(st, pool, n_vars, opt);
     return e.run();
 }

@@ -103,7 +103,9 @@ enum : uint32_t {
     N_KEC_REGS = 62,     // half), v[41 + 2i] (high) on entry; 12 spare registers up to v101
     R_TEMP_KEC = 102,    // first free VGPR of a tape that hashes
     // SGPRs
+    S_VALID = 30,        // valid-lane mask of the current 64-row chunk
     S_RES = 32,          // the tape's root mask
+    S_SCRATCH = 34,      // s[34:35]: scratch between tapes (short-circuit tests inside one)
     S_BOOL0 = 40, N_BOOL_PAIRS = 16,   // Bool lane masks s[40:71]
     S_KSTAGE = 72, N_KSTAGE = 4,       // constant staging s72..s75
     S_DIV_RA = 76, S_DIV_TGT = 78, S_DIV_KIND = 80, S_DIV_YNZ = 82, S_DIV_DUMMY = 84,
@@ -139,7 +141,22 @@ struct TapeCode {
 struct Options {
     uint32_t max_vgpr = 128;    // VGPR budget of the kernel (occupancy: 512 / max_vgpr waves)
     uint32_t max_vgpr_keccak = 168;  // ... of tapes that hash (the state holds 62 VGPRs)
+    // Short-circuit conjunctions: a root AND chain is evaluated conjunct by conjunct (cheapest
+    // and most selective first, schedule_conjuncts) and the wave leaves the tape as soon as no
+    // valid lane (s[30:31]) satisfies the conjuncts so far; its root mask is then 0, the value
+    // every skipped row has, so counts, first hits and Bool root values are unchanged.
+    bool short_circuit = true;
+    // Conjunct order: pass rates measured on this many sample rows (uniform 256-bit columns,
+    // compile.h sample_bools); 0 = static guesses only.
+    uint32_t sample_rows = 256;
 };
+
+// The SSA of `st` reordered for short-circuit evaluation of its root conjunction.  Returns false
+// (out untouched) when the root is not an AND of at least two conjuncts.  check[v] = 1 marks the
+// virtual registers (the first conjunct, then each partial conjunction) after which the emitter
+// tests the running mask.
+bool schedule_conjuncts(const SsaTape& st, const std::vector<uint32_t>& pool,
+                        uint32_t sample_rows, SsaTape& out, std::vector<uint8_t>& check);
 
 // Emit one tape (SSA after folding) with constants from `pool` (8 limbs per entry).
 TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,

@@ -127,6 +127,7 @@ class JitInfo(C.Structure):
 
 
 JIT_VALUES = 1
+JIT_FULL_EVAL = 2
 
 
 class Guide(C.Structure):
@@ -291,10 +292,12 @@ class CompiledTapes:
         self.n_tapes = len(tapeset.tapes)
         self.n_vars = tapeset.n_vars
 
-    def jit(self, values: bool = False, max_vgpr: int = 0) -> dict:
+    def jit(self, values: bool = False, max_vgpr: int = 0, short_circuit: bool = True) -> dict:
         """Compile the tapes the JIT covers to native gfx950 code (mh_tapes_jit); later runs
-        over the whole set use it.  Returns mh_tapes_jit_info as a dict."""
-        _check(self.ctx.lib.mh_tapes_jit(self.h, JIT_VALUES if values else 0, max_vgpr))
+        over the whole set use it.  short_circuit=False evaluates every conjunct of every row
+        (MH_JIT_FULL_EVAL; same results).  Returns mh_tapes_jit_info as a dict."""
+        flags = (JIT_VALUES if values else 0) | (0 if short_circuit else JIT_FULL_EVAL)
+        _check(self.ctx.lib.mh_tapes_jit(self.h, flags, max_vgpr))
         return self.jit_info()
 
     def jit_info(self) -> dict:

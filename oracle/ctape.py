@@ -39,6 +39,8 @@ def lib():
         _lib.ct_count.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                   C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
                                   C.c_void_p, C.c_void_p]
+        _lib.ct_count_lazy.restype = C.c_int
+        _lib.ct_count_lazy.argtypes = _lib.ct_count.argtypes
         _lib.ct_max_threads.restype = C.c_int
     return _lib
 
@@ -64,14 +66,18 @@ def evaluate(ts, tape: int, assignment) -> int:
     return sum(int(out[k]) << (32 * k) for k in range(34))
 
 
-def count(ts, seed: int, row_first: int, rows: int, threads: int = 0, tapes=None):
-    """(hit_count[u64], first_hit[u64]) over generated rows, for tapes[:n] (default all)."""
+def count(ts, seed: int, row_first: int, rows: int, threads: int = 0, tapes=None,
+          short_circuit: bool = False):
+    """(hit_count[u64], first_hit[u64]) over generated rows, for tapes[:n] (default all).
+    short_circuit: evaluate a Bool AND's second operand only when the first holds
+    (ct_count_lazy; same results, less work)."""
     nodes, offs, consts = _flat(ts)
     n = len(ts.tapes) if tapes is None else tapes
     cnt = np.zeros(max(n, 1), dtype=np.uint64)
     first = np.zeros(max(n, 1), dtype=np.uint64)
     th = threads or lib().ct_max_threads()
-    r = lib().ct_count(nodes.ctypes.data, offs.ctypes.data, n, consts.ctypes.data,
+    fn = lib().ct_count_lazy if short_circuit else lib().ct_count
+    r = fn(nodes.ctypes.data, offs.ctypes.data, n, consts.ctypes.data,
                        len(ts.pool.values), ts.n_vars, seed, row_first, rows, th,
                        cnt.ctypes.data, first.ctypes.data)
     if r != 0:
@@ -79,15 +85,17 @@ def count(ts, seed: int, row_first: int, rows: int, threads: int = 0, tapes=None
     return cnt[:n], first[:n]
 
 
-def benchmark(ts, seed: int, seconds: float = 15.0, tapes: int = 100):
+def benchmark(ts, seed: int, seconds: float = 15.0, tapes: int = 100,
+              short_circuit: bool = True):
     """Evals/s of this port on the host cores, on a bounded sample of the bench workload:
-    the first `tapes` tapes over generated rows, rows grown until ~`seconds` of work."""
+    the first `tapes` tapes over generated rows, rows grown until ~`seconds` of work.
+    short_circuit: the lazy evaluator (the scalar counterpart of the device's short circuit)."""
     th = lib().ct_max_threads()
     tapes = min(tapes, len(ts.tapes))
     rows = 256
     while True:
         t0 = time.perf_counter()
-        count(ts, seed, 0, rows, th, tapes)
+        count(ts, seed, 0, rows, th, tapes, short_circuit=short_circuit)
         dt = time.perf_counter() - t0
         if dt >= seconds * 0.5 or rows >= 1 << 26:
             break
@@ -97,8 +105,9 @@ def benchmark(ts, seed: int, seconds: float = 15.0, tapes: int = 100):
         "unit": "evals/s",
         "cores": th,
         "kind": "port",
-        "sample": "oracle/tape_eval.c (OpenMP, %d threads): first %d synthetic tapes x %d "
-                  "generated rows, %.1f s" % (th, tapes, rows, dt),
+        "sample": "oracle/tape_eval.c (OpenMP, %d threads%s): first %d synthetic tapes x %d "
+                  "generated rows, %.1f s" % (th, ", short-circuit ANDs" if short_circuit else "",
+                                             tapes, rows, dt),
     }
 
 

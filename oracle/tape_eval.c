@@ -274,18 +274,10 @@ static int vsigned_lt(const val_t* x, const val_t* y, int w) {
     return vcmp(x, y) < 0;
 }
 
-/* Evaluate one tape; out receives the root (16 limbs).  Returns 0, or -1 on a malformed tape. */
-int ct_eval(const node_t* nd, uint64_t n, const uint32_t* consts, uint32_t n_consts,
-            const uint32_t* assign /* [n_vars][8] */, uint32_t n_vars, uint32_t* out) {
-    static __thread val_t* V = NULL;  /* per-thread scratch, grown on demand */
-    static __thread uint64_t cap = 0;
-    if (n > cap) {
-        free(V);
-        cap = n < 256 ? 256 : n;
-        V = (val_t*)malloc(sizeof(val_t) * cap);
-        if (!V) { cap = 0; return -1; }
-    }
-    for (uint64_t i = 0; i < n; ++i) {
+/* Value of node i from the values V[] of its operands.  Returns 0, or -1 on a malformed node. */
+static int node_value(const node_t* nd, uint64_t i, const uint32_t* consts, uint32_t n_consts,
+                      const uint32_t* assign, uint32_t n_vars, val_t* V) {
+    {
         const node_t* t = &nd[i];
         const int w = t->width;
         val_t z;
@@ -467,10 +459,76 @@ int ct_eval(const node_t* nd, uint64_t n, const uint32_t* consts, uint32_t n_con
         }
         V[i] = z;
     }
-    memcpy(out, V[n - 1].v, sizeof(uint32_t) * NL);
     return 0;
 bad:
     return -1;
+}
+
+static __thread val_t* g_V = NULL;  /* per-thread scratch, grown on demand */
+static __thread uint8_t* g_done = NULL;
+static __thread uint64_t g_cap = 0;
+
+static int scratch(uint64_t n) {
+    if (n <= g_cap) return 0;
+    free(g_V);
+    free(g_done);
+    g_cap = n < 256 ? 256 : n;
+    g_V = (val_t*)malloc(sizeof(val_t) * g_cap);
+    g_done = (uint8_t*)malloc(g_cap);
+    if (!g_V || !g_done) { g_cap = 0; return -1; }
+    return 0;
+}
+
+/* Evaluate one tape; out receives the root (16 limbs).  Returns 0, or -1 on a malformed tape. */
+int ct_eval(const node_t* nd, uint64_t n, const uint32_t* consts, uint32_t n_consts,
+            const uint32_t* assign /* [n_vars][8] */, uint32_t n_vars, uint32_t* out) {
+    if (scratch(n)) return -1;
+    for (uint64_t i = 0; i < n; ++i)
+        if (node_value(nd, i, consts, n_consts, assign, n_vars, g_V)) return -1;
+    memcpy(out, g_V[n - 1].v, sizeof(uint32_t) * NL);
+    return 0;
+}
+
+/* Short-circuit evaluation of node i: operands on demand (memoised in g_done), the second
+ * operand of a Bool AND only when the first holds -- what a scalar evaluator does for a path
+ * condition, so the CPU baseline skips the same work the GPU's wave-level short circuit does. */
+static int lazy(const node_t* nd, uint64_t i, const uint32_t* consts, uint32_t n_consts,
+                const uint32_t* assign, uint32_t n_vars) {
+    if (g_done[i]) return 0;
+    const node_t* t = &nd[i];
+    if (t->op == AND) {
+        if (t->a >= i || t->b >= i) return -1;
+        if (lazy(nd, t->a, consts, n_consts, assign, n_vars)) return -1;
+        if (!(g_V[t->a].v[0] & 1)) {
+            memset(&g_V[i], 0, sizeof(val_t));
+        } else {
+            if (lazy(nd, t->b, consts, n_consts, assign, n_vars)) return -1;
+            memset(&g_V[i], 0, sizeof(val_t));
+            g_V[i].v[0] = g_V[t->b].v[0] & 1;
+        }
+        g_done[i] = 1;
+        return 0;
+    }
+    const uint64_t ops[3] = {t->a, t->b, t->c};
+    const int ar = t->op <= FALSE_ ? 0 : t->op == ITE ? 3 :
+                   (t->op == BVNEG || t->op == BVNOT || t->op == NOT || t->op == EXTRACT ||
+                    t->op == ZEXT || t->op == SEXT || t->op == KECCAK) ? 1 : 2;
+    for (int k = 0; k < ar; ++k) {
+        if (ops[k] >= i) return -1;
+        if (lazy(nd, ops[k], consts, n_consts, assign, n_vars)) return -1;
+    }
+    if (node_value(nd, i, consts, n_consts, assign, n_vars, g_V)) return -1;
+    g_done[i] = 1;
+    return 0;
+}
+
+int ct_eval_lazy(const node_t* nd, uint64_t n, const uint32_t* consts, uint32_t n_consts,
+                 const uint32_t* assign, uint32_t n_vars, uint32_t* out) {
+    if (n == 0 || scratch(n)) return -1;
+    memset(g_done, 0, n);
+    if (lazy(nd, n - 1, consts, n_consts, assign, n_vars)) return -1;
+    memcpy(out, g_V[n - 1].v, sizeof(uint32_t) * NL);
+    return 0;
 }
 
 /* ---- counter-based assignment generator (restated from mh_gen_limb) ------------------------- */
@@ -492,9 +550,10 @@ static void gen_row(uint64_t seed, uint32_t n_vars, uint64_t index, uint32_t* a)
 
 /* Per-tape hit counts and first witnesses over generated rows [row_first, row_first+rows),
  * evaluated on `threads` OpenMP threads.  Returns 0 or -1. */
-int ct_count(const node_t* nodes, const uint64_t* offs, uint32_t n_tapes, const uint32_t* consts,
-             uint32_t n_consts, uint32_t n_vars, uint64_t seed, uint64_t row_first,
-             uint64_t rows, int threads, uint64_t* count, uint64_t* first) {
+static int count_rows(const node_t* nodes, const uint64_t* offs, uint32_t n_tapes,
+                      const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, uint64_t seed,
+                      uint64_t row_first, uint64_t rows, int threads, uint64_t* count,
+                      uint64_t* first, int short_circuit) {
     int err = 0;
     for (uint32_t t = 0; t < n_tapes; ++t) { count[t] = 0; first[t] = ~0ull; }
 #pragma omp parallel num_threads(threads)
@@ -509,8 +568,12 @@ int ct_count(const node_t* nodes, const uint64_t* offs, uint32_t n_tapes, const 
             const uint64_t idx = row_first + (uint64_t)r;
             gen_row(seed, n_vars, idx, a);
             for (uint32_t t = 0; t < n_tapes; ++t) {
-                if (ct_eval(nodes + offs[t], offs[t + 1] - offs[t], consts, n_consts, a, n_vars,
-                            out) != 0) {
+                const int rc = short_circuit
+                    ? ct_eval_lazy(nodes + offs[t], offs[t + 1] - offs[t], consts, n_consts, a,
+                                   n_vars, out)
+                    : ct_eval(nodes + offs[t], offs[t + 1] - offs[t], consts, n_consts, a, n_vars,
+                              out);
+                if (rc != 0) {
                     err = 1;
                     continue;
                 }
@@ -532,6 +595,22 @@ int ct_count(const node_t* nodes, const uint64_t* offs, uint32_t n_tapes, const 
         free(lf);
     }
     return err ? -1 : 0;
+}
+
+int ct_count(const node_t* nodes, const uint64_t* offs, uint32_t n_tapes, const uint32_t* consts,
+             uint32_t n_consts, uint32_t n_vars, uint64_t seed, uint64_t row_first,
+             uint64_t rows, int threads, uint64_t* count, uint64_t* first) {
+    return count_rows(nodes, offs, n_tapes, consts, n_consts, n_vars, seed, row_first, rows,
+                      threads, count, first, 0);
+}
+
+/* The same counts with short-circuit evaluation of Bool ANDs (ct_eval_lazy). */
+int ct_count_lazy(const node_t* nodes, const uint64_t* offs, uint32_t n_tapes,
+                  const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, uint64_t seed,
+                  uint64_t row_first, uint64_t rows, int threads, uint64_t* count,
+                  uint64_t* first) {
+    return count_rows(nodes, offs, n_tapes, consts, n_consts, n_vars, seed, row_first, rows,
+                      threads, count, first, 1);
 }
 
 int ct_max_threads(void) {

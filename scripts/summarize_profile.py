@@ -6,7 +6,7 @@ Writes
   profiles/<tag>/pmc_counters.json  per sieve-kernel PMC sums, one entry per pass
   profiles/<tag>/summary.json       derived figures (below)
   profiles/pmc_summary.json         {"entries": [...]}: the derived figures of the latest profile of
-                                    each (variant, engine, tapes, rows) workload, read by bench.py
+                                    each (variant, engine, tapes, rows, short_circuit) workload, read by bench.py
 
 Derived figures, per sieve launch group (one mh_run = one launch of each kernel variant the tape
 set needs; the variants run back to back on one stream):
@@ -100,6 +100,7 @@ def main(tag: str) -> None:
                                     for v in per_kernel.values()),
         "engine": (pmc_bench or bench)["config"].get("engine", "interp"),
         "variant": (pmc_bench or bench)["config"].get("variant", "plain"),
+        "short_circuit": bool((pmc_bench or bench)["config"].get("short_circuit", False)),
         "exec_lane_ops_per_launch": tot_valu * 64,
         "valu_busy": tot_valu * 2 / (1024 * tot_gui) if tot_gui else None,
         "effective_clock_ghz": None,
@@ -114,7 +115,8 @@ def main(tag: str) -> None:
     if os.path.exists(path):
         old = json.load(open(path))
         entries = old.get("entries", []) if "entries" in old else []
-    key = lambda e: (e.get("variant", "plain"), e.get("engine"), e["tapes"], e["rows_per_gpu"])
+    key = lambda e: (e.get("variant", "plain"), e.get("engine"), e["tapes"], e["rows_per_gpu"],
+                     bool(e.get("short_circuit", False)))
     entries = [e for e in entries if key(e) != key(summary)] + [summary]
     json.dump({"entries": entries}, open(path, "w"), indent=1)
     print(json.dumps(summary, indent=1))

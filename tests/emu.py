@@ -120,6 +120,12 @@ def jit_eval(emu: "Emulator", ts: TapeSet, tape: int, soa: np.ndarray, max_vgpr:
     return JitResult(info, vals, "")
 
 
+def set_short_circuit(emu: "Emulator", on: bool) -> None:
+    """Options::short_circuit of the emulator's JIT builds (default on, like mh_tapes_jit)."""
+    f = _jit_fn(emu.lib, "emu_jit_set_short_circuit", None, [C.c_int])
+    f(int(on))
+
+
 def jit_module(emu: "Emulator", ts: TapeSet, values: bool = False, max_vgpr: int = 128,
                assemble: bool = True):
     """(module text, code object bytes, tapes jitted) for a whole tape set."""

@@ -372,6 +372,9 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
     }
 }
 
+bool g_short_circuit = true;  // Options::short_circuit of the emulated builds
+uint32_t g_sample_rows = Options().sample_rows;
+
 bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                     const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, uint32_t tape,
                     uint32_t max_vgpr, std::vector<uint32_t>& pool, TapeCode& tc, std::string& e) {
@@ -386,6 +389,8 @@ bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes
     }
     Options opt;
     opt.max_vgpr = max_vgpr;
+    opt.short_circuit = g_short_circuit;
+    opt.sample_rows = g_sample_rows;
     tc = emit_tape(st, pool, n_vars, opt);
     return true;
 }
@@ -430,6 +435,12 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
             for (int r = 0; r < 512; ++r)
                 for (int l = 0; l < 64; ++l) w.v[r][l] = 0xDEAD0000u + (uint32_t)r;
             for (int r = 0; r < 128; ++r) w.s[r] = 0xBEEF0000u + (uint32_t)r;
+            {  // the kernel's valid-lane mask of this chunk (short-circuit tests read it)
+                const uint64_t left = rows - base;
+                const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+                w.s[S_VALID] = (uint32_t)valid;
+                w.s[S_VALID + 1] = (uint32_t)(valid >> 32);
+            }
             w.vcc = 0x5555AAAA5555AAAAull;
             // the kernel prologue's shift windows: lane l of wave 0, zero words outside [D, D+8)
             for (int l = 0; l < 64; ++l) w.v[R_LDS][l] = 4u * (uint32_t)l;
@@ -484,6 +495,8 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
     std::vector<uint32_t> ids;
     Options opt;
     opt.max_vgpr = max_vgpr;
+    opt.short_circuit = g_short_circuit;
+    opt.sample_rows = g_sample_rows;
     for (uint32_t t = 0; t < n_tapes; ++t) {
         SsaTape st;
         std::string e;
@@ -515,6 +528,9 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
     }
     return (int64_t)m.text.size();
 }
+
+extern "C" void emu_jit_set_short_circuit(int on) { g_short_circuit = on != 0; }
+extern "C" void emu_jit_set_sample_rows(uint32_t n) { g_sample_rows = n; }
 
 extern "C" void emu_jit_op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, int reset) {
     op_stats(valu, wide, count, reset != 0);

@@ -229,3 +229,27 @@ def test_jit_bench_config_pinned(gpu_ctx):
     cnt, first = ctape.count(sub, seed, 0, rows, threads=min(16, os.cpu_count() or 1))
     assert np.array_equal(hc[pick], cnt) and np.array_equal(fh[pick], first)
     print("jit: %s" % info)
+
+
+def test_jit_short_circuit_matches_full_eval(gpu_ctx):
+    """Short-circuit conjunctions (the default) against MH_JIT_FULL_EVAL on the same tapes and
+    rows: identical counts and first hits in both modes, over partial row blocks too."""
+    ts = synth.generate(1000)
+    seed, rows = synth.load_spec()["assignment_seed"], (1 << 18) + 77
+    a = gpu_ctx.assignments(ts.n_vars, rows)
+    a.generate(seed, 0)
+    sc = gpu_ctx.compile(ts)
+    sc.jit()
+    full = gpu_ctx.compile(ts)
+    full.jit(short_circuit=False)
+    for mode in (native.MODE_COUNT_ALL, native.MODE_FIRST_HIT):
+        f1, c1 = native.run(gpu_ctx, sc, a, mode=mode)
+        f0, c0 = native.run(gpu_ctx, full, a, mode=mode)
+        assert np.array_equal(f1, f0)
+        if mode == native.MODE_COUNT_ALL:
+            assert np.array_equal(c1, c0) and int((c0 > 0).sum()) > 50
+    f1, c1 = native.run(gpu_ctx, sc, a, row_first=333, row_count=rows - 1000, index_base=5,
+                        mode=native.MODE_COUNT_ALL)
+    f0, c0 = native.run(gpu_ctx, full, a, row_first=333, row_count=rows - 1000, index_base=5,
+                        mode=native.MODE_COUNT_ALL)
+    assert np.array_equal(c1, c0) and np.array_equal(f1, f0)

@@ -12,7 +12,7 @@ import pytest
 from mythril_amd import synth
 from mythril_amd.tape import Op, TapeSet
 from oracle import smt_eval
-from tests.emu import jit_eval, jit_module
+from tests.emu import jit_eval, jit_module, set_short_circuit
 from tests.evm_translate import Unsupported, lift_constants, vmtest_tapes
 from tests.fuzz import TapeFuzzer, assignment_soa, soa_row
 
@@ -312,3 +312,58 @@ def test_module_wait_states(emu):
     for values in (False, True):
         text, _, _ = jit_module(emu, ts, values=values, assemble=False)
         assert _hazards(text) == []
+
+
+def test_short_circuit_jit(emu):
+    """Short-circuit conjunctions (Options::short_circuit, on by default): config-5 tapes and
+    LASER-like conjunctions give the same root value on every row as the full evaluation and
+    the oracle, while executing far fewer VALU per wave; a partial last chunk (70 rows) whose
+    only satisfying lanes lie past the end still counts nothing for them."""
+    ts = synth.generate(40)
+    seed = synth.load_spec()["assignment_seed"]
+    rows = [smt_eval.gen_assignment(seed, ts.n_vars, r) for r in range(130)]
+    soa = soa_of(rows, ts.n_vars)
+    dyn = {}
+    try:
+        for sc in (False, True):
+            set_short_circuit(emu, sc)
+            vals, valu = [], 0
+            for i in range(len(ts.tapes)):
+                res = jit_eval(emu, ts, i, soa)
+                assert res.ok, res.why
+                vals.append(res.values)
+                valu += res.dyn["valu"]
+            dyn[sc] = (vals, valu)
+    finally:
+        set_short_circuit(emu, True)
+    assert dyn[True][0] == dyn[False][0]
+    assert dyn[True][1] < 0.6 * dyn[False][1], (dyn[True][1], dyn[False][1])
+    for i, t in enumerate(ts.tapes[:10]):
+        for r in range(0, len(rows), 7):
+            assert dyn[True][0][i][r] == int(smt_eval.evaluate(t.nodes, ts.pool.values,
+                                                                soa_row(soa, r)))
+    # conjunctions whose conjuncts hold on some lanes only: x < 2^255, y == x & 0xff..,
+    # z != 0, ite-guarded mul, with row 0 (copied into the unused lanes of the last chunk)
+    # the only row satisfying the cheap conjunct
+    ts2 = TapeSet(["x", "y", "z"])
+    b = ts2.builder()
+    x, y, z = (b.var(v, 256) for v in ("x", "y", "z"))
+    c = lambda v: b.const(v, 256)
+    eq = b.op(Op.EQ, y, c(12345))
+    lt = b.op(Op.BVULT, x, c(1 << 255))
+    nz = b.op(Op.NOT, b.op(Op.EQ, z, c(0)))
+    mul = b.op(Op.BVUGT, b.op(Op.BVMUL, x, z), c(7))
+    root = b.op(Op.AND, b.op(Op.AND, b.op(Op.AND, mul, nz), lt), eq)
+    ts2.add(b.finish(root))
+    rng = random.Random(77)
+    rws = []
+    for r in range(70):
+        rws.append([rng.getrandbits(256 - (r % 3)), 12345 if r in (0, 5, 40) else rng.getrandbits(8),
+                    rng.getrandbits(256) if r % 4 else 0])
+    soa2 = soa_of(rws, 3)
+    res = jit_eval(emu, ts2, 0, soa2)
+    assert res.ok, res.why
+    for r in range(70):
+        want = int(smt_eval.evaluate(ts2.tapes[0].nodes, ts2.pool.values, soa_row(soa2, r)))
+        assert res.values[r] == want, r
+    assert res.values[0] == 1 or res.values[5] == 1 or res.values[40] == 1

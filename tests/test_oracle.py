@@ -180,3 +180,16 @@ def test_generator_reproducible():
     assert a.pool.values == b.pool.values
     sizes = [len(t.nodes) for t in a.tapes]
     assert min(sizes) >= 16
+
+
+def test_c_oracle_short_circuit_counts():
+    """ct_count_lazy (a Bool AND's second operand evaluated only when the first holds, the CPU
+    baseline's evaluator) gives the eager evaluator's counts and first witnesses."""
+    from mythril_amd import synth
+
+    ts = synth.generate(60)
+    seed = synth.load_spec()["assignment_seed"]
+    eager = ctape.count(ts, seed, 0, 3000, threads=4)
+    lazy = ctape.count(ts, seed, 0, 3000, threads=4, short_circuit=True)
+    assert (eager[0] == lazy[0]).all() and (eager[1] == lazy[1]).all()
+    assert eager[0].sum() > 0
