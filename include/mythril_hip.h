@@ -68,7 +68,11 @@ enum mh_op {
     MH_OP_BVSUB_NOUDFL_U = 63,  /* z3.BVSubNoUnderflow(a, b, False) -> Bool  (b <=u a)            */
     MH_OP_EVM_EXP = 70,       /* a ** b mod 2^width                                               */
     MH_OP_EVM_SIGNEXTEND = 71,/* a = byte index k, b = x (yellow-paper SIGNEXTEND)                 */
-    MH_OP_EVM_BYTE = 72       /* a = byte index i, b = x (yellow-paper BYTE)                       */
+    MH_OP_EVM_BYTE = 72,      /* a = byte index i, b = x (yellow-paper BYTE)                       */
+    MH_OP_EVM_ADDMOD = 73,    /* (a + b) mod c, exact sum (yellow-paper ADDMOD); c == 0 gives 0, or */
+    MH_OP_EVM_MULMOD = 74     /* (a * b) mod c ...  with imm0 = 1 the low 256 bits of a op b: the
+                                 value of z3's extract[255:0](bvurem(zext a op zext b, zext c)),
+                                 a shape mh_tapes_compile also recognises and rewrites to these */
 };
 
 typedef struct mh_node {

@@ -55,6 +55,8 @@ uint64_t op_cost(const mh_node& n, const std::vector<mh_node>& t) {
         case MH_OP_BVMUL_NOOVFL_U: return 128;
         case MH_OP_EVM_EXP: return 256ull * 2 * 64;
         case MH_OP_EVM_SIGNEXTEND: case MH_OP_EVM_BYTE: return 24;
+        case MH_OP_EVM_ADDMOD: return 8 + 2200;              // sum + 512-bit remainder
+        case MH_OP_EVM_MULMOD: return 128 + 2200;            // product + 512-bit remainder
         default: return 0;
     }
 }
@@ -355,7 +357,7 @@ struct Lowering {
 
 int arity(const mh_node& nd) {
     if (nd.op <= MH_OP_FALSE) return 0;
-    if (nd.op == MH_OP_ITE) return 3;
+    if (nd.op == MH_OP_ITE || nd.op == MH_OP_EVM_ADDMOD || nd.op == MH_OP_EVM_MULMOD) return 3;
     if (nd.op == MH_OP_BVNEG || nd.op == MH_OP_BVNOT || nd.op == MH_OP_NOT ||
         nd.op == MH_OP_EXTRACT || nd.op == MH_OP_ZEXT || nd.op == MH_OP_SEXT ||
         nd.op == MH_OP_KECCAK)
@@ -513,6 +515,17 @@ bool Lowering::lower(std::vector<Val>& vals) {
                     else
                         out.vreg = masked(emit(D_ASHR_V, sext256(a, w), b, -1, 256), w);
                 }
+                break;
+            }
+            case MH_OP_EVM_ADDMOD: case MH_OP_EVM_MULMOD: {
+                if (w != 256 || W(nd.a) != 256 || W(nd.b) != 256 || W(nd.c) != 256 ||
+                    nd.imm0 > 1)
+                    return fail("ADDMOD / MULMOD take three 256-bit words");
+                const int a = narrow(nd.a), b = narrow(nd.b), c = narrow(nd.c);
+                if (a < 0 || b < 0 || c < 0) return fail("ADDMOD / MULMOD operand wider than 256");
+                features |= F_EVM;
+                out.vreg = emit(nd.op == MH_OP_EVM_ADDMOD ? D_ADDMOD : D_MULMOD, a, b, c, 256,
+                                nd.imm0);
                 break;
             }
             case MH_OP_BVNEG: {
@@ -842,7 +855,9 @@ int fold_constants(Lowering& L, int root_v) {
         const uint8_t op = code[i].op;
         if (op >= D_UDIV_R && op <= D_SMOD_C) feats |= F_DIV;
         else if (op == D_KECCAK) feats |= F_KECCAK;
-        else if (op == D_EXP || op == D_SIGNEXT || op == D_BYTE) feats |= F_EVM;
+        else if (op == D_EXP || op == D_SIGNEXT || op == D_BYTE || op == D_ADDMOD ||
+                 op == D_MULMOD)
+            feats |= F_EVM;
         else if (op >= D_FIRST_COMPLEX) feats |= F_CPLX;
         live.push_back(code[i]);
     }
@@ -904,6 +919,48 @@ void sample_bools(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t
     }
 }
 
+namespace {
+
+// z3's form of the yellow-paper ADDMOD / MULMOD (what LASER would build with exact semantics, and
+// what a z3 term carries into the SMT-LIB reader):
+//     extract[255:0](bvurem(zext256(a) op zext256(b), zext256(n)))      op = bvadd / bvmul
+// becomes MH_OP_EVM_ADDMOD / MULMOD(a, b, n) with imm0 = 1 (n == 0: bvurem returns the 512-bit
+// dividend, whose low 256 bits are a op b), so the 512-bit intermediates never reach the device.
+// The node keeps its index; the wide nodes it no longer reads become dead.
+void rewrite_wide_modops(std::vector<mh_node>& t) {
+    auto zext256 = [&](uint32_t k, uint32_t* inner) {
+        const mh_node& z = t[k];
+        if (z.op != MH_OP_ZEXT || z.width != 512 || z.imm0 != 256 || z.a >= k ||
+            t[z.a].width != 256)
+            return false;
+        *inner = z.a;
+        return true;
+    };
+    for (size_t i = 0; i < t.size(); ++i) {
+        mh_node& e = t[i];
+        if (e.op != MH_OP_EXTRACT || e.imm0 != 255 || e.imm1 != 0 || e.width != 256 || e.a >= i)
+            continue;
+        const mh_node& r = t[e.a];
+        if (r.op != MH_OP_BVUREM || r.width != 512 || r.a >= e.a || r.b >= e.a) continue;
+        const mh_node& s = t[r.a];
+        if ((s.op != MH_OP_BVADD && s.op != MH_OP_BVMUL) || s.width != 512 || s.a >= r.a ||
+            s.b >= r.a)
+            continue;
+        uint32_t a, b, n;
+        if (!zext256(s.a, &a) || !zext256(s.b, &b) || !zext256(r.b, &n)) continue;
+        const uint8_t op = s.op == MH_OP_BVADD ? MH_OP_EVM_ADDMOD : MH_OP_EVM_MULMOD;
+        e = mh_node{};
+        e.op = op;
+        e.width = 256;
+        e.a = a;
+        e.b = b;
+        e.c = n;
+        e.imm0 = 1;
+    }
+}
+
+}  // namespace
+
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,
@@ -913,6 +970,7 @@ int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* con
         return MH_E_INVALID;
     }
     std::vector<mh_node> t(nodes, nodes + n_nodes);
+    rewrite_wide_modops(t);
     Lowering L(t, consts, n_consts, n_vars, dconsts, dconst_index);
     std::vector<Val> vals;
     if (!L.lower(vals)) {
@@ -971,7 +1029,7 @@ std::vector<mh_node> rematerialize(const mh_node* t, size_t n, uint32_t max_size
         switch (nd.op) {
             case MH_OP_BVMUL: case MH_OP_BVUDIV: case MH_OP_BVUREM: case MH_OP_BVSDIV:
             case MH_OP_BVSREM: case MH_OP_BVSMOD: case MH_OP_KECCAK: case MH_OP_EVM_EXP:
-            case MH_OP_BVMUL_NOOVFL_U:
+            case MH_OP_BVMUL_NOOVFL_U: case MH_OP_EVM_ADDMOD: case MH_OP_EVM_MULMOD:
                 ok = false;
                 break;
             default:

@@ -83,6 +83,8 @@ enum mh_dop : uint8_t {
     D_LOADVAR,                     // X = assignment column aux (columns beyond the pinned ones)
     D_END,                         // end of tape: X holds the root
     D_WINDOW,                      // end of a 64-slot window: continue with the next one
+    D_ADDMOD, D_MULMOD,            // EVM ADDMOD / MULMOD: (X op y) mod R[c], exact; aux bit 0:
+                                   // R[c] == 0 gives the low 256 bits of X op y (else 0)
     D_NUM_OPS
 };
 

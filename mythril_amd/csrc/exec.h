@@ -61,7 +61,7 @@ MH_FN void copy8(u32* z, const u32* x) {
 }
 
 // z = f(x, y, c3) for a complex op (op >= D_FIRST_COMPLEX): x = R[a'], y = R[b] or the inline
-// constant, c3 = R[c] (KECCAK's third piece).  Width-w semantics on canonical operands.  E
+// constant, c3 = R[c] (KECCAK's third piece, ADDMOD / MULMOD's modulus).  Width-w semantics on canonical operands.  E
 // provides var(col, v) for D_LOADVAR.  Shared by the device's C++ path and step().
 template <int FEAT, class E>
 MH_FN void complex_op(const E& env, u32 w1, const u32* x, const u32* y, const u32* c3, u32* z) {
@@ -100,6 +100,9 @@ MH_FN void complex_op(const E& env, u32 w1, const u32* x, const u32* y, const u3
             break;
         case D_BYTE:
             if constexpr ((FEAT & F_EVM) != 0) evm_byte(x, y, z);
+            break;
+        case D_ADDMOD: case D_MULMOD:
+            if constexpr ((FEAT & F_EVM) != 0) evm_modop(op == D_MULMOD, x, y, c3, z, aux & 1u);
             break;
         case D_KECCAK:
             if constexpr ((FEAT & F_KECCAK) != 0) {

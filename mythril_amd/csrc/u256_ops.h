@@ -615,6 +615,67 @@ MH_FN void divmod_family(u32 kind, const u32* x, const u32* y, u32* z, u32 w) {
     }
 }
 
+// ---- EVM ADDMOD / MULMOD: a 512-bit intermediate ------------------------------------------------
+// r = u mod y for u < 2^512 (u16: 16 limbs) and y != 0: Knuth algorithm D over 32-bit digits,
+// udivrem256's long path with eight more digit positions.  u << s spans 24 limbs (s < 256 is the
+// normalisation shift); the top digit position is 8 + s / 32 <= 15, and a lane whose divisor
+// needs fewer positions gets zero digits at the extra ones (its window is below v there), so all
+// lanes run the same steps.
+MH_FN void urem512(const u32* u16, const u32* y, u32* r) {
+    u32 s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (y[k]) s = 32u * (7 - k) + clz32(y[k]);
+    u32 v[8];
+    shl256(y, s, v);
+    u32 u[25];
+    {
+        u32 lo[8], hi[8], t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { lo[k] = u16[k]; hi[k] = u16[8 + k]; }
+        const u32 rs = 256u - s;  // bits of each half shifted into the next (none for s = 0)
+        shl256(lo, s, t);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u[k] = t[k];
+        shl256(hi, s, t);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u[8 + k] = t[k];
+        shr256(lo, rs >= 256u ? 0u : rs, t, 0u);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u[8 + k] |= s ? t[k] : 0u;
+        shr256(hi, rs >= 256u ? 0u : rs, t, 0u);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u[16 + k] = s ? t[k] : 0u;
+        u[24] = 0;
+    }
+    const double vinv = recip_f64((double)(v[7] ? v[7] : 1u));
+#define MH_RSTEP(J) (void)knuth_step<J>(u, v, vinv);
+    MH_RSTEP(15) MH_RSTEP(14) MH_RSTEP(13) MH_RSTEP(12) MH_RSTEP(11) MH_RSTEP(10) MH_RSTEP(9)
+    MH_RSTEP(8) MH_RSTEP(7) MH_RSTEP(6) MH_RSTEP(5) MH_RSTEP(4) MH_RSTEP(3) MH_RSTEP(2)
+    MH_RSTEP(1) MH_RSTEP(0)
+#undef MH_RSTEP
+    shr256(u, s, r, 0u);  // the remainder is u[0..7] >> s
+}
+
+// Yellow-paper ADDMOD (mul = false) / MULMOD (mul = true) of 256-bit words: (x op y) mod n with
+// the exact sum / product; n == 0 gives 0, or with zero_low the low 256 bits of x op y (z3's
+// extract[255:0](bvurem(zext x op zext y, zext n)), SMT-LIB's x % 0 = x).
+MH_FN void evm_modop(bool mul, const u32* x, const u32* y, const u32* n, u32* z, bool zero_low) {
+    u32 u[16];
+    if (mul) {
+        mul_full256(x, y, u);
+    } else {
+        u[8] = add256(x, y, u);
+#pragma unroll
+        for (int k = 9; k < 16; ++k) u[k] = 0;
+    }
+    const bool nz = !is_zero256(n);
+    u32 r[8];
+    urem512(u, n, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) z[k] = nz ? r[k] : (zero_low ? u[k] : 0u);
+}
+
 // ---- EVM word helpers (256-bit only) -----------------------------------------------------------
 MH_FN void evm_exp(const u32* base, const u32* e, u32* z, u32 w) {
     u32 res[8] = {1, 0, 0, 0, 0, 0, 0, 0};

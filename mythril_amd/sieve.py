@@ -71,7 +71,7 @@ def local_tape(b: TapeBuilder, root: int, columns: Sequence[str]) -> np.ndarray:
 
 # ops whose recomputation is cheap enough to duplicate instead of keeping a value live
 _HEAVY = {Op.BVMUL, Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD, Op.KECCAK,
-          Op.EVM_EXP, Op.BVMUL_NOOVFL_U}
+          Op.EVM_EXP, Op.BVMUL_NOOVFL_U, Op.EVM_ADDMOD, Op.EVM_MULMOD}
 
 
 def rematerialize(nodes: np.ndarray, max_size: int) -> np.ndarray:

@@ -467,6 +467,14 @@ def to_smtlib(constraints: Sequence, minimize: Sequence = (), maximize: Sequence
             return "(bvule %s %s)" % (expr(bb), expr(a))
         if op == Op.KECCAK:
             raise SmtlibError("KECCAK (concrete hash) has no SMT-LIB form")
+        if op in (Op.EVM_ADDMOD, Op.EVM_MULMOD):  # z3's exact form (mythril_hip.h)
+            zx = lambda k: "((_ zero_extend 256) %s)" % expr(k)
+            r = "((_ extract 255 0) (bvurem (%s %s %s) %s))" % (
+                "bvadd" if op == Op.EVM_ADDMOD else "bvmul", zx(a), zx(bb), zx(c))
+            if i0 == 1:
+                return r
+            zero = "#x" + "0" * 64
+            return "(ite (= %s %s) %s %s)" % (expr(c), zero, zero, r)
         if op in (Op.EVM_EXP, Op.EVM_SIGNEXTEND, Op.EVM_BYTE):
             raise SmtlibError("%s has no SMT-LIB form" % op.name)
         k = ARITY[op]

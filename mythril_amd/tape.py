@@ -70,6 +70,8 @@ class Op(enum.IntEnum):
     EVM_EXP = 70
     EVM_SIGNEXTEND = 71
     EVM_BYTE = 72
+    EVM_ADDMOD = 73   # (a + b) mod c, exact (imm0 = 1: c == 0 gives (a + b) mod 2^256, else 0)
+    EVM_MULMOD = 74   # (a * b) mod c, exact (same zero rule)
     # host-only term kinds: built by the term layer (smt.py, smtlib.py) and removed by
     # lower.py before a tape reaches mh_tapes_compile (which rejects them)
     ARRAY = 80        # free array symbol: imm0 = array id, imm1 = domain width, width = range
@@ -100,7 +102,7 @@ F_ARRAY = 1  # mh_node.flags bit of host-only array-sorted nodes (never sent to 
 ARITY = {
     Op.CONST: 0, Op.VAR: 0, Op.TRUE: 0, Op.FALSE: 0,
     Op.BVNEG: 1, Op.BVNOT: 1, Op.NOT: 1, Op.EXTRACT: 1, Op.ZEXT: 1, Op.SEXT: 1, Op.KECCAK: 1,
-    Op.ITE: 3, Op.ARRAY: 0, Op.CONST_ARRAY: 1, Op.STORE: 3, Op.UF: 1,
+    Op.ITE: 3, Op.EVM_ADDMOD: 3, Op.EVM_MULMOD: 3, Op.ARRAY: 0, Op.CONST_ARRAY: 1, Op.STORE: 3, Op.UF: 1,
 }
 for _op in Op:
     ARITY.setdefault(_op, 2)
@@ -340,6 +342,11 @@ class TapeBuilder:
         elif op == Op.KECCAK:
             if ws[0] == BOOL or ws[0] % 8:
                 raise TapeError("KECCAK input must be a whole number of bytes, got %d" % ws[0])
+            w = 256
+        elif op in (Op.EVM_ADDMOD, Op.EVM_MULMOD):
+            if ws != [256, 256, 256] or imm0 not in (0, 1):
+                raise TapeError("%s needs three 256-bit words and imm0 0/1, got %s"
+                                % (op.name, ws))
             w = 256
         else:
             raise TapeError("op %s is not built with op()" % op.name)

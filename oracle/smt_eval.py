@@ -18,6 +18,7 @@ that mythril.laser.smt constructs:
   and/or/xor/not         And/Or/Xor/Not                        bool.py:87-124
   *_no_overflow          BVAddNoOverflow/BVMulNoOverflow/BVSubNoUnderflow  bitvec_helper.py:178-227
   keccak                 find_concrete_keccak                  keccak_function_manager.py:43-57
+  EVM_ADDMOD/MULMOD        yellow-paper ADDMOD/MULMOD, exact sum / product (evm_modop)
   EVM_EXP/SIGNEXTEND/BYTE  concrete branches of instructions.py:599-631 (pow mod 2^256),
                          :634-662 (SIGNEXTEND), :401-430 (BYTE)
 
@@ -48,7 +49,7 @@ AND, OR, XOR, NOT = 40, 41, 42, 43
 ITE = 45
 EXTRACT, CONCAT, ZEXT, SEXT = 50, 51, 52, 53
 KECCAK, BVADD_NOOVFL_U, BVMUL_NOOVFL_U, BVSUB_NOUDFL_U = 60, 61, 62, 63
-EVM_EXP, EVM_SIGNEXTEND, EVM_BYTE = 70, 71, 72
+EVM_EXP, EVM_SIGNEXTEND, EVM_BYTE, EVM_ADDMOD, EVM_MULMOD = 70, 71, 72, 73, 74
 
 
 def _mask(w: int) -> int:
@@ -137,6 +138,17 @@ def evm_signextend(k: int, x: int, w: int) -> int:
     return x & ((1 << testbit) - 1) | (x & (1 << testbit))
 
 
+def evm_modop(mul: bool, x: int, y: int, n: int, zero_low: bool) -> int:
+    """Yellow-paper ADDMOD / MULMOD: (x + y) mod n, (x * y) mod n with the sum / product taken
+    exactly (a 512-bit intermediate; instructions.py:569-596 states the same with z3 terms on
+    concrete values).  n == 0 gives 0, or, with zero_low (mh_node.imm0 = 1), the low 256 bits of
+    x op y -- extract[255:0](bvurem(zext x op zext y, zext n)), SMT-LIB's x % 0 = x."""
+    u = x * y if mul else x + y
+    if n == 0:
+        return u & _mask(256) if zero_low else 0
+    return u % n
+
+
 def evm_byte(i: int, x: int, w: int) -> int:
     """instructions.py:401-430 (concrete index): byte i (0 = most significant) of a 256-bit word."""
     if i >= w // 8:
@@ -210,6 +222,8 @@ def evaluate(nodes, consts: Sequence[int], assignment: Sequence[int], all_values
                 v = evm_signextend(x, y, w)
             else:
                 v = evm_byte(x, y, w)
+        elif op in (EVM_ADDMOD, EVM_MULMOD):
+            v = evm_modop(op == EVM_MULMOD, vals[a], vals[b], vals[c], i0 == 1)
         elif op == BVNEG:
             v = bvneg(vals[a], w)
         elif op == BVNOT:

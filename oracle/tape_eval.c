@@ -39,7 +39,7 @@ enum {
     AND = 40, OR, XOR, NOT, ITE = 45,
     EXTRACT = 50, CONCAT, ZEXT, SEXT,
     KECCAK = 60, ADD_NOOVFL = 61, MUL_NOOVFL = 62, SUB_NOUDFL = 63,
-    EVM_EXP = 70, EVM_SIGNEXTEND = 71, EVM_BYTE = 72
+    EVM_EXP = 70, EVM_SIGNEXTEND = 71, EVM_BYTE = 72, EVM_ADDMOD = 73, EVM_MULMOD = 74
 };
 
 static void vmask(val_t* x, int w) {
@@ -283,7 +283,8 @@ static int node_value(const node_t* nd, uint64_t i, const uint32_t* consts, uint
         val_t z;
         memset(&z, 0, sizeof(z));
         /* results never exceed their width, and MUL_NOOVFL needs the double-width product */
-        g_nl = (t->op == MUL_NOOVFL || t->op == ADD_NOOVFL) ? NL : (w + 31) / 32 + 1;
+        g_nl = (t->op == MUL_NOOVFL || t->op == ADD_NOOVFL || t->op == EVM_ADDMOD ||
+                t->op == EVM_MULMOD) ? NL : (w + 31) / 32 + 1;
         if (g_nl > NL || w == 0) g_nl = NL;
         const val_t *x = t->a < i ? &V[t->a] : NULL, *y = t->b < i ? &V[t->b] : NULL;
         switch (t->op) {
@@ -427,6 +428,22 @@ static int node_value(const node_t* nd, uint64_t i, const uint32_t* consts, uint
                 z = res;
                 break;
             }
+            case EVM_ADDMOD: case EVM_MULMOD: {
+                /* yellow-paper ADDMOD / MULMOD: the exact sum / product (<= 512 bits) mod c;
+                 * c == 0 gives 0, or with imm0 = 1 the low 256 bits (bvurem's x % 0 = x) */
+                if (t->c >= i) goto bad;
+                val_t u, q, r;
+                memset(&u, 0, sizeof(u));
+                if (t->op == EVM_ADDMOD) vadd(x, y, &u);
+                else vmul(x, y, &u);
+                if (viszero(&V[t->c])) {
+                    if (t->imm0 == 1) { z = u; vmask(&z, 256); }
+                    break;
+                }
+                vdivmod(&u, &V[t->c], &q, &r);
+                z = r;
+                break;
+            }
             case EVM_SIGNEXTEND: {
                 val_t lim;
                 memset(&lim, 0, sizeof(lim));
@@ -510,7 +527,8 @@ static int lazy(const node_t* nd, uint64_t i, const uint32_t* consts, uint32_t n
         return 0;
     }
     const uint64_t ops[3] = {t->a, t->b, t->c};
-    const int ar = t->op <= FALSE_ ? 0 : t->op == ITE ? 3 :
+    const int ar = t->op <= FALSE_ ? 0 : (t->op == ITE || t->op == EVM_ADDMOD ||
+                                         t->op == EVM_MULMOD) ? 3 :
                    (t->op == BVNEG || t->op == BVNOT || t->op == NOT || t->op == EXTRACT ||
                     t->op == ZEXT || t->op == SEXT || t->op == KECCAK) ? 1 : 2;
     for (int k = 0; k < ar; ++k) {
