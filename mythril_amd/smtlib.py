@@ -287,6 +287,29 @@ class Reader:
             acc = self.b.op(op, acc, x)
         return acc
 
+    def _add_noovfl(self, e: int, z: int) -> Optional[int]:
+        """z3's BVAddNoOverflow(x, y, False) (bitvec_helper.py:178-189 builds it; z3 prints
+        (= ((_ extract w w) (bvadd ((_ zero_extend 1) x) ((_ zero_extend 1) y))) #b0)) back to
+        the one predicate, so the tape stays within 256 bits and the guide sees the overflow
+        shape.  None when (e, z) is not that form."""
+        nodes, pool = self.b.nodes, self.b.pool.values
+        zo, zw, *_, zi0, _ = nodes[z]
+        if Op(zo) != Op.CONST or zw != 1 or pool[zi0] & 1:
+            return None
+        eo, ew, ea, _, _, hi, lo = nodes[e]
+        if Op(eo) != Op.EXTRACT or hi != lo or ew != 1:
+            return None
+        so, sw, sa, sb, *_ = nodes[ea]
+        if Op(so) != Op.BVADD or sw != hi + 1:
+            return None
+        inner = []
+        for k in (sa, sb):
+            ko, kw, ka, _, _, ki0, _ = nodes[k]
+            if Op(ko) != Op.ZEXT or ki0 != 1 or nodes[ka][1] != hi:
+                return None
+            inner.append(ka)
+        return self.b.op(Op.BVADD_NOOVFL_U, inner[0], inner[1])
+
     def _apply(self, head: str, a: List[int]) -> int:
         b = self.b
         if head in _BV_BIN:
@@ -319,6 +342,12 @@ class Reader:
         if head == "=":
             if any(b.is_array(x) for x in a):
                 raise SmtlibError("equality between arrays is not supported")
+            if len(a) == 2:
+                nov = self._add_noovfl(a[0], a[1])
+                if nov is None:
+                    nov = self._add_noovfl(a[1], a[0])
+                if nov is not None:
+                    return nov
             eqs = [b.op(Op.EQ, a[i], a[i + 1]) for i in range(len(a) - 1)]
             return self._fold(Op.AND, eqs)
         if head == "distinct":

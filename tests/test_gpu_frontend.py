@@ -122,3 +122,33 @@ def test_parent_witness_is_reused(gpu_ctx):
     m = frontend.get_model(tuple(cs))
     assert s.stats.rounds - rounds_before == 1  # found in the first round
     assert _oracle_holds(ctx, cs, m.schema, m.values)
+
+
+@pytest.mark.parametrize("qi", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+def test_solver_log_queries_on_gpu(gpu_ctx, qi):
+    """--solver-log ingestion: every LASER-shaped SAT query in the SMT-LIB2 form the reference's
+    get_model writes (support/model.py:44-55, z3's sexpr()), read back by smtlib.parse and
+    answered by the sieve on the GPU; each witness is a model of the PARSED query (oracle)."""
+    from mythril_amd import smtlib
+
+    ctx, qs = queries()
+    name, cs = qs[qi]
+    try:
+        text = smtlib.to_smtlib(cs)
+    except smtlib.SmtlibError:
+        pytest.skip("query holds a device-only op")
+    q = smtlib.parse(text)
+    m = frontend.get_model(tuple(q.constraints))
+    assert _oracle_holds(q.ctx, q.constraints, m.schema, m.values), name
+
+
+def test_z3_style_solver_log_on_gpu(gpu_ctx):
+    """z3-printed text (let bindings, keccak UF and its inverse, distinct, =>, bvcomp,
+    rotate_left, an objective) parsed and solved on the GPU; the witness checked by the oracle
+    with the lowering's keccak interpretation."""
+    from mythril_amd import smtlib
+    from tests.test_smtlib import Z3_STYLE
+
+    q = smtlib.parse(Z3_STYLE)
+    m = frontend.get_model(tuple(q.constraints))
+    assert _oracle_holds(q.ctx, q.constraints, m.schema, m.values)

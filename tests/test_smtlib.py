@@ -194,3 +194,25 @@ def test_importer_memory_is_bounded():
     n0 = imp([raw])[1][0].node
     before = imp.n_nodes()
     assert imp([raw])[1][0].node == n0 and imp.n_nodes() == before
+
+
+def test_add_no_overflow_form_reads_back_as_the_predicate():
+    """z3's printed BVAddNoOverflow(x, y, False) -- (= ((_ extract w w) (bvadd ((_ zero_extend 1)
+    x) ((_ zero_extend 1) y))) #b0), either side order -- reads back as the one predicate, so the
+    parsed query stays within 256 bits and lowers for the device."""
+    from mythril_amd.lower import lower_query
+    from mythril_amd.tape import Op
+
+    ctx, qs = queries()
+    cs = dict(qs)["overflow"]
+    q = smtlib.parse(smtlib.to_smtlib(cs))
+    tape = q.ctx.b.finish(And(*q.constraints).node)
+    ops = {Op(int(o)) for o in tape.nodes["op"]}
+    assert Op.BVADD_NOOVFL_U in ops and max(int(w) for w in tape.nodes["width"]) <= 256
+    lower_query(q.ctx.b, [c.node for c in q.constraints])
+    text = ("(declare-fun x () (_ BitVec 8))\n(declare-fun y () (_ BitVec 8))\n"
+            "(assert (= #b0 ((_ extract 8 8) (bvadd ((_ zero_extend 1) x) "
+            "((_ zero_extend 1) y)))))\n")
+    q2 = smtlib.parse(text)
+    t2 = q2.ctx.b.finish(q2.constraints[0].node)
+    assert Op(int(t2.nodes["op"][-1])) == Op.BVADD_NOOVFL_U
