@@ -66,8 +66,10 @@ uint32_t prefix_mask(uint32_t m) { int t = top_bit(m); return t < 0 ? 0u : ((2u 
 class Emitter {
 public:
     Emitter(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
-            const Options& opt, const std::vector<uint8_t>* check = nullptr)
-        : st_(st), pool_(pool), n_vars_(n_vars), opt_(opt), check_(check) {}
+            const Options& opt, const std::vector<uint8_t>* check = nullptr,
+            std::vector<double>* insn_cost = nullptr)
+        : st_(st), pool_(pool), n_vars_(n_vars), opt_(opt), check_(check),
+          insn_cost_(insn_cost) {}
 
     TapeCode run();
 
@@ -77,6 +79,7 @@ private:
     uint32_t n_vars_;
     Options opt_;
     const std::vector<uint8_t>* check_;  // short-circuit test after these vregs (or null)
+    std::vector<double>* insn_cost_;     // out: VALU emitted per SSA instruction (or null)
     bool sc_used_ = false;
     std::vector<MI> code_;
     std::vector<Val> vals_;
@@ -1108,7 +1111,12 @@ double sc_cost(const SsaInsn& v) {
 // chain's ANDs are rebuilt in that order (the last one defines the root), each operand cone is
 // emitted just before the AND that consumes it, in the original relative order.
 bool schedule_impl(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t sample_rows,
-                   SsaTape& out, std::vector<uint8_t>& check) {
+                   const std::vector<double>* insn_cost, SsaTape& out,
+                   std::vector<uint8_t>& check) {
+    auto cost = [&](int i) {
+        return insn_cost && (size_t)i < insn_cost->size() ? (*insn_cost)[i] + 0.5
+                                                           : sc_cost(st.code[i]);
+    };
     const auto& code = st.code;
     const int n = (int)code.size();
     if (st.root < 0 || !st.root_bool || n == 0) return false;
@@ -1183,7 +1191,7 @@ bool schedule_impl(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_
             if (taken[k]) continue;
             double c = 0;
             for (int i : cone[k])
-                if (!done[i]) c += sc_cost(code[i]);
+                if (!done[i]) c += cost(i);
             double rej = reject_p(conj[k]);
             if (n_alive) {
                 uint32_t fails = 0;
@@ -1258,6 +1266,7 @@ TapeCode Emitter::run() {
     try {
         const auto& code = st_.code;
         const int nv = st_.n_vregs;
+        if (insn_cost_) insn_cost_->assign(code.size(), 0.0);
         if (st_.n_pinned != (int)n_vars_ || n_vars_ > 4) fail("assignment columns not pinned");
         bool has_div = false, has_kec = false;
         for (const SsaInsn& v : code) {
@@ -1286,6 +1295,7 @@ TapeCode Emitter::run() {
             const SsaInsn& v = code[i];
             const uint8_t op = v.op;
             cur_op_ = op;
+            const uint32_t valu_before = n_valu_;
             ++op_count[op];
             auto Y = [&]() -> Val { return v.cidx >= 0 ? const_val(v.cidx) : val(v.b); };
             switch (op) {
@@ -1369,6 +1379,12 @@ TapeCode Emitter::run() {
                 release(vals_[r]);
             }
             if (check_ && (*check_)[v.d]) sc_check(vals_[v.d]);
+            if (insn_cost_) {
+                // a division-family call runs ~110 VALU in the subroutine (jit_mix.json)
+                const bool call = op >= D_UDIV_R && op <= D_SMOD_C;
+                (*insn_cost_)[i] = (double)(n_valu_ - valu_before) + (call ? 110.0 : 0.0) +
+                                   (op == D_KECCAK ? 7000.0 : 0.0);
+            }
         }
         // root
         const Val& root = val(st_.root);
@@ -1510,8 +1526,9 @@ std::string opnd_str(const Opnd& o, const std::string& prefix) {
 }  // namespace
 
 bool schedule_conjuncts(const SsaTape& st, const std::vector<uint32_t>& pool,
-                        uint32_t sample_rows, SsaTape& out, std::vector<uint8_t>& check) {
-    return schedule_impl(st, pool, sample_rows, out, check);
+                        uint32_t sample_rows, const std::vector<double>* insn_cost, SsaTape& out,
+                        std::vector<uint8_t>& check) {
+    return schedule_impl(st, pool, sample_rows, insn_cost, out, check);
 }
 
 // ---- the division subroutine ---------------------------------------------------------------
@@ -2202,14 +2219,14 @@ Module build_module(const std::vector<const TapeCode*>& codes,
                 line(o, "s_mov_b64 exec, -1");
                 continue;
             }
+            // no valid row of this chunk satisfies the tape (the common case): nothing to count
             line(o, "s_and_b64 s[32:33], s[32:33], s[30:31]");
+            line(o, "s_cbranch_scc0 %s_nf", pre);
             line(o, "s_bcnt1_i32_b64 s34, s[32:33]");
             line(o, "v_readlane_b32 s35, v3, %u", t);
             line(o, "s_add_u32 s35, s35, s34");
             line(o, "v_writelane_b32 v3, s35, %u", t);
             line(o, "s_nop 4");
-            line(o, "s_cmp_eq_u64 s[32:33], 0");
-            line(o, "s_cbranch_scc1 %s_nf", pre);
             line(o, "v_readlane_b32 s35, v4, %u", t);
             line(o, "s_cmp_lg_u32 s35, 0");
             line(o, "s_cbranch_scc1 %s_nf", pre);
@@ -2393,17 +2410,21 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
 
 TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
                    const Options& opt) {
+    // source order first: the tape's code when there is no conjunction to reorder, and the VALU
+    // each SSA instruction costs (the scheduler's cost model) when there is
+    std::vector<double> cost;
+    Emitter e(st, pool, n_vars, opt, nullptr, opt.short_circuit ? &cost : nullptr);
+    TapeCode tc0 = e.run();
     if (opt.short_circuit) {
         SsaTape sc;
         std::vector<uint8_t> check;
-        if (schedule_conjuncts(st, pool, opt.sample_rows, sc, check)) {
-            Emitter e(sc, pool, n_vars, opt, &check);
-            TapeCode tc = e.run();
+        if (schedule_conjuncts(st, pool, opt.sample_rows, tc0.ok ? &cost : nullptr, sc, check)) {
+            Emitter e2(sc, pool, n_vars, opt, &check);
+            TapeCode tc = e2.run();
             if (tc.ok) return tc;  // else (register pressure of the new order): source order
         }
     }
-    Emitter e(st, pool, n_vars, opt);
-    return e.run();
+    return tc0;
 }
 
 }  // namespace jit

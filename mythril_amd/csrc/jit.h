@@ -151,12 +151,14 @@ struct Options {
     uint32_t sample_rows = 256;
 };
 
-// The SSA of `st` reordered for short-circuit evaluation of its root conjunction.  Returns false
+// The SSA of `st` reordered for short-circuit evaluation of its root conjunction (insn_cost: VALU
+// per SSA instruction from a source-order emission; null = a static per-op table).  Returns false
 // (out untouched) when the root is not an AND of at least two conjuncts.  check[v] = 1 marks the
 // virtual registers (the first conjunct, then each partial conjunction) after which the emitter
 // tests the running mask.
 bool schedule_conjuncts(const SsaTape& st, const std::vector<uint32_t>& pool,
-                        uint32_t sample_rows, SsaTape& out, std::vector<uint8_t>& check);
+                        uint32_t sample_rows, const std::vector<double>* insn_cost, SsaTape& out,
+                        std::vector<uint8_t>& check);
 
 // Emit one tape (SSA after folding) with constants from `pool` (8 limbs per entry).
 TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
