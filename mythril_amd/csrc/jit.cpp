@@ -280,9 +280,56 @@ private:
 int Emitter::chain(bool sub, const Limb* a, const Limb* b, int top, Limb* res, uint32_t junk,
                    std::vector<uint32_t>& tmp) {
     int cs = 0;
+    uint32_t same = ~0u;  // register holding the value of the last "carry passes through" limb
     for (int k = 0; k <= top; ++k) {
         const Limb x = a[k], y = b[k];
         if (x.k == L_UNDEF || y.k == L_UNDEF) fail("internal: chain over an undemanded limb");
+        if (cs == 2 && x.is_c() && y.is_c()) {
+            // carry / borrow c in VCC, both limbs constant: x - x - c = -c and 2^32-1 + c wrap
+            // with the carry passing through unchanged, so a run of such limbs (the top of a
+            // narrow value's sign extension, say) shares one register; any other constant pair
+            // decides the carry out at compile time
+            const bool through = sub ? x.v == y.v : (uint64_t)x.v + y.v == 0xFFFFFFFFull;
+            if (through) {
+                if (res) {
+                    if (same == ~0u) {
+                        same = valloc();
+                        emit(M_V_ADDC_CO, {V(same), S(S_DIV_DUMMY, 2), IMM(sub ? 0u : ~0u),
+                                           IMM(sub ? 0u : 0u), VCC()}, true);
+                        if (sub) code_.back().op = M_V_SUBB_CO;
+                    } else {
+                        vretain(same);
+                    }
+                    res[k] = Limb::R(same);
+                }
+                continue;
+            }
+            same = ~0u;
+            if (!res) {  // only the final carry matters: it is known from here on
+                cs = sub ? (x.v < y.v ? 1 : 0) : ((uint64_t)x.v + y.v > 0xFFFFFFFFull ? 1 : 0);
+                continue;
+            }
+            const uint32_t dst = valloc();
+            if (sub) {
+                if (is_inline(x.v) && is_inline(y.v))
+                    emit(M_V_SUBB_CO, {V(dst), S(S_DIV_DUMMY, 2), IMM(x.v), IMM(y.v), VCC()}, true);
+                else
+                    emit(M_V_SUBB_CO, {V(dst), S(S_DIV_DUMMY, 2), V(vgpr_of(x, tmp)),
+                                       V(vgpr_of(y, tmp)), VCC()}, true);
+                cs = x.v < y.v ? 1 : 0;
+            } else {
+                const uint32_t sv = x.v + y.v;  // < 2^32 - 1 or wrapped: carry out known
+                if (is_inline(sv))
+                    emit(M_V_ADDC_CO, {V(dst), S(S_DIV_DUMMY, 2), IMM(sv), IMM(0), VCC()}, true);
+                else
+                    emit(M_V_ADDC_CO, {V(dst), S(S_DIV_DUMMY, 2), V(vgpr_of(Limb::C(sv), tmp)),
+                                       IMM(0), VCC()}, true);
+                cs = (uint64_t)x.v + y.v > 0xFFFFFFFFull ? 1 : 0;
+            }
+            res[k] = Limb::R(dst);
+            continue;
+        }
+        same = ~0u;
         if (cs != 2 && x.is_c() && y.is_c()) {
             const uint64_t xv = x.v, yv = y.v;
             if (sub) {
