@@ -285,6 +285,12 @@ mh::KParams make_params(const mh_tapeset* ts, uint32_t tape_first, const mh_assi
 
 // Rows per workgroup of the JIT kernels: 4 waves, each over a contiguous run of 64-row chunks.
 uint32_t jit_rows_per_wg(uint64_t row_count) {
+    static const uint32_t forced = [] {  // diagnostic: MH_JIT_ROWS_PER_WG (multiple of 256)
+        const char* e = std::getenv("MH_JIT_ROWS_PER_WG");
+        const uint32_t v = e ? (uint32_t)atoi(e) : 0u;
+        return (v >= 256 && v % 256 == 0) ? v : 0u;
+    }();
+    if (forced) return forced;
     uint64_t r = 256;
     while (r < 16384 && r * 2048 < row_count) r *= 2;  // >= ~2048 row blocks before growing
     return (uint32_t)r;
@@ -896,7 +902,10 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
     opt.short_circuit = (flags & MH_JIT_FULL_EVAL) == 0;
     if (const char* e = std::getenv("MH_JIT_SC")) opt.short_circuit = opt.short_circuit && atoi(e) != 0;
     if (opt.max_vgpr > 512 || opt.max_vgpr < 96) return set_err(MH_E_INVALID, "max_vgpr outside 96..512");
-    uint32_t threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // build threads = code objects = launches per run: 4 (MI355X, config 5, profiles/r02y:
+    // 16 objects 3.195e11 evals/s, 4 3.222e11, 1 3.226e11 -- each launch drains its tail
+    // before the next starts; 4 keeps the emission and assembly parallel)
+    uint32_t threads = std::max(1u, std::min(4u, std::thread::hardware_concurrency()));
     if (const char* e = std::getenv("MH_JIT_THREADS")) threads = (uint32_t)std::max(1, atoi(e));
     std::vector<mh::jit::Built> built;
     mh::jit::BuildStats stats;

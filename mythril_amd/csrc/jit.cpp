@@ -2380,6 +2380,20 @@ Module build_module(const std::vector<const TapeCode*>& codes,
     return m;
 }
 
+// Code bytes per tape group (MH_JIT_GROUP_KB for A/B; a group's chunk loop branches back over
+// the whole group, and s_cbranch reaches +-128 KB, so at most 112 KB).  Measured on MI355X,
+// config 5 (profiles/r02y): 24 KB 2.52e11 evals/s, 40 KB 2.91e11, 56 KB 3.09e11, 80 KB 3.18e11,
+// 96 KB 3.20e11, 128 KB 3.20e11 -- fewer, larger groups reload the assignment columns less
+// often; the instruction cache streams the larger groups fine.
+uint32_t default_group_bytes() {
+    static const uint32_t g = [] {
+        const char* e = std::getenv("MH_JIT_GROUP_KB");
+        const uint32_t kb = e ? (uint32_t)atoi(e) : 0u;
+        return (kb >= 4 && kb <= 112) ? kb * 1024u : 96u * 1024u;
+    }();
+    return g;
+}
+
 bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                    const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, bool values,
                    const Options& opt, uint32_t threads, std::vector<Built>& out,
@@ -2426,7 +2440,8 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
         if (codes.empty()) return;
         std::vector<const TapeCode*> ptrs;
         for (const TapeCode& c : codes) ptrs.push_back(&c);
-        Module m = build_module(ptrs, ids, n_vars, false);
+        const uint32_t group_bytes = default_group_bytes();
+        Module m = build_module(ptrs, ids, n_vars, false, group_bytes);
         b.n_groups = (uint32_t)m.group_first.size();
         b.max_vgpr = m.max_vgpr;
         std::string log;
@@ -2435,7 +2450,7 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
             return;
         }
         if (values) {
-            Module mv = build_module(ptrs, ids, n_vars, true);
+            Module mv = build_module(ptrs, ids, n_vars, true, group_bytes);
             if (!assemble(mv.text, b.hsaco_values, log)) b.err = "assemble (values): " + log.substr(0, 2000);
         }
     };

@@ -191,9 +191,10 @@ struct Module {
 };
 // values = true: every tape stores its root value (8 limbs per row, the parity path) instead of
 // counting hits.
+uint32_t default_group_bytes();  // 96 KB, or MH_JIT_GROUP_KB
 Module build_module(const std::vector<const TapeCode*>& codes,
                     const std::vector<uint32_t>& tape_ids, uint32_t n_vars, bool values,
-                    uint32_t group_bytes = 40 * 1024);
+                    uint32_t group_bytes);
 
 // Diagnostics: static VALU (and 4-cycle VALU) emitted per SSA op kind since the last reset
 // (not thread safe; tests / scripts only).

@@ -510,7 +510,7 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
         }
     }
     *n_jitted = (uint32_t)ok.size();
-    Module m = build_module(ok, ids, n_vars, values != 0);
+    Module m = build_module(ok, ids, n_vars, values != 0, default_group_bytes());
     if (text && cap) {
         const size_t n = std::min<size_t>(cap - 1, m.text.size());
         memcpy(text, m.text.data(), n);
