@@ -766,7 +766,7 @@ bool bool_result(uint8_t op) {
 // before any solver sees them (laser/smt/bitvec.py, `simplify` calls); nodes whose value does not
 // depend on the assignment are not counted as per-evaluation work (compile_tape's alg_ops).
 // Returns the root's register after aliasing; recomputes the feature bits.
-int fold_constants(Lowering& L, int root_v) {
+int fold_constants(Lowering& L, int root_v, bool value_numbering) {
     std::vector<VInsn>& code = L.code;
     const int nv = L.n_vregs;
     std::vector<char> known(nv, 0);
@@ -775,10 +775,58 @@ int fold_constants(Lowering& L, int root_v) {
     for (int r = 0; r < nv; ++r) rep[r] = r;
     auto R = [&](int r) { return r < 0 ? r : rep[r]; };
     auto K = [&](int r) { return r >= 0 && known[r]; };
+    // value numbering (native code only: the interpreter's 15 registers rely on cheap shared
+    // terms being duplicated, Sieve.rematerialize): an instruction with the same op, operands and
+    // immediates as an earlier one is that one (every op is pure)
+    std::unordered_map<std::string, int> seen_insn;
+    auto set_bool = [&](VInsn& v, bool b) {
+        known[v.d] = 1;
+        u32* z = &val[(size_t)v.d * 8];
+        for (int k = 0; k < 8; ++k) z[k] = 0;
+        z[0] = b ? 1u : 0u;
+        v = VInsn{b ? (uint8_t)D_TRUE : (uint8_t)D_FALSE, v.d, -1, -1, -1, 1, 0, -1, 0};
+    };
     for (VInsn& v : code) {
         v.a = R(v.a);
         v.b = R(v.b);
         v.c = R(v.c);
+        if (value_numbering) {
+            const int key[8] = {v.op, v.a, v.b, v.c, (int)v.width, (int)v.aux, v.cidx,
+                                (int)v.w1raw};
+            std::string k(reinterpret_cast<const char*>(key), sizeof(key));
+            auto it = seen_insn.find(k);
+            if (it != seen_insn.end()) {
+                rep[v.d] = it->second;  // uses are renamed; the copy is dead code below
+                continue;
+            }
+            seen_insn.emplace(std::move(k), v.d);
+        }
+        // identities of an op applied to one value twice (what z3's simplify does to x - x,
+        // x ^ x, x & x, x == x, ...): the result is a constant or the operand itself
+        if (v.cidx < 0 && v.a >= 0 && v.a == v.b) {
+            switch (v.op) {
+                case D_SUB_R: case D_RSUB_R: case D_XOR_R:
+                    known[v.d] = 1;
+                    std::memset(&val[(size_t)v.d * 8], 0, 32);
+                    v = VInsn{D_LOADC, v.d, -1, -1, -1, 256, 0, L.zero_const(), 0};
+                    continue;
+                case D_AND_R: case D_OR_R: case D_BAND: case D_BOR:
+                    rep[v.d] = v.a;
+                    continue;
+                case D_EQ_R: case D_ULE_R: case D_UGE_R: case D_SLE_R: case D_SGE_R: case D_BEQ:
+                    set_bool(v, true);
+                    continue;
+                case D_ULT_R: case D_UGT_R: case D_SLT_R: case D_SGT_R: case D_BXOR:
+                    set_bool(v, false);
+                    continue;
+                default:
+                    break;
+            }
+        }
+        if ((v.op == D_ITE || v.op == D_BITE) && v.b >= 0 && v.b == v.c) {  // (cond, t, t)
+            rep[v.d] = v.b;
+            continue;
+        }
         const uint8_t op = v.op;
         if (op == D_LOADC) {
             known[v.d] = 1;
@@ -964,7 +1012,7 @@ void rewrite_wide_modops(std::vector<mh_node>& t) {
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,
-                       std::string& err) {
+                       std::string& err, bool value_numbering) {
     if (n_nodes == 0) {
         err = "empty tape";
         return MH_E_INVALID;
@@ -995,7 +1043,7 @@ int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* con
         err = "root wider than 256 bits";
         return MH_E_UNSUPPORTED;
     }
-    if (!std::getenv("MH_NO_FOLD")) root_v = fold_constants(L, root_v);
+    if (!std::getenv("MH_NO_FOLD")) root_v = fold_constants(L, root_v, value_numbering);
     st.code.swap(L.code);
     st.root = root_v;
     st.n_vregs = L.n_vregs;

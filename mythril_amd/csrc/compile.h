@@ -45,10 +45,12 @@ struct SsaTape {
 };
 
 // Lower one tape to SSA, fold constants and drop dead code (compile_tape's first half).
+// value_numbering merges identical instructions (the native code's register file has room for
+// the longer live ranges; the interpreter's does not).
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& out,
-                       std::string& err);
+                       std::string& err, bool value_numbering = false);
 
 // Bool values of the SSA registers `want` on n_rows sample rows (each pinned column a uniform
 // 256-bit value from a splitmix64 stream seeded by `seed`), by the device's own instruction

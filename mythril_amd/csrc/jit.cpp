@@ -519,6 +519,11 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
     }
     int top = 7;
     while (top > 0 && a[top].is_c() && b[top].is_c() && a[top].v == b[top].v) --top;
+    if (a[top].is_c() && b[top].is_c() && a[top].v != b[top].v) {
+        // the highest limb that differs is known on both sides: it decides, whatever is below
+        free_tmp(tmp);
+        return bool_const((a[top].v < b[top].v) != negate);
+    }
     // top run where exactly one side is known zero
     int hi_side = 0;  // 1: b zero on [m+1, top], 2: a zero there
     int m = top;
@@ -2416,7 +2421,7 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
             SsaTape st;
             std::string e;
             if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts, n_consts,
-                               n_vars, pool, index, st, e) != MH_OK) {
+                               n_vars, pool, index, st, e, true) != MH_OK) {
                 stats.why[t] = "lowering: " + e;
                 continue;
             }

@@ -383,7 +383,7 @@ bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes
     std::string err;
     if (tape >= n_tapes) { e = "tape index"; return false; }
     if (lower_tape_ssa(nodes + offs[tape], (size_t)(offs[tape + 1] - offs[tape]), consts,
-                       n_consts, n_vars, pool, index, st, err) != MH_OK) {
+                       n_consts, n_vars, pool, index, st, err, true) != MH_OK) {
         e = "lowering: " + err;
         return false;
     }
@@ -501,7 +501,7 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
         SsaTape st;
         std::string e;
         if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts, n_consts,
-                           n_vars, pool, index, st, e) != MH_OK)
+                           n_vars, pool, index, st, e, true) != MH_OK)
             continue;
         codes[t] = emit_tape(st, pool, n_vars, opt);
         if (codes[t].ok) {
