@@ -35,7 +35,7 @@ def main():
         for v in range(4):
             for k in range(8):
                 soa[v, k, r] = (a[v] >> (32 * k)) & 0xFFFFFFFF
-    tot = dict(valu=0, wide=0, salu=0, div_valu=0, div_wide=0, f64=0)
+    tot = dict(valu=0, wide=0, salu=0, div_valu=0, div_wide=0, f64=0, alive_valu=0)
     import ctypes as C
     tagf = emu.lib.emu_jit_tag_valu
     tagf.restype = None

@@ -81,6 +81,9 @@ class JitResult:
         # executed per 64-row chunk (wave): VALU, 4-cycle VALU, SALU, division VALU / 4-cycle
         self.dyn = dict(zip(("valu", "wide", "salu", "div_valu", "div_wide", "f64"),
                             (int(x) for x in info[8:14])))
+        # VALU weighted by the fraction of lanes still satisfying the conjuncts tested so far:
+        # what perfect lane compaction would execute
+        self.dyn["alive_valu"] = int(info[14]) / 16.0
 
 
 def _jit_fn(lib, name, restype, argtypes):

@@ -86,7 +86,9 @@ struct Err {
 // inside the division subroutine
 struct Counts {
     uint64_t valu = 0, wide = 0, salu = 0, div_valu = 0, div_wide = 0, f64 = 0;
+    double alive_valu = 0;  // VALU weighted by the fraction of lanes still alive (compaction bound)
 } g_counts;
+uint64_t g_alive = ~0ull;  // lanes that satisfy every conjunct tested so far (short circuit)
 uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
 // executed VALU by the SSA op kind that emitted it: [tag] body, [256 + tag] inside the division
 // subroutine called by that op (tag 255 = prologue / untagged)
@@ -117,6 +119,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
         if (m.op <= M_V_CMP_LE_F64) {
             const bool wd = is_wide(m);
             ++g_counts.valu;
+            g_counts.alive_valu += __builtin_popcountll(g_alive) / 64.0;
             g_counts.wide += wd;
             g_counts.f64 += m.op >= M_V_CVT_F64_U32;
             if (depth) { ++g_counts.div_valu; g_counts.div_wide += wd; }
@@ -306,6 +309,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 uint64_t r = m.op == M_S_AND_B64 ? a & b : m.op == M_S_OR_B64 ? a | b :
                              m.op == M_S_XOR_B64 ? a ^ b : m.op == M_S_XNOR_B64 ? ~(a ^ b) :
                              m.op == M_S_ANDN2_B64 ? a & ~b : a | ~b;
+                if (m.op == M_S_AND_B64 && o[0].k == O_S && o[0].v == S_SCRATCH) g_alive = r;
                 w.set_mask(o[0], r);
                 w.scc = r != 0;
                 break;
@@ -454,6 +458,7 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
                         const uint64_t row = base + (uint64_t)l < rows ? base + (uint64_t)l : 0;
                         w.v[R_COL0 + 8 * c + k][l] = assign[((uint64_t)c * 8 + k) * rows + row];
                     }
+            g_alive = (uint64_t)w.s[S_VALID] | ((uint64_t)w.s[S_VALID + 1] << 32);
             run(w, tc.code, div);
             ++chunks;
             const uint64_t res = (uint64_t)w.s[S_RES] | ((uint64_t)w.s[S_RES + 1] << 32);
@@ -478,6 +483,7 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
     info[11] = (uint32_t)(g_counts.div_valu / chunks);
     info[12] = (uint32_t)(g_counts.div_wide / chunks);
     info[13] = (uint32_t)(g_counts.f64 / chunks);
+    info[14] = (uint32_t)(g_counts.alive_valu * 16.0 / (double)chunks);  // x16 fixed point
     return 0;
 }
 
