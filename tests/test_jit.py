@@ -367,3 +367,28 @@ def test_short_circuit_jit(emu):
         want = int(smt_eval.evaluate(ts2.tapes[0].nodes, ts2.pool.values, soa_row(soa2, r)))
         assert res.values[r] == want, r
     assert res.values[0] == 1 or res.values[5] == 1 or res.values[40] == 1
+
+
+def test_short_circuit_constant_conjuncts_jit(emu):
+    """Conjunctions with constant conjuncts (a known-false one is scheduled first and ends every
+    wave by an unconditional branch; a known-true one never tests) and a Bool-valued root that is
+    not a conjunction: values equal the oracle's and the full evaluation's."""
+    ts = TapeSet(["x", "y", "z"])
+    b = ts.builder()
+    x, y, z = (b.var(v, 256) for v in ("x", "y", "z"))
+    lt = b.op(Op.BVULT, x, y)
+    eq = b.op(Op.EQ, b.op(Op.BVAND, z, b.const(1, 256)), b.const(1, 256))
+    mul = b.op(Op.BVUGT, b.op(Op.BVMUL, x, z), y)
+    ts.add(b.finish(b.op(Op.AND, b.op(Op.AND, lt, b.false()), eq)))
+    ts.add(b.finish(b.op(Op.AND, b.op(Op.AND, b.true(), lt), b.op(Op.AND, mul, eq))))
+    ts.add(b.finish(b.op(Op.OR, lt, b.op(Op.AND, eq, mul))))
+    ts.add(b.finish(b.op(Op.AND, lt, lt)))
+    rng = random.Random(12)
+    rows = [[rng.getrandbits(256) for _ in range(3)] for _ in range(130)]
+    soa = soa_of(rows, 3)
+    for sc in (True, False):
+        set_short_circuit(emu, sc)
+        try:
+            assert check_tapes(emu, ts, soa) == len(ts.tapes)
+        finally:
+            set_short_circuit(emu, True)
