@@ -2407,17 +2407,18 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
     out.assign(threads, Built());
     stats.jitted.assign(n_tapes, 0);
     stats.why.assign(n_tapes, std::string());
-    std::vector<uint64_t> bytes(threads, 0), valu(threads, 0), wide(threads, 0);
-    auto work = [&](uint32_t s) {
-        const uint32_t lo = (uint32_t)((uint64_t)n_tapes * s / threads);
-        const uint32_t hi = (uint32_t)((uint64_t)n_tapes * (s + 1) / threads);
-        Built& b = out[s];
+    std::vector<uint64_t> bytes(threads + 1, 0), valu(threads + 1, 0), wide(threads + 1, 0);
+    std::vector<std::vector<uint32_t>> overflow(threads);
+    // one code object from the tapes `list`, emitted under `o`; tapes over the register budget
+    // go to `over` (null: they stay on the interpreter)
+    auto build = [&](const std::vector<uint32_t>& list, const Options& o, Built& b, uint32_t s,
+                     std::vector<uint32_t>* over) {
         std::vector<uint32_t> pool;
         std::unordered_map<std::string, uint32_t> index;
         std::vector<TapeCode> codes;
-        codes.reserve(hi - lo);
+        codes.reserve(list.size());
         std::vector<uint32_t> ids;
-        for (uint32_t t = lo; t < hi; ++t) {
+        for (uint32_t t : list) {
             SsaTape st;
             std::string e;
             if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts, n_consts,
@@ -2425,16 +2426,18 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                 stats.why[t] = "lowering: " + e;
                 continue;
             }
-            TapeCode tc = emit_tape(st, pool, n_vars, opt);
+            TapeCode tc = emit_tape(st, pool, n_vars, o);
             if (tc.ok && code_bytes(tc) > 96 * 1024) {
                 tc.ok = false;
                 tc.why = "tape code larger than 96 KB";
             }
             if (!tc.ok) {
                 stats.why[t] = tc.why;
+                if (over && tc.why.find("VGPR pressure") != std::string::npos) over->push_back(t);
                 continue;
             }
             stats.jitted[t] = 1;
+            stats.why[t].clear();
             bytes[s] += code_bytes(tc);
             valu[s] += tc.n_valu;
             wide[s] += tc.n_valu_wide;
@@ -2459,11 +2462,29 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
             if (!assemble(mv.text, b.hsaco_values, log)) b.err = "assemble (values): " + log.substr(0, 2000);
         }
     };
+    auto work = [&](uint32_t s) {
+        const uint32_t lo = (uint32_t)((uint64_t)n_tapes * s / threads);
+        const uint32_t hi = (uint32_t)((uint64_t)n_tapes * (s + 1) / threads);
+        std::vector<uint32_t> list;
+        for (uint32_t t = lo; t < hi; ++t) list.push_back(t);
+        build(list, opt, out[s], s, &overflow[s]);
+    };
     std::vector<std::thread> pool;
     for (uint32_t s = 1; s < threads; ++s) pool.emplace_back(work, s);
     work(0);
     for (auto& th : pool) th.join();
-    for (uint32_t s = 0; s < threads; ++s) {
+    // occupancy class: the tapes over the register budget, in one code object of their own
+    // with the larger budget (fewer waves per SIMD for them only) instead of the interpreter
+    std::vector<uint32_t> big;
+    for (const auto& v : overflow) big.insert(big.end(), v.begin(), v.end());
+    const uint32_t big_budget = std::max(opt.max_vgpr, opt.max_vgpr_keccak);
+    if (!big.empty() && big_budget > opt.max_vgpr) {
+        Options o2 = opt;
+        o2.max_vgpr = big_budget;
+        out.emplace_back();
+        build(big, o2, out.back(), threads, nullptr);
+    }
+    for (uint32_t s = 0; s < out.size(); ++s) {
         if (!out[s].err.empty()) {
             err = out[s].err;
             return false;
