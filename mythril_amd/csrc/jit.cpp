@@ -1162,6 +1162,14 @@ double sc_cost(const SsaInsn& v) {
 // (0.98), anything else half the time.  The order only moves work, never changes a result.  The
 // chain's ANDs are rebuilt in that order (the last one defines the root), each operand cone is
 // emitted just before the AND that consumes it, in the original relative order.
+bool order_search_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("MH_SC_SEARCH");
+        return e == nullptr || atoi(e) != 0;
+    }();
+    return on;
+}
+
 bool schedule_impl(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t sample_rows,
                    const std::vector<double>* insn_cost, SsaTape& out,
                    std::vector<uint8_t>& check) {
@@ -1274,6 +1282,49 @@ bool schedule_impl(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_
         if (n_alive)
             for (uint32_t r = 0; r < sample_rows; ++r)
                 if (alive[r] && !bits[best][r]) { alive[r] = 0; --n_alive; }
+    }
+    // local search on the sample: the expected VALU of an order is the sum over conjuncts of
+    // (the cost of its cone's new part) x (fraction of the sample's 64-row waves still alive
+    // before it); moving a conjunct to another position is kept when that sum drops
+    if (sample_rows >= 64 && conj.size() > 2 && order_search_enabled()) {
+        const uint32_t nw = sample_rows / 64;
+        auto expected = [&](const std::vector<int>& ord) {
+            std::vector<char> dn(n, 0);
+            std::vector<uint8_t> al(sample_rows, 1);
+            double total = 0;
+            uint32_t waves = nw;
+            for (int k : ord) {
+                double c = 0;
+                for (int i : cone[k])
+                    if (!dn[i]) { c += cost(i); dn[i] = 1; }
+                total += c * (double)waves / (double)nw;
+                waves = 0;
+                for (uint32_t w0 = 0; w0 + 64 <= sample_rows; w0 += 64) {
+                    bool any = false;
+                    for (uint32_t r = w0; r < w0 + 64; ++r) {
+                        al[r] = al[r] && bits[k][r];
+                        any |= al[r] != 0;
+                    }
+                    waves += any;
+                }
+            }
+            return total;
+        };
+        double best_e = expected(order);
+        for (int pass = 0; pass < 4; ++pass) {
+            bool improved = false;
+            for (size_t i = 0; i < order.size(); ++i)
+                for (size_t j = 0; j < order.size(); ++j) {
+                    if (i == j) continue;
+                    std::vector<int> o2 = order;
+                    const int k = o2[i];
+                    o2.erase(o2.begin() + (long)i);
+                    o2.insert(o2.begin() + (long)j, k);
+                    const double e = expected(o2);
+                    if (e < best_e - 1e-9) { best_e = e; order.swap(o2); improved = true; }
+                }
+            if (!improved) break;
+        }
     }
     // every instruction is either in the chain or in some cone (dead code was dropped)
     for (int i = 0; i < n; ++i)
