@@ -2547,8 +2547,106 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
     return true;
 }
 
+namespace {
+
+// VGPRs an instruction writes (first, count); count 0 = none.  VALU ops write o[0] (a pair for
+// v_mad_u64_u32 and the f64 ops) except the compares, which write an SGPR pair / VCC; LDS reads
+// write o[0]; nothing else writes VGPRs.
+std::pair<uint32_t, uint32_t> vgpr_writes(const MI& m) {
+    const bool valu = m.op <= M_V_CMP_LE_F64 &&
+                      !(m.op >= M_V_CMP_EQ && m.op <= M_V_CMP_GE) && m.op != M_V_CMP_LE_F64;
+    const bool lds_read = m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32;
+    if ((valu || lds_read) && m.o[0].k == O_V) return {m.o[0].v, m.o[0].n};
+    return {0, 0};
+}
+
+bool touches(const Opnd& o, uint32_t r) { return o.k == O_V && r >= o.v && r < o.v + o.n; }
+
+// Copy coalescing at division call sites: `v_mov DY+k / DR+k, vX` where vX was written by one
+// single-register VALU instruction earlier in the same straight-line stretch and is dead after
+// the copy -- that instruction writes DY+k / DR+k directly (its reads of vX in between follow)
+// and the copy goes.  Returns the number of copies removed.
+uint32_t coalesce_div_moves(std::vector<MI>& code) {
+    uint32_t removed = 0;
+    std::vector<char> gone(code.size(), 0);
+    for (size_t p = 0; p < code.size(); ++p) {
+        const MI& mv = code[p];
+        if (mv.op != M_V_MOV || mv.e64 || mv.o[0].k != O_V || mv.o[0].n != 1 ||
+            mv.o[1].k != O_V || mv.o[1].n != 1)
+            continue;
+        const uint32_t t = mv.o[0].v, x = mv.o[1].v;
+        if (!((t >= R_DY && t < R_DY + 8) || (t >= R_DR && t < R_DR + 8)) || x < R_TEMP0) continue;
+        // the call this copy feeds: only copies / scalar moves until it
+        size_t c = p + 1;
+        while (c < code.size() && (code[c].op == M_V_MOV || code[c].op == M_S_MOV_B32)) ++c;
+        if (c >= code.size() || code[c].op != M_CALL_DIV) continue;
+        // x dead after the copy (forward, to the tape's end: the subroutine keeps to v40-v79)
+        bool live = false;
+        for (size_t f = p + 1; f < code.size() && !live; ++f) {
+            if (gone[f]) continue;
+            const MI& m = code[f];
+            const auto w = vgpr_writes(m);
+            for (int k = 0; k < 5; ++k) {
+                if (w.second && k == 0) continue;
+                if (touches(m.o[k], x)) live = true;
+            }
+            if (!live && w.second && x >= w.first && x < w.first + w.second) break;  // rewritten
+        }
+        if (live) continue;
+        // the producer: the last writer of x, in straight-line code, with t untouched since
+        size_t q = p;
+        bool ok = false;
+        while (q-- > 0) {
+            if (gone[q]) continue;
+            const MI& m = code[q];
+            if (m.op == M_LABEL || m.op == M_CALL_DIV || m.op == M_CALL_KEC || m.op == M_RET ||
+                m.op == M_S_CBRANCH_SCC0 || m.op == M_S_CBRANCH_SCC1 || m.op == M_S_BRANCH)
+                break;
+            bool tt = false, pair_read = false;
+            const auto w = vgpr_writes(m);
+            for (int k = 0; k < 5; ++k) {
+                tt |= touches(m.o[k], t);
+                if (!(w.second && k == 0) && m.o[k].n > 1 && touches(m.o[k], x)) pair_read = true;
+            }
+            if (w.second && x >= w.first && x < w.first + w.second) {
+                ok = w.second == 1 && w.first == x && !tt;
+                break;
+            }
+            if (tt || pair_read) break;
+        }
+        if (!ok) continue;
+        code[q].o[0].v = t;
+        for (size_t i = q + 1; i < p; ++i)
+            for (int k = 0; k < 5; ++k)
+                if (code[i].o[k].k == O_V && code[i].o[k].n == 1 && code[i].o[k].v == x)
+                    code[i].o[k].v = t;
+        gone[p] = 1;
+        ++removed;
+    }
+    if (removed) {
+        std::vector<MI> out;
+        out.reserve(code.size() - removed);
+        for (size_t i = 0; i < code.size(); ++i)
+            if (!gone[i]) out.push_back(code[i]);
+        code.swap(out);
+    }
+    return removed;
+}
+
+}  // namespace
+
 TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
                    const Options& opt) {
+    TapeCode tc = emit_tape_body(st, pool, n_vars, opt);
+    if (tc.ok && opt.coalesce) {
+        const uint32_t r = coalesce_div_moves(tc.code);
+        tc.n_valu -= r;
+    }
+    return tc;
+}
+
+TapeCode emit_tape_body(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
+                        const Options& opt) {
     // source order first: the tape's code when there is no conjunction to reorder, and the VALU
     // each SSA instruction costs (the scheduler's cost model) when there is
     std::vector<double> cost;

@@ -149,6 +149,9 @@ struct Options {
     // Conjunct order: pass rates measured on this many sample rows (uniform 256-bit columns,
     // compile.h sample_bools); 0 = static guesses only.
     uint32_t sample_rows = 256;
+    // Producers of division operands write the subroutine's input registers directly where the
+    // copy at the call site would be the value's last use (coalesce_div_moves).
+    bool coalesce = true;
 };
 
 // The SSA of `st` reordered for short-circuit evaluation of its root conjunction (insn_cost: VALU
@@ -163,6 +166,8 @@ bool schedule_conjuncts(const SsaTape& st, const std::vector<uint32_t>& pool,
 // Emit one tape (SSA after folding) with constants from `pool` (8 limbs per entry).
 TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
                    const Options& opt);
+TapeCode emit_tape_body(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
+                        const Options& opt);  // emit_tape without the copy coalescing
 
 // The division subroutine (x in v[R_DR..], y in v[R_DY..], kind in S_DIV_KIND: 0 udiv, 1 urem,
 // 2 sdiv, 3 srem, 4 smod; result in v[R_DQ..]).
