@@ -21,7 +21,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -2450,25 +2452,59 @@ uint32_t default_group_bytes() {
     return g;
 }
 
+// VGPRs a code object holding tape `tc` allocates (build_module's rule for one tape).
+uint32_t module_vgprs(const TapeCode& tc, uint32_t n_vars) {
+    uint32_t v = std::max<uint32_t>(R_COL0 + 8 * n_vars, tc.max_vgpr);
+    if (tc.calls_kec) v = std::max<uint32_t>(v, R_TEMP_KEC);
+    if (tc.calls_div) v = std::max<uint32_t>(v, R_TEMP0);
+    return (std::max<uint32_t>(v, 8) + 7) & ~7u;
+}
+
+// Occupancy classes below the budget (MH_JIT_CLASSES, comma-separated VGPR ceilings): a code
+// object's waves per SIMD are set by its worst tape, so tapes can be binned by the VGPRs their
+// code object needs, each bin its own code object(s).  Off by default: on MI355X, config 5
+// (profiles/r02ad), one class 3.383e11 evals/s, {64, 80, 96} 3.384-3.386e11, {72, 80, 96}
+// 3.389e11, {80, 96} 3.392e11 -- within run-to-run noise, as an issue-bound kernel predicts
+// (more waves per SIMD do not add VALU issue slots).
+std::vector<uint32_t> occupancy_classes(uint32_t budget) {
+    std::vector<uint32_t> c;
+    if (const char* e = std::getenv("MH_JIT_CLASSES")) {
+        c.clear();
+        for (const char* p = e; *p;) {
+            char* q = nullptr;
+            const unsigned long x = strtoul(p, &q, 10);
+            if (q == p) break;
+            if (x >= 16 && x < budget) c.push_back((uint32_t)x);
+            p = *q ? q + 1 : q;
+        }
+    }
+    std::sort(c.begin(), c.end());
+    c.erase(std::unique(c.begin(), c.end()), c.end());
+    while (!c.empty() && c.back() >= budget) c.pop_back();
+    c.push_back(budget);
+    return c;
+}
+
 bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                    const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, bool values,
                    const Options& opt, uint32_t threads, std::vector<Built>& out,
                    BuildStats& stats, std::string& err) {
     threads = std::max<uint32_t>(1, std::min<uint32_t>(threads, (n_tapes + 63) / 64));
-    out.assign(threads, Built());
+    out.clear();
     stats.jitted.assign(n_tapes, 0);
     stats.why.assign(n_tapes, std::string());
-    std::vector<uint64_t> bytes(threads + 1, 0), valu(threads + 1, 0), wide(threads + 1, 0);
-    std::vector<std::vector<uint32_t>> overflow(threads);
-    // one code object from the tapes `list`, emitted under `o`; tapes over the register budget
-    // go to `over` (null: they stay on the interpreter)
-    auto build = [&](const std::vector<uint32_t>& list, const Options& o, Built& b, uint32_t s,
-                     std::vector<uint32_t>* over) {
+    // 1. emission, one slice of consecutive tapes per thread; tapes over the register budget go
+    //    to `over` (null: they stay on the interpreter)
+    struct Slice {
+        std::vector<TapeCode> codes;
+        std::vector<uint32_t> ids, over;
+    };
+    std::vector<Slice> slices(threads + 1);
+    auto emit_list = [&](const std::vector<uint32_t>& list, const Options& o, Slice& sl,
+                         bool keep_over) {
         std::vector<uint32_t> pool;
         std::unordered_map<std::string, uint32_t> index;
-        std::vector<TapeCode> codes;
-        codes.reserve(list.size());
-        std::vector<uint32_t> ids;
+        sl.codes.reserve(list.size());
         for (uint32_t t : list) {
             SsaTape st;
             std::string e;
@@ -2484,33 +2520,14 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
             }
             if (!tc.ok) {
                 stats.why[t] = tc.why;
-                if (over && tc.why.find("VGPR pressure") != std::string::npos) over->push_back(t);
+                if (keep_over && tc.why.find("VGPR pressure") != std::string::npos)
+                    sl.over.push_back(t);
                 continue;
             }
             stats.jitted[t] = 1;
             stats.why[t].clear();
-            bytes[s] += code_bytes(tc);
-            valu[s] += tc.n_valu;
-            wide[s] += tc.n_valu_wide;
-            codes.push_back(std::move(tc));
-            ids.push_back(t);
-        }
-        b.tape_ids = ids;
-        if (codes.empty()) return;
-        std::vector<const TapeCode*> ptrs;
-        for (const TapeCode& c : codes) ptrs.push_back(&c);
-        const uint32_t group_bytes = default_group_bytes();
-        Module m = build_module(ptrs, ids, n_vars, false, group_bytes);
-        b.n_groups = (uint32_t)m.group_first.size();
-        b.max_vgpr = m.max_vgpr;
-        std::string log;
-        if (!assemble(m.text, b.hsaco, log)) {
-            b.err = "assemble: " + log.substr(0, 2000);
-            return;
-        }
-        if (values) {
-            Module mv = build_module(ptrs, ids, n_vars, true, group_bytes);
-            if (!assemble(mv.text, b.hsaco_values, log)) b.err = "assemble (values): " + log.substr(0, 2000);
+            sl.codes.push_back(std::move(tc));
+            sl.ids.push_back(t);
         }
     };
     auto work = [&](uint32_t s) {
@@ -2518,31 +2535,95 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
         const uint32_t hi = (uint32_t)((uint64_t)n_tapes * (s + 1) / threads);
         std::vector<uint32_t> list;
         for (uint32_t t = lo; t < hi; ++t) list.push_back(t);
-        build(list, opt, out[s], s, &overflow[s]);
+        emit_list(list, opt, slices[s], true);
     };
-    std::vector<std::thread> pool;
-    for (uint32_t s = 1; s < threads; ++s) pool.emplace_back(work, s);
-    work(0);
-    for (auto& th : pool) th.join();
-    // occupancy class: the tapes over the register budget, in one code object of their own
-    // with the larger budget (fewer waves per SIMD for them only) instead of the interpreter
+    {
+        std::vector<std::thread> pool;
+        for (uint32_t s = 1; s < threads; ++s) pool.emplace_back(work, s);
+        work(0);
+        for (auto& th : pool) th.join();
+    }
+    // the tapes over the register budget, emitted with the larger one (fewer waves per SIMD for
+    // them only) instead of the interpreter
     std::vector<uint32_t> big;
-    for (const auto& v : overflow) big.insert(big.end(), v.begin(), v.end());
+    for (uint32_t s = 0; s < threads; ++s)
+        big.insert(big.end(), slices[s].over.begin(), slices[s].over.end());
     const uint32_t big_budget = std::max(opt.max_vgpr, opt.max_vgpr_keccak);
     if (!big.empty() && big_budget > opt.max_vgpr) {
         Options o2 = opt;
         o2.max_vgpr = big_budget;
-        out.emplace_back();
-        build(big, o2, out.back(), threads, nullptr);
+        emit_list(big, o2, slices[threads], false);
     }
-    for (uint32_t s = 0; s < out.size(); ++s) {
-        if (!out[s].err.empty()) {
-            err = out[s].err;
+    // 2. occupancy classes over every emitted tape (tape order kept inside a class), each class
+    //    cut into pieces of about n_tapes / threads tapes: one code object per piece
+    const std::vector<uint32_t> cls = occupancy_classes(opt.max_vgpr);
+    struct Piece {
+        std::vector<const TapeCode*> codes;
+        std::vector<uint32_t> ids;
+    };
+    std::vector<std::vector<std::pair<const TapeCode*, uint32_t>>> bins(cls.size() + 1);
+    for (const Slice& sl : slices)
+        for (size_t i = 0; i < sl.codes.size(); ++i) {
+            const TapeCode& tc = sl.codes[i];
+            stats.code_bytes += code_bytes(tc);
+            stats.valu_static += tc.n_valu;
+            stats.valu_wide_static += tc.n_valu_wide;
+            const uint32_t need = module_vgprs(tc, n_vars);
+            size_t c = 0;
+            while (c < cls.size() && need > cls[c]) ++c;
+            bins[c].push_back({&tc, sl.ids[i]});
+        }
+    const size_t per_piece = std::max<size_t>(64, (n_tapes + threads - 1) / threads);
+    std::vector<Piece> pieces;
+    for (auto& bin : bins) {
+        if (bin.empty()) continue;
+        std::stable_sort(bin.begin(), bin.end(),
+                         [](const auto& a, const auto& b) { return a.second < b.second; });
+        const size_t n_p = (bin.size() + per_piece - 1) / per_piece;
+        for (size_t p = 0; p < n_p; ++p) {
+            pieces.emplace_back();
+            const size_t lo = bin.size() * p / n_p, hi = bin.size() * (p + 1) / n_p;
+            for (size_t i = lo; i < hi; ++i) {
+                pieces.back().codes.push_back(bin[i].first);
+                pieces.back().ids.push_back(bin[i].second);
+            }
+        }
+    }
+    // 3. module text and assembly, the pieces shared out over the threads
+    out.assign(pieces.size(), Built());
+    const uint32_t group_bytes = default_group_bytes();
+    std::atomic<size_t> next{0};
+    auto assemble_work = [&]() {
+        for (size_t p; (p = next.fetch_add(1)) < pieces.size();) {
+            Built& b = out[p];
+            b.tape_ids = pieces[p].ids;
+            Module m = build_module(pieces[p].codes, pieces[p].ids, n_vars, false, group_bytes);
+            b.n_groups = (uint32_t)m.group_first.size();
+            b.max_vgpr = m.max_vgpr;
+            std::string log;
+            if (!assemble(m.text, b.hsaco, log)) {
+                b.err = "assemble: " + log.substr(0, 2000);
+                continue;
+            }
+            if (values) {
+                Module mv = build_module(pieces[p].codes, pieces[p].ids, n_vars, true, group_bytes);
+                if (!assemble(mv.text, b.hsaco_values, log))
+                    b.err = "assemble (values): " + log.substr(0, 2000);
+            }
+        }
+    };
+    {
+        std::vector<std::thread> pool;
+        const size_t nt = std::min<size_t>(std::max<uint32_t>(threads, 1), pieces.size());
+        for (size_t s = 1; s < nt; ++s) pool.emplace_back(assemble_work);
+        assemble_work();
+        for (auto& th : pool) th.join();
+    }
+    for (const Built& b : out) {
+        if (!b.err.empty()) {
+            err = b.err;
             return false;
         }
-        stats.code_bytes += bytes[s];
-        stats.valu_static += valu[s];
-        stats.valu_wide_static += wide[s];
     }
     return true;
 }

@@ -211,9 +211,11 @@ uint32_t code_bytes(const TapeCode& tc);
 // comgr: assemble + link `text` into a gfx950 code object (jit_comgr.cpp).
 bool assemble(const std::string& text, std::vector<char>& hsaco, std::string& log);
 
-// A whole tape set to code objects: tapes are lowered and emitted, cut into `threads` contiguous
-// slices, and each slice becomes one code object (count kernel, and the values kernel when
-// asked), built and assembled on its own thread.  No HIP calls: capi.cpp loads the results.
+// A whole tape set to code objects: tapes are lowered and emitted over `threads` contiguous
+// slices, binned into occupancy classes by the VGPRs their code object needs
+// (occupancy_classes), and each class cut into pieces of about n_tapes / threads tapes; each
+// piece becomes one code object (count kernel, and the values kernel when asked), assembled on
+// `threads` threads.  No HIP calls: capi.cpp loads the results.
 struct Built {
     std::vector<char> hsaco, hsaco_values;
     uint32_t n_groups = 0;
@@ -226,6 +228,8 @@ struct BuildStats {
     std::vector<std::string> why;      // per tape: reason when not jitted
     uint64_t code_bytes = 0, valu_static = 0, valu_wide_static = 0;
 };
+uint32_t module_vgprs(const TapeCode& tc, uint32_t n_vars);
+std::vector<uint32_t> occupancy_classes(uint32_t budget);  // ascending ceilings, last = budget
 bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                    const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, bool values,
                    const Options& opt, uint32_t threads, std::vector<Built>& out,

@@ -151,3 +151,24 @@ def jit_module(emu: "Emulator", ts: TapeSet, values: bool = False, max_vgpr: int
     if n < 0:
         raise EmuError(int(n), err.value.decode())
     return text.value.decode(), int(hs.value), int(nj.value)
+
+
+def jit_build(emu: "Emulator", ts: TapeSet, max_vgpr: int = 128, threads: int = 4):
+    """build_tapeset as mh_tapes_jit runs it: ([(max_vgpr, n_tapes)] per code object, per-tape
+    object index or -1)."""
+    f = _jit_fn(emu.lib, "emu_jit_build", C.c_int32,
+                [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                 C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_char_p, C.c_int])
+    nodes, offs, consts = ts.flatten()
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32)
+    objs = np.zeros(2 * 256, dtype=np.uint32)
+    tape_obj = np.zeros(len(ts.tapes), dtype=np.int32)
+    err = C.create_string_buffer(8192)
+    n = f(nodes.ctypes.data, offs.ctypes.data, len(ts.tapes), consts.ctypes.data,
+          len(ts.pool.values), ts.n_vars, max_vgpr, threads, objs.ctypes.data, 256,
+          tape_obj.ctypes.data, err, 8192)
+    if n < 0:
+        raise EmuError(int(n), err.value.decode())
+    return [(int(objs[2 * i]), int(objs[2 * i + 1])) for i in range(min(n, 256))], tape_obj

@@ -562,3 +562,33 @@ extern "C" void emu_jit_div_hist(uint64_t* out, int reset) {
         if (reset) g_div_hist[i] = 0;
     }
 }
+
+// build_tapeset as mh_tapes_jit runs it (no device): per code object, its max VGPR count and
+// tape count into objs[2 i], objs[2 i + 1] (at most max_objs), and each tape's object index
+// (or -1: not jitted) into tape_obj.  Returns the number of code objects, < 0 on error.
+extern "C" int32_t emu_jit_build(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
+                                 const uint32_t* consts, uint32_t n_consts, uint32_t n_vars,
+                                 uint32_t max_vgpr, uint32_t threads, uint32_t* objs,
+                                 uint32_t max_objs, int32_t* tape_obj, char* err, int errlen) {
+    Options opt;
+    opt.max_vgpr = max_vgpr;
+    opt.short_circuit = g_short_circuit;
+    opt.sample_rows = g_sample_rows;
+    std::vector<Built> built;
+    BuildStats stats;
+    std::string e;
+    if (!build_tapeset(nodes, offs, n_tapes, consts, n_consts, n_vars, false, opt, threads, built,
+                       stats, e)) {
+        snprintf(err, errlen, "%s", e.c_str());
+        return -1;
+    }
+    for (uint32_t t = 0; t < n_tapes; ++t) tape_obj[t] = -1;
+    for (uint32_t i = 0; i < built.size(); ++i) {
+        if (i < max_objs) {
+            objs[2 * i] = built[i].max_vgpr;
+            objs[2 * i + 1] = (uint32_t)built[i].tape_ids.size();
+        }
+        for (uint32_t t : built[i].tape_ids) tape_obj[t] = (int32_t)i;
+    }
+    return (int32_t)built.size();
+}

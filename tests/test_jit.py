@@ -12,7 +12,7 @@ import pytest
 from mythril_amd import synth
 from mythril_amd.tape import Op, TapeSet
 from oracle import smt_eval
-from tests.emu import jit_eval, jit_module, set_short_circuit
+from tests.emu import jit_build, jit_eval, jit_module, set_short_circuit
 from tests.evm_translate import Unsupported, lift_constants, vmtest_tapes
 from tests.fuzz import TapeFuzzer, assignment_soa, soa_row
 
@@ -254,6 +254,32 @@ def test_module_assembles(emu):
         assert nj >= 110
         assert nbytes > 1000
         assert ".amdhsa_kernel mh_jit" in text
+
+
+def test_occupancy_classes(emu, monkeypatch):
+    """build_tapeset bins tapes by the VGPRs their code object needs: every jitted tape lands in
+    exactly one code object, each object's VGPR count is within its class ceiling (so it runs at
+    that class's waves per SIMD), tapes keep their order inside an object, and one class (the
+    default, MH_JIT_CLASSES=0) gives the same tapes in objects at the single budget."""
+    ts = synth.generate(300)
+    monkeypatch.setenv("MH_JIT_CLASSES", "64,80,96")
+    objs, where = jit_build(emu, ts)
+    assert (where >= 0).sum() == 300
+    ceilings = (64, 80, 96, 128)
+    for i, (maxv, n) in enumerate(objs):
+        assert n == (where == i).sum() and n > 0
+        assert maxv <= 128
+    # objects of a lower class really are smaller (more waves per SIMD)
+    assert min(m for m, _ in objs) <= 80
+    classes = sorted({min(c for c in ceilings if c >= m) for m, _ in objs})
+    assert len(classes) >= 2, objs
+    for i in range(len(objs)):
+        ids = np.nonzero(where == i)[0]
+        assert np.all(np.diff(ids) > 0)
+    monkeypatch.setenv("MH_JIT_CLASSES", "0")
+    objs1, where1 = jit_build(emu, ts)
+    assert np.array_equal(where1 >= 0, where >= 0)
+    assert len(objs1) <= 4
 
 
 def test_jit_coverage_and_static_cost(emu):
