@@ -251,8 +251,9 @@ int32_t mh_comm_destroy(mh_ctx* ctx);
  * 2 v_add_u32; 3 v_xor_b32; 4 v_alignbit_b32; 5 v_cndmask_b32; 6 v_or3_b32; 7 v_readlane_b32;
  * 8 v_mov_b32; 9 v_add_co_u32 (carry-out only); 10 v_sub_co/v_subb through VCC;
  * 11 v_cndmask_b32_e32 (VCC mask); 12 v_cmp_eq_u32_e32 (VCC write); 13 v_xor_b32 with a literal;
- * 14 v_lshlrev_b32; 15 v_add3_u32; 16 v_fma_f64.                                                 */
-#define MH_MB_NUM_KINDS 17
+ * 14 v_lshlrev_b32; 15 v_add3_u32; 16 v_fma_f64; 17 v_xnor_b32; 18 v_and_b32; 19 v_or_b32;
+ * 20 v_not_b32.                                                                                  */
+#define MH_MB_NUM_KINDS 21
 int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
                             double* lane_ops_per_s);
 /* Round-1 form: kinds 0..2 of mh_microbench_issue at 8 waves per SIMD.                           */

@@ -1559,6 +1559,7 @@ const char* op_name(uint16_t op) {
         case M_V_OR: return "v_or_b32";
         case M_V_XOR: return "v_xor_b32";
         case M_V_NOT: return "v_not_b32";
+        case M_V_XNOR: return "v_xnor_b32";
         case M_V_OR3: return "v_or3_b32";
         case M_V_ALIGNBIT: return "v_alignbit_b32";
         case M_V_LSHLREV: return "v_lshlrev_b32";
@@ -1961,6 +1962,41 @@ const int kRhoPi[24][2] = {{10, 1}, {7, 3},   {11, 6},  {17, 10}, {18, 15}, {3, 
                            {20, 62}, {14, 18}, {22, 39}, {9, 61},  {6, 20},  {1, 44}};
 }  // namespace
 
+namespace {
+
+// Complement states through theta: a column parity is stored complemented when an odd number of
+// its lanes are, D[x] = C[x-1] ^ rot(C[x+1], 1) when exactly one of the two is, and lane (x, y) ^= D[x].
+void kec_theta_states(uint8_t* comp) {
+    uint8_t c[5] = {0}, d[5];
+    for (int i = 0; i < 25; ++i) c[i % 5] ^= comp[i];
+    for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ c[(x + 1) % 5];
+    for (int i = 0; i < 25; ++i) comp[i] ^= d[i % 5];
+}
+
+// ... and through rho + pi (rotations keep a complement; pi moves it with the lane).
+void kec_rhopi_states(uint8_t* comp) {
+    uint8_t cur = comp[1];
+    for (int step = 0; step < 24; ++step) {
+        const int dst = kRhoPi[step][0];
+        const uint8_t t = comp[dst];
+        comp[dst] = cur;
+        cur = t;
+    }
+}
+
+// The complement plan (scripts/kec_plan.py, a beam search over the issue cost): lanes stored
+// complemented at entry (two v_not each), and per round the state of every chi output (bit
+// x + 5y).  Positions whose operands share a state keep b0's state whatever the plan says (v_bfi);
+// the free ones take the planned state (xor, or xnor when it is not the natural one).  Over the
+// 24 rounds: 132 v_bfi positions of 600 and 34 xnor positions, vs 600 v_bfi without complements.
+const uint32_t kKecInit = 0x0400000u;
+const uint32_t kKecPlan[24] = {
+    0x068bb68u, 0x02e4e13u, 0x1c06466u, 0x0c37227u, 0x0c4310cu, 0x1102786u, 0x19c30d0u, 0x0766471u,
+    0x110c621u, 0x0601678u, 0x10ce186u, 0x1c8e266u, 0x04310c6u, 0x0096583u, 0x138e181u, 0x191c4ecu,
+    0x0431886u, 0x0a3c580u, 0x11c1863u, 0x1889592u, 0x1319212u, 0x03218c6u, 0x0c5a310u, 0x0cc2090u};
+
+}  // namespace
+
 const KecCode& kec_routine() {
     static const KecCode kc = [] {
         KecCode k;
@@ -1985,6 +2021,23 @@ const KecCode& kec_routine() {
             return r;
         };
         auto give = [&](uint32_t r) { spare.push_back(r); };
+        // lane complementing (MH_JIT_KEC_COMPLEMENT=0 turns it off): per-lane stored-complemented
+        // flags, tracked through theta and rho-pi at build time, and the chi output states of
+        // every round (kKecPlan)
+        static const bool complement = [] {
+            const char* e = std::getenv("MH_JIT_KEC_COMPLEMENT");
+            return !(e && atoi(e) == 0);
+        }();
+        uint8_t comp[25] = {0};
+        uint8_t plan[24][25];
+        for (int r = 0; r < 24; ++r)
+            for (int i = 0; i < 25; ++i) plan[r][i] = (uint8_t)((kKecPlan[r] >> i) & 1);
+        if (complement)
+            for (int i = 0; i < 25; ++i)
+                if ((kKecInit >> i) & 1) {
+                    comp[i] = 1;
+                    for (int h = 0; h < 2; ++h) E(M_V_NOT, {V(map[i][h]), V(map[i][h])});
+                }
         // rotl64 of (lo, hi) by r (1..63, not 32) into two fresh registers
         auto rotl = [&](uint32_t lo, uint32_t hi, int r, uint32_t* out) {
             if (r > 32) { std::swap(lo, hi); r -= 32; }
@@ -2015,6 +2068,7 @@ const KecCode& kec_routine() {
                 give(d[1]);
             }
             for (int x = 0; x < 5; ++x) { give(c[x][0]); give(c[x][1]); }
+            kec_theta_states(comp);
             // rho + pi
             uint32_t cur[2] = {map[1][0], map[1][1]};
             for (int step = 0; step < 24; ++step) {
@@ -2030,24 +2084,47 @@ const KecCode& kec_routine() {
                 cur[1] = t[1];
                 // the last step's t is lane 1's original registers, freed by the first step
             }
-            // chi
+            kec_rhopi_states(comp);
+            // chi, on lanes that may be stored complemented (comp[i]: register value = ~lane i).
+            // Row y, position x: o = b0 ^ (~b1 & b2).  With b1, b2 in opposite complement states
+            // ~b1 & b2 is one AND (b1 stored complemented) or the complement of one OR (b2 stored
+            // complemented), and the output's complement state is free: xor or xnor with b0.
+            // With equal states it is v_bfi over the stored values (state of b0 kept).  The
+            // states chosen for the free outputs (kKecPlan) keep both rare.
             for (int y = 0; y < 25; y += 5) {
                 uint32_t nrow[5][2];
-                for (int x = 0; x < 5; ++x)
+                uint8_t ncomp[5];
+                for (int x = 0; x < 5; ++x) {
+                    const int i0 = y + x, i1 = y + (x + 1) % 5, i2 = y + (x + 2) % 5;
+                    const bool r1 = comp[i1], r2 = comp[i2];
                     for (int h = 0; h < 2; ++h) {
-                        const uint32_t b0 = map[y + x][h], b1 = map[y + (x + 1) % 5][h],
-                                       b2 = map[y + (x + 2) % 5][h];
+                        const uint32_t b0 = map[i0][h], b1 = map[i1][h], b2 = map[i2][h];
                         const uint32_t t = take();
-                        E(M_V_XOR, {V(t), V(b0), V(b2)});
                         nrow[x][h] = take();
-                        E(M_V_BFI, {V(nrow[x][h]), V(b1), V(b0), V(t)});
+                        if (!complement || r1 == r2) {
+                            // r1 = r2 = 0: b0' ^ (~b1' & b2') = bfi(b1', b0', b0' ^ b2');
+                            // r1 = r2 = 1: ~b1 & b2 = b1' & ~b2' -> bfi(b2', b0', b0' ^ b1')
+                            const uint32_t sel = r1 ? b2 : b1, oth = r1 ? b1 : b2;
+                            E(M_V_XOR, {V(t), V(b0), V(oth)});
+                            E(M_V_BFI, {V(nrow[x][h]), V(sel), V(b0), V(t)});
+                        } else {
+                            E(r1 ? M_V_AND : M_V_OR, {V(t), V(b1), V(b2)});
+                            // natural state of b0' ^ t: comp[i0] (AND), comp[i0] ^ 1 (OR)
+                            const bool nat = comp[i0] ^ !r1;
+                            E(nat == plan[round][i0] ? M_V_XOR : M_V_XNOR,
+                              {V(nrow[x][h]), V(b0), V(t)});
+                        }
                         give(t);
                     }
-                for (int x = 0; x < 5; ++x)
+                    ncomp[x] = (!complement || r1 == r2) ? comp[i0] : plan[round][i0];
+                }
+                for (int x = 0; x < 5; ++x) {
+                    comp[y + x] = ncomp[x];
                     for (int h = 0; h < 2; ++h) {
                         give(map[y + x][h]);
                         map[y + x][h] = nrow[x][h];
                     }
+                }
             }
             // iota
             const uint64_t rc = kKeccakRC[round];
@@ -2057,6 +2134,7 @@ const KecCode& kec_routine() {
             }
         }
         for (int i = 0; i < 4; ++i) {
+            for (int h = 0; h < 2 && comp[i]; ++h) E(M_V_NOT, {V(map[i][h]), V(map[i][h])});
             k.out[2 * i] = map[i][0];
             k.out[2 * i + 1] = map[i][1];
         }

@@ -55,7 +55,7 @@ enum Op : uint16_t {
     // VALU (e64 flag selects the VOP3 encoding where both exist)
     M_V_MOV, M_V_ADD_U32, M_V_SUB_U32, M_V_SUBREV_U32,
     M_V_ADD_CO, M_V_ADDC_CO, M_V_SUB_CO, M_V_SUBB_CO, M_V_SUBREV_CO, M_V_SUBBREV_CO,
-    M_V_AND, M_V_OR, M_V_XOR, M_V_NOT, M_V_OR3,
+    M_V_AND, M_V_OR, M_V_XOR, M_V_NOT, M_V_OR3, M_V_XNOR,
     M_V_ALIGNBIT, M_V_LSHLREV, M_V_LSHRREV, M_V_ASHRREV,
     M_V_CNDMASK,   // d = mask ? src1 : src0
     M_V_CMP_EQ, M_V_CMP_NE, M_V_CMP_LT, M_V_CMP_LE, M_V_CMP_GT, M_V_CMP_GE,  // u32

@@ -410,6 +410,12 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink
                              : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "v"(e));
                 a0 = (u32)d0 ^ (u32)d1 ^ (u32)d2 ^ (u32)d3;
             }
+            if constexpr (KIND == 17) MB_ONE("v_xnor_b32");
+            if constexpr (KIND == 18) MB_ONE("v_and_b32");
+            if constexpr (KIND == 19) MB_ONE("v_or_b32");
+            if constexpr (KIND == 20)
+                asm volatile(MB8("v_not_b32 %0, %0\n v_not_b32 %1, %1\n v_not_b32 %2, %2\n v_not_b32 %3, %3\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
 #undef MB_ONE
         }
     }
@@ -480,7 +486,7 @@ hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uin
     case k: hipLaunchKernelGGL(microbench_kernel<k>, dim3(blocks), dim3(kBlock), 0, stream, iters, sink); break;
         MB_CASE(0) MB_CASE(1) MB_CASE(2) MB_CASE(3) MB_CASE(4) MB_CASE(5) MB_CASE(6) MB_CASE(7)
         MB_CASE(8) MB_CASE(9) MB_CASE(10) MB_CASE(11) MB_CASE(12) MB_CASE(13) MB_CASE(14)
-        MB_CASE(15) MB_CASE(16)
+        MB_CASE(15) MB_CASE(16) MB_CASE(17) MB_CASE(18) MB_CASE(19) MB_CASE(20)
 #undef MB_CASE
         default: return hipErrorInvalidValue;
     }

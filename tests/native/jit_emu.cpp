@@ -185,6 +185,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
             case M_V_OR: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) | w.r32(o[2], l); }); break;
             case M_V_XOR: each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) ^ w.r32(o[2], l); }); break;
             case M_V_NOT: each([&](int l) { w.v[o[0].v][l] = ~w.r32(o[1], l); }); break;
+            case M_V_XNOR: each([&](int l) { w.v[o[0].v][l] = ~(w.r32(o[1], l) ^ w.r32(o[2], l)); }); break;
             case M_V_OR3:
                 each([&](int l) { w.v[o[0].v][l] = w.r32(o[1], l) | w.r32(o[2], l) | w.r32(o[3], l); });
                 break;

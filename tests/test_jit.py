@@ -167,6 +167,25 @@ def test_keccak_variant_tapes_jit(emu):
     assert check_tapes(emu, ts, soa, require_all=False) >= 22
 
 
+def test_keccak_complement_plan(emu, monkeypatch):
+    """Lane complementing in the Keccak-f[1600] subroutine: chi mostly as AND / OR + xor
+    (2-cycle VALU) instead of xor + v_bfi (4-cycle), the same instruction count; the values are
+    pinned by the keccak tests above (emulator) and tests/test_gpu_jit.py (device)."""
+    import collections
+
+    ts = synth.generate(2, keccak=True)
+    text, _, _ = jit_module(emu, ts, max_vgpr=168, assemble=False)
+    kec = text[text.index("mh_kec:"):text.index(".Lmh_jit_end")]
+    ops = collections.Counter(ln.split()[0] for ln in kec.splitlines()
+                              if ln.strip() and not ln.strip().endswith(":")
+                              and not ln.startswith("."))
+    assert ops["v_bfi_b32"] <= 24 * 12, ops
+    assert ops["v_xnor_b32"] <= 24 * 4, ops
+    assert ops["v_and_b32"] + ops["v_or_b32"] >= 24 * 36, ops
+    n = sum(ops.values())
+    assert n <= 24 * 260 + 16, ops
+
+
 def test_immediate_and_variable_shifts_jit(emu):
     rng = random.Random(31)
     ts = TapeSet()

@@ -5,7 +5,7 @@ rows): VALU per wave-evaluation, split into 2-cycle and 4-cycle issue classes (t
 issue costs of profiles/r02a/valu_peak.json) and into tape body vs the division subroutine.
 With a measured evals/s it gives the cycle-weighted VALU issue busy of the native kernel.
 
-    python scripts/jit_mix.py [n_tapes] [evals_per_s]
+    python tests/tools/jit_mix.py [n_tapes] [evals_per_s]
 """
 import json
 import os
@@ -13,7 +13,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 from mythril_amd import synth  # noqa: E402
