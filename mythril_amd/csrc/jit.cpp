@@ -2048,14 +2048,17 @@ const KecCode& kec_routine() {
         };
         for (int round = 0; round < 24; ++round) {
             // theta
+            // (the ten column-parity chains interleaved: a wave's dependent VALU ops 10 apart)
             uint32_t c[5][2];
             for (int x = 0; x < 5; ++x)
                 for (int h = 0; h < 2; ++h) {
                     c[x][h] = take();
                     E(M_V_XOR, {V(c[x][h]), V(map[x][h]), V(map[x + 5][h])});
-                    for (int y = 2; y < 5; ++y)
-                        E(M_V_XOR, {V(c[x][h]), V(map[x + 5 * y][h]), V(c[x][h])});
                 }
+            for (int y = 2; y < 5; ++y)
+                for (int x = 0; x < 5; ++x)
+                    for (int h = 0; h < 2; ++h)
+                        E(M_V_XOR, {V(c[x][h]), V(map[x + 5 * y][h]), V(c[x][h])});
             for (int x = 0; x < 5; ++x) {
                 uint32_t d[2];
                 rotl(c[(x + 1) % 5][0], c[(x + 1) % 5][1], 1, d);
@@ -2090,7 +2093,9 @@ const KecCode& kec_routine() {
             // ~b1 & b2 is one AND (b1 stored complemented) or the complement of one OR (b2 stored
             // complemented), and the output's complement state is free: xor or xnor with b0.
             // With equal states it is v_bfi over the stored values (state of b0 kept).  The
-            // states chosen for the free outputs (kKecPlan) keep both rare.
+            // states chosen for the free outputs (kKecPlan) keep both rare.  Per row the ten
+            // first operations come first and the ten second ones then write in place, so
+            // dependent operations are ten apart.
             for (int y = 0; y < 25; y += 5) {
                 uint32_t nrow[5][2];
                 uint8_t ncomp[5];
@@ -2099,22 +2104,28 @@ const KecCode& kec_routine() {
                     const bool r1 = comp[i1], r2 = comp[i2];
                     for (int h = 0; h < 2; ++h) {
                         const uint32_t b0 = map[i0][h], b1 = map[i1][h], b2 = map[i2][h];
-                        const uint32_t t = take();
                         nrow[x][h] = take();
+                        if (!complement || r1 == r2)
+                            E(M_V_XOR, {V(nrow[x][h]), V(b0), V(r1 ? b1 : b2)});
+                        else
+                            E(r1 ? M_V_AND : M_V_OR, {V(nrow[x][h]), V(b1), V(b2)});
+                    }
+                }
+                for (int x = 0; x < 5; ++x) {
+                    const int i0 = y + x, i1 = y + (x + 1) % 5, i2 = y + (x + 2) % 5;
+                    const bool r1 = comp[i1], r2 = comp[i2];
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t b0 = map[i0][h], b1 = map[i1][h], b2 = map[i2][h];
+                        const uint32_t t = nrow[x][h];
                         if (!complement || r1 == r2) {
                             // r1 = r2 = 0: b0' ^ (~b1' & b2') = bfi(b1', b0', b0' ^ b2');
                             // r1 = r2 = 1: ~b1 & b2 = b1' & ~b2' -> bfi(b2', b0', b0' ^ b1')
-                            const uint32_t sel = r1 ? b2 : b1, oth = r1 ? b1 : b2;
-                            E(M_V_XOR, {V(t), V(b0), V(oth)});
-                            E(M_V_BFI, {V(nrow[x][h]), V(sel), V(b0), V(t)});
+                            E(M_V_BFI, {V(t), V(r1 ? b2 : b1), V(b0), V(t)});
                         } else {
-                            E(r1 ? M_V_AND : M_V_OR, {V(t), V(b1), V(b2)});
                             // natural state of b0' ^ t: comp[i0] (AND), comp[i0] ^ 1 (OR)
                             const bool nat = comp[i0] ^ !r1;
-                            E(nat == plan[round][i0] ? M_V_XOR : M_V_XNOR,
-                              {V(nrow[x][h]), V(b0), V(t)});
+                            E(nat == plan[round][i0] ? M_V_XOR : M_V_XNOR, {V(t), V(b0), V(t)});
                         }
-                        give(t);
                     }
                     ncomp[x] = (!complement || r1 == r2) ? comp[i0] : plan[round][i0];
                 }
