@@ -197,26 +197,35 @@ class Sieve:
                 stack += [b.nodes[n][3], b.nodes[n][2]]
             else:
                 conj.append(n)
-        cols: Dict[int, frozenset] = {}
-        order, seen, st = [], set(), [(c, False) for c in conj]
+        # column sets per node, memoised on the builder: nodes are immutable and hash-consed, so
+        # a query that extends its parent (svm.py:257-262) only visits its new nodes
+        cols: Dict[int, frozenset] = b.__dict__.setdefault("_bucket_cols", {})
+        order, st = [], [(c, False) for c in conj if c not in cols]
+        seen = set()
         while st:
             n, done = st.pop()
             if done:
                 order.append(n)
                 continue
-            if n in seen:
+            if n in seen or n in cols:
                 continue
             seen.add(n)
             st.append((n, True))
             op, _, a, bb, c, _, _ = b.nodes[n]
-            st += [(x, False) for x in (a, bb, c)[:ARITY[op]] if x not in seen]
+            st += [(x, False) for x in (a, bb, c)[:ARITY[op]] if x not in seen and x not in cols]
+        empty = frozenset()
         for n in order:
             op, _, a, bb, c, i0, _ = b.nodes[n]
             if op == Op.VAR:
                 cols[n] = frozenset((i0,))
-            else:
-                kids = (a, bb, c)[:ARITY[op]]
-                cols[n] = frozenset().union(*(cols[x] for x in kids)) if kids else frozenset()
+                continue
+            kids = (a, bb, c)[:ARITY[op]]
+            if not kids:
+                cols[n] = empty
+                continue
+            sets = [cols[x] for x in kids]
+            big = max(sets, key=len)
+            cols[n] = big if all(x <= big for x in sets) else big.union(*sets)
         parent: Dict[int, int] = {}
 
         def find(x):
