@@ -101,12 +101,30 @@ def main() -> None:
     assign.generate(seed, index_base)
     fh = torch.empty(n_tapes, dtype=torch.int64, device=dev)
     hc = torch.empty(n_tapes, dtype=torch.int64, device=dev)
+    exchange = None
     if world > 1:
         # the library's own RCCL communicator (mh_comm_init): rank 0's id reaches the others
-        # through torch.distributed; the per-step exchange then never leaves the C-ABI
-        box = [native.comm_unique_id() if rank == 0 else None]
+        # through torch.distributed; the per-step exchange then never leaves the C-ABI.  If any
+        # rank cannot open it, every rank uses torch.distributed's RCCL for the same MIN / SUM
+        # (shard.allreduce_results) instead.
+        box = [None]
+        if rank == 0:
+            try:
+                box = [native.comm_unique_id()]
+            except Exception as e:  # pragma: no cover - depends on the node's RCCL
+                log("[rank 0] mh_comm_unique_id failed: %s" % e)
         dist.broadcast_object_list(box, src=0)
-        ctx.comm_init(box[0], rank, world)
+        ok = 0
+        if box[0] is not None:
+            try:
+                ctx.comm_init(box[0], rank, world)
+                ok = 1
+            except Exception as e:  # pragma: no cover
+                log("[rank %d] mh_comm_init failed: %s" % (rank, e))
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        exchange = "library" if int(flag.item()) == 1 else "torch"
+        log("[rank %d] result exchange: %s" % (rank, exchange))
     torch.cuda.synchronize(dev)
     log("[rank %d] setup %.1fs: %d tapes, %d insns, %d rows, %.0f alg-ops/row"
         % (rank, time.time() - t0, n_tapes, sum(i["n_insns"] for i in info), rows,
@@ -116,8 +134,10 @@ def main() -> None:
         native.results_reset(ctx, fh.data_ptr(), hc.data_ptr(), n_tapes)
         native.run_async(ctx, ct, assign, fh.data_ptr(), hc.data_ptr(), index_base=index_base,
                          mode=native.MODE_COUNT_ALL)
-        if world > 1:  # the one exchange: MIN of first witnesses, SUM of counts (RCCL)
+        if exchange == "library":  # the one exchange: MIN of first witnesses, SUM of counts
             ctx.comm_allreduce(fh.data_ptr(), hc.data_ptr(), n_tapes)
+        elif exchange == "torch":
+            shard.allreduce_results(fh, hc)
 
     for i in range(args.warmup):
         step(False)
@@ -230,7 +250,8 @@ def main() -> None:
             "mode": "count_all",
             "engine": args.engine,
             "short_circuit": short_circuit,
-            "parallelism": "dp%d (row shards, all-reduce of per-tape results)" % world,
+            "parallelism": "dp%d (row shards, all-reduce of per-tape results%s)"
+                           % (world, "" if exchange is None else ", %s RCCL" % exchange),
         },
         "per_gpu": value / world,
         "kernel_ms": kms,
