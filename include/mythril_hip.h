@@ -252,8 +252,9 @@ int32_t mh_comm_destroy(mh_ctx* ctx);
  * 8 v_mov_b32; 9 v_add_co_u32 (carry-out only); 10 v_sub_co/v_subb through VCC;
  * 11 v_cndmask_b32_e32 (VCC mask); 12 v_cmp_eq_u32_e32 (VCC write); 13 v_xor_b32 with a literal;
  * 14 v_lshlrev_b32; 15 v_add3_u32; 16 v_fma_f64; 17 v_xnor_b32; 18 v_and_b32; 19 v_or_b32;
- * 20 v_not_b32.                                                                                  */
-#define MH_MB_NUM_KINDS 21
+ * 20 v_not_b32; with a partial EXEC mask: 21 v_xor_b32 (low 32 lanes), 22 v_alignbit_b32 (low 32),
+ * 23 v_xor_b32 (low 16), 24 v_xor_b32 (every other lane).                                       */
+#define MH_MB_NUM_KINDS 25
 int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
                             double* lane_ops_per_s);
 /* Round-1 form: kinds 0..2 of mh_microbench_issue at 8 waves per SIMD.                           */

@@ -416,6 +416,26 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink
             if constexpr (KIND == 20)
                 asm volatile(MB8("v_not_b32 %0, %0\n v_not_b32 %1, %1\n v_not_b32 %2, %2\n v_not_b32 %3, %3\n")
                              : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+            // partial EXEC masks: does the SIMD skip lane groups that are all inactive?
+            if constexpr (KIND >= 21 && KIND <= 24) {
+                constexpr uint64_t kExec = KIND == 21 || KIND == 22 ? 0x00000000FFFFFFFFull
+                                         : KIND == 23 ? 0x000000000000FFFFull
+                                                      : 0x5555555555555555ull;
+                if constexpr (KIND == 22)
+                    asm volatile("s_mov_b64 s[22:23], exec\n s_mov_b64 exec, %9\n"
+                                 MB8("v_alignbit_b32 %0, %0, %1, 7\n v_alignbit_b32 %1, %1, %2, 9\n"
+                                     "v_alignbit_b32 %2, %2, %3, 11\n v_alignbit_b32 %3, %3, %4, 13\n")
+                                 "s_mov_b64 exec, s[22:23]\n"
+                                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                                 : "v"(y), "s"(kExec) : "s22", "s23");
+                else
+                    asm volatile("s_mov_b64 s[22:23], exec\n s_mov_b64 exec, %9\n"
+                                 MB8("v_xor_b32 %0, %0, %8\n v_xor_b32 %1, %1, %8\n"
+                                     "v_xor_b32 %2, %2, %8\n v_xor_b32 %3, %3, %8\n")
+                                 "s_mov_b64 exec, s[22:23]\n"
+                                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                                 : "v"(y), "s"(kExec) : "s22", "s23");
+            }
 #undef MB_ONE
         }
     }
@@ -487,6 +507,7 @@ hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uin
         MB_CASE(0) MB_CASE(1) MB_CASE(2) MB_CASE(3) MB_CASE(4) MB_CASE(5) MB_CASE(6) MB_CASE(7)
         MB_CASE(8) MB_CASE(9) MB_CASE(10) MB_CASE(11) MB_CASE(12) MB_CASE(13) MB_CASE(14)
         MB_CASE(15) MB_CASE(16) MB_CASE(17) MB_CASE(18) MB_CASE(19) MB_CASE(20)
+        MB_CASE(21) MB_CASE(22) MB_CASE(23) MB_CASE(24)
 #undef MB_CASE
         default: return hipErrorInvalidValue;
     }

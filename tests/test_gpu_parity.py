@@ -396,10 +396,12 @@ def test_bench_config_pinned(gpu_ctx):
 
 def test_microbench_issue(gpu_ctx):
     """mh_microbench_issue runs every kind and reports a plausible rate (below 2x the nominal
-    2-cycle wave64 issue rate of 78.6 T lane-ops/s)."""
+    2-cycle wave64 issue rate of 78.6 T lane-ops/s; the partial-EXEC kinds count 64 lanes per
+    wave-instruction, so a SIMD that skipped inactive lane groups could report up to 4x)."""
     for kind in range(len(native.MB_KINDS)):
         r = gpu_ctx.microbench(kind, 4)
-        assert 1e11 < r < 2 * 78.7e12, (native.MB_KINDS[kind], r)
+        bound = 4 if "exec" in native.MB_KINDS[kind] else 2
+        assert 1e11 < r < bound * 78.7e12, (native.MB_KINDS[kind], r)
 
 
 def test_unsupported_and_invalid(gpu_ctx):
