@@ -2293,6 +2293,12 @@ Module build_module(const std::vector<const TapeCode*>& codes,
     if (any_kec) maxv = std::max<uint32_t>(maxv, R_TEMP_KEC);
     if (any_div) maxv = std::max<uint32_t>(maxv, R_TEMP0);
     maxv = std::max<uint32_t>(maxv, 8);
+    static const uint32_t pad = [] {  // diagnostic: MH_JIT_PAD_VGPR (occupancy A/B)
+        const char* e = std::getenv("MH_JIT_PAD_VGPR");
+        const uint32_t v = e ? (uint32_t)atoi(e) : 0u;
+        return v <= 512 ? v : 0u;
+    }();
+    maxv = std::max(maxv, pad);
     maxv = (maxv + 7) & ~7u;
     m.max_vgpr = maxv;
     m.n_sgpr = S_NEXT_FREE;
