@@ -1791,11 +1791,11 @@ std::vector<MI> div_routine() {
         E(M_S_MOV_B32, {K64HI, IMM(0x3feffff8u)});  // 1 - 2^-18
         E(M_V_CMP_LE_F64, {VCC(), K64, FT});
         E(M_S_AND_B64, {TM, VCC(), YNZ});
-        // R[j..] -= c * y (the product's limbs above limb 7 only feed the borrow)
-        E(M_V_MOV, {V(R_CARRY), IMM(0)});
-        E(M_V_MOV, {V(R_CARRY + 1), IMM(0)});
+        // R[j..] -= c * y (the product's limbs above limb 7 only feed the borrow); the carry
+        // pair's high word stays 0 from the first copy on (the first product adds nothing)
         for (int k = 0; k < 8; ++k) {
-            E(M_V_MAD_U64_U32, {MAD, DUMMY, C, Yr(k), CARRY});
+            E(M_V_MAD_U64_U32, {MAD, DUMMY, C, Yr(k), k ? CARRY : IMM(0)});
+            if (k == 0) E(M_V_MOV, {V(R_CARRY + 1), IMM(0)});
             E(M_V_MOV, {V(R_CARRY), V(R_MAD + 1)});
             const int limb = j + k;
             if (limb <= 7) {
