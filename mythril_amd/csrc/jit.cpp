@@ -891,7 +891,7 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
             if (k < top) {
                 const uint32_t np = valloc_pair();
                 emit(M_V_MOV, {V(np), V((uint32_t)init + 1)});
-                emit(M_V_MOV, {V(np + 1), IMM(0)});
+                if (k + 1 < top) emit(M_V_MOV, {V(np + 1), IMM(0)});
                 vrelease((uint32_t)init + 1);
                 init = (int)np;
                 init_max >>= 32;
@@ -900,7 +900,9 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
             }
             continue;
         }
-        const bool count = k < top && colmax >> 64;
+        // overflows out of column k's pair weigh 2^(32 (k + 2)): they matter only below the
+        // top column (the top column keeps just its low word, which they cannot change)
+        const bool count = k + 1 < top && colmax >> 64;
         const uint32_t acc = valloc_pair();
         uint32_t np = 0;
         if (k < top) np = valloc_pair();
@@ -933,7 +935,8 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
         }
         R.l[k] = Limb::R(acc);
         if (k < top) {
-            if (!count) emit(M_V_MOV, {V(np + 1), IMM(0)});
+            // the top column reads only the low word of its carry-in pair
+            if (!count && k + 1 < top) emit(M_V_MOV, {V(np + 1), IMM(0)});
             emit(M_V_MOV, {V(np), V(acc + 1)});
             init = (int)np;
             init_max = colmax >> 32;
@@ -980,8 +983,50 @@ void Emitter::op_div(int d, int a, int b, int cidx, uint32_t kind, int cur) {
     // (every SMT-LIB sign rule reduces to the unsigned form for non-negative x and y)
     if (kind >= 2 && A.l[7].is_c() && !(A.l[7].v >> 31) && B.l[7].is_c() && !(B.l[7].v >> 31))
         kind = kind == 2 ? 0u : 1u;
-    for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DY + k), src(B.l[k])});
-    for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DR + k), src(A.l[k])});
+    if (kind < 2) {
+        for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DY + k), src(B.l[k])});
+        for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(R_DR + k), src(A.l[k])});
+    } else {
+        // signed kinds: the subroutine divides |x| by |y| and takes the signs from v[R_SX],
+        // v[R_SY]; |v| = (v ^ m) - m (m = the sign mask) is formed here, reading the operand
+        // where it lives, instead of a copy plus the same work inside the subroutine.  Both sign
+        // masks first (an operand may sit in R, which the second load overwrites).
+        auto sign_of = [&](const Val& X, uint32_t sreg) {
+            if (X.l[7].is_c()) emit(M_V_MOV, {V(sreg), IMM((X.l[7].v >> 31) ? ~0u : 0u)});
+            else emit(M_V_ASHRREV, {V(sreg), IMM(31), V(X.l[7].v)});
+        };
+        auto load_abs = [&](uint32_t base, uint32_t sreg, const Val& X) {
+            bool allc = true;
+            for (int k = 0; k < 8; ++k) allc = allc && X.l[k].is_c();
+            const bool known = X.l[7].is_c(), neg = known && (X.l[7].v >> 31);
+            if (allc) {  // |X| on the host
+                uint32_t c[8];
+                uint64_t borrow = neg ? 1 : 0;
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t t = (uint64_t)(neg ? ~X.l[k].v : X.l[k].v) + borrow;
+                    c[k] = (uint32_t)t;
+                    borrow = t >> 32;
+                }
+                for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(base + k), IMM(c[k])});
+                return;
+            }
+            if (known && !neg) {
+                for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(base + k), src(X.l[k])});
+                return;
+            }
+            for (int k = 0; k < 8; ++k) {
+                if (X.l[k].is_c(0)) emit(M_V_MOV, {V(base + k), V(sreg)});
+                else emit(M_V_XOR, {V(base + k), src(X.l[k]), V(sreg)});
+            }
+            emit(M_V_SUB_CO, {V(base), VCC(), V(base), V(sreg)});
+            for (int k = 1; k < 8; ++k)
+                emit(M_V_SUBB_CO, {V(base + k), VCC(), V(base + k), V(sreg), VCC()});
+        };
+        sign_of(B, R_SY);
+        sign_of(A, R_SX);
+        load_abs(R_DY, R_SY, B);
+        load_abs(R_DR, R_SX, A);
+    }
     emit(M_S_MOV_B32, {S(S_DIV_KIND), IMM(kind)});
     emit(M_CALL_DIV, {IMM((uint32_t)code_.size())});
     Val& R = out(d);
@@ -1678,17 +1723,7 @@ std::vector<MI> div_routine() {
     };
     auto Rl = [](int k) { return V(R_DR + k); };
     auto Yl = [](int k) { return V(R_DY + k); };
-    // signed kinds: |x|, |y| as (v ^ m) - m with m = sign mask
-    E(M_S_CMP_LT_U32, {KIND, IMM(2)});
-    E(M_S_CBRANCH_SCC1, {LBL(L_UNS)});
-    for (int w = 0; w < 2; ++w) {
-        const uint32_t base = w == 0 ? R_DR : R_DY;
-        const Opnd m = w == 0 ? SX : SY;
-        E(M_V_ASHRREV, {m, IMM(31), V(base + 7)});
-        for (int k = 0; k < 8; ++k) E(M_V_XOR, {V(base + k), V(base + k), m});
-        E(M_V_SUB_CO, {V(base), VCC(), V(base), m});
-        for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {V(base + k), VCC(), V(base + k), m, VCC()});
-    }
+    // signed kinds arrive as |x|, |y| with the sign masks in SX, SY (the call site forms them)
     L(L_UNS);
     // the quotient registers start at 0 for the kinds that return the quotient (the digit steps
     // write only the digits they compute); remainder kinds leave them as they are

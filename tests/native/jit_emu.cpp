@@ -93,6 +93,8 @@ uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
 // executed VALU by the SSA op kind that emitted it: [tag] body, [256 + tag] inside the division
 // subroutine called by that op (tag 255 = prologue / untagged)
 uint64_t g_tag_valu[512];
+uint64_t g_opc_valu[2][256];  // executed VALU by machine opcode (tape body / division subroutine)
+uint64_t g_mov_tag[256];      // executed v_mov in tape bodies by the SSA op that emitted them
 uint64_t g_div_label[128];  // division subroutine: executions of each label (path statistics)
 
 bool is_wide(const MI& m) {
@@ -124,6 +126,8 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
             g_counts.f64 += m.op >= M_V_CVT_F64_U32;
             if (depth) { ++g_counts.div_valu; g_counts.div_wide += wd; }
             ++g_tag_valu[depth ? 256 + caller_tag : m.tag];
+            ++g_opc_valu[depth ? 1 : 0][m.op & 255];
+            if (!depth && m.op == M_V_MOV) ++g_mov_tag[m.tag];
         } else if (m.op <= M_S_CMP_LT_U32) {
             ++g_counts.salu;
         }
@@ -592,4 +596,19 @@ extern "C" int32_t emu_jit_build(const mh_node* nodes, const uint64_t* offs, uin
         for (uint32_t t : built[i].tape_ids) tape_obj[t] = (int32_t)i;
     }
     return (int32_t)built.size();
+}
+
+extern "C" void emu_jit_opcode_valu(uint64_t* out, int reset) {
+    for (int d = 0; d < 2; ++d)
+        for (int i = 0; i < 256; ++i) {
+            out[256 * d + i] = g_opc_valu[d][i];
+            if (reset) g_opc_valu[d][i] = 0;
+        }
+}
+
+extern "C" void emu_jit_mov_tags(uint64_t* out, int reset) {
+    for (int i = 0; i < 256; ++i) {
+        out[i] = g_mov_tag[i];
+        if (reset) g_mov_tag[i] = 0;
+    }
 }
