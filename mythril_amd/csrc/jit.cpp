@@ -1711,7 +1711,8 @@ std::vector<MI> div_routine() {
                TM = S(S_DIV_TM, 2), K64 = S(S_DIV_F64K, 2), KIND = S(S_DIV_KIND);
     const Opnd K64LO = S(S_DIV_F64K), K64HI = S(S_DIV_F64K + 1);
     enum : uint32_t { L_UNS = 1, L_DONE, L_TOP3, L_CONV, L_ZQ, L_NOZQ, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
-                      L_SDIV, L_SREM, L_SMOD, L_NARROW = 50, L_NNEG0 = 60, L_NGE0 = 70 };
+                      L_SDIV, L_SREM, L_SMOD, L_NARROW = 50, L_NNEG0 = 60, L_NGE0 = 70,
+                      L_NOYZ = 80, L_CZ0 = 90 };
     auto to_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
         E(M_S_MOV_B32, {K64LO, IMM(0)});
         E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});
@@ -1817,7 +1818,12 @@ std::vector<MI> div_routine() {
         E(M_S_MOV_B32, {K64HI, IMM(0x41efffffu)});
         E(M_V_MIN_F64, {FC, FC, K64});
         E(M_V_CVT_U32_F64, {C, FC});
+        // y = 0 lanes (their NaN estimate became the clamp) take digit 0; skipped when no lane
+        // divides by zero
+        E(M_S_CMP_EQ_U64, {YNZ, IMM(0xFFFFFFFFu)});
+        E(M_S_CBRANCH_SCC1, {LBL(L_CZ0 + j)});
         E(M_V_CNDMASK, {C, IMM(0), C, YNZ}, true);
+        L(L_CZ0 + j);
         // the estimate is within 2^-19 of R / (y 2^32j), so c is one too small only in lanes
         // whose estimate has a fraction above 1 - 2^-18: without such a lane the "R >= y" test
         // below (a 9-instruction borrow chain) is skipped
@@ -1943,8 +1949,11 @@ std::vector<MI> div_routine() {
     E(M_S_CBRANCH_SCC1, {LBL(L_SMOD)});
     E(M_S_CMP_EQ_U32, {KIND, IMM(3)});
     E(M_S_CBRANCH_SCC1, {LBL(L_SREM)});
-    // y = 0: q = 2^256 - 1 (R already holds |x|)
+    // y = 0: q = 2^256 - 1 (R already holds |x|); nothing to do when no lane divides by zero
+    E(M_S_CMP_EQ_U64, {YNZ, IMM(0xFFFFFFFFu)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_NOYZ)});
     for (int k = 0; k < 8; ++k) E(M_V_CNDMASK, {Xr(k), IMM(0xFFFFFFFFu), Xr(k), YNZ}, true);
+    L(L_NOYZ);
     E(M_S_CMP_EQ_U32, {KIND, IMM(0)});
     E(M_S_CBRANCH_SCC1, {LBL(L_WB)});
     L(L_SDIV);  // q negated when the signs differ
@@ -2846,6 +2855,12 @@ uint32_t coalesce_div_moves(std::vector<MI>& code) {
 
 }  // namespace
 
+static std::atomic<uint64_t> g_sc_fallbacks{0};
+
+uint64_t sc_fallbacks(bool reset) {
+    return reset ? g_sc_fallbacks.exchange(0) : g_sc_fallbacks.load();
+}
+
 TapeCode emit_tape(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t n_vars,
                    const Options& opt) {
     TapeCode tc = emit_tape_body(st, pool, n_vars, opt);
@@ -2870,6 +2885,7 @@ TapeCode emit_tape_body(const SsaTape& st, const std::vector<uint32_t>& pool, ui
             Emitter e2(sc, pool, n_vars, opt, &check);
             TapeCode tc = e2.run();
             if (tc.ok) return tc;  // else (register pressure of the new order): source order
+            g_sc_fallbacks.fetch_add(1, std::memory_order_relaxed);
         }
     }
     return tc0;

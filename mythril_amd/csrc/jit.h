@@ -201,6 +201,10 @@ Module build_module(const std::vector<const TapeCode*>& codes,
                     const std::vector<uint32_t>& tape_ids, uint32_t n_vars, bool values,
                     uint32_t group_bytes);
 
+// Diagnostics: tapes whose short-circuit order ran out of registers and kept the source order
+// (since the last reset).
+uint64_t sc_fallbacks(bool reset);
+
 // Diagnostics: static VALU (and 4-cycle VALU) emitted per SSA op kind since the last reset
 // (not thread safe; tests / scripts only).
 void op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, bool reset);

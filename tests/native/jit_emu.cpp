@@ -95,6 +95,7 @@ uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
 uint64_t g_tag_valu[512];
 uint64_t g_opc_valu[2][256];  // executed VALU by machine opcode (tape body / division subroutine)
 uint64_t g_mov_tag[256];      // executed v_mov in tape bodies by the SSA op that emitted them
+uint64_t g_tag_op[256][128];  // executed tape-body VALU by (SSA op, machine opcode)
 uint64_t g_div_label[128];  // division subroutine: executions of each label (path statistics)
 
 bool is_wide(const MI& m) {
@@ -128,6 +129,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
             ++g_tag_valu[depth ? 256 + caller_tag : m.tag];
             ++g_opc_valu[depth ? 1 : 0][m.op & 255];
             if (!depth && m.op == M_V_MOV) ++g_mov_tag[m.tag];
+            if (!depth) ++g_tag_op[m.tag][m.op & 127];
         } else if (m.op <= M_S_CMP_LT_U32) {
             ++g_counts.salu;
         }
@@ -612,3 +614,13 @@ extern "C" void emu_jit_mov_tags(uint64_t* out, int reset) {
         if (reset) g_mov_tag[i] = 0;
     }
 }
+
+extern "C" void emu_jit_tag_op(uint64_t* out, int reset) {
+    for (int t = 0; t < 256; ++t)
+        for (int o = 0; o < 128; ++o) {
+            out[128 * t + o] = g_tag_op[t][o];
+            if (reset) g_tag_op[t][o] = 0;
+        }
+}
+
+extern "C" uint64_t emu_jit_sc_fallbacks(int reset) { return sc_fallbacks(reset != 0); }
