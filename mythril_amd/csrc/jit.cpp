@@ -124,6 +124,8 @@ private:
         }
     }
 
+    uint32_t next_lbl_ = 0x1000;  // tape-local labels of in-op branches
+
     // ---- VGPRs (reference counted; columns and fixed registers are never freed)
     uint32_t valloc() {
         for (uint32_t r = vbase_; r < vmax_; ++r)
@@ -779,6 +781,11 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
         emit(M_S_OR_B64, {P(big), P(big), VCC()});
     }
     free_tmp(tmp);  // the amount's temporaries (y0 stays live in B or is re-read below)
+    // every lane shifting by >= 256 (a full-width symbolic amount, the common case): the result
+    // is 0, or the sign for arithmetic shifts, written by the uniform branch at the end
+    const uint32_t l_fast = next_lbl_++, l_end = next_lbl_++;
+    emit(M_S_CMP_EQ_U64, {P(big), IMM(0xFFFFFFFFu)});
+    emit(M_S_CBRANCH_SCC1, {LBL(l_fast)});
     // operand limbs into VGPRs (ASHR: x ^ s), two at a time, each pair's temporaries freed as
     // soon as it is in LDS (register pressure: the network's eight temporaries are gone)
     uint32_t sgn = ~0u;
@@ -856,6 +863,23 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
         if (arith) emit(M_V_XOR, {V(o), V(o), V(sgn)});
         R.l[k] = Limb::R(o);
     }
+    emit(M_S_BRANCH, {LBL(l_end)});
+    emit(M_LABEL, {LBL(l_fast)});
+    uint32_t first = ~0u;
+    for (int k = 0; k < 8; ++k) {
+        if (!((dm >> k) & 1)) continue;
+        const uint32_t o = R.l[k].v;
+        if (!arith) {
+            emit(M_V_MOV, {V(o), IMM(0)});
+        } else if (first != ~0u) {
+            emit(M_V_MOV, {V(o), V(first)});
+        } else {
+            if (A.l[7].is_c()) emit(M_V_MOV, {V(o), IMM((A.l[7].v >> 31) ? ~0u : 0u)});
+            else emit(M_V_ASHRREV, {V(o), IMM(31), V(A.l[7].v)});
+            first = o;
+        }
+    }
+    emit(M_LABEL, {LBL(l_end)});
     if (arith) vrelease(sgn);
     free_tmp(tmp);
     free_tmp_pairs(tp);
