@@ -556,9 +556,36 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
         }
         and_all_zero(regs, &p, tmp);
     }
+    // uniform fast path: when the top limbs differ in every lane -- all but certain for
+    // full-width operands -- the top limb alone decides: one compare tests that, one decides
+    const bool fast = p < 0 && m == top && top >= 2 && !(a[top].is_c() && b[top].is_c());
+    uint32_t l_join = 0;
+    if (fast) {
+        l_join = next_lbl_++;
+        const uint32_t l_chain = next_lbl_++;
+        // v_cmp_<op>_u32 vcc, x, y (x may be a constant; a constant y swaps the operands)
+        auto cmp = [&](uint16_t op, const Limb& x, const Limb& y) {
+            if (y.is_c() && !x.is_c()) {
+                const uint16_t rev = op == M_V_CMP_LT ? M_V_CMP_GT : op;
+                emit(rev, {VCC(), IMM(y.v), V(x.v)});
+            } else {
+                emit(op, {VCC(), src(x), V(y.v)});
+            }
+        };
+        cmp(M_V_CMP_NE, a[top], b[top]);
+        emit(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
+        emit(M_S_CBRANCH_SCC0, {LBL(l_chain)});
+        cmp(M_V_CMP_LT, a[top], b[top]);  // the borrow of A - B
+        emit(M_S_BRANCH, {LBL(l_join)});
+        emit(M_LABEL, {LBL(l_chain)});
+    }
     const uint32_t junk = valloc();
     tmp.push_back(junk);
     const int cs = chain(true, a, b, m, nullptr, junk, tmp);
+    if (fast) {
+        if (cs != 2) fail("internal: uniform compare path over a known borrow");
+        emit(M_LABEL, {LBL(l_join)});
+    }
     free_tmp(tmp);
     // combine: lo = borrow (A[lo] < B[lo]); result = hi_side 1: p && lo; 2: !p || lo
     if (p < 0) {
