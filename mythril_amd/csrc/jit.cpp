@@ -471,13 +471,11 @@ void Emitter::and_all_zero(const std::vector<uint32_t>& regs, int* p, std::vecto
 Val Emitter::op_eq(const Val& A, const Val& B) {
     int p = -1;
     std::vector<uint32_t> zero_regs, tmp;  // VGPR limbs compared against a known zero
+    std::vector<std::pair<Limb, Limb>> cmps;  // (constant or VGPR, VGPR) limb pairs
     for (int k = 0; k < 8; ++k) {
         Limb x = A.l[k], y = B.l[k];
         if (x.is_c() && y.is_c()) {
-            if (x.v != y.v) {
-                if (p >= 0) --pref_[p];
-                return bool_const(false);
-            }
+            if (x.v != y.v) return bool_const(false);
             continue;
         }
         if (x.is_r() && y.is_r() && x.v == y.v) continue;
@@ -486,16 +484,28 @@ Val Emitter::op_eq(const Val& A, const Val& B) {
             zero_regs.push_back(y.v);
             continue;
         }
-        emit(M_V_CMP_EQ, {VCC(), src(x), V(y.v)});
+        cmps.push_back({x, y});
+    }
+    // once the first compare finds no equal lane (full-width operands: nearly always) the
+    // value is false in every lane: the other compares are skipped
+    const size_t rest = cmps.size() + (zero_regs.empty() ? 0 : 1);
+    const uint32_t l_end = rest >= 3 ? next_lbl_++ : 0;
+    for (size_t i = 0; i < cmps.size(); ++i) {
+        emit(M_V_CMP_EQ, {VCC(), src(cmps[i].first), V(cmps[i].second.v)});
         if (p < 0) {
             p = palloc();
             emit(M_S_MOV_B64, {P(p), VCC()});
+            if (l_end) {
+                emit(M_S_CMP_EQ_U64, {P(p), IMM(0)});
+                emit(M_S_CBRANCH_SCC1, {LBL(l_end)});
+            }
         } else {
             emit(M_S_AND_B64, {P(p), P(p), VCC()});
         }
     }
     and_all_zero(zero_regs, &p, tmp);
     free_tmp(tmp);
+    if (l_end && p >= 0) emit(M_LABEL, {LBL(l_end)});
     if (p < 0) return bool_const(true);
     return bool_mask(p);
 }
@@ -1763,7 +1773,7 @@ std::vector<MI> div_routine() {
     const Opnd K64LO = S(S_DIV_F64K), K64HI = S(S_DIV_F64K + 1);
     enum : uint32_t { L_UNS = 1, L_DONE, L_TOP3, L_CONV, L_ZQ, L_NOZQ, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
                       L_SDIV, L_SREM, L_SMOD, L_NARROW = 50, L_NNEG0 = 60, L_NGE0 = 70,
-                      L_NOYZ = 80, L_CZ0 = 90 };
+                      L_NOYZ = 80, L_CZ0 = 90, L_RLT = 100, L_RLTD, L_YSLOW, L_YDONE };
     auto to_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
         E(M_S_MOV_B32, {K64LO, IMM(0)});
         E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});
@@ -1786,14 +1796,33 @@ std::vector<MI> div_routine() {
     L(L_ZQ);
     for (int k = 0; k < 8; ++k) E(M_V_MOV, {Xr(k), IMM(0)});
     L(L_NOZQ);
+    // TM = lanes with y >= 2^32, YNZ = lanes with y != 0: every lane when every lane's top limb
+    // is nonzero (full-width divisors), else from an OR over the limbs
+    E(M_V_CMP_NE, {VCC(), IMM(0), Yr(7)});
+    E(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
+    E(M_S_CBRANCH_SCC0, {LBL(L_YSLOW)});
+    E(M_S_MOV_B64, {TM, IMM(0xFFFFFFFFu)});
+    E(M_S_MOV_B64, {YNZ, IMM(0xFFFFFFFFu)});
+    E(M_S_BRANCH, {LBL(L_YDONE)});
+    L(L_YSLOW);
     E(M_V_OR3, {T1, Yr(1), Yr(2), Yr(3)});
     E(M_V_OR3, {T1, T1, Yr(4), Yr(5)});
     E(M_V_OR3, {T1, T1, Yr(6), Yr(7)});
     E(M_V_CMP_NE, {TM, IMM(0), T1}, true);  // lanes with y >= 2^32
     E(M_V_OR, {T1, T1, Yr(0)});
     E(M_V_CMP_NE, {YNZ, IMM(0), T1}, true);
+    L(L_YDONE);
+    // lanes with x < y (no digit): the top limbs decide when they differ in every lane, else
+    // the borrow chain
+    E(M_V_CMP_NE, {VCC(), Rr(7), Yr(7)});
+    E(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
+    E(M_S_CBRANCH_SCC0, {LBL(L_RLT)});
+    E(M_V_CMP_LT, {VCC(), Rr(7), Yr(7)});
+    E(M_S_BRANCH, {LBL(L_RLTD)});
+    L(L_RLT);
     E(M_V_SUB_CO, {T1, VCC(), Rr(0), Yr(0)});
     for (int k = 1; k < 8; ++k) E(M_V_SUBB_CO, {T1, VCC(), Rr(k), Yr(k), VCC()});
+    L(L_RLTD);
     E(M_S_ANDN2_B64, {MSK, YNZ, VCC()});
     E(M_S_CMP_EQ_U64, {MSK, IMM(0)});
     E(M_S_CBRANCH_SCC1, {LBL(L_DONE)});
