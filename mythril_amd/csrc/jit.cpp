@@ -793,6 +793,15 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
     std::vector<uint32_t> tmp;
     std::vector<int> tp;
     const uint32_t dm = dem_[d];
+    // every lane shifting by >= 256 (a full-width symbolic amount, the common case): the result
+    // is 0, or the sign for arithmetic shifts, written by the uniform branch at the end; a
+    // nonzero top limb of the amount in every lane decides it with one compare
+    const uint32_t l_fast = next_lbl_++, l_end = next_lbl_++;
+    if (B.l[7].is_r()) {
+        emit(M_V_CMP_NE, {VCC(), IMM(0), V(B.l[7].v)});
+        emit(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
+        emit(M_S_CBRANCH_SCC1, {LBL(l_fast)});
+    }
     const uint32_t y0 = vgpr_of(B.l[0], tmp);
     const int big = palloc();
     tp.push_back(big);
@@ -818,9 +827,6 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
         emit(M_S_OR_B64, {P(big), P(big), VCC()});
     }
     free_tmp(tmp);  // the amount's temporaries (y0 stays live in B or is re-read below)
-    // every lane shifting by >= 256 (a full-width symbolic amount, the common case): the result
-    // is 0, or the sign for arithmetic shifts, written by the uniform branch at the end
-    const uint32_t l_fast = next_lbl_++, l_end = next_lbl_++;
     emit(M_S_CMP_EQ_U64, {P(big), IMM(0xFFFFFFFFu)});
     emit(M_S_CBRANCH_SCC1, {LBL(l_fast)});
     // operand limbs into VGPRs (ASHR: x ^ s), two at a time, each pair's temporaries freed as
