@@ -116,7 +116,7 @@ private:
                               op == M_V_OR3 || op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 ||
                               op == M_V_LSHL_ADD || op == M_V_PERM || op == M_V_BFI ||
                               op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
-                              (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) || op >= M_V_CVT_F64_U32;
+                              (op >= M_V_CMP_EQ && op <= M_V_CMP_GT_I32) || op >= M_V_CVT_F64_U32;
             if (wide) ++n_wide_;
             if (cur_op_ >= 0) { ++op_valu[cur_op_]; op_wide[cur_op_] += wide; }
         } else if (op <= M_S_CMP_LT_U32) {
@@ -519,20 +519,30 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
     std::vector<uint32_t> tmp;
     Limb a[8], b[8];
     for (int k = 0; k < 8; ++k) { a[k] = A.l[k]; b[k] = B.l[k]; }
-    if (signed_) {  // bias the sign bit: signed order = unsigned order of x ^ 2^255
+    // signed: bias the sign bit (signed order = unsigned order of x ^ 2^255); constant limbs
+    // now, register limbs where the borrow chain needs them (the uniform path compares the
+    // unbiased top limbs as signed words)
+    bool bias_regs = false;
+    if (signed_) {
         for (Limb* l : {&a[7], &b[7]}) {
-            if (l->is_c()) {
-                l->v ^= 0x80000000u;
-            } else {
-                const uint32_t t = valloc();
-                tmp.push_back(t);
-                emit(M_V_XOR, {V(t), IMM(0x80000000u), V(l->v)});
-                *l = Limb::R(t);
-            }
+            if (l->is_c()) l->v ^= 0x80000000u;
+            else bias_regs = true;
         }
     }
+    auto bias = [&]() {
+        if (!bias_regs) return;
+        bias_regs = false;
+        for (Limb* l : {&a[7], &b[7]}) {
+            if (l->is_c()) continue;
+            const uint32_t t = valloc();
+            tmp.push_back(t);
+            emit(M_V_XOR, {V(t), IMM(0x80000000u), V(l->v)});
+            *l = Limb::R(t);
+        }
+    };
     int top = 7;
     while (top > 0 && a[top].is_c() && b[top].is_c() && a[top].v == b[top].v) --top;
+    if (top < 7) bias();  // (limb 7 constant on both sides: no register bias anyway)
     if (a[top].is_c() && b[top].is_c() && a[top].v != b[top].v) {
         // the highest limb that differs is known on both sides: it decides, whatever is below
         free_tmp(tmp);
@@ -549,6 +559,7 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
         while (m > 0 && a[m].is_c(0)) --m;
     }
     if (hi_side && m == top) hi_side = 0;
+    if (hi_side) bias();
     int p = -1;  // the high-run mask (A[hi] == 0 / B[hi] == 0)
     if (hi_side) {
         std::vector<uint32_t> regs;
@@ -573,22 +584,31 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
     if (fast) {
         l_join = next_lbl_++;
         const uint32_t l_chain = next_lbl_++;
-        // v_cmp_<op>_u32 vcc, x, y (x may be a constant; a constant y swaps the operands)
-        auto cmp = [&](uint16_t op, const Limb& x, const Limb& y) {
+        // v_cmp_<op> vcc, x, y (x may be a constant; a constant y swaps the operands)
+        auto cmp = [&](uint16_t op, Limb x, Limb y) {
             if (y.is_c() && !x.is_c()) {
-                const uint16_t rev = op == M_V_CMP_LT ? M_V_CMP_GT : op;
+                const uint16_t rev = op == M_V_CMP_LT ? M_V_CMP_GT
+                                   : op == M_V_CMP_LT_I32 ? M_V_CMP_GT_I32 : op;
                 emit(rev, {VCC(), IMM(y.v), V(x.v)});
             } else {
                 emit(op, {VCC(), src(x), V(y.v)});
             }
         };
-        cmp(M_V_CMP_NE, a[top], b[top]);
+        // signed top limbs compare unbiased as signed words (constants were biased above)
+        Limb xa = a[top], xb = b[top];
+        const bool sgn_top = signed_ && top == 7;
+        if (sgn_top) {
+            if (xa.is_c()) xa.v ^= 0x80000000u;
+            if (xb.is_c()) xb.v ^= 0x80000000u;
+        }
+        cmp(M_V_CMP_NE, xa, xb);
         emit(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
         emit(M_S_CBRANCH_SCC0, {LBL(l_chain)});
-        cmp(M_V_CMP_LT, a[top], b[top]);  // the borrow of A - B
+        cmp(sgn_top ? M_V_CMP_LT_I32 : M_V_CMP_LT, xa, xb);  // the borrow of A - B
         emit(M_S_BRANCH, {LBL(l_join)});
         emit(M_LABEL, {LBL(l_chain)});
     }
+    bias();
     const uint32_t junk = valloc();
     tmp.push_back(junk);
     const int cs = chain(true, a, b, m, nullptr, junk, tmp);
@@ -1684,6 +1704,8 @@ const char* op_name(uint16_t op) {
         case M_V_CMP_LE: return "v_cmp_le_u32";
         case M_V_CMP_GT: return "v_cmp_gt_u32";
         case M_V_CMP_GE: return "v_cmp_ge_u32";
+        case M_V_CMP_LT_I32: return "v_cmp_lt_i32";
+        case M_V_CMP_GT_I32: return "v_cmp_gt_i32";
         case M_V_MAD_U64_U32: return "v_mad_u64_u32";
         case M_V_LSHL_ADD: return "v_lshl_add_u32";
         case M_V_PERM: return "v_perm_b32";
@@ -2860,7 +2882,7 @@ namespace {
 // write o[0]; nothing else writes VGPRs.
 std::pair<uint32_t, uint32_t> vgpr_writes(const MI& m) {
     const bool valu = m.op <= M_V_CMP_LE_F64 &&
-                      !(m.op >= M_V_CMP_EQ && m.op <= M_V_CMP_GE) && m.op != M_V_CMP_LE_F64;
+                      !(m.op >= M_V_CMP_EQ && m.op <= M_V_CMP_GT_I32) && m.op != M_V_CMP_LE_F64;
     const bool lds_read = m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32;
     if ((valu || lds_read) && m.o[0].k == O_V) return {m.o[0].v, m.o[0].n};
     return {0, 0};

@@ -59,6 +59,7 @@ enum Op : uint16_t {
     M_V_ALIGNBIT, M_V_LSHLREV, M_V_LSHRREV, M_V_ASHRREV,
     M_V_CNDMASK,   // d = mask ? src1 : src0
     M_V_CMP_EQ, M_V_CMP_NE, M_V_CMP_LT, M_V_CMP_LE, M_V_CMP_GT, M_V_CMP_GE,  // u32
+    M_V_CMP_LT_I32, M_V_CMP_GT_I32,
     M_V_MAD_U64_U32,
     M_V_LSHL_ADD,    // d = (s0 << s1) + s2
     M_V_PERM,        // v_perm_b32 d, s0, s1, sel (byte select from {s0, s1})

@@ -104,7 +104,7 @@ bool is_wide(const MI& m) {
            op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO || op == M_V_OR3 ||
            op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 || op == M_V_LSHL_ADD ||
            op == M_V_PERM || op == M_V_BFI ||
-           (op >= M_V_CMP_EQ && op <= M_V_CMP_GE) ||
+           (op >= M_V_CMP_EQ && op <= M_V_CMP_GT_I32) ||
            op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
            op >= M_V_CVT_F64_U32;
 }
@@ -213,7 +213,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 break;
             }
             case M_V_CMP_EQ: case M_V_CMP_NE: case M_V_CMP_LT: case M_V_CMP_LE: case M_V_CMP_GT:
-            case M_V_CMP_GE: {
+            case M_V_CMP_GE: case M_V_CMP_LT_I32: case M_V_CMP_GT_I32: {
                 uint64_t cm = 0;
                 for (int l = 0; l < 64; ++l) {
                     const uint32_t a = w.r32(o[1], l), b = w.r32(o[2], l);
@@ -224,6 +224,8 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                         case M_V_CMP_LT: r = a < b; break;
                         case M_V_CMP_LE: r = a <= b; break;
                         case M_V_CMP_GT: r = a > b; break;
+                        case M_V_CMP_LT_I32: r = (int32_t)a < (int32_t)b; break;
+                        case M_V_CMP_GT_I32: r = (int32_t)a > (int32_t)b; break;
                         default: r = a >= b; break;
                     }
                     if (r) cm |= 1ull << l;
