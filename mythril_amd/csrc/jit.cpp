@@ -92,6 +92,10 @@ private:
     int pref_[N_BOOL_PAIRS] = {};
     uint32_t kstage_ = 0;
     uint32_t n_valu_ = 0, n_wide_ = 0, n_salu_ = 0;
+    // VALU emitted on the unlikely side of a uniform branch (cold_ > 0): static counts keep
+    // them, the scheduler's cost model (insn_cost_) does not
+    uint32_t n_valu_cold_ = 0;
+    int cold_ = 0;
     bool calls_div_ = false;
     bool uses_lds_ = false;
     bool calls_kec_ = false;
@@ -111,6 +115,7 @@ private:
         code_.push_back(m);
         if (op <= M_V_CMP_LE_F64) {
             ++n_valu_;
+            if (cold_ > 0) ++n_valu_cold_;
             const bool wide = e64 || op == M_V_ADD_CO || op == M_V_ADDC_CO || op == M_V_SUB_CO ||
                               op == M_V_SUBB_CO || op == M_V_SUBREV_CO || op == M_V_SUBBREV_CO ||
                               op == M_V_OR3 || op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 ||
@@ -499,13 +504,17 @@ Val Emitter::op_eq(const Val& A, const Val& B) {
                 emit(M_S_CMP_EQ_U64, {P(p), IMM(0)});
                 emit(M_S_CBRANCH_SCC1, {LBL(l_end)});
             }
+            if (l_end) ++cold_;
         } else {
             emit(M_S_AND_B64, {P(p), P(p), VCC()});
         }
     }
     and_all_zero(zero_regs, &p, tmp);
     free_tmp(tmp);
-    if (l_end && p >= 0) emit(M_LABEL, {LBL(l_end)});
+    if (l_end && p >= 0) {
+        --cold_;
+        emit(M_LABEL, {LBL(l_end)});
+    }
     if (p < 0) return bool_const(true);
     return bool_mask(p);
 }
@@ -607,13 +616,18 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
         cmp(sgn_top ? M_V_CMP_LT_I32 : M_V_CMP_LT, xa, xb);  // the borrow of A - B
         emit(M_S_BRANCH, {LBL(l_join)});
         emit(M_LABEL, {LBL(l_chain)});
+        ++cold_;
+        bias();
+        --cold_;
     }
     bias();
+    if (fast) ++cold_;
     const uint32_t junk = valloc();
     tmp.push_back(junk);
     const int cs = chain(true, a, b, m, nullptr, junk, tmp);
     if (fast) {
         if (cs != 2) fail("internal: uniform compare path over a known borrow");
+        --cold_;
         emit(M_LABEL, {LBL(l_join)});
     }
     free_tmp(tmp);
@@ -817,10 +831,12 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
     // is 0, or the sign for arithmetic shifts, written by the uniform branch at the end; a
     // nonzero top limb of the amount in every lane decides it with one compare
     const uint32_t l_fast = next_lbl_++, l_end = next_lbl_++;
-    if (B.l[7].is_r()) {
+    const bool fast_likely = B.l[7].is_r();
+    if (fast_likely) {
         emit(M_V_CMP_NE, {VCC(), IMM(0), V(B.l[7].v)});
         emit(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
         emit(M_S_CBRANCH_SCC1, {LBL(l_fast)});
+        ++cold_;
     }
     const uint32_t y0 = vgpr_of(B.l[0], tmp);
     const int big = palloc();
@@ -926,6 +942,7 @@ void Emitter::op_vshift(int d, const Val& A, const Val& B, uint8_t op) {
         if (arith) emit(M_V_XOR, {V(o), V(o), V(sgn)});
         R.l[k] = Limb::R(o);
     }
+    if (fast_likely) --cold_;
     emit(M_S_BRANCH, {LBL(l_end)});
     emit(M_LABEL, {LBL(l_fast)});
     uint32_t first = ~0u;
@@ -1532,7 +1549,7 @@ TapeCode Emitter::run() {
             const SsaInsn& v = code[i];
             const uint8_t op = v.op;
             cur_op_ = op;
-            const uint32_t valu_before = n_valu_;
+            const uint32_t valu_before = n_valu_, cold_before = n_valu_cold_;
             ++op_count[op];
             auto Y = [&]() -> Val { return v.cidx >= 0 ? const_val(v.cidx) : val(v.b); };
             switch (op) {
@@ -1617,9 +1634,10 @@ TapeCode Emitter::run() {
             }
             if (check_ && (*check_)[v.d]) sc_check(vals_[v.d]);
             if (insn_cost_) {
-                // a division-family call runs ~110 VALU in the subroutine (jit_mix.json)
+                // a division-family call runs ~90 VALU in the subroutine (tests/tools/jit_mix.py)
                 const bool call = op >= D_UDIV_R && op <= D_SMOD_C;
-                (*insn_cost_)[i] = (double)(n_valu_ - valu_before) + (call ? 110.0 : 0.0) +
+                (*insn_cost_)[i] = (double)(n_valu_ - valu_before) -
+                                   (double)(n_valu_cold_ - cold_before) + (call ? 90.0 : 0.0) +
                                    (op == D_KECCAK ? 7000.0 : 0.0);
             }
         }
