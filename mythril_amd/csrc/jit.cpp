@@ -570,9 +570,9 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
     if (hi_side && m == top) hi_side = 0;
     if (hi_side) bias();
     int p = -1;  // the high-run mask (A[hi] == 0 / B[hi] == 0)
+    std::vector<uint32_t> regs;
+    const Limb* o = hi_side == 1 ? a : b;  // the side that is not zero there
     if (hi_side) {
-        std::vector<uint32_t> regs;
-        const Limb* o = hi_side == 1 ? a : b;  // the side that is not zero there
         for (int k = m + 1; k <= top; ++k) {
             if (o[k].is_c()) {
                 if (o[k].v) {  // decided by a known nonzero limb
@@ -584,77 +584,104 @@ Val Emitter::op_ult(const Val& A, const Val& B, bool signed_, bool negate) {
             }
             regs.push_back(o[k].v);
         }
-        and_all_zero(regs, &p, tmp);
     }
-    // uniform fast path: when the top limbs differ in every lane -- all but certain for
-    // full-width operands -- the top limb alone decides: one compare tests that, one decides
-    const bool fast = p < 0 && m == top && top >= 2 && !(a[top].is_c() && b[top].is_c());
-    uint32_t l_join = 0;
-    if (fast) {
-        l_join = next_lbl_++;
-        const uint32_t l_chain = next_lbl_++;
-        // v_cmp_<op> vcc, x, y (x may be a constant; a constant y swaps the operands)
-        auto cmp = [&](uint16_t op, Limb x, Limb y) {
-            if (y.is_c() && !x.is_c()) {
-                const uint16_t rev = op == M_V_CMP_LT ? M_V_CMP_GT
-                                   : op == M_V_CMP_LT_I32 ? M_V_CMP_GT_I32 : op;
-                emit(rev, {VCC(), IMM(y.v), V(x.v)});
-            } else {
-                emit(op, {VCC(), src(x), V(y.v)});
+    auto finish = [&]() -> Val {
+        if (hi_side) and_all_zero(regs, &p, tmp);
+        // uniform fast path: when the top limbs differ in every lane -- all but certain for
+        // full-width operands -- the top limb alone decides: one compare tests that, one decides
+        const bool fast = p < 0 && m == top && top >= 2 && !(a[top].is_c() && b[top].is_c());
+        uint32_t l_join = 0;
+        if (fast) {
+            l_join = next_lbl_++;
+            const uint32_t l_chain = next_lbl_++;
+            // v_cmp_<op> vcc, x, y (x may be a constant; a constant y swaps the operands)
+            auto cmp = [&](uint16_t op, Limb x, Limb y) {
+                if (y.is_c() && !x.is_c()) {
+                    const uint16_t rev = op == M_V_CMP_LT ? M_V_CMP_GT
+                                       : op == M_V_CMP_LT_I32 ? M_V_CMP_GT_I32 : op;
+                    emit(rev, {VCC(), IMM(y.v), V(x.v)});
+                } else {
+                    emit(op, {VCC(), src(x), V(y.v)});
+                }
+            };
+            // signed top limbs compare unbiased as signed words (constants were biased above)
+            Limb xa = a[top], xb = b[top];
+            const bool sgn_top = signed_ && top == 7;
+            if (sgn_top) {
+                if (xa.is_c()) xa.v ^= 0x80000000u;
+                if (xb.is_c()) xb.v ^= 0x80000000u;
             }
-        };
-        // signed top limbs compare unbiased as signed words (constants were biased above)
-        Limb xa = a[top], xb = b[top];
-        const bool sgn_top = signed_ && top == 7;
-        if (sgn_top) {
-            if (xa.is_c()) xa.v ^= 0x80000000u;
-            if (xb.is_c()) xb.v ^= 0x80000000u;
+            cmp(M_V_CMP_NE, xa, xb);
+            emit(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
+            emit(M_S_CBRANCH_SCC0, {LBL(l_chain)});
+            cmp(sgn_top ? M_V_CMP_LT_I32 : M_V_CMP_LT, xa, xb);  // the borrow of A - B
+            emit(M_S_BRANCH, {LBL(l_join)});
+            emit(M_LABEL, {LBL(l_chain)});
+            ++cold_;
+            bias();
+            --cold_;
         }
-        cmp(M_V_CMP_NE, xa, xb);
-        emit(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
-        emit(M_S_CBRANCH_SCC0, {LBL(l_chain)});
-        cmp(sgn_top ? M_V_CMP_LT_I32 : M_V_CMP_LT, xa, xb);  // the borrow of A - B
-        emit(M_S_BRANCH, {LBL(l_join)});
-        emit(M_LABEL, {LBL(l_chain)});
-        ++cold_;
         bias();
-        --cold_;
-    }
-    bias();
-    if (fast) ++cold_;
-    const uint32_t junk = valloc();
-    tmp.push_back(junk);
-    const int cs = chain(true, a, b, m, nullptr, junk, tmp);
-    if (fast) {
-        if (cs != 2) fail("internal: uniform compare path over a known borrow");
-        --cold_;
-        emit(M_LABEL, {LBL(l_join)});
-    }
-    free_tmp(tmp);
-    // combine: lo = borrow (A[lo] < B[lo]); result = hi_side 1: p && lo; 2: !p || lo
-    if (p < 0) {
-        if (cs != 2) return bool_const((cs == 1) != negate);
-        const int q = palloc();
-        emit(negate ? M_S_NOT_B64 : M_S_MOV_B64, {P(q), VCC()});
-        return bool_mask(q);
-    }
-    // p holds "the other side's high run is zero"
-    if (cs != 2) {
-        const bool lo = cs == 1;
-        if (hi_side == 1) {  // p && lo
-            if (!lo) { --pref_[p]; return bool_const(negate); }
-            if (negate) emit(M_S_NOT_B64, {P(p), P(p)});
+        if (fast) ++cold_;
+        const uint32_t junk = valloc();
+        tmp.push_back(junk);
+        const int cs = chain(true, a, b, m, nullptr, junk, tmp);
+        if (fast) {
+            if (cs != 2) fail("internal: uniform compare path over a known borrow");
+            --cold_;
+            emit(M_LABEL, {LBL(l_join)});
+        }
+        free_tmp(tmp);
+        // combine: lo = borrow (A[lo] < B[lo]); result = hi_side 1: p && lo; 2: !p || lo
+        if (p < 0) {
+            if (cs != 2) return bool_const((cs == 1) != negate);
+            const int q = palloc();
+            emit(negate ? M_S_NOT_B64 : M_S_MOV_B64, {P(q), VCC()});
+            return bool_mask(q);
+        }
+        // p holds "the other side's high run is zero"
+        if (cs != 2) {
+            const bool lo = cs == 1;
+            if (hi_side == 1) {  // p && lo
+                if (!lo) { --pref_[p]; return bool_const(negate); }
+                if (negate) emit(M_S_NOT_B64, {P(p), P(p)});
+                return bool_mask(p);
+            }
+            // !p || lo
+            if (lo) { --pref_[p]; return bool_const(!negate); }
+            if (!negate) emit(M_S_NOT_B64, {P(p), P(p)});
             return bool_mask(p);
         }
-        // !p || lo
-        if (lo) { --pref_[p]; return bool_const(!negate); }
-        if (!negate) emit(M_S_NOT_B64, {P(p), P(p)});
+        if (hi_side == 1) emit(M_S_AND_B64, {P(p), P(p), VCC()});
+        else emit(M_S_ORN2_B64, {P(p), VCC(), P(p)});  // lo || !p
+        if (negate) emit(M_S_NOT_B64, {P(p), P(p)});
         return bool_mask(p);
+    };
+    // uniform path of a high run: when the nonzero side's top limb is nonzero in every lane
+    // (a full-width value against a narrow one), that side is the larger one in every lane
+    if (hi_side && !regs.empty() && o[top].is_r()) {
+        const int q = palloc();
+        const uint32_t l_slow = next_lbl_++, l_join2 = next_lbl_++;
+        emit(M_V_CMP_NE, {VCC(), IMM(0), V(o[top].v)});
+        emit(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
+        emit(M_S_CBRANCH_SCC0, {LBL(l_slow)});
+        const bool lt = hi_side == 2;  // B has the nonzero high part: A < B
+        emit(M_S_MOV_B64, {P(q), IMM((lt != negate) ? 0xFFFFFFFFu : 0u)});
+        emit(M_S_BRANCH, {LBL(l_join2)});
+        emit(M_LABEL, {LBL(l_slow)});
+        ++cold_;
+        const Val r = finish();
+        --cold_;
+        if (r.bconst >= 0) {
+            emit(M_S_MOV_B64, {P(q), IMM(r.bconst ? 0xFFFFFFFFu : 0u)});
+        } else {
+            emit(M_S_MOV_B64, {P(q), P(r.pair)});
+            release(r);
+        }
+        emit(M_LABEL, {LBL(l_join2)});
+        return bool_mask(q);
     }
-    if (hi_side == 1) emit(M_S_AND_B64, {P(p), P(p), VCC()});
-    else emit(M_S_ORN2_B64, {P(p), VCC(), P(p)});  // lo || !p
-    if (negate) emit(M_S_NOT_B64, {P(p), P(p)});
-    return bool_mask(p);
+    return finish();
 }
 
 void Emitter::op_ite(int d, const Val& C, const Val& T, const Val& E) {
