@@ -1037,7 +1037,9 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
         const uint32_t acc = valloc_pair();
         uint32_t np = 0;
         if (k < top) np = valloc_pair();
-        bool first = true;
+        bool first = true, first_count = true;
+        u128 run = init_max;  // bound of the column's accumulator so far
+        const u128 M64 = ((u128)1 << 64) - 1;
         for (auto [i, j] : terms) {
             Limb x = A.l[i], y = B.l[j];
             if (x.is_c() && !y.is_c()) std::swap(x, y);
@@ -1053,13 +1055,20 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
                 s1 = V(y.v);
             }
             const Opnd s2 = first ? (init >= 0 ? V((uint32_t)init, 2) : IMM(0)) : V(acc, 2);
-            emit(M_V_MAD_U64_U32, {V(acc, 2), count ? VCC() : S(S_DIV_DUMMY, 2), s0, s1, s2});
-            if (count) {
-                if (first) emit(M_V_ADDC_CO, {V(np + 1), VCC(), IMM(0), IMM(0), VCC()}, true);
+            // this product can carry out of the pair only if the bound so far plus its own
+            // reaches 2^64 (the first product over a small carry-in cannot)
+            const u128 pm = maxv(A.l[i]) * maxv(B.l[j]);
+            const bool c_here = count && run + pm > M64;
+            run = std::min(run + pm, M64);
+            emit(M_V_MAD_U64_U32, {V(acc, 2), c_here ? VCC() : S(S_DIV_DUMMY, 2), s0, s1, s2});
+            if (c_here) {
+                if (first_count) emit(M_V_ADDC_CO, {V(np + 1), VCC(), IMM(0), IMM(0), VCC()}, true);
                 else emit(M_V_ADDC_CO, {V(np + 1), VCC(), IMM(0), V(np + 1), VCC()});
+                first_count = false;
             }
             first = false;
         }
+        if (count && first_count) emit(M_V_MOV, {V(np + 1), IMM(0)});  // no product could carry
         if (init >= 0) {
             vrelease((uint32_t)init);
             vrelease((uint32_t)init + 1);
