@@ -276,7 +276,9 @@ def main() -> None:
                     "kernel time; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (a wave64 VALU op "
                     "issues over 2 cycles; valu_busy_pmc uses the same peak). Carry, compare, "
                     "shift, VOP3 and mad ops issue at 4 cycles (profiles/r02e/valu_peak.json), "
-                    "so the kernel is issue-bound near 0.6: DESIGN.md 5.1. frac_optable prices "
+                    "so the SIMDs are saturated with VALU issue near 0.55-0.6; the uniform "
+                    "shortcuts remove VALU work behind scalar branches, which lowers this "
+                    "fraction while raising the rate: DESIGN.md 5.1. frac_optable prices "
                     "SURVEY 8d's op-cost table (division family 1100 ops) per evaluation, "
                     "which the native code undercuts (demanded limbs, folded constants, "
                     "short circuit); it is not a utilisation.",
