@@ -1855,7 +1855,7 @@ std::vector<MI> div_routine() {
     const Opnd K64LO = S(S_DIV_F64K), K64HI = S(S_DIV_F64K + 1);
     enum : uint32_t { L_UNS = 1, L_DONE, L_TOP3, L_CONV, L_ZQ, L_NOZQ, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
                       L_SDIV, L_SREM, L_SMOD, L_NARROW = 50, L_NNEG0 = 60, L_NGE0 = 70,
-                      L_NOYZ = 80, L_CZ0 = 90, L_RLT = 100, L_RLTD, L_YSLOW, L_YDONE };
+                      L_NOYZ = 80, L_CZ0 = 90, L_RLT = 100, L_RLTD, L_YSLOW, L_YDONE, L_TOPALL };
     auto to_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
         E(M_S_MOV_B32, {K64LO, IMM(0)});
         E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});
@@ -1943,9 +1943,14 @@ std::vector<MI> div_routine() {
     top3_f64(FY, Yl);
     recip();
     // lanes outside MSK (x < y, or y = 0) may have y < 2^224, where the top limbs say nothing:
-    // 1/y := 0 there, so every digit estimate is 0 and R keeps x, as their results need
+    // 1/y := 0 there, so every digit estimate is 0 and R keeps x, as their results need.  Not
+    // needed when every lane has y >= 2^224 (VCC still holds y's top limb != 0 per lane): an
+    // x < y lane then estimates a digit of 0, or 1 that the add-back corrects
+    E(M_S_CMP_EQ_U64, {VCC(), IMM(0xFFFFFFFFu)});
+    E(M_S_CBRANCH_SCC1, {LBL(L_TOPALL)});
     E(M_V_CNDMASK, {V(R_FY), IMM(0), V(R_FY), MSK}, true);
     E(M_V_CNDMASK, {V(R_FY + 1), IMM(0), V(R_FY + 1), MSK}, true);
+    L(L_TOPALL);
     top3_f64(FR, Rl);
     L(L_CONV);
     E(M_V_MUL_F64, {FC, FR, FY});
