@@ -3,9 +3,9 @@
 
 One step = every tape of the synthetic tape set (10^4 seeded random 256-bit constraint tapes,
 mythril_amd/synth_spec.json) evaluated against this rank's shard of candidate assignments,
-resident in HBM (2^23 rows per GPU by default, i.e. 2^26 over 8 GPUs), in throughput mode: every
-(tape, assignment) pair is evaluated to its Bool (MH_MODE_COUNT_ALL), per-tape hit counts and
-smallest witnesses are reduced in LDS and flushed by atomics.  With N ranks the rows are sharded
+resident in HBM (config 5's 2^26 rows per GPU by default, 8 GiB of columns), in throughput mode:
+every (tape, assignment) pair's Bool is decided (MH_MODE_COUNT_ALL), per-tape hit counts and
+smallest witnesses are reduced in registers and flushed by atomics.  With N ranks the rows are sharded
 (weak scaling) and the only exchange is one all-reduce (MIN of witness index, SUM of counts) of
 2 x 8 B per tape over RCCL.
 
@@ -27,6 +27,7 @@ sys.path.insert(0, HERE)
 
 NOMINAL_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # u32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
 PMC_SUMMARY = os.path.join(HERE, "profiles", "pmc_summary.json")
+ALG_WORK = os.path.join(HERE, "profiles", "alg_work.json")
 
 
 def log(*a):
@@ -34,10 +35,14 @@ def log(*a):
 
 
 def cpu_baseline(ts, seed, seconds: float):
-    """Oracle port (oracle/tape_eval.c, OpenMP on all host cores) on a bounded sample."""
+    """Oracle port (oracle/tape_eval.c, OpenMP on all host cores) on a bounded sample, with the
+    single-core figure of the same port beside it (SURVEY §8d CPU baseline (1))."""
     from oracle import ctape
 
-    return ctape.benchmark(ts, seed, seconds)
+    out = ctape.benchmark(ts, seed, seconds)
+    one = ctape.benchmark(ts, seed, seconds / 2, threads=1)
+    out["single_core"] = {"value": one["value"], "cores": 1, "sample": one["sample"]}
+    return out
 
 
 def main() -> None:
@@ -47,7 +52,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tapes", type=int, default=None, help="default: spec n_tapes (10^4)")
     ap.add_argument("--rows-per-gpu", type=int, default=None,
-                    help="default 2^23 (plain), 2^20 (keccak variant)")
+                    help="default 2^26 (plain: config 5 on one GPU), 2^20 (keccak variant)")
     ap.add_argument("--variant", choices=["plain", "keccak"], default="plain",
                     help="keccak: SURVEY §8d's keccak variant (one keccak256 of a 512-bit "
                          "input per tape); the headline line is the plain config 5")
@@ -66,12 +71,14 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.rows_per_gpu is None:
-        args.rows_per_gpu = 1 << 20 if args.variant == "keccak" else 1 << 23
+        args.rows_per_gpu = 1 << 20 if args.variant == "keccak" else 1 << 26
 
     import torch
     import torch.distributed as dist
 
     from mythril_amd import native, shard, synth
+
+    build_id = native.codegen_id()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -206,7 +213,6 @@ def main() -> None:
                     "every row evaluated), timed after the headline steps",
         }
         log("[rank 0] full-eval companion: %s" % companion)
-    achieved_table = alg_ops_per_row * rows / (kms / 1e3) / 1e12
     try:
         peak_measured = ctx.microbench(0) / 1e12
     except Exception as e:  # pragma: no cover
@@ -214,17 +220,31 @@ def main() -> None:
         peak_measured = None
     traffic = valu_busy = exec_ops = None
     pmc_tag = None
-    if os.path.exists(PMC_SUMMARY):  # the committed PMC profile of this exact workload
+    if os.path.exists(PMC_SUMMARY):  # the committed PMC profile of this workload and build
         for pmc in json.load(open(PMC_SUMMARY)).get("entries", []):
             if pmc.get("tapes") == n_tapes and pmc.get("rows_per_gpu") == rows and \
                     pmc.get("engine", "interp") == args.engine and \
                     pmc.get("variant", "plain") == args.variant and \
-                    bool(pmc.get("short_circuit", False)) == short_circuit:
+                    bool(pmc.get("short_circuit", False)) == short_circuit and \
+                    pmc.get("codegen_id") == build_id:
                 traffic = pmc.get("hbm_bytes_per_launch")
                 valu_busy = pmc.get("valu_busy")
                 exec_ops = pmc.get("exec_lane_ops_per_launch")
                 pmc_tag = pmc.get("tag")
     exec_rate = (exec_ops / (kms / 1e3) / 1e12) if exec_ops else None
+    # algorithmic work per evaluation of this build (scripts/alg_work.py): the lane-ops a
+    # row-exact lazy evaluator needs with this code's per-op costs; neither mode can do less
+    alg = None
+    if os.path.exists(ALG_WORK) and args.engine == "jit" and n_tapes == spec["n_tapes"]:
+        for e in json.load(open(ALG_WORK)).get("entries", []):
+            if e.get("codegen_id") == build_id and e.get("variant") == args.variant:
+                alg = e
+    alg_per_eval = alg["alg_lane_ops_per_eval"] if alg else None
+    alg_rate = (alg_per_eval * n_tapes * rows / (kms / 1e3) / 1e12) if alg else None
+    if companion is not None and alg:
+        companion["roofline_achieved"] = alg_per_eval * n_tapes * rows / (
+            companion["kernel_ms"] / 1e3) / 1e12
+        companion["roofline_frac"] = companion["roofline_achieved"] / NOMINAL_PEAK_TOPS
     line = {
         "metric": "constraint-evals/sec",
         "value": value,
@@ -256,32 +276,37 @@ def main() -> None:
         "per_gpu": value / world,
         "kernel_ms": kms,
         "tapes_with_witness": hits,
+        "build": build_id,
         "jit": jit_info,
         "roofline": {
             "bound": "valu",
-            "achieved": exec_rate,
+            "achieved": alg_rate,
             "peak": NOMINAL_PEAK_TOPS,
             "unit": "T u32-ops/s",
-            "frac": (exec_rate / NOMINAL_PEAK_TOPS) if exec_rate else None,
+            "frac": (alg_rate / NOMINAL_PEAK_TOPS) if alg_rate else None,
             "traffic": traffic,
             "traffic_unit": "bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, profiles/)",
+            "alg_lane_ops_per_eval": alg_per_eval,
+            "alg_profile": ("profiles/alg_work.json build %s (%d tapes x %d rows)"
+                            % (build_id, alg["tapes_sampled"], alg["rows"])) if alg else None,
+            "executed": exec_rate,
+            "frac_executed": (exec_rate / NOMINAL_PEAK_TOPS) if exec_rate else None,
+            "exec_lane_ops_per_eval": (exec_ops / (n_tapes * rows)) if exec_ops else None,
             "pmc_profile": pmc_tag,
             "valu_busy_pmc": valu_busy,
-            "exec_lane_ops_per_eval": (exec_ops / (n_tapes * rows)) if exec_ops else None,
             "peak_measured_add_chain": peak_measured,
-            "alg_ops_per_eval": alg_ops_per_row / n_tapes,
-            "frac_optable": achieved_table / NOMINAL_PEAK_TOPS,
-            "note": "achieved = executed VALU lane-ops per launch (PMC SQ_INSTS_VALU x 64 of the "
-                    "profile named by pmc_profile, same workload and build options) / this run's "
-                    "kernel time; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (a wave64 VALU op "
-                    "issues over 2 cycles; valu_busy_pmc uses the same peak). Carry, compare, "
-                    "shift, VOP3 and mad ops issue at 4 cycles (profiles/r02e/valu_peak.json), "
-                    "so the SIMDs are saturated with VALU issue near 0.55-0.6; the uniform "
-                    "shortcuts remove VALU work behind scalar branches, which lowers this "
-                    "fraction while raising the rate: DESIGN.md 5.1. frac_optable prices "
-                    "SURVEY 8d's op-cost table (division family 1100 ops) per evaluation, "
-                    "which the native code undercuts (demanded limbs, folded constants, "
-                    "short circuit); it is not a utilisation.",
+            "optable_ops_per_eval": alg_ops_per_row / n_tapes,
+            "note": "achieved = algorithmic lane-ops per launch / this run's kernel time: per "
+                    "(tape, row) the VALU lane-ops of the conjuncts up to and including the "
+                    "row's first false one, in the emitted order, at this code's per-op cost "
+                    "(alg_lane_ops_per_eval, measured per build by scripts/alg_work.py on the "
+                    "host emulator of the emitted code); no mode executes less, so frac <= 1 "
+                    "here and in full_eval. executed = PMC SQ_INSTS_VALU x 64 of the profile of "
+                    "this build (pmc_profile; null when none) / kernel time; frac_executed / "
+                    "frac = the lanes a wave keeps busy for rows already decided. peak = 256 CU "
+                    "x 4 SIMD x 32 lanes x 2.4 GHz (a wave64 VALU op issues over 2 cycles). "
+                    "optable_ops_per_eval prices SURVEY 8d's op table, which the native code "
+                    "undercuts (DESIGN 5.1): informational, not a work count.",
         },
     }
     if companion is not None:

@@ -87,7 +87,10 @@ typedef struct mh_node {
 enum {
     MH_MODE_FIRST_HIT = 0,   /* per tape: smallest satisfying assignment index (early exit allowed) */
     MH_MODE_COUNT_ALL = 1    /* per tape: number of satisfying assignments AND smallest index;       */
-                             /*           every (tape, assignment) pair is evaluated (throughput)    */
+                             /*           every (tape, assignment) pair's Bool is determined: no   */
+                             /*           early exit across assignments (the native code may stop  */
+                             /*           a wave's evaluation once every row of it has a false     */
+                             /*           conjunct -- counts and indices are the same)              */
 };
 #define MH_NO_HIT 0xFFFFFFFFFFFFFFFFull
 
@@ -197,17 +200,21 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
 
 /* ---- measurement ----------------------------------------------------------------------------- */
 /* ---- native-code path (no reference counterpart: replaces the interpreter for throughput runs)
- * mh_tapes_jit compiles every tape of the set that the JIT covers (the asm-core op set plus the
- * division family, at most 4 assignment columns) to straight-line gfx950 machine code -- one
+ * mh_tapes_jit compiles every tape of the set that the JIT covers to gfx950 machine code -- one
  * code object per slice of tape groups, assembled in-process by comgr and loaded with
- * hipModuleLoadData (src/jit.cpp).  Afterwards mh_run / mh_run_async over the whole tape set run
- * the jitted tapes through that code and the rest through the interpreter; results are
- * identical.  flags: MH_JIT_VALUES also builds the values kernel behind mh_jit_eval_all;
- * MH_JIT_FULL_EVAL turns off short-circuit evaluation of root conjunctions (by default a wave
- * leaves a tape once no row of its 64 satisfies the conjuncts evaluated so far -- the results
- * are the same either way; the environment variable MH_JIT_SC=0 does the same).
- * max_vgpr: register budget per wave (occupancy = 512 / max_vgpr waves per SIMD), 0 = default
- * 128.  Cost: a few seconds per thousand tapes, once per tape set, outside any timed region.      */
+ * hipModuleLoadData (mythril_amd/csrc/jit.cpp).  Covered: every op of the IR (the EVM word ops,
+ * ADDMOD / MULMOD and the overflow predicates are restated on native operations; EXP and
+ * MULMOD by a per-lane operand run as loops), any number of assignment columns (up to 4 are held
+ * in registers for a whole 64-row chunk, above that each tape loads the limbs it uses); a tape is
+ * refused only when its code exceeds 96 KB or its registers 168 VGPRs (mh_tapes_jitted tells).
+ * Afterwards mh_run / mh_run_async over the whole tape set run the jitted tapes through that code
+ * and the rest through the interpreter; results are identical.  flags: MH_JIT_VALUES also builds
+ * the values kernel behind mh_jit_eval_all; MH_JIT_FULL_EVAL turns off short-circuit evaluation
+ * of root conjunctions (by default a wave leaves a tape once no row of its 64 satisfies the
+ * conjuncts evaluated so far -- the results are the same either way; the environment variable
+ * MH_JIT_SC=0 does the same).  max_vgpr: register budget per wave, 96..256 (occupancy =
+ * min(8, 512 / max_vgpr) waves per SIMD), 0 = default 128.  Cost: a few seconds per thousand
+ * tapes, once per tape set, outside any timed region.                                            */
 #define MH_JIT_VALUES 1u
 #define MH_JIT_FULL_EVAL 2u
 typedef struct mh_jit_info {

@@ -901,7 +901,9 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
     opt.max_vgpr = max_vgpr ? max_vgpr : 128;
     opt.short_circuit = (flags & MH_JIT_FULL_EVAL) == 0;
     if (const char* e = std::getenv("MH_JIT_SC")) opt.short_circuit = opt.short_circuit && atoi(e) != 0;
-    if (opt.max_vgpr > 512 || opt.max_vgpr < 96) return set_err(MH_E_INVALID, "max_vgpr outside 96..512");
+    // gfx950 has 256 architectural VGPRs per wave (an allocation above it would only fail later,
+    // in the assembler)
+    if (opt.max_vgpr > 256 || opt.max_vgpr < 96) return set_err(MH_E_INVALID, "max_vgpr outside 96..256");
     // build threads = code objects per occupancy class = launches per run: 4 (MI355X, config 5,
     // profiles/r02y: 16 objects 3.195e11 evals/s, 4 3.222e11, 1 3.226e11 -- each launch drains
     // its tail before the next starts; 4 keeps the emission and assembly parallel)

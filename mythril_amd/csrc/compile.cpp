@@ -346,6 +346,146 @@ struct Lowering {
     // (hi << wb) | lo for canonical parts, wb + width(hi) <= 256
     int concat(int hi, int lo, uint32_t wb) { return emit(D_OR_R, shl_imm(hi, wb), lo, -1); }
 
+    // ---- native-code forms (jit = true, the JIT's lowering): the complex ops the JIT has no
+    // machine code for, restated on ops it has.  Same values as exec.h complex_op on canonical
+    // operands (tests/test_jit.py checks each against the oracle).
+    bool jit = false;
+
+    int small_const(uint32_t x) {
+        const uint32_t m[8] = {x, 0, 0, 0, 0, 0, 0, 0};
+        return (int)const_index(m, 256);
+    }
+    // limbs of constant node k masked to w bits
+    void const_limbs(uint32_t k, uint32_t w, uint32_t* m) const {
+        const mh_node& c = t[(size_t)(*vals_)[k].remat];
+        for (int i = 0; i < 8; ++i) m[i] = consts[8ull * c.imm0 + i] & lane_mask(i, w);
+    }
+    // 248 - 8 k mod 2^256: the right shift that brings big-endian byte k of a word to the bottom
+    int byte_shift(int k) {
+        return emit(D_RSUB_R, shl_imm(k, 3), -1, -1, 256, 0, small_const(248));
+    }
+    // SIGNEXTEND(k, x): for k < 31, x shifted left and arithmetically right by 248 - 8k (the sign
+    // bit 8k + 7 lands on bit 255 and is copied back down); x itself otherwise
+    int jit_signextend(uint32_t nk, uint32_t nx) {
+        if (is_const_node(nk)) {
+            uint32_t m[8];
+            const_limbs(nk, 256, m);
+            const int x = vreg_of(nx);
+            if (m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7] || m[0] > 30) return x;
+            const uint32_t s = 248 - 8 * m[0];
+            return ashr_imm(shl_imm(x, s), s, 256);
+        }
+        const int k = vreg_of(nk), x = vreg_of(nx);
+        if (k < 0 || x < 0) return -1;
+        const int s = byte_shift(k);
+        const int u = emit(D_ASHR_V, emit(D_SHL_V, x, s, -1, 256), s, -1, 256);
+        const int in_range = emit(D_ULT_R, k, -1, -1, 256, 0, small_const(31));
+        return emit(D_ITE, in_range, u, x, 256);
+    }
+    // BYTE(i, x): (x >> (248 - 8 i)) & 0xff for i < 32, else 0
+    int jit_byte(uint32_t ni, uint32_t nx) {
+        if (is_const_node(ni)) {
+            uint32_t m[8];
+            const_limbs(ni, 256, m);
+            if (m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7] || m[0] > 31)
+                return emit(D_LOADC, -1, -1, -1, 256, 0, zero_const());
+            const uint32_t s = 248 - 8 * m[0];
+            int x = vreg_of(nx);
+            if (x < 0) return -1;
+            if (s) x = shr_imm(x, s);
+            return emit(D_AND_R, x, -1, -1, 256, 0, small_const(0xFF));
+        }
+        const int i = vreg_of(ni), x = vreg_of(nx);
+        if (i < 0 || x < 0) return -1;
+        const int u = emit(D_AND_R, emit(D_LSHR_V, x, byte_shift(i), -1, 256), -1, -1, 256, 0,
+                           small_const(0xFF));
+        const int in_range = emit(D_ULT_R, i, -1, -1, 256, 0, small_const(32));
+        return emit(D_ITE, in_range, u, emit(D_LOADC, -1, -1, -1, 256, 0, zero_const()), 256);
+    }
+    // EXP(b, e) mod 2^w: a constant exponent as left-to-right square and multiply, a symbolic one
+    // stays D_EXP (the native code's loop, jit.cpp op_exp)
+    int jit_exp(uint32_t nb, uint32_t ne, uint32_t w) {
+        if (!is_const_node(ne)) {  // a per-lane exponent: the native code's EXP loop
+            const int b = vreg_of(nb), x = vreg_of(ne);
+            return b < 0 || x < 0 ? -1 : masked(emit(D_EXP, b, x, -1, 256), w);
+        }
+        uint32_t e[8];
+        const_limbs(ne, w, e);
+        int top = -1;
+        for (int i = 255; i >= 0 && top < 0; --i)
+            if ((e[i >> 5] >> (i & 31)) & 1u) top = i;
+        if (top < 0) return emit(D_LOADC, -1, -1, -1, 256, 0, small_const(1));
+        const int b = vreg_of(nb);
+        if (b < 0) return -1;
+        int r = b;
+        for (int i = top - 1; i >= 0; --i) {
+            r = emit(D_MUL_R, r, r, -1, 256);
+            if ((e[i >> 5] >> (i & 31)) & 1u) r = emit(D_MUL_R, r, b, -1, 256);
+        }
+        return masked(r, w);
+    }
+    // BVAddNoOverflow(a, b, False) at width w: b <= a ^ (2^w - 1)  (a + b < 2^w)
+    int jit_add_noovfl(uint32_t na, uint32_t nb, uint32_t w) {
+        if (is_const_node(nb) && !is_const_node(na)) std::swap(na, nb);
+        if (is_const_node(na)) {
+            uint32_t m[8];
+            const_limbs(na, w, m);
+            for (int i = 0; i < 8; ++i) m[i] = ~m[i] & lane_mask(i, w);
+            const int b = vreg_of(nb);
+            return b < 0 ? -1 : emit(D_ULE_R, b, -1, -1, 256, 0, (int)const_index(m, 256));
+        }
+        const int a = vreg_of(na);
+        if (a < 0) return -1;
+        const int na_ = emit(D_XOR_R, a, -1, -1, 256, 0, mask_const(w));
+        if (is_const_node(nb)) return emit(D_UGE_R, na_, -1, -1, 256, 0, const_of(nb));
+        const int b = vreg_of(nb);
+        return b < 0 ? -1 : emit(D_ULE_R, b, na_, -1, 256);
+    }
+    // BVMulNoOverflow(a, b, False) at width w: b <= floor((2^w - 1) / a)  (a = 0: the quotient
+    // is 2^256 - 1, SMT-LIB x / 0, and the compare holds, as a * b = 0 does not overflow)
+    int jit_mul_noovfl(uint32_t na, uint32_t nb, uint32_t w) {
+        if (is_const_node(nb) && !is_const_node(na)) std::swap(na, nb);
+        if (is_const_node(na)) {
+            uint32_t c[8], mw[8], q[8];
+            const_limbs(na, w, c);
+            if (!(c[0] | c[1] | c[2] | c[3] | c[4] | c[5] | c[6] | c[7]))
+                return emit(D_TRUE, -1, -1, -1, 1);
+            for (int i = 0; i < 8; ++i) mw[i] = lane_mask(i, w);
+            divmod_family(0, mw, c, q, 256);
+            const int b = vreg_of(nb);
+            return b < 0 ? -1 : emit(D_ULE_R, b, -1, -1, 256, 0, (int)const_index(q, 256));
+        }
+        const int a = vreg_of(na), b = vreg_of(nb);
+        if (a < 0 || b < 0) return -1;
+        const int q = emit(D_UDIV_R, emit(D_LOADC, -1, -1, -1, 256, 0, mask_const(w)), a, -1, 256);
+        return emit(D_ULE_R, b, q, -1, 256);
+    }
+    // yellow-paper ADDMOD (exact sum): t = (a mod n) + (b mod n) mod 2^256, minus n when the
+    // exact sum (carry or t >= n) reaches n; n = 0 leaves t = a + b mod 2^256 (zero_low) or 0
+    int jit_addmod(int a, int b, int n, bool zero_low) {
+        const int r1 = emit(D_UREM_R, a, n, -1, 256), r2 = emit(D_UREM_R, b, n, -1, 256);
+        const int t_ = emit(D_ADD_R, r1, r2, -1, 256);
+        const int ge = emit(D_BOR, emit(D_ULT_R, t_, r1, -1, 256), emit(D_UGE_R, t_, n, -1, 256),
+                            -1, 1);
+        int r = emit(D_ITE, ge, emit(D_SUB_R, t_, n, -1, 256), t_, 256);
+        if (!zero_low) {
+            const int nz = emit(D_EQ_R, n, -1, -1, 256, 0, zero_const());
+            r = emit(D_ITE, nz, emit(D_LOADC, -1, -1, -1, 256, 0, zero_const()), r, 256);
+        }
+        return r;
+    }
+    // yellow-paper MULMOD (exact product): (a mod n) * (b mod n) mod n by the native code's
+    // double-and-add loop (D_MULMOD with aux bit 1: operands reduced); n = 0 gives the low 256
+    // bits of a * b (zero_low) or 0
+    int jit_mulmod(int a, int b, int n, bool zero_low) {
+        const int x = emit(D_UREM_R, a, n, -1, 256), y = emit(D_UREM_R, b, n, -1, 256);
+        const int r = emit(D_MULMOD, x, y, n, 256, zero_low ? 3u : 2u);
+        const int nz = emit(D_EQ_R, n, -1, -1, 256, 0, zero_const());
+        const int z = zero_low ? emit(D_MUL_R, a, b, -1, 256)
+                               : emit(D_LOADC, -1, -1, -1, 256, 0, zero_const());
+        return emit(D_ITE, nz, z, r, 256);
+    }
+
     std::vector<Piece> pieces_of(uint32_t k, uint32_t width) {
         const Val& v = (*vals_)[k];
         if (!v.wide()) return {Piece{vreg_of(k), width}};
@@ -474,6 +614,13 @@ bool Lowering::lower(std::vector<Val>& vals) {
                 }
                 if ((op == D_SIGNEXT || op == D_BYTE) && w != 256)
                     return fail("EVM word ops are 256-bit");
+                if (jit && (op == D_SIGNEXT || op == D_BYTE || op == D_EXP)) {
+                    out.vreg = op == D_SIGNEXT ? jit_signextend(nd.a, nd.b)
+                               : op == D_BYTE  ? jit_byte(nd.a, nd.b)
+                                               : jit_exp(nd.a, nd.b, w);
+                    if (out.vreg < 0) return fail(err.empty() ? "EVM word op operand" : err);
+                    break;
+                }
                 if (w < 256 && (op == D_SDIV_R || op == D_SREM_R || op == D_SMOD_R)) {
                     // signed division at width w = 256-bit signed division of the sign-extended
                     // operands, masked (all SMT-LIB sign cases agree mod 2^w)
@@ -523,6 +670,11 @@ bool Lowering::lower(std::vector<Val>& vals) {
                     return fail("ADDMOD / MULMOD take three 256-bit words");
                 const int a = narrow(nd.a), b = narrow(nd.b), c = narrow(nd.c);
                 if (a < 0 || b < 0 || c < 0) return fail("ADDMOD / MULMOD operand wider than 256");
+                if (jit) {
+                    out.vreg = nd.op == MH_OP_EVM_ADDMOD ? jit_addmod(a, b, c, nd.imm0 != 0)
+                                                         : jit_mulmod(a, b, c, nd.imm0 != 0);
+                    break;
+                }
                 features |= F_EVM;
                 out.vreg = emit(nd.op == MH_OP_EVM_ADDMOD ? D_ADDMOD : D_MULMOD, a, b, c, 256,
                                 nd.imm0);
@@ -568,6 +720,12 @@ bool Lowering::lower(std::vector<Val>& vals) {
                     case MH_OP_BVADD_NOOVFL_U: op = D_UADD_NOOVFL; features |= F_CPLX; break;
                     case MH_OP_BVMUL_NOOVFL_U: op = D_UMUL_NOOVFL; features |= F_CPLX; break;
                     case MH_OP_BVSUB_NOUDFL_U: op = D_UGE_R; break;  // b <= a
+                }
+                if (jit && (op == D_UADD_NOOVFL || op == D_UMUL_NOOVFL)) {
+                    out.vreg = op == D_UADD_NOOVFL ? jit_add_noovfl(nd.a, nd.b, wa)
+                                                   : jit_mul_noovfl(nd.a, nd.b, wa);
+                    if (out.vreg < 0) return fail("overflow predicate operand");
+                    break;
                 }
                 const bool narrow_signed = !full && (nd.op == MH_OP_BVSLT || nd.op == MH_OP_BVSLE ||
                                                      nd.op == MH_OP_BVSGT || nd.op == MH_OP_BVSGE);
@@ -952,8 +1110,18 @@ void sample_bools(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t
                 else ld(1, v.b);
                 ld(2, v.c);
             }
-            if (v.op == D_LOADC) std::memcpy(m.R[3], pool.data() + 8ull * (uint32_t)v.cidx, 32);
-            else if (v.op == D_LOADVAR) std::memset(m.R[3], 0, 32);
+            if (v.op == D_LOADC) {
+                std::memcpy(m.R[3], pool.data() + 8ull * (uint32_t)v.cidx, 32);
+            } else if (v.op == D_LOADVAR) {  // a column not pinned: uniform too, per (row, column)
+                uint64_t h = seed ^ (0xD1B54A32D192ED03ull * (r + 1)) ^ (0x8CB92BA72F3D8DD7ull * (v.aux + 1));
+                for (int k = 0; k < 8; ++k) {
+                    h += 0x9E3779B97F4A7C15ull;
+                    uint64_t z = h;
+                    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+                    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+                    m.R[3][k] = (u32)(z ^ (z >> 31));
+                }
+            }
             else {
                 const u32 w1 = v.op == D_KECCAK ? v.w1raw
                                                 : (v.op | ((v.width & 0x1FFu) << 8) | (v.aux << 17));
@@ -1012,7 +1180,7 @@ void rewrite_wide_modops(std::vector<mh_node>& t) {
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,
-                       std::string& err, bool value_numbering) {
+                       std::string& err, bool value_numbering, bool jit_forms) {
     if (n_nodes == 0) {
         err = "empty tape";
         return MH_E_INVALID;
@@ -1020,6 +1188,7 @@ int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* con
     std::vector<mh_node> t(nodes, nodes + n_nodes);
     rewrite_wide_modops(t);
     Lowering L(t, consts, n_consts, n_vars, dconsts, dconst_index);
+    L.jit = jit_forms;
     std::vector<Val> vals;
     if (!L.lower(vals)) {
         err = L.err;

@@ -273,6 +273,11 @@ private:
     void op_div(int d, int a, int b, int cidx, uint32_t kind, int cur);
     void rescue_div_regs(int cur, uint32_t end = R_TEMP0);
     void op_keccak(const SsaInsn& v, int cur);
+    void op_exp(int d, const Val& A, const Val& E);
+    void addmod_regs(const uint32_t* u, const uint32_t* v, const uint32_t* n, uint32_t* r,
+                     int when = -1);
+    void op_mulmod(int d, const Val& X, const Val& Y, const Val& N);
+    int scratch_ = -1;  // a virtual register past the tape's own (op_exp's products)
     void demand();
     void sc_check(const Val& v);
     Val& out(int d) {
@@ -1086,6 +1091,154 @@ void Emitter::op_mul(int d, const Val& A, const Val& B) {
     free_tmp(tmp);
 }
 
+// EXP(b, e) mod 2^256 for a per-lane exponent (EVM EXP, exec.h evm_exp): square and multiply from
+// the exponent's low bit up, in a loop that runs while some valid lane still has exponent bits
+// left (a wave-uniform exit, as evm_exp's any_lane test); the running result, the running square
+// and the exponent are loop-carried registers.  The result is the full 256 bits (the lowering
+// masks narrower widths).
+void Emitter::op_exp(int d, const Val& A, const Val& E) {
+    uint32_t res[8], b[8], e[8];
+    for (int k = 0; k < 8; ++k) {
+        res[k] = valloc();
+        emit(M_V_MOV, {V(res[k]), IMM(k == 0 ? 1u : 0u)});
+    }
+    for (int k = 0; k < 8; ++k) {
+        b[k] = valloc();
+        emit(M_V_MOV, {V(b[k]), src(A.l[k])});
+    }
+    for (int k = 0; k < 8; ++k) {
+        e[k] = valloc();
+        emit(M_V_MOV, {V(e[k]), src(E.l[k])});
+    }
+    const uint32_t t = valloc();
+    const int p = palloc();
+    const uint32_t top = next_lbl_++, done = next_lbl_++;
+    emit(M_LABEL, {LBL(top)});
+    emit(M_V_OR3, {V(t), V(e[0]), V(e[1]), V(e[2])});
+    emit(M_V_OR3, {V(t), V(t), V(e[3]), V(e[4])});
+    emit(M_V_OR3, {V(t), V(t), V(e[5]), V(e[6])});
+    emit(M_V_OR, {V(t), V(e[7]), V(t)});
+    emit(M_V_CMP_NE, {VCC(), IMM(0), V(t)});
+    emit(M_S_AND_B64, {S(S_SCRATCH, 2), VCC(), S(S_VALID, 2)});
+    emit(M_S_CBRANCH_SCC0, {LBL(done)});
+    emit(M_V_AND, {V(t), IMM(1), V(e[0])});
+    emit(M_V_CMP_NE, {P(p), IMM(0), V(t)}, true);
+    Val R, B;
+    R.defined = B.defined = true;
+    for (int k = 0; k < 8; ++k) {
+        R.l[k] = Limb::R(res[k]);
+        B.l[k] = Limb::R(b[k]);
+    }
+    op_mul(scratch_, R, B);  // res = bit ? res * b : res
+    {
+        Val prod = vals_[scratch_];
+        for (int k = 0; k < 8; ++k)
+            emit(M_V_CNDMASK, {V(res[k]), V(res[k]), src(prod.l[k]), P(p)}, true);
+        release(prod);
+    }
+    op_mul(scratch_, B, B);  // b = b * b
+    {
+        Val sq = vals_[scratch_];
+        for (int k = 0; k < 8; ++k) emit(M_V_MOV, {V(b[k]), src(sq.l[k])});
+        release(sq);
+    }
+    for (int k = 0; k < 7; ++k) emit(M_V_ALIGNBIT, {V(e[k]), V(e[k + 1]), V(e[k]), IMM(1)});
+    emit(M_V_LSHRREV, {V(e[7]), IMM(1), V(e[7])});
+    emit(M_S_BRANCH, {LBL(top)});
+    emit(M_LABEL, {LBL(done)});
+    --pref_[p];
+    vrelease(t);
+    for (int k = 0; k < 8; ++k) {
+        vrelease(b[k]);
+        vrelease(e[k]);
+    }
+    Val& O = out(d);
+    for (int k = 0; k < 8; ++k) O.l[k] = Limb::R(res[k]);
+}
+
+// r = (u + v) mod n for u, v < n (8-limb VGPR arrays; r may be u or v): the exact sum minus n
+// when the sum carries out or s - n does not borrow.  n = 0 leaves r = u + v mod 2^256.  With a
+// Bool pair `when`, lanes outside it keep r.
+void Emitter::addmod_regs(const uint32_t* u, const uint32_t* v, const uint32_t* n, uint32_t* r,
+                          int when) {
+    uint32_t sm[8], df[8];
+    for (int k = 0; k < 8; ++k) {
+        sm[k] = valloc();
+        df[k] = valloc();
+    }
+    emit(M_V_ADD_CO, {V(sm[0]), VCC(), V(u[0]), V(v[0])});
+    for (int k = 1; k < 8; ++k) emit(M_V_ADDC_CO, {V(sm[k]), VCC(), V(u[k]), V(v[k]), VCC()});
+    const int pc = palloc();
+    emit(M_S_MOV_B64, {P(pc), VCC()});
+    emit(M_V_SUB_CO, {V(df[0]), VCC(), V(sm[0]), V(n[0])});
+    for (int k = 1; k < 8; ++k) emit(M_V_SUBB_CO, {V(df[k]), VCC(), V(sm[k]), V(n[k]), VCC()});
+    emit(M_S_ORN2_B64, {P(pc), P(pc), VCC()});  // carry out, or no borrow: s >= n
+    for (int k = 0; k < 8; ++k) {
+        if (when < 0) {
+            emit(M_V_CNDMASK, {V(r[k]), V(sm[k]), V(df[k]), P(pc)}, true);
+        } else {
+            emit(M_V_CNDMASK, {V(sm[k]), V(sm[k]), V(df[k]), P(pc)}, true);
+            emit(M_V_CNDMASK, {V(r[k]), V(r[k]), V(sm[k]), P(when)}, true);
+        }
+    }
+    --pref_[pc];
+    for (int k = 0; k < 8; ++k) {
+        vrelease(sm[k]);
+        vrelease(df[k]);
+    }
+}
+
+// Yellow-paper MULMOD on operands the lowering has already reduced mod n (x, y < n; exec.h
+// evm_modop): x * y mod n by double and add over y's bits from the low end, r += p and
+// p = 2 p mod n, in a loop that runs while some valid lane has bits of y left.  The lowering
+// selects the n = 0 result around it.
+void Emitter::op_mulmod(int d, const Val& X, const Val& Y, const Val& N) {
+    uint32_t r[8], p[8], y[8], n[8];
+    for (int k = 0; k < 8; ++k) {
+        r[k] = valloc();
+        emit(M_V_MOV, {V(r[k]), IMM(0)});
+        p[k] = valloc();
+        emit(M_V_MOV, {V(p[k]), src(X.l[k])});
+        y[k] = valloc();
+        emit(M_V_MOV, {V(y[k]), src(Y.l[k])});
+        if (N.l[k].is_r()) {  // read where it lives (never written here)
+            n[k] = N.l[k].v;
+            vretain(n[k]);
+        } else {
+            n[k] = valloc();
+            emit(M_V_MOV, {V(n[k]), src(N.l[k])});
+        }
+    }
+    const uint32_t t = valloc();
+    const int pb = palloc();
+    const uint32_t top = next_lbl_++, done = next_lbl_++;
+    emit(M_LABEL, {LBL(top)});
+    emit(M_V_OR3, {V(t), V(y[0]), V(y[1]), V(y[2])});
+    emit(M_V_OR3, {V(t), V(t), V(y[3]), V(y[4])});
+    emit(M_V_OR3, {V(t), V(t), V(y[5]), V(y[6])});
+    emit(M_V_OR, {V(t), V(y[7]), V(t)});
+    emit(M_V_CMP_NE, {VCC(), IMM(0), V(t)});
+    emit(M_S_AND_B64, {S(S_SCRATCH, 2), VCC(), S(S_VALID, 2)});
+    emit(M_S_CBRANCH_SCC0, {LBL(done)});
+    emit(M_V_AND, {V(t), IMM(1), V(y[0])});
+    emit(M_V_CMP_NE, {P(pb), IMM(0), V(t)}, true);
+    addmod_regs(r, p, n, r, pb);  // r = bit ? r + p mod n : r
+    addmod_regs(p, p, n, p);      // p = 2 p mod n
+    for (int k = 0; k < 7; ++k) emit(M_V_ALIGNBIT, {V(y[k]), V(y[k + 1]), V(y[k]), IMM(1)});
+    emit(M_V_LSHRREV, {V(y[7]), IMM(1), V(y[7])});
+    emit(M_S_BRANCH, {LBL(top)});
+    emit(M_LABEL, {LBL(done)});
+    --pref_[pb];
+    vrelease(t);
+    for (int k = 0; k < 8; ++k) {
+        vrelease(p[k]);
+        vrelease(y[k]);
+        vrelease(n[k]);
+    }
+    Val& O = out(d);
+    for (int k = 0; k < 8; ++k) O.l[k] = Limb::R(r[k]);
+}
+
 // The result stays where the subroutine leaves it (the quotient / signed remainders in DQ, the
 // unsigned remainder in DR) until the next call: limbs of live values that sit in the
 // subroutine's registers are moved out just before it (rescue_div_regs).
@@ -1261,6 +1414,11 @@ void Emitter::demand() {
                 break;
             }
             case D_ITE: D(v.b, dd); D(v.c, dd); break;
+            case D_EXP: case D_MULMOD:
+                D(v.a, 0xFF);
+                D(v.b, 0xFF);
+                D(v.c, 0xFF);
+                break;
             case D_SHL_V: case D_LSHR_V: case D_ASHR_V:
                 D(v.a, 0xFF);
                 D(v.b, 0xFF);
@@ -1330,6 +1488,8 @@ double sc_cost(const SsaInsn& v) {
     if (op >= D_UDIV_R && op <= D_SMOD_C) return 130;
     if (op == D_SHL_V || op == D_LSHR_V || op == D_ASHR_V) return 35;
     if (op == D_KECCAK) return 7000;
+    if (op == D_EXP) return 40000;
+    if (op == D_MULMOD) return 20000;
     if (op == D_ADD_R || op == D_SUB_R || op == D_RSUB_R) return 10;
     if (op >= D_EQ_R && op <= D_SGE_C) return 9;
     if (op == D_AND_R || op == D_OR_R || op == D_XOR_R || op == D_ITE) return 6;
@@ -1557,18 +1717,27 @@ TapeCode Emitter::run() {
         const auto& code = st_.code;
         const int nv = st_.n_vregs;
         if (insn_cost_) insn_cost_->assign(code.size(), 0.0);
-        if (st_.n_pinned != (int)n_vars_ || n_vars_ > 4) fail("assignment columns not pinned");
+        const uint32_t n_pin = pinned_cols(n_vars_);
+        if (st_.n_pinned != (int)n_pin) fail("assignment columns not pinned as the module pins them");
         bool has_div = false, has_kec = false;
         for (const SsaInsn& v : code) {
             if (v.op == D_KECCAK) { has_kec = true; continue; }
-            if (v.op >= D_FIRST_COMPLEX) fail("complex op (interpreter only)");
+            if (v.op == D_LOADVAR || v.op == D_EXP) continue;
+            if (v.op == D_MULMOD && (v.aux & 2u)) continue;  // operands reduced by the lowering
+            if (v.op >= D_FIRST_COMPLEX) {
+                fail(v.op == D_EXP ? "EXP with a symbolic exponent (interpreter only)"
+                     : v.op == D_MULMOD ? "MULMOD (interpreter only)"
+                                        : "complex op (interpreter only)");
+            }
             if (v.op >= D_UDIV_R && v.op <= D_SMOD_C) has_div = true;
         }
-        vbase_ = has_kec ? R_TEMP_KEC : has_div ? R_TEMP0 : R_TEMP_NODIV;
+        // without pinned columns v[R_COL0..R_DIV0) are free for temporaries (below the
+        // subroutines' registers only when no subroutine is called)
+        vbase_ = has_kec ? R_TEMP_KEC : has_div ? R_TEMP0 : n_pin ? R_TEMP_NODIV : R_COL0;
         vmax_ = std::min<uint32_t>(has_kec ? std::max(opt_.max_vgpr, opt_.max_vgpr_keccak)
-                                           : opt_.max_vgpr, 512);
+                                           : opt_.max_vgpr, 256);
         if (vmax_ <= vbase_ + 16) fail("VGPR budget too small");
-        vhigh_ = R_COL0 + 8 * n_vars_;
+        vhigh_ = R_COL0 + 8 * n_pin;
         vals_.assign(nv, Val());
         for (int c = 0; c < st_.n_pinned; ++c) {
             Val& v = vals_[c];
@@ -1581,6 +1750,11 @@ TapeCode Emitter::run() {
                 if (r >= 0) last_[r] = i;
         if (st_.root >= 0) last_[st_.root] = INT_MAX;
         demand();
+        // op_exp's products: one virtual register past the tape's, all limbs demanded
+        scratch_ = nv;
+        vals_.push_back(Val());
+        last_.push_back(-1);
+        dem_.push_back(0xFF);
         for (int i = 0; i < (int)code.size(); ++i) {
             const SsaInsn& v = code[i];
             const uint8_t op = v.op;
@@ -1596,6 +1770,18 @@ TapeCode Emitter::run() {
                     break;
                 }
                 case D_LOADC: vals_[v.d] = const_val(v.cidx); break;
+                case D_LOADVAR: {  // a column not pinned: the demanded limbs, one load each
+                    const uint32_t dm = dem_[v.d];
+                    Val& R = out(v.d);
+                    for (int k = 0; k < 8; ++k)
+                        if ((dm >> k) & 1u) {
+                            const uint32_t r = valloc();
+                            emit(M_LOADCOL, {V(r), IMM(8u * v.aux + (uint32_t)k)});
+                            R.l[k] = Limb::R(r);
+                        }
+                    if (dm) emit(M_S_WAITCNT_VM, {IMM(0)});
+                    break;
+                }
                 case D_TRUE: vals_[v.d] = bool_const(true); break;
                 case D_FALSE: vals_[v.d] = bool_const(false); break;
                 case D_ADD_R: op_addsub(v.d, val(v.a), Y(), false); break;
@@ -1637,6 +1823,8 @@ TapeCode Emitter::run() {
                     op_div(v.d, v.a, v.b, v.cidx, (uint32_t)(op - D_UDIV_R) >> 1, i);
                     break;
                 case D_KECCAK: op_keccak(v, i); break;
+                case D_EXP: op_exp(v.d, val(v.a), Y()); break;
+                case D_MULMOD: op_mulmod(v.d, val(v.a), val(v.b), val(v.c)); break;
                 default:
                     if (op >= D_SHR0 && op <= D_SHR7) {
                         const uint32_t s = 32u * (op - D_SHR0) + (v.aux & 31u);
@@ -2395,6 +2583,23 @@ std::string print(const MI& m, const std::string& prefix) {
         snprintf(b, sizeof b, "s_setpc_b64 s[%u:%u]", S_DIV_RA, S_DIV_RA + 1);
         return b;
     }
+    if (m.op == M_LOADCOL) {
+        char b[320];
+        const uint32_t j = m.o[1].v;
+        snprintf(b, sizeof b,
+                 "s_mul_i32 s28, s27, 0x%x\n"
+                 "s_mul_hi_u32 s29, s27, 0x%x\n"
+                 "s_add_u32 s28, s28, s4\n"
+                 "s_addc_u32 s29, s29, s5\n"
+                 "global_load_dword v%u, v2, s[28:29]",
+                 j, j, m.o[0].v);
+        return b;
+    }
+    if (m.op == M_S_WAITCNT_VM) {
+        char b[64];
+        snprintf(b, sizeof b, "s_waitcnt vmcnt(%u)", m.o[0].v);
+        return b;
+    }
     if (m.op == M_DS_WRITE2ST64 || m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32 ||
         m.op == M_S_WAITCNT_LGKM) {
         char b[128];
@@ -2436,6 +2641,7 @@ uint32_t code_bytes(const TapeCode& tc) {
     for (const MI& m : tc.code) {
         if (m.op == M_LABEL) continue;
         if (m.op == M_CALL_DIV || m.op == M_CALL_KEC) { b += 24; continue; }
+        if (m.op == M_LOADCOL) { b += 36; continue; }
         bool lit = false;
         for (const Opnd& o : m.o) lit |= o.k == O_IMM && !is_inline(o.v);
         const bool vop3 = m.e64 || m.op == M_V_OR3 || m.op == M_V_ALIGNBIT ||
@@ -2471,7 +2677,8 @@ void line(std::string& out, const char* fmt, ...) {
 //   s[36:37] jump-table address, s38 = group index.
 //   v0 = workitem id, v1 = lane, v2 = row offset in bytes, v3 = per-tape hit counts (lane t =
 //   the group's tape t), v4 = per-tape first hit + 1 (0 = none), v5..v7 atomics / stores,
-//   v[8:39] the assignment columns, v[40:79] the division subroutine, v80.. tape temporaries.
+//   v[8:39] the assignment columns (tape sets of <= 4 columns; above that the tape code loads
+//   the limbs it demands, M_LOADCOL), v[40:79] the division subroutine, v80.. tape temporaries.
 Module build_module(const std::vector<const TapeCode*>& codes,
                     const std::vector<uint32_t>& tape_ids, uint32_t n_vars, bool values,
                     uint32_t group_bytes) {
@@ -2493,7 +2700,8 @@ Module build_module(const std::vector<const TapeCode*>& codes,
         m.group_first.push_back(first);
         m.group_count.push_back((uint32_t)codes.size() - first);
     }
-    uint32_t maxv = R_COL0 + 8 * n_vars;
+    const uint32_t n_pin = pinned_cols(n_vars);
+    uint32_t maxv = R_COL0 + 8 * n_pin;
     bool any_div = false, any_lds = false, any_kec = false;
     for (const TapeCode* tc : codes) {
         maxv = std::max(maxv, tc->max_vgpr);
@@ -2589,14 +2797,14 @@ Module build_module(const std::vector<const TapeCode*>& codes,
         line(o, "v_min_u32 v2, s34, v2");
         line(o, "v_lshlrev_b32 v2, 2, v2");
         line(o, "s_mov_b64 s[28:29], s[4:5]");
-        for (uint32_t j = 0; j < 8 * n_vars; ++j) {
+        for (uint32_t j = 0; j < 8 * n_pin; ++j) {
             if (j) {
                 line(o, "s_add_u32 s28, s28, s27");
                 line(o, "s_addc_u32 s29, s29, 0");
             }
             line(o, "global_load_dword v%u, v2, s[28:29]", R_COL0 + j);
         }
-        line(o, "s_waitcnt vmcnt(0)");
+        if (n_pin) line(o, "s_waitcnt vmcnt(0)");
         for (uint32_t t = 0; t < gn; ++t) {
             const TapeCode& tc = *codes[g0 + t];
             char pre[64];
@@ -2760,7 +2968,7 @@ uint32_t default_group_bytes() {
 
 // VGPRs a code object holding tape `tc` allocates (build_module's rule for one tape).
 uint32_t module_vgprs(const TapeCode& tc, uint32_t n_vars) {
-    uint32_t v = std::max<uint32_t>(R_COL0 + 8 * n_vars, tc.max_vgpr);
+    uint32_t v = std::max<uint32_t>(R_COL0 + 8 * pinned_cols(n_vars), tc.max_vgpr);
     if (tc.calls_kec) v = std::max<uint32_t>(v, R_TEMP_KEC);
     if (tc.calls_div) v = std::max<uint32_t>(v, R_TEMP0);
     return (std::max<uint32_t>(v, 8) + 7) & ~7u;
@@ -2815,7 +3023,7 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
             SsaTape st;
             std::string e;
             if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts, n_consts,
-                               n_vars, pool, index, st, e, true) != MH_OK) {
+                               n_vars, pool, index, st, e, true, true) != MH_OK) {
                 stats.why[t] = "lowering: " + e;
                 continue;
             }

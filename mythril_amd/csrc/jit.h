@@ -81,6 +81,10 @@ enum Op : uint16_t {
     M_DS_READ2ST64,   // dst pair, addr, IMM offset0, IMM offset1 (units of 256 B)
     M_DS_READ_B32,    // dst, addr, IMM offset (bytes)
     M_S_WAITCNT_LGKM, // IMM count
+    // assignment columns that are not pinned (tape sets over 4 columns): limb j of this lane's
+    // row, loaded on use -- s[28:29] = assign + j * stride, global_load_dword dst, v2, s[28:29]
+    M_LOADCOL,        // dst, IMM j (= 8 * column + limb)
+    M_S_WAITCNT_VM,   // IMM count
     M_NUM_OPS
 };
 
@@ -90,6 +94,11 @@ struct MI {
     uint8_t tag = 0xFF;   // SSA op kind that emitted it (diagnostics; 0xFF = none)
     Opnd o[5];
 };
+
+// Assignment columns held in v[R_COL0..] for a whole chunk: every column of a tape set of at most
+// this many columns; none above it (the tape code loads the limbs it demands, M_LOADCOL).
+constexpr uint32_t kMaxPinnedCols = 4;
+inline uint32_t pinned_cols(uint32_t n_vars) { return n_vars <= kMaxPinnedCols ? n_vars : 0u; }
 
 // ---- register map of the generated kernel (documented in jit.cpp) ----------------------
 enum : uint32_t {
@@ -140,7 +149,8 @@ struct TapeCode {
 };
 
 struct Options {
-    uint32_t max_vgpr = 128;    // VGPR budget of the kernel (occupancy: 512 / max_vgpr waves)
+    uint32_t max_vgpr = 128;    // VGPR budget of the kernel (occupancy: 512 / max_vgpr waves per
+                                // SIMD, at most 8; 96..256 -- gfx950 has 256 architectural VGPRs)
     uint32_t max_vgpr_keccak = 168;  // ... of tapes that hash (the state holds 62 VGPRs)
     // Short-circuit conjunctions: a root AND chain is evaluated conjunct by conjunct (cheapest
     // and most selective first, schedule_conjuncts) and the wave leaves the tape as soon as no

@@ -205,6 +205,25 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
+CODEGEN_SOURCES = ("jit.cpp", "jit.h", "compile.cpp", "compile.h", "exec.h", "u256_ops.h",
+                   "dev_isa.h", "jit_comgr.cpp", "capi.cpp")
+
+
+def codegen_id() -> str:
+    """Identifier of the code the library generates: a hash of the sources that decide the
+    emitted machine code (the library is built from them in-tree).  Profiles that price this
+    code (profiles/pmc_summary.json, profiles/alg_work.json) record it, and bench.py uses a
+    profile only for the build it was taken on."""
+    import hashlib
+
+    h = hashlib.sha256()
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    for f in CODEGEN_SOURCES:
+        with open(os.path.join(d, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def gen_limb(seed: int, var: int, index: int, limb: int) -> int:
     return int(load().mh_gen_limb(seed, var, index, limb))
 

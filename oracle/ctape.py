@@ -86,11 +86,12 @@ def count(ts, seed: int, row_first: int, rows: int, threads: int = 0, tapes=None
 
 
 def benchmark(ts, seed: int, seconds: float = 15.0, tapes: int = 100,
-              short_circuit: bool = True):
+              short_circuit: bool = True, threads: int = 0):
     """Evals/s of this port on the host cores, on a bounded sample of the bench workload:
     the first `tapes` tapes over generated rows, rows grown until ~`seconds` of work.
-    short_circuit: the lazy evaluator (the scalar counterpart of the device's short circuit)."""
-    th = lib().ct_max_threads()
+    short_circuit: the lazy evaluator (the scalar counterpart of the device's short circuit).
+    threads: 0 = every host thread OpenMP offers, 1 = the single-core figure."""
+    th = threads or lib().ct_max_threads()
     tapes = min(tapes, len(ts.tapes))
     rows = 256
     while True:

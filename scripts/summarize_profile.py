@@ -94,6 +94,7 @@ def main(tag: str) -> None:
                   / per_kernel[k]["dispatches"] for k in per_kernel)
     summary = {
         "tag": tag,
+        "codegen_id": (pmc_bench or bench).get("build"),
         "tapes": (pmc_bench or bench)["config"]["tapes"],
         "rows_per_gpu": (pmc_bench or bench)["config"]["rows_per_gpu"],
         "hbm_bytes_per_launch": sum(v["fetch_bytes_per_launch"] + v["write_bytes_per_launch"]

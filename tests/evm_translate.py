@@ -229,10 +229,12 @@ def final_storage(pre: Dict[int, int], pairs, values) -> Dict[int, int]:
     return {k: v for k, v in st.items() if v != 0}
 
 
-def lift_constants(ts):
+def lift_constants(ts, keep_exponents=False):
     """The same tapes with every constant leaf turned into an assignment column holding that
     constant (one row), so the compiler cannot fold them: the device evaluates every op of a
-    VMTest on registers.  Returns (lifted tapeset, soa [n_cols, 8, 1] u32)."""
+    VMTest on registers.  keep_exponents leaves the exponents of EVM_EXP constant (LASER only
+    builds EXP over constants, instructions.py:599-631; the native code takes a constant
+    exponent).  Returns (lifted tapeset, soa [n_cols, 8, 1] u32)."""
     import numpy as np
 
     from mythril_amd.tape import Op, Tape, TapeSet
@@ -241,8 +243,11 @@ def lift_constants(ts):
     out = TapeSet()
     for t in ts.tapes:
         nodes = t.nodes.copy()
+        keep = set()
+        if keep_exponents:
+            keep = {int(n["b"]) for n in nodes if int(n["op"]) == int(Op.EVM_EXP)}
         for i in range(len(nodes)):
-            if int(nodes[i]["op"]) == int(Op.CONST):
+            if int(nodes[i]["op"]) == int(Op.CONST) and i not in keep:
                 w = int(nodes[i]["width"])
                 v = ts.pool.values[int(nodes[i]["imm0"])] & ((1 << w) - 1)
                 name = "k%d_%x" % (w, v)
@@ -253,9 +258,43 @@ def lift_constants(ts):
                 nodes[i]["imm0"] = out.var_index[name]
                 nodes[i]["imm1"] = 0
         out.tapes.append(Tape(nodes))
+    if keep_exponents:
+        out.pool = ts.pool
     soa = np.zeros((max(out.n_vars, 1), 8, 1), dtype=np.uint32)
     for name, v in cols.items():
         c = out.var_index[name]
         for k in range(8):
             soa[c, k, 0] = (v >> (32 * k)) & 0xFFFFFFFF
     return out, soa
+
+
+def vmtest_batch(vectors, mode: str, lifted: bool):
+    """Every translatable vector's tapes in ONE tape set (one JIT build for the whole corpus):
+    (tapeset, soa [n_cols, 8, 1], [(name, first tape, pairs, expected, pre)]).  Constants are
+    re-pooled; lifted turns every constant leaf into a column (lift_constants) shared by value."""
+    import numpy as np
+
+    from mythril_amd.tape import Op, Tape, TapeSet
+
+    out = TapeSet()
+    index = []
+    for vec in vectors:
+        try:
+            ts, pairs, expected, pre = vmtest_tapes(vec, mode)
+        except Unsupported:
+            continue
+        index.append((vec["name"], len(out.tapes), pairs, expected, pre))
+        for t in ts.tapes:
+            nodes = t.nodes.copy()
+            for i in range(len(nodes)):
+                if int(nodes[i]["op"]) == int(Op.CONST):
+                    nodes[i]["imm0"] = out.pool.add(ts.pool.values[int(nodes[i]["imm0"])])
+                elif int(nodes[i]["op"]) == int(Op.VAR):
+                    raise ValueError("VMTest tapes are concrete")
+            out.tapes.append(Tape(nodes))
+    if lifted:
+        out, soa = lift_constants(out)
+    else:
+        soa = np.zeros((1, 8, 1), dtype=np.uint32)
+    return out, soa, index
+

@@ -107,7 +107,12 @@ class TapeFuzzer:
             wa = rng.randrange(1, w)
             return b.op(Op.ZEXT if c == "zext" else Op.SEXT, self.bv(wa, d), imm0=w - wa)
         if c == "evm":
-            op = rng.choice([Op.EVM_SIGNEXTEND, Op.EVM_BYTE, Op.EVM_EXP])
+            op = rng.choice([Op.EVM_SIGNEXTEND, Op.EVM_BYTE, Op.EVM_EXP, Op.EVM_ADDMOD,
+                             Op.EVM_MULMOD])
+            if op in (Op.EVM_ADDMOD, Op.EVM_MULMOD):
+                n = self.bv(w, d) if rng.random() < 0.6 else b.const(
+                    rng.choice([0, 1, 7, (1 << 255) + 3, (1 << 256) - 1, rng.getrandbits(100)]), 256)
+                return b.op(op, self.bv(w, d), self.bv(w, d), n, imm0=rng.choice([0, 1]))
             if op == Op.EVM_EXP:
                 e = b.const(rng.choice([0, 1, 2, 3, 255, 256, rng.getrandbits(16)]), 256)
                 return b.op(op, self.bv(w, d), e if rng.random() < 0.7 else self.bv(w, d))

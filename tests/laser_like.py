@@ -174,3 +174,50 @@ def queries():
     out.append(("unsat_actor", [sender_is_actor(sender), sender == symbol_factory.BitVecVal(5,
                                                                                             256)]))
     return ctx, out
+
+
+def hard_queries():
+    """UNSAT variants of the largest SAT shapes: each adds a conjunct that contradicts the path
+    condition in a way constant folding cannot see, so the sieve runs every round and misses
+    (what an infeasible JUMPI branch costs LASER on top of z3, svm.py:257-262)."""
+    ctx, qs = queries()
+    d = dict(qs)
+    out = []
+    # KillBilly: the third transaction's sender is both ATTACKER and CREATOR
+    sender3 = symbol_factory.BitVecSym("sender_3", 256)
+    out.append(("killbilly_unsat", d["killbilly"] + [sender3 == symbol_factory.BitVecVal(
+        CREATOR, 256)]))
+    # transfer overflow of two words that are both below 2^128
+    cd = Calldata("1")
+    lim = symbol_factory.BitVecVal(1 << 128, 256)
+    out.append(("overflow_unsat", d["overflow"] + [ULT(cd.word(4), lim), ULT(cd.word(36), lim)]))
+    # storage slot 0 holds the sender (or a zero value when the key word is 0) and must be the
+    # attacker, while the sender is not and the value is zero
+    sender = symbol_factory.BitVecSym("sender_1", 256)
+    value = symbol_factory.BitVecSym("call_value1", 256)
+    out.append(("k_storage_unsat", d["k_storage"] + [
+        Not(sender == symbol_factory.BitVecVal(ATTACKER, 256)),
+        value == symbol_factory.BitVecVal(0, 256)]))
+    return ctx, out
+
+
+def query_tapeset(b, constraints):
+    """The tape set the sieve builds for one query (Sieve.solve's steps 1-3): lowered root,
+    schema, one tape per variable-disjoint bucket, and the harvested guide."""
+    from mythril_amd.candidates import build_guide
+    from mythril_amd.lower import lower_query
+    from mythril_amd.sieve import Sieve, local_tape
+    from mythril_amd.tape import Op, Tape, TapeSet
+
+    root, schema = lower_query(b, [c.node for c in constraints])
+    cols = list(schema.columns)
+    ts = TapeSet(cols)
+    ts.pool = b.pool
+    for conj, _ in Sieve.buckets(b, root):
+        acc = conj[0]
+        for x in conj[1:]:
+            acc = b.op(Op.AND, acc, x)
+        ts.tapes.append(Tape(local_tape(b, acc, cols)))
+    guide = build_guide(b, root, schema, cols, None).arrays()
+    return ts, schema, guide
+

@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -89,6 +90,8 @@ struct Counts {
     double alive_valu = 0;  // VALU weighted by the fraction of lanes still alive (compaction bound)
 } g_counts;
 uint64_t g_alive = ~0ull;  // lanes that satisfy every conjunct tested so far (short circuit)
+const uint32_t* g_mem = nullptr;  // "global memory": the SoA assignment buffer at address 0
+uint64_t g_mem_words = 0;
 uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
 // executed VALU by the SSA op kind that emitted it: [tag] body, [256 + tag] inside the division
 // subroutine called by that op (tag 255 = prologue / untagged)
@@ -379,7 +382,21 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 }
                 break;
             }
-            case M_S_WAITCNT_LGKM: break;
+            case M_S_WAITCNT_LGKM: case M_S_WAITCNT_VM: break;
+            case M_LOADCOL: {
+                // the kernel's address arithmetic: s[28:29] = s[4:5] + j * s27, then
+                // global_load_dword dst, v2, s[28:29] (v2 = the lane's row * 4)
+                const uint64_t base = (uint64_t)w.s[4] | ((uint64_t)w.s[5] << 32);
+                const uint64_t addr = base + (uint64_t)o[1].v * w.s[27];
+                w.s[28] = (uint32_t)addr;
+                w.s[29] = (uint32_t)(addr >> 32);
+                for (int l = 0; l < 64; ++l) {
+                    const uint64_t byte = addr + w.v[2][l];
+                    if ((byte & 3) || byte / 4 >= g_mem_words) throw Err{"emulator: global address"};
+                    w.v[o[0].v][l] = g_mem[byte / 4];
+                }
+                break;
+            }
             default: throw Err{"emulator: unknown op " + std::to_string(m.op)};
         }
     }
@@ -396,7 +413,7 @@ bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes
     std::string err;
     if (tape >= n_tapes) { e = "tape index"; return false; }
     if (lower_tape_ssa(nodes + offs[tape], (size_t)(offs[tape + 1] - offs[tape]), consts,
-                       n_consts, n_vars, pool, index, st, err, true) != MH_OK) {
+                       n_consts, n_vars, pool, index, st, err, true, true) != MH_OK) {
         e = "lowering: " + err;
         return false;
     }
@@ -461,12 +478,20 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
             for (uint32_t wd = 0; wd < LDS_WORDS; ++wd)
                 if (wd < LDS_D || wd >= LDS_D + 8)
                     for (int l = 0; l < 64; ++l) w.lds[wd * 64 + l] = 0;
-            for (uint32_t c = 0; c < n_vars; ++c)
+            for (uint32_t c = 0; c < pinned_cols(n_vars); ++c)
                 for (int k = 0; k < 8; ++k)
                     for (int l = 0; l < 64; ++l) {
                         const uint64_t row = base + (uint64_t)l < rows ? base + (uint64_t)l : 0;
                         w.v[R_COL0 + 8 * c + k][l] = assign[((uint64_t)c * 8 + k) * rows + row];
                     }
+            // the chunk loop's state the tape code reads: v2 = clamped row * 4, s[4:5] = the
+            // buffer (address 0 here), s27 = column stride in bytes
+            for (int l = 0; l < 64; ++l)
+                w.v[2][l] = 4u * (uint32_t)std::min<uint64_t>(base + (uint64_t)l, rows - 1);
+            w.s[4] = w.s[5] = 0;
+            w.s[27] = (uint32_t)(4 * rows);
+            g_mem = assign;
+            g_mem_words = (uint64_t)n_vars * 8 * rows;
             g_alive = (uint64_t)w.s[S_VALID] | ((uint64_t)w.s[S_VALID + 1] << 32);
             run(w, tc.code, div);
             ++chunks;
@@ -516,7 +541,7 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
         SsaTape st;
         std::string e;
         if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts, n_consts,
-                           n_vars, pool, index, st, e, true) != MH_OK)
+                           n_vars, pool, index, st, e, true, true) != MH_OK)
             continue;
         codes[t] = emit_tape(st, pool, n_vars, opt);
         if (codes[t].ok) {

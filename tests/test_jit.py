@@ -12,13 +12,14 @@ import pytest
 from mythril_amd import synth
 from mythril_amd.tape import Op, TapeSet
 from oracle import smt_eval
-from tests.emu import jit_build, jit_eval, jit_module, set_short_circuit
-from tests.evm_translate import Unsupported, lift_constants, vmtest_tapes
+from tests.emu import EmuError, jit_build, jit_eval, jit_module, set_short_circuit
+from tests.evm_translate import Unsupported, final_storage, lift_constants, vmtest_tapes
 from tests.fuzz import TapeFuzzer, assignment_soa, soa_row
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 VMTESTS = json.load(open(os.path.join(HERE, "golden", "vmtests.json")))
 EIP145 = json.load(open(os.path.join(HERE, "golden", "eip145.json")))
+LASER_DIVERGENT = {"addmodDivByZero", "addmodDivByZero1", "addmodDivByZero2", "mulmoddivByZero"}
 
 
 def soa_of(rows_vals, n_vars):
@@ -55,6 +56,29 @@ def test_fuzz_tapes_jit(emu, seed):
     soa = assignment_soa(rng, ts.n_vars, 70)
     n = check_tapes(emu, ts, soa, require_all=False)
     assert n >= 12
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzz_wide_schema_jit(emu, seed):
+    """Random tapes over 7 columns (tape sets over 4 columns: the code loads each demanded limb
+    from the SoA buffer instead of pinning the columns), every op including the EVM word ops,
+    ADDMOD / MULMOD and the overflow predicates: all jitted (retried at 168 VGPRs like
+    mh_tapes_jit), values equal to the oracle's on every row."""
+    rng = random.Random(7100 + seed)
+    ts = TapeSet()
+    fz = TapeFuzzer(rng, ts, n_vars=7, max_depth=4, allow_keccak=seed % 2 == 1)
+    for _ in range(16):
+        fz.tape()
+    soa = assignment_soa(rng, ts.n_vars, 70)
+    for i, t in enumerate(ts.tapes):
+        why, budget = jit_refusal(emu, ts, i, soa)
+        assert why is None or "larger than 96 KB" in why, (i, why)
+        if why:
+            continue
+        res = jit_eval(emu, ts, i, soa, budget)
+        for r in range(soa.shape[2]):
+            want = int(smt_eval.evaluate(t.nodes, ts.pool.values, soa_row(soa, r)))
+            assert res.values[r] == want, (i, r, hex(res.values[r]), hex(want))
 
 
 def test_synthetic_tapes_jit(emu):
@@ -242,26 +266,64 @@ def test_eip145_jit(emu, op):
     assert res.values == [int(v["expected"], 16) for v in EIP145[op]]
 
 
-def test_vmtests_lifted_jit(emu):
-    """The reference's VMTests known answers with every constant lifted into a column: each op
-    of each vector runs as JIT code (vectors with > 4 columns or 512-bit arithmetic excepted)."""
-    checked = 0
+# Why the native code may refuse a VMTest tape: none is expected (the tests below assert every
+# tape is jitted); a refusal would have to name one of these.
+JIT_REFUSALS = ()
+
+
+def jit_refusal(emu, ts, i, soa):
+    """(None, max_vgpr) when tape i is jitted, else (the refusal text, None).  A tape over the
+    128-VGPR budget is retried at 168, as mh_tapes_jit does (its own occupancy class)."""
+    for budget in (128, 168):
+        try:
+            res = jit_eval(emu, ts, i, soa, budget)
+        except EmuError as e:
+            if "lowering:" not in str(e):
+                raise
+            return str(e), None
+        if res.ok:
+            return None, budget
+        if "VGPR pressure" not in res.why:
+            break
+    return res.why, None
+
+
+@pytest.mark.parametrize("mode", ["laser", "evm"])
+@pytest.mark.parametrize("keep_exp", [False, True])
+def test_vmtests_lifted_jit(emu, mode, keep_exp):
+    """The reference's VMTests known answers with every constant lifted into a column (so no op
+    folds on the host; keep_exp: EXP exponents stay constant): each op of each vector runs as
+    JIT code, tape sets over 4 columns loading the limbs each use demands.  Every refusal is one
+    of JIT_REFUSALS; the storage the jitted tapes produce is the vector's post-state whenever
+    every tape of the vector is jitted."""
+    checked, full, refused = 0, 0, {}
     for vec in VMTESTS:
         try:
-            ts, pairs, expected, pre = vmtest_tapes(vec, "laser")
+            ts, pairs, expected, pre = vmtest_tapes(vec, mode)
         except Unsupported:
             continue
-        lts, soa = lift_constants(ts)
-        if lts.n_vars > 4:
-            continue
+        lts, soa = lift_constants(ts, keep_exponents=keep_exp)
+        vals, complete = [], True
         for i, t in enumerate(ts.tapes):
-            res = jit_eval(emu, lts, i, soa)
-            if not res.ok:
-                continue
+            why, budget = jit_refusal(emu, lts, i, soa)
             want = int(smt_eval.evaluate(t.nodes, ts.pool.values, []))
-            assert res.values[0] == want, (vec["name"], i)
+            if why is not None:
+                assert any(r in why for r in JIT_REFUSALS), (vec["name"], i, why)
+                refused.setdefault(why.split("(")[0].split(":")[-1].strip(), []).append(vec["name"])
+                complete = False
+                vals.append(want)
+                continue
+            got = jit_eval(emu, lts, i, soa, budget).values[0]
+            assert got == want, (vec["name"], i, hex(got), hex(want))
+            vals.append(got)
             checked += 1
-    assert checked >= 100
+        if complete:
+            full += 1
+            if not (mode == "laser" and vec["name"] in LASER_DIVERGENT):
+                assert final_storage(pre, pairs, vals) == expected, vec["name"]
+    print("%s: %d tapes jitted, %d vectors fully native, refused: %s" % (
+        mode, checked, full, {k: len(set(v)) for k, v in refused.items()}))
+    assert not refused and checked >= 1350 and full >= 340
 
 
 def test_module_assembles(emu):
@@ -437,3 +499,29 @@ def test_short_circuit_constant_conjuncts_jit(emu):
             assert check_tapes(emu, ts, soa) == len(ts.tapes)
         finally:
             set_short_circuit(emu, True)
+
+
+def test_laser_query_tapes_jit(emu):
+    """The sieve's tape sets for the LASER-shaped queries (tests/laser_like.py, SAT and the UNSAT
+    hard variants; 1..109 columns, so most load their limbs on use) through the JIT's code on
+    guided rows (oracle/guided_gen.py, the device generator's restatement): every tape jitted,
+    values equal to the oracle's on every row."""
+    from oracle.guided_gen import generate_row
+    from tests.laser_like import hard_queries, queries, query_tapeset
+
+    n = 0
+    for maker in (queries, hard_queries):
+        ctx, qs = maker()
+        for name, cs in qs:
+            ts, schema, guide = query_tapeset(ctx.b, cs)
+            rows = [generate_row(0xC0FFEE, g, guide) for g in range(96)]
+            soa = soa_of(rows, max(ts.n_vars, 1))
+            for i, t in enumerate(ts.tapes):
+                why, budget = jit_refusal(emu, ts, i, soa)
+                assert why is None, (name, i, why)
+                res = jit_eval(emu, ts, i, soa, budget)
+                for r in range(len(rows)):
+                    want = int(smt_eval.evaluate(t.nodes, ts.pool.values, rows[r]))
+                    assert res.values[r] == want, (name, i, r)
+                n += 1
+    assert n >= 30
