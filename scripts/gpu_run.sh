@@ -1,0 +1,34 @@
+#!/bin/bash
+# One GPU session on the box (run via gpurun from the repo root):
+#   gpurun -- bash scripts/gpu_run.sh <tag> <step>...
+# steps (each under its own time limit, stopping at the first failure):
+#   native    tests/test_gpu_native.py (native code on the reference vectors, query shapes, 2^26)
+#   gpu       the whole -m gpu suite
+#   smoke     __graft_entry__.smoke()
+#   bench     default bench.py (N=1)
+#   miss      scripts/miss_cost.py (per-stage cost of sieve misses, JIT build vs interpreter)
+#   counters  rocprofv3 -L (the PMC counters this box offers)
+#   profile   scripts/profile.sh <tag> (kernel trace + PMC passes of the default bench)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    native)   timeout -k 10 1000 $PYT tests/test_gpu_native.py > "$OUT/pytest_native.txt" 2>&1 ;;
+    gpu)      timeout -k 10 1100 $PYT -m gpu tests > "$OUT/pytest_gpu.txt" 2>&1 ;;
+    smoke)    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 ;;
+    bench)    timeout -k 10 600 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.log" ;;
+    miss)     timeout -k 10 400 python -u scripts/miss_cost.py 5 > "$OUT/miss_cost.jsonl" 2> "$OUT/miss_cost.log" ;;
+    counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 ;;
+    profile)  bash scripts/profile.sh "$TAG" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  echo "== $step rc=$rc $(date +%T)"
+  [ $rc -eq 0 ] || exit $rc
+done
