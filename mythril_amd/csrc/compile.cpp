@@ -924,7 +924,7 @@ bool bool_result(uint8_t op) {
 // before any solver sees them (laser/smt/bitvec.py, `simplify` calls); nodes whose value does not
 // depend on the assignment are not counted as per-evaluation work (compile_tape's alg_ops).
 // Returns the root's register after aliasing; recomputes the feature bits.
-int fold_constants(Lowering& L, int root_v, bool value_numbering) {
+int fold_constants(Lowering& L, int root_v, int value_numbering) {
     std::vector<VInsn>& code = L.code;
     const int nv = L.n_vregs;
     std::vector<char> known(nv, 0);
@@ -948,7 +948,7 @@ int fold_constants(Lowering& L, int root_v, bool value_numbering) {
         v.a = R(v.a);
         v.b = R(v.b);
         v.c = R(v.c);
-        if (value_numbering) {
+        if (value_numbering && !(value_numbering == kVnNoLoads && v.op == D_LOADVAR)) {
             const int key[8] = {v.op, v.a, v.b, v.c, (int)v.width, (int)v.aux, v.cidx,
                                 (int)v.w1raw};
             std::string k(reinterpret_cast<const char*>(key), sizeof(key));
@@ -1180,7 +1180,7 @@ void rewrite_wide_modops(std::vector<mh_node>& t) {
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,
-                       std::string& err, bool value_numbering, bool jit_forms) {
+                       std::string& err, int value_numbering, bool jit_forms) {
     if (n_nodes == 0) {
         err = "empty tape";
         return MH_E_INVALID;

@@ -46,14 +46,17 @@ struct SsaTape {
 
 // Lower one tape to SSA, fold constants and drop dead code (compile_tape's first half).
 // value_numbering merges identical instructions (the native code's register file has room for
-// the longer live ranges; the interpreter's does not).  jit_forms restates the complex ops the
+// the longer live ranges; the interpreter's does not); kVnNoLoads merges all but the column loads
+// (D_LOADVAR: every use loads again, the native code's fallback under register pressure).
+// jit_forms restates the complex ops the
 // native code has no machine code for (EVM SIGNEXTEND / BYTE / ADDMOD, EXP by a constant, the
 // overflow predicates) on ops it has; the columns of a tape set over MH_MAX_PRELOAD columns stay
 // D_LOADVAR (the native code loads the limbs each use demands).
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& out,
-                       std::string& err, bool value_numbering = false, bool jit_forms = false);
+                       std::string& err, int value_numbering = 0, bool jit_forms = false);
+constexpr int kVnAll = 1, kVnNoLoads = 2;
 
 // Bool values of the SSA registers `want` on n_rows sample rows (each pinned column a uniform
 // 256-bit value from a splitmix64 stream seeded by `seed`), by the device's own instruction

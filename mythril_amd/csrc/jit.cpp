@@ -3028,6 +3028,16 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                 continue;
             }
             TapeCode tc = emit_tape(st, pool, n_vars, o);
+            if (!tc.ok && !keep_over && pinned_cols(n_vars) == 0 &&
+                tc.why.find("VGPR pressure") != std::string::npos) {
+                // still over the larger budget: every column use loads again instead of one
+                // load kept live across the tape
+                SsaTape st2;
+                if (lower_tape_ssa(nodes + offs[t], (size_t)(offs[t + 1] - offs[t]), consts,
+                                   n_consts, n_vars, pool, index, st2, e, kVnNoLoads,
+                                   true) == MH_OK)
+                    tc = emit_tape(st2, pool, n_vars, o);
+            }
             if (tc.ok && code_bytes(tc) > 96 * 1024) {
                 tc.ok = false;
                 tc.why = "tape code larger than 96 KB";

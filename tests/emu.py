@@ -129,6 +129,13 @@ def set_short_circuit(emu: "Emulator", on: bool) -> None:
     f(int(on))
 
 
+def set_value_numbering(emu: "Emulator", vn: int) -> None:
+    """Value numbering of the emulator's lowering: 1 all (default), 2 all but the column loads
+    (mh_tapes_jit's last retry under register pressure)."""
+    f = _jit_fn(emu.lib, "emu_jit_set_vn", None, [C.c_int])
+    f(int(vn))
+
+
 def jit_module(emu: "Emulator", ts: TapeSet, values: bool = False, max_vgpr: int = 128,
                assemble: bool = True):
     """(module text, code object bytes, tapes jitted) for a whole tape set."""

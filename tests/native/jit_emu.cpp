@@ -403,6 +403,7 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
 }
 
 bool g_short_circuit = true;  // Options::short_circuit of the emulated builds
+int g_vn = kVnAll;            // value numbering of the emulated lowering (build_tapeset's retry)
 uint32_t g_sample_rows = Options().sample_rows;
 
 bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
@@ -413,7 +414,7 @@ bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes
     std::string err;
     if (tape >= n_tapes) { e = "tape index"; return false; }
     if (lower_tape_ssa(nodes + offs[tape], (size_t)(offs[tape + 1] - offs[tape]), consts,
-                       n_consts, n_vars, pool, index, st, err, true, true) != MH_OK) {
+                       n_consts, n_vars, pool, index, st, err, g_vn, true) != MH_OK) {
         e = "lowering: " + err;
         return false;
     }
@@ -570,6 +571,7 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
 }
 
 extern "C" void emu_jit_set_short_circuit(int on) { g_short_circuit = on != 0; }
+extern "C" void emu_jit_set_vn(int vn) { g_vn = vn; }
 extern "C" void emu_jit_set_sample_rows(uint32_t n) { g_sample_rows = n; }
 
 extern "C" void emu_jit_op_stats(uint64_t* valu, uint64_t* wide, uint64_t* count, int reset) {

@@ -12,7 +12,8 @@ import pytest
 from mythril_amd import synth
 from mythril_amd.tape import Op, TapeSet
 from oracle import smt_eval
-from tests.emu import EmuError, jit_build, jit_eval, jit_module, set_short_circuit
+from tests.emu import (EmuError, jit_build, jit_eval, jit_module, set_short_circuit,
+                       set_value_numbering)
 from tests.evm_translate import Unsupported, final_storage, lift_constants, vmtest_tapes
 from tests.fuzz import TapeFuzzer, assignment_soa, soa_row
 
@@ -75,7 +76,7 @@ def test_fuzz_wide_schema_jit(emu, seed):
         assert why is None or "larger than 96 KB" in why, (i, why)
         if why:
             continue
-        res = jit_eval(emu, ts, i, soa, budget)
+        res = jit_run(emu, ts, i, soa, budget)
         for r in range(soa.shape[2]):
             want = int(smt_eval.evaluate(t.nodes, ts.pool.values, soa_row(soa, r)))
             assert res.values[r] == want, (i, r, hex(res.values[r]), hex(want))
@@ -272,20 +273,34 @@ JIT_REFUSALS = ()
 
 
 def jit_refusal(emu, ts, i, soa):
-    """(None, max_vgpr) when tape i is jitted, else (the refusal text, None).  A tape over the
-    128-VGPR budget is retried at 168, as mh_tapes_jit does (its own occupancy class)."""
-    for budget in (128, 168):
+    """(None, (max_vgpr, value numbering)) when tape i is jitted, else (the refusal text, None).
+    As mh_tapes_jit: a tape over the 128-VGPR budget is retried at 168 (its own occupancy
+    class), and one still over it, in a tape set whose columns load on use, with a load per use."""
+    tries = [(128, 1), (168, 1)] + ([(168, 2)] if ts.n_vars > 4 else [])
+    for budget, vn in tries:
+        set_value_numbering(emu, vn)
         try:
             res = jit_eval(emu, ts, i, soa, budget)
         except EmuError as e:
             if "lowering:" not in str(e):
                 raise
             return str(e), None
+        finally:
+            set_value_numbering(emu, 1)
         if res.ok:
-            return None, budget
+            return None, (budget, vn)
         if "VGPR pressure" not in res.why:
             break
     return res.why, None
+
+
+def jit_run(emu, ts, i, soa, how):
+    """jit_eval at the (budget, value numbering) jit_refusal found."""
+    set_value_numbering(emu, how[1])
+    try:
+        return jit_eval(emu, ts, i, soa, how[0])
+    finally:
+        set_value_numbering(emu, 1)
 
 
 @pytest.mark.parametrize("mode", ["laser", "evm"])
@@ -313,7 +328,7 @@ def test_vmtests_lifted_jit(emu, mode, keep_exp):
                 complete = False
                 vals.append(want)
                 continue
-            got = jit_eval(emu, lts, i, soa, budget).values[0]
+            got = jit_run(emu, lts, i, soa, budget).values[0]
             assert got == want, (vec["name"], i, hex(got), hex(want))
             vals.append(got)
             checked += 1
@@ -519,9 +534,25 @@ def test_laser_query_tapes_jit(emu):
             for i, t in enumerate(ts.tapes):
                 why, budget = jit_refusal(emu, ts, i, soa)
                 assert why is None, (name, i, why)
-                res = jit_eval(emu, ts, i, soa, budget)
+                res = jit_run(emu, ts, i, soa, budget)
                 for r in range(len(rows)):
                     want = int(smt_eval.evaluate(t.nodes, ts.pool.values, rows[r]))
                     assert res.values[r] == want, (name, i, r)
                 n += 1
     assert n >= 30
+
+
+@pytest.mark.parametrize("mode", ["laser", "evm"])
+def test_vmtest_batch_jit(emu, mode):
+    """The corpus as tests/test_gpu_native.py hands it to mh_tapes_jit: every vector's tapes in
+    one tape set over the shared lifted columns (about 100, all loaded on use).  Every tape is
+    jitted (with mh_tapes_jit's retries) and its value is the oracle's."""
+    from tests.evm_translate import vmtest_batch
+
+    ts, soa, index = vmtest_batch(VMTESTS, mode, True)
+    row = soa_row(soa, 0)
+    for i, t in enumerate(ts.tapes):
+        why, how = jit_refusal(emu, ts, i, soa)
+        assert why is None, (i, why)
+        got = jit_run(emu, ts, i, soa, how).values[0]
+        assert got == int(smt_eval.evaluate(t.nodes, ts.pool.values, row)), i
