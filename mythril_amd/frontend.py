@@ -29,6 +29,7 @@ reports must stay z3 Optimize output, analysis/solver.py:48-96).
 """
 from __future__ import annotations
 
+import inspect
 import logging
 import threading
 import time
@@ -43,7 +44,9 @@ log = logging.getLogger(__name__)
 _tls = threading.local()
 _config = {
     "fallback": None,   # callable(constraints, minimize, maximize, enforce_execution_time)
-    "verify": None,     # callable(constraints, model) -> bool (z3 re-verification)
+    "verify": None,     # callable(constraints, model[, timeout_ms=...]) -> bool (z3 re-check);
+                        # timeout_ms (what is left of get_model's budget) is passed only to a
+                        # verifier that declares it (or **kwargs)
     "to_terms": None,   # callable(constraints) -> (smt.Context, [Bool]) for foreign terms
     "log_writer": None,  # callable(constraints, minimize, maximize) -> SMT-LIB2 text (foreign)
     "fallback_logs": False,  # the fallback writes --solver-log files itself (the reference's)
@@ -75,6 +78,20 @@ def configure(*, fallback: Optional[Callable] = None, verify: Optional[Callable]
     get_model.cache_clear()
 
 
+def _takes_timeout(fn) -> bool:
+    try:
+        ps = inspect.signature(fn).parameters.values()
+    except (TypeError, ValueError):
+        return False
+    return any(p.name == "timeout_ms" or p.kind == p.VAR_KEYWORD for p in ps)
+
+
+def _verify(verify, constraints, m, left) -> bool:
+    if _takes_timeout(verify):
+        return bool(verify(constraints, m, timeout_ms=left))
+    return bool(verify(constraints, m))
+
+
 def reset() -> None:
     """Back to defaults (tests, plugin stop)."""
     _config.update(fallback=None, verify=None, to_terms=None, log_writer=None,
@@ -84,12 +101,23 @@ def reset() -> None:
 
 
 def sieve():
-    """This thread's sieve (device context + buffers), created on first use."""
+    """This thread's sieve (device context + buffers), created on first use.  A failure to
+    create it (no library, no gfx950 device) is remembered: later queries go straight to the
+    fallback without importing their terms or probing the device again, until the sieve is
+    reconfigured (configure with sieve options, reset)."""
     s = getattr(_tls, "sieve", None)
     if s is None:
+        failed = getattr(_tls, "sieve_failed", None)
+        if failed is not None:
+            raise failed
         from .sieve import Sieve
 
-        s = _tls.sieve = Sieve(**_config["sieve_kwargs"])
+        try:
+            s = _tls.sieve = Sieve(**_config["sieve_kwargs"])
+        except Exception as e:
+            _tls.sieve_failed = e
+            log.warning("constraint sieve unavailable, every query goes to the fallback: %s", e)
+            raise
     return s
 
 
@@ -106,6 +134,7 @@ def close_sieve() -> None:
     if s is not None:
         s.close()
         _tls.sieve = None
+    _tls.sieve_failed = None
 
 
 def _log_query(constraints, minimize, maximize) -> None:
@@ -160,8 +189,8 @@ def sieve_model(constraints, timeout_ms: Optional[float] = None):
     stats = SolverStatistics()
     t0 = time.perf_counter()
     try:
+        s = sieve()  # first: an unusable device skips the term import
         ctx, terms = _terms(constraints)
-        s = sieve()
         key = tuple(t.node for t in terms)
         budget = None if timeout_ms is None else max(timeout_ms, 0.0) / 1000.0
         w = s.solve(ctx.b, [t.node for t in terms], key=key, budget_s=budget)
@@ -184,7 +213,7 @@ def sieve_model(constraints, timeout_ms: Optional[float] = None):
         left = None if timeout_ms is None else timeout_ms - 1000.0 * (time.perf_counter() - t0)
         try:
             ok = left is None or left > 0
-            ok = ok and verify(constraints, m, timeout_ms=left)
+            ok = ok and _verify(verify, constraints, m, left)
         except Exception as e:  # noqa: BLE001 - a failing verifier rejects
             log.debug("sieve witness verifier error: %s", e)
             ok = False
