@@ -438,10 +438,10 @@ int32_t mh_ctx_destroy(mh_ctx* ctx) {
 int32_t mh_ctx_set_stream(mh_ctx* ctx, void* hip_stream) {
     if (!ctx) return set_err(MH_E_INVALID, "null ctx");
     if (int32_t r = use_device(ctx)) return r;
-    if (ctx->own_stream && ctx->stream) {
-        MH_HIP(hipStreamSynchronize(ctx->stream));
-        MH_HIP(hipStreamDestroy(ctx->stream));
-    }
+    // uploads queued on the current stream (tape sets, guides: asynchronous copies from pinned
+    // staging) must land before anything on the new stream reads them
+    MH_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->own_stream && ctx->stream) MH_HIP(hipStreamDestroy(ctx->stream));
     ctx->stream = (hipStream_t)hip_stream;  // NULL = the device's null stream
     ctx->own_stream = false;
     return MH_OK;

@@ -45,3 +45,26 @@ def test_version_and_errors_without_device():
 def test_generator_restatement_matches_library():
     for seed, var, idx, limb in [(0, 0, 0, 0), (1, 2, 3, 4), (0xDEADBEEF, 3, 1 << 40, 7)]:
         assert native.gen_limb(seed, var, idx, limb) == smt_eval.gen_limb(seed, var, idx, limb)
+
+
+def test_comm_argument_validation_without_device():
+    """mh_comm_* (the library's RCCL exchange) refuse bad arguments with
+    MH_E_INVALID before touching RCCL or a device, and never abort the process."""
+    lib = native.load()
+    uid = (C.c_uint8 * 128)()
+    assert lib.mh_comm_init(None, uid, 0, 1) == native.MH_E_INVALID
+    assert b"null" in lib.mh_last_error()
+    assert lib.mh_comm_unique_id(None) == native.MH_E_INVALID
+    assert lib.mh_comm_allreduce_results(None, None, None, 0) == native.MH_E_INVALID
+    assert lib.mh_comm_destroy(None) == native.MH_E_INVALID
+
+
+def test_comm_rank_world_checks(monkeypatch):
+    """rank / world are checked before RCCL is opened (a ctx handle is needed to get that far:
+    a fake, never dereferenced past the argument checks, stands in on a GPU-less host)."""
+    lib = native.load()
+    uid = (C.c_uint8 * 128)()
+    fake = C.c_void_p(1)  # not a ctx: every call below must fail on its arguments first
+    for rank, world in ((0, 0), (-1, 2), (2, 2), (5, 1)):
+        assert lib.mh_comm_init(fake, uid, rank, world) == native.MH_E_INVALID, (rank, world)
+        assert b"rank" in lib.mh_last_error()
