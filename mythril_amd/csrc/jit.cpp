@@ -2103,9 +2103,15 @@ std::vector<MI> div_routine() {
     // y's and R's top three limbs give both to 2^-64 relative (R >= y there; lower limbs of R
     // only shift the estimate by < 2^-64, which the +-1 corrections absorb): 6 f64 ops per
     // conversion instead of 15
+    // 1/y: v_rcp_f64 is an approximation (LLVM's f64 divide refines it twice); two Newton
+    // steps bring it to f64 rounding, which the skipped-correction test below relies on (one
+    // step left digit estimates off by up to ~2^-12 on MI355X: a digit one short, found at 2^24
+    // config-5 rows)
     auto recip = [&]() {
         E(M_V_RCP_F64, {FC, FY});
         E(M_S_NOP, {IMM(1)});  // trans result -> non-trans VALU use needs a wait state
+        E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
+        E(M_V_FMA_F64, {FC, FC, FT, FC});
         E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
         E(M_V_FMA_F64, {FY, FC, FT, FC});
     };
@@ -2248,7 +2254,9 @@ std::vector<MI> div_routine() {
     E(M_V_RCP_F64, {FC, FY});
     E(M_S_NOP, {IMM(1)});
     E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
-    E(M_V_FMA_F64, {FY, FC, FT, FC});          // FY = 1/d
+    E(M_V_FMA_F64, {FC, FC, FT, FC});
+    E(M_V_FMA_F64, {FT, NEG(FY), FC, FONE()});
+    E(M_V_FMA_F64, {FY, FC, FT, FC});          // FY = 1/d (two Newton steps, as above)
     // y = 0 lanes: 1/d := 0, so their digit estimates are 0, nothing is subtracted and R keeps
     // |x| (the SMT-LIB x % 0 = x); their quotient is fixed to 2^256 - 1 at the end
     E(M_V_CNDMASK, {V(R_FY), IMM(0), V(R_FY), YNZ}, true);

@@ -377,12 +377,16 @@ MH_FN u32 knuth_step(u32* u, const u32* v, double vinv) {
     return qh;
 }
 
-// 1/d to ~2^-52 relative: hardware reciprocal + one Newton step on the device.  Only feeds an
-// estimate that udivrem256 corrects exactly, so host and device may round differently.
+// 1/d to f64 rounding: the hardware reciprocal is an approximation (LLVM refines it twice for
+// an f64 divide), so two Newton steps on the device -- one left the native code's digit
+// estimates ~2^-12 off on MI355X, and the fast path below needs 2^-49.  Only feeds an estimate
+// that udivrem256 corrects exactly, so host and device may round differently.
 MH_FN double recip_f64(double d) {
 #if defined(__HIP_DEVICE_COMPILE__)
     double r = __builtin_amdgcn_rcp(d);
-    const double e = __builtin_fma(-d, r, 1.0);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
     return __builtin_fma(r, e, r);
 #else
     return 1.0 / d;

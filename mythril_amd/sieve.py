@@ -7,9 +7,11 @@ mythril/laser/ethereum/state/constraints.py:25-35, support/model.py:15-62):
 2. harvest a candidate guide from the lowered term and the parent query's witness
    (candidates.py);
 3. compile the conjunction as one device tape over the query's own columns (mh_tapes_compile);
-4. per round: fill ``rows`` assignment rows on the device from the guide
-   (mh_assign_generate_guided), run the tape over them in MH_MODE_FIRST_HIT (the kernel stops
-   at the first satisfying lane of each wave), read back the smallest satisfying row;
+4. two launches at most: ``first_rows`` guided rows (mh_assign_generate_guided), then, when a
+   group is still unsolved, the remaining ``(max_rounds - 1) * rows`` rows in ONE launch; each
+   runs the tapes in MH_MODE_FIRST_HIT and reads back the smallest satisfying row per group
+   (the same rows, indices and witnesses as round-by-round launches over the same indices,
+   with one synchronisation instead of one per round: a miss costs two launches);
 5. on a hit, download that one row: the witness (column name -> value).
 
 Everything on the device path raises on failure; the caller (frontend.get_model) treats any
@@ -143,12 +145,13 @@ class Sieve:
         self.ctx.close()
 
     def _buffer(self, n_cols: int) -> native.Assignments:
-        if self.assign is None or self.assign.n_vars < n_cols:
+        rows = max(self.first_rows, (self.max_rounds - 1) * self.rows)
+        if self.assign is None or self.assign.n_vars < n_cols or self.assign.capacity < rows:
             if self.assign is not None:
                 self.assign.close()
             cap = max(n_cols, 64)
             cap = 1 << (cap - 1).bit_length()
-            self.assign = self.ctx.assignments(cap, self.rows)
+            self.assign = self.ctx.assignments(cap, rows)
         return self.assign
 
     def remember(self, key: tuple, w: Witness) -> None:
@@ -304,8 +307,10 @@ class Sieve:
             solved = [False] * len(groups)
             first_index = None
             offset = 0
-            for rnd in range(self.max_rounds):
-                n = self.first_rows if rnd == 0 else self.rows
+            launches = [self.first_rows]
+            if self.max_rounds > 1:
+                launches.append((self.max_rounds - 1) * self.rows)
+            for rnd, n in enumerate(launches):
                 base = (self.stats.queries << 24) + offset
                 offset += n
                 ta = time.perf_counter()

@@ -556,3 +556,20 @@ def test_vmtest_batch_jit(emu, mode):
         assert why is None, (i, why)
         got = jit_run(emu, ts, i, soa, how).values[0]
         assert got == int(smt_eval.evaluate(t.nodes, ts.pool.values, row)), i
+
+
+# 64-row chunks of config 5 where MI355X's native code once missed a hit (one Newton step on
+# v_rcp_f64 left a digit estimate too far off for the division's skipped-correction test;
+# scripts/diag_find_row.py located them at 2^24 and 2^25 rows): (tape, first row of the chunk)
+DIV_REGRESSION_CHUNKS = ((2191, 10630848), (8720, 21484032))
+
+
+def test_division_regression_chunks_jit(emu):
+    ts = synth.generate()
+    seed = synth.load_spec()["assignment_seed"]
+    for tape, r0 in DIV_REGRESSION_CHUNKS:
+        rows = [smt_eval.gen_assignment(seed, ts.n_vars, r0 + i) for i in range(64)]
+        sub = TapeSet(ts.var_names)
+        sub.pool = ts.pool
+        sub.tapes = [ts.tapes[tape]]
+        check_tapes(emu, sub, soa_of(rows, ts.n_vars))
