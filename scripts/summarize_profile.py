@@ -61,7 +61,7 @@ def main(tag: str) -> None:
     with open(os.path.join(dst, "bench_trace.json"), "w") as f:
         f.write(bench_line + "\n")
     bench = json.loads(bench_line)
-    passes = {p: load_pass(src, p) for p in ("sq1", "sq2", "tcc1", "tcc2")}
+    passes = {p: load_pass(src, p) for p in ("sq1", "sq2", "sq3", "tcc1", "tcc2", "sqc1", "sqc2")}
     json.dump(passes, open(os.path.join(dst, "pmc_counters.json"), "w"), indent=1)
 
     pmc_out = open(os.path.join(src, "sq1.out")).read() if os.path.exists(
@@ -89,6 +89,39 @@ def main(tag: str) -> None:
             "fetch_bytes_per_launch": fetch / n,
             "write_bytes_per_launch": write / n,
         }
+        # where the waves' issue time goes (quad-cycle counters, disjoint: WAIT_ANY parked at
+        # s_waitcnt / barriers, WAIT_INST_ANY ready but not issued, ACTIVE_INST_ANY issuing) and
+        # the instruction supply (SQC instruction cache, SQ instruction fetch)
+        sq3 = (passes.get("sq3") or {}).get(k, {})
+        c1 = (passes.get("sqc1") or {}).get(k, {})
+        c2 = (passes.get("sqc2") or {}).get(k, {})
+        wave_cyc = sq1.get("SQ_WAVE_CYCLES", 0.0)
+        if wave_cyc:
+            per_kernel[k]["wave_time"] = {
+                "wait_any": sq2.get("SQ_WAIT_ANY", 0.0) / wave_cyc,
+                "wait_inst_any": sq2.get("SQ_WAIT_INST_ANY", 0.0) / wave_cyc,
+                "active_inst_any": sq2.get("SQ_ACTIVE_INST_ANY", 0.0) / wave_cyc,
+                "active_valu": sq1.get("SQ_ACTIVE_INST_VALU", 0.0) / wave_cyc,
+                "active_sca": sq2.get("SQ_ACTIVE_INST_SCA", 0.0) / wave_cyc,
+                "active_misc": sq3.get("SQ_ACTIVE_INST_MISC", 0.0) / wave_cyc,
+                "active_lds": sq3.get("SQ_ACTIVE_INST_LDS", 0.0) / wave_cyc,
+                "active_vmem": sq3.get("SQ_ACTIVE_INST_VMEM", 0.0) / wave_cyc,
+                "wait_inst_lds": sq3.get("SQ_WAIT_INST_LDS", 0.0) / wave_cyc,
+            }
+        if c1:
+            req = c1.get("SQC_ICACHE_REQ", 0.0)
+            per_kernel[k]["icache"] = {
+                "req": req,
+                "hit_rate": c1.get("SQC_ICACHE_HITS", 0.0) / req if req else None,
+                "misses": c1.get("SQC_ICACHE_MISSES", 0.0),
+                "misses_duplicate": c1.get("SQC_ICACHE_MISSES_DUPLICATE", 0.0),
+                "tc_inst_req": c2.get("SQC_TC_INST_REQ"),
+                "busy_cycles": c2.get("SQC_ICACHE_BUSY_CYCLES"),
+                "tc_stall": c2.get("SQC_TC_STALL"),
+                "ifetch": sq3.get("SQ_IFETCH"),
+                "ifetch_level": sq3.get("SQ_IFETCH_LEVEL"),
+                "branches": sq2.get("SQ_INSTS_BRANCH"),
+            }
     tot_valu = sum(v["valu_insts_per_launch"] for v in per_kernel.values())
     tot_gui = sum((passes["sq2"] or {}).get(k, {}).get("GRBM_GUI_ACTIVE", 0.0) / 8.0
                   / per_kernel[k]["dispatches"] for k in per_kernel)
