@@ -204,14 +204,19 @@ __device__ __forceinline__ void sieve_body(const KParams& p) {
     preload<NR>(m, p);
     const u64 block_first = p.index_base + p.row_first + (u64)blockIdx.x * kSieveBlock;
     const u64 wave_first = block_first + (tid & ~63u);
-    for (u32 cb = 0; cb < p.n_ids;) {
+    // grid y splits the tape list (a short run -- a query's 256-row first round is one
+    // workgroup -- spreads its tapes over CUs instead of running them all on one)
+    const u32 id_lo = (u32)((u64)p.n_ids * blockIdx.y / gridDim.y);
+    const u32 n_ids = (u32)((u64)p.n_ids * (blockIdx.y + 1) / gridDim.y) - id_lo;
+    const u32* tape_ids = p.tape_ids + id_lo;
+    for (u32 cb = 0; cb < n_ids;) {
         __syncthreads();  // previous chunk's LDS fully consumed
         if (tid < (u32)kChunk) {
             // chunk formation by wave 0: the bucket's tapes are contiguous in the word array,
             // so the chunk is the longest prefix of the next kChunk tapes within kLdsInsns
             const u32 i = cb + tid;
-            const bool in = i < p.n_ids;
-            const u32 t = in ? p.tape_ids[i] : 0u;
+            const bool in = i < n_ids;
+            const u32 t = in ? tape_ids[i] : 0u;
             const mh_dev_tape h = p.tapes[t];
             const u32 base = __builtin_amdgcn_readfirstlane(h.insn_off);
             const u32 end = h.insn_off + h.n_insns - base;
@@ -273,7 +278,8 @@ __device__ __forceinline__ void sieve_body(const KParams& p) {
                         const u64 r = row - p.row_first;
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
-                            p.values_out[((u64)(cb + j) * 8 + k) * p.row_count + r] = X[k];
+                            p.values_out[((u64)(id_lo + cb + j) * 8 + k) * p.row_count + r] =
+                                X[k];
                     }
                 }
                 const u32 res = rb ? (X[0] & 1u) : (is_zero256(X) ? 0u : 1u);
@@ -462,8 +468,11 @@ __attribute__((amdgpu_waves_per_eu(sieve_min_waves(NR, FEAT), 8))) sieve_kernel(
 template <int NR, int FEAT>
 hipError_t launch_variant(const KParams& p, hipStream_t stream) {
     const u64 blocks = (p.row_count + kSieveBlock - 1) / kSieveBlock;
-    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks), dim3(kSieveBlock), 0, stream,
-                       p);
+    // fewer row blocks than CUs: split the tapes over grid y until the chip has ~256 workgroups
+    u64 gy = 1;
+    if (blocks < 256) gy = std::min<u64>(p.n_ids, (256 + blocks - 1) / blocks);
+    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks, (unsigned)gy),
+                       dim3(kSieveBlock), 0, stream, p);
     return hipGetLastError();
 }
 

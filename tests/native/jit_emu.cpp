@@ -87,6 +87,7 @@ struct Err {
     std::string m;
 };
 
+uint64_t g_chunk_valu0 = 0;
 // executed-instruction counters (per wave): VALU, of them 4-cycle class, SALU, and the part
 // inside the division subroutine
 struct Counts {
@@ -94,6 +95,8 @@ struct Counts {
     double alive_valu = 0;  // VALU weighted by the fraction of lanes still alive (compaction bound)
 } g_counts;
 uint64_t g_alive = ~0ull;  // lanes that satisfy every conjunct tested so far (short circuit)
+// compaction study: VALU before the chunk's first short-circuit test, and the live lanes then
+uint64_t g_valu_head = 0, g_head_done = 0, g_alive_hist[65];
 const uint32_t* g_mem = nullptr;  // "global memory": the SoA assignment buffer at address 0
 uint64_t g_mem_words = 0;
 uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
@@ -334,7 +337,14 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                 uint64_t r = m.op == M_S_AND_B64 ? a & b : m.op == M_S_OR_B64 ? a | b :
                              m.op == M_S_XOR_B64 ? a ^ b : m.op == M_S_XNOR_B64 ? ~(a ^ b) :
                              m.op == M_S_ANDN2_B64 ? a & ~b : a | ~b;
-                if (m.op == M_S_AND_B64 && o[0].k == O_S && o[0].v == S_SCRATCH) g_alive = r;
+                if (m.op == M_S_AND_B64 && o[0].k == O_S && o[0].v == S_SCRATCH) {
+                    g_alive = r;
+                    if (!g_head_done && !depth) {
+                        g_head_done = 1;
+                        g_valu_head += g_counts.valu - g_chunk_valu0;
+                        ++g_alive_hist[__builtin_popcountll(r)];
+                    }
+                }
                 w.set_mask(o[0], r);
                 w.scc = r != 0;
                 break;
@@ -507,7 +517,10 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
             g_mem = assign;
             g_mem_words = (uint64_t)n_vars * 8 * rows;
             g_alive = (uint64_t)w.s[S_VALID] | ((uint64_t)w.s[S_VALID + 1] << 32);
+            g_head_done = 0;
+            g_chunk_valu0 = g_counts.valu;
             run(w, tc.code, div);
+            if (!g_head_done) ++g_alive_hist[64];  // no test: the whole tape is the head
             ++chunks;
             const uint64_t res = (uint64_t)w.s[S_RES] | ((uint64_t)w.s[S_RES + 1] << 32);
             for (int l = 0; l < 64 && base + (uint64_t)l < rows; ++l) {
@@ -666,3 +679,14 @@ extern "C" void emu_jit_tag_op(uint64_t* out, int reset) {
 }
 
 extern "C" uint64_t emu_jit_sc_fallbacks(int reset) { return sc_fallbacks(reset != 0); }
+
+// compaction study: [0] VALU before the first short-circuit test (all chunks), [1..65] chunks by
+// live lanes at that test (64 = no test)
+extern "C" void emu_jit_head_stats(uint64_t* out, int reset) {
+    out[0] = g_valu_head;
+    for (int i = 0; i <= 64; ++i) out[1 + i] = g_alive_hist[i];
+    if (reset) {
+        g_valu_head = 0;
+        for (int i = 0; i <= 64; ++i) g_alive_hist[i] = 0;
+    }
+}
