@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .lower import Schema
+from .lower import Schema, var_names
 from .tape import BOOL, Op, TapeBuilder
 
 Alt = Dict[str, int]          # column name -> value
@@ -130,31 +130,60 @@ def _limbs(vals: Sequence[int]) -> np.ndarray:
     return np.frombuffer(buf, dtype="<u4").reshape(len(vals), 8).astype(np.uint32)
 
 
+MEMO_LIMIT = 1 << 20  # entries per builder-level memo before it is dropped
+
+
+def _memo(b: TapeBuilder, name: str) -> dict:
+    """A memo living on the builder: lowered nodes are immutable and hash-consed, so what is
+    derived from a node alone holds for every later query that contains it (a LASER query
+    extends its parent's, svm.py:257-262)."""
+    m = b.__dict__.get(name)
+    if m is None or len(m) > MEMO_LIMIT:
+        m = b.__dict__[name] = {}
+    return m
+
+
 class Harvester:
     def __init__(self, b: TapeBuilder, schema: Schema, columns: Sequence[str]):
         self.b = b
         self.schema = schema
         self.columns = list(columns)
-        self.col_of_var = {}
-        for name in self.columns:
-            self.col_of_var[b.var_index[name]] = name
+        # every VAR under a lowered query is one of its columns
+        self.col_of_var = var_names(b)
         self.pools: Dict[str, List[int]] = {c: [] for c in self.columns}
         self.sets: List[Tuple[int, List[Alt]]] = []
-        self._inv_memo: Dict[Tuple[int, int, int], Optional[List[Alt]]] = {}
+        # inversions by (node, value, mask) / (node, truth), with the hints each produced
+        # (transitively), so a memo hit replays them exactly as a fresh inversion would
+        self._inv_memo: Dict[tuple, tuple] = _memo(b, "_guide_inv")
+        self._cap: List[list] = []
         self._consts_by_width: Dict[int, List[int]] = {}
         self.hints: List[Tuple[int, List[Alt]]] = []
         self.copy_sets: List[List[List[Copy]]] = []
         self._hint_keys = set()
 
+    def _memoised(self, key: tuple, compute):
+        got = self._inv_memo.get(key)
+        if got is None:
+            self._cap.append([])
+            try:
+                r = compute()
+            finally:
+                hints = self._cap.pop()
+            self._inv_memo[key] = (r, tuple(hints))
+            if self._cap:
+                self._cap[-1].extend(hints)
+            return r
+        r, hints = got
+        for h in hints:
+            self._hint(h)
+        return r
+
     # -- inversion -------------------------------------------------------------------------
     def invert_bits(self, n: int, value: int, mask: int, depth: int = 0) -> Optional[List[Alt]]:
         """Partial assignments making (term n) & mask == value & mask; None = don't know."""
-        key = (n, value, mask)
-        if key in self._inv_memo:
-            return self._inv_memo[key]
-        r = self._invert_bits(n, value & mask, mask, depth) if depth < 64 else None
-        self._inv_memo[key] = r
-        return r
+        return self._memoised(
+            (n, value, mask),
+            lambda: self._invert_bits(n, value & mask, mask, depth) if depth < 64 else None)
 
     def _invert_bits(self, n: int, value: int, mask: int, depth: int) -> Optional[List[Alt]]:
         b = self.b
@@ -257,6 +286,9 @@ class Harvester:
         """Partial assignments making Bool node n == truth; None = don't know."""
         if depth > 64:
             return None
+        return self._memoised(("bool", n, truth), lambda: self._invert_bool(n, truth, depth))
+
+    def _invert_bool(self, n: int, truth: bool, depth: int) -> Optional[List[Alt]]:
         b = self.b
         op, w, a, bb, c, i0, i1 = b.nodes[n]
         cv = b.const_value(n)
@@ -395,6 +427,8 @@ class Harvester:
         return alts
 
     def _hint(self, alts: List[Alt]) -> None:
+        if self._cap:
+            self._cap[-1].append(alts)
         key = tuple(tuple(sorted(a.items())) for a in alts)
         if key not in self._hint_keys and len(self._hint_keys) < MAX_SETS // 4:
             self._hint_keys.add(key)
@@ -425,26 +459,34 @@ class Harvester:
 
         b = self.b
         nodes, pool_values = b.nodes, b.pool.values
+        conjuncts = self._conjuncts(root)
+        consts_of = _memo(b, "_guide_consts")
         self.query_consts = qc = set()
-        seen, stack = set(), [root]
-        while stack:  # the constants of this query (the pool is shared by all queries)
-            n = stack.pop()
-            if n in seen:
-                continue
-            seen.add(n)
-            node = nodes[n]
-            op = node[0]
-            if op == Op.CONST:
-                qc.add(pool_values[node[5]])
-            k = ARITY[op]
-            if k:
-                stack += node[2:2 + k]
+        for conj in conjuncts:  # the constants of this query (the pool is shared by all queries)
+            got = consts_of.get(conj)
+            if got is None:
+                got, seen, stack = set(), set(), [conj]
+                while stack:
+                    n = stack.pop()
+                    if n in seen:
+                        continue
+                    seen.add(n)
+                    node = nodes[n]
+                    op = node[0]
+                    if op == Op.CONST:
+                        got.add(pool_values[node[5]])
+                    k = ARITY[op]
+                    if k:
+                        stack += node[2:2 + k]
+                got = consts_of[conj] = frozenset(got)
+            qc |= got
         if parent:
             alt = {k: v for k, v in parent.items() if k in self.pools}
             if alt:
                 self.sets.append((PROB_PARENT, [alt]))
         seen_eq = set()
-        for conj in self._conjuncts(root):
+        eq_pairs = _memo(b, "_guide_eq")
+        for conj in conjuncts:
             alts = self.invert_bool(conj, True)
             if alts and alts != [{}]:
                 self.sets.append((PROB_DEFAULT, [a for a in alts if a][:MAX_ALTS]))
@@ -453,15 +495,21 @@ class Harvester:
                 if n in seen_eq:
                     continue
                 seen_eq.add(n)
-                _, _, x, y, _, _, _ = b.nodes[n]
-                w = b.widths[x]
-                if w == BOOL or b.const_value(x) is not None or b.const_value(y) is not None:
+                pair = eq_pairs.get(n)
+                if pair is None:  # (x, y, copy alternatives) after peeling shared wrappers
+                    _, _, x, y, _, _, _ = b.nodes[n]
+                    if b.widths[x] == BOOL or b.const_value(x) is not None \
+                            or b.const_value(y) is not None:
+                        pair = ()
+                    else:
+                        x, y = self.strip_common(x, y)
+                        # t == t (keccak inverse conditions after lowering): always true
+                        pair = () if x == y else (x, y, self.copy_alternatives(x, y))
+                    eq_pairs[n] = pair
+                if not pair:
                     continue
-                x, y = self.strip_common(x, y)
-                if x == y:  # t == t (keccak inverse conditions after lowering): always true
-                    continue
+                x, y, calts = pair
                 w = b.widths[x]
-                calts = self.copy_alternatives(x, y)
                 if calts:
                     if len(self.copy_sets) < MAX_SETS // 4:
                         self.copy_sets.append(calts)
@@ -480,11 +528,12 @@ class Harvester:
         # hints first: the exact requirements of the conjuncts (later sets) override them
         self.sets = self.sets[:1] + self.hints + self.sets[1:] if parent else \
             self.hints + self.sets
+        pools = self.pools
         for _, alts in self.sets:
             for alt in alts:
                 for name, v in alt.items():
-                    p = self.pools[name]
-                    if v not in p and len(p) < MAX_POOL:
+                    p = pools[name]
+                    if len(p) < MAX_POOL and v not in p:
                         p.append(v)
         widths = [self.schema.columns[c].width for c in self.columns]
         for name, w in zip(self.columns, widths):
@@ -503,8 +552,13 @@ class Harvester:
         store-chain reads lower to ite(key == stored_key, ...))."""
         from .tape import ARITY
 
+        memo = _memo(self.b, "_guide_eq_nodes")
+        got = memo.get(root)
+        if got is not None:
+            return got
         out, seen, stack = [], set(), [root]
         b = self.b
+        memo[root] = out
         while stack and len(seen) < limit:
             n = stack.pop()
             if n in seen:

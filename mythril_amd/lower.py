@@ -30,6 +30,7 @@ z3 unchanged.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -69,6 +70,77 @@ class Schema:
     uf_cells: Dict[str, Dict[int, str]] = field(default_factory=dict)
     keccak: Dict[str, KeccakMap] = field(default_factory=dict)
     columns: Dict[str, Column] = field(default_factory=dict)         # column name -> Column
+
+
+@dataclass
+class Harvest:
+    """What pass 1 reads off some constraints: constant keys per array / function, concrete
+    keccak pairs and the lowest keccak bound.  One per constraint, memoised on the builder, so a
+    query that extends its parent (svm.py:257-262) only walks its new constraint."""
+
+    cells: Dict[str, set] = field(default_factory=dict)
+    uf_cells: Dict[str, set] = field(default_factory=dict)
+    keccak: Dict[str, Dict[int, int]] = field(default_factory=dict)
+    bounds: Dict[str, int] = field(default_factory=dict)
+
+    def merge(self, o: "Harvest") -> None:
+        for name, keys in o.cells.items():
+            self.cells.setdefault(name, set()).update(keys)
+        for name, keys in o.uf_cells.items():
+            self.uf_cells.setdefault(name, set()).update(keys)
+        for f, pairs in o.keccak.items():
+            self.keccak.setdefault(f, {}).update(pairs)
+        for f, v in o.bounds.items():
+            self.bounds[f] = min(v, self.bounds.get(f, v))
+
+    def fingerprint(self) -> tuple:
+        """Everything the rewrite of pass 2 depends on: equal fingerprints lower every term to the
+        same column-only term."""
+        return (tuple(sorted((n, tuple(sorted(k))) for n, k in self.cells.items())),
+                tuple(sorted((n, tuple(sorted(k))) for n, k in self.uf_cells.items())),
+                tuple(sorted((f, tuple(sorted(p.items())), (self.bounds.get(f, 0) + 63) & ~63)
+                             for f, p in self.keccak.items())))
+
+
+def node_columns(b: TapeBuilder, roots: Iterable[int]) -> Dict[int, frozenset]:
+    """The VAR indices under each node reachable from `roots` (memoised on the builder: nodes
+    are immutable and hash-consed, so later queries only visit their new nodes)."""
+    cols: Dict[int, frozenset] = b.__dict__.setdefault("_node_cols", {})
+    order, st = [], [(r, False) for r in roots if r not in cols]
+    seen = set()
+    while st:
+        n, done = st.pop()
+        if done:
+            order.append(n)
+            continue
+        if n in seen or n in cols:
+            continue
+        seen.add(n)
+        st.append((n, True))
+        op, _, a, bb, c, _, _ = b.nodes[n]
+        st += [(x, False) for x in (a, bb, c)[:ARITY[op]] if x not in seen and x not in cols]
+    empty = frozenset()
+    for n in order:
+        op, _, a, bb, c, i0, _ = b.nodes[n]
+        if op == Op.VAR:
+            cols[n] = frozenset((i0,))
+            continue
+        kids = (a, bb, c)[:ARITY[op]]
+        if not kids:
+            cols[n] = empty
+            continue
+        sets = [cols[x] for x in kids]
+        big = max(sets, key=len)
+        cols[n] = big if all(x <= big for x in sets) else big.union(*sets)
+    return cols
+
+
+def var_names(b: TapeBuilder) -> Dict[int, str]:
+    """VAR index -> column name (cached; the builder's var_index only grows)."""
+    got = b.__dict__.get("_var_names")
+    if got is None or len(got) != len(b.var_index):
+        got = b.__dict__["_var_names"] = {v: k for k, v in b.var_index.items()}
+    return got
 
 
 def cell_name(arr: str, key: int) -> str:
@@ -126,8 +198,12 @@ class Lowering:
     def harvest(self, roots: Sequence[int]) -> None:
         if self.frozen:
             return
+        self.apply_harvest(self.collect(roots))
+
+    def collect(self, roots: Sequence[int]) -> "Harvest":
+        """The constant keys, keccak pairs and keccak bounds the terms under `roots` state."""
         b = self.b
-        bounds: Dict[str, List[int]] = {}
+        h = Harvest()
         for n in _walk(b, roots):
             op, w, a, bb, c, i0, i1 = b.nodes[n]
             if op == Op.SELECT:
@@ -135,18 +211,18 @@ class Lowering:
                 if base is not None:
                     name = self.sym.array_names[b.nodes[base][5]]
                     key = b.const_value(bb)
-                    cells = self.schema.cells.setdefault(name, {})
+                    cells = h.cells.setdefault(name, set())
                     if key is not None:
-                        cells.setdefault(key, cell_name(name, key))
+                        cells.add(key)
             elif op == Op.UF:
                 fname = self.sym.function_names[i0]
                 if is_keccak(fname):
-                    self.schema.keccak.setdefault(fname, KeccakMap(0))
+                    h.keccak.setdefault(fname, {})
                 elif not fname.endswith("-1"):
-                    cells = self.schema.uf_cells.setdefault(fname, {})
+                    cells = h.uf_cells.setdefault(fname, set())
                     key = b.const_value(a)
                     if key is not None:
-                        cells.setdefault(key, cell_name(fname, key))
+                        cells.add(key)
             elif op == Op.EQ or op in ORDERED:
                 for x, y in ((a, bb), (bb, a)):
                     f = self._keccak_app(x)
@@ -156,12 +232,24 @@ class Lowering:
                     if op == Op.EQ:
                         arg = b.const_value(b.nodes[x][2])
                         if arg is not None:  # keccak256_N(c) == k: a concrete pair
-                            self.schema.keccak.setdefault(f, KeccakMap(0)).pairs[arg] = kv
+                            h.keccak.setdefault(f, {})[arg] = kv
                     else:
-                        bounds.setdefault(f, []).append(kv)
-        for f, km in self.schema.keccak.items():
-            lo = min(bounds.get(f, [0]))
-            km.base = (lo + 63) & ~63
+                        h.bounds[f] = min(kv, h.bounds.get(f, kv))
+        return h
+
+    def apply_harvest(self, h: "Harvest") -> None:
+        for name, keys in h.cells.items():
+            cells = self.schema.cells.setdefault(name, {})
+            for key in sorted(keys):
+                cells.setdefault(key, cell_name(name, key))
+        for name, keys in h.uf_cells.items():
+            cells = self.schema.uf_cells.setdefault(name, {})
+            for key in sorted(keys):
+                cells.setdefault(key, cell_name(name, key))
+        for f, pairs in h.keccak.items():
+            km = self.schema.keccak.setdefault(f, KeccakMap(0))
+            km.pairs.update(pairs)
+            km.base = (h.bounds.get(f, 0) + 63) & ~63
 
     def _keccak_app(self, n: int) -> Optional[str]:
         op, _, _, _, _, i0, _ = self.b.nodes[n]
@@ -387,18 +475,52 @@ class Lowering:
         return self._table(fname, w, x, cells, "ufcell", "ufelse")
 
 
+MAX_LOWERINGS = 64  # pass-2 memos kept per builder, by harvest fingerprint (LRU)
+
+
 def lower_query(b: TapeBuilder, roots: Sequence[int],
                 frozen: Optional[Schema] = None) -> Tuple[int, Schema]:
-    """Lower the conjunction of Bool `roots`: (root node of the column-only term, schema)."""
-    L = Lowering(b, frozen)
-    L.harvest(roots)
-    low = [L.lower(r) for r in roots]
+    """Lower the conjunction of Bool `roots`: (root node of the column-only term, schema).
+
+    Without ``frozen`` both passes are memoised on the builder: pass 1 per constraint
+    (``Harvest``), pass 2 per harvest fingerprint (the rewrite of a node depends on nothing
+    else), so a LASER query that adds one constraint to its parent's (svm.py:257-262) lowers only
+    that constraint.  The schema's columns are the ones the lowered term reads, in VAR order."""
+    if frozen is not None:
+        L = Lowering(b, frozen)
+        low = [L.lower(r) for r in roots]
+        schema = L.schema
+    else:
+        per_root: Dict[int, Harvest] = b.__dict__.setdefault("_harvest_of", {})
+        h = Harvest()
+        for r in roots:
+            got = per_root.get(r)
+            if got is None:
+                got = per_root[r] = Lowering(b).collect([r])
+            h.merge(got)
+        fp = h.fingerprint()
+        lows = b.__dict__.setdefault("_lowerings", OrderedDict())
+        L = lows.get(fp)
+        if L is None:
+            L = lows[fp] = Lowering(b)
+            L.apply_harvest(h)
+            if len(lows) > MAX_LOWERINGS:
+                lows.popitem(last=False)
+        else:
+            lows.move_to_end(fp)
+        low = [L.lower(r) for r in roots]
+        cols = node_columns(b, low)
+        used = frozenset().union(*(cols[r] for r in low)) if low else frozenset()
+        names = var_names(b)
+        full = L.schema
+        schema = Schema(full.cells, full.uf_cells, full.keccak,
+                        {names[v]: full.columns[names[v]] for v in sorted(used)})
     for r in low:
         if b.widths[r] != BOOL:
             raise TapeError("constraints must be Bool")
     if not low:
-        return b.true(), L.schema
+        return b.true(), schema
     acc = low[0]
     for x in low[1:]:
         acc = b.op(Op.AND, acc, x)
-    return acc, L.schema
+    return acc, schema

@@ -15,7 +15,7 @@ import numpy as np
 
 from . import native
 from .lower import Schema, lower_query
-from .tape import BOOL, Tape, TapeError, TapeSet
+from .tape import BOOL, TapeError
 
 if TYPE_CHECKING:  # pragma: no cover
     from .sieve import Sieve
@@ -89,12 +89,9 @@ class Model:
         columns = list(schema.columns) or ["__ground__"]
         if columns == ["__ground__"]:
             b.var("__ground__", 1)
-        from .sieve import local_tape
+        from .sieve import local_tapeset
 
-        ts = TapeSet(columns)
-        ts.pool = b.pool
-        nodes = local_tape(b, root, columns)
-        ts.tapes.append(Tape(nodes))
+        ts = local_tapeset(b, [root], columns)
         dev = self.sieve.ctx
         ct = self.sieve.compile(ts)
         try:

@@ -29,8 +29,8 @@ import numpy as np
 
 from . import native
 from .candidates import build_guide
-from .lower import Schema, lower_query
-from .tape import Op, TapeBuilder, TapeSet
+from .lower import Schema, lower_query, node_columns
+from .tape import NODE_DTYPE, Op, Tape, TapeBuilder, TapeSet
 
 
 @dataclass
@@ -69,6 +69,48 @@ def local_tape(b: TapeBuilder, root: int, columns: Sequence[str]) -> np.ndarray:
     if is_var.any():
         nodes["imm0"][is_var] = [local[int(x)] for x in nodes["imm0"][is_var]]
     return nodes
+
+
+class LocalPool:
+    """The constants one query's tapes read, renumbered 0..k-1 (the builder's pool holds every
+    constant of the run: uploading it with each query would grow with the run)."""
+
+    def __init__(self, rows: np.ndarray):
+        self.rows = rows
+        self.values = range(len(rows))
+
+    def to_array(self) -> np.ndarray:
+        return self.rows
+
+
+def local_tapeset(b: TapeBuilder, roots: Sequence[int], columns: Sequence[str]) -> TapeSet:
+    """One tape per root over the query's own columns (VAR renumbered to `columns` order) and
+    its own constant pool (CONST renumbered to the constants the tapes read)."""
+    ts = TapeSet(columns)
+    tapes = [b.finish(r).nodes for r in roots]
+    nodes = np.concatenate(tapes) if tapes else np.zeros(0, dtype=NODE_DTYPE)
+    ops, imm0 = nodes["op"], nodes["imm0"].astype(np.int64)
+    is_var = ops == int(Op.VAR)
+    is_const = ops == int(Op.CONST)
+    new0 = imm0.copy()
+    if is_var.any():
+        lut = np.full(len(b.var_index), -1, dtype=np.int64)
+        for i, c in enumerate(columns):
+            lut[b.var_index[c]] = i
+        new0[is_var] = lut[imm0[is_var]]
+        if (new0[is_var] < 0).any():
+            raise ValueError("a tape reads a variable outside the query's columns")
+    used = np.unique(imm0[is_const])
+    new0[is_const] = np.searchsorted(used, imm0[is_const])
+    nodes = nodes.copy()
+    nodes["imm0"] = new0.astype(nodes["imm0"].dtype)
+    ts.pool = LocalPool(np.ascontiguousarray(b.pool.to_array()[used]) if len(used)
+                        else np.zeros((1, 8), dtype=np.uint32))
+    off = 0
+    for t in tapes:
+        ts.tapes.append(Tape(nodes[off:off + len(t)]))
+        off += len(t)
+    return ts
 
 
 # ops whose recomputation is cheap enough to duplicate instead of keeping a value live
@@ -191,8 +233,6 @@ class Sieve:
         laser/smt/solver/independence_solver.py:38-83, over lowered columns): [(conjunct nodes,
         column var indices)].  Groups share no column, so each can take its witness from a
         different candidate row."""
-        from .tape import ARITY
-
         conj, stack = [], [root]
         while stack:
             n = stack.pop()
@@ -202,33 +242,7 @@ class Sieve:
                 conj.append(n)
         # column sets per node, memoised on the builder: nodes are immutable and hash-consed, so
         # a query that extends its parent (svm.py:257-262) only visits its new nodes
-        cols: Dict[int, frozenset] = b.__dict__.setdefault("_bucket_cols", {})
-        order, st = [], [(c, False) for c in conj if c not in cols]
-        seen = set()
-        while st:
-            n, done = st.pop()
-            if done:
-                order.append(n)
-                continue
-            if n in seen or n in cols:
-                continue
-            seen.add(n)
-            st.append((n, True))
-            op, _, a, bb, c, _, _ = b.nodes[n]
-            st += [(x, False) for x in (a, bb, c)[:ARITY[op]] if x not in seen and x not in cols]
-        empty = frozenset()
-        for n in order:
-            op, _, a, bb, c, i0, _ = b.nodes[n]
-            if op == Op.VAR:
-                cols[n] = frozenset((i0,))
-                continue
-            kids = (a, bb, c)[:ARITY[op]]
-            if not kids:
-                cols[n] = empty
-                continue
-            sets = [cols[x] for x in kids]
-            big = max(sets, key=len)
-            cols[n] = big if all(x <= big for x in sets) else big.union(*sets)
+        cols = node_columns(b, conj)
         parent: Dict[int, int] = {}
 
         def find(x):
@@ -251,12 +265,10 @@ class Sieve:
         return list(groups.values())
 
     def solve(self, b: TapeBuilder, roots: Sequence[int], key: Optional[tuple] = None,
-              pool=None, budget_s: Optional[float] = None) -> Optional[Witness]:
+              budget_s: Optional[float] = None) -> Optional[Witness]:
         """A witness of the conjunction of Bool nodes `roots` of builder `b`, or None.
         ``budget_s`` (get_model's remaining solver budget) caps this query's rounds below the
         sieve's own ``self.budget_s``; no round starts once it is spent."""
-        from .tape import Tape
-
         t0 = time.perf_counter()
         budget = self.budget_s if budget_s is None else min(self.budget_s, budget_s)
         self.stats.queries += 1
@@ -279,16 +291,15 @@ class Sieve:
         t_g = time.perf_counter()
         st.add("guide", t_g - t_l)
         groups = self.buckets(b, root)
-        ts = TapeSet(columns)
-        ts.pool = pool if pool is not None else b.pool
         names = {b.var_index[c]: c for c in columns}
-        group_cols = []
+        group_cols, accs = [], []
         for conj, vs in groups:
             acc = conj[0]
             for x in conj[1:]:
                 acc = b.op(Op.AND, acc, x)
-            ts.tapes.append(Tape(local_tape(b, acc, columns)))
+            accs.append(acc)
             group_cols.append([names[v] for v in vs])
+        ts = local_tapeset(b, accs, columns)
         if len(groups) > 1:
             self.stats.extra["bucketed"] = self.stats.extra.get("bucketed", 0) + 1
         t1 = time.perf_counter()

@@ -15,6 +15,7 @@ reference construction that produces each one are tabulated in DESIGN.md
 from __future__ import annotations
 
 import enum
+from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -22,6 +23,7 @@ import numpy as np
 
 BOOL = 0
 MAX_WIDTH = 1088  # 136 bytes: one Keccak block
+FINISH_CACHE = 256  # tapes of recent AND roots kept per builder (TapeBuilder.finish)
 
 
 class Op(enum.IntEnum):
@@ -356,24 +358,44 @@ class TapeBuilder:
         return self._add(op, w, a, b, c, imm0, imm1)
 
     def finish(self, root: int) -> "Tape":
-        """Return the tape of the sub-DAG reachable from ``root`` (root last, topological)."""
+        """Return the tape of the sub-DAG reachable from ``root`` (root last, topological).
+
+        Post-order of AND(x, y) is x's post-order, then y's nodes not under x, then the AND; a
+        path condition grows by one conjunct per LASER query (svm.py:257-262), so the tapes of
+        recent AND roots are kept and a child query's tape extends its parent's."""
+        cache = self.__dict__.setdefault("_finished", OrderedDict())
+        got = cache.get(root)
+        if got is not None:
+            cache.move_to_end(root)
+            return Tape(got[1])
+        node = self.nodes[root]
+        base = cache.get(node[2]) if node[0] == Op.AND else None
+        if base is not None:
+            remap = dict(base[0])
+            start = [(node[3], False)]
+        else:
+            remap = {}
+            start = [(root, False)]
         order: List[int] = []
+        stack = start
         seen = set()
-        stack = [(root, False)]
         while stack:
             n, done = stack.pop()
             if done:
+                remap[n] = len(remap)
                 order.append(n)
                 continue
-            if n in seen:
+            if n in seen or n in remap:
                 continue
             seen.add(n)
             stack.append((n, True))
-            node = self.nodes[n]
-            for child in reversed(node[2 : 2 + ARITY[node[0]]]):
-                if child not in seen:
+            nd = self.nodes[n]
+            for child in reversed(nd[2 : 2 + ARITY[nd[0]]]):
+                if child not in seen and child not in remap:
                     stack.append((child, False))
-        remap = {old: new for new, old in enumerate(order)}
+        if base is not None and root not in remap:
+            remap[root] = len(remap)
+            order.append(root)
         rows = []
         flags = self.flags
         for old in order:
@@ -381,7 +403,15 @@ class TapeBuilder:
             k = ARITY[op]
             rows.append((op, flags[old], w, remap[a] if k > 0 else 0, remap[b] if k > 1 else 0,
                          remap[c] if k > 2 else 0, i0, i1))
-        return Tape(np.array(rows, dtype=NODE_DTYPE))
+        arr = np.array(rows, dtype=NODE_DTYPE)
+        if base is not None:
+            arr = np.concatenate([base[1], arr])
+        if node[0] == Op.AND:
+            arr.flags.writeable = False  # shared with later tapes: callers copy to modify
+            cache[root] = (remap, arr)
+            while len(cache) > FINISH_CACHE:
+                cache.popitem(last=False)
+        return Tape(arr)
 
 
 class Symbols:
