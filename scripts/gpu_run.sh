@@ -7,6 +7,7 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     default bench.py (N=1)
 #   miss      scripts/miss_cost.py (per-stage cost of sieve misses, JIT build vs interpreter)
+#   queries   scripts/sieve_queries.py (per-query latency, LASER order and cold)
 #   counters  rocprofv3 -L (the PMC counters this box offers)
 #   profile   scripts/profile.sh <tag> (kernel trace + PMC passes of the default bench)
 set -o pipefail
@@ -24,6 +25,7 @@ for step in "$@"; do
     smoke)    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 ;;
     bench)    timeout -k 10 600 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.log" ;;
     miss)     timeout -k 10 400 python -u scripts/miss_cost.py 5 > "$OUT/miss_cost.jsonl" 2> "$OUT/miss_cost.log" ;;
+    queries)  timeout -k 10 400 python -u scripts/sieve_queries.py > "$OUT/sieve_queries.jsonl" 2> "$OUT/sieve_queries.log" ;;
     counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 ;;
     profile)  bash scripts/profile.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
