@@ -134,7 +134,8 @@ int32_t mh_tapes_info(const mh_tapeset* ts, mh_tape_info* info /* [n_tapes] */, 
 
 /* ---- assignments ----------------------------------------------------------------------------- */
 /* Layout in HBM: column v, limb k (0 = least significant) of assignment i is word
- * ((v * 8 + k) * capacity + i).  Every column is a 256-bit word.                                 */
+ * ((v * 8 + k) * stride + i), stride = capacity + a few padding rows (library-internal: the
+ * device memory is only reached through these calls).  Every column is a 256-bit word.          */
 int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_assign** out);
 int32_t mh_assign_destroy(mh_assign* as);
 /* host_soa has the same layout with `count` in place of capacity; fills [first, first+count).   */
@@ -260,8 +261,11 @@ int32_t mh_comm_destroy(mh_ctx* ctx);
  * 11 v_cndmask_b32_e32 (VCC mask); 12 v_cmp_eq_u32_e32 (VCC write); 13 v_xor_b32 with a literal;
  * 14 v_lshlrev_b32; 15 v_add3_u32; 16 v_fma_f64; 17 v_xnor_b32; 18 v_and_b32; 19 v_or_b32;
  * 20 v_not_b32; with a partial EXEC mask: 21 v_xor_b32 (low 32 lanes), 22 v_alignbit_b32 (low 32),
- * 23 v_xor_b32 (low 16), 24 v_xor_b32 (every other lane).                                       */
-#define MH_MB_NUM_KINDS 25
+ * 23 v_xor_b32 (low 16), 24 v_xor_b32 (every other lane); dependent chains (each instruction
+ * reads the previous one's result: latency, at 1 wave per SIMD): 25 v_mad_u64_u32 into one
+ * accumulator, 26 v_add_u32, 27 v_addc_co_u32 through VCC, 28 two v_mad_u64_u32 accumulators
+ * interleaved, 29 v_mad_u64_u32 + v_addc carry count (product scanning), 30 v_cmp + v_cndmask. */
+#define MH_MB_NUM_KINDS 31
 int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
                             double* lane_ops_per_s);
 /* Round-1 form: kinds 0..2 of mh_microbench_issue at 8 waves per SIMD.                           */

@@ -204,6 +204,7 @@ struct mh_assign {
     mh_ctx* ctx = nullptr;
     uint32_t n_vars = 0;
     uint64_t capacity = 0;
+    uint64_t stride = 0;           // words between column-limbs (capacity + assign_pad_rows)
     uint32_t* d = nullptr;
     uint32_t* d_guide = nullptr;   // packed mh_guide (grow-only)
     size_t guide_words = 0;
@@ -273,7 +274,7 @@ mh::KParams make_params(const mh_tapeset* ts, uint32_t tape_first, const mh_assi
     p.tapes = ts->d_tapes;
     p.consts = ts->d_consts;
     p.assign = as->d;
-    p.capacity = as->capacity;
+    p.capacity = as->stride;
     p.n_pre = ts->n_vars <= MH_MAX_PRELOAD ? ts->n_vars : 0;
     p.result_base = tape_first;
     p.row_first = row_first;
@@ -301,7 +302,7 @@ int32_t launch_jit(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as, uint6
                    uint64_t* d_hit_count, uint32_t* d_values) {
     mh::jit::KernArgs a{};
     a.assign = (uint64_t)(uintptr_t)as->d;
-    a.capacity = as->capacity;
+    a.capacity = as->stride;
     a.row_first = row_first;
     a.row_count = row_count;
     a.index_base = index_base;
@@ -311,7 +312,7 @@ int32_t launch_jit(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as, uint6
     a.n_rowblocks = (uint32_t)((row_count + a.rows_per_wg - 1) / a.rows_per_wg);
     a.values_out = (uint64_t)(uintptr_t)d_values;
     a.mode = mode;
-    if (as->capacity >= (1ull << 30) || row_first + row_count > (1ull << 31))
+    if (as->stride >= (1ull << 30) || row_first + row_count > (1ull << 31))
         return set_err(MH_E_UNSUPPORTED, "JIT kernels address < 2^30 rows per column");
     for (const auto& j : ts->jit) {
         hipFunction_t fn = d_values ? j.vfn : j.fn;
@@ -600,6 +601,19 @@ int32_t mh_tapes_info(const mh_tapeset* ts, mh_tape_info* info, uint32_t n_tapes
     return MH_OK;
 }
 
+// Rows of padding after each column-limb.  The limbs of one row lie `stride` words apart; with
+// a power-of-two stride (2^26 rows = 256 MiB) the 32 limbs a chunk loads alias in the address
+// bits that pick the HBM channel.  MH_ASSIGN_PAD_ROWS overrides (A/B).
+uint64_t assign_pad_rows(uint64_t capacity) {
+    static const long long forced = [] {
+        const char* e = std::getenv("MH_ASSIGN_PAD_ROWS");
+        return e ? atoll(e) : -1ll;
+    }();
+    if (forced >= 0) return (uint64_t)forced;
+    (void)capacity;
+    return 0;
+}
+
 int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_assign** out) {
     if (!ctx || !out) return set_err(MH_E_INVALID, "null argument");
     *out = nullptr;
@@ -611,7 +625,8 @@ int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_ass
     ++ctx->children;
     as->n_vars = n_vars;
     as->capacity = capacity;
-    hipError_t e = hipMalloc(&as->d, (size_t)n_vars * 8 * capacity * sizeof(uint32_t));
+    as->stride = capacity + assign_pad_rows(capacity);
+    hipError_t e = hipMalloc(&as->d, (size_t)n_vars * 8 * as->stride * sizeof(uint32_t));
     if (e != hipSuccess) {
         mh_assign_destroy(as);
         return set_err(MH_E_NOMEM, std::string("assignment buffer: ") + hipGetErrorString(e));
@@ -640,7 +655,7 @@ int32_t mh_assign_upload(mh_assign* as, const uint32_t* host_soa, uint64_t first
         return set_err(MH_E_INVALID, "row range out of bounds");
     if (int32_t r = use_device(as->ctx)) return r;
     for (uint64_t col = 0; col < (uint64_t)as->n_vars * 8; ++col) {
-        MH_HIP(hipMemcpyAsync(as->d + col * as->capacity + first, host_soa + col * count,
+        MH_HIP(hipMemcpyAsync(as->d + col * as->stride + first, host_soa + col * count,
                               count * sizeof(uint32_t), hipMemcpyHostToDevice, as->ctx->stream));
     }
     MH_HIP(hipStreamSynchronize(as->ctx->stream));
@@ -657,7 +672,7 @@ int32_t mh_assign_download(const mh_assign* as, uint32_t* host_soa, uint64_t fir
     // one strided copy of every column-limb's [first, first + count) slice (a query reads one
     // witness row: one call instead of one per column-limb)
     MH_HIP(hipMemcpy2DAsync(host_soa, count * sizeof(uint32_t), as->d + first,
-                            as->capacity * sizeof(uint32_t), count * sizeof(uint32_t),
+                            as->stride * sizeof(uint32_t), count * sizeof(uint32_t),
                             (size_t)as->n_vars * 8, hipMemcpyDeviceToHost, as->ctx->stream));
     MH_HIP(hipStreamSynchronize(as->ctx->stream));
     return MH_OK;
@@ -666,7 +681,7 @@ int32_t mh_assign_download(const mh_assign* as, uint32_t* host_soa, uint64_t fir
 int32_t mh_assign_generate(mh_assign* as, uint64_t seed, uint64_t global_base) {
     if (!as) return set_err(MH_E_INVALID, "null handle");
     if (int32_t r = use_device(as->ctx)) return r;
-    MH_HIP(mh::launch_generate(as->d, as->capacity, as->n_vars, seed, global_base,
+    MH_HIP(mh::launch_generate(as->d, as->stride, as->capacity, as->n_vars, seed, global_base,
                                as->ctx->stream));
     return MH_OK;
 }
@@ -771,7 +786,7 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
     k.alt_off = as->d_guide + o_aoff;
     k.entry_col = as->d_guide + o_ecol;
     k.entry_val = as->d_guide + o_eval;
-    MH_HIP(mh::launch_generate_guided(as->d, as->capacity, first, count, seed, global_base, k,
+    MH_HIP(mh::launch_generate_guided(as->d, as->stride, first, count, seed, global_base, k,
                                       as->ctx->stream));
     return MH_OK;
 }

@@ -14,7 +14,7 @@ struct KParams {
     const uint32_t* consts;      // device constant pool, 8 limbs per entry
     const uint32_t* assign;      // SoA assignment buffer
     const uint32_t* tape_ids;    // the tapes this launch evaluates (one kernel-variant bucket)
-    uint64_t capacity;           // rows allocated per column
+    uint64_t capacity;           // column stride in words (>= rows allocated per column)
     uint32_t n_pre;              // columns preloaded into R0..R(n_pre-1)
     uint32_t n_ids;              // entries of tape_ids
     uint32_t result_base;        // results are indexed by tape id - result_base
@@ -40,8 +40,8 @@ inline uint32_t variant_of(uint32_t n_regs, uint32_t features) {
 constexpr uint32_t kNumVariants = 12;
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream);
-hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars, uint64_t seed,
-                           uint64_t base, hipStream_t stream);
+hipError_t launch_generate(uint32_t* assign, uint64_t stride, uint64_t rows, uint32_t n_vars,
+                           uint64_t seed, uint64_t base, hipStream_t stream);
 // Device form of mh_guide (pointers into one device buffer owned by the mh_assign).
 struct KGuide {
     uint32_t n_cols, n_sets;

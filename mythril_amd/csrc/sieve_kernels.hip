@@ -303,15 +303,15 @@ __device__ __forceinline__ void sieve_body(const KParams& p) {
     }
 }
 
-__global__ void __launch_bounds__(kBlock) generate_kernel(u32* assign, u64 capacity, u32 n_vars,
-                                                          u64 seed, u64 base) {
+__global__ void __launch_bounds__(kBlock) generate_kernel(u32* assign, u64 stride, u64 rows,
+                                                          u32 n_vars, u64 seed, u64 base) {
     const u64 row = (u64)blockIdx.x * kBlock + threadIdx.x;
-    if (row >= capacity) return;
+    if (row >= rows) return;
     for (u32 v = 0; v < n_vars; ++v) {
 #pragma unroll
         for (u32 k = 0; k < 8; ++k) {
             const u64 key = splitmix64(seed ^ (((u64)v * 8 + k) * 0xD1B54A32D192ED03ull));
-            assign[((u64)v * 8 + k) * capacity + row] = (u32)splitmix64(key ^ (base + row));
+            assign[((u64)v * 8 + k) * stride + row] = (u32)splitmix64(key ^ (base + row));
         }
     }
 }
@@ -422,6 +422,40 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink
             if constexpr (KIND == 20)
                 asm volatile(MB8("v_not_b32 %0, %0\n v_not_b32 %1, %1\n v_not_b32 %2, %2\n v_not_b32 %3, %3\n")
                              : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
+            // dependent chains (latency at one wave per SIMD, not throughput): one accumulator
+            if constexpr (KIND == 25) {  // v_mad_u64_u32 into one 64-bit accumulator
+                u64 m0 = ((u64)a1 << 32) | a0;
+                asm volatile(MB8("v_mad_u64_u32 %0, s[20:21], %1, %2, %0\n v_mad_u64_u32 %0, s[20:21], %1, %2, %0\n"
+                                 "v_mad_u64_u32 %0, s[20:21], %1, %2, %0\n v_mad_u64_u32 %0, s[20:21], %1, %2, %0\n")
+                             : "+v"(m0) : "v"(a2), "v"(y) : "s20", "s21");
+                a0 = (u32)m0; a1 = (u32)(m0 >> 32);
+            }
+            if constexpr (KIND == 26)  // v_add_u32 into one register
+                asm volatile(MB8("v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n"
+                                 "v_add_u32 %0, %0, %1\n") : "+v"(a0) : "v"(y));
+            if constexpr (KIND == 27)  // v_addc_co_u32 through VCC and one register
+                asm volatile("v_add_co_u32 %0, vcc, %0, %1\n"
+                             MB8("v_addc_co_u32 %0, vcc, %0, %1, vcc\n v_addc_co_u32 %0, vcc, %0, %1, vcc\n"
+                                 "v_addc_co_u32 %0, vcc, %0, %1, vcc\n v_addc_co_u32 %0, vcc, %0, %1, vcc\n")
+                             : "+v"(a0) : "v"(y) : "vcc");
+            if constexpr (KIND == 28) {  // two v_mad_u64_u32 accumulators interleaved
+                u64 m0 = ((u64)a1 << 32) | a0, m1 = ((u64)a3 << 32) | a2;
+                asm volatile(MB8("v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n v_mad_u64_u32 %1, s[22:23], %2, %3, %1\n"
+                                 "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n v_mad_u64_u32 %1, s[22:23], %2, %3, %1\n")
+                             : "+v"(m0), "+v"(m1) : "v"(a4), "v"(y) : "s20", "s21", "s22", "s23");
+                a0 = (u32)m0 ^ (u32)m1; a1 = (u32)(m0 >> 32) ^ (u32)(m1 >> 32);
+            }
+            if constexpr (KIND == 29) {  // product scanning: mad into the accumulator, carry count
+                u64 m0 = ((u64)a1 << 32) | a0;
+                asm volatile(MB8("v_mad_u64_u32 %0, vcc, %2, %3, %0\n v_addc_co_u32 %1, vcc, 0, %1, vcc\n")
+                             MB8("v_mad_u64_u32 %0, vcc, %2, %3, %0\n v_addc_co_u32 %1, vcc, 0, %1, vcc\n")
+                             : "+v"(m0), "+v"(a3) : "v"(a4), "v"(y) : "vcc");
+                a0 = (u32)m0; a1 = (u32)(m0 >> 32);
+            }
+            if constexpr (KIND == 30)  // v_cmp into VCC, then v_cndmask reading it (compare chains)
+                asm volatile(MB8("v_cmp_lt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc\n")
+                             MB8("v_cmp_lt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc\n")
+                             : "+v"(a0) : "v"(y) : "vcc");
             // partial EXEC masks: does the SIMD skip lane groups that are all inactive?
             if constexpr (KIND >= 21 && KIND <= 24) {
                 constexpr uint64_t kExec = KIND == 21 || KIND == 22 ? 0x00000000FFFFFFFFull
@@ -499,12 +533,12 @@ hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream) 
     }
 }
 
-hipError_t launch_generate(uint32_t* assign, uint64_t capacity, uint32_t n_vars, uint64_t seed,
-                           uint64_t base, hipStream_t stream) {
-    const u64 blocks = (capacity + kBlock - 1) / kBlock;
+hipError_t launch_generate(uint32_t* assign, uint64_t stride, uint64_t rows, uint32_t n_vars,
+                           uint64_t seed, uint64_t base, hipStream_t stream) {
+    const u64 blocks = (rows + kBlock - 1) / kBlock;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL(generate_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, assign,
-                       capacity, n_vars, seed, base);
+                       stride, rows, n_vars, seed, base);
     return hipGetLastError();
 }
 
@@ -516,7 +550,8 @@ hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uin
         MB_CASE(0) MB_CASE(1) MB_CASE(2) MB_CASE(3) MB_CASE(4) MB_CASE(5) MB_CASE(6) MB_CASE(7)
         MB_CASE(8) MB_CASE(9) MB_CASE(10) MB_CASE(11) MB_CASE(12) MB_CASE(13) MB_CASE(14)
         MB_CASE(15) MB_CASE(16) MB_CASE(17) MB_CASE(18) MB_CASE(19) MB_CASE(20)
-        MB_CASE(21) MB_CASE(22) MB_CASE(23) MB_CASE(24)
+        MB_CASE(21) MB_CASE(22) MB_CASE(23) MB_CASE(24) MB_CASE(25) MB_CASE(26) MB_CASE(27)
+        MB_CASE(28) MB_CASE(29) MB_CASE(30)
 #undef MB_CASE
         default: return hipErrorInvalidValue;
     }

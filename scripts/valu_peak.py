@@ -4,7 +4,7 @@ instruction kind at 1, 2, 4 and 8 waves per SIMD.  Prints one JSON object:
   {kind: {waves: lane-ops/s}}, plus the derived cycles per wave64 instruction per SIMD at the
   nominal 2.4 GHz clock (cycles = 1024 SIMDs x 2.4e9 x 64 / rate).
 
-    python scripts/valu_peak.py > profiles/<tag>/valu_peak.json
+    python scripts/valu_peak.py [kind names...] > profiles/<tag>/valu_peak.json
 """
 import json
 import os
@@ -18,7 +18,10 @@ from mythril_amd import native  # noqa: E402
 def main():
     ctx = native.Context(0)
     out = {"clock_ghz_nominal": 2.4, "simds": 1024, "kinds": {}}
+    only = set(sys.argv[1:])
     for kind, name in enumerate(native.MB_KINDS):
+        if only and name not in only:
+            continue
         row = {}
         for waves in (1, 2, 4, 8):
             r = ctx.microbench(kind, waves)
