@@ -264,8 +264,10 @@ int32_t mh_comm_destroy(mh_ctx* ctx);
  * 23 v_xor_b32 (low 16), 24 v_xor_b32 (every other lane); dependent chains (each instruction
  * reads the previous one's result: latency, at 1 wave per SIMD): 25 v_mad_u64_u32 into one
  * accumulator, 26 v_add_u32, 27 v_addc_co_u32 through VCC, 28 two v_mad_u64_u32 accumulators
- * interleaved, 29 v_mad_u64_u32 + v_addc carry count (product scanning), 30 v_cmp + v_cndmask. */
-#define MH_MB_NUM_KINDS 31
+ * interleaved, 29 v_mad_u64_u32 + v_addc carry count (product scanning), 30 v_cmp + v_cndmask;
+ * mixed classes (independent): 31 v_mad_u64_u32 / v_add_u32 alternating, 32 v_addc_co_u32
+ * chains / v_xor_b32 alternating, 33 two v_mad_u64_u32 per two v_add_u32.                    */
+#define MH_MB_NUM_KINDS 34
 int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
                             double* lane_ops_per_s);
 /* Round-1 form: kinds 0..2 of mh_microbench_issue at 8 waves per SIMD.                           */

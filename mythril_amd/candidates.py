@@ -143,6 +143,30 @@ def _memo(b: TapeBuilder, name: str) -> dict:
     return m
 
 
+HINTS_PER_COLUMN = 2  # single-column hint sets kept per column and direction
+
+
+def _prune_hints(hints: List[Tuple[int, List[Alt]]]) -> List[Tuple[int, List[Alt]]]:
+    """Drop dominated single-column hints.  The conditions of a calldata word's byte reads,
+    ``i < calldatasize`` for each byte index i (calldata.py:234-247), each give a boundary hint on
+    the size; every one is implied by the largest index's.  Per column, the sets with the
+    HINTS_PER_COLUMN largest and smallest values are kept (lower and upper bounds), in their
+    order; hints over several columns are all kept."""
+    by_col: Dict[str, List[int]] = {}
+    for i, (_, alts) in enumerate(hints):
+        cols = {c for a in alts for c in a}
+        if len(cols) == 1 and all(len(a) == 1 for a in alts):
+            by_col.setdefault(next(iter(cols)), []).append(i)
+    drop = set()
+    for c, idx in by_col.items():
+        if len(idx) <= 2 * HINTS_PER_COLUMN:
+            continue
+        hi = sorted(idx, key=lambda i: -max(a[c] for a in hints[i][1]))[:HINTS_PER_COLUMN]
+        lo = sorted(idx, key=lambda i: min(a[c] for a in hints[i][1]))[:HINTS_PER_COLUMN]
+        drop.update(set(idx) - set(hi) - set(lo))
+    return [h for i, h in enumerate(hints) if i not in drop]
+
+
 class Harvester:
     def __init__(self, b: TapeBuilder, schema: Schema, columns: Sequence[str]):
         self.b = b
@@ -526,8 +550,8 @@ class Harvester:
             if len(self.sets) >= MAX_SETS:
                 break
         # hints first: the exact requirements of the conjuncts (later sets) override them
-        self.sets = self.sets[:1] + self.hints + self.sets[1:] if parent else \
-            self.hints + self.sets
+        hints = _prune_hints(self.hints)
+        self.sets = self.sets[:1] + hints + self.sets[1:] if parent else hints + self.sets
         pools = self.pools
         for _, alts in self.sets:
             for alt in alts:

@@ -719,6 +719,14 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
     const uint32_t n_ent = ns ? g->alt_off[n_alts] : 0;
     if (n_ent && (!g->entry_col || !g->entry_val))
         return set_err(MH_E_INVALID, "guide: null entry arrays");
+    // the leading sets without a copy entry (the kernel resolves their writes in LDS)
+    uint32_t n_value_sets = 0;
+    for (bool copy = false; n_value_sets < ns && !copy; ) {
+        for (uint32_t e = g->alt_off[g->set_off[n_value_sets]];
+             e < g->alt_off[g->set_off[n_value_sets + 1]] && !copy; ++e)
+            copy = (g->entry_col[e] & MH_GUIDE_COPY) != 0;
+        if (!copy) ++n_value_sets;
+    }
     for (uint32_t e = 0; e < n_ent; ++e) {
         const uint32_t c = g->entry_col[e];
         const uint32_t dst = c & ~MH_GUIDE_COPY;
@@ -778,6 +786,9 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
     mh::KGuide k;
     k.n_cols = nc;
     k.n_sets = ns;
+    k.n_value_sets = n_value_sets;
+    k.n_alts = n_alts;
+    k.n_entries = n_ent;
     k.width = as->d_guide + o_width;
     k.pool_off = as->d_guide + o_poff;
     k.pool = as->d_guide + o_pool;

@@ -1,5 +1,5 @@
 // Guided candidate generator (mh_assign_generate_guided): one thread per assignment row, SoA
-// writes (column v limb k of row r at word (v*8 + k)*capacity + r), so a wave's 64 lanes store
+// writes (column v limb k of row r at word (v*8 + k)*stride + r), so a wave's 64 lanes store
 // 256 contiguous bytes per limb.  The semantics are stated in include/mythril_hip.h and restated
 // bit for bit in oracle/guided_gen.py; the harvest that fills the guide is
 // mythril_amd/candidates.py.  Off the hot path: written once per query, before the sieve reads it.
@@ -52,77 +52,148 @@ __device__ void extract_bits(const u32* v, u32 lo, u32 n, u32* out) {
     for (u32 k = 0; k < 8; ++k) out[k] &= limb_mask(n, k);
 }
 
+// the column's generated value before any set applies: a small value, uniform limbs, or a draw
+// from the column's pool
+__device__ __forceinline__ void base_value(const mh::KGuide& g, u32 v, u64 seed, u64 gidx, u32* val) {
+    const u32 m0 = gen_limb(seed ^ kSaltMode, v, gidx, 0);
+    const u32 mode = m0 & 0xFFu;
+    const u32 plo = g.pool_off[v], phi = g.pool_off[v + 1];
+    if (mode < 64) {
+        val[0] = (m0 >> 8) & 0xFFu;
+#pragma unroll
+        for (u32 k = 1; k < 8; ++k) val[k] = 0;
+    } else if (mode < 128 || phi == plo) {
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) val[k] = gen_limb(seed, v, gidx, k);
+    } else {
+        const u32 m1 = gen_limb(seed ^ kSaltMode, v, gidx, 1);
+        const u32* src = g.pool + (u64)(plo + m1 % (phi - plo)) * 8;
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) val[k] = src[k];
+    }
+}
+
+// the alternative set j applies to this row, or ~0u (a per-row draw against the set's probability)
+__device__ __forceinline__ u32 chosen_alt(const mh::KGuide& g, u32 j, u64 seed, u64 gidx) {
+    const u32 s = gen_limb(seed ^ kSaltSet, j, gidx, 0);
+    const u32 a0 = g.set_off[j], n_alt = g.set_off[j + 1] - a0;
+    if ((s & 0xFFu) >= g.set_prob[j] || n_alt == 0) return ~0u;
+    return a0 + (s >> 8) % n_alt;
+}
+
+// one entry applied to the row in memory: a value, or bits copied from another column
+__device__ void apply_entry(u32* assign, u64 stride, u64 row, const mh::KGuide& g, u32 e) {
+    const u32 c = g.entry_col[e];
+    const u32* ev = g.entry_val + (u64)e * 8;
+    if (c & kCopy) {
+        const u32 dst = c & ~kCopy, src = ev[0], dlo = ev[1], slo = ev[2], nb = ev[3];
+        u32 sv[8], bits[8], dv[8], m[8], one[8];
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) {
+            sv[k] = assign[((u64)src * 8 + k) * stride + row];
+            dv[k] = assign[((u64)dst * 8 + k) * stride + row];
+        }
+        extract_bits(sv, slo, nb, bits);
+        // shift bits and an nb-wide mask left by dlo
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) one[k] = limb_mask(nb, k);
+        const u32 q = dlo >> 5, r = dlo & 31;
+#pragma unroll
+        for (int k = 7; k >= 0; --k) {
+            const int s0 = k - (int)q, s1 = k - (int)q - 1;
+            const u32 ba = s0 >= 0 ? bits[s0] : 0u, bb = s1 >= 0 ? bits[s1] : 0u;
+            const u32 ma = s0 >= 0 ? one[s0] : 0u, mb = s1 >= 0 ? one[s1] : 0u;
+            sv[k] = r ? ((ba << r) | (bb >> (32 - r))) : ba;
+            m[k] = r ? ((ma << r) | (mb >> (32 - r))) : ma;
+        }
+        const u32 w = g.width[dst];
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k)
+            assign[((u64)dst * 8 + k) * stride + row] =
+                ((dv[k] & ~m[k]) | (sv[k] & m[k])) & limb_mask(w, k);
+    } else {
+        const u32 w = g.width[c];
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k)
+            assign[((u64)c * 8 + k) * stride + row] = ev[k] & limb_mask(w, k);
+    }
+}
+
+// Every column's base value written, then every set applied in order, in memory.
 __global__ void __launch_bounds__(kBlock)
-    guided_kernel(u32* assign, u64 capacity, u64 first, u64 count, u64 seed, u64 base,
+    guided_kernel(u32* assign, u64 stride, u64 first, u64 count, u64 seed, u64 base,
                   mh::KGuide g) {
     const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
     if (i >= count) return;
     const u64 row = first + i;
     const u64 gidx = base + row;
     for (u32 v = 0; v < g.n_cols; ++v) {
-        const u32 w = g.width[v];
-        const u32 m0 = gen_limb(seed ^ kSaltMode, v, gidx, 0);
-        const u32 mode = m0 & 0xFFu;
-        const u32 plo = g.pool_off[v], phi = g.pool_off[v + 1];
         u32 val[8];
-        if (mode < 64) {
-            val[0] = (m0 >> 8) & 0xFFu;
-#pragma unroll
-            for (u32 k = 1; k < 8; ++k) val[k] = 0;
-        } else if (mode < 128 || phi == plo) {
-#pragma unroll
-            for (u32 k = 0; k < 8; ++k) val[k] = gen_limb(seed, v, gidx, k);
-        } else {
-            const u32 m1 = gen_limb(seed ^ kSaltMode, v, gidx, 1);
-            const u32* src = g.pool + (u64)(plo + m1 % (phi - plo)) * 8;
-#pragma unroll
-            for (u32 k = 0; k < 8; ++k) val[k] = src[k];
-        }
+        base_value(g, v, seed, gidx, val);
+        const u32 w = g.width[v];
 #pragma unroll
         for (u32 k = 0; k < 8; ++k)
-            assign[((u64)v * 8 + k) * capacity + row] = val[k] & limb_mask(w, k);
+            assign[((u64)v * 8 + k) * stride + row] = val[k] & limb_mask(w, k);
     }
     for (u32 j = 0; j < g.n_sets; ++j) {
-        const u32 s = gen_limb(seed ^ kSaltSet, j, gidx, 0);
-        const u32 a0 = g.set_off[j], n_alt = g.set_off[j + 1] - a0;
-        if ((s & 0xFFu) >= g.set_prob[j] || n_alt == 0) continue;
-        const u32 alt = a0 + (s >> 8) % n_alt;
-        for (u32 e = g.alt_off[alt]; e < g.alt_off[alt + 1]; ++e) {
-            const u32 c = g.entry_col[e];
-            const u32* ev = g.entry_val + (u64)e * 8;
-            if (c & kCopy) {
-                const u32 dst = c & ~kCopy, src = ev[0], dlo = ev[1], slo = ev[2], nb = ev[3];
-                u32 sv[8], bits[8], dv[8], m[8], one[8];
+        const u32 alt = chosen_alt(g, j, seed, gidx);
+        if (alt == ~0u) continue;
+        for (u32 e = g.alt_off[alt]; e < g.alt_off[alt + 1]; ++e) apply_entry(assign, stride, row, g, e);
+    }
+}
+
+// The same rows, with the leading value-only sets resolved in LDS: a value entry only decides
+// which value a column ends with (the last one applied), so each lane records the last entry
+// per column (its own LDS slots: [column][lane]) and every column is written once; the sets
+// from the first one with a copy entry on run in memory as above.  The alternative and entry
+// offsets of those sets are staged in LDS too: each lane walks its own alternatives, so in
+// memory every set cost two or three dependent vector loads.  A query's guide holds hundreds of
+// sets; the in-memory form stored 8 limbs per applied entry, lane-divergently
+// (profiles/r03h: 0.20 ms per launch on average, up to 0.58).
+constexpr u32 kNoEntry = 0xFFFFFFFFu;
+constexpr u32 kLdsRows = 64;
+
+__global__ void __launch_bounds__(kLdsRows)
+    guided_lds_kernel(u32* assign, u64 stride, u64 first, u64 count, u64 seed, u64 base,
+                      mh::KGuide g) {
+    extern __shared__ u32 s_lds[];
+    u32* s_last = s_lds;                               // [n_cols][kLdsRows]
+    u32* s_alt = s_lds + g.n_cols * kLdsRows;          // alt_off of the value sets
+    const u32 n_alt_v = g.set_off[g.n_value_sets];     // alternatives of the value sets
+    u32* s_ecol = s_alt + n_alt_v + 1;                 // entry_col of their entries
+    const u32 n_ent_v = g.alt_off[n_alt_v];
+    const u32 lane = threadIdx.x;
+    for (u32 k = lane; k <= n_alt_v; k += kLdsRows) s_alt[k] = g.alt_off[k];
+    for (u32 k = lane; k < n_ent_v; k += kLdsRows) s_ecol[k] = g.entry_col[k];
+    __syncthreads();
+    const u64 i = (u64)blockIdx.x * kLdsRows + lane;
+    if (i >= count) return;  // past the barrier; lanes touch only their own s_last slots
+    const u64 row = first + i;
+    const u64 gidx = base + row;
+    for (u32 v = 0; v < g.n_cols; ++v) s_last[v * kLdsRows + lane] = kNoEntry;
+    for (u32 j = 0; j < g.n_value_sets; ++j) {
+        const u32 alt = chosen_alt(g, j, seed, gidx);
+        if (alt == ~0u) continue;
+        for (u32 e = s_alt[alt]; e < s_alt[alt + 1]; ++e) s_last[s_ecol[e] * kLdsRows + lane] = e;
+    }
+    for (u32 v = 0; v < g.n_cols; ++v) {
+        const u32 e = s_last[v * kLdsRows + lane];
+        u32 val[8];
+        if (e == kNoEntry) {
+            base_value(g, v, seed, gidx, val);
+        } else {
 #pragma unroll
-                for (u32 k = 0; k < 8; ++k) {
-                    sv[k] = assign[((u64)src * 8 + k) * capacity + row];
-                    dv[k] = assign[((u64)dst * 8 + k) * capacity + row];
-                }
-                extract_bits(sv, slo, nb, bits);
-                // shift bits and an nb-wide mask left by dlo
-#pragma unroll
-                for (u32 k = 0; k < 8; ++k) one[k] = limb_mask(nb, k);
-                const u32 q = dlo >> 5, r = dlo & 31;
-#pragma unroll
-                for (int k = 7; k >= 0; --k) {
-                    const int s0 = k - (int)q, s1 = k - (int)q - 1;
-                    const u32 ba = s0 >= 0 ? bits[s0] : 0u, bb = s1 >= 0 ? bits[s1] : 0u;
-                    const u32 ma = s0 >= 0 ? one[s0] : 0u, mb = s1 >= 0 ? one[s1] : 0u;
-                    sv[k] = r ? ((ba << r) | (bb >> (32 - r))) : ba;
-                    m[k] = r ? ((ma << r) | (mb >> (32 - r))) : ma;
-                }
-                const u32 w = g.width[dst];
-#pragma unroll
-                for (u32 k = 0; k < 8; ++k)
-                    assign[((u64)dst * 8 + k) * capacity + row] =
-                        ((dv[k] & ~m[k]) | (sv[k] & m[k])) & limb_mask(w, k);
-            } else {
-                const u32 w = g.width[c];
-#pragma unroll
-                for (u32 k = 0; k < 8; ++k)
-                    assign[((u64)c * 8 + k) * capacity + row] = ev[k] & limb_mask(w, k);
-            }
+            for (u32 k = 0; k < 8; ++k) val[k] = g.entry_val[(u64)e * 8 + k];
         }
+        const u32 w = g.width[v];
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k)
+            assign[((u64)v * 8 + k) * stride + row] = val[k] & limb_mask(w, k);
+    }
+    for (u32 j = g.n_value_sets; j < g.n_sets; ++j) {
+        const u32 alt = chosen_alt(g, j, seed, gidx);
+        if (alt == ~0u) continue;
+        for (u32 e = g.alt_off[alt]; e < g.alt_off[alt + 1]; ++e) apply_entry(assign, stride, row, g, e);
     }
 }
 
@@ -130,13 +201,23 @@ __global__ void __launch_bounds__(kBlock)
 
 namespace mh {
 
-hipError_t launch_generate_guided(uint32_t* assign, uint64_t capacity, uint64_t first,
+hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
                                   hipStream_t stream) {
-    const u64 blocks = (count + kBlock - 1) / kBlock;
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(guided_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, assign,
-                       capacity, first, count, seed, base, g);
+    if (count == 0) return hipSuccess;
+    // LDS form while the last-entry slots (256 B per column) and the value sets' offsets fit
+    // 64 KB per 64-row workgroup; the host counts the value sets' alternatives and entries as
+    // n_alts / n_entries bound them
+    const size_t lds = ((size_t)g.n_cols * kLdsRows + g.n_alts + 1 + g.n_entries) * sizeof(u32);
+    if (g.n_cols && lds <= 64 * 1024) {
+        const u64 blocks = (count + kLdsRows - 1) / kLdsRows;
+        hipLaunchKernelGGL(guided_lds_kernel, dim3((unsigned)blocks), dim3(kLdsRows), lds, stream,
+                           assign, stride, first, count, seed, base, g);
+    } else {
+        const u64 blocks = (count + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL(guided_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, assign,
+                           stride, first, count, seed, base, g);
+    }
     return hipGetLastError();
 }
 

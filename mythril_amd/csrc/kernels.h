@@ -45,6 +45,8 @@ hipError_t launch_generate(uint32_t* assign, uint64_t stride, uint64_t rows, uin
 // Device form of mh_guide (pointers into one device buffer owned by the mh_assign).
 struct KGuide {
     uint32_t n_cols, n_sets;
+    uint32_t n_value_sets;      // sets [0, n_value_sets) hold no copy entry
+    uint32_t n_alts, n_entries; // set_off[n_sets], alt_off[n_alts]
     const uint32_t* width;      // [n_cols]
     const uint32_t* pool_off;   // [n_cols + 1]
     const uint32_t* pool;       // x 8 limbs
@@ -54,7 +56,7 @@ struct KGuide {
     const uint32_t* entry_col;  // [n_entries]
     const uint32_t* entry_val;  // x 8 limbs
 };
-hipError_t launch_generate_guided(uint32_t* assign, uint64_t capacity, uint64_t first,
+hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
                                   hipStream_t stream);
 hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uint32_t* sink,

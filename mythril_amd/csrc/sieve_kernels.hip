@@ -456,6 +456,26 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink
                 asm volatile(MB8("v_cmp_lt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc\n")
                              MB8("v_cmp_lt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc\n")
                              : "+v"(a0) : "v"(y) : "vcc");
+            // mixed classes (independent): do quarter-rate and full-rate issue costs add?
+            if constexpr (KIND == 31) {  // v_mad_u64_u32 / v_add_u32 alternating
+                u64 m0 = ((u64)a1 << 32) | a0, m1 = ((u64)a3 << 32) | a2;
+                asm volatile(MB8("v_mad_u64_u32 %0, s[20:21], %4, %5, %0\n v_add_u32 %2, %2, %5\n"
+                                 "v_mad_u64_u32 %1, s[22:23], %4, %5, %1\n v_add_u32 %3, %3, %5\n")
+                             : "+v"(m0), "+v"(m1), "+v"(a4), "+v"(a5) : "v"(a6), "v"(y)
+                             : "s20", "s21", "s22", "s23");
+                a0 = (u32)m0 ^ (u32)m1; a1 = (u32)(m0 >> 32) ^ (u32)(m1 >> 32);
+            }
+            if constexpr (KIND == 32)  // v_addc_co_u32 chain / v_xor_b32 alternating
+                asm volatile("v_add_co_u32 %0, vcc, %0, %4\n"
+                             MB8("v_addc_co_u32 %0, vcc, %0, %4, vcc\n v_xor_b32 %2, %2, %4\n"
+                                 "v_addc_co_u32 %1, vcc, %1, %4, vcc\n v_xor_b32 %3, %3, %4\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(y) : "vcc");
+            if constexpr (KIND == 33)  // two v_mad_u64_u32 per v_add_u32 (the multiply's mix)
+                asm volatile(MB8("v_mad_u64_u32 v[40:41], s[20:21], %4, %5, v[40:41]\n"
+                                 "v_mad_u64_u32 v[42:43], s[22:23], %4, %5, v[42:43]\n"
+                                 "v_add_u32 %0, %0, %5\n v_add_u32 %1, %1, %5\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a6), "v"(y)
+                             : "s20", "s21", "s22", "s23", "v40", "v41", "v42", "v43");
             // partial EXEC masks: does the SIMD skip lane groups that are all inactive?
             if constexpr (KIND >= 21 && KIND <= 24) {
                 constexpr uint64_t kExec = KIND == 21 || KIND == 22 ? 0x00000000FFFFFFFFull
@@ -551,7 +571,7 @@ hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uin
         MB_CASE(8) MB_CASE(9) MB_CASE(10) MB_CASE(11) MB_CASE(12) MB_CASE(13) MB_CASE(14)
         MB_CASE(15) MB_CASE(16) MB_CASE(17) MB_CASE(18) MB_CASE(19) MB_CASE(20)
         MB_CASE(21) MB_CASE(22) MB_CASE(23) MB_CASE(24) MB_CASE(25) MB_CASE(26) MB_CASE(27)
-        MB_CASE(28) MB_CASE(29) MB_CASE(30)
+        MB_CASE(28) MB_CASE(29) MB_CASE(30) MB_CASE(31) MB_CASE(32) MB_CASE(33)
 #undef MB_CASE
         default: return hipErrorInvalidValue;
     }

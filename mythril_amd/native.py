@@ -87,7 +87,8 @@ MB_KINDS = ("add_co_chain", "mad_u64_u32", "add_u32", "xor_b32", "alignbit_b32",
             "cndmask_e32_vcc", "cmp_eq_e32", "xor_literal", "lshlrev_b32", "add3_u32", "fma_f64",
             "xnor_b32", "and_b32", "or_b32", "not_b32", "xor_exec32", "alignbit_exec32",
             "xor_exec16", "xor_exec_alt", "dep_mad_u64_u32", "dep_add_u32", "dep_addc_vcc",
-            "dep_mad_2chains", "dep_mad_carry", "dep_cmp_cndmask")
+            "dep_mad_2chains", "dep_mad_carry", "dep_cmp_cndmask", "mix_mad_add", "mix_addc_xor",
+            "mix_mad2_add2")
 
 
 class NativeUnavailable(RuntimeError):

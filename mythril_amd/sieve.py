@@ -164,7 +164,7 @@ def rematerialize(nodes: np.ndarray, max_size: int) -> np.ndarray:
 class Sieve:
     """A device context plus reusable buffers; one per thread (handles are not shared)."""
 
-    def __init__(self, device: int = 0, rows: int = 1 << 16, max_rounds: int = 4,
+    def __init__(self, device: int = 0, rows: int = 1 << 16, max_rounds: int = 2,
                  seed: int = 0x5EED5EED, budget_s: float = 0.25, first_rows: int = 256):
         self.ctx = native.Context(device)
         self.rows = rows
@@ -172,6 +172,10 @@ class Sieve:
         # SAT witness of tests/laser_like.py within the first 16 rows): a small first round
         # answers those at a fraction of the latency, the full-size rounds follow
         self.first_rows = min(first_rows, rows)
+        # a miss pays every round before z3 runs (an infeasible JUMPI branch, svm.py:257-262):
+        # one 2^16-row round after the guided 256 keeps a miss near 1 ms of device time
+        # (profiles/r03f: three such rounds took 1.6-2.3 ms) while no LASER-shaped SAT query
+        # needed more than the first 256 rows
         self.max_rounds = max_rounds
         self.seed = seed
         self.budget_s = budget_s

@@ -1,7 +1,7 @@
 """ORACLE (test infrastructure only — never imported by the product path).
 
 Restatement of the guided candidate generator ``mh_assign_generate_guided``
-(include/mythril_hip.h, mythril_amd/csrc/sieve_kernels.hip ``guided_kernel``), bit for bit:
+(include/mythril_hip.h, mythril_amd/csrc/generate.hip ``guided_kernel`` / ``guided_lds_kernel``), bit for bit:
 
     g = global_base + row
     per column v (width w, pool P_v):

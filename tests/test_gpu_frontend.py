@@ -56,6 +56,56 @@ def test_guided_generator_matches_oracle(gpu_ctx, qi):
             assert gv == wv, (qi, r, cols[v])
 
 
+def _random_guide(rng, n_cols, n_sets):
+    """Guide arrays in mh_guide order with value and copy sets in random order (the generator's
+    LDS form resolves the leading value-only sets, the rest run in memory)."""
+    width = rng.choice([1, 8, 32, 160, 256], size=n_cols).astype(np.uint16)
+    pool_n = rng.integers(0, 4, size=n_cols)
+    pool_off = np.concatenate([[0], np.cumsum(pool_n)]).astype(np.uint32)
+    pool = rng.integers(0, 1 << 32, size=(max(int(pool_off[-1]), 1), 8), dtype=np.uint64)
+    set_off, alt_off, e_col, e_val, prob = [0], [0], [], [], []
+    for j in range(n_sets):
+        copy = rng.random() < 0.2
+        for _ in range(int(rng.integers(1, 4))):
+            for _ in range(int(rng.integers(1, 6))):
+                c = int(rng.integers(0, n_cols))
+                if copy:
+                    src = int(rng.integers(0, n_cols))
+                    nb = int(rng.integers(1, 65))
+                    e_col.append(c | 0x80000000)
+                    e_val.append([src, int(rng.integers(0, 192)), int(rng.integers(0, 192)), nb,
+                                  0, 0, 0, 0])
+                else:
+                    e_col.append(c)
+                    e_val.append(list(rng.integers(0, 1 << 32, size=8)))
+            alt_off.append(len(e_col))
+        set_off.append(len(alt_off) - 1)
+        prob.append(int(rng.integers(0, 256)))
+    return dict(width=width, pool_off=pool_off, pool=pool.astype(np.uint32),
+                set_off=np.array(set_off, dtype=np.uint32),
+                set_prob=np.array(prob or [0], dtype=np.uint8),
+                alt_off=np.array(alt_off, dtype=np.uint32),
+                entry_col=np.array(e_col or [0], dtype=np.uint32),
+                entry_val=np.array(e_val or [[0] * 8], dtype=np.uint64).astype(np.uint32))
+
+
+@pytest.mark.parametrize("n_cols,n_sets", [(7, 60), (150, 300), (200, 100)])
+def test_guided_generator_random_guides(gpu_ctx, n_cols, n_sets):
+    """Random guides (value and copy sets interleaved, up to 200 columns: past the LDS form's
+    192) against oracle/guided_gen.py, bit for bit on sampled rows."""
+    rng = np.random.default_rng(n_cols * 1000 + n_sets)
+    arrays = _random_guide(rng, n_cols, n_sets)
+    rows, seed, base = 200, 0xABCD + n_cols, 1 << 30
+    a = gpu_ctx.assignments(n_cols, rows)
+    a.generate_guided(seed, arrays, global_base=base, first=0, count=rows)
+    got = a.download(0, rows)
+    for r in list(range(0, rows, 23)) + [rows - 1]:
+        want = generate_row(seed, base + r, arrays)
+        for v, wv in enumerate(want):
+            gv = sum(int(got[v, k, r]) << (32 * k) for k in range(8))
+            assert gv == wv, (n_cols, r, v)
+
+
 def test_guided_generator_rejects_malformed_guides(gpu_ctx):
     ctx, qs = queries()
     _, cs = qs[0]
