@@ -787,8 +787,6 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
     k.n_cols = nc;
     k.n_sets = ns;
     k.n_value_sets = n_value_sets;
-    k.n_alts = n_alts;
-    k.n_entries = n_ent;
     k.width = as->d_guide + o_width;
     k.pool_off = as->d_guide + o_poff;
     k.pool = as->d_guide + o_pool;

@@ -142,54 +142,57 @@ __global__ void __launch_bounds__(kBlock)
     }
 }
 
-// The same rows, with the leading value-only sets resolved in LDS: a value entry only decides
-// which value a column ends with (the last one applied), so each lane records the last entry
-// per column (its own LDS slots: [column][lane]) and every column is written once; the sets
-// from the first one with a copy entry on run in memory as above.  The alternative and entry
-// offsets of those sets are staged in LDS too: each lane walks its own alternatives, so in
-// memory every set cost two or three dependent vector loads.  A query's guide holds hundreds of
-// sets; the in-memory form stored 8 limbs per applied entry, lane-divergently
-// (profiles/r03h: 0.20 ms per launch on average, up to 0.58).
-constexpr u32 kNoEntry = 0xFFFFFFFFu;
+// The same rows, spread over kWaves waves per 64 rows, with the leading value-only sets
+// resolved in LDS: a value entry only decides which value a column ends with -- the last one
+// applied, i.e. the largest entry index, since entries are laid out in set order -- so the waves
+// split the sets, each lane drawing its row's alternative of a set and keeping the largest
+// entry per column with an LDS atomic max ([column][row] slots); then the waves split the
+// columns and write each column of each row once (the base value, or the winning entry's).  The
+// sets from the first one with a copy entry on run in memory, in order, on wave 0.  The one-lane-
+// per-row form stored 8 limbs per applied entry, lane-divergently, and left a 256-row launch
+// four waves: 0.20 ms per launch on average, up to 0.58 (profiles/r03h).
 constexpr u32 kLdsRows = 64;
+constexpr u32 kWaves = 8;
 
-__global__ void __launch_bounds__(kLdsRows)
+__global__ void __launch_bounds__(kLdsRows * kWaves)
     guided_lds_kernel(u32* assign, u64 stride, u64 first, u64 count, u64 seed, u64 base,
                       mh::KGuide g) {
-    extern __shared__ u32 s_lds[];
-    u32* s_last = s_lds;                               // [n_cols][kLdsRows]
-    u32* s_alt = s_lds + g.n_cols * kLdsRows;          // alt_off of the value sets
-    const u32 n_alt_v = g.set_off[g.n_value_sets];     // alternatives of the value sets
-    u32* s_ecol = s_alt + n_alt_v + 1;                 // entry_col of their entries
-    const u32 n_ent_v = g.alt_off[n_alt_v];
-    const u32 lane = threadIdx.x;
-    for (u32 k = lane; k <= n_alt_v; k += kLdsRows) s_alt[k] = g.alt_off[k];
-    for (u32 k = lane; k < n_ent_v; k += kLdsRows) s_ecol[k] = g.entry_col[k];
+    extern __shared__ u32 s_last[];  // [n_cols][kLdsRows]: 1 + the winning entry, 0 = none
+    const u32 lane = threadIdx.x % kLdsRows, wave = threadIdx.x / kLdsRows;
+    for (u32 k = threadIdx.x; k < g.n_cols * kLdsRows; k += kLdsRows * kWaves) s_last[k] = 0;
     __syncthreads();
     const u64 i = (u64)blockIdx.x * kLdsRows + lane;
-    if (i >= count) return;  // past the barrier; lanes touch only their own s_last slots
-    const u64 row = first + i;
+    const bool live = i < count;
+    const u64 row = first + (live ? i : 0);
     const u64 gidx = base + row;
-    for (u32 v = 0; v < g.n_cols; ++v) s_last[v * kLdsRows + lane] = kNoEntry;
-    for (u32 j = 0; j < g.n_value_sets; ++j) {
-        const u32 alt = chosen_alt(g, j, seed, gidx);
-        if (alt == ~0u) continue;
-        for (u32 e = s_alt[alt]; e < s_alt[alt + 1]; ++e) s_last[s_ecol[e] * kLdsRows + lane] = e;
-    }
-    for (u32 v = 0; v < g.n_cols; ++v) {
-        const u32 e = s_last[v * kLdsRows + lane];
-        u32 val[8];
-        if (e == kNoEntry) {
-            base_value(g, v, seed, gidx, val);
-        } else {
-#pragma unroll
-            for (u32 k = 0; k < 8; ++k) val[k] = g.entry_val[(u64)e * 8 + k];
+    if (live) {
+        for (u32 j = wave; j < g.n_value_sets; j += kWaves) {
+            const u32 alt = chosen_alt(g, j, seed, gidx);
+            if (alt == ~0u) continue;
+            for (u32 e = g.alt_off[alt]; e < g.alt_off[alt + 1]; ++e)
+                atomicMax(&s_last[g.entry_col[e] * kLdsRows + lane], e + 1);
         }
-        const u32 w = g.width[v];
-#pragma unroll
-        for (u32 k = 0; k < 8; ++k)
-            assign[((u64)v * 8 + k) * stride + row] = val[k] & limb_mask(w, k);
     }
+    __syncthreads();
+    if (live) {
+        for (u32 v = wave; v < g.n_cols; v += kWaves) {
+            const u32 e = s_last[v * kLdsRows + lane];
+            u32 val[8];
+            if (e == 0) {
+                base_value(g, v, seed, gidx, val);
+            } else {
+#pragma unroll
+                for (u32 k = 0; k < 8; ++k) val[k] = g.entry_val[(u64)(e - 1) * 8 + k];
+            }
+            const u32 w = g.width[v];
+#pragma unroll
+            for (u32 k = 0; k < 8; ++k)
+                assign[((u64)v * 8 + k) * stride + row] = val[k] & limb_mask(w, k);
+        }
+    }
+    if (g.n_value_sets == g.n_sets) return;
+    __syncthreads();  // every column written (and visible to the workgroup) before the copies
+    if (!live || wave != 0) return;
     for (u32 j = g.n_value_sets; j < g.n_sets; ++j) {
         const u32 alt = chosen_alt(g, j, seed, gidx);
         if (alt == ~0u) continue;
@@ -205,14 +208,12 @@ hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t fi
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
                                   hipStream_t stream) {
     if (count == 0) return hipSuccess;
-    // LDS form while the last-entry slots (256 B per column) and the value sets' offsets fit
-    // 64 KB per 64-row workgroup; the host counts the value sets' alternatives and entries as
-    // n_alts / n_entries bound them
-    const size_t lds = ((size_t)g.n_cols * kLdsRows + g.n_alts + 1 + g.n_entries) * sizeof(u32);
-    if (g.n_cols && lds <= 64 * 1024) {
+    // LDS form while the last-entry slots (256 B per column) fit 48 KB per workgroup
+    const size_t lds = (size_t)g.n_cols * kLdsRows * sizeof(u32);
+    if (g.n_cols && lds <= 48 * 1024) {
         const u64 blocks = (count + kLdsRows - 1) / kLdsRows;
-        hipLaunchKernelGGL(guided_lds_kernel, dim3((unsigned)blocks), dim3(kLdsRows), lds, stream,
-                           assign, stride, first, count, seed, base, g);
+        hipLaunchKernelGGL(guided_lds_kernel, dim3((unsigned)blocks), dim3(kLdsRows * kWaves), lds,
+                           stream, assign, stride, first, count, seed, base, g);
     } else {
         const u64 blocks = (count + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(guided_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, assign,

@@ -121,7 +121,8 @@ private:
                               op == M_V_OR3 || op == M_V_ALIGNBIT || op == M_V_MAD_U64_U32 ||
                               op == M_V_LSHL_ADD || op == M_V_PERM || op == M_V_BFI ||
                               op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
-                              (op >= M_V_CMP_EQ && op <= M_V_CMP_GT_I32) || op >= M_V_CVT_F64_U32;
+                              (op >= M_V_CMP_EQ && op <= M_V_CMP_GT_I32) || op >= M_V_CVT_F64_U32 ||
+                              op == M_V_RCP_F32 || op == M_V_CMP_GT_F32 || op == M_V_CMP_LE_F32;
             if (wide) ++n_wide_;
             if (cur_op_ >= 0) { ++op_valu[cur_op_]; op_wide[cur_op_] += wide; }
         } else if (op <= M_S_CMP_LT_U32) {
@@ -1952,6 +1953,14 @@ const char* op_name(uint16_t op) {
         case M_V_LSHL_ADD: return "v_lshl_add_u32";
         case M_V_PERM: return "v_perm_b32";
         case M_V_BFI: return "v_bfi_b32";
+        case M_V_CVT_F32_U32: return "v_cvt_f32_u32";
+        case M_V_FMA_F32: return "v_fma_f32";
+        case M_V_RCP_F32: return "v_rcp_f32";
+        case M_V_MUL_F32: return "v_mul_f32";
+        case M_V_CVT_U32_F32: return "v_cvt_u32_f32";
+        case M_V_FRACT_F32: return "v_fract_f32";
+        case M_V_CMP_GT_F32: return "v_cmp_gt_f32";
+        case M_V_CMP_LE_F32: return "v_cmp_le_f32";
         case M_V_CVT_F64_U32: return "v_cvt_f64_u32";
         case M_V_FMA_F64: return "v_fma_f64";
         case M_V_RCP_F64: return "v_rcp_f64";
@@ -2043,7 +2052,8 @@ std::vector<MI> div_routine() {
     const Opnd K64LO = S(S_DIV_F64K), K64HI = S(S_DIV_F64K + 1);
     enum : uint32_t { L_UNS = 1, L_DONE, L_TOP3, L_CONV, L_ZQ, L_NOZQ, L_STEP0 = 10, L_NONEG0 = 20, L_NOGE0 = 30, L_WB = 40,
                       L_SDIV, L_SREM, L_SMOD, L_NARROW = 50, L_NNEG0 = 60, L_NGE0 = 70,
-                      L_NOYZ = 80, L_CZ0 = 90, L_RLT = 100, L_RLTD, L_YSLOW, L_YDONE, L_TOPALL };
+                      L_NOYZ = 80, L_CZ0 = 90, L_RLT = 100, L_RLTD, L_YSLOW, L_YDONE, L_TOPALL,
+                      L_F32 = 110, L_F32OK, L_STEP0_BODY };
     auto to_f64 = [&](Opnd dst, Opnd (*limb)(int)) {
         E(M_S_MOV_B32, {K64LO, IMM(0)});
         E(M_S_MOV_B32, {K64HI, IMM(0x41f00000u)});
@@ -2128,11 +2138,42 @@ std::vector<MI> div_routine() {
     };
     E(M_V_CMP_NE, {VCC(), IMM(0), Yr(7)});
     E(M_S_ANDN2_B64, {TM, MSK, VCC()});
-    E(M_S_CBRANCH_SCC0, {LBL(L_TOP3)});
+    E(M_S_CBRANCH_SCC0, {LBL(L_F32)});
     to_f64(FY, Yl);
     recip();
     to_f64(FR, Rl);
     E(M_S_BRANCH, {LBL(L_CONV)});
+    // Small quotients of full-width divisors (every lane that needs a digit has y >= 2^224, and
+    // its estimate is below 2^10: random full-width x / y almost always): the digit from f32
+    // estimates of the top two limbs, R7:R6 / Y7:Y6.  Truncating both to 64 bits moves R / y by
+    // < 2^-32 relative (Y7 >= 1); the two conversions, the reciprocal (1 ulp) and the product add
+    // < 2^-20.5 relative, so for an estimate below 2^10 the error is < 2^-9.9 absolute: the
+    // digit is exact or one off, an estimate one high leaves R negative (the add-back below) and
+    // one low has a fraction above 1 - 2^-9.9 (the "R >= y" test runs in waves with such a
+    // lane).  4 f32 conversions, 2 fma, a reciprocal and a product instead of 19 f64 ops.
+    L(L_F32);
+    E(M_S_MOV_B32, {K64LO, IMM(0x4f800000u)});  // 2^32 as f32
+    E(M_V_CVT_F32_U32, {V(R_FT), Rr(7)});
+    E(M_V_CVT_F32_U32, {V(R_FT + 1), Rr(6)});
+    E(M_V_FMA_F32, {V(R_FR), V(R_FT), K64LO, V(R_FT + 1)});
+    E(M_V_CVT_F32_U32, {V(R_FT), Yr(7)});
+    E(M_V_CVT_F32_U32, {V(R_FT + 1), Yr(6)});
+    E(M_V_FMA_F32, {V(R_FY), V(R_FT), K64LO, V(R_FT + 1)});
+    E(M_V_RCP_F32, {V(R_FY), V(R_FY)});
+    E(M_S_NOP, {IMM(1)});  // trans result -> non-trans VALU use needs a wait state
+    E(M_V_MUL_F32, {V(R_FC), V(R_FR), V(R_FY)});
+    E(M_V_CMP_GT_F32, {VCC(), IMM(0x44800000u), V(R_FC)});  // estimate < 2^10
+    E(M_S_ANDN2_B64, {TM, MSK, VCC()});
+    E(M_S_CBRANCH_SCC0, {LBL(L_F32OK)});
+    E(M_V_CMP_NE, {VCC(), IMM(0), Yr(7)});  // the f64 path reads y7 != 0 from VCC
+    E(M_S_BRANCH, {LBL(L_TOP3)});
+    L(L_F32OK);
+    E(M_V_CVT_U32_F32, {C, V(R_FC)});
+    E(M_V_CNDMASK, {C, IMM(0), C, MSK}, true);  // lanes without a digit (x < y, y = 0): 0
+    E(M_V_FRACT_F32, {V(R_FT), V(R_FC)});
+    E(M_V_CMP_LE_F32, {VCC(), IMM(0x3f7f8000u), V(R_FT)});  // 1 - 2^-9 <= fraction
+    E(M_S_AND_B64, {TM, VCC(), MSK});
+    E(M_S_BRANCH, {LBL(L_STEP0_BODY)});
     L(L_TOP3);
     top3_f64(FY, Yl);
     recip();
@@ -2195,6 +2236,7 @@ std::vector<MI> div_routine() {
         E(M_S_AND_B64, {TM, VCC(), YNZ});
         // R[j..] -= c * y (the product's limbs above limb 7 only feed the borrow); the carry
         // pair's high word stays 0 from the first copy on (the first product adds nothing)
+        if (j == 0) L(L_STEP0_BODY);
         for (int k = 0; k < 8; ++k) {
             E(M_V_MAD_U64_U32, {MAD, DUMMY, C, Yr(k), k ? CARRY : IMM(0)});
             if (k == 0) E(M_V_MOV, {V(R_CARRY + 1), IMM(0)});
@@ -3167,7 +3209,8 @@ namespace {
 // write o[0]; nothing else writes VGPRs.
 std::pair<uint32_t, uint32_t> vgpr_writes(const MI& m) {
     const bool valu = m.op <= M_V_CMP_LE_F64 &&
-                      !(m.op >= M_V_CMP_EQ && m.op <= M_V_CMP_GT_I32) && m.op != M_V_CMP_LE_F64;
+                      !(m.op >= M_V_CMP_EQ && m.op <= M_V_CMP_GT_I32) && m.op != M_V_CMP_LE_F64 &&
+                      m.op != M_V_CMP_GT_F32 && m.op != M_V_CMP_LE_F32;
     const bool lds_read = m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32;
     if ((valu || lds_read) && m.o[0].k == O_V) return {m.o[0].v, m.o[0].n};
     return {0, 0};

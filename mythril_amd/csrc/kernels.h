@@ -46,7 +46,6 @@ hipError_t launch_generate(uint32_t* assign, uint64_t stride, uint64_t rows, uin
 struct KGuide {
     uint32_t n_cols, n_sets;
     uint32_t n_value_sets;      // sets [0, n_value_sets) hold no copy entry
-    uint32_t n_alts, n_entries; // set_off[n_sets], alt_off[n_alts]
     const uint32_t* width;      // [n_cols]
     const uint32_t* pool_off;   // [n_cols + 1]
     const uint32_t* pool;       // x 8 limbs

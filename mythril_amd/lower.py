@@ -351,7 +351,10 @@ class Lowering:
             return self.eq(args[0], args[1])
         if args == [a, bb, c][:k]:
             return n
-        return b.op(Op(op), *args, imm0=i0, imm1=i1)
+        # the same op over operands of the same sorts (a lowered term keeps its width): the
+        # node was checked when it was built, so it is hash-consed without re-checking
+        args += [0] * (3 - k)
+        return b._add(op, w, args[0], args[1], args[2], i0, i1)
 
     # -- wide equalities: the device compares at most 256 bits ---------------------------------
     def _pieces(self, n: int) -> List[int]:

@@ -11,7 +11,8 @@
 // and a model better than the hardware hid a defect once -- one refinement step left digit
 // estimates up to ~2^-12 off, which the division's skipped-correction test assumed below 2^-19
 // (found on MI355X at 2^24 rows, scripts/diag_find_row.py; the emulator then returned the right
-// value because its reciprocal was exact).
+// value because its reciprocal was exact).  v_rcp_f32 is modelled 1 ulp off the rounded
+// reciprocal (up or down by the input's low mantissa bits), the hardware's documented bound.
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -75,6 +76,17 @@ struct Wave {
         }
         return o.neg ? -d : d;
     }
+    float f32(const Opnd& o, int l) const {
+        const uint32_t b = r32(o, l);
+        float f;
+        memcpy(&f, &b, 4);
+        return f;
+    }
+    void wf32(const Opnd& o, int l, float f) {
+        uint32_t b;
+        memcpy(&b, &f, 4);
+        v[o.v][l] = b;
+    }
     void wf64(const Opnd& o, int l, double d) {
         uint64_t b;
         memcpy(&b, &d, 8);
@@ -116,7 +128,8 @@ bool is_wide(const MI& m) {
            op == M_V_PERM || op == M_V_BFI ||
            (op >= M_V_CMP_EQ && op <= M_V_CMP_GT_I32) ||
            op == M_V_LSHLREV || op == M_V_LSHRREV || op == M_V_ASHRREV ||
-           op >= M_V_CVT_F64_U32;
+           op >= M_V_CVT_F64_U32 || op == M_V_RCP_F32 || op == M_V_CMP_GT_F32 ||
+           op == M_V_CMP_LE_F32;
 }
 
 void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int depth = 0,
@@ -287,6 +300,49 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                     w.v[o[0].v][l] = (m & w.r32(o[2], l)) | (~m & w.r32(o[3], l));
                 });
                 break;
+            case M_V_CVT_F32_U32: each([&](int l) { w.wf32(o[0], l, (float)w.r32(o[1], l)); }); break;
+            case M_V_FMA_F32:
+                each([&](int l) { w.wf32(o[0], l, fmaf(w.f32(o[1], l), w.f32(o[2], l), w.f32(o[3], l))); });
+                break;
+            case M_V_MUL_F32: each([&](int l) { w.wf32(o[0], l, w.f32(o[1], l) * w.f32(o[2], l)); }); break;
+            case M_V_RCP_F32:
+                each([&](int l) {
+                    const float x = w.f32(o[1], l);
+                    float r = (float)(1.0 / (double)x);
+                    uint32_t xb;
+                    memcpy(&xb, &x, 4);
+                    if (isfinite(r) && r != 0.0f) {
+                        if (xb & 1u) r = nextafterf(r, INFINITY);
+                        else if (xb & 2u) r = nextafterf(r, 0.0f);
+                    }
+                    w.wf32(o[0], l, r);
+                });
+                break;
+            case M_V_CVT_U32_F32:
+                each([&](int l) {
+                    const float d = w.f32(o[1], l);
+                    uint32_t r;
+                    if (isnan(d) || d <= 0) r = 0;
+                    else if (d >= 4294967295.0f) r = 0xFFFFFFFFu;
+                    else r = (uint32_t)d;
+                    w.v[o[0].v][l] = r;
+                });
+                break;
+            case M_V_FRACT_F32:
+                each([&](int l) {
+                    const float x = w.f32(o[1], l);
+                    w.wf32(o[0], l, isfinite(x) ? fminf(x - floorf(x), 0.99999994f) : NAN);
+                });
+                break;
+            case M_V_CMP_GT_F32: case M_V_CMP_LE_F32: {
+                uint64_t cm = 0;
+                for (int l = 0; l < 64; ++l) {
+                    const float a = w.f32(o[1], l), b = w.f32(o[2], l);
+                    if (m.op == M_V_CMP_GT_F32 ? a > b : a <= b) cm |= 1ull << l;
+                }
+                w.set_mask(o[0], cm);
+                break;
+            }
             case M_V_CVT_F64_U32: each([&](int l) { w.wf64(o[0], l, (double)w.r32(o[1], l)); }); break;
             case M_V_FMA_F64:
                 each([&](int l) { w.wf64(o[0], l, fma(w.f64(o[1], l), w.f64(o[2], l), w.f64(o[3], l))); });

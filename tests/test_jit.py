@@ -159,6 +159,40 @@ def test_division_uniform_paths_jit(emu):
         check_tapes(emu, ts, soa_of(division_wave_rows(seed), 2))
 
 
+def small_quotient_rows(seed):
+    """64-row waves for the division's f32 small-quotient path (every lane that needs a digit
+    has y >= 2^224 and an estimate below 2^10): x = q y + r with q up to 1023 and r at both
+    ends of [0, y) -- the digit on an integer boundary, where the f32 estimate is one off and a
+    correction must run -- plus a wave whose largest quotient reaches 2^10 (the f64 path), and
+    waves mixing lanes with x < y and y = 0 (outside the digit mask)."""
+    rng = random.Random(seed)
+    M = (1 << 256) - 1
+    rows = []
+    for wave in range(6):
+        for i in range(64):
+            y = rng.getrandbits(256) | (1 << (224 + rng.randrange(32)))
+            qmax = (1 << 10) - 1
+            if wave == 5 and i == 0:  # the wave's largest estimate reaches 2^10
+                y, qmax = rng.getrandbits(240) | (1 << 240), 1 << 10
+            q = qmax if wave == 5 and i == 0 else rng.choice([1, 2, 3, 1023, rng.randrange(1, qmax + 1)])
+            r = rng.choice([0, 1, 2, y - 1, y - 2, y - (y >> 20), y >> 20, rng.randrange(y)])
+            x = q * y + r
+            if x > M or wave == 4 and i % 4 == 0:
+                x, y = (rng.randrange(y), y) if i % 8 else (rng.getrandbits(256), 0)
+            rows.append([x & M, y])
+    return rows
+
+
+def test_division_small_quotient_jit(emu):
+    ts = TapeSet()
+    b = ts.builder()
+    x, y = b.var("x"), b.var("y")
+    for op in (Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD):
+        ts.add(b.finish(b.op(op, x, y)))
+    for seed in range(4):
+        check_tapes(emu, ts, soa_of(small_quotient_rows(seed), 2))
+
+
 def test_keccak_message_cuts_jit(emu):
     """Keccak-256 in the native code (the mh_kec subroutine, absorb and byte swaps at the call
     site) for messages of 1..96 bytes cut from several pieces, plus constant pieces: every value
@@ -397,7 +431,7 @@ def test_jit_coverage_and_static_cost(emu):
 def _hazards(text):
     """Pairs of adjacent instructions in the module text that break a manually inserted wait
     state of CDNA3/4 the JIT must honour: a VALU write of vN directly followed by
-    v_readlane / v_readfirstlane of vN; v_rcp_f64 directly followed by a use of its result;
+    v_readlane / v_readfirstlane of vN; v_rcp_f64 / v_rcp_f32 directly followed by a use of its result;
     a VALU write of an SGPR directly followed by a global_* instruction using that SGPR."""
     import re
     bad = []
@@ -414,7 +448,7 @@ def _hazards(text):
                 src = ln.split()[2].rstrip(",")
                 if re.fullmatch(r"v\d+", dst) and dst == src:
                     bad.append((prev, ln))
-            if p_ins == "v_rcp_f64":
+            if p_ins in ("v_rcp_f64", "v_rcp_f32"):
                 bad.append((prev, ln))
             if ins.startswith("global_") and p_ins.startswith("v_") and dst.startswith("s"):
                 if dst.split("[")[0] in ln or dst in ln:
