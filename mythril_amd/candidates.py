@@ -258,6 +258,12 @@ class Harvester:
                 if cond and cond != [{}]:
                     self._hint(cond)
                 out += r
+            if len(out) > 1 and {} in out:
+                # one branch already holds whatever the columns are (a calldata byte past
+                # calldatasize reads 0): the other branch's assignments also satisfy the term,
+                # and keeping the empty alternative beside them only multiplies the
+                # combinations of every enclosing concat (up to MAX_ALTS each)
+                out = [x for x in out if x]
             return out[:MAX_ALTS]
         if not full:
             return None
