@@ -141,13 +141,19 @@ __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, I
             // complex op: operands out of the register file by asm, the op in C++, the result
             // back by asm -- the C++ code never touches the planes, so they stay in their VGPRs
             typedef typename AsmCore<NR>::v8_t v8_t;
-            v8_t xv, yv, cv;
-            AsmCore<NR>::fetch(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6, m.R.p7,
-                               ic.w0, ic.w1, ip, w0, w1, xv, yv, cv);
-            u32 x[8], y[8], c3[8], z[8];
+            u32 z[8];
+            if (op == D_LOADVAR) {
+                // a column beyond the preloaded ones (wide query schemas): no operands to fetch
+                m.var((w1 >> 17) & MH_AUX_MAX, z);
+            } else {
+                v8_t xv, yv, cv;
+                AsmCore<NR>::fetch(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
+                                   m.R.p7, ic.w0, ic.w1, ip, w0, w1, xv, yv, cv);
+                u32 x[8], y[8], c3[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) { x[k] = xv[k]; y[k] = yv[k]; c3[k] = cv[k]; }
-            complex_op<FEAT>(m, w1, x, y, c3, z);
+                for (int k = 0; k < 8; ++k) { x[k] = xv[k]; y[k] = yv[k]; c3[k] = cv[k]; }
+                complex_op<FEAT>(m, w1, x, y, c3, z);
+            }
             v8_t zv;
 #pragma unroll
             for (int k = 0; k < 8; ++k) zv[k] = z[k];
