@@ -34,7 +34,7 @@ from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
-from .tape import ARITY, BOOL, F_ARRAY, Op, TapeBuilder, TapeError
+from .tape import ARITY, BOOL, F_ARRAY, F_HOST, Op, TapeBuilder, TapeError
 
 KECCAK_SHIFT = 139   # keep 117 bits of the hash ...
 KECCAK_ALIGN = 6     # ... as multiples of 64: H - base < 2^123 < PART
@@ -155,10 +155,12 @@ def is_keccak(name: str) -> bool:
     return name.startswith("keccak256_") and not name.endswith("-1")
 
 
-def _walk(b: TapeBuilder, roots: Iterable[int]) -> List[int]:
-    """Every node reachable from roots (array chains included), children before parents."""
+def _walk(b: TapeBuilder, roots: Iterable[int], host_only: bool = False) -> List[int]:
+    """Every node reachable from roots (array chains included), children before parents; with
+    ``host_only``, only the nodes that are or read host-only terms (F_HOST)."""
     order, seen = [], set()
-    stack = [(r, False) for r in roots]
+    fl = b.flags
+    stack = [(r, False) for r in roots if not host_only or fl[r] & F_HOST]
     while stack:
         n, done = stack.pop()
         if done:
@@ -171,7 +173,7 @@ def _walk(b: TapeBuilder, roots: Iterable[int]) -> List[int]:
         op, _, a, bb, c, _, _ = b.nodes[n]
         k = _arity(op)
         for ch in (a, bb, c)[:k][::-1]:
-            if ch not in seen:
+            if ch not in seen and (not host_only or fl[ch] & F_HOST):
                 stack.append((ch, False))
     return order
 
@@ -204,7 +206,8 @@ class Lowering:
         """The constant keys, keccak pairs and keccak bounds the terms under `roots` state."""
         b = self.b
         h = Harvest()
-        for n in _walk(b, roots):
+        # keys, keccak pairs and bounds all sit on host-only terms or their parents
+        for n in _walk(b, roots, host_only=True):
             op, w, a, bb, c, i0, i1 = b.nodes[n]
             if op == Op.SELECT:
                 base = self._array_base(a)
@@ -318,6 +321,12 @@ class Lowering:
         memo = self.memo
         if root in memo:
             return memo[root]
+        # a term that reads no host-only term lowers to itself (not with a frozen schema:
+        # Model.eval registers every variable it meets, fresh ones read 0)
+        fl = self.b.flags
+        prune = not self.frozen
+        if prune and not fl[root] & F_HOST:
+            return root
         stack = [(root, False)]
         while stack:
             n, ready = stack.pop()
@@ -326,7 +335,11 @@ class Lowering:
             if not ready:
                 stack.append((n, True))
                 for d in self._deps(n):
-                    if d not in memo:
+                    if d in memo:
+                        continue
+                    if prune and not fl[d] & F_HOST:
+                        memo[d] = d
+                    else:
                         stack.append((d, False))
                 continue
             memo[n] = self._rewrite(n)
@@ -516,8 +529,14 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
         used = frozenset().union(*(cols[r] for r in low)) if low else frozenset()
         names = var_names(b)
         full = L.schema
-        schema = Schema(full.cells, full.uf_cells, full.keccak,
-                        {names[v]: full.columns[names[v]] for v in sorted(used)})
+        cols = {}
+        for v in sorted(used):
+            name = names[v]
+            col = full.columns.get(name)
+            if col is None:  # a plain variable under a term the rewrite left as it was
+                col = full.columns[name] = Column(name, b.symbols.var_widths[name], "var", name)
+            cols[name] = col
+        schema = Schema(full.cells, full.uf_cells, full.keccak, cols)
     for r in low:
         if b.widths[r] != BOOL:
             raise TapeError("constraints must be Bool")

@@ -99,6 +99,7 @@ assert NODE_DTYPE.itemsize == 24
 
 HOST_ONLY = {Op.ARRAY, Op.CONST_ARRAY, Op.STORE, Op.SELECT, Op.UF}
 F_ARRAY = 1  # mh_node.flags bit of host-only array-sorted nodes (never sent to the device)
+F_HOST = 2   # lowering rewrites the node: it is or reads a host-only term or an EQ over > 256 bits
 
 # operand arity per op (number of node operands a, b, c used)
 ARITY = {
@@ -179,6 +180,12 @@ class TapeBuilder:
         got = self._memo.get(key)
         if got is not None:
             return got
+        k = ARITY[op]
+        if op in HOST_ONLY or (op == Op.EQ and self.widths[a] > 256):
+            flags |= F_HOST
+        elif k:
+            fl = self.flags
+            flags |= (fl[a] | (fl[b] if k > 1 else 0) | (fl[c] if k > 2 else 0)) & F_HOST
         idx = len(self.nodes)
         self.nodes.append(key)
         self.widths.append(width)
