@@ -177,6 +177,20 @@ typedef struct mh_guide {
 int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_base,
                                   uint64_t first, uint64_t count, const mh_guide* guide);
 
+/* Host-only: harvest the guide of one query from its lowered tape (the algorithm of
+ * mythril_amd/candidates.py, same arrays; no device is touched).  `nodes` is ONE tape whose root
+ * (last node) is the query's Bool path condition, VAR imm0 = column 0..n_cols-1, CONST imm0 =
+ * index into `consts` (n_consts x 8 limbs).  The parent query's witness (svm.py:257-262) is
+ * n_parent (column, value) pairs, value = 8 limbs, in the witness's order; n_parent = 0 for none.
+ * On MH_OK *guide points into *out, which owns the arrays until mh_harvest_free(*out).
+ * Replaces the Python harvest behind mythril_amd/candidates.build_guide for Sieve.solve.         */
+typedef struct mh_harvest mh_harvest;
+int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, const uint32_t* consts,
+                         uint32_t n_consts, const uint16_t* col_width, uint32_t n_cols,
+                         const uint32_t* parent_cols, const uint32_t* parent_vals,
+                         uint32_t n_parent, mh_harvest** out, mh_guide* guide);
+int32_t mh_harvest_free(mh_harvest* h);
+
 /* ---- evaluation ------------------------------------------------------------------------------ */
 /* Evaluate tapes [tape_first, tape_first+tape_count) over assignment rows [row_first,
  * row_first+row_count) of `as`.  Results are indexed by tape - tape_first and hold GLOBAL indices

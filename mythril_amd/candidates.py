@@ -510,10 +510,9 @@ class Harvester:
                         stack += node[2:2 + k]
                 got = consts_of[conj] = frozenset(got)
             qc |= got
-        if parent:
-            alt = {k: v for k, v in parent.items() if k in self.pools}
-            if alt:
-                self.sets.append((PROB_PARENT, [alt]))
+        alt = {k: v for k, v in parent.items() if k in self.pools} if parent else {}
+        if alt:
+            self.sets.append((PROB_PARENT, [alt]))
         seen_eq = set()
         eq_pairs = _memo(b, "_guide_eq")
         for conj in conjuncts:
@@ -557,7 +556,7 @@ class Harvester:
                 break
         # hints first: the exact requirements of the conjuncts (later sets) override them
         hints = _prune_hints(self.hints)
-        self.sets = self.sets[:1] + hints + self.sets[1:] if parent else hints + self.sets
+        self.sets = self.sets[:1] + hints + self.sets[1:] if alt else hints + self.sets
         pools = self.pools
         for _, alts in self.sets:
             for alt in alts:

@@ -223,6 +223,12 @@ int32_t set_err(int32_t code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+}  // namespace
+
+// mh_last_error text for the host-only entry points of other translation units (harvest.cpp)
+int32_t mh_detail_set_err(int32_t code, const char* msg) { return set_err(code, msg); }
+
+namespace {
 
 #define MH_HIP(call)                                                                      \
     do {                                                                                  \

@@ -1,0 +1,1011 @@
+// Candidate guide harvest on the host (mh_guide_harvest): what the sieve's guided rows try for
+// one query.  The algorithm is mythril_amd/candidates.py's (documented there and restated here
+// step for step, so the two produce the same mh_guide arrays -- tests/test_harvest.py): every
+// conjunct of the lowered path condition inverted toward its columns (concat / extract / zext /
+// and-mask / ite / +c / -c / xor c / *odd c / not / neg), Or as alternatives, ordered compares as
+// boundary values, overflow predicates as extreme operands; symbolic equalities as bit copies or
+// tried with the query's constants; ite conditions as soft hints (dominated single-column hints
+// pruned); the parent query's witness first; per-column pools.  It runs on the query's lowered
+// tape (VAR imm0 = column, CONST imm0 = index into the query's constants), so a LASER query's
+// guide costs microseconds instead of the Python harvester's milliseconds.
+//
+// Values are bit-vectors of up to 1088 bits (tape.MAX_WIDTH), held in a fixed 1152-bit word with
+// Python's wrap-then-mask arithmetic.  Alternatives keep Python dict order (insertion order,
+// update keeps a key's position), because pool order -- and so the generated rows -- follows it.
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mythril_hip.h"
+
+namespace {
+
+constexpr int NL = 36;  // 1152-bit values
+constexpr int kMaxAlts = 16, kMaxSets = 1024, kMaxPool = 64, kMaxEqConsts = 24;
+constexpr int kProbDefault = 208, kProbParent = 192, kProbHint = 64, kHintsPerColumn = 2;
+constexpr uint32_t kCopyFlag = 0x80000000u;
+
+// op codes of include/mythril_hip.h (enum mh_op) / mythril_amd/tape.py Op
+enum : uint8_t {
+    CONST = MH_OP_CONST, VAR = MH_OP_VAR, TRUE_ = MH_OP_TRUE, FALSE_ = MH_OP_FALSE,
+    BVADD = MH_OP_BVADD, BVSUB = MH_OP_BVSUB, BVMUL = MH_OP_BVMUL, BVNEG = MH_OP_BVNEG,
+    BVNOT = MH_OP_BVNOT, BVAND = MH_OP_BVAND, BVXOR = MH_OP_BVXOR, BVSHL = MH_OP_BVSHL,
+    BVLSHR = MH_OP_BVLSHR, EQ = MH_OP_EQ, BVULT = MH_OP_BVULT, BVULE = MH_OP_BVULE,
+    BVUGT = MH_OP_BVUGT, BVUGE = MH_OP_BVUGE, BVSLT = MH_OP_BVSLT, BVSLE = MH_OP_BVSLE,
+    BVSGT = MH_OP_BVSGT, BVSGE = MH_OP_BVSGE, AND = MH_OP_AND, OR = MH_OP_OR, NOT = MH_OP_NOT,
+    ITE = MH_OP_ITE, EXTRACT = MH_OP_EXTRACT, CONCAT = MH_OP_CONCAT, ZEXT = MH_OP_ZEXT,
+    SEXT = MH_OP_SEXT, KECCAK = MH_OP_KECCAK, ADD_NOOVFL_U = MH_OP_BVADD_NOOVFL_U,
+    MUL_NOOVFL_U = MH_OP_BVMUL_NOOVFL_U, SUB_NOUDFL_U = MH_OP_BVSUB_NOUDFL_U,
+};
+
+struct U {  // unsigned 1152-bit integer, arithmetic mod 2^1152
+    uint32_t w[NL];
+    U() { memset(w, 0, sizeof w); }
+    static U of(uint64_t x) { U r; r.w[0] = (uint32_t)x; r.w[1] = (uint32_t)(x >> 32); return r; }
+    bool zero() const { for (uint32_t x : w) if (x) return false; return true; }
+    bool operator==(const U& o) const { return memcmp(w, o.w, sizeof w) == 0; }
+    bool operator!=(const U& o) const { return !(*this == o); }
+    bool operator<(const U& o) const {
+        for (int i = NL - 1; i >= 0; --i)
+            if (w[i] != o.w[i]) return w[i] < o.w[i];
+        return false;
+    }
+    int bitlen() const {
+        for (int i = NL - 1; i >= 0; --i)
+            if (w[i]) return 32 * i + 32 - __builtin_clz(w[i]);
+        return 0;
+    }
+    bool bit(int i) const { return (w[i >> 5] >> (i & 31)) & 1u; }
+};
+U operator&(U a, const U& b) { for (int i = 0; i < NL; ++i) a.w[i] &= b.w[i]; return a; }
+U operator|(U a, const U& b) { for (int i = 0; i < NL; ++i) a.w[i] |= b.w[i]; return a; }
+U operator^(U a, const U& b) { for (int i = 0; i < NL; ++i) a.w[i] ^= b.w[i]; return a; }
+U operator~(U a) { for (uint32_t& x : a.w) x = ~x; return a; }
+U operator+(const U& a, const U& b) {
+    U r;
+    uint64_t c = 0;
+    for (int i = 0; i < NL; ++i) { c += (uint64_t)a.w[i] + b.w[i]; r.w[i] = (uint32_t)c; c >>= 32; }
+    return r;
+}
+U operator-(const U& a, const U& b) { return a + (~b + U::of(1)); }
+U neg(const U& a) { return ~a + U::of(1); }
+U operator*(const U& a, const U& b) {
+    U r;
+    for (int i = 0; i < NL; ++i) {
+        if (!a.w[i]) continue;
+        uint64_t c = 0;
+        for (int j = 0; i + j < NL; ++j) {
+            c += (uint64_t)a.w[i] * b.w[j] + r.w[i + j];
+            r.w[i + j] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+    return r;
+}
+U shl(const U& a, int s) {
+    U r;
+    if (s >= 32 * NL) return r;
+    const int q = s >> 5, b = s & 31;
+    for (int i = NL - 1; i >= q; --i) {
+        uint32_t v = a.w[i - q] << b;
+        if (b && i - q - 1 >= 0) v |= a.w[i - q - 1] >> (32 - b);
+        r.w[i] = v;
+    }
+    return r;
+}
+U shr(const U& a, int s) {
+    U r;
+    if (s >= 32 * NL) return r;
+    const int q = s >> 5, b = s & 31;
+    for (int i = 0; i + q < NL; ++i) {
+        uint32_t v = a.w[i + q] >> b;
+        if (b && i + q + 1 < NL) v |= a.w[i + q + 1] << (32 - b);
+        r.w[i] = v;
+    }
+    return r;
+}
+// 2^w - 1 for w in 0..1088 (< 1152), built once
+const U& mask(int w) {
+    static const std::vector<U> table = [] {
+        std::vector<U> t(1089);
+        for (int i = 1; i <= 1088; ++i) t[i] = shl(U::of(1), i) - U::of(1);
+        return t;
+    }();
+    return table[w];
+}
+
+// a column value (columns are 1..256 bits wide): what alternatives and pools hold
+struct V {
+    uint32_t w[8];
+    bool operator==(const V& o) const { return memcmp(w, o.w, sizeof w) == 0; }
+    bool operator!=(const V& o) const { return !(*this == o); }
+    bool operator<(const V& o) const {
+        for (int i = 7; i >= 0; --i)
+            if (w[i] != o.w[i]) return w[i] < o.w[i];
+        return false;
+    }
+};
+V lo256(const U& u) { V v; memcpy(v.w, u.w, sizeof v.w); return v; }
+
+// the inverse of an odd k mod 2^w (Newton: x <- x (2 - k x), 5 correct bits doubling)
+U inverse_mod(const U& k, int w) {
+    U x = k;  // k * k = 1 mod 8 for odd k
+    for (int i = 0; i < 12; ++i) x = x * (U::of(2) - k * x);
+    return x & mask(w);
+}
+
+// One harvest allocates thousands of small vectors (alternatives, memo entries) and frees them
+// all at the end: they come from a per-thread bump arena that mh_guide_harvest resets.
+struct Arena {
+    std::vector<std::unique_ptr<char[]>> blocks;
+    std::vector<size_t> sizes;
+    size_t cur = 0, off = 0;
+    void* alloc(size_t n, size_t align) {
+        for (;;) {
+            if (cur < blocks.size()) {
+                const size_t o = (off + align - 1) & ~(align - 1);
+                if (o + n <= sizes[cur]) {
+                    off = o + n;
+                    return blocks[cur].get() + o;
+                }
+                ++cur;
+                off = 0;
+                continue;
+            }
+            const size_t sz = std::max<size_t>(n + align, (size_t)1 << 20);
+            blocks.emplace_back(new char[sz]);
+            sizes.push_back(sz);
+        }
+    }
+    void reset() {
+        cur = off = 0;
+        while (blocks.size() > 16) {  // keep at most 16 MB between harvests
+            blocks.pop_back();
+            sizes.pop_back();
+        }
+    }
+};
+thread_local Arena g_arena;
+
+template <class T>
+struct ArenaAlloc {
+    using value_type = T;
+    ArenaAlloc() = default;
+    template <class O>
+    ArenaAlloc(const ArenaAlloc<O>&) {}
+    T* allocate(size_t n) { return static_cast<T*>(g_arena.alloc(n * sizeof(T), alignof(T))); }
+    void deallocate(T*, size_t) {}
+    template <class O>
+    bool operator==(const ArenaAlloc<O>&) const { return true; }
+    template <class O>
+    bool operator!=(const ArenaAlloc<O>&) const { return false; }
+};
+template <class T>
+using AVec = std::vector<T, ArenaAlloc<T>>;
+
+struct Node {
+    uint8_t op;
+    uint16_t width;
+    uint32_t a, b, c, imm0, imm1;
+};
+
+using Alt = AVec<std::pair<uint32_t, V>>;  // (column, value) in dict insertion order
+using Alts = AVec<Alt>;
+// an inversion's result, shared by the memo and its callers; none = "don't know" (Python None)
+struct Res {
+    bool none = true;
+    std::shared_ptr<const Alts> p;
+    const Alts& alts() const {
+        static const Alts kEmpty;
+        return p ? *p : kEmpty;
+    }
+};
+
+Res none_() { return Res(); }
+Res of(Alts a) {
+    Res r;
+    r.none = false;
+    r.p = std::allocate_shared<const Alts>(ArenaAlloc<Alts>(), std::move(a));
+    return r;
+}
+Res one_empty() { return of(Alts{Alt{}}); }  // [{}]
+
+const V* find(const Alt& a, uint32_t k) {
+    for (const auto& kv : a)
+        if (kv.first == k) return &kv.second;
+    return nullptr;
+}
+// dict(y).update(x)
+Alt updated(const Alt& y, const Alt& x) {
+    Alt z = y;
+    for (const auto& kv : x) {
+        bool hit = false;
+        for (auto& zz : z)
+            if (zz.first == kv.first) { zz.second = kv.second; hit = true; break; }
+        if (!hit) z.push_back(kv);
+    }
+    return z;
+}
+bool is_only_empty(const Alts& a) { return a.size() == 1 && a[0].empty(); }
+Alts head(const Alts& a, size_t n) { return Alts(a.begin(), a.begin() + std::min(n, a.size())); }
+
+// candidates.py _merge
+Alts merge(const Alts& xs, const Alts& ys) {
+    if (is_only_empty(ys)) return head(xs, kMaxAlts);
+    if (is_only_empty(xs)) return head(ys, kMaxAlts);
+    if (xs.size() == 1 && ys.size() == 1) {
+        const Alt* x = &xs[0];
+        const Alt* y = &ys[0];
+        if (y->size() < x->size()) std::swap(x, y);
+        for (const auto& kv : *x) {
+            const V* v = find(*y, kv.first);
+            if (v && *v != kv.second) return {};
+        }
+        return {updated(*y, *x)};
+    }
+    Alts out;
+    for (const Alt& x : xs)
+        for (const Alt& y : ys) {
+            bool clash = false;
+            for (const auto& kv : y) {
+                const V* v = find(x, kv.first);
+                if (v && *v != kv.second) { clash = true; break; }
+            }
+            if (clash) continue;
+            out.push_back(updated(x, y));
+            if ((int)out.size() >= kMaxAlts) return out;
+        }
+    return out;
+}
+
+struct Seg { int lo, n; uint32_t col; int col_lo; };
+struct Copy { uint32_t dst, src; int dlo, slo, nb; };
+
+struct Harvester {
+    std::vector<Node> nd;
+    std::vector<U> pool;              // the query's constants
+    std::vector<int> cv_state;        // const_value memo: 0 unknown, 1 constant, 2 not
+    AVec<U> cv;
+    uint32_t n_cols = 0;
+    std::vector<uint16_t> widths;
+    // inversion memo: key -> (result, hints produced, transitively)
+    // (kind, node, value, mask) with values interned; hints by id (one per distinct hint)
+    struct Key {
+        uint32_t kind, n, v, m;
+        bool operator==(const Key& o) const { return kind == o.kind && n == o.n && v == o.v && m == o.m; }
+    };
+    struct KeyHash {
+        size_t operator()(const Key& k) const {
+            uint64_t h = ((uint64_t)k.n << 32 | k.v) * 0x9E3779B97F4A7C15ull;
+            h ^= ((uint64_t)k.m << 1 | k.kind) * 0xC2B2AE3D27D4EB4Full;
+            return (size_t)(h ^ (h >> 31));
+        }
+    };
+    struct UHash {
+        size_t operator()(const U& u) const {
+            uint64_t h = 1469598103934665603ull;
+            for (int i = 0; i < NL; ++i) h = (h ^ u.w[i]) * 1099511628211ull;
+            return (size_t)h;
+        }
+    };
+    struct Memo { Res r; AVec<uint32_t> hints; };
+    std::unordered_map<U, uint32_t, UHash, std::equal_to<U>, ArenaAlloc<std::pair<const U, uint32_t>>>
+        interned;
+    std::unordered_map<Key, Memo, KeyHash, std::equal_to<Key>, ArenaAlloc<std::pair<const Key, Memo>>>
+        memo;
+    AVec<AVec<uint32_t>> cap;
+    AVec<std::pair<int, Alts>> sets;
+    AVec<uint32_t> hints;      // hint ids in the order they became hint sets
+    std::map<AVec<uint32_t>, uint32_t, std::less<AVec<uint32_t>>,
+             ArenaAlloc<std::pair<const AVec<uint32_t>, uint32_t>>> hint_ids;
+    AVec<Alts> hint_alts;      // by id: the alternatives a hint set holds
+    AVec<char> hint_done;      // by id: already a hint of this query
+    std::unordered_map<const Alts*, uint32_t, std::hash<const Alts*>, std::equal_to<const Alts*>,
+                       ArenaAlloc<std::pair<const Alts* const, uint32_t>>> hint_of_result;
+    AVec<std::shared_ptr<const Alts>> hint_results;
+    int n_hints = 0;
+    std::vector<std::vector<std::vector<Copy>>> copy_sets;
+    std::vector<U> query_consts;
+    std::map<int, std::vector<U>> consts_by_width;
+
+    static int arity(uint8_t op) {  // tape.py ARITY (lowered tapes hold no host-only ops)
+        switch (op) {
+            case CONST: case VAR: case TRUE_: case FALSE_: return 0;
+            case BVNEG: case BVNOT: case NOT: case EXTRACT: case ZEXT: case SEXT: case KECCAK:
+                return 1;
+            case ITE: case MH_OP_EVM_ADDMOD: case MH_OP_EVM_MULMOD: return 3;
+            default: return 2;
+        }
+    }
+    const U* const_value(uint32_t n) {
+        if (cv_state[n] == 0) {
+            const Node& x = nd[n];
+            bool ok = false;
+            U v;
+            if (x.op == CONST) { v = pool[x.imm0]; ok = true; }
+            else if (x.op == TRUE_) { v = U::of(1); ok = true; }
+            else if (x.op == FALSE_) { ok = true; }
+            else if (x.op == CONCAT) {
+                const U* hi = const_value(x.a);
+                const U* lo = hi ? const_value(x.b) : nullptr;
+                if (hi && lo) { v = shl(*hi, nd[x.b].width) | *lo; ok = true; }
+            } else if (x.op == EXTRACT || x.op == ZEXT || x.op == SEXT) {
+                const U* a = const_value(x.a);
+                if (a) {
+                    ok = true;
+                    if (x.op == EXTRACT) v = shr(*a, (int)x.imm1) & mask((int)(x.imm0 - x.imm1 + 1));
+                    else if (x.op == SEXT && a->bit(nd[x.a].width - 1))
+                        v = *a | shl(mask((int)x.imm0), nd[x.a].width);
+                    else v = *a;
+                }
+            }
+            cv_state[n] = ok ? 1 : 2;
+            cv[n] = v;
+        }
+        return cv_state[n] == 1 ? &cv[n] : nullptr;
+    }
+
+    template <class F>
+    Res memoised(const Key& key, F compute) {
+        auto it = memo.find(key);
+        if (it == memo.end()) {
+            cap.emplace_back();
+            Res r = compute();
+            AVec<uint32_t> hs = std::move(cap.back());
+            cap.pop_back();
+            if (!cap.empty()) cap.back().insert(cap.back().end(), hs.begin(), hs.end());
+            memo.emplace(key, Memo{r, std::move(hs)});
+            return r;
+        }
+        const Memo& m = it->second;
+        for (uint32_t id : m.hints) emit_hint(id);
+        return m.r;
+    }
+    uint32_t intern(const U& u) {
+        auto it = interned.find(u);
+        if (it != interned.end()) return it->second;
+        return interned.emplace(u, (uint32_t)interned.size()).first->second;
+    }
+    static void push_u(std::vector<uint32_t>& k, const U& v) {
+        int top = NL;
+        while (top > 0 && !v.w[top - 1]) --top;
+        k.push_back((uint32_t)top);
+        k.insert(k.end(), v.w, v.w + top);
+    }
+
+    Res invert_bits(uint32_t n, const U& value, const U& msk, int depth = 0) {
+        return memoised(Key{0u, n, intern(value), intern(msk)}, [&]() {
+            return depth < 64 ? invert_bits_(n, value & msk, msk, depth) : none_();
+        });
+    }
+    Res invert_bits_(uint32_t n, const U& value, const U& msk, int depth) {
+        const Node x = nd[n];
+        const bool full = msk == mask(x.width);
+        if (const U* c = const_value(n)) return (*c & msk) == value ? one_empty() : of({});
+        if (x.op == VAR) {
+            if (x.imm0 >= n_cols) return none_();
+            return of({Alt{{x.imm0, lo256(value)}}});
+        }
+        if (x.op == CONCAT) {
+            Alts acc{Alt{}};
+            for (const auto& leaf : concat_leaves(n)) {
+                const U m = shr(msk, leaf.second) & mask(nd[leaf.first].width);
+                if (m.zero()) continue;
+                Res r = invert_bits(leaf.first, shr(value, leaf.second) & m, m, depth + 1);
+                if (r.none || is_only_empty(r.alts())) continue;
+                const Alts& ra = r.alts();
+                if (acc.size() == 1 && ra.size() == 1 && ra[0].size() < acc[0].size()) {
+                    // _merge's one-pair case with the accumulated alternative the larger: it
+                    // keeps its order and gains r's new columns at the end -- in place
+                    bool clash = false;
+                    for (const auto& kv : ra[0]) {
+                        const V* v = find(acc[0], kv.first);
+                        if (v) { clash |= *v != kv.second; continue; }
+                        acc[0].push_back(kv);
+                    }
+                    if (clash) return of({});
+                    continue;
+                }
+                acc = merge(acc, ra);
+                if (acc.empty()) return of(acc);
+            }
+            return of(std::move(acc));
+        }
+        if (x.op == EXTRACT) return invert_bits(x.a, shl(value, x.imm1), shl(msk, x.imm1), depth + 1);
+        if (x.op == BVAND) {
+            const uint32_t pr[2][2] = {{x.a, x.b}, {x.b, x.a}};
+            for (const auto& p : pr) {
+                if (const U* m = const_value(p[1])) {
+                    if (!(value & ~*m & msk).zero()) return of({});
+                    return invert_bits(p[0], value & *m, msk & *m, depth + 1);
+                }
+            }
+            return none_();
+        }
+        if (x.op == ZEXT || x.op == SEXT) {
+            const int wa = nd[x.a].width;
+            if (x.op == ZEXT && !shr(value, wa).zero()) return of({});
+            return invert_bits(x.a, value & mask(wa), msk & mask(wa), depth + 1);
+        }
+        if (x.op == ITE) {
+            Alts out;
+            const std::pair<uint32_t, bool> br[2] = {{x.b, true}, {x.c, false}};
+            for (const auto& p : br) {
+                Res r = invert_bits(p.first, value, msk, depth + 1);
+                if (r.none || r.alts().empty()) continue;
+                Res cond = invert_bool(x.a, p.second, depth + 1);
+                if (!cond.none && !cond.alts().empty() && !is_only_empty(cond.alts())) hint(cond);
+                out.insert(out.end(), r.alts().begin(), r.alts().end());
+            }
+            bool has_empty = false;
+            for (const Alt& a : out) has_empty |= a.empty();
+            if (out.size() > 1 && has_empty) {
+                Alts kept;
+                for (const Alt& a : out) if (!a.empty()) kept.push_back(a);
+                out.swap(kept);
+            }
+            return of(head(out, kMaxAlts));
+        }
+        if (!full) return none_();
+        const U m = mask(x.width);
+        if (x.op == BVADD || x.op == BVSUB || x.op == BVXOR || x.op == BVMUL) {
+            const U* ka = const_value(x.a);
+            const U* kb = const_value(x.b);
+            uint32_t t;
+            U k;
+            if (kb) { t = x.a; k = *kb; }
+            else if (ka) { t = x.b; k = *ka; }
+            else return none_();
+            U v;
+            if (x.op == BVADD) v = value - k;
+            else if (x.op == BVSUB) v = t == x.a ? value + k : k - value;
+            else if (x.op == BVXOR) v = value ^ k;
+            else {
+                if (!k.bit(0)) return none_();
+                v = value * inverse_mod(k, x.width);
+            }
+            return invert_bits(t, v & m, m, depth + 1);
+        }
+        if (x.op == BVNOT) return invert_bits(x.a, ~value & m, m, depth + 1);
+        if (x.op == BVNEG) return invert_bits(x.a, neg(value) & m, m, depth + 1);
+        return none_();
+    }
+
+    std::unordered_map<uint32_t, std::vector<std::pair<uint32_t, int>>> leaves_memo;
+    const std::vector<std::pair<uint32_t, int>>& concat_leaves(uint32_t n) {
+        auto it = leaves_memo.find(n);
+        if (it != leaves_memo.end()) return it->second;
+        std::vector<std::pair<uint32_t, int>> got;
+        std::vector<std::pair<uint32_t, int>> st{{n, 0}};
+        while (!st.empty()) {
+            auto [x, lo] = st.back();
+            st.pop_back();
+            if (nd[x].op == CONCAT) {
+                st.push_back({nd[x].a, lo + nd[nd[x].b].width});
+                st.push_back({nd[x].b, lo});
+            } else {
+                got.push_back({x, lo});
+            }
+        }
+        return leaves_memo[n] = std::move(got);
+    }
+
+    Res invert_bool(uint32_t n, bool truth, int depth = 0) {
+        if (depth > 64) return none_();
+        return memoised(Key{1u, n, truth ? 1u : 0u, 0u}, [&]() { return invert_bool_(n, truth, depth); });
+    }
+    Res invert_bool_(uint32_t n, bool truth, int depth) {
+        const Node x = nd[n];
+        if (const U* c = const_value(n)) return (!c->zero()) == truth ? one_empty() : of({});
+        if (x.op == NOT) return invert_bool(x.a, !truth, depth + 1);
+        if (x.op == AND || x.op == OR) {
+            const bool conj = (x.op == AND) == truth;
+            Res a = invert_bool(x.a, truth, depth + 1);
+            Res b = invert_bool(x.b, truth, depth + 1);
+            if (conj) return of(merge(a.none ? Alts{Alt{}} : a.alts(), b.none ? Alts{Alt{}} : b.alts()));
+            Alts out;
+            if (!a.none) out = a.alts();
+            if (!b.none) out.insert(out.end(), b.alts().begin(), b.alts().end());
+            if (a.none && b.none) return none_();
+            return of(head(out, kMaxAlts));
+        }
+        if (x.op == EQ) {
+            if (nd[x.a].width == 0) return none_();
+            const U* ka = const_value(x.a);
+            const U* kb = const_value(x.b);
+            uint32_t t;
+            const U* k;
+            if (kb) { t = x.a; k = kb; } else { t = x.b; k = ka; }
+            if (!k) return none_();
+            if (truth) return invert_bits(t, *k, mask(nd[t].width));
+            return one_empty();
+        }
+        if (x.op == ADD_NOOVFL_U || x.op == MUL_NOOVFL_U || x.op == SUB_NOUDFL_U) {
+            const int wt = nd[x.a].width;
+            const U M = mask(wt);
+            std::vector<std::pair<U, U>> pairs;
+            if (x.op == SUB_NOUDFL_U) {
+                if (truth) pairs = {{U::of(0), U::of(0)}, {U::of(1), U::of(0)}};
+                else pairs = {{U::of(0), U::of(1)}, {U::of(1), U::of(2)}};
+            } else if (truth) {
+                pairs = {{U::of(0), U::of(0)}, {U::of(1), U::of(1)}};
+            } else {
+                pairs = {{M, U::of(2)}, {M, M}};
+            }
+            Alts out;
+            for (const auto& p : pairs) {
+                Res ra = invert_bits(x.a, p.first, M);
+                Res rb = invert_bits(x.b, p.second, M);
+                if (ra.none && rb.none) continue;
+                Alts mg = merge(ra.none ? Alts{Alt{}} : ra.alts(), rb.none ? Alts{Alt{}} : rb.alts());
+                out.insert(out.end(), mg.begin(), mg.end());
+            }
+            if (out.empty()) return none_();
+            return of(head(out, kMaxAlts));
+        }
+        if (x.op >= BVULT && x.op <= BVSGE) {
+            const U* ka = const_value(x.a);
+            const U* kb = const_value(x.b);
+            if (!ka && !kb) return none_();
+            const int wt = nd[x.a].width;
+            const uint32_t t = ka ? x.b : x.a;
+            const U k = ka ? *ka : *kb;
+            Alts out;
+            for (const U& v : boundary(x.op, k, t == x.a, truth, wt)) {
+                Res r = invert_bits(t, v, mask(wt));
+                if (!r.none && !r.alts().empty()) out.insert(out.end(), r.alts().begin(), r.alts().end());
+            }
+            return of(head(out, kMaxAlts));
+        }
+        return none_();
+    }
+
+    static std::vector<U> boundary(uint8_t op, const U& k, bool var_left, bool truth, int w) {
+        const U m = mask(w);
+        const bool less = op == BVULT || op == BVULE || op == BVSLT || op == BVSLE;
+        bool strict = op == BVULT || op == BVUGT || op == BVSLT || op == BVSGT;
+        bool want_below = less == var_left;
+        if (!truth) { want_below = !want_below; strict = !strict; }
+        std::vector<U> vals;
+        if (want_below) {
+            if (strict) vals = {k - U::of(1), shr(k, 1), U::of(0)};
+            else vals = {k, k - U::of(1), U::of(0)};
+        } else {
+            if (strict) vals = {k + U::of(1), k + U::of(2), shl(k, 1) + U::of(1)};
+            else vals = {k, k + U::of(1)};
+        }
+        for (U& v : vals) v = v & m;
+        return vals;
+    }
+
+    // bits of term n that are bits of a column: (lo, nbits, column, column_lo); false = computes
+    bool segments(uint32_t n, std::vector<Seg>& out, int depth = 0) {
+        out.clear();
+        if (depth > 64) return false;
+        const Node x = nd[n];
+        if (const_value(n)) return true;
+        if (x.op == VAR) {
+            if (x.imm0 >= n_cols) return false;
+            out.push_back({0, (int)x.width, x.imm0, 0});
+            return true;
+        }
+        if (x.op == CONCAT) {
+            std::vector<Seg> hi, lo;
+            if (!segments(x.a, hi, depth + 1) || !segments(x.b, lo, depth + 1)) return false;
+            const int wb = nd[x.b].width;
+            out = lo;
+            for (const Seg& s : hi) out.push_back({s.lo + wb, s.n, s.col, s.col_lo});
+            return true;
+        }
+        if (x.op == EXTRACT) {
+            std::vector<Seg> inner;
+            if (!segments(x.a, inner, depth + 1)) return false;
+            for (const Seg& s : inner) {
+                const int s0 = std::max(s.lo, (int)x.imm1), s1 = std::min(s.lo + s.n, (int)x.imm0 + 1);
+                if (s0 < s1) out.push_back({s0 - (int)x.imm1, s1 - s0, s.col, s.col_lo + (s0 - s.lo)});
+            }
+            return true;
+        }
+        if (x.op == ZEXT) return segments(x.a, out, depth + 1);
+        if (x.op == BVAND) {
+            const uint32_t pr[2][2] = {{x.a, x.b}, {x.b, x.a}};
+            for (const auto& p : pr) {
+                const U* m = const_value(p[1]);
+                if (m && ((*m) & ((*m) + U::of(1))).zero()) {
+                    std::vector<Seg> inner;
+                    if (!segments(p[0], inner, depth + 1)) return false;
+                    const int k = m->bitlen();
+                    for (const Seg& s : inner)
+                        if (s.lo < k) out.push_back({s.lo, std::min(s.n, k - s.lo), s.col, s.col_lo});
+                    return true;
+                }
+            }
+            return false;
+        }
+        if (x.op == ITE) {
+            if (const_value(x.c)) return segments(x.b, out, depth + 1);
+            if (const_value(x.b)) return segments(x.c, out, depth + 1);
+        }
+        return false;
+    }
+
+    std::vector<std::vector<Copy>> copy_alternatives(uint32_t x, uint32_t y) {
+        std::vector<Seg> sx, sy;
+        const bool okx = segments(x, sx), oky = segments(y, sy);
+        if (!okx || !oky || sx.empty() || sy.empty()) return {};
+        std::vector<std::vector<Copy>> alts;
+        const std::vector<Seg>* sides[2][2] = {{&sx, &sy}, {&sy, &sx}};
+        for (auto& sd : sides) {
+            std::vector<Copy> copies;
+            for (const Seg& d : *sd[0])
+                for (const Seg& s : *sd[1]) {
+                    const int s0 = std::max(d.lo, s.lo), s1 = std::min(d.lo + d.n, s.lo + s.n);
+                    if (s0 < s1 && d.col != s.col)
+                        copies.push_back({d.col, s.col, d.col_lo + (s0 - d.lo), s.col_lo + (s0 - s.lo), s1 - s0});
+                }
+            if (!copies.empty()) {
+                if (copies.size() > 256) copies.resize(256);
+                alts.push_back(std::move(copies));
+            }
+        }
+        return alts;
+    }
+
+    // candidates.py Harvester._hint: a hint is identified by its alternatives' items (each
+    // alternative's sorted by column); the first MAX_SETS/4 distinct ones become hint sets
+    void hint(const Res& r) {
+        // the same (memoised) inversion result is the same hint: look it up by identity first
+        auto known = hint_of_result.find(r.p.get());
+        if (known != hint_of_result.end()) return emit_hint(known->second);
+        const Alts& alts = r.alts();
+        AVec<uint32_t> key;
+        for (const Alt& a : alts) {
+            Alt s = a;
+            std::sort(s.begin(), s.end(), [](const auto& p, const auto& q) { return p.first < q.first; });
+            key.push_back(0xFFFFFFFFu);
+            for (const auto& kv : s) {
+                key.push_back(kv.first);
+                key.insert(key.end(), kv.second.w, kv.second.w + 8);
+            }
+        }
+        auto got = hint_ids.emplace(std::move(key), (uint32_t)hint_alts.size());
+        if (got.second) {
+            Alts kept;
+            for (const Alt& a : alts) if (!a.empty()) kept.push_back(a);
+            hint_alts.push_back(head(kept, kMaxAlts));
+            hint_done.push_back(0);
+        }
+        hint_results.push_back(r.p);  // keeps the identity valid
+        hint_of_result.emplace(r.p.get(), got.first->second);
+        emit_hint(got.first->second);
+    }
+    void emit_hint(uint32_t id) {
+        if (!cap.empty()) cap.back().push_back(id);
+        if (!hint_done[id] && n_hints < kMaxSets / 4) {
+            hint_done[id] = 1;
+            ++n_hints;
+            hints.push_back(id);
+        }
+    }
+
+    std::vector<uint32_t> conjuncts(uint32_t root) {
+        std::vector<uint32_t> out, st{root};
+        while (!st.empty()) {
+            const uint32_t n = st.back();
+            st.pop_back();
+            if (nd[n].op == AND) { st.push_back(nd[n].b); st.push_back(nd[n].a); }
+            else out.push_back(n);
+        }
+        return out;
+    }
+
+    std::vector<uint32_t> eq_seen;
+    uint32_t eq_epoch = 0;
+    std::vector<uint32_t> eq_nodes(uint32_t root, size_t limit = 4096) {
+        std::vector<uint32_t> out, st{root};
+        ++eq_epoch;  // seen = stamped with this walk's epoch
+        if (eq_seen.size() != nd.size()) eq_seen.assign(nd.size(), 0);
+        size_t n_seen = 0;
+        while (!st.empty() && n_seen < limit) {
+            const uint32_t n = st.back();
+            st.pop_back();
+            if (eq_seen[n] == eq_epoch) continue;
+            eq_seen[n] = eq_epoch;
+            ++n_seen;
+            if (nd[n].op == EQ) out.push_back(n);
+            const int k = arity(nd[n].op);
+            if (k >= 1) st.push_back(nd[n].a);
+            if (k >= 2) st.push_back(nd[n].b);
+            if (k >= 3) st.push_back(nd[n].c);
+        }
+        return out;
+    }
+
+    std::pair<uint32_t, uint32_t> strip_common(uint32_t x, uint32_t y) {
+        for (int i = 0; i < 64; ++i) {
+            const Node ox = nd[x], oy = nd[y];
+            if (ox.op != oy.op || ox.width != oy.width) break;
+            const uint8_t op = ox.op;
+            if (op == KECCAK || op == BVNOT || op == BVNEG ||
+                ((op == ZEXT || op == SEXT) && ox.imm0 == oy.imm0)) {
+                x = ox.a; y = oy.a;
+                continue;
+            }
+            if (op == BVADD || op == BVSUB || op == BVXOR || op == BVSHL || op == BVLSHR ||
+                op == BVMUL || op == CONCAT) {
+                const U* bx = const_value(ox.b);
+                const U* by = const_value(oy.b);
+                if (ox.b == oy.b || (bx && by && *bx == *by)) { x = ox.a; y = oy.a; continue; }
+                const U* ax = const_value(ox.a);
+                const U* ay = const_value(oy.a);
+                if (ox.a == oy.a || (ax && ay && *ax == *ay)) { x = ox.b; y = oy.b; continue; }
+            }
+            break;
+        }
+        return {x, y};
+    }
+
+    const std::vector<U>& consts_of_width(int w) {
+        auto it = consts_by_width.find(w);
+        if (it != consts_by_width.end()) return it->second;
+        const U m = mask(w);
+        std::vector<U> vals;
+        for (const U& v : query_consts) vals.push_back(v & m);
+        std::sort(vals.begin(), vals.end());
+        vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+        std::stable_sort(vals.begin(), vals.end(), [](const U& p, const U& q) {
+            const int bp = p.bitlen(), bq = q.bitlen();
+            const int gp = bp > 8, gq = bq > 8;
+            if (gp != gq) return gp > gq;
+            if (bp != bq) return bp > bq;
+            return p < q;
+        });
+        if ((int)vals.size() > kMaxEqConsts) vals.resize(kMaxEqConsts);
+        return consts_by_width[w] = std::move(vals);
+    }
+
+    void harvest(uint32_t root, const Alt* parent, std::vector<std::vector<V>>& pools,
+                 std::vector<std::pair<int, const Alts*>>& out_sets,
+                 std::vector<std::vector<std::vector<Copy>>>& out_copies) {
+        const std::vector<uint32_t> conj = conjuncts(root);
+        {   // the query's constants
+            std::vector<char> seen(nd.size(), 0);
+            std::vector<uint32_t> st(conj.begin(), conj.end());
+            std::vector<U> qc;
+            while (!st.empty()) {
+                const uint32_t n = st.back();
+                st.pop_back();
+                if (seen[n]) continue;
+                seen[n] = 1;
+                if (nd[n].op == CONST) qc.push_back(pool[nd[n].imm0]);
+                const int k = arity(nd[n].op);
+                if (k >= 1) st.push_back(nd[n].a);
+                if (k >= 2) st.push_back(nd[n].b);
+                if (k >= 3) st.push_back(nd[n].c);
+            }
+            std::sort(qc.begin(), qc.end());
+            qc.erase(std::unique(qc.begin(), qc.end()), qc.end());
+            query_consts.swap(qc);
+        }
+        if (parent && !parent->empty()) sets.push_back({kProbParent, {*parent}});
+        std::vector<char> seen_eq(nd.size(), 0);
+        std::unordered_map<uint32_t, std::tuple<bool, uint32_t, uint32_t,
+                                                std::vector<std::vector<Copy>>>> eq_pairs;
+        for (uint32_t cj : conj) {
+            Res alts = invert_bool(cj, true);
+            if (!alts.none && !alts.alts().empty() && !is_only_empty(alts.alts())) {
+                Alts kept;
+                for (const Alt& a : alts.alts()) if (!a.empty()) kept.push_back(a);
+                sets.push_back({kProbDefault, head(kept, kMaxAlts)});
+            }
+            for (uint32_t n : eq_nodes(cj)) {
+                if (seen_eq[n]) continue;
+                seen_eq[n] = 1;
+                uint32_t x = nd[n].a, y = nd[n].b;
+                if (nd[x].width == 0 || const_value(x) || const_value(y)) continue;
+                std::tie(x, y) = strip_common(x, y);
+                if (x == y) continue;
+                auto calts = copy_alternatives(x, y);
+                const int w = nd[x].width;
+                if (!calts.empty()) {
+                    if ((int)copy_sets.size() < kMaxSets / 4) copy_sets.push_back(std::move(calts));
+                    continue;
+                }
+                for (const U& k : consts_of_width(w)) {
+                    Res rx = invert_bits(x, k, mask(w));
+                    Res ry = invert_bits(y, k, mask(w));
+                    if (!rx.none && !rx.alts().empty() && !ry.none && !ry.alts().empty()) {
+                        Alts both = merge(rx.alts(), ry.alts());
+                        if (!both.empty() && !is_only_empty(both))
+                            sets.push_back({kProbDefault / 2, head(both, kMaxAlts)});
+                    }
+                }
+                if ((int)sets.size() >= kMaxSets) break;
+            }
+            if ((int)sets.size() >= kMaxSets) break;
+        }
+        out_sets.clear();
+        const bool first_parent = parent && !parent->empty() && !sets.empty();
+        if (first_parent) out_sets.push_back({sets[0].first, &sets[0].second});
+        for (uint32_t id : prune_hints()) out_sets.push_back({kProbHint, &hint_alts[id]});
+        for (size_t i = first_parent ? 1 : 0; i < sets.size(); ++i)
+            out_sets.push_back({sets[i].first, &sets[i].second});
+        pools.assign(n_cols, {});
+        auto add_pool = [&](uint32_t c, const V& v) {
+            auto& p = pools[c];
+            if ((int)p.size() >= kMaxPool) return;
+            for (const V& x : p) if (x == v) return;
+            p.push_back(v);
+        };
+        for (const auto& s : out_sets)
+            for (const Alt& a : *s.second)
+                for (const auto& kv : a) add_pool(kv.first, kv.second);
+        for (uint32_t c = 0; c < n_cols; ++c) {
+            const int w = widths[c];
+            for (const U& v : {U::of(0), U::of(1), mask(w), shl(U::of(1), w - 1)}) add_pool(c, lo256(v));
+        }
+        if ((int)out_sets.size() > kMaxSets) out_sets.resize(kMaxSets);
+        out_copies = copy_sets;
+        if ((int)out_copies.size() > kMaxSets / 4) out_copies.resize(kMaxSets / 4);
+    }
+
+    // candidates.py _prune_hints: per column, of the single-column hint sets only the
+    // kHintsPerColumn with the largest and with the smallest values stay (in their order)
+    std::vector<uint32_t> prune_hints() const {
+        std::map<uint32_t, std::vector<size_t>> by_col;
+        for (size_t i = 0; i < hints.size(); ++i) {
+            const Alts& alts = hint_alts[hints[i]];
+            bool single = !alts.empty();
+            for (const Alt& a : alts)
+                if (a.size() != 1 || a[0].first != alts[0][0].first) { single = false; break; }
+            if (single) by_col[alts[0][0].first].push_back(i);
+        }
+        std::vector<char> drop(hints.size(), 0);
+        for (auto& kv : by_col) {
+            const std::vector<size_t>& idx = kv.second;
+            if ((int)idx.size() <= 2 * kHintsPerColumn) continue;
+            std::vector<V> hi_v(hints.size()), lo_v(hints.size());
+            for (size_t i : idx) {
+                const Alts& alts = hint_alts[hints[i]];
+                V mx = alts[0][0].second, mn = mx;
+                for (const Alt& a : alts) { mx = std::max(mx, a[0].second); mn = std::min(mn, a[0].second); }
+                hi_v[i] = mx;
+                lo_v[i] = mn;
+            }
+            std::vector<size_t> hi = idx, lo = idx;
+            std::stable_sort(hi.begin(), hi.end(), [&](size_t p, size_t q) { return hi_v[q] < hi_v[p]; });
+            std::stable_sort(lo.begin(), lo.end(), [&](size_t p, size_t q) { return lo_v[p] < lo_v[q]; });
+            for (size_t i : idx) drop[i] = 1;
+            for (int j = 0; j < kHintsPerColumn; ++j) drop[hi[j]] = drop[lo[j]] = 0;
+        }
+        std::vector<uint32_t> out;
+        for (size_t i = 0; i < hints.size(); ++i) if (!drop[i]) out.push_back(hints[i]);
+        return out;
+    }
+};
+
+}  // namespace
+
+struct mh_harvest {  // owns the arrays an mh_guide from mh_guide_harvest points into
+    std::vector<uint32_t> pool_off, pool, set_off, alt_off, entry_col, entry_val;
+    std::vector<uint8_t> set_prob;
+    std::vector<uint16_t> width16;
+};
+
+int32_t mh_detail_set_err(int32_t code, const char* msg);  // capi.cpp
+
+extern "C" int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, const uint32_t* consts,
+                                    uint32_t n_consts, const uint16_t* col_width, uint32_t n_cols,
+                                    const uint32_t* parent_cols, const uint32_t* parent_vals,
+                                    uint32_t n_parent, mh_harvest** out, mh_guide* guide) {
+    if (!out || !guide) return mh_detail_set_err(MH_E_INVALID, "null out pointer");
+    *out = nullptr;
+    if (!nodes || n_nodes == 0 || (n_consts && !consts) || (n_cols && !col_width) ||
+        (n_parent && (!parent_cols || !parent_vals)))
+        return mh_detail_set_err(MH_E_INVALID, "null or empty argument");
+    try {
+        struct ArenaReset {  // declared first: runs after every arena-backed local is gone
+            ~ArenaReset() { g_arena.reset(); }
+        } arena_reset;
+        Harvester h;
+        h.nd.resize(n_nodes);
+        for (uint32_t i = 0; i < n_nodes; ++i) {
+            const mh_node& s = nodes[i];
+            Node& d = h.nd[i];
+            d.op = s.op; d.width = s.width; d.a = s.a; d.b = s.b; d.c = s.c;
+            d.imm0 = s.imm0; d.imm1 = s.imm1;
+            const int k = Harvester::arity(s.op);
+            if (s.width > 1088 || (k >= 1 && s.a >= i) || (k >= 2 && s.b >= i) ||
+                (k >= 3 && s.c >= i) || (s.op == CONST && s.imm0 >= n_consts) ||
+                (s.op == EXTRACT && (s.imm1 > s.imm0 || s.imm0 >= 1088)))
+                return mh_detail_set_err(MH_E_INVALID, "malformed tape node");
+        }
+        h.pool.resize(n_consts);
+        for (uint32_t i = 0; i < n_consts; ++i)
+            for (int k = 0; k < 8; ++k) h.pool[i].w[k] = consts[8ull * i + k];
+        h.cv_state.assign(n_nodes, 0);
+        h.cv.resize(n_nodes);
+        h.n_cols = n_cols;
+        h.widths.assign(col_width, col_width + n_cols);
+        for (uint16_t w : h.widths)
+            if (w < 1 || w > 256) return mh_detail_set_err(MH_E_INVALID, "column width not 1..256");
+        Alt parent;
+        for (uint32_t i = 0; i < n_parent; ++i) {
+            if (parent_cols[i] >= n_cols)
+                return mh_detail_set_err(MH_E_INVALID, "parent column out of range");
+            V v;
+            for (int k = 0; k < 8; ++k) v.w[k] = parent_vals[8ull * i + k];
+            parent.push_back({parent_cols[i], v});
+        }
+        std::vector<std::vector<V>> pools;
+        std::vector<std::pair<int, const Alts*>> sets;
+        std::vector<std::vector<std::vector<Copy>>> copies;
+        h.harvest(n_nodes - 1, n_parent ? &parent : nullptr, pools, sets, copies);
+        auto r = std::make_unique<mh_harvest>();
+        r->width16.assign(h.widths.begin(), h.widths.end());
+        r->pool_off.push_back(0);
+        auto put = [](std::vector<uint32_t>& dst, const V& v) { dst.insert(dst.end(), v.w, v.w + 8); };
+        for (const auto& p : pools) {
+            for (const V& v : p) put(r->pool, v);
+            r->pool_off.push_back((uint32_t)(r->pool.size() / 8));
+        }
+        r->set_off.push_back(0);
+        r->alt_off.push_back(0);
+        for (const auto& s : sets) {
+            r->set_prob.push_back((uint8_t)s.first);
+            for (const Alt& a : *s.second) {
+                for (const auto& kv : a) {
+                    r->entry_col.push_back(kv.first);
+                    put(r->entry_val, kv.second);
+                }
+                r->alt_off.push_back((uint32_t)r->entry_col.size());
+            }
+            r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
+        }
+        for (const auto& alts : copies) {
+            r->set_prob.push_back((uint8_t)kProbDefault);
+            for (const auto& alt : alts) {
+                for (const Copy& c : alt) {
+                    r->entry_col.push_back(c.dst | kCopyFlag);
+                    const uint32_t ev[8] = {c.src, (uint32_t)c.dlo, (uint32_t)c.slo, (uint32_t)c.nb,
+                                            0, 0, 0, 0};
+                    r->entry_val.insert(r->entry_val.end(), ev, ev + 8);
+                }
+                r->alt_off.push_back((uint32_t)r->entry_col.size());
+            }
+            r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
+        }
+        const uint32_t n_sets = (uint32_t)r->set_prob.size();
+        // never-empty arrays, as candidates.Guide.arrays() gives them (one zero entry)
+        if (r->pool.empty()) r->pool.assign(8, 0);
+        if (r->set_prob.empty()) r->set_prob.push_back(0);
+        if (r->entry_col.empty()) r->entry_col.push_back(0);
+        if (r->entry_val.empty()) r->entry_val.assign(8, 0);
+        guide->n_cols = n_cols;
+        guide->col_width = r->width16.data();
+        guide->pool_off = r->pool_off.data();
+        guide->pool = r->pool.data();
+        guide->n_sets = n_sets;
+        guide->set_prob = r->set_prob.data();
+        guide->set_off = r->set_off.data();
+        guide->alt_off = r->alt_off.data();
+        guide->entry_col = r->entry_col.data();
+        guide->entry_val = r->entry_val.data();
+        *out = r.release();
+        return MH_OK;
+    } catch (const std::bad_alloc&) {
+        return mh_detail_set_err(MH_E_NOMEM, "host allocation failed");
+    }
+}
+
+extern "C" int32_t mh_harvest_free(mh_harvest* h) {
+    delete h;
+    return MH_OK;
+}

@@ -78,6 +78,9 @@ SIGNATURES = {
     "mh_comm_destroy": (C.c_int32, [_vp]),
     "mh_ctx_enable_timing": (C.c_int32, [_vp, C.c_int32]),
     "mh_ctx_kernel_time": (C.c_int32, [_vp, C.POINTER(C.c_double), _u64p]),
+    "mh_guide_harvest": (C.c_int32, [_vp, C.c_uint32, _u32p, C.c_uint32, C.POINTER(C.c_uint16),
+                                     C.c_uint32, _u32p, _u32p, C.c_uint32, C.POINTER(_vp), _vp]),
+    "mh_harvest_free": (C.c_int32, [_vp]),
 }
 
 
@@ -152,6 +155,47 @@ class Guide(C.Structure):
 
 
 _lib: Optional[C.CDLL] = None
+
+
+def _limb_rows(vals) -> np.ndarray:
+    """[n, 8] u32 limbs of 256-bit values."""
+    buf = b"".join((int(v) & ((1 << 256) - 1)).to_bytes(32, "little") for v in vals)
+    return np.frombuffer(buf, dtype="<u4").reshape(-1, 8).copy()
+
+
+def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
+                  parent: Sequence[Tuple[int, int]] = ()) -> dict:
+    """mh_guide_harvest: the guide of one lowered query tape (root last, VAR imm0 = column,
+    CONST imm0 = row of `consts`), as the arrays candidates.Guide.arrays() gives -- the same
+    values (tests/test_harvest.py).  `parent` = the parent witness as (column, value) pairs in
+    the witness's order.  Host-only: no device is touched."""
+    lib = load()
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1, 8)
+    w = np.ascontiguousarray(widths, dtype=np.uint16)
+    pc = np.ascontiguousarray([c for c, _ in parent], dtype=np.uint32)
+    pv = _limb_rows([v for _, v in parent]) if len(parent) else np.zeros((1, 8), np.uint32)
+    h = C.c_void_p()
+    g = Guide()
+    _check(lib.mh_guide_harvest(nodes.ctypes.data, len(nodes), _ptr(consts), len(consts),
+                                w.ctypes.data_as(C.POINTER(C.c_uint16)), len(w), _ptr(pc),
+                                _ptr(pv), len(pc), C.byref(h), C.byref(g)))
+    try:
+        def arr(p, n, dt=np.uint32):
+            return np.ctypeslib.as_array(p, (n,)).astype(dt, copy=True)
+
+        n_cols, n_sets = g.n_cols, g.n_sets
+        pool_off = arr(g.pool_off, n_cols + 1)
+        set_off = arr(g.set_off, n_sets + 1)
+        alt_off = arr(g.alt_off, int(set_off[-1]) + 1)
+        n_entries = max(int(alt_off[-1]), 1)
+        return dict(
+            width=arr(g.col_width, n_cols, np.uint16), pool_off=pool_off,
+            pool=arr(g.pool, 8 * max(int(pool_off[-1]), 1)).reshape(-1, 8), set_off=set_off,
+            set_prob=arr(g.set_prob, max(n_sets, 1), np.uint8), alt_off=alt_off,
+            entry_col=arr(g.entry_col, n_entries), entry_val=arr(g.entry_val, 8 * n_entries).reshape(-1, 8))
+    finally:
+        lib.mh_harvest_free(h)
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:

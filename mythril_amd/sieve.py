@@ -5,7 +5,7 @@ mythril/laser/ethereum/state/constraints.py:25-35, support/model.py:15-62):
 
 1. lower arrays / keccak UFs onto scalar columns (lower.py) — ``LoweringUnsupported`` -> None;
 2. harvest a candidate guide from the lowered term and the parent query's witness
-   (candidates.py);
+   (mh_guide_harvest, harvest.cpp -- the algorithm of candidates.py, same arrays);
 3. compile the conjunction as one device tape over the query's own columns (mh_tapes_compile);
 4. two launches at most: ``first_rows`` guided rows (mh_assign_generate_guided), then, when a
    group is still unsolved, the remaining ``(max_rounds - 1) * rows`` rows in ONE launch; each
@@ -28,7 +28,6 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import native
-from .candidates import build_guide
 from .lower import Schema, lower_query, node_columns
 from .tape import NODE_DTYPE, Op, Tape, TapeBuilder, TapeSet
 
@@ -290,10 +289,6 @@ class Sieve:
             from .lower import Column
 
             schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
-        parent = self.witnesses.get(key[:-1]) if key else None
-        guide = build_guide(b, root, schema, columns, parent).arrays()
-        t_g = time.perf_counter()
-        st.add("guide", t_g - t_l)
         groups = self.buckets(b, root)
         names = {b.var_index[c]: c for c in columns}
         group_cols, accs = [], []
@@ -306,8 +301,18 @@ class Sieve:
         ts = local_tapeset(b, accs, columns)
         if len(groups) > 1:
             self.stats.extra["bucketed"] = self.stats.extra.get("bucketed", 0) + 1
+        t_t = time.perf_counter()
+        st.add("tapes", t_t - t_l)
+        # the guide is harvested natively from the root's tape -- the one tape of a query whose
+        # conjuncts share columns (the same AND chain), else a tape of its own
+        gts = ts if accs == [root] else local_tapeset(b, [root], columns)
+        col_index = {c: i for i, c in enumerate(columns)}
+        parent = self.witnesses.get(key[:-1]) if key else None
+        guide = native.harvest_guide(
+            gts.tapes[0].nodes, gts.pool.to_array(), [schema.columns[c].width for c in columns],
+            [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else ())
         t1 = time.perf_counter()
-        st.add("tapes", t1 - t_g)
+        st.add("guide", t1 - t_t)
         self.stats.host_s += t1 - t0
         ct = self.compile(ts)
         t_c = time.perf_counter()
@@ -317,7 +322,6 @@ class Sieve:
         st.add("compile_native", nt)
         try:
             assign = self._buffer(len(columns))
-            col_index = {c: i for i, c in enumerate(columns)}
             values: Dict[str, int] = {}
             solved = [False] * len(groups)
             first_index = None

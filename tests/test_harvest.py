@@ -1,0 +1,107 @@
+"""mh_guide_harvest (mythril_amd/csrc/harvest.cpp) against the Python harvester it restates
+(mythril_amd/candidates.py): the same guide arrays, bit for bit, for every LASER-shaped query of
+tests/laser_like.py, asked in LASER order (each query extends its parent by one conjunct,
+svm.py:257-262, so the Python side also answers from its builder-level memos) and with parent
+witnesses.  Host-only: runs without a GPU."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from mythril_amd import native
+from mythril_amd.candidates import build_guide
+from mythril_amd.lower import lower_query
+from mythril_amd.sieve import local_tapeset
+
+from . import laser_like
+
+KEYS = ("width", "pool_off", "pool", "set_off", "set_prob", "alt_off", "entry_col", "entry_val")
+
+
+def _lib_or_skip():
+    try:
+        native.load()
+    except native.NativeUnavailable as e:  # pragma: no cover - build() makes it
+        pytest.skip(str(e))
+
+
+def _parent_of(cols, widths, salt: str):
+    """A deterministic parent witness over some of the columns, plus one name the query does
+    not read (the parent's own columns are not all the child's)."""
+    out = {}
+    for i, (c, w) in enumerate(zip(cols, widths)):
+        h = int.from_bytes(hashlib.sha256(("%s/%s" % (salt, c)).encode()).digest(), "little")
+        if h % 3:
+            out[c] = h & ((1 << w) - 1) if h % 5 else 0
+    out["__not_a_column__"] = 7
+    return out
+
+
+def _compare(b, roots, parent=None):
+    root, schema = lower_query(b, roots)
+    cols = list(schema.columns)
+    if not cols:
+        return 0
+    widths = [schema.columns[c].width for c in cols]
+    want = build_guide(b, root, schema, cols, parent).arrays()
+    ts = local_tapeset(b, [root], cols)
+    index = {c: i for i, c in enumerate(cols)}
+    par = [(index[k], v) for k, v in (parent or {}).items() if k in index]
+    got = native.harvest_guide(ts.tapes[0].nodes, ts.pool.to_array(), widths, par)
+    for k in KEYS:
+        assert got[k].dtype == want[k].dtype, k
+        assert got[k].shape == want[k].shape, (k, got[k].shape, want[k].shape)
+        assert np.array_equal(got[k], want[k]), k
+    return len(want["set_off"]) - 1
+
+
+@pytest.mark.parametrize("which", ["queries", "hard_queries"])
+def test_harvest_matches_python_laser_order(which):
+    _lib_or_skip()
+    ctx, qs = getattr(laser_like, which)()
+    total = 0
+    for name, cs in qs:
+        for k in range(1, len(cs) + 1):  # LASER order: parent prefixes first
+            total += _compare(ctx.b, [c.node for c in cs[:k]])
+    assert total > 0
+
+
+def test_harvest_matches_python_with_parents():
+    _lib_or_skip()
+    ctx, qs = laser_like.queries()
+    for name, cs in qs:
+        root, schema = lower_query(ctx.b, [c.node for c in cs])
+        cols = list(schema.columns)
+        widths = [schema.columns[c].width for c in cols]
+        for salt in ("a", "b"):
+            _compare(ctx.b, [c.node for c in cs], _parent_of(cols, widths, name + salt))
+        # a parent that shares no column with the query adds no set
+        _compare(ctx.b, [c.node for c in cs], {"__not_a_column__": 1})
+
+
+def test_harvest_cold_builder():
+    """Each query on a fresh builder (no memo from earlier queries on the Python side)."""
+    _lib_or_skip()
+    names = [n for n, _ in laser_like.queries()[1]]
+    for name in names:
+        ctx, qs = laser_like.queries()
+        cs = dict(qs)[name]
+        _compare(ctx.b, [c.node for c in cs])
+
+
+def test_harvest_rejects_malformed():
+    _lib_or_skip()
+    from mythril_amd.tape import NODE_DTYPE, Op
+
+    nodes = np.zeros(2, dtype=NODE_DTYPE)
+    nodes[0] = (int(Op.VAR), 0, 8, 0, 0, 0, 0, 0)
+    nodes[1] = (int(Op.EQ), 0, 0, 0, 1, 0, 0, 0)  # operand b refers to itself
+    with pytest.raises(native.SieveError):
+        native.harvest_guide(nodes, np.zeros((1, 8), np.uint32), [8])
+    nodes[1] = (int(Op.CONST), 0, 8, 0, 0, 0, 5, 0)  # const index out of range
+    with pytest.raises(native.SieveError):
+        native.harvest_guide(nodes, np.zeros((1, 8), np.uint32), [8])
+    with pytest.raises(native.SieveError):  # parent column out of range
+        native.harvest_guide(nodes[:1], np.zeros((1, 8), np.uint32), [8], [(3, 1)])
