@@ -103,35 +103,33 @@ class Harvest:
 
 
 def node_columns(b: TapeBuilder, roots: Iterable[int]) -> Dict[int, frozenset]:
-    """The VAR indices under each node reachable from `roots` (memoised on the builder: nodes
-    are immutable and hash-consed, so later queries only visit their new nodes)."""
+    """The VAR indices under each of `roots` (memoised per root on the builder: nodes are
+    immutable and hash-consed).  A walk stops at any node already in the memo, so a LASER query
+    that extends its parent's (svm.py:257-262) only visits its new conjunct; the nodes between
+    are not given sets of their own (a set per node cost more than the walk)."""
     cols: Dict[int, frozenset] = b.__dict__.setdefault("_node_cols", {})
-    order, st = [], [(r, False) for r in roots if r not in cols]
-    seen = set()
-    while st:
-        n, done = st.pop()
-        if done:
-            order.append(n)
+    nodes, var = b.nodes, Op.VAR
+    for r in roots:
+        if r in cols:
             continue
-        if n in seen or n in cols:
-            continue
-        seen.add(n)
-        st.append((n, True))
-        op, _, a, bb, c, _, _ = b.nodes[n]
-        st += [(x, False) for x in (a, bb, c)[:ARITY[op]] if x not in seen and x not in cols]
-    empty = frozenset()
-    for n in order:
-        op, _, a, bb, c, i0, _ = b.nodes[n]
-        if op == Op.VAR:
-            cols[n] = frozenset((i0,))
-            continue
-        kids = (a, bb, c)[:ARITY[op]]
-        if not kids:
-            cols[n] = empty
-            continue
-        sets = [cols[x] for x in kids]
-        big = max(sets, key=len)
-        cols[n] = big if all(x <= big for x in sets) else big.union(*sets)
+        vs, seen, st = set(), set(), [r]
+        while st:
+            n = st.pop()
+            if n in seen:
+                continue
+            seen.add(n)
+            got = cols.get(n)
+            if got is not None:
+                vs |= got
+                continue
+            op, _, a, bb, c, i0, _ = nodes[n]
+            if op == var:
+                vs.add(i0)
+                continue
+            k = ARITY[op]
+            if k:
+                st += (a, bb, c)[:k]
+        cols[r] = frozenset(vs)
     return cols
 
 

@@ -298,18 +298,23 @@ class Sieve:
                 acc = b.op(Op.AND, acc, x)
             accs.append(acc)
             group_cols.append([names[v] for v in vs])
-        ts = local_tapeset(b, accs, columns)
+        # the guide is harvested natively from the root's tape: the one tape of a query whose
+        # conjuncts share columns (the same AND chain), else an extra tape of the same tape set
+        # (same constants), not compiled
+        if accs == [root]:
+            ts = local_tapeset(b, accs, columns)
+            root_nodes = ts.tapes[0].nodes
+        else:
+            ts = local_tapeset(b, [root] + accs, columns)
+            root_nodes = ts.tapes.pop(0).nodes
         if len(groups) > 1:
             self.stats.extra["bucketed"] = self.stats.extra.get("bucketed", 0) + 1
         t_t = time.perf_counter()
         st.add("tapes", t_t - t_l)
-        # the guide is harvested natively from the root's tape -- the one tape of a query whose
-        # conjuncts share columns (the same AND chain), else a tape of its own
-        gts = ts if accs == [root] else local_tapeset(b, [root], columns)
         col_index = {c: i for i, c in enumerate(columns)}
         parent = self.witnesses.get(key[:-1]) if key else None
         guide = native.harvest_guide(
-            gts.tapes[0].nodes, gts.pool.to_array(), [schema.columns[c].width for c in columns],
+            root_nodes, ts.pool.to_array(), [schema.columns[c].width for c in columns],
             [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else ())
         t1 = time.perf_counter()
         st.add("guide", t1 - t_t)
