@@ -193,6 +193,14 @@ class Lowering:
         self.schema = frozen if frozen is not None else Schema()
         self.memo: Dict[int, int] = {}
         self.sym = b.symbols
+        # rewrites that read the harvest's tables (a table lookup at a symbolic key, a keccak
+        # application) depend on the fingerprint; every other rewrite is the same under any
+        # harvest that contains the node's own (a constant key is in it): those are kept on the
+        # builder for every Lowering, so a query whose new constraint adds table keys (a fresh
+        # calldata word) does not re-lower its parent's constraints
+        self.dep: set = set()
+        self.stable: Dict[int, int] = (b.__dict__.setdefault("_stable_lower", {})
+                                       if frozen is None else {})
 
     # -- pass 1: harvest ------------------------------------------------------------------
     def harvest(self, roots: Sequence[int]) -> None:
@@ -279,7 +287,9 @@ class Lowering:
         if name not in self.schema.columns:
             # frozen (Model.eval): no new cells are ever made (constant keys outside the table
             # read the else column); a new else / variable column reads 0 (model completion)
-            self.schema.columns[name] = Column(name, width, kind, symbol, key)
+            col = self.schema.columns[name] = Column(name, width, kind, symbol, key)
+            if not self.frozen:  # a column's name fixes what it is, under every harvest
+                self.b.__dict__.setdefault("_lower_columns", {}).setdefault(name, col)
         return self.b.var(name, width)
 
     def _deps(self, n: int) -> List[int]:
@@ -325,23 +335,51 @@ class Lowering:
         prune = not self.frozen
         if prune and not fl[root] & F_HOST:
             return root
-        stack = [(root, False)]
+        stable, dep = self.stable, self.dep
+        got = stable.get(root)
+        if got is not None:
+            memo[root] = got
+            return got
+        nodes, table_ops = self.b.nodes, (Op.SELECT, Op.UF)
+        stack = [(root, None)]
         while stack:
-            n, ready = stack.pop()
+            n, deps = stack.pop()
             if n in memo:
                 continue
-            if not ready:
-                stack.append((n, True))
-                for d in self._deps(n):
+            if deps is None:  # first visit: operands first
+                deps = self._deps(n)
+                stack.append((n, deps))
+                for d in deps:
                     if d in memo:
                         continue
                     if prune and not fl[d] & F_HOST:
                         memo[d] = d
+                        continue
+                    got = stable.get(d)
+                    if got is not None:
+                        memo[d] = got
                     else:
-                        stack.append((d, False))
+                        stack.append((d, None))
                 continue
-            memo[n] = self._rewrite(n)
+            low = memo[n] = self._rewrite(n)
+            if (nodes[n][0] in table_ops and self._reads_tables(n)) or any(d in dep for d in deps):
+                dep.add(n)
+            elif prune:
+                stable[n] = low
         return memo[root]
+
+    def _reads_tables(self, n: int) -> bool:
+        """Whether the rewrite of n itself depends on the harvest's tables (see __init__)."""
+        b = self.b
+        op, _, a, bb, _, i0, _ = b.nodes[n]
+        if op == Op.SELECT:
+            return self._array_base(a) is not None and b.const_value(bb) is None
+        if op == Op.UF:
+            fname = self.sym.function_names[i0]
+            if is_keccak(fname):
+                return True
+            return not fname.endswith("-1") and b.const_value(a) is None
+        return False
 
     def _rewrite(self, n: int) -> int:
         b, memo = self.b, self.memo
@@ -531,8 +569,12 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
         for v in sorted(used):
             name = names[v]
             col = full.columns.get(name)
-            if col is None:  # a plain variable under a term the rewrite left as it was
-                col = full.columns[name] = Column(name, b.symbols.var_widths[name], "var", name)
+            if col is None:  # made by an earlier Lowering (a stable rewrite), else a plain
+                # variable under a term the rewrite left as it was
+                col = b.__dict__.get("_lower_columns", {}).get(name)
+                if col is None:
+                    col = Column(name, b.symbols.var_widths[name], "var", name)
+                full.columns[name] = col
             cols[name] = col
         schema = Schema(full.cells, full.uf_cells, full.keccak, cols)
     for r in low:

@@ -145,3 +145,36 @@ def test_inverse_of_something_else_is_unsupported():
     y = symbol_factory.BitVecSym("y", 256)
     with pytest.raises(LoweringUnsupported):
         ctx.query(inv(y) == y)
+
+
+class _NoStable(dict):
+    """A `_stable_lower` memo that never remembers: every Lowering rewrites from scratch."""
+
+    def __setitem__(self, k, v):
+        pass
+
+
+@pytest.mark.parametrize("which", ["queries", "hard_queries"])
+def test_shared_rewrites_match_fresh_lowering(which):
+    """Rewrites kept on the builder across harvest fingerprints (Lowering.stable) give the
+    same lowered tapes and columns as lowering every query from scratch, in LASER order (each
+    query extends its parent by one constraint, svm.py:257-262)."""
+    from mythril_amd.sieve import local_tapeset
+    from tests import laser_like
+
+    ctx_a, qs_a = getattr(laser_like, which)()
+    ctx_b, qs_b = getattr(laser_like, which)()
+    ctx_b.b.__dict__["_stable_lower"] = _NoStable()
+    for (name, cs_a), (_, cs_b) in zip(qs_a, qs_b):
+        for k in range(1, len(cs_a) + 1):
+            ra, sa = lower_query(ctx_a.b, [c.node for c in cs_a[:k]])
+            rb, sb = lower_query(ctx_b.b, [c.node for c in cs_b[:k]])
+            assert list(sa.columns.values()) == list(sb.columns.values()), (name, k)
+            cols = list(sa.columns)
+            if not cols:
+                continue
+            ta = local_tapeset(ctx_a.b, [ra], cols)
+            tb = local_tapeset(ctx_b.b, [rb], cols)
+            assert ta.tapes[0].nodes.tobytes() == tb.tapes[0].nodes.tobytes(), (name, k)
+            assert (ta.pool.to_array() == tb.pool.to_array()).all(), (name, k)
+    assert len(ctx_a.b.__dict__["_stable_lower"]) > 0
