@@ -924,8 +924,13 @@ extern "C" int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, cons
             const int k = Harvester::arity(s.op);
             if (s.width > 1088 || (k >= 1 && s.a >= i) || (k >= 2 && s.b >= i) ||
                 (k >= 3 && s.c >= i) || (s.op == CONST && s.imm0 >= n_consts) ||
-                (s.op == EXTRACT && (s.imm1 > s.imm0 || s.imm0 >= 1088)))
+                (s.op == EXTRACT && (s.imm1 > s.imm0 || s.imm0 >= 1088)) ||
+                ((s.op == ZEXT || s.op == SEXT) && s.imm0 > 1088))
                 return mh_detail_set_err(MH_E_INVALID, "malformed tape node");
+            // bit-layout operands are bit-vectors (the harvest reads their top bit / width)
+            if ((s.op == EXTRACT || s.op == ZEXT || s.op == SEXT || s.op == CONCAT) &&
+                (h.nd[s.a].width == 0 || (s.op == CONCAT && h.nd[s.b].width == 0)))
+                return mh_detail_set_err(MH_E_INVALID, "bit-layout op over a Bool operand");
         }
         h.pool.resize(n_consts);
         for (uint32_t i = 0; i < n_consts; ++i)

@@ -202,3 +202,18 @@ def test_harvest_matches_python_random_queries():
         compared += _compare(ctx.b, [c.node for c in cs]) >= 0
         _compare(ctx.b, [c.node for c in cs], _parent_of(cols, widths, "r%d" % i))
     assert compared >= 100
+
+
+def test_harvest_rejects_bad_layout_nodes():
+    _lib_or_skip()
+    from mythril_amd.tape import NODE_DTYPE, Op
+
+    nodes = np.zeros(2, dtype=NODE_DTYPE)
+    nodes[0] = (int(Op.VAR), 0, 8, 0, 0, 0, 0, 0)
+    nodes[1] = (int(Op.ZEXT), 0, 16, 0, 0, 0, 5000, 0)  # extension beyond any width
+    with pytest.raises(native.SieveError):
+        native.harvest_guide(nodes, np.zeros((1, 8), np.uint32), [8])
+    nodes[0] = (int(Op.TRUE), 0, 0, 0, 0, 0, 0, 0)
+    nodes[1] = (int(Op.SEXT), 0, 8, 0, 0, 0, 8, 0)  # sign extension of a Bool
+    with pytest.raises(native.SieveError):
+        native.harvest_guide(nodes, np.zeros((1, 8), np.uint32), [8])
