@@ -12,10 +12,13 @@ hard variants) and report, per query, two latencies (medians of SIEVE_QUERY_REPS
 plus hit or miss, launches, per-stage milliseconds of the last timed incremental solve, and any
 exception (the front end swallows them to fall back; this script shows them).  One JSON line
 per query.  No query is ever timed twice on the same terms (get_model's lru_cache answers a
-repeated query before the sieve sees it).
+repeated query before the sieve sees it).  Each timed solve starts after a gc.collect(): every rep
+rebuilds all the shapes on a fresh term context, and the collector's pause for that harness garbage
+is not the query's.
 
     python scripts/sieve_queries.py [rows_per_round]
 """
+import gc
 import json
 import os
 import sys
@@ -61,6 +64,7 @@ def main():
                     solve(s, qctx, cs[:k])
                 before = dict(s.stats.stage_s)
                 r0 = s.stats.rounds
+                gc.collect()  # the harness's own garbage (every rep rebuilds all the shapes)
                 t0 = time.perf_counter()
                 w = solve(s, qctx, cs)
                 inc.append((time.perf_counter() - t0) * 1e3)
@@ -68,6 +72,7 @@ def main():
                           for k, v in s.stats.stage_s.items() if v - before.get(k, 0.0) > 0}
                 rounds = s.stats.rounds - r0
                 qctx, cs = fresh(kind, name)
+                gc.collect()
                 t0 = time.perf_counter()
                 wc = solve(s, qctx, cs)
                 cold.append((time.perf_counter() - t0) * 1e3)

@@ -124,10 +124,13 @@ def test_guided_generator_rejects_malformed_guides(gpu_ctx):
         a.generate_guided(1, arrays, first=60, count=10)
 
 
-@pytest.mark.parametrize("qi", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
-def test_sieve_witnesses_are_models(gpu_ctx, qi):
+SAT_SHAPES = [n for n, _ in queries()[1] if not n.startswith("unsat")]
+
+
+@pytest.mark.parametrize("name", SAT_SHAPES)
+def test_sieve_witnesses_are_models(gpu_ctx, name):
     ctx, qs = queries()
-    name, cs = qs[qi]
+    cs = dict(qs)[name]
     m = frontend.get_model(tuple(cs))  # no fallback: a miss would raise UnsatError
     assert _oracle_holds(ctx, cs, m.schema, m.values), name
     for c in cs:  # Model.eval on the device agrees
@@ -174,15 +177,15 @@ def test_parent_witness_is_reused(gpu_ctx):
     assert _oracle_holds(ctx, cs, m.schema, m.values)
 
 
-@pytest.mark.parametrize("qi", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
-def test_solver_log_queries_on_gpu(gpu_ctx, qi):
+@pytest.mark.parametrize("name", SAT_SHAPES)
+def test_solver_log_queries_on_gpu(gpu_ctx, name):
     """--solver-log ingestion: every LASER-shaped SAT query in the SMT-LIB2 form the reference's
     get_model writes (support/model.py:44-55, z3's sexpr()), read back by smtlib.parse and
     answered by the sieve on the GPU; each witness is a model of the PARSED query (oracle)."""
     from mythril_amd import smtlib
 
     ctx, qs = queries()
-    name, cs = qs[qi]
+    cs = dict(qs)[name]
     try:
         text = smtlib.to_smtlib(cs)
     except smtlib.SmtlibError:
