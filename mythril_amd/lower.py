@@ -157,22 +157,29 @@ def _walk(b: TapeBuilder, roots: Iterable[int], host_only: bool = False) -> List
     """Every node reachable from roots (array chains included), children before parents; with
     ``host_only``, only the nodes that are or read host-only terms (F_HOST)."""
     order, seen = [], set()
-    fl = b.flags
-    stack = [(r, False) for r in roots if not host_only or fl[r] & F_HOST]
+    fl, nodes = b.flags, b.nodes
+    want = F_HOST if host_only else -1  # flags & -1 is nonzero for every node but flags 0
+    # a node is pushed as n (visit) and later as ~n (emit, after its operands)
+    stack = [r for r in roots if not host_only or fl[r] & F_HOST]
     while stack:
-        n, done = stack.pop()
-        if done:
-            order.append(n)
+        n = stack.pop()
+        if n < 0:
+            order.append(~n)
             continue
         if n in seen:
             continue
         seen.add(n)
-        stack.append((n, True))
-        op, _, a, bb, c, _, _ = b.nodes[n]
-        k = _arity(op)
-        for ch in (a, bb, c)[:k][::-1]:
-            if ch not in seen and (not host_only or fl[ch] & F_HOST):
-                stack.append((ch, False))
+        stack.append(~n)
+        op, _, a, bb, c, _, _ = nodes[n]
+        k = ARITY[op]
+        if k == 0:
+            continue
+        if k > 2 and c not in seen and (not host_only or fl[c] & want):
+            stack.append(c)
+        if k > 1 and bb not in seen and (not host_only or fl[bb] & want):
+            stack.append(bb)
+        if a not in seen and (not host_only or fl[a] & want):
+            stack.append(a)
     return order
 
 
