@@ -102,12 +102,24 @@ class Harvest:
                              for f, p in self.keccak.items())))
 
 
+MEMO_LIMIT = 1 << 21  # entries of a builder-level memo before it is dropped (a long run's bound)
+
+
+def _memo(b: TapeBuilder, name: str) -> dict:
+    """A memo on the builder (its nodes are immutable and hash-consed), started afresh once it
+    holds MEMO_LIMIT entries."""
+    m = b.__dict__.get(name)
+    if m is None or len(m) > MEMO_LIMIT:
+        m = b.__dict__[name] = {}
+    return m
+
+
 def node_columns(b: TapeBuilder, roots: Iterable[int]) -> Dict[int, frozenset]:
     """The VAR indices under each of `roots` (memoised per root on the builder: nodes are
     immutable and hash-consed).  A walk stops at any node already in the memo, so a LASER query
     that extends its parent's (svm.py:257-262) only visits its new conjunct; the nodes between
     are not given sets of their own (a set per node cost more than the walk)."""
-    cols: Dict[int, frozenset] = b.__dict__.setdefault("_node_cols", {})
+    cols: Dict[int, frozenset] = _memo(b, "_node_cols")
     nodes, var = b.nodes, Op.VAR
     for r in roots:
         if r in cols:
@@ -206,8 +218,6 @@ class Lowering:
         # builder for every Lowering, so a query whose new constraint adds table keys (a fresh
         # calldata word) does not re-lower its parent's constraints
         self.dep: set = set()
-        self.stable: Dict[int, int] = (b.__dict__.setdefault("_stable_lower", {})
-                                       if frozen is None else {})
 
     # -- pass 1: harvest ------------------------------------------------------------------
     def harvest(self, roots: Sequence[int]) -> None:
@@ -342,7 +352,8 @@ class Lowering:
         prune = not self.frozen
         if prune and not fl[root] & F_HOST:
             return root
-        stable, dep = self.stable, self.dep
+        stable = _memo(self.b, "_stable_lower") if prune else {}
+        dep = self.dep
         got = stable.get(root)
         if got is not None:
             memo[root] = got
@@ -550,7 +561,7 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
         low = [L.lower(r) for r in roots]
         schema = L.schema
     else:
-        per_root: Dict[int, Harvest] = b.__dict__.setdefault("_harvest_of", {})
+        per_root: Dict[int, Harvest] = _memo(b, "_harvest_of")
         h = Harvest()
         for r in roots:
             got = per_root.get(r)
