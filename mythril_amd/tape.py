@@ -369,7 +369,7 @@ class TapeBuilder:
 
         Post-order of AND(x, y) is x's post-order, then y's nodes not under x, then the AND; a
         path condition grows by one conjunct per LASER query (svm.py:257-262), so the tapes of
-        recent AND roots are kept and a child query's tape extends its parent's."""
+        recent roots are kept and a child query's tape extends its parent's."""
         cache = self.__dict__.setdefault("_finished", OrderedDict())
         got = cache.get(root)
         if got is not None:
@@ -413,11 +413,12 @@ class TapeBuilder:
         arr = np.array(rows, dtype=NODE_DTYPE)
         if base is not None:
             arr = np.concatenate([base[1], arr])
-        if node[0] == Op.AND:
-            arr.flags.writeable = False  # shared with later tapes: callers copy to modify
-            cache[root] = (remap, arr)
-            while len(cache) > FINISH_CACHE:
-                cache.popitem(last=False)
+        # every root is kept (a one-constraint query's root is its conjunct, the next query's
+        # AND extends it)
+        arr.flags.writeable = False  # shared with later tapes: callers copy to modify
+        cache[root] = (remap, arr)
+        while len(cache) > FINISH_CACHE:
+            cache.popitem(last=False)
         return Tape(arr)
 
 
