@@ -292,8 +292,21 @@ struct Lowering {
             const mh_node& c = t[(size_t)v.remat];
             if (c.op == MH_OP_TRUE) return emit(D_TRUE, -1, -1, -1, 1);
             if (c.op == MH_OP_FALSE) return emit(D_FALSE, -1, -1, -1, 1);
-            if (c.op == MH_OP_VAR)
-                return masked(emit(D_LOADVAR, -1, -1, -1, 256, c.imm0), c.width);
+            if (c.op == MH_OP_VAR) {
+                const uint64_t key = (uint64_t)c.imm0 << 16 | c.width;
+                bool hold = false;
+                if (hold_vars) {
+                    auto u = uses_.find(key);
+                    hold = u != uses_.end() && u->second >= kHoldUses;
+                }
+                if (hold) {
+                    auto it = held_.find(key);
+                    if (it != held_.end()) return it->second;
+                }
+                const int r = masked(emit(D_LOADVAR, -1, -1, -1, 256, c.imm0), c.width);
+                if (hold) held_.emplace(key, r);
+                return r;
+            }
             return emit(D_LOADC, -1, -1, -1, 256, 0,
                         (int)const_index(consts + 8ull * c.imm0, c.width));
         }
@@ -350,6 +363,15 @@ struct Lowering {
     // machine code for, restated on ops it has.  Same values as exec.h complex_op on canonical
     // operands (tests/test_jit.py checks each against the oracle).
     bool jit = false;
+    // interpreter: a loaded-on-use column read by at least kHoldUses operands is loaded once and
+    // kept in a register (each load is a complex op, ~1 us of a wave's time; calldata bytes all
+    // compare their index with calldatasize) -- off again when the tape runs out of registers
+    bool hold_vars = false;
+    // (uses are counted per column and width: a rematerialised tape gives every use of a column
+    // a VAR node of its own)
+    static constexpr uint32_t kHoldUses = 3;
+    std::unordered_map<uint64_t, uint32_t> uses_;
+    std::unordered_map<uint64_t, int> held_;
 
     int small_const(uint32_t x) {
         const uint32_t m[8] = {x, 0, 0, 0, 0, 0, 0, 0};
@@ -521,6 +543,18 @@ bool Lowering::lower(std::vector<Val>& vals) {
     }
     vals.assign(n, Val());
     vals_ = &vals;
+    if (hold_vars) {  // operand references per (column, width), live nodes
+        for (size_t i = 0; i < n; ++i) {
+            if (!live[i]) continue;
+            const mh_node& nd = t[i];
+            const int ar = arity(nd);
+            const uint32_t ops[3] = {nd.a, nd.b, nd.c};
+            for (int k = 0; k < ar; ++k) {
+                const mh_node& o = t[ops[k]];
+                if (o.op == MH_OP_VAR) ++uses_[(uint64_t)o.imm0 << 16 | o.width];
+            }
+        }
+    }
     // evaluation order: post-order DFS from the root, operands with the larger Sethi-Ullman
     // register need first (the input order is only required to be topological)
     std::vector<uint32_t> need(n, 1);
@@ -1180,7 +1214,7 @@ void rewrite_wide_modops(std::vector<mh_node>& t) {
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,
-                       std::string& err, int value_numbering, bool jit_forms) {
+                       std::string& err, int value_numbering, bool jit_forms, bool hold_vars) {
     if (n_nodes == 0) {
         err = "empty tape";
         return MH_E_INVALID;
@@ -1189,6 +1223,7 @@ int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* con
     rewrite_wide_modops(t);
     Lowering L(t, consts, n_consts, n_vars, dconsts, dconst_index);
     L.jit = jit_forms;
+    L.hold_vars = hold_vars;
     std::vector<Val> vals;
     if (!L.lower(vals)) {
         err = L.err;
@@ -1279,25 +1314,34 @@ std::vector<mh_node> rematerialize(const mh_node* t, size_t n, uint32_t max_size
 int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                           uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                           std::unordered_map<std::string, uint32_t>& dconst_index,
-                          std::vector<uint32_t>& words, CompiledTape& out, std::string& err);
+                          std::vector<uint32_t>& words, CompiledTape& out, std::string& err,
+                          bool hold_vars);
 
 }  // namespace
 
-// A tape that runs out of registers is retried with cheap shared sub-terms duplicated at their
-// uses, widening what counts as cheap (8, 32, 256 nodes).
+// A tape that runs out of registers is retried without held columns (Lowering::hold_vars), then
+// with cheap shared sub-terms duplicated at their uses, widening what counts as cheap (8, 32, 256
+// nodes) -- each size first with held columns, then without.
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                      uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                      std::unordered_map<std::string, uint32_t>& dconst_index,
                      std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
-    int32_t r = compile_tape_once(nodes, n_nodes, consts, n_consts, n_vars, dconsts, dconst_index,
-                                  words, out, err);
-    for (uint32_t sz : {8u, 32u, 256u}) {
-        if (r != MH_E_UNSUPPORTED || err.find("register pressure") == std::string::npos) break;
-        std::vector<mh_node> t2 = rematerialize(nodes, n_nodes, sz);
-        err.clear();
-        r = compile_tape_once(t2.data(), t2.size(), consts, n_consts, n_vars, dconsts,
-                              dconst_index, words, out, err);
-        out.n_nodes = (uint32_t)n_nodes;
+    const bool hold = n_vars > MH_MAX_PRELOAD && !std::getenv("MH_NO_HOLD_VARS");
+    int32_t r = MH_E_UNSUPPORTED;
+    for (uint32_t sz : {0u, 8u, 32u, 256u}) {
+        std::vector<mh_node> t2;
+        if (sz) t2 = rematerialize(nodes, n_nodes, sz);
+        const mh_node* tn = sz ? t2.data() : nodes;
+        const size_t nn = sz ? t2.size() : n_nodes;
+        for (bool h : {true, false}) {
+            if (h && !hold) continue;
+            err.clear();
+            r = compile_tape_once(tn, nn, consts, n_consts, n_vars, dconsts, dconst_index, words,
+                                  out, err, h);
+            out.n_nodes = (uint32_t)n_nodes;
+            if (r != MH_E_UNSUPPORTED || err.find("register pressure") == std::string::npos)
+                return r;
+        }
     }
     return r;
 }
@@ -1307,10 +1351,11 @@ namespace {
 int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                           uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                           std::unordered_map<std::string, uint32_t>& dconst_index,
-                          std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
+                          std::vector<uint32_t>& words, CompiledTape& out, std::string& err,
+                          bool hold_vars) {
     SsaTape st;
     if (int32_t r = lower_tape_ssa(nodes, n_nodes, consts, n_consts, n_vars, dconsts,
-                                   dconst_index, st, err))
+                                   dconst_index, st, err, 0, false, hold_vars))
         return r;
     out.alg_ops = st.alg_ops;
     out.n_nodes = (uint32_t)n_nodes;

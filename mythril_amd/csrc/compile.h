@@ -55,7 +55,8 @@ struct SsaTape {
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                        std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& out,
-                       std::string& err, int value_numbering = 0, bool jit_forms = false);
+                       std::string& err, int value_numbering = 0, bool jit_forms = false,
+                       bool hold_vars = false);
 constexpr int kVnAll = 1, kVnNoLoads = 2;
 
 // Bool values of the SSA registers `want` on n_rows sample rows (each pinned column a uniform

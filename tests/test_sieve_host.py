@@ -28,7 +28,7 @@ def _soa(rows, n_cols):
     return soa
 
 
-@pytest.mark.parametrize("qi", range(12))
+@pytest.mark.parametrize("qi", range(len(queries()[1])))
 def test_queries_compile_and_match_oracle(emu, qi):
     ctx, qs = queries()
     name, cs = qs[qi]
@@ -96,3 +96,31 @@ def test_buckets_split_variable_disjoint_conjuncts():
     assert sizes["selector"] == 2        # calldata bytes + size  |  sender in ACTORS
     assert sizes["owner_check"] == 1     # Storage[0] == sender ties them
     assert sizes["keccak_alias"] == 1
+
+
+def test_hot_columns_are_loaded_once(emu):
+    """A loaded-on-use column read by many operands (every calldata byte compares its index with
+    calldatasize, calldata.py:48-54) is loaded once and held in a register by the interpreter's
+    compiler (compile.cpp Lowering::hold_vars): fewer D_LOADVAR complex ops, same values."""
+    import os
+
+    from mythril_amd.sieve import local_tapeset
+
+    ctx, qs = queries()
+    cs = dict(qs)["overflow"]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    cols = list(schema.columns)
+    ts = local_tapeset(ctx.b, [root], cols)
+    guide = build_guide(ctx.b, root, schema, cols).arrays()
+    rows = [generate_row(5, r, guide) for r in range(64)]
+    soa = _soa(rows, len(cols))
+    held, _ = emu.eval(ts, 0, soa)
+    n_held = emu.n_slots(ts)
+    os.environ["MH_NO_HOLD_VARS"] = "1"
+    try:
+        plain, _ = emu.eval(ts, 0, soa)
+        n_plain = emu.n_slots(ts)
+    finally:
+        del os.environ["MH_NO_HOLD_VARS"]
+    assert [bool(x) for x in held] == [bool(x) for x in plain]
+    assert n_held < n_plain, (n_held, n_plain)
