@@ -8,6 +8,7 @@
 #   bench     default bench.py (N=1)
 #   miss      scripts/miss_cost.py (per-stage cost of sieve misses, JIT build vs interpreter)
 #   queries   scripts/sieve_queries.py (per-query latency, LASER order and cold)
+#   latency   two more passes of sieve_queries.py at 9 repetitions (sieve_queries_{a,b}.jsonl)
 #   counters  rocprofv3 -L (the PMC counters this box offers)
 #   profile   scripts/profile.sh <tag> (kernel trace + PMC passes of the default bench)
 set -o pipefail
@@ -26,6 +27,10 @@ for step in "$@"; do
     bench)    timeout -k 10 600 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.log" ;;
     miss)     timeout -k 10 400 python -u scripts/miss_cost.py 5 > "$OUT/miss_cost.jsonl" 2> "$OUT/miss_cost.log" ;;
     queries)  timeout -k 10 400 python -u scripts/sieve_queries.py > "$OUT/sieve_queries.jsonl" 2> "$OUT/sieve_queries.log" ;;
+    latency)  SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py \
+                > "$OUT/sieve_queries_a.jsonl" 2> "$OUT/a.log" && \
+              SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py \
+                > "$OUT/sieve_queries_b.jsonl" 2> "$OUT/b.log" ;;
     counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 ;;
     profile)  bash scripts/profile.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
