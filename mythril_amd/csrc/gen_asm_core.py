@@ -46,6 +46,11 @@ PREFETCH = SMEM_INSNS and os.environ.get("MH_GEN_PREFETCH", "1") != "0"
 # (MH_GEN_PREFETCH_CONSTS=0: constants by their own s_load_dwordx8)
 PREFETCH_CONSTS = PREFETCH and SMEM_CONSTS and os.environ.get("MH_GEN_PREFETCH_CONSTS", "1") != "0"
 NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
+# D_LOADVAR (a column beyond the preloaded ones) in the core, as 8 global loads, instead of an
+# exit to the C++ driver (~1 us of a wave's time per exit); only in the
+# run_lv form the complex-op kernel variants use (MH_GEN_LOADVAR=0: every LOADVAR exits)
+LOADVAR = os.environ.get("MH_GEN_LOADVAR", "1") != "0"
+D_LOADVAR = 118     # dev_isa.h (static_assert in the .inc)
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
 OPS = ["EXIT", "NOP",
@@ -94,8 +99,9 @@ SGPR_CLOBBERS = ["s%d" % i for i in range(40, 88 if PREFETCH_CONSTS else 72)]
 
 
 class Core:
-    def __init__(self, nr: int):
+    def __init__(self, nr: int, loadvar: bool = False):
         self.nr = nr
+        self.loadvar = loadvar
         self.nr1 = nr + 1
         self.sb = 8 * self.nr1  # scratch base
         self.no_wb = False
@@ -255,6 +261,25 @@ class Core:
         off = self.idx_off()
         if name == "EXIT":
             return ["s_branch L_out_%="]
+        if name == "LOADVAR":
+            # X = column aux of this lane's row: limb k at vbase + ((8 col + k) cap4) + voff
+            # (SoA planes, KParams::assign); the address is SALU arithmetic in s[56:57] (no
+            # VALU-written SGPR reaches the loads), the row's byte offset the VGPR voff
+            lo, hi = S_K[0], S_K[1]
+            body = ["s_lshr_b32 {}, {}, 17".format(S_T, S_W1),
+                    "s_and_b32 {0}, {0}, 0x3fff".format(S_T),
+                    "s_lshl_b32 {0}, {0}, 3".format(S_T),
+                    "s_mul_i32 {}, {}, %[cap4]".format(lo, S_T),
+                    "s_mul_hi_u32 {}, {}, %[cap4]".format(hi, S_T),
+                    "s_add_u32 {0}, {0}, %[vlo]".format(lo),
+                    "s_addc_u32 {0}, {0}, %[vhi]".format(hi)]
+            for k in range(8):
+                if k:
+                    body += ["s_add_u32 {0}, {0}, %[cap4]".format(lo),
+                             "s_addc_u32 {0}, {0}, 0".format(hi)]
+                body.append("global_load_dword {}, %[voff], s[{}:{}]".format(X(k), lo[1:], hi[1:]))
+            body.append("s_waitcnt vmcnt(0)")
+            return body + self.wb() + self.dispatch(1)
         if name == "NOP":
             body = a_src0 + ["v_mov_b32 {}, {}".format(X(k), P(k)) for k in range(8)] + off
             return body + self.wb() + self.dispatch(1)
@@ -692,8 +717,10 @@ class Core:
         for i in range(NSLOTS):
             lines.append(".org L_tab_%= + {}".format(i * SLOT))
             name = OPS[i] if i < len(OPS) else "EXIT"
+            if i == D_LOADVAR and self.loadvar:
+                name = "LOADVAR"
             h = self.handler(name)
-            if name in OUT_OF_LINE:  # too long for a slot: jump to a body after the table
+            if name in OUT_OF_LINE or name == "LOADVAR":  # too long for a slot: jump to a body after the table
                 lines.append("s_branch L_body_{}_%=".format(name))
                 bodies += ["L_body_{}_%=:".format(name)] + h
             else:
@@ -733,35 +760,48 @@ def emit(out):
     w("#pragma once\n\n")
     for name, num in OPNUM.items():
         w("static_assert(D_{} == {}, \"asm core opcode numbering\");\n".format(name, num))
-    w("static_assert(D_NUM_ASM == {}, \"asm core covers every asm op\");\n\n".format(len(OPS)))
+    w("static_assert(D_NUM_ASM == {}, \"asm core covers every asm op\");\n".format(len(OPS)))
+    w("static_assert(D_LOADVAR == {}, \"asm core LOADVAR slot\");\n".format(D_LOADVAR))
+    w("#define MH_ASM_LOADVAR {}\n\n".format(int(LOADVAR)))
     w("template <int NR> struct AsmCore;\n\n")
     for nr in (7, 9, 15):
         c = Core(nr)
         nr1 = nr + 1
         w("template <> struct AsmCore<{}> {{\n".format(nr))
         w("    typedef u32 plane_t __attribute__((ext_vector_type({})));\n".format(nr1))
-        w("    // runs asm-core instructions from slot ip of the window (ic0, ic1); returns the\n")
-        w("    // slot of the first instruction it does not handle\n")
-        w("    __device__ __forceinline__ static u32 run(plane_t& p0, plane_t& p1, plane_t& p2,\n")
-        w("                                              plane_t& p3, plane_t& p4, plane_t& p5,\n")
-        w("                                              plane_t& p6, plane_t& p7, u32 ic0, u32 ic1,\n")
-        w("                                              u32 ip, const void* gwin) {\n")
-        w("        asm volatile(\n")
-        for line in c.asm_text():
-            w("            \"{}\\n\"\n".format(line))
         cons = []
         for k in range(8):
             cons.append("\"+{{v[{}:{}]}}\"(p{})".format(k * nr1, k * nr1 + nr, k))
-        w("            : {}, [ip] \"+s\"(ip)\n".format(", ".join(cons)))
-        w("            : [ic0] \"v\"(ic0), [ic1] \"v\"(ic1), [gwin] \"s\"(gwin)\n")
-        check_registers(c, c.asm_text(), N_SCRATCH)
-        check_registers(c, c.fetch_text(), N_SCRATCH)
-        check_registers(c, c.commit_text(), N_SCRATCH)
         clob = ["\"v{}\"".format(c.sb + j) for j in range(N_SCRATCH)] + \
                ["\"{}\"".format(s) for s in SGPR_CLOBBERS] + ["\"vcc\"", "\"scc\"", "\"m0\""]
-        w("            : {});\n".format(", ".join(clob)))
-        w("        return ip;\n")
-        w("    }\n")
+        forms = [(c, "run", "")]
+        if LOADVAR:
+            forms.append((Core(nr, loadvar=True), "run_lv",
+                          ", u32 vlo, u32 vhi, u32 cap4, u32 voff"))
+        for core, fname, extra in forms:
+            w("    // runs asm-core instructions from slot ip of the window (ic0, ic1); returns the\n")
+            w("    // slot of the first instruction it does not handle\n")
+            if extra:
+                w("    // (run_lv also runs D_LOADVAR: columns at vhi:vlo, cap4 bytes per limb plane,\n")
+                w("    // this lane's row at byte offset voff)\n")
+            w("    __device__ __forceinline__ static u32 {}(plane_t& p0, plane_t& p1, plane_t& p2,\n".format(fname))
+            w("            plane_t& p3, plane_t& p4, plane_t& p5, plane_t& p6, plane_t& p7, u32 ic0,\n")
+            w("            u32 ic1, u32 ip, const void* gwin{}) {{\n".format(extra))
+            w("        asm volatile(\n")
+            for line in core.asm_text():
+                w("            \"{}\\n\"\n".format(line))
+            w("            : {}, [ip] \"+s\"(ip)\n".format(", ".join(cons)))
+            ins = "[ic0] \"v\"(ic0), [ic1] \"v\"(ic1), [gwin] \"s\"(gwin)"
+            if extra:
+                ins += (", [vlo] \"s\"(vlo), [vhi] \"s\"(vhi), [cap4] \"s\"(cap4), "
+                        "[voff] \"v\"(voff)")
+            w("            : {}\n".format(ins))
+            check_registers(core, core.asm_text(), N_SCRATCH)
+            w("            : {});\n".format(", ".join(clob)))
+            w("        return ip;\n")
+            w("    }\n")
+        check_registers(c, c.fetch_text(), N_SCRATCH)
+        check_registers(c, c.commit_text(), N_SCRATCH)
         sb = c.sb
         vec = "typedef u32 v8_t __attribute__((ext_vector_type(8)));\n"
         w("    " + vec)

@@ -115,8 +115,18 @@ __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, I
     u32 win = 0, ip = 0;
     for (;;) {
 #if MH_ASM_CORE
-        ip = AsmCore<NR>::run(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6, m.R.p7,
-                              ic.w0, ic.w1, ip, gsrc + win);
+        if constexpr (FEAT != 0 && MH_ASM_LOADVAR) {
+            // columns beyond the preloaded ones load inside the core (no exit per LOADVAR);
+            // launch_sieve keeps capacity * 4 within 32 bits
+            const u64 a = (u64)(uintptr_t)m.p->assign;
+            ip = AsmCore<NR>::run_lv(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
+                                     m.R.p7, ic.w0, ic.w1, ip, gsrc + win, (u32)a,
+                                     (u32)(a >> 32), (u32)(m.p->capacity * 4u),
+                                     (u32)m.lrow * 4u);
+        } else {
+            ip = AsmCore<NR>::run(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
+                                  m.R.p7, ic.w0, ic.w1, ip, gsrc + win);
+        }
 #endif
         const u32 w0 = __builtin_amdgcn_readlane(ic.w0, ip);
         const u32 w1 = __builtin_amdgcn_readlane(ic.w1, ip);
@@ -542,6 +552,8 @@ namespace mh {
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream) {
     if (p.row_count == 0 || p.n_ids == 0) return hipSuccess;
+    // the asm core's LOADVAR addresses a limb plane with a 32-bit byte stride
+    if (p.capacity >= (1ull << 30)) return hipErrorInvalidValue;
     constexpr int kCplx = F_CPLX, kKec = F_CPLX | F_KECCAK, kAll = F_CPLX | F_KECCAK | F_EVM;
     switch (variant) {
         case 0: return launch_variant<MH_NR_SMALL, 0>(p, stream);

@@ -9,6 +9,7 @@
 #   miss      scripts/miss_cost.py (per-stage cost of sieve misses, JIT build vs interpreter)
 #   queries   scripts/sieve_queries.py (per-query latency, LASER order and cold)
 #   latency   two more passes of sieve_queries.py at 9 repetitions (sieve_queries_{a,b}.jsonl)
+#   interp    scripts/interp_op_cost.py (interpreter cost of a loaded column / a complex op)
 #   counters  rocprofv3 -L (the PMC counters this box offers)
 #   profile   scripts/profile.sh <tag> (kernel trace + PMC passes of the default bench)
 set -o pipefail
@@ -31,6 +32,7 @@ for step in "$@"; do
                 > "$OUT/sieve_queries_a.jsonl" 2> "$OUT/a.log" && \
               SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py \
                 > "$OUT/sieve_queries_b.jsonl" 2> "$OUT/b.log" ;;
+    interp)   timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost.jsonl" 2> "$OUT/interp_op_cost.log" ;;
     counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 ;;
     profile)  bash scripts/profile.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -28,7 +28,8 @@ def _asm_lines(lines):
     out = []
     for ln in lines:
         ln = (ln.replace("%[ip]", "s39").replace("%[ic0]", "v200").replace("%[ic1]", "v201")
-              .replace("%[gwin]", "s[80:81]")
+              .replace("%[gwin]", "s[80:81]").replace("%[voff]", "v202")
+              .replace("%[vlo]", "s36").replace("%[vhi]", "s37").replace("%[cap4]", "s38")
               .replace("%=", "0"))
         if ln.endswith(":"):
             continue
@@ -58,6 +59,7 @@ def test_handlers_fit_their_slots(nr):
 def test_gpr_index_mode_is_balanced(nr):
     core = G.Core(nr)
     bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
+    bodies.append(("LOADVAR", G.Core(nr, loadvar=True).handler("LOADVAR")))
 
     for name, lines in bodies:
         on = False
@@ -94,6 +96,7 @@ def test_indexed_slots_hold_vgprs(nr):
     mixtures)."""
     core = G.Core(nr)
     bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
+    bodies.append(("LOADVAR", G.Core(nr, loadvar=True).handler("LOADVAR")))
     bodies += [("fetch", core.fetch_text()), ("commit", core.commit_text())]
     vgpr = re.compile(r"^v(\d+|\[\d+:\d+\])$")
     for name, lines in bodies:
@@ -170,6 +173,7 @@ def test_indexed_operands_stay_in_the_register_file(nr):
     core = G.Core(nr)
     planes = 8 * (nr + 1)
     bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
+    bodies.append(("LOADVAR", G.Core(nr, loadvar=True).handler("LOADVAR")))
     bodies += [("fetch", core.fetch_text()), ("commit", core.commit_text())]
     vreg = re.compile(r"^v(?:(\d+)|\[(\d+):(\d+)\])$")
     checked = 0
@@ -199,3 +203,40 @@ def test_indexed_operands_stay_in_the_register_file(nr):
                 assert hi + nr < planes, (name, ln, "index reaches v%d" % (hi + nr))
                 checked += 1
     assert checked > 100
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not installed")
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_loadvar_handler(nr):
+    """The in-core D_LOADVAR (run_lv): assembles for gfx950; its table slot jumps to the body
+    only in the run_lv form (run keeps the exit, the asm-only variants never see a LOADVAR);
+    limb k lands in X's plane k from the address vbase + (8 col + k) cap4 + voff; the loads
+    complete before the write-back; the prefetched next words are taken as in every handler."""
+    core = G.Core(nr, loadvar=True)
+    lines = core.handler("LOADVAR")
+    src = "\n".join(_asm_lines(lines)) + "\n"
+    p = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "-show-encoding"],
+                       input=src, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[:400]
+    loads = [ln for ln in lines if ln.startswith("global_load_dword")]
+    assert loads == ["global_load_dword {}, %[voff], s[56:57]".format(core.X(k)) for k in range(8)]
+    assert lines.index("s_waitcnt vmcnt(0)") > lines.index(loads[-1])
+    assert lines.index("s_waitcnt vmcnt(0)") < next(i for i, ln in enumerate(lines)
+                                                     if ln.startswith("s_set_gpr_idx_on"))
+    assert sum(ln == "s_add_u32 s56, s56, %[cap4]" for ln in lines) == 7
+    text = core.asm_text()
+    slot = text.index(".org L_tab_%= + {}".format(G.D_LOADVAR * G.SLOT))
+    assert text[slot + 1] == "s_branch L_body_LOADVAR_%="
+    plain = G.Core(nr).asm_text()
+    slot = plain.index(".org L_tab_%= + {}".format(G.D_LOADVAR * G.SLOT))
+    assert plain[slot + 1] == "s_branch L_out_%=" and not any("%[voff]" in ln for ln in plain)
+    G.check_registers(core, text, G.N_SCRATCH)
+
+
+def test_loadvar_slot_matches_isa_header():
+    src = open(os.path.join(CSRC, "dev_isa.h")).read()
+    body = src[src.index("enum mh_dop"):src.index("D_NUM_OPS")]
+    body = "\n".join(line.split("//")[0] for line in body.splitlines())
+    body = body[body.index("D_FIRST_COMPLEX = 112,") + len("D_FIRST_COMPLEX = 112,"):]
+    after = re.findall(r"\b(D_[A-Z0-9_]+)\b", body.replace("= D_FIRST_COMPLEX", ""))
+    assert 112 + after.index("D_LOADVAR") == G.D_LOADVAR

@@ -513,3 +513,39 @@ def test_handles_outlive_their_context(gpu_ctx):
     ct.close()
     cts[0].close()
     a.close()             # the last child frees the context
+
+
+def test_wide_columns_full_occupancy(gpu_ctx):
+    """Tapes over 24 columns: 20 beyond the 4 preloaded ones, read by D_LOADVAR, which the asm
+    core of the complex-op variants runs itself (gen_asm_core.py run_lv: 8 global loads, no exit
+    to the C++ driver).  At 2^20 rows (4096 workgroups, >= 2 waves per SIMD, where round 1's
+    asm-core defects showed) every tape's hit count and first hit equal the C oracle's, and on a
+    96-row upload every tape's value equals the Python oracle's."""
+    from oracle import ctape
+
+    rng = random.Random(7700)
+    ts = TapeSet()
+    fz = TapeFuzzer(rng, ts, n_vars=24, allow_keccak=False, max_depth=4)
+    for _ in range(48):
+        fz.tape(root_bool=True)
+    ct = gpu_ctx.compile(ts)
+    assert sum(1 for x in ct.info() if x["features"] & 8) >= 24  # F_CPLX: the run_lv variants
+    seed, rows = 0x1D3A, 1 << 20
+    a = gpu_ctx.assignments(ts.n_vars, rows)
+    a.generate(seed, 0)
+    fh, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    cnt, first = ctape.count(ts, seed, 0, rows, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(hc, cnt), "hit counts differ from the C oracle"
+    assert np.array_equal(fh, first), "first hits differ from the C oracle"
+    assert 0 < int((hc > 0).sum()) < len(ts.tapes) + 1
+    ts2 = TapeSet()
+    fz = TapeFuzzer(random.Random(7701), ts2, n_vars=24, allow_keccak=False, max_depth=4)
+    for _ in range(24):
+        fz.tape()
+    soa = assignment_soa(random.Random(7702), ts2.n_vars, 96)
+    ct2 = gpu_ctx.compile(ts2)
+    a2 = upload(gpu_ctx, soa)
+    for i, t in enumerate(ts2.tapes):
+        got = native.limbs_to_ints(native.eval_values(gpu_ctx, ct2, i, a2))
+        for r in range(soa.shape[2]):
+            assert got[r] == int(smt_eval.evaluate(t.nodes, ts2.pool.values, soa_row(soa, r))), (i, r)
