@@ -51,6 +51,10 @@ NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
 # run_lv form the complex-op kernel variants use (MH_GEN_LOADVAR=0: every LOADVAR exits)
 LOADVAR = os.environ.get("MH_GEN_LOADVAR", "1") != "0"
 D_LOADVAR = 118     # dev_isa.h (static_assert in the .inc)
+# likewise z3's unsigned BVAddNoOverflow (D_UADD_NOOVFL, exec.h's rule: no carry out of 256 bits
+# and no bit at or above the width), in run_lv only
+D_UADD_NOOVFL = 112
+CORE_COMPLEX = {D_LOADVAR: "LOADVAR", D_UADD_NOOVFL: "UADD_NOOVFL"}
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
 OPS = ["EXIT", "NOP",
@@ -280,6 +284,34 @@ class Core:
                 body.append("global_load_dword {}, %[voff], s[{}:{}]".format(X(k), lo[1:], hi[1:]))
             body.append("s_waitcnt vmcnt(0)")
             return body + self.wb() + self.dispatch(1)
+        if name == "UADD_NOOVFL":
+            # y = inline constant (F_YC, 4 slots follow) or R[b]; t = R[a'] + y in S8..15;
+            # h = carry | OR_k (t[k] & ~mask_k(w)), with ~mask_k = ~((1 << clamp(w - 32k, 0, 32))
+            # - 1) built in SALU (w is wave-uniform); X = (h == 0), Bool in limb 0
+            body = self.consts()
+            body += ["s_bitcmp1_b32 {}, 31".format(S_W1), "s_cbranch_scc0 L_uno_r_%="]
+            body += ["v_mov_b32 {}, {}".format(Y(k), S_K[k]) for k in range(8)]
+            body += ["s_branch L_uno_y_%=", "L_uno_r_%=:"] + self.y_reg() + ["L_uno_y_%=:"]
+            body += a_src0
+            body.append("v_add_co_u32 {}, vcc, {}, {}".format(S(8), P(0), Y(0)))
+            body += ["v_addc_co_u32 {}, vcc, {}, {}, vcc".format(S(8 + k), P(k), Y(k))
+                     for k in range(1, 8)]
+            body += off
+            body += ["v_cndmask_b32_e64 {}, 0, 1, vcc".format(S(16)),
+                     "s_lshr_b32 {}, {}, 8".format(S_T, S_W1),
+                     "s_and_b32 {0}, {0}, 0x1ff".format(S_T)]
+            for k in range(8):
+                body += ["s_sub_i32 {}, {}, {}".format(S_R, S_T, 32 * k),
+                         "s_max_i32 {0}, {0}, 0".format(S_R),
+                         "s_min_i32 {0}, {0}, 32".format(S_R),
+                         "s_bfm_b64 s[{}:{}], {}, 0".format(S_Q[1:], S_R[1:], S_R),
+                         "s_not_b32 {0}, {0}".format(S_Q),
+                         "v_and_or_b32 {0}, {1}, {2}, {0}".format(S(16), S_Q, S(8 + k))]
+            body += ["v_cmp_eq_u32 vcc, 0, {}".format(S(16))] + self.bool_out(True) + self.wb(1)
+            body += ["s_bitcmp1_b32 {}, 31".format(S_W1),
+                     "s_cselect_b32 {}, 5, 1".format(S_T),
+                     "s_add_u32 %[ip], %[ip], {}".format(S_T)]
+            return body + self.dispatch(0)
         if name == "NOP":
             body = a_src0 + ["v_mov_b32 {}, {}".format(X(k), P(k)) for k in range(8)] + off
             return body + self.wb() + self.dispatch(1)
@@ -717,10 +749,10 @@ class Core:
         for i in range(NSLOTS):
             lines.append(".org L_tab_%= + {}".format(i * SLOT))
             name = OPS[i] if i < len(OPS) else "EXIT"
-            if i == D_LOADVAR and self.loadvar:
-                name = "LOADVAR"
+            if self.loadvar and i in CORE_COMPLEX:
+                name = CORE_COMPLEX[i]
             h = self.handler(name)
-            if name in OUT_OF_LINE or name == "LOADVAR":  # too long for a slot: jump to a body after the table
+            if name in OUT_OF_LINE or name in CORE_COMPLEX.values():  # too long for a slot: jump to a body after the table
                 lines.append("s_branch L_body_{}_%=".format(name))
                 bodies += ["L_body_{}_%=:".format(name)] + h
             else:
@@ -762,6 +794,7 @@ def emit(out):
         w("static_assert(D_{} == {}, \"asm core opcode numbering\");\n".format(name, num))
     w("static_assert(D_NUM_ASM == {}, \"asm core covers every asm op\");\n".format(len(OPS)))
     w("static_assert(D_LOADVAR == {}, \"asm core LOADVAR slot\");\n".format(D_LOADVAR))
+    w("static_assert(D_UADD_NOOVFL == {}, \"asm core UADD_NOOVFL slot\");\n".format(D_UADD_NOOVFL))
     w("#define MH_ASM_LOADVAR {}\n\n".format(int(LOADVAR)))
     w("template <int NR> struct AsmCore;\n\n")
     for nr in (7, 9, 15):

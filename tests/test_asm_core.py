@@ -59,7 +59,7 @@ def test_handlers_fit_their_slots(nr):
 def test_gpr_index_mode_is_balanced(nr):
     core = G.Core(nr)
     bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
-    bodies.append(("LOADVAR", G.Core(nr, loadvar=True).handler("LOADVAR")))
+    bodies += [(n, G.Core(nr, loadvar=True).handler(n)) for n in G.CORE_COMPLEX.values()]
 
     for name, lines in bodies:
         on = False
@@ -96,7 +96,7 @@ def test_indexed_slots_hold_vgprs(nr):
     mixtures)."""
     core = G.Core(nr)
     bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
-    bodies.append(("LOADVAR", G.Core(nr, loadvar=True).handler("LOADVAR")))
+    bodies += [(n, G.Core(nr, loadvar=True).handler(n)) for n in G.CORE_COMPLEX.values()]
     bodies += [("fetch", core.fetch_text()), ("commit", core.commit_text())]
     vgpr = re.compile(r"^v(\d+|\[\d+:\d+\])$")
     for name, lines in bodies:
@@ -173,7 +173,7 @@ def test_indexed_operands_stay_in_the_register_file(nr):
     core = G.Core(nr)
     planes = 8 * (nr + 1)
     bodies = [(n, core.handler(n)) for n in G.OPS] + [("div", core.div_body())]
-    bodies.append(("LOADVAR", G.Core(nr, loadvar=True).handler("LOADVAR")))
+    bodies += [(n, G.Core(nr, loadvar=True).handler(n)) for n in G.CORE_COMPLEX.values()]
     bodies += [("fetch", core.fetch_text()), ("commit", core.commit_text())]
     vreg = re.compile(r"^v(?:(\d+)|\[(\d+):(\d+)\])$")
     checked = 0
@@ -233,6 +233,34 @@ def test_loadvar_handler(nr):
     G.check_registers(core, text, G.N_SCRATCH)
 
 
+@pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not installed")
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_uadd_noovfl_handler(nr):
+    """The in-core D_UADD_NOOVFL (run_lv only): assembles; y from the constant bank when F_YC
+    (advance 5) else R[b] (advance 1); the 8-limb carry chain reads R[a'] through one SRC0 index;
+    one SALU-built mask per limb; a Bool written back in limb 0; the next words loaded in the
+    dispatch (the advance is not static)."""
+    core = G.Core(nr, loadvar=True)
+    lines = core.handler("UADD_NOOVFL")
+    src = "\n".join(_asm_lines(lines)) + "\n"
+    p = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "-show-encoding"],
+                       input=src, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[:400]
+    assert sum(ln.startswith("v_addc_co_u32") for ln in lines) == 7
+    assert sum(ln.startswith("v_and_or_b32") for ln in lines) == 8
+    assert sum(ln.startswith("s_bfm_b64") for ln in lines) == 8
+    assert "s_cselect_b32 {}, 5, 1".format(G.S_T) in lines
+    assert lines[-9:-7] == ["s_lshl_b32 {}, %[ip], 3".format(G.S_T),
+                            "s_load_dwordx16 {}, %[gwin], {}".format(G.S_BANK, G.S_T)] \
+        or not G.PREFETCH_CONSTS
+    text = core.asm_text()
+    slot = text.index(".org L_tab_%= + {}".format(G.D_UADD_NOOVFL * G.SLOT))
+    assert text[slot + 1] == "s_branch L_body_UADD_NOOVFL_%="
+    plain = G.Core(nr).asm_text()
+    slot = plain.index(".org L_tab_%= + {}".format(G.D_UADD_NOOVFL * G.SLOT))
+    assert plain[slot + 1] == "s_branch L_out_%="
+
+
 def test_loadvar_slot_matches_isa_header():
     src = open(os.path.join(CSRC, "dev_isa.h")).read()
     body = src[src.index("enum mh_dop"):src.index("D_NUM_OPS")]
@@ -240,3 +268,4 @@ def test_loadvar_slot_matches_isa_header():
     body = body[body.index("D_FIRST_COMPLEX = 112,") + len("D_FIRST_COMPLEX = 112,"):]
     after = re.findall(r"\b(D_[A-Z0-9_]+)\b", body.replace("= D_FIRST_COMPLEX", ""))
     assert 112 + after.index("D_LOADVAR") == G.D_LOADVAR
+    assert 112 + after.index("D_UADD_NOOVFL") == G.D_UADD_NOOVFL
