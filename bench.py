@@ -78,7 +78,7 @@ def main() -> None:
 
     from mythril_amd import native, shard, synth
 
-    build_id = native.codegen_id()
+    build_id = native.codegen_id(args.engine)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

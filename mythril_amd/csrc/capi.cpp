@@ -819,6 +819,14 @@ int32_t mh_results_reset(mh_ctx* ctx, uint64_t* d_first_hit, uint64_t* d_hit_cou
     return MH_OK;
 }
 
+// A complex-op interpreter tape over a buffer of 2^30 rows per column or more (kernels.h).
+static int32_t refuse_capacity(uint64_t capacity) {
+    return set_err(MH_E_UNSUPPORTED,
+                   "interpreter tapes with complex ops (keccak, EVM helpers, overflow predicates, "
+                   "loaded columns) address < 2^30 rows per column; this buffer's stride is " +
+                   std::to_string(capacity) + " rows");
+}
+
 int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
                      const mh_assign* as, uint64_t row_first, uint64_t row_count,
                      uint64_t index_base, uint32_t mode, uint64_t* d_first_hit,
@@ -829,6 +837,21 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
     mh::KParams p = make_params(ts, tape_first, as, row_first, row_count, index_base, mode);
     p.first_hit = reinterpret_cast<unsigned long long*>(d_first_hit);
     p.hit_count = reinterpret_cast<unsigned long long*>(d_hit_count);
+    // the native code takes the jitted tapes of a whole-set run; the interpreter the rest
+    const bool use_jit = ts->has_jit && tape_first == 0 && tape_count == ts->n_tapes;
+    const std::vector<uint32_t>& ids = use_jit ? ts->ids_rest : ts->ids;
+    const uint32_t* boff = use_jit ? ts->bucket_off_rest : ts->bucket_off;
+    uint32_t* d_ids = use_jit ? ts->d_ids_rest : ts->d_ids;
+    // the interpreter's tapes of each kernel-variant bucket inside the requested range
+    const uint32_t *lo[mh::kNumVariants], *hi[mh::kNumVariants];
+    for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+        const uint32_t* b = ids.data() + boff[v];
+        const uint32_t* e = ids.data() + boff[v + 1];
+        lo[v] = std::lower_bound(b, e, tape_first);
+        hi[v] = std::lower_bound(lo[v], e, tape_first + tape_count);
+        // refused before anything is launched
+        if (hi[v] != lo[v] && !mh::variant_fits(v, p.capacity)) return refuse_capacity(p.capacity);
+    }
     std::pair<hipEvent_t, hipEvent_t> sp{nullptr, nullptr};
     if (ctx->timing) {
         MH_HIP(hipEventCreate(&sp.first));
@@ -836,25 +859,16 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
         ctx->spans.push_back(sp);
         MH_HIP(hipEventRecord(sp.first, ctx->stream));
     }
-    // the native code takes the jitted tapes of a whole-set run; the interpreter the rest
-    const bool use_jit = ts->has_jit && tape_first == 0 && tape_count == ts->n_tapes;
     if (use_jit && row_count) {
         if (int32_t r = launch_jit(ctx, ts, as, row_first, row_count, index_base, mode,
                                    d_first_hit, d_hit_count, nullptr))
             return r;
     }
-    const std::vector<uint32_t>& ids = use_jit ? ts->ids_rest : ts->ids;
-    const uint32_t* boff = use_jit ? ts->bucket_off_rest : ts->bucket_off;
-    uint32_t* d_ids = use_jit ? ts->d_ids_rest : ts->d_ids;
-    // one launch per kernel-variant bucket, over the bucket's tapes inside the requested range
+    // one launch per kernel-variant bucket
     for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
-        const uint32_t* b = ids.data() + boff[v];
-        const uint32_t* e = ids.data() + boff[v + 1];
-        const uint32_t* lo = std::lower_bound(b, e, tape_first);
-        const uint32_t* hi = std::lower_bound(lo, e, tape_first + tape_count);
-        if (hi == lo) continue;
-        p.tape_ids = d_ids + (lo - ids.data());
-        p.n_ids = (uint32_t)(hi - lo);
+        if (hi[v] == lo[v]) continue;
+        p.tape_ids = d_ids + (lo[v] - ids.data());
+        p.n_ids = (uint32_t)(hi[v] - lo[v]);
         MH_HIP(mh::launch_sieve(p, v, ctx->stream));
     }
     if (ctx->timing) MH_HIP(hipEventRecord(sp.second, ctx->stream));
@@ -898,6 +912,8 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
     if (!out && row_count) return set_err(MH_E_INVALID, "null out");
     if (row_count == 0) return MH_OK;
     if (int32_t r = use_device(ctx)) return r;
+    const uint32_t variant = mh::variant_of(ts->info[tape].n_regs, ts->info[tape].features);
+    if (!mh::variant_fits(variant, as->stride)) return refuse_capacity(as->stride);
     // the production sieve kernel in values mode, over a one-tape list
     uint32_t* d = nullptr;
     MH_HIP(hipMalloc(&d, (8 * row_count + 8) * sizeof(uint32_t)));
@@ -911,8 +927,7 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
     const uint32_t ids[8] = {tape, 0, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0, 0, 0};
     hipError_t e = hipMemcpy(d_id, ids, sizeof(ids), hipMemcpyHostToDevice);
     if (e == hipSuccess)
-        e = mh::launch_sieve(p, mh::variant_of(ts->info[tape].n_regs, ts->info[tape].features),
-                             ctx->stream);
+        e = mh::launch_sieve(p, variant, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpy(out, d, 8 * row_count * sizeof(uint32_t), hipMemcpyDeviceToHost);

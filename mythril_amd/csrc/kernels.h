@@ -38,6 +38,13 @@ inline uint32_t variant_of(uint32_t n_regs, uint32_t features) {
     return nr_class(n_regs) * 4 + fc;  // 0..11
 }
 constexpr uint32_t kNumVariants = 12;
+// The complex-op variants (feature class != 0) load columns inside the asm core (run_lv) with a
+// 32-bit byte stride per limb plane: their buffers hold fewer than 2^30 rows per column.  The
+// asm-only variants index columns with 64-bit arithmetic and take any capacity.
+constexpr uint64_t kLoadvarMaxCapacity = 1ull << 30;
+inline bool variant_fits(uint32_t variant, uint64_t capacity) {
+    return (variant & 3u) == 0 || capacity < kLoadvarMaxCapacity;
+}
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream);
 hipError_t launch_generate(uint32_t* assign, uint64_t stride, uint64_t rows, uint32_t n_vars,

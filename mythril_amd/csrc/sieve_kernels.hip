@@ -552,8 +552,9 @@ namespace mh {
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream) {
     if (p.row_count == 0 || p.n_ids == 0) return hipSuccess;
-    // the asm core's LOADVAR addresses a limb plane with a 32-bit byte stride
-    if (p.capacity >= (1ull << 30)) return hipErrorInvalidValue;
+    // the complex-op variants' LOADVAR addresses a limb plane with a 32-bit byte stride (the
+    // C-ABI refuses such runs first, with MH_E_UNSUPPORTED and a message)
+    if (!variant_fits(variant, p.capacity)) return hipErrorInvalidValue;
     constexpr int kCplx = F_CPLX, kKec = F_CPLX | F_KECCAK, kAll = F_CPLX | F_KECCAK | F_EVM;
     switch (variant) {
         case 0: return launch_variant<MH_NR_SMALL, 0>(p, stream);

@@ -55,6 +55,11 @@ _config = {
 }
 
 
+class SieveUnavailable(RuntimeError):
+    """This thread's sieve could not be created (no library, no gfx950 device); the message
+    is the original failure's."""
+
+
 def configure(*, fallback: Optional[Callable] = None, verify: Optional[Callable] = None,
               to_terms: Optional[Callable] = None, enabled: Optional[bool] = None,
               log_writer: Optional[Callable] = None, fallback_logs: Optional[bool] = None,
@@ -109,13 +114,15 @@ def sieve():
     if s is None:
         failed = getattr(_tls, "sieve_failed", None)
         if failed is not None:
-            raise failed
+            # a fresh exception per query: re-raising one saved object would chain every
+            # query's frames (and their constraints) onto its traceback
+            raise SieveUnavailable(failed)
         from .sieve import Sieve
 
         try:
             s = _tls.sieve = Sieve(**_config["sieve_kwargs"])
         except Exception as e:
-            _tls.sieve_failed = e
+            _tls.sieve_failed = "%s: %s" % (type(e).__name__, e)
             log.warning("constraint sieve unavailable, every query goes to the fallback: %s", e)
             raise
     return s

@@ -5,16 +5,13 @@ denotes a complete model — scalar symbols, array tables with an else-value, ke
 concrete pairs plus the interval map — and ``eval`` evaluates any term under it ON THE DEVICE:
 the term is lowered with the query's frozen schema (a constant key outside the table reads the
 else-value, exactly what the model assigns it), compiled, and evaluated over the one witness row
-(``mh_eval_values``, the parity path of the C-ABI).
+(``mh_eval_values``, the parity path of the C-ABI, through ``Sieve.eval_terms``).
 """
 from __future__ import annotations
 
 from typing import TYPE_CHECKING, List, Optional, Union
 
-import numpy as np
-
-from . import native
-from .lower import Schema, lower_query
+from .lower import Schema
 from .tape import BOOL, TapeError
 
 if TYPE_CHECKING:  # pragma: no cover
@@ -89,26 +86,7 @@ class Model:
         columns = list(schema.columns) or ["__ground__"]
         if columns == ["__ground__"]:
             b.var("__ground__", 1)
-        from .sieve import local_tapeset
-
-        ts = local_tapeset(b, [root], columns)
-        dev = self.sieve.ctx
-        ct = self.sieve.compile(ts)
-        try:
-            assign = dev.assignments(len(columns), 1)
-            try:
-                soa = np.zeros((len(columns), 8, 1), dtype=np.uint32)
-                for i, c in enumerate(columns):
-                    v = self.values.get(c, 0)
-                    for k in range(8):
-                        soa[i, k, 0] = (v >> (32 * k)) & 0xFFFFFFFF
-                assign.upload(soa)
-                out = native.eval_values(dev, ct, 0, assign, 0, 1)
-            finally:
-                assign.close()
-        finally:
-            ct.close()
-        v = sum(int(out[k, 0]) << (32 * k) for k in range(8))
+        v = self.sieve.eval_terms(b, [root], columns, self.values)[0]
         if width == BOOL:
             return bool(v)
         return BitVecValue(v, width)

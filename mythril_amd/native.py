@@ -253,18 +253,24 @@ def comm_unique_id() -> bytes:
 
 CODEGEN_SOURCES = ("jit.cpp", "jit.h", "compile.cpp", "compile.h", "exec.h", "u256_ops.h",
                    "dev_isa.h", "jit_comgr.cpp", "capi.cpp")
+# the interpreter's and the generator's code: the asm core (generated by gen_asm_core.py), the
+# kernel templates around it, the compiler that emits its instruction words
+INTERP_SOURCES = ("gen_asm_core.py", "asm_core.inc", "sieve_kernels.hip", "generate.hip",
+                  "kernels.h", "compile.cpp", "compile.h", "exec.h", "u256_ops.h", "dev_isa.h",
+                  "capi.cpp")
 
 
-def codegen_id() -> str:
-    """Identifier of the code the library generates: a hash of the sources that decide the
-    emitted machine code (the library is built from them in-tree).  Profiles that price this
-    code (profiles/pmc_summary.json, profiles/alg_work.json) record it, and bench.py uses a
-    profile only for the build it was taken on."""
+def codegen_id(engine: str = "jit") -> str:
+    """Identifier of the code one engine runs: a hash of the sources that decide it ("jit": the
+    emitted native code; "interp": the interpreter kernels and the generator).  Profiles that
+    price this code (profiles/pmc_summary.json, profiles/alg_work.json) record it, and bench.py
+    uses a profile only for the build and engine it was taken on."""
     import hashlib
 
+    srcs = {"jit": CODEGEN_SOURCES, "interp": INTERP_SOURCES}[engine]
     h = hashlib.sha256()
     d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
-    for f in CODEGEN_SOURCES:
+    for f in srcs:
         with open(os.path.join(d, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()[:16]

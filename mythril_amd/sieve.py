@@ -112,6 +112,82 @@ def local_tapeset(b: TapeBuilder, roots: Sequence[int], columns: Sequence[str]) 
     return ts
 
 
+def substitute(b: TapeBuilder, root: int, env: Dict[int, int]) -> int:
+    """`root` with every VAR whose index is in `env` replaced by env's term (a rebuild of the
+    nodes above the replaced ones; hash-consing shares everything else)."""
+    nodes, out = b.nodes, {}
+    st = [root]
+    from .tape import ARITY
+
+    while st:
+        n = st[-1]
+        if n in out:
+            st.pop()
+            continue
+        op, w, a, bb, c, i0, i1 = nodes[n]
+        if op == Op.VAR:
+            out[n] = env.get(i0, n)
+            st.pop()
+            continue
+        k = ARITY[Op(op)]
+        kids = (a, bb, c)[:k]
+        todo = [x for x in kids if x not in out]
+        if todo:
+            st += todo
+            continue
+        st.pop()
+        new = tuple(out[x] for x in kids)
+        out[n] = n if new == kids else b.op(Op(op), *new, imm0=i0, imm1=i1)
+    return out[root]
+
+
+def eliminate_definitions(b: TapeBuilder, conj: Sequence[int], schema: Schema
+                          ) -> Tuple[List[int], List[Tuple[str, int]]]:
+    """Solve-for-a-symbol on the lowered conjuncts: a conjunct ``v == t`` whose one side is a
+    scalar symbol ``v`` and whose other side is a computed term ``t`` over other columns (not a
+    constant, not a symbol: the guide already proposes those) defines ``v``.  The definition is
+    dropped and ``v`` replaced by ``t`` in every other conjunct; the query is equisatisfiable, and
+    a row satisfying the rest extends to a model with ``v = t(row)``.  This is what a query like
+    ``b == keccak(2 * keccak(a))`` (tests/laser/keccak_tests.py:122-138) needs: no candidate row
+    guesses a 256-bit hash, but every row of ``a`` determines ``b``.
+
+    Returns (remaining conjuncts over the other columns, [(column, defining term)]) with every
+    defining term over undefined columns only."""
+    kinds = schema.columns
+    var_col = {b.var_index[n]: n for n, c in kinds.items() if c.kind == "var"}
+    nodes = b.nodes
+    env: Dict[int, int] = {}
+    defs: List[Tuple[str, int]] = []
+    rest: List[int] = []
+    for cn in conj:
+        op, _, a, bb, _, _, _ = nodes[cn]
+        done = False
+        if op == Op.EQ:
+            for vn, t in ((a, bb), (bb, a)):
+                nv = nodes[vn]
+                if nv[0] != Op.VAR or nv[5] not in var_col or nv[5] in env:
+                    continue
+                if nodes[t][0] in (Op.VAR, Op.CONST):
+                    continue
+                t2 = substitute(b, t, env) if env else t
+                reads = node_columns(b, [t2])[t2]
+                if not reads or nv[5] in reads:
+                    continue
+                one = {nv[5]: t2}
+                for v in list(env):  # earlier definitions may read v: keep them closed
+                    env[v] = substitute(b, env[v], one)
+                env[nv[5]] = t2
+                defs.append((var_col[nv[5]], nv[5]))
+                done = True
+                break
+        if not done:
+            rest.append(cn)
+    if not env:
+        return list(conj), []
+    return ([substitute(b, cn, env) for cn in rest],
+            [(col, env[idx]) for col, idx in defs])
+
+
 # ops whose recomputation is cheap enough to duplicate instead of keeping a value live
 _HEAVY = {Op.BVMUL, Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD, Op.KECCAK,
           Op.EVM_EXP, Op.BVMUL_NOOVFL_U, Op.EVM_ADDMOD, Op.EVM_MULMOD}
@@ -231,11 +307,8 @@ class Sieve:
                 self.stats.extra[k] = self.stats.extra.get(k, 0) + 1
 
     @staticmethod
-    def buckets(b: TapeBuilder, root: int) -> List[Tuple[List[int], set]]:
-        """Variable-disjoint groups of the conjuncts of `root` (the DependenceMap of
-        laser/smt/solver/independence_solver.py:38-83, over lowered columns): [(conjunct nodes,
-        column var indices)].  Groups share no column, so each can take its witness from a
-        different candidate row."""
+    def conjuncts(b: TapeBuilder, root: int) -> List[int]:
+        """The leaves of `root`'s AND tree, left to right."""
         conj, stack = [], [root]
         while stack:
             n = stack.pop()
@@ -243,6 +316,52 @@ class Sieve:
                 stack += [b.nodes[n][3], b.nodes[n][2]]
             else:
                 conj.append(n)
+        return conj
+
+    def solve_definitions(self, b: TapeBuilder, root: int, schema: Schema
+                          ) -> Tuple[int, List[Tuple[str, int]]]:
+        """`root` with its definitions eliminated (eliminate_definitions), and the definitions."""
+        conj = self.conjuncts(b, root)
+        rest, defs = eliminate_definitions(b, conj, schema)
+        if not defs:
+            return root, []
+        self.stats.extra["definitions"] = self.stats.extra.get("definitions", 0) + len(defs)
+        if not rest:
+            return b.true(), defs
+        acc = rest[0]
+        for x in rest[1:]:
+            acc = b.op(Op.AND, acc, x)
+        return acc, defs
+
+    def eval_terms(self, b: TapeBuilder, terms: Sequence[int], columns: Sequence[str],
+                   values: Dict[str, int]) -> List[int]:
+        """The values of `terms` (bit-vector or Bool nodes over `columns`) under one assignment,
+        evaluated on the device (mh_eval_values over a one-row buffer)."""
+        ts = local_tapeset(b, terms, columns)
+        ct = self.compile(ts)
+        try:
+            assign = self.ctx.assignments(len(columns), 1)
+            try:
+                soa = np.zeros((len(columns), 8, 1), dtype=np.uint32)
+                for i, c in enumerate(columns):
+                    v = values.get(c, 0)
+                    for k in range(8):
+                        soa[i, k, 0] = (v >> (32 * k)) & 0xFFFFFFFF
+                assign.upload(soa)
+                return [_limbs(native.eval_values(self.ctx, ct, i, assign, 0, 1)[:, 0])
+                        for i in range(len(terms))]
+            finally:
+                assign.close()
+        finally:
+            ct.close()
+
+    @classmethod
+    def buckets(cls, b: TapeBuilder, root: int) -> List[Tuple[List[int], set]]:
+        """Variable-disjoint groups of the conjuncts of `root` (the DependenceMap of
+        laser/smt/solver/independence_solver.py:38-83, over lowered columns): [(conjunct nodes,
+        column var indices)].  Groups share no column, so each can take its witness from a
+        different candidate row."""
+        conj = cls.conjuncts(b, root)
         # column sets per node, memoised on the builder: nodes are immutable and hash-consed, so
         # a query that extends its parent (svm.py:257-262) only visits its new nodes
         cols = node_columns(b, conj)
@@ -289,6 +408,7 @@ class Sieve:
             from .lower import Column
 
             schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
+        root, defs = self.solve_definitions(b, root, schema)
         groups = self.buckets(b, root)
         names = {b.var_index[c]: c for c in columns}
         group_cols, accs = [], []
@@ -364,6 +484,12 @@ class Sieve:
                 if all(solved):
                     for c in columns:  # columns no conjunct reads: any value is a model
                         values.setdefault(c, 0)
+                    if defs:  # defined symbols take their terms' values under the row
+                        td = time.perf_counter()
+                        got = self.eval_terms(b, [t for _, t in defs], columns, values)
+                        for (c, _), v in zip(defs, got):
+                            values[c] = v
+                        st.add("definitions", time.perf_counter() - td)
                     w = Witness(schema, values, first_index, rnd + 1)
                     if key:
                         self.remember(key, w)

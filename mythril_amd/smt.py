@@ -85,6 +85,21 @@ class Expression:
     def size(self) -> int:
         return self.ctx.b.width(self.node)
 
+    @property
+    def raw(self) -> "Expression":
+        """expression.py:17-25 exposes the z3 term as ``.raw``; this package's term is itself
+        (so ``model.eval(x.raw)`` and ``model[x.raw.decl()]`` read as in the reference)."""
+        return self
+
+    def decl(self) -> str:
+        """z3 ``ExprRef.decl()`` of a symbol: its name, the key ``Model.__getitem__`` and
+        ``Model.decls()`` use."""
+        b = self.ctx.b
+        if b.nodes[self.node][0] != Op.VAR:
+            raise TapeError("decl() of a term that is not a symbol")
+        idx = b.nodes[self.node][5]
+        return next(n for n, i in b.var_index.items() if i == idx)
+
     def __hash__(self) -> int:
         return hash((id(self.ctx), self.node))
 

@@ -100,6 +100,32 @@ def test_sieve_failure_falls_back():
     assert SolverStatistics().sieve_errors == before + 1
 
 
+def test_remembered_sieve_failure_raises_fresh_exceptions():
+    """After a failed construction every query gets a NEW exception carrying the message (a
+    re-raised saved exception would chain each query's frames, and their constraints, onto one
+    traceback for the rest of the run)."""
+    frontend.configure(fallback=lambda *a: "z3", device=12345)
+    _x()
+    with pytest.raises(Exception):
+        frontend.sieve()
+    seen = []
+    for _ in range(3):
+        with pytest.raises(frontend.SieveUnavailable) as ei:
+            frontend.sieve()
+        seen.append(ei.value)
+    assert len({id(e) for e in seen}) == 3
+    assert all(len(list(_tb(e))) < 4 for e in seen)
+    x = smt.symbol_factory.BitVecSym("y", 256)
+    assert frontend.get_model((x == 2,)) == "z3"
+
+
+def _tb(e):
+    tb = e.__traceback__
+    while tb is not None:
+        yield tb
+        tb = tb.tb_next
+
+
 class FakeLaser:
     """The hook registry of LaserEVM (svm.py:578-643)."""
 

@@ -549,3 +549,45 @@ def test_wide_columns_full_occupancy(gpu_ctx):
         got = native.limbs_to_ints(native.eval_values(gpu_ctx, ct2, i, a2))
         for r in range(soa.shape[2]):
             assert got[r] == int(smt_eval.evaluate(t.nodes, ts2.pool.values, soa_row(soa, r))), (i, r)
+
+
+def test_capacity_above_2_30_rows(gpu_ctx):
+    """A buffer of 2^30 + 64 rows per column (one column, 32 GiB): an asm-only tape runs over its
+    last rows (64-bit column indexing) and matches the oracle; a complex-op tape (its core loads
+    columns with a 32-bit limb-plane stride, run_lv) is refused with MH_E_UNSUPPORTED and a
+    message, before anything is launched (the refusal is scoped to those variants)."""
+    cap = (1 << 30) + 64
+    ts = TapeSet(["x"])
+    b = ts.builder()
+    x = b.var("x", 256)
+    ts.add(b.finish(b.op(Op.BVULT, b.op(Op.BVADD, x, b.const(3, 256)), b.const(1 << 255, 256))))
+    ct = gpu_ctx.compile(ts)
+    cx = TapeSet(["x"])
+    bx = cx.builder()
+    xx = bx.var("x", 256)
+    cx.add(bx.finish(bx.op(Op.BVMUL_NOOVFL_U, xx, bx.const(3, 256))))
+    ctc = gpu_ctx.compile(cx)
+    a = gpu_ctx.assignments(1, cap)
+    try:
+        rows = 256
+        first = cap - rows
+        rng = random.Random(30)
+        vals = [rng.getrandbits(256) for _ in range(rows)]
+        soa = np.zeros((1, 8, rows), dtype=np.uint32)
+        for r, v in enumerate(vals):
+            for k in range(8):
+                soa[0, k, r] = (v >> (32 * k)) & 0xFFFFFFFF
+        a.upload(soa, first=first)
+        fh, hc = native.run(gpu_ctx, ct, a, row_first=first, row_count=rows, index_base=0)
+        want = [r for r, v in enumerate(vals)
+                if smt_eval.evaluate(ts.tapes[0].nodes, ts.pool.values, [v])]
+        assert int(hc[0]) == len(want)
+        assert int(fh[0]) == (first + want[0] if want else native.NO_HIT)
+        with pytest.raises(native.Unsupported, match="2\\^30 rows"):
+            native.run(gpu_ctx, ctc, a, row_first=first, row_count=rows)
+        with pytest.raises(native.Unsupported, match="2\\^30 rows"):
+            native.eval_values(gpu_ctx, ctc, 0, a, first, rows)
+    finally:
+        a.close()
+        ct.close()
+        ctc.close()

@@ -34,17 +34,17 @@ def model_of(schema, row):
     for f, km in schema.keccak.items():
         inv = {}
 
-        def fwd(x, km=km, inv=inv, width=None):
+        # the argument width is bound per function (a late-bound closure variable would give
+        # every keccak function the last one's width)
+        def fwd(x, km=km, inv=inv, nbytes=int(f.split("_")[1]) // 8):
             if x in km.pairs:
                 y = km.pairs[x]
             else:
-                nbytes = fwd.width // 8
                 h = int.from_bytes(keccak256(x.to_bytes(nbytes, "big")), "big")
                 y = (km.base + ((h >> KECCAK_SHIFT) << KECCAK_ALIGN)) % (1 << 256)
             inv[y] = x
             return y
 
-        fwd.width = int(f.split("_")[1])
         funcs[f] = fwd
         funcs[f + "-1"] = (lambda y, inv=inv: inv.get(y, 0))
     for f, cells in schema.uf_cells.items():
