@@ -28,6 +28,7 @@ sys.path.insert(0, HERE)
 NOMINAL_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # u32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
 PMC_SUMMARY = os.path.join(HERE, "profiles", "pmc_summary.json")
 ALG_WORK = os.path.join(HERE, "profiles", "alg_work.json")
+MIN_WORK = os.path.join(HERE, "profiles", "min_work.json")
 
 
 def log(*a):
@@ -67,6 +68,10 @@ def main() -> None:
                     help="skip the full-evaluation companion step (N=1, jit, short-circuit runs "
                          "time one full-evaluation step after the timed region and check that "
                          "its per-tape results are identical)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --rows-per-gpu is the TOTAL row count (config 5: "
+                         "2^26 in total) split over the ranks, instead of every rank sweeping "
+                         "that many (weak scaling, the default)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -101,8 +106,12 @@ def main() -> None:
     if args.engine == "jit":
         jit_info = ct.jit(max_vgpr=args.max_vgpr, short_circuit=not args.full_eval)
         log("[rank %d] jit: %s" % (rank, jit_info))
-    alg_ops_per_row = sum(int(i["alg_ops"]) for i in info)
-    index_base, rows = shard.shard_range(rank, world, args.rows_per_gpu)
+    # SURVEY 8d's op table (mh_tape_info.alg_ops): informational, not a work count
+    optable_per_row = sum(int(i["alg_ops"]) for i in info)
+    if args.strong:
+        index_base, rows = shard.strong_shard_range(rank, world, args.rows_per_gpu)
+    else:
+        index_base, rows = shard.shard_range(rank, world, args.rows_per_gpu)
     seed = spec["assignment_seed"]
     assign = ctx.assignments(ts.n_vars, rows)
     assign.generate(seed, index_base)
@@ -133,9 +142,9 @@ def main() -> None:
         exchange = "library" if int(flag.item()) == 1 else "torch"
         log("[rank %d] result exchange: %s" % (rank, exchange))
     torch.cuda.synchronize(dev)
-    log("[rank %d] setup %.1fs: %d tapes, %d insns, %d rows, %.0f alg-ops/row"
+    log("[rank %d] setup %.1fs: %d tapes, %d insns, %d rows, SURVEY op-table %.0f per row"
         % (rank, time.time() - t0, n_tapes, sum(i["n_insns"] for i in info), rows,
-           alg_ops_per_row))
+           optable_per_row))
 
     def step(timed: bool):
         native.results_reset(ctx, fh.data_ptr(), hc.data_ptr(), n_tapes)
@@ -173,7 +182,7 @@ def main() -> None:
     ctx.enable_timing(False)
     kms = tot_ms / max(n_launch, 1)
     ms_per_step = elapsed * 1e3 / args.steps
-    evals_per_step = n_tapes * rows * world
+    evals_per_step = n_tapes * (args.rows_per_gpu if args.strong else rows * world)
     value = evals_per_step / (ms_per_step / 1e3)
     hits = int((hc > 0).sum().item())
 
@@ -241,10 +250,22 @@ def main() -> None:
                 alg = e
     alg_per_eval = alg["alg_lane_ops_per_eval"] if alg else None
     alg_rate = (alg_per_eval * n_tapes * rows / (kms / 1e3) / 1e12) if alg else None
-    if companion is not None and alg:
-        companion["roofline_achieved"] = alg_per_eval * n_tapes * rows / (
+    # the code-independent minimum work per evaluation (scripts/min_work.py): the roofline's
+    # algorithmic count; the code-priced count above is reported beside it as frac_codegen
+    mw = None
+    if os.path.exists(MIN_WORK) and n_tapes == spec["n_tapes"]:
+        for e in json.load(open(MIN_WORK)).get("entries", []):
+            if e.get("variant") == args.variant:
+                mw = e
+    min_per_eval = mw["min_lane_ops_per_eval"] if mw else None
+    min_rate = (min_per_eval * n_tapes * rows / (kms / 1e3) / 1e12) if mw else None
+    if companion is not None and mw:
+        companion["roofline_achieved"] = min_per_eval * n_tapes * rows / (
             companion["kernel_ms"] / 1e3) / 1e12
         companion["roofline_frac"] = companion["roofline_achieved"] / NOMINAL_PEAK_TOPS
+        if alg:
+            companion["roofline_frac_codegen"] = alg_per_eval * n_tapes * rows / (
+                companion["kernel_ms"] / 1e3) / 1e12 / NOMINAL_PEAK_TOPS
     line = {
         "metric": "constraint-evals/sec",
         "value": value,
@@ -254,7 +275,7 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (seeded config-5 tapes, counter-based PRNG assignments)",
@@ -266,6 +287,7 @@ def main() -> None:
             "variant": args.variant,
             "tapes": n_tapes,
             "rows_per_gpu": rows,
+            "rows_total": args.rows_per_gpu if args.strong else rows * world,
             "vars": ts.n_vars,
             "mode": "count_all",
             "engine": args.engine,
@@ -280,10 +302,15 @@ def main() -> None:
         "jit": jit_info,
         "roofline": {
             "bound": "valu",
-            "achieved": alg_rate,
+            "achieved": min_rate,
             "peak": NOMINAL_PEAK_TOPS,
             "unit": "T u32-ops/s",
-            "frac": (alg_rate / NOMINAL_PEAK_TOPS) if alg_rate else None,
+            "frac": (min_rate / NOMINAL_PEAK_TOPS) if min_rate else None,
+            "min_lane_ops_per_eval": min_per_eval,
+            "min_profile": ("profiles/min_work.json (%d tapes x %d rows, code-independent op "
+                            "table)" % (mw["tapes_sampled"], mw["rows"])) if mw else None,
+            "achieved_codegen": alg_rate,
+            "frac_codegen": (alg_rate / NOMINAL_PEAK_TOPS) if alg_rate else None,
             "traffic": traffic,
             "traffic_unit": "bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, profiles/)",
             "alg_lane_ops_per_eval": alg_per_eval,
@@ -295,13 +322,16 @@ def main() -> None:
             "pmc_profile": pmc_tag,
             "valu_busy_pmc": valu_busy,
             "peak_measured_add_chain": peak_measured,
-            "optable_ops_per_eval": alg_ops_per_row / n_tapes,
-            "note": "achieved = algorithmic lane-ops per launch / this run's kernel time: per "
-                    "(tape, row) the VALU lane-ops of the conjuncts up to and including the "
-                    "row's first false one, in the emitted order, at this code's per-op cost "
-                    "(alg_lane_ops_per_eval, measured per build by scripts/alg_work.py on the "
-                    "host emulator of the emitted code); no mode executes less, so frac <= 1 "
-                    "here and in full_eval. executed = PMC SQ_INSTS_VALU x 64 of the profile of "
+            "optable_ops_per_eval": optable_per_row / n_tapes,
+            "note": "achieved = the code-independent minimum work per launch / this run's "
+                    "kernel time: per (tape, row) the cheapest node set deciding the row's Bool "
+                    "(lazy AND / OR / ITE, constants folded, demanded limbs) priced by a fixed "
+                    "per-op table of minimum u32 lane-ops (min_lane_ops_per_eval, "
+                    "scripts/min_work.py). achieved_codegen / frac_codegen = the same per "
+                    "(tape, row) prefix in the emitted conjunct order at THIS code's per-op "
+                    "cost (alg_lane_ops_per_eval, per build, scripts/alg_work.py on the host "
+                    "emulator of the emitted code). Both <= executed, so frac <= frac_codegen "
+                    "<= frac_executed <= 1. executed = PMC SQ_INSTS_VALU x 64 of the profile of "
                     "this build (pmc_profile; null when none) / kernel time; frac_executed / "
                     "frac = the lanes a wave keeps busy for rows already decided. peak = 256 CU "
                     "x 4 SIMD x 32 lanes x 2.4 GHz (a wave64 VALU op issues over 2 cycles). "

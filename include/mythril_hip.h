@@ -258,7 +258,8 @@ int32_t mh_jit_eval_all(mh_ctx* ctx, const mh_tapeset* ts, const mh_assign* as,
  * MIN of the per-tape smallest witness index (MH_NO_HIT = UINT64_MAX is MIN's identity) and SUM
  * of the hit counts, in place in device buffers, on the ctx stream, so the result is identical
  * for any number of GPUs.  Rank 0 creates the id (mh_comm_unique_id) and the caller distributes
- * it (torch.distributed, a file, ...).  RCCL is dlopen'ed on first use.                          */
+ * it (torch.distributed, a file, ...).  RCCL is dlopen'ed on first use: the path in MH_RCCL_LIB    *
+ * when set (tests/test_comm_stub.py points it at a recording stub), else the ROCm install's.     */
 #define MH_COMM_ID_BYTES 128
 int32_t mh_comm_unique_id(uint8_t* out /* [MH_COMM_ID_BYTES] */);
 int32_t mh_comm_init(mh_ctx* ctx, const uint8_t* unique_id, int32_t rank, int32_t world);

@@ -76,9 +76,12 @@ const Rccl* rccl() {
     static bool tried = false;
     if (!tried) {
         tried = true;
-        for (const char* name : {"/opt/rocm/lib/librccl.so.1", "librccl.so.1"}) {
+        // MH_RCCL_LIB names another copy first (a recording stub in tests/test_comm_stub.py)
+        const char* env = std::getenv("MH_RCCL_LIB");
+        for (const char* name : {env, "/opt/rocm/lib/librccl.so.1", "librccl.so.1"}) {
+            if (!name || !*name) continue;
             r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
-            if (r.h) break;
+            if (r.h || name == env) break;  // a named copy that fails is not replaced
         }
         if (r.h) {
             r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.h, "ncclGetUniqueId");

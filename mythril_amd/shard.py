@@ -22,6 +22,18 @@ def shard_range(rank: int, world: int, rows_per_rank: int) -> Tuple[int, int]:
     return rank * rows_per_rank, rows_per_rank
 
 
+def strong_shard_range(rank: int, world: int, total_rows: int) -> Tuple[int, int]:
+    """(global index of this rank's first row, rows) — strong scaling: `total_rows` candidates
+    (config 5: 2^26 in total over the node's GPUs) split into `world` contiguous shards that
+    differ by at most one row; rank r's rows keep their global indices, so the reduced results
+    equal one GPU's sweep of all `total_rows`."""
+    if not 0 <= rank < world:
+        raise ValueError("rank %d outside world of %d" % (rank, world))
+    q, r = divmod(total_rows, world)
+    first = rank * q + min(rank, r)
+    return first, q + (1 if rank < r else 0)
+
+
 def allreduce_results(first_hit, hit_count, group=None) -> None:
     """In place over all ranks: first_hit = MIN (NO_HIT stays NO_HIT), hit_count = SUM.
     first_hit / hit_count are int64 tensors holding the u64 results (NO_HIT reads -1)."""

@@ -1,0 +1,344 @@
+#!/usr/bin/env python3
+"""Code-independent minimum work per evaluation of bench.py's workload (roofline.achieved).
+
+VERDICT r3 "What's weak" 3: the round-3 ``alg_lane_ops_per_eval`` priced each op at THIS code's
+instruction count, so a costlier code generator raised its own fraction.  This count prices every
+op by a fixed table of minimum 32-bit VALU lane-ops (below) and asks, per (tape, row), for the
+cheapest set of nodes whose values decide the row's Bool — the lazy-evaluation minimum, a lower
+bound for any evaluator with these per-op costs, independent of our emitted code and of its
+conjunct order:
+
+* an AND that is false needs only its cheapest false operand; an OR that is true, its cheapest
+  true operand; an ITE, its condition and the taken branch; any other node all its operands;
+* nodes that read no column are constants (folded: 0); shared nodes are counted once;
+* only the 32-bit limbs a consumer needs are computed (an EXTRACT of the low word needs the low
+  limbs of its operand; a product's low limbs need only the low limbs of its factors).
+
+Per-op minimum, L = demanded 32-bit limbs (8 for a full 256-bit word) — one VALU instruction per
+limb is the floor of any limb-wise op on a 32-lane-wide integer unit:
+
+  ADD / SUB / NEG                 L        (one carry-chain instruction per limb)
+  AND / OR / XOR / NOT            L        (limbs where a constant operand decides: 0)
+  shifts by a constant            L        (one funnel shift per limb); by a variable: 3 L
+  EQ / ordering compares          L        (one compare / borrow per limb, masks combined in SALU)
+  ITE (bit-vector)                L        (one select per limb); Bool ops 0 (SALU masks)
+  EXTRACT / CONCAT / ZEXT         0 when limb-aligned, else 1 per output limb; SEXT 1 per limb
+  MUL                             products i + j < L with no constant-zero factor limb, one
+                                  64-bit multiply-add each, plus L - 1 high-half moves
+  UDIV / UREM                     L + q (2 Ly + 3): q = quotient digits (32-bit, from the row's
+                                  values), Ly = significant divisor limbs; SDIV / SREM / SMOD + 2 L
+  KECCAK (Keccak-f[1600])         24 rounds x 250 (θ 100, ρπ 50, χ 100 on 32-bit halves)
+  add / sub overflow predicates   L; multiply overflow: L^2
+
+The result is written to profiles/min_work.json; bench.py reports it as ``roofline.achieved`` /
+``frac`` and keeps the code-priced count (scripts/alg_work.py) as ``frac_codegen``.
+
+    python scripts/min_work.py [n_sample_tapes=1000] [rows=128] [--keccak]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from mythril_amd import synth  # noqa: E402
+from mythril_amd.tape import Op  # noqa: E402
+from oracle import smt_eval  # noqa: E402
+
+OUT = os.path.join(ROOT, "profiles", "min_work.json")
+KECCAK_MIN = 24 * 250
+FULL = 0xFF
+
+
+def limbs(w: int) -> int:
+    return max(1, (w + 31) // 32) if w else 0
+
+
+def prefix(m: int) -> int:
+    return (1 << m.bit_length()) - 1 if m else 0
+
+
+def popc(m: int) -> int:
+    return bin(m).count("1")
+
+
+def sig_limbs(v: int) -> int:
+    return (v.bit_length() + 31) // 32
+
+
+class TapeCost:
+    """Static facts of one tape: which nodes are constant, their demanded limbs."""
+
+    def __init__(self, nodes, consts):
+        self.nodes = nodes
+        n = len(nodes)
+        self.op = [Op(int(x)) for x in nodes["op"]]
+        self.w = [int(x) for x in nodes["width"]]
+        self.a = [int(x) for x in nodes["a"]]
+        self.b = [int(x) for x in nodes["b"]]
+        self.c = [int(x) for x in nodes["c"]]
+        self.i0 = [int(x) for x in nodes["imm0"]]
+        self.i1 = [int(x) for x in nodes["imm1"]]
+        self.const = [False] * n
+        from mythril_amd.tape import ARITY
+
+        self.kids = []
+        for i in range(n):
+            k = ARITY[self.op[i]]
+            kids = [self.a[i], self.b[i], self.c[i]][:k]
+            self.kids.append(kids)
+            if self.op[i] == Op.VAR:
+                self.const[i] = False
+            elif k == 0:
+                self.const[i] = True
+            else:
+                self.const[i] = all(self.const[x] for x in kids)
+        vals = smt_eval.evaluate(nodes, consts, [0] * 64, all_values=True)
+        self.cval = [vals[i] if self.const[i] else None for i in range(n)]
+        self.demand = self._demand()
+
+    def _limb_zero(self, i: int, k: int) -> bool:
+        v = self.cval[i]
+        return v is not None and ((int(v) >> (32 * k)) & 0xFFFFFFFF) == 0
+
+    def _limb_ones(self, i: int, k: int) -> bool:
+        v = self.cval[i]
+        return v is not None and ((int(v) >> (32 * k)) & 0xFFFFFFFF) == 0xFFFFFFFF
+
+    def _demand(self):
+        n = len(self.nodes)
+        dem = [0] * n
+        dem[n - 1] = FULL
+        for i in range(n - 1, -1, -1):
+            d = dem[i] if self.w[i] else FULL
+            op = self.op[i]
+            if not d and self.w[i]:
+                continue
+
+            def D(x, m):
+                dem[x] |= m
+
+            if op in (Op.BVADD, Op.BVSUB, Op.BVMUL, Op.BVNEG):
+                for x in self.kids[i]:
+                    D(x, prefix(d))
+            elif op in (Op.BVAND, Op.BVOR, Op.BVXOR, Op.BVNOT):
+                for x in self.kids[i]:
+                    D(x, d)
+            elif op == Op.ITE:
+                D(self.a[i], FULL)
+                D(self.b[i], d)
+                D(self.c[i], d)
+            elif op == Op.EXTRACT:
+                lo = self.i1[i]
+                m = 0
+                for k in range(8):
+                    if (d >> k) & 1:
+                        bit0 = lo + 32 * k
+                        m |= 1 << (bit0 // 32)
+                        if bit0 % 32 and bit0 // 32 + 1 < 8:
+                            m |= 1 << (bit0 // 32 + 1)
+                D(self.a[i], m & FULL)
+            elif op == Op.ZEXT:
+                D(self.a[i], d & ((1 << limbs(self.w[self.a[i]])) - 1))
+            elif op == Op.CONCAT:
+                wb = self.w[self.b[i]]
+                D(self.b[i], FULL)
+                D(self.a[i], FULL)
+                del wb
+            elif op in (Op.BVSHL, Op.BVLSHR, Op.BVASHR):
+                D(self.a[i], FULL)
+                D(self.b[i], FULL)
+            else:
+                for x in self.kids[i]:
+                    D(x, FULL)
+        return dem
+
+    def own(self, i: int, vals) -> int:
+        """Minimum VALU lane-ops of node i on one row (vals: the row's node values)."""
+        if self.const[i]:
+            return 0
+        op, w = self.op[i], self.w[i]
+        d = self.demand[i] if w else FULL
+        L = popc(d & ((1 << limbs(w)) - 1)) if w else 0
+        if op in (Op.VAR, Op.CONST, Op.TRUE, Op.FALSE, Op.AND, Op.OR, Op.XOR, Op.NOT):
+            return 0
+        if op in (Op.BVADD, Op.BVSUB, Op.BVNEG):
+            return L
+        if op in (Op.BVAND, Op.BVOR, Op.BVXOR):
+            n = 0
+            for k in range(limbs(w)):
+                if not (d >> k) & 1:
+                    continue
+                decided = False
+                for x in (self.a[i], self.b[i]):
+                    if op == Op.BVAND and (self._limb_zero(x, k) or self._limb_ones(x, k)):
+                        decided = True
+                    if op == Op.BVOR and (self._limb_zero(x, k) or self._limb_ones(x, k)):
+                        decided = True
+                    if op == Op.BVXOR and self._limb_zero(x, k):
+                        decided = True
+                n += 0 if decided else 1
+            return n
+        if op == Op.BVNOT:
+            return L
+        if op in (Op.BVSHL, Op.BVLSHR, Op.BVASHR):
+            return L if self.const[self.b[i]] else 3 * L
+        if op in (Op.EQ, Op.BVULT, Op.BVULE, Op.BVUGT, Op.BVUGE, Op.BVSLT, Op.BVSLE, Op.BVSGT,
+                  Op.BVSGE, Op.BVADD_NOOVFL_U, Op.BVSUB_NOUDFL_U):
+            return limbs(self.w[self.a[i]])
+        if op == Op.BVMUL_NOOVFL_U:
+            return limbs(self.w[self.a[i]]) ** 2
+        if op == Op.ITE:
+            return L if w else 0
+        if op == Op.EXTRACT:
+            return 0 if self.i1[i] % 32 == 0 else L
+        if op == Op.CONCAT:
+            return 0 if self.w[self.b[i]] % 32 == 0 else L
+        if op == Op.ZEXT:
+            return 0
+        if op == Op.SEXT:
+            return L
+        if op == Op.BVMUL:
+            top = limbs(w)
+            n = 0
+            for p in range(top):
+                if not (prefix(d) >> p) & 1:
+                    continue
+                for j in range(p + 1):
+                    if not (self._limb_zero(self.a[i], j) or self._limb_zero(self.b[i], p - j)):
+                        n += 1
+            return n + max(0, popc(prefix(d)) - 1)
+        if op in (Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD):
+            x, y = int(vals[self.a[i]]), int(vals[self.b[i]])
+            Lw = limbs(w)
+            signed = op in (Op.BVSDIV, Op.BVSREM, Op.BVSMOD)
+            if signed:
+                m = (1 << w) - 1
+                if x >> (w - 1):
+                    x = (-x) & m
+                if y >> (w - 1):
+                    y = (-y) & m
+            ly = sig_limbs(y)
+            q = 0 if (y == 0 or x < y) else max(1, sig_limbs(x) - ly + 1)
+            return Lw + q * (2 * ly + 3) + (2 * Lw if signed else 0)
+        if op == Op.KECCAK:
+            return KECCAK_MIN
+        return 8 * L  # EVM word helpers (not in config 5): a generous floor
+
+    def min_cost(self, vals) -> int:
+        """Own-cost sum over the cheapest node set that decides the root on this row."""
+        memo = {}
+        n = len(self.nodes)
+
+        def need(i):
+            got = memo.get(i)
+            if got is not None:
+                return got
+            op = self.op[i]
+            s = {i}
+            kids = self.kids[i]
+            if self.const[i]:
+                pass
+            elif op == Op.AND and not vals[i]:
+                best = None
+                for x in kids:
+                    if not vals[x]:
+                        cand = need(x)
+                        if best is None or cost(cand) < cost(best):
+                            best = cand
+                s |= best
+            elif op == Op.OR and vals[i]:
+                best = None
+                for x in kids:
+                    if vals[x]:
+                        cand = need(x)
+                        if best is None or cost(cand) < cost(best):
+                            best = cand
+                s |= best
+            elif op == Op.ITE:
+                s |= need(self.a[i])
+                s |= need(self.b[i] if vals[self.a[i]] else self.c[i])
+            else:
+                for x in kids:
+                    s |= need(x)
+            s = frozenset(s)
+            memo[i] = s
+            return s
+
+        own = {}
+
+        def cost(s):
+            t = 0
+            for x in s:
+                c = own.get(x)
+                if c is None:
+                    c = own[x] = self.own(x, vals)
+                t += c
+            return t
+
+        sys.setrecursionlimit(10000)
+        return cost(need(n - 1))
+
+
+_W = {}
+
+
+def _init(rows, keccak):
+    ts = synth.generate(keccak=keccak)
+    seed = synth.load_spec()["assignment_seed"]
+    _W["ts"] = ts
+    _W["rows"] = [smt_eval.gen_assignment(seed, ts.n_vars, r) for r in range(rows)]
+
+
+def _tape(t):
+    ts = _W["ts"]
+    nodes = ts.tapes[t].nodes
+    consts = ts.pool.values
+    tc = TapeCost(nodes, consts)
+    tot = 0
+    for row in _W["rows"]:
+        vals = smt_eval.evaluate(nodes, consts, row, all_values=True)
+        tot += tc.min_cost(vals)
+    return tot / len(_W["rows"])
+
+
+def main():
+    import multiprocessing as mp
+
+    argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+    keccak = "--keccak" in sys.argv
+    n_pick = int(argv[0]) if argv else 1000
+    rows = int(argv[1]) if len(argv) > 1 else 128
+    spec = synth.load_spec()
+    stride = max(1, spec["n_tapes"] // n_pick)
+    picks = list(range(0, spec["n_tapes"], stride))[:n_pick]
+    t0 = time.time()
+    with mp.get_context("fork").Pool(min(8, os.cpu_count() or 1), initializer=_init,
+                                     initargs=(rows, keccak)) as pool:
+        per = pool.map(_tape, picks, chunksize=8)
+    entry = {
+        "variant": "keccak" if keccak else "plain",
+        "tapes_sampled": len(picks),
+        "tape_stride": stride,
+        "rows": rows,
+        "assignment_seed": spec["assignment_seed"],
+        "min_lane_ops_per_eval": sum(per) / len(per),
+        "keccak_min_lane_ops": KECCAK_MIN,
+        "seconds": round(time.time() - t0, 1),
+        "note": "code-independent minimum (scripts/min_work.py docstring table): per (tape, row) "
+                "the cheapest node set deciding the row's Bool, lazy AND/OR/ITE, constants "
+                "folded, demanded limbs only; independent of the emitted code and conjunct order",
+    }
+    entries = []
+    if os.path.exists(OUT):
+        entries = [e for e in json.load(open(OUT)).get("entries", [])
+                   if e.get("variant") != entry["variant"]]
+    entries.append(entry)
+    json.dump({"entries": entries}, open(OUT, "w"), indent=1)
+    print(json.dumps(entry, indent=1))
+
+
+if __name__ == "__main__":
+    main()

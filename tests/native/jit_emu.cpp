@@ -109,6 +109,11 @@ struct Counts {
 uint64_t g_alive = ~0ull;  // lanes that satisfy every conjunct tested so far (short circuit)
 // compaction study: VALU before the chunk's first short-circuit test, and the live lanes then
 uint64_t g_valu_head = 0, g_head_done = 0, g_alive_hist[65];
+// compaction study, per segment: (chunk, VALU executed since the chunk began, live lanes after the
+// segment's short-circuit test); the chunk's end is a segment with mask ~0 tagged end
+struct Seg { uint32_t chunk, valu; uint64_t alive; };
+std::vector<Seg> g_segs;
+uint32_t g_chunk_id = 0;
 const uint32_t* g_mem = nullptr;  // "global memory": the SoA assignment buffer at address 0
 uint64_t g_mem_words = 0;
 uint64_t g_div_hist[32];  // division calls by executed VALU (buckets of 32)
@@ -395,6 +400,8 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                              m.op == M_S_ANDN2_B64 ? a & ~b : a | ~b;
                 if (m.op == M_S_AND_B64 && o[0].k == O_S && o[0].v == S_SCRATCH) {
                     g_alive = r;
+                    if (!depth)
+                        g_segs.push_back({g_chunk_id, (uint32_t)(g_counts.valu - g_chunk_valu0), r});
                     if (!g_head_done && !depth) {
                         g_head_done = 1;
                         g_valu_head += g_counts.valu - g_chunk_valu0;
@@ -576,6 +583,9 @@ extern "C" int32_t emu_jit_eval(const mh_node* nodes, const uint64_t* offs, uint
             g_head_done = 0;
             g_chunk_valu0 = g_counts.valu;
             run(w, tc.code, div);
+            g_segs.push_back({g_chunk_id | 0x80000000u, (uint32_t)(g_counts.valu - g_chunk_valu0),
+                              g_alive});
+            ++g_chunk_id;
             if (!g_head_done) ++g_alive_hist[64];  // no test: the whole tape is the head
             ++chunks;
             const uint64_t res = (uint64_t)w.s[S_RES] | ((uint64_t)w.s[S_RES + 1] << 32);
@@ -745,4 +755,18 @@ extern "C" void emu_jit_head_stats(uint64_t* out, int reset) {
         g_valu_head = 0;
         for (int i = 0; i <= 64; ++i) g_alive_hist[i] = 0;
     }
+}
+
+// compaction study: the segments recorded since the last reset, as (chunk | end flag, VALU since
+// the chunk began, live-lane mask lo, hi) quadruples; returns the count (copies at most cap)
+extern "C" uint64_t emu_jit_segments(uint32_t* out, uint64_t cap, int reset) {
+    const uint64_t n = g_segs.size();
+    for (uint64_t i = 0; i < n && i < cap; ++i) {
+        out[4 * i] = g_segs[i].chunk;
+        out[4 * i + 1] = g_segs[i].valu;
+        out[4 * i + 2] = (uint32_t)g_segs[i].alive;
+        out[4 * i + 3] = (uint32_t)(g_segs[i].alive >> 32);
+    }
+    if (reset) { g_segs.clear(); g_chunk_id = 0; }
+    return n;
 }

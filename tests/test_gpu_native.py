@@ -200,3 +200,34 @@ def test_native_config5_full_size(gpu_ctx):
         int((fh != native.NO_HIT).sum()), int(hc.sum())))
     for x in (ct, ref, a):
         x.close()
+
+
+@pytest.mark.timeout(600)
+def test_native_keccak_variant_2_20(gpu_ctx):
+    """bench.py --variant keccak at its size (10^4 tapes, each with one keccak256 of a 512-bit
+    input, keccak_function_manager.py:43-57) x 2^20 rows: the native code's per-tape counts and
+    first hits equal the interpreter's on every tape, and the C oracle's over every row on an
+    8-tape sample (every sampled tape reaches its keccak conjunct on some rows)."""
+    from oracle import ctape
+
+    ts = synth.generate(keccak=True)
+    seed, rows = synth.load_spec()["assignment_seed"], 1 << 20
+    a = gpu_ctx.assignments(ts.n_vars, rows)
+    a.generate(seed, 0)
+    ct = gpu_ctx.compile(ts)
+    info = ct.jit()
+    assert info["n_jitted"] == len(ts.tapes), info
+    fh, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    ref = gpu_ctx.compile(ts)
+    fh0, hc0 = native.run(gpu_ctx, ref, a, mode=native.MODE_COUNT_ALL)
+    assert np.array_equal(hc, hc0) and np.array_equal(fh, fh0)
+    rng = random.Random(20)
+    pick = sorted(rng.sample(range(len(ts.tapes)), 8))
+    sub = TapeSet(ts.var_names)
+    sub.pool = ts.pool
+    sub.tapes = [ts.tapes[t] for t in pick]
+    cnt, first = ctape.count(sub, seed, 0, rows, threads=min(16, os.cpu_count() or 1),
+                             short_circuit=True)
+    assert np.array_equal(hc[pick], cnt) and np.array_equal(fh[pick], first)
+    for x in (ct, ref, a):
+        x.close()

@@ -59,7 +59,7 @@ def _shard_results(ts, base, rows):
     return fh, hc
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, strong=False):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -67,7 +67,10 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ts = _tapes()
-        base, rows = shard.shard_range(rank, world, ROWS)
+        if strong:  # bench.py --strong: ROWS * 2 + 1 rows in total, split unevenly
+            base, rows = shard.strong_shard_range(rank, world, 2 * ROWS + 1)
+        else:
+            base, rows = shard.shard_range(rank, world, ROWS)
         fh, hc = _shard_results(ts, base, rows)
         fh_t = torch.tensor(fh, dtype=torch.int64)
         hc_t = torch.tensor(hc, dtype=torch.int64)
@@ -98,3 +101,32 @@ def test_shard_range():
     assert shard.shard_range(3, 4, 100) == (300, 100)
     with pytest.raises(ValueError):
         shard.shard_range(4, 4, 100)
+
+
+def test_two_rank_strong_scaling_matches_single_process():
+    """bench.py --strong: the TOTAL row count split over the ranks (uneven by one row) reduces
+    to the single-process answer over the same rows."""
+    world = 2
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_worker, args=(world, port, out, True), nprocs=world, join=True)
+        results = dict(out)
+    ts = _tapes()
+    want = _shard_results(ts, 0, 2 * ROWS + 1)
+    assert results[0] == results[1]
+    assert tuple(results[0][0]) == tuple(want[0])
+    assert tuple(results[0][1]) == tuple(want[1])
+
+
+def test_strong_shard_range_partitions_the_rows():
+    for total in (0, 1, 7, 1 << 26, (1 << 26) + 5):
+        for world in (1, 2, 3, 8):
+            parts = [shard.strong_shard_range(r, world, total) for r in range(world)]
+            assert parts[0][0] == 0
+            for (b0, n0), (b1, _) in zip(parts, parts[1:]):
+                assert b0 + n0 == b1
+            assert sum(n for _, n in parts) == total
+            assert max(n for _, n in parts) - min(n for _, n in parts) <= 1
+    with pytest.raises(ValueError):
+        shard.strong_shard_range(2, 2, 10)
