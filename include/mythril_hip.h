@@ -191,6 +191,52 @@ int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, const uint32_t*
                          uint32_t n_parent, mh_harvest** out, mh_guide* guide);
 int32_t mh_harvest_free(mh_harvest* h);
 
+/* ---- SMT-LIB import (the product path's first stage) -----------------------------------------
+ * Replaces the Python SMT-LIB reader behind mythril_amd/smtlib.Z3Importer, which imports every
+ * constraint LASER hands get_model (mythril/support/model.py:37-57; laser/smt/solver/solver.py:
+ * 28-37) from z3's Solver.sexpr() text.  A session reads SMT-LIB2 commands (declare-fun,
+ * declare-const, define-fun, assert, minimize, maximize; let, n-ary connectives, indexed
+ * operators, select / store / (as const ..), unary uninterpreted functions) and hash-conses the
+ * terms against the nodes it has already handed to the host.  mh_smtlib_read returns only the
+ * nodes the host does not have yet, in creation order (operands: a host id >= 0, or -(k + 1) for
+ * record k of the same batch), and one result per assert / minimize / maximize (the same
+ * reference form).  The host builds each record in its own term store and must answer with
+ * mh_smtlib_commit (the host id of every record) or mh_smtlib_rollback before the next read.
+ * Batch arrays stay valid until the next read.  Malformed text: MH_E_INVALID, nothing changes.    */
+typedef struct mh_smtlib mh_smtlib;
+typedef struct {
+    uint8_t op;           /* mh_op, or the host-only kinds 80..84 (ARRAY, CONST_ARRAY, STORE,
+                             SELECT, UF: imm1 = domain width, width = range width)               */
+    uint8_t pad0;
+    uint16_t pad1;
+    uint32_t width;       /* 0 = Bool                                                            */
+    int64_t a, b, c;      /* operands (only the op's arity is meaningful)                         */
+    uint32_t imm0, imm1;  /* EXTRACT hi / lo, ZEXT / SEXT bits; arrays / UFs: imm1 = domain       */
+    uint32_t name_off, name_len;  /* VAR / ARRAY / UF: symbol name in batch.names                */
+    uint32_t const_off;   /* CONST: 8 little-endian u32 limbs at batch.const_limbs[const_off]    */
+    uint32_t pad2;
+} mh_smt_record;
+enum { MH_SMT_ASSERT = 0, MH_SMT_MINIMIZE = 1, MH_SMT_MAXIMIZE = 2 };
+typedef struct {
+    uint32_t kind;        /* MH_SMT_ASSERT / MINIMIZE / MAXIMIZE                                 */
+    uint32_t pad;
+    int64_t node;         /* host id, or -(k + 1) for record k                                    */
+} mh_smt_result;
+typedef struct {
+    const mh_smt_record* records;
+    uint64_t n_records;
+    const uint32_t* const_limbs;
+    const char* names;
+    const mh_smt_result* results;
+    uint64_t n_results;
+} mh_smt_batch;
+int32_t mh_smtlib_create(mh_smtlib** out);
+int32_t mh_smtlib_destroy(mh_smtlib* s);
+int32_t mh_smtlib_read(mh_smtlib* s, const char* text, uint64_t len, mh_smt_batch* out);
+int32_t mh_smtlib_commit(mh_smtlib* s, const int64_t* host_ids, uint64_t n);
+int32_t mh_smtlib_rollback(mh_smtlib* s);
+uint64_t mh_smtlib_size(const mh_smtlib* s);  /* nodes the session mirrors                      */
+
 /* ---- evaluation ------------------------------------------------------------------------------ */
 /* Evaluate tapes [tape_first, tape_first+tape_count) over assignment rows [row_first,
  * row_first+row_count) of `as`.  Results are indexed by tape - tape_first and hold GLOBAL indices

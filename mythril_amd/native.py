@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -81,7 +81,27 @@ SIGNATURES = {
     "mh_guide_harvest": (C.c_int32, [_vp, C.c_uint32, _u32p, C.c_uint32, C.POINTER(C.c_uint16),
                                      C.c_uint32, _u32p, _u32p, C.c_uint32, C.POINTER(_vp), _vp]),
     "mh_harvest_free": (C.c_int32, [_vp]),
+    "mh_smtlib_create": (C.c_int32, [C.POINTER(_vp)]),
+    "mh_smtlib_destroy": (C.c_int32, [_vp]),
+    "mh_smtlib_read": (C.c_int32, [_vp, C.c_char_p, C.c_uint64, _vp]),
+    "mh_smtlib_commit": (C.c_int32, [_vp, C.POINTER(C.c_int64), C.c_uint64]),
+    "mh_smtlib_rollback": (C.c_int32, [_vp]),
+    "mh_smtlib_size": (C.c_uint64, [_vp]),
 }
+
+# mh_smt_record / mh_smt_result (include/mythril_hip.h)
+SMT_RECORD_DTYPE = np.dtype([("op", "u1"), ("pad0", "u1"), ("pad1", "<u2"), ("width", "<u4"),
+                             ("a", "<i8"), ("b", "<i8"), ("c", "<i8"), ("imm0", "<u4"),
+                             ("imm1", "<u4"), ("name_off", "<u4"), ("name_len", "<u4"),
+                             ("const_off", "<u4"), ("pad2", "<u4")])
+SMT_RESULT_DTYPE = np.dtype([("kind", "<u4"), ("pad", "<u4"), ("node", "<i8")])
+assert SMT_RECORD_DTYPE.itemsize == 56 and SMT_RESULT_DTYPE.itemsize == 16
+SMT_ASSERT, SMT_MINIMIZE, SMT_MAXIMIZE = 0, 1, 2
+
+
+class SmtBatch(C.Structure):
+    _fields_ = [("records", _vp), ("n_records", C.c_uint64), ("const_limbs", _vp),
+                ("names", _vp), ("results", _vp), ("n_results", C.c_uint64)]
 
 
 # mh_microbench_issue kinds (include/mythril_hip.h)
@@ -196,6 +216,119 @@ def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
             entry_col=arr(g.entry_col, n_entries), entry_val=arr(g.entry_val, 8 * n_entries).reshape(-1, 8))
     finally:
         lib.mh_harvest_free(h)
+
+
+class SmtlibSession:
+    """An SMT-LIB reader session (mh_smtlib): reads z3-printed text into a term builder,
+    handing over only the nodes the builder does not have yet (include/mythril_hip.h)."""
+
+    def __init__(self):
+        self.lib = load()
+        h = C.c_void_p()
+        _check(self.lib.mh_smtlib_create(C.byref(h)))
+        self.h = h
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.mh_smtlib_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return int(self.lib.mh_smtlib_size(self.h))
+
+    def read(self, text: str, b) -> List[Tuple[int, int]]:
+        """Parse `text` into builder `b`; [(SMT_ASSERT / MINIMIZE / MAXIMIZE, node)]."""
+        data = text.encode()
+        batch = SmtBatch()
+        _check(self.lib.mh_smtlib_read(self.h, data, len(data), C.byref(batch)))
+        n = int(batch.n_records)
+        ids: List[int] = []
+        if n:
+            try:
+                ids = self._merge(batch, n, b)
+            except Exception:
+                self.lib.mh_smtlib_rollback(self.h)
+                raise
+            arr = (C.c_int64 * n)(*ids)
+            _check(self.lib.mh_smtlib_commit(self.h, arr, n))
+        out = []
+        nr = int(batch.n_results)
+        if nr:
+            res = np.frombuffer((C.c_char * (nr * 16)).from_address(batch.results),
+                                dtype=SMT_RESULT_DTYPE)
+            for kind, _, node in res.tolist():
+                out.append((kind, node if node >= 0 else ids[-node - 1]))
+        return out
+
+    @staticmethod
+    def _merge(batch, n: int, b) -> List[int]:
+        """Build the batch's records in builder `b` (TapeBuilder._add's bookkeeping inlined for
+        the plain ops: the reader checked their sorts with TapeBuilder.op's rules)."""
+        from .tape import ARITY, F_HOST
+
+        recs = np.frombuffer((C.c_char * (n * 56)).from_address(batch.records),
+                             dtype=SMT_RECORD_DTYPE).tolist()
+        nl = max((r[9] + r[10] for r in recs), default=0)
+        names = C.string_at(batch.names, nl).decode() if nl else ""
+        nc = max((r[11] + 8 for r in recs if r[0] == 0), default=0)
+        cbuf = C.string_at(batch.const_limbs, 4 * nc) if nc else b""
+        arity = _ARITY_BY_INT or _arity_table(ARITY)
+        memo, nodes, widths, flags = b._memo, b.nodes, b.widths, b.flags
+        ids = [0] * n
+        for k, (op, _, _, w, a, bb, c, i0, i1, noff, nlen, coff, _) in enumerate(recs):
+            if a < 0:
+                a = ids[-a - 1]
+            if bb < 0:
+                bb = ids[-bb - 1]
+            if c < 0:
+                c = ids[-c - 1]
+            if 2 <= op < 80:  # plain ops (TRUE / FALSE included): TapeBuilder._add
+                key = (op, w, a, bb, c, i0, i1)
+                h = memo.get(key)
+                if h is None:
+                    ar = arity[op]
+                    if op == 30 and widths[a] > 256:
+                        f = F_HOST
+                    elif ar:
+                        f = (flags[a] | (flags[bb] if ar > 1 else 0)
+                             | (flags[c] if ar > 2 else 0)) & F_HOST
+                    else:
+                        f = 0
+                    h = len(nodes)
+                    nodes.append(key)
+                    widths.append(w)
+                    flags.append(f)
+                    memo[key] = h
+            elif op == 0:  # CONST (<= 256 bits; wider ones arrive as CONCATs)
+                h = b.const(int.from_bytes(cbuf[4 * coff:4 * coff + 32], "little"), w)
+            elif op == 1:
+                h = b.var(names[noff:noff + nlen], w)
+            elif op == 80:
+                h = b.array(names[noff:noff + nlen], i1, w)
+            elif op == 81:
+                h = b.const_array(i1, a)
+            elif op == 82:
+                h = b.store(a, bb, c)
+            elif op == 83:
+                h = b.select(a, bb)
+            else:
+                h = b.apply(names[noff:noff + nlen], i1, w, a)
+            ids[k] = h
+        return ids
+
+
+_ARITY_BY_INT: List[int] = []
+
+
+def _arity_table(arity) -> List[int]:
+    _ARITY_BY_INT[:] = [arity.get(o, 2) for o in range(256)]
+    return _ARITY_BY_INT
 
 
 def load(path: str = LIB_PATH) -> C.CDLL:

@@ -15,7 +15,9 @@
   (shared sub-terms as ``define-fun``), so ``--solver-log`` keeps working when the sieve
   front end answers, and ``parse(to_smtlib(q))`` round-trips.
 * ``from_z3(constraints)`` imports the reference's z3-backed ``Bool``s (``.raw``) through
-  ``sexpr()``, memoised per z3 AST (``get_id``), for the get_model front end.
+  ``sexpr()``, memoised per z3 AST (``get_id``), for the get_model front end; the text is read
+  by the C++ session behind ``mh_smtlib_read`` (``NativeReader``), ``Reader`` below is its
+  Python statement and parity reference.
 """
 from __future__ import annotations
 
@@ -525,6 +527,43 @@ def to_smtlib(constraints: Sequence, minimize: Sequence = (), maximize: Sequence
     return "\n".join(lines + body) + "\n"
 
 
+class NativeReader:
+    """The product path's SMT-LIB reader: the C++ session behind mh_smtlib_read (same fragment
+    and the same terms as ``Reader``, tests/test_smtlib_native.py), hash-consing against what it
+    has already handed to this context's builder, so a constraint that extends its parent's only
+    builds its new nodes on the host."""
+
+    def __init__(self, ctx: Optional[smt.Context] = None):
+        from . import native
+
+        self.ctx = ctx if ctx is not None else smt.Context()
+        self.b = self.ctx.b
+        self.session = native.SmtlibSession()
+
+    def read(self, text: str, q: Query) -> None:
+        from . import native
+
+        try:
+            items = self.session.read(text, self.b)
+        except native.SieveError as e:
+            raise SmtlibError(str(e)) from None
+        for kind, node in items:
+            if kind == native.SMT_ASSERT:
+                q.constraints.append(smt.Bool(node, self.ctx))
+            elif kind == native.SMT_MINIMIZE:
+                q.minimize.append(smt.BitVec(node, self.ctx))
+            else:
+                q.maximize.append(smt.BitVec(node, self.ctx))
+
+
+def parse_native(text: str, ctx: Optional[smt.Context] = None) -> Query:
+    """``parse`` through the C++ reader."""
+    r = NativeReader(ctx)
+    q = Query(r.ctx)
+    r.read(text, q)
+    return q
+
+
 # -- z3 import -------------------------------------------------------------------------------
 def _z3_sexpr(raw) -> str:
     import z3  # only on a box where the reference runs
@@ -549,7 +588,7 @@ class Z3Importer:
                  max_nodes: int = 1 << 21, sexpr_of=None, on_reset=None):
         from collections import OrderedDict
 
-        self.reader = Reader(ctx)
+        self.reader = NativeReader(ctx)
         self.memo: "OrderedDict[int, Tuple[object, int]]" = OrderedDict()
         self.max_memo = max_memo
         self.max_nodes = max_nodes
@@ -558,7 +597,8 @@ class Z3Importer:
         self.resets = 0
 
     def reset(self) -> None:
-        self.reader = Reader()
+        self.reader.session.close()
+        self.reader = NativeReader()
         self.memo.clear()
         self.resets += 1
         if self.on_reset is not None:
@@ -577,8 +617,7 @@ class Z3Importer:
             got = self.memo.get(key)
             if got is None or got[0] is not raw:
                 q = Query(self.reader.ctx)
-                for cmd in read_sexps(self.sexpr_of(raw)):
-                    self.reader.command(cmd, q)
+                self.reader.read(self.sexpr_of(raw), q)
                 node = q.constraints[-1].node if len(q.constraints) == 1 else \
                     smt.And(*q.constraints).node
                 got = self.memo[key] = (raw, node)

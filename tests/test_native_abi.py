@@ -13,7 +13,8 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 def declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|uint32_t|const char\*)\s+(mh_\w+)\s*\(", text,
+    return sorted(set(re.findall(
+        r"^\s*(?:int32_t|uint32_t|uint64_t|const char\*)\s+(mh_\w+)\s*\(", text,
                                  re.M)))
 
 
