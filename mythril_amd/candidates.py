@@ -45,6 +45,15 @@ def _mask(w: int) -> int:
     return (1 << w) - 1
 
 
+def _interval_values(lo: int, hi: int) -> List[int]:
+    """Values of [lo, hi] a guide proposes: both ends, the middle, lo + 1 (distinct, in order)."""
+    out: List[int] = []
+    for v in (lo, hi, lo + (hi - lo) // 2, lo + 1):
+        if lo <= v <= hi and v not in out:
+            out.append(v)
+    return out
+
+
 def _merge(xs: List[Alt], ys: List[Alt]) -> List[Alt]:
     if len(ys) == 1 and not ys[0]:
         return xs[:MAX_ALTS]
@@ -554,6 +563,19 @@ class Harvester:
                     break
             if len(self.sets) >= MAX_SETS:
                 break
+        # bounds on one term from several conjuncts (calldatasize guards of the ABI decoder,
+        # argument range checks): values inside their intersection, last, so they override the
+        # single-conjunct boundary values that satisfy one bound and break another
+        for t, (lo, hi, n_bounds) in self._intervals(conjuncts).items():
+            if n_bounds < 2 or lo > hi or len(self.sets) >= MAX_SETS:
+                continue
+            out: List[Alt] = []
+            for v in _interval_values(lo, hi):
+                r = self.invert_bits(t, v, _mask(b.widths[t]))
+                if r:
+                    out += [a for a in r if a]
+            if out:
+                self.sets.append((PROB_DEFAULT, out[:MAX_ALTS]))
         # hints first: the exact requirements of the conjuncts (later sets) override them
         hints = _prune_hints(self.hints)
         self.sets = self.sets[:1] + hints + self.sets[1:] if alt else hints + self.sets
@@ -575,6 +597,57 @@ class Harvester:
         copy_sets = [(PROB_DEFAULT, alts) for alts in self.copy_sets]
         return Guide(self.columns, widths, [self.pools[c] for c in self.columns],
                      self.sets[:MAX_SETS], copy_sets[:MAX_SETS // 4])
+
+    def _bound_of(self, n: int) -> Optional[Tuple[int, int, int]]:
+        """(term, lo, hi): conjunct n bounds a symbolic term to [lo, hi] (unsigned, inclusive)
+        against a constant -- ULT / ULE / UGT / UGE either way round, their negations, and the
+        Or(x < k, x == k) form of smt.ULE / smt.UGE; None otherwise."""
+        b = self.b
+        op, w, a, bb, c, i0, i1 = b.nodes[n]
+        truth = True
+        if op == Op.NOT:
+            truth = False
+            op, w, a, bb, c, i0, i1 = b.nodes[a]
+        strict_ops = {Op.BVULT: (True, True), Op.BVULE: (True, False),
+                      Op.BVUGT: (False, True), Op.BVUGE: (False, False)}
+        if op == Op.OR:  # Or(cmp(x, k), x == k): the non-strict comparison
+            l, r = b.nodes[a], b.nodes[bb]
+            if r[0] != Op.EQ or l[0] not in (Op.BVULT, Op.BVUGT) or (l[2], l[3]) != (r[2], r[3]):
+                return None
+            op = Op.BVULE if l[0] == Op.BVULT else Op.BVUGE
+            a, bb = l[2], l[3]
+        if op not in strict_ops:
+            return None
+        ka, kb = b.const_value(a), b.const_value(bb)
+        if (ka is None) == (kb is None):
+            return None
+        less, strict = strict_ops[op]
+        t, k = (a, kb) if kb is not None else (bb, ka)
+        if kb is None:  # k op t: flip to t op' k
+            less = not less
+        if not truth:  # not (t < k) == t >= k
+            less, strict = not less, not strict
+        m = _mask(b.widths[t])
+        if less:
+            lo, hi = 0, k - 1 if strict else k
+        else:
+            lo, hi = k + 1 if strict else k, m
+        return t, lo, hi
+
+    def _intervals(self, conjuncts: Sequence[int]) -> Dict[int, Tuple[int, int, int]]:
+        """Per bounded term (first-seen order): the intersection of its bounds, and their count."""
+        out: Dict[int, Tuple[int, int, int]] = {}
+        for cj in conjuncts:
+            got = self._bound_of(cj)
+            if got is None:
+                continue
+            t, lo, hi = got
+            if t in out:
+                plo, phi, n = out[t]
+                out[t] = (max(lo, plo), min(hi, phi), n + 1)
+            else:
+                out[t] = (lo, hi, 1)
+        return out
 
     def _eq_nodes(self, root: int, limit: int = 4096) -> List[int]:
         """Equalities anywhere under a conjunct (also inside ite conditions of bit-vector terms:

@@ -831,6 +831,20 @@ struct Harvester {
             }
             if ((int)sets.size() >= kMaxSets) break;
         }
+        // bounds on one term from several conjuncts (calldatasize guards, argument range
+        // checks): values inside their intersection, last, so they override the single-bound
+        // boundary values (candidates.py harvest, _intervals / _interval_values)
+        for (const Interval& iv : intervals(conj)) {
+            if (iv.n < 2 || iv.empty || (int)sets.size() >= kMaxSets) continue;
+            const int w = nd[iv.t].width;
+            Alts out;
+            for (const U& v : interval_values(iv.lo, iv.hi)) {
+                Res r = invert_bits(iv.t, v, mask(w));
+                if (!r.none && !r.alts().empty())
+                    for (const Alt& a : r.alts()) if (!a.empty()) out.push_back(a);
+            }
+            if (!out.empty()) sets.push_back({kProbDefault, head(out, kMaxAlts)});
+        }
         out_sets.clear();
         const bool first_parent = parent && !parent->empty() && !sets.empty();
         if (first_parent) out_sets.push_back({sets[0].first, &sets[0].second});
@@ -854,6 +868,88 @@ struct Harvester {
         if ((int)out_sets.size() > kMaxSets) out_sets.resize(kMaxSets);
         out_copies = copy_sets;
         if ((int)out_copies.size() > kMaxSets / 4) out_copies.resize(kMaxSets / 4);
+    }
+
+    // candidates.py _bound_of: conjunct n bounds a symbolic term to [lo, hi] (unsigned,
+    // inclusive) against a constant -- ULT / ULE / UGT / UGE either way round, their negations,
+    // and Or(x < k, x == k) (smt.ULE / smt.UGE); false otherwise
+    struct Interval { uint32_t t; U lo, hi; int n; bool empty; };
+    bool bound_of(uint32_t n, uint32_t& t, U& lo, U& hi, bool& empty) {
+        uint8_t op = nd[n].op;
+        uint32_t a = nd[n].a, b = nd[n].b;
+        bool truth = true;
+        if (op == NOT) {
+            truth = false;
+            op = nd[a].op;
+            b = nd[a].b;
+            a = nd[a].a;
+        }
+        if (op == OR) {  // Or(cmp(x, k), x == k): the non-strict comparison
+            const Node& l = nd[a];
+            const Node& r = nd[b];
+            if (r.op != EQ || (l.op != BVULT && l.op != BVUGT) || l.a != r.a || l.b != r.b)
+                return false;
+            op = l.op == BVULT ? BVULE : BVUGE;
+            a = l.a;
+            b = l.b;
+        }
+        if (op != BVULT && op != BVULE && op != BVUGT && op != BVUGE) return false;
+        const U* ka = const_value(a);
+        const U* kb = const_value(b);
+        if ((ka == nullptr) == (kb == nullptr)) return false;
+        bool less = op == BVULT || op == BVULE;
+        bool strict = op == BVULT || op == BVUGT;
+        t = kb ? a : b;
+        const U k = kb ? *kb : *ka;
+        if (!kb) less = !less;
+        if (!truth) { less = !less; strict = !strict; }
+        const U m = mask(nd[t].width);
+        empty = false;
+        if (less) {
+            lo = U::of(0);
+            if (strict && k == U::of(0)) empty = true;
+            hi = strict ? k - U::of(1) : k;
+        } else {
+            if (strict && k == m) empty = true;
+            lo = strict ? k + U::of(1) : k;
+            hi = m;
+        }
+        return true;
+    }
+    std::vector<Interval> intervals(const std::vector<uint32_t>& conj) {
+        std::vector<Interval> out;
+        std::unordered_map<uint32_t, size_t> at;
+        for (uint32_t cj : conj) {
+            uint32_t t;
+            U lo, hi;
+            bool empty;
+            if (!bound_of(cj, t, lo, hi, empty)) continue;
+            auto it = at.find(t);
+            if (it == at.end()) {
+                at.emplace(t, out.size());
+                out.push_back(Interval{t, lo, hi, 1, empty});
+            } else {
+                Interval& iv = out[it->second];
+                if (iv.lo < lo) iv.lo = lo;
+                if (hi < iv.hi) iv.hi = hi;
+                iv.empty = iv.empty || empty;
+                ++iv.n;
+            }
+        }
+        for (Interval& iv : out) if (iv.hi < iv.lo) iv.empty = true;
+        return out;
+    }
+    // candidates.py _interval_values: both ends, the middle, lo + 1 (distinct, in order)
+    static std::vector<U> interval_values(const U& lo, const U& hi) {
+        std::vector<U> out;
+        const U cand[4] = {lo, hi, lo + shr(hi - lo, 1), lo + U::of(1)};
+        for (const U& v : cand) {
+            if (v < lo || hi < v) continue;
+            bool dup = false;
+            for (const U& x : out) dup = dup || x == v;
+            if (!dup) out.push_back(v);
+        }
+        return out;
     }
 
     // candidates.py _prune_hints: per column, of the single-column hint sets only the

@@ -205,3 +205,21 @@ def test_z3_style_solver_log_on_gpu(gpu_ctx):
     q = smtlib.parse(Z3_STYLE)
     m = frontend.get_model(tuple(q.constraints))
     assert _oracle_holds(q.ctx, q.constraints, m.schema, m.values)
+
+
+@pytest.mark.parametrize("name", ["killbilly", "ether_thief", "overflow"])
+def test_long_path_on_gpu(gpu_ctx, name):
+    """A 200-constraint path (tests/laser_paths.py) through get_model in LASER order (every
+    prefix first, keyed as the plugin keys it): the final witness is a model of the whole
+    ORIGINAL path (oracle/term_eval.py), and the UNSAT variant goes to the fallback."""
+    from tests.laser_paths import grow
+
+    ctx, cs = grow(name, 200)
+    s = frontend.sieve()
+    for k in range(1, len(cs)):
+        s.solve(ctx.b, [c.node for c in cs[:k]], key=tuple(c.node for c in cs[:k]))
+    m = frontend.get_model(tuple(cs))
+    assert _oracle_holds(ctx, cs, m.schema, m.values), name
+    ctx, cs = grow(name, 200, unsat=True)
+    frontend.configure(fallback=lambda *a: "z3")
+    assert frontend.get_model(tuple(cs)) == "z3"

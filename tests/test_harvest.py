@@ -217,3 +217,39 @@ def test_harvest_rejects_bad_layout_nodes():
     nodes[1] = (int(Op.SEXT), 0, 8, 0, 0, 0, 8, 0)  # sign extension of a Bool
     with pytest.raises(native.SieveError):
         native.harvest_guide(nodes, np.zeros((1, 8), np.uint32), [8])
+
+
+@pytest.mark.parametrize("name", ["killbilly", "overflow", "ether_thief"])
+def test_harvest_matches_python_on_grown_paths(name):
+    """Paths grown to 60 constraints (tests/laser_paths.py): several bounds on one term (the ABI
+    decoder's calldatasize guards, argument range checks) give interval sets; LASER order, every
+    prefix, plus the UNSAT variant at 120."""
+    from .laser_paths import grow
+
+    _lib_or_skip()
+    ctx, cs = grow(name, 60)
+    for k in range(1, len(cs) + 1):
+        _compare(ctx.b, [c.node for c in cs[:k]])
+    ctx, cs = grow(name, 120, unsat=True)
+    _compare(ctx.b, [c.node for c in cs])
+
+
+def test_interval_sets_propose_values_inside_every_bound():
+    """Not(size < 68), size < 5000, Not(size < 4): the interval set's values lie in [68, 4999]
+    (the single-bound sets alone propose 4, 5, 0 ... which break the other bounds)."""
+    from mythril_amd.candidates import _interval_values
+    from mythril_amd.smt import Not, ULT, symbol_factory as F
+
+    from .laser_like import Calldata
+
+    ctx, _ = laser_like.queries()
+    cd = Calldata("9")
+    cs = [Not(ULT(cd.size, F.BitVecVal(68, 256))), ULT(cd.size, F.BitVecVal(5000, 256)),
+          Not(ULT(cd.size, F.BitVecVal(4, 256)))]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    cols = list(schema.columns)
+    g = build_guide(ctx.b, root, schema, cols)
+    last = g.sets[-1][1]
+    vals = sorted(a["9_calldatasize"] for a in last)
+    assert vals == sorted(_interval_values(68, 4999)) and all(68 <= v <= 4999 for v in vals)
+    _compare(ctx.b, [c.node for c in cs])
