@@ -12,6 +12,10 @@
 #   interp    scripts/interp_op_cost.py (interpreter cost of a loaded column / a complex op)
 #   counters  rocprofv3 -L (the PMC counters this box offers)
 #   profile   scripts/profile.sh <tag> (kernel trace + PMC passes of the default bench)
+#   kbench    bench.py --variant keccak (config 4's kernel, 2^20 rows)
+#   kprofile  scripts/profile.sh <tag>_keccak --variant keccak
+#   paths     scripts/path_scaling.py (latency against path length, 25..400 constraints)
+#   strong    bench.py --strong at N=1 (config 5 literally: 2^26 rows in total)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:?tag}
@@ -35,6 +39,10 @@ for step in "$@"; do
     interp)   timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost.jsonl" 2> "$OUT/interp_op_cost.log" ;;
     counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 ;;
     profile)  bash scripts/profile.sh "$TAG" ;;
+    kbench)   timeout -k 10 400 python -u bench.py --variant keccak --cpu-seconds 5 > "$OUT/bench_keccak.json" 2> "$OUT/bench_keccak.log" ;;
+    kprofile) bash scripts/profile.sh "${TAG}_keccak" --variant keccak ;;
+    paths)    timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" ;;
+    strong)   timeout -k 10 400 python -u bench.py --strong --no-companion --cpu-seconds 3 > "$OUT/bench_strong.json" 2> "$OUT/bench_strong.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
