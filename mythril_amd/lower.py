@@ -549,7 +549,8 @@ MAX_LOWERINGS = 64  # pass-2 memos kept per builder, by harvest fingerprint (LRU
 
 
 def lower_query(b: TapeBuilder, roots: Sequence[int],
-                frozen: Optional[Schema] = None) -> Tuple[int, Schema]:
+                frozen: Optional[Schema] = None, _fresh_prefix: bool = False
+                ) -> Tuple[int, Schema]:
     """Lower the conjunction of Bool `roots`: (root node of the column-only term, schema).
 
     Without ``frozen`` both passes are memoised on the builder: pass 1 per constraint
@@ -560,6 +561,8 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
         L = Lowering(b, frozen)
         low = [L.lower(r) for r in roots]
         schema = L.schema
+    elif not _fresh_prefix and len(roots) > 1 and _prefix_state(b, roots) is not None:
+        return _lower_extend(b, roots)
     else:
         per_root: Dict[int, Harvest] = _memo(b, "_harvest_of")
         h = Harvest()
@@ -581,20 +584,7 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
         low = [L.lower(r) for r in roots]
         cols = node_columns(b, low)
         used = frozenset().union(*(cols[r] for r in low)) if low else frozenset()
-        names = var_names(b)
-        full = L.schema
-        cols = {}
-        for v in sorted(used):
-            name = names[v]
-            col = full.columns.get(name)
-            if col is None:  # made by an earlier Lowering (a stable rewrite), else a plain
-                # variable under a term the rewrite left as it was
-                col = b.__dict__.get("_lower_columns", {}).get(name)
-                if col is None:
-                    col = Column(name, b.symbols.var_widths[name], "var", name)
-                full.columns[name] = col
-            cols[name] = col
-        schema = Schema(full.cells, full.uf_cells, full.keccak, cols)
+        schema = _schema_of(b, L, used)
     for r in low:
         if b.widths[r] != BOOL:
             raise TapeError("constraints must be Bool")
@@ -603,4 +593,80 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
     acc = low[0]
     for x in low[1:]:
         acc = b.op(Op.AND, acc, x)
+    if frozen is None:
+        _remember_prefix(b, roots, h, fp, L, low, used, acc)
     return acc, schema
+
+
+# -- LASER order: a query that extends its parent's roots by one constraint -------------------
+PREFIX_STATES = 256  # lowered prefixes kept per builder
+
+
+@dataclass
+class _Prefix:
+    harvest: Harvest
+    fp: tuple
+    lowering: "Lowering"
+    low: List[int]
+    used: frozenset
+    acc: int
+
+
+def _prefix_state(b: TapeBuilder, roots: Sequence[int]) -> Optional[_Prefix]:
+    cache = b.__dict__.get("_lower_prefixes")
+    return None if cache is None else cache.get(tuple(roots[:-1]))
+
+
+def _remember_prefix(b, roots, h, fp, L, low, used, acc) -> None:
+    cache = b.__dict__.setdefault("_lower_prefixes", OrderedDict())
+    cache[tuple(roots)] = _Prefix(h, fp, L, list(low), used, acc)
+    while len(cache) > PREFIX_STATES:
+        cache.popitem(last=False)
+
+
+def _lower_extend(b: TapeBuilder, roots: Sequence[int]) -> Tuple[int, "Schema"]:
+    """lower_query of `roots` from the lowered state of ``roots[:-1]`` (svm.py:257-262: every new
+    state's query is its parent's plus one constraint): the new constraint's harvest is merged
+    into the parent's; an unchanged fingerprint keeps the parent's lowering and its lowered
+    conjuncts, so only the new constraint is lowered and ANDed on.  The result is lower_query's
+    from scratch (tests/test_lowering.py compares them)."""
+    par = _prefix_state(b, roots)
+    new = roots[-1]
+    per_root: Dict[int, Harvest] = _memo(b, "_harvest_of")
+    hn = per_root.get(new)
+    if hn is None:
+        hn = per_root[new] = Lowering(b).collect([new])
+    h = Harvest({k: set(v) for k, v in par.harvest.cells.items()},
+                {k: set(v) for k, v in par.harvest.uf_cells.items()},
+                {k: dict(v) for k, v in par.harvest.keccak.items()}, dict(par.harvest.bounds))
+    h.merge(hn)
+    fp = h.fingerprint()
+    if fp != par.fp:  # new keys / keccak pairs: every constraint's rewrite may change
+        return lower_query(b, list(roots[:-1]) + [new], _fresh_prefix=True)
+    L = par.lowering
+    x = L.lower(new)
+    if b.widths[x] != BOOL:
+        raise TapeError("constraints must be Bool")
+    low = par.low + [x]
+    used = par.used | node_columns(b, [x])[x]
+    acc = b._add(Op.AND, BOOL, par.acc, x)
+    _remember_prefix(b, roots, h, fp, L, low, used, acc)
+    return acc, _schema_of(b, L, used)
+
+
+def _schema_of(b: TapeBuilder, L: "Lowering", used: frozenset) -> "Schema":
+    """The query's schema: the columns of the VARs its lowered term reads, in VAR order."""
+    names = var_names(b)
+    full = L.schema
+    cols = {}
+    for v in sorted(used):
+        name = names[v]
+        col = full.columns.get(name)
+        if col is None:  # made by an earlier Lowering (a stable rewrite), else a plain
+            # variable under a term the rewrite left as it was
+            col = b.__dict__.get("_lower_columns", {}).get(name)
+            if col is None:
+                col = Column(name, b.symbols.var_widths[name], "var", name)
+            full.columns[name] = col
+        cols[name] = col
+    return Schema(full.cells, full.uf_cells, full.keccak, cols)

@@ -188,6 +188,122 @@ def eliminate_definitions(b: TapeBuilder, conj: Sequence[int], schema: Schema
             [(col, env[idx]) for col, idx in defs])
 
 
+def _may_define(b: TapeBuilder, root: int) -> bool:
+    """Whether a conjunct of `root` has the shape of a definition (``v == t`` with a symbol on
+    one side and a computed term on the other; eliminate_definitions decides), memoised per
+    node on the builder: a child query's AND node answers from its parent's."""
+    memo = b.__dict__.setdefault("_may_define", {})
+    got = memo.get(root)
+    if got is not None:
+        return got
+    nodes = b.nodes
+    stack, order = [root], []
+    while stack:  # the AND nodes not answered yet, parents after children
+        n = stack.pop()
+        if n in memo:
+            continue
+        order.append(n)
+        if nodes[n][0] == Op.AND:
+            stack += [x for x in (nodes[n][2], nodes[n][3]) if x not in memo]
+    for n in reversed(order):
+        op, _, a, bb = nodes[n][:4]
+        if op == Op.AND:
+            memo[n] = memo[a] or memo[bb]
+        elif op == Op.EQ:
+            ka, kb = nodes[a][0], nodes[bb][0]
+            memo[n] = ((ka == Op.VAR and kb not in (Op.VAR, Op.CONST))
+                       or (kb == Op.VAR and ka not in (Op.VAR, Op.CONST)))
+        else:
+            memo[n] = False
+    return memo[root]
+
+
+class _Group:
+    __slots__ = ("first", "idx", "conj", "vars", "acc")
+
+    def __init__(self, first, idx, conj, vars_, acc):
+        self.first, self.idx, self.conj, self.vars, self.acc = first, idx, conj, vars_, acc
+
+
+class _BucketState:
+    """The variable-disjoint groups of an AND chain's conjuncts, extendable by more conjuncts.
+    Groups are immutable (a child state shares its parent's)."""
+
+    def __init__(self):
+        self.n = 0
+        self.groups: Dict[object, _Group] = {}
+        self.var_group: Dict[int, object] = {}
+
+    def copy(self) -> "_BucketState":
+        st = _BucketState()
+        st.n, st.groups, st.var_group = self.n, dict(self.groups), dict(self.var_group)
+        return st
+
+    def add(self, b: TapeBuilder, cn: int, vs: frozenset) -> None:
+        i = self.n
+        self.n += 1
+        and_ = int(Op.AND)
+        if not vs:  # a ground conjunct: its own group (one per node)
+            key = ("ground", cn)
+            g = self.groups.get(key)
+            self.groups[key] = (_Group(i, (i,), (cn,), frozenset(), cn) if g is None else
+                                _Group(g.first, g.idx + (i,), g.conj + (cn,), g.vars,
+                                       b._add(and_, 0, g.acc, cn)))
+            return
+        gids = {self.var_group[v] for v in vs if v in self.var_group}
+        if not gids:
+            key = ("vars", i)
+            self.groups[key] = _Group(i, (i,), (cn,), vs, cn)
+        elif len(gids) == 1:
+            key = next(iter(gids))
+            g = self.groups[key]
+            self.groups[key] = _Group(g.first, g.idx + (i,), g.conj + (cn,), g.vars | vs,
+                                      b._add(and_, 0, g.acc, cn))
+        else:  # the conjunct joins several groups: one group, conjuncts in path order
+            members = [self.groups.pop(k) for k in gids]
+            pairs = sorted([p for g in members for p in zip(g.idx, g.conj)] + [(i, cn)])
+            acc = pairs[0][1]
+            for _, x in pairs[1:]:
+                acc = b._add(and_, 0, acc, x)
+            vars_ = frozenset(vs).union(*[g.vars for g in members])
+            key = ("vars", min(g.first for g in members))
+            self.groups[key] = _Group(pairs[0][0], tuple(p[0] for p in pairs),
+                                      tuple(p[1] for p in pairs), vars_, acc)
+        for v in self.groups[key].vars:
+            self.var_group[v] = key
+
+    def ordered(self) -> List[_Group]:
+        return sorted(self.groups.values(), key=lambda g: g.first)
+
+
+BUCKET_STATES = 256  # states of recent AND roots kept per builder
+
+
+def _bucket_state(b: TapeBuilder, root: int) -> _BucketState:
+    """The grouping of `root`'s conjuncts, memoised per AND root on the builder: a query that
+    extends its parent (svm.py:257-262, root = AND(parent, new)) adds only its new conjunct."""
+    memo = b.__dict__.setdefault("_bucket_states", OrderedDict())
+    got = memo.get(root)
+    if got is not None:
+        memo.move_to_end(root)
+        return got
+    node = b.nodes[root]
+    base = memo.get(node[2]) if node[0] == Op.AND else None
+    if base is not None:
+        st = base.copy()
+        new = Sieve.conjuncts(b, node[3])
+    else:
+        st = _BucketState()
+        new = Sieve.conjuncts(b, root)
+    cols = node_columns(b, new)
+    for cn in new:
+        st.add(b, cn, cols[cn])
+    memo[root] = st
+    while len(memo) > BUCKET_STATES:
+        memo.popitem(last=False)
+    return st
+
+
 # ops whose recomputation is cheap enough to duplicate instead of keeping a value live
 _HEAVY = {Op.BVMUL, Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD, Op.KECCAK,
           Op.EVM_EXP, Op.BVMUL_NOOVFL_U, Op.EVM_ADDMOD, Op.EVM_MULMOD}
@@ -320,7 +436,11 @@ class Sieve:
 
     def solve_definitions(self, b: TapeBuilder, root: int, schema: Schema
                           ) -> Tuple[int, List[Tuple[str, int]]]:
-        """`root` with its definitions eliminated (eliminate_definitions), and the definitions."""
+        """`root` with its definitions eliminated (eliminate_definitions), and the definitions.
+        A root whose conjuncts hold no candidate definition (memoised per AND node) is returned
+        as it is without a walk over its conjuncts."""
+        if not _may_define(b, root):
+            return root, []
         conj = self.conjuncts(b, root)
         rest, defs = eliminate_definitions(b, conj, schema)
         if not defs:
@@ -359,32 +479,14 @@ class Sieve:
     def buckets(cls, b: TapeBuilder, root: int) -> List[Tuple[List[int], set]]:
         """Variable-disjoint groups of the conjuncts of `root` (the DependenceMap of
         laser/smt/solver/independence_solver.py:38-83, over lowered columns): [(conjunct nodes,
-        column var indices)].  Groups share no column, so each can take its witness from a
-        different candidate row."""
-        conj = cls.conjuncts(b, root)
-        # column sets per node, memoised on the builder: nodes are immutable and hash-consed, so
-        # a query that extends its parent (svm.py:257-262) only visits its new nodes
-        cols = node_columns(b, conj)
-        parent: Dict[int, int] = {}
+        column var indices)], in order of each group's first conjunct.  Groups share no column,
+        so each can take its witness from a different candidate row."""
+        return [(list(g.conj), set(g.vars)) for g in _bucket_state(b, root).ordered()]
 
-        def find(x):
-            while parent.setdefault(x, x) != x:
-                parent[x] = parent[parent[x]]
-                x = parent[x]
-            return x
-
-        for cn in conj:
-            vs = list(cols[cn])
-            for v in vs[1:]:
-                parent[find(v)] = find(vs[0])
-        groups: Dict[object, Tuple[List[int], set]] = {}
-        for cn in conj:
-            vs = cols[cn]
-            key = find(next(iter(vs))) if vs else ("ground", cn)
-            g = groups.setdefault(key, ([], set()))
-            g[0].append(cn)
-            g[1].update(vs)
-        return list(groups.values())
+    @staticmethod
+    def bucket_roots(b: TapeBuilder, root: int) -> List[Tuple[int, List[int]]]:
+        """Per group of ``buckets``: (the AND of its conjuncts in order, its var indices)."""
+        return [(g.acc, list(g.vars)) for g in _bucket_state(b, root).ordered()]
 
     def solve(self, b: TapeBuilder, roots: Sequence[int], key: Optional[tuple] = None,
               budget_s: Optional[float] = None) -> Optional[Witness]:
@@ -409,15 +511,10 @@ class Sieve:
 
             schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
         root, defs = self.solve_definitions(b, root, schema)
-        groups = self.buckets(b, root)
+        groups = self.bucket_roots(b, root)
         names = {b.var_index[c]: c for c in columns}
-        group_cols, accs = [], []
-        for conj, vs in groups:
-            acc = conj[0]
-            for x in conj[1:]:
-                acc = b.op(Op.AND, acc, x)
-            accs.append(acc)
-            group_cols.append([names[v] for v in vs])
+        group_cols = [[names[v] for v in vs] for _, vs in groups]
+        accs = [acc for acc, _ in groups]
         # the guide is harvested natively from the root's tape: the one tape of a query whose
         # conjuncts share columns (the same AND chain), else an extra tape of the same tape set
         # (same constants), not compiled
