@@ -16,6 +16,7 @@
 #   kprofile  scripts/profile.sh <tag>_keccak --variant keccak
 #   paths     scripts/path_scaling.py (latency against path length, 25..400 constraints)
 #   strong    bench.py --strong at N=1 (config 5 literally: 2^26 rows in total)
+#   import    scripts/import_cost.py (the z3 import stage per new constraint, C++ vs Python)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:?tag}
@@ -42,6 +43,7 @@ for step in "$@"; do
     kbench)   timeout -k 10 400 python -u bench.py --variant keccak --cpu-seconds 5 > "$OUT/bench_keccak.json" 2> "$OUT/bench_keccak.log" ;;
     kprofile) bash scripts/profile.sh "${TAG}_keccak" --variant keccak ;;
     paths)    timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" ;;
+    import)   timeout -k 10 300 python -u scripts/import_cost.py > "$OUT/import_cost.jsonl" 2> "$OUT/import_cost.log" ;;
     strong)   timeout -k 10 400 python -u bench.py --strong --no-companion --cpu-seconds 3 > "$OUT/bench_strong.json" 2> "$OUT/bench_strong.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
