@@ -237,6 +237,78 @@ int32_t mh_smtlib_commit(mh_smtlib* s, const int64_t* host_ids, uint64_t n);
 int32_t mh_smtlib_rollback(mh_smtlib* s);
 uint64_t mh_smtlib_size(const mh_smtlib* s);  /* nodes the session mirrors                      */
 
+/* ---- query compiler (the host stages of one get_model query) ---------------------------------
+ * Replaces the Python stages behind mythril_amd/sieve.py Sieve.solve for a query: lower_query
+ * (mythril_amd/lower.py: arrays, store chains, keccak and other uninterpreted functions onto
+ * scalar columns), Sieve.bucket_roots (the DependenceMap of laser/smt/solver/
+ * independence_solver.py:38-83 over the lowered columns) and local_tapeset (one device tape per
+ * group over the query's own columns and constants).  An mh_terms session mirrors the host's
+ * hash-consed term store (tape.py TapeBuilder); mh_terms_append hands it the nodes (flags
+ * included: F_ARRAY 1, F_HOST 2; host-only kinds 80..84 as in mh_smt_record), the constant pool
+ * entries (8 limbs each) and the variable / array / function names (NUL-terminated, back to back,
+ * numbered in order) the host made since the last call.  mh_query_build compiles the conjunction
+ * of `roots`: tape 0 is the root (the guide's input, mh_guide_harvest); with n_groups > 1 tapes
+ * 1..n_groups are the column-disjoint groups in order of their first conjunct, with n_groups == 1
+ * tape 0 is the one group's.  VAR imm0 = column (0..n_columns-1), CONST imm0 = constant
+ * (0..n_consts-1).  A ground query has one Bool column "__ground__" no tape reads.  flags
+ * MH_QUERY_DEFINITIONS: a conjunct has the shape variable == computed term, which the host's
+ * definition elimination (sieve.py eliminate_definitions) may use -- the host may discard the
+ * result and take its own stages.  Constructs the lowering does not model are MH_E_UNSUPPORTED
+ * (the query goes to z3).  A session is used by one thread at a time.                            */
+typedef struct mh_terms mh_terms;
+typedef struct mh_query mh_query;
+enum { MH_COL_VAR = 0, MH_COL_CELL = 1, MH_COL_ELSE = 2, MH_COL_UFCELL = 3, MH_COL_UFELSE = 4 };
+enum { MH_TABLE_CELLS = 0, MH_TABLE_UF_CELLS = 1, MH_TABLE_KECCAK = 2 };
+#define MH_QUERY_DEFINITIONS 1u
+#define MH_QUERY_KEY_LIMBS 36  /* limbs of a table entry / cell key (1152 bits; keccak arguments are
+                                   up to 1088 bits wide)                                        */
+typedef struct {
+    uint32_t name_off, name_len;      /* column name in info.names ("x", "A[0x4]", "A[*]")         */
+    uint32_t symbol_off, symbol_len;  /* variable / array / function name                          */
+    uint32_t width;
+    uint32_t kind;                    /* MH_COL_*                                                  */
+    uint32_t key_off;                 /* cells: key = MH_QUERY_KEY_LIMBS limbs at key_limbs[
+                                         MH_QUERY_KEY_LIMBS * key_off]; else ~0u                  */
+    uint32_t pad;
+} mh_query_column;                    /* 32 bytes                                                  */
+typedef struct {
+    uint32_t kind;                    /* MH_TABLE_*                                                */
+    uint32_t name_off, name_len;      /* array / function name in info.names                       */
+    uint32_t limb_off;                /* first entry in table_limbs (MH_QUERY_KEY_LIMBS limbs each)  */
+    uint32_t n_items;                 /* CELLS: n_items keys (ascending, every harvested key);
+                                         KECCAK: the interval base, then n_items (argument, hash)
+                                         pairs                                                     */
+    uint32_t pad;
+} mh_query_table;                     /* 24 bytes                                                  */
+typedef struct {
+    const mh_node* nodes;             /* every tape, back to back                                  */
+    const uint64_t* tape_off;         /* [n_tapes + 1]                                             */
+    const uint32_t* consts;           /* [n_consts][8]                                             */
+    const mh_query_column* columns;
+    const char* names;
+    const uint32_t* key_limbs;
+    const uint32_t* group_cols;       /* the columns of group g: group_cols[group_off[g] ..        */
+    const uint32_t* group_off;        /*   group_off[g + 1]), ascending; [n_groups + 1]            */
+    const mh_query_table* tables;
+    const uint32_t* table_limbs;
+    uint32_t n_tapes, n_consts, n_columns, names_len, n_groups, n_tables, flags;
+    uint32_t n_keys;                  /* entries of key_limbs                                      */
+    uint32_t n_table_entries;         /* entries of table_limbs                                    */
+    uint32_t pad;
+} mh_query_info;
+int32_t mh_terms_create(mh_terms** out);
+int32_t mh_terms_destroy(mh_terms* t);
+int32_t mh_terms_append(mh_terms* t, const mh_node* nodes, uint64_t n_nodes,
+                        const uint32_t* consts, uint64_t n_consts, const char* var_names,
+                        uint64_t n_vars, const char* array_names, uint64_t n_arrays,
+                        const char* fn_names, uint64_t n_fns);
+/* nodes, constants, variables, arrays, functions the session holds                                */
+int32_t mh_terms_sizes(const mh_terms* t, uint64_t* out /* [5] */);
+/* On MH_OK *info points into *out, which owns the arrays until mh_query_free(*out).              */
+int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_query** out,
+                       mh_query_info* info);
+int32_t mh_query_free(mh_query* q);
+
 /* ---- evaluation ------------------------------------------------------------------------------ */
 /* Evaluate tapes [tape_first, tape_first+tape_count) over assignment rows [row_first,
  * row_first+row_count) of `as`.  Results are indexed by tape - tape_first and hold GLOBAL indices

@@ -1,0 +1,1079 @@
+// The query compiler behind the C-ABI (mh_terms_*, mh_query_*): lowering, bucketing and tape
+// linearisation of one get_model query in C++ (Sieve.solve's host stages).
+//
+// A session (mh_terms) mirrors the host's hash-consed term store (mythril_amd/tape.py
+// TapeBuilder): its nodes with their flags, its 256-bit constant pool and the symbol tables
+// (variable, array and function names), appended incrementally.  mh_query_build then does what
+// mythril_amd/lower.py lower_query, sieve.py Sieve.bucket_roots and sieve.py local_tapeset do for
+// the conjunction of some root nodes, with the same results (tests/test_query_native.py):
+//
+//  * pass 1 (lower.py Lowering.collect / apply_harvest): the constant keys each free array and
+//    each non-keccak function is read at, the concrete keccak pairs keccak256_N(c) == k and the
+//    lowest bound a keccak application is compared with;
+//  * pass 2 (Lowering.lower / _rewrite): only nodes that are or read host-only terms (F_HOST) are
+//    rewritten -- select / store chains to ite chains over the store keys and the array's cell
+//    columns (name "A[0x..]", else column "A[*]"), K(v) to v, keccak256_N to ite(x == c_i, k_i,
+//    base + ((keccak(x) >> 139) << 6)), keccak256_N-1(keccak256_N(x)) to x, other functions
+//    tabled like arrays, equalities wider than 256 bits split on both sides' concat boundaries;
+//  * the AND leaves of the lowered conjunction split into column-disjoint groups (Sieve.buckets,
+//    the DependenceMap of laser/smt/solver/independence_solver.py:38-83), ordered by their first
+//    conjunct, ground conjuncts one group per node;
+//  * the root tape (the guide's input) and, with more than one group, one tape per group (the
+//    AND of its conjuncts in path order), over the query's own columns and constants.
+//
+// A query whose lowered conjuncts have the shape of a symbol definition (sieve.py
+// eliminate_definitions: variable == computed term) is flagged MH_QUERY_DEFINITIONS; the host
+// then takes its Python stages.  A session is used by one thread at a time (scratch is shared).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mythril_hip.h"
+
+int32_t mh_detail_set_err(int32_t code, const char* msg);  // capi.cpp
+
+namespace {
+
+enum : uint8_t {
+    CONST = 0, VAR = 1, TRUE_ = 2, FALSE_ = 3, BVADD = 10, BVSHL = 23, BVLSHR = 24, EQ = 30,
+    BVULT = 31, BVSGE = 38, AND = 40, ITE = 45, EXTRACT = 50, CONCAT = 51, ZEXT = 52, SEXT = 53,
+    KECCAK = 60, ARRAY = 80, CONST_ARRAY = 81, STORE = 82, SELECT = 83, UF = 84,
+};
+constexpr uint8_t F_ARRAY = 1, F_HOST = 2;
+constexpr uint32_t KECCAK_SHIFT = 139, KECCAK_ALIGN = 6;  // lower.py KECCAK_SHIFT / KECCAK_ALIGN
+constexpr int NL = MH_QUERY_KEY_LIMBS;                     // 1152-bit host values (<= 1088 used)
+constexpr uint32_t OV_CONST = 0x80000000u;  // query-made CONST imm0: index into the query's values
+constexpr uint32_t CELL_COL = 0x40000000u;  // query-made VAR imm0: index into the query's cells
+
+struct Fail {
+    int32_t code;
+    std::string msg;
+};
+[[noreturn]] void unsupported(const std::string& m) { throw Fail{MH_E_UNSUPPORTED, m}; }
+[[noreturn]] void invalid(const std::string& m) { throw Fail{MH_E_INVALID, m}; }
+
+int arity(uint8_t op) {  // tape.py ARITY
+    switch (op) {
+        case CONST: case VAR: case TRUE_: case FALSE_: case ARRAY: return 0;
+        case MH_OP_BVNEG: case MH_OP_BVNOT: case MH_OP_NOT: case EXTRACT: case ZEXT: case SEXT:
+        case KECCAK: case CONST_ARRAY: case UF: return 1;
+        case ITE: case MH_OP_EVM_ADDMOD: case MH_OP_EVM_MULMOD: case STORE: return 3;
+        default: return 2;
+    }
+}
+
+struct Big {  // unsigned, little-endian u32 limbs
+    uint32_t w[NL] = {};
+    bool operator==(const Big& o) const { return memcmp(w, o.w, sizeof w) == 0; }
+    bool operator<(const Big& o) const {
+        for (int i = NL - 1; i >= 0; --i)
+            if (w[i] != o.w[i]) return w[i] < o.w[i];
+        return false;
+    }
+    bool zero() const {
+        for (uint32_t x : w)
+            if (x) return false;
+        return true;
+    }
+    Big shr(uint32_t s) const {
+        Big r;
+        const uint32_t q = s / 32, b = s % 32;
+        for (uint32_t i = 0; i + q < NL; ++i) {
+            uint64_t v = w[i + q] >> b;
+            if (b && i + q + 1 < NL) v |= (uint64_t)w[i + q + 1] << (32 - b);
+            r.w[i] = (uint32_t)v;
+        }
+        return r;
+    }
+    Big shl(uint32_t s) const {
+        Big r;
+        const uint32_t q = s / 32, b = s % 32;
+        for (uint32_t i = q; i < NL; ++i) {
+            uint64_t v = (uint64_t)w[i - q] << b;
+            if (b && i > q) v |= w[i - q - 1] >> (32 - b);
+            r.w[i] = (uint32_t)v;
+        }
+        return r;
+    }
+    Big masked(uint32_t bits) const {
+        Big r = *this;
+        for (uint32_t i = 0; i < NL; ++i) {
+            const uint32_t lo = 32 * i;
+            if (lo >= bits) r.w[i] = 0;
+            else if (bits - lo < 32) r.w[i] &= (1u << (bits - lo)) - 1u;
+        }
+        return r;
+    }
+    Big operator|(const Big& o) const {
+        Big r;
+        for (int i = 0; i < NL; ++i) r.w[i] = w[i] | o.w[i];
+        return r;
+    }
+    Big plus(uint32_t v) const {
+        Big r = *this;
+        uint64_t c = v;
+        for (int i = 0; i < NL && c; ++i) {
+            c += r.w[i];
+            r.w[i] = (uint32_t)c;
+            c >>= 32;
+        }
+        return r;
+    }
+    bool bit(uint32_t i) const { return (w[i / 32] >> (i % 32)) & 1u; }
+    std::string hex() const {  // Python's "%#x"
+        static const char* d = "0123456789abcdef";
+        int i = NL * 8 - 1;
+        while (i > 0 && !((w[i / 8] >> (4 * (i % 8))) & 15u)) --i;
+        std::string s = "0x";
+        for (; i >= 0; --i) s += d[(w[i / 8] >> (4 * (i % 8))) & 15u];
+        return s;
+    }
+};
+struct BigHash {
+    size_t operator()(const Big& b) const {
+        uint64_t h = 1469598103934665603ull;
+        for (int i = 0; i < 9; ++i) h = (h ^ b.w[i]) * 1099511628211ull;  // low 288 bits
+        return (size_t)h;
+    }
+};
+
+struct Key {
+    uint32_t op, width, a, b, c, imm0, imm1;
+    bool operator==(const Key& o) const {
+        return op == o.op && width == o.width && a == o.a && b == o.b && c == o.c &&
+               imm0 == o.imm0 && imm1 == o.imm1;
+    }
+};
+struct KeyHash {
+    size_t operator()(const Key& k) const {
+        uint64_t h = 0x9E3779B97F4A7C15ull * (k.op + 1);
+        const uint32_t v[6] = {k.width, k.a, k.b, k.c, k.imm0, k.imm1};
+        for (uint32_t x : v) h = (h ^ x) * 0xFF51AFD7ED558CCDull + (h >> 29);
+        return (size_t)h;
+    }
+};
+Key key_of(const mh_node& x) { return Key{x.op, x.width, x.a, x.b, x.c, x.imm0, x.imm1}; }
+
+// a node -> value map valid for one epoch (reset in O(1) between queries)
+struct Stamped {
+    std::vector<uint32_t> stamp, val;
+    uint32_t epoch = 1;
+    void reset(size_t n) {
+        if (++epoch == 0) {
+            std::fill(stamp.begin(), stamp.end(), 0u);
+            epoch = 1;
+        }
+        if (stamp.size() < n) {
+            stamp.resize(n, 0u);
+            val.resize(n);
+        }
+    }
+    bool has(size_t i) const { return i < stamp.size() && stamp[i] == epoch; }
+    uint32_t get(size_t i) const { return val[i]; }
+    void set(size_t i, uint32_t v) {
+        if (i >= stamp.size()) {
+            const size_t n = std::max(i + 1, 2 * stamp.size());
+            stamp.resize(n, 0u);
+            val.resize(n);
+        }
+        stamp[i] = epoch;
+        val[i] = v;
+    }
+};
+
+}  // namespace
+
+struct mh_terms {
+    std::vector<mh_node> nodes;
+    std::unordered_map<Key, uint32_t, KeyHash> memo;  // TapeBuilder._memo
+    std::vector<Big> pool;
+    std::unordered_map<Big, uint32_t, BigHash> pool_index;
+    std::vector<std::string> var_names, array_names, fn_names;
+    // const_value of the mirrored nodes (immutable): 0 unknown, 1 none, k + 2 = cv_vals[k]
+    std::vector<uint32_t> cv_state;
+    std::vector<Big> cv_vals;
+    Stamped memo_lower, seen, local;  // per-query scratch
+};
+
+namespace {
+
+struct Column {
+    std::string name, symbol;
+    uint32_t width, kind;
+    bool has_key;
+    Big key;
+};
+
+struct KeccakMap {
+    Big bound, base;
+    bool has_bound = false;
+    std::vector<std::pair<Big, Big>> pairs;  // (argument, hash); a later statement of a key wins
+    void put(const Big& arg, const Big& h) {
+        for (auto& p : pairs)
+            if (p.first == arg) {
+                p.second = h;
+                return;
+            }
+        pairs.emplace_back(arg, h);
+    }
+};
+
+using Tables = std::vector<std::pair<std::string, std::vector<Big>>>;
+
+class Query {
+public:
+    explicit Query(mh_terms& t) : T(t), n_mirror((uint32_t)t.nodes.size()) {
+        T.memo_lower.reset(n_mirror);
+        T.seen.reset(n_mirror);
+        if (T.cv_state.size() < n_mirror) T.cv_state.resize(n_mirror, 0u);
+    }
+
+    // ---- nodes: mirrored ids [0, n_mirror), the query's own above -----------------------------
+    const mh_node& nd(uint32_t n) const { return n < n_mirror ? T.nodes[n] : ov[n - n_mirror]; }
+    uint32_t width(uint32_t n) const { return nd(n).width; }
+
+    uint32_t add(uint8_t op, uint32_t w, uint32_t a = 0, uint32_t b = 0, uint32_t c = 0,
+                 uint32_t i0 = 0, uint32_t i1 = 0) {
+        const Key k{op, w, a, b, c, i0, i1};
+        auto m = T.memo.find(k);  // hash-consed against the host's nodes first
+        if (m != T.memo.end()) return m->second;
+        auto it = ov_memo.find(k);
+        if (it != ov_memo.end()) return it->second;
+        mh_node x{};
+        x.op = op;
+        x.width = (uint16_t)w;
+        x.a = a;
+        x.b = b;
+        x.c = c;
+        x.imm0 = i0;
+        x.imm1 = i1;
+        ov.push_back(x);
+        const uint32_t id = n_mirror + (uint32_t)ov.size() - 1;
+        ov_memo.emplace(k, id);
+        return id;
+    }
+    uint32_t konst(const Big& v, uint32_t w) {  // TapeBuilder.const
+        if (w > 256) {
+            const uint32_t lo = konst(v.masked(256), 256);
+            const uint32_t hi = konst(v.shr(256), w - 256);
+            return add(CONCAT, w, hi, lo);
+        }
+        const Big m = v.masked(w);
+        auto p = T.pool_index.find(m);
+        if (p != T.pool_index.end()) return add(CONST, w, 0, 0, 0, p->second);
+        auto it = ov_index.find(m);
+        if (it == ov_index.end()) {
+            it = ov_index.emplace(m, (uint32_t)ov_vals.size()).first;
+            ov_vals.push_back(m);
+        }
+        return add(CONST, w, 0, 0, 0, OV_CONST | it->second);
+    }
+    const Big& const_of(uint32_t n) const {  // a CONST node's value
+        const uint32_t i0 = nd(n).imm0;
+        return n >= n_mirror && (i0 & OV_CONST) ? ov_vals[i0 & ~OV_CONST] : T.pool.at(i0);
+    }
+
+    // TapeBuilder.const_value: CONST / TRUE / FALSE and CONCAT / EXTRACT / ZEXT / SEXT over them
+    const Big* const_value(uint32_t n) {
+        if (n < n_mirror) {
+            const uint32_t s = T.cv_state[n];
+            if (s) return s == 1 ? nullptr : &T.cv_vals[s - 2];
+        } else {
+            auto it = ov_cv.find(n);
+            if (it != ov_cv.end()) return it->second < 0 ? nullptr : &ov_cv_vals[(size_t)it->second];
+        }
+        const mh_node x = nd(n);
+        bool ok = false;
+        Big v;
+        if (x.op == CONST) {
+            ok = true;
+            v = const_of(n);
+        } else if (x.op == TRUE_) {
+            ok = true;
+            v.w[0] = 1;
+        } else if (x.op == FALSE_) {
+            ok = true;
+        } else if (x.op == CONCAT) {
+            if (const Big* hi = const_value(x.a)) {
+                const Big h = *hi;
+                if (const Big* lo = const_value(x.b)) {
+                    ok = true;
+                    v = h.shl(width(x.b)) | *lo;
+                }
+            }
+        } else if (x.op == EXTRACT || x.op == ZEXT || x.op == SEXT) {
+            if (const Big* a = const_value(x.a)) {
+                ok = true;
+                if (x.op == EXTRACT) {
+                    v = a->shr(x.imm1).masked(x.imm0 - x.imm1 + 1);
+                } else if (x.op == SEXT && a->bit(width(x.a) - 1)) {
+                    Big ones;
+                    for (uint32_t i = 0; i < x.imm0; ++i) ones.w[i / 32] |= 1u << (i % 32);
+                    v = *a | ones.shl(width(x.a));
+                } else {
+                    v = *a;
+                }
+            }
+        }
+        // std::deque-like stability is not needed: callers copy before the next const_value
+        if (n < n_mirror) {
+            if (!ok) {
+                T.cv_state[n] = 1;
+                return nullptr;
+            }
+            T.cv_vals.push_back(v);
+            T.cv_state[n] = (uint32_t)T.cv_vals.size() + 1;
+            return &T.cv_vals.back();
+        }
+        if (!ok) {
+            ov_cv[n] = -1;
+            return nullptr;
+        }
+        ov_cv_vals.push_back(v);
+        ov_cv[n] = (int64_t)ov_cv_vals.size() - 1;
+        return &ov_cv_vals.back();
+    }
+
+    // ---- pass 1: lower.py Lowering.collect + apply_harvest -----------------------------------
+    const std::string& array_name(uint32_t n) const { return T.array_names.at(nd(n).imm0); }
+    const std::string& fn_name(uint32_t n) const { return T.fn_names.at(nd(n).imm0); }
+    static bool inverse(const std::string& f) {
+        return f.size() >= 2 && f.compare(f.size() - 2, 2, "-1") == 0;
+    }
+    static bool keccak_fn(const std::string& f) { return f.rfind("keccak256_", 0) == 0 && !inverse(f); }
+
+    int64_t array_base(uint32_t arr) const {  // the ARRAY under a store chain, -1 for K(...)
+        for (;;) {
+            const uint8_t op = nd(arr).op;
+            if (op == STORE) arr = nd(arr).a;
+            else if (op == ARRAY) return arr;
+            else if (op == CONST_ARRAY) return -1;
+            else unsupported("array term is not a store chain");
+        }
+    }
+    static std::vector<Big>& keys_of(Tables& tabs, std::unordered_map<std::string, size_t>& idx,
+                                     const std::string& n) {
+        auto it = idx.find(n);
+        if (it == idx.end()) {
+            it = idx.emplace(n, tabs.size()).first;
+            tabs.emplace_back(n, std::vector<Big>());
+        }
+        return tabs[it->second].second;
+    }
+    KeccakMap& keccak_map(const std::string& f) {
+        auto it = kidx.find(f);
+        if (it == kidx.end()) {
+            it = kidx.emplace(f, keccak.size()).first;
+            keccak.emplace_back(f, KeccakMap());
+        }
+        return keccak[it->second].second;
+    }
+
+    void harvest(const std::vector<uint32_t>& roots) {
+        // children before parents, host-only nodes and their parents only (lower.py _walk)
+        std::vector<int64_t> st;
+        for (uint32_t r : roots)
+            if (nd(r).flags & F_HOST) st.push_back(r);
+        while (!st.empty()) {
+            const int64_t s = st.back();
+            st.pop_back();
+            if (s < 0) {
+                collect((uint32_t)~s);
+                continue;
+            }
+            if (T.seen.has((size_t)s)) continue;
+            T.seen.set((size_t)s, 1);
+            st.push_back(~s);
+            const mh_node& x = nd((uint32_t)s);
+            const uint32_t kids[3] = {x.a, x.b, x.c};
+            for (int j = arity(x.op) - 1; j >= 0; --j)
+                if (!T.seen.has(kids[j]) && (nd(kids[j]).flags & F_HOST)) st.push_back(kids[j]);
+        }
+        for (Tables* tabs : {&cells, &uf_cells})
+            for (auto& kv : *tabs) {
+                std::sort(kv.second.begin(), kv.second.end());
+                kv.second.erase(std::unique(kv.second.begin(), kv.second.end()), kv.second.end());
+            }
+        for (auto& kv : keccak) {
+            KeccakMap& km = kv.second;
+            km.base = km.has_bound ? km.bound.plus(63) : Big();
+            km.base.w[0] &= ~63u;
+            km.base = km.base.masked(256);
+        }
+    }
+    void collect(uint32_t n) {
+        const mh_node x = nd(n);
+        if (x.op == SELECT) {
+            const int64_t base = array_base(x.a);
+            if (base >= 0) {
+                auto& keys = keys_of(cells, cell_of, array_name((uint32_t)base));
+                if (const Big* k = const_value(x.b)) keys.push_back(*k);
+            }
+        } else if (x.op == UF) {
+            const std::string& f = fn_name(n);
+            if (keccak_fn(f)) {
+                keccak_map(f);
+            } else if (!inverse(f)) {
+                auto& keys = keys_of(uf_cells, uf_of, f);
+                if (const Big* k = const_value(x.a)) keys.push_back(*k);
+            }
+        } else if (x.op == EQ || (x.op >= BVULT && x.op <= BVSGE)) {
+            const uint32_t sides[2][2] = {{x.a, x.b}, {x.b, x.a}};
+            for (const auto& s : sides) {
+                const mh_node& app = nd(s[0]);
+                if (app.op != UF || !keccak_fn(fn_name(s[0]))) continue;
+                const Big* kv = const_value(s[1]);
+                if (!kv) continue;
+                const Big hv = *kv;
+                KeccakMap& km = keccak_map(fn_name(s[0]));
+                if (x.op == EQ) {
+                    if (const Big* arg = const_value(app.a)) km.put(*arg, hv);
+                } else if (!km.has_bound || hv < km.bound) {
+                    km.bound = hv;
+                    km.has_bound = true;
+                }
+            }
+        }
+    }
+
+    // ---- pass 2: lower.py Lowering.lower / _rewrite -------------------------------------------
+    uint32_t cell_column(const std::string& name, uint32_t w, uint32_t kind,
+                         const std::string& sym, const Big* key) {
+        auto it = cell_index.find(name);
+        if (it == cell_index.end()) {
+            it = cell_index.emplace(name, (uint32_t)ccols.size()).first;
+            ccols.push_back(Column{name, sym, w, kind, key != nullptr, key ? *key : Big()});
+        }
+        return add(VAR, w, 0, 0, 0, CELL_COL | it->second);
+    }
+
+    void deps(uint32_t n, std::vector<uint32_t>& d) {  // Lowering._deps
+        d.clear();
+        const mh_node& x = nd(n);
+        if (x.op == SELECT) {
+            d.push_back(x.b);
+            uint32_t arr = x.a;
+            while (nd(arr).op == STORE) {
+                d.push_back(nd(arr).b);
+                d.push_back(nd(arr).c);
+                arr = nd(arr).a;
+            }
+            if (nd(arr).op == CONST_ARRAY) d.push_back(nd(arr).a);
+            else if (nd(arr).op != ARRAY) unsupported("array term is not a store chain");
+            return;
+        }
+        if (x.op == UF) {
+            const std::string& f = fn_name(n);
+            if (inverse(f)) {
+                const mh_node& in = nd(x.a);
+                const std::string fwd = f.substr(0, f.size() - 2);
+                if (in.op != UF || T.fn_names.at(in.imm0) != fwd)
+                    unsupported(f + " applied to something other than " + fwd + "(...)");
+                d.push_back(in.a);
+            } else {
+                d.push_back(x.a);
+            }
+            return;
+        }
+        if (x.flags & F_ARRAY) unsupported("array-sorted term used as a value");
+        const uint32_t kids[3] = {x.a, x.b, x.c};
+        for (int j = 0; j < arity(x.op); ++j) {
+            if (nd(kids[j]).flags & F_ARRAY) unsupported("operator over arrays");
+            d.push_back(kids[j]);
+        }
+    }
+
+    uint32_t low(uint32_t n) const {  // the lowered form of an operand
+        return T.memo_lower.has(n) ? T.memo_lower.get(n) : n;
+    }
+    uint32_t lower(uint32_t root) {
+        if (!(nd(root).flags & F_HOST)) return root;  // reads no host-only term: itself
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        std::vector<uint32_t> d;
+        while (!st.empty()) {
+            const auto [n, expanded] = st.back();
+            st.pop_back();
+            if (T.memo_lower.has(n)) continue;
+            if (!expanded) {
+                st.push_back({n, true});
+                deps(n, d);
+                for (uint32_t x : d)
+                    if ((nd(x).flags & F_HOST) && !T.memo_lower.has(x)) st.push_back({x, false});
+                continue;
+            }
+            T.memo_lower.set(n, rewrite(n));
+        }
+        return T.memo_lower.get(root);
+    }
+
+    uint32_t rewrite(uint32_t n) {
+        const mh_node x = nd(n);
+        if (x.op == SELECT) return select(x.a, low(x.b));
+        if (x.op == UF) return apply(n);
+        const int k = arity(x.op);
+        if (k == 0) return n;
+        const uint32_t kids[3] = {x.a, x.b, x.c};
+        uint32_t args[3] = {0, 0, 0};
+        bool same = true;
+        for (int j = 0; j < k; ++j) {
+            args[j] = low(kids[j]);
+            same = same && args[j] == kids[j];
+        }
+        if (x.op == EQ && width(args[0]) > 256) return eq(args[0], args[1]);
+        if (same) return n;
+        return add(x.op, x.width, args[0], args[1], args[2], x.imm0, x.imm1);
+    }
+
+    uint32_t eq(uint32_t x, uint32_t y) {  // Lowering.eq
+        const uint32_t w = width(x);
+        if (w <= 256) return add(EQ, 0, x, y);
+        struct Seg {
+            uint32_t lo, hi, p;
+        };
+        std::vector<Seg> sides[2];
+        std::vector<uint32_t> cuts{w};
+        const uint32_t ts[2] = {x, y};
+        for (int s = 0; s < 2; ++s) {
+            uint32_t pos = w;
+            for (uint32_t p : pieces(ts[s])) {
+                const uint32_t pw = width(p);
+                sides[s].push_back({pos - pw, pos, p});
+                cuts.push_back(pos - pw);
+                pos -= pw;
+            }
+        }
+        std::sort(cuts.begin(), cuts.end());
+        cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+        int64_t acc = -1;
+        for (size_t i = 0; i + 1 < cuts.size(); ++i) {
+            const uint32_t lo = cuts[i], hi = cuts[i + 1];
+            uint32_t parts[2] = {0, 0};
+            for (int s = 0; s < 2; ++s)
+                for (const Seg& g : sides[s])
+                    if (g.lo <= lo && hi <= g.hi) {
+                        parts[s] = slice(g.p, hi - g.lo, lo - g.lo);
+                        break;
+                    }
+            const uint32_t e = add(EQ, 0, parts[0], parts[1]);
+            acc = acc < 0 ? e : add(AND, 0, (uint32_t)acc, e);
+        }
+        return (uint32_t)acc;
+    }
+    std::vector<uint32_t> pieces(uint32_t n) {  // Lowering._pieces: CONCAT leaves, high first
+        std::vector<uint32_t> out, st{n};
+        while (!st.empty()) {
+            const uint32_t x = st.back();
+            st.pop_back();
+            const mh_node v = nd(x);
+            if (v.op == CONCAT) {
+                st.push_back(v.b);
+                st.push_back(v.a);
+            } else if (v.op == ZEXT) {
+                st.push_back(v.a);
+                st.push_back(konst(Big(), v.imm0));
+            } else if (v.width > 256 && !const_value(x)) {
+                unsupported(std::to_string(v.width) + "-bit operand of a wide equality");
+            } else {
+                out.push_back(x);
+            }
+        }
+        return out;
+    }
+    uint32_t slice(uint32_t piece, uint32_t hi, uint32_t lo) {  // bits [lo, hi) (Lowering._slice)
+        if (lo == 0 && hi == width(piece)) return piece;
+        if (const Big* c = const_value(piece)) {
+            const Big v = c->shr(lo);
+            return konst(v, hi - lo);
+        }
+        return add(EXTRACT, hi - lo, piece, 0, 0, hi - 1, lo);
+    }
+
+    uint32_t select(uint32_t arr, uint32_t idx) {  // Lowering._select
+        const mh_node a = nd(arr);
+        if (a.op == STORE) {
+            const uint32_t key = low(a.b), val = low(a.c);
+            const uint32_t rest = select(a.a, idx);
+            return add(ITE, width(val), eq(idx, key), val, rest);
+        }
+        if (a.op == CONST_ARRAY) return low(a.a);
+        const std::string& name = array_name(arr);
+        auto it = cell_of.find(name);
+        return table(name, a.width, idx, it == cell_of.end() ? nullptr : &cells[it->second].second,
+                     MH_COL_CELL, MH_COL_ELSE);
+    }
+    uint32_t table(const std::string& name, uint32_t rng, uint32_t idx,
+                   const std::vector<Big>* keys, uint32_t kcell, uint32_t kelse) {  // _table
+        const Big* kp = const_value(idx);
+        const Big key = kp ? *kp : Big();
+        if (kp && keys && std::binary_search(keys->begin(), keys->end(), key))
+            return cell_column(name + "[" + key.hex() + "]", rng, kcell, name, &key);
+        uint32_t acc = cell_column(name + "[*]", rng, kelse, name, nullptr);
+        if (kp || !keys) return acc;  // a constant key outside the table reads the else value
+        for (size_t i = keys->size(); i-- > 0;) {
+            const Big k = (*keys)[i];
+            const uint32_t cell = cell_column(name + "[" + k.hex() + "]", rng, kcell, name, &k);
+            const uint32_t kn = konst(k, width(idx));
+            acc = add(ITE, rng, eq(idx, kn), cell, acc);
+        }
+        return acc;
+    }
+    uint32_t apply(uint32_t n) {  // Lowering._apply
+        const mh_node x = nd(n);
+        const std::string& f = fn_name(n);
+        if (inverse(f)) return low(nd(x.a).a);
+        const uint32_t a = low(x.a);
+        if (keccak_fn(f)) {
+            auto it = kidx.find(f);
+            if (it == kidx.end()) unsupported("keccak function " + f + " not harvested");
+            const KeccakMap km = keccak[it->second].second;
+            Big s1, s2;
+            s1.w[0] = KECCAK_SHIFT;
+            s2.w[0] = KECCAK_ALIGN;
+            uint32_t h = add(KECCAK, 256, a);
+            h = add(BVLSHR, 256, h, konst(s1, 256));
+            h = add(BVSHL, 256, h, konst(s2, 256));
+            uint32_t acc = km.base.zero() ? h : add(BVADD, 256, h, konst(km.base, 256));
+            if (x.width != 256)
+                unsupported("keccak function " + f + " has range " + std::to_string(x.width));
+            std::vector<std::pair<Big, Big>> pairs = km.pairs;
+            std::sort(pairs.begin(), pairs.end(),
+                      [](const std::pair<Big, Big>& p, const std::pair<Big, Big>& q) {
+                          return q.first < p.first;
+                      });
+            for (const auto& pr : pairs) {
+                const uint32_t c = eq(a, konst(pr.first, width(a)));
+                acc = add(ITE, 256, c, konst(pr.second, 256), acc);
+            }
+            return acc;
+        }
+        auto it = uf_of.find(f);
+        return table(f, x.width, a, it == uf_of.end() ? nullptr : &uf_cells[it->second].second,
+                     MH_COL_UFCELL, MH_COL_UFELSE);
+    }
+
+    // ---- the root tape (sieve.py local_tapeset): VAR imm0 = query column, CONST imm0 = query
+    // constant; has_col = the node reads a column ----------------------------------------------
+    void linearise(uint32_t root) {
+        T.local.reset(n_mirror + ov.size());
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        while (!st.empty()) {
+            const auto [n, done] = st.back();
+            st.pop_back();
+            if (T.local.has(n)) continue;
+            const mh_node& x = nd(n);
+            const int k = arity(x.op);
+            const uint32_t kids[3] = {x.a, x.b, x.c};
+            if (!done) {
+                st.push_back({n, true});
+                for (int j = k - 1; j >= 0; --j)
+                    if (!T.local.has(kids[j])) st.push_back({kids[j], false});
+                continue;
+            }
+            if (x.op >= ARRAY || (x.flags & F_ARRAY)) invalid("a host-only term survived lowering");
+            mh_node y = x;
+            y.flags = 0;
+            uint8_t hc = 0;
+            uint32_t* opnd[3] = {&y.a, &y.b, &y.c};
+            for (int j = 0; j < 3; ++j) {
+                *opnd[j] = j < k ? T.local.get(kids[j]) : 0;
+                if (j < k) hc |= has_col[*opnd[j]];
+            }
+            if (x.op == VAR) {
+                y.imm0 = column_of(n);
+                hc = 1;
+            } else if (x.op == CONST) {
+                y.imm0 = const_index(n);
+            }
+            T.local.set(n, (uint32_t)tape.size());
+            tape.push_back(y);
+            has_col.push_back(hc);
+        }
+    }
+    uint32_t column_of(uint32_t n) {  // a VAR node's query column (numbered by first use)
+        const mh_node& x = nd(n);
+        const bool cell = n >= n_mirror && (x.imm0 & CELL_COL);
+        auto& m = cell ? cell_cols : var_cols;
+        const uint32_t k = cell ? x.imm0 & ~CELL_COL : x.imm0;
+        auto it = m.find(k);
+        if (it != m.end()) return it->second;
+        const uint32_t q = (uint32_t)cols.size();
+        if (cell) {
+            cols.push_back(ccols.at(k));
+        } else {
+            const std::string& name = T.var_names.at(k);
+            cols.push_back(Column{name, name, x.width, MH_COL_VAR, false, Big()});
+        }
+        m.emplace(k, q);
+        return q;
+    }
+    uint32_t const_index(uint32_t n) {
+        const uint32_t i0 = nd(n).imm0;
+        auto& m = n >= n_mirror && (i0 & OV_CONST) ? own_consts : pool_consts;
+        auto it = m.find(i0);
+        if (it != m.end()) return it->second;
+        const uint32_t q = (uint32_t)qpool.size();
+        qpool.push_back(const_of(n));
+        m.emplace(i0, q);
+        return q;
+    }
+
+    mh_terms& T;
+    const uint32_t n_mirror;
+    std::vector<mh_node> ov;  // nodes the query made
+    std::unordered_map<Key, uint32_t, KeyHash> ov_memo;
+    std::vector<Big> ov_vals;  // constants outside the host's pool
+    std::unordered_map<Big, uint32_t, BigHash> ov_index;
+    std::unordered_map<uint32_t, int64_t> ov_cv;
+    std::vector<Big> ov_cv_vals;
+    // the harvest (Schema.cells / uf_cells / keccak), in first-seen order
+    Tables cells, uf_cells;
+    std::unordered_map<std::string, size_t> cell_of, uf_of, kidx;
+    std::vector<std::pair<std::string, KeccakMap>> keccak;
+    std::vector<Column> ccols;  // every cell / else column lowering made
+    std::unordered_map<std::string, uint32_t> cell_index;
+    // the root tape
+    std::vector<mh_node> tape;
+    std::vector<uint8_t> has_col;
+    std::vector<Column> cols;  // query columns, in first-use order
+    std::unordered_map<uint32_t, uint32_t> var_cols, cell_cols, pool_consts, own_consts;
+    std::vector<Big> qpool;
+};
+
+}  // namespace
+
+struct mh_query {
+    std::vector<mh_node> nodes;
+    std::vector<uint64_t> tape_off;
+    std::vector<uint32_t> consts;
+    std::vector<mh_query_column> columns;
+    std::string names;
+    std::vector<uint32_t> key_limbs, group_cols, group_off, table_limbs;
+    std::vector<mh_query_table> tables;
+};
+
+namespace {
+
+void put_big(std::vector<uint32_t>& v, const Big& b) { v.insert(v.end(), b.w, b.w + 8); }
+void put_key(std::vector<uint32_t>& v, const Big& b) { v.insert(v.end(), b.w, b.w + NL); }
+uint32_t put_name(std::string& s, const std::string& n) {
+    const uint32_t off = (uint32_t)s.size();
+    s += n;
+    return off;
+}
+
+// sieve.py _may_define, narrowed to what eliminate_definitions can use: a plain variable on one
+// side, a computed term that reads columns on the other
+bool may_define(const std::vector<mh_node>& tape, const std::vector<uint8_t>& has_col,
+                const std::vector<Column>& cols, uint32_t cj) {
+    const mh_node& x = tape[cj];
+    if (x.op != EQ) return false;
+    const uint32_t s[2][2] = {{x.a, x.b}, {x.b, x.a}};
+    for (const auto& p : s) {
+        const mh_node& v = tape[p[0]];
+        const uint8_t t = tape[p[1]].op;
+        if (v.op == VAR && cols[v.imm0].kind == MH_COL_VAR && t != VAR && t != CONST && has_col[p[1]])
+            return true;
+    }
+    return false;
+}
+
+void build(Query& Q, const uint32_t* roots, uint32_t n_roots, mh_query& q, uint32_t& flags) {
+    const std::vector<uint32_t> rs(roots, roots + n_roots);
+    Q.harvest(rs);
+    uint32_t root = 0;
+    for (uint32_t i = 0; i < n_roots; ++i) {  // lower_query: the AND of the lowered roots
+        const uint32_t x = Q.lower(rs[i]);
+        if (Q.width(x) != 0 || (Q.nd(x).flags & F_ARRAY)) invalid("constraints must be Bool");
+        root = i == 0 ? x : Q.add(AND, 0, root, x);
+    }
+    if (!n_roots) root = Q.add(TRUE_, 0);
+    Q.linearise(root);
+    const std::vector<mh_node>& tape = Q.tape;
+    const uint32_t N = (uint32_t)tape.size();
+    for (const Column& c : Q.cols)  // a variable named like a cell would make two columns one
+        if (c.kind == MH_COL_VAR && Q.cell_index.count(c.name))
+            unsupported("variable " + c.name + " is named like an array cell");
+    // conjuncts: the AND leaves of the root, left to right (Sieve.conjuncts)
+    std::vector<uint32_t> conj, st{N - 1};
+    while (!st.empty()) {
+        const uint32_t n = st.back();
+        st.pop_back();
+        if (tape[n].op == AND) {
+            st.push_back(tape[n].b);
+            st.push_back(tape[n].a);
+        } else {
+            conj.push_back(n);
+        }
+    }
+    for (uint32_t cj : conj)
+        if (may_define(tape, Q.has_col, Q.cols, cj)) flags |= MH_QUERY_DEFINITIONS;
+    // column-disjoint groups: conjuncts that reach a common node reading columns share a group
+    std::vector<int32_t> owner(N, -1);
+    std::vector<uint32_t> uf(conj.size());
+    for (uint32_t i = 0; i < uf.size(); ++i) uf[i] = i;
+    auto find = [&](uint32_t x) {
+        while (uf[x] != x) x = uf[x] = uf[uf[x]];
+        return x;
+    };
+    for (uint32_t i = 0; i < conj.size(); ++i) {
+        st.assign(1, conj[i]);
+        while (!st.empty()) {
+            const uint32_t n = st.back();
+            st.pop_back();
+            if (!Q.has_col[n]) continue;
+            if (owner[n] >= 0) {
+                const uint32_t a = find(i), b = find((uint32_t)owner[n]);
+                uf[std::max(a, b)] = std::min(a, b);  // the earlier conjunct stays the root
+                continue;
+            }
+            owner[n] = (int32_t)i;
+            const mh_node& x = tape[n];
+            const uint32_t kids[3] = {x.a, x.b, x.c};
+            for (int j = 0; j < arity(x.op); ++j) st.push_back(kids[j]);
+        }
+    }
+    std::vector<std::vector<uint32_t>> gconj;  // conjunct tape nodes per group, path order
+    std::unordered_map<int64_t, uint32_t> gid;
+    std::vector<uint32_t> group_of(conj.size(), UINT32_MAX);  // by union-find root
+    for (uint32_t i = 0; i < conj.size(); ++i) {
+        const int64_t key = Q.has_col[conj[i]] ? (int64_t)find(i) : -(int64_t)conj[i] - 1;
+        auto it = gid.find(key);
+        if (it == gid.end()) {
+            it = gid.emplace(key, (uint32_t)gconj.size()).first;
+            gconj.emplace_back();
+        }
+        gconj[it->second].push_back(conj[i]);
+        if (key >= 0) group_of[(size_t)key] = it->second;
+    }
+    const uint32_t G = (uint32_t)gconj.size();
+    std::vector<std::vector<uint32_t>> gcols(G);
+    for (uint32_t n = 0; n < N; ++n)
+        if (tape[n].op == VAR && owner[n] >= 0)
+            gcols[group_of[find((uint32_t)owner[n])]].push_back(tape[n].imm0);
+    // tapes: the root's, then (more than one group) each group's AND chain over the root's nodes
+    q.nodes = tape;
+    q.tape_off = {0, N};
+    if (G > 1) {
+        std::vector<int32_t> remap(N, -1);
+        std::vector<uint32_t> touched;
+        std::vector<std::pair<uint32_t, bool>> s2;
+        for (uint32_t g = 0; g < G; ++g) {
+            const size_t base = q.nodes.size();
+            for (uint32_t n : touched) remap[n] = -1;
+            touched.clear();
+            int64_t acc = -1;
+            for (uint32_t cj : gconj[g]) {
+                s2.assign(1, {cj, false});
+                while (!s2.empty()) {
+                    const auto [n, done] = s2.back();
+                    s2.pop_back();
+                    if (remap[n] >= 0) continue;
+                    const mh_node& x = tape[n];
+                    const int k = arity(x.op);
+                    const uint32_t kids[3] = {x.a, x.b, x.c};
+                    if (!done) {
+                        s2.push_back({n, true});
+                        for (int j = k - 1; j >= 0; --j)
+                            if (remap[kids[j]] < 0) s2.push_back({kids[j], false});
+                        continue;
+                    }
+                    mh_node y = x;
+                    y.a = k > 0 ? (uint32_t)remap[x.a] : 0;
+                    y.b = k > 1 ? (uint32_t)remap[x.b] : 0;
+                    y.c = k > 2 ? (uint32_t)remap[x.c] : 0;
+                    remap[n] = (int32_t)(q.nodes.size() - base);
+                    touched.push_back(n);
+                    q.nodes.push_back(y);
+                }
+                if (acc < 0) {
+                    acc = remap[cj];
+                    continue;
+                }
+                mh_node a{};
+                a.op = AND;
+                a.a = (uint32_t)acc;
+                a.b = (uint32_t)remap[cj];
+                acc = (int64_t)(q.nodes.size() - base);
+                q.nodes.push_back(a);
+            }
+            if ((size_t)acc != q.nodes.size() - base - 1) invalid("group tape root is not its last node");
+            q.tape_off.push_back(q.nodes.size());
+        }
+    }
+    for (const Big& v : Q.qpool) put_big(q.consts, v);
+    if (Q.qpool.empty()) put_big(q.consts, Big());
+    // columns; a ground query reads one Bool column (Sieve.solve's "__ground__")
+    std::vector<Column> cols = Q.cols;
+    if (cols.empty()) cols.push_back(Column{"__ground__", "__ground__", 1, MH_COL_VAR, false, Big()});
+    for (const Column& c : cols) {
+        mh_query_column mc{};
+        mc.name_off = put_name(q.names, c.name);
+        mc.name_len = (uint32_t)c.name.size();
+        mc.symbol_off = put_name(q.names, c.symbol);
+        mc.symbol_len = (uint32_t)c.symbol.size();
+        mc.width = c.width;
+        mc.kind = c.kind;
+        mc.key_off = c.has_key ? (uint32_t)(q.key_limbs.size() / NL) : UINT32_MAX;
+        if (c.has_key) put_key(q.key_limbs, c.key);
+        q.columns.push_back(mc);
+    }
+    q.group_off.push_back(0);
+    for (auto& gc : gcols) {
+        std::sort(gc.begin(), gc.end());
+        gc.erase(std::unique(gc.begin(), gc.end()), gc.end());
+        q.group_cols.insert(q.group_cols.end(), gc.begin(), gc.end());
+        q.group_off.push_back((uint32_t)q.group_cols.size());
+    }
+    // the schema's tables: every harvested key (read or not), keccak bases and pairs
+    for (int t = 0; t < 2; ++t)
+        for (const auto& kv : t == 0 ? Q.cells : Q.uf_cells) {
+            mh_query_table tb{};
+            tb.kind = t == 0 ? MH_TABLE_CELLS : MH_TABLE_UF_CELLS;
+            tb.name_off = put_name(q.names, kv.first);
+            tb.name_len = (uint32_t)kv.first.size();
+            tb.limb_off = (uint32_t)(q.table_limbs.size() / NL);
+            tb.n_items = (uint32_t)kv.second.size();
+            for (const Big& k : kv.second) put_key(q.table_limbs, k);
+            q.tables.push_back(tb);
+        }
+    for (const auto& kv : Q.keccak) {
+        mh_query_table tb{};
+        tb.kind = MH_TABLE_KECCAK;
+        tb.name_off = put_name(q.names, kv.first);
+        tb.name_len = (uint32_t)kv.first.size();
+        tb.limb_off = (uint32_t)(q.table_limbs.size() / NL);
+        tb.n_items = (uint32_t)kv.second.pairs.size();
+        put_key(q.table_limbs, kv.second.base);  // then (argument, hash) pairs
+        for (const auto& pr : kv.second.pairs) {
+            put_key(q.table_limbs, pr.first);
+            put_key(q.table_limbs, pr.second);
+        }
+        q.tables.push_back(tb);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mh_terms_create(mh_terms** out) {
+    if (!out) return mh_detail_set_err(MH_E_INVALID, "null out");
+    *out = new (std::nothrow) mh_terms();
+    return *out ? MH_OK : mh_detail_set_err(MH_E_NOMEM, "mh_terms_create");
+}
+
+int32_t mh_terms_destroy(mh_terms* t) {
+    if (!t) return mh_detail_set_err(MH_E_INVALID, "null terms");
+    delete t;
+    return MH_OK;
+}
+
+int32_t mh_terms_append(mh_terms* t, const mh_node* nodes, uint64_t n_nodes,
+                        const uint32_t* consts, uint64_t n_consts, const char* var_names,
+                        uint64_t n_vars, const char* array_names, uint64_t n_arrays,
+                        const char* fn_names, uint64_t n_fns) {
+    if (!t || (n_nodes && !nodes) || (n_consts && !consts) || (n_vars && !var_names) ||
+        (n_arrays && !array_names) || (n_fns && !fn_names))
+        return mh_detail_set_err(MH_E_INVALID, "null argument");
+    try {
+        for (uint64_t i = 0; i < n_consts; ++i) {
+            Big v;
+            memcpy(v.w, consts + 8 * i, 32);
+            t->pool_index.emplace(v, (uint32_t)t->pool.size());
+            t->pool.push_back(v);
+        }
+        const size_t n0 = t->nodes.size();
+        for (uint64_t i = 0; i < n_nodes; ++i) {
+            const mh_node& x = nodes[i];
+            const uint32_t id = (uint32_t)(n0 + i);
+            const int k = arity(x.op);
+            if ((k > 0 && x.a >= id) || (k > 1 && x.b >= id) || (k > 2 && x.c >= id) ||
+                (x.op == CONST && x.imm0 >= t->pool.size())) {
+                for (size_t j = n0; j < t->nodes.size(); ++j) t->memo.erase(key_of(t->nodes[j]));
+                t->nodes.resize(n0);
+                return mh_detail_set_err(MH_E_INVALID, "node operand outside the term store");
+            }
+            t->nodes.push_back(x);
+            t->memo.emplace(key_of(x), id);
+        }
+        auto names = [](const char* p, uint64_t n, std::vector<std::string>& out) {
+            for (uint64_t i = 0; i < n; ++i) {  // NUL-terminated, back to back
+                const size_t len = strlen(p);
+                out.emplace_back(p, len);
+                p += len + 1;
+            }
+        };
+        names(var_names, n_vars, t->var_names);
+        names(array_names, n_arrays, t->array_names);
+        names(fn_names, n_fns, t->fn_names);
+    } catch (const std::bad_alloc&) {
+        return mh_detail_set_err(MH_E_NOMEM, "mh_terms_append");
+    }
+    return MH_OK;
+}
+
+int32_t mh_terms_sizes(const mh_terms* t, uint64_t* out /* [5] */) {
+    if (!t || !out) return mh_detail_set_err(MH_E_INVALID, "null argument");
+    out[0] = t->nodes.size();
+    out[1] = t->pool.size();
+    out[2] = t->var_names.size();
+    out[3] = t->array_names.size();
+    out[4] = t->fn_names.size();
+    return MH_OK;
+}
+
+int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_query** out,
+                       mh_query_info* info) {
+    if (!t || !out || !info || (n_roots && !roots)) return mh_detail_set_err(MH_E_INVALID, "null argument");
+    *out = nullptr;
+    for (uint32_t i = 0; i < n_roots; ++i)
+        if (roots[i] >= t->nodes.size()) return mh_detail_set_err(MH_E_INVALID, "root outside the term store");
+    std::unique_ptr<mh_query> q(new (std::nothrow) mh_query());
+    if (!q) return mh_detail_set_err(MH_E_NOMEM, "mh_query_build");
+    uint32_t flags = 0;
+    try {
+        Query Q(*t);
+        build(Q, roots, n_roots, *q, flags);
+    } catch (const Fail& f) {
+        return mh_detail_set_err(f.code, f.msg.c_str());
+    } catch (const std::out_of_range&) {
+        return mh_detail_set_err(MH_E_INVALID, "malformed term store (index out of range)");
+    } catch (const std::bad_alloc&) {
+        return mh_detail_set_err(MH_E_NOMEM, "mh_query_build");
+    }
+    mh_query* r = q.release();
+    *info = mh_query_info{};
+    info->nodes = r->nodes.data();
+    info->tape_off = r->tape_off.data();
+    info->n_tapes = (uint32_t)r->tape_off.size() - 1;
+    info->consts = r->consts.data();
+    info->n_consts = (uint32_t)(r->consts.size() / 8);
+    info->columns = r->columns.data();
+    info->n_columns = (uint32_t)r->columns.size();
+    info->names = r->names.data();
+    info->names_len = (uint32_t)r->names.size();
+    info->key_limbs = r->key_limbs.data();
+    info->group_cols = r->group_cols.data();
+    info->group_off = r->group_off.data();
+    info->n_groups = (uint32_t)r->group_off.size() - 1;
+    info->tables = r->tables.data();
+    info->n_tables = (uint32_t)r->tables.size();
+    info->table_limbs = r->table_limbs.data();
+    info->flags = flags;
+    info->n_keys = (uint32_t)(r->key_limbs.size() / NL);
+    info->n_table_entries = (uint32_t)(r->table_limbs.size() / NL);
+    *out = r;
+    return MH_OK;
+}
+
+int32_t mh_query_free(mh_query* q) {
+    if (!q) return mh_detail_set_err(MH_E_INVALID, "null query");
+    delete q;
+    return MH_OK;
+}
+
+}  // extern "C"

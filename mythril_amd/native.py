@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+from itertools import chain
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -87,6 +88,13 @@ SIGNATURES = {
     "mh_smtlib_commit": (C.c_int32, [_vp, C.POINTER(C.c_int64), C.c_uint64]),
     "mh_smtlib_rollback": (C.c_int32, [_vp]),
     "mh_smtlib_size": (C.c_uint64, [_vp]),
+    "mh_terms_create": (C.c_int32, [C.POINTER(_vp)]),
+    "mh_terms_destroy": (C.c_int32, [_vp]),
+    "mh_terms_append": (C.c_int32, [_vp, _vp, C.c_uint64, _u32p, C.c_uint64, C.c_char_p,
+                                    C.c_uint64, C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64]),
+    "mh_terms_sizes": (C.c_int32, [_vp, _u64p]),
+    "mh_query_build": (C.c_int32, [_vp, _u32p, C.c_uint32, C.POINTER(_vp), _vp]),
+    "mh_query_free": (C.c_int32, [_vp]),
 }
 
 # mh_smt_record / mh_smt_result (include/mythril_hip.h)
@@ -321,6 +329,177 @@ class SmtlibSession:
                 h = b.apply(names[noff:noff + nlen], i1, w, a)
             ids[k] = h
         return ids
+
+
+# mh_query_column / mh_query_table (include/mythril_hip.h)
+QUERY_COLUMN_DTYPE = np.dtype([("name_off", "<u4"), ("name_len", "<u4"), ("symbol_off", "<u4"),
+                               ("symbol_len", "<u4"), ("width", "<u4"), ("kind", "<u4"),
+                               ("key_off", "<u4"), ("pad", "<u4")])
+QUERY_TABLE_DTYPE = np.dtype([("kind", "<u4"), ("name_off", "<u4"), ("name_len", "<u4"),
+                              ("limb_off", "<u4"), ("n_items", "<u4"), ("pad", "<u4")])
+assert QUERY_COLUMN_DTYPE.itemsize == 32 and QUERY_TABLE_DTYPE.itemsize == 24
+COLUMN_KINDS = ("var", "cell", "else", "ufcell", "ufelse")  # MH_COL_*
+TABLE_CELLS, TABLE_UF_CELLS, TABLE_KECCAK = 0, 1, 2
+QUERY_DEFINITIONS = 1
+QUERY_KEY_LIMBS = 36
+
+
+class QueryInfo(C.Structure):
+    """mh_query_info (include/mythril_hip.h)."""
+
+    _fields_ = [("nodes", _vp), ("tape_off", _u64p), ("consts", _u32p), ("columns", _vp),
+                ("names", _vp), ("key_limbs", _u32p), ("group_cols", _u32p),
+                ("group_off", _u32p), ("tables", _vp), ("table_limbs", _u32p),
+                ("n_tapes", C.c_uint32), ("n_consts", C.c_uint32), ("n_columns", C.c_uint32),
+                ("names_len", C.c_uint32), ("n_groups", C.c_uint32), ("n_tables", C.c_uint32),
+                ("flags", C.c_uint32), ("n_keys", C.c_uint32), ("n_table_entries", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+
+class CompiledQuery:
+    """What mh_query_build returns, copied out of the library: the tapes (tape 0 the root; with
+    several groups, tapes 1.. the groups'), the query constants, the column names and widths,
+    each group's column indices and the flags; ``columns`` [(name, width, kind, symbol, key)] and
+    ``tables`` [(kind, name, items)] are decoded on first use (a witness's schema is read only
+    when a model is evaluated, mythril/laser/smt/model.py:45-59)."""
+
+    __slots__ = ("tapes", "consts", "names", "widths", "groups", "flags", "_raw", "_columns",
+                 "_tables")
+
+    def __init__(self, info: QueryInfo):
+        def raw(p, nbytes):
+            return C.string_at(p, nbytes) if nbytes else b""
+
+        nt = info.n_tapes
+        off = np.frombuffer(raw(info.tape_off, 8 * (nt + 1)), dtype=np.uint64).tolist()
+        nodes = np.frombuffer(raw(info.nodes, 24 * off[-1]), dtype=NODE_DTYPE)
+        self.tapes = [nodes[off[i]:off[i + 1]] for i in range(nt)]
+        self.consts = np.frombuffer(raw(info.consts, 32 * info.n_consts),
+                                    dtype=np.uint32).reshape(-1, 8)
+        names = raw(info.names, info.names_len).decode()
+        cols = np.frombuffer(raw(info.columns, 32 * info.n_columns), dtype=QUERY_COLUMN_DTYPE)
+        no, nl = cols["name_off"].tolist(), cols["name_len"].tolist()
+        self.names = [names[o:o + n] for o, n in zip(no, nl)]
+        self.widths = cols["width"]
+        ng = info.n_groups
+        goff = np.frombuffer(raw(info.group_off, 4 * (ng + 1)), dtype=np.uint32).tolist()
+        gcols = np.frombuffer(raw(info.group_cols, 4 * goff[-1]), dtype=np.uint32).tolist()
+        self.groups = [gcols[goff[g]:goff[g + 1]] for g in range(ng)]
+        self.flags = int(info.flags)
+        kb = 4 * QUERY_KEY_LIMBS
+        self._raw = (names, cols, raw(info.key_limbs, kb * info.n_keys),
+                     raw(info.tables, 24 * info.n_tables),
+                     raw(info.table_limbs, kb * info.n_table_entries))
+        self._columns = self._tables = None
+
+    @staticmethod
+    def _ints(data: bytes) -> List[int]:
+        k = 4 * QUERY_KEY_LIMBS
+        return [int.from_bytes(data[i:i + k], "little") for i in range(0, len(data), k)]
+
+    @property
+    def columns(self) -> List[tuple]:
+        if self._columns is None:
+            names, cols, key_limbs, _, _ = self._raw
+            keys = self._ints(key_limbs)
+            self._columns = [(names[no:no + nl], w, COLUMN_KINDS[k], names[so:so + sl],
+                              None if ko == 0xFFFFFFFF else keys[ko])
+                             for no, nl, so, sl, w, k, ko, _ in cols.tolist()]
+        return self._columns
+
+    @property
+    def tables(self) -> List[tuple]:
+        if self._tables is None:
+            names, _, _, tabs, limbs = self._raw
+            vals = self._ints(limbs)
+            self._tables = [
+                (k, names[no:no + nl], vals[lo:lo + (2 * n + 1 if k == TABLE_KECCAK else n)])
+                for k, no, nl, lo, n, _ in np.frombuffer(tabs, dtype=QUERY_TABLE_DTYPE).tolist()]
+        return self._tables
+
+
+def _ints(rows: np.ndarray) -> List[int]:
+    """[n, k] u32 limbs -> n ints."""
+    rows = np.ascontiguousarray(rows, dtype="<u4")
+    data, k = rows.tobytes(), 4 * rows.shape[1]
+    return [int.from_bytes(data[k * i:k * i + k], "little") for i in range(len(rows))]
+
+
+class TermMirror:
+    """An mh_terms session mirroring one TapeBuilder (tape.py): each sync hands the library the
+    nodes, constants and names the builder made since the last one; build() compiles a query
+    (mh_query_build).  One per builder, kept on it (``TermMirror.of``)."""
+
+    def __init__(self):
+        self.lib = load()
+        h = C.c_void_p()
+        _check(self.lib.mh_terms_create(C.byref(h)))
+        self.h = h
+        self.n = [0, 0, 0, 0, 0]  # nodes, constants, variables, arrays, functions sent
+
+    @classmethod
+    def of(cls, b) -> "TermMirror":
+        m = b.__dict__.get("_term_mirror")
+        if m is None:
+            m = b.__dict__["_term_mirror"] = cls()
+        return m
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.mh_terms_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self, b) -> None:
+        n0, c0, v0, a0, f0 = self.n
+        n1 = len(b.nodes)
+        pool = b.pool
+        c1 = len(pool.values)
+        v1 = len(b.var_index)
+        sym = b.symbols
+        a1, f1 = len(sym.array_names), len(sym.function_names)
+        if [n1, c1, v1, a1, f1] == self.n:
+            return
+        if n1 > n0:
+            k = n1 - n0
+            rows = np.fromiter(chain.from_iterable(b.nodes[n0:n1]), np.int64, 7 * k).reshape(k, 7)
+            nodes = np.empty(k, dtype=NODE_DTYPE)
+            nodes["op"] = rows[:, 0]
+            nodes["flags"] = np.fromiter(b.flags[n0:n1], np.uint8, k)
+            nodes["width"] = rows[:, 1]
+            for j, f in enumerate(("a", "b", "c", "imm0", "imm1")):
+                nodes[f] = rows[:, 2 + j]
+        else:
+            nodes = np.zeros(1, dtype=NODE_DTYPE)
+        consts = (np.ascontiguousarray(pool.to_array()[c0:c1]) if c1 > c0
+                  else np.zeros((1, 8), dtype=np.uint32))
+
+        def names(seq) -> bytes:
+            return b"".join(s.encode() + b"\0" for s in seq)
+
+        vn = names(list(b.var_index)[v0:v1]) if v1 > v0 else b""
+        an = names(sym.array_names[a0:a1]) if a1 > a0 else b""
+        fn = names(sym.function_names[f0:f1]) if f1 > f0 else b""
+        _check(self.lib.mh_terms_append(self.h, nodes.ctypes.data, n1 - n0, _ptr(consts), c1 - c0,
+                                        vn, v1 - v0, an, a1 - a0, fn, f1 - f0))
+        self.n = [n1, c1, v1, a1, f1]
+
+    def build(self, b, roots: Sequence[int]) -> CompiledQuery:
+        """mh_query_build of the conjunction of `roots` (after a sync with `b`)."""
+        self.sync(b)
+        r = np.ascontiguousarray(roots, dtype=np.uint32)
+        h = C.c_void_p()
+        info = QueryInfo()
+        _check(self.lib.mh_query_build(self.h, _ptr(r), len(r), C.byref(h), C.byref(info)))
+        try:
+            return CompiledQuery(info)
+        finally:
+            self.lib.mh_query_free(h)
 
 
 _ARITY_BY_INT: List[int] = []

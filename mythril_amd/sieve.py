@@ -28,7 +28,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import native
-from .lower import Schema, lower_query, node_columns
+from .lower import Column, KeccakMap, Schema, cell_name, lower_query, node_columns
 from .tape import NODE_DTYPE, Op, Tape, TapeBuilder, TapeSet
 
 
@@ -94,8 +94,11 @@ def local_tapeset(b: TapeBuilder, roots: Sequence[int], columns: Sequence[str]) 
     new0 = imm0.copy()
     if is_var.any():
         lut = np.full(len(b.var_index), -1, dtype=np.int64)
+        vi = b.var_index
         for i, c in enumerate(columns):
-            lut[b.var_index[c]] = i
+            v = vi.get(c)  # a column no builder term reads (a native query's cell) maps nothing
+            if v is not None:
+                lut[v] = i
         new0[is_var] = lut[imm0[is_var]]
         if (new0[is_var] < 0).any():
             raise ValueError("a tape reads a variable outside the query's columns")
@@ -110,6 +113,34 @@ def local_tapeset(b: TapeBuilder, roots: Sequence[int], columns: Sequence[str]) 
         ts.tapes.append(Tape(nodes[off:off + len(t)]))
         off += len(t)
     return ts
+
+
+class NativeSchema(Schema):
+    """The Schema of a query the native compiler built, decoded on first use: a witness's
+    schema is read only when a model is evaluated (mythril/laser/smt/model.py:45-59, model.py
+    here), LASER's is_possible never reads it (constraints.py:25-35)."""
+
+    _FIELDS = ("cells", "uf_cells", "keccak", "columns")
+
+    def __init__(self, cq: "native.CompiledQuery"):  # noqa: super().__init__ deferred
+        self.__dict__["_cq"] = cq
+
+    def __getattr__(self, name):
+        if name not in self._FIELDS or "_cq" not in self.__dict__:
+            raise AttributeError(name)
+        cq = self.__dict__.pop("_cq")
+        cols = {n: Column(n, w, k, s, key) for n, w, k, s, key in cq.columns}
+        cells: Dict[str, Dict[int, str]] = {}
+        uf_cells: Dict[str, Dict[int, str]] = {}
+        keccak: Dict[str, KeccakMap] = {}
+        for kind, name_, items in cq.tables:
+            if kind == native.TABLE_KECCAK:
+                keccak[name_] = KeccakMap(items[0], dict(zip(items[1::2], items[2::2])))
+            else:
+                (cells if kind == native.TABLE_CELLS else uf_cells)[name_] = {
+                    k: cell_name(name_, k) for k in items}
+        Schema.__init__(self, cells, uf_cells, keccak, cols)
+        return self.__dict__[name]
 
 
 def substitute(b: TapeBuilder, root: int, env: Dict[int, int]) -> int:
@@ -356,8 +387,12 @@ class Sieve:
     """A device context plus reusable buffers; one per thread (handles are not shared)."""
 
     def __init__(self, device: int = 0, rows: int = 1 << 16, max_rounds: int = 2,
-                 seed: int = 0x5EED5EED, budget_s: float = 0.25, first_rows: int = 256):
+                 seed: int = 0x5EED5EED, budget_s: float = 0.25, first_rows: int = 256,
+                 native_query: bool = True):
         self.ctx = native.Context(device)
+        # host stages by the native query compiler (csrc/query.cpp); False: the Python stages
+        # (lower.py, buckets, local_tapeset) it is checked against (tests/test_query_native.py)
+        self.native_query = native_query
         self.rows = rows
         # the harvested guide usually solves a LASER query in its first rows (round 1 found every
         # SAT witness of tests/laser_like.py within the first 16 rows): a small first round
@@ -475,6 +510,60 @@ class Sieve:
         finally:
             ct.close()
 
+    def _host_native(self, b: TapeBuilder, roots: Sequence[int]):
+        """The host stages by the native query compiler (mh_query_build: lowering, groups and
+        tapes in one call, csrc/query.cpp), or None for a query with a candidate definition
+        (those take _host_python, whose eliminate_definitions solves for the symbol)."""
+        t0 = time.perf_counter()
+        cq = native.TermMirror.of(b).build(b, roots)
+        st = self.stats
+        st.add("lower", time.perf_counter() - t0)
+        if cq.flags & native.QUERY_DEFINITIONS:
+            st.extra["host_python"] = st.extra.get("host_python", 0) + 1
+            return None
+        columns = cq.names
+        ts = TapeSet(columns)
+        ts.pool = LocalPool(cq.consts)
+        tapes = cq.tapes
+        ts.tapes = [Tape(t) for t in (tapes if len(tapes) == 1 else tapes[1:])]
+        if len(cq.groups) > 1:
+            st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
+        return columns, cq.widths, NativeSchema(cq), tapes[0], ts, cq.groups, []
+
+    def _host_python(self, b: TapeBuilder, roots: Sequence[int]):
+        """The host stages in Python: lower_query, definitions, buckets, local tapes."""
+        t0 = time.perf_counter()
+        st = self.stats
+        root, schema = lower_query(b, roots)
+        t_l = time.perf_counter()
+        st.add("lower", t_l - t0)
+        columns = list(schema.columns)
+        if not columns:  # ground query: one row decides it
+            columns = ["__ground__"]
+            b.var("__ground__", 1)
+            from .lower import Column
+
+            schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
+        root, defs = self.solve_definitions(b, root, schema)
+        groups = self.bucket_roots(b, root)
+        col_of = {b.var_index[c]: i for i, c in enumerate(columns)}
+        group_cols = [[col_of[v] for v in vs] for _, vs in groups]
+        accs = [acc for acc, _ in groups]
+        # the guide is harvested natively from the root's tape: the one tape of a query whose
+        # conjuncts share columns (the same AND chain), else an extra tape of the same tape set
+        # (same constants), not compiled
+        if accs == [root]:
+            ts = local_tapeset(b, accs, columns)
+            root_nodes = ts.tapes[0].nodes
+        else:
+            ts = local_tapeset(b, [root] + accs, columns)
+            root_nodes = ts.tapes.pop(0).nodes
+        if len(groups) > 1:
+            st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
+        st.add("tapes", time.perf_counter() - t_l)
+        widths = [schema.columns[c].width for c in columns]
+        return columns, widths, schema, root_nodes, ts, group_cols, defs
+
     @classmethod
     def buckets(cls, b: TapeBuilder, root: int) -> List[Tuple[List[int], set]]:
         """Variable-disjoint groups of the conjuncts of `root` (the DependenceMap of
@@ -500,38 +589,15 @@ class Sieve:
             self.stats.misses += 1
             return None
         st = self.stats
-        root, schema = lower_query(b, roots)
-        t_l = time.perf_counter()
-        st.add("lower", t_l - t0)
-        columns = list(schema.columns)
-        if not columns:  # ground query: one row decides it
-            columns = ["__ground__"]
-            b.var("__ground__", 1)
-            from .lower import Column
-
-            schema.columns["__ground__"] = Column("__ground__", 1, "var", "__ground__")
-        root, defs = self.solve_definitions(b, root, schema)
-        groups = self.bucket_roots(b, root)
-        names = {b.var_index[c]: c for c in columns}
-        group_cols = [[names[v] for v in vs] for _, vs in groups]
-        accs = [acc for acc, _ in groups]
-        # the guide is harvested natively from the root's tape: the one tape of a query whose
-        # conjuncts share columns (the same AND chain), else an extra tape of the same tape set
-        # (same constants), not compiled
-        if accs == [root]:
-            ts = local_tapeset(b, accs, columns)
-            root_nodes = ts.tapes[0].nodes
-        else:
-            ts = local_tapeset(b, [root] + accs, columns)
-            root_nodes = ts.tapes.pop(0).nodes
-        if len(groups) > 1:
-            self.stats.extra["bucketed"] = self.stats.extra.get("bucketed", 0) + 1
+        host = self._host_native(b, roots) if self.native_query else None
+        if host is None:
+            host = self._host_python(b, roots)
+        columns, widths, schema, root_nodes, ts, group_cols, defs = host
         t_t = time.perf_counter()
-        st.add("tapes", t_t - t_l)
         col_index = {c: i for i, c in enumerate(columns)}
         parent = self.witnesses.get(key[:-1]) if key else None
         guide = native.harvest_guide(
-            root_nodes, ts.pool.to_array(), [schema.columns[c].width for c in columns],
+            root_nodes, ts.pool.to_array(), widths,
             [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else ())
         t1 = time.perf_counter()
         st.add("guide", t1 - t_t)
@@ -545,7 +611,7 @@ class Sieve:
         try:
             assign = self._buffer(len(columns))
             values: Dict[str, int] = {}
-            solved = [False] * len(groups)
+            solved = [False] * len(group_cols)
             first_index = None
             offset = 0
             launches = [self.first_rows]
@@ -575,7 +641,7 @@ class Sieve:
                         st.add("download", time.perf_counter() - td)
                     vals = rows_read[row]
                     for c in group_cols[g]:
-                        values[c] = _limbs(vals[col_index[c], :, 0])
+                        values[columns[c]] = _limbs(vals[c, :, 0])
                     solved[g] = True
                     first_index = hit if first_index is None else min(first_index, hit)
                 if all(solved):

@@ -17,6 +17,9 @@
 #   paths     scripts/path_scaling.py (latency against path length, 25..400 constraints)
 #   strong    bench.py --strong at N=1 (config 5 literally: 2^26 rows in total)
 #   import    scripts/import_cost.py (the z3 import stage per new constraint, C++ vs Python)
+#   pylatency latency's two passes with the Python host stages (SIEVE_HOST=python)
+#   pypaths   paths with the Python host stages
+#   qcost     scripts/query_cost.py (host stages per query, native compiler vs Python)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:?tag}
@@ -45,6 +48,12 @@ for step in "$@"; do
     paths)    timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" ;;
     import)   timeout -k 10 300 python -u scripts/import_cost.py > "$OUT/import_cost.jsonl" 2> "$OUT/import_cost.log" ;;
     strong)   timeout -k 10 400 python -u bench.py --strong --no-companion --cpu-seconds 3 > "$OUT/bench_strong.json" 2> "$OUT/bench_strong.log" ;;
+    pylatency) SIEVE_HOST=python SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py \
+                > "$OUT/sieve_queries_py_a.jsonl" 2> "$OUT/py_a.log" && \
+              SIEVE_HOST=python SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py \
+                > "$OUT/sieve_queries_py_b.jsonl" 2> "$OUT/py_b.log" ;;
+    pypaths)  SIEVE_HOST=python timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_py.jsonl" 2> "$OUT/path_scaling_py.log" ;;
+    qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?

@@ -13,6 +13,8 @@ SafeMath checks LASER adds along a path), on one Sieve, one JSON line per (shape
   pays before z3), and its interpreter time per round (``run`` stage / launches);
 * the stages of the last LASER-order solve and the columns / tape nodes of the query.
 
+SIEVE_HOST=python: the Python host stages instead of the native query compiler.
+
     python scripts/path_scaling.py [lengths=25,50,100,200,400]
 """
 import gc
@@ -44,7 +46,7 @@ def laser_order(s, ctx, cs, timed_last=8):
 
 def main():
     lengths = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "25,50,100,200,400").split(",")]
-    s = Sieve()
+    s = Sieve(native_query=os.environ.get("SIEVE_HOST", "native") == "native")
     ctx, cs = grow("killbilly", 25)
     s.solve(ctx.b, [c.node for c in cs])  # warm-up: HIP runtime, code object loads
     for name in ("killbilly", "overflow", "ether_thief"):

@@ -16,6 +16,9 @@ repeated query before the sieve sees it).  Each timed solve starts after a gc.co
 rebuilds all the shapes on a fresh term context, and the collector's pause for that harness garbage
 is not the query's.
 
+SIEVE_HOST=python runs the host stages in Python (lower.py / buckets / local_tapeset) instead of
+the native query compiler (csrc/query.cpp), for the A/B of DESIGN §6.
+
     python scripts/sieve_queries.py [rows_per_round]
 """
 import gc
@@ -48,7 +51,7 @@ def solve(s, ctx, cs, keyed=True):
 def main():
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
     reps = int(os.environ.get("SIEVE_QUERY_REPS", "5"))
-    s = Sieve(rows=rows)
+    s = Sieve(rows=rows, native_query=os.environ.get("SIEVE_HOST", "native") == "native")
     ctx, qs = queries()
     # warm-up: the first query of a process pays the HIP runtime's lazy initialisation and the
     # code object load; LASER issues thousands of queries per process

@@ -223,3 +223,30 @@ def test_long_path_on_gpu(gpu_ctx, name):
     ctx, cs = grow(name, 200, unsat=True)
     frontend.configure(fallback=lambda *a: "z3")
     assert frontend.get_model(tuple(cs)) == "z3"
+
+
+def test_native_and_python_host_stages_agree(gpu_ctx):
+    """Sieve.solve with the native query compiler (csrc/query.cpp) and with the Python stages it
+    replaced: the same hit or miss on every LASER-shaped query in LASER order, and every native
+    witness is a model of the ORIGINAL query (oracle)."""
+    from mythril_amd.sieve import Sieve
+    from tests.laser_like import hard_queries
+
+    for make in (queries, hard_queries):
+        ctx, qs = make()
+        ctx_py, qs_py = make()
+        s_nat, s_py = Sieve(), Sieve(native_query=False)
+        try:
+            for (name, cs), (_, cs_py) in zip(qs, qs_py):
+                for k in range(1, len(cs) + 1):
+                    nodes = [c.node for c in cs[:k]]
+                    w = s_nat.solve(ctx.b, nodes, key=tuple(nodes))
+                    nodes_py = [c.node for c in cs_py[:k]]
+                    w_py = s_py.solve(ctx_py.b, nodes_py, key=tuple(nodes_py))
+                    assert (w is None) == (w_py is None), (name, k)
+                    if w is not None:
+                        assert _oracle_holds(ctx, cs[:k], w.schema, w.values), (name, k)
+            assert s_nat.stats.hits > 10
+        finally:
+            s_nat.close()
+            s_py.close()
