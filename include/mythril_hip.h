@@ -104,7 +104,9 @@ typedef struct mh_tape_info {
     uint32_t n_insns;        /* device instructions after legalisation                            */
     uint32_t n_regs;         /* peak registers used (of MH_NUM_REGS)                              */
     uint32_t features;       /* bit 0: division family, bit 1: keccak, bit 2: EVM_EXP             */
-    uint64_t alg_ops;        /* algorithmic u32 ALU ops per evaluation (op-cost table) */
+    uint64_t alg_ops;        /* SURVEY.md §8(d)'s op-cost table summed over the tape (1100 per
+                                division, ...): a reporting figure, not a work count -- the
+                                roofline prices a code-independent minimum     */
 } mh_tape_info;
 
 /* ---- library / device ------------------------------------------------------------------------ */

@@ -23,7 +23,9 @@ import numpy as np
 
 BOOL = 0
 MAX_WIDTH = 1088  # 136 bytes: one Keccak block
-FINISH_CACHE = 256  # tapes of recent AND roots kept per builder (TapeBuilder.finish)
+FINISH_CACHE = 256  # tapes of recent AND roots kept per builder (TapeBuilder.finish) ...
+FINISH_CACHE_NODES = 1 << 20  # ... holding at most this many nodes in all (each entry keeps a
+                              # node -> index map and the tape: a bound on memory, not entries)
 
 
 class Op(enum.IntEnum):
@@ -417,8 +419,10 @@ class TapeBuilder:
         # AND extends it)
         arr.flags.writeable = False  # shared with later tapes: callers copy to modify
         cache[root] = (remap, arr)
-        while len(cache) > FINISH_CACHE:
-            cache.popitem(last=False)
+        held = self.__dict__.get("_finished_nodes", 0) + len(arr)
+        while len(cache) > 1 and (len(cache) > FINISH_CACHE or held > FINISH_CACHE_NODES):
+            held -= len(cache.popitem(last=False)[1][1])
+        self._finished_nodes = held
         return Tape(arr)
 
 

@@ -116,7 +116,7 @@ def test_jit_division_digit_boundaries(gpu_ctx):
     """Quotient digits on an integer boundary (x = q y + {-1, 0, 1}) and the uniform paths of
     the division subroutine (tests/test_jit.py division_wave_rows), where the hardware's
     reciprocal decides whether a digit estimate lands one off and a correction must run."""
-    from tests.test_jit import division_wave_rows, small_quotient_rows
+    from tests.test_jit import division_wave_rows, mixed_top_limb_rows, small_quotient_rows
 
     ts = TapeSet()
     b = ts.builder()
@@ -124,7 +124,8 @@ def test_jit_division_digit_boundaries(gpu_ctx):
     for op in (Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD):
         ts.add(b.finish(b.op(op, x, y)))
     for seed in range(4):
-        for rows in (division_wave_rows(seed), small_quotient_rows(seed)):
+        for rows in (division_wave_rows(seed), small_quotient_rows(seed),
+                     mixed_top_limb_rows(seed)):
             n, _ = jit_values_match(gpu_ctx, ts, soa_of(rows, 2))
             assert n == len(ts.tapes)
 

@@ -205,6 +205,34 @@ def test_division_edges_on_gpu(gpu_ctx):
                 assert got[r] == smt_eval.evaluate(t.nodes, ts.pool.values, [p, q]), (w, i, p, q)
 
 
+def test_division_directed_rows_on_gpu(gpu_ctx):
+    """The interpreter on the division vectors the native code is checked with
+    (tests/test_gpu_jit.py::test_jit_division_digit_boundaries): divisors just above 2^224,
+    quotients near 2^10 and on integer boundaries (x = k y - 1, k y, k y + y - 1), waves mixing
+    divisors with and without a top limb, zero divisors -- bit-exact against the oracle."""
+    from tests.test_jit import division_wave_rows, mixed_top_limb_rows, small_quotient_rows
+
+    ts = TapeSet()
+    b = ts.builder()
+    x, y = b.var("x"), b.var("y")
+    for op in (Op.BVUDIV, Op.BVUREM, Op.BVSDIV, Op.BVSREM, Op.BVSMOD):
+        ts.add(b.finish(b.op(op, x, y)))
+    ct = gpu_ctx.compile(ts)
+    for seed in range(2):
+        rows = division_wave_rows(seed) + small_quotient_rows(seed) + mixed_top_limb_rows(seed)
+        soa = np.zeros((2, 8, len(rows)), dtype=np.uint32)
+        for r, (p, q) in enumerate(rows):
+            for k in range(8):
+                soa[0, k, r] = (p >> (32 * k)) & 0xFFFFFFFF
+                soa[1, k, r] = (q >> (32 * k)) & 0xFFFFFFFF
+        a = upload(gpu_ctx, soa)
+        for i, t in enumerate(ts.tapes):
+            got = native.limbs_to_ints(native.eval_values(gpu_ctx, ct, i, a))
+            for r, (p, q) in enumerate(rows):
+                assert got[r] == smt_eval.evaluate(t.nodes, ts.pool.values, [p, q]), (seed, i, r)
+        a.close()
+
+
 def test_keccak_on_gpu(gpu_ctx):
     from oracle.keccak import keccak256
 

@@ -183,6 +183,28 @@ def small_quotient_rows(seed):
     return rows
 
 
+def mixed_top_limb_rows(seed):
+    """64-row waves whose lanes alternate divisors with a nonzero top limb (y >= 2^224, the
+    small-quotient estimate) and divisors below 2^224 (the long digit loop), x on integer
+    boundaries of both (x = k y - 1, k y, k y + y - 1, quotients near 2^10)."""
+    rng = random.Random(seed)
+    M = (1 << 256) - 1
+    rows = []
+    for wave in range(4):
+        for i in range(64):
+            if i % 2:
+                y = (1 << 224) + rng.choice([1, 2, rng.getrandbits(20), rng.getrandbits(224)])
+                k = rng.choice([1, 2, 1022, 1023, 1024, rng.randrange(1, 1 << 10)])
+            else:
+                y = rng.getrandbits(rng.choice([32, 100, 200, 224])) | 1
+                k = rng.getrandbits(rng.choice([10, 32, 256 - y.bit_length()]))
+            x = k * y + rng.choice([-1, 0, y - 1])
+            if x > M or x < 0:
+                x = rng.randrange(y)
+            rows.append([x, y])
+    return rows
+
+
 def test_division_small_quotient_jit(emu):
     ts = TapeSet()
     b = ts.builder()
@@ -191,6 +213,7 @@ def test_division_small_quotient_jit(emu):
         ts.add(b.finish(b.op(op, x, y)))
     for seed in range(4):
         check_tapes(emu, ts, soa_of(small_quotient_rows(seed), 2))
+        check_tapes(emu, ts, soa_of(mixed_top_limb_rows(seed), 2))
 
 
 def test_keccak_message_cuts_jit(emu):

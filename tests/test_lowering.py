@@ -178,3 +178,29 @@ def test_shared_rewrites_match_fresh_lowering(which):
             assert ta.tapes[0].nodes.tobytes() == tb.tapes[0].nodes.tobytes(), (name, k)
             assert (ta.pool.to_array() == tb.pool.to_array()).all(), (name, k)
     assert len(ctx_a.b.__dict__["_stable_lower"]) > 0
+
+
+def test_finish_cache_is_bounded_by_nodes(monkeypatch):
+    """TapeBuilder.finish keeps recent roots' tapes for LASER-order extension, bounded by the
+    nodes it holds in all (FINISH_CACHE_NODES), and a cached tape equals a fresh one."""
+    from mythril_amd import tape as tape_mod
+    from tests.laser_paths import grow
+
+    monkeypatch.setattr(tape_mod, "FINISH_CACHE_NODES", 4000)
+    ctx, cs = grow("killbilly", 60)
+    b = ctx.b
+    acc = cs[0].node
+    tapes = []
+    for c in cs[1:]:
+        acc = b.op(Op.AND, acc, c.node)
+        tapes.append((acc, b.finish(acc).nodes.tobytes()))
+    cache = b.__dict__["_finished"]
+    held = sum(len(arr) for _, arr in cache.values())
+    assert held == b.__dict__["_finished_nodes"]
+    assert held <= 4000 or len(cache) == 1
+    assert len(cache) < len(tapes)
+    ctx2, cs2 = grow("killbilly", 60)  # the same terms, nothing cached: the same tapes
+    acc2 = cs2[0].node
+    for c, (_, want) in zip(cs2[1:], tapes):
+        acc2 = ctx2.b.op(Op.AND, acc2, c.node)
+    assert ctx2.b.finish(acc2).nodes.tobytes() == tapes[-1][1]
