@@ -262,6 +262,10 @@ typedef struct mh_query mh_query;
 enum { MH_COL_VAR = 0, MH_COL_CELL = 1, MH_COL_ELSE = 2, MH_COL_UFCELL = 3, MH_COL_UFELSE = 4 };
 enum { MH_TABLE_CELLS = 0, MH_TABLE_UF_CELLS = 1, MH_TABLE_KECCAK = 2 };
 #define MH_QUERY_DEFINITIONS 1u
+#define MH_QUERY_REFUTED 2u     /* the conjunction contradicts itself syntactically (a FALSE
+                                   conjunct, a conjunct and its negation, a term pinned to an
+                                   empty range by equalities / disequalities / unsigned bounds
+                                   against constants): no witness exists                       */
 #define MH_QUERY_KEY_LIMBS 36  /* limbs of a table entry / cell key (1152 bits; keccak arguments are
                                    up to 1088 bits wide)                                        */
 typedef struct {

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -118,6 +119,34 @@ struct Big {  // unsigned, little-endian u32 limbs
         uint64_t c = v;
         for (int i = 0; i < NL && c; ++i) {
             c += r.w[i];
+            r.w[i] = (uint32_t)c;
+            c >>= 32;
+        }
+        return r;
+    }
+    Big minus_one() const {  // *this - 1, for *this > 0
+        Big r = *this;
+        for (int i = 0; i < NL; ++i)
+            if (r.w[i]--) break;
+        return r;
+    }
+    Big times(const Big& o) const {  // exact for operands below 2^576
+        Big r;
+        for (int i = 0; i < NL / 2; ++i) {
+            uint64_t carry = 0;
+            for (int j = 0; i + j < NL; ++j) {
+                const uint64_t cur = (uint64_t)w[i] * (j < NL / 2 ? o.w[j] : 0u) + r.w[i + j] + carry;
+                r.w[i + j] = (uint32_t)cur;
+                carry = cur >> 32;
+            }
+        }
+        return r;
+    }
+    Big operator+(const Big& o) const {
+        Big r;
+        uint64_t c = 0;
+        for (int i = 0; i < NL; ++i) {
+            c += (uint64_t)w[i] + o.w[i];
             r.w[i] = (uint32_t)c;
             c >>= 32;
         }
@@ -781,6 +810,173 @@ bool may_define(const std::vector<mh_node>& tape, const std::vector<uint8_t>& ha
     return false;
 }
 
+struct Cmp {
+    uint8_t op;
+    uint32_t t, c;  // tape nodes: the term, the constant
+};
+
+// t op c for a comparison node of a bit-vector term t with a constant c (either side; a constant on
+// the left mirrors the comparison)
+bool cmp_of_plain(const std::vector<mh_node>& tape, uint32_t n, Cmp& out) {
+    const mh_node& x = tape[n];
+    uint8_t op = x.op;
+    if (op != EQ && !(op >= BVULT && op <= MH_OP_BVUGE)) return false;
+    const bool ca = tape[x.a].op == CONST, cb = tape[x.b].op == CONST;
+    if (ca == cb || tape[x.a].width == 0) return false;
+    if (ca)
+        op = op == BVULT ? MH_OP_BVUGT : op == MH_OP_BVULE ? MH_OP_BVUGE
+           : op == MH_OP_BVUGT ? BVULT : op == MH_OP_BVUGE ? MH_OP_BVULE : op;
+    out = {op, ca ? x.b : x.a, ca ? x.a : x.b};
+    return true;
+}
+
+// A conjunction that contradicts itself syntactically (sound, not complete): a FALSE conjunct, a
+// conjunct and its negation, or one term pinned by its conjuncts -- t == c, t != c, unsigned
+// comparisons of t with constants and their negations -- to an empty range.  Over the lowered
+// root tape, whose nodes are hash-consed (equal terms are one node).  Such a query cannot have a
+// witness: the device rounds are skipped (the query still goes to the fallback solver).
+bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
+    const std::vector<mh_node>& tape = Q.tape;
+    std::unordered_map<uint32_t, char> asserted;
+    for (uint32_t cj : conj) asserted[cj] = 1;
+    struct Range {
+        Big lo, hi;
+        std::vector<uint32_t> ne;  // constants t must differ from
+    };
+    std::unordered_map<uint32_t, Range> ranges;
+    auto range = [&](uint32_t t) -> Range& {
+        auto it = ranges.find(t);
+        if (it == ranges.end()) {
+            Range r;
+            const uint32_t w = tape[t].width;
+            for (uint32_t i = 0; i < w && i < 32u * NL; ++i) r.hi.w[i / 32] |= 1u << (i % 32);
+            it = ranges.emplace(t, r).first;
+        }
+        return it->second;
+    };
+    // smt.py's ULE / UGE (bitvec_helper.py: Or(ULT(a, b), a == b)) read as BVULE / BVUGE
+    auto cmp_of = [&](uint32_t n, Cmp& out) -> bool {
+        const mh_node& x = tape[n];
+        if (x.op == MH_OP_OR) {
+            Cmp p, e;
+            if (!cmp_of_plain(tape, x.a, p) || !cmp_of_plain(tape, x.b, e)) return false;
+            if (p.op == EQ) std::swap(p, e);
+            if (e.op != EQ || p.t != e.t || p.c != e.c) return false;
+            if (p.op != BVULT && p.op != MH_OP_BVUGT) return false;
+            out = {(uint8_t)(p.op == BVULT ? MH_OP_BVULE : MH_OP_BVUGE), p.t, p.c};
+            return true;
+        }
+        return cmp_of_plain(tape, n, out);
+    };
+    for (uint32_t cj : conj) {
+        const mh_node& x0 = tape[cj];
+        if (x0.op == FALSE_) return true;
+        bool neg = false;
+        uint32_t n = cj;
+        if (x0.op == MH_OP_NOT) {
+            if (asserted.count(x0.a)) return true;
+            neg = true;
+            n = x0.a;
+        }
+        Cmp k;
+        if (!cmp_of(n, k)) continue;
+        uint8_t op = k.op;
+        const uint32_t t = k.t;
+        const Big* c = &Q.qpool[tape[k.c].imm0];
+        if (neg)  // not (t < c) is t >= c, ...; not (t == c) is t != c
+            op = op == BVULT ? MH_OP_BVUGE : op == MH_OP_BVULE ? MH_OP_BVUGT
+               : op == MH_OP_BVUGT ? MH_OP_BVULE : op == MH_OP_BVUGE ? BVULT : op;
+        Range& r = range(t);
+        if (op == EQ && neg) {
+            r.ne.push_back(k.c);
+            continue;
+        }
+        if (op == EQ || op == MH_OP_BVULE || op == BVULT) {  // an upper bound
+            if (op == BVULT && c->zero()) return true;
+            const Big h = op == BVULT ? c->minus_one() : *c;
+            if (h < r.hi) r.hi = h;
+        }
+        if (op == EQ || op == MH_OP_BVUGE || op == MH_OP_BVUGT) {  // a lower bound
+            Big l = *c;
+            if (op == MH_OP_BVUGT) {
+                if (!(*c < r.hi) && !(r.hi < *c)) return true;  // t > max of the range so far
+                l = c->plus(1);
+            }
+            if (r.lo < l) r.lo = l;
+        }
+        if (r.hi < r.lo) return true;
+    }
+    for (const auto& kv : ranges) {  // a range pinned to one value that a disequality excludes
+        const Range& r = kv.second;
+        if (r.lo == r.hi)
+            for (uint32_t ne : r.ne)
+                if (Q.qpool[tape[ne].imm0] == r.lo) return true;
+    }
+    // second pass: comparisons of two terms and the no-overflow predicates
+    // (bitvec_helper.py:178-227) decided by the terms' ranges
+    auto bounds = [&](uint32_t t, Big& lo, Big& hi) {
+        if (tape[t].op == CONST) {
+            lo = hi = Q.qpool[tape[t].imm0];
+            return;
+        }
+        auto it = ranges.find(t);
+        if (it != ranges.end()) {
+            lo = it->second.lo;
+            hi = it->second.hi;
+            return;
+        }
+        lo = Big();
+        hi = Big();
+        for (uint32_t i = 0; i < tape[t].width && i < 32u * NL; ++i) hi.w[i / 32] |= 1u << (i % 32);
+    };
+    auto le = [](const Big& a, const Big& b) { return !(b < a); };
+    // 1 = true under every value in the ranges, 0 = false under every one, -1 = either
+    std::function<int(uint32_t, int)> decide = [&](uint32_t n, int depth) -> int {
+        const mh_node& x = tape[n];
+        if (depth > 8) return -1;
+        switch (x.op) {
+            case TRUE_: return 1;
+            case FALSE_: return 0;
+            case MH_OP_NOT: {
+                const int v = decide(x.a, depth + 1);
+                return v < 0 ? -1 : 1 - v;
+            }
+            case MH_OP_OR: case AND: {
+                const int a = decide(x.a, depth + 1), b = decide(x.b, depth + 1);
+                if (x.op == MH_OP_OR) return a == 1 || b == 1 ? 1 : (a == 0 && b == 0 ? 0 : -1);
+                return a == 0 || b == 0 ? 0 : (a == 1 && b == 1 ? 1 : -1);
+            }
+            default: break;
+        }
+        const bool cmp = x.op == EQ || (x.op >= BVULT && x.op <= MH_OP_BVUGE);
+        const bool pred = x.op == MH_OP_BVADD_NOOVFL_U || x.op == MH_OP_BVMUL_NOOVFL_U ||
+                          x.op == MH_OP_BVSUB_NOUDFL_U;
+        if ((!cmp && !pred) || tape[x.a].width == 0) return -1;
+        Big la, ha, lb, hb;
+        bounds(x.a, la, ha);
+        bounds(x.b, lb, hb);
+        Big top;  // 2^width
+        const uint32_t w = tape[x.a].width;
+        top.w[w / 32] |= 1u << (w % 32);
+        switch (x.op) {
+            case EQ: return hb < la || ha < lb ? 0 : (la == ha && lb == hb && la == lb ? 1 : -1);
+            case BVULT: return ha < lb ? 1 : (le(hb, la) ? 0 : -1);
+            case MH_OP_BVULE: return le(ha, lb) ? 1 : (hb < la ? 0 : -1);
+            case MH_OP_BVUGT: return hb < la ? 1 : (le(ha, lb) ? 0 : -1);
+            case MH_OP_BVUGE: return le(hb, la) ? 1 : (ha < lb ? 0 : -1);
+            case MH_OP_BVADD_NOOVFL_U: return (ha + hb) < top ? 1 : (le(top, la + lb) ? 0 : -1);
+            case MH_OP_BVMUL_NOOVFL_U:
+                if (w > 512) return -1;
+                return ha.times(hb) < top ? 1 : (le(top, la.times(lb)) ? 0 : -1);
+            case MH_OP_BVSUB_NOUDFL_U: return le(hb, la) ? 1 : (ha < lb ? 0 : -1);
+            default: return -1;
+        }
+    };
+    for (uint32_t cj : conj)
+        if (decide(cj, 0) == 0) return true;
+    return false;
+}
+
 void build(Query& Q, const uint32_t* roots, uint32_t n_roots, mh_query& q, uint32_t& flags) {
     const std::vector<uint32_t> rs(roots, roots + n_roots);
     Q.harvest(rs);
@@ -811,6 +1007,7 @@ void build(Query& Q, const uint32_t* roots, uint32_t n_roots, mh_query& q, uint3
     }
     for (uint32_t cj : conj)
         if (may_define(tape, Q.has_col, Q.cols, cj)) flags |= MH_QUERY_DEFINITIONS;
+    if (refuted(Q, conj)) flags |= MH_QUERY_REFUTED;
     // column-disjoint groups: conjuncts that reach a common node reading columns share a group
     std::vector<int32_t> owner(N, -1);
     std::vector<uint32_t> uf(conj.size());

@@ -341,6 +341,7 @@ assert QUERY_COLUMN_DTYPE.itemsize == 32 and QUERY_TABLE_DTYPE.itemsize == 24
 COLUMN_KINDS = ("var", "cell", "else", "ufcell", "ufelse")  # MH_COL_*
 TABLE_CELLS, TABLE_UF_CELLS, TABLE_KECCAK = 0, 1, 2
 QUERY_DEFINITIONS = 1
+QUERY_REFUTED = 2
 QUERY_KEY_LIMBS = 36
 
 

@@ -115,6 +115,9 @@ def local_tapeset(b: TapeBuilder, roots: Sequence[int], columns: Sequence[str]) 
     return ts
 
 
+REFUTED = object()  # _host_native's answer for a query that contradicts itself
+
+
 class NativeSchema(Schema):
     """The Schema of a query the native compiler built, decoded on first use: a witness's
     schema is read only when a model is evaluated (mythril/laser/smt/model.py:45-59, model.py
@@ -512,12 +515,17 @@ class Sieve:
 
     def _host_native(self, b: TapeBuilder, roots: Sequence[int]):
         """The host stages by the native query compiler (mh_query_build: lowering, groups and
-        tapes in one call, csrc/query.cpp), or None for a query with a candidate definition
-        (those take _host_python, whose eliminate_definitions solves for the symbol)."""
+        tapes in one call, csrc/query.cpp); None for a query with a candidate definition (those
+        take _host_python, whose eliminate_definitions solves for the symbol); REFUTED for a
+        conjunction that contradicts itself syntactically (MH_QUERY_REFUTED: x == 1 and x == 2,
+        p and not p, bounds with an empty range), which no row can satisfy."""
         t0 = time.perf_counter()
         cq = native.TermMirror.of(b).build(b, roots)
         st = self.stats
         st.add("lower", time.perf_counter() - t0)
+        if cq.flags & native.QUERY_REFUTED:
+            st.extra["refuted"] = st.extra.get("refuted", 0) + 1
+            return REFUTED
         if cq.flags & native.QUERY_DEFINITIONS:
             st.extra["host_python"] = st.extra.get("host_python", 0) + 1
             return None
@@ -590,6 +598,10 @@ class Sieve:
             return None
         st = self.stats
         host = self._host_native(b, roots) if self.native_query else None
+        if host is REFUTED:  # no witness exists: no device round (the fallback still runs)
+            self.stats.misses += 1
+            self.stats.host_s += time.perf_counter() - t0
+            return None
         if host is None:
             host = self._host_python(b, roots)
         columns, widths, schema, root_nodes, ts, group_cols, defs = host

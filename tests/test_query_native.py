@@ -103,7 +103,9 @@ def test_laser_like_in_laser_order(which):
     for name, cs in qs:
         nodes = [c.node for c in cs]
         for k in range(1, len(nodes) + 1):
-            check_query(ctx.b, nodes[:k], (name, k))
+            cq = check_query(ctx.b, nodes[:k], (name, k))
+            if which == "queries" and name != "unsat_actor":  # SAT: never refuted
+                assert not cq.flags & native.QUERY_REFUTED, (name, k)
             n += 1
     assert n > 20
 
@@ -121,7 +123,74 @@ def test_grown_paths(shape):
 def test_reference_cases(case):
     ctx, cs = case.build()
     nodes = [c.node for c in cs if hasattr(c, "node")]
-    check_query(ctx.b, nodes, case.name)
+    cq = check_query(ctx.b, nodes, case.name)
+    if case.expected == "sat" and cq is not None:
+        assert not cq.flags & native.QUERY_REFUTED, case.name
+
+
+def test_refutation():
+    """MH_QUERY_REFUTED: syntactic contradictions are found, satisfiable neighbours are not."""
+    from mythril_amd import smt
+    from mythril_amd.smt import Not, ULE, ULT, UGT, symbol_factory
+
+    ctx = smt.set_context(smt.Context())
+    x = symbol_factory.BitVecSym("x", 256)
+    y = symbol_factory.BitVecSym("y", 8)
+    p = x + 1 == 7
+    v = symbol_factory.BitVecVal
+
+    def refuted(*cs):
+        return bool(native.TermMirror.of(ctx.b).build(ctx.b, [c.node for c in cs]).flags
+                    & native.QUERY_REFUTED)
+
+    assert refuted(x == 1, x == 2)
+    assert refuted(p, Not(p))
+    assert refuted(x == 5, Not(x == 5))
+    assert refuted(ULT(x, v(10, 256)), UGT(x, v(20, 256)))
+    assert refuted(ULT(x, v(0, 256)))
+    assert refuted(UGT(y, v(255, 8)))
+    assert refuted(ULE(x, v(3, 256)), Not(ULT(x, v(4, 256))))
+    assert refuted(ULE(v(4, 256), x), ULE(x, v(4, 256)), Not(x == 4))
+    assert not refuted(x == 1, x + 0 == 1)
+    assert not refuted(ULT(x, v(10, 256)), UGT(x, v(8, 256)))
+    assert not refuted(ULE(x, v(4, 256)), ULE(v(4, 256), x))
+    assert not refuted(p, x == 6)  # refuted by arithmetic, not syntax: the device decides
+    assert not refuted(Not(x == 5), ULE(x, v(6, 256)))
+    assert not refuted(y == 255, UGT(y, v(254, 8)))
+    # the no-overflow predicates and term-term comparisons, decided by the operands' ranges
+    from mythril_amd.smt import BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow
+
+    z = symbol_factory.BitVecSym("z", 256)
+    lim = v(1 << 128, 256)
+    assert refuted(ULT(x, lim), ULT(z, lim), Not(BVAddNoOverflow(x, z, False)))
+    assert not refuted(ULT(x, lim), Not(BVAddNoOverflow(x, z, False)))
+    assert refuted(ULT(x, v(1 << 100, 256)), ULT(z, v(1 << 100, 256)),
+                   Not(BVMulNoOverflow(x, z, False)))
+    assert not refuted(ULT(x, v(1 << 200, 256)), ULT(z, v(1 << 100, 256)),
+                       Not(BVMulNoOverflow(x, z, False)))
+    assert refuted(ULT(x, v(5, 256)), UGT(z, v(9, 256)), Not(ULT(x, z)))
+    assert not refuted(ULT(x, v(5, 256)), UGT(z, v(3, 256)), Not(ULT(x, z)))
+    assert refuted(UGT(x, v(9, 256)), ULT(z, v(5, 256)), Not(BVSubNoUnderflow(x, z, False)))
+    assert not refuted(UGT(x, v(2, 256)), ULT(z, v(5, 256)), Not(BVSubNoUnderflow(x, z, False)))
+
+
+def test_unsat_shapes_refuted():
+    """tests/laser_like.py hard_queries: KillBilly's third sender pinned to two actors, and the
+    transfer overflow of two words below 2^128, are refuted without a device round (also on the
+    grown paths); k_storage_unsat and ether_thief_unsat need more than syntax and ranges."""
+    ctx, qs = laser_like.hard_queries()
+    flags = {n: native.TermMirror.of(ctx.b).build(ctx.b, [c.node for c in cs]).flags
+             for n, cs in qs}
+    assert flags["killbilly_unsat"] & native.QUERY_REFUTED
+    assert flags["overflow_unsat"] & native.QUERY_REFUTED
+    assert not flags["ether_thief_unsat"] & native.QUERY_REFUTED
+    for shape in ("killbilly", "overflow"):
+        ctx, cs = grow(shape, 100, unsat=True)
+        cq = native.TermMirror.of(ctx.b).build(ctx.b, [c.node for c in cs])
+        assert cq.flags & native.QUERY_REFUTED, shape
+        ctx, cs = grow(shape, 100)
+        cq = native.TermMirror.of(ctx.b).build(ctx.b, [c.node for c in cs])
+        assert not cq.flags & native.QUERY_REFUTED, shape
 
 
 def test_empty_and_ground_queries():
@@ -168,3 +237,53 @@ def test_malformed_append_is_refused():
                                            native.C.byref(native.C.c_void_p()),
                                            native.C.byref(native.QueryInfo())))
     m.close()
+
+
+def test_refutation_is_sound_on_random_conjunctions():
+    """Random conjunctions of comparisons, negations, ULE/UGE (Or forms) and the no-overflow
+    predicates over three 4-bit symbols: every one MH_QUERY_REFUTED flags has no satisfying
+    assignment (all 4096 enumerated with the oracle), and some are flagged."""
+    import itertools
+    import random
+
+    from mythril_amd import smt
+    from mythril_amd.smt import (And, BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow, Not,
+                                 UGE, UGT, ULE, ULT, symbol_factory)
+    from oracle import smt_eval as E
+
+    rng = random.Random(77)
+    flagged = 0
+    for trial in range(150):
+        ctx = smt.set_context(smt.Context())
+        xs = [symbol_factory.BitVecSym(n, 4) for n in "xyz"]
+
+        def term():
+            return rng.choice(xs) if rng.random() < 0.8 else symbol_factory.BitVecVal(
+                rng.randrange(16), 4)
+
+        def atom():
+            a, b = term(), term()
+            k = rng.randrange(9)
+            c = [lambda: a == b, lambda: ULT(a, b), lambda: UGT(a, b), lambda: ULE(a, b),
+                 lambda: UGE(a, b), lambda: BVAddNoOverflow(a, b, False),
+                 lambda: BVMulNoOverflow(a, b, False), lambda: BVSubNoUnderflow(a, b, False),
+                 lambda: a == symbol_factory.BitVecVal(rng.randrange(16), 4)][k]()
+            return Not(c) if rng.random() < 0.3 else c
+
+        cs = [atom() for _ in range(rng.randrange(2, 6))]
+        cs = [c for c in cs if not isinstance(c, bool)]
+        if not cs:
+            continue
+        try:
+            cq = native.TermMirror.of(ctx.b).build(ctx.b, [c.node for c in cs])
+        except native.SieveError:
+            continue
+        if not cq.flags & native.QUERY_REFUTED:
+            continue
+        flagged += 1
+        tape = ctx.b.finish(And(*cs).node)
+        names = sorted(ctx.b.var_index, key=ctx.b.var_index.get)
+        for vals in itertools.product(range(16), repeat=3):
+            assign = [dict(zip("xyz", vals)).get(n, 0) for n in names]
+            assert not E.evaluate(tape.nodes, ctx.b.pool.values, assign), (trial, vals)
+    assert flagged >= 10

@@ -62,3 +62,24 @@ def test_reference_outcome_on_fake_device(monkeypatch, name, native_query):
                 assert m.eval(c, model_completion=True) is True, name
     finally:
         frontend.reset()
+
+
+def test_refuted_query_skips_the_device(monkeypatch):
+    """A query that contradicts itself (MH_QUERY_REFUTED: KillBilly's third sender pinned to two
+    actors, an overflow of two words below 2^128) is a miss without a device round; an UNSAT
+    query neither syntax nor ranges refute (ether_thief_unsat) still runs its rounds and misses."""
+    from tests.laser_like import hard_queries
+
+    fake_device.install(monkeypatch)
+    ctx, qs = hard_queries()
+    s = Sieve(rows=256, budget_s=60.0)  # the CPU stand-in is slow: no budget cut
+    cs = dict(qs)["killbilly_unsat"]
+    r0 = s.stats.rounds
+    assert s.solve(ctx.b, [c.node for c in cs]) is None
+    assert s.stats.rounds == r0 and s.stats.extra.get("refuted") == 1
+    cs = dict(qs)["overflow_unsat"]
+    assert s.solve(ctx.b, [c.node for c in cs]) is None
+    assert s.stats.rounds == r0 and s.stats.extra.get("refuted") == 2
+    cs = dict(qs)["ether_thief_unsat"]
+    assert s.solve(ctx.b, [c.node for c in cs]) is None
+    assert s.stats.rounds == r0 + 2 and s.stats.misses == 3
