@@ -967,19 +967,21 @@ struct Harvester {
         for (auto& kv : by_col) {
             const std::vector<size_t>& idx = kv.second;
             if ((int)idx.size() <= 2 * kHintsPerColumn) continue;
-            std::vector<V> hi_v(hints.size()), lo_v(hints.size());
-            for (size_t i : idx) {
-                const Alts& alts = hint_alts[hints[i]];
+            // extremes per hint, indexed by position in idx (not by hint: one column's hints)
+            std::vector<V> hi_v(idx.size()), lo_v(idx.size());
+            for (size_t j = 0; j < idx.size(); ++j) {
+                const Alts& alts = hint_alts[hints[idx[j]]];
                 V mx = alts[0][0].second, mn = mx;
                 for (const Alt& a : alts) { mx = std::max(mx, a[0].second); mn = std::min(mn, a[0].second); }
-                hi_v[i] = mx;
-                lo_v[i] = mn;
+                hi_v[j] = mx;
+                lo_v[j] = mn;
             }
-            std::vector<size_t> hi = idx, lo = idx;
+            std::vector<size_t> hi(idx.size()), lo(idx.size());
+            for (size_t j = 0; j < idx.size(); ++j) hi[j] = lo[j] = j;
             std::stable_sort(hi.begin(), hi.end(), [&](size_t p, size_t q) { return hi_v[q] < hi_v[p]; });
             std::stable_sort(lo.begin(), lo.end(), [&](size_t p, size_t q) { return lo_v[p] < lo_v[q]; });
             for (size_t i : idx) drop[i] = 1;
-            for (int j = 0; j < kHintsPerColumn; ++j) drop[hi[j]] = drop[lo[j]] = 0;
+            for (int j = 0; j < kHintsPerColumn; ++j) drop[idx[hi[j]]] = drop[idx[lo[j]]] = 0;
         }
         std::vector<uint32_t> out;
         for (size_t i = 0; i < hints.size(); ++i) if (!drop[i]) out.push_back(hints[i]);
