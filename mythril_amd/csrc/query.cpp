@@ -47,6 +47,7 @@ enum : uint8_t {
 constexpr uint8_t F_ARRAY = 1, F_HOST = 2;
 constexpr uint32_t KECCAK_SHIFT = 139, KECCAK_ALIGN = 6;  // lower.py KECCAK_SHIFT / KECCAK_ALIGN
 constexpr int NL = MH_QUERY_KEY_LIMBS;                     // 1152-bit host values (<= 1088 used)
+constexpr uint32_t OWN = 0x80000000u;       // node id of a query-made node: OWN | index into ov
 constexpr uint32_t OV_CONST = 0x80000000u;  // query-made CONST imm0: index into the query's values
 constexpr uint32_t CELL_COL = 0x40000000u;  // query-made VAR imm0: index into the query's cells
 
@@ -225,7 +226,8 @@ struct mh_terms {
     // const_value of the mirrored nodes (immutable): 0 unknown, 1 none, k + 2 = cv_vals[k]
     std::vector<uint32_t> cv_state;
     std::vector<Big> cv_vals;
-    Stamped memo_lower, seen, local;  // per-query scratch
+    Stamped memo_lower, seen, local;  // per-query scratch (mirrored node ids)
+    std::unique_ptr<class QueryState> last;  // the last query, kept for a child that extends it
 };
 
 namespace {
@@ -255,23 +257,28 @@ using Tables = std::vector<std::pair<std::string, std::vector<Big>>>;
 
 class Query {
 public:
-    explicit Query(mh_terms& t) : T(t), n_mirror((uint32_t)t.nodes.size()) {
-        T.memo_lower.reset(n_mirror);
-        T.seen.reset(n_mirror);
-        if (T.cv_state.size() < n_mirror) T.cv_state.resize(n_mirror, 0u);
+    // a fresh query: the per-query scratch starts a new epoch
+    explicit Query(mh_terms& t) : T(t) {
+        T.memo_lower.reset(T.nodes.size());
+        T.seen.reset(T.nodes.size());
+        T.local.reset(T.nodes.size());
+        sync();
+    }
+    void sync() {  // the mirror may have grown since the query was made
+        if (T.cv_state.size() < T.nodes.size()) T.cv_state.resize(T.nodes.size(), 0u);
     }
 
-    // ---- nodes: mirrored ids [0, n_mirror), the query's own above -----------------------------
-    const mh_node& nd(uint32_t n) const { return n < n_mirror ? T.nodes[n] : ov[n - n_mirror]; }
+    // ---- nodes: mirrored ids below OWN, the query's own OWN | i -------------------------------
+    const mh_node& nd(uint32_t n) const { return n & OWN ? ov[n & ~OWN] : T.nodes[n]; }
     uint32_t width(uint32_t n) const { return nd(n).width; }
 
     uint32_t add(uint8_t op, uint32_t w, uint32_t a = 0, uint32_t b = 0, uint32_t c = 0,
                  uint32_t i0 = 0, uint32_t i1 = 0) {
         const Key k{op, w, a, b, c, i0, i1};
-        auto m = T.memo.find(k);  // hash-consed against the host's nodes first
-        if (m != T.memo.end()) return m->second;
-        auto it = ov_memo.find(k);
+        auto it = ov_memo.find(k);  // the query's own first (a node the host made later is the same)
         if (it != ov_memo.end()) return it->second;
+        auto m = T.memo.find(k);  // hash-consed against the host's nodes
+        if (m != T.memo.end()) return m->second;
         mh_node x{};
         x.op = op;
         x.width = (uint16_t)w;
@@ -281,7 +288,7 @@ public:
         x.imm0 = i0;
         x.imm1 = i1;
         ov.push_back(x);
-        const uint32_t id = n_mirror + (uint32_t)ov.size() - 1;
+        const uint32_t id = OWN | (uint32_t)(ov.size() - 1);
         ov_memo.emplace(k, id);
         return id;
     }
@@ -303,12 +310,12 @@ public:
     }
     const Big& const_of(uint32_t n) const {  // a CONST node's value
         const uint32_t i0 = nd(n).imm0;
-        return n >= n_mirror && (i0 & OV_CONST) ? ov_vals[i0 & ~OV_CONST] : T.pool.at(i0);
+        return (n & OWN) && (i0 & OV_CONST) ? ov_vals[i0 & ~OV_CONST] : T.pool.at(i0);
     }
 
     // TapeBuilder.const_value: CONST / TRUE / FALSE and CONCAT / EXTRACT / ZEXT / SEXT over them
     const Big* const_value(uint32_t n) {
-        if (n < n_mirror) {
+        if (!(n & OWN)) {
             const uint32_t s = T.cv_state[n];
             if (s) return s == 1 ? nullptr : &T.cv_vals[s - 2];
         } else {
@@ -348,8 +355,8 @@ public:
                 }
             }
         }
-        // std::deque-like stability is not needed: callers copy before the next const_value
-        if (n < n_mirror) {
+        // callers copy a value before the next const_value (the vectors may grow)
+        if (!(n & OWN)) {
             if (!ok) {
                 T.cv_state[n] = 1;
                 return nullptr;
@@ -686,20 +693,35 @@ public:
 
     // ---- the root tape (sieve.py local_tapeset): VAR imm0 = query column, CONST imm0 = query
     // constant; has_col = the node reads a column ----------------------------------------------
+    // continues the tape of an earlier call (a child query's root extends its parent's); equal
+    // tape nodes are one (a node the host made after the query made its own copy)
+    bool lhas(uint32_t n) const {
+        return n & OWN ? (n & ~OWN) < local_own.size() && local_own[n & ~OWN] >= 0 : T.local.has(n);
+    }
+    uint32_t lget(uint32_t n) const {
+        return n & OWN ? (uint32_t)local_own[n & ~OWN] : T.local.get(n);
+    }
+    void lset(uint32_t n, uint32_t v) {
+        if (n & OWN) {
+            if (local_own.size() <= (n & ~OWN)) local_own.resize(ov.size(), -1);
+            local_own[n & ~OWN] = v;
+        } else {
+            T.local.set(n, v);
+        }
+    }
     void linearise(uint32_t root) {
-        T.local.reset(n_mirror + ov.size());
         std::vector<std::pair<uint32_t, bool>> st{{root, false}};
         while (!st.empty()) {
             const auto [n, done] = st.back();
             st.pop_back();
-            if (T.local.has(n)) continue;
+            if (lhas(n)) continue;
             const mh_node& x = nd(n);
             const int k = arity(x.op);
             const uint32_t kids[3] = {x.a, x.b, x.c};
             if (!done) {
                 st.push_back({n, true});
                 for (int j = k - 1; j >= 0; --j)
-                    if (!T.local.has(kids[j])) st.push_back({kids[j], false});
+                    if (!lhas(kids[j])) st.push_back({kids[j], false});
                 continue;
             }
             if (x.op >= ARRAY || (x.flags & F_ARRAY)) invalid("a host-only term survived lowering");
@@ -708,7 +730,7 @@ public:
             uint8_t hc = 0;
             uint32_t* opnd[3] = {&y.a, &y.b, &y.c};
             for (int j = 0; j < 3; ++j) {
-                *opnd[j] = j < k ? T.local.get(kids[j]) : 0;
+                *opnd[j] = j < k ? lget(kids[j]) : 0;
                 if (j < k) hc |= has_col[*opnd[j]];
             }
             if (x.op == VAR) {
@@ -717,14 +739,16 @@ public:
             } else if (x.op == CONST) {
                 y.imm0 = const_index(n);
             }
-            T.local.set(n, (uint32_t)tape.size());
+            auto ins = tape_memo.emplace(key_of(y), (uint32_t)tape.size());
+            lset(n, ins.first->second);
+            if (!ins.second) continue;
             tape.push_back(y);
             has_col.push_back(hc);
         }
     }
     uint32_t column_of(uint32_t n) {  // a VAR node's query column (numbered by first use)
         const mh_node& x = nd(n);
-        const bool cell = n >= n_mirror && (x.imm0 & CELL_COL);
+        const bool cell = (n & OWN) && (x.imm0 & CELL_COL);
         auto& m = cell ? cell_cols : var_cols;
         const uint32_t k = cell ? x.imm0 & ~CELL_COL : x.imm0;
         auto it = m.find(k);
@@ -741,7 +765,7 @@ public:
     }
     uint32_t const_index(uint32_t n) {
         const uint32_t i0 = nd(n).imm0;
-        auto& m = n >= n_mirror && (i0 & OV_CONST) ? own_consts : pool_consts;
+        auto& m = (n & OWN) && (i0 & OV_CONST) ? own_consts : pool_consts;
         auto it = m.find(i0);
         if (it != m.end()) return it->second;
         const uint32_t q = (uint32_t)qpool.size();
@@ -751,7 +775,6 @@ public:
     }
 
     mh_terms& T;
-    const uint32_t n_mirror;
     std::vector<mh_node> ov;  // nodes the query made
     std::unordered_map<Key, uint32_t, KeyHash> ov_memo;
     std::vector<Big> ov_vals;  // constants outside the host's pool
@@ -767,6 +790,8 @@ public:
     // the root tape
     std::vector<mh_node> tape;
     std::vector<uint8_t> has_col;
+    std::vector<int64_t> local_own;  // tape index of the query's own nodes, -1 none
+    std::unordered_map<Key, uint32_t, KeyHash> tape_memo;
     std::vector<Column> cols;  // query columns, in first-use order
     std::unordered_map<uint32_t, uint32_t> var_cols, cell_cols, pool_consts, own_consts;
     std::vector<Big> qpool;
@@ -977,62 +1002,133 @@ bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
     return false;
 }
 
-void build(Query& Q, const uint32_t* roots, uint32_t n_roots, mh_query& q, uint32_t& flags) {
-    const std::vector<uint32_t> rs(roots, roots + n_roots);
-    Q.harvest(rs);
-    uint32_t root = 0;
-    for (uint32_t i = 0; i < n_roots; ++i) {  // lower_query: the AND of the lowered roots
-        const uint32_t x = Q.lower(rs[i]);
-        if (Q.width(x) != 0 || (Q.nd(x).flags & F_ARRAY)) invalid("constraints must be Bool");
-        root = i == 0 ? x : Q.add(AND, 0, root, x);
+// the AND leaves of tape node n, left to right (Sieve.conjuncts)
+void and_leaves(const std::vector<mh_node>& tape, uint32_t n, std::vector<uint32_t>& out) {
+    std::vector<uint32_t> st{n};
+    while (!st.empty()) {
+        const uint32_t x = st.back();
+        st.pop_back();
+        if (tape[x].op == AND) {
+            st.push_back(tape[x].b);
+            st.push_back(tape[x].a);
+        } else {
+            out.push_back(x);
+        }
     }
-    if (!n_roots) root = Q.add(TRUE_, 0);
-    Q.linearise(root);
+}
+
+// Harvest tables compared before and after a new constraint (lower.py Harvest.fingerprint)
+struct Fingerprint {
+    Tables cells, uf_cells;
+    std::vector<std::pair<std::string, std::pair<Big, std::vector<std::pair<Big, Big>>>>> keccak;
+    explicit Fingerprint(const Query& Q) : cells(Q.cells), uf_cells(Q.uf_cells) {
+        for (const auto& kv : Q.keccak) keccak.push_back({kv.first, {kv.second.base, kv.second.pairs}});
+    }
+    bool same(const Query& Q) const {
+        if (cells != Q.cells || uf_cells != Q.uf_cells || keccak.size() != Q.keccak.size()) return false;
+        for (size_t i = 0; i < keccak.size(); ++i)
+            if (keccak[i].first != Q.keccak[i].first || !(keccak[i].second.first == Q.keccak[i].second.base) ||
+                keccak[i].second.second != Q.keccak[i].second.pairs)
+                return false;
+        return true;
+    }
+};
+
+}  // namespace
+
+// One query's state, kept on the session (mh_terms.last): a child query whose roots are its
+// parent's plus one constraint (svm.py:257-262) extends it when the new constraint adds nothing to
+// the harvest -- only that constraint is harvested, lowered, linearised and grouped (lower.py
+// _lower_extend / sieve.py _bucket_state do the same in Python); otherwise the query is built
+// afresh.  Either way the result equals the from-scratch one (tests/test_query_native.py).
+class QueryState {
+public:
+    explicit QueryState(mh_terms& t) : Q(t) {}
+
+    void start(const uint32_t* rs, uint32_t n) {
+        roots.assign(rs, rs + n);
+        Q.harvest(roots);
+        for (uint32_t i = 0; i < n; ++i) {  // lower_query: the AND of the lowered roots
+            const uint32_t x = lowered(roots[i]);
+            root = i == 0 ? x : Q.add(AND, 0, root, x);
+        }
+        if (!n) root = Q.add(TRUE_, 0);
+        Q.linearise(root);
+        add_conjuncts(Q.lget(root));
+    }
+
+    bool extend(uint32_t r) {  // false: r changes the harvest, build afresh
+        Q.sync();
+        const Fingerprint before(Q);
+        Q.harvest({r});
+        if (!before.same(Q)) return false;
+        const uint32_t x = lowered(r);
+        roots.push_back(r);
+        root = Q.add(AND, 0, root, x);
+        Q.linearise(root);
+        add_conjuncts(Q.lget(x));
+        return true;
+    }
+
+    void emit(mh_query& q, uint32_t& flags);
+
+    Query Q;
+    std::vector<uint32_t> roots;
+
+private:
+    uint32_t lowered(uint32_t r) {
+        const uint32_t x = Q.lower(r);
+        if (Q.width(x) != 0 || (Q.nd(x).flags & F_ARRAY)) invalid("constraints must be Bool");
+        return x;
+    }
+    // new conjuncts: definitions flag, column-disjoint groups by a union-find over the conjuncts
+    // that reach a common node reading columns
+    void add_conjuncts(uint32_t tape_node) {
+        const size_t first = conj.size();
+        and_leaves(Q.tape, tape_node, conj);
+        owner.resize(Q.tape.size(), -1);
+        std::vector<uint32_t> st;
+        for (size_t i = first; i < conj.size(); ++i) {
+            uf.push_back((uint32_t)i);
+            defines = defines || may_define(Q.tape, Q.has_col, Q.cols, conj[i]);
+            st.assign(1, conj[i]);
+            while (!st.empty()) {
+                const uint32_t n = st.back();
+                st.pop_back();
+                if (!Q.has_col[n]) continue;
+                if (owner[n] >= 0) {
+                    const uint32_t a = find((uint32_t)i), b = find((uint32_t)owner[n]);
+                    uf[std::max(a, b)] = std::min(a, b);  // the earlier conjunct stays the root
+                    continue;
+                }
+                owner[n] = (int32_t)i;
+                const mh_node& x = Q.tape[n];
+                const uint32_t kids[3] = {x.a, x.b, x.c};
+                for (int j = 0; j < arity(x.op); ++j) st.push_back(kids[j]);
+            }
+        }
+    }
+    uint32_t find(uint32_t x) {
+        while (uf[x] != x) x = uf[x] = uf[uf[x]];
+        return x;
+    }
+
+    uint32_t root = 0;            // node id of the lowered conjunction
+    std::vector<uint32_t> conj;   // its AND leaves (tape nodes), in order
+    std::vector<int32_t> owner;   // per tape node: the first conjunct reaching it
+    std::vector<uint32_t> uf;     // union-find over conj
+    bool defines = false;
+};
+
+void QueryState::emit(mh_query& q, uint32_t& flags) {
     const std::vector<mh_node>& tape = Q.tape;
     const uint32_t N = (uint32_t)tape.size();
+    if (Q.lget(root) != N - 1) unsupported("the query's root is not the last node of its tape");
     for (const Column& c : Q.cols)  // a variable named like a cell would make two columns one
         if (c.kind == MH_COL_VAR && Q.cell_index.count(c.name))
             unsupported("variable " + c.name + " is named like an array cell");
-    // conjuncts: the AND leaves of the root, left to right (Sieve.conjuncts)
-    std::vector<uint32_t> conj, st{N - 1};
-    while (!st.empty()) {
-        const uint32_t n = st.back();
-        st.pop_back();
-        if (tape[n].op == AND) {
-            st.push_back(tape[n].b);
-            st.push_back(tape[n].a);
-        } else {
-            conj.push_back(n);
-        }
-    }
-    for (uint32_t cj : conj)
-        if (may_define(tape, Q.has_col, Q.cols, cj)) flags |= MH_QUERY_DEFINITIONS;
+    if (defines) flags |= MH_QUERY_DEFINITIONS;
     if (refuted(Q, conj)) flags |= MH_QUERY_REFUTED;
-    // column-disjoint groups: conjuncts that reach a common node reading columns share a group
-    std::vector<int32_t> owner(N, -1);
-    std::vector<uint32_t> uf(conj.size());
-    for (uint32_t i = 0; i < uf.size(); ++i) uf[i] = i;
-    auto find = [&](uint32_t x) {
-        while (uf[x] != x) x = uf[x] = uf[uf[x]];
-        return x;
-    };
-    for (uint32_t i = 0; i < conj.size(); ++i) {
-        st.assign(1, conj[i]);
-        while (!st.empty()) {
-            const uint32_t n = st.back();
-            st.pop_back();
-            if (!Q.has_col[n]) continue;
-            if (owner[n] >= 0) {
-                const uint32_t a = find(i), b = find((uint32_t)owner[n]);
-                uf[std::max(a, b)] = std::min(a, b);  // the earlier conjunct stays the root
-                continue;
-            }
-            owner[n] = (int32_t)i;
-            const mh_node& x = tape[n];
-            const uint32_t kids[3] = {x.a, x.b, x.c};
-            for (int j = 0; j < arity(x.op); ++j) st.push_back(kids[j]);
-        }
-    }
     std::vector<std::vector<uint32_t>> gconj;  // conjunct tape nodes per group, path order
     std::unordered_map<int64_t, uint32_t> gid;
     std::vector<uint32_t> group_of(conj.size(), UINT32_MAX);  // by union-find root
@@ -1153,8 +1249,6 @@ void build(Query& Q, const uint32_t* roots, uint32_t n_roots, mh_query& q, uint3
     }
 }
 
-}  // namespace
-
 extern "C" {
 
 int32_t mh_terms_create(mh_terms** out) {
@@ -1233,13 +1327,24 @@ int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_
     if (!q) return mh_detail_set_err(MH_E_NOMEM, "mh_query_build");
     uint32_t flags = 0;
     try {
-        Query Q(*t);
-        build(Q, roots, n_roots, *q, flags);
+        QueryState* st = t->last.get();
+        // a child of the last query (its roots plus one) extends it when the harvest is unchanged
+        const bool child = st && n_roots == st->roots.size() + 1 &&
+                           std::equal(st->roots.begin(), st->roots.end(), roots);
+        if (!child || !st->extend(roots[n_roots - 1])) {
+            t->last.reset();  // a fresh query starts a new epoch of the scratch maps
+            t->last.reset(new QueryState(*t));
+            t->last->start(roots, n_roots);
+        }
+        t->last->emit(*q, flags);
     } catch (const Fail& f) {
+        t->last.reset();
         return mh_detail_set_err(f.code, f.msg.c_str());
     } catch (const std::out_of_range&) {
+        t->last.reset();
         return mh_detail_set_err(MH_E_INVALID, "malformed term store (index out of range)");
     } catch (const std::bad_alloc&) {
+        t->last.reset();
         return mh_detail_set_err(MH_E_NOMEM, "mh_query_build");
     }
     mh_query* r = q.release();
