@@ -192,6 +192,21 @@ int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, const uint32_t*
                          const uint32_t* parent_cols, const uint32_t* parent_vals,
                          uint32_t n_parent, mh_harvest** out, mh_guide* guide);
 int32_t mh_harvest_free(mh_harvest* h);
+/* The same harvest by a session kept across a path's queries: when the tape, the constants and
+ * the column widths extend the last call's (a LASER child whose new constraint left its parent's
+ * lowering unchanged: mh_query_build then emits the parent's tape as a prefix), the memoised
+ * inversions of the earlier conjuncts are reused and only the new ones are computed; otherwise the
+ * session starts afresh.  The guide is the one mh_guide_harvest gives for the same arguments.
+ * mh_harvester_stats: [calls that extended, calls that started afresh, arena bytes held].         */
+typedef struct mh_harvester mh_harvester;
+int32_t mh_harvester_create(mh_harvester** out);
+int32_t mh_harvester_destroy(mh_harvester* s);
+int32_t mh_harvester_stats(const mh_harvester* s, uint64_t* out /* [3] */);
+int32_t mh_guide_harvest_with(mh_harvester* s, const mh_node* nodes, uint32_t n_nodes,
+                              const uint32_t* consts, uint32_t n_consts, const uint16_t* col_width,
+                              uint32_t n_cols, const uint32_t* parent_cols,
+                              const uint32_t* parent_vals, uint32_t n_parent, mh_harvest** out,
+                              mh_guide* guide);
 
 /* ---- SMT-LIB import (the product path's first stage) -----------------------------------------
  * Replaces the Python SMT-LIB reader behind mythril_amd/smtlib.Z3Importer, which imports every

@@ -142,7 +142,8 @@ U inverse_mod(const U& k, int w) {
 }
 
 // One harvest allocates thousands of small vectors (alternatives, memo entries) and frees them
-// all at the end: they come from a per-thread bump arena that mh_guide_harvest resets.
+// all at the end: they come from a bump arena -- per thread, reset by mh_guide_harvest, or a
+// harvester session's own, kept while its memo is (mh_harvester).
 struct Arena {
     std::vector<std::unique_ptr<char[]>> blocks;
     std::vector<size_t> sizes;
@@ -171,8 +172,14 @@ struct Arena {
             sizes.pop_back();
         }
     }
+    size_t used() const {
+        size_t n = off;
+        for (size_t i = 0; i < cur && i < sizes.size(); ++i) n += sizes[i];
+        return n;
+    }
 };
 thread_local Arena g_arena;
+thread_local Arena* g_cur = &g_arena;  // the arena ArenaAlloc draws from
 
 template <class T>
 struct ArenaAlloc {
@@ -180,7 +187,7 @@ struct ArenaAlloc {
     ArenaAlloc() = default;
     template <class O>
     ArenaAlloc(const ArenaAlloc<O>&) {}
-    T* allocate(size_t n) { return static_cast<T*>(g_arena.alloc(n * sizeof(T), alignof(T))); }
+    T* allocate(size_t n) { return static_cast<T*>(g_cur->alloc(n * sizeof(T), alignof(T))); }
     void deallocate(T*, size_t) {}
     template <class O>
     bool operator==(const ArenaAlloc<O>&) const { return true; }
@@ -314,6 +321,18 @@ struct Harvester {
     std::vector<std::vector<std::vector<Copy>>> copy_sets;
     std::vector<U> query_consts;
     std::map<int, std::vector<U>> consts_by_width;
+
+    // a kept harvester's next query (its tape extends the last one's): the memo, interned values
+    // and hint ids stay, the query's own sets and hints start empty
+    void begin_query() {
+        sets.clear();
+        hints.clear();
+        std::fill(hint_done.begin(), hint_done.end(), 0);
+        n_hints = 0;
+        copy_sets.clear();
+        query_consts.clear();
+        consts_by_width.clear();
+    }
 
     static int arity(uint8_t op) {  // tape.py ARITY (lowered tapes hold no host-only ops)
         switch (op) {
@@ -999,111 +1018,226 @@ struct mh_harvest {  // owns the arrays an mh_guide from mh_guide_harvest points
 
 int32_t mh_detail_set_err(int32_t code, const char* msg);  // capi.cpp
 
+namespace {
+
+// Append the tape nodes, constants and column widths beyond what h holds (a fresh harvester holds
+// none), harvest, and fill *out / *guide.
+int32_t harvest_into(Harvester& h, const mh_node* nodes, uint32_t n_nodes, const uint32_t* consts,
+                     uint32_t n_consts, const uint16_t* col_width, uint32_t n_cols,
+                     const uint32_t* parent_cols, const uint32_t* parent_vals, uint32_t n_parent,
+                     mh_harvest** out, mh_guide* guide) {
+    const uint32_t n0 = (uint32_t)h.nd.size();
+    h.nd.resize(n_nodes);
+    for (uint32_t i = n0; i < n_nodes; ++i) {
+        const mh_node& s = nodes[i];
+        Node& d = h.nd[i];
+        d.op = s.op; d.width = s.width; d.a = s.a; d.b = s.b; d.c = s.c;
+        d.imm0 = s.imm0; d.imm1 = s.imm1;
+        const int k = Harvester::arity(s.op);
+        if (s.width > 1088 || (k >= 1 && s.a >= i) || (k >= 2 && s.b >= i) ||
+            (k >= 3 && s.c >= i) || (s.op == CONST && s.imm0 >= n_consts) ||
+            (s.op == EXTRACT && (s.imm1 > s.imm0 || s.imm0 >= 1088)) ||
+            ((s.op == ZEXT || s.op == SEXT) && s.imm0 > 1088))
+            return mh_detail_set_err(MH_E_INVALID, "malformed tape node");
+        // bit-layout operands are bit-vectors (the harvest reads their top bit / width)
+        if ((s.op == EXTRACT || s.op == ZEXT || s.op == SEXT || s.op == CONCAT) &&
+            (h.nd[s.a].width == 0 || (s.op == CONCAT && h.nd[s.b].width == 0)))
+            return mh_detail_set_err(MH_E_INVALID, "bit-layout op over a Bool operand");
+    }
+    const uint32_t c0 = (uint32_t)h.pool.size();
+    h.pool.resize(n_consts);
+    for (uint32_t i = c0; i < n_consts; ++i)
+        for (int k = 0; k < 8; ++k) h.pool[i].w[k] = consts[8ull * i + k];
+    h.cv_state.resize(n_nodes, 0);
+    h.cv.resize(n_nodes);
+    h.n_cols = n_cols;
+    h.widths.assign(col_width, col_width + n_cols);
+    for (uint16_t w : h.widths)
+        if (w < 1 || w > 256) return mh_detail_set_err(MH_E_INVALID, "column width not 1..256");
+    Alt parent;
+    for (uint32_t i = 0; i < n_parent; ++i) {
+        if (parent_cols[i] >= n_cols)
+            return mh_detail_set_err(MH_E_INVALID, "parent column out of range");
+        V v;
+        for (int k = 0; k < 8; ++k) v.w[k] = parent_vals[8ull * i + k];
+        parent.push_back({parent_cols[i], v});
+    }
+    std::vector<std::vector<V>> pools;
+    std::vector<std::pair<int, const Alts*>> sets;
+    std::vector<std::vector<std::vector<Copy>>> copies;
+    h.harvest(n_nodes - 1, n_parent ? &parent : nullptr, pools, sets, copies);
+    auto r = std::make_unique<mh_harvest>();
+    r->width16.assign(h.widths.begin(), h.widths.end());
+    r->pool_off.push_back(0);
+    auto put = [](std::vector<uint32_t>& dst, const V& v) { dst.insert(dst.end(), v.w, v.w + 8); };
+    for (const auto& p : pools) {
+        for (const V& v : p) put(r->pool, v);
+        r->pool_off.push_back((uint32_t)(r->pool.size() / 8));
+    }
+    r->set_off.push_back(0);
+    r->alt_off.push_back(0);
+    for (const auto& s : sets) {
+        r->set_prob.push_back((uint8_t)s.first);
+        for (const Alt& a : *s.second) {
+            for (const auto& kv : a) {
+                r->entry_col.push_back(kv.first);
+                put(r->entry_val, kv.second);
+            }
+            r->alt_off.push_back((uint32_t)r->entry_col.size());
+        }
+        r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
+    }
+    for (const auto& alts : copies) {
+        r->set_prob.push_back((uint8_t)kProbDefault);
+        for (const auto& alt : alts) {
+            for (const Copy& c : alt) {
+                r->entry_col.push_back(c.dst | kCopyFlag);
+                const uint32_t ev[8] = {c.src, (uint32_t)c.dlo, (uint32_t)c.slo, (uint32_t)c.nb,
+                                        0, 0, 0, 0};
+                r->entry_val.insert(r->entry_val.end(), ev, ev + 8);
+            }
+            r->alt_off.push_back((uint32_t)r->entry_col.size());
+        }
+        r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
+    }
+    const uint32_t n_sets = (uint32_t)r->set_prob.size();
+    // never-empty arrays, as candidates.Guide.arrays() gives them (one zero entry)
+    if (r->pool.empty()) r->pool.assign(8, 0);
+    if (r->set_prob.empty()) r->set_prob.push_back(0);
+    if (r->entry_col.empty()) r->entry_col.push_back(0);
+    if (r->entry_val.empty()) r->entry_val.assign(8, 0);
+    guide->n_cols = n_cols;
+    guide->col_width = r->width16.data();
+    guide->pool_off = r->pool_off.data();
+    guide->pool = r->pool.data();
+    guide->n_sets = n_sets;
+    guide->set_prob = r->set_prob.data();
+    guide->set_off = r->set_off.data();
+    guide->alt_off = r->alt_off.data();
+    guide->entry_col = r->entry_col.data();
+    guide->entry_val = r->entry_val.data();
+    *out = r.release();
+    return MH_OK;
+}
+
+bool check_args(const mh_node* nodes, uint32_t n_nodes, const uint32_t* consts, uint32_t n_consts,
+                const uint16_t* col_width, uint32_t n_cols, const uint32_t* parent_cols,
+                const uint32_t* parent_vals, uint32_t n_parent) {
+    return nodes && n_nodes && (!n_consts || consts) && (!n_cols || col_width) &&
+           (!n_parent || (parent_cols && parent_vals));
+}
+
+}  // namespace
+
+// A harvester kept across the queries of a path: when a query's tape, constants and column widths
+// extend the last query's (a child of a LASER state whose constraint left its parent's lowering
+// as it was, query.cpp), the memoised inversions, interned values and hint ids of the earlier
+// queries stay valid (they are functions of the tape prefix) and only the new conjuncts are
+// inverted afresh; the guide is the one mh_guide_harvest gives (tests/test_harvest.py).
+struct mh_harvester {
+    Arena arena;
+    std::unique_ptr<Harvester> h;
+    std::vector<mh_node> nodes;
+    std::vector<uint32_t> consts;
+    std::vector<uint16_t> widths;
+    uint64_t reused = 0, fresh = 0;
+};
+
+namespace {
+constexpr size_t kSessionArenaBytes = (size_t)256 << 20;  // start afresh beyond this
+struct UseArena {  // ArenaAlloc draws from `a` while in scope
+    Arena* prev;
+    explicit UseArena(Arena* a) : prev(g_cur) { g_cur = a; }
+    ~UseArena() { g_cur = prev; }
+};
+}  // namespace
+
 extern "C" int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, const uint32_t* consts,
                                     uint32_t n_consts, const uint16_t* col_width, uint32_t n_cols,
                                     const uint32_t* parent_cols, const uint32_t* parent_vals,
                                     uint32_t n_parent, mh_harvest** out, mh_guide* guide) {
     if (!out || !guide) return mh_detail_set_err(MH_E_INVALID, "null out pointer");
     *out = nullptr;
-    if (!nodes || n_nodes == 0 || (n_consts && !consts) || (n_cols && !col_width) ||
-        (n_parent && (!parent_cols || !parent_vals)))
+    if (!check_args(nodes, n_nodes, consts, n_consts, col_width, n_cols, parent_cols, parent_vals,
+                    n_parent))
         return mh_detail_set_err(MH_E_INVALID, "null or empty argument");
     try {
+        UseArena use(&g_arena);
         struct ArenaReset {  // declared first: runs after every arena-backed local is gone
             ~ArenaReset() { g_arena.reset(); }
         } arena_reset;
         Harvester h;
-        h.nd.resize(n_nodes);
-        for (uint32_t i = 0; i < n_nodes; ++i) {
-            const mh_node& s = nodes[i];
-            Node& d = h.nd[i];
-            d.op = s.op; d.width = s.width; d.a = s.a; d.b = s.b; d.c = s.c;
-            d.imm0 = s.imm0; d.imm1 = s.imm1;
-            const int k = Harvester::arity(s.op);
-            if (s.width > 1088 || (k >= 1 && s.a >= i) || (k >= 2 && s.b >= i) ||
-                (k >= 3 && s.c >= i) || (s.op == CONST && s.imm0 >= n_consts) ||
-                (s.op == EXTRACT && (s.imm1 > s.imm0 || s.imm0 >= 1088)) ||
-                ((s.op == ZEXT || s.op == SEXT) && s.imm0 > 1088))
-                return mh_detail_set_err(MH_E_INVALID, "malformed tape node");
-            // bit-layout operands are bit-vectors (the harvest reads their top bit / width)
-            if ((s.op == EXTRACT || s.op == ZEXT || s.op == SEXT || s.op == CONCAT) &&
-                (h.nd[s.a].width == 0 || (s.op == CONCAT && h.nd[s.b].width == 0)))
-                return mh_detail_set_err(MH_E_INVALID, "bit-layout op over a Bool operand");
-        }
-        h.pool.resize(n_consts);
-        for (uint32_t i = 0; i < n_consts; ++i)
-            for (int k = 0; k < 8; ++k) h.pool[i].w[k] = consts[8ull * i + k];
-        h.cv_state.assign(n_nodes, 0);
-        h.cv.resize(n_nodes);
-        h.n_cols = n_cols;
-        h.widths.assign(col_width, col_width + n_cols);
-        for (uint16_t w : h.widths)
-            if (w < 1 || w > 256) return mh_detail_set_err(MH_E_INVALID, "column width not 1..256");
-        Alt parent;
-        for (uint32_t i = 0; i < n_parent; ++i) {
-            if (parent_cols[i] >= n_cols)
-                return mh_detail_set_err(MH_E_INVALID, "parent column out of range");
-            V v;
-            for (int k = 0; k < 8; ++k) v.w[k] = parent_vals[8ull * i + k];
-            parent.push_back({parent_cols[i], v});
-        }
-        std::vector<std::vector<V>> pools;
-        std::vector<std::pair<int, const Alts*>> sets;
-        std::vector<std::vector<std::vector<Copy>>> copies;
-        h.harvest(n_nodes - 1, n_parent ? &parent : nullptr, pools, sets, copies);
-        auto r = std::make_unique<mh_harvest>();
-        r->width16.assign(h.widths.begin(), h.widths.end());
-        r->pool_off.push_back(0);
-        auto put = [](std::vector<uint32_t>& dst, const V& v) { dst.insert(dst.end(), v.w, v.w + 8); };
-        for (const auto& p : pools) {
-            for (const V& v : p) put(r->pool, v);
-            r->pool_off.push_back((uint32_t)(r->pool.size() / 8));
-        }
-        r->set_off.push_back(0);
-        r->alt_off.push_back(0);
-        for (const auto& s : sets) {
-            r->set_prob.push_back((uint8_t)s.first);
-            for (const Alt& a : *s.second) {
-                for (const auto& kv : a) {
-                    r->entry_col.push_back(kv.first);
-                    put(r->entry_val, kv.second);
-                }
-                r->alt_off.push_back((uint32_t)r->entry_col.size());
-            }
-            r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
-        }
-        for (const auto& alts : copies) {
-            r->set_prob.push_back((uint8_t)kProbDefault);
-            for (const auto& alt : alts) {
-                for (const Copy& c : alt) {
-                    r->entry_col.push_back(c.dst | kCopyFlag);
-                    const uint32_t ev[8] = {c.src, (uint32_t)c.dlo, (uint32_t)c.slo, (uint32_t)c.nb,
-                                            0, 0, 0, 0};
-                    r->entry_val.insert(r->entry_val.end(), ev, ev + 8);
-                }
-                r->alt_off.push_back((uint32_t)r->entry_col.size());
-            }
-            r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
-        }
-        const uint32_t n_sets = (uint32_t)r->set_prob.size();
-        // never-empty arrays, as candidates.Guide.arrays() gives them (one zero entry)
-        if (r->pool.empty()) r->pool.assign(8, 0);
-        if (r->set_prob.empty()) r->set_prob.push_back(0);
-        if (r->entry_col.empty()) r->entry_col.push_back(0);
-        if (r->entry_val.empty()) r->entry_val.assign(8, 0);
-        guide->n_cols = n_cols;
-        guide->col_width = r->width16.data();
-        guide->pool_off = r->pool_off.data();
-        guide->pool = r->pool.data();
-        guide->n_sets = n_sets;
-        guide->set_prob = r->set_prob.data();
-        guide->set_off = r->set_off.data();
-        guide->alt_off = r->alt_off.data();
-        guide->entry_col = r->entry_col.data();
-        guide->entry_val = r->entry_val.data();
-        *out = r.release();
-        return MH_OK;
+        return harvest_into(h, nodes, n_nodes, consts, n_consts, col_width, n_cols, parent_cols,
+                            parent_vals, n_parent, out, guide);
     } catch (const std::bad_alloc&) {
+        return mh_detail_set_err(MH_E_NOMEM, "host allocation failed");
+    }
+}
+
+extern "C" int32_t mh_harvester_create(mh_harvester** out) {
+    if (!out) return mh_detail_set_err(MH_E_INVALID, "null out pointer");
+    *out = new (std::nothrow) mh_harvester();
+    return *out ? MH_OK : mh_detail_set_err(MH_E_NOMEM, "mh_harvester_create");
+}
+
+extern "C" int32_t mh_harvester_destroy(mh_harvester* s) {
+    if (!s) return mh_detail_set_err(MH_E_INVALID, "null harvester");
+    {
+        UseArena use(&s->arena);
+        s->h.reset();
+    }
+    delete s;
+    return MH_OK;
+}
+
+extern "C" int32_t mh_harvester_stats(const mh_harvester* s, uint64_t* out /* [3] */) {
+    if (!s || !out) return mh_detail_set_err(MH_E_INVALID, "null argument");
+    out[0] = s->reused;
+    out[1] = s->fresh;
+    out[2] = s->arena.used();
+    return MH_OK;
+}
+
+extern "C" int32_t mh_guide_harvest_with(mh_harvester* s, const mh_node* nodes, uint32_t n_nodes,
+                                         const uint32_t* consts, uint32_t n_consts,
+                                         const uint16_t* col_width, uint32_t n_cols,
+                                         const uint32_t* parent_cols, const uint32_t* parent_vals,
+                                         uint32_t n_parent, mh_harvest** out, mh_guide* guide) {
+    if (!s || !out || !guide) return mh_detail_set_err(MH_E_INVALID, "null argument");
+    *out = nullptr;
+    if (!check_args(nodes, n_nodes, consts, n_consts, col_width, n_cols, parent_cols, parent_vals,
+                    n_parent))
+        return mh_detail_set_err(MH_E_INVALID, "null or empty argument");
+    UseArena use(&s->arena);
+    try {
+        const size_t pn = s->nodes.size(), pc = s->consts.size() / 8, pw = s->widths.size();
+        const bool extends = s->h && n_nodes >= pn && n_consts >= pc && n_cols >= pw &&
+                             s->arena.used() < kSessionArenaBytes &&
+                             memcmp(nodes, s->nodes.data(), pn * sizeof(mh_node)) == 0 &&
+                             memcmp(consts, s->consts.data(), pc * 32) == 0 &&
+                             memcmp(col_width, s->widths.data(), pw * sizeof(uint16_t)) == 0;
+        if (extends) {
+            s->h->begin_query();
+            ++s->reused;
+        } else {
+            s->h.reset();
+            s->arena.reset();
+            s->h.reset(new Harvester());
+            ++s->fresh;
+        }
+        s->nodes.assign(nodes, nodes + n_nodes);
+        s->consts.assign(consts, consts + 8ull * n_consts);
+        s->widths.assign(col_width, col_width + n_cols);
+        const int32_t r = harvest_into(*s->h, nodes, n_nodes, consts, n_consts, col_width, n_cols,
+                                       parent_cols, parent_vals, n_parent, out, guide);
+        if (r != MH_OK) {  // a malformed tape leaves nothing to extend
+            s->h.reset();
+            s->nodes.clear();
+        }
+        return r;
+    } catch (const std::bad_alloc&) {
+        s->h.reset();
+        s->nodes.clear();
         return mh_detail_set_err(MH_E_NOMEM, "host allocation failed");
     }
 }

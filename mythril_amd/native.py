@@ -82,6 +82,12 @@ SIGNATURES = {
     "mh_guide_harvest": (C.c_int32, [_vp, C.c_uint32, _u32p, C.c_uint32, C.POINTER(C.c_uint16),
                                      C.c_uint32, _u32p, _u32p, C.c_uint32, C.POINTER(_vp), _vp]),
     "mh_harvest_free": (C.c_int32, [_vp]),
+    "mh_harvester_create": (C.c_int32, [C.POINTER(_vp)]),
+    "mh_harvester_destroy": (C.c_int32, [_vp]),
+    "mh_harvester_stats": (C.c_int32, [_vp, _u64p]),
+    "mh_guide_harvest_with": (C.c_int32, [_vp, _vp, C.c_uint32, _u32p, C.c_uint32,
+                                          C.POINTER(C.c_uint16), C.c_uint32, _u32p, _u32p,
+                                          C.c_uint32, C.POINTER(_vp), _vp]),
     "mh_smtlib_create": (C.c_int32, [C.POINTER(_vp)]),
     "mh_smtlib_destroy": (C.c_int32, [_vp]),
     "mh_smtlib_read": (C.c_int32, [_vp, C.c_char_p, C.c_uint64, _vp]),
@@ -192,11 +198,14 @@ def _limb_rows(vals) -> np.ndarray:
 
 
 def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
-                  parent: Sequence[Tuple[int, int]] = ()) -> dict:
+                  parent: Sequence[Tuple[int, int]] = (), session: "Optional[GuideSession]" = None
+                  ) -> dict:
     """mh_guide_harvest: the guide of one lowered query tape (root last, VAR imm0 = column,
     CONST imm0 = row of `consts`), as the arrays candidates.Guide.arrays() gives -- the same
     values (tests/test_harvest.py).  `parent` = the parent witness as (column, value) pairs in
-    the witness's order.  Host-only: no device is touched."""
+    the witness's order.  With `session` (a GuideSession) the harvest reuses the session's memo
+    when the tape extends the last one (mh_guide_harvest_with; the same arrays).  Host-only: no
+    device is touched."""
     lib = load()
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
     consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1, 8)
@@ -205,9 +214,13 @@ def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
     pv = _limb_rows([v for _, v in parent]) if len(parent) else np.zeros((1, 8), np.uint32)
     h = C.c_void_p()
     g = Guide()
-    _check(lib.mh_guide_harvest(nodes.ctypes.data, len(nodes), _ptr(consts), len(consts),
-                                w.ctypes.data_as(C.POINTER(C.c_uint16)), len(w), _ptr(pc),
-                                _ptr(pv), len(pc), C.byref(h), C.byref(g)))
+    args = (nodes.ctypes.data, len(nodes), _ptr(consts), len(consts),
+            w.ctypes.data_as(C.POINTER(C.c_uint16)), len(w), _ptr(pc), _ptr(pv), len(pc),
+            C.byref(h), C.byref(g))
+    if session is None:
+        _check(lib.mh_guide_harvest(*args))
+    else:
+        _check(lib.mh_guide_harvest_with(session.h, *args))
     try:
         def arr(p, n, dt=np.uint32):
             return np.ctypeslib.as_array(p, (n,)).astype(dt, copy=True)
@@ -224,6 +237,33 @@ def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
             entry_col=arr(g.entry_col, n_entries), entry_val=arr(g.entry_val, 8 * n_entries).reshape(-1, 8))
     finally:
         lib.mh_harvest_free(h)
+
+
+class GuideSession:
+    """An mh_harvester: guide harvests that reuse the memo of the path's earlier queries."""
+
+    def __init__(self):
+        self.lib = load()
+        h = C.c_void_p()
+        _check(self.lib.mh_harvester_create(C.byref(h)))
+        self.h = h
+
+    def stats(self) -> Tuple[int, int, int]:
+        """(harvests that extended the last tape, harvests that started afresh, arena bytes)."""
+        out = (C.c_uint64 * 3)()
+        _check(self.lib.mh_harvester_stats(self.h, out))
+        return int(out[0]), int(out[1]), int(out[2])
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.mh_harvester_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class SmtlibSession:

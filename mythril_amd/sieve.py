@@ -3,10 +3,14 @@
 For one query (the tuple of Bool constraints ``Constraints.is_possible`` hands to ``get_model``,
 mythril/laser/ethereum/state/constraints.py:25-35, support/model.py:15-62):
 
-1. lower arrays / keccak UFs onto scalar columns (lower.py) — ``LoweringUnsupported`` -> None;
+1. lower arrays / keccak UFs onto scalar columns, split the conjuncts into column-disjoint groups
+   and linearise the tapes -- in one native call (mh_query_build, csrc/query.cpp; the Python
+   stages lower.py / buckets / local_tapeset are its reference and the definitions path);
+   unsupported constructs -> the fallback, a self-contradicting query -> no device round;
 2. harvest a candidate guide from the lowered term and the parent query's witness
-   (mh_guide_harvest, harvest.cpp -- the algorithm of candidates.py, same arrays);
-3. compile the conjunction as one device tape over the query's own columns (mh_tapes_compile);
+   (mh_guide_harvest_with, harvest.cpp -- the algorithm of candidates.py, same arrays; the
+   session reuses the inversions of the path's earlier queries);
+3. compile the group tapes over the query's own columns (mh_tapes_compile);
 4. two launches at most: ``first_rows`` guided rows (mh_assign_generate_guided), then, when a
    group is still unsolved, the remaining ``(max_rounds - 1) * rows`` rows in ONE launch; each
    runs the tapes in MH_MODE_FIRST_HIT and reads back the smallest satisfying row per group
@@ -396,6 +400,8 @@ class Sieve:
         # host stages by the native query compiler (csrc/query.cpp); False: the Python stages
         # (lower.py, buckets, local_tapeset) it is checked against (tests/test_query_native.py)
         self.native_query = native_query
+        # guide harvests that reuse the memo of the path's earlier queries (mh_harvester)
+        self.guides = native.GuideSession()
         self.rows = rows
         # the harvested guide usually solves a LASER query in its first rows (round 1 found every
         # SAT witness of tests/laser_like.py within the first 16 rows): a small first round
@@ -417,6 +423,7 @@ class Sieve:
         if self.assign is not None:
             self.assign.close()
             self.assign = None
+        self.guides.close()
         self.ctx.close()
 
     def _buffer(self, n_cols: int) -> native.Assignments:
@@ -610,7 +617,8 @@ class Sieve:
         parent = self.witnesses.get(key[:-1]) if key else None
         guide = native.harvest_guide(
             root_nodes, ts.pool.to_array(), widths,
-            [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else ())
+            [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else (),
+            session=self.guides)
         t1 = time.perf_counter()
         st.add("guide", t1 - t_t)
         self.stats.host_s += t1 - t0

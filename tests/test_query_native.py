@@ -9,6 +9,7 @@ same harvested tables (every array / function key, keccak bases and pairs), the 
 column-disjoint groups and the SAME tapes once column and constant numbering are read by name and
 value: node for node, operand for operand.  Host-only (no device); the library must be built.
 """
+import numpy as np
 import pytest
 
 from mythril_amd import native
@@ -287,3 +288,45 @@ def test_refutation_is_sound_on_random_conjunctions():
             assign = [dict(zip("xyz", vals)).get(n, 0) for n in names]
             assert not E.evaluate(tape.nodes, ctx.b.pool.values, assign), (trial, vals)
     assert flagged >= 10
+
+
+def _guide_equal(a, b):
+    return a.keys() == b.keys() and all(np.array_equal(a[k], b[k]) for k in a)
+
+
+@pytest.mark.parametrize("shape", ["killbilly", "overflow", "ether_thief"])
+def test_guide_session_matches_fresh_harvest(shape):
+    """mh_guide_harvest_with (a harvester kept across a path's queries) gives the arrays of
+    mh_guide_harvest on every query of a grown path in LASER order, with and without a parent
+    witness, and reuses its memo for the children that extend their parent's tape."""
+    import random
+
+    ctx, cs = grow(shape, 60)
+    nodes = [c.node for c in cs]
+    sess = native.GuideSession()
+    rng = random.Random(5)
+    m = native.TermMirror.of(ctx.b)
+    for k in range(1, len(nodes) + 1):
+        cq = m.build(ctx.b, nodes[:k])
+        parent = [(c, rng.getrandbits(int(cq.widths[c]))) for c in range(len(cq.names))
+                  if rng.random() < 0.3] if k % 2 else ()
+        want = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, parent)
+        got = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, parent, session=sess)
+        assert _guide_equal(got, want), (shape, k)
+    reused, fresh, _ = sess.stats()
+    assert reused > len(nodes) // 2, (reused, fresh)
+    sess.close()
+
+
+def test_guide_session_laser_like():
+    ctx, qs = laser_like.queries()
+    sess = native.GuideSession()
+    m = native.TermMirror.of(ctx.b)
+    for name, cs in qs:
+        nodes = [c.node for c in cs]
+        for k in range(1, len(nodes) + 1):
+            cq = m.build(ctx.b, nodes[:k])
+            want = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths)
+            got = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, session=sess)
+            assert _guide_equal(got, want), (name, k)
+    sess.close()
