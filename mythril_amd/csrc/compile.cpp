@@ -1322,25 +1322,44 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
 // A tape that runs out of registers is retried without held columns (Lowering::hold_vars), then
 // with cheap shared sub-terms duplicated at their uses, widening what counts as cheap (8, 32, 256
 // nodes) -- each size first with held columns, then without.
+// The attempt that fitted the last tape compiled on this thread is tried first: a LASER query's
+// tapes grow by one conjunct per query (svm.py:257-262), and a long path's tape needs the same
+// rematerialisation as its parent's, so the attempts that ran out of registers for the parent are
+// not repeated for every child (the code differs, the values do not).
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                      uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                      std::unordered_map<std::string, uint32_t>& dconst_index,
                      std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
+    static thread_local int hint = 0;  // index into the attempt list of the last success
     const bool hold = n_vars > MH_MAX_PRELOAD && !std::getenv("MH_NO_HOLD_VARS");
+    static const uint32_t kSizes[4] = {0u, 8u, 32u, 256u};
+    std::vector<int> order;
+    for (int a = 0; a < 8; ++a)
+        if (!((a & 1) == 0 && !hold)) order.push_back(a);  // a = 2 * size index + (no hold)
+    auto it = std::find(order.begin(), order.end(), hint);
+    if (it != order.end()) std::rotate(order.begin(), it, it + 1);  // the hint first, then in order
     int32_t r = MH_E_UNSUPPORTED;
-    for (uint32_t sz : {0u, 8u, 32u, 256u}) {
+    const size_t words0 = words.size(), dconsts0 = dconsts.size();
+    for (int a : order) {
+        const uint32_t sz = kSizes[a >> 1];
+        const bool h = (a & 1) == 0;
         std::vector<mh_node> t2;
         if (sz) t2 = rematerialize(nodes, n_nodes, sz);
         const mh_node* tn = sz ? t2.data() : nodes;
         const size_t nn = sz ? t2.size() : n_nodes;
-        for (bool h : {true, false}) {
-            if (h && !hold) continue;
-            err.clear();
-            r = compile_tape_once(tn, nn, consts, n_consts, n_vars, dconsts, dconst_index, words,
-                                  out, err, h);
-            out.n_nodes = (uint32_t)n_nodes;
-            if (r != MH_E_UNSUPPORTED || err.find("register pressure") == std::string::npos)
-                return r;
+        err.clear();
+        words.resize(words0);  // a failed attempt leaves nothing behind
+        if (dconsts.size() != dconsts0) {
+            dconsts.resize(dconsts0);
+            for (auto i = dconst_index.begin(); i != dconst_index.end();)
+                i = i->second >= dconsts0 / 8 ? dconst_index.erase(i) : std::next(i);
+        }
+        r = compile_tape_once(tn, nn, consts, n_consts, n_vars, dconsts, dconst_index, words, out,
+                              err, h);
+        out.n_nodes = (uint32_t)n_nodes;
+        if (r != MH_E_UNSUPPORTED || err.find("register pressure") == std::string::npos) {
+            if (r == MH_OK) hint = a;
+            return r;
         }
     }
     return r;
