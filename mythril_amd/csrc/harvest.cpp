@@ -321,6 +321,9 @@ struct Harvester {
     std::vector<std::vector<std::vector<Copy>>> copy_sets;
     std::vector<U> query_consts;
     std::map<int, std::vector<U>> consts_by_width;
+    std::map<int, std::vector<uint32_t>> const_ids_by_width;  // their interned ids
+    // eq_nodes per conjunct (a function of the tape prefix: kept across a session's queries)
+    std::unordered_map<uint32_t, std::vector<uint32_t>> eq_nodes_of;
 
     // a kept harvester's next query (its tape extends the last one's): the memo, interned values
     // and hint ids stay, the query's own sets and hints start empty
@@ -332,6 +335,7 @@ struct Harvester {
         copy_sets.clear();
         query_consts.clear();
         consts_by_width.clear();
+        const_ids_by_width.clear();
     }
 
     static int arity(uint8_t op) {  // tape.py ARITY (lowered tapes hold no host-only ops)
@@ -400,7 +404,12 @@ struct Harvester {
     }
 
     Res invert_bits(uint32_t n, const U& value, const U& msk, int depth = 0) {
-        return memoised(Key{0u, n, intern(value), intern(msk)}, [&]() {
+        return invert_bits_ids(n, intern(value), intern(msk), value, msk, depth);
+    }
+    // the same with the value and mask already interned (the eq loop's constants)
+    Res invert_bits_ids(uint32_t n, uint32_t vid, uint32_t mid, const U& value, const U& msk,
+                        int depth = 0) {
+        return memoised(Key{0u, n, vid, mid}, [&]() {
             return depth < 64 ? invert_bits_(n, value & msk, msk, depth) : none_();
         });
     }
@@ -790,6 +799,15 @@ struct Harvester {
         return consts_by_width[w] = std::move(vals);
     }
 
+    const std::vector<uint32_t>& const_ids_of_width(int w) {
+        auto it = const_ids_by_width.find(w);
+        if (it != const_ids_by_width.end()) return it->second;
+        std::vector<uint32_t> ids;
+        const U m = mask(w);
+        for (const U& k : consts_of_width(w)) ids.push_back(intern(k & m));
+        return const_ids_by_width[w] = std::move(ids);
+    }
+
     void harvest(uint32_t root, const Alt* parent, std::vector<std::vector<V>>& pools,
                  std::vector<std::pair<int, const Alts*>>& out_sets,
                  std::vector<std::vector<std::vector<Copy>>>& out_copies) {
@@ -824,7 +842,9 @@ struct Harvester {
                 for (const Alt& a : alts.alts()) if (!a.empty()) kept.push_back(a);
                 sets.push_back({kProbDefault, head(kept, kMaxAlts)});
             }
-            for (uint32_t n : eq_nodes(cj)) {
+            auto eqn = eq_nodes_of.find(cj);
+            if (eqn == eq_nodes_of.end()) eqn = eq_nodes_of.emplace(cj, eq_nodes(cj)).first;
+            for (uint32_t n : eqn->second) {
                 if (seen_eq[n]) continue;
                 seen_eq[n] = 1;
                 uint32_t x = nd[n].a, y = nd[n].b;
@@ -837,9 +857,14 @@ struct Harvester {
                     if ((int)copy_sets.size() < kMaxSets / 4) copy_sets.push_back(std::move(calts));
                     continue;
                 }
-                for (const U& k : consts_of_width(w)) {
-                    Res rx = invert_bits(x, k, mask(w));
-                    Res ry = invert_bits(y, k, mask(w));
+                const std::vector<U>& ks = consts_of_width(w);
+                const std::vector<uint32_t>& kids = const_ids_of_width(w);
+                const U mw = mask(w);
+                const uint32_t mid = intern(mw);
+                for (size_t ki = 0; ki < ks.size(); ++ki) {
+                    const U& k = ks[ki];
+                    Res rx = invert_bits_ids(x, kids[ki], mid, k, mw);
+                    Res ry = invert_bits_ids(y, kids[ki], mid, k, mw);
                     if (!rx.none && !rx.alts().empty() && !ry.none && !ry.alts().empty()) {
                         Alts both = merge(rx.alts(), ry.alts());
                         if (!both.empty() && !is_only_empty(both))

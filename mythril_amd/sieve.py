@@ -657,11 +657,13 @@ class Sieve:
                     row = hit - base
                     if row not in rows_read:
                         td = time.perf_counter()
-                        rows_read[row] = assign.download(row, 1)
+                        # the row's columns as 32 little-endian bytes each
+                        rows_read[row] = np.ascontiguousarray(
+                            assign.download(row, 1)[:len(columns), :, 0], dtype="<u4").tobytes()
                         st.add("download", time.perf_counter() - td)
-                    vals = rows_read[row]
+                    raw = rows_read[row]
                     for c in group_cols[g]:
-                        values[columns[c]] = _limbs(vals[c, :, 0])
+                        values[columns[c]] = int.from_bytes(raw[32 * c:32 * c + 32], "little")
                     solved[g] = True
                     first_index = hit if first_index is None else min(first_index, hit)
                 if all(solved):
