@@ -643,15 +643,20 @@ class Sieve:
                 ta = time.perf_counter()
                 assign.generate_guided(self.seed, guide, global_base=base, count=n)
                 tb = time.perf_counter()
+                # a later round runs only the tapes from the first to the last unsolved group
+                g0 = solved.index(False)
+                g1 = len(solved) - solved[::-1].index(False)
                 fh, _ = native.run(self.ctx, ct, assign, mode=native.MODE_FIRST_HIT,
-                                   index_base=base, row_count=n)
+                                   index_base=base, row_count=n, tape_first=g0,
+                                   tape_count=g1 - g0)
+                fh = [native.NO_HIT] * g0 + fh.tolist()
                 tr = time.perf_counter()
                 st.add("generate", tb - ta)
                 st.add("run", tr - tb)
                 self.stats.rounds += 1
                 self.stats.rows += n
                 rows_read: Dict[int, np.ndarray] = {}
-                for g, hit in enumerate(fh.tolist()):
+                for g, hit in enumerate(fh):
                     if solved[g] or hit == native.NO_HIT:
                         continue
                     row = hit - base

@@ -83,3 +83,27 @@ def test_refuted_query_skips_the_device(monkeypatch):
     cs = dict(qs)["ether_thief_unsat"]
     assert s.solve(ctx.b, [c.node for c in cs]) is None
     assert s.stats.rounds == r0 + 2 and s.stats.misses == 3
+
+
+def test_later_round_runs_only_unsolved_groups(monkeypatch):
+    """Round 2 (2^16 rows in the product) launches only the tapes from the first to the last
+    group round 1 left unsolved: here group 0 (x == 5) is solved by the guide, group 1
+    (y * y == 2, no solution mod 2^256) is not."""
+    from mythril_amd import native, smt
+    from mythril_amd.smt import symbol_factory
+
+    fake_device.install(monkeypatch)
+    calls = []
+    real = native.run
+
+    def recording(ctx, tapes, assign, **kw):
+        calls.append((kw.get("tape_first", 0), kw.get("tape_count")))
+        return real(ctx, tapes, assign, **kw)
+
+    monkeypatch.setattr(native, "run", recording)
+    ctx = smt.set_context(smt.Context())
+    x = symbol_factory.BitVecSym("x", 256)
+    y = symbol_factory.BitVecSym("y", 256)
+    s = Sieve(rows=64, first_rows=64, budget_s=60.0)
+    assert s.solve(ctx.b, [(x == 5).node, (y * y == 2).node]) is None
+    assert calls == [(0, 2), (1, 1)]
