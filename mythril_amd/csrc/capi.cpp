@@ -867,8 +867,30 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
                                    d_first_hit, d_hit_count, nullptr))
             return r;
     }
-    // one launch per kernel-variant bucket
-    for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+    // one launch per kernel-variant bucket; a short run over the whole set (a query's guided
+    // first round) is one launch of the variant that covers them all -- the register classes and
+    // the feature sets nest (kernels.h variant_of), and the ids are laid out bucket by bucket in
+    // the order of their words, so the whole id list is one contiguous word range
+    static const uint64_t merge_rows = [] {
+        const char* e = std::getenv("MH_MERGE_ROWS");
+        return e ? std::strtoull(e, nullptr, 10) : 4096ull;
+    }();
+    uint32_t n_buckets = 0, vmax_nr = 0, vmax_fc = 0;
+    for (uint32_t v = 0; v < mh::kNumVariants; ++v)
+        if (hi[v] != lo[v]) {
+            ++n_buckets;
+            vmax_nr = std::max(vmax_nr, v / 4);
+            vmax_fc = std::max(vmax_fc, v % 4);
+        }
+    const uint32_t vmerged = vmax_nr * 4 + vmax_fc;
+    if (!use_jit && n_buckets > 1 && row_count <= merge_rows && tape_first == 0 &&
+        tape_count == ts->n_tapes && mh::variant_fits(vmerged, p.capacity)) {
+        p.tape_ids = d_ids;
+        p.n_ids = (uint32_t)ids.size();
+        MH_HIP(mh::launch_sieve(p, vmerged, ctx->stream));
+        n_buckets = 0;
+    }
+    for (uint32_t v = 0; v < mh::kNumVariants && n_buckets; ++v) {
         if (hi[v] == lo[v]) continue;
         p.tape_ids = d_ids + (lo[v] - ids.data());
         p.n_ids = (uint32_t)(hi[v] - lo[v]);

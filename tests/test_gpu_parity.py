@@ -619,3 +619,40 @@ def test_capacity_above_2_30_rows(gpu_ctx):
         a.close()
         ct.close()
         ctc.close()
+
+
+def test_merged_short_run_matches_per_variant(gpu_ctx):
+    """A short run over the whole tape set is one launch of the variant covering every tape
+    (capi.cpp mh_run_async, MH_MERGE_ROWS); over a sub-range it is one launch per variant.  Both
+    give the oracle's counts and first witnesses on a set mixing plain, division, keccak and EVM
+    tapes (every register class the fuzzer reaches)."""
+    rng = random.Random(4242)
+    ts = TapeSet()
+    fz = TapeFuzzer(rng, ts, n_vars=3, max_depth=4)
+    for _ in range(24):
+        fz.tape()
+    b = ts.builder()
+    x, y = b.var("v0"), b.var("v1")
+    ts.add(b.finish(b.op(Op.EQ, b.op(Op.BVAND, b.op(Op.KECCAK, x), b.const(3, 256)),
+                         b.const(1, 256))))
+    ts.add(b.finish(b.op(Op.BVULT, b.op(Op.EVM_EXP, x, b.const(3, 256)), y)))
+    ts.add(b.finish(b.op(Op.BVUGT, b.op(Op.BVUDIV, x, y), b.const(5, 256))))
+    soa = assignment_soa(rng, ts.n_vars, 512)
+    ct = gpu_ctx.compile(ts)
+    a = upload(gpu_ctx, soa)
+    want_counts, want_first = [], []
+    for t in ts.tapes:
+        hits = [r for r in range(soa.shape[2])
+                if smt_eval.evaluate(t.nodes, ts.pool.values, soa_row(soa, r))]
+        want_counts.append(len(hits))
+        want_first.append(hits[0] if hits else native.NO_HIT)
+    fh, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)  # merged
+    assert [int(v) for v in hc] == want_counts
+    assert [int(v) for v in fh] == want_first
+    n = len(ts.tapes)
+    fh2, hc2 = native.run(gpu_ctx, ct, a, tape_first=1, tape_count=n - 1,
+                          mode=native.MODE_COUNT_ALL)  # per variant
+    assert [int(v) for v in hc2] == want_counts[1:]
+    assert [int(v) for v in fh2] == want_first[1:]
+    variants = {(i["n_regs"], i["features"]) for i in ct.info()}
+    assert len(variants) > 1
