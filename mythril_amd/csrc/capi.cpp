@@ -867,34 +867,30 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
                                    d_first_hit, d_hit_count, nullptr))
             return r;
     }
-    // one launch per kernel-variant bucket; a short run over the whole set (a query's guided
-    // first round) is one launch of the variant that covers them all -- the register classes and
-    // the feature sets nest (kernels.h variant_of), and the ids are laid out bucket by bucket in
-    // the order of their words, so the whole id list is one contiguous word range
+    // one launch per kernel-variant bucket; a short run (a query's guided first round) is one
+    // launch per register class instead: the feature sets nest (kernels.h variant_of: a kernel
+    // with more handlers runs a tape that needs fewer), the register classes do not (a tape's
+    // instruction words address its class's registers), and a class's buckets are consecutive
+    // in the id list, which is laid out in the order of the tapes' words
     static const uint64_t merge_rows = [] {
         const char* e = std::getenv("MH_MERGE_ROWS");
         return e ? std::strtoull(e, nullptr, 10) : 4096ull;
     }();
-    uint32_t n_buckets = 0, vmax_nr = 0, vmax_fc = 0;
-    for (uint32_t v = 0; v < mh::kNumVariants; ++v)
-        if (hi[v] != lo[v]) {
-            ++n_buckets;
-            vmax_nr = std::max(vmax_nr, v / 4);
-            vmax_fc = std::max(vmax_fc, v % 4);
-        }
-    const uint32_t vmerged = vmax_nr * 4 + vmax_fc;
-    if (!use_jit && n_buckets > 1 && row_count <= merge_rows && tape_first == 0 &&
-        tape_count == ts->n_tapes && mh::variant_fits(vmerged, p.capacity)) {
-        p.tape_ids = d_ids;
-        p.n_ids = (uint32_t)ids.size();
-        MH_HIP(mh::launch_sieve(p, vmerged, ctx->stream));
-        n_buckets = 0;
-    }
-    for (uint32_t v = 0; v < mh::kNumVariants && n_buckets; ++v) {
+    // (over the whole set only: every bucket is then whole, so a class's buckets are one range)
+    const bool merge = !use_jit && row_count <= merge_rows && tape_first == 0 &&
+                       tape_count == ts->n_tapes;
+    for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
         if (hi[v] == lo[v]) continue;
-        p.tape_ids = d_ids + (lo[v] - ids.data());
-        p.n_ids = (uint32_t)(hi[v] - lo[v]);
-        MH_HIP(mh::launch_sieve(p, v, ctx->stream));
+        uint32_t last = v;  // with merging: the class's last nonempty bucket, ids lo[v]..hi[last]
+        if (merge)
+            for (uint32_t u = v + 1; u < (v / 4 + 1) * 4; ++u)
+                if (hi[u] != lo[u]) last = u;
+        const uint32_t* b = lo[v];
+        const uint32_t* e = hi[last];
+        p.tape_ids = d_ids + (b - ids.data());
+        p.n_ids = (uint32_t)(e - b);
+        MH_HIP(mh::launch_sieve(p, last, ctx->stream));
+        v = last;
     }
     if (ctx->timing) MH_HIP(hipEventRecord(sp.second, ctx->stream));
     return MH_OK;

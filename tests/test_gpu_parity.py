@@ -622,10 +622,10 @@ def test_capacity_above_2_30_rows(gpu_ctx):
 
 
 def test_merged_short_run_matches_per_variant(gpu_ctx):
-    """A short run over the whole tape set is one launch of the variant covering every tape
-    (capi.cpp mh_run_async, MH_MERGE_ROWS); over a sub-range it is one launch per variant.  Both
-    give the oracle's counts and first witnesses on a set mixing plain, division, keccak and EVM
-    tapes (every register class the fuzzer reaches)."""
+    """A short run over the whole tape set is one launch per register class, of the variant with
+    every feature the class's tapes need (capi.cpp mh_run_async, MH_MERGE_ROWS); over a sub-range
+    it is one launch per variant.  Both give the oracle's counts and first witnesses on a set
+    mixing plain, division, keccak and EVM tapes (every register class the fuzzer reaches)."""
     rng = random.Random(4242)
     ts = TapeSet()
     fz = TapeFuzzer(rng, ts, n_vars=3, max_depth=4)
