@@ -55,7 +55,7 @@ for step in "$@"; do
                 > "$OUT/sieve_queries_py_b.jsonl" 2> "$OUT/py_b.log" ;;
     pypaths)  SIEVE_HOST=python timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_py.jsonl" 2> "$OUT/path_scaling_py.log" ;;
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
-    qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/qprof" -o qprof -- \
+    qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
