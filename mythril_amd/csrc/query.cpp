@@ -410,10 +410,18 @@ public:
     }
 
     void harvest(const std::vector<uint32_t>& roots) {
-        // children before parents, host-only nodes and their parents only (lower.py _walk)
+        // per root, in order, children before parents, host-only nodes and their parents only
+        // (lower.py _walk over each constraint; Harvest.merge: a later root's keccak pair wins)
         std::vector<int64_t> st;
-        for (uint32_t r : roots)
-            if (nd(r).flags & F_HOST) st.push_back(r);
+        for (uint32_t r : roots) {
+            if (!(nd(r).flags & F_HOST)) continue;
+            T.seen.reset(T.nodes.size());
+            st.assign(1, r);
+            walk_host(st);
+        }
+        finish_harvest();
+    }
+    void walk_host(std::vector<int64_t>& st) {
         while (!st.empty()) {
             const int64_t s = st.back();
             st.pop_back();
@@ -429,6 +437,8 @@ public:
             for (int j = arity(x.op) - 1; j >= 0; --j)
                 if (!T.seen.has(kids[j]) && (nd(kids[j]).flags & F_HOST)) st.push_back(kids[j]);
         }
+    }
+    void finish_harvest() {  // lower.py apply_harvest: sorted keys, the keccak bases
         for (Tables* tabs : {&cells, &uf_cells})
             for (auto& kv : *tabs) {
                 std::sort(kv.second.begin(), kv.second.end());

@@ -330,3 +330,76 @@ def test_guide_session_laser_like():
             got = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, session=sess)
             assert _guide_equal(got, want), (name, k)
     sess.close()
+
+
+def _random_query(rng, n):
+    """n random constraints over free arrays, K arrays, store chains, selects at constant and
+    symbolic indices, a tabled function, a keccak function with concrete pairs, bounds and its
+    inverse, and a wide (512-bit) equality of concatenations."""
+    from mythril_amd import smt
+    from mythril_amd.smt import (K, Array, Concat, Function, If, Not, ULT, UGT,
+                                 symbol_factory)
+
+    ctx = smt.set_context(smt.Context())
+    v = symbol_factory.BitVecVal
+    xs = [symbol_factory.BitVecSym("x%d" % i, 256) for i in range(3)]
+    arrs = [Array("A", 256, 256), Array("B", 256, 8)]
+    kar = K(256, 256, 7)
+    f = Function("f", 256, 256)
+    kec = Function("keccak256_256", 256, 256)
+    inv = Function("keccak256_256-1", 256, 256)
+    keys = [v(k, 256) for k in (0, 1, 4, 36, 1 << 160)]
+
+    def term(d=0):
+        r = rng.random()
+        if d > 2 or r < 0.25:
+            return rng.choice(xs + keys)
+        if r < 0.45:
+            a = rng.choice(arrs + [kar])
+            idx = rng.choice(keys) if rng.random() < 0.6 else term(d + 1)
+            if a.range == 8:
+                return smt.ZeroExt(248, a[idx])
+            return a[idx]
+        if r < 0.55:
+            return f(rng.choice(keys) if rng.random() < 0.5 else term(d + 1))
+        if r < 0.65:
+            return kec(term(d + 1))
+        if r < 0.7:
+            return inv(kec(term(d + 1)))
+        if r < 0.85:
+            return term(d + 1) + term(d + 1)
+        return If(ULT(term(d + 1), term(d + 1)), term(d + 1), term(d + 1))
+
+    cs = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.1:  # a store into a free array, read back
+            a = rng.choice(arrs[:1])
+            a[rng.choice(keys)] = term(1)
+            cs.append(a[term(2)] == term(2))
+        elif r < 0.2:
+            cs.append(kec(rng.choice(keys)) == v(rng.getrandbits(256), 256))
+        elif r < 0.3:
+            cs.append(UGT(kec(term(1)), v(rng.getrandbits(200) << 40, 256)))
+        elif r < 0.38:
+            cs.append(Concat(term(1), term(1)) == Concat(term(1), term(1)))
+        elif r < 0.7:
+            c = term() == term()
+            cs.append(Not(c) if rng.random() < 0.3 else c)
+        else:
+            cs.append(ULT(term(), term()))
+    return ctx, cs
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_queries_match_python_stages(seed):
+    """Random queries over arrays, stores, K, a tabled function, keccak with pairs / bounds /
+    inverse and wide equalities, built in LASER order (every prefix: extensions and afresh
+    builds both happen): the native result equals the Python stages node for node."""
+    import random
+
+    rng = random.Random(seed)
+    ctx, cs = _random_query(rng, 10)
+    nodes = [c.node for c in cs if hasattr(c, "node")]
+    for k in range(1, len(nodes) + 1):
+        check_query(ctx.b, nodes[:k], (seed, k))
