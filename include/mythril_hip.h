@@ -424,6 +424,14 @@ int32_t mh_comm_destroy(mh_ctx* ctx);
 #define MH_MB_NUM_KINDS 34
 int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
                             double* lane_ops_per_s);
+/* Survivor-gather micro-benchmark (the memory side of the lane compaction costed in DESIGN.md
+ * §5.1): 2^log2_rows rows x 128 B of columns, the rows a hash keeps at permille / 1000 listed in
+ * ascending order, each survivor's 128 B read per launch -- layout 0 the sieve's SoA columns
+ * (32 scattered 4-byte loads), 1 row-major (8 contiguous 16-byte loads), 2 the SoA streaming read
+ * of every row.  Median launch ms over `reps`, useful GB/s (survivors, or rows, x 128 B).        */
+int32_t mh_microbench_gather(int32_t device, uint32_t log2_rows, uint32_t permille,
+                             uint32_t layout, uint32_t reps, double* ms, double* gbps,
+                             uint64_t* survivors);
 /* Round-1 form: kinds 0..2 of mh_microbench_issue at 8 waves per SIMD.                           */
 int32_t mh_microbench_valu(mh_ctx* ctx, uint32_t kind, double* ops_per_s);
 /* Kernel timing on the ctx stream.  While enabled, every sieve launch (mh_run / mh_run_async) is

@@ -69,6 +69,9 @@ SIGNATURES = {
     "mh_eval_values": (C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint64, C.c_uint64, _u32p]),
     "mh_microbench_valu": (C.c_int32, [_vp, C.c_uint32, C.POINTER(C.c_double)]),
     "mh_microbench_issue": (C.c_int32, [_vp, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]),
+    "mh_microbench_gather": (C.c_int32, [C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.POINTER(C.c_double),
+                                         C.POINTER(C.c_double), _u64p]),
     "mh_tapes_jit": (C.c_int32, [_vp, C.c_uint32, C.c_uint32]),
     "mh_tapes_jit_info": (C.c_int32, [_vp, _vp]),
     "mh_tapes_jitted": (C.c_int32, [_vp, C.POINTER(C.c_uint8), C.c_uint32]),
@@ -862,3 +865,12 @@ def limbs_to_ints(arr: np.ndarray) -> Sequence[int]:
             v |= int(arr[k, j]) << (32 * k)
         out.append(v)
     return out
+
+
+def microbench_gather(device: int, log2_rows: int, permille: int, layout: int,
+                      reps: int = 5) -> Tuple[float, float, int]:
+    """mh_microbench_gather: (median ms per launch, useful GB/s, survivors)."""
+    ms, gbps, n = C.c_double(), C.c_double(), C.c_uint64()
+    _check(load().mh_microbench_gather(device, log2_rows, permille, layout, reps, C.byref(ms),
+                                       C.byref(gbps), C.byref(n)))
+    return ms.value, gbps.value, int(n.value)

@@ -21,6 +21,7 @@
 #   pypaths   paths with the Python host stages
 #   qcost     scripts/query_cost.py (host stages per query, native compiler vs Python)
 #   qprofile  rocprofv3 kernel trace + stats of one pass of sieve_queries.py (query-path kernels)
+#   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:?tag}
@@ -57,6 +58,7 @@ for step in "$@"; do
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;
+    gather)   timeout -k 10 300 python -u scripts/gather_bench.py > "$OUT/gather.jsonl" 2> "$OUT/gather.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
