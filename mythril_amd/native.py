@@ -225,8 +225,9 @@ def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
     else:
         _check(lib.mh_guide_harvest_with(session.h, *args))
     try:
-        def arr(p, n, dt=np.uint32):
-            return np.ctypeslib.as_array(p, (n,)).astype(dt, copy=True)
+        def arr(p, n, dt=np.uint32):  # a copy of n elements at p (one memcpy)
+            dt = np.dtype(dt)
+            return np.frombuffer(C.string_at(C.cast(p, C.c_void_p), n * dt.itemsize), dtype=dt)
 
         n_cols, n_sets = g.n_cols, g.n_sets
         pool_off = arr(g.pool_off, n_cols + 1)
