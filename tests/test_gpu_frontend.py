@@ -250,3 +250,33 @@ def test_native_and_python_host_stages_agree(gpu_ctx):
         finally:
             s_nat.close()
             s_py.close()
+
+
+def test_random_queries_native_witnesses_are_models(gpu_ctx):
+    """Random queries over arrays, stores, K, a tabled function, keccak with pairs / bounds /
+    inverse and wide equalities (tests/test_query_native.py _random_query), every prefix in
+    LASER order through Sieve.solve with the native query compiler: every witness is a model of
+    the ORIGINAL prefix (oracle/term_eval.py), and some prefixes are answered."""
+    import random
+
+    from mythril_amd.sieve import Sieve
+    from tests.test_query_native import _random_query
+
+    s = Sieve()
+    hits = 0
+    try:
+        for seed in range(16):
+            ctx, cs = _random_query(random.Random(seed), 8)
+            cs = [c for c in cs if hasattr(c, "node")]
+            for k in range(1, len(cs) + 1):
+                nodes = [c.node for c in cs[:k]]
+                try:
+                    w = s.solve(ctx.b, nodes, key=tuple(nodes))
+                except native.Unsupported:
+                    continue
+                if w is not None:
+                    hits += 1
+                    assert _oracle_holds(ctx, cs[:k], w.schema, w.values), (seed, k)
+    finally:
+        s.close()
+    assert hits >= 16

@@ -27,8 +27,10 @@ def model_of(schema, row):
     cols = schema.columns
     vars_ = {c.name: row[c.name] for c in cols.values() if c.kind == "var"}
     arrays = {}
+    # a harvested cell no lowered conjunct reads is not in the witness: any value is a model,
+    # and Model.eval reads it as 0 (model completion)
     for arr, cells in schema.cells.items():
-        tab = {k: row[n] for k, n in cells.items()}
+        tab = {k: row.get(n, 0) for k, n in cells.items()}
         arrays[arr] = (tab, row.get("%s[*]" % arr, 0))
     funcs = {}
     for f, km in schema.keccak.items():
@@ -48,7 +50,7 @@ def model_of(schema, row):
         funcs[f] = fwd
         funcs[f + "-1"] = (lambda y, inv=inv: inv.get(y, 0))
     for f, cells in schema.uf_cells.items():
-        tab = {k: row[n] for k, n in cells.items()}
+        tab = {k: row.get(n, 0) for k, n in cells.items()}
         dflt = row.get("%s[*]" % f, 0)
         funcs[f] = (lambda x, tab=tab, dflt=dflt: tab.get(x, dflt))
     return vars_, arrays, funcs
