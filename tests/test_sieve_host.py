@@ -1,109 +1,126 @@
-"""Sieve.solve's host logic on the CPU (tests/fake_device.py stands in for the device): with the
-native query compiler (csrc/query.cpp) and with the Python stages it replaced, every LASER-shaped
-SAT query of tests/laser_like.py is answered with a witness that is a model of the ORIGINAL query
-(oracle/term_eval.py), UNSAT ones miss, and the model evaluates its constraints to True; the
-reference's own outcome cases (tests/reference_cases.py) through frontend.get_model likewise.
+"""Host side of the sieve engine (mythril_amd/sieve.py), checked with the oracle and the
+test-only host emulator of the device ISA (tests/native/emu.cpp, the product tape compiler).
+
+* every LASER-shaped query of tests/laser_like.py compiles for the device (with
+  rematerialisation where overlapping calldata words exceed the register file) and the compiled
+  code agrees with the oracle on guided candidate rows;
+* ``rematerialize`` preserves the value of a tape and lowers its register need.
 """
+import numpy as np
 import pytest
 
-from mythril_amd import frontend
-from mythril_amd.model import Model
-from mythril_amd.sieve import Sieve
-from tests import fake_device
+from mythril_amd.candidates import build_guide
+from mythril_amd.lower import lower_query
+from mythril_amd.sieve import local_tape, rematerialize
+from mythril_amd.tape import Tape, TapeSet
+from oracle import smt_eval as E
+from oracle.guided_gen import generate_row
+from tests.emu import EmuError
 from tests.laser_like import queries
-from tests.reference_cases import BY_NAME, CASES
-from tests.test_reference_fixtures import holds_original
-from tests.test_gpu_frontend import _oracle_holds
-
-SHAPES = ["selector", "owner_check", "balance", "keccak_mapping", "keccak_alias", "ether_thief",
-          "overflow", "killbilly", "unsat_actor"]
 
 
-@pytest.mark.parametrize("native_query", [True, False])
-@pytest.mark.parametrize("name", SHAPES)
-def test_solve_on_fake_device(monkeypatch, name, native_query):
-    fake_device.install(monkeypatch)
+def _soa(rows, n_cols):
+    soa = np.zeros((n_cols, 8, len(rows)), dtype=np.uint32)
+    for j, row in enumerate(rows):
+        for i, v in enumerate(row):
+            for k in range(8):
+                soa[i, k, j] = (v >> (32 * k)) & 0xFFFFFFFF
+    return soa
+
+
+@pytest.mark.parametrize("qi", range(len(queries()[1])))
+def test_queries_compile_and_match_oracle(emu, qi):
     ctx, qs = queries()
-    cs = dict(qs)[name]
-    s = Sieve(rows=256, native_query=native_query)
-    nodes = [c.node for c in cs]
-    for k in range(1, len(nodes) + 1):  # LASER order, keyed as get_model keys it
-        w = s.solve(ctx.b, nodes[:k], key=tuple(nodes[:k]))
-    if name.startswith("unsat"):
-        assert w is None
-        return
-    assert w is not None, name
-    assert _oracle_holds(ctx, cs, w.schema, w.values), name
-    m = Model(s, ctx, w.schema, w.values, w.index)
-    for c in cs:
-        assert m.eval(c, model_completion=True) is True, name
+    name, cs = qs[qi]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    cols = list(schema.columns)
+    guide = build_guide(ctx.b, root, schema, cols).arrays()
+    nodes = local_tape(ctx.b, root, cols)
+    ts = TapeSet(cols)
+    ts.pool = ctx.b.pool
+    rows = [generate_row(11 + qi, r, guide) for r in range(96)]
+    soa = _soa(rows, len(cols))
+    got = None
+    for size in (0, 8, 32, 256):  # the retry ladder of Sieve.compile
+        ts.tapes[:] = [Tape(nodes if size == 0 else rematerialize(nodes, size))]
+        try:
+            got, nregs = emu.eval(ts, 0, soa)
+            break
+        except EmuError as e:
+            assert "register pressure" in str(e), (name, str(e))
+    assert got is not None, name
+    for j, row in enumerate(rows):
+        want = E.evaluate(nodes, ctx.b.pool.values, row)
+        assert bool(got[j]) == bool(want), (name, j)
+        # the rematerialised tape is the same function
+        assert bool(E.evaluate(ts.tapes[0].nodes, ctx.b.pool.values, row)) == bool(want)
 
 
-@pytest.mark.parametrize("native_query", [True, False])
-@pytest.mark.parametrize("name", [c.name for c in CASES])
-def test_reference_outcome_on_fake_device(monkeypatch, name, native_query):
-    """tests/test_gpu_reference_fixtures.py's outcome test through frontend.get_model, with the
-    fake device: UNSAT reaches the fallback unchanged, SAT gives a model of the original query."""
-    fake_device.install(monkeypatch)
-    frontend.reset()
+def test_rematerialize_removes_sharing_of_cheap_terms():
+    ctx, qs = queries()
+    cs = dict(qs)["address_arg"]
+    root, _ = lower_query(ctx.b, [c.node for c in cs])
+    nodes = local_tape(ctx.b, root, list(ctx.b.var_index))
+    r = rematerialize(nodes, 8)
+    # reachable part of r: every cheap node has one user
+    from mythril_amd.tape import ARITY, Op
+
+    n = len(r)
+    reach = np.zeros(n, dtype=bool)
+    reach[-1] = True
+    uses = np.zeros(n, dtype=int)
+    for i in range(n - 1, -1, -1):
+        if not reach[i]:
+            continue
+        for x in [r["a"][i], r["b"][i], r["c"][i]][:ARITY[Op(int(r["op"][i]))]]:
+            reach[x] = True
+            uses[x] += 1
+    shared_ites = [i for i in range(n) if reach[i] and int(r["op"][i]) == Op.ITE
+                   and uses[i] > 1]
+    assert not shared_ites
+
+
+def test_buckets_split_variable_disjoint_conjuncts():
+    from mythril_amd.sieve import Sieve
+
+    ctx, qs = queries()
+    sizes = {}
+    for name, cs in qs:
+        root, schema = lower_query(ctx.b, [c.node for c in cs])
+        groups = Sieve.buckets(ctx.b, root)
+        cols = [v for _, vs in groups for v in vs]
+        assert len(cols) == len(set(cols)), name  # disjoint
+        names = {ctx.b.var_index[c] for c in schema.columns}
+        assert set(cols) == names, name  # every column of the query is in some group
+        sizes[name] = sum(1 for _, vs in groups if vs)  # ground conjuncts form groups too
+    assert sizes["selector"] == 2        # calldata bytes + size  |  sender in ACTORS
+    assert sizes["owner_check"] == 1     # Storage[0] == sender ties them
+    assert sizes["keccak_alias"] == 1
+
+
+def test_hot_columns_are_loaded_once(emu):
+    """A loaded-on-use column read by many operands (every calldata byte compares its index with
+    calldatasize, calldata.py:48-54) is loaded once and held in a register by the interpreter's
+    compiler (compile.cpp Lowering::hold_vars): fewer D_LOADVAR complex ops, same values."""
+    import os
+
+    from mythril_amd.sieve import local_tapeset
+
+    ctx, qs = queries()
+    cs = dict(qs)["overflow"]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    cols = list(schema.columns)
+    ts = local_tapeset(ctx.b, [root], cols)
+    guide = build_guide(ctx.b, root, schema, cols).arrays()
+    rows = [generate_row(5, r, guide) for r in range(64)]
+    soa = _soa(rows, len(cols))
+    held, _ = emu.eval(ts, 0, soa)
+    n_held = emu.n_slots(ts)
+    os.environ["MH_NO_HOLD_VARS"] = "1"
     try:
-        frontend.configure(rows=256, native_query=native_query)
-        case = BY_NAME[name]
-        ctx, cs = case.build()
-        calls = []
-        frontend.configure(fallback=lambda c, *a: calls.append(c) or "fallback")
-        m = frontend.get_model(tuple(cs))
-        if case.expected == "unsat" or case.fallback_reason:
-            assert m == "fallback" and len(calls) == 1, name
-        else:
-            assert isinstance(m, Model) and not calls, name
-            assert holds_original(ctx, cs, m.schema, m.values), name
-            for c in cs:
-                assert m.eval(c, model_completion=True) is True, name
+        plain, _ = emu.eval(ts, 0, soa)
+        n_plain = emu.n_slots(ts)
     finally:
-        frontend.reset()
-
-
-def test_refuted_query_skips_the_device(monkeypatch):
-    """A query that contradicts itself (MH_QUERY_REFUTED: KillBilly's third sender pinned to two
-    actors, an overflow of two words below 2^128) is a miss without a device round; an UNSAT
-    query neither syntax nor ranges refute (ether_thief_unsat) still runs its rounds and misses."""
-    from tests.laser_like import hard_queries
-
-    fake_device.install(monkeypatch)
-    ctx, qs = hard_queries()
-    s = Sieve(rows=256, budget_s=60.0)  # the CPU stand-in is slow: no budget cut
-    cs = dict(qs)["killbilly_unsat"]
-    r0 = s.stats.rounds
-    assert s.solve(ctx.b, [c.node for c in cs]) is None
-    assert s.stats.rounds == r0 and s.stats.extra.get("refuted") == 1
-    cs = dict(qs)["overflow_unsat"]
-    assert s.solve(ctx.b, [c.node for c in cs]) is None
-    assert s.stats.rounds == r0 and s.stats.extra.get("refuted") == 2
-    cs = dict(qs)["ether_thief_unsat"]
-    assert s.solve(ctx.b, [c.node for c in cs]) is None
-    assert s.stats.rounds == r0 + 2 and s.stats.misses == 3
-
-
-def test_later_round_runs_only_unsolved_groups(monkeypatch):
-    """Round 2 (2^16 rows in the product) launches only the tapes from the first to the last
-    group round 1 left unsolved: here group 0 (x == 5) is solved by the guide, group 1
-    (y * y == 2, no solution mod 2^256) is not."""
-    from mythril_amd import native, smt
-    from mythril_amd.smt import symbol_factory
-
-    fake_device.install(monkeypatch)
-    calls = []
-    real = native.run
-
-    def recording(ctx, tapes, assign, **kw):
-        calls.append((kw.get("tape_first", 0), kw.get("tape_count")))
-        return real(ctx, tapes, assign, **kw)
-
-    monkeypatch.setattr(native, "run", recording)
-    ctx = smt.set_context(smt.Context())
-    x = symbol_factory.BitVecSym("x", 256)
-    y = symbol_factory.BitVecSym("y", 256)
-    s = Sieve(rows=64, first_rows=64, budget_s=60.0)
-    assert s.solve(ctx.b, [(x == 5).node, (y * y == 2).node]) is None
-    assert calls == [(0, 2), (1, 1)]
+        del os.environ["MH_NO_HOLD_VARS"]
+    assert [bool(x) for x in held] == [bool(x) for x in plain]
+    assert n_held < n_plain, (n_held, n_plain)

@@ -1,0 +1,109 @@
+"""Sieve.solve's host logic on the CPU (tests/fake_device.py stands in for the device): with the
+native query compiler (csrc/query.cpp) and with the Python stages it replaced, every LASER-shaped
+SAT query of tests/laser_like.py is answered with a witness that is a model of the ORIGINAL query
+(oracle/term_eval.py), UNSAT ones miss, and the model evaluates its constraints to True; the
+reference's own outcome cases (tests/reference_cases.py) through frontend.get_model likewise.
+"""
+import pytest
+
+from mythril_amd import frontend
+from mythril_amd.model import Model
+from mythril_amd.sieve import Sieve
+from tests import fake_device
+from tests.laser_like import queries
+from tests.reference_cases import BY_NAME, CASES
+from tests.test_reference_fixtures import holds_original
+from tests.test_gpu_frontend import _oracle_holds
+
+SHAPES = ["selector", "owner_check", "balance", "keccak_mapping", "keccak_alias", "ether_thief",
+          "overflow", "killbilly", "unsat_actor"]
+
+
+@pytest.mark.parametrize("native_query", [True, False])
+@pytest.mark.parametrize("name", SHAPES)
+def test_solve_on_fake_device(monkeypatch, name, native_query):
+    fake_device.install(monkeypatch)
+    ctx, qs = queries()
+    cs = dict(qs)[name]
+    s = Sieve(rows=256, native_query=native_query)
+    nodes = [c.node for c in cs]
+    for k in range(1, len(nodes) + 1):  # LASER order, keyed as get_model keys it
+        w = s.solve(ctx.b, nodes[:k], key=tuple(nodes[:k]))
+    if name.startswith("unsat"):
+        assert w is None
+        return
+    assert w is not None, name
+    assert _oracle_holds(ctx, cs, w.schema, w.values), name
+    m = Model(s, ctx, w.schema, w.values, w.index)
+    for c in cs:
+        assert m.eval(c, model_completion=True) is True, name
+
+
+@pytest.mark.parametrize("native_query", [True, False])
+@pytest.mark.parametrize("name", [c.name for c in CASES])
+def test_reference_outcome_on_fake_device(monkeypatch, name, native_query):
+    """tests/test_gpu_reference_fixtures.py's outcome test through frontend.get_model, with the
+    fake device: UNSAT reaches the fallback unchanged, SAT gives a model of the original query."""
+    fake_device.install(monkeypatch)
+    frontend.reset()
+    try:
+        frontend.configure(rows=256, native_query=native_query)
+        case = BY_NAME[name]
+        ctx, cs = case.build()
+        calls = []
+        frontend.configure(fallback=lambda c, *a: calls.append(c) or "fallback")
+        m = frontend.get_model(tuple(cs))
+        if case.expected == "unsat" or case.fallback_reason:
+            assert m == "fallback" and len(calls) == 1, name
+        else:
+            assert isinstance(m, Model) and not calls, name
+            assert holds_original(ctx, cs, m.schema, m.values), name
+            for c in cs:
+                assert m.eval(c, model_completion=True) is True, name
+    finally:
+        frontend.reset()
+
+
+def test_refuted_query_skips_the_device(monkeypatch):
+    """A query that contradicts itself (MH_QUERY_REFUTED: KillBilly's third sender pinned to two
+    actors, an overflow of two words below 2^128) is a miss without a device round; an UNSAT
+    query neither syntax nor ranges refute (ether_thief_unsat) still runs its rounds and misses."""
+    from tests.laser_like import hard_queries
+
+    fake_device.install(monkeypatch)
+    ctx, qs = hard_queries()
+    s = Sieve(rows=256, budget_s=60.0)  # the CPU stand-in is slow: no budget cut
+    cs = dict(qs)["killbilly_unsat"]
+    r0 = s.stats.rounds
+    assert s.solve(ctx.b, [c.node for c in cs]) is None
+    assert s.stats.rounds == r0 and s.stats.extra.get("refuted") == 1
+    cs = dict(qs)["overflow_unsat"]
+    assert s.solve(ctx.b, [c.node for c in cs]) is None
+    assert s.stats.rounds == r0 and s.stats.extra.get("refuted") == 2
+    cs = dict(qs)["ether_thief_unsat"]
+    assert s.solve(ctx.b, [c.node for c in cs]) is None
+    assert s.stats.rounds == r0 + 2 and s.stats.misses == 3
+
+
+def test_later_round_runs_only_unsolved_groups(monkeypatch):
+    """Round 2 (2^16 rows in the product) launches only the tapes from the first to the last
+    group round 1 left unsolved: here group 0 (x == 5) is solved by the guide, group 1
+    (y * y == 2, no solution mod 2^256) is not."""
+    from mythril_amd import native, smt
+    from mythril_amd.smt import symbol_factory
+
+    fake_device.install(monkeypatch)
+    calls = []
+    real = native.run
+
+    def recording(ctx, tapes, assign, **kw):
+        calls.append((kw.get("tape_first", 0), kw.get("tape_count")))
+        return real(ctx, tapes, assign, **kw)
+
+    monkeypatch.setattr(native, "run", recording)
+    ctx = smt.set_context(smt.Context())
+    x = symbol_factory.BitVecSym("x", 256)
+    y = symbol_factory.BitVecSym("y", 256)
+    s = Sieve(rows=64, first_rows=64, budget_s=60.0)
+    assert s.solve(ctx.b, [(x == 5).node, (y * y == 2).node]) is None
+    assert calls == [(0, 2), (1, 1)]
