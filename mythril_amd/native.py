@@ -476,17 +476,22 @@ class TermMirror:
     (mh_query_build).  One per builder, kept on it (``TermMirror.of``)."""
 
     def __init__(self):
+        import threading
+
         self.lib = load()
         h = C.c_void_p()
         _check(self.lib.mh_terms_create(C.byref(h)))
         self.h = h
         self.n = [0, 0, 0, 0, 0]  # nodes, constants, variables, arrays, functions sent
+        # one session per builder, used by one thread at a time (query.cpp keeps scratch and the
+        # last query's state on it): sieves of several threads over one builder take turns
+        self.lock = threading.Lock()
 
     @classmethod
     def of(cls, b) -> "TermMirror":
         m = b.__dict__.get("_term_mirror")
-        if m is None:
-            m = b.__dict__["_term_mirror"] = cls()
+        if m is None:  # setdefault: two threads racing here end up with the same session
+            m = b.__dict__.setdefault("_term_mirror", cls())
         return m
 
     def close(self) -> None:
@@ -536,15 +541,16 @@ class TermMirror:
 
     def build(self, b, roots: Sequence[int]) -> CompiledQuery:
         """mh_query_build of the conjunction of `roots` (after a sync with `b`)."""
-        self.sync(b)
         r = np.ascontiguousarray(roots, dtype=np.uint32)
-        h = C.c_void_p()
-        info = QueryInfo()
-        _check(self.lib.mh_query_build(self.h, _ptr(r), len(r), C.byref(h), C.byref(info)))
-        try:
-            return CompiledQuery(info)
-        finally:
-            self.lib.mh_query_free(h)
+        with self.lock:
+            self.sync(b)
+            h = C.c_void_p()
+            info = QueryInfo()
+            _check(self.lib.mh_query_build(self.h, _ptr(r), len(r), C.byref(h), C.byref(info)))
+            try:
+                return CompiledQuery(info)
+            finally:
+                self.lib.mh_query_free(h)
 
 
 _ARITY_BY_INT: List[int] = []

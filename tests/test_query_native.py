@@ -403,3 +403,33 @@ def test_random_queries_match_python_stages(seed):
     nodes = [c.node for c in cs if hasattr(c, "node")]
     for k in range(1, len(nodes) + 1):
         check_query(ctx.b, nodes[:k], (seed, k))
+
+
+def test_mirror_shared_by_threads():
+    """Sieves of several threads over one builder take turns on its session: every result is the
+    one a single thread gets."""
+    import threading
+
+    ctx, qs = laser_like.queries()
+    want = {}
+    for name, cs in qs:
+        cq = native.TermMirror.of(ctx.b).build(ctx.b, [c.node for c in cs])
+        want[name] = [t.tobytes() for t in cq.tapes]
+    errors = []
+
+    def work(seed):
+        import random
+
+        rng = random.Random(seed)
+        for _ in range(30):
+            name, cs = rng.choice(qs)
+            cq = native.TermMirror.of(ctx.b).build(ctx.b, [c.node for c in cs])
+            if [t.tobytes() for t in cq.tapes] != want[name]:
+                errors.append(name)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
