@@ -54,6 +54,12 @@ struct mh_ctx {
     size_t h_stage_bytes = 0;
     hipEvent_t stage_ev = nullptr;
     bool stage_pending = false;
+    // compiled tapes by content (the tape's nodes, the values of the constants it reads, the
+    // column count): a LASER query's groups mostly repeat its parent's (svm.py:257-262), and a
+    // tape's instruction words are self-contained (constants inline), so a repeated tape reuses
+    // its words; cleared beyond compile_cache_limit words
+    std::unordered_map<std::string, std::pair<std::vector<uint32_t>, mh::CompiledTape>> compile_cache;
+    size_t compile_cache_words = 0;
 };
 
 namespace {
@@ -480,9 +486,30 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     std::vector<uint32_t> ids, bucket_off(mh::kNumVariants + 1, 0);
     try {
         std::vector<std::vector<uint32_t>> tw(n_tapes);
+        static const bool use_cache = [] {
+            const char* e = std::getenv("MH_COMPILE_CACHE");
+            return !(e && e[0] == '0');
+        }();
+        constexpr size_t kCacheWords = (size_t)16 << 20;  // 128 MB of instruction words
+        std::string key;
         for (uint32_t t = 0; t < n_tapes; ++t) {
             const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
             if (e <= b) return set_err(MH_E_INVALID, "tape " + std::to_string(t) + " is empty");
+            if (use_cache) {  // the tape's content: nodes, constant values, column count
+                key.assign(reinterpret_cast<const char*>(&n_vars), sizeof n_vars);
+                key.append(reinterpret_cast<const char*>(nodes + b), (size_t)(e - b) * sizeof(mh_node));
+                for (uint64_t i = b; i < e; ++i)
+                    if (nodes[i].op == MH_OP_CONST && nodes[i].imm0 < n_consts)
+                        key.append(reinterpret_cast<const char*>(consts + 8ull * nodes[i].imm0), 32);
+                auto hit = ctx->compile_cache.find(key);
+                if (hit != ctx->compile_cache.end()) {
+                    tw[t] = hit->second.first;
+                    const mh::CompiledTape& ct = hit->second.second;
+                    heads[t] = mh_dev_tape{0, ct.n_insns, ct.root_bool, ct.n_regs};
+                    info[t] = mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops};
+                    continue;
+                }
+            }
             mh::CompiledTape ct;
             std::string err;
             int32_t r = mh::compile_tape(nodes + b, (size_t)(e - b), consts, n_consts, n_vars,
@@ -490,6 +517,14 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
             if (r != MH_OK) return set_err(r, "tape " + std::to_string(t) + ": " + err);
             heads[t] = mh_dev_tape{0, ct.n_insns, ct.root_bool, ct.n_regs};
             info[t] = mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops};
+            if (use_cache) {
+                if (ctx->compile_cache_words + tw[t].size() > kCacheWords) {
+                    ctx->compile_cache.clear();
+                    ctx->compile_cache_words = 0;
+                }
+                ctx->compile_cache_words += tw[t].size();
+                ctx->compile_cache.emplace(key, std::make_pair(tw[t], ct));
+            }
         }
         // bucket by kernel variant; instruction words laid out bucket by bucket (ascending tape
         // id inside a bucket) so that any run of consecutive bucket entries is one contiguous

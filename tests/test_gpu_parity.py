@@ -656,3 +656,38 @@ def test_merged_short_run_matches_per_variant(gpu_ctx):
     assert [int(v) for v in fh2] == want_first[1:]
     variants = {(i["n_regs"], i["features"]) for i in ct.info()}
     assert len(variants) > 1
+
+
+def test_compile_cache_reuses_identical_tapes(gpu_ctx):
+    """mh_tapes_compile keeps compiled tapes by content per context: a LASER child's unchanged
+    groups reuse their parent's words.  A set compiled twice, and a set where one tape changed and
+    the others repeat, give the oracle's counts and the same tape info as a first compile."""
+    rng = random.Random(77)
+    ts = TapeSet()
+    fz = TapeFuzzer(rng, ts, n_vars=3, max_depth=4)
+    for _ in range(12):
+        fz.tape()
+    soa = assignment_soa(rng, ts.n_vars, 256)
+    a = upload(gpu_ctx, soa)
+
+    def oracle(tset):
+        out = []
+        for t in tset.tapes:
+            out.append(sum(1 for r in range(soa.shape[2])
+                           if smt_eval.evaluate(t.nodes, tset.pool.values, soa_row(soa, r))))
+        return out
+
+    want = oracle(ts)
+    infos = []
+    for _ in range(2):  # the second compile hits the cache for every tape
+        ct = gpu_ctx.compile(ts)
+        _, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+        assert [int(v) for v in hc] == want
+        infos.append(ct.info())
+        ct.close()
+    assert infos[0] == infos[1]
+    fz.tape()  # one more tape: the first 12 repeat, the new one compiles
+    ts.tapes[5], ts.tapes[-1] = ts.tapes[-1], ts.tapes[5]
+    ct = gpu_ctx.compile(ts)
+    _, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    assert [int(v) for v in hc] == oracle(ts)
