@@ -338,6 +338,14 @@ int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t 
                const mh_assign* as, uint64_t row_first, uint64_t row_count, uint64_t index_base,
                uint32_t mode, uint64_t* first_hit /* [tape_count] or NULL */,
                uint64_t* hit_count /* [tape_count] or NULL */);
+/* mh_run plus each tape's witness row: rows_out [tape_count][n_cols][8] u32 receives columns
+ * 0..n_cols-1 (n_cols <= the buffer's columns) of the row first_hit names, all zero for a tape
+ * without a hit -- the model get_model returns (support/model.py:15-62) read back in the same
+ * device-to-host copy as the results instead of one mh_assign_download per distinct row.        */
+int32_t mh_run_rows(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+                    const mh_assign* as, uint64_t row_first, uint64_t row_count,
+                    uint64_t index_base, uint32_t mode, uint64_t* first_hit, uint64_t* hit_count,
+                    uint32_t n_cols, uint32_t* rows_out);
 /* Device-pointer form: enqueues on the ctx stream and returns.  d_first_hit / d_hit_count are
  * device buffers of tape_count u64; they are NOT reset (callers initialise them to MH_NO_HIT / 0
  * with mh_results_reset), so several launches can accumulate into them.                          */

@@ -23,6 +23,8 @@
 #include "jit.h"
 #include "kernels.h"
 
+constexpr uint32_t kSideStreams = 3;  // with the ctx stream: GPU_MAX_HW_QUEUES (4) queues
+
 struct mh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -60,6 +62,11 @@ struct mh_ctx {
     // its words; cleared beyond compile_cache_limit words
     std::unordered_map<std::string, std::pair<std::vector<uint32_t>, mh::CompiledTape>> compile_cache;
     size_t compile_cache_words = 0;
+    // a short run's launches (one per register class) are a few waves each walking a long tape:
+    // latency-bound, so they overlap on side streams (forked from and joined back into `stream`
+    // by events) instead of queueing behind each other; created on first use
+    hipStream_t side[kSideStreams] = {};
+    hipEvent_t fork_ev = nullptr, join_ev[kSideStreams] = {};
 };
 
 namespace {
@@ -425,6 +432,14 @@ void ctx_free(mh_ctx* ctx) {
         (void)hipEventDestroy(sp.second);
     }
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    for (uint32_t i = 0; i < kSideStreams; ++i) {
+        if (ctx->side[i]) {
+            (void)hipStreamSynchronize(ctx->side[i]);
+            (void)hipStreamDestroy(ctx->side[i]);
+        }
+        if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
+    }
+    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->d_buf) (void)hipFree(ctx->d_buf);
     if (ctx->h_buf) (void)hipHostFree(ctx->h_buf);
@@ -914,34 +929,67 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
     // (over the whole set only: every bucket is then whole, so a class's buckets are one range)
     const bool merge = !use_jit && row_count <= merge_rows && tape_first == 0 &&
                        tape_count == ts->n_tapes;
+    struct Launch { const uint32_t *b, *e; uint32_t variant; };
+    Launch launches[mh::kNumVariants];
+    uint32_t n_launch = 0;
     for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
         if (hi[v] == lo[v]) continue;
         uint32_t last = v;  // with merging: the class's last nonempty bucket, ids lo[v]..hi[last]
         if (merge)
             for (uint32_t u = v + 1; u < (v / 4 + 1) * 4; ++u)
                 if (hi[u] != lo[u]) last = u;
-        const uint32_t* b = lo[v];
-        const uint32_t* e = hi[last];
-        p.tape_ids = d_ids + (b - ids.data());
-        p.n_ids = (uint32_t)(e - b);
-        MH_HIP(mh::launch_sieve(p, last, ctx->stream));
+        launches[n_launch++] = Launch{lo[v], hi[last], last};
         v = last;
+    }
+    static const bool fanout = [] {
+        const char* e = std::getenv("MH_FANOUT");
+        return !(e && e[0] == '0');
+    }();
+    // a short run's launches overlap on the side streams; the results they write are disjoint
+    // (per tape), and the join puts everything after them back in `stream`'s order
+    const uint32_t n_side = fanout && merge ? std::min(n_launch - (n_launch > 0), kSideStreams) : 0;
+    if (n_side) {
+        if (!ctx->fork_ev) MH_HIP(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+        for (uint32_t i = 0; i < n_side; ++i) {
+            if (!ctx->side[i])
+                MH_HIP(hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking));
+            if (!ctx->join_ev[i])
+                MH_HIP(hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming));
+        }
+        MH_HIP(hipEventRecord(ctx->fork_ev, ctx->stream));
+        for (uint32_t i = 0; i < n_side; ++i) MH_HIP(hipStreamWaitEvent(ctx->side[i], ctx->fork_ev, 0));
+    }
+    for (uint32_t i = 0; i < n_launch; ++i) {
+        p.tape_ids = d_ids + (launches[i].b - ids.data());
+        p.n_ids = (uint32_t)(launches[i].e - launches[i].b);
+        // launch 0 on the ctx stream, the others round-robin over the side streams
+        hipStream_t s = n_side && i ? ctx->side[(i - 1) % n_side] : ctx->stream;
+        MH_HIP(mh::launch_sieve(p, launches[i].variant, s));
+    }
+    for (uint32_t i = 0; i < n_side; ++i) {
+        MH_HIP(hipEventRecord(ctx->join_ev[i], ctx->side[i]));
+        MH_HIP(hipStreamWaitEvent(ctx->stream, ctx->join_ev[i], 0));
     }
     if (ctx->timing) MH_HIP(hipEventRecord(sp.second, ctx->stream));
     return MH_OK;
 }
 
-int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
-               const mh_assign* as, uint64_t row_first, uint64_t row_count, uint64_t index_base,
-               uint32_t mode, uint64_t* first_hit, uint64_t* hit_count) {
+int32_t mh_run_rows(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+                    const mh_assign* as, uint64_t row_first, uint64_t row_count,
+                    uint64_t index_base, uint32_t mode, uint64_t* first_hit, uint64_t* hit_count,
+                    uint32_t n_cols, uint32_t* rows_out) {
     if (int32_t r = check_run_args(ctx, ts, tape_first, tape_count, as, row_first, row_count, mode))
         return r;
+    if (n_cols && (!rows_out || n_cols > as->n_vars))
+        return set_err(MH_E_INVALID, "mh_run_rows: rows_out null or n_cols beyond the buffer's columns");
     if (int32_t r = use_device(ctx)) return r;
     const size_t n = std::max<uint32_t>(tape_count, 1);
+    const size_t res_bytes = 2 * n * sizeof(uint64_t);
+    const size_t row_bytes = (size_t)tape_count * n_cols * 8 * sizeof(uint32_t);
     void* dv = nullptr;
     void* hv = nullptr;
-    MH_HIP(ctx_dbuf(ctx, 2 * n * sizeof(uint64_t), &dv));
-    MH_HIP(ctx_hbuf(ctx, 2 * n * sizeof(uint64_t), &hv));
+    MH_HIP(ctx_dbuf(ctx, res_bytes + row_bytes, &dv));
+    MH_HIP(ctx_hbuf(ctx, res_bytes + row_bytes, &hv));
     uint64_t* d = static_cast<uint64_t*>(dv);
     uint64_t* h = static_cast<uint64_t*>(hv);
     int32_t r = mh_results_reset(ctx, d, d + n, (uint32_t)n);
@@ -949,16 +997,27 @@ int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t 
         r = mh_run_async(ctx, ts, tape_first, tape_count, as, row_first, row_count, index_base,
                          mode, d, d + n);
     hipError_t e = hipSuccess;
-    if (r == MH_OK)  // both result arrays in one copy into pinned memory
-        e = hipMemcpyAsync(h, d, 2 * n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (r == MH_OK && row_bytes)
+        e = mh::launch_witness_rows(as->d, as->stride, d, tape_count, index_base, n_cols,
+                                    reinterpret_cast<uint32_t*>(d + 2 * n), ctx->stream);
+    if (r == MH_OK && e == hipSuccess)  // results and rows in one copy into pinned memory
+        e = hipMemcpyAsync(h, d, res_bytes + row_bytes, hipMemcpyDeviceToHost, ctx->stream);
     if (r == MH_OK && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (r == MH_OK && e == hipSuccess && first_hit && tape_count)
         std::memcpy(first_hit, h, tape_count * sizeof(uint64_t));
     if (r == MH_OK && e == hipSuccess && hit_count && tape_count)
         std::memcpy(hit_count, h + n, tape_count * sizeof(uint64_t));
+    if (r == MH_OK && e == hipSuccess && row_bytes) std::memcpy(rows_out, h + 2 * n, row_bytes);
     if (r != MH_OK) return r;
     if (e != hipSuccess) return set_err(MH_E_DEVICE, std::string("mh_run: ") + hipGetErrorString(e));
     return MH_OK;
+}
+
+int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t tape_count,
+               const mh_assign* as, uint64_t row_first, uint64_t row_count, uint64_t index_base,
+               uint32_t mode, uint64_t* first_hit, uint64_t* hit_count) {
+    return mh_run_rows(ctx, ts, tape_first, tape_count, as, row_first, row_count, index_base, mode,
+                       first_hit, hit_count, 0, nullptr);
 }
 
 int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const mh_assign* as,

@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(kBlock)
 // per-row form stored 8 limbs per applied entry, lane-divergently, and left a 256-row launch
 // four waves: 0.20 ms per launch on average, up to 0.58 (profiles/r03h).
 constexpr u32 kLdsRows = 64;
-constexpr u32 kWaves = 8;
+constexpr u32 kWaves = 16;  // a 256-row launch: 4 workgroups of 16 waves, 4 waves per SIMD
 
 __global__ void __launch_bounds__(kLdsRows * kWaves)
     guided_lds_kernel(u32* assign, u64 stride, u64 first, u64 count, u64 seed, u64 base,
@@ -200,9 +200,30 @@ __global__ void __launch_bounds__(kLdsRows * kWaves)
     }
 }
 
+// one workgroup per tape: the words of its witness row (a row outside the buffer reads as none)
+__global__ void __launch_bounds__(kBlock)
+    witness_rows_kernel(const u32* assign, u64 stride, const u64* first_hit, u64 index_base,
+                        u32 n_cols, u32* out) {
+    const u64 h = first_hit[blockIdx.x];
+    const u64 row = h - index_base;
+    const bool hit = h != ~0ull && h >= index_base && row < stride;
+    const u32 words = n_cols * 8;
+    u32* o = out + (u64)blockIdx.x * words;
+    for (u32 w = threadIdx.x; w < words; w += kBlock) o[w] = hit ? assign[(u64)w * stride + row] : 0u;
+}
+
 }  // namespace
 
 namespace mh {
+
+hipError_t launch_witness_rows(const uint32_t* assign, uint64_t stride, const uint64_t* first_hit,
+                               uint32_t n_tapes, uint64_t index_base, uint32_t n_cols,
+                               uint32_t* out, hipStream_t stream) {
+    if (n_tapes == 0 || n_cols == 0) return hipSuccess;
+    hipLaunchKernelGGL(witness_rows_kernel, dim3(n_tapes), dim3(kBlock), 0, stream, assign, stride,
+                       first_hit, index_base, n_cols, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,

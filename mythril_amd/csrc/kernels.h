@@ -65,6 +65,11 @@ struct KGuide {
 hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
                                   hipStream_t stream);
+// each tape's witness row (mh_run_rows): out[t][w] = column word w (column w / 8, limb w % 8) of
+// the buffer row first_hit[t] - index_base, zero for a tape without a hit
+hipError_t launch_witness_rows(const uint32_t* assign, uint64_t stride, const uint64_t* first_hit,
+                               uint32_t n_tapes, uint64_t index_base, uint32_t n_cols,
+                               uint32_t* out, hipStream_t stream);
 hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uint32_t* sink,
                              hipStream_t stream);
 

@@ -64,6 +64,8 @@ SIGNATURES = {
     "mh_results_reset": (C.c_int32, [_vp, _vp, _vp, C.c_uint32]),
     "mh_run": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
                            C.c_uint64, C.c_uint32, _u64p, _u64p]),
+    "mh_run_rows": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
+                                C.c_uint64, C.c_uint32, _u64p, _u64p, C.c_uint32, _u32p]),
     "mh_run_async": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
                                  C.c_uint64, C.c_uint32, _vp, _vp]),
     "mh_eval_values": (C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint64, C.c_uint64, _u32p]),
@@ -836,6 +838,22 @@ def run(ctx: Context, tapes: CompiledTapes, assign: Assignments, *, tape_first: 
     _check(ctx.lib.mh_run(ctx.h, tapes.h, tape_first, tc, assign.h, row_first, rc, index_base,
                           mode, _ptr(fh, C.c_uint64), _ptr(hc, C.c_uint64)))
     return fh[:tc], hc[:tc]
+
+
+def run_rows(ctx: Context, tapes: CompiledTapes, assign: Assignments, n_cols: int, *,
+             tape_first: int = 0, tape_count: Optional[int] = None, row_first: int = 0,
+             row_count: Optional[int] = None, index_base: int = 0, mode: int = MODE_FIRST_HIT):
+    """Blocking run plus each tape's witness row (mh_run_rows): (first_hit, hit_count,
+    rows u32 [tape, column < n_cols, limb]; zero for a tape without a hit)."""
+    tc = tapes.n_tapes - tape_first if tape_count is None else tape_count
+    rc = assign.capacity - row_first if row_count is None else row_count
+    fh = np.zeros(max(tc, 1), dtype=np.uint64)
+    hc = np.zeros(max(tc, 1), dtype=np.uint64)
+    rows = np.zeros((max(tc, 1), max(n_cols, 1), 8), dtype=np.uint32)
+    _check(ctx.lib.mh_run_rows(ctx.h, tapes.h, tape_first, tc, assign.h, row_first, rc,
+                               index_base, mode, _ptr(fh, C.c_uint64), _ptr(hc, C.c_uint64),
+                               n_cols, _ptr(rows)))
+    return fh[:tc], hc[:tc], rows[:tc, :n_cols]
 
 
 def run_async(ctx: Context, tapes: CompiledTapes, assign: Assignments, d_first_hit: int,

@@ -646,27 +646,21 @@ class Sieve:
                 # a later round runs only the tapes from the first to the last unsolved group
                 g0 = solved.index(False)
                 g1 = len(solved) - solved[::-1].index(False)
-                fh, _ = native.run(self.ctx, ct, assign, mode=native.MODE_FIRST_HIT,
-                                   index_base=base, row_count=n, tape_first=g0,
-                                   tape_count=g1 - g0)
-                fh = [native.NO_HIT] * g0 + fh.tolist()
+                # first witnesses and their rows' columns come back in one copy (mh_run_rows)
+                fh, _, wrows = native.run_rows(self.ctx, ct, assign, len(columns),
+                                               mode=native.MODE_FIRST_HIT, index_base=base,
+                                               row_count=n, tape_first=g0, tape_count=g1 - g0)
                 tr = time.perf_counter()
                 st.add("generate", tb - ta)
                 st.add("run", tr - tb)
                 self.stats.rounds += 1
                 self.stats.rows += n
-                rows_read: Dict[int, np.ndarray] = {}
-                for g, hit in enumerate(fh):
+                for i, hit in enumerate(fh.tolist()):
+                    g = g0 + i
                     if solved[g] or hit == native.NO_HIT:
                         continue
-                    row = hit - base
-                    if row not in rows_read:
-                        td = time.perf_counter()
-                        # the row's columns as 32 little-endian bytes each
-                        rows_read[row] = np.ascontiguousarray(
-                            assign.download(row, 1)[:len(columns), :, 0], dtype="<u4").tobytes()
-                        st.add("download", time.perf_counter() - td)
-                    raw = rows_read[row]
+                    # the row's columns as 32 little-endian bytes each
+                    raw = np.ascontiguousarray(wrows[i], dtype="<u4").tobytes()
                     for c in group_cols[g]:
                         values[columns[c]] = int.from_bytes(raw[32 * c:32 * c + 32], "little")
                     solved[g] = True

@@ -691,3 +691,36 @@ def test_compile_cache_reuses_identical_tapes(gpu_ctx):
     ct = gpu_ctx.compile(ts)
     _, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
     assert [int(v) for v in hc] == oracle(ts)
+
+
+def test_run_rows_returns_witness_columns(gpu_ctx):
+    """mh_run_rows: each tape's first hit and the columns of that row in one copy, equal to
+    mh_run's results and to mh_assign_download of the row; zero rows for tapes without a hit.
+    The set spans several register classes, so the short run's launches overlap on the side
+    streams (capi.cpp mh_run_async fan-out)."""
+    rng = random.Random(9191)
+    ts = TapeSet()
+    fz = TapeFuzzer(rng, ts, n_vars=3, max_depth=4)
+    for _ in range(16):
+        fz.tape()
+    b = ts.builder()
+    x, y = b.var("v0"), b.var("v1")
+    ts.add(b.finish(b.op(Op.BVUGT, b.op(Op.BVUDIV, x, y), b.const(5, 256))))
+    ts.add(b.finish(b.op(Op.EQ, x, b.const(12345, 256))))  # no hit on random rows
+    soa = assignment_soa(rng, ts.n_vars, 256)
+    a = upload(gpu_ctx, soa)
+    ct = gpu_ctx.compile(ts)
+    base = 1 << 20
+    fh, hc = native.run(gpu_ctx, ct, a, mode=native.MODE_FIRST_HIT, index_base=base)
+    fh2, hc2, rows = native.run_rows(gpu_ctx, ct, a, ts.n_vars, mode=native.MODE_FIRST_HIT,
+                                     index_base=base)
+    assert fh.tolist() == fh2.tolist() and hc.tolist() == hc2.tolist()
+    assert int(fh[-1]) == native.NO_HIT and not rows[-1].any()
+    for t, h in enumerate(fh.tolist()):
+        if h == native.NO_HIT:
+            assert not rows[t].any()
+            continue
+        r = h - base
+        assert smt_eval.evaluate(ts.tapes[t].nodes, ts.pool.values, soa_row(soa, r))
+        assert (rows[t] == a.download(r, 1)[:, :, 0]).all()
+    ct.close()

@@ -94,13 +94,13 @@ def test_later_round_runs_only_unsolved_groups(monkeypatch):
 
     fake_device.install(monkeypatch)
     calls = []
-    real = native.run
+    real = native.run_rows
 
-    def recording(ctx, tapes, assign, **kw):
+    def recording(ctx, tapes, assign, n_cols, **kw):
         calls.append((kw.get("tape_first", 0), kw.get("tape_count")))
-        return real(ctx, tapes, assign, **kw)
+        return real(ctx, tapes, assign, n_cols, **kw)
 
-    monkeypatch.setattr(native, "run", recording)
+    monkeypatch.setattr(native, "run_rows", recording)
     ctx = smt.set_context(smt.Context())
     x = symbol_factory.BitVecSym("x", 256)
     y = symbol_factory.BitVecSym("y", 256)
