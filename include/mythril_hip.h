@@ -123,6 +123,10 @@ int32_t mh_ctx_destroy(mh_ctx* ctx);
  * null stream).  The ctx starts on a stream of its own.                                          */
 int32_t mh_ctx_set_stream(mh_ctx* ctx, void* hip_stream);
 int32_t mh_ctx_synchronize(mh_ctx* ctx);
+/* mh_tapes_compile keeps each compiled tape by content (nodes, constant values, column count)
+ * for the ctx's later compiles, up to 16M instruction words (MH_COMPILE_CACHE=0: off).  This drops
+ * them (memory, or a measurement that must not reuse an earlier query's code).                   */
+int32_t mh_ctx_clear_cache(mh_ctx* ctx);
 
 /* ---- tapes ----------------------------------------------------------------------------------- */
 /* nodes: all tapes concatenated; tape_offsets[n_tapes+1] delimit them (node indices).

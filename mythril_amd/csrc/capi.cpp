@@ -59,7 +59,7 @@ struct mh_ctx {
     // compiled tapes by content (the tape's nodes, the values of the constants it reads, the
     // column count): a LASER query's groups mostly repeat its parent's (svm.py:257-262), and a
     // tape's instruction words are self-contained (constants inline), so a repeated tape reuses
-    // its words; cleared beyond compile_cache_limit words
+    // its words; cleared beyond kCacheWords words (mh_tapes_compile) or by mh_ctx_clear_cache
     std::unordered_map<std::string, std::pair<std::vector<uint32_t>, mh::CompiledTape>> compile_cache;
     size_t compile_cache_words = 0;
     // a short run's launches (one per register class) are a few waves each walking a long tape:
@@ -463,6 +463,13 @@ int32_t mh_ctx_destroy(mh_ctx* ctx) {
         return MH_OK;
     }
     ctx_free(ctx);
+    return MH_OK;
+}
+
+int32_t mh_ctx_clear_cache(mh_ctx* ctx) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    ctx->compile_cache.clear();
+    ctx->compile_cache_words = 0;
     return MH_OK;
 }
 

@@ -49,6 +49,7 @@ SIGNATURES = {
     "mh_ctx_destroy": (C.c_int32, [_vp]),
     "mh_ctx_set_stream": (C.c_int32, [_vp, _vp]),
     "mh_ctx_synchronize": (C.c_int32, [_vp]),
+    "mh_ctx_clear_cache": (C.c_int32, [_vp]),
     "mh_tapes_compile": (C.c_int32, [_vp, _vp, _u64p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
                                      C.POINTER(_vp)]),
     "mh_tapes_destroy": (C.c_int32, [_vp]),
@@ -660,6 +661,10 @@ class Context:
 
     def synchronize(self) -> None:
         _check(self.lib.mh_ctx_synchronize(self.h))
+
+    def clear_cache(self) -> None:
+        """Drop the compiled tapes mh_tapes_compile keeps by content (mh_ctx_clear_cache)."""
+        _check(self.lib.mh_ctx_clear_cache(self.h))
 
     def close(self) -> None:
         if self.h:

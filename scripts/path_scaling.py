@@ -8,7 +8,7 @@ SafeMath checks LASER adds along a path), on one Sieve, one JSON line per (shape
 * ``ms_laser`` — the path's last query timed after its parent prefixes were solved in LASER
   order (svm.py:257-262; each prefix keyed as frontend.get_model keys it), median of the last 8
   queries of the path, plus the mean over the whole path (``ms_laser_mean``);
-* ``ms_cold`` — the full path on fresh terms, nothing solved before;
+* ``ms_cold`` — the full path on fresh terms, nothing solved (or compiled) before;
 * ``ms_miss`` — the UNSAT variant's last query in LASER order (what an infeasible JUMPI branch
   pays before z3), and its interpreter time per round (``run`` stage / launches);
 * the stages of the last LASER-order solve and the columns / tape nodes of the query.
@@ -54,6 +54,7 @@ def main():
             rec = {"shape": name, "constraints": n}
             try:
                 ctx, cs = grow(name, n)
+                s.ctx.clear_cache()  # no code of the previous (shorter) path of this shape
                 before = dict(s.stats.stage_s)
                 r0 = s.stats.rounds
                 times, hits, w = laser_order(s, ctx, cs)
@@ -67,6 +68,7 @@ def main():
                     k: round((v - before.get(k, 0.0)) * 1e3 / len(cs), 4)
                     for k, v in s.stats.stage_s.items() if v - before.get(k, 0.0) > 0}
                 ctx, cs = grow(name, n)
+                s.ctx.clear_cache()  # cold: nothing compiled before either
                 gc.collect()
                 t0 = time.perf_counter()
                 wc = s.solve(ctx.b, [c.node for c in cs])

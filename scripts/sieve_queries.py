@@ -5,9 +5,10 @@ hard variants) and report, per query, two latencies (medians of SIEVE_QUERY_REPS
 * ``ms_incremental`` — the query as LASER issues it: every new state's ``is_possible`` extends
   its parent's path condition by one constraint (svm.py:257-262), so the parent prefixes
   cs[:1] .. cs[:-1] are solved first (untimed, with their keys, as frontend.get_model does) on
-  fresh terms, then cs is timed;
+  fresh terms, then cs is timed (the ctx's compiled-tape cache cleared before the prefixes: it
+  holds the parents' tapes, as in LASER, not an earlier repetition's);
 * ``ms_cold`` — the same query on fresh terms with nothing solved before it (the first query
-  that reads these calldata words / storage slots).
+  that reads these calldata words / storage slots; compiled-tape cache cleared).
 
 plus hit or miss, launches, per-stage milliseconds of the last timed incremental solve, and any
 exception (the front end swallows them to fall back; this script shows them).  One JSON line
@@ -62,6 +63,9 @@ def main():
         try:
             inc, cold = [], []
             for _ in range(reps):
+                # the ctx keeps compiled tapes by content: a repetition must not reuse the code of
+                # the one before (the prefixes below refill it as LASER's parents would)
+                s.ctx.clear_cache()
                 qctx, cs = fresh(kind, name)
                 for k in range(1, len(cs)):
                     solve(s, qctx, cs[:k])
@@ -75,6 +79,7 @@ def main():
                           for k, v in s.stats.stage_s.items() if v - before.get(k, 0.0) > 0}
                 rounds = s.stats.rounds - r0
                 qctx, cs = fresh(kind, name)
+                s.ctx.clear_cache()
                 gc.collect()
                 t0 = time.perf_counter()
                 wc = solve(s, qctx, cs)
