@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <iterator>
 #include <map>
 #include <memory>
 #include <set>
@@ -314,12 +315,19 @@ struct Harvester {
              ArenaAlloc<std::pair<const AVec<uint32_t>, uint32_t>>> hint_ids;
     AVec<Alts> hint_alts;      // by id: the alternatives a hint set holds
     AVec<char> hint_done;      // by id: already a hint of this query
+    // by id, for prune_hints: the one column every alternative sets (-1: not a single-column
+    // set) and the largest / smallest value it proposes (a hint set never changes once made)
+    AVec<int32_t> hint_col;
+    AVec<V> hint_hi, hint_lo;
     std::unordered_map<const Alts*, uint32_t, std::hash<const Alts*>, std::equal_to<const Alts*>,
                        ArenaAlloc<std::pair<const Alts* const, uint32_t>>> hint_of_result;
     AVec<std::shared_ptr<const Alts>> hint_results;
     int n_hints = 0;
     std::vector<std::vector<std::vector<Copy>>> copy_sets;
     std::vector<U> query_consts;
+    // the last query's conjuncts and constants (sorted, unique), kept across a session's queries
+    std::vector<uint32_t> last_conj;
+    std::vector<U> last_qc;
     std::map<int, std::vector<U>> consts_by_width;
     std::map<int, std::vector<uint32_t>> const_ids_by_width;  // their interned ids
     // eq_nodes per conjunct (a function of the tape prefix: kept across a session's queries)
@@ -709,6 +717,18 @@ struct Harvester {
             for (const Alt& a : alts) if (!a.empty()) kept.push_back(a);
             hint_alts.push_back(head(kept, kMaxAlts));
             hint_done.push_back(0);
+            const Alts& ha = hint_alts.back();
+            int32_t col = ha.empty() ? -1 : (int32_t)ha[0][0].first;
+            for (const Alt& a : ha)
+                if (a.size() != 1 || (int32_t)a[0].first != col) { col = -1; break; }
+            V mx{}, mn{};
+            if (col >= 0) {
+                mx = mn = ha[0][0].second;
+                for (const Alt& a : ha) { mx = std::max(mx, a[0].second); mn = std::min(mn, a[0].second); }
+            }
+            hint_col.push_back(col);
+            hint_hi.push_back(mx);
+            hint_lo.push_back(mn);
         }
         hint_results.push_back(r.p);  // keeps the identity valid
         hint_of_result.emplace(r.p.get(), got.first->second);
@@ -812,9 +832,13 @@ struct Harvester {
                  std::vector<std::pair<int, const Alts*>>& out_sets,
                  std::vector<std::vector<std::vector<Copy>>>& out_copies) {
         const std::vector<uint32_t> conj = conjuncts(root);
-        {   // the query's constants
+        {   // the query's constants; a query whose conjuncts extend the last one's (LASER order)
+            // adds only its new conjuncts' constants to the last set (the same sorted union)
+            const bool extends = conj.size() >= last_conj.size() &&
+                                 std::equal(last_conj.begin(), last_conj.end(), conj.begin());
+            const size_t from = extends ? last_conj.size() : 0;
             std::vector<char> seen(nd.size(), 0);
-            std::vector<uint32_t> st(conj.begin(), conj.end());
+            std::vector<uint32_t> st(conj.begin() + (long)from, conj.end());
             std::vector<U> qc;
             while (!st.empty()) {
                 const uint32_t n = st.back();
@@ -829,7 +853,17 @@ struct Harvester {
             }
             std::sort(qc.begin(), qc.end());
             qc.erase(std::unique(qc.begin(), qc.end()), qc.end());
-            query_consts.swap(qc);
+            if (extends && !last_qc.empty()) {
+                std::vector<U> all;
+                all.reserve(last_qc.size() + qc.size());
+                std::merge(last_qc.begin(), last_qc.end(), qc.begin(), qc.end(),
+                           std::back_inserter(all));
+                all.erase(std::unique(all.begin(), all.end()), all.end());
+                qc.swap(all);
+            }
+            query_consts = qc;
+            last_qc.swap(qc);
+            last_conj = conj;
         }
         if (parent && !parent->empty()) sets.push_back({kProbParent, {*parent}});
         std::vector<char> seen_eq(nd.size(), 0);
@@ -1000,13 +1034,8 @@ struct Harvester {
     // kHintsPerColumn with the largest and with the smallest values stay (in their order)
     std::vector<uint32_t> prune_hints() const {
         std::map<uint32_t, std::vector<size_t>> by_col;
-        for (size_t i = 0; i < hints.size(); ++i) {
-            const Alts& alts = hint_alts[hints[i]];
-            bool single = !alts.empty();
-            for (const Alt& a : alts)
-                if (a.size() != 1 || a[0].first != alts[0][0].first) { single = false; break; }
-            if (single) by_col[alts[0][0].first].push_back(i);
-        }
+        for (size_t i = 0; i < hints.size(); ++i)
+            if (hint_col[hints[i]] >= 0) by_col[(uint32_t)hint_col[hints[i]]].push_back(i);
         std::vector<char> drop(hints.size(), 0);
         for (auto& kv : by_col) {
             const std::vector<size_t>& idx = kv.second;
@@ -1014,11 +1043,8 @@ struct Harvester {
             // extremes per hint, indexed by position in idx (not by hint: one column's hints)
             std::vector<V> hi_v(idx.size()), lo_v(idx.size());
             for (size_t j = 0; j < idx.size(); ++j) {
-                const Alts& alts = hint_alts[hints[idx[j]]];
-                V mx = alts[0][0].second, mn = mx;
-                for (const Alt& a : alts) { mx = std::max(mx, a[0].second); mn = std::min(mn, a[0].second); }
-                hi_v[j] = mx;
-                lo_v[j] = mn;
+                hi_v[j] = hint_hi[hints[idx[j]]];
+                lo_v[j] = hint_lo[hints[idx[j]]];
             }
             std::vector<size_t> hi(idx.size()), lo(idx.size());
             for (size_t j = 0; j < idx.size(); ++j) hi[j] = lo[j] = j;
