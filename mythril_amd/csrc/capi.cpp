@@ -67,6 +67,9 @@ struct mh_ctx {
     // by events) instead of queueing behind each other; created on first use
     hipStream_t side[kSideStreams] = {};
     hipEvent_t fork_ev = nullptr, join_ev[kSideStreams] = {};
+    // the wave masks of a conjunct-parallel short run (grow-only)
+    unsigned long long* d_masks = nullptr;
+    size_t masks_bytes = 0;
 };
 
 namespace {
@@ -214,6 +217,15 @@ struct mh_tapeset {
     std::vector<uint32_t> ids_rest;
     uint32_t bucket_off_rest[mh::kNumVariants + 1] = {};
     mh_jit_info jinfo{};
+    // conjunct-parallel short runs (mh_run_async): a long tape's root conjunction cut into parts
+    // of consecutive conjuncts, each compiled as a tape of its own (ids n_tapes, n_tapes + 1, ..,
+    // in the order of their tapes) and bucketed like the tapes; the buckets without the split
+    // tapes; per split tape, ascending: (tape, first part id, parts)
+    uint32_t n_parts = 0;
+    std::vector<uint32_t> ids_unsplit, part_ids, part_parent, split_tab;
+    uint32_t bucket_off_unsplit[mh::kNumVariants + 1] = {};
+    uint32_t bucket_off_parts[mh::kNumVariants + 1] = {};
+    uint32_t *d_ids_unsplit = nullptr, *d_part_ids = nullptr, *d_split = nullptr;
 };
 
 struct mh_assign {
@@ -440,6 +452,7 @@ void ctx_free(mh_ctx* ctx) {
         if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
     }
     if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
+    if (ctx->d_masks) (void)hipFree(ctx->d_masks);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->d_buf) (void)hipFree(ctx->d_buf);
     if (ctx->h_buf) (void)hipHostFree(ctx->h_buf);
@@ -506,6 +519,9 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     std::vector<mh_dev_tape> heads(n_tapes);
     std::vector<mh_tape_info> info(n_tapes);
     std::vector<uint32_t> ids, bucket_off(mh::kNumVariants + 1, 0);
+    // conjunct-parallel parts (mh_tapeset): heads n_tapes.. and their buckets
+    std::vector<uint32_t> ids_unsplit, part_ids, part_parent, split_tab;
+    uint32_t off_unsplit[mh::kNumVariants + 1] = {}, off_parts[mh::kNumVariants + 1] = {};
     try {
         std::vector<std::vector<uint32_t>> tw(n_tapes);
         static const bool use_cache = [] {
@@ -514,55 +530,118 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
         }();
         constexpr size_t kCacheWords = (size_t)16 << 20;  // 128 MB of instruction words
         std::string key;
-        for (uint32_t t = 0; t < n_tapes; ++t) {
-            const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
-            if (e <= b) return set_err(MH_E_INVALID, "tape " + std::to_string(t) + " is empty");
+        // one tape's words and summary, from the cache when its content was compiled before
+        auto compile_one = [&](const mh_node* tn, size_t nn, std::vector<uint32_t>& w,
+                               mh::CompiledTape& ct, std::string& err) -> int32_t {
             if (use_cache) {  // the tape's content: nodes, constant values, column count
                 key.assign(reinterpret_cast<const char*>(&n_vars), sizeof n_vars);
-                key.append(reinterpret_cast<const char*>(nodes + b), (size_t)(e - b) * sizeof(mh_node));
-                for (uint64_t i = b; i < e; ++i)
-                    if (nodes[i].op == MH_OP_CONST && nodes[i].imm0 < n_consts)
-                        key.append(reinterpret_cast<const char*>(consts + 8ull * nodes[i].imm0), 32);
+                key.append(reinterpret_cast<const char*>(tn), nn * sizeof(mh_node));
+                for (size_t i = 0; i < nn; ++i)
+                    if (tn[i].op == MH_OP_CONST && tn[i].imm0 < n_consts)
+                        key.append(reinterpret_cast<const char*>(consts + 8ull * tn[i].imm0), 32);
                 auto hit = ctx->compile_cache.find(key);
                 if (hit != ctx->compile_cache.end()) {
-                    tw[t] = hit->second.first;
-                    const mh::CompiledTape& ct = hit->second.second;
-                    heads[t] = mh_dev_tape{0, ct.n_insns, ct.root_bool, ct.n_regs};
-                    info[t] = mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops};
-                    continue;
+                    w = hit->second.first;
+                    ct = hit->second.second;
+                    return MH_OK;
                 }
             }
-            mh::CompiledTape ct;
-            std::string err;
-            int32_t r = mh::compile_tape(nodes + b, (size_t)(e - b), consts, n_consts, n_vars,
-                                         dconsts, dindex, tw[t], ct, err);
-            if (r != MH_OK) return set_err(r, "tape " + std::to_string(t) + ": " + err);
-            heads[t] = mh_dev_tape{0, ct.n_insns, ct.root_bool, ct.n_regs};
-            info[t] = mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops};
-            if (use_cache) {
-                if (ctx->compile_cache_words + tw[t].size() > kCacheWords) {
+            const int32_t r = mh::compile_tape(tn, nn, consts, n_consts, n_vars, dconsts, dindex,
+                                               w, ct, err);
+            if (r == MH_OK && use_cache) {
+                if (ctx->compile_cache_words + w.size() > kCacheWords) {
                     ctx->compile_cache.clear();
                     ctx->compile_cache_words = 0;
                 }
-                ctx->compile_cache_words += tw[t].size();
-                ctx->compile_cache.emplace(key, std::make_pair(tw[t], ct));
+                ctx->compile_cache_words += w.size();
+                ctx->compile_cache.emplace(key, std::make_pair(w, ct));
             }
+            return r;
+        };
+        for (uint32_t t = 0; t < n_tapes; ++t) {
+            const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
+            if (e <= b) return set_err(MH_E_INVALID, "tape " + std::to_string(t) + " is empty");
+            mh::CompiledTape ct;
+            std::string err;
+            const int32_t r = compile_one(nodes + b, (size_t)(e - b), tw[t], ct, err);
+            if (r != MH_OK) return set_err(r, "tape " + std::to_string(t) + ": " + err);
+            heads[t] = mh_dev_tape{0, ct.n_insns, ct.root_bool, ct.n_regs};
+            info[t] = mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops};
+        }
+        // conjunct-parallel parts of the long tapes (a query round's latency is its longest
+        // tape walked by one wave per SIMD: parts walk in parallel, mh_run_async); MH_SPLIT_INSNS
+        // = the instruction slots from which a tape is cut (0: never), one part per that many
+        const char* se = std::getenv("MH_SPLIT_INSNS");
+        const uint32_t split_min = se ? (uint32_t)std::strtoul(se, nullptr, 10) : 384u;
+        constexpr uint32_t kMaxParts = 8;
+        std::vector<std::vector<uint32_t>> pw;
+        std::vector<mh_tape_info> pinfo;
+        std::vector<mh_dev_tape> pheads;
+        for (uint32_t t = 0; split_min && t < n_tapes; ++t) {
+            if (info[t].n_insns < split_min || !heads[t].root_bool) continue;
+            const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
+            const uint32_t want = std::min<uint32_t>(kMaxParts, (info[t].n_insns + split_min - 1) / split_min);
+            std::vector<std::vector<mh_node>> parts;
+            if (!mh::split_conjunction(nodes + b, (uint32_t)(e - b), std::max<uint32_t>(want, 2), parts))
+                continue;
+            const size_t p0 = pw.size();
+            bool ok = true;
+            for (const auto& tp : parts) {
+                std::vector<uint32_t> w;
+                mh::CompiledTape ct;
+                std::string err;
+                if (compile_one(tp.data(), tp.size(), w, ct, err) != MH_OK || !ct.root_bool) {
+                    ok = false;  // (register pressure of a part, say): the tape runs whole
+                    break;
+                }
+                pw.push_back(std::move(w));
+                pinfo.push_back(mh_tape_info{ct.n_nodes, ct.n_insns, ct.n_regs, ct.features, ct.alg_ops});
+                pheads.push_back(mh_dev_tape{0, ct.n_insns, ct.root_bool, ct.n_regs});
+            }
+            if (!ok) {
+                pw.resize(p0);
+                pinfo.resize(p0);
+                pheads.resize(p0);
+                continue;
+            }
+            split_tab.insert(split_tab.end(), {t, n_tapes + (uint32_t)p0, (uint32_t)parts.size()});
+            for (size_t i = p0; i < pw.size(); ++i) part_parent.push_back(t);
         }
         // bucket by kernel variant; instruction words laid out bucket by bucket (ascending tape
         // id inside a bucket) so that any run of consecutive bucket entries is one contiguous
-        // range of words, which the kernel stages into LDS with one coalesced copy
+        // range of words, which the kernel stages into LDS with one coalesced copy; the parts
+        // after the tapes, likewise
+        std::vector<char> is_split(n_tapes, 0);
+        for (size_t i = 0; i < split_tab.size(); i += 3) is_split[split_tab[i]] = 1;
         std::vector<std::vector<uint32_t>> bucket(mh::kNumVariants);
         for (uint32_t t = 0; t < n_tapes; ++t)
             bucket[mh::variant_of(info[t].n_regs, info[t].features)].push_back(t);
         for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
             bucket_off[v] = (uint32_t)ids.size();
+            off_unsplit[v] = (uint32_t)ids_unsplit.size();
             for (uint32_t t : bucket[v]) {
                 heads[t].insn_off = (uint32_t)(words.size() / 2);
                 words.insert(words.end(), tw[t].begin(), tw[t].end());
                 ids.push_back(t);
+                if (!is_split[t]) ids_unsplit.push_back(t);
             }
         }
         bucket_off[mh::kNumVariants] = (uint32_t)ids.size();
+        off_unsplit[mh::kNumVariants] = (uint32_t)ids_unsplit.size();
+        std::vector<std::vector<uint32_t>> pbucket(mh::kNumVariants);
+        for (uint32_t i = 0; i < (uint32_t)pw.size(); ++i)
+            pbucket[mh::variant_of(pinfo[i].n_regs, pinfo[i].features)].push_back(i);
+        heads.resize(n_tapes + pw.size());
+        for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+            off_parts[v] = (uint32_t)part_ids.size();
+            for (uint32_t i : pbucket[v]) {
+                heads[n_tapes + i] = pheads[i];
+                heads[n_tapes + i].insn_off = (uint32_t)(words.size() / 2);
+                words.insert(words.end(), pw[i].begin(), pw[i].end());
+                part_ids.push_back(n_tapes + i);
+            }
+        }
+        off_parts[mh::kNumVariants] = (uint32_t)part_ids.size();
     } catch (const std::bad_alloc&) {
         return set_err(MH_E_NOMEM, "host allocation during compile");
     }
@@ -588,17 +667,28 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
         return set_err(MH_E_NOMEM, "host copy of the tapes");
     }
     ts->ids = std::move(ids);
-    for (uint32_t v = 0; v <= mh::kNumVariants; ++v) ts->bucket_off[v] = bucket_off[v];
+    for (uint32_t v = 0; v <= mh::kNumVariants; ++v) {
+        ts->bucket_off[v] = bucket_off[v];
+        ts->bucket_off_unsplit[v] = off_unsplit[v];
+        ts->bucket_off_parts[v] = off_parts[v];
+    }
     ts->info = std::move(info);
+    ts->n_parts = (uint32_t)part_parent.size();
+    ts->ids_unsplit = std::move(ids_unsplit);
+    ts->part_ids = std::move(part_ids);
+    ts->part_parent = std::move(part_parent);
+    ts->split_tab = std::move(split_tab);
     // one device block and one async copy from pinned staging (a query compiles a tape set per
     // call: four synchronous pageable copies cost more than the kernels they feed)
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t b_insns = words.size() * sizeof(uint32_t),
-                 b_ids = std::max<size_t>(1, ts->ids.size()) * sizeof(uint32_t),
-                 b_tapes = std::max<size_t>(1, n_tapes) * sizeof(mh_dev_tape),
+    auto b_u32 = [](const std::vector<uint32_t>& v) { return std::max<size_t>(1, v.size()) * 4; };
+    const size_t b_insns = words.size() * sizeof(uint32_t), b_ids = b_u32(ts->ids),
+                 b_tapes = std::max<size_t>(1, heads.size()) * sizeof(mh_dev_tape),
                  b_consts = dconsts.size() * sizeof(uint32_t);
     const size_t o_ids = al(b_insns), o_tapes = o_ids + al(b_ids), o_consts = o_tapes + al(b_tapes),
-                 total = o_consts + al(b_consts);
+                 o_unsplit = o_consts + al(b_consts), o_parts = o_unsplit + al(b_u32(ts->ids_unsplit)),
+                 o_split = o_parts + al(b_u32(ts->part_ids)),
+                 total = o_split + al(b_u32(ts->split_tab));
     hipError_t e = pool_alloc(ctx, (char**)&ts->d_block, total);
     if (e == hipSuccess && ctx->stage_pending) {
         e = hipEventSynchronize(ctx->stage_ev);
@@ -617,13 +707,22 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
         char* h = (char*)ctx->h_stage;
         std::memcpy(h, words.data(), b_insns);
         if (!ts->ids.empty()) std::memcpy(h + o_ids, ts->ids.data(), ts->ids.size() * sizeof(uint32_t));
-        if (n_tapes) std::memcpy(h + o_tapes, heads.data(), n_tapes * sizeof(mh_dev_tape));
+        if (!heads.empty()) std::memcpy(h + o_tapes, heads.data(), heads.size() * sizeof(mh_dev_tape));
         std::memcpy(h + o_consts, dconsts.data(), b_consts);
+        auto put = [&](size_t o, const std::vector<uint32_t>& v) {
+            if (!v.empty()) std::memcpy(h + o, v.data(), v.size() * sizeof(uint32_t));
+        };
+        put(o_unsplit, ts->ids_unsplit);
+        put(o_parts, ts->part_ids);
+        put(o_split, ts->split_tab);
         char* d = (char*)ts->d_block;
         ts->d_insns = (uint2*)d;
         ts->d_ids = (uint32_t*)(d + o_ids);
         ts->d_tapes = (mh_dev_tape*)(d + o_tapes);
         ts->d_consts = (uint32_t*)(d + o_consts);
+        ts->d_ids_unsplit = (uint32_t*)(d + o_unsplit);
+        ts->d_part_ids = (uint32_t*)(d + o_parts);
+        ts->d_split = (uint32_t*)(d + o_split);
         e = hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->stream);
         if (e == hipSuccess) e = hipEventRecord(ctx->stage_ev, ctx->stream);
         if (e == hipSuccess) ctx->stage_pending = true;
@@ -899,9 +998,18 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
     p.hit_count = reinterpret_cast<unsigned long long*>(d_hit_count);
     // the native code takes the jitted tapes of a whole-set run; the interpreter the rest
     const bool use_jit = ts->has_jit && tape_first == 0 && tape_count == ts->n_tapes;
-    const std::vector<uint32_t>& ids = use_jit ? ts->ids_rest : ts->ids;
-    const uint32_t* boff = use_jit ? ts->bucket_off_rest : ts->bucket_off;
-    uint32_t* d_ids = use_jit ? ts->d_ids_rest : ts->d_ids;
+    // a short interpreter run over a set with split tapes runs their parts instead (conjunct-
+    // parallel: each part is a tape of its own, its waves write Bool masks, the combine kernel
+    // ANDs them per split tape); MH_SPLIT_ROWS = the largest such run
+    static const uint64_t split_rows = [] {
+        const char* e = std::getenv("MH_SPLIT_ROWS");
+        return e ? std::strtoull(e, nullptr, 10) : 65536ull;
+    }();
+    const bool split = !use_jit && ts->n_parts && row_count <= split_rows;
+    const std::vector<uint32_t>& ids = use_jit ? ts->ids_rest : split ? ts->ids_unsplit : ts->ids;
+    const uint32_t* boff = use_jit ? ts->bucket_off_rest
+                                   : split ? ts->bucket_off_unsplit : ts->bucket_off;
+    uint32_t* d_ids = use_jit ? ts->d_ids_rest : split ? ts->d_ids_unsplit : ts->d_ids;
     // the interpreter's tapes of each kernel-variant bucket inside the requested range
     const uint32_t *lo[mh::kNumVariants], *hi[mh::kNumVariants];
     for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
@@ -911,6 +1019,40 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
         hi[v] = std::lower_bound(lo[v], e, tape_first + tape_count);
         // refused before anything is launched
         if (hi[v] != lo[v] && !mh::variant_fits(v, p.capacity)) return refuse_capacity(p.capacity);
+    }
+    // the split tapes inside the range (split_tab ascends by tape, part ids with it) and their
+    // parts per bucket
+    uint32_t s_lo = 0, s_hi = 0, part_lo = 0, part_hi = 0;
+    const uint32_t *plo[mh::kNumVariants] = {}, *phi[mh::kNumVariants] = {};
+    if (split) {
+        const uint32_t n_split = (uint32_t)ts->split_tab.size() / 3;
+        while (s_lo < n_split && ts->split_tab[3 * s_lo] < tape_first) ++s_lo;
+        s_hi = s_lo;
+        while (s_hi < n_split && ts->split_tab[3 * s_hi] < tape_first + tape_count) ++s_hi;
+        if (s_hi > s_lo) {
+            part_lo = ts->split_tab[3 * s_lo + 1];
+            part_hi = ts->split_tab[3 * (s_hi - 1) + 1] + ts->split_tab[3 * (s_hi - 1) + 2];
+        }
+        for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+            const uint32_t* b = ts->part_ids.data() + ts->bucket_off_parts[v];
+            const uint32_t* e = ts->part_ids.data() + ts->bucket_off_parts[v + 1];
+            plo[v] = std::lower_bound(b, e, part_lo);
+            phi[v] = std::lower_bound(plo[v], e, part_hi);
+            if (phi[v] != plo[v] && !mh::variant_fits(v, p.capacity)) return refuse_capacity(p.capacity);
+        }
+    }
+    const uint64_t mask_stride = mh::sieve_mask_stride(row_count);
+    if (part_hi > part_lo) {
+        const size_t need = (size_t)(part_hi - part_lo) * mask_stride * sizeof(unsigned long long);
+        if (need > ctx->masks_bytes) {
+            if (ctx->d_masks) MH_HIP(hipFree(ctx->d_masks));
+            ctx->d_masks = nullptr;
+            ctx->masks_bytes = 0;
+            size_t n = 1 << 16;
+            while (n < need) n <<= 1;
+            MH_HIP(hipMalloc(&ctx->d_masks, n));
+            ctx->masks_bytes = n;
+        }
     }
     std::pair<hipEvent_t, hipEvent_t> sp{nullptr, nullptr};
     if (ctx->timing) {
@@ -936,25 +1078,31 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
     // (over the whole set only: every bucket is then whole, so a class's buckets are one range)
     const bool merge = !use_jit && row_count <= merge_rows && tape_first == 0 &&
                        tape_count == ts->n_tapes;
-    struct Launch { const uint32_t *b, *e; uint32_t variant; };
-    Launch launches[mh::kNumVariants];
+    struct Launch { const uint32_t *b, *e; uint32_t variant; bool part; };
+    Launch launches[2 * mh::kNumVariants];
     uint32_t n_launch = 0;
-    for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
-        if (hi[v] == lo[v]) continue;
-        uint32_t last = v;  // with merging: the class's last nonempty bucket, ids lo[v]..hi[last]
-        if (merge)
-            for (uint32_t u = v + 1; u < (v / 4 + 1) * 4; ++u)
-                if (hi[u] != lo[u]) last = u;
-        launches[n_launch++] = Launch{lo[v], hi[last], last};
-        v = last;
+    for (int part = 0; part < 2; ++part) {
+        const uint32_t* const* L = part ? plo : lo;
+        const uint32_t* const* H = part ? phi : hi;
+        if (part && !split) break;
+        for (uint32_t v = 0; v < mh::kNumVariants; ++v) {
+            if (H[v] == L[v]) continue;
+            uint32_t last = v;  // with merging: the class's last nonempty bucket, L[v]..H[last]
+            if (merge)
+                for (uint32_t u = v + 1; u < (v / 4 + 1) * 4; ++u)
+                    if (H[u] != L[u]) last = u;
+            launches[n_launch++] = Launch{L[v], H[last], last, part != 0};
+            v = last;
+        }
     }
     static const bool fanout = [] {
         const char* e = std::getenv("MH_FANOUT");
         return !(e && e[0] == '0');
     }();
     // a short run's launches overlap on the side streams; the results they write are disjoint
-    // (per tape), and the join puts everything after them back in `stream`'s order
-    const uint32_t n_side = fanout && merge ? std::min(n_launch - (n_launch > 0), kSideStreams) : 0;
+    // (per tape / per part), and the join puts everything after them back in `stream`'s order
+    const uint32_t n_side =
+        fanout && (merge || split) ? std::min(n_launch - (n_launch > 0), kSideStreams) : 0;
     if (n_side) {
         if (!ctx->fork_ev) MH_HIP(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
         for (uint32_t i = 0; i < n_side; ++i) {
@@ -967,16 +1115,30 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
         for (uint32_t i = 0; i < n_side; ++i) MH_HIP(hipStreamWaitEvent(ctx->side[i], ctx->fork_ev, 0));
     }
     for (uint32_t i = 0; i < n_launch; ++i) {
-        p.tape_ids = d_ids + (launches[i].b - ids.data());
-        p.n_ids = (uint32_t)(launches[i].e - launches[i].b);
+        mh::KParams q = p;
+        if (launches[i].part) {  // wave masks instead of results
+            q.tape_ids = ts->d_part_ids + (launches[i].b - ts->part_ids.data());
+            q.masks = ctx->d_masks;
+            q.mask_base = part_lo;
+            q.mask_stride = mask_stride;
+            q.first_hit = nullptr;
+            q.hit_count = nullptr;
+        } else {
+            q.tape_ids = d_ids + (launches[i].b - ids.data());
+        }
+        q.n_ids = (uint32_t)(launches[i].e - launches[i].b);
         // launch 0 on the ctx stream, the others round-robin over the side streams
         hipStream_t s = n_side && i ? ctx->side[(i - 1) % n_side] : ctx->stream;
-        MH_HIP(mh::launch_sieve(p, launches[i].variant, s));
+        MH_HIP(mh::launch_sieve(q, launches[i].variant, s));
     }
     for (uint32_t i = 0; i < n_side; ++i) {
         MH_HIP(hipEventRecord(ctx->join_ev[i], ctx->side[i]));
         MH_HIP(hipStreamWaitEvent(ctx->stream, ctx->join_ev[i], 0));
     }
+    if (s_hi > s_lo)  // every part's masks written: the split tapes' results
+        MH_HIP(mh::launch_combine(ctx->d_masks, mask_stride, ts->d_split + 3 * s_lo, s_hi - s_lo,
+                                  tape_first, index_base + row_first, p.first_hit, p.hit_count,
+                                  ctx->stream));
     if (ctx->timing) MH_HIP(hipEventRecord(sp.second, ctx->stream));
     return MH_OK;
 }

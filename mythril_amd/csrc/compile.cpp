@@ -22,6 +22,7 @@
 #include "exec.h"
 
 #include <algorithm>
+#include <numeric>
 #include <cstdlib>
 #include <functional>
 #include <cstring>
@@ -1522,5 +1523,106 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
 }
 
 }  // namespace
+
+static int ir_arity(uint8_t op) {
+    switch (op) {
+        case MH_OP_CONST: case MH_OP_VAR: case MH_OP_TRUE: case MH_OP_FALSE: return 0;
+        case MH_OP_BVNEG: case MH_OP_BVNOT: case MH_OP_NOT: case MH_OP_EXTRACT: case MH_OP_ZEXT:
+        case MH_OP_SEXT: case MH_OP_KECCAK: return 1;
+        case MH_OP_ITE: case MH_OP_EVM_ADDMOD: case MH_OP_EVM_MULMOD: return 3;
+        default: return 2;
+    }
+}
+
+// compile.h split_conjunction
+bool split_conjunction(const mh_node* nd, uint32_t n, uint32_t want,
+                       std::vector<std::vector<mh_node>>& out) {
+    std::vector<uint32_t> conj, st{n - 1};
+    while (!st.empty()) {  // the root's AND chain, left to right
+        const uint32_t u = st.back();
+        st.pop_back();
+        if (nd[u].op == MH_OP_AND && nd[u].width == 0 && nd[u].a < u && nd[u].b < u) {
+            st.push_back(nd[u].b);
+            st.push_back(nd[u].a);
+        } else {
+            conj.push_back(u);
+        }
+    }
+    if (conj.size() < 2 || want < 2) return false;
+    std::vector<uint32_t> mark(n, 0), cone(conj.size(), 0);
+    uint32_t stamp = 0;
+    auto reach = [&](uint32_t root, uint32_t s, std::vector<uint32_t>* keep) {
+        uint32_t cnt = 0;
+        std::vector<uint32_t> stk{root};
+        while (!stk.empty()) {
+            const uint32_t u = stk.back();
+            stk.pop_back();
+            if (u >= n || mark[u] == s) continue;
+            mark[u] = s;
+            ++cnt;
+            if (keep) keep->push_back(u);
+            const int k = ir_arity(nd[u].op);
+            if (k >= 1) stk.push_back(nd[u].a);
+            if (k >= 2) stk.push_back(nd[u].b);
+            if (k >= 3) stk.push_back(nd[u].c);
+        }
+        return cnt;
+    };
+    uint64_t total = 0;
+    for (size_t i = 0; i < conj.size(); ++i) total += cone[i] = reach(conj[i], ++stamp, nullptr);
+    const uint32_t parts = std::min<uint32_t>(want, (uint32_t)conj.size());
+    out.clear();
+    size_t i = 0;
+    for (uint32_t p = 0; p < parts && i < conj.size(); ++p) {
+        // consecutive conjuncts up to this part's share of what is left
+        const uint64_t left = std::accumulate(cone.begin() + (long)i, cone.end(), (uint64_t)0);
+        const uint64_t share = (left + (parts - p) - 1) / (parts - p);
+        const size_t rest_parts = parts - p - 1;
+        std::vector<uint32_t> mine;
+        uint64_t sum = 0;
+        while (i < conj.size() && (mine.empty() || (sum < share && conj.size() - i > rest_parts))) {
+            sum += cone[i];
+            mine.push_back(conj[i++]);
+        }
+        if (p + 1 == parts)
+            while (i < conj.size()) mine.push_back(conj[i++]);
+        std::vector<uint32_t> keep;
+        ++stamp;
+        for (uint32_t r : mine) reach(r, stamp, &keep);
+        std::sort(keep.begin(), keep.end());
+        std::vector<uint32_t> idx(n, UINT32_MAX);
+        std::vector<mh_node> tp;
+        tp.reserve(keep.size() + mine.size());
+        for (uint32_t u : keep) {
+            mh_node x = nd[u];
+            const int k = ir_arity(x.op);
+            if (k >= 1) x.a = idx[x.a];
+            if (k >= 2) x.b = idx[x.b];
+            if (k >= 3) x.c = idx[x.c];
+            idx[u] = (uint32_t)tp.size();
+            tp.push_back(x);
+        }
+        uint32_t acc = idx[mine[0]];
+        for (size_t j = 1; j < mine.size(); ++j) {
+            mh_node a{};
+            a.op = MH_OP_AND;
+            a.width = 0;
+            a.a = acc;
+            a.b = idx[mine[j]];
+            acc = (uint32_t)tp.size();
+            tp.push_back(a);
+        }
+        if (acc != tp.size() - 1) {  // a lone conjunct that is not its cone's last node
+            mh_node a{};
+            a.op = MH_OP_AND;
+            a.a = acc;
+            a.b = acc;
+            tp.push_back(a);
+        }
+        out.push_back(std::move(tp));
+    }
+    return out.size() >= 2;
+}
+
 
 }  // namespace mh

@@ -74,4 +74,12 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
                      std::unordered_map<std::string, uint32_t>& dconst_index,
                      std::vector<uint32_t>& words, CompiledTape& out, std::string& err);
 
+// A tape whose root is a conjunction, cut into at most `want` parts of consecutive conjuncts of
+// about equal cone size: each part the nodes its conjuncts reach, in tape order and re-indexed,
+// then the AND of its conjuncts, so a row satisfies the tape iff it satisfies every part (the
+// conjunct-parallel short runs of mh_run_async).  False when the root has fewer than two
+// conjuncts or `want` < 2.
+bool split_conjunction(const mh_node* nodes, uint32_t n_nodes, uint32_t want,
+                       std::vector<std::vector<mh_node>>& out);
+
 }  // namespace mh

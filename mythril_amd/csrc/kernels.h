@@ -24,6 +24,13 @@ struct KParams {
     unsigned long long* first_hit;  // [tapes of the run]
     unsigned long long* hit_count;  // [tapes of the run]
     uint32_t* values_out;           // parity path: [n_ids][8][row_count] root values, or null
+    // conjunct-parallel short runs (capi.cpp mh_run_async): each wave of a part-tape writes its
+    // 64-row Bool mask to masks[(tape id - mask_base) * mask_stride + wave of the run] instead
+    // of first hits / counts, which the combine kernel then ANDs per split tape
+    unsigned long long* masks;
+    uint32_t mask_base;
+    uint32_t pad2;
+    uint64_t mask_stride;           // waves of the run's grid (sieve_mask_stride)
 };
 
 // Kernel variants: register-file size class (NR 7 / 9 / 15) x feature set (asm only / + C++
@@ -70,6 +77,15 @@ hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t fi
 hipError_t launch_witness_rows(const uint32_t* assign, uint64_t stride, const uint64_t* first_hit,
                                uint32_t n_tapes, uint64_t index_base, uint32_t n_cols,
                                uint32_t* out, hipStream_t stream);
+// waves a run of row_count rows launches (the masks' row stride of a conjunct-parallel run)
+uint64_t sieve_mask_stride(uint64_t row_count);
+// per split tape i (split[3i] = tape id, split[3i+1] = its first part's mask row, split[3i+2] =
+// parts): the AND of its parts' masks per wave -> atomicMin of the first row (index0 + 64 w +
+// lane) into first_hit[tape - result_base] and the count into hit_count (either may be null)
+hipError_t launch_combine(const unsigned long long* masks, uint64_t stride, const uint32_t* split,
+                          uint32_t n_split, uint32_t result_base, uint64_t index0,
+                          unsigned long long* first_hit, unsigned long long* hit_count,
+                          hipStream_t stream);
 hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uint32_t* sink,
                              hipStream_t stream);
 

@@ -300,7 +300,13 @@ __device__ __forceinline__ void sieve_body(const KParams& p) {
                 }
                 const u32 res = rb ? (X[0] & 1u) : (is_zero256(X) ? 0u : 1u);
                 const unsigned long long mask = __builtin_amdgcn_ballot_w64(valid && res);
-                if (mask && (tid & 63u) == 0) {
+                if (p.masks) {  // a part of a split tape: its wave mask, combined later
+                    if ((tid & 63u) == 0) {
+                        const u32 t = __builtin_amdgcn_readfirstlane(s_tid[j]);
+                        const u64 w = ((u64)blockIdx.x * kSieveBlock + (tid & ~63u)) / 64u;
+                        p.masks[(u64)(t - p.mask_base) * p.mask_stride + w] = mask;
+                    }
+                } else if (mask && (tid & 63u) == 0) {
                     atomicAdd(&s_cnt[j], (unsigned long long)__builtin_popcountll(mask));
                     atomicMin(&s_min[j], (unsigned long long)(wave_first + __builtin_ctzll(mask)));
                 }
@@ -535,12 +541,34 @@ __attribute__((amdgpu_waves_per_eu(sieve_min_waves(NR, FEAT), 8))) sieve_kernel(
     sieve_body<NR, FEAT>(p);
 }
 
+// one workgroup per split tape: the AND of its parts' wave masks (kernels.h launch_combine)
+__global__ void __launch_bounds__(256)
+    combine_kernel(const unsigned long long* masks, u64 stride, const u32* split, u32 result_base,
+                   u64 index0, unsigned long long* first_hit, unsigned long long* hit_count) {
+    const u32 t = split[3 * blockIdx.x], s0 = split[3 * blockIdx.x + 1],
+              k = split[3 * blockIdx.x + 2];
+    u64 first = ~0ull, cnt = 0;
+    for (u64 w = threadIdx.x; w < stride; w += 256) {
+        unsigned long long m = ~0ull;
+        for (u32 i = 0; i < k; ++i) m &= masks[(u64)(s0 + i) * stride + w];
+        if (m) {
+            cnt += (u64)__builtin_popcountll(m);
+            if (first == ~0ull) first = index0 + 64 * w + (u64)__builtin_ctzll(m);
+        }
+    }
+    if (first != ~0ull && first_hit) atomicMin(&first_hit[t - result_base], first);
+    if (cnt && hit_count) atomicAdd(&hit_count[t - result_base], cnt);
+}
+
 template <int NR, int FEAT>
 hipError_t launch_variant(const KParams& p, hipStream_t stream) {
     const u64 blocks = (p.row_count + kSieveBlock - 1) / kSieveBlock;
     // fewer row blocks than CUs: split the tapes over grid y until the chip has ~256 workgroups
     u64 gy = 1;
     if (blocks < 256) gy = std::min<u64>(p.n_ids, (256 + blocks - 1) / blocks);
+    // the parts of split tapes (conjunct-parallel short runs) each get their own workgroups up
+    // to 4096 in all: a part walked after another on the same workgroup gains no latency
+    if (p.masks && blocks < 4096) gy = std::max<u64>(gy, std::min<u64>(p.n_ids, 4096 / blocks));
     hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks, (unsigned)gy),
                        dim3(kSieveBlock), 0, stream, p);
     return hipGetLastError();
@@ -549,6 +577,20 @@ hipError_t launch_variant(const KParams& p, hipStream_t stream) {
 }  // namespace
 
 namespace mh {
+
+uint64_t sieve_mask_stride(uint64_t row_count) {
+    return (row_count + kSieveBlock - 1) / kSieveBlock * (kSieveBlock / 64);
+}
+
+hipError_t launch_combine(const unsigned long long* masks, uint64_t stride, const uint32_t* split,
+                          uint32_t n_split, uint32_t result_base, uint64_t index0,
+                          unsigned long long* first_hit, unsigned long long* hit_count,
+                          hipStream_t stream) {
+    if (n_split == 0) return hipSuccess;
+    hipLaunchKernelGGL(combine_kernel, dim3(n_split), dim3(256), 0, stream, masks, stride, split,
+                       result_base, index0, first_hit, hit_count);
+    return hipGetLastError();
+}
 
 hipError_t launch_sieve(const KParams& p, uint32_t variant, hipStream_t stream) {
     if (p.row_count == 0 || p.n_ids == 0) return hipSuccess;

@@ -129,3 +129,21 @@ extern "C" int32_t emu_compile_words(const mh_node* nodes, const uint64_t* offs,
     if (words.size() <= cap) memcpy(out, words.data(), words.size() * 4);
     return MH_OK;
 }
+
+// compile.h split_conjunction, for tests/test_split.py: the parts back to back in `out` (cap
+// nodes), part p = out[offs[p] .. offs[p + 1]).  Returns the parts (0: not split), -1 when `out`
+// is too small.
+extern "C" int32_t emu_split(const mh_node* nodes, uint32_t n, uint32_t want, mh_node* out,
+                             uint64_t cap, uint64_t* offs) {
+    std::vector<std::vector<mh_node>> parts;
+    if (!mh::split_conjunction(nodes, n, want, parts)) return 0;
+    uint64_t at = 0;
+    offs[0] = 0;
+    for (size_t p = 0; p < parts.size(); ++p) {
+        if (at + parts[p].size() > cap) return -1;
+        memcpy(out + at, parts[p].data(), parts[p].size() * sizeof(mh_node));
+        at += parts[p].size();
+        offs[p + 1] = at;
+    }
+    return (int32_t)parts.size();
+}

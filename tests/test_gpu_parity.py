@@ -724,3 +724,59 @@ def test_run_rows_returns_witness_columns(gpu_ctx):
         assert smt_eval.evaluate(ts.tapes[t].nodes, ts.pool.values, soa_row(soa, r))
         assert (rows[t] == a.download(r, 1)[:, :, 0]).all()
     ct.close()
+
+
+@pytest.mark.parametrize("rows", [256, 4096, 65536])
+def test_conjunct_parallel_split_runs(gpu_ctx, rows):
+    """A short run over a set whose long tapes are split into conjunct parts (MH_SPLIT_INSNS:
+    the slots from which a tape is cut; mh_tapes_compile reads it per call) gives, per tape, the
+    counts and first witnesses of the unsplit set -- whole set (merged launches on side streams,
+    parts spread over grid y), a tape range that cuts through the split tapes, FIRST_HIT and
+    COUNT_ALL -- and the oracle's on a tape sample."""
+    rng = random.Random(rows)
+    ts = TapeSet()
+    fz = TapeFuzzer(rng, ts, n_vars=3, allow_keccak=rows <= 4096, max_depth=3)
+    for _ in range(12):  # conjunctions of 2..8 random Bool terms
+        root = fz.boolean(3)
+        for _ in range(rng.randrange(1, 8)):
+            root = fz.b.op(Op.AND, root, fz.boolean(3))
+        ts.add(fz.b.finish(root))
+    b = ts.builder()
+    x, y = b.var("v0"), b.var("v1")
+    # satisfiable by many rows: every part passes somewhere, the AND is what decides
+    ts.add(b.finish(b.op(Op.AND, b.op(Op.BVULT, x, y), b.op(Op.BVUGT, x, b.const(5, 256)))))
+    soa = assignment_soa(rng, ts.n_vars, rows)
+    a = upload(gpu_ctx, soa)
+    old = os.environ.get("MH_SPLIT_INSNS")
+    try:
+        os.environ["MH_SPLIT_INSNS"] = "0"
+        whole = gpu_ctx.compile(ts)
+        os.environ["MH_SPLIT_INSNS"] = "8"
+        cut = gpu_ctx.compile(ts)
+    finally:
+        if old is None:
+            os.environ.pop("MH_SPLIT_INSNS", None)
+        else:
+            os.environ["MH_SPLIT_INSNS"] = old
+    n = len(ts.tapes)
+    for mode in (native.MODE_FIRST_HIT, native.MODE_COUNT_ALL):
+        for first, count in ((0, n), (3, n - 5), (n - 1, 1)):
+            want = native.run(gpu_ctx, whole, a, tape_first=first, tape_count=count, mode=mode,
+                              index_base=1000)
+            got = native.run(gpu_ctx, cut, a, tape_first=first, tape_count=count, mode=mode,
+                             index_base=1000)
+            assert [int(v) for v in got[0]] == [int(v) for v in want[0]], (mode, first)
+            if mode == native.MODE_COUNT_ALL:
+                assert [int(v) for v in got[1]] == [int(v) for v in want[1]], (mode, first)
+    fh, hc = native.run(gpu_ctx, cut, a, mode=native.MODE_COUNT_ALL, index_base=1000)
+    for t in range(0, n, 4 if rows > 4096 else 1):  # the oracle on a sample of rows
+        sample = range(0, rows, max(1, rows // 512))
+        hits = [r for r in sample
+                if smt_eval.evaluate(ts.tapes[t].nodes, ts.pool.values, soa_row(soa, r))]
+        if rows <= 512:
+            assert int(hc[t]) == len(hits)
+            assert int(fh[t]) == (1000 + hits[0] if hits else native.NO_HIT)
+        elif hits:
+            assert int(fh[t]) <= 1000 + hits[0]
+    whole.close()
+    cut.close()
