@@ -1137,8 +1137,8 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
     }
     if (s_hi > s_lo)  // every part's masks written: the split tapes' results
         MH_HIP(mh::launch_combine(ctx->d_masks, mask_stride, ts->d_split + 3 * s_lo, s_hi - s_lo,
-                                  tape_first, index_base + row_first, p.first_hit, p.hit_count,
-                                  ctx->stream));
+                                  part_lo, tape_first, index_base + row_first, p.first_hit,
+                                  p.hit_count, ctx->stream));
     if (ctx->timing) MH_HIP(hipEventRecord(sp.second, ctx->stream));
     return MH_OK;
 }

@@ -79,13 +79,14 @@ hipError_t launch_witness_rows(const uint32_t* assign, uint64_t stride, const ui
                                uint32_t* out, hipStream_t stream);
 // waves a run of row_count rows launches (the masks' row stride of a conjunct-parallel run)
 uint64_t sieve_mask_stride(uint64_t row_count);
-// per split tape i (split[3i] = tape id, split[3i+1] = its first part's mask row, split[3i+2] =
-// parts): the AND of its parts' masks per wave -> atomicMin of the first row (index0 + 64 w +
-// lane) into first_hit[tape - result_base] and the count into hit_count (either may be null)
+// per split tape i (split[3i] = tape id, split[3i+1] = its first part's id, whose masks are
+// row id - mask_base, split[3i+2] = parts): the AND of its parts' masks per wave -> atomicMin of
+// the first row (index0 + 64 w + lane) into first_hit[tape - result_base] and the count into
+// hit_count (either may be null)
 hipError_t launch_combine(const unsigned long long* masks, uint64_t stride, const uint32_t* split,
-                          uint32_t n_split, uint32_t result_base, uint64_t index0,
-                          unsigned long long* first_hit, unsigned long long* hit_count,
-                          hipStream_t stream);
+                          uint32_t n_split, uint32_t mask_base, uint32_t result_base,
+                          uint64_t index0, unsigned long long* first_hit,
+                          unsigned long long* hit_count, hipStream_t stream);
 hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uint32_t* sink,
                              hipStream_t stream);
 

@@ -543,9 +543,10 @@ __attribute__((amdgpu_waves_per_eu(sieve_min_waves(NR, FEAT), 8))) sieve_kernel(
 
 // one workgroup per split tape: the AND of its parts' wave masks (kernels.h launch_combine)
 __global__ void __launch_bounds__(256)
-    combine_kernel(const unsigned long long* masks, u64 stride, const u32* split, u32 result_base,
-                   u64 index0, unsigned long long* first_hit, unsigned long long* hit_count) {
-    const u32 t = split[3 * blockIdx.x], s0 = split[3 * blockIdx.x + 1],
+    combine_kernel(const unsigned long long* masks, u64 stride, const u32* split, u32 mask_base,
+                   u32 result_base, u64 index0, unsigned long long* first_hit,
+                   unsigned long long* hit_count) {
+    const u32 t = split[3 * blockIdx.x], s0 = split[3 * blockIdx.x + 1] - mask_base,
               k = split[3 * blockIdx.x + 2];
     u64 first = ~0ull, cnt = 0;
     for (u64 w = threadIdx.x; w < stride; w += 256) {
@@ -583,12 +584,12 @@ uint64_t sieve_mask_stride(uint64_t row_count) {
 }
 
 hipError_t launch_combine(const unsigned long long* masks, uint64_t stride, const uint32_t* split,
-                          uint32_t n_split, uint32_t result_base, uint64_t index0,
-                          unsigned long long* first_hit, unsigned long long* hit_count,
-                          hipStream_t stream) {
+                          uint32_t n_split, uint32_t mask_base, uint32_t result_base,
+                          uint64_t index0, unsigned long long* first_hit,
+                          unsigned long long* hit_count, hipStream_t stream) {
     if (n_split == 0) return hipSuccess;
     hipLaunchKernelGGL(combine_kernel, dim3(n_split), dim3(256), 0, stream, masks, stride, split,
-                       result_base, index0, first_hit, hit_count);
+                       mask_base, result_base, index0, first_hit, hit_count);
     return hipGetLastError();
 }
 
