@@ -570,9 +570,12 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
         }
         // conjunct-parallel parts of the long tapes (a query round's latency is its longest
         // tape walked by one wave per SIMD: parts walk in parallel, mh_run_async); MH_SPLIT_INSNS
-        // = the instruction slots from which a tape is cut (0: never), one part per that many
+        // = the instruction slots from which a tape is cut, one part per that many.  Off by
+        // default: measured on the LASER-shaped queries and paths, the parts' compile
+        // costs a LASER child about what the parallel walk saves, and the 2^16-row miss round
+        // pays the parts' duplicated sub-terms
         const char* se = std::getenv("MH_SPLIT_INSNS");
-        const uint32_t split_min = se ? (uint32_t)std::strtoul(se, nullptr, 10) : 384u;
+        const uint32_t split_min = se ? (uint32_t)std::strtoul(se, nullptr, 10) : 0u;
         constexpr uint32_t kMaxParts = 8;
         std::vector<std::vector<uint32_t>> pw;
         std::vector<mh_tape_info> pinfo;
