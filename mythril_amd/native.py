@@ -334,7 +334,9 @@ class SmtlibSession:
         nc = max((r[11] + 8 for r in recs if r[0] == 0), default=0)
         cbuf = C.string_at(batch.const_limbs, 4 * nc) if nc else b""
         arity = _ARITY_BY_INT or _arity_table(ARITY)
-        memo, nodes, widths, flags = b._memo, b.nodes, b.widths, b.flags
+        from .tape import NODE_PACK
+
+        memo, nodes, widths, flags, packed = b._memo, b.nodes, b.widths, b.flags, b.node_bytes
         ids = [0] * n
         for k, (op, _, _, w, a, bb, c, i0, i1, noff, nlen, coff, _) in enumerate(recs):
             if a < 0:
@@ -359,6 +361,7 @@ class SmtlibSession:
                     nodes.append(key)
                     widths.append(w)
                     flags.append(f)
+                    packed += NODE_PACK(op, f, w, a, bb, c, i0, i1)
                     memo[key] = h
             elif op == 0:  # CONST (<= 256 bits; wider ones arrive as CONCATs)
                 h = b.const(int.from_bytes(cbuf[4 * coff:4 * coff + 32], "little"), w)
@@ -520,13 +523,19 @@ class TermMirror:
             return
         if n1 > n0:
             k = n1 - n0
-            rows = np.fromiter(chain.from_iterable(b.nodes[n0:n1]), np.int64, 7 * k).reshape(k, 7)
-            nodes = np.empty(k, dtype=NODE_DTYPE)
-            nodes["op"] = rows[:, 0]
-            nodes["flags"] = np.fromiter(b.flags[n0:n1], np.uint8, k)
-            nodes["width"] = rows[:, 1]
-            for j, f in enumerate(("a", "b", "c", "imm0", "imm1")):
-                nodes[f] = rows[:, 2 + j]
+            packed = getattr(b, "node_bytes", None)
+            if packed is not None and len(packed) == 24 * n1:
+                # the builder's packed mh_node records (the slice is a copy: nothing of the
+                # builder's stays exported)
+                nodes = np.frombuffer(bytes(packed[24 * n0:24 * n1]), dtype=NODE_DTYPE)
+            else:
+                rows = np.fromiter(chain.from_iterable(b.nodes[n0:n1]), np.int64, 7 * k).reshape(k, 7)
+                nodes = np.empty(k, dtype=NODE_DTYPE)
+                nodes["op"] = rows[:, 0]
+                nodes["flags"] = np.fromiter(b.flags[n0:n1], np.uint8, k)
+                nodes["width"] = rows[:, 1]
+                for j, f in enumerate(("a", "b", "c", "imm0", "imm1")):
+                    nodes[f] = rows[:, 2 + j]
         else:
             nodes = np.zeros(1, dtype=NODE_DTYPE)
         consts = (np.ascontiguousarray(pool.to_array()[c0:c1]) if c1 > c0

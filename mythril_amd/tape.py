@@ -15,6 +15,7 @@ reference construction that produces each one are tabulated in DESIGN.md
 from __future__ import annotations
 
 import enum
+import struct
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -98,6 +99,7 @@ NODE_DTYPE = np.dtype(
     ]
 )
 assert NODE_DTYPE.itemsize == 24
+NODE_PACK = struct.Struct("<BBHIIIII").pack  # one NODE_DTYPE record
 
 HOST_ONLY = {Op.ARRAY, Op.CONST_ARRAY, Op.STORE, Op.SELECT, Op.UF}
 F_ARRAY = 1  # mh_node.flags bit of host-only array-sorted nodes (never sent to the device)
@@ -175,6 +177,9 @@ class TapeBuilder:
         self.widths: List[int] = []
         self.flags: List[int] = []
         self._memo: Dict[tuple, int] = {}
+        # the same nodes packed as the C-ABI's mh_node (24 bytes each, NODE_DTYPE), appended
+        # alongside: native.TermMirror.sync hands a range of them to the library as they are
+        self.node_bytes = bytearray()
 
     # -- node creation ------------------------------------------------------------------------
     def _add(self, op: Op, width: int, a=0, b=0, c=0, imm0=0, imm1=0, flags=0) -> int:
@@ -192,6 +197,7 @@ class TapeBuilder:
         self.nodes.append(key)
         self.widths.append(width)
         self.flags.append(flags)
+        self.node_bytes += NODE_PACK(key[0], flags, width, a, b, c, imm0, imm1)
         self._memo[key] = idx
         return idx
 

@@ -433,3 +433,28 @@ def test_mirror_shared_by_threads():
     for t in th:
         t.join()
     assert not errors
+
+
+def test_builder_packed_nodes_match_the_node_list():
+    """TapeBuilder.node_bytes (the mh_node records TermMirror.sync hands over as they are) equals
+    the builder's node tuples and flags, for nodes made by TapeBuilder._add and by the SMT-LIB
+    reader's inlined merge (native.SmtlibSession._merge)."""
+    import random
+
+    from mythril_amd import smtlib
+    from mythril_amd.native import NODE_DTYPE
+    from tests.laser_like import queries
+    from tests.z3_style import z3_sexpr
+
+    ctx, qs = queries()
+    nat = smtlib.NativeReader()
+    for _, cs in qs[:6]:
+        for c in cs:
+            nat.read(z3_sexpr(c), smtlib.Query(nat.ctx))
+    ctx2, _ = _random_query(random.Random(3), 9)
+    for b in (ctx.b, nat.b, ctx2.b):
+        got = np.frombuffer(bytes(b.node_bytes), dtype=NODE_DTYPE)
+        assert len(got) == len(b.nodes)
+        want = np.array([(n[0], f, n[1], n[2], n[3], n[4], n[5], n[6])
+                         for n, f in zip(b.nodes, b.flags)], dtype=NODE_DTYPE)
+        assert (got == want).all()
