@@ -350,6 +350,13 @@ int32_t mh_run_rows(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint
                     const mh_assign* as, uint64_t row_first, uint64_t row_count,
                     uint64_t index_base, uint32_t mode, uint64_t* first_hit, uint64_t* hit_count,
                     uint32_t n_cols, uint32_t* rows_out);
+/* One guided round of a query in one call: mh_assign_generate_guided of rows [0, count) of `as`
+ * (global indices global_base + row) then mh_run_rows over them with index_base = global_base --
+ * the sieve's round (Sieve.solve) without a host round trip between the generator and the run.   */
+int32_t mh_query_round(mh_ctx* ctx, const mh_tapeset* ts, mh_assign* as, const mh_guide* guide,
+                       uint64_t seed, uint64_t global_base, uint64_t count, uint32_t tape_first,
+                       uint32_t tape_count, uint32_t mode, uint64_t* first_hit,
+                       uint64_t* hit_count, uint32_t n_cols, uint32_t* rows_out);
 /* Device-pointer form: enqueues on the ctx stream and returns.  d_first_hit / d_hit_count are
  * device buffers of tape_count u64; they are NOT reset (callers initialise them to MH_NO_HIT / 0
  * with mh_results_reset), so several launches can accumulate into them.                          */

@@ -976,8 +976,8 @@ uint32_t mh_gen_limb(uint64_t seed, uint32_t var, uint64_t index, uint32_t limb)
 int32_t mh_results_reset(mh_ctx* ctx, uint64_t* d_first_hit, uint64_t* d_hit_count, uint32_t n) {
     if (!ctx) return set_err(MH_E_INVALID, "null ctx");
     if (int32_t r = use_device(ctx)) return r;
-    if (d_first_hit) MH_HIP(hipMemsetAsync(d_first_hit, 0xFF, n * sizeof(uint64_t), ctx->stream));
-    if (d_hit_count) MH_HIP(hipMemsetAsync(d_hit_count, 0, n * sizeof(uint64_t), ctx->stream));
+    // one small kernel for both arrays (two hipMemsetAsync were two fill launches per run)
+    MH_HIP(mh::launch_results_reset(d_first_hit, d_hit_count, n, ctx->stream));
     return MH_OK;
 }
 
@@ -1190,6 +1190,18 @@ int32_t mh_run(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uint32_t 
                uint32_t mode, uint64_t* first_hit, uint64_t* hit_count) {
     return mh_run_rows(ctx, ts, tape_first, tape_count, as, row_first, row_count, index_base, mode,
                        first_hit, hit_count, 0, nullptr);
+}
+
+int32_t mh_query_round(mh_ctx* ctx, const mh_tapeset* ts, mh_assign* as, const mh_guide* guide,
+                       uint64_t seed, uint64_t global_base, uint64_t count, uint32_t tape_first,
+                       uint32_t tape_count, uint32_t mode, uint64_t* first_hit,
+                       uint64_t* hit_count, uint32_t n_cols, uint32_t* rows_out) {
+    if (!ctx || !as || as->ctx != ctx) return set_err(MH_E_INVALID, "null or foreign assignment buffer");
+    if (int32_t r = check_run_args(ctx, ts, tape_first, tape_count, as, 0, count, mode)) return r;
+    // the generator, the run and the copy queue back to back on the ctx stream: one host sync
+    if (int32_t r = mh_assign_generate_guided(as, seed, global_base, 0, count, guide)) return r;
+    return mh_run_rows(ctx, ts, tape_first, tape_count, as, 0, count, global_base, mode, first_hit,
+                       hit_count, n_cols, rows_out);
 }
 
 int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const mh_assign* as,

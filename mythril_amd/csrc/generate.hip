@@ -200,6 +200,14 @@ __global__ void __launch_bounds__(kLdsRows * kWaves)
     }
 }
 
+__global__ void __launch_bounds__(kBlock)
+    results_reset_kernel(u64* first_hit, u64* hit_count, u32 n) {
+    const u32 i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (first_hit) first_hit[i] = ~0ull;
+    if (hit_count) hit_count[i] = 0;
+}
+
 // one workgroup per tape: the words of its witness row (a row outside the buffer reads as none)
 __global__ void __launch_bounds__(kBlock)
     witness_rows_kernel(const u32* assign, u64 stride, const u64* first_hit, u64 index_base,
@@ -215,6 +223,14 @@ __global__ void __launch_bounds__(kBlock)
 }  // namespace
 
 namespace mh {
+
+hipError_t launch_results_reset(uint64_t* first_hit, uint64_t* hit_count, uint32_t n,
+                                hipStream_t stream) {
+    if (n == 0 || (!first_hit && !hit_count)) return hipSuccess;
+    hipLaunchKernelGGL(results_reset_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                       first_hit, hit_count, n);
+    return hipGetLastError();
+}
 
 hipError_t launch_witness_rows(const uint32_t* assign, uint64_t stride, const uint64_t* first_hit,
                                uint32_t n_tapes, uint64_t index_base, uint32_t n_cols,

@@ -72,6 +72,9 @@ struct KGuide {
 hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
                                   hipStream_t stream);
+// first_hit[0..n) = MH_NO_HIT, hit_count[0..n) = 0 in one launch (either may be null)
+hipError_t launch_results_reset(uint64_t* first_hit, uint64_t* hit_count, uint32_t n,
+                                hipStream_t stream);
 // each tape's witness row (mh_run_rows): out[t][w] = column word w (column w / 8, limb w % 8) of
 // the buffer row first_hit[t] - index_base, zero for a tape without a hit
 hipError_t launch_witness_rows(const uint32_t* assign, uint64_t stride, const uint64_t* first_hit,

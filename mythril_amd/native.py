@@ -67,6 +67,9 @@ SIGNATURES = {
                            C.c_uint64, C.c_uint32, _u64p, _u64p]),
     "mh_run_rows": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
                                 C.c_uint64, C.c_uint32, _u64p, _u64p, C.c_uint32, _u32p]),
+    "mh_query_round": (C.c_int32, [_vp, _vp, _vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64,
+                                   C.c_uint32, C.c_uint32, C.c_uint32, _u64p, _u64p, C.c_uint32,
+                                   _u32p]),
     "mh_run_async": (C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
                                  C.c_uint64, C.c_uint32, _vp, _vp]),
     "mh_eval_values": (C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint64, C.c_uint64, _u32p]),
@@ -203,15 +206,56 @@ def _limb_rows(vals) -> np.ndarray:
     return np.frombuffer(buf, dtype="<u4").reshape(-1, 8).copy()
 
 
+def _guide_arrays(g: "Guide") -> dict:
+    """The arrays of an mh_guide the library owns, copied (one memcpy each)."""
+    def arr(p, n, dt=np.uint32):
+        dt = np.dtype(dt)
+        return np.frombuffer(C.string_at(C.cast(p, C.c_void_p), n * dt.itemsize), dtype=dt)
+
+    n_cols, n_sets = g.n_cols, g.n_sets
+    pool_off = arr(g.pool_off, n_cols + 1)
+    set_off = arr(g.set_off, n_sets + 1)
+    alt_off = arr(g.alt_off, int(set_off[-1]) + 1)
+    n_entries = max(int(alt_off[-1]), 1)
+    return dict(
+        width=arr(g.col_width, n_cols, np.uint16), pool_off=pool_off,
+        pool=arr(g.pool, 8 * max(int(pool_off[-1]), 1)).reshape(-1, 8), set_off=set_off,
+        set_prob=arr(g.set_prob, max(n_sets, 1), np.uint8), alt_off=alt_off,
+        entry_col=arr(g.entry_col, n_entries), entry_val=arr(g.entry_val, 8 * n_entries).reshape(-1, 8))
+
+
+class GuideHandle:
+    """A harvested guide left in the library (mh_harvest): query_round hands its mh_guide to the
+    generator as it is; arrays() copies it out (tests, the CPU stand-in of the device)."""
+
+    def __init__(self, lib, h: C.c_void_p, g: "Guide"):
+        self.lib, self.h, self.guide = lib, h, g
+
+    def arrays(self) -> dict:
+        return _guide_arrays(self.guide)
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.mh_harvest_free(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
-                  parent: Sequence[Tuple[int, int]] = (), session: "Optional[GuideSession]" = None
-                  ) -> dict:
+                  parent: Sequence[Tuple[int, int]] = (), session: "Optional[GuideSession]" = None,
+                  keep: bool = False):
     """mh_guide_harvest: the guide of one lowered query tape (root last, VAR imm0 = column,
     CONST imm0 = row of `consts`), as the arrays candidates.Guide.arrays() gives -- the same
     values (tests/test_harvest.py).  `parent` = the parent witness as (column, value) pairs in
     the witness's order.  With `session` (a GuideSession) the harvest reuses the session's memo
-    when the tape extends the last one (mh_guide_harvest_with; the same arrays).  Host-only: no
-    device is touched."""
+    when the tape extends the last one (mh_guide_harvest_with; the same arrays).  keep=True
+    returns a GuideHandle instead (the guide stays in the library for query_round).  Host-only:
+    no device is touched."""
     lib = load()
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
     consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1, 8)
@@ -227,23 +271,13 @@ def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
         _check(lib.mh_guide_harvest(*args))
     else:
         _check(lib.mh_guide_harvest_with(session.h, *args))
+    handle = GuideHandle(lib, h, g)
+    if keep:
+        return handle
     try:
-        def arr(p, n, dt=np.uint32):  # a copy of n elements at p (one memcpy)
-            dt = np.dtype(dt)
-            return np.frombuffer(C.string_at(C.cast(p, C.c_void_p), n * dt.itemsize), dtype=dt)
-
-        n_cols, n_sets = g.n_cols, g.n_sets
-        pool_off = arr(g.pool_off, n_cols + 1)
-        set_off = arr(g.set_off, n_sets + 1)
-        alt_off = arr(g.alt_off, int(set_off[-1]) + 1)
-        n_entries = max(int(alt_off[-1]), 1)
-        return dict(
-            width=arr(g.col_width, n_cols, np.uint16), pool_off=pool_off,
-            pool=arr(g.pool, 8 * max(int(pool_off[-1]), 1)).reshape(-1, 8), set_off=set_off,
-            set_prob=arr(g.set_prob, max(n_sets, 1), np.uint8), alt_off=alt_off,
-            entry_col=arr(g.entry_col, n_entries), entry_val=arr(g.entry_val, 8 * n_entries).reshape(-1, 8))
+        return handle.arrays()
     finally:
-        lib.mh_harvest_free(h)
+        handle.close()
 
 
 class GuideSession:
@@ -867,6 +901,21 @@ def run_rows(ctx: Context, tapes: CompiledTapes, assign: Assignments, n_cols: in
     _check(ctx.lib.mh_run_rows(ctx.h, tapes.h, tape_first, tc, assign.h, row_first, rc,
                                index_base, mode, _ptr(fh, C.c_uint64), _ptr(hc, C.c_uint64),
                                n_cols, _ptr(rows)))
+    return fh[:tc], hc[:tc], rows[:tc, :n_cols]
+
+
+def query_round(ctx: Context, tapes: CompiledTapes, assign: "Assignments", guide: GuideHandle,
+                seed: int, global_base: int, count: int, n_cols: int, *, tape_first: int = 0,
+                tape_count: Optional[int] = None, mode: int = MODE_FIRST_HIT):
+    """One guided round (mh_query_round): rows [0, count) generated from `guide`, then
+    run_rows over them with index_base = global_base.  Returns (first_hit, hit_count, rows)."""
+    tc = tapes.n_tapes - tape_first if tape_count is None else tape_count
+    fh = np.zeros(max(tc, 1), dtype=np.uint64)
+    hc = np.zeros(max(tc, 1), dtype=np.uint64)
+    rows = np.zeros((max(tc, 1), max(n_cols, 1), 8), dtype=np.uint32)
+    _check(ctx.lib.mh_query_round(ctx.h, tapes.h, assign.h, C.byref(guide.guide), seed,
+                                  global_base, count, tape_first, tc, mode, _ptr(fh, C.c_uint64),
+                                  _ptr(hc, C.c_uint64), n_cols, _ptr(rows)))
     return fh[:tc], hc[:tc], rows[:tc, :n_cols]
 
 

@@ -618,7 +618,7 @@ class Sieve:
         guide = native.harvest_guide(
             root_nodes, ts.pool.to_array(), widths,
             [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else (),
-            session=self.guides)
+            session=self.guides, keep=True)  # stays in the library for the rounds
         t1 = time.perf_counter()
         st.add("guide", t1 - t_t)
         self.stats.host_s += t1 - t0
@@ -640,18 +640,17 @@ class Sieve:
             for rnd, n in enumerate(launches):
                 base = (self.stats.queries << 24) + offset
                 offset += n
-                ta = time.perf_counter()
-                assign.generate_guided(self.seed, guide, global_base=base, count=n)
                 tb = time.perf_counter()
                 # a later round runs only the tapes from the first to the last unsolved group
                 g0 = solved.index(False)
                 g1 = len(solved) - solved[::-1].index(False)
-                # first witnesses and their rows' columns come back in one copy (mh_run_rows)
-                fh, _, wrows = native.run_rows(self.ctx, ct, assign, len(columns),
-                                               mode=native.MODE_FIRST_HIT, index_base=base,
-                                               row_count=n, tape_first=g0, tape_count=g1 - g0)
+                # generator, run, and the first witnesses with their rows' columns in one call and
+                # one copy back (mh_query_round)
+                fh, _, wrows = native.query_round(self.ctx, ct, assign, guide, self.seed, base, n,
+                                                  len(columns), tape_first=g0,
+                                                  tape_count=g1 - g0,
+                                                  mode=native.MODE_FIRST_HIT)
                 tr = time.perf_counter()
-                st.add("generate", tb - ta)
                 st.add("run", tr - tb)
                 self.stats.rounds += 1
                 self.stats.rows += n
@@ -685,6 +684,7 @@ class Sieve:
             return None
         finally:
             ct.close()
+            guide.close()
             self.stats.device_s += time.perf_counter() - t1
 
 

@@ -1,8 +1,8 @@
 """A CPU stand-in for the device side of mythril_amd.native, for tests of Sieve.solve's host logic
 without a GPU (test infrastructure only: the product path never imports this).
 
-``install(monkeypatch)`` replaces native.Context, native.run, native.run_rows and
-native.eval_values with restatements on the oracle: the guided generator (oracle/guided_gen.py, the restatement of
+``install(monkeypatch)`` replaces native.Context, native.run, native.run_rows, native.query_round
+and native.eval_values with restatements on the oracle: the guided generator (oracle/guided_gen.py, the restatement of
 mh_assign_generate_guided, pinned against the device by tests/test_gpu_frontend.py) and the tape
 evaluator (oracle/smt_eval.py).  FIRST_HIT is the smallest satisfying row per tape.  Slow (Python
 big-int evaluation): use small rounds, e.g. Sieve(rows=256).
@@ -97,6 +97,14 @@ def fake_run_rows(ctx, tapes, assign, n_cols, *, tape_first=0, tape_count=None, 
     return fh, cnt, rows
 
 
+def fake_query_round(ctx, tapes, assign, guide, seed, global_base, count, n_cols, *,
+                     tape_first=0, tape_count=None, mode=native.MODE_FIRST_HIT):
+    assign.generate_guided(seed, guide.arrays(), global_base=global_base, count=count)
+    return fake_run_rows(ctx, tapes, assign, n_cols, tape_first=tape_first,
+                         tape_count=tape_count, row_count=count, index_base=global_base,
+                         mode=mode)
+
+
 def fake_eval_values(ctx, tapes, tape, assign, row_first=0, row_count=None):
     rc = assign.capacity - row_first if row_count is None else row_count
     out = np.zeros((8, max(rc, 1)), dtype=np.uint32)
@@ -111,4 +119,5 @@ def install(monkeypatch):
     monkeypatch.setattr(native, "Context", FakeContext)
     monkeypatch.setattr(native, "run", fake_run)
     monkeypatch.setattr(native, "run_rows", fake_run_rows)
+    monkeypatch.setattr(native, "query_round", fake_query_round)
     monkeypatch.setattr(native, "eval_values", fake_eval_values)

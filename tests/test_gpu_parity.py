@@ -780,3 +780,41 @@ def test_conjunct_parallel_split_runs(gpu_ctx, rows):
             assert int(fh[t]) <= 1000 + hits[0]
     whole.close()
     cut.close()
+
+
+def test_query_round_equals_generate_then_run_rows(gpu_ctx):
+    """mh_query_round (the guided generator, the run and the witness rows in one call, results
+    reset by one kernel) gives what mh_assign_generate_guided followed by mh_run_rows gives, for
+    every LASER-shaped query's first round: first witnesses, counts and witness rows."""
+    from mythril_amd.sieve import Sieve
+    from tests.laser_like import queries
+
+    ctx, qs = queries()
+    s = Sieve(rows=4096)
+    try:
+        for name, cs in qs:
+            host = s._host_native(ctx.b, [c.node for c in cs])
+            if host is None or not isinstance(host, tuple):
+                continue
+            columns, widths, _, root, ts, _, _ = host
+            guide = native.harvest_guide(root, ts.pool.to_array(), widths, keep=True)
+            ct = s.compile(ts)
+            a1 = s.ctx.assignments(len(columns), 256)
+            a2 = s.ctx.assignments(len(columns), 256)
+            base = 7 << 24
+            for mode in (native.MODE_FIRST_HIT, native.MODE_COUNT_ALL):
+                fh, hc, rows = native.query_round(s.ctx, ct, a1, guide, 99, base, 256,
+                                                  len(columns), mode=mode)
+                a2.generate_guided(99, guide.arrays(), global_base=base, count=256)
+                fh2, hc2, rows2 = native.run_rows(s.ctx, ct, a2, len(columns), mode=mode,
+                                                  index_base=base, row_count=256)
+                assert fh.tolist() == fh2.tolist(), name
+                assert (rows == rows2).all(), name
+                if mode == native.MODE_COUNT_ALL:
+                    assert hc.tolist() == hc2.tolist(), name
+            ct.close()
+            a1.close()
+            a2.close()
+            guide.close()
+    finally:
+        s.close()

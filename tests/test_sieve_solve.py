@@ -94,13 +94,13 @@ def test_later_round_runs_only_unsolved_groups(monkeypatch):
 
     fake_device.install(monkeypatch)
     calls = []
-    real = native.run_rows
+    real = native.query_round
 
-    def recording(ctx, tapes, assign, n_cols, **kw):
+    def recording(ctx, tapes, assign, guide, seed, base, count, n_cols, **kw):
         calls.append((kw.get("tape_first", 0), kw.get("tape_count")))
-        return real(ctx, tapes, assign, n_cols, **kw)
+        return real(ctx, tapes, assign, guide, seed, base, count, n_cols, **kw)
 
-    monkeypatch.setattr(native, "run_rows", recording)
+    monkeypatch.setattr(native, "query_round", recording)
     ctx = smt.set_context(smt.Context())
     x = symbol_factory.BitVecSym("x", 256)
     y = symbol_factory.BitVecSym("y", 256)
