@@ -448,8 +448,8 @@ class CompiledQuery:
     ``tables`` [(kind, name, items)] are decoded on first use (a witness's schema is read only
     when a model is evaluated, mythril/laser/smt/model.py:45-59)."""
 
-    __slots__ = ("tapes", "consts", "names", "widths", "groups", "flags", "_raw", "_columns",
-                 "_tables")
+    __slots__ = ("tapes", "consts", "names", "widths", "groups", "flags", "nodes", "tape_off",
+                 "_raw", "_columns", "_tables")
 
     def __init__(self, info: QueryInfo):
         def raw(p, nbytes):
@@ -458,6 +458,7 @@ class CompiledQuery:
         nt = info.n_tapes
         off = np.frombuffer(raw(info.tape_off, 8 * (nt + 1)), dtype=np.uint64).tolist()
         nodes = np.frombuffer(raw(info.nodes, 24 * off[-1]), dtype=NODE_DTYPE)
+        self.nodes, self.tape_off = nodes, off  # every tape back to back
         self.tapes = [nodes[off[i]:off[i + 1]] for i in range(nt)]
         self.consts = np.frombuffer(raw(info.consts, 32 * info.n_consts),
                                     dtype=np.uint32).reshape(-1, 8)

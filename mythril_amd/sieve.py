@@ -464,6 +464,7 @@ class Sieve:
                 if level[t] >= len(sizes):
                     raise
                 ts.tapes[t] = Tape(rematerialize(orig[t], sizes[level[t]]))
+                ts.flat = None  # the tapes no longer lie back to back
                 k = "remat_%d" % sizes[level[t]]
                 self.stats.extra[k] = self.stats.extra.get(k, 0) + 1
 
@@ -541,6 +542,10 @@ class Sieve:
         ts.pool = LocalPool(cq.consts)
         tapes = cq.tapes
         ts.tapes = [Tape(t) for t in (tapes if len(tapes) == 1 else tapes[1:])]
+        # the group tapes already lie back to back (tapes 1.., or the one tape): no concatenation
+        k = 0 if len(tapes) == 1 else 1
+        off = np.asarray(cq.tape_off[k:], dtype=np.uint64)
+        ts.flat = (cq.nodes[cq.tape_off[k]:cq.tape_off[-1]], off - off[0], cq.consts)
         if len(cq.groups) > 1:
             st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
         return columns, cq.widths, NativeSchema(cq), tapes[0], ts, cq.groups, []

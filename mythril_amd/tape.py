@@ -489,6 +489,9 @@ class TapeSet:
             self.var_index.setdefault(n, len(self.var_index))
         self.tapes: List[Tape] = []
         self.symbols = Symbols()
+        # flatten()'s result when the tapes already lie back to back in one array (a native
+        # query's, mythril_amd/sieve.py); whoever replaces a tape resets it
+        self.flat: Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]] = None
 
     def builder(self) -> TapeBuilder:
         return TapeBuilder(self.pool, self.var_index, self.symbols)
@@ -511,6 +514,8 @@ class TapeSet:
 
     def flatten(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """(nodes, tape_offsets[n+1] as u64, consts[n_consts, 8] as u32) for mh_tapes_compile."""
+        if self.flat is not None:
+            return self.flat
         offs = np.zeros(len(self.tapes) + 1, dtype=np.uint64)
         for i, t in enumerate(self.tapes):
             offs[i + 1] = offs[i] + len(t.nodes)

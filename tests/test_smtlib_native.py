@@ -142,7 +142,7 @@ def test_import_cost_per_new_constraint():
     """DESIGN §6 import column: the C++ reader per new constraint in LASER order (the Python
     reader beside it).  The C++ parse is ~10 ns per character; what is left is the host builder's
     ~1.5 us per node the constraint adds (a fresh calldata word: 165-330 nodes)."""
-    worst_nat, worst_py = 0.0, 0.0
+    worst_nat, worst_py, sum_nat, sum_py = 0.0, 0.0, 0.0, 0.0
     for name, cs in _all_queries():
         texts = [z3_sexpr(c) for c in cs]
         py, nat = smtlib.Reader(), smtlib.NativeReader()
@@ -156,9 +156,13 @@ def test_import_cost_per_new_constraint():
             t2 = time.perf_counter()
             worst_py = max(worst_py, t1 - t0)
             worst_nat = max(worst_nat, t2 - t1)
+            sum_py += t1 - t0
+            sum_nat += t2 - t1
     print("import per new constraint, worst: native %.3f ms, python %.3f ms"
           % (worst_nat * 1e3, worst_py * 1e3))
-    assert worst_nat < worst_py / 2
+    # totals, not the worst single constraint: one scheduler hiccup on a loaded CI host must
+    # not decide it
+    assert sum_nat < sum_py / 2
 
 
 def test_z3_importer_uses_the_native_reader():
