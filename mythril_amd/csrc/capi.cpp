@@ -236,10 +236,6 @@ struct mh_assign {
     uint32_t* d = nullptr;
     uint32_t* d_guide = nullptr;   // packed mh_guide (grow-only)
     size_t guide_words = 0;
-    // the spread generator's [n_cols][rows] last-entry slots (kernels.h kGenSpreadRows; zero
-    // between launches, grow-only)
-    uint32_t* d_last = nullptr;
-    size_t last_words = 0;
     std::vector<uint32_t> h_guide; // host packing of the guide
     uint32_t* h_pinned = nullptr;  // pinned staging of the packed guide (grow-only)
     size_t pinned_words = 0;
@@ -815,7 +811,6 @@ int32_t mh_assign_destroy(mh_assign* as) {
     if (as->h_pinned) (void)hipHostFree(as->h_pinned);
     if (as->d) (void)hipFree(as->d);
     if (as->d_guide) (void)hipFree(as->d_guide);
-    if (as->d_last) (void)hipFree(as->d_last);
     mh_ctx* ctx = as->ctx;
     delete as;
     ctx_unref(ctx);
@@ -968,22 +963,8 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
     k.alt_off = as->d_guide + o_aoff;
     k.entry_col = as->d_guide + o_ecol;
     k.entry_val = as->d_guide + o_eval;
-    uint32_t* last = nullptr;
-    if (count <= mh::kGenSpreadRows && n_value_sets >= mh::kGenSpreadSets && nc) {
-        const size_t need = (size_t)nc * count;
-        if (need > as->last_words) {
-            if (as->d_last) MH_HIP(hipFree(as->d_last));
-            as->d_last = nullptr;
-            as->last_words = 0;
-            const size_t n = std::max<size_t>(need, (size_t)1 << 16);
-            MH_HIP(hipMalloc(&as->d_last, n * sizeof(uint32_t)));
-            MH_HIP(hipMemsetAsync(as->d_last, 0, n * sizeof(uint32_t), as->ctx->stream));
-            as->last_words = n;
-        }
-        last = as->d_last;
-    }
     MH_HIP(mh::launch_generate_guided(as->d, as->stride, first, count, seed, global_base, k,
-                                      as->ctx->stream, last));
+                                      as->ctx->stream));
     return MH_OK;
 }
 

@@ -6,8 +6,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <algorithm>
-
 #include "kernels.h"
 
 namespace {
@@ -202,64 +200,6 @@ __global__ void __launch_bounds__(kLdsRows * kWaves)
     }
 }
 
-// The same rows for a short run (a query's 256-row round) with many value sets, spread over
-// more workgroups: in the LDS form each 64-row block walks every set on its own 16 waves, so a
-// 300-set guide kept 4 workgroups busy for ~75 us.  Phase 1 spreads the sets over `gy`
-// workgroups per 64-row block, each lane keeping the largest entry per (column, row) with an
-// atomic max in `last` ([n_cols][count], zero on entry); phase 2 writes every column of every row
-// once and leaves `last` zero again; phase 3 runs the copy sets in memory, in order, one thread
-// per row -- the LDS form's three steps with the same winners, so the same rows.
-__global__ void __launch_bounds__(kLdsRows * kWaves)
-    guided_sets_kernel(u32* last, u64 first, u64 count, u64 seed, u64 base, mh::KGuide g) {
-    const u32 lane = threadIdx.x % kLdsRows, wave = threadIdx.x / kLdsRows;
-    const u64 i = (u64)blockIdx.x * kLdsRows + lane;
-    if (i >= count) return;
-    const u64 gidx = base + first + i;
-    for (u32 j = blockIdx.y * kWaves + wave; j < g.n_value_sets; j += gridDim.y * kWaves) {
-        const u32 alt = chosen_alt(g, j, seed, gidx);
-        if (alt == ~0u) continue;
-        for (u32 e = g.alt_off[alt]; e < g.alt_off[alt + 1]; ++e)
-            atomicMax(&last[(u64)g.entry_col[e] * count + i], e + 1);
-    }
-}
-
-__global__ void __launch_bounds__(kLdsRows * kWaves)
-    guided_cols_kernel(u32* assign, u64 stride, u32* last, u64 first, u64 count, u64 seed,
-                       u64 base, mh::KGuide g) {
-    const u32 lane = threadIdx.x % kLdsRows, wave = threadIdx.x / kLdsRows;
-    const u64 i = (u64)blockIdx.x * kLdsRows + lane;
-    if (i >= count) return;
-    const u64 row = first + i, gidx = base + row;
-    for (u32 v = blockIdx.y * kWaves + wave; v < g.n_cols; v += gridDim.y * kWaves) {
-        const u32 e = last[(u64)v * count + i];
-        last[(u64)v * count + i] = 0;
-        u32 val[8];
-        if (e == 0) {
-            base_value(g, v, seed, gidx, val);
-        } else {
-#pragma unroll
-            for (u32 k = 0; k < 8; ++k) val[k] = g.entry_val[(u64)(e - 1) * 8 + k];
-        }
-        const u32 w = g.width[v];
-#pragma unroll
-        for (u32 k = 0; k < 8; ++k)
-            assign[((u64)v * 8 + k) * stride + row] = val[k] & limb_mask(w, k);
-    }
-}
-
-__global__ void __launch_bounds__(kBlock)
-    guided_copies_kernel(u32* assign, u64 stride, u64 first, u64 count, u64 seed, u64 base,
-                         mh::KGuide g) {
-    const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= count) return;
-    const u64 row = first + i, gidx = base + row;
-    for (u32 j = g.n_value_sets; j < g.n_sets; ++j) {
-        const u32 alt = chosen_alt(g, j, seed, gidx);
-        if (alt == ~0u) continue;
-        for (u32 e = g.alt_off[alt]; e < g.alt_off[alt + 1]; ++e) apply_entry(assign, stride, row, g, e);
-    }
-}
-
 __global__ void __launch_bounds__(kBlock)
     results_reset_kernel(u64* first_hit, u64* hit_count, u32 n) {
     const u32 i = blockIdx.x * kBlock + threadIdx.x;
@@ -303,23 +243,8 @@ hipError_t launch_witness_rows(const uint32_t* assign, uint64_t stride, const ui
 
 hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
-                                  hipStream_t stream, uint32_t* last) {
+                                  hipStream_t stream) {
     if (count == 0) return hipSuccess;
-    const u64 blocks64 = (count + kLdsRows - 1) / kLdsRows;
-    if (last && count <= kGenSpreadRows && g.n_value_sets >= kGenSpreadSets) {
-        // a short run over many sets: the spread form (one workgroup column per 2 x 16 sets)
-        const u32 gy = std::min<u32>(16u, (g.n_value_sets + 2 * kWaves - 1) / (2 * kWaves));
-        const u32 gc = std::min<u32>(16u, (g.n_cols + kWaves - 1) / kWaves);
-        hipLaunchKernelGGL(guided_sets_kernel, dim3((unsigned)blocks64, gy), dim3(kLdsRows * kWaves),
-                           0, stream, last, first, count, seed, base, g);
-        hipLaunchKernelGGL(guided_cols_kernel, dim3((unsigned)blocks64, std::max(gc, 1u)),
-                           dim3(kLdsRows * kWaves), 0, stream, assign, stride, last, first, count,
-                           seed, base, g);
-        if (g.n_value_sets < g.n_sets)
-            hipLaunchKernelGGL(guided_copies_kernel, dim3((unsigned)((count + kBlock - 1) / kBlock)),
-                               dim3(kBlock), 0, stream, assign, stride, first, count, seed, base, g);
-        return hipGetLastError();
-    }
     // LDS form while the last-entry slots (256 B per column) fit 48 KB per workgroup
     const size_t lds = (size_t)g.n_cols * kLdsRows * sizeof(u32);
     if (g.n_cols && lds <= 48 * 1024) {

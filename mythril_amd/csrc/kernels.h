@@ -69,13 +69,9 @@ struct KGuide {
     const uint32_t* entry_col;  // [n_entries]
     const uint32_t* entry_val;  // x 8 limbs
 };
-// a run of at most kGenSpreadRows rows over a guide of at least kGenSpreadSets value sets takes
-// the spread form when `last` ([n_cols][count] u32, zero; left zero) is given
-constexpr uint64_t kGenSpreadRows = 4096;
-constexpr uint32_t kGenSpreadSets = 32;
 hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,
-                                  hipStream_t stream, uint32_t* last = nullptr);
+                                  hipStream_t stream);
 // first_hit[0..n) = MH_NO_HIT, hit_count[0..n) = 0 in one launch (either may be null)
 hipError_t launch_results_reset(uint64_t* first_hit, uint64_t* hit_count, uint32_t n,
                                 hipStream_t stream);

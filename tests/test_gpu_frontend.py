@@ -280,49 +280,3 @@ def test_random_queries_native_witnesses_are_models(gpu_ctx):
     finally:
         s.close()
     assert hits >= 16
-
-
-@pytest.mark.parametrize("rows,first,n_cols,n_value", [(256, 0, 40, 300), (4096, 0, 150, 64),
-                                                       (1000, 24, 9, 40)])
-def test_spread_generator_matches_oracle(gpu_ctx, rows, first, n_cols, n_value):
-    """A short run over a guide of many value sets takes the spread generator (generate.hip:
-    sets over more workgroups, last entries through a global buffer, then the copy sets): bit
-    for bit what oracle/guided_gen.py gives, also for a row range not starting at 0, and the
-    buffer is left zero for the next run (a second guide right after gives its own rows)."""
-    rng = np.random.default_rng(rows + n_value)
-    values = _random_guide_values(rng, n_cols, n_value)
-    copies = _random_guide(rng, n_cols, 12)
-    arrays = _concat_guides(values, copies)
-    seed, base = 0x5EED + rows, 1 << 24
-    a = gpu_ctx.assignments(n_cols, first + rows)
-    for arr in (arrays, values):  # the second run finds the last-entry buffer zero again
-        a.generate_guided(seed, arr, global_base=base, first=first, count=rows)
-        got = a.download(first, rows)
-        for r in list(range(0, rows, max(1, rows // 40))) + [rows - 1]:
-            want = generate_row(seed, base + first + r, arr)
-            for v, wv in enumerate(want):
-                gv = sum(int(got[v, k, r]) << (32 * k) for k in range(8))
-                assert gv == wv, (rows, r, v)
-
-
-def _random_guide_values(rng, n_cols, n_sets):
-    """A guide of value sets only (no copy entries): the generator resolves all in its first step."""
-    g = _random_guide(rng, n_cols, n_sets)
-    ec = g["entry_col"] & 0x7FFFFFFF
-    copy = (g["entry_col"] & 0x80000000) != 0
-    ev = g["entry_val"].copy()
-    ev[copy] = rng.integers(0, 1 << 32, size=(int(copy.sum()), 8), dtype=np.uint64).astype(np.uint32)
-    g["entry_col"], g["entry_val"] = ec.astype(np.uint32), ev
-    return g
-
-
-def _concat_guides(a, b):
-    """The sets of guide a, then those of guide b (same columns, a's pools)."""
-    ea = len(a["entry_col"]) if int(a["alt_off"][-1]) else 0
-    na = int(a["set_off"][-1])
-    return dict(width=a["width"], pool_off=a["pool_off"], pool=a["pool"],
-                set_off=np.concatenate([a["set_off"], b["set_off"][1:] + na]).astype(np.uint32),
-                set_prob=np.concatenate([a["set_prob"], b["set_prob"]]).astype(np.uint8),
-                alt_off=np.concatenate([a["alt_off"], b["alt_off"][1:] + ea]).astype(np.uint32),
-                entry_col=np.concatenate([a["entry_col"][:ea], b["entry_col"]]).astype(np.uint32),
-                entry_val=np.concatenate([a["entry_val"][:ea], b["entry_val"]]).astype(np.uint32))
