@@ -9,14 +9,13 @@ mythril/laser/ethereum/state/constraints.py:25-35, support/model.py:15-62):
    unsupported constructs -> the fallback, a self-contradicting query -> no device round;
 2. harvest a candidate guide from the lowered term and the parent query's witness
    (mh_guide_harvest_with, harvest.cpp -- the algorithm of candidates.py, same arrays; the
-   session reuses the inversions of the path's earlier queries);
-3. compile the group tapes over the query's own columns (mh_tapes_compile);
-4. two launches at most: ``first_rows`` guided rows (mh_assign_generate_guided), then, when a
-   group is still unsolved, the remaining ``(max_rounds - 1) * rows`` rows in ONE launch; each
-   runs the tapes in MH_MODE_FIRST_HIT and reads back the smallest satisfying row per group
-   (the same rows, indices and witnesses as round-by-round launches over the same indices,
-   with one synchronisation instead of one per round: a miss costs two launches);
-5. on a hit, download that one row: the witness (column name -> value).
+   session reuses the inversions of the path's earlier queries); the guide stays in the library;
+3. compile the group tapes over the query's own columns (mh_tapes_compile; tapes compiled
+   before in this context, a LASER parent's unchanged groups, come from its cache);
+4. two rounds at most, each ONE call (mh_query_round: guided generator, MH_MODE_FIRST_HIT run,
+   and the witness rows, one host sync): ``first_rows`` guided rows, then, when a group is still
+   unsolved, the remaining ``(max_rounds - 1) * rows`` rows over the unsolved groups' tapes;
+5. on a hit, the witness (column name -> value) from the row that came back with the results.
 
 Everything on the device path raises on failure; the caller (frontend.get_model) treats any
 exception as "no answer from the sieve" and asks the fallback solver, so the reference's
