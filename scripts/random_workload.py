@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Latency distribution of the sieve over a broad random query workload: random
+conjunctions over free arrays, K arrays, stores, selects at constant and symbolic indices, a
+tabled function, keccak with concrete pairs / bounds / its inverse and wide equalities
+(tests/test_query_native._random_query), each asked in LASER order -- every prefix a query, the
+parent solved first (svm.py:257-262) -- on one Sieve, as a long symbolic-execution run would.
+Per query the outcome (hit, refuted, miss, host fallback for a definition, error) and the wall
+time; one JSON line with counts and p50 / p90 / p99 / max per outcome.
+
+    python scripts/random_workload.py [n_paths=300] [max_len=12]
+"""
+import json
+import os
+import random
+import sys
+import time
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+
+from mythril_amd.sieve import Sieve  # noqa: E402
+from tests.test_query_native import _random_query  # noqa: E402
+
+
+def main():
+    n_paths = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    max_len = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    s = Sieve()
+    ctx, cs = _random_query(random.Random(12345), 4)  # warm-up: runtime, code objects
+    s.solve(ctx.b, [c.node for c in cs])
+    times = {"hit": [], "refuted": [], "miss": [], "error": []}
+    t_all = time.perf_counter()
+    for seed in range(n_paths):
+        rng = random.Random(seed)
+        ctx, cs = _random_query(rng, 2 + seed % (max_len - 1))
+        nodes = [c.node for c in cs]
+        for k in range(1, len(nodes) + 1):
+            r0 = s.stats.extra.get("refuted", 0)
+            t0 = time.perf_counter()
+            try:
+                w = s.solve(ctx.b, nodes[:k], key=tuple(nodes[:k]))
+                dt = (time.perf_counter() - t0) * 1e3
+                if w is not None:
+                    times["hit"].append(dt)
+                elif s.stats.extra.get("refuted", 0) > r0:
+                    times["refuted"].append(dt)
+                else:
+                    times["miss"].append(dt)
+            except Exception:  # noqa: BLE001 - the front end falls back on any error
+                times["error"].append((time.perf_counter() - t0) * 1e3)
+    out = {"paths": n_paths, "queries": sum(len(v) for v in times.values()),
+           "wall_s": round(time.perf_counter() - t_all, 2),
+           "host_python": s.stats.extra.get("host_python", 0)}
+    for k, v in times.items():
+        if v:
+            a = np.array(v)
+            out[k] = {"n": len(v), "p50": round(float(np.percentile(a, 50)), 3),
+                      "p90": round(float(np.percentile(a, 90)), 3),
+                      "p99": round(float(np.percentile(a, 99)), 3),
+                      "max": round(float(a.max()), 3)}
+        else:
+            out[k] = {"n": 0}
+    print(json.dumps(out), flush=True)
+    s.close()
+
+
+if __name__ == "__main__":
+    main()
