@@ -408,6 +408,13 @@ int32_t mh_ctx_create(int32_t device, mh_ctx** out) {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     c->own_stream = c->stream != nullptr;
+    // the short-run fan-out's side streams and events up front: a stream created on first use
+    // took 14.4 ms inside the query that first needed it (profiles/r04x)
+    for (uint32_t i = 0; i < kSideStreams && e == hipSuccess; ++i) {
+        e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&c->scratch, 64);
     if (e == hipSuccess) {
         // one block of the smallest class ready for the first query, and the pinned upload
@@ -1223,13 +1230,16 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
     p.first_hit = reinterpret_cast<unsigned long long*>(d_id + 2);
     p.hit_count = reinterpret_cast<unsigned long long*>(d_id + 4);
     p.values_out = d;
+    // copies on the ctx stream: the first use of the null stream creates a hardware queue
+    // (20.6 ms, profiles/r04x), which a query's first definitions evaluation paid
     const uint32_t ids[8] = {tape, 0, 0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0, 0, 0};
-    hipError_t e = hipMemcpy(d_id, ids, sizeof(ids), hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpyAsync(d_id, ids, sizeof(ids), hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
         e = mh::launch_sieve(p, variant, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e == hipSuccess)
-        e = hipMemcpy(out, d, 8 * row_count * sizeof(uint32_t), hipMemcpyDeviceToHost);
+        e = hipMemcpyAsync(out, d, 8 * row_count * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     (void)hipFree(d);
     if (e != hipSuccess)
         return set_err(MH_E_DEVICE, std::string("mh_eval_values: ") + hipGetErrorString(e));
