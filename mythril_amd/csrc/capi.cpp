@@ -829,10 +829,12 @@ int32_t mh_assign_upload(mh_assign* as, const uint32_t* host_soa, uint64_t first
     if (first > as->capacity || count > as->capacity - first)
         return set_err(MH_E_INVALID, "row range out of bounds");
     if (int32_t r = use_device(as->ctx)) return r;
-    for (uint64_t col = 0; col < (uint64_t)as->n_vars * 8; ++col) {
-        MH_HIP(hipMemcpyAsync(as->d + col * as->stride + first, host_soa + col * count,
-                              count * sizeof(uint32_t), hipMemcpyHostToDevice, as->ctx->stream));
-    }
+    if (count == 0) return MH_OK;
+    // one strided copy into every column-limb's [first, first + count) slice: a definitions
+    // evaluation uploads one row, which one copy per column-limb made 0.15 ms (profiles/r04z)
+    MH_HIP(hipMemcpy2DAsync(as->d + first, as->stride * sizeof(uint32_t), host_soa,
+                            count * sizeof(uint32_t), count * sizeof(uint32_t),
+                            (size_t)as->n_vars * 8, hipMemcpyHostToDevice, as->ctx->stream));
     MH_HIP(hipStreamSynchronize(as->ctx->stream));
     return MH_OK;
 }
