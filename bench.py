@@ -11,12 +11,19 @@ smallest witnesses are reduced in registers and flushed by atomics.  With N rank
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+`--gpus N` with N > 1 and no launcher around it (WORLD_SIZE unset) starts the second form itself,
+as a child process before anything touches the GPU, and exits with its return code; rank 0's
+JSON line reaches stdout unchanged.  Scaling is weak by default (every rank sweeps
+--rows-per-gpu rows); `--strong` splits that many rows over the ranks.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -44,6 +51,45 @@ def cpu_baseline(ts, seed, seconds: float):
     one = ctape.benchmark(ts, seed, seconds / 2, threads=1)
     out["single_core"] = {"value": one["value"], "cores": 1, "sample": one["sample"]}
     return out
+
+
+def launch_ranks(argv, n: int) -> int:
+    """`bench.py --gpus N` run bare: one process per GPU through torch.distributed.run, started as
+    a CHILD (never an exec: nothing has initialised the GPU yet, and the ranks must own it).
+    stdout/stderr are inherited, so the driver reads rank 0's one JSON line as from a direct run."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + list(argv)
+    log("[launcher] %d ranks: %s" % (n, " ".join(cmd)))
+    return subprocess.run(cmd).returncode
+
+
+def launch_check(args) -> None:
+    """--launch-check: the multi-rank plumbing without a GPU (gloo): every rank reports in and
+    rank 0 prints one JSON line naming the ranks that ran.  Used by tests/test_bench_launch.py."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    ranks = torch.zeros(world, dtype=torch.int64)
+    ranks[rank] = rank + 1
+    if world > 1:
+        dist.all_reduce(ranks)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world,
+                          "ranks": [int(r) - 1 for r in ranks.tolist()],
+                          "scaling": "strong" if args.strong else "weak"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main() -> None:
@@ -74,7 +120,16 @@ def main() -> None:
                          "that many (weak scaling, the default)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="check the rank launch only (gloo, no GPU): one JSON line with the ranks")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if args.launch_check:
+        launch_check(args)
+        return
     if args.rows_per_gpu is None:
         args.rows_per_gpu = 1 << 20 if args.variant == "keccak" else 1 << 26
 
@@ -88,6 +143,8 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     if world > 1:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local_rank)
