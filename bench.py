@@ -138,8 +138,6 @@ def main() -> None:
 
     from mythril_amd import native, shard, synth
 
-    build_id = native.codegen_id(args.engine)
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -163,6 +161,9 @@ def main() -> None:
     if args.engine == "jit":
         jit_info = ct.jit(max_vgpr=args.max_vgpr, short_circuit=not args.full_eval)
         log("[rank %d] jit: %s" % (rank, jit_info))
+    # the code this run executes: a hash of the emitted module texts (jit) or of the library's
+    # device code objects (interp) -- profiles of that code are keyed by it, host edits keep them
+    build_id = ct.code_id() if args.engine == "jit" else native.interp_code_id()
     # SURVEY 8d's op table (mh_tape_info.alg_ops): informational, not a work count
     optable_per_row = sum(int(i["alg_ops"]) for i in info)
     if args.strong:

@@ -403,6 +403,15 @@ typedef struct mh_jit_info {
 } mh_jit_info;
 int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr);
 int32_t mh_tapes_jit_info(const mh_tapeset* ts, mh_jit_info* out);
+/* Identifier of the native code mh_tapes_jit built: FNV-1a 64 over its code objects' module texts
+ * (count kernels, in launch order).  Profiles of the emitted code are keyed by it, so a host-only
+ * change (capi.cpp, the query path) keeps them valid.  mh_jit_code_id computes the same value
+ * WITHOUT a device or the assembler (emission only), from the arguments mh_tapes_compile takes and
+ * mh_tapes_jit's flags / max_vgpr (the tapes are validated as mh_tapes_compile does).             */
+int32_t mh_tapes_jit_code_id(const mh_tapeset* ts, uint64_t* out);
+int32_t mh_jit_code_id(const mh_node* nodes, const uint64_t* tape_offsets, uint32_t n_tapes,
+                       const uint32_t* consts, uint32_t n_consts, uint32_t n_vars,
+                       uint32_t flags, uint32_t max_vgpr, uint64_t* out);
 /* 1 if tape t runs on the native path.                                                           */
 int32_t mh_tapes_jitted(const mh_tapeset* ts, uint8_t* out /* [n_tapes] */, uint32_t n_tapes);
 /* Parity path of the native code: root values of every jitted tape over rows

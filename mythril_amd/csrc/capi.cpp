@@ -217,6 +217,7 @@ struct mh_tapeset {
     std::vector<uint32_t> ids_rest;
     uint32_t bucket_off_rest[mh::kNumVariants + 1] = {};
     mh_jit_info jinfo{};
+    uint64_t code_id = 0;   // mh::jit::code_id of the count kernels' module texts
     // conjunct-parallel short runs (mh_run_async): a long tape's root conjunction cut into parts
     // of consecutive conjuncts, each compiled as a tape of its own (ids n_tapes, n_tapes + 1, ..,
     // in the order of their tapes) and bucketed like the tapes; the buckets without the split
@@ -1263,8 +1264,7 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
     // build threads = code objects per occupancy class = launches per run: 4 (MI355X, config 5,
     // profiles/r02y: 16 objects 3.195e11 evals/s, 4 3.222e11, 1 3.226e11 -- each launch drains
     // its tail before the next starts; 4 keeps the emission and assembly parallel)
-    uint32_t threads = std::max(1u, std::min(4u, std::thread::hardware_concurrency()));
-    if (const char* e = std::getenv("MH_JIT_THREADS")) threads = (uint32_t)std::max(1, atoi(e));
+    const uint32_t threads = mh::jit::default_threads();
     std::vector<mh::jit::Built> built;
     mh::jit::BuildStats stats;
     std::string err;
@@ -1278,6 +1278,7 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
         return set_err(MH_E_NOMEM, "host allocation during JIT build");
     }
     if (!ok) return set_err(MH_E_UNSUPPORTED, "JIT: " + err);
+    const uint64_t code_id = mh::jit::code_id(built);
     std::vector<mh_tapeset::JitMod> mods;
     mods.reserve(built.size());
     auto unload = [&]() {
@@ -1330,6 +1331,7 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
     std::copy(boff, boff + mh::kNumVariants + 1, ts->bucket_off_rest);
     ts->d_ids_rest = d_rest;
     ts->has_jit = true;
+    ts->code_id = code_id;
     mh_jit_info& ji = ts->jinfo;
     ji = mh_jit_info{};
     for (uint8_t x : stats.jitted) ji.n_jitted += x;
@@ -1340,6 +1342,55 @@ int32_t mh_tapes_jit(mh_tapeset* ts, uint32_t flags, uint32_t max_vgpr) {
     ji.valu_static = stats.valu_static;
     ji.valu_wide_static = stats.valu_wide_static;
     ji.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return MH_OK;
+}
+
+int32_t mh_tapes_jit_code_id(const mh_tapeset* ts, uint64_t* out) {
+    if (!ts || !out) return set_err(MH_E_INVALID, "null argument");
+    if (!ts->has_jit) return set_err(MH_E_INVALID, "no native code (mh_tapes_jit first)");
+    *out = ts->code_id;
+    return MH_OK;
+}
+
+int32_t mh_jit_code_id(const mh_node* nodes, const uint64_t* tape_offsets, uint32_t n_tapes,
+                       const uint32_t* consts, uint32_t n_consts, uint32_t n_vars,
+                       uint32_t flags, uint32_t max_vgpr, uint64_t* out) {
+    if (!out || (n_tapes && (!nodes || !tape_offsets)) || (n_consts && !consts))
+        return set_err(MH_E_INVALID, "null argument");
+    // the same validation mh_tapes_compile gives a tape set (the JIT reads only checked IR)
+    try {
+        std::vector<uint32_t> dconsts, w;
+        std::unordered_map<std::string, uint32_t> dindex;
+        for (uint32_t t = 0; t < n_tapes; ++t) {
+            const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
+            if (e <= b) return set_err(MH_E_INVALID, "tape " + std::to_string(t) + " is empty");
+            mh::CompiledTape ct;
+            std::string err;
+            w.clear();
+            const int32_t r = mh::compile_tape(nodes + b, (size_t)(e - b), consts, n_consts,
+                                               n_vars, dconsts, dindex, w, ct, err);
+            if (r != MH_OK) return set_err(r, "tape " + std::to_string(t) + ": " + err);
+        }
+    } catch (const std::bad_alloc&) {
+        return set_err(MH_E_NOMEM, "host allocation during validation");
+    }
+    mh::jit::Options opt;
+    opt.max_vgpr = max_vgpr ? max_vgpr : 128;
+    if (opt.max_vgpr > 256 || opt.max_vgpr < 96) return set_err(MH_E_INVALID, "max_vgpr outside 96..256");
+    opt.short_circuit = (flags & MH_JIT_FULL_EVAL) == 0;
+    if (const char* e = std::getenv("MH_JIT_SC")) opt.short_circuit = opt.short_circuit && atoi(e) != 0;
+    opt.assemble = false;
+    std::vector<mh::jit::Built> built;
+    mh::jit::BuildStats stats;
+    std::string err;
+    try {
+        if (!mh::jit::build_tapeset(nodes, tape_offsets, n_tapes, consts, n_consts, n_vars, false,
+                                    opt, mh::jit::default_threads(), built, stats, err))
+            return set_err(MH_E_UNSUPPORTED, "JIT: " + err);
+    } catch (const std::bad_alloc&) {
+        return set_err(MH_E_NOMEM, "host allocation during JIT build");
+    }
+    *out = mh::jit::code_id(built);
     return MH_OK;
 }
 

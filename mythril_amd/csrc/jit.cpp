@@ -3049,6 +3049,27 @@ std::vector<uint32_t> occupancy_classes(uint32_t budget) {
     return c;
 }
 
+static uint64_t fnv1a64(const void* p, size_t n, uint64_t h) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 0x100000001b3ull;
+    return h;
+}
+
+uint32_t default_threads() {
+    uint32_t threads = std::max(1u, std::min(4u, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("MH_JIT_THREADS")) threads = (uint32_t)std::max(1, atoi(e));
+    return threads;
+}
+
+uint64_t code_id(const std::vector<Built>& built) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (const Built& b : built) {
+        h = fnv1a64(&b.text_hash, sizeof b.text_hash, h);
+        h = fnv1a64(&b.n_groups, sizeof b.n_groups, h);
+    }
+    return h;
+}
+
 bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                    const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, bool values,
                    const Options& opt, uint32_t threads, std::vector<Built>& out,
@@ -3174,6 +3195,8 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
             Module m = build_module(pieces[p].codes, pieces[p].ids, n_vars, false, group_bytes);
             b.n_groups = (uint32_t)m.group_first.size();
             b.max_vgpr = m.max_vgpr;
+            b.text_hash = fnv1a64(m.text.data(), m.text.size(), 0xcbf29ce484222325ull);
+            if (!opt.assemble) continue;
             std::string log;
             if (!assemble(m.text, b.hsaco, log)) {
                 b.err = "assemble: " + log.substr(0, 2000);

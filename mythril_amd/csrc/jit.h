@@ -166,6 +166,9 @@ struct Options {
     // Producers of division operands write the subroutine's input registers directly where the
     // copy at the call site would be the value's last use (coalesce_div_moves).
     bool coalesce = true;
+    // Assemble the module texts (comgr).  false: emission and module text only -- enough for the
+    // code id (Built::text_hash), with no assembler and no device.
+    bool assemble = true;
 };
 
 // The SSA of `st` reordered for short-circuit evaluation of its root conjunction (insn_cost: VALU
@@ -239,6 +242,7 @@ struct Built {
     uint32_t n_groups = 0;
     uint32_t max_vgpr = 0;
     std::vector<uint32_t> tape_ids;    // jitted tapes of this slice
+    uint64_t text_hash = 0;            // FNV-1a 64 of the count kernel's module text
     std::string err;
 };
 struct BuildStats {
@@ -252,6 +256,12 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                    const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, bool values,
                    const Options& opt, uint32_t threads, std::vector<Built>& out,
                    BuildStats& stats, std::string& err);
+// Build threads mh_tapes_jit uses (code objects per occupancy class): min(4, hardware threads),
+// or MH_JIT_THREADS.  The cut into code objects, hence the code id, depends on it.
+uint32_t default_threads();
+// Identifier of the emitted code of a build: FNV-1a 64 over the code objects' module texts in
+// order (what the GPU executes, independent of the host sources around it).
+uint64_t code_id(const std::vector<Built>& built);
 
 // Kernel arguments (the kernarg layout build_module's prologue reads).
 struct KernArgs {

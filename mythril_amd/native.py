@@ -80,6 +80,9 @@ SIGNATURES = {
                                          C.POINTER(C.c_double), _u64p]),
     "mh_tapes_jit": (C.c_int32, [_vp, C.c_uint32, C.c_uint32]),
     "mh_tapes_jit_info": (C.c_int32, [_vp, _vp]),
+    "mh_tapes_jit_code_id": (C.c_int32, [_vp, _u64p]),
+    "mh_jit_code_id": (C.c_int32, [_vp, _u64p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
+                                   C.c_uint32, C.c_uint32, _u64p]),
     "mh_tapes_jitted": (C.c_int32, [_vp, C.POINTER(C.c_uint8), C.c_uint32]),
     "mh_jit_eval_all": (C.c_int32, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _u32p]),
     "mh_comm_unique_id": (C.c_int32, [_vp]),
@@ -661,29 +664,75 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
-CODEGEN_SOURCES = ("jit.cpp", "jit.h", "compile.cpp", "compile.h", "exec.h", "u256_ops.h",
-                   "dev_isa.h", "jit_comgr.cpp", "capi.cpp")
-# the interpreter's and the generator's code: the asm core (generated by gen_asm_core.py), the
-# kernel templates around it, the compiler that emits its instruction words
-INTERP_SOURCES = ("gen_asm_core.py", "asm_core.inc", "sieve_kernels.hip", "generate.hip",
-                  "kernels.h", "compile.cpp", "compile.h", "exec.h", "u256_ops.h", "dev_isa.h",
-                  "capi.cpp")
+_CODE_IDS = {}
 
 
-def codegen_id(engine: str = "jit") -> str:
-    """Identifier of the code one engine runs: a hash of the sources that decide it ("jit": the
-    emitted native code; "interp": the interpreter kernels and the generator).  Profiles that
-    price this code (profiles/pmc_summary.json, profiles/alg_work.json) record it, and bench.py
-    uses a profile only for the build and engine it was taken on."""
+def jit_code_id(tapeset: TapeSet, short_circuit: bool = True, max_vgpr: int = 0) -> str:
+    """Identifier of the native code mh_tapes_jit would build for `tapeset` (mh_jit_code_id):
+    a hash of the emitted module texts, computed on the host without a device or the assembler.
+    Equal to CompiledTapes.code_id() after CompiledTapes.jit() with the same options."""
+    nodes, offs, consts = tapeset.flatten()
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32)
+    out = C.c_uint64()
+    _check(load().mh_jit_code_id(nodes.ctypes.data_as(C.c_void_p), _ptr(offs, C.c_uint64),
+                                 len(tapeset.tapes), _ptr(consts), len(tapeset.pool.values),
+                                 tapeset.n_vars, 0 if short_circuit else JIT_FULL_EVAL, max_vgpr,
+                                 C.byref(out)))
+    return "%016x" % out.value
+
+
+def _elf_section(path: str, name: bytes) -> bytes:
+    """The bytes of one section of a 64-bit little-endian ELF file."""
+    import struct
+
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        raise ValueError("%s: not a 64-bit little-endian ELF" % path)
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def sh(i):  # (name offset, offset, size)
+        b = shoff + i * shentsize
+        nm, = struct.unpack_from("<I", data, b)
+        off, size = struct.unpack_from("<QQ", data, b + 0x18)
+        return nm, off, size
+
+    _, stroff, _ = sh(shstrndx)
+    for i in range(shnum):
+        nm, off, size = sh(i)
+        end = data.index(b"\0", stroff + nm)
+        if data[stroff + nm:end] == name:
+            return data[off:off + size]
+    raise ValueError("%s: no section %r" % (path, name))
+
+
+def interp_code_id() -> str:
+    """Identifier of the interpreter's and the generator's device code: a hash of the code objects
+    libmythril_hip.so embeds (its .hip_fatbin section: sieve_kernels.hip, generate.hip and the
+    micro-benchmarks), so a host-only edit leaves it unchanged."""
     import hashlib
 
-    srcs = {"jit": CODEGEN_SOURCES, "interp": INTERP_SOURCES}[engine]
-    h = hashlib.sha256()
-    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
-    for f in srcs:
-        with open(os.path.join(d, f), "rb") as fh:
-            h.update(f.encode() + b"\0" + fh.read())
-    return h.hexdigest()[:16]
+    return hashlib.sha256(_elf_section(LIB_PATH, b".hip_fatbin")).hexdigest()[:16]
+
+
+def codegen_id(engine: str = "jit", variant: str = "plain", short_circuit: bool = True) -> str:
+    """Identifier of the code one engine runs on bench.py's workload ("jit": the native code
+    emitted for the config-5 tape set of `variant`, jit_code_id; "interp": the device code objects
+    of the library, interp_code_id).  Profiles that price this code (profiles/pmc_summary.json,
+    profiles/alg_work.json) record it, and bench.py uses a profile only for the code it runs."""
+    key = (engine, variant, short_circuit)
+    if key not in _CODE_IDS:
+        if engine == "interp":
+            _CODE_IDS[key] = interp_code_id()
+        else:
+            from . import synth
+
+            ts = synth.generate(None, keccak=variant == "keccak")
+            _CODE_IDS[key] = jit_code_id(ts, short_circuit=short_circuit)
+    return _CODE_IDS[key]
 
 
 def gen_limb(seed: int, var: int, index: int, limb: int) -> int:
@@ -786,6 +835,12 @@ class CompiledTapes:
         flags = (JIT_VALUES if values else 0) | (0 if short_circuit else JIT_FULL_EVAL)
         _check(self.ctx.lib.mh_tapes_jit(self.h, flags, max_vgpr))
         return self.jit_info()
+
+    def code_id(self) -> str:
+        """Identifier of the native code jit() built (mh_tapes_jit_code_id; see jit_code_id)."""
+        out = C.c_uint64()
+        _check(self.ctx.lib.mh_tapes_jit_code_id(self.h, C.byref(out)))
+        return "%016x" % out.value
 
     def jit_info(self) -> dict:
         ji = JitInfo()

@@ -255,3 +255,14 @@ def test_jit_short_circuit_matches_full_eval(gpu_ctx):
     f0, c0 = native.run(gpu_ctx, full, a, row_first=333, row_count=rows - 1000, index_base=5,
                         mode=native.MODE_COUNT_ALL)
     assert np.array_equal(c1, c0) and np.array_equal(f1, f0)
+
+
+def test_code_id_equals_the_device_free_id(gpu_ctx):
+    """CompiledTapes.code_id() (mh_tapes_jit_code_id, after a real build and load) is the id
+    mh_jit_code_id computes on the host: bench.py's profile keys need no device to check."""
+    ts = synth.generate(48)
+    for sc in (True, False):
+        ct = gpu_ctx.compile(ts)
+        ct.jit(short_circuit=sc)
+        assert ct.code_id() == native.jit_code_id(ts, short_circuit=sc)
+        ct.close()
