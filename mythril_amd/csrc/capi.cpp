@@ -25,6 +25,15 @@
 
 constexpr uint32_t kSideStreams = 3;  // with the ctx stream: GPU_MAX_HW_QUEUES (4) queues
 
+// MH_FANOUT=0 turns the short-run fan-out over side streams off (read once per process)
+static bool fanout_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("MH_FANOUT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 struct mh_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -409,13 +418,15 @@ int32_t mh_ctx_create(int32_t device, mh_ctx** out) {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     c->own_stream = c->stream != nullptr;
-    // the short-run fan-out's side streams and events up front: a stream created on first use
-    // took 14.4 ms inside the query that first needed it (profiles/r04x)
-    for (uint32_t i = 0; i < kSideStreams && e == hipSuccess; ++i) {
+    // the short-run fan-out's side streams and events up front, when the fan-out is on: a stream
+    // created on first use took 14.4 ms inside the query that first needed it (profiles/r04x).
+    // With MH_FANOUT=0 a ctx holds its one stream (hardware queues are few per process)
+    for (uint32_t i = 0; i < kSideStreams && e == hipSuccess && fanout_enabled(); ++i) {
         e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming);
     }
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
+    if (e == hipSuccess && fanout_enabled())
+        e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&c->scratch, 64);
     if (e == hipSuccess) {
         // one block of the smallest class ready for the first query, and the pinned upload
@@ -1108,22 +1119,12 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
             v = last;
         }
     }
-    static const bool fanout = [] {
-        const char* e = std::getenv("MH_FANOUT");
-        return !(e && e[0] == '0');
-    }();
-    // a short run's launches overlap on the side streams; the results they write are disjoint
-    // (per tape / per part), and the join puts everything after them back in `stream`'s order
-    const uint32_t n_side =
-        fanout && (merge || split) ? std::min(n_launch - (n_launch > 0), kSideStreams) : 0;
+    // a short run's launches overlap on the side streams (made with the ctx when the fan-out
+    // is on); the results they write are disjoint (per tape / per part), and the join puts
+    // everything after them back in `stream`'s order
+    const uint32_t n_side = fanout_enabled() && (merge || split)
+                                ? std::min(n_launch - (n_launch > 0), kSideStreams) : 0;
     if (n_side) {
-        if (!ctx->fork_ev) MH_HIP(hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
-        for (uint32_t i = 0; i < n_side; ++i) {
-            if (!ctx->side[i])
-                MH_HIP(hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking));
-            if (!ctx->join_ev[i])
-                MH_HIP(hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming));
-        }
         MH_HIP(hipEventRecord(ctx->fork_ev, ctx->stream));
         for (uint32_t i = 0; i < n_side; ++i) MH_HIP(hipStreamWaitEvent(ctx->side[i], ctx->fork_ev, 0));
     }

@@ -1281,6 +1281,18 @@ int32_t mh_terms_append(mh_terms* t, const mh_node* nodes, uint64_t n_nodes,
     if (!t || (n_nodes && !nodes) || (n_consts && !consts) || (n_vars && !var_names) ||
         (n_arrays && !array_names) || (n_fns && !fn_names))
         return mh_detail_set_err(MH_E_INVALID, "null argument");
+    // validate every node against the store as it will be after this append, then append:
+    // a rejected batch changes nothing (TermMirror.sync sends it again after an error)
+    const size_t n0 = t->nodes.size(), p0 = t->pool.size();
+    const size_t v0 = t->var_names.size(), a0 = t->array_names.size(), f0 = t->fn_names.size();
+    for (uint64_t i = 0; i < n_nodes; ++i) {
+        const mh_node& x = nodes[i];
+        const uint64_t id = n0 + i;
+        const int k = arity(x.op);
+        if ((k > 0 && x.a >= id) || (k > 1 && x.b >= id) || (k > 2 && x.c >= id) ||
+            (x.op == CONST && x.imm0 >= p0 + n_consts))
+            return mh_detail_set_err(MH_E_INVALID, "node operand outside the term store");
+    }
     try {
         for (uint64_t i = 0; i < n_consts; ++i) {
             Big v;
@@ -1288,19 +1300,9 @@ int32_t mh_terms_append(mh_terms* t, const mh_node* nodes, uint64_t n_nodes,
             t->pool_index.emplace(v, (uint32_t)t->pool.size());
             t->pool.push_back(v);
         }
-        const size_t n0 = t->nodes.size();
         for (uint64_t i = 0; i < n_nodes; ++i) {
-            const mh_node& x = nodes[i];
-            const uint32_t id = (uint32_t)(n0 + i);
-            const int k = arity(x.op);
-            if ((k > 0 && x.a >= id) || (k > 1 && x.b >= id) || (k > 2 && x.c >= id) ||
-                (x.op == CONST && x.imm0 >= t->pool.size())) {
-                for (size_t j = n0; j < t->nodes.size(); ++j) t->memo.erase(key_of(t->nodes[j]));
-                t->nodes.resize(n0);
-                return mh_detail_set_err(MH_E_INVALID, "node operand outside the term store");
-            }
-            t->nodes.push_back(x);
-            t->memo.emplace(key_of(x), id);
+            t->nodes.push_back(nodes[i]);
+            t->memo.emplace(key_of(nodes[i]), (uint32_t)(n0 + i));
         }
         auto names = [](const char* p, uint64_t n, std::vector<std::string>& out) {
             for (uint64_t i = 0; i < n; ++i) {  // NUL-terminated, back to back
@@ -1313,6 +1315,21 @@ int32_t mh_terms_append(mh_terms* t, const mh_node* nodes, uint64_t n_nodes,
         names(array_names, n_arrays, t->array_names);
         names(fn_names, n_fns, t->fn_names);
     } catch (const std::bad_alloc&) {
+        // back to the sizes on entry; map entries are dropped only where they point at an
+        // appended element (an equal earlier constant or node keeps its own entry)
+        for (size_t j = n0; j < t->nodes.size(); ++j) {
+            auto it = t->memo.find(key_of(t->nodes[j]));
+            if (it != t->memo.end() && it->second >= n0) t->memo.erase(it);
+        }
+        for (size_t j = p0; j < t->pool.size(); ++j) {
+            auto it = t->pool_index.find(t->pool[j]);
+            if (it != t->pool_index.end() && it->second >= p0) t->pool_index.erase(it);
+        }
+        t->nodes.resize(n0);
+        t->pool.resize(p0);
+        t->var_names.resize(v0);
+        t->array_names.resize(a0);
+        t->fn_names.resize(f0);
         return mh_detail_set_err(MH_E_NOMEM, "mh_terms_append");
     }
     return MH_OK;

@@ -668,5 +668,9 @@ def _schema_of(b: TapeBuilder, L: "Lowering", used: frozenset) -> "Schema":
             if col is None:
                 col = Column(name, b.symbols.var_widths[name], "var", name)
             full.columns[name] = col
+        if col.kind != "var" and name in b.symbols.user_vars:
+            # a declared symbol named like a cell: one column would stand for both (the native
+            # compiler refuses the same, csrc/query.cpp QueryState::emit)
+            raise LoweringUnsupported("variable %s is named like an array cell" % name)
         cols[name] = col
     return Schema(full.cells, full.uf_cells, full.keccak, cols)

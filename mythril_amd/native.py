@@ -403,7 +403,7 @@ class SmtlibSession:
             elif op == 0:  # CONST (<= 256 bits; wider ones arrive as CONCATs)
                 h = b.const(int.from_bytes(cbuf[4 * coff:4 * coff + 32], "little"), w)
             elif op == 1:
-                h = b.var(names[noff:noff + nlen], w)
+                h = b.user_var(names[noff:noff + nlen], w)
             elif op == 80:
                 h = b.array(names[noff:noff + nlen], i1, w)
             elif op == 81:

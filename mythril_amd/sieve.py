@@ -23,6 +23,7 @@ behaviour is kept on every error (SURVEY.md §5 "fail closed").
 """
 from __future__ import annotations
 
+import threading
 import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -127,14 +128,28 @@ class NativeSchema(Schema):
     here), LASER's is_possible never reads it (constraints.py:25-35)."""
 
     _FIELDS = ("cells", "uf_cells", "keccak", "columns")
+    # one decode at a time, process-wide (a remembered witness may be read by several threads;
+    # decodes are rare and short); not on the instance, so copies and pickles see only _cq
+    _DECODE_LOCK = threading.Lock()
 
     def __init__(self, cq: "native.CompiledQuery"):  # noqa: super().__init__ deferred
         self.__dict__["_cq"] = cq
 
     def __getattr__(self, name):
-        if name not in self._FIELDS or "_cq" not in self.__dict__:
+        if name not in self._FIELDS:
             raise AttributeError(name)
-        cq = self.__dict__.pop("_cq")
+        # the compiled query is dropped only once the Schema is complete, so a decode that
+        # raises leaves the next read to try again
+        with NativeSchema._DECODE_LOCK:
+            if name in self.__dict__:
+                return self.__dict__[name]
+            if "_cq" not in self.__dict__:
+                raise AttributeError(name)
+            self._decode(self.__dict__["_cq"])
+            del self.__dict__["_cq"]
+        return self.__dict__[name]
+
+    def _decode(self, cq) -> None:
         cols = {n: Column(n, w, k, s, key) for n, w, k, s, key in cq.columns}
         cells: Dict[str, Dict[int, str]] = {}
         uf_cells: Dict[str, Dict[int, str]] = {}
@@ -146,7 +161,6 @@ class NativeSchema(Schema):
                 (cells if kind == native.TABLE_CELLS else uf_cells)[name_] = {
                     k: cell_name(name_, k) for k in items}
         Schema.__init__(self, cells, uf_cells, keccak, cols)
-        return self.__dict__[name]
 
 
 def substitute(b: TapeBuilder, root: int, env: Dict[int, int]) -> int:
@@ -527,8 +541,15 @@ class Sieve:
         conjunction that contradicts itself syntactically (MH_QUERY_REFUTED: x == 1 and x == 2,
         p and not p, bounds with an empty range), which no row can satisfy."""
         t0 = time.perf_counter()
-        cq = native.TermMirror.of(b).build(b, roots)
         st = self.stats
+        try:
+            cq = native.TermMirror.of(b).build(b, roots)
+        except native.Unsupported:
+            # a shape the native compiler refuses (a variable named like an array cell, ...):
+            # the Python stages it restates may still take it
+            st.extra["native_unsupported"] = st.extra.get("native_unsupported", 0) + 1
+            st.add("lower", time.perf_counter() - t0)
+            return None
         st.add("lower", time.perf_counter() - t0)
         if cq.flags & native.QUERY_REFUTED:
             st.extra["refuted"] = st.extra.get("refuted", 0) + 1

@@ -263,7 +263,7 @@ class _SymbolFactory:
     @staticmethod
     def BoolSym(name: str, annotations=None) -> Bool:
         ctx = context()
-        v = _b(ctx).var(name, 1)
+        v = _b(ctx).user_var(name, 1)
         one = _b(ctx).const(1, 1)
         return Bool(_b(ctx).op(Op.EQ, v, one), ctx, annotations)
 
@@ -275,7 +275,7 @@ class _SymbolFactory:
     @staticmethod
     def BitVecSym(name: str, size: int, annotations=None) -> BitVec:
         ctx = context()
-        return BitVec(_b(ctx).var(name, size), ctx, annotations)
+        return BitVec(_b(ctx).user_var(name, size), ctx, annotations)
 
 
 symbol_factory = _SymbolFactory()

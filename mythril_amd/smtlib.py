@@ -247,9 +247,9 @@ class Reader:
         if kind != "const":
             raise SmtlibError("function %r used as a constant" % t)
         if sort.kind == "bool":
-            return b.op(Op.EQ, b.var(t, 1), b.const(1, 1))
+            return b.op(Op.EQ, b.user_var(t, 1), b.const(1, 1))
         if sort.kind == "bv":
-            return b.var(t, sort.width)
+            return b.user_var(t, sort.width)
         return b.array(t, sort.domain, sort.width)
 
     def _indexed(self, head: list, x: int) -> int:

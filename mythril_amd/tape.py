@@ -302,6 +302,12 @@ class TapeBuilder:
             self.var_index[name] = len(self.var_index)
         return self._add(Op.VAR, width, imm0=self.var_index[name])
 
+    def user_var(self, name: str, width: int = 256) -> int:
+        """var() for a symbol the terms declare (not a column lowering makes)."""
+        n = self.var(name, width)
+        self.symbols.user_vars.add(name)
+        return n
+
     def true(self) -> int:
         return self._add(Op.TRUE, BOOL)
 
@@ -442,6 +448,10 @@ class Symbols:
         self.array_names: List[str] = []
         self.function_names: List[str] = []
         self.var_widths: Dict[str, int] = {}
+        # names of the scalar symbols terms declare (BitVecSym, the z3 import), as opposed to the
+        # columns lowering makes (array cells "A[0x5]", else columns "A[*]"): a query holding both
+        # under one name is refused (lower._schema_of), as the native compiler refuses it
+        self.user_vars: set = set()
 
     def array_id(self, name: str, domain: int, value_range: int) -> int:
         got = self.arrays.get(name)

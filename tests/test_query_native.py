@@ -240,6 +240,40 @@ def test_malformed_append_is_refused():
     m.close()
 
 
+def test_rejected_append_changes_nothing():
+    """A batch with a bad node after constants and good nodes leaves the store as it was (no
+    constant lands twice when the batch is sent again), and the next good batch appends."""
+    m = native.TermMirror()
+    sizes = (native.C.c_uint64 * 5)()
+
+    def store():
+        native._check(m.lib.mh_terms_sizes(m.h, sizes))
+        return list(sizes)
+
+    consts = native.np.arange(16, dtype=native.np.uint32)  # two 256-bit constants
+    batch = native.np.zeros(3, dtype=native.NODE_DTYPE)
+    batch["op"] = [int(Op.CONST), int(Op.CONST), int(Op.BVADD)]
+    batch["width"] = 256
+    batch["imm0"] = [0, 1, 0]
+    batch["a"], batch["b"] = [0, 0, 0], [0, 0, 1]
+    bad = batch.copy()
+    bad["a"][2] = 7  # operand outside the store
+    with pytest.raises(native.SieveError):
+        native._check(m.lib.mh_terms_append(m.h, bad.ctypes.data, 3, native._ptr(consts), 2,
+                                            b"v\0", 1, None, 0, None, 0))
+    assert store() == [0, 0, 0, 0, 0]
+    bad2 = batch.copy()
+    bad2["imm0"][1] = 2  # a constant index past this batch's constants
+    with pytest.raises(native.SieveError):
+        native._check(m.lib.mh_terms_append(m.h, bad2.ctypes.data, 3, native._ptr(consts), 2,
+                                            None, 0, None, 0, None, 0))
+    assert store() == [0, 0, 0, 0, 0]
+    native._check(m.lib.mh_terms_append(m.h, batch.ctypes.data, 3, native._ptr(consts), 2,
+                                        b"v\0", 1, None, 0, None, 0))
+    assert store() == [3, 2, 1, 0, 0]
+    m.close()
+
+
 def test_refutation_is_sound_on_random_conjunctions():
     """Random conjunctions of comparisons, negations, ULE/UGE (Or forms) and the no-overflow
     predicates over three 4-bit symbols: every one MH_QUERY_REFUTED flags has no satisfying

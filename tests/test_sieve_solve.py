@@ -107,3 +107,62 @@ def test_later_round_runs_only_unsolved_groups(monkeypatch):
     s = Sieve(rows=64, first_rows=64, budget_s=60.0)
     assert s.solve(ctx.b, [(x == 5).node, (y * y == 2).node]) is None
     assert calls == [(0, 2), (1, 1)]
+
+
+def test_native_refusal_takes_the_python_stages(monkeypatch):
+    """A query the native compiler refuses goes through the Python host stages, and
+    both refuse a declared symbol named like an array cell: one column would stand for the
+    symbol and the cell, and the model would lose the symbol.  Such a query reaches the fallback
+    unchanged; without the collision the same shape is solved."""
+    from mythril_amd import smt
+    from mythril_amd.lower import LoweringUnsupported
+    from mythril_amd.smt import Array, symbol_factory
+
+    fake_device.install(monkeypatch)
+    for name, solved in (("A[0x5]", False), ("A_5", True)):
+        ctx = smt.set_context(smt.Context())
+        a = Array("A", 256, 256)
+        v = symbol_factory.BitVecSym(name, 256)
+        cs = [a[symbol_factory.BitVecVal(5, 256)] == symbol_factory.BitVecVal(7, 256),
+              v == symbol_factory.BitVecVal(7, 256)]
+        s = Sieve(rows=256, native_query=True)
+        if not solved:
+            with pytest.raises(LoweringUnsupported):
+                s.solve(ctx.b, [c.node for c in cs])
+            assert s.stats.extra.get("native_unsupported") == 1
+            continue
+        w = s.solve(ctx.b, [c.node for c in cs])
+        assert w is not None and _oracle_holds(ctx, cs, w.schema, w.values)
+
+
+def test_native_schema_decode_failure_is_retried():
+    """NativeSchema keeps its compiled query until the decode succeeds: a failing
+    first read leaves the schema readable, and concurrent reads decode it once."""
+    import threading
+
+    from mythril_amd import native
+    from mythril_amd.sieve import NativeSchema
+
+    class CQ:
+        calls = 0
+
+        @property
+        def columns(self):
+            CQ.calls += 1
+            if CQ.calls == 1:
+                raise RuntimeError("first decode fails")
+            return [("x", 256, "var", "x", None)]
+
+        tables = [(native.TABLE_CELLS, "A", [5])]
+
+    sch = NativeSchema(CQ())
+    with pytest.raises(RuntimeError):
+        sch.columns
+    out = []
+    ts = [threading.Thread(target=lambda: out.append(sorted(sch.columns))) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert out == [["x"]] * 8 and CQ.calls == 2
+    assert sch.cells == {"A": {5: "A[0x5]"}}
