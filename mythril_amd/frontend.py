@@ -214,7 +214,9 @@ def sieve_model(constraints, timeout_ms: Optional[float] = None):
     if w is None:
         stats.sieve_misses += 1
         return None
-    m = Model(s, ctx, w.schema, w.values, w.index)
+    conv = _config["to_terms"]  # reads reference terms for Model.eval / Model[decl]
+    m = Model(s, ctx, w.schema, w.values, w.index,
+              importer=conv if hasattr(conv, "term") else None)
     verify = _config["verify"]
     if verify is not None:
         left = None if timeout_ms is None else timeout_ms - 1000.0 * (time.perf_counter() - t0)

@@ -264,6 +264,7 @@ class _SymbolFactory:
     def BoolSym(name: str, annotations=None) -> Bool:
         ctx = context()
         v = _b(ctx).user_var(name, 1)
+        _b(ctx).symbols.bool_vars.add(name)
         one = _b(ctx).const(1, 1)
         return Bool(_b(ctx).op(Op.EQ, v, one), ctx, annotations)
 

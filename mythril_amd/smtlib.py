@@ -247,7 +247,9 @@ class Reader:
         if kind != "const":
             raise SmtlibError("function %r used as a constant" % t)
         if sort.kind == "bool":
-            return b.op(Op.EQ, b.user_var(t, 1), b.const(1, 1))
+            v = b.user_var(t, 1)
+            b.symbols.bool_vars.add(t)
+            return b.op(Op.EQ, v, b.const(1, 1))
         if sort.kind == "bv":
             return b.user_var(t, sort.width)
         return b.array(t, sort.domain, sort.width)
@@ -573,6 +575,18 @@ def _z3_sexpr(raw) -> str:
     return s.sexpr()
 
 
+def _z3_term_sexpr(raw) -> str:
+    """SMT-LIB2 of one reference term of any sort, as z3 prints it: a Bool as an assert, a
+    bit-vector as an Optimize objective (``(minimize t)``: the reader hands its node back)."""
+    import z3
+
+    if z3.is_bool(raw):
+        return _z3_sexpr(raw)
+    o = z3.Optimize()
+    o.minimize(raw)
+    return o.sexpr()
+
+
 class Z3Importer:
     """z3-backed reference terms -> sieve terms, memoised per z3 AST id (callable as the
     front end's ``to_terms``).
@@ -585,7 +599,7 @@ class Z3Importer:
     ``Solver.sexpr()`` by default)."""
 
     def __init__(self, ctx: Optional[smt.Context] = None, max_memo: int = 1 << 16,
-                 max_nodes: int = 1 << 21, sexpr_of=None, on_reset=None):
+                 max_nodes: int = 1 << 21, sexpr_of=None, on_reset=None, term_sexpr_of=None):
         from collections import OrderedDict
 
         self.reader = NativeReader(ctx)
@@ -593,6 +607,8 @@ class Z3Importer:
         self.max_memo = max_memo
         self.max_nodes = max_nodes
         self.sexpr_of = sexpr_of or _z3_sexpr
+        # one term of any sort (Model.eval / Model[decl] of reference terms): _z3_term_sexpr
+        self.term_sexpr_of = term_sexpr_of or _z3_term_sexpr
         self.on_reset = on_reset
         self.resets = 0
 
@@ -627,3 +643,33 @@ class Z3Importer:
                 self.memo.move_to_end(key)
             out.append(smt.Bool(got[1], self.reader.ctx))
         return self.reader.ctx, out
+
+    @property
+    def ctx(self) -> smt.Context:
+        return self.reader.ctx
+
+    def term(self, raw) -> "smt.Expression":
+        """One reference term of any sort (a z3 ``ExprRef``: Bool or bit-vector, up to 512 bits
+        and beyond) as a term of this importer's context, for Model.eval / Model[decl] of the
+        reference's callers (calldata.py:240-244, analysis/solver.py:141,174-176,
+        keccak_function_manager.py:113).  Memoised with the constraints; never resets the
+        context (a model's terms must stay in the context its witness was found in)."""
+        key = ("term", raw.get_id())
+        got = self.memo.get(key)
+        if got is None or got[0] is not raw:
+            q = Query(self.reader.ctx)
+            self.reader.read(self.term_sexpr_of(raw), q)
+            if len(q.constraints) == 1 and not q.minimize and not q.maximize:
+                node, is_bool = q.constraints[0].node, True
+            elif len(q.minimize) == 1 and not q.constraints:
+                node, is_bool = q.minimize[0].node, False
+            else:
+                raise SmtlibError("a single term was expected, got %d asserts and %d objectives"
+                                  % (len(q.constraints), len(q.minimize) + len(q.maximize)))
+            got = self.memo[key] = (raw, (node, is_bool))
+            while len(self.memo) > self.max_memo:
+                self.memo.popitem(last=False)
+        else:
+            self.memo.move_to_end(key)
+        node, is_bool = got[1]
+        return (smt.Bool if is_bool else smt.BitVec)(node, self.reader.ctx)

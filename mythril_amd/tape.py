@@ -452,6 +452,7 @@ class Symbols:
         # columns lowering makes (array cells "A[0x5]", else columns "A[*]"): a query holding both
         # under one name is refused (lower._schema_of), as the native compiler refuses it
         self.user_vars: set = set()
+        self.bool_vars: set = set()  # ... of them Bool symbols (1-bit columns compared with 1)
 
     def array_id(self, name: str, domain: int, value_range: int) -> int:
         got = self.arrays.get(name)

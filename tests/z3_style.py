@@ -13,8 +13,10 @@ from mythril_amd.smtlib import _OPNAME, _bv, _sort_str, _sym
 from mythril_amd.tape import ARITY, F_ARRAY, Op
 
 
-def z3_sexpr(c) -> str:
-    """The declarations and the assert of Bool term `c`, z3-style (shared terms as lets)."""
+def z3_sexpr(c, head: str = "assert") -> str:
+    """The declarations and the assert of Bool term `c`, z3-style (shared terms as lets).
+    head="minimize": what ``z3.Optimize().minimize(t).sexpr()`` prints for a bit-vector term
+    (the import of a single term, smtlib._z3_term_sexpr)."""
     b = c.ctx.b
     order: List[int] = []
     uses: Dict[int, int] = {}
@@ -100,4 +102,4 @@ def z3_sexpr(c) -> str:
     body = expr(c.node)
     for name, text in reversed(binds):
         body = "(let ((%s %s))\n  %s)" % (name, text, body)
-    return "\n".join(decls + ["(assert %s)" % body]) + "\n"
+    return "\n".join(decls + ["(%s %s)" % (head, body)]) + "\n"
