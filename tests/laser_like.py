@@ -58,29 +58,38 @@ def sender_is_actor(sender: BitVec) -> smt.Bool:
 
 
 class KeccakManager:
-    """keccak_function_manager.py:24-149 restated over the test term API."""
+    """keccak_function_manager.py:24-149 restated over the test term API, exactly: a concrete
+    input's hash is remembered (``concrete_hashes``, keyed by value and width as the reference's
+    dict of BitVecVals is) and every later symbolic input's condition ORs over ALL remembered
+    pairs, whatever their width -- ``key == func_input`` zero-pads the narrower side
+    (bitvec.py:16-22), so an 8-bit key 100 admits a 256-bit input 100 (:145-148).  The state is
+    plain integers, so one manager can serve several term contexts in turn, as the reference's
+    module-level manager serves every test of a pytest session."""
 
     def __init__(self):
         self.store = {}
         self.hooks = {}
         self.counter = TOTAL_PARTS - 34534
-        self.concrete = []  # (data term, hash term)
+        self.concrete = {}  # (value, width) -> hash, in insertion order (:40, :95)
 
     def functions(self, length: int):
-        if length not in self.store:
-            self.store[length] = (Function("keccak256_%d" % length, length, 256),
-                                  Function("keccak256_%d-1" % length, 256, length))
-        return self.store[length]
+        # terms of the CURRENT context (a shared manager outlives the contexts of its cases)
+        ctx = smt.context()
+        got = self.store.get(length)
+        if got is None or got[0] is not ctx:
+            got = self.store[length] = (ctx, Function("keccak256_%d" % length, length, 256),
+                                        Function("keccak256_%d-1" % length, 256, length))
+        return got[1], got[2]
 
     def create(self, data: BitVec):
         length = data.size()
         f, inv = self.functions(length)
-        if data.value is not None:
+        if data.value is not None:  # :92-97
             h = int.from_bytes(keccak256(data.value.to_bytes(length // 8, "big")), "big")
             hv = symbol_factory.BitVecVal(h, 256)
-            self.concrete.append((data, hv))
+            self.concrete[(data.value, length)] = h
             return hv, And(f(data) == hv, inv(f(data)) == data)
-        if length not in self.hooks:
+        if length not in self.hooks:  # :128-133
             self.hooks[length] = self.counter
             self.counter -= INTERVAL_DIFFERENCE
         lo = self.hooks[length] * PART
@@ -90,9 +99,9 @@ class KeccakManager:
                    ULT(f(data), symbol_factory.BitVecVal(hi, 256)),
                    URem(f(data), symbol_factory.BitVecVal(64, 256)) == 0)
         conc = symbol_factory.Bool(False)
-        for key, hv in self.concrete:
-            if key.size() == length:
-                conc = Or(conc, And(f(data) == hv, key == data))
+        for (value, width), h in self.concrete.items():  # :145-148, every width
+            key = symbol_factory.BitVecVal(value, width)
+            conc = Or(conc, And(f(data) == symbol_factory.BitVecVal(h, 256), key == data))
         return f(data), And(inv(f(data)) == data, Or(cond, conc))
 
 

@@ -4,9 +4,12 @@ mythril_amd.smt term API (test helpers; data, not copied source).
 Each case names the reference test it restates and the outcome that test asserts:
 
 * tests/laser/keccak_tests.py:7-138 — keccak UF equalities through the keccak function
-  manager (restated as tests/laser_like.KeccakManager, keccak_function_manager.py:83-149);
-  a fresh manager per case (the reference shares one module-level manager, whose concrete
-  hashes then enter later cases' Or-chains; no case's outcome depends on that);
+  manager (restated exactly as tests/laser_like.KeccakManager, keccak_function_manager.py:24-149),
+  in two variants: a fresh manager per case (``CASES``), and one manager shared by all the
+  module's cases in file order (``shared_keccak_cases``), as the reference's module-level
+  manager is -- its remembered concrete hashes then enter later cases' Or-chains.  Where the
+  restated query is satisfiable against the test's asserted "unsat" (the reference's code and
+  its assertion diverge), ``DIVERGENT`` names the case and the witness that shows it;
 * tests/laser/state/calldata_test.py:14-91 — concrete and symbolic calldata (calldata.py);
 * tests/laser/state/storage_test.py:11-58 — concrete (K) and symbolic storage (account.py:18-82);
 * tests/laser/smt/independece_solver_test.py:42-145 — the DependenceMap partition and the
@@ -85,18 +88,18 @@ def _fresh():
 # -- keccak_tests.py --------------------------------------------------------------------------
 
 def _keccak_basic(mk1, mk2):
-    def build():
+    def build(km=None):
         ctx = _fresh()
-        km = KeccakManager()
+        km = km or KeccakManager()
         o1, c1 = km.create(mk1())
         o2, c2 = km.create(mk2())
         return ctx, [And(c1, c2), o1 == o2]
     return build
 
 
-def _keccak_symbol_and_val():
+def _keccak_symbol_and_val(km=None):
     ctx = _fresh()
-    km = KeccakManager()
+    km = km or KeccakManager()
     n = BVS("n", 256)
     o1, c1 = km.create(BVV(100, 256))
     o2, c2 = km.create(n)
@@ -104,9 +107,9 @@ def _keccak_symbol_and_val():
 
 
 def _keccak_complex(distinct: bool):
-    def build():
+    def build(km=None):
         ctx = _fresh()
-        km = KeccakManager()
+        km = km or KeccakManager()
         a, b = BVS("a", 160), BVS("b", 160)
         o1, c1 = km.create(a)
         o2, c2 = km.create(b)
@@ -121,16 +124,16 @@ def _keccak_complex(distinct: bool):
     return build
 
 
-def _keccak_simple_number():
+def _keccak_simple_number(km=None):
     ctx = _fresh()
-    km = KeccakManager()
+    km = km or KeccakManager()
     o, c = km.create(BVS("a", 160))
     return ctx, [c, BVV(10, 256) == o]
 
 
-def _keccak_other_num():
+def _keccak_other_num(km=None):
     ctx = _fresh()
-    km = KeccakManager()
+    km = km or KeccakManager()
     a, b = BVS("a", 160), BVS("b", 256)
     o, c = km.create(a)
     cs = [c]
@@ -287,6 +290,45 @@ BY_NAME = {c.name: c for c in CASES}
 
 def case_ids():
     return [c.name for c in CASES]
+
+
+KECCAK_MODULE = [c.name for c in CASES if c.ref.startswith(KT)]  # keccak_tests.py, file order
+
+
+def _k(value: int, nbytes: int) -> int:
+    from oracle.keccak import keccak256
+
+    return int.from_bytes(keccak256(value.to_bytes(nbytes, "big")), "big")
+
+
+# Cases whose restated query -- the reference's own construction, exactly -- is satisfiable
+# although the reference test asserts "unsat": the reference's code and its assertion diverge.
+# Each entry: why, and a model (vars, functions) the ORACLE checks against the query
+# (tests/test_reference_fixtures.py::test_divergent_cases_are_satisfiable).  The sieve answers
+# neither with a witness (its keccak lowering gives keccak256_256 its own interval values, so it
+# cannot make keccak256_256(100) equal an 8-bit input's hash); the query reaches the fallback,
+# where z3 decides it.
+DIVERGENT = {
+    "keccak_basic_val8_100_sym_N1": (
+        "keccak_function_manager.py:145-148 ORs every remembered concrete pair into N1's "
+        "condition, and `key == func_input` zero-pads the 8-bit key 100 (bitvec.py:16-22): "
+        "N1 = 100 with keccak256_256(100) = keccak(0x64) satisfies o1 == o2",
+        {"N1": 100},
+        {"keccak256_8": {100: _k(100, 1)}, "keccak256_8-1": {_k(100, 1): 100},
+         "keccak256_256": {100: _k(100, 1)}, "keccak256_256-1": {_k(100, 1): 100}}),
+}
+
+
+def shared_keccak_cases():
+    """keccak_tests.py's cases in file order over ONE manager (the reference's module-level
+    ``keccak_function_manager``): [(case, ctx, constraints)], each case in a fresh context."""
+    km = KeccakManager()
+    out = []
+    for name in KECCAK_MODULE:
+        case = BY_NAME[name]
+        ctx, cs = case.build(km)
+        out.append((case, ctx, cs))
+    return out
 
 
 def dependence_map_case():

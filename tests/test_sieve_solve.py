@@ -11,7 +11,7 @@ from mythril_amd.model import Model
 from mythril_amd.sieve import Sieve
 from tests import fake_device
 from tests.laser_like import queries
-from tests.reference_cases import BY_NAME, CASES
+from tests.reference_cases import BY_NAME, CASES, DIVERGENT, shared_keccak_cases
 from tests.test_reference_fixtures import holds_original
 from tests.test_gpu_frontend import _oracle_holds
 
@@ -53,7 +53,9 @@ def test_reference_outcome_on_fake_device(monkeypatch, name, native_query):
         calls = []
         frontend.configure(fallback=lambda c, *a: calls.append(c) or "fallback")
         m = frontend.get_model(tuple(cs))
-        if case.expected == "unsat" or case.fallback_reason:
+        if name in DIVERGENT and isinstance(m, Model):
+            assert holds_original(ctx, cs, m.schema, m.values), name
+        elif case.expected == "unsat" or case.fallback_reason:
             assert m == "fallback" and len(calls) == 1, name
         else:
             assert isinstance(m, Model) and not calls, name
@@ -62,6 +64,26 @@ def test_reference_outcome_on_fake_device(monkeypatch, name, native_query):
                 assert m.eval(c, model_completion=True) is True, name
     finally:
         frontend.reset()
+
+
+@pytest.mark.parametrize("native_query", [True, False])
+def test_shared_keccak_manager_outcomes_on_fake_device(monkeypatch, native_query):
+    """keccak_tests.py over one shared manager, in file order, through get_model."""
+    fake_device.install(monkeypatch)
+    for case, ctx, cs in shared_keccak_cases():
+        frontend.reset()
+        try:
+            frontend.configure(rows=256, native_query=native_query)
+            calls = []
+            frontend.configure(fallback=lambda c, *a: calls.append(c) or "fallback")
+            m = frontend.get_model(tuple(cs))
+            if isinstance(m, Model):
+                assert case.expected == "sat" or case.name in DIVERGENT, case.name
+                assert holds_original(ctx, cs, m.schema, m.values), case.name
+            else:
+                assert case.expected == "unsat" and len(calls) == 1, case.name
+        finally:
+            frontend.reset()
 
 
 def test_refuted_query_skips_the_device(monkeypatch):
