@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Recall of the sieve on queries that are SAT by construction.
+
+Paths of tests/planted.py (a model drawn first, every constraint oriented to hold under it and
+checked by the oracle) are asked in LASER order on one Sieve -- every prefix a query, its parent
+solved first (svm.py:257-262) -- so every query is satisfiable and every miss is a query the
+sieve could have answered and z3 must.  Per query: the outcome (a hit in the first, 256-row round
+or only in the second, 2^16-row round; a miss; a refutation -- a soundness failure, since M is a
+model; an unsupported shape), the wall time, and for a hit that the witness is a model of the
+original query (oracle/term_eval.py).  One JSON line per family with the recall overall, per
+round, per shape class of the query's newest constraint, latency percentiles; with --extended,
+the misses are asked again of a sieve with 2^20-row second rounds (how many more rows would
+recover).
+
+    python scripts/planted_recall.py [n_paths=100] [path_len=24] [--extended] [--fake]
+
+--fake runs on tests/fake_device.py (CPU; use small sizes).
+"""
+import json
+import os
+import sys
+import time
+from collections import Counter, defaultdict
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+
+from mythril_amd.sieve import Sieve  # noqa: E402
+from tests.planted import FAMILIES, planted_path  # noqa: E402
+from tests.test_reference_fixtures import holds_original  # noqa: E402
+
+
+def _pct(v):
+    if not v:
+        return {"n": 0}
+    a = np.array(v)
+    return {"n": len(v), "p50": round(float(np.percentile(a, 50)), 3),
+            "p90": round(float(np.percentile(a, 90)), 3),
+            "p99": round(float(np.percentile(a, 99)), 3), "max": round(float(a.max()), 3)}
+
+
+def run_family(s, family, n_paths, path_len, big=None, check=True):
+    """Every prefix of n_paths planted paths in LASER order on sieve `s`.  Returns the summary
+    and the list of missed (seed, prefix) pairs."""
+    outcomes = Counter()
+    by_kind = defaultdict(Counter)
+    times = defaultdict(list)
+    bad, missed = [], []
+    for seed in range(n_paths):
+        ctx, cs, m, kinds = planted_path(family, seed, path_len)
+        nodes = [c.node for c in cs]
+        for k in range(1, len(nodes) + 1):
+            r0 = s.stats.extra.get("refuted", 0)
+            t0 = time.perf_counter()
+            try:
+                w = s.solve(ctx.b, nodes[:k], key=tuple(nodes[:k]))
+                dt = (time.perf_counter() - t0) * 1e3
+                if w is not None:
+                    kind = "hit_r%d" % w.rounds
+                    if check and not holds_original(ctx, cs[:k], w.schema, w.values):
+                        bad.append((seed, k))
+                elif s.stats.extra.get("refuted", 0) > r0:
+                    kind = "refuted"
+                else:
+                    kind = "miss"
+                    missed.append((seed, k))
+            except Exception as e:  # noqa: BLE001 - the front end falls back on any error
+                dt = (time.perf_counter() - t0) * 1e3
+                kind = "unsupported" if "Unsupported" in type(e).__name__ else "error"
+            outcomes[kind] += 1
+            by_kind[kinds[k - 1]][kind] += 1
+            times[kind].append(dt)
+    n = sum(outcomes.values())
+    hits = outcomes["hit_r1"] + outcomes["hit_r2"]
+    out = {
+        "family": family, "paths": n_paths, "path_len": path_len, "queries": n,
+        "recall": round(hits / max(n, 1), 4),
+        "hit_round1": outcomes["hit_r1"], "hit_round2_only": outcomes["hit_r2"],
+        "miss": outcomes["miss"], "refuted": outcomes["refuted"],
+        "unsupported": outcomes["unsupported"], "error": outcomes["error"],
+        "invalid_witnesses": len(bad),
+        "by_newest_constraint": {
+            k: {"n": sum(c.values()), "recall": round((c["hit_r1"] + c["hit_r2"]) /
+                                                      max(sum(c.values()), 1), 4),
+                "round2_only": c["hit_r2"], "miss": c["miss"]}
+            for k, c in sorted(by_kind.items())},
+        "ms": {k: _pct(v) for k, v in sorted(times.items())},
+    }
+    if big is not None and missed:
+        rec = 0
+        for seed, k in missed:
+            ctx, cs, m, kinds = planted_path(family, seed, path_len)
+            nodes = [c.node for c in cs]
+            try:
+                w = big.solve(ctx.b, nodes[:k])
+            except Exception:  # noqa: BLE001
+                w = None
+            rec += w is not None
+        out["extended_rows"] = big.rows
+        out["misses_recovered_by_extended"] = rec
+    return out
+
+
+def main():
+    argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+    n_paths = int(argv[0]) if argv else 100
+    path_len = int(argv[1]) if len(argv) > 1 else 24
+    fake = "--fake" in sys.argv
+    if fake:
+        import pytest
+
+        from tests import fake_device
+
+        fake_device.install(pytest.MonkeyPatch())
+    s = Sieve(rows=256) if fake else Sieve()
+    big = None
+    if "--extended" in sys.argv:
+        big = Sieve(rows=1 << 20)
+    for family in FAMILIES:
+        out = run_family(s, family, n_paths, path_len, big)
+        out["device"] = "fake (CPU)" if fake else "gpu"
+        print(json.dumps(out), flush=True)
+    s.close()
+    if big is not None:
+        big.close()
+
+
+if __name__ == "__main__":
+    main()
