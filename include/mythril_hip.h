@@ -272,9 +272,11 @@ uint64_t mh_smtlib_size(const mh_smtlib* s);  /* nodes the session mirrors      
  * 1..n_groups are the column-disjoint groups in order of their first conjunct, with n_groups == 1
  * tape 0 is the one group's.  VAR imm0 = column (0..n_columns-1), CONST imm0 = constant
  * (0..n_consts-1).  A ground query has one Bool column "__ground__" no tape reads.  flags
- * MH_QUERY_DEFINITIONS: a conjunct has the shape variable == computed term, which the host's
- * definition elimination (sieve.py eliminate_definitions) may use -- the host may discard the
- * result and take its own stages.  Constructs the lowering does not model are MH_E_UNSUPPORTED
+ * MH_QUERY_DEFINITIONS: conjuncts of the shape variable == computed term over other columns were
+ * eliminated (sieve.py eliminate_definitions): the defined variables are substituted away, the
+ * root and group tapes are the remaining conjunction's, and one more tape per definition (the
+ * last n_defs) computes the defined column's value from the witness row.  Constructs the
+ * lowering does not model are MH_E_UNSUPPORTED
  * (the query goes to z3).  A session is used by one thread at a time.                            */
 typedef struct mh_terms mh_terms;
 typedef struct mh_query mh_query;
@@ -319,7 +321,10 @@ typedef struct {
     uint32_t n_tapes, n_consts, n_columns, names_len, n_groups, n_tables, flags;
     uint32_t n_keys;                  /* entries of key_limbs                                      */
     uint32_t n_table_entries;         /* entries of table_limbs                                    */
-    uint32_t pad;
+    uint32_t n_defs;                  /* MH_QUERY_DEFINITIONS: definitions eliminated; the last
+                                         n_defs tapes are their terms, the root and group tapes
+                                         come first (n_tapes - n_defs of them)                     */
+    const uint32_t* def_cols;         /* [n_defs]: the column each definition tape's value gives   */
 } mh_query_info;
 int32_t mh_terms_create(mh_terms** out);
 int32_t mh_terms_destroy(mh_terms* t);

@@ -818,6 +818,7 @@ struct mh_query {
     std::string names;
     std::vector<uint32_t> key_limbs, group_cols, group_off, table_limbs;
     std::vector<mh_query_table> tables;
+    std::vector<uint32_t> def_cols;  // the column each definition tape (the last ones) gives
 };
 
 namespace {
@@ -1028,6 +1029,230 @@ void and_leaves(const std::vector<mh_node>& tape, uint32_t n, std::vector<uint32
     }
 }
 
+
+// The query's tapes: the root's (tape 0), then with several groups each group's AND chain over
+// the root tape's nodes (sieve.py local_tapeset(b, [root] + accs, columns))
+void emit_tapes(mh_query& q, const std::vector<mh_node>& tape,
+                const std::vector<std::vector<uint32_t>>& gconj) {
+    const uint32_t N = (uint32_t)tape.size();
+    const uint32_t G = (uint32_t)gconj.size();
+    q.nodes = tape;
+    q.tape_off = {0, N};
+    if (G <= 1) return;
+    std::vector<int32_t> remap(N, -1);
+    std::vector<uint32_t> touched;
+    std::vector<std::pair<uint32_t, bool>> s2;
+    for (uint32_t g = 0; g < G; ++g) {
+        const size_t base = q.nodes.size();
+        for (uint32_t n : touched) remap[n] = -1;
+        touched.clear();
+        int64_t acc = -1;
+        for (uint32_t cj : gconj[g]) {
+            s2.assign(1, {cj, false});
+            while (!s2.empty()) {
+                const auto [n, done] = s2.back();
+                s2.pop_back();
+                if (remap[n] >= 0) continue;
+                const mh_node& x = tape[n];
+                const int k = arity(x.op);
+                const uint32_t kids[3] = {x.a, x.b, x.c};
+                if (!done) {
+                    s2.push_back({n, true});
+                    for (int j = k - 1; j >= 0; --j)
+                        if (remap[kids[j]] < 0) s2.push_back({kids[j], false});
+                    continue;
+                }
+                mh_node y = x;
+                y.a = k > 0 ? (uint32_t)remap[x.a] : 0;
+                y.b = k > 1 ? (uint32_t)remap[x.b] : 0;
+                y.c = k > 2 ? (uint32_t)remap[x.c] : 0;
+                remap[n] = (int32_t)(q.nodes.size() - base);
+                touched.push_back(n);
+                q.nodes.push_back(y);
+            }
+            if (acc < 0) {
+                acc = remap[cj];
+                continue;
+            }
+            mh_node a{};
+            a.op = AND;
+            a.a = (uint32_t)acc;
+            a.b = (uint32_t)remap[cj];
+            acc = (int64_t)(q.nodes.size() - base);
+            q.nodes.push_back(a);
+        }
+        if ((size_t)acc != q.nodes.size() - base - 1) invalid("group tape root is not its last node");
+        q.tape_off.push_back(q.nodes.size());
+    }
+}
+
+void put_groups(mh_query& q, std::vector<std::vector<uint32_t>>& gcols) {
+    q.group_off.assign(1, 0);
+    for (auto& gc : gcols) {
+        std::sort(gc.begin(), gc.end());
+        gc.erase(std::unique(gc.begin(), gc.end()), gc.end());
+        q.group_cols.insert(q.group_cols.end(), gc.begin(), gc.end());
+        q.group_off.push_back((uint32_t)q.group_cols.size());
+    }
+}
+
+// Column-disjoint groups of `conj` on a tape (the DependenceMap; QueryState keeps the same
+// union-find incrementally): conjuncts reaching a common column-reading node are one group,
+// groups in order of their first conjunct, a ground conjunct its own group per node
+void group_conjuncts(const std::vector<mh_node>& tape, const std::vector<uint8_t>& hc,
+                     const std::vector<uint32_t>& conj,
+                     std::vector<std::vector<uint32_t>>& gconj,
+                     std::vector<std::vector<uint32_t>>& gcols) {
+    std::vector<int32_t> owner(tape.size(), -1);
+    std::vector<uint32_t> uf(conj.size());
+    auto find = [&](uint32_t x) {
+        while (uf[x] != x) x = uf[x] = uf[uf[x]];
+        return x;
+    };
+    std::vector<uint32_t> st;
+    for (uint32_t i = 0; i < conj.size(); ++i) {
+        uf[i] = i;
+        st.assign(1, conj[i]);
+        while (!st.empty()) {
+            const uint32_t n = st.back();
+            st.pop_back();
+            if (!hc[n]) continue;
+            if (owner[n] >= 0) {
+                const uint32_t a = find(i), b = find((uint32_t)owner[n]);
+                uf[std::max(a, b)] = std::min(a, b);
+                continue;
+            }
+            owner[n] = (int32_t)i;
+            const mh_node& x = tape[n];
+            const uint32_t kids[3] = {x.a, x.b, x.c};
+            for (int j = 0; j < arity(x.op); ++j) st.push_back(kids[j]);
+        }
+    }
+    std::unordered_map<int64_t, uint32_t> gid;
+    std::vector<uint32_t> group_of(conj.size(), UINT32_MAX);
+    for (uint32_t i = 0; i < conj.size(); ++i) {
+        const int64_t key = hc[conj[i]] ? (int64_t)find(i) : -(int64_t)conj[i] - 1;
+        auto it = gid.find(key);
+        if (it == gid.end()) {
+            it = gid.emplace(key, (uint32_t)gconj.size()).first;
+            gconj.emplace_back();
+        }
+        gconj[it->second].push_back(conj[i]);
+        if (key >= 0) group_of[(size_t)key] = it->second;
+    }
+    gcols.assign(gconj.size(), {});
+    for (uint32_t n = 0; n < tape.size(); ++n)
+        if (tape[n].op == VAR && owner[n] >= 0)
+            gcols[group_of[find((uint32_t)owner[n])]].push_back(tape[n].imm0);
+}
+
+// sieve.py eliminate_definitions over a copy of the root tape (the session's tape stays the
+// linearisation a LASER child extends): nodes hash-consed as in the tape, VAR imm0 = column
+struct DefTape {
+    std::vector<mh_node> t;
+    std::vector<uint8_t> hc;
+    std::unordered_map<Key, uint32_t, KeyHash> memo;
+
+    uint32_t add(mh_node y) {
+        y.flags = 0;
+        auto ins = memo.emplace(key_of(y), (uint32_t)t.size());
+        if (!ins.second) return ins.first->second;
+        uint8_t h = y.op == VAR;
+        const uint32_t kids[3] = {y.a, y.b, y.c};
+        for (int j = 0; j < arity(y.op); ++j) h |= hc[kids[j]];
+        t.push_back(y);
+        hc.push_back(h);
+        return ins.first->second;
+    }
+    // sieve.py substitute: `root` with every VAR of a column in env replaced by env's term
+    uint32_t subst(uint32_t root, const std::unordered_map<uint32_t, uint32_t>& env) {
+        std::unordered_map<uint32_t, uint32_t> out;
+        std::vector<uint32_t> st{root};
+        while (!st.empty()) {
+            const uint32_t n = st.back();
+            if (out.count(n)) {
+                st.pop_back();
+                continue;
+            }
+            const mh_node x = t[n];
+            if (x.op == VAR) {
+                auto e = env.find(x.imm0);
+                out[n] = e == env.end() ? n : e->second;
+                st.pop_back();
+                continue;
+            }
+            if (!hc[n]) {  // reads no column: itself
+                out[n] = n;
+                st.pop_back();
+                continue;
+            }
+            const int k = arity(x.op);
+            const uint32_t kids[3] = {x.a, x.b, x.c};
+            bool todo = false;
+            for (int j = 0; j < k; ++j)
+                if (!out.count(kids[j])) {
+                    st.push_back(kids[j]);
+                    todo = true;
+                }
+            if (todo) continue;
+            st.pop_back();
+            mh_node y = x;
+            uint32_t* o[3] = {&y.a, &y.b, &y.c};
+            bool same = true;
+            for (int j = 0; j < k; ++j) {
+                *o[j] = out[kids[j]];
+                same = same && *o[j] == kids[j];
+            }
+            out[n] = same ? n : add(y);
+        }
+        return out[root];
+    }
+    // the columns a term reads (lower.node_columns)
+    void reads(uint32_t root, std::vector<uint32_t>& cols) const {
+        std::vector<uint32_t> st{root};
+        std::unordered_map<uint32_t, bool> seen;
+        cols.clear();
+        while (!st.empty()) {
+            const uint32_t n = st.back();
+            st.pop_back();
+            if (!hc[n] || !seen.emplace(n, true).second) continue;
+            const mh_node& x = t[n];
+            if (x.op == VAR) {
+                cols.push_back(x.imm0);
+                continue;
+            }
+            const uint32_t kids[3] = {x.a, x.b, x.c};
+            for (int j = 0; j < arity(x.op); ++j) st.push_back(kids[j]);
+        }
+    }
+    // the nodes below `root` in post order (operands first, a before b before c), as
+    // TapeBuilder.finish / local_tapeset number them
+    void linearise(uint32_t root, std::vector<mh_node>& out, std::vector<uint8_t>* ohc) const {
+        std::unordered_map<uint32_t, uint32_t> at;
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        while (!st.empty()) {
+            const auto [n, done] = st.back();
+            st.pop_back();
+            if (at.count(n)) continue;
+            const mh_node& x = t[n];
+            const int k = arity(x.op);
+            const uint32_t kids[3] = {x.a, x.b, x.c};
+            if (!done) {
+                st.push_back({n, true});
+                for (int j = k - 1; j >= 0; --j)
+                    if (!at.count(kids[j])) st.push_back({kids[j], false});
+                continue;
+            }
+            mh_node y = x;
+            uint32_t* o[3] = {&y.a, &y.b, &y.c};
+            for (int j = 0; j < 3; ++j) *o[j] = j < k ? at.at(kids[j]) : 0;
+            at.emplace(n, (uint32_t)out.size());
+            out.push_back(y);
+            if (ohc) ohc->push_back(hc[n]);
+        }
+    }
+};
+
 // Harvest tables compared before and after a new constraint (lower.py Harvest.fingerprint)
 struct Fingerprint {
     Tables cells, uf_cells;
@@ -1123,6 +1348,7 @@ private:
         while (uf[x] != x) x = uf[x] = uf[uf[x]];
         return x;
     }
+    bool emit_definitions(mh_query& q);
 
     uint32_t root = 0;            // node id of the lowered conjunction
     std::vector<uint32_t> conj;   // its AND leaves (tape nodes), in order
@@ -1138,75 +1364,29 @@ void QueryState::emit(mh_query& q, uint32_t& flags) {
     for (const Column& c : Q.cols)  // a variable named like a cell would make two columns one
         if (c.kind == MH_COL_VAR && Q.cell_index.count(c.name))
             unsupported("variable " + c.name + " is named like an array cell");
-    if (defines) flags |= MH_QUERY_DEFINITIONS;
     if (refuted(Q, conj)) flags |= MH_QUERY_REFUTED;
-    std::vector<std::vector<uint32_t>> gconj;  // conjunct tape nodes per group, path order
-    std::unordered_map<int64_t, uint32_t> gid;
-    std::vector<uint32_t> group_of(conj.size(), UINT32_MAX);  // by union-find root
-    for (uint32_t i = 0; i < conj.size(); ++i) {
-        const int64_t key = Q.has_col[conj[i]] ? (int64_t)find(i) : -(int64_t)conj[i] - 1;
-        auto it = gid.find(key);
-        if (it == gid.end()) {
-            it = gid.emplace(key, (uint32_t)gconj.size()).first;
-            gconj.emplace_back();
-        }
-        gconj[it->second].push_back(conj[i]);
-        if (key >= 0) group_of[(size_t)key] = it->second;
-    }
-    const uint32_t G = (uint32_t)gconj.size();
-    std::vector<std::vector<uint32_t>> gcols(G);
-    for (uint32_t n = 0; n < N; ++n)
-        if (tape[n].op == VAR && owner[n] >= 0)
-            gcols[group_of[find((uint32_t)owner[n])]].push_back(tape[n].imm0);
-    // tapes: the root's, then (more than one group) each group's AND chain over the root's nodes
-    q.nodes = tape;
-    q.tape_off = {0, N};
-    if (G > 1) {
-        std::vector<int32_t> remap(N, -1);
-        std::vector<uint32_t> touched;
-        std::vector<std::pair<uint32_t, bool>> s2;
-        for (uint32_t g = 0; g < G; ++g) {
-            const size_t base = q.nodes.size();
-            for (uint32_t n : touched) remap[n] = -1;
-            touched.clear();
-            int64_t acc = -1;
-            for (uint32_t cj : gconj[g]) {
-                s2.assign(1, {cj, false});
-                while (!s2.empty()) {
-                    const auto [n, done] = s2.back();
-                    s2.pop_back();
-                    if (remap[n] >= 0) continue;
-                    const mh_node& x = tape[n];
-                    const int k = arity(x.op);
-                    const uint32_t kids[3] = {x.a, x.b, x.c};
-                    if (!done) {
-                        s2.push_back({n, true});
-                        for (int j = k - 1; j >= 0; --j)
-                            if (remap[kids[j]] < 0) s2.push_back({kids[j], false});
-                        continue;
-                    }
-                    mh_node y = x;
-                    y.a = k > 0 ? (uint32_t)remap[x.a] : 0;
-                    y.b = k > 1 ? (uint32_t)remap[x.b] : 0;
-                    y.c = k > 2 ? (uint32_t)remap[x.c] : 0;
-                    remap[n] = (int32_t)(q.nodes.size() - base);
-                    touched.push_back(n);
-                    q.nodes.push_back(y);
-                }
-                if (acc < 0) {
-                    acc = remap[cj];
-                    continue;
-                }
-                mh_node a{};
-                a.op = AND;
-                a.a = (uint32_t)acc;
-                a.b = (uint32_t)remap[cj];
-                acc = (int64_t)(q.nodes.size() - base);
-                q.nodes.push_back(a);
+    if (defines && emit_definitions(q)) {
+        flags |= MH_QUERY_DEFINITIONS;
+    } else {
+        std::vector<std::vector<uint32_t>> gconj;  // conjunct tape nodes per group, path order
+        std::unordered_map<int64_t, uint32_t> gid;
+        std::vector<uint32_t> group_of(conj.size(), UINT32_MAX);  // by union-find root
+        for (uint32_t i = 0; i < conj.size(); ++i) {
+            const int64_t key = Q.has_col[conj[i]] ? (int64_t)find(i) : -(int64_t)conj[i] - 1;
+            auto it = gid.find(key);
+            if (it == gid.end()) {
+                it = gid.emplace(key, (uint32_t)gconj.size()).first;
+                gconj.emplace_back();
             }
-            if ((size_t)acc != q.nodes.size() - base - 1) invalid("group tape root is not its last node");
-            q.tape_off.push_back(q.nodes.size());
+            gconj[it->second].push_back(conj[i]);
+            if (key >= 0) group_of[(size_t)key] = it->second;
         }
+        std::vector<std::vector<uint32_t>> gcols(gconj.size());
+        for (uint32_t n = 0; n < N; ++n)
+            if (tape[n].op == VAR && owner[n] >= 0)
+                gcols[group_of[find((uint32_t)owner[n])]].push_back(tape[n].imm0);
+        emit_tapes(q, tape, gconj);
+        put_groups(q, gcols);
     }
     for (const Big& v : Q.qpool) put_big(q.consts, v);
     if (Q.qpool.empty()) put_big(q.consts, Big());
@@ -1224,13 +1404,6 @@ void QueryState::emit(mh_query& q, uint32_t& flags) {
         mc.key_off = c.has_key ? (uint32_t)(q.key_limbs.size() / NL) : UINT32_MAX;
         if (c.has_key) put_key(q.key_limbs, c.key);
         q.columns.push_back(mc);
-    }
-    q.group_off.push_back(0);
-    for (auto& gc : gcols) {
-        std::sort(gc.begin(), gc.end());
-        gc.erase(std::unique(gc.begin(), gc.end()), gc.end());
-        q.group_cols.insert(q.group_cols.end(), gc.begin(), gc.end());
-        q.group_off.push_back((uint32_t)q.group_cols.size());
     }
     // the schema's tables: every harvested key (read or not), keccak bases and pairs
     for (int t = 0; t < 2; ++t)
@@ -1258,6 +1431,77 @@ void QueryState::emit(mh_query& q, uint32_t& flags) {
         }
         q.tables.push_back(tb);
     }
+}
+
+// sieve.py solve_definitions / eliminate_definitions, natively: a conjunct
+// `v == t` with a plain variable v on one side and a computed term t over other columns on the
+// other (not a constant, not a symbol: the guide proposes those) defines v; it is dropped and v
+// replaced by t in every other conjunct, definitions kept closed (every defining term reads
+// undefined columns only).  The remaining conjunction is the query's root, grouped afresh; one
+// tape per definition follows the group tapes, whose value under the witness row is v's.
+// Equisatisfiable: a row satisfying the rest extends to a model with v = t(row).  false: no
+// conjunct defines anything (the query is emitted as it is).
+bool QueryState::emit_definitions(mh_query& q) {
+    DefTape D{Q.tape, Q.has_col, Q.tape_memo};
+    std::unordered_map<uint32_t, uint32_t> env;  // column -> defining term
+    std::vector<uint32_t> def_cols, rest, rd;
+    for (uint32_t cn : conj) {
+        const mh_node x = D.t[cn];
+        bool done = false;
+        if (x.op == EQ) {
+            const uint32_t sides[2][2] = {{x.a, x.b}, {x.b, x.a}};
+            for (const auto& sd : sides) {
+                const mh_node v = D.t[sd[0]];
+                if (v.op != VAR || Q.cols.at(v.imm0).kind != MH_COL_VAR || env.count(v.imm0))
+                    continue;
+                const uint8_t top = D.t[sd[1]].op;
+                if (top == VAR || top == CONST) continue;
+                const uint32_t t2 = env.empty() ? sd[1] : D.subst(sd[1], env);
+                D.reads(t2, rd);
+                if (rd.empty() || std::find(rd.begin(), rd.end(), v.imm0) != rd.end()) continue;
+                const std::unordered_map<uint32_t, uint32_t> one{{v.imm0, t2}};
+                for (auto& e : env) e.second = D.subst(e.second, one);
+                env[v.imm0] = t2;
+                def_cols.push_back(v.imm0);
+                done = true;
+                break;
+            }
+        }
+        if (!done) rest.push_back(cn);
+    }
+    if (env.empty()) return false;
+    uint32_t r;
+    if (rest.empty()) {
+        mh_node t{};
+        t.op = TRUE_;
+        r = D.add(t);
+    } else {
+        r = D.subst(rest[0], env);
+        for (size_t i = 1; i < rest.size(); ++i) {
+            mh_node a{};
+            a.op = AND;
+            a.a = r;
+            a.b = D.subst(rest[i], env);
+            r = D.add(a);
+        }
+    }
+    std::vector<mh_node> tape;
+    std::vector<uint8_t> hc;
+    D.linearise(r, tape, &hc);
+    std::vector<uint32_t> leaves;
+    and_leaves(tape, (uint32_t)tape.size() - 1, leaves);
+    std::vector<std::vector<uint32_t>> gconj, gcols;
+    group_conjuncts(tape, hc, leaves, gconj, gcols);
+    emit_tapes(q, tape, gconj);
+    put_groups(q, gcols);
+    for (uint32_t c : def_cols) {  // the definitions' tapes, in definition order
+        std::vector<mh_node> dt;
+        D.linearise(env.at(c), dt, nullptr);
+        q.nodes.insert(q.nodes.end(), dt.begin(), dt.end());
+        q.tape_off.push_back(q.nodes.size());
+        q.def_cols.push_back(c);
+    }
+    return true;
 }
 
 extern "C" {
@@ -1396,6 +1640,8 @@ int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_
     info->flags = flags;
     info->n_keys = (uint32_t)(r->key_limbs.size() / NL);
     info->n_table_entries = (uint32_t)(r->table_limbs.size() / NL);
+    info->n_defs = (uint32_t)r->def_cols.size();
+    info->def_cols = r->def_cols.data();
     *out = r;
     return MH_OK;
 }

@@ -441,7 +441,7 @@ class QueryInfo(C.Structure):
                 ("n_tapes", C.c_uint32), ("n_consts", C.c_uint32), ("n_columns", C.c_uint32),
                 ("names_len", C.c_uint32), ("n_groups", C.c_uint32), ("n_tables", C.c_uint32),
                 ("flags", C.c_uint32), ("n_keys", C.c_uint32), ("n_table_entries", C.c_uint32),
-                ("pad", C.c_uint32)]
+                ("n_defs", C.c_uint32), ("def_cols", _u32p)]
 
 
 class CompiledQuery:
@@ -452,17 +452,22 @@ class CompiledQuery:
     when a model is evaluated, mythril/laser/smt/model.py:45-59)."""
 
     __slots__ = ("tapes", "consts", "names", "widths", "groups", "flags", "nodes", "tape_off",
-                 "_raw", "_columns", "_tables")
+                 "defs", "def_tapes", "_raw", "_columns", "_tables")
 
     def __init__(self, info: QueryInfo):
         def raw(p, nbytes):
             return C.string_at(p, nbytes) if nbytes else b""
 
-        nt = info.n_tapes
-        off = np.frombuffer(raw(info.tape_off, 8 * (nt + 1)), dtype=np.uint64).tolist()
+        nd = info.n_defs
+        nt = info.n_tapes - nd  # the root and group tapes; the definitions' tapes follow
+        off = np.frombuffer(raw(info.tape_off, 8 * (info.n_tapes + 1)),
+                            dtype=np.uint64).tolist()
         nodes = np.frombuffer(raw(info.nodes, 24 * off[-1]), dtype=NODE_DTYPE)
-        self.nodes, self.tape_off = nodes, off  # every tape back to back
+        self.nodes, self.tape_off = nodes, off[:nt + 1]  # root and group tapes back to back
         self.tapes = [nodes[off[i]:off[i + 1]] for i in range(nt)]
+        # MH_QUERY_DEFINITIONS: column index of each defined symbol, and the tape of its term
+        self.defs = np.frombuffer(raw(info.def_cols, 4 * nd), dtype=np.uint32).tolist()
+        self.def_tapes = [nodes[off[nt + i]:off[nt + i + 1]] for i in range(nd)]
         self.consts = np.frombuffer(raw(info.consts, 32 * info.n_consts),
                                     dtype=np.uint32).reshape(-1, 8)
         names = raw(info.names, info.names_len).decode()

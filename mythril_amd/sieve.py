@@ -122,6 +122,15 @@ def local_tapeset(b: TapeBuilder, roots: Sequence[int], columns: Sequence[str]) 
 REFUTED = object()  # _host_native's answer for a query that contradicts itself
 
 
+class NativeDefs(list):
+    """The definitions the native query compiler eliminated (MH_QUERY_DEFINITIONS):
+    [(column, tape of its defining term)] over the query's columns and constants ``consts``."""
+
+    def __init__(self, items, consts):
+        super().__init__(items)
+        self.consts = consts
+
+
 class NativeSchema(Schema):
     """The Schema of a query the native compiler built, decoded on first use: a witness's
     schema is read only when a model is evaluated (mythril/laser/smt/model.py:45-59, model.py
@@ -516,7 +525,23 @@ class Sieve:
                    values: Dict[str, int]) -> List[int]:
         """The values of `terms` (bit-vector or Bool nodes over `columns`) under one assignment,
         evaluated on the device (mh_eval_values over a one-row buffer)."""
-        ts = local_tapeset(b, terms, columns)
+        return self.eval_tapeset(local_tapeset(b, terms, columns), columns, values)
+
+    def eval_definitions(self, b: TapeBuilder, defs, columns: Sequence[str],
+                         values: Dict[str, int]) -> List[int]:
+        """The defined columns' values under the witness row: the native compiler's definition
+        tapes (NativeDefs), or the Python stages' terms."""
+        if isinstance(defs, NativeDefs):
+            ts = TapeSet(columns)
+            ts.pool = LocalPool(defs.consts)
+            ts.tapes = [Tape(t) for _, t in defs]
+            return self.eval_tapeset(ts, columns, values)
+        return self.eval_terms(b, [t for _, t in defs], columns, values)
+
+    def eval_tapeset(self, ts: TapeSet, columns: Sequence[str],
+                     values: Dict[str, int]) -> List[int]:
+        """The root values of every tape of `ts` under one assignment of `columns`."""
+        terms = ts.tapes
         ct = self.compile(ts)
         try:
             assign = self.ctx.assignments(len(columns), 1)
@@ -554,10 +579,12 @@ class Sieve:
         if cq.flags & native.QUERY_REFUTED:
             st.extra["refuted"] = st.extra.get("refuted", 0) + 1
             return REFUTED
-        if cq.flags & native.QUERY_DEFINITIONS:
-            st.extra["host_python"] = st.extra.get("host_python", 0) + 1
-            return None
         columns = cq.names
+        defs = []
+        if cq.flags & native.QUERY_DEFINITIONS:  # solved for the defined symbols natively
+            st.extra["definitions"] = st.extra.get("definitions", 0) + len(cq.defs)
+            defs = NativeDefs([(columns[c], t) for c, t in zip(cq.defs, cq.def_tapes)],
+                              cq.consts)
         ts = TapeSet(columns)
         ts.pool = LocalPool(cq.consts)
         tapes = cq.tapes
@@ -568,7 +595,7 @@ class Sieve:
         ts.flat = (cq.nodes[cq.tape_off[k]:cq.tape_off[-1]], off - off[0], cq.consts)
         if len(cq.groups) > 1:
             st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
-        return columns, cq.widths, NativeSchema(cq), tapes[0], ts, cq.groups, []
+        return columns, cq.widths, NativeSchema(cq), tapes[0], ts, cq.groups, defs
 
     def _host_python(self, b: TapeBuilder, roots: Sequence[int]):
         """The host stages in Python: lower_query, definitions, buckets, local tapes."""
@@ -694,7 +721,7 @@ class Sieve:
                         values.setdefault(c, 0)
                     if defs:  # defined symbols take their terms' values under the row
                         td = time.perf_counter()
-                        got = self.eval_terms(b, [t for _, t in defs], columns, values)
+                        got = self.eval_definitions(b, defs, columns, values)
                         for (c, _), v in zip(defs, got):
                             values[c] = v
                         st.add("definitions", time.perf_counter() - td)

@@ -39,17 +39,24 @@ def _values(rows):
 
 
 def python_stages(b, roots):
+    """The Python host stages of Sieve._host_python: lowering, definitions (solved for and
+    substituted away, Sieve.solve_definitions), groups, the root tape."""
     root, schema = lower_query(b, roots)
     cols = list(schema.columns) or ["__ground__"]
+    rest, defs = eliminate_definitions(b, Sieve.conjuncts(b, root), schema)
+    if defs:
+        root = rest[0] if rest else b.true()
+        for x in rest[1:]:
+            root = b.op(Op.AND, root, x)
     groups = Sieve.buckets(b, root)
     names = {b.var_index[c]: c for c in cols if c in b.var_index}
     ts = local_tapeset(b, [root], cols)
-    return root, schema, cols, groups, names, ts
+    return root, schema, cols, groups, names, ts, defs
 
 
 def check_query(b, roots, label):
     try:
-        root, schema, cols, groups, names, ts = python_stages(b, roots)
+        root, schema, cols, groups, names, ts, defs = python_stages(b, roots)
     except LoweringUnsupported:
         with pytest.raises(native.Unsupported):
             native.TermMirror.of(b).build(b, roots)
@@ -90,10 +97,14 @@ def check_query(b, roots, label):
             assert canon(t, ncols, _values(cq.consts)) == canon(gt.nodes, cols, pool), label
     else:
         assert len(cq.tapes) == 1, label
-    # a query the Python stages would eliminate a definition in is flagged
-    _, defs = eliminate_definitions(b, Sieve.conjuncts(b, root), schema)
+    # definitions: the same symbols solved for, in the same order, by the same terms
+    assert bool(cq.flags & native.QUERY_DEFINITIONS) == bool(defs), label
+    assert [ncols[c] for c in cq.defs] == [c for c, _ in defs], label
     if defs:
-        assert cq.flags & native.QUERY_DEFINITIONS, label
+        dts = local_tapeset(b, [t for _, t in defs], cols)
+        pool = _values(dts.pool.to_array())
+        for t, dt in zip(cq.def_tapes, dts.tapes):
+            assert canon(t, ncols, _values(cq.consts)) == canon(dt.nodes, cols, pool), label
     return cq
 
 
@@ -492,3 +503,38 @@ def test_builder_packed_nodes_match_the_node_list():
         want = np.array([(n[0], f, n[1], n[2], n[3], n[4], n[5], n[6])
                          for n, f in zip(b.nodes, b.flags)], dtype=NODE_DTYPE)
         assert (got == want).all()
+
+
+def test_definitions_are_solved_natively():
+    """Definitions eliminated by the native compiler: a chain of them kept
+    closed, a query that is nothing but definitions (TRUE root), the keccak_other_num shape, in
+    LASER order -- each equal to the Python stages (check_query), and the defined column's tape
+    evaluates, under a row satisfying the rest, to a value that satisfies the whole query."""
+    from mythril_amd import smt
+    from mythril_amd.smt import ULT, symbol_factory
+    from oracle import smt_eval as E
+
+    ctx = smt.set_context(smt.Context())
+    v = symbol_factory.BitVecVal
+    a, b_, c, d = (symbol_factory.BitVecSym(n, 256) for n in "abcd")
+    cs = [b_ == a * v(3, 256) + v(1, 256),       # b := 3a + 1
+          c == b_ + a,                            # c := b + a, closed: 4a + 1
+          ULT(a, v(1000, 256)),
+          d == c * c]                             # d := (4a + 1)^2
+    nodes = [x.node for x in cs]
+    seen_defs = []
+    for k in range(1, len(nodes) + 1):
+        cq = check_query(ctx.b, nodes[:k], ("chain", k))
+        seen_defs.append(len(cq.defs))
+    assert seen_defs == [1, 2, 2, 3]
+    ncols = cq.names
+    assert sorted(ncols[c] for c in cq.defs) == ["b", "c", "d"]
+    # the remaining root reads only a; evaluate the definitions at a = 5
+    row = [5 if n == "a" else 0 for n in ncols]
+    consts = _values(cq.consts)
+    got = {ncols[c]: E.evaluate(t, consts, row) for c, t in zip(cq.defs, cq.def_tapes)}
+    assert got == {"b": 16, "c": 21, "d": 441}
+    # nothing but definitions: the root is TRUE, one ground group
+    cq = check_query(ctx.b, [nodes[0]], "one")
+    assert cq.flags & native.QUERY_DEFINITIONS and len(cq.tapes) == 1
+    assert int(cq.tapes[0]["op"][-1]) == int(Op.TRUE)
