@@ -135,9 +135,33 @@ def planted_random(rng: random.Random, n: int):
     ftab = {k: _draw256(rng) for k in keys if rng.random() < 0.5}
     fels = _draw256(rng)
     m.funcs["f"] = lambda x: ftab.get(x, fels)
-    kec = Function("keccak256_256", 256, 256)
-    inv = Function("keccak256_256-1", 256, 256)
-    _keccak_pair(m, "keccak256_256", 32, _real_keccak(32))
+    # keccak as LASER builds it: every application through the keccak manager, whose condition
+    # (interval / mod 64 / inverse, or a remembered concrete pair) joins the path before the
+    # constraint that uses it (keccak_function_manager.py:83-149).  M: the real hash on the keys
+    # the family hashes concretely, the manager's interval elsewhere (a multiple of 64)
+    km = L.KeccakManager()
+    km.functions(256)
+    real = _real_keccak(32)
+    keyset = set(keys)
+
+    fixed: Dict[int, int] = {}  # M is a function: a point's value never changes once read
+
+    def kimage(x):
+        if x not in fixed:
+            if x in keyset or (x, 256) in km.concrete or 256 not in km.hooks:
+                fixed[x] = real(x)
+            else:
+                fixed[x] = km.hooks[256] * L.PART + ((real(x) >> 139) << 6)
+        return fixed[x]
+
+    _keccak_pair(m, "keccak256_256", 32, kimage)
+    pending: List[smt.Bool] = []
+
+    def kec(t):
+        h, cond = km.create(t)
+        pending.append(cond)
+        return h
+
     kv = [BVV(k, 256) for k in keys]
 
     def term(d=0):
@@ -150,15 +174,24 @@ def planted_random(rng: random.Random, n: int):
             return smt.ZeroExt(248, a[idx]) if a.range == 8 else a[idx]
         if r < 0.55:
             return f(rng.choice(kv) if rng.random() < 0.5 else term(d + 1))
-        if r < 0.65:
-            return kec(term(d + 1))
         if r < 0.7:
-            return inv(kec(term(d + 1)))
+            return kec(term(d + 1))
         if r < 0.85:
             return term(d + 1) + term(d + 1)
         return If(ULT(term(d + 1), term(d + 1)), term(d + 1), term(d + 1))
 
     p = _Path(ctx, m)
+
+    class _Keccak(_Path):  # the manager's conditions first, then the constraint
+        def add(self, c):
+            kind, self.kind = self.kind, "keccak_cond"
+            for x in pending:
+                _Path.add(self, x)
+            pending.clear()
+            self.kind = kind
+            _Path.add(self, c)
+
+    p.__class__ = _Keccak
     for _ in range(n):
         r = rng.random()
         if r < 0.1:  # a store into the free array, read back
