@@ -21,7 +21,7 @@ from __future__ import annotations
 from typing import TYPE_CHECKING, List, Optional, Union
 
 from .lower import Schema
-from .tape import BOOL, Op
+from .tape import BOOL, Op, TapeError
 
 if TYPE_CHECKING:  # pragma: no cover
     from .sieve import Sieve
@@ -219,9 +219,9 @@ class Model:
         if width == BOOL or width <= SLICE:
             v = self.sieve.eval_terms(b, [root], columns, self.values)[0]
             return bool(v) if width == BOOL else BitVecValue(v, width)
-        # wider than one device evaluation: 256-bit slices of the lowered term, low first
-        roots = [b.op(Op.EXTRACT, root, imm0=min(lo + SLICE, width) - 1, imm1=lo)
-                 for lo in range(0, width, SLICE)]
+        # wider than the device's 256-bit operations: the lowered term rewritten as terms of its
+        # 256-bit slices (Slicer), every slice evaluated on the device, low first
+        roots = Slicer(b).slices(root)
         parts = self.sieve.eval_terms(b, roots, columns, self.values)
         return BitVecValue(sum(int(p) << (SLICE * i) for i, p in enumerate(parts)), width)
 
@@ -236,3 +236,140 @@ def lower_query_value(b, node: int, frozen: Schema):
     schema = deepcopy(frozen)
     L = Lowering(b, schema)
     return L.lower(node), schema
+
+
+class Slicer:
+    """A term wider than 256 bits as the list of its 256-bit slices (low first; the last one
+    ``width % 256`` bits when that is not 0), each a term of at most 256 bits the device
+    evaluates: concatenation, extraction, zero / sign extension, ITE and the bitwise ops split
+    per slice; addition, subtraction and negation carry between slices through 256-bit
+    compares.  Any other operator wider than 256 bits raises TapeError (Model.eval of such a
+    term is not supported)."""
+
+    def __init__(self, b):
+        self.b = b
+        self.memo = {}
+
+    def _widths(self, w):
+        return [min(SLICE, w - lo) for lo in range(0, w, SLICE)]
+
+    def bits(self, sl, lo: int, hi: int) -> int:
+        """A term of bits [lo, hi) (hi - lo <= 256) of the value whose slices are `sl`."""
+        b = self.b
+        parts = []  # high first, for CONCAT
+        pos = lo
+        while pos < hi:
+            k = pos // SLICE
+            top = min(hi, (k + 1) * SLICE)
+            x = sl[k]
+            a, z = pos - k * SLICE, top - k * SLICE  # bits [a, z) of slice k
+            if a == 0 and z == b.width(x):
+                parts.append(x)
+            else:
+                parts.append(b.op(Op.EXTRACT, x, imm0=z - 1, imm1=a))
+            pos = top
+        out = parts[0]
+        for x in parts[1:]:
+            out = b.op(Op.CONCAT, x, out)
+        return out
+
+    def _pack(self, pieces):
+        """Slices of the concatenation of `pieces` [(term, width)] given low first."""
+        b = self.b
+        total = sum(w for _, w in pieces)
+        # one list of <= 256-bit parts with their bit offsets, then regrouped into slices
+        sl, offs = [], []
+        pos = 0
+        for t, w in pieces:
+            for part, pw in zip(self.slices(t) if w > SLICE else [t], self._widths(w)):
+                sl.append(part)
+                offs.append((pos, pw))
+                pos += pw
+        out = []
+        for lo in range(0, total, SLICE):
+            hi = min(total, lo + SLICE)
+            chunk = []
+            for part, (o, pw) in zip(sl, offs):
+                a, z = max(lo, o), min(hi, o + pw)
+                if a < z:
+                    chunk.append(part if (a, z) == (o, o + pw) else
+                                 b.op(Op.EXTRACT, part, imm0=z - o - 1, imm1=a - o))
+            acc = chunk[0]
+            for x in chunk[1:]:
+                acc = b.op(Op.CONCAT, x, acc)
+            out.append(acc)
+        return out
+
+    def slices(self, n: int):
+        got = self.memo.get(n)
+        if got is not None:
+            return got
+        b = self.b
+        w = b.width(n)
+        if w <= SLICE:
+            out = [n]
+        else:
+            op, _, a, bb, c, i0, i1 = b.nodes[n]
+            op = Op(op)
+            cv = b.const_value(n)
+            if cv is not None:
+                out = [b.const((cv >> lo) & ((1 << sw) - 1), sw)
+                       for lo, sw in zip(range(0, w, SLICE), self._widths(w))]
+            elif op == Op.CONCAT:  # a high, bb low
+                out = self._pack([(bb, b.width(bb)), (a, b.width(a))])
+            elif op == Op.ZEXT:
+                out = self._pack([(a, b.width(a)), (b.const(0, i0), i0)] if i0 <= SLICE else
+                                 [(a, b.width(a))] + [(b.const(0, sw), sw) for sw in
+                                                      self._widths(i0)])
+            elif op == Op.SEXT:
+                wa = b.width(a)
+                sign = b.op(Op.EQ, b.op(Op.EXTRACT, self.bits(self.slices(a), wa - 1, wa)
+                                        if wa > SLICE else a, imm0=0, imm1=0)
+                            if wa > SLICE else b.op(Op.EXTRACT, a, imm0=wa - 1, imm1=wa - 1),
+                            b.const(1, 1))
+                fill = [(b.op(Op.ITE, sign, b.const((1 << sw) - 1, sw), b.const(0, sw)), sw)
+                        for sw in self._widths(i0)]
+                out = self._pack([(a, wa)] + fill)
+            elif op == Op.EXTRACT:
+                src = self.slices(a)
+                out = [self.bits(src, i1 + lo, i1 + lo + sw)
+                       for lo, sw in zip(range(0, w, SLICE), self._widths(w))]
+            elif op in (Op.BVAND, Op.BVOR, Op.BVXOR):
+                out = [b.op(op, x, y) for x, y in zip(self.slices(a), self.slices(bb))]
+            elif op == Op.BVNOT:
+                out = [b.op(op, x) for x in self.slices(a)]
+            elif op == Op.ITE:
+                out = [b.op(Op.ITE, a, x, y) for x, y in zip(self.slices(bb), self.slices(c))]
+            elif op in (Op.BVADD, Op.BVSUB, Op.BVNEG):
+                xs = self.slices(a)
+                ys = self.slices(bb) if op != Op.BVNEG else \
+                    [b.const(0, sw) for sw in self._widths(w)]
+                if op == Op.BVNEG:
+                    xs, ys = ys, xs
+                out = self._carry_chain(xs, ys, op == Op.BVADD)
+            else:
+                raise TapeError("Model.eval: %s wider than 256 bits (%d) is not supported"
+                                % (op.name, w))
+        self.memo[n] = out
+        return out
+
+    def _carry_chain(self, xs, ys, add: bool):
+        """x + y (add) or x - y, slice by slice; the carry / borrow into slice k as a 0/1 term."""
+        b = self.b
+        out = []
+        carry = None  # Bool node: a carry (borrow) into the current slice
+        for x, y in zip(xs, ys):
+            sw = b.width(x)
+            one, zero = b.const(1, sw), b.const(0, sw)
+            t = b.op(Op.BVADD if add else Op.BVSUB, x, y)
+            c1 = b.op(Op.BVULT, t, x) if add else b.op(Op.BVULT, x, y)
+            if carry is None:
+                out.append(t)
+                carry = c1
+                continue
+            cin = b.op(Op.ITE, carry, one, zero)
+            s = b.op(Op.BVADD if add else Op.BVSUB, t, cin)
+            c2 = b.op(Op.BVULT, s, t) if add else b.op(Op.BVULT, t, cin)
+            out.append(s)
+            carry = b.op(Op.OR, c1, c2)
+        return out

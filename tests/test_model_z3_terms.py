@@ -225,3 +225,41 @@ def test_model_interps_of_arrays_and_functions(monkeypatch, z3_world):
 def test_reference_reads_on_gpu(gpu_ctx, z3_world):
     frontend.configure(rows=256)
     check_reference_reads(*laser_query())
+
+
+def test_wide_terms_are_sliced_for_the_device():
+    """Model.eval of a term wider than 256 bits: Slicer rewrites it as terms of its 256-bit slices
+    (no device operation wider than 256 bits); their values, joined, equal the ORACLE's value of
+    the wide term -- carries across slices, unaligned concatenation and extraction, extensions."""
+    import random
+
+    from mythril_amd.model import Slicer
+    from mythril_amd.smt import Extract, SignExt, ZeroExt
+    from oracle import smt_eval as E
+
+    ctx = smt.set_context(smt.Context())
+    b = ctx.b
+    x, y = symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecSym("y", 256)
+    z = symbol_factory.BitVecSym("z", 40)
+    terms = [ZeroExt(1, x) + ZeroExt(1, y), Concat(x, y), Concat(z, x, y),
+             ZeroExt(256, x) - ZeroExt(256, y), Extract(300, 20, Concat(z, x, y)),
+             SignExt(100, x) + Concat(Extract(59, 0, y), z, x), -(ZeroExt(8, x)),
+             Concat(x, y) ^ Concat(y, x), smt.If(x == y, Concat(x, y), Concat(y, x)),
+             SignExt(280, z) + ZeroExt(280, z)]
+    names = [n for n, _ in sorted(b.var_index.items(), key=lambda kv: kv[1])]
+    rng = random.Random(1)
+    for t in terms:
+        sl = Slicer(b).slices(t.node)
+        assert all(b.width(s) <= 256 for s in sl)
+        assert sum(b.width(s) for s in sl) == b.width(t.node)
+        for _ in range(16):
+            vals = {"x": rng.getrandbits(256), "y": rng.getrandbits(256), "z": rng.getrandbits(40)}
+            if rng.random() < 0.25:
+                vals["y"] = vals["x"]
+            row = [vals[n] for n in names]
+            want = E.evaluate(b.finish(t.node).nodes, b.pool.values, row)
+            got = sum(E.evaluate(b.finish(s).nodes, b.pool.values, row) << (256 * i)
+                      for i, s in enumerate(sl))
+            assert got == want, t.node
+    with pytest.raises(smt.TapeError if hasattr(smt, "TapeError") else Exception):
+        Slicer(b).slices((ZeroExt(256, x) * ZeroExt(256, y)).node)
