@@ -417,7 +417,7 @@ class Sieve:
 
     def __init__(self, device: int = 0, rows: int = 1 << 16, max_rounds: int = 2,
                  seed: int = 0x5EED5EED, budget_s: float = 0.25, first_rows: int = 256,
-                 native_query: bool = True):
+                 native_query: bool = True, second_round: Optional[str] = None):
         self.ctx = native.Context(device)
         # host stages by the native query compiler (csrc/query.cpp); False: the Python stages
         # (lower.py, buckets, local_tapeset) it is checked against (tests/test_query_native.py)
@@ -434,6 +434,16 @@ class Sieve:
         # (profiles/r03f: three such rounds took 1.6-2.3 ms) while no LASER-shaped SAT query
         # needed more than the first 256 rows
         self.max_rounds = max_rounds
+        # when the rounds after the first run (SIEVE_ROUND2 overrides): "always"; "progress" --
+        # only when the first round solved some of the query's groups but not all (a query
+        # whose first round found nothing at all is left to the fallback at once); "never"
+        import os
+
+        self.second_round = second_round or os.environ.get("SIEVE_ROUND2", "always")
+        if self.second_round not in ("always", "progress", "never"):
+            raise ValueError("second_round must be always / progress / never")
+        # the last solve's rounds (diagnostics: scripts/planted_recall.py)
+        self.last_rounds: Dict[str, int] = {}
         self.seed = seed
         self.budget_s = budget_s
         self.assign: Optional[native.Assignments] = None
@@ -652,6 +662,7 @@ class Sieve:
         t0 = time.perf_counter()
         budget = self.budget_s if budget_s is None else min(self.budget_s, budget_s)
         self.stats.queries += 1
+        self.last_rounds = {}
         if budget <= 0:
             self.stats.misses += 1
             return None
@@ -689,7 +700,17 @@ class Sieve:
             launches = [self.first_rows]
             if self.max_rounds > 1:
                 launches.append((self.max_rounds - 1) * self.rows)
+            self.last_rounds = {"groups": len(group_cols), "r1_solved": 0, "rounds": 0}
             for rnd, n in enumerate(launches):
+                if rnd == 1:
+                    k = sum(solved)
+                    self.last_rounds["r1_solved"] = k
+                    if self.second_round == "never" or (self.second_round == "progress"
+                                                        and k == 0):
+                        self.stats.extra["round2_skipped"] = \
+                            self.stats.extra.get("round2_skipped", 0) + 1
+                        break
+                self.last_rounds["rounds"] = rnd + 1
                 base = (self.stats.queries << 24) + offset
                 offset += n
                 tb = time.perf_counter()

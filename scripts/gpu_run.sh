@@ -23,6 +23,8 @@
 #   qprofile  rocprofv3 kernel trace + stats of one pass of sieve_queries.py (query-path kernels)
 #   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
 #   recall    scripts/planted_recall.py (recall on planted-SAT paths, per round and shape class)
+#   round2    planted_recall and path_scaling with the second round gated on first-round progress
+#             (SIEVE_ROUND2=progress) and never run (recall only)
 #   occupancy bench.py at 168 and 256 VGPRs (3 and 2 waves per SIMD; the LDS-resident compaction
 #             design of DESIGN §10 needs one of them)
 set -o pipefail
@@ -61,6 +63,9 @@ for step in "$@"; do
     recall)   timeout -k 10 900 python -u scripts/planted_recall.py 100 24 --extended > "$OUT/planted_recall.jsonl" 2> "$OUT/planted_recall.log" ;;
     occupancy) MH_JIT_PAD_VGPR=168 timeout -k 10 400 python -u bench.py --no-companion --no-cpu-baseline --steps 2 > "$OUT/bench_vgpr168.json" 2> "$OUT/bench_vgpr168.log" && \
               MH_JIT_PAD_VGPR=256 timeout -k 10 400 python -u bench.py --no-companion --no-cpu-baseline --steps 2 > "$OUT/bench_vgpr256.json" 2> "$OUT/bench_vgpr256.log" ;;
+    round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
+              timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \
+              SIEVE_ROUND2=progress timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_progress.jsonl" 2> "$OUT/path_scaling_progress.log" ;;
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;

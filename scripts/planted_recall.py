@@ -13,6 +13,7 @@ the misses are asked again of a sieve with 2^20-row second rounds (how many more
 recover).
 
     python scripts/planted_recall.py [n_paths=100] [path_len=24] [--extended] [--fake]
+                                     [--round2=always|progress|never]
 
 --fake runs on tests/fake_device.py (CPU; use small sizes).
 """
@@ -46,6 +47,7 @@ def run_family(s, family, n_paths, path_len, big=None, check=True):
     and the list of missed (seed, prefix) pairs."""
     outcomes = Counter()
     by_kind = defaultdict(Counter)
+    progress = Counter()  # first-round progress (some groups solved) of round-2 hits and misses
     times = defaultdict(list)
     bad, missed = [], []
     for seed in range(n_paths):
@@ -71,6 +73,10 @@ def run_family(s, family, n_paths, path_len, big=None, check=True):
                 kind = "unsupported" if "Unsupported" in type(e).__name__ else "error"
             outcomes[kind] += 1
             by_kind[kinds[k - 1]][kind] += 1
+            lr = s.last_rounds
+            if kind in ("hit_r2", "miss") and lr:
+                part = 0 < lr.get("r1_solved", 0) < lr.get("groups", 0)
+                progress[kind + ("_r1_partial" if part else "_r1_none")] += 1
             times[kind].append(dt)
     n = sum(outcomes.values())
     hits = outcomes["hit_r1"] + outcomes["hit_r2"]
@@ -81,6 +87,8 @@ def run_family(s, family, n_paths, path_len, big=None, check=True):
         "miss": outcomes["miss"], "refuted": outcomes["refuted"],
         "unsupported": outcomes["unsupported"], "error": outcomes["error"],
         "invalid_witnesses": len(bad),
+        "second_round": s.second_round,
+        "first_round_progress": dict(progress),
         "by_newest_constraint": {
             k: {"n": sum(c.values()), "recall": round((c["hit_r1"] + c["hit_r2"]) /
                                                       max(sum(c.values()), 1), 4),
@@ -114,7 +122,8 @@ def main():
         from tests import fake_device
 
         fake_device.install(pytest.MonkeyPatch())
-    s = Sieve(rows=256) if fake else Sieve()
+    policy = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--round2=")), None)
+    s = Sieve(rows=256, second_round=policy) if fake else Sieve(second_round=policy)
     big = None
     if "--extended" in sys.argv:
         big = Sieve(rows=1 << 20)

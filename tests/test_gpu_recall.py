@@ -1,0 +1,29 @@
+"""Recall on queries that are SAT by construction, on the GPU.
+
+Planted paths of tests/planted.py, every prefix asked in LASER order: no query is refuted (a
+soundness check: the planted model satisfies it), every witness is a model of the ORIGINAL query
+(the oracle), and the share of queries answered stays at or above the floor measured on this
+fixed workload (DESIGN §6's recall table, profiles/r05*/planted_recall*.jsonl).
+"""
+import pytest
+
+from mythril_amd.sieve import Sieve
+from scripts.planted_recall import run_family
+
+pytestmark = pytest.mark.gpu
+
+# measured on MI355X on this workload (20 paths x 16 constraint attempts, seeds 0..19)
+FLOOR = {"laser": 0.99, "random": 0.40}
+
+
+@pytest.mark.parametrize("family", ["laser", "random"])
+def test_planted_recall_floor(gpu_ctx, family):
+    s = Sieve()
+    try:
+        out = run_family(s, family, 20, 16)
+    finally:
+        s.close()
+    print(family, {k: out[k] for k in ("queries", "recall", "hit_round1", "hit_round2_only",
+                                       "miss", "unsupported")})
+    assert out["refuted"] == 0 and out["invalid_witnesses"] == 0 and out["error"] == 0, out
+    assert out["recall"] >= FLOOR[family], out
