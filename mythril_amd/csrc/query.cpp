@@ -9,7 +9,7 @@
 //
 //  * pass 1 (lower.py Lowering.collect / apply_harvest): the constant keys each free array and
 //    each non-keccak function is read at, the concrete keccak pairs keccak256_N(c) == k and the
-//    lowest bound a keccak application is compared with;
+//    greatest lower bound a keccak application is compared with;
 //  * pass 2 (Lowering.lower / _rewrite): only nodes that are or read host-only terms (F_HOST) are
 //    rewritten -- select / store chains to ite chains over the store keys and the array's cell
 //    columns (name "A[0x..]", else column "A[*]"), K(v) to v, keccak256_N to ite(x == c_i, k_i,
@@ -479,8 +479,24 @@ public:
                 KeccakMap& km = keccak_map(fn_name(s[0]));
                 if (x.op == EQ) {
                     if (const Big* arg = const_value(app.a)) km.put(*arg, hv);
-                } else if (!km.has_bound || hv < km.bound) {
-                    km.bound = hv;
+                    continue;
+                }
+                // a lower bound on the application (f > k, f >= k, k < f, k <= f): the
+                // interval's base is the greatest of them; upper bounds and signed orders
+                // bound nothing here (lower.py Lowering.collect)
+                const bool left = &s == &sides[0];
+                bool lower = false, strict = false;
+                if (left && (x.op == MH_OP_BVUGT || x.op == MH_OP_BVUGE)) {
+                    lower = true;
+                    strict = x.op == MH_OP_BVUGT;
+                } else if (!left && (x.op == BVULT || x.op == MH_OP_BVULE)) {
+                    lower = true;
+                    strict = x.op == BVULT;
+                }
+                if (!lower) continue;
+                const Big lb = strict ? hv.plus(1) : hv;
+                if (!km.has_bound || km.bound < lb) {
+                    km.bound = lb;
                     km.has_bound = true;
                 }
             }

@@ -17,8 +17,9 @@ into a term over scalar *columns* whose every assignment denotes one complete z3
   ``H(x) = base + ((keccak256(x) >> 139) << 6)``: a function of the argument (so congruence
   holds), injective up to keccak collisions in 117 bits (so the inverse condition
   ``keccak256_N-1(keccak256_N(x)) == x`` holds, lowered to ``x``), a multiple of 64, and inside
-  ``[base, base + 2^123)``, where ``base`` is the interval's lower bound harvested from the
-  query, rounded up to a multiple of 64 — the interval of ``_create_condition`` (:121-149) is
+  ``[base, base + 2^123)``, where ``base`` is the greatest lower bound the query states on the
+  function's values (``ULE(lo, f(x))`` of the manager's condition, ``UGT(f(x), c)``, ...),
+  rounded up to a multiple of 64 — the interval of ``_create_condition`` (:121-149) is
   ``PART = (2^256-1) // 10^40 > 2^123 + 64`` wide, so the interval and ``mod 64`` conditions hold
   by construction.  The hash runs on the device's Keccak-f[1600].
 * any other uninterpreted function is tabled like an array (cells over constant arguments plus
@@ -35,6 +36,12 @@ from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from .tape import ARITY, BOOL, F_ARRAY, F_HOST, Op, TapeBuilder, TapeError
+
+def keccak_base(lower_bound: int) -> int:
+    """The interval base of a keccak function's values: its greatest harvested lower bound,
+    rounded up to a multiple of 64 (mod 2^256)."""
+    return ((lower_bound + 63) & ~63) & ((1 << 256) - 1)
+
 
 KECCAK_SHIFT = 139   # keep 117 bits of the hash ...
 KECCAK_ALIGN = 6     # ... as multiples of 64: H - base < 2^123 < PART
@@ -75,7 +82,7 @@ class Schema:
 @dataclass
 class Harvest:
     """What pass 1 reads off some constraints: constant keys per array / function, concrete
-    keccak pairs and the lowest keccak bound.  One per constraint, memoised on the builder, so a
+    keccak pairs and the greatest lower bound on each keccak function.  One per constraint, memoised on the builder, so a
     query that extends its parent (svm.py:257-262) only walks its new constraint."""
 
     cells: Dict[str, set] = field(default_factory=dict)
@@ -91,14 +98,14 @@ class Harvest:
         for f, pairs in o.keccak.items():
             self.keccak.setdefault(f, {}).update(pairs)
         for f, v in o.bounds.items():
-            self.bounds[f] = min(v, self.bounds.get(f, v))
+            self.bounds[f] = max(v, self.bounds.get(f, v))
 
     def fingerprint(self) -> tuple:
         """Everything the rewrite of pass 2 depends on: equal fingerprints lower every term to the
         same column-only term."""
         return (tuple(sorted((n, tuple(sorted(k))) for n, k in self.cells.items())),
                 tuple(sorted((n, tuple(sorted(k))) for n, k in self.uf_cells.items())),
-                tuple(sorted((f, tuple(sorted(p.items())), (self.bounds.get(f, 0) + 63) & ~63)
+                tuple(sorted((f, tuple(sorted(p.items())), keccak_base(self.bounds.get(f, 0)))
                              for f, p in self.keccak.items())))
 
 
@@ -259,8 +266,16 @@ class Lowering:
                         arg = b.const_value(b.nodes[x][2])
                         if arg is not None:  # keccak256_N(c) == k: a concrete pair
                             h.keccak.setdefault(f, {})[arg] = kv
-                    else:
-                        h.bounds[f] = min(kv, h.bounds.get(f, kv))
+                        continue
+                    # a lower bound on the application (f > k, f >= k, k < f, k <= f); upper
+                    # bounds and signed orders bound nothing here
+                    lb = None
+                    if x == a and op in (Op.BVUGT, Op.BVUGE):
+                        lb = kv + (op == Op.BVUGT)
+                    elif x == bb and op in (Op.BVULT, Op.BVULE):
+                        lb = kv + (op == Op.BVULT)
+                    if lb is not None:
+                        h.bounds[f] = max(lb, h.bounds.get(f, lb))
         return h
 
     def apply_harvest(self, h: "Harvest") -> None:
@@ -275,7 +290,7 @@ class Lowering:
         for f, pairs in h.keccak.items():
             km = self.schema.keccak.setdefault(f, KeccakMap(0))
             km.pairs.update(pairs)
-            km.base = (h.bounds.get(f, 0) + 63) & ~63
+            km.base = keccak_base(h.bounds.get(f, 0))
 
     def _keccak_app(self, n: int) -> Optional[str]:
         op, _, _, _, _, i0, _ = self.b.nodes[n]
