@@ -25,6 +25,8 @@
 #   recall    scripts/planted_recall.py (recall on planted-SAT paths, per round and shape class)
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
 #             (SIEVE_ROUND2=progress) and never run (recall only)
+#   policy    sieve_queries.py (9 reps) and path_scaling.py with the second round always run and
+#             gated on first-round progress (SIEVE_ROUND2=always / progress), back to back
 #   occupancy bench.py at 168 and 256 VGPRs (3 and 2 waves per SIMD; the LDS-resident compaction
 #             design of DESIGN §10 needs one of them)
 set -o pipefail
@@ -66,6 +68,9 @@ for step in "$@"; do
     round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
               timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \
               SIEVE_ROUND2=progress timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_progress.jsonl" 2> "$OUT/path_scaling_progress.log" ;;
+    policy)   for pol in always progress; do \
+                SIEVE_ROUND2=$pol SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_$pol.jsonl" 2> "$OUT/sieve_queries_$pol.log" && \
+                SIEVE_ROUND2=$pol timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_$pol.jsonl" 2> "$OUT/path_scaling_$pol.log" || exit 1; done ;;
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;

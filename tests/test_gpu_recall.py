@@ -12,8 +12,9 @@ from scripts.planted_recall import run_family
 
 pytestmark = pytest.mark.gpu
 
-# measured on MI355X on this workload (20 paths x 16 constraint attempts, seeds 0..19)
-FLOOR = {"laser": 0.99, "random": 0.40}
+# measured on MI355X on this workload (20 paths x 16 constraint attempts, seeds 0..19):
+# LASER 1.000 (326 queries), random 0.653 (455; profiles/r05d/pytest_recall.txt)
+FLOOR = {"laser": 0.99, "random": 0.60}
 
 
 @pytest.mark.parametrize("family", ["laser", "random"])
