@@ -1481,6 +1481,9 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
         slots.push_back(w1);
     };
     auto pos = [&]() { return (uint32_t)(slots.size() / 2); };
+    // D_LOADVAR names the NEXT column the tape loads in its b | c << 8 fields (0xffff: none): the
+    // asm core prefetches it while the instructions in between run (gen_asm_core.py LOADVAR)
+    int64_t last_lv = -1;
     for (size_t i = 0; i < code.size(); ++i) {
         const VInsn& v = code[i];
         auto P = [&](int r) -> uint32_t { return (r < 0 || phys[r] < 0) ? 0u : (uint32_t)phys[r]; };
@@ -1510,7 +1513,16 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
             put(0, D_WINDOW);
             while (pos() % MH_WINDOW) put(0, 0);
         }
-        put(a | (b << 8) | (d << 16) | (c << 24), w1);
+        if (v.op == D_LOADVAR) {
+            if (last_lv >= 0) {  // the previous LOADVAR prefetches this column
+                uint32_t& pw0 = slots[2 * (size_t)last_lv];
+                pw0 = (pw0 & 0x00FF00FFu) | ((v.aux & 0xFFu) << 8) | ((v.aux >> 8) << 24);
+            }
+            last_lv = pos();
+            put(a | (0xFFu << 8) | (d << 16) | (0xFFu << 24), w1);
+        } else {
+            put(a | (b << 8) | (d << 16) | (c << 24), w1);
+        }
         if (v.cidx >= 0) {
             const uint32_t* lim = dconsts.data() + 8ull * (uint32_t)v.cidx;
             for (int k = 0; k < 4; ++k) put(lim[2 * k], lim[2 * k + 1]);

@@ -149,6 +149,10 @@ MH_FN u32 step(M& m, u32 w0, u32 w1, u32 ip) {
     if (yconst) {
         m.iconst(ip + 1, y);
         len = 5;
+    } else if (op == D_LOADVAR) {
+        // no register operand: b / c carry the next column the tape loads (the asm core's
+        // prefetch, compile.cpp), so neither is read
+        zero8(y);
     } else if (full_y) {
         m.read(b, y);
     } else {
@@ -244,7 +248,8 @@ MH_FN u32 step(M& m, u32 w0, u32 w1, u32 ip) {
         default:
             if (op >= D_FIRST_COMPLEX) {
                 u32 c3[8];
-                m.read(c, c3);
+                if (op == D_LOADVAR) zero8(c3);
+                else m.read(c, c3);
                 complex_op<FEAT>(m, w1, x, y, c3, z);
             }
             break;

@@ -55,6 +55,13 @@ D_LOADVAR = 118     # dev_isa.h (static_assert in the .inc)
 # and no bit at or above the width), in run_lv only
 D_UADD_NOOVFL = 112
 CORE_COMPLEX = {D_LOADVAR: "LOADVAR", D_UADD_NOOVFL: "UADD_NOOVFL"}
+# D_LOADVAR prefetches the NEXT column the tape loads (its number in the word's b / c fields,
+# compile.cpp; 0xffff: none) into 8 spare VGPRs without waiting, so the column load of the next
+# LOADVAR overlaps the instructions between the two (MH_GEN_LV_PREFETCH=0: no prefetch).  The
+# prefetch lives within one run of the core: every exit drains it (s_waitcnt vmcnt(0)) and an
+# entry starts with none in flight.
+LV_PREFETCH = LOADVAR and os.environ.get("MH_GEN_LV_PREFETCH", "1") != "0"
+LV_NONE = 0xFFFF
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
 OPS = ["EXIT", "NOP",
@@ -98,6 +105,7 @@ S_F64 = ("s68", "s69")
 S_NW0, S_NW1 = ("s72", "s73") if PREFETCH_CONSTS else ("s64", "s65")
 S_BANK = "s[72:87]"
 S_NT = "s66"                     # prefetch address temp
+S_PFC = "s45"                    # LOADVAR prefetch: the column in flight to the PF registers
 DISPATCH_MARK = "@@dispatch_words"   # replaced per handler (prefetched or loaded in the dispatch)
 SGPR_CLOBBERS = ["s%d" % i for i in range(40, 88 if PREFETCH_CONSTS else 72)]
 
@@ -122,6 +130,31 @@ class Core:
 
     def Y(self, k):
         return self.S(k)
+
+    def PF(self, k):  # run_lv: the column LOADVAR prefetched (8 VGPRs after the scratch)
+        assert 0 <= k < 8
+        return "v%d" % (self.sb + N_SCRATCH + k)
+
+    def lv_address(self, col_sgpr):
+        """s[56:57] = address of limb 0 of column `col_sgpr` (SoA planes: vbase + 8 col cap4); the
+        row's byte offset is the VGPR voff.  SALU only: no VALU-written SGPR reaches the loads."""
+        lo, hi = S_K[0], S_K[1]
+        return ["s_lshl_b32 {}, {}, 3".format(S_T, col_sgpr),
+                "s_mul_i32 {}, {}, %[cap4]".format(lo, S_T),
+                "s_mul_hi_u32 {}, {}, %[cap4]".format(hi, S_T),
+                "s_add_u32 {0}, {0}, %[vlo]".format(lo),
+                "s_addc_u32 {0}, {0}, %[vhi]".format(hi)]
+
+    def lv_loads(self, dst):
+        """8 global loads of the column at s[56:57] into dst(0..7), no wait."""
+        lo, hi = S_K[0], S_K[1]
+        body = []
+        for k in range(8):
+            if k:
+                body += ["s_add_u32 {0}, {0}, %[cap4]".format(lo),
+                         "s_addc_u32 {0}, {0}, 0".format(hi)]
+            body.append("global_load_dword {}, %[voff], s[{}:{}]".format(dst(k), lo[1:], hi[1:]))
+        return body
 
     # ---- building blocks
     def dispatch(self, adv):
@@ -269,20 +302,30 @@ class Core:
             # X = column aux of this lane's row: limb k at vbase + ((8 col + k) cap4) + voff
             # (SoA planes, KParams::assign); the address is SALU arithmetic in s[56:57] (no
             # VALU-written SGPR reaches the loads), the row's byte offset the VGPR voff
-            lo, hi = S_K[0], S_K[1]
-            body = ["s_lshr_b32 {}, {}, 17".format(S_T, S_W1),
-                    "s_and_b32 {0}, {0}, 0x3fff".format(S_T),
-                    "s_lshl_b32 {0}, {0}, 3".format(S_T),
-                    "s_mul_i32 {}, {}, %[cap4]".format(lo, S_T),
-                    "s_mul_hi_u32 {}, {}, %[cap4]".format(hi, S_T),
-                    "s_add_u32 {0}, {0}, %[vlo]".format(lo),
-                    "s_addc_u32 {0}, {0}, %[vhi]".format(hi)]
-            for k in range(8):
-                if k:
-                    body += ["s_add_u32 {0}, {0}, %[cap4]".format(lo),
-                             "s_addc_u32 {0}, {0}, 0".format(hi)]
-                body.append("global_load_dword {}, %[voff], s[{}:{}]".format(X(k), lo[1:], hi[1:]))
-            body.append("s_waitcnt vmcnt(0)")
+            body = ["s_lshr_b32 {}, {}, 17".format(S_R, S_W1),
+                    "s_and_b32 {0}, {0}, 0x3fff".format(S_R)]
+            if not LV_PREFETCH:
+                body += self.lv_address(S_R) + self.lv_loads(X) + ["s_waitcnt vmcnt(0)"]
+                return body + self.wb() + self.dispatch(1)
+            # the column prefetched by the previous LOADVAR: wait for it and copy; otherwise
+            # load it now
+            body += ["s_cmp_eq_u32 {}, {}".format(S_R, S_PFC),
+                     "s_cbranch_scc0 L_lv_ld_%=",
+                     "s_waitcnt vmcnt(0)"]
+            body += ["v_mov_b32 {}, {}".format(X(k), self.PF(k)) for k in range(8)]
+            body += ["s_branch L_lv_pf_%=", "L_lv_ld_%=:"]
+            body += self.lv_address(S_R) + self.lv_loads(X) + ["s_waitcnt vmcnt(0)"]
+            # the next column this tape loads (w0 bits 8..15 | 24..31 << 8): in flight to PF
+            # while the instructions up to its LOADVAR run
+            body += ["L_lv_pf_%=:",
+                     "s_bfe_u32 {}, {}, 0x80008".format(S_R, S_W0),
+                     "s_lshr_b32 {}, {}, 24".format(S_Q, S_W0),
+                     "s_lshl_b32 {0}, {0}, 8".format(S_Q),
+                     "s_or_b32 {}, {}, {}".format(S_PFC, S_R, S_Q),
+                     "s_cmpk_eq_u32 {}, 0x{:x}".format(S_PFC, LV_NONE),
+                     "s_cbranch_scc1 L_lv_wb_%="]
+            body += self.lv_address(S_PFC) + self.lv_loads(self.PF)
+            body += ["L_lv_wb_%=:"]
             return body + self.wb() + self.dispatch(1)
         if name == "UADD_NOOVFL":
             # y = inline constant (F_YC, 4 slots follow) or R[b]; t = R[a'] + y in S8..15;
@@ -743,6 +786,8 @@ class Core:
                  "L_pc_%=:",
                  "s_add_u32 {0}, {0}, (L_tab_%= - L_pc_%=)".format(S_TAB),
                  "s_addc_u32 {0}, {0}, 0".format(S_TAB_HI)]
+        if self.loadvar and LV_PREFETCH:  # nothing in flight on entry
+            lines.append("s_mov_b32 {}, 0x{:x}".format(S_PFC, LV_NONE))
         lines += self.resolve(self.dispatch(0))
         lines += [".p2align 8", "L_tab_%=:"]
         bodies = []
@@ -759,10 +804,13 @@ class Core:
                 lines += h
         lines += [".org L_tab_%= + {}".format(NSLOTS * SLOT)] + bodies + self.resolve(self.div_body())
         lines += ["L_out_%=:"]
+        if self.loadvar and LV_PREFETCH:  # a prefetch still in flight lands before the exit
+            lines.append("s_waitcnt vmcnt(0)")
         return lines
 
 
 N_SCRATCH = 32  # S0..S31, declared clobbered by the core (division uses all 32)
+N_PF = 8        # run_lv with LV_PREFETCH: the prefetched column, after the scratch
 
 
 def check_registers(core, lines, n_scratch):
@@ -812,6 +860,9 @@ def emit(out):
             forms.append((Core(nr, loadvar=True), "run_lv",
                           ", u32 vlo, u32 vhi, u32 cap4, u32 voff"))
         for core, fname, extra in forms:
+            n_scr = N_SCRATCH + (N_PF if core.loadvar and LV_PREFETCH else 0)
+            clob = ["\"v{}\"".format(c.sb + j) for j in range(n_scr)] + \
+                   ["\"{}\"".format(s) for s in SGPR_CLOBBERS] + ["\"vcc\"", "\"scc\"", "\"m0\""]
             w("    // runs asm-core instructions from slot ip of the window (ic0, ic1); returns the\n")
             w("    // slot of the first instruction it does not handle\n")
             if extra:
@@ -829,7 +880,7 @@ def emit(out):
                 ins += (", [vlo] \"s\"(vlo), [vhi] \"s\"(vhi), [cap4] \"s\"(cap4), "
                         "[voff] \"v\"(voff)")
             w("            : {}\n".format(ins))
-            check_registers(core, core.asm_text(), N_SCRATCH)
+            check_registers(core, core.asm_text(), n_scr)
             w("            : {});\n".format(", ".join(clob)))
             w("        return ip;\n")
             w("    }\n")

@@ -27,6 +27,10 @@
 #             (SIEVE_ROUND2=progress) and never run (recall only)
 #   policy    sieve_queries.py (9 reps) and path_scaling.py with the second round always run and
 #             gated on first-round progress (SIEVE_ROUND2=always / progress), back to back
+#   nopf      interp, paths and queries (9 reps) on the variant library built without the
+#             interpreter's LOADVAR prefetch (scripts/build_variant.sh nopf MH_GEN_LV_PREFETCH=0)
+#   qpmc      scripts/qprofile_pmc.sh <tag> (PMC passes of the query-path kernels)
+#   qpmcnopf  the same on the no-prefetch variant library
 #   occupancy bench.py at 168 and 256 VGPRs (3 and 2 waves per SIMD; the LDS-resident compaction
 #             design of DESIGN §10 needs one of them)
 set -o pipefail
@@ -71,6 +75,13 @@ for step in "$@"; do
     policy)   for pol in always progress; do \
                 SIEVE_ROUND2=$pol SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_$pol.jsonl" 2> "$OUT/sieve_queries_$pol.log" && \
                 SIEVE_ROUND2=$pol timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_$pol.jsonl" 2> "$OUT/path_scaling_$pol.log" || exit 1; done ;;
+    nopf)     export MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_nopf.so && \
+              timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost_nopf.jsonl" 2> "$OUT/interp_op_cost_nopf.log" && \
+              timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_nopf.jsonl" 2> "$OUT/path_scaling_nopf.log" && \
+              SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_nopf.jsonl" 2> "$OUT/sieve_queries_nopf.log"; \
+              rc=$?; unset MYTHRIL_HIP_LIB; (exit $rc) ;;
+    qpmc)     bash scripts/qprofile_pmc.sh "$TAG" ;;
+    qpmcnopf) MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_nopf.so bash scripts/qprofile_pmc.sh "${TAG}_nopf" ;;
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;

@@ -219,18 +219,40 @@ def test_loadvar_handler(nr):
                        input=src, capture_output=True, text=True)
     assert p.returncode == 0, p.stderr[:400]
     loads = [ln for ln in lines if ln.startswith("global_load_dword")]
-    assert loads == ["global_load_dword {}, %[voff], s[56:57]".format(core.X(k)) for k in range(8)]
-    assert lines.index("s_waitcnt vmcnt(0)") > lines.index(loads[-1])
-    assert lines.index("s_waitcnt vmcnt(0)") < next(i for i, ln in enumerate(lines)
-                                                     if ln.startswith("s_set_gpr_idx_on"))
-    assert sum(ln == "s_add_u32 s56, s56, %[cap4]" for ln in lines) == 7
+    own = ["global_load_dword {}, %[voff], s[56:57]".format(core.X(k)) for k in range(8)]
+    pf = ["global_load_dword {}, %[voff], s[56:57]".format(core.PF(k)) for k in range(8)]
+    if G.LV_PREFETCH:
+        # its own column into X (unless the previous LOADVAR prefetched it: then a wait and a
+        # copy from PF), then the next column into PF, not waited for
+        assert loads == own + pf
+        waits = [i for i, ln in enumerate(lines) if ln == "s_waitcnt vmcnt(0)"]
+        assert len(waits) == 2
+        copy = [i for i, ln in enumerate(lines) if ln.startswith("v_mov_b32") and "v%d" % (
+            core.sb + G.N_SCRATCH) in ln]
+        assert waits[0] < copy[0]  # the prefetched column has landed before it is copied
+        assert lines.index(own[-1]) < waits[1] < lines.index(pf[0])
+        assert lines.index(pf[-1]) < next(i for i, ln in enumerate(lines)
+                                          if ln.startswith("s_set_gpr_idx_on"))
+        assert sum(ln == "s_add_u32 s56, s56, %[cap4]" for ln in lines) == 14
+        text = core.asm_text()
+        # every run starts with nothing in flight and drains the prefetch before it exits
+        assert text[text.index("L_out_%=:") + 1] == "s_waitcnt vmcnt(0)"
+        assert "s_mov_b32 {}, 0x{:x}".format(G.S_PFC, G.LV_NONE) in text[:8]
+        G.check_registers(core, text, G.N_SCRATCH + G.N_PF)
+    else:
+        assert loads == own
+        assert lines.index("s_waitcnt vmcnt(0)") > lines.index(loads[-1])
+        assert lines.index("s_waitcnt vmcnt(0)") < next(i for i, ln in enumerate(lines)
+                                                         if ln.startswith("s_set_gpr_idx_on"))
+        assert sum(ln == "s_add_u32 s56, s56, %[cap4]" for ln in lines) == 7
     text = core.asm_text()
     slot = text.index(".org L_tab_%= + {}".format(G.D_LOADVAR * G.SLOT))
     assert text[slot + 1] == "s_branch L_body_LOADVAR_%="
     plain = G.Core(nr).asm_text()
     slot = plain.index(".org L_tab_%= + {}".format(G.D_LOADVAR * G.SLOT))
     assert plain[slot + 1] == "s_branch L_out_%=" and not any("%[voff]" in ln for ln in plain)
-    G.check_registers(core, text, G.N_SCRATCH)
+    if not G.LV_PREFETCH:
+        G.check_registers(core, text, G.N_SCRATCH)
 
 
 @pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not installed")
