@@ -77,6 +77,7 @@ bool commutes(uint8_t op) {
     switch (op) {
         case D_ADD_R: case D_AND_R: case D_OR_R: case D_XOR_R: case D_EQ_R: case D_MUL_R:
         case D_UADD_NOOVFL: case D_UMUL_NOOVFL: case D_BAND: case D_BOR: case D_BXOR: case D_BEQ:
+        case D_BANDZ:
             return true;
         default:
             return false;
@@ -1368,6 +1369,85 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
 
 namespace {
 
+// Short-circuit conjunctions of the interpreter (the native code orders its own, jit.cpp): the
+// root's AND chain -- the BANDs reachable from the root through single-use BANDs -- is flattened
+// and emitted again conjunct by conjunct: each conjunct's cone (the instructions it needs that no
+// earlier conjunct emitted, in their lowered order) just before the AND that takes it in, every
+// AND but the last a D_BANDZ, where a wave with no lane left true leaves the tape (its root is 0
+// in every lane).  Newest conjunct first: a LASER query's tape is its parent's conjunction and the
+// new constraint (svm.py:257-262), the conjunct that rows guided by the parent's witness are the
+// least likely to satisfy.  MH_INTERP_SC=0 keeps the tape as lowered, =given the conjuncts' order.
+// Counts, first witnesses and root values are those of the tape as lowered.
+void short_circuit(SsaTape& st) {
+    static const int mode = [] {
+        const char* e = std::getenv("MH_INTERP_SC");
+        return !e ? 2 : std::strcmp(e, "0") == 0 ? 0 : std::strcmp(e, "given") == 0 ? 1 : 2;
+    }();
+    if (!mode || !st.root_bool || st.root < 0) return;
+    std::vector<SsaInsn>& code = st.code;
+    const int n = (int)code.size();
+    std::vector<int> def(st.n_vregs, -1), uses(st.n_vregs, 0);
+    for (int i = 0; i < n; ++i) {
+        def[code[i].d] = i;
+        for (int r : {code[i].a, code[i].b, code[i].c})
+            if (r >= 0) ++uses[r];
+    }
+    if (def[st.root] < 0 || code[def[st.root]].op != D_BAND) return;
+    std::vector<char> chain(n, 0), is_conj(st.n_vregs, 0);
+    std::vector<int> conj, stack{st.root};
+    while (!stack.empty()) {
+        const int r = stack.back();
+        stack.pop_back();
+        const int i = def[r];
+        if (i >= 0 && code[i].op == D_BAND && code[i].cidx < 0 && code[i].b >= 0 &&
+            (r == st.root || uses[r] == 1)) {
+            chain[i] = 1;
+            stack.push_back(code[i].b);
+            stack.push_back(code[i].a);
+        } else if (!is_conj[r]) {
+            is_conj[r] = 1;
+            conj.push_back(r);
+        }
+    }
+    if (conj.size() < 2) return;
+    if (mode == 2) std::reverse(conj.begin(), conj.end());
+    std::vector<SsaInsn> out;
+    out.reserve(code.size() + conj.size());
+    std::vector<char> emitted(n, 0);
+    int acc = -1;
+    for (size_t k = 0; k < conj.size(); ++k) {
+        std::vector<int> cone;
+        if (def[conj[k]] >= 0 && !emitted[def[conj[k]]]) {
+            stack.assign(1, def[conj[k]]);
+            emitted[def[conj[k]]] = 1;
+            while (!stack.empty()) {
+                const int i = stack.back();
+                stack.pop_back();
+                if (chain[i]) return;  // a chain AND read inside a conjunct: keep the tape
+                cone.push_back(i);
+                for (int r : {code[i].a, code[i].b, code[i].c}) {
+                    if (r < 0 || def[r] < 0 || emitted[def[r]]) continue;
+                    emitted[def[r]] = 1;
+                    stack.push_back(def[r]);
+                }
+            }
+            std::sort(cone.begin(), cone.end());
+        }
+        for (int i : cone) out.push_back(code[i]);
+        const bool last = k + 1 == conj.size();
+        const int d = st.n_vregs++;
+        // the first conjunct is tested alone (x & x)
+        out.push_back(SsaInsn{last ? (uint8_t)D_BAND : (uint8_t)D_BANDZ, d, k ? acc : conj[k],
+                              conj[k], -1, 1, 0, -1, 0});
+        acc = d;
+    }
+    size_t n_chain = 0;
+    for (int i = 0; i < n; ++i) n_chain += chain[i];
+    if (out.size() != code.size() - n_chain + conj.size()) return;  // something outside: keep
+    code.swap(out);
+    st.root = acc;
+}
+
 int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                           uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                           std::unordered_map<std::string, uint32_t>& dconst_index,
@@ -1379,6 +1459,7 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
         return r;
     out.alg_ops = st.alg_ops;
     out.n_nodes = (uint32_t)n_nodes;
+    short_circuit(st);
     std::vector<VInsn>& code = st.code;
     const int n_pinned = st.n_pinned;
     int root_v = st.root;

@@ -73,6 +73,10 @@ enum mh_dop : uint8_t {
     //   D_SHL0 + p: X = R[a'] << (aux ? 32 p + 32 - aux : 32 (p + 1)) mod 2^256, aux < 32
     D_SHR0, D_SHR1, D_SHR2, D_SHR3, D_SHR4, D_SHR5, D_SHR6, D_SHR7,
     D_SHL0, D_SHL1, D_SHL2, D_SHL3, D_SHL4, D_SHL5, D_SHL6, D_SHL7,
+    // short-circuit AND of a tape's root conjunction (compile.cpp short_circuit): X = R[a'] &
+    // R[b] limb 0 like D_BAND, and when X is 0 in every lane the tape's root is 0 in every lane,
+    // so the asm core leaves at this op and the driver ends the tape (X = 0 is the root)
+    D_BANDZ,
     D_NUM_ASM,
     // ---- C++ (exec.h); y = R[b] or the inline constant (F_YC)
     D_FIRST_COMPLEX = 112,
@@ -115,7 +119,7 @@ static inline unsigned mh_xform(unsigned op) {
 // ops whose result is a Bool (0/1 in limb 0)
 static inline bool mh_produces_bool(unsigned op) {
     op = mh_base_op(op);
-    return (op >= D_EQ_R && op <= D_SGE_C) || (op >= D_BAND && op <= D_FALSE) || op == D_BITE ||
+    return (op >= D_EQ_R && op <= D_SGE_C) || (op >= D_BAND && op <= D_FALSE) || op == D_BITE || op == D_BANDZ ||
            op == D_UADD_NOOVFL || op == D_UMUL_NOOVFL;
 }
 

@@ -195,7 +195,7 @@ MH_FN u32 step(M& m, u32 w0, u32 w1, u32 ip) {
         // Bool operands are canonical 0/1 in limb 0 (dev_isa.h), so, exactly like the asm core,
         // no mask: a producer that left other bits set would show here as a non-0/1 result,
         // which the host emulator rejects (tests/native/emu.cpp, mh_produces_bool)
-        case D_BAND: if constexpr (SIMPLE) z[0] = x[0] & y[0]; break;
+        case D_BAND: case D_BANDZ: if constexpr (SIMPLE) z[0] = x[0] & y[0]; break;
         case D_BOR: if constexpr (SIMPLE) z[0] = x[0] | y[0]; break;
         case D_BXOR: if constexpr (SIMPLE) z[0] = x[0] ^ y[0]; break;
         case D_BEQ: if constexpr (SIMPLE) z[0] = x[0] ^ y[0] ^ 1u; break;

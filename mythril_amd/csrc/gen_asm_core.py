@@ -81,7 +81,7 @@ OPS = ["EXIT", "NOP",
        "UGE_RX", "UGE_CX", "SLT_RX", "SLT_CX", "SGT_RX", "SGT_CX", "SLE_RX", "SLE_CX",
        "SGE_RX", "SGE_CX",
        "MUL_RX", "MUL_CX", "LOADC_X"] + \
-      ["SHR%d" % q for q in range(8)] + ["SHL%d" % q for q in range(8)]
+      ["SHR%d" % q for q in range(8)] + ["SHL%d" % q for q in range(8)] + ["BANDZ"]
 DIV_KIND = {"UDIV_R": 0, "UDIV_C": 0, "UREM_R": 1, "UREM_C": 1, "SDIV_R": 2, "SDIV_C": 2,
             "SREM_R": 3, "SREM_C": 3, "SMOD_R": 4, "SMOD_C": 4}
 OPNUM = {n: i for i, n in enumerate(OPS)}
@@ -464,6 +464,16 @@ class Core:
             if name == "BEQ":
                 body.append("v_xor_b32 {0}, 1, {0}".format(X(0)))
             return body + self.wb(1) + self.dispatch(1)
+        if name == "BANDZ":
+            # BAND, then the short-circuit test: no lane true -> leave the core at this op (the
+            # driver ends the tape; X = 0 is its root).  The next words' prefetch is waited for
+            # before leaving (its SGPRs are the compiler's again after the asm block).
+            body = self.y_reg(1) + a_src0 + ["v_and_b32 {}, {}, {}".format(X(0), P(0), Y(0))] + off
+            body += self.wb(1) + ["v_cmp_ne_u32 vcc, 0, {}".format(X(0)),
+                                  "s_cmp_eq_u64 vcc, 0",
+                                  "s_cbranch_scc1 L_bz_%="]
+            return body + self.dispatch(1) + ["L_bz_%=:", "s_waitcnt lgkmcnt(0)",
+                                              "s_branch L_out_%="]
         if name == "BNOT":
             body = a_src1 + ["v_xor_b32 {}, 1, {}".format(X(0), P(0))] + off  # R[a'] in src1
             return body + self.wb(1) + self.dispatch(1)

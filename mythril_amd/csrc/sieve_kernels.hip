@@ -131,7 +131,8 @@ __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, I
         const u32 w0 = __builtin_amdgcn_readlane(ic.w0, ip);
         const u32 w1 = __builtin_amdgcn_readlane(ic.w1, ip);
         const u32 op = w1 & 0xFFu;
-        if (op == D_END) break;
+        // D_BANDZ: the asm core left there because the conjunction is 0 in every lane (X = 0)
+        if (op == D_END || op == D_BANDZ) break;
         if (op == D_WINDOW) {
             win += MH_WINDOW;
             const u32 j = win + (threadIdx.x & 63u);

@@ -21,6 +21,7 @@
 #   pypaths   paths with the Python host stages
 #   qcost     scripts/query_cost.py (host stages per query, native compiler vs Python)
 #   qprofile  rocprofv3 kernel trace + stats of one pass of sieve_queries.py (query-path kernels)
+#   pprofile  rocprofv3 kernel trace + stats of path_scaling.py at 400 constraints
 #   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
 #   recall    scripts/planted_recall.py (recall on planted-SAT paths, per round and shape class)
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
@@ -29,6 +30,8 @@
 #             gated on first-round progress (SIEVE_ROUND2=always / progress), back to back
 #   nopf      interp, paths and queries (9 reps) on the variant library built without the
 #             interpreter's LOADVAR prefetch (scripts/build_variant.sh nopf MH_GEN_LV_PREFETCH=0)
+#   scab      paths and queries (9 reps) with the interpreter's short-circuit conjunctions off
+#             (MH_INTERP_SC=0) and in the conjuncts' given order (MH_INTERP_SC=given)
 #   qpmc      scripts/qprofile_pmc.sh <tag> (PMC passes of the query-path kernels)
 #   qpmcnopf  the same on the no-prefetch variant library
 #   occupancy bench.py at 168 and 256 VGPRs (3 and 2 waves per SIMD; the LDS-resident compaction
@@ -80,11 +83,16 @@ for step in "$@"; do
               timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_nopf.jsonl" 2> "$OUT/path_scaling_nopf.log" && \
               SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_nopf.jsonl" 2> "$OUT/sieve_queries_nopf.log"; \
               rc=$?; unset MYTHRIL_HIP_LIB; (exit $rc) ;;
+    scab)     for sc in 0 given; do \
+                MH_INTERP_SC=$sc timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_sc$sc.jsonl" 2> "$OUT/path_scaling_sc$sc.log" && \
+                MH_INTERP_SC=$sc SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_sc$sc.jsonl" 2> "$OUT/sieve_queries_sc$sc.log" || exit 1; done ;;
     qpmc)     bash scripts/qprofile_pmc.sh "$TAG" ;;
     qpmcnopf) MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_nopf.so bash scripts/qprofile_pmc.sh "${TAG}_nopf" ;;
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;
+    pprofile) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pprof" -o pprof -- \
+                python -u scripts/path_scaling.py 400 > "$OUT/pprof.jsonl" 2> "$OUT/pprof.log" ;;
     gather)   timeout -k 10 300 python -u scripts/gather_bench.py > "$OUT/gather.jsonl" 2> "$OUT/gather.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -49,6 +49,10 @@ class Emulator:
 
     def n_slots(self, ts: TapeSet) -> int:
         """Instruction slots the compiler emits for the whole tape set (emu_compile_words)."""
+        return len(self.words(ts)) // 2
+
+    def words(self, ts: TapeSet) -> np.ndarray:
+        """The slot words (w0, w1 pairs) the compiler emits for the whole tape set."""
         f = self.lib.emu_compile_words
         f.restype = C.c_int32
         f.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
@@ -68,7 +72,7 @@ class Emulator:
               nrx.ctypes.data, err, 256)
         if r != 0:
             raise EmuError(r, err.value.decode())
-        return int(nw.value) // 2
+        return out[:int(nw.value)].copy()
 
 
 class JitResult:

@@ -87,6 +87,9 @@ extern "C" int32_t emu_eval(const mh_node* nodes, const uint64_t* offs, uint32_t
                 continue;
             }
             s += step<F_DIV | F_KECCAK | F_EVM, true>(m, w0, w1, s);
+            // the device leaves the tape at a D_BANDZ whose conjunction is 0 in every lane of a
+            // wave; here in the lane alone (stricter: the root must then be 0 for this row)
+            if (op == D_BANDZ && (m.R[nrx][0] & 1u) == 0) break;
             if (mh_produces_bool(op) && m.R[nrx][0] > 1u) {
                 // the device's Bool handlers assume canonical operands (dev_isa.h): a
                 // producer that breaks it must fail here, not only on the GPU

@@ -124,3 +124,52 @@ def test_hot_columns_are_loaded_once(emu):
         del os.environ["MH_NO_HOLD_VARS"]
     assert [bool(x) for x in held] == [bool(x) for x in plain]
     assert n_held < n_plain, (n_held, n_plain)
+
+
+def test_root_conjunction_short_circuits(emu):
+    """The interpreter's compiler flattens a query's root AND chain and emits every AND but the
+    last as D_BANDZ (compile.cpp short_circuit): a wave whose lanes are all false there leaves
+    the tape.  The emulator leaves at a false D_BANDZ per lane, so
+    test_queries_compile_and_match_oracle checks that the root is then 0 for that row."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "mythril_amd", "csrc"))
+    import gen_asm_core as G
+
+    from mythril_amd.tape import Op
+
+    ctx, qs = queries()
+    seen = 0
+    for name, cs in qs:
+        root, schema = lower_query(ctx.b, [c.node for c in cs])
+        cols = list(schema.columns)
+        nodes = local_tape(ctx.b, root, cols)
+        n_conj, stack = 0, [len(nodes) - 1]
+        while stack:  # the root's AND chain (single-use ANDs) as the compiler sees it
+            i = stack.pop()
+            if int(nodes[i]["op"]) == int(Op.AND):
+                stack += [int(nodes[i]["b"]), int(nodes[i]["a"])]
+            else:
+                n_conj += 1
+        ts = TapeSet(cols)
+        ts.pool = ctx.b.pool
+        for size in (0, 8, 32, 256):
+            ts.tapes[:] = [Tape(nodes if size == 0 else rematerialize(nodes, size))]
+            try:
+                w = emu.words(ts)
+                break
+            except EmuError as e:
+                assert "register pressure" in str(e), (name, str(e))
+        ops = [int(x) & 0xFF for x in w[1::2]]
+        n_z = ops.count(G.OPNUM["BANDZ"])
+        if n_conj < 2:
+            assert n_z == 0, name
+            continue
+        seen += 1
+        # conjuncts the fold or the lowering merged may be fewer than the source's
+        assert 1 <= n_z <= n_conj - 1, (name, n_z, n_conj)
+        last_and = max(i for i, o in enumerate(ops) if o in (G.OPNUM["BAND"], G.OPNUM["BANDZ"]))
+        assert ops[last_and] == G.OPNUM["BAND"], name  # the last AND needs no test
+    assert seen >= 5
