@@ -984,6 +984,7 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
     k.alt_off = as->d_guide + o_aoff;
     k.entry_col = as->d_guide + o_ecol;
     k.entry_val = as->d_guide + o_eval;
+    k.span_words = (uint32_t)(o_eval - o_prob);
     MH_HIP(mh::launch_generate_guided(as->d, as->stride, first, count, seed, global_base, k,
                                       as->ctx->stream));
     return MH_OK;

@@ -151,15 +151,30 @@ __global__ void __launch_bounds__(kBlock)
 // sets from the first one with a copy entry on run in memory, in order, on wave 0.  The one-lane-
 // per-row form stored 8 limbs per applied entry, lane-divergently, and left a 256-row launch
 // four waves: 0.20 ms per launch on average, up to 0.58 (profiles/r03h).
+// STAGED (round 5): the guide's set / alternative / entry-column arrays are copied into LDS
+// first, so a set's chain of dependent reads (its probability and alternatives, the chosen
+// alternative's entries, each entry's column) costs LDS latency instead of a global load's
+// (ET-400's 256-row launch: 304 sets, 16 waves each walking 19 of them, 70 us of mostly load
+// latency, profiles/r05f/pprof).
 constexpr u32 kLdsRows = 64;
 constexpr u32 kWaves = 16;  // a 256-row launch: 4 workgroups of 16 waves, 4 waves per SIMD
+constexpr size_t kGenLds = 64 * 1024;  // LDS of one generator workgroup at most
 
+template <bool STAGED>
 __global__ void __launch_bounds__(kLdsRows * kWaves)
     guided_lds_kernel(u32* assign, u64 stride, u64 first, u64 count, u64 seed, u64 base,
                       mh::KGuide g) {
     extern __shared__ u32 s_last[];  // [n_cols][kLdsRows]: 1 + the winning entry, 0 = none
     const u32 lane = threadIdx.x % kLdsRows, wave = threadIdx.x / kLdsRows;
     for (u32 k = threadIdx.x; k < g.n_cols * kLdsRows; k += kLdsRows * kWaves) s_last[k] = 0;
+    if constexpr (STAGED) {  // the span after the last-entry slots; the pointers rebased on it
+        u32* s_span = s_last + g.n_cols * kLdsRows;
+        for (u32 k = threadIdx.x; k < g.span_words; k += kLdsRows * kWaves) s_span[k] = g.set_prob[k];
+        g.set_off = s_span + (g.set_off - g.set_prob);
+        g.alt_off = s_span + (g.alt_off - g.set_prob);
+        g.entry_col = s_span + (g.entry_col - g.set_prob);
+        g.set_prob = s_span;
+    }
     __syncthreads();
     const u64 i = (u64)blockIdx.x * kLdsRows + lane;
     const bool live = i < count;
@@ -247,10 +262,14 @@ hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t fi
     if (count == 0) return hipSuccess;
     // LDS form while the last-entry slots (256 B per column) fit 48 KB per workgroup
     const size_t lds = (size_t)g.n_cols * kLdsRows * sizeof(u32);
-    if (g.n_cols && lds <= 48 * 1024) {
-        const u64 blocks = (count + kLdsRows - 1) / kLdsRows;
-        hipLaunchKernelGGL(guided_lds_kernel, dim3((unsigned)blocks), dim3(kLdsRows * kWaves), lds,
-                           stream, assign, stride, first, count, seed, base, g);
+    const size_t staged = lds + (size_t)g.span_words * sizeof(u32);
+    const u64 blocks = (count + kLdsRows - 1) / kLdsRows;
+    if (g.n_cols && staged <= kGenLds) {
+        hipLaunchKernelGGL(guided_lds_kernel<true>, dim3((unsigned)blocks), dim3(kLdsRows * kWaves),
+                           staged, stream, assign, stride, first, count, seed, base, g);
+    } else if (g.n_cols && lds <= 48 * 1024) {
+        hipLaunchKernelGGL(guided_lds_kernel<false>, dim3((unsigned)blocks), dim3(kLdsRows * kWaves),
+                           lds, stream, assign, stride, first, count, seed, base, g);
     } else {
         const u64 blocks = (count + kBlock - 1) / kBlock;
         hipLaunchKernelGGL(guided_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, assign,

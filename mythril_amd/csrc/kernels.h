@@ -68,6 +68,9 @@ struct KGuide {
     const uint32_t* alt_off;    // [n_alts + 1]
     const uint32_t* entry_col;  // [n_entries]
     const uint32_t* entry_val;  // x 8 limbs
+    // set_prob | set_off | alt_off | entry_col lie back to back from set_prob (span_words
+    // words): the generator stages them in LDS when they fit
+    uint32_t span_words;
 };
 hipError_t launch_generate_guided(uint32_t* assign, uint64_t stride, uint64_t first,
                                   uint64_t count, uint64_t seed, uint64_t base, const KGuide& g,

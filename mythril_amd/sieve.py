@@ -23,6 +23,7 @@ behaviour is kept on every error (SURVEY.md §5 "fail closed").
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from collections import OrderedDict
@@ -416,7 +417,7 @@ class Sieve:
     """A device context plus reusable buffers; one per thread (handles are not shared)."""
 
     def __init__(self, device: int = 0, rows: int = 1 << 16, max_rounds: int = 2,
-                 seed: int = 0x5EED5EED, budget_s: float = 0.25, first_rows: int = 256,
+                 seed: int = 0x5EED5EED, budget_s: float = 0.25, first_rows: Optional[int] = None,
                  native_query: bool = True, second_round: Optional[str] = None):
         self.ctx = native.Context(device)
         # host stages by the native query compiler (csrc/query.cpp); False: the Python stages
@@ -428,6 +429,8 @@ class Sieve:
         # the harvested guide usually solves a LASER query in its first rows (round 1 found every
         # SAT witness of tests/laser_like.py within the first 16 rows): a small first round
         # answers those at a fraction of the latency, the full-size rounds follow
+        if first_rows is None:  # SIEVE_FIRST_ROWS overrides the default (measurements)
+            first_rows = int(os.environ.get("SIEVE_FIRST_ROWS", "256"))
         self.first_rows = min(first_rows, rows)
         # a miss pays every round before z3 runs (an infeasible JUMPI branch, svm.py:257-262):
         # one 2^16-row round after the guided 256 keeps a miss near 1 ms of device time
@@ -437,8 +440,6 @@ class Sieve:
         # when the rounds after the first run (SIEVE_ROUND2 overrides): "always"; "progress" --
         # only when the first round solved some of the query's groups but not all (a query
         # whose first round found nothing at all is left to the fallback at once); "never"
-        import os
-
         self.second_round = second_round or os.environ.get("SIEVE_ROUND2", "always")
         if self.second_round not in ("always", "progress", "never"):
             raise ValueError("second_round must be always / progress / never")

@@ -32,6 +32,8 @@
 #             interpreter's LOADVAR prefetch (scripts/build_variant.sh nopf MH_GEN_LV_PREFETCH=0)
 #   scab      paths and queries (9 reps) with the interpreter's short-circuit conjunctions off
 #             (MH_INTERP_SC=0) and in the conjuncts' given order (MH_INTERP_SC=given)
+#   rows1     paths, queries (9 reps) and planted recall with first rounds of 256 / 4096 / 16384
+#             rows (SIEVE_FIRST_ROWS)
 #   qpmc      scripts/qprofile_pmc.sh <tag> (PMC passes of the query-path kernels)
 #   qpmcnopf  the same on the no-prefetch variant library
 #   occupancy bench.py at 168 and 256 VGPRs (3 and 2 waves per SIMD; the LDS-resident compaction
@@ -86,6 +88,10 @@ for step in "$@"; do
     scab)     for sc in 0 given; do \
                 MH_INTERP_SC=$sc timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_sc$sc.jsonl" 2> "$OUT/path_scaling_sc$sc.log" && \
                 MH_INTERP_SC=$sc SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_sc$sc.jsonl" 2> "$OUT/sieve_queries_sc$sc.log" || exit 1; done ;;
+    rows1)    for fr in 256 4096 16384; do \
+                SIEVE_FIRST_ROWS=$fr timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_fr$fr.jsonl" 2> "$OUT/path_scaling_fr$fr.log" && \
+                SIEVE_FIRST_ROWS=$fr SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_fr$fr.jsonl" 2> "$OUT/sieve_queries_fr$fr.log" && \
+                SIEVE_FIRST_ROWS=$fr timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_fr$fr.jsonl" 2> "$OUT/planted_recall_fr$fr.log" || exit 1; done ;;
     qpmc)     bash scripts/qprofile_pmc.sh "$TAG" ;;
     qpmcnopf) MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_nopf.so bash scripts/qprofile_pmc.sh "${TAG}_nopf" ;;
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
