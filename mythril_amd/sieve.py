@@ -428,9 +428,12 @@ class Sieve:
         self.rows = rows
         # the harvested guide usually solves a LASER query in its first rows (round 1 found every
         # SAT witness of tests/laser_like.py within the first 16 rows): a small first round
-        # answers those at a fraction of the latency, the full-size rounds follow
+        # answers those at a fraction of the latency, the full-size rounds follow.  4096 rows
+        # (64 waves, one per SIMD of 64 CUs) take the 256-row round's time -- a short round is
+        # latency-bound per wave -- and find in round 1 most of what round 2 found after 256
+        # (planted random paths: 179 -> 60 round-2-only hits, profiles/r05g)
         if first_rows is None:  # SIEVE_FIRST_ROWS overrides the default (measurements)
-            first_rows = int(os.environ.get("SIEVE_FIRST_ROWS", "256"))
+            first_rows = int(os.environ.get("SIEVE_FIRST_ROWS", "4096"))
         self.first_rows = min(first_rows, rows)
         # a miss pays every round before z3 runs (an infeasible JUMPI branch, svm.py:257-262):
         # one 2^16-row round after the guided 256 keeps a miss near 1 ms of device time
@@ -439,8 +442,11 @@ class Sieve:
         self.max_rounds = max_rounds
         # when the rounds after the first run (SIEVE_ROUND2 overrides): "always"; "progress" --
         # only when the first round solved some of the query's groups but not all (a query
-        # whose first round found nothing at all is left to the fallback at once); "never"
-        self.second_round = second_round or os.environ.get("SIEVE_ROUND2", "always")
+        # whose first round found nothing at all is left to the fallback at once); "never".
+        # Default "progress": a first round that solves no group is almost always an UNSAT query
+        # (EtherThief's UNSAT variant: 0.73 -> 0.45 ms, 400 constraints 2.48 -> 1.78 ms) and
+        # the planted-SAT paths lose 2 of 2449 LASER-family answers (profiles/r05h)
+        self.second_round = second_round or os.environ.get("SIEVE_ROUND2", "progress")
         if self.second_round not in ("always", "progress", "never"):
             raise ValueError("second_round must be always / progress / never")
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)

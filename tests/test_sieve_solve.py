@@ -89,7 +89,9 @@ def test_shared_keccak_manager_outcomes_on_fake_device(monkeypatch, native_query
 def test_refuted_query_skips_the_device(monkeypatch):
     """A query that contradicts itself (MH_QUERY_REFUTED: KillBilly's third sender pinned to two
     actors, an overflow of two words below 2^128) is a miss without a device round; an UNSAT
-    query neither syntax nor ranges refute (ether_thief_unsat) still runs its rounds and misses."""
+    query neither syntax nor ranges refute (ether_thief_unsat) still runs its first round and
+    misses -- and only that round by default (second_round "progress": its first round solved
+    no group), both rounds under "always"."""
     from tests.laser_like import hard_queries
 
     fake_device.install(monkeypatch)
@@ -103,8 +105,13 @@ def test_refuted_query_skips_the_device(monkeypatch):
     assert s.solve(ctx.b, [c.node for c in cs]) is None
     assert s.stats.rounds == r0 and s.stats.extra.get("refuted") == 2
     cs = dict(qs)["ether_thief_unsat"]
+    assert s.second_round == "progress"
     assert s.solve(ctx.b, [c.node for c in cs]) is None
-    assert s.stats.rounds == r0 + 2 and s.stats.misses == 3
+    assert s.stats.rounds == r0 + 1 and s.stats.misses == 3
+    assert s.stats.extra.get("round2_skipped") == 1
+    s.second_round = "always"
+    assert s.solve(ctx.b, [c.node for c in cs]) is None
+    assert s.stats.rounds == r0 + 3 and s.stats.misses == 4
 
 
 def test_later_round_runs_only_unsolved_groups(monkeypatch):
