@@ -45,6 +45,7 @@ PREFETCH = SMEM_INSNS and os.environ.get("MH_GEN_PREFETCH", "1") != "0"
 # constants, so a constant-operand handler copies them from the bank instead of loading
 # (MH_GEN_PREFETCH_CONSTS=0: constants by their own s_load_dwordx8)
 PREFETCH_CONSTS = PREFETCH and SMEM_CONSTS and os.environ.get("MH_GEN_PREFETCH_CONSTS", "1") != "0"
+WINDOW = 64         # dev_isa.h MH_WINDOW
 NSLOTS = 128        # op byte < 128 (dev_isa.h static_assert)
 # D_LOADVAR (a column beyond the preloaded ones) in the core, as 8 global loads, instead of an
 # exit to the C++ driver (~1 us of a wave's time per exit); only in the
@@ -61,6 +62,13 @@ CORE_COMPLEX = {D_LOADVAR: "LOADVAR", D_UADD_NOOVFL: "UADD_NOOVFL"}
 # prefetch lives within one run of the core: every exit drains it (s_waitcnt vmcnt(0)) and an
 # entry starts with none in flight.
 LV_PREFETCH = LOADVAR and os.environ.get("MH_GEN_LV_PREFETCH", "1") != "0"
+# D_WINDOW inside the core (round 5): ip counts slots from the tape's first one and gwin is the
+# tape's base, so a window change is ip = next multiple of 64 and the next words' scalar load --
+# not an exit to the C++ driver, which reloaded its lane-held window from memory and re-entered
+# the core (a round trip per 64 slots: 70 on EtherThief-400's tape).  Needs the words and
+# constants by scalar loads (the lane-held window is then only the C++ driver's).
+CORE_WINDOW = SMEM_INSNS and SMEM_CONSTS and os.environ.get("MH_GEN_CORE_WINDOW", "1") != "0"
+D_WINDOW = 120      # dev_isa.h (static_assert in the .inc)
 LV_NONE = 0xFFFF
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
@@ -298,6 +306,11 @@ class Core:
         off = self.idx_off()
         if name == "EXIT":
             return ["s_branch L_out_%="]
+        if name == "WINDOW":
+            # the next window starts at the next multiple of 64 slots; its words are loaded by
+            # the dispatch (no static advance: resolve() must not prefetch from the old ip)
+            return ["s_add_u32 %[ip], %[ip], {}".format(WINDOW),
+                    "s_andn2_b32 %[ip], %[ip], {}".format(WINDOW - 1)] + self.dispatch(0)
         if name == "LOADVAR":
             # X = column aux of this lane's row: limb k at vbase + ((8 col + k) cap4) + voff
             # (SoA planes, KParams::assign); the address is SALU arithmetic in s[56:57] (no
@@ -804,6 +817,8 @@ class Core:
         for i in range(NSLOTS):
             lines.append(".org L_tab_%= + {}".format(i * SLOT))
             name = OPS[i] if i < len(OPS) else "EXIT"
+            if CORE_WINDOW and i == D_WINDOW:
+                name = "WINDOW"
             if self.loadvar and i in CORE_COMPLEX:
                 name = CORE_COMPLEX[i]
             h = self.handler(name)
@@ -853,6 +868,9 @@ def emit(out):
     w("static_assert(D_NUM_ASM == {}, \"asm core covers every asm op\");\n".format(len(OPS)))
     w("static_assert(D_LOADVAR == {}, \"asm core LOADVAR slot\");\n".format(D_LOADVAR))
     w("static_assert(D_UADD_NOOVFL == {}, \"asm core UADD_NOOVFL slot\");\n".format(D_UADD_NOOVFL))
+    w("static_assert(D_WINDOW == {} && MH_WINDOW == {}, \"asm core WINDOW slot\");\n".format(D_WINDOW, WINDOW))
+    # ip of the run functions: slot index from the tape's first slot (1) or in the window (0)
+    w("#define MH_ASM_CORE_WINDOW {}\n".format(int(CORE_WINDOW)))
     w("#define MH_ASM_LOADVAR {}\n\n".format(int(LOADVAR)))
     w("template <int NR> struct AsmCore;\n\n")
     for nr in (7, 9, 15):

@@ -115,17 +115,39 @@ __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, I
     u32 win = 0, ip = 0;
     for (;;) {
 #if MH_ASM_CORE
+        // MH_ASM_CORE_WINDOW: the core takes the slot from the tape's first one and changes
+        // windows itself; the lane-held window ic is reloaded here only when it came back in
+        // another window than it left
+        const u32 at = MH_ASM_CORE_WINDOW ? win + ip : ip;
+        const uint2* base = MH_ASM_CORE_WINDOW ? gsrc : gsrc + win;
+        u32 back;
         if constexpr (FEAT != 0 && MH_ASM_LOADVAR) {
             // columns beyond the preloaded ones load inside the core (no exit per LOADVAR);
             // launch_sieve keeps capacity * 4 within 32 bits
             const u64 a = (u64)(uintptr_t)m.p->assign;
-            ip = AsmCore<NR>::run_lv(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
-                                     m.R.p7, ic.w0, ic.w1, ip, gsrc + win, (u32)a,
-                                     (u32)(a >> 32), (u32)(m.p->capacity * 4u),
-                                     (u32)m.lrow * 4u);
+            back = AsmCore<NR>::run_lv(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
+                                       m.R.p7, ic.w0, ic.w1, at, base, (u32)a,
+                                       (u32)(a >> 32), (u32)(m.p->capacity * 4u),
+                                       (u32)m.lrow * 4u);
         } else {
-            ip = AsmCore<NR>::run(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
-                                  m.R.p7, ic.w0, ic.w1, ip, gsrc + win);
+            back = AsmCore<NR>::run(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
+                                    m.R.p7, ic.w0, ic.w1, at, base);
+        }
+        if (MH_ASM_CORE_WINDOW) {
+            const u32 w = back & ~(u32)(MH_WINDOW - 1);
+            if (w != win) {
+                win = w;
+                const u32 j = win + (threadIdx.x & 63u);
+                ic.w0 = ic.w1 = 0u;
+                if (j < n) {
+                    const uint2 v = src[j];
+                    ic.w0 = v.x;
+                    ic.w1 = v.y;
+                }
+            }
+            ip = back - win;
+        } else {
+            ip = back;
         }
 #endif
         const u32 w0 = __builtin_amdgcn_readlane(ic.w0, ip);

@@ -30,6 +30,8 @@
 #             gated on first-round progress (SIEVE_ROUND2=always / progress), back to back
 #   nopf      interp, paths and queries (9 reps) on the variant library built without the
 #             interpreter's LOADVAR prefetch (scripts/build_variant.sh nopf MH_GEN_LV_PREFETCH=0)
+#   ab_<v>    the same on any variant library mythril_amd/libmythril_hip_<v>.so
+#             (scripts/build_variant.sh <v> GENERATOR_SWITCH=...)
 #   scab      paths and queries (9 reps) with the interpreter's short-circuit conjunctions off
 #             (MH_INTERP_SC=0) and in the conjuncts' given order (MH_INTERP_SC=given)
 #   rows1     paths, queries (9 reps) and planted recall with first rounds of 256 / 4096 / 16384
@@ -80,10 +82,10 @@ for step in "$@"; do
     policy)   for pol in always progress; do \
                 SIEVE_ROUND2=$pol SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_$pol.jsonl" 2> "$OUT/sieve_queries_$pol.log" && \
                 SIEVE_ROUND2=$pol timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_$pol.jsonl" 2> "$OUT/path_scaling_$pol.log" || exit 1; done ;;
-    nopf)     export MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_nopf.so && \
-              timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost_nopf.jsonl" 2> "$OUT/interp_op_cost_nopf.log" && \
-              timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_nopf.jsonl" 2> "$OUT/path_scaling_nopf.log" && \
-              SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_nopf.jsonl" 2> "$OUT/sieve_queries_nopf.log"; \
+    nopf|ab_*) V=${step#ab_}; export MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_$V.so && \
+              timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost_$V.jsonl" 2> "$OUT/interp_op_cost_$V.log" && \
+              timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_$V.jsonl" 2> "$OUT/path_scaling_$V.log" && \
+              SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_$V.jsonl" 2> "$OUT/sieve_queries_$V.log"; \
               rc=$?; unset MYTHRIL_HIP_LIB; (exit $rc) ;;
     scab)     for sc in 0 given; do \
                 MH_INTERP_SC=$sc timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_sc$sc.jsonl" 2> "$OUT/path_scaling_sc$sc.log" && \

@@ -291,3 +291,30 @@ def test_loadvar_slot_matches_isa_header():
     after = re.findall(r"\b(D_[A-Z0-9_]+)\b", body.replace("= D_FIRST_COMPLEX", ""))
     assert 112 + after.index("D_LOADVAR") == G.D_LOADVAR
     assert 112 + after.index("D_UADD_NOOVFL") == G.D_UADD_NOOVFL
+
+
+@pytest.mark.parametrize("nr", [7, 9, 15])
+def test_window_change_stays_in_the_core(nr):
+    """With CORE_WINDOW the D_WINDOW slot of the table holds a handler that moves ip to the next
+    multiple of 64 slots (ip counts from the tape's first slot) and dispatches there -- the C++
+    driver sees a window change only when the core leaves for another reason."""
+    if not G.CORE_WINDOW:
+        pytest.skip("generator built without CORE_WINDOW")
+    core = G.Core(nr)
+    h = core.handler("WINDOW")
+    assert h[:2] == ["s_add_u32 %[ip], %[ip], 64", "s_andn2_b32 %[ip], %[ip], 63"]
+    assert h[-1] == "s_setpc_b64 s[46:47]" and not any("L_out" in ln for ln in h)
+    # the words are loaded at the new ip, after it is set (no prefetch from the old one)
+    loads = [i for i, ln in enumerate(h) if ln.startswith("s_load_dword")]
+    assert len(loads) == 1 and loads[0] > 1 and h[loads[0] - 1] == "s_lshl_b32 s44, %[ip], 3"
+    text = core.asm_text()
+    at = text.index(".org L_tab_%= + {}".format(G.D_WINDOW * G.SLOT))
+    assert text[at + 1:at + 1 + len(h)] == h
+    if os.path.exists(LLVM_MC):
+        src = "\n".join(_asm_lines(h)) + "\n"
+        p = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "-show-encoding"],
+                           input=src, capture_output=True, text=True)
+        assert p.returncode == 0, p.stderr[:400]
+        size = sum(len(re.findall(r"0x[0-9a-f]{2}", m))
+                   for m in re.findall(r"encoding: \[(.*?)\]", p.stdout))
+        assert 0 < size <= G.SLOT
