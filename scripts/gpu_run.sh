@@ -9,7 +9,8 @@
 #   miss      scripts/miss_cost.py (per-stage cost of sieve misses, JIT build vs interpreter)
 #   queries   scripts/sieve_queries.py (per-query latency, LASER order and cold)
 #   latency   two more passes of sieve_queries.py at 9 repetitions (sieve_queries_{a,b}.jsonl)
-#   interp    scripts/interp_op_cost.py (interpreter cost of a loaded column / a complex op)
+#   interp    scripts/interp_op_cost.py (interpreter cost of a loaded column / a complex op;
+#             MH_INTERP_SC=0: its conjunctions are false on random rows, the ops are the point)
 #   counters  rocprofv3 -L (the PMC counters this box offers)
 #   profile   scripts/profile.sh <tag> (kernel trace + PMC passes of the default bench)
 #   kbench    bench.py --variant keccak (config 4's kernel, 2^20 rows)
@@ -21,6 +22,7 @@
 #   pypaths   paths with the Python host stages
 #   qcost     scripts/query_cost.py (host stages per query, native compiler vs Python)
 #   qprofile  rocprofv3 kernel trace + stats of one pass of sieve_queries.py (query-path kernels)
+#   pprof4    pprofile for the default and the nowin variant library at 256 / 4096 first rows
 #   pprofile  rocprofv3 kernel trace + stats of path_scaling.py at 400 constraints
 #   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
 #   recall    scripts/planted_recall.py (recall on planted-SAT paths, per round and shape class)
@@ -60,7 +62,7 @@ for step in "$@"; do
                 > "$OUT/sieve_queries_a.jsonl" 2> "$OUT/a.log" && \
               SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py \
                 > "$OUT/sieve_queries_b.jsonl" 2> "$OUT/b.log" ;;
-    interp)   timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost.jsonl" 2> "$OUT/interp_op_cost.log" ;;
+    interp)   MH_INTERP_SC=0 timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost.jsonl" 2> "$OUT/interp_op_cost.log" ;;
     counters) timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 ;;
     profile)  bash scripts/profile.sh "$TAG" ;;
     kbench)   timeout -k 10 400 python -u bench.py --variant keccak --cpu-seconds 5 > "$OUT/bench_keccak.json" 2> "$OUT/bench_keccak.log" ;;
@@ -83,7 +85,7 @@ for step in "$@"; do
                 SIEVE_ROUND2=$pol SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_$pol.jsonl" 2> "$OUT/sieve_queries_$pol.log" && \
                 SIEVE_ROUND2=$pol timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_$pol.jsonl" 2> "$OUT/path_scaling_$pol.log" || exit 1; done ;;
     nopf|ab_*) V=${step#ab_}; export MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_$V.so && \
-              timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost_$V.jsonl" 2> "$OUT/interp_op_cost_$V.log" && \
+              MH_INTERP_SC=0 timeout -k 10 300 python -u scripts/interp_op_cost.py > "$OUT/interp_op_cost_$V.jsonl" 2> "$OUT/interp_op_cost_$V.log" && \
               timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_$V.jsonl" 2> "$OUT/path_scaling_$V.log" && \
               SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_$V.jsonl" 2> "$OUT/sieve_queries_$V.log"; \
               rc=$?; unset MYTHRIL_HIP_LIB; (exit $rc) ;;
@@ -99,6 +101,10 @@ for step in "$@"; do
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;
+    pprof4)   for v in "" nowin; do for fr in 256 4096; do \
+                lib=$PWD/mythril_amd/libmythril_hip${v:+_$v}.so; tag=pprof${v:+_$v}_fr$fr; \
+                MYTHRIL_HIP_LIB=$lib SIEVE_FIRST_ROWS=$fr timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$tag" -o $tag -- \
+                  python -u scripts/path_scaling.py 400 > "$OUT/$tag.jsonl" 2> "$OUT/$tag.log" || exit 1; done; done ;;
     pprofile) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pprof" -o pprof -- \
                 python -u scripts/path_scaling.py 400 > "$OUT/pprof.jsonl" 2> "$OUT/pprof.log" ;;
     gather)   timeout -k 10 300 python -u scripts/gather_bench.py > "$OUT/gather.jsonl" 2> "$OUT/gather.log" ;;
