@@ -453,8 +453,9 @@ int32_t mh_comm_destroy(mh_ctx* ctx);
  * accumulator, 26 v_add_u32, 27 v_addc_co_u32 through VCC, 28 two v_mad_u64_u32 accumulators
  * interleaved, 29 v_mad_u64_u32 + v_addc carry count (product scanning), 30 v_cmp + v_cndmask;
  * mixed classes (independent): 31 v_mad_u64_u32 / v_add_u32 alternating, 32 v_addc_co_u32
- * chains / v_xor_b32 alternating, 33 two v_mad_u64_u32 per two v_add_u32.                    */
-#define MH_MB_NUM_KINDS 34
+ * chains / v_xor_b32 alternating, 33 two v_mad_u64_u32 per two v_add_u32; gfx950's
+ * v_bitop3_b32: 34 alone (x ^ (~y & z)), 35 alternating with v_alignbit_b32.                    */
+#define MH_MB_NUM_KINDS 36
 int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
                             double* lane_ops_per_s);
 /* Survivor-gather micro-benchmark (the memory side of the lane compaction costed in DESIGN.md

@@ -521,6 +521,17 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink
                                  "v_add_u32 %0, %0, %5\n v_add_u32 %1, %1, %5\n")
                              : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a6), "v"(y)
                              : "s20", "s21", "s22", "s23", "v40", "v41", "v42", "v43");
+            // gfx950's 3-input bitwise op (truth table 0xd2: x ^ (~y & z), Keccak's chi)
+            if constexpr (KIND == 34)
+                asm volatile(MB8("v_bitop3_b32 %0, %0, %8, %4 bitop3:0xd2\n v_bitop3_b32 %1, %1, %8, %5 bitop3:0xd2\n"
+                                 "v_bitop3_b32 %2, %2, %8, %6 bitop3:0xd2\n v_bitop3_b32 %3, %3, %8, %7 bitop3:0xd2\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y));
+            if constexpr (KIND == 35)  // v_bitop3_b32 / v_alignbit_b32 alternating (theta + rho)
+                asm volatile(MB8("v_bitop3_b32 %0, %0, %8, %4 bitop3:0x96\n v_alignbit_b32 %1, %1, %5, 7\n"
+                                 "v_bitop3_b32 %2, %2, %8, %6 bitop3:0x96\n v_alignbit_b32 %3, %3, %7, 9\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y));
             // partial EXEC masks: does the SIMD skip lane groups that are all inactive?
             if constexpr (KIND >= 21 && KIND <= 24) {
                 constexpr uint64_t kExec = KIND == 21 || KIND == 22 ? 0x00000000FFFFFFFFull
@@ -656,7 +667,8 @@ hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uin
         MB_CASE(8) MB_CASE(9) MB_CASE(10) MB_CASE(11) MB_CASE(12) MB_CASE(13) MB_CASE(14)
         MB_CASE(15) MB_CASE(16) MB_CASE(17) MB_CASE(18) MB_CASE(19) MB_CASE(20)
         MB_CASE(21) MB_CASE(22) MB_CASE(23) MB_CASE(24) MB_CASE(25) MB_CASE(26) MB_CASE(27)
-        MB_CASE(28) MB_CASE(29) MB_CASE(30) MB_CASE(31) MB_CASE(32) MB_CASE(33)
+        MB_CASE(28) MB_CASE(29) MB_CASE(30) MB_CASE(31) MB_CASE(32) MB_CASE(33) MB_CASE(34)
+        MB_CASE(35)
 #undef MB_CASE
         default: return hipErrorInvalidValue;
     }

@@ -137,7 +137,7 @@ MB_KINDS = ("add_co_chain", "mad_u64_u32", "add_u32", "xor_b32", "alignbit_b32",
             "xnor_b32", "and_b32", "or_b32", "not_b32", "xor_exec32", "alignbit_exec32",
             "xor_exec16", "xor_exec_alt", "dep_mad_u64_u32", "dep_add_u32", "dep_addc_vcc",
             "dep_mad_2chains", "dep_mad_carry", "dep_cmp_cndmask", "mix_mad_add", "mix_addc_xor",
-            "mix_mad2_add2")
+            "mix_mad2_add2", "bitop3_b32", "mix_bitop3_alignbit")
 
 
 class NativeUnavailable(RuntimeError):
