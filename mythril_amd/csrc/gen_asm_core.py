@@ -69,6 +69,11 @@ LV_PREFETCH = LOADVAR and os.environ.get("MH_GEN_LV_PREFETCH", "1") != "0"
 # constants by scalar loads (the lane-held window is then only the C++ driver's).
 CORE_WINDOW = SMEM_INSNS and SMEM_CONSTS and os.environ.get("MH_GEN_CORE_WINDOW", "1") != "0"
 D_WINDOW = 120      # dev_isa.h (static_assert in the .inc)
+# ... and the window after the one the core enters is pulled into the caches by one vector load
+# of its 64 slots (8 B per lane, into 2 VGPRs nobody reads), issued at the window change and at
+# entry: the slots' scalar loads then hit L2 instead of each 64-byte line missing in turn (the
+# C++ driver's window reload did this by accident; without it the in-core change was slower)
+WIN_PREFETCH = CORE_WINDOW and os.environ.get("MH_GEN_WIN_PREFETCH", "1") != "0"
 LV_NONE = 0xFFFF
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
@@ -142,6 +147,27 @@ class Core:
     def PF(self, k):  # run_lv: the column LOADVAR prefetched (8 VGPRs after the scratch)
         assert 0 <= k < 8
         return "v%d" % (self.sb + N_SCRATCH + k)
+
+    def WP(self):  # the window prefetch's destination pair (after PF; never read)
+        r = self.sb + N_SCRATCH + N_PF
+        return "v[{}:{}]".format(r, r + 1)
+
+    def win_prefetch(self):
+        """One vector load of the 64 slots from slot S_T on (lane j: slot min(S_T + j, n - 1), so
+        nothing past the tape's last slot is read), when S_T is inside the tape; no wait."""
+        if not WIN_PREFETCH:
+            return []
+        t = self.S(0)
+        return ["s_cmp_lt_u32 {}, %[nsl]".format(S_T),
+                "s_cbranch_scc0 L_wpf_%=_{}".format(self._wpf),
+                "v_mbcnt_lo_u32_b32 {}, -1, 0".format(t),
+                "v_mbcnt_hi_u32_b32 {0}, -1, {0}".format(t),
+                "v_add_u32 {0}, {1}, {0}".format(t, S_T),
+                "s_sub_u32 {}, %[nsl], 1".format(S_T),
+                "v_min_u32 {0}, {1}, {0}".format(t, S_T),
+                "v_lshlrev_b32 {0}, 3, {0}".format(t),
+                "global_load_dwordx2 {}, {}, %[gwin]".format(self.WP(), t),
+                "L_wpf_%=_{}:".format(self._wpf)]
 
     def lv_address(self, col_sgpr):
         """s[56:57] = address of limb 0 of column `col_sgpr` (SoA planes: vbase + 8 col cap4); the
@@ -308,9 +334,13 @@ class Core:
             return ["s_branch L_out_%="]
         if name == "WINDOW":
             # the next window starts at the next multiple of 64 slots; its words are loaded by
-            # the dispatch (no static advance: resolve() must not prefetch from the old ip)
-            return ["s_add_u32 %[ip], %[ip], {}".format(WINDOW),
-                    "s_andn2_b32 %[ip], %[ip], {}".format(WINDOW - 1)] + self.dispatch(0)
+            # the dispatch (no static advance: resolve() must not prefetch from the old ip);
+            # the window after it is prefetched
+            self._wpf = "w"
+            return (["s_add_u32 %[ip], %[ip], {}".format(WINDOW),
+                     "s_andn2_b32 %[ip], %[ip], {}".format(WINDOW - 1),
+                     "s_add_u32 {}, %[ip], {}".format(S_T, WINDOW)] + self.win_prefetch() +
+                    self.dispatch(0))
         if name == "LOADVAR":
             # X = column aux of this lane's row: limb k at vbase + ((8 col + k) cap4) + voff
             # (SoA planes, KParams::assign); the address is SALU arithmetic in s[56:57] (no
@@ -811,6 +841,10 @@ class Core:
                  "s_addc_u32 {0}, {0}, 0".format(S_TAB_HI)]
         if self.loadvar and LV_PREFETCH:  # nothing in flight on entry
             lines.append("s_mov_b32 {}, 0x{:x}".format(S_PFC, LV_NONE))
+        if WIN_PREFETCH:  # the window after the one the core starts in
+            self._wpf = "e"
+            lines += ["s_andn2_b32 {}, %[ip], {}".format(S_T, WINDOW - 1),
+                      "s_add_u32 {0}, {0}, {1}".format(S_T, WINDOW)] + self.win_prefetch()
         lines += self.resolve(self.dispatch(0))
         lines += [".p2align 8", "L_tab_%=:"]
         bodies = []
@@ -829,13 +863,21 @@ class Core:
                 lines += h
         lines += [".org L_tab_%= + {}".format(NSLOTS * SLOT)] + bodies + self.resolve(self.div_body())
         lines += ["L_out_%=:"]
-        if self.loadvar and LV_PREFETCH:  # a prefetch still in flight lands before the exit
+        if (self.loadvar and LV_PREFETCH) or WIN_PREFETCH:  # prefetches land before the exit
             lines.append("s_waitcnt vmcnt(0)")
         return lines
 
 
 N_SCRATCH = 32  # S0..S31, declared clobbered by the core (division uses all 32)
 N_PF = 8        # run_lv with LV_PREFETCH: the prefetched column, after the scratch
+
+
+def n_scratch(core):
+    """VGPRs after the planes a core's asm text may name: the scratch, the LOADVAR prefetch's 8
+    (run_lv), the window prefetch's pair (after them)."""
+    if WIN_PREFETCH:
+        return N_SCRATCH + N_PF + 2
+    return N_SCRATCH + (N_PF if core.loadvar and LV_PREFETCH else 0)
 
 
 def check_registers(core, lines, n_scratch):
@@ -888,7 +930,7 @@ def emit(out):
             forms.append((Core(nr, loadvar=True), "run_lv",
                           ", u32 vlo, u32 vhi, u32 cap4, u32 voff"))
         for core, fname, extra in forms:
-            n_scr = N_SCRATCH + (N_PF if core.loadvar and LV_PREFETCH else 0)
+            n_scr = n_scratch(core)
             clob = ["\"v{}\"".format(c.sb + j) for j in range(n_scr)] + \
                    ["\"{}\"".format(s) for s in SGPR_CLOBBERS] + ["\"vcc\"", "\"scc\"", "\"m0\""]
             w("    // runs asm-core instructions from slot ip of the window (ic0, ic1); returns the\n")
@@ -898,12 +940,12 @@ def emit(out):
                 w("    // this lane's row at byte offset voff)\n")
             w("    __device__ __forceinline__ static u32 {}(plane_t& p0, plane_t& p1, plane_t& p2,\n".format(fname))
             w("            plane_t& p3, plane_t& p4, plane_t& p5, plane_t& p6, plane_t& p7, u32 ic0,\n")
-            w("            u32 ic1, u32 ip, const void* gwin{}) {{\n".format(extra))
+            w("            u32 ic1, u32 ip, const void* gwin, u32 nsl{}) {{\n".format(extra))
             w("        asm volatile(\n")
             for line in core.asm_text():
                 w("            \"{}\\n\"\n".format(line))
             w("            : {}, [ip] \"+s\"(ip)\n".format(", ".join(cons)))
-            ins = "[ic0] \"v\"(ic0), [ic1] \"v\"(ic1), [gwin] \"s\"(gwin)"
+            ins = "[ic0] \"v\"(ic0), [ic1] \"v\"(ic1), [gwin] \"s\"(gwin), [nsl] \"s\"(nsl)"
             if extra:
                 ins += (", [vlo] \"s\"(vlo), [vhi] \"s\"(vhi), [cap4] \"s\"(cap4), "
                         "[voff] \"v\"(voff)")

@@ -126,12 +126,12 @@ __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, I
             // launch_sieve keeps capacity * 4 within 32 bits
             const u64 a = (u64)(uintptr_t)m.p->assign;
             back = AsmCore<NR>::run_lv(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
-                                       m.R.p7, ic.w0, ic.w1, at, base, (u32)a,
+                                       m.R.p7, ic.w0, ic.w1, at, base, n, (u32)a,
                                        (u32)(a >> 32), (u32)(m.p->capacity * 4u),
                                        (u32)m.lrow * 4u);
         } else {
             back = AsmCore<NR>::run(m.R.p0, m.R.p1, m.R.p2, m.R.p3, m.R.p4, m.R.p5, m.R.p6,
-                                    m.R.p7, ic.w0, ic.w1, at, base);
+                                    m.R.p7, ic.w0, ic.w1, at, base, n);
         }
         if (MH_ASM_CORE_WINDOW) {
             const u32 w = back & ~(u32)(MH_WINDOW - 1);

@@ -22,7 +22,8 @@
 #   pypaths   paths with the Python host stages
 #   qcost     scripts/query_cost.py (host stages per query, native compiler vs Python)
 #   qprofile  rocprofv3 kernel trace + stats of one pass of sieve_queries.py (query-path kernels)
-#   pprof4    pprofile for the default and the nowin variant library at 256 / 4096 first rows
+#   pprof4    pprofile for the default and variant libraries ($PV, default nowin) at first-round
+#             sizes $PFR (default 256 4096)
 #   bitop3    scripts/valu_peak.py for v_bitop3_b32 beside xor / alignbit / cndmask
 #   pprofile  rocprofv3 kernel trace + stats of path_scaling.py at 400 constraints
 #   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
@@ -102,7 +103,7 @@ for step in "$@"; do
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \
                 python -u scripts/sieve_queries.py > "$OUT/qprof.jsonl" 2> "$OUT/qprof.log" ;;
-    pprof4)   for v in "" nowin; do for fr in 256 4096; do \
+    pprof4)   for v in "" ${PV:-nowin}; do for fr in ${PFR:-256 4096}; do \
                 lib=$PWD/mythril_amd/libmythril_hip${v:+_$v}.so; tag=pprof${v:+_$v}_fr$fr; \
                 MYTHRIL_HIP_LIB=$lib SIEVE_FIRST_ROWS=$fr timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$tag" -o $tag -- \
                   python -u scripts/path_scaling.py 400 > "$OUT/$tag.jsonl" 2> "$OUT/$tag.log" || exit 1; done; done ;;

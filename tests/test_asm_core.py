@@ -29,7 +29,7 @@ def _asm_lines(lines):
     for ln in lines:
         ln = (ln.replace("%[ip]", "s39").replace("%[ic0]", "v200").replace("%[ic1]", "v201")
               .replace("%[gwin]", "s[80:81]").replace("%[voff]", "v202")
-              .replace("%[vlo]", "s36").replace("%[vhi]", "s37").replace("%[cap4]", "s38")
+              .replace("%[vlo]", "s36").replace("%[vhi]", "s37").replace("%[cap4]", "s38").replace("%[nsl]", "s34")
               .replace("%=", "0"))
         if ln.endswith(":"):
             continue
@@ -77,7 +77,7 @@ def test_gpr_index_mode_is_balanced(nr):
 @pytest.mark.parametrize("nr", [7, 9, 15])
 def test_registers_are_declared(nr):
     core = G.Core(nr)
-    G.check_registers(core, core.asm_text(), G.N_SCRATCH)
+    G.check_registers(core, core.asm_text(), G.n_scratch(core))
 
 
 def test_opcode_table_matches_isa_header():
@@ -238,7 +238,7 @@ def test_loadvar_handler(nr):
         # every run starts with nothing in flight and drains the prefetch before it exits
         assert text[text.index("L_out_%=:") + 1] == "s_waitcnt vmcnt(0)"
         assert "s_mov_b32 {}, 0x{:x}".format(G.S_PFC, G.LV_NONE) in text[:8]
-        G.check_registers(core, text, G.N_SCRATCH + G.N_PF)
+        G.check_registers(core, text, G.n_scratch(core))
     else:
         assert loads == own
         assert lines.index("s_waitcnt vmcnt(0)") > lines.index(loads[-1])
@@ -252,7 +252,7 @@ def test_loadvar_handler(nr):
     slot = plain.index(".org L_tab_%= + {}".format(G.D_LOADVAR * G.SLOT))
     assert plain[slot + 1] == "s_branch L_out_%=" and not any("%[voff]" in ln for ln in plain)
     if not G.LV_PREFETCH:
-        G.check_registers(core, text, G.N_SCRATCH)
+        G.check_registers(core, text, G.n_scratch(core))
 
 
 @pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not installed")
