@@ -1953,6 +1953,7 @@ const char* op_name(uint16_t op) {
         case M_V_LSHL_ADD: return "v_lshl_add_u32";
         case M_V_PERM: return "v_perm_b32";
         case M_V_BFI: return "v_bfi_b32";
+        case M_V_BITOP3: return "v_bitop3_b32";
         case M_V_CVT_F32_U32: return "v_cvt_f32_u32";
         case M_V_FMA_F32: return "v_fma_f32";
         case M_V_RCP_F32: return "v_rcp_f32";
@@ -2446,6 +2447,14 @@ const uint32_t kKecPlan[24] = {
 
 }  // namespace
 
+bool kec_bitop3() {
+    static const bool on = [] {
+        const char* e = std::getenv("MH_JIT_KEC_BITOP3");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 const KecCode& kec_routine() {
     static const KecCode kc = [] {
         KecCode k;
@@ -2481,7 +2490,7 @@ const KecCode& kec_routine() {
         uint8_t plan[24][25];
         for (int r = 0; r < 24; ++r)
             for (int i = 0; i < 25; ++i) plan[r][i] = (uint8_t)((kKecPlan[r] >> i) & 1);
-        if (complement)
+        if (complement && !kec_bitop3())
             for (int i = 0; i < 25; ++i)
                 if ((kKecInit >> i) & 1) {
                     comp[i] = 1;
@@ -2495,7 +2504,71 @@ const KecCode& kec_routine() {
             E(M_V_ALIGNBIT, {V(out[0]), V(lo), V(hi), IMM((uint32_t)(32 - r))});
             E(M_V_ALIGNBIT, {V(out[1]), V(hi), V(lo), IMM((uint32_t)(32 - r))});
         };
-        for (int round = 0; round < 24; ++round) {
+        // gfx950's v_bitop3_b32 (MH_JIT_KEC_BITOP3=0: the complement plan below instead): a
+        // three-input bitwise op at the issue rate of v_xor (profiles/r05j/valu_bitop3.json:
+        // 2.6-2.8 cycles per wave instruction at 2-8 waves per SIMD, v_xor 2.9, v_alignbit 4.7).
+        // theta's column parities are two XOR3 per half, D[x] folds into the XOR3 that applies
+        // it (lane ^ C[x-1] ^ rot(C[x+1], 1)), chi is one op per half (table 0xd2: b0 ^ (~b1 &
+        // b2)).  Per round 120 bitop3 + 58 alignbit + iota's xor, against 196 two-cycle and 64
+        // four-cycle ops of the complement plan.  No lane is stored complemented.
+        const bool bitop3 = kec_bitop3();
+        auto B3 = [&](uint32_t d, uint32_t a, uint32_t b, uint32_t c, uint32_t tt) {
+            E(M_V_BITOP3, {V(d), V(a), V(b), V(c), IMM(tt)});
+        };
+        for (int round = 0; bitop3 && round < 24; ++round) {
+            uint32_t c[5][2];
+            for (int x = 0; x < 5; ++x)  // the ten parities interleaved (dependent ops 10 apart)
+                for (int h = 0; h < 2; ++h) {
+                    c[x][h] = take();
+                    B3(c[x][h], map[x][h], map[x + 5][h], map[x + 10][h], 0x96);
+                }
+            for (int x = 0; x < 5; ++x)
+                for (int h = 0; h < 2; ++h)
+                    B3(c[x][h], c[x][h], map[x + 15][h], map[x + 20][h], 0x96);
+            for (int x = 0; x < 5; ++x) {
+                uint32_t d[2];
+                rotl(c[(x + 1) % 5][0], c[(x + 1) % 5][1], 1, d);
+                for (int h = 0; h < 2; ++h)
+                    for (int y = 0; y < 5; ++y)
+                        B3(map[x + 5 * y][h], map[x + 5 * y][h], c[(x + 4) % 5][h], d[h], 0x96);
+                give(d[0]);
+                give(d[1]);
+            }
+            for (int x = 0; x < 5; ++x) { give(c[x][0]); give(c[x][1]); }
+            uint32_t cur[2] = {map[1][0], map[1][1]};
+            for (int step = 0; step < 24; ++step) {
+                const int dst = kRhoPi[step][0];
+                const uint32_t t[2] = {map[dst][0], map[dst][1]};
+                uint32_t nv[2];
+                rotl(cur[0], cur[1], kRhoPi[step][1], nv);
+                map[dst][0] = nv[0];
+                map[dst][1] = nv[1];
+                give(cur[0]);
+                give(cur[1]);
+                cur[0] = t[0];
+                cur[1] = t[1];
+            }
+            for (int y = 0; y < 25; y += 5) {
+                uint32_t nrow[5][2];
+                for (int x = 0; x < 5; ++x)
+                    for (int h = 0; h < 2; ++h) {
+                        nrow[x][h] = take();
+                        B3(nrow[x][h], map[y + x][h], map[y + (x + 1) % 5][h],
+                           map[y + (x + 2) % 5][h], 0xd2);
+                    }
+                for (int x = 0; x < 5; ++x)
+                    for (int h = 0; h < 2; ++h) {
+                        give(map[y + x][h]);
+                        map[y + x][h] = nrow[x][h];
+                    }
+            }
+            const uint64_t rc = kKeccakRC[round];
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t w = (uint32_t)(rc >> (32 * h));
+                if (w) E(M_V_XOR, {V(map[0][h]), IMM(w), V(map[0][h])});
+            }
+        }
+        for (int round = 0; !bitop3 && round < 24; ++round) {
             // theta
             // (the ten column-parity chains interleaved: a wave's dependent VALU ops 10 apart)
             uint32_t c[5][2];
@@ -2669,6 +2742,12 @@ std::string print(const MI& m, const std::string& prefix) {
     std::string s = op_name(m.op);
     if (m.e64) s += "_e64";
     if (m.op == M_S_NOP) return s + " " + std::to_string(m.o[0].v);
+    if (m.op == M_V_BITOP3) {
+        char b[128];
+        snprintf(b, sizeof b, "v_bitop3_b32 v%u, v%u, v%u, v%u bitop3:0x%x", m.o[0].v, m.o[1].v,
+                 m.o[2].v, m.o[3].v, m.o[4].v & 0xFFu);
+        return b;
+    }
     bool first = true;
     for (const Opnd& o : m.o) {
         if (o.k == O_NONE) break;
@@ -2697,7 +2776,7 @@ uint32_t code_bytes(const TapeCode& tc) {
         const bool vop3 = m.e64 || m.op == M_V_OR3 || m.op == M_V_ALIGNBIT ||
                           m.op == M_V_MAD_U64_U32 || m.op == M_V_FMA_F64 || m.op == M_V_MUL_F64 ||
                           m.op == M_V_MIN_F64 || m.op == M_V_LSHL_ADD || m.op == M_V_PERM ||
-                          m.op == M_V_BFI || m.op == M_DS_WRITE2ST64 ||
+                          m.op == M_V_BFI || m.op == M_V_BITOP3 || m.op == M_DS_WRITE2ST64 ||
                           m.op == M_DS_READ2ST64 || m.op == M_DS_READ_B32;
         b += (vop3 || lit) ? 8 : 4;
     }

@@ -64,6 +64,7 @@ enum Op : uint16_t {
     M_V_LSHL_ADD,    // d = (s0 << s1) + s2
     M_V_PERM,        // v_perm_b32 d, s0, s1, sel (byte select from {s0, s1})
     M_V_BFI,         // d = (s0 & s1) | (~s0 & s2)
+    M_V_BITOP3,      // gfx950: d = bit i of table o[4] at index s0 << 2 | s1 << 1 | s2 (per bit)
     // f32 (the division's small-quotient estimate)
     M_V_CVT_F32_U32, M_V_FMA_F32, M_V_RCP_F32, M_V_MUL_F32, M_V_CVT_U32_F32, M_V_FRACT_F32,
     M_V_CMP_GT_F32, M_V_CMP_LE_F32,  // VCC / SGPR pair = s0 > s1 / s0 <= s1

@@ -305,6 +305,16 @@ void run(Wave& w, const std::vector<MI>& code, const std::vector<MI>& div, int d
                     w.v[o[0].v][l] = (m & w.r32(o[2], l)) | (~m & w.r32(o[3], l));
                 });
                 break;
+            case M_V_BITOP3:  // bit i = table bit (s0_i << 2 | s1_i << 1 | s2_i)
+                each([&](int l) {
+                    const uint32_t a = w.r32(o[1], l), b = w.r32(o[2], l), c = w.r32(o[3], l);
+                    uint32_t r = 0;
+                    for (int t = 0; t < 8; ++t)
+                        if ((o[4].v >> t) & 1u)
+                            r |= ((t & 4) ? a : ~a) & ((t & 2) ? b : ~b) & ((t & 1) ? c : ~c);
+                    w.v[o[0].v][l] = r;
+                });
+                break;
             case M_V_CVT_F32_U32: each([&](int l) { w.wf32(o[0], l, (float)w.r32(o[1], l)); }); break;
             case M_V_FMA_F32:
                 each([&](int l) { w.wf32(o[0], l, fmaf(w.f32(o[1], l), w.f32(o[2], l), w.f32(o[3], l))); });

@@ -249,23 +249,55 @@ def test_keccak_variant_tapes_jit(emu):
     assert check_tapes(emu, ts, soa, require_all=False) >= 22
 
 
-def test_keccak_complement_plan(emu, monkeypatch):
-    """Lane complementing in the Keccak-f[1600] subroutine: chi mostly as AND / OR + xor
-    (2-cycle VALU) instead of xor + v_bfi (4-cycle), the same instruction count; the values are
-    pinned by the keccak tests above (emulator) and tests/test_gpu_jit.py (device)."""
+def _kec_ops(emu):
     import collections
 
     ts = synth.generate(2, keccak=True)
     text, _, _ = jit_module(emu, ts, max_vgpr=168, assemble=False)
     kec = text[text.index("mh_kec:"):text.index(".Lmh_jit_end")]
-    ops = collections.Counter(ln.split()[0] for ln in kec.splitlines()
-                              if ln.strip() and not ln.strip().endswith(":")
-                              and not ln.startswith("."))
-    assert ops["v_bfi_b32"] <= 24 * 12, ops
-    assert ops["v_xnor_b32"] <= 24 * 4, ops
-    assert ops["v_and_b32"] + ops["v_or_b32"] >= 24 * 36, ops
-    n = sum(ops.values())
-    assert n <= 24 * 260 + 16, ops
+    return collections.Counter(ln.split()[0] for ln in kec.splitlines()
+                               if ln.strip() and not ln.strip().endswith(":")
+                               and not ln.startswith("."))
+
+
+def test_keccak_bitop3_rounds(emu):
+    """gfx950's v_bitop3_b32 in the Keccak-f[1600] subroutine (the default): theta's parities as
+    XOR3 pairs, D folded into the XOR3 that applies it, chi one op per half -- 120 bitop3 + 58
+    alignbit per round (+ iota's xor); the values are pinned by the keccak tests above (emulator,
+    which restates bitop3's truth-table semantics) and tests/test_gpu_jit.py (device)."""
+    if os.environ.get("MH_JIT_KEC_BITOP3") == "0":
+        pytest.skip("bitop3 rounds switched off")
+    ops = _kec_ops(emu)
+    assert ops["v_bitop3_b32"] == 24 * 120, ops
+    assert ops["v_alignbit_b32"] == 24 * 58, ops
+    assert ops["v_bfi_b32"] == 0 and ops["v_not_b32"] == 0, ops
+    assert sum(ops.values()) <= 24 * 180 + 16, ops
+
+
+def test_keccak_complement_plan():
+    """MH_JIT_KEC_BITOP3=0: lane complementing in the Keccak-f[1600] subroutine, chi mostly as
+    AND / OR + xor (2-cycle VALU) instead of xor + v_bfi (4-cycle), the same instruction count
+    (the switch is read once per process: checked in a child)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import json\n"
+        "from tests.conftest import build_emulator\n"
+        "from tests.emu import Emulator\n"
+        "from tests.test_jit import _kec_ops\n"
+        "print(json.dumps(_kec_ops(Emulator(build_emulator()))))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                         env=dict(os.environ, MH_JIT_KEC_BITOP3="0"), timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    ops = json.loads(out.stdout.strip().splitlines()[-1])
+    get = lambda k: ops.get(k, 0)  # noqa: E731
+    assert get("v_bfi_b32") <= 24 * 12, ops
+    assert get("v_xnor_b32") <= 24 * 4, ops
+    assert get("v_and_b32") + get("v_or_b32") >= 24 * 36, ops
+    assert get("v_bitop3_b32") == 0, ops
+    assert sum(ops.values()) <= 24 * 260 + 16, ops
 
 
 def test_immediate_and_variable_shifts_jit(emu):
