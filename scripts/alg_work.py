@@ -17,7 +17,7 @@ rate of either mode, and roofline.frac <= 1 for both.
 The figures are per build (native.codegen_id()); bench.py reads profiles/alg_work.json only for
 the build it runs.
 
-    python scripts/alg_work.py [n_sample_tapes=10000] [rows=256] [--full]
+    python scripts/alg_work.py [n_sample_tapes=10000] [rows=256] [--full] [--variant=keccak]
 """
 import json
 import os
@@ -40,8 +40,8 @@ OUT = os.path.join(ROOT, "profiles", "alg_work.json")
 _W = {}
 
 
-def _init(rows, full):
-    ts = synth.generate()
+def _init(rows, full, variant="plain"):
+    ts = synth.generate(None, keccak=variant == "keccak")
     seed = synth.load_spec()["assignment_seed"]
     soa = np.zeros((ts.n_vars, 8, rows), dtype=np.uint32)
     for r in range(rows):
@@ -63,18 +63,21 @@ def _tape(t):
     return res.dyn["valu"], res.dyn["alive_valu"]
 
 
-def measure(picks, rows, full, procs):
+def measure(picks, rows, full, procs, variant="plain"):
     import multiprocessing as mp
 
-    with mp.get_context("fork").Pool(procs, initializer=_init, initargs=(rows, full)) as pool:
+    with mp.get_context("fork").Pool(procs, initializer=_init,
+                                     initargs=(rows, full, variant)) as pool:
         out = pool.map(_tape, picks, chunksize=16)
     return (sum(v for v, _ in out) / len(out), sum(a for _, a in out) / len(out))
 
 
 def main():
-    n_pick = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
-    rows = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     full = "--full" in sys.argv
+    variant = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--variant=")), "plain")
+    argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+    n_pick = int(argv[0]) if argv else 10000
+    rows = int(argv[1]) if len(argv) > 1 else 256
     procs = min(8, os.cpu_count() or 1)
     spec = synth.load_spec()
     n_tapes = spec["n_tapes"]
@@ -82,10 +85,10 @@ def main():
     picks = list(range(0, n_tapes, stride))[:n_pick]
     build_emulator()
     t0 = time.time()
-    sc_valu, sc_alive = measure(picks, rows, False, procs)
+    sc_valu, sc_alive = measure(picks, rows, False, procs, variant)
     entry = {
-        "codegen_id": native.codegen_id(),
-        "variant": "plain",
+        "codegen_id": native.codegen_id("jit", variant),
+        "variant": variant,
         "tapes_sampled": len(picks),
         "tape_stride": stride,
         "rows": rows,
@@ -95,7 +98,7 @@ def main():
         "lane_efficiency_sc": sc_alive / sc_valu,
     }
     if full:
-        entry["exec_lane_ops_per_eval_full"] = measure(picks, rows, True, procs)[0]
+        entry["exec_lane_ops_per_eval_full"] = measure(picks, rows, True, procs, variant)[0]
     entry["emulator_s"] = round(time.time() - t0, 1)
     entry["note"] = ("per (tape, row) evaluation, tapes x generated rows 0..rows-1, host wave "
                      "emulator over the emitted tape bodies (the kernel's per-chunk column loads "

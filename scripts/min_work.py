@@ -27,7 +27,11 @@ limb is the floor of any limb-wise op on a 32-lane-wide integer unit:
                                   64-bit multiply-add each, plus L - 1 high-half moves
   UDIV / UREM                     L + q (2 Ly + 3): q = quotient digits (32-bit, from the row's
                                   values), Ly = significant divisor limbs; SDIV / SREM / SMOD + 2 L
-  KECCAK (Keccak-f[1600])         24 rounds x 250 (θ 100, ρπ 50, χ 100 on 32-bit halves)
+  KECCAK (Keccak-f[1600])         24 rounds x 178 on 32-bit halves with gfx950's three-input
+                                  bitwise op (v_bitop3): θ's five-way parities 2 x 10, D's
+                                  rotations 10, D applied 50 (folded into one 3-input op per
+                                  half), ρ 48, χ 50 (one op per half); ι not counted (round 4's
+                                  table priced 250 per round with two-input ops only)
   add / sub overflow predicates   L; multiply overflow: L^2
 
 The result is written to profiles/min_work.json; bench.py reports it as ``roofline.achieved`` /
@@ -48,7 +52,7 @@ from mythril_amd.tape import Op  # noqa: E402
 from oracle import smt_eval  # noqa: E402
 
 OUT = os.path.join(ROOT, "profiles", "min_work.json")
-KECCAK_MIN = 24 * 250
+KECCAK_MIN = 24 * 178
 FULL = 0xFF
 
 
