@@ -309,7 +309,7 @@ struct Harvester {
     std::unordered_map<Key, Memo, KeyHash, std::equal_to<Key>, ArenaAlloc<std::pair<const Key, Memo>>>
         memo;
     AVec<AVec<uint32_t>> cap;
-    AVec<std::pair<int, Alts>> sets;
+    AVec<std::pair<int, std::shared_ptr<const Alts>>> sets;
     AVec<uint32_t> hints;      // hint ids in the order they became hint sets
     std::map<AVec<uint32_t>, uint32_t, std::less<AVec<uint32_t>>,
              ArenaAlloc<std::pair<const AVec<uint32_t>, uint32_t>>> hint_ids;
@@ -332,6 +332,28 @@ struct Harvester {
     std::map<int, std::vector<uint32_t>> const_ids_by_width;  // their interned ids
     // eq_nodes per conjunct (a function of the tape prefix: kept across a session's queries)
     std::unordered_map<uint32_t, std::vector<uint32_t>> eq_nodes_of;
+    // What a conjunct and an equality node contribute to a query, kept across a session's
+    // queries (functions of the tape prefix, like the memo): the set pushed (null: none) and
+    // the hint ids the inversions emit, replayed in order -- exactly what the memo's hits would
+    // do, without copying the alternatives again (a 400-constraint path re-read every earlier
+    // conjunct's sets and every (equality, constant) pair per query)
+    struct Contribution {
+        std::shared_ptr<const Alts> set;
+        std::vector<uint32_t> hints;
+    };
+    std::unordered_map<uint32_t, Contribution> conj_done;
+    struct EqPlan {
+        bool skip = false;        // a Bool, a constant side, or both sides equal once stripped
+        uint32_t x = 0, y = 0;
+        std::vector<std::vector<Copy>> copies;  // copy alternatives (then no value pairs)
+        std::unordered_map<uint32_t, Contribution> by_const;  // by the constant's interned id
+    };
+    std::unordered_map<uint32_t, EqPlan> eq_plan;
+    std::vector<uint32_t> memo_hints(const Key& k) const {
+        auto it = memo.find(k);
+        if (it == memo.end()) return {};
+        return std::vector<uint32_t>(it->second.hints.begin(), it->second.hints.end());
+    }
 
     // a kept harvester's next query (its tape extends the last one's): the memo, interned values
     // and hint ids stay, the query's own sets and hints start empty
@@ -865,45 +887,84 @@ struct Harvester {
             last_qc.swap(qc);
             last_conj = conj;
         }
-        if (parent && !parent->empty()) sets.push_back({kProbParent, {*parent}});
+        if (parent && !parent->empty())
+            sets.push_back({kProbParent, std::make_shared<const Alts>(Alts{*parent})});
         std::vector<char> seen_eq(nd.size(), 0);
         std::unordered_map<uint32_t, std::tuple<bool, uint32_t, uint32_t,
                                                 std::vector<std::vector<Copy>>>> eq_pairs;
+        auto replay = [&](const Contribution& c, int prob) {
+            for (uint32_t id : c.hints) emit_hint(id);
+            if (c.set) sets.push_back({prob, c.set});
+        };
         for (uint32_t cj : conj) {
-            Res alts = invert_bool(cj, true);
-            if (!alts.none && !alts.alts().empty() && !is_only_empty(alts.alts())) {
-                Alts kept;
-                for (const Alt& a : alts.alts()) if (!a.empty()) kept.push_back(a);
-                sets.push_back({kProbDefault, head(kept, kMaxAlts)});
+            auto cd = conj_done.find(cj);
+            if (cd != conj_done.end()) {
+                replay(cd->second, kProbDefault);
+            } else {
+                Res alts = invert_bool(cj, true);
+                Contribution c;
+                c.hints = memo_hints(Key{1u, cj, 1u, 0u});
+                if (!alts.none && !alts.alts().empty() && !is_only_empty(alts.alts())) {
+                    Alts kept;
+                    for (const Alt& a : alts.alts()) if (!a.empty()) kept.push_back(a);
+                    c.set = std::make_shared<const Alts>(head(kept, kMaxAlts));
+                    sets.push_back({kProbDefault, c.set});
+                }
+                conj_done.emplace(cj, std::move(c));
             }
             auto eqn = eq_nodes_of.find(cj);
             if (eqn == eq_nodes_of.end()) eqn = eq_nodes_of.emplace(cj, eq_nodes(cj)).first;
             for (uint32_t n : eqn->second) {
                 if (seen_eq[n]) continue;
                 seen_eq[n] = 1;
-                uint32_t x = nd[n].a, y = nd[n].b;
-                if (nd[x].width == 0 || const_value(x) || const_value(y)) continue;
-                std::tie(x, y) = strip_common(x, y);
-                if (x == y) continue;
-                auto calts = copy_alternatives(x, y);
-                const int w = nd[x].width;
-                if (!calts.empty()) {
-                    if ((int)copy_sets.size() < kMaxSets / 4) copy_sets.push_back(std::move(calts));
+                auto pit = eq_plan.find(n);
+                if (pit == eq_plan.end()) {
+                    EqPlan pl;
+                    uint32_t x = nd[n].a, y = nd[n].b;
+                    if (nd[x].width == 0 || const_value(x) || const_value(y)) {
+                        pl.skip = true;
+                    } else {
+                        std::tie(x, y) = strip_common(x, y);
+                        pl.skip = x == y;
+                        pl.x = x;
+                        pl.y = y;
+                        if (!pl.skip) pl.copies = copy_alternatives(x, y);
+                    }
+                    pit = eq_plan.emplace(n, std::move(pl)).first;
+                }
+                EqPlan& pl = pit->second;
+                if (pl.skip) continue;
+                if (!pl.copies.empty()) {
+                    if ((int)copy_sets.size() < kMaxSets / 4) copy_sets.push_back(pl.copies);
                     continue;
                 }
+                const uint32_t x = pl.x, y = pl.y;
+                const int w = nd[x].width;
                 const std::vector<U>& ks = consts_of_width(w);
                 const std::vector<uint32_t>& kids = const_ids_of_width(w);
                 const U mw = mask(w);
                 const uint32_t mid = intern(mw);
                 for (size_t ki = 0; ki < ks.size(); ++ki) {
+                    auto bc = pl.by_const.find(kids[ki]);
+                    if (bc != pl.by_const.end()) {
+                        replay(bc->second, kProbDefault / 2);
+                        continue;
+                    }
                     const U& k = ks[ki];
                     Res rx = invert_bits_ids(x, kids[ki], mid, k, mw);
                     Res ry = invert_bits_ids(y, kids[ki], mid, k, mw);
+                    Contribution c;
+                    c.hints = memo_hints(Key{0u, x, kids[ki], mid});
+                    const std::vector<uint32_t> hy = memo_hints(Key{0u, y, kids[ki], mid});
+                    c.hints.insert(c.hints.end(), hy.begin(), hy.end());
                     if (!rx.none && !rx.alts().empty() && !ry.none && !ry.alts().empty()) {
                         Alts both = merge(rx.alts(), ry.alts());
-                        if (!both.empty() && !is_only_empty(both))
-                            sets.push_back({kProbDefault / 2, head(both, kMaxAlts)});
+                        if (!both.empty() && !is_only_empty(both)) {
+                            c.set = std::make_shared<const Alts>(head(both, kMaxAlts));
+                            sets.push_back({kProbDefault / 2, c.set});
+                        }
                     }
+                    pl.by_const.emplace(kids[ki], std::move(c));
                 }
                 if ((int)sets.size() >= kMaxSets) break;
             }
@@ -921,14 +982,15 @@ struct Harvester {
                 if (!r.none && !r.alts().empty())
                     for (const Alt& a : r.alts()) if (!a.empty()) out.push_back(a);
             }
-            if (!out.empty()) sets.push_back({kProbDefault, head(out, kMaxAlts)});
+            if (!out.empty())
+                sets.push_back({kProbDefault, std::make_shared<const Alts>(head(out, kMaxAlts))});
         }
         out_sets.clear();
         const bool first_parent = parent && !parent->empty() && !sets.empty();
-        if (first_parent) out_sets.push_back({sets[0].first, &sets[0].second});
+        if (first_parent) out_sets.push_back({sets[0].first, sets[0].second.get()});
         for (uint32_t id : prune_hints()) out_sets.push_back({kProbHint, &hint_alts[id]});
         for (size_t i = first_parent ? 1 : 0; i < sets.size(); ++i)
-            out_sets.push_back({sets[i].first, &sets[i].second});
+            out_sets.push_back({sets[i].first, sets[i].second.get()});
         pools.assign(n_cols, {});
         auto add_pool = [&](uint32_t c, const V& v) {
             auto& p = pools[c];

@@ -377,6 +377,31 @@ def test_guide_session_laser_like():
     sess.close()
 
 
+@pytest.mark.parametrize("family", ["random", "laser"])
+def test_guide_session_planted_paths(family):
+    """The session's per-conjunct and per-(equality, constant) contributions (harvest.cpp
+    Harvester::conj_done / eq_plan) replay exactly what a fresh harvest computes: planted paths
+    (keccak manager conditions, stores, wide equalities) in LASER order, every prefix."""
+    from tests.planted import planted_path
+
+    for seed in range(3):
+        ctx, cs, _, _ = planted_path(family, seed, 20)
+        nodes = [c.node for c in cs]
+        sess = native.GuideSession()
+        m = native.TermMirror.of(ctx.b)
+        for k in range(1, len(nodes) + 1):
+            try:
+                cq = m.build(ctx.b, nodes[:k])
+            except native.Unsupported:
+                continue
+            if cq.flags & native.QUERY_REFUTED:
+                continue
+            want = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths)
+            got = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, session=sess)
+            assert _guide_equal(got, want), (family, seed, k)
+        sess.close()
+
+
 def _random_query(rng, n):
     """n random constraints over free arrays, K arrays, store chains, selects at constant and
     symbolic indices, a tabled function, a keccak function with concrete pairs, bounds and its
