@@ -534,7 +534,7 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
         return set_err(MH_E_INVALID, "null argument");
     *out = nullptr;
     std::vector<uint32_t> words, dconsts;
-    std::unordered_map<std::string, uint32_t> dindex;
+    mh::ConstIndex dindex;
     std::vector<mh_dev_tape> heads(n_tapes);
     std::vector<mh_tape_info> info(n_tapes);
     std::vector<uint32_t> ids, bucket_off(mh::kNumVariants + 1, 0);
@@ -1362,7 +1362,7 @@ int32_t mh_jit_code_id(const mh_node* nodes, const uint64_t* tape_offsets, uint3
     // the same validation mh_tapes_compile gives a tape set (the JIT reads only checked IR)
     try {
         std::vector<uint32_t> dconsts, w;
-        std::unordered_map<std::string, uint32_t> dindex;
+        mh::ConstIndex dindex;
         for (uint32_t t = 0; t < n_tapes; ++t) {
             const uint64_t b = tape_offsets[t], e = tape_offsets[t + 1];
             if (e <= b) return set_err(MH_E_INVALID, "tape " + std::to_string(t) + " is empty");

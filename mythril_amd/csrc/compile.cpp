@@ -152,7 +152,7 @@ struct Lowering {
     uint32_t n_vars;
     bool pinned;
     std::vector<uint32_t>& pool;  // deduplicated 256-bit constants (8 limbs each)
-    std::unordered_map<std::string, uint32_t>& pool_index;
+    ConstIndex& pool_index;
     std::vector<VInsn> code;
     int n_vregs = 0;
     uint32_t features = 0;
@@ -160,7 +160,7 @@ struct Lowering {
     std::vector<Val>* vals_ = nullptr;
 
     Lowering(const std::vector<mh_node>& tape, const uint32_t* c, uint32_t nc, uint32_t nv,
-             std::vector<uint32_t>& pl, std::unordered_map<std::string, uint32_t>& pi)
+             std::vector<uint32_t>& pl, ConstIndex& pi)
         : t(tape), consts(c), n_consts(nc), n_vars(nv), pinned(nv <= MH_MAX_PRELOAD),
           pool(pl), pool_index(pi) {
         if (pinned) n_vregs = (int)nv;  // vregs 0..nv-1 are the pinned columns
@@ -181,13 +181,12 @@ struct Lowering {
     }
 
     uint32_t const_index(const uint32_t* limbs, uint32_t width) {
-        uint32_t m[8];
-        for (int k = 0; k < 8; ++k) m[k] = limbs[k] & lane_mask(k, width);
-        std::string key(reinterpret_cast<const char*>(m), sizeof(m));
+        ConstKey key;
+        for (int k = 0; k < 8; ++k) key.w[k] = limbs[k] & lane_mask(k, width);
         auto it = pool_index.find(key);
         if (it != pool_index.end()) return it->second;
         uint32_t idx = (uint32_t)(pool.size() / 8);
-        pool.insert(pool.end(), m, m + 8);
+        pool.insert(pool.end(), key.w, key.w + 8);
         pool_index.emplace(key, idx);
         return idx;
     }
@@ -565,7 +564,9 @@ bool Lowering::lower(std::vector<Val>& vals) {
         const int ar = arity(nd);
         const uint32_t ops[3] = {nd.a, nd.b, nd.c};
         for (int k = 0; k < ar; ++k) ch[k] = ops[k];
-        std::stable_sort(ch, ch + ar, [&](uint32_t x, uint32_t y) { return need[x] > need[y]; });
+        // stable insertion sort of at most three (std::stable_sort allocates a buffer per call)
+        for (int k = 1; k < ar; ++k)
+            for (int j = k; j > 0 && need[ch[j]] > need[ch[j - 1]]; --j) std::swap(ch[j], ch[j - 1]);
         return ar;
     };
     for (size_t i = 0; i < n; ++i) {
@@ -1215,7 +1216,7 @@ void rewrite_wide_modops(std::vector<mh_node>& t) {
 
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
-                       std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& st,
+                       ConstIndex& dconst_index, SsaTape& st,
                        std::string& err, int value_numbering, bool jit_forms, bool hold_vars) {
     if (n_nodes == 0) {
         err = "empty tape";
@@ -1295,27 +1296,28 @@ std::vector<mh_node> rematerialize(const mh_node* t, size_t n, uint32_t max_size
     std::vector<mh_node> out;
     std::vector<uint32_t> remap(n, 0);
     // inside a duplicated sub-term every cheap node is copied too, so copies share nothing
-    std::function<uint32_t(uint32_t, bool)> copy = [&](uint32_t k, bool deep) -> uint32_t {
+    // (a recursive lambda called through itself: no std::function per call)
+    auto copy = [&](auto&& self, uint32_t k, bool deep) -> uint32_t {
         mh_node nd = t[k];
         const int ar = arity(nd);
         uint32_t* ops[3] = {&nd.a, &nd.b, &nd.c};
         for (int j = 0; j < ar; ++j) {
             const uint32_t x = *ops[j];
-            *ops[j] = (cheap[x] && (deep || dup[x])) ? copy(x, true) : remap[x];
+            *ops[j] = (cheap[x] && (deep || dup[x])) ? self(self, x, true) : remap[x];
         }
         out.push_back(nd);
         return (uint32_t)(out.size() - 1);
     };
     for (size_t i = 0; i < n; ++i) {
         if (dup[i] && i != n - 1) continue;
-        remap[i] = copy((uint32_t)i, false);
+        remap[i] = copy(copy, (uint32_t)i, false);
     }
     return out;
 }
 
 int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                           uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
-                          std::unordered_map<std::string, uint32_t>& dconst_index,
+                          ConstIndex& dconst_index,
                           std::vector<uint32_t>& words, CompiledTape& out, std::string& err,
                           bool hold_vars);
 
@@ -1330,7 +1332,7 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
 // not repeated for every child (the code differs, the values do not).
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                      uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
-                     std::unordered_map<std::string, uint32_t>& dconst_index,
+                     ConstIndex& dconst_index,
                      std::vector<uint32_t>& words, CompiledTape& out, std::string& err) {
     static thread_local int hint = 0;  // index into the attempt list of the last success
     const bool hold = n_vars > MH_MAX_PRELOAD && !std::getenv("MH_NO_HOLD_VARS");
@@ -1450,7 +1452,7 @@ void short_circuit(SsaTape& st) {
 
 int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                           uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
-                          std::unordered_map<std::string, uint32_t>& dconst_index,
+                          ConstIndex& dconst_index,
                           std::vector<uint32_t>& words, CompiledTape& out, std::string& err,
                           bool hold_vars) {
     SsaTape st;

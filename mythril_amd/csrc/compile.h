@@ -44,6 +44,24 @@ struct SsaTape {
     uint64_t alg_ops = 0;
 };
 
+// Deduplicating index of the 8-limb constant pool (limbs -> pool row)
+struct ConstKey {
+    uint32_t w[8];
+    bool operator==(const ConstKey& o) const {
+        for (int k = 0; k < 8; ++k)
+            if (w[k] != o.w[k]) return false;
+        return true;
+    }
+};
+struct ConstKeyHash {
+    size_t operator()(const ConstKey& k) const {
+        uint64_t h = 1469598103934665603ull;
+        for (uint32_t x : k.w) h = (h ^ x) * 1099511628211ull;
+        return (size_t)(h ^ (h >> 29));
+    }
+};
+using ConstIndex = std::unordered_map<ConstKey, uint32_t, ConstKeyHash>;
+
 // Lower one tape to SSA, fold constants and drop dead code (compile_tape's first half).
 // value_numbering merges identical instructions (the native code's register file has room for
 // the longer live ranges; the interpreter's does not); kVnNoLoads merges all but the column loads
@@ -54,7 +72,7 @@ struct SsaTape {
 // D_LOADVAR (the native code loads the limbs each use demands).
 int32_t lower_tape_ssa(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                        uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
-                       std::unordered_map<std::string, uint32_t>& dconst_index, SsaTape& out,
+                       ConstIndex& dconst_index, SsaTape& out,
                        std::string& err, int value_numbering = 0, bool jit_forms = false,
                        bool hold_vars = false);
 constexpr int kVnAll = 1, kVnNoLoads = 2;
@@ -71,7 +89,7 @@ void sample_bools(const SsaTape& st, const std::vector<uint32_t>& pool, uint32_t
 // constants to the shared device pool `dconsts` (8 limbs each, deduplicated via dconst_index).
 int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* consts,
                      uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
-                     std::unordered_map<std::string, uint32_t>& dconst_index,
+                     ConstIndex& dconst_index,
                      std::vector<uint32_t>& words, CompiledTape& out, std::string& err);
 
 // A tape whose root is a conjunction, cut into at most `want` parts of consecutive conjuncts of

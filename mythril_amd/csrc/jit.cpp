@@ -3167,7 +3167,7 @@ bool build_tapeset(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
     auto emit_list = [&](const std::vector<uint32_t>& list, const Options& o, Slice& sl,
                          bool keep_over) {
         std::vector<uint32_t> pool;
-        std::unordered_map<std::string, uint32_t> index;
+        ConstIndex index;
         sl.codes.reserve(list.size());
         for (uint32_t t : list) {
             SsaTape st;

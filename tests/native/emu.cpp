@@ -41,7 +41,7 @@ extern "C" int32_t emu_eval(const mh_node* nodes, const uint64_t* offs, uint32_t
                             uint32_t tape, const uint32_t* assign, uint64_t rows, uint32_t* out,
                             uint32_t* n_regs_out, char* err, int errlen) {
     std::vector<uint32_t> dconsts, words;
-    std::unordered_map<std::string, uint32_t> dindex;
+    mh::ConstIndex dindex;
     CompiledTape sel{};
     uint32_t sel_off = 0;
     for (uint32_t t = 0; t < n_tapes; ++t) {
@@ -116,7 +116,7 @@ extern "C" int32_t emu_compile_words(const mh_node* nodes, const uint64_t* offs,
                                      uint32_t* out, uint64_t cap, uint64_t* n_words_out,
                                      uint32_t* nrx_out, char* err, int errlen) {
     std::vector<uint32_t> dconsts, words;
-    std::unordered_map<std::string, uint32_t> dindex;
+    mh::ConstIndex dindex;
     for (uint32_t t = 0; t < n_tapes; ++t) {
         CompiledTape ct;
         std::string e;

@@ -505,7 +505,7 @@ uint32_t g_sample_rows = Options().sample_rows;
 bool lower_and_emit(const mh_node* nodes, const uint64_t* offs, uint32_t n_tapes,
                     const uint32_t* consts, uint32_t n_consts, uint32_t n_vars, uint32_t tape,
                     uint32_t max_vgpr, std::vector<uint32_t>& pool, TapeCode& tc, std::string& e) {
-    std::unordered_map<std::string, uint32_t> index;
+    mh::ConstIndex index;
     SsaTape st;
     std::string err;
     if (tape >= n_tapes) { e = "tape index"; return false; }
@@ -632,7 +632,7 @@ extern "C" int64_t emu_jit_module(const mh_node* nodes, const uint64_t* offs, ui
                                   char* text, uint64_t cap, uint64_t* hsaco_size,
                                   uint32_t* n_jitted, char* err, int errlen) {
     std::vector<uint32_t> pool;
-    std::unordered_map<std::string, uint32_t> index;
+    mh::ConstIndex index;
     std::vector<TapeCode> codes(n_tapes);
     std::vector<const TapeCode*> ok;
     std::vector<uint32_t> ids;
