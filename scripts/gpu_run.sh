@@ -16,6 +16,7 @@
 #   kbench    bench.py --variant keccak (config 4's kernel, 2^20 rows)
 #   kprofile  scripts/profile.sh <tag>_keccak --variant keccak
 #   paths     scripts/path_scaling.py (latency against path length, 25..400 constraints)
+#   ibench    bench.py --engine interp (config 5 on the interpreter, one step)
 #   strong    bench.py --strong at N=1 (config 5 literally: 2^26 rows in total)
 #   import    scripts/import_cost.py (the z3 import stage per new constraint, C++ vs Python)
 #   pylatency latency's two passes with the Python host stages (SIEVE_HOST=python)
@@ -72,6 +73,7 @@ for step in "$@"; do
     kprofile) bash scripts/profile.sh "${TAG}_keccak" --variant keccak ;;
     paths)    timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" ;;
     import)   timeout -k 10 300 python -u scripts/import_cost.py > "$OUT/import_cost.jsonl" 2> "$OUT/import_cost.log" ;;
+    ibench)   timeout -k 10 600 python -u bench.py --engine interp --steps 1 --warmup 1 --no-companion --no-cpu-baseline > "$OUT/bench_interp.json" 2> "$OUT/bench_interp.log" ;;
     strong)   timeout -k 10 400 python -u bench.py --strong --no-companion --cpu-seconds 3 > "$OUT/bench_strong.json" 2> "$OUT/bench_strong.log" ;;
     pylatency) SIEVE_HOST=python SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py \
                 > "$OUT/sieve_queries_py_a.jsonl" 2> "$OUT/py_a.log" && \
