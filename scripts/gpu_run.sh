@@ -102,6 +102,7 @@ for step in "$@"; do
                 SIEVE_FIRST_ROWS=$fr SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_fr$fr.jsonl" 2> "$OUT/sieve_queries_fr$fr.log" && \
                 SIEVE_FIRST_ROWS=$fr timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_fr$fr.jsonl" 2> "$OUT/planted_recall_fr$fr.log" || exit 1; done ;;
     qpmc)     bash scripts/qprofile_pmc.sh "$TAG" ;;
+    qpmc256)  SIEVE_FIRST_ROWS=256 bash scripts/qprofile_pmc.sh "${TAG}_256" ;;
     qpmcnopf) MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_nopf.so bash scripts/qprofile_pmc.sh "${TAG}_nopf" ;;
     qcost)    timeout -k 10 300 python -u scripts/query_cost.py > "$OUT/query_cost.jsonl" 2> "$OUT/query_cost.log" ;;
     qprofile) MH_TRACE_COMPILE=1 SIEVE_QUERY_REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o qprof -- \

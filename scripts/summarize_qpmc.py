@@ -16,8 +16,9 @@ HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kind(name, grid):
-    if "sieve_kernel" in name:
-        return "sieve_256" if int(grid) <= 256 else "sieve_long"
+    if "sieve_kernel" in name:  # first rounds (256 rows before round 5, 4096 since)
+        g = int(grid)
+        return "sieve_256" if g <= 256 else "sieve_4096" if g <= 4096 else "sieve_long"
     if "guided" in name:
         return "generate"
     return None
