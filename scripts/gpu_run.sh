@@ -27,6 +27,7 @@
 #             sizes $PFR (default 256 4096)
 #   bitop3    scripts/valu_peak.py for v_bitop3_b32 beside xor / alignbit / cndmask
 #   hostprof  scripts/solve_profile.py (cProfile of LASER-order queries at 400 constraints)
+#   hiptrace  rocprofv3 HIP runtime + kernel trace of solve_profile.py (EtherThief-400)
 #   pprofile  rocprofv3 kernel trace + stats of path_scaling.py at 400 constraints
 #   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
 #   recall    scripts/planted_recall.py (recall on planted-SAT paths, per round and shape class)
@@ -114,6 +115,8 @@ for step in "$@"; do
     bitop3)   timeout -k 10 300 python -u scripts/valu_peak.py bitop3_b32 mix_bitop3_alignbit xor_b32 alignbit_b32 cndmask_b32 > "$OUT/valu_bitop3.json" 2> "$OUT/valu_bitop3.log" ;;
     hostprof) timeout -k 10 300 python -u scripts/solve_profile.py ether_thief 400 40 > "$OUT/solve_profile_et400.txt" 2>&1 && \
               timeout -k 10 300 python -u scripts/solve_profile.py killbilly 400 40 > "$OUT/solve_profile_kb400.txt" 2>&1 ;;
+    hiptrace) timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --stats --output-format csv -d "$OUT/htrace" -o htrace -- \
+                python -u scripts/solve_profile.py ether_thief 400 40 > "$OUT/htrace.txt" 2> "$OUT/htrace.log" ;;
     pprofile) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pprof" -o pprof -- \
                 python -u scripts/path_scaling.py 400 > "$OUT/pprof.jsonl" 2> "$OUT/pprof.log" ;;
     gather)   timeout -k 10 300 python -u scripts/gather_bench.py > "$OUT/gather.jsonl" 2> "$OUT/gather.log" ;;
