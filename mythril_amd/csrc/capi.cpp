@@ -717,11 +717,12 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
         ctx->stage_pending = false;
     }
     if (e == hipSuccess && total > ctx->h_stage_bytes) {
+        const size_t n = std::max<size_t>({total, 2 * ctx->h_stage_bytes, (size_t)1 << 20});
         if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
         ctx->h_stage = nullptr;
         ctx->h_stage_bytes = 0;
-        e = hipHostMalloc(&ctx->h_stage, std::max<size_t>(total, 1 << 20), hipHostMallocDefault);
-        if (e == hipSuccess) ctx->h_stage_bytes = std::max<size_t>(total, 1 << 20);
+        e = hipHostMalloc(&ctx->h_stage, n, hipHostMallocDefault);
+        if (e == hipSuccess) ctx->h_stage_bytes = n;
     }
     if (e == hipSuccess && !ctx->stage_ev)
         e = hipEventCreateWithFlags(&ctx->stage_ev, hipEventDisableTiming);
@@ -946,12 +947,16 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
         std::copy(g->entry_col, g->entry_col + n_ent, h.begin() + o_ecol);
         std::copy(g->entry_val, g->entry_val + (size_t)n_ent * 8, h.begin() + o_eval);
     }
+    // both buffers grow geometrically: a LASER child's guide is a little larger than its
+    // parent's, and a pinned reallocation per query cost ~0.24 ms (hipHostFree 0.19 +
+    // hipHostMalloc 0.05, EtherThief-400, profiles/r05o/htrace)
+    const size_t grow = std::max<size_t>({words, 2 * as->guide_words, (size_t)1 << 14});
     if (words > as->guide_words) {
         if (as->d_guide) MH_HIP(hipFree(as->d_guide));
         as->d_guide = nullptr;
         as->guide_words = 0;
-        MH_HIP(hipMalloc(&as->d_guide, words * sizeof(uint32_t)));
-        as->guide_words = words;
+        MH_HIP(hipMalloc(&as->d_guide, grow * sizeof(uint32_t)));
+        as->guide_words = grow;
     }
     // pinned staging: the async copy needs no stream sync; the next call's packing waits on
     // the event of this copy before it overwrites the staging buffer
@@ -960,11 +965,12 @@ int32_t mh_assign_generate_guided(mh_assign* as, uint64_t seed, uint64_t global_
         as->staged_pending = false;
     }
     if (words > as->pinned_words) {
+        const size_t pgrow = std::max<size_t>({words, 2 * as->pinned_words, (size_t)1 << 14});
         if (as->h_pinned) MH_HIP(hipHostFree(as->h_pinned));
         as->h_pinned = nullptr;
         as->pinned_words = 0;
-        MH_HIP(hipHostMalloc(&as->h_pinned, words * sizeof(uint32_t), hipHostMallocDefault));
-        as->pinned_words = words;
+        MH_HIP(hipHostMalloc(&as->h_pinned, pgrow * sizeof(uint32_t), hipHostMallocDefault));
+        as->pinned_words = pgrow;
     }
     if (!as->staged) MH_HIP(hipEventCreateWithFlags(&as->staged, hipEventDisableTiming));
     std::memcpy(as->h_pinned, h.data(), words * sizeof(uint32_t));
