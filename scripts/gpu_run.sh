@@ -43,6 +43,7 @@
 #             (MH_INTERP_SC=0) and in the conjuncts' given order (MH_INTERP_SC=given)
 #   rows1     paths, queries (9 reps) and planted recall with first rounds of 256 / 4096 / 16384
 #             rows (SIEVE_FIRST_ROWS)
+#   split     paths and queries with conjunct-parallel rounds (MH_SPLIT_INSNS in $SPLITS)
 #   qpmc      scripts/qprofile_pmc.sh <tag> (PMC passes of the query-path kernels)
 #   qpmcnopf  the same on the no-prefetch variant library
 #   occupancy bench.py at 168 and 256 VGPRs (3 and 2 waves per SIMD; the LDS-resident compaction
@@ -102,6 +103,9 @@ for step in "$@"; do
                 SIEVE_FIRST_ROWS=$fr timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_fr$fr.jsonl" 2> "$OUT/path_scaling_fr$fr.log" && \
                 SIEVE_FIRST_ROWS=$fr SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_fr$fr.jsonl" 2> "$OUT/sieve_queries_fr$fr.log" && \
                 SIEVE_FIRST_ROWS=$fr timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_fr$fr.jsonl" 2> "$OUT/planted_recall_fr$fr.log" || exit 1; done ;;
+    split)    for si in ${SPLITS:-384 1024}; do \
+                MH_SPLIT_INSNS=$si timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_split$si.jsonl" 2> "$OUT/path_scaling_split$si.log" && \
+                MH_SPLIT_INSNS=$si SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_split$si.jsonl" 2> "$OUT/sieve_queries_split$si.log" || exit 1; done ;;
     qpmc)     bash scripts/qprofile_pmc.sh "$TAG" ;;
     qpmc256)  SIEVE_FIRST_ROWS=256 bash scripts/qprofile_pmc.sh "${TAG}_256" ;;
     qpmcnopf) MYTHRIL_HIP_LIB=$PWD/mythril_amd/libmythril_hip_nopf.so bash scripts/qprofile_pmc.sh "${TAG}_nopf" ;;
