@@ -74,10 +74,6 @@ D_WINDOW = 120      # dev_isa.h (static_assert in the .inc)
 # entry: the slots' scalar loads then hit L2 instead of each 64-byte line missing in turn (the
 # C++ driver's window reload did this by accident; without it the in-core change was slower)
 WIN_PREFETCH = CORE_WINDOW and os.environ.get("MH_GEN_WIN_PREFETCH", "1") != "0"
-# ... and the scalar cache is warmed with the window the core enters: one s_load_dwordx16 per
-# 64-byte line (8 slots) of it, all in flight together and awaited once, instead of each line's
-# first word load missing in turn (a line's miss outlasts the handlers that would hide it)
-WIN_WARM = CORE_WINDOW and os.environ.get("MH_GEN_WIN_WARM", "1") != "0"
 LV_NONE = 0xFFFF
 
 # opcode numbers: must match enum mh_dop in dev_isa.h (checked by a static_assert in the .inc)
@@ -155,22 +151,6 @@ class Core:
     def WP(self):  # the window prefetch's destination pair (after PF; never read)
         r = self.sb + N_SCRATCH + N_PF
         return "v[{}:{}]".format(r, r + 1)
-
-    def win_warm(self):
-        """Scalar loads of the 8 lines of the window holding ip (slots below the tape's end
-        only), into the bank, awaited: afterwards the dispatch's word loads hit the scalar
-        cache.  The bank is free here (the dispatch that follows reloads it)."""
-        if not WIN_WARM:
-            return []
-        out = ["s_andn2_b32 {}, %[ip], {}".format(S_Q, WINDOW - 1)]
-        for k in range(WINDOW // 8):
-            if k:
-                out.append("s_add_u32 {0}, {0}, 8".format(S_Q))
-            out += ["s_cmp_lt_u32 {}, %[nsl]".format(S_Q),
-                    "s_cbranch_scc0 L_warm_%=_{}".format(self._wpf),
-                    "s_lshl_b32 {}, {}, 3".format(S_T, S_Q),
-                    "s_load_dwordx16 {}, %[gwin], {}".format(S_BANK, S_T)]
-        return out + ["L_warm_%=_{}:".format(self._wpf), "s_waitcnt lgkmcnt(0)"]
 
     def win_prefetch(self):
         """One vector load of the 64 slots from slot S_T on (lane j: slot min(S_T + j, n - 1), so
@@ -360,7 +340,7 @@ class Core:
             return (["s_add_u32 %[ip], %[ip], {}".format(WINDOW),
                      "s_andn2_b32 %[ip], %[ip], {}".format(WINDOW - 1),
                      "s_add_u32 {}, %[ip], {}".format(S_T, WINDOW)] + self.win_prefetch() +
-                    self.win_warm() + self.dispatch(0))
+                    self.dispatch(0))
         if name == "LOADVAR":
             # X = column aux of this lane's row: limb k at vbase + ((8 col + k) cap4) + voff
             # (SoA planes, KParams::assign); the address is SALU arithmetic in s[56:57] (no
@@ -865,9 +845,6 @@ class Core:
             self._wpf = "e"
             lines += ["s_andn2_b32 {}, %[ip], {}".format(S_T, WINDOW - 1),
                       "s_add_u32 {0}, {0}, {1}".format(S_T, WINDOW)] + self.win_prefetch()
-        if WIN_WARM:  # ... and the lines of the one it starts in
-            self._wpf = "e"
-            lines += self.win_warm()
         lines += self.resolve(self.dispatch(0))
         lines += [".p2align 8", "L_tab_%=:"]
         bodies = []
@@ -879,8 +856,7 @@ class Core:
             if self.loadvar and i in CORE_COMPLEX:
                 name = CORE_COMPLEX[i]
             h = self.handler(name)
-            if name in OUT_OF_LINE or name in CORE_COMPLEX.values() or \
-                    (name == "WINDOW" and WIN_WARM):  # too long for a slot: a body after the table
+            if name in OUT_OF_LINE or name in CORE_COMPLEX.values():  # too long for a slot: jump to a body after the table
                 lines.append("s_branch L_body_{}_%=".format(name))
                 bodies += ["L_body_{}_%=:".format(name)] + h
             else:

@@ -306,22 +306,11 @@ def test_window_change_stays_in_the_core(nr):
     assert h[-1] == "s_setpc_b64 s[46:47]" and not any("L_out" in ln for ln in h)
     # the words are loaded at the new ip, after it is set (no prefetch from the old one)
     loads = [i for i, ln in enumerate(h) if ln.startswith("s_load_dword")]
-    assert loads[-1] > 1 and h[loads[-1] - 1] == "s_lshl_b32 s44, %[ip], 3"
-    if G.WIN_WARM:
-        # the window's 8 scalar-cache lines, all awaited before the dispatch's own load (their
-        # destination is the bank that load fills)
-        assert len(loads) == 1 + G.WINDOW // 8
-        waits = [i for i, ln in enumerate(h) if ln == "s_waitcnt lgkmcnt(0)"]
-        assert loads[-2] < waits[0] < loads[-1]
-    else:
-        assert len(loads) == 1
+    assert len(loads) == 1 and loads[0] > 1 and h[loads[0] - 1] == "s_lshl_b32 s44, %[ip], 3"
     text = core.asm_text()
     at = text.index(".org L_tab_%= + {}".format(G.D_WINDOW * G.SLOT))
-    if G.WIN_WARM:  # out of line: the slot jumps to the body after the table
-        assert text[at + 1] == "s_branch L_body_WINDOW_%="
-        at = text.index("L_body_WINDOW_%=:")
     assert text[at + 1:at + 1 + len(h)] == h
-    if os.path.exists(LLVM_MC) and not G.WIN_WARM:
+    if os.path.exists(LLVM_MC):
         src = "\n".join(_asm_lines(h)) + "\n"
         p = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "-show-encoding"],
                            input=src, capture_output=True, text=True)
