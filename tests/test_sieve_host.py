@@ -173,3 +173,43 @@ def test_root_conjunction_short_circuits(emu):
         last_and = max(i for i, o in enumerate(ops) if o in (G.OPNUM["BAND"], G.OPNUM["BANDZ"]))
         assert ops[last_and] == G.OPNUM["BAND"], name  # the last AND needs no test
     assert seen >= 5
+
+
+def test_short_circuit_edge_shapes(emu):
+    """Root conjunctions the short-circuit pass must keep exact: a conjunct twice, a chain AND
+    also read inside a conjunct, a conjunct that is a shared sub-term of another, constant
+    conjuncts, a lone conjunct, a non-Bool root -- the emulator leaves at a false D_BANDZ per
+    lane and must still agree with the oracle on every row."""
+    import random
+
+    from mythril_amd.tape import Op
+    from tests.fuzz import assignment_soa, soa_row
+
+    ts = TapeSet()
+    b = ts.builder()
+    x, y, z = b.var("x"), b.var("y"), b.var("z")
+    c1 = b.op(Op.BVULT, x, y)
+    c2 = b.op(Op.NOT, b.op(Op.EQ, b.op(Op.BVADD, x, z), b.const(5, 256)))
+    c3 = b.op(Op.BVUGT, z, b.const(1 << 200, 256))
+    a12 = b.op(Op.AND, c1, c2)
+    shapes = [
+        b.op(Op.AND, c1, c1),                                   # the same conjunct twice
+        b.op(Op.AND, a12, b.op(Op.NOT, a12)),                   # a chain AND read inside
+        b.op(Op.AND, b.op(Op.AND, a12, c3), b.op(Op.OR, a12, c3)),
+        b.op(Op.AND, b.op(Op.AND, c1, b.true()), c3),
+        b.op(Op.AND, b.false(), c2),
+        c3,                                                      # a lone conjunct
+        b.op(Op.AND, b.op(Op.AND, b.op(Op.AND, c1, c2), c3), c2),
+        b.op(Op.BVADD, x, y),                                    # not a Bool
+    ]
+    for s in shapes:
+        ts.add(b.finish(s))
+    soa = assignment_soa(random.Random(77), ts.n_vars, 64)
+    for r in range(16):  # rows where x < y and z is large: the conjunctions can hold
+        for k in range(8):
+            soa[0, k, r], soa[1, k, r] = 0, 0xFFFFFFFF
+        soa[2, 7, r] = 0xFFFFFFFF
+    for i, t in enumerate(ts.tapes):
+        got, _ = emu.eval(ts, i, soa)
+        for r in range(soa.shape[2]):
+            assert got[r] == int(E.evaluate(t.nodes, ts.pool.values, soa_row(soa, r))), (i, r)
