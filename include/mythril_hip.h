@@ -135,6 +135,15 @@ int32_t mh_ctx_clear_cache(mh_ctx* ctx);
 int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape_offsets,
                          uint32_t n_tapes, const uint32_t* consts, uint32_t n_consts,
                          uint32_t n_vars, mh_tapeset** out);
+/* The same on a worker thread of the context, so the caller's other host work (the guide harvest,
+ * mh_guide_harvest_with) runs meanwhile: returns at once; mh_tapes_compile_wait gives what
+ * mh_tapes_compile would have.  The arrays must stay valid, and the caller makes no other call on
+ * this context, until the wait; one compile at a time per context.                               */
+int32_t mh_tapes_compile_async(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape_offsets,
+                               uint32_t n_tapes, const uint32_t* consts, uint32_t n_consts,
+                               uint32_t n_vars);
+int32_t mh_tapes_compile_wait(mh_ctx* ctx, mh_tapeset** out,
+                              double* compile_s /* the compile's own seconds, or NULL */);
 int32_t mh_tapes_destroy(mh_tapeset* ts);
 int32_t mh_tapes_info(const mh_tapeset* ts, mh_tape_info* info /* [n_tapes] */, uint32_t n_tapes);
 

@@ -8,9 +8,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -33,6 +35,8 @@ static bool fanout_enabled() {
     }();
     return on;
 }
+
+struct AsyncCompile;  // mh_tapes_compile_async's worker (below)
 
 struct mh_ctx {
     int device = 0;
@@ -79,6 +83,25 @@ struct mh_ctx {
     // the wave masks of a conjunct-parallel short run (grow-only)
     unsigned long long* d_masks = nullptr;
     size_t masks_bytes = 0;
+    // mh_tapes_compile_async: one worker thread, started on first use, joined by ctx_free
+    AsyncCompile* acomp = nullptr;
+};
+
+// One compile at a time, handed to a worker thread that waits on a condition variable (a thread
+// per call would cost its creation; a Python thread costs GIL hand-offs around the native call)
+struct AsyncCompile {
+    std::mutex m;
+    std::condition_variable cv;
+    std::thread th;
+    bool stop = false, job = false, done = false;
+    const mh_node* nodes = nullptr;
+    const uint64_t* offs = nullptr;
+    uint32_t n_tapes = 0, n_consts = 0, n_vars = 0;
+    const uint32_t* consts = nullptr;
+    int32_t rc = MH_OK;
+    std::string err;
+    mh_tapeset* out = nullptr;
+    double seconds = 0;
 };
 
 namespace {
@@ -456,6 +479,17 @@ int32_t mh_ctx_create(int32_t device, mh_ctx** out) {
 
 namespace {
 void ctx_free(mh_ctx* ctx) {
+    if (AsyncCompile* a = ctx->acomp) {
+        {
+            std::unique_lock<std::mutex> lk(a->m);
+            a->cv.wait(lk, [&] { return !a->job || a->done; });  // a pending compile finishes
+            a->stop = true;
+        }
+        a->cv.notify_all();
+        if (a->th.joinable()) a->th.join();
+        delete a;
+        ctx->acomp = nullptr;
+    }
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto& sp : ctx->spans) {
@@ -490,6 +524,19 @@ void ctx_unref(mh_ctx* ctx) {
 int32_t mh_ctx_destroy(mh_ctx* ctx) {
     if (!ctx) return MH_OK;
     if (ctx->released) return set_err(MH_E_INVALID, "context already destroyed");
+    if (AsyncCompile* a = ctx->acomp) {  // a compile nobody collected: finish and drop it
+        mh_tapeset* left = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(a->m);
+            a->cv.wait(lk, [&] { return !a->job || a->done; });
+            if (a->job) {
+                left = a->out;
+                a->out = nullptr;
+                a->job = false;
+            }
+        }
+        if (left) (void)mh_tapes_destroy(left);
+    }
     if (ctx->children > 0) {
         ctx->released = true;
         return MH_OK;
@@ -521,6 +568,75 @@ int32_t mh_ctx_synchronize(mh_ctx* ctx) {
     if (!ctx) return set_err(MH_E_INVALID, "null ctx");
     if (int32_t r = use_device(ctx)) return r;
     MH_HIP(hipStreamSynchronize(ctx->stream));
+    return MH_OK;
+}
+
+int32_t mh_tapes_compile_async(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape_offsets,
+                               uint32_t n_tapes, const uint32_t* consts, uint32_t n_consts,
+                               uint32_t n_vars) {
+    if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    try {
+        if (!ctx->acomp) {
+            AsyncCompile* a = new AsyncCompile();
+            a->th = std::thread([ctx, a] {
+                std::unique_lock<std::mutex> lk(a->m);
+                for (;;) {
+                    a->cv.wait(lk, [&] { return a->stop || (a->job && !a->done); });
+                    if (a->stop) return;
+                    lk.unlock();
+                    mh_tapeset* out = nullptr;
+                    const auto t0 = std::chrono::steady_clock::now();
+                    const int32_t rc = mh_tapes_compile(ctx, a->nodes, a->offs, a->n_tapes,
+                                                        a->consts, a->n_consts, a->n_vars, &out);
+                    const double dt = std::chrono::duration<double>(
+                                          std::chrono::steady_clock::now() - t0).count();
+                    const std::string err = rc == MH_OK ? std::string() : mh_last_error();
+                    lk.lock();
+                    a->rc = rc;
+                    a->err = err;
+                    a->out = out;
+                    a->seconds = dt;
+                    a->done = true;
+                    a->cv.notify_all();
+                }
+            });
+            ctx->acomp = a;
+        }
+    } catch (const std::exception&) {
+        return set_err(MH_E_NOMEM, "compile worker thread");
+    }
+    AsyncCompile* a = ctx->acomp;
+    {
+        std::lock_guard<std::mutex> lk(a->m);
+        if (a->job) return set_err(MH_E_INVALID, "a compile is already pending on this ctx");
+        a->nodes = nodes;
+        a->offs = tape_offsets;
+        a->n_tapes = n_tapes;
+        a->consts = consts;
+        a->n_consts = n_consts;
+        a->n_vars = n_vars;
+        a->out = nullptr;
+        a->rc = MH_OK;
+        a->done = false;
+        a->job = true;
+    }
+    a->cv.notify_all();
+    return MH_OK;
+}
+
+int32_t mh_tapes_compile_wait(mh_ctx* ctx, mh_tapeset** out, double* compile_s) {
+    if (!ctx || !out) return set_err(MH_E_INVALID, "null argument");
+    *out = nullptr;
+    AsyncCompile* a = ctx->acomp;
+    if (!a) return set_err(MH_E_INVALID, "no compile pending on this ctx");
+    std::unique_lock<std::mutex> lk(a->m);
+    if (!a->job) return set_err(MH_E_INVALID, "no compile pending on this ctx");
+    a->cv.wait(lk, [&] { return a->done; });
+    a->job = false;
+    *out = a->out;
+    a->out = nullptr;
+    if (compile_s) *compile_s = a->seconds;
+    if (a->rc != MH_OK) return set_err(a->rc, a->err);
     return MH_OK;
 }
 

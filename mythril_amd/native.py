@@ -52,6 +52,9 @@ SIGNATURES = {
     "mh_ctx_clear_cache": (C.c_int32, [_vp]),
     "mh_tapes_compile": (C.c_int32, [_vp, _vp, _u64p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
                                      C.POINTER(_vp)]),
+    "mh_tapes_compile_async": (C.c_int32, [_vp, _vp, _u64p, C.c_uint32, _u32p, C.c_uint32,
+                                           C.c_uint32]),
+    "mh_tapes_compile_wait": (C.c_int32, [_vp, C.POINTER(C.c_void_p), C.POINTER(C.c_double)]),
     "mh_tapes_destroy": (C.c_int32, [_vp]),
     "mh_tapes_info": (C.c_int32, [_vp, _vp, C.c_uint32]),
     "mh_assign_create": (C.c_int32, [_vp, C.c_uint32, C.c_uint64, C.POINTER(_vp)]),
@@ -778,6 +781,11 @@ class Context:
     def compile(self, tapeset: TapeSet) -> "CompiledTapes":
         return CompiledTapes(self, tapeset)
 
+    def compile_async(self, tapeset: TapeSet) -> "PendingCompile":
+        """mh_tapes_compile_async: the compile runs on the context's worker thread; the caller
+        does host-only work meanwhile (no other call on this context) and then .wait()s."""
+        return PendingCompile(self, tapeset)
+
     def assignments(self, n_vars: int, capacity: int) -> "Assignments":
         return Assignments(self, n_vars, capacity)
 
@@ -810,18 +818,59 @@ class Context:
         return v.value
 
 
-class CompiledTapes:
-    """mh_tapeset: tapes lowered to device code, resident in HBM."""
+def _compile_args(tapeset: TapeSet):
+    nodes, offs, consts = tapeset.flatten()
+    return (np.ascontiguousarray(nodes, dtype=NODE_DTYPE), np.ascontiguousarray(offs, dtype=np.uint64),
+            np.ascontiguousarray(consts, dtype=np.uint32))
+
+
+class PendingCompile:
+    """A compile on the context's worker thread (Context.compile_async); its input arrays are
+    held here until wait() returns the CompiledTapes."""
 
     def __init__(self, ctx: Context, tapeset: TapeSet):
         import time
 
-        self.ctx = ctx
+        self.ctx, self.tapeset = ctx, tapeset
         t0 = time.perf_counter()
-        nodes, offs, consts = tapeset.flatten()
-        nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
-        offs = np.ascontiguousarray(offs, dtype=np.uint64)
-        consts = np.ascontiguousarray(consts, dtype=np.uint32)
+        self.args = _compile_args(tapeset)
+        nodes, offs, consts = self.args
+        self.t1 = time.perf_counter()
+        self.flatten_s = self.t1 - t0
+        _check(ctx.lib.mh_tapes_compile_async(
+            ctx.h, nodes.ctypes.data_as(C.c_void_p), _ptr(offs, C.c_uint64), len(tapeset.tapes),
+            _ptr(consts), len(tapeset.pool.values), tapeset.n_vars))
+
+    def wait(self) -> "CompiledTapes":
+        import time
+
+        h, secs = C.c_void_p(), C.c_double()
+        try:
+            _check(self.ctx.lib.mh_tapes_compile_wait(self.ctx.h, C.byref(h), C.byref(secs)))
+        finally:
+            self.args = None
+        # timing: host flatten, the compile's own seconds on the worker (it overlapped the
+        # caller's work; the wait itself is what the caller paid for it)
+        self.wait_s = time.perf_counter() - self.t1
+        return CompiledTapes(self.ctx, self.tapeset, _handle=h,
+                             _timing=(self.flatten_s, secs.value))
+
+
+class CompiledTapes:
+    """mh_tapeset: tapes lowered to device code, resident in HBM."""
+
+    def __init__(self, ctx: Context, tapeset: TapeSet, _handle=None, _timing=None):
+        import time
+
+        self.ctx = ctx
+        if _handle is not None:  # from PendingCompile.wait
+            self.h = _handle
+            self.timing = _timing
+            self.n_tapes = len(tapeset.tapes)
+            self.n_vars = tapeset.n_vars
+            return
+        t0 = time.perf_counter()
+        nodes, offs, consts = _compile_args(tapeset)
         h = C.c_void_p()
         t1 = time.perf_counter()
         _check(ctx.lib.mh_tapes_compile(

@@ -457,26 +457,18 @@ class Sieve:
         self.stats = SieveStats()
         self.witnesses: "OrderedDict[tuple, Dict[str, int]]" = OrderedDict()
         self.max_witnesses = 1 << 14
-        # the tape compile runs on a worker thread while this one harvests the guide: both are
-        # native calls that release the GIL, both only read the query's tapes, and the round
-        # needs both (SIEVE_OVERLAP=0: one after the other)
+        # the tape compile runs on the context's worker thread (mh_tapes_compile_async) while
+        # this one harvests the guide: the harvest is host-only, both only read the query's
+        # tapes, and the round needs both (SIEVE_OVERLAP=0: one after the other)
         self.overlap = os.environ.get("SIEVE_OVERLAP", "1") != "0"
-        self._pool = None
 
     def close(self) -> None:
-        if self._pool is not None:
-            self._pool.shutdown(wait=True)
-            self._pool = None
         if self.assign is not None:
             self.assign.close()
             self.assign = None
         self.guides.close()
         self.ctx.close()
 
-    def _compile_timed(self, ts: TapeSet):
-        t0 = time.perf_counter()
-        ct = self.compile(ts)
-        return ct, time.perf_counter() - t0
 
     def _buffer(self, n_cols: int) -> native.Assignments:
         rows = max(self.first_rows, (self.max_rounds - 1) * self.rows)
@@ -696,13 +688,9 @@ class Sieve:
             host = self._host_python(b, roots)
         columns, widths, schema, root_nodes, ts, group_cols, defs = host
         t_t = time.perf_counter()
-        fut = None
-        if self.overlap:
-            if self._pool is None:
-                from concurrent.futures import ThreadPoolExecutor
-
-                self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="sieve-compile")
-            fut = self._pool.submit(self._compile_timed, ts)
+        pending = None
+        if self.overlap and hasattr(self.ctx, "compile_async"):
+            pending = self.ctx.compile_async(ts)
         col_index = {c: i for i, c in enumerate(columns)}
         parent = self.witnesses.get(key[:-1]) if key else None
         try:
@@ -711,9 +699,9 @@ class Sieve:
                 [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else (),
                 session=self.guides, keep=True)  # stays in the library for the rounds
         except BaseException:
-            if fut is not None:  # the compile's tapes are not needed
+            if pending is not None:  # the compile's tapes are not needed
                 try:
-                    fut.result()[0].close()
+                    pending.wait().close()
                 except Exception:  # noqa: BLE001 - the harvest's error is the one to report
                     pass
             raise
@@ -721,13 +709,18 @@ class Sieve:
         st.add("guide", t1 - t_t)
         self.stats.host_s += t1 - t0
         try:
-            if fut is None:
+            ct = None
+            if pending is not None:
+                try:
+                    ct = pending.wait()
+                except native.Unsupported:  # register pressure: Sieve.compile's retries
+                    ct = None
+                if ct is not None:  # its own duration; the part the harvest did not hide
+                    st.add("compile", ct.timing[1])
+                    st.add("compile_wait", time.perf_counter() - t1)
+            if ct is None:
                 ct = self.compile(ts)
                 st.add("compile", time.perf_counter() - t1)
-            else:  # its own duration, the part of it the harvest did not hide in "compile_wait"
-                ct, dt = fut.result()
-                st.add("compile", dt)
-                st.add("compile_wait", time.perf_counter() - t1)
         except BaseException:
             guide.close()
             raise

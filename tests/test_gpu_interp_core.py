@@ -115,3 +115,27 @@ def test_long_conjunction_values(gpu_ctx):
             assert got[r] == want, (i, r)
             seen_true += want
     assert seen_true > 0
+
+
+def test_async_compile_equals_compile(gpu_ctx):
+    """mh_tapes_compile_async on the context's worker thread gives the tape set mh_tapes_compile
+    gives (the same per-tape summaries and results), a second pending compile is refused, and a
+    context destroyed with an uncollected compile releases it."""
+    ts = _tapes(9103)
+    ct = gpu_ctx.compile(ts)
+    pend = gpu_ctx.compile_async(ts)
+    with pytest.raises(native.SieveError):
+        gpu_ctx.compile_async(ts)  # one at a time per context
+    ct2 = pend.wait()
+    assert ct2.info() == ct.info()
+    a = gpu_ctx.assignments(ts.n_vars, 4096)
+    a.generate(0x77, 0)
+    r1 = native.run(gpu_ctx, ct, a, mode=native.MODE_COUNT_ALL)
+    r2 = native.run(gpu_ctx, ct2, a, mode=native.MODE_COUNT_ALL)
+    assert all(np.array_equal(x, y) for x, y in zip(r1, r2))
+    for c in (ct, ct2):
+        c.close()
+    a.close()
+    ctx = native.Context(0)
+    ctx.compile_async(ts)
+    ctx.close()  # the pending compile is finished and dropped, the worker joined

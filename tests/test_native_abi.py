@@ -69,3 +69,12 @@ def test_comm_rank_world_checks(monkeypatch):
     for rank, world in ((0, 0), (-1, 2), (2, 2), (5, 1)):
         assert lib.mh_comm_init(fake, uid, rank, world) == native.MH_E_INVALID, (rank, world)
         assert b"rank" in lib.mh_last_error()
+
+
+def test_async_compile_argument_validation_without_device():
+    """mh_tapes_compile_async / _wait refuse a null context and a wait with nothing pending."""
+    lib = native.load()
+    h = C.c_void_p()
+    assert lib.mh_tapes_compile_async(None, None, None, 0, None, 0, 0) == native.MH_E_INVALID
+    assert lib.mh_tapes_compile_wait(None, C.byref(h), None) == native.MH_E_INVALID
+    assert b"null" in lib.mh_last_error()
