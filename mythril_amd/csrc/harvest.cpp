@@ -311,6 +311,7 @@ struct Harvester {
     AVec<AVec<uint32_t>> cap;
     AVec<std::pair<int, std::shared_ptr<const Alts>>> sets;
     AVec<uint32_t> hints;      // hint ids in the order they became hint sets
+    std::vector<uint64_t> pool_digest;  // harvest(): digests of pools[c] at [c * kMaxPool ...)
     std::map<AVec<uint32_t>, uint32_t, std::less<AVec<uint32_t>>,
              ArenaAlloc<std::pair<const AVec<uint32_t>, uint32_t>>> hint_ids;
     AVec<Alts> hint_alts;      // by id: the alternatives a hint set holds
@@ -992,10 +993,19 @@ struct Harvester {
         for (size_t i = first_parent ? 1 : 0; i < sets.size(); ++i)
             out_sets.push_back({sets[i].first, sets[i].second.get()});
         pools.assign(n_cols, {});
+        // first occurrences in order, at most kMaxPool per column; the duplicate test compares
+        // a 64-bit digest of each value before the value itself (a long path's sets repeat values)
+        pool_digest.assign((size_t)n_cols * kMaxPool, 0);
         auto add_pool = [&](uint32_t c, const V& v) {
             auto& p = pools[c];
-            if ((int)p.size() >= kMaxPool) return;
-            for (const V& x : p) if (x == v) return;
+            const size_t n = p.size();
+            if ((int)n >= kMaxPool) return;
+            uint64_t h = 0x9E3779B97F4A7C15ull;
+            for (int k = 0; k < 8; ++k) h = (h ^ v.w[k]) * 0x100000001B3ull;
+            uint64_t* dg = pool_digest.data() + (size_t)c * kMaxPool;
+            for (size_t i = 0; i < n; ++i)
+                if (dg[i] == h && p[i] == v) return;
+            dg[n] = h;
             p.push_back(v);
         };
         for (const auto& s : out_sets)
@@ -1181,37 +1191,63 @@ int32_t harvest_into(Harvester& h, const mh_node* nodes, uint32_t n_nodes, const
     h.harvest(n_nodes - 1, n_parent ? &parent : nullptr, pools, sets, copies);
     auto r = std::make_unique<mh_harvest>();
     r->width16.assign(h.widths.begin(), h.widths.end());
-    r->pool_off.push_back(0);
-    auto put = [](std::vector<uint32_t>& dst, const V& v) { dst.insert(dst.end(), v.w, v.w + 8); };
-    for (const auto& p : pools) {
-        for (const V& v : p) put(r->pool, v);
-        r->pool_off.push_back((uint32_t)(r->pool.size() / 8));
-    }
-    r->set_off.push_back(0);
-    r->alt_off.push_back(0);
+    // sized exactly first (a long path's guide holds thousands of entries), then written in place
+    size_t n_pool = 0, n_alt = 0, n_ent = 0;
+    for (const auto& p : pools) n_pool += p.size();
     for (const auto& s : sets) {
-        r->set_prob.push_back((uint8_t)s.first);
-        for (const Alt& a : *s.second) {
-            for (const auto& kv : a) {
-                r->entry_col.push_back(kv.first);
-                put(r->entry_val, kv.second);
-            }
-            r->alt_off.push_back((uint32_t)r->entry_col.size());
-        }
-        r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
+        n_alt += s.second->size();
+        for (const Alt& a : *s.second) n_ent += a.size();
     }
     for (const auto& alts : copies) {
-        r->set_prob.push_back((uint8_t)kProbDefault);
+        n_alt += alts.size();
+        for (const auto& alt : alts) n_ent += alt.size();
+    }
+    r->pool_off.resize(pools.size() + 1);
+    r->pool.resize(8 * n_pool);
+    r->set_off.resize(sets.size() + copies.size() + 1);
+    r->set_prob.resize(sets.size() + copies.size());
+    r->alt_off.resize(n_alt + 1);
+    r->entry_col.resize(n_ent);
+    r->entry_val.resize(8 * n_ent);
+    uint32_t* pv = r->pool.data();
+    r->pool_off[0] = 0;
+    for (size_t c = 0; c < pools.size(); ++c) {
+        for (const V& v : pools[c]) { memcpy(pv, v.w, sizeof v.w); pv += 8; }
+        r->pool_off[c + 1] = (uint32_t)((pv - r->pool.data()) / 8);
+    }
+    uint32_t* ec = r->entry_col.data();
+    uint32_t* ev = r->entry_val.data();
+    uint32_t* ao = r->alt_off.data();
+    uint32_t ne = 0, na = 0, ns = 0;
+    *ao++ = 0;
+    r->set_off[0] = 0;
+    for (const auto& s : sets) {
+        r->set_prob[ns] = (uint8_t)s.first;
+        for (const Alt& a : *s.second) {
+            for (const auto& kv : a) {
+                ec[ne] = kv.first;
+                memcpy(ev + 8ull * ne, kv.second.w, sizeof kv.second.w);
+                ++ne;
+            }
+            *ao++ = ne;
+            ++na;
+        }
+        r->set_off[++ns] = na;
+    }
+    for (const auto& alts : copies) {
+        r->set_prob[ns] = (uint8_t)kProbDefault;
         for (const auto& alt : alts) {
             for (const Copy& c : alt) {
-                r->entry_col.push_back(c.dst | kCopyFlag);
-                const uint32_t ev[8] = {c.src, (uint32_t)c.dlo, (uint32_t)c.slo, (uint32_t)c.nb,
-                                        0, 0, 0, 0};
-                r->entry_val.insert(r->entry_val.end(), ev, ev + 8);
+                ec[ne] = c.dst | kCopyFlag;
+                const uint32_t w[8] = {c.src, (uint32_t)c.dlo, (uint32_t)c.slo, (uint32_t)c.nb,
+                                       0, 0, 0, 0};
+                memcpy(ev + 8ull * ne, w, sizeof w);
+                ++ne;
             }
-            r->alt_off.push_back((uint32_t)r->entry_col.size());
+            *ao++ = ne;
+            ++na;
         }
-        r->set_off.push_back((uint32_t)r->alt_off.size() - 1);
+        r->set_off[++ns] = na;
     }
     const uint32_t n_sets = (uint32_t)r->set_prob.size();
     // never-empty arrays, as candidates.Guide.arrays() gives them (one zero entry)
