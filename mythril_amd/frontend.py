@@ -195,6 +195,7 @@ def sieve_model(constraints, timeout_ms: Optional[float] = None):
 
     stats = SolverStatistics()
     t0 = time.perf_counter()
+    _tls.miss_key = None
     try:
         s = sieve()  # first: an unusable device skips the term import
         ctx, terms = _terms(constraints)
@@ -213,6 +214,7 @@ def sieve_model(constraints, timeout_ms: Optional[float] = None):
         return None
     if w is None:
         stats.sieve_misses += 1
+        _tls.miss_key = key  # the fallback's model of this query is learnt (learn_from_fallback)
         return None
     conv = _config["to_terms"]  # reads reference terms for Model.eval / Model[decl]
     m = Model(s, ctx, w.schema, w.values, w.index,
@@ -247,6 +249,7 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
     constraints = [c for c in constraints if type(c) != bool]
     stats = SolverStatistics()
     fallback = _config["fallback"]
+    _tls.miss_key = None  # set by this call's sieve miss only
     if _config["enabled"] and not minimize and not maximize:
         t0 = time.perf_counter()
         m = sieve_model(constraints, timeout)
@@ -262,4 +265,52 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         log.debug("sieve found no witness and no fallback solver is configured")
         raise UnsatError
     # the fallback (the reference's get_model) counts itself through stat_smt_query
-    return fallback(tuple(constraints), minimize, maximize, enforce_execution_time)
+    model = fallback(tuple(constraints), minimize, maximize, enforce_execution_time)
+    learn_from_fallback(model)
+    return model
+
+
+def z3_column_reader(model, z3):
+    """value_of(column) over a z3 model -- the reference's Model (laser/smt/model.py:12-59: its
+    ``raw`` z3 ModelRefs) or a z3 ModelRef -- for Sieve.learn: a variable's value, an array cell
+    ``Select(A, key)``, a function cell ``f(key)``, each evaluated with model completion; None
+    for the else columns (any value completes a model) and for symbols the model does not
+    declare."""
+    models = list(getattr(model, "raw", None) or [model])
+    decls = {}
+    for zm in models:
+        for d in zm.decls():
+            decls.setdefault(d.name(), (zm, d))
+
+    def value_of(col):
+        hit = decls.get(col.symbol)
+        if hit is None or col.kind not in ("var", "cell", "ufcell"):
+            return None
+        zm, d = hit
+        if col.kind == "var":
+            v = zm.eval(d(), model_completion=True)
+        elif col.kind == "cell":
+            v = zm.eval(z3.Select(d(), z3.BitVecVal(col.key, d.range().domain().size())),
+                        model_completion=True)
+        else:
+            v = zm.eval(d(z3.BitVecVal(col.key, d.domain(0).size())), model_completion=True)
+        return v.as_long() if z3.is_bv_value(v) else None
+
+    return value_of
+
+
+def learn_from_fallback(model) -> None:
+    """The fallback's model of the query the sieve just missed becomes that query's witness in
+    the sieve (Sieve.learn), so the query's children are generated around it.  Best effort: no
+    z3, a model of another shape or any error leaves the sieve as it was."""
+    key = getattr(_tls, "miss_key", None)
+    _tls.miss_key = None
+    s = getattr(_tls, "sieve", None)
+    if key is None or s is None or model is None:
+        return
+    try:
+        import z3
+
+        s.learn(key, z3_column_reader(model, z3))
+    except Exception as e:  # noqa: BLE001 - learning never changes the answer
+        log.debug("fallback model not learnt: %s", e)

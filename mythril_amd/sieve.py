@@ -28,7 +28,7 @@ import threading
 import time
 from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -457,6 +457,9 @@ class Sieve:
         self.stats = SieveStats()
         self.witnesses: "OrderedDict[tuple, Dict[str, int]]" = OrderedDict()
         self.max_witnesses = 1 << 14
+        # the last query this sieve missed after a device round, (key, schema): a model the
+        # fallback then finds for it is learnt as its witness (learn)
+        self.last_miss: Optional[Tuple[tuple, Schema]] = None
         # the tape compile runs on the context's worker thread (mh_tapes_compile_async) while
         # this one harvests the guide: the harvest is host-only, both only read the query's
         # tapes, and the round needs both (SIEVE_OVERLAP=0: one after the other)
@@ -481,10 +484,37 @@ class Sieve:
         return self.assign
 
     def remember(self, key: tuple, w: Witness) -> None:
-        self.witnesses[key] = w.values
+        self._store(key, w.values)
+
+    def _store(self, key: tuple, values: Dict[str, int]) -> None:
+        self.witnesses[key] = values
         self.witnesses.move_to_end(key)
         while len(self.witnesses) > self.max_witnesses:
             self.witnesses.popitem(last=False)
+
+    def learn(self, key: tuple, value_of: Callable[[Column], Optional[int]]) -> int:
+        """A model the fallback found for the query this sieve missed last (the same ``key``)
+        becomes that query's remembered witness, so the query's LASER children are generated
+        around it as around a witness of the sieve's own (svm.py:257-262: the children of a state
+        z3 found feasible are asked next).  Without it one miss leaves every later query of the
+        path without parent-guided rows.  ``value_of(column)`` is the model's value of a column
+        (lower.Column: a variable, an array cell or a function cell), None where the model does
+        not fix it.  Returns the number of columns learnt."""
+        lm, self.last_miss = self.last_miss, None
+        if not key or lm is None or lm[0] != key:
+            return 0
+        values: Dict[str, int] = {}
+        for name, col in lm[1].columns.items():
+            try:
+                v = value_of(col)
+            except Exception:  # noqa: BLE001 - a column the model cannot evaluate stays free
+                v = None
+            if v is not None:
+                values[name] = int(v) & ((1 << col.width) - 1)
+        if values:
+            self._store(key, values)
+            self.stats.extra["learnt"] = self.stats.extra.get("learnt", 0) + 1
+        return len(values)
 
     def compile(self, ts: TapeSet) -> native.CompiledTapes:
         """Compile a query's tapes; a tape that runs out of registers is retried with cheap
@@ -675,6 +705,7 @@ class Sieve:
         budget = self.budget_s if budget_s is None else min(self.budget_s, budget_s)
         self.stats.queries += 1
         self.last_rounds = {}
+        self.last_miss = None
         if budget <= 0:
             self.stats.misses += 1
             return None
@@ -791,6 +822,7 @@ class Sieve:
                 if time.perf_counter() - t0 > budget:
                     break
             self.stats.misses += 1
+            self.last_miss = (key, schema) if key else None
             return None
         finally:
             ct.close()

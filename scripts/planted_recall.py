@@ -13,7 +13,12 @@ the misses are asked again of a sieve with 2^20-row second rounds (how many more
 recover).
 
     python scripts/planted_recall.py [n_paths=100] [path_len=24] [--extended] [--fake]
-                                     [--round2=always|progress|never]
+                                     [--round2=always|progress|never] [--feedback]
+
+--feedback: after a miss, the planted model M is learnt as the missed query's witness
+(Sieve.learn, what frontend.learn_from_fallback does with the fallback's model), as if z3 had
+answered the miss with M -- an upper bound on what learning z3's models gives, since z3's model of
+a prefix need not satisfy the path's later constraints as M does.
 
 --fake runs on tests/fake_device.py (CPU; use small sizes).
 """
@@ -42,7 +47,21 @@ def _pct(v):
             "p99": round(float(np.percentile(a, 99)), 3), "max": round(float(a.max()), 3)}
 
 
-def run_family(s, family, n_paths, path_len, big=None, check=True):
+def planted_value(m):
+    """value_of(column) for Sieve.learn under the planted model M."""
+    def value_of(col):
+        if col.kind == "var":
+            return m.vars.get(col.symbol)
+        if col.kind in ("cell", "else") and col.symbol in m.arrays:
+            table, els = m.arrays[col.symbol]
+            return els if col.kind == "else" else table.get(col.key, els)
+        if col.kind == "ufcell" and col.symbol in m.funcs:
+            return m.funcs[col.symbol](col.key)
+        return None
+    return value_of
+
+
+def run_family(s, family, n_paths, path_len, big=None, check=True, feedback=False):
     """Every prefix of n_paths planted paths in LASER order on sieve `s`.  Returns the summary
     and the list of missed (seed, prefix) pairs."""
     outcomes = Counter()
@@ -50,6 +69,7 @@ def run_family(s, family, n_paths, path_len, big=None, check=True):
     progress = Counter()  # first-round progress (some groups solved) of round-2 hits and misses
     times = defaultdict(list)
     bad, missed = [], []
+    learnt0 = s.stats.extra.get("learnt", 0)
     for seed in range(n_paths):
         ctx, cs, m, kinds = planted_path(family, seed, path_len)
         nodes = [c.node for c in cs]
@@ -68,6 +88,8 @@ def run_family(s, family, n_paths, path_len, big=None, check=True):
                 else:
                     kind = "miss"
                     missed.append((seed, k))
+                    if feedback:
+                        s.learn(tuple(nodes[:k]), planted_value(m))
             except Exception as e:  # noqa: BLE001 - the front end falls back on any error
                 dt = (time.perf_counter() - t0) * 1e3
                 kind = "unsupported" if "Unsupported" in type(e).__name__ else "error"
@@ -88,6 +110,7 @@ def run_family(s, family, n_paths, path_len, big=None, check=True):
         "unsupported": outcomes["unsupported"], "error": outcomes["error"],
         "invalid_witnesses": len(bad),
         "second_round": s.second_round,
+        "feedback": feedback, "learnt": s.stats.extra.get("learnt", 0) - learnt0,
         "first_round_progress": dict(progress),
         "by_newest_constraint": {
             k: {"n": sum(c.values()), "recall": round((c["hit_r1"] + c["hit_r2"]) /
@@ -128,7 +151,7 @@ def main():
     if "--extended" in sys.argv:
         big = Sieve(rows=1 << 20)
     for family in FAMILIES:
-        out = run_family(s, family, n_paths, path_len, big)
+        out = run_family(s, family, n_paths, path_len, big, feedback="--feedback" in sys.argv)
         out["device"] = "fake (CPU)" if fake else "gpu"
         print(json.dumps(out), flush=True)
     s.close()

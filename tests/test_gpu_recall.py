@@ -28,3 +28,23 @@ def test_planted_recall_floor(gpu_ctx, family):
                                        "miss", "unsupported")})
     assert out["refuted"] == 0 and out["invalid_witnesses"] == 0 and out["error"] == 0, out
     assert out["recall"] >= FLOOR[family], out
+
+
+def test_learnt_fallback_models_do_not_lower_recall(gpu_ctx):
+    """The same random-family workload with every miss answered by the planted model, learnt as
+    the missed query's witness (Sieve.learn; frontend.learn_from_fallback does it with z3's
+    model): at least the recall without, no refutation, every witness a model of the original
+    query."""
+    outs = []
+    for feedback in (False, True):
+        s = Sieve()
+        try:
+            outs.append(run_family(s, "random", 20, 16, feedback=feedback))
+        finally:
+            s.close()
+    base, fed = outs
+    print("random recall without / with learnt models", base["recall"], fed["recall"],
+          "learnt", fed["learnt"])
+    assert fed["refuted"] == 0 and fed["invalid_witnesses"] == 0 and fed["error"] == 0, fed
+    assert 0 < fed["learnt"] <= fed["miss"]
+    assert fed["recall"] >= base["recall"], (base, fed)

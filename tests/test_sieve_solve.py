@@ -195,3 +195,158 @@ def test_native_schema_decode_failure_is_retried():
         t.join()
     assert out == [["x"]] * 8 and CQ.calls == 2
     assert sch.cells == {"A": {5: "A[0x5]"}}
+
+
+class _Val:
+    def __init__(self, v):
+        self.v = v
+
+    def as_long(self):
+        return self.v
+
+
+class _Sort:
+    def __init__(self, bits, domain=None):
+        self.bits, self._domain = bits, domain
+
+    def size(self):
+        return self.bits
+
+    def domain(self):
+        return self._domain
+
+
+class _Decl:
+    """A z3 FuncDecl stand-in: a constant (arity 0) or a unary function."""
+
+    def __init__(self, name, rng, dom=None):
+        self._name, self._rng, self._dom = name, rng, dom
+
+    def name(self):
+        return self._name
+
+    def range(self):
+        return self._rng
+
+    def domain(self, i):
+        return self._dom
+
+    def __call__(self, *args):
+        return ("app", self._name) + tuple(args)
+
+
+class _Z3:
+    """The z3 calls frontend.z3_column_reader makes, over _Model's tables."""
+
+    @staticmethod
+    def BitVecVal(v, bits):
+        return ("val", v, bits)
+
+    @staticmethod
+    def Select(a, k):
+        return ("select", a, k)
+
+    @staticmethod
+    def is_bv_value(v):
+        return isinstance(v, _Val)
+
+
+class _Model:
+    """A z3 ModelRef stand-in: scalars {name: int}, arrays {name: {key: int}}, functions alike."""
+
+    def __init__(self, scalars=(), arrays=(), funcs=()):
+        self.scalars, self.arrays, self.funcs = dict(scalars), dict(arrays), dict(funcs)
+
+    def decls(self):
+        out = [_Decl(n, _Sort(256)) for n in self.scalars]
+        out += [_Decl(n, _Sort(8, domain=_Sort(256))) for n in self.arrays]
+        out += [_Decl(n, _Sort(256), dom=_Sort(512)) for n in self.funcs]
+        return out
+
+    def eval(self, t, model_completion=False):
+        assert model_completion
+        if t[0] == "select":
+            return _Val(self.arrays[t[1][1]].get(t[2][1], 0))
+        if len(t) == 2:
+            return _Val(self.scalars[t[1]])
+        return _Val(self.funcs[t[1]].get(t[2][1], 0))
+
+
+def test_z3_column_reader_reads_vars_cells_and_function_cells():
+    from mythril_amd.lower import Column
+
+    m = _Model({"x": 5}, {"calldata": {4: 0xAB}}, {"f": {9: 77}})
+    value_of = frontend.z3_column_reader(m, _Z3)
+    assert value_of(Column("x", 256, "var", "x")) == 5
+    assert value_of(Column("calldata[4]", 8, "cell", "calldata", 4)) == 0xAB
+    assert value_of(Column("f(9)", 256, "ufcell", "f", 9)) == 77
+    assert value_of(Column("calldata[*]", 8, "else", "calldata")) is None  # any value
+    assert value_of(Column("y", 256, "var", "y")) is None  # not declared by the model
+
+
+def test_fallback_model_is_learnt_as_the_parent_witness(monkeypatch):
+    """A query the sieve misses and the fallback solves: the fallback's model becomes the query's
+    witness in the sieve (Sieve.learn), so its LASER child -- the same constraints and one more --
+    is answered from rows generated around that model, where without it the child misses too."""
+    import random
+    import sys
+
+    from mythril_amd.smt import symbol_factory
+
+    fake_device.install(monkeypatch)
+    monkeypatch.setitem(sys.modules, "z3", _Z3)
+    rng = random.Random(77)
+    x0, y0 = rng.getrandbits(256) | 1, rng.getrandbits(256) | 1
+    k = (x0 * y0) % (1 << 256)
+    for learn in (True, False):
+        frontend.reset()
+        try:
+            frontend.configure(rows=256)
+            from mythril_amd import smt
+
+            smt.set_context(smt.Context())
+            x, y, z = (symbol_factory.BitVecSym(n, 256) for n in "xyz")
+            c1 = x * y == symbol_factory.BitVecVal(k, 256)
+            c2 = z == symbol_factory.BitVecVal(7, 256)
+            calls = []
+
+            def fallback(cs, mn, mx, enf):
+                calls.append(len(cs))
+                return _Model({"x": x0, "y": y0, "z": 0}) if learn else "z3 model"
+
+            frontend.configure(fallback=fallback)
+            assert frontend.get_model((c1,)) is not None and calls == [1]  # the sieve missed
+            m = frontend.get_model((c1, c2))
+            if learn:
+                assert isinstance(m, Model) and calls == [1], "the child was not answered"
+                assert (m.values["x"], m.values["y"], m.values["z"]) == (x0, y0, 7)
+                assert frontend.sieve().stats.extra.get("learnt") == 1
+            else:
+                assert calls == [1, 2]
+        finally:
+            frontend.reset()
+
+
+def test_only_a_missed_query_learns(monkeypatch):
+    """A model for a query the sieve did not miss in the same get_model call (objectives, a
+    disabled sieve) is not learnt, nor one for another key."""
+    import sys
+
+    from mythril_amd import smt
+    from mythril_amd.smt import symbol_factory
+
+    fake_device.install(monkeypatch)
+    monkeypatch.setitem(sys.modules, "z3", _Z3)
+    frontend.reset()
+    try:
+        frontend.configure(rows=256)
+        smt.set_context(smt.Context())
+        x = symbol_factory.BitVecSym("x", 256)
+        c1 = x * x == symbol_factory.BitVecVal(3, 256)  # no square root: the sieve misses
+        frontend.configure(fallback=lambda cs, *a: _Model({"x": 1}))
+        frontend.get_model((c1,), minimize=(x,))  # objectives: no sieve query, nothing learnt
+        s = frontend.sieve()
+        assert s.stats.extra.get("learnt", 0) == 0
+        assert s.learn(("other",), lambda col: 1) == 0  # not the missed key
+    finally:
+        frontend.reset()
