@@ -21,6 +21,7 @@
 // with the register budget (and occupancy) they need rather than the worst tape's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dev_isa.h"
 #include "exec.h"
@@ -46,6 +47,21 @@ constexpr int kBlock = 256;
 // flushes) but ran 7 % slower (1.92e10 vs 2.07e10 evals/s: longer barriers around the LDS
 // staging); the kernel is VALU-bound at ~2 GB/s of HBM, so 256 stays.
 constexpr int kSieveBlock = MH_SIEVE_BLOCK;
+// A short run (a query's guided first round: 4096 rows, 64 waves) is latency-bound, one wave per
+// SIMD walking the whole tape; its workgroups are one wave each, so each wave gets a CU of its
+// own (the CU's scalar unit, scalar and instruction caches): EtherThief-400's rounds 123 -> 112
+// us (NR 15), 151 -> 136 us (NR 9 with complex ops) (profiles/r05zb; two waves per SIMD instead
+// were slower, profiles/r05za).  Longer runs keep 256-thread workgroups, whose waves share one
+// LDS instruction stage.  MH_SIEVE_SHORT_BLOCK=256 for A/B.
+constexpr u64 kShortRows = 4096;
+inline int short_block() {
+    static const int b = [] {
+        const char* e = std::getenv("MH_SIEVE_SHORT_BLOCK");
+        return e && atoi(e) == 256 ? 256 : 64;
+    }();
+    return b;
+}
+inline int sieve_block(u64 rows) { return rows <= kShortRows ? short_block() : kSieveBlock; }
 #ifndef MH_SIEVE_WAVES9
 #define MH_SIEVE_WAVES9 1  // 0: every sieve variant at its natural register allocation
 #endif
@@ -227,7 +243,7 @@ __device__ __forceinline__ InsnCache lds_insns(const uint2* s_insn, u32 off, u32
     return c;
 }
 
-template <int NR, int FEAT>
+template <int NR, int FEAT, int BLOCK>
 __device__ __forceinline__ void sieve_body(const KParams& p) {
     __shared__ uint2 s_insn[kLdsInsns];
     __shared__ u32 s_off[kChunk], s_n[kChunk], s_rb[kChunk], s_tid[kChunk];
@@ -235,13 +251,13 @@ __device__ __forceinline__ void sieve_body(const KParams& p) {
     __shared__ unsigned long long s_min[kChunk];
     __shared__ unsigned long long s_cnt[kChunk];
     const u32 tid = threadIdx.x;
-    const u64 row = p.row_first + (u64)blockIdx.x * kSieveBlock + tid;
+    const u64 row = p.row_first + (u64)blockIdx.x * BLOCK + tid;
     const bool valid = row < p.row_first + p.row_count;
     DevMachine<NR> m;
     m.p = &p;
     m.lrow = valid ? row : p.row_first;
     preload<NR>(m, p);
-    const u64 block_first = p.index_base + p.row_first + (u64)blockIdx.x * kSieveBlock;
+    const u64 block_first = p.index_base + p.row_first + (u64)blockIdx.x * BLOCK;
     const u64 wave_first = block_first + (tid & ~63u);
     // grid y splits the tape list (a short run -- a query's 256-row first round is one
     // workgroup -- spreads its tapes over CUs instead of running them all on one)
@@ -282,7 +298,7 @@ __device__ __forceinline__ void sieve_body(const KParams& p) {
         const u32 wbase = __builtin_amdgcn_readfirstlane(s_meta[1]);
         const u32 nwords = __builtin_amdgcn_readfirstlane(s_meta[2]);
         const bool stream = __builtin_amdgcn_readfirstlane(s_meta[3]) != 0;
-        for (u32 k = tid; k < nwords; k += kSieveBlock) s_insn[k] = p.insns[wbase + k];
+        for (u32 k = tid; k < nwords; k += BLOCK) s_insn[k] = p.insns[wbase + k];
         __syncthreads();
         u32 off = __builtin_amdgcn_readfirstlane(s_off[0]);
         u32 n = __builtin_amdgcn_readfirstlane(s_n[0]);
@@ -326,7 +342,7 @@ __device__ __forceinline__ void sieve_body(const KParams& p) {
                 if (p.masks) {  // a part of a split tape: its wave mask, combined later
                     if ((tid & 63u) == 0) {
                         const u32 t = __builtin_amdgcn_readfirstlane(s_tid[j]);
-                        const u64 w = ((u64)blockIdx.x * kSieveBlock + (tid & ~63u)) / 64u;
+                        const u64 w = ((u64)blockIdx.x * BLOCK + (tid & ~63u)) / 64u;
                         p.masks[(u64)(t - p.mask_base) * p.mask_stride + w] = mask;
                     }
                 } else if (mask && (tid & 63u) == 0) {
@@ -569,10 +585,10 @@ constexpr int sieve_min_waves(int nr, int feat) {
     return MH_SIEVE_WAVES9 == 0 ? 1 : nr == 9 && feat == 0 ? 4 : nr == 9 && feat >= 8 ? 2 : 1;
 }
 
-template <int NR, int FEAT>
-__global__ void __launch_bounds__(kSieveBlock)
+template <int NR, int FEAT, int BLOCK>
+__global__ void __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(sieve_min_waves(NR, FEAT), 8))) sieve_kernel(const KParams p) {
-    sieve_body<NR, FEAT>(p);
+    sieve_body<NR, FEAT, BLOCK>(p);
 }
 
 // one workgroup per split tape: the AND of its parts' wave masks (kernels.h launch_combine)
@@ -595,26 +611,33 @@ __global__ void __launch_bounds__(256)
     if (cnt && hit_count) atomicAdd(&hit_count[t - result_base], cnt);
 }
 
-template <int NR, int FEAT>
-hipError_t launch_variant(const KParams& p, hipStream_t stream) {
-    const u64 blocks = (p.row_count + kSieveBlock - 1) / kSieveBlock;
+template <int NR, int FEAT, int BLOCK>
+hipError_t launch_block(const KParams& p, hipStream_t stream) {
+    const u64 blocks = (p.row_count + BLOCK - 1) / BLOCK;
     // fewer row blocks than CUs: split the tapes over grid y until the chip has ~256 workgroups
     u64 gy = 1;
     if (blocks < 256) gy = std::min<u64>(p.n_ids, (256 + blocks - 1) / blocks);
     // the parts of split tapes (conjunct-parallel short runs) each get their own workgroups up
     // to 4096 in all: a part walked after another on the same workgroup gains no latency
     if (p.masks && blocks < 4096) gy = std::max<u64>(gy, std::min<u64>(p.n_ids, 4096 / blocks));
-    hipLaunchKernelGGL((sieve_kernel<NR, FEAT>), dim3((unsigned)blocks, (unsigned)gy),
-                       dim3(kSieveBlock), 0, stream, p);
+    hipLaunchKernelGGL((sieve_kernel<NR, FEAT, BLOCK>), dim3((unsigned)blocks, (unsigned)gy),
+                       dim3(BLOCK), 0, stream, p);
     return hipGetLastError();
+}
+
+template <int NR, int FEAT>
+hipError_t launch_variant(const KParams& p, hipStream_t stream) {
+    return sieve_block(p.row_count) == 64 ? launch_block<NR, FEAT, 64>(p, stream)
+                                          : launch_block<NR, FEAT, kSieveBlock>(p, stream);
 }
 
 }  // namespace
 
 namespace mh {
 
-uint64_t sieve_mask_stride(uint64_t row_count) {
-    return (row_count + kSieveBlock - 1) / kSieveBlock * (kSieveBlock / 64);
+uint64_t sieve_mask_stride(uint64_t row_count) {  // the waves of the run's workgroups
+    const u64 b = (u64)sieve_block(row_count);
+    return (row_count + b - 1) / b * (b / 64);
 }
 
 hipError_t launch_combine(const unsigned long long* masks, uint64_t stride, const uint32_t* split,
