@@ -888,24 +888,58 @@ bool cmp_of_plain(const std::vector<mh_node>& tape, uint32_t n, Cmp& out) {
 // comparisons of t with constants and their negations -- to an empty range.  Over the lowered
 // root tape, whose nodes are hash-consed (equal terms are one node).  Such a query cannot have a
 // witness: the device rounds are skipped (the query still goes to the fallback solver).
-bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
-    const std::vector<mh_node>& tape = Q.tape;
-    std::unordered_map<uint32_t, char> asserted;
-    for (uint32_t cj : conj) asserted[cj] = 1;
+// Scratch of refuted(), kept per thread across queries: per tape node an epoch stamp for "asserted"
+// and one for "has a range" (with the range's index), so a query costs its conjuncts, not a hash
+// map built afresh (a 400-constraint path's refutation was ~45 % of its query build).
+struct RefuteScratch {
     struct Range {
         Big lo, hi;
         std::vector<uint32_t> ne;  // constants t must differ from
     };
-    std::unordered_map<uint32_t, Range> ranges;
-    auto range = [&](uint32_t t) -> Range& {
-        auto it = ranges.find(t);
-        if (it == ranges.end()) {
-            Range r;
-            const uint32_t w = tape[t].width;
-            for (uint32_t i = 0; i < w && i < 32u * NL; ++i) r.hi.w[i / 32] |= 1u << (i % 32);
-            it = ranges.emplace(t, r).first;
+    uint32_t epoch = 0;
+    std::vector<uint32_t> asserted, has_range, range_of;
+    std::vector<Range> ranges;
+    std::vector<uint32_t> range_terms;
+    void begin(size_t n) {
+        if (++epoch == 0) {  // wrapped: every stamp is stale again
+            std::fill(asserted.begin(), asserted.end(), 0);
+            std::fill(has_range.begin(), has_range.end(), 0);
+            epoch = 1;
         }
-        return it->second;
+        if (asserted.size() < n) {
+            asserted.resize(n, 0);
+            has_range.resize(n, 0);
+            range_of.resize(n, 0);
+        }
+        ranges.clear();
+        range_terms.clear();
+    }
+};
+
+// 2^w - 1 (w bits set, at most the 32 NL a Big holds)
+Big ones(uint32_t w) {
+    Big r;
+    const uint32_t n = std::min<uint32_t>(w, 32u * NL);
+    for (uint32_t i = 0; i < n / 32; ++i) r.w[i] = ~0u;
+    if (n % 32) r.w[n / 32] = (1u << (n % 32)) - 1u;
+    return r;
+}
+
+bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
+    const std::vector<mh_node>& tape = Q.tape;
+    thread_local RefuteScratch S;
+    S.begin(tape.size());
+    const uint32_t ep = S.epoch;
+    for (uint32_t cj : conj) S.asserted[cj] = ep;
+    auto range = [&](uint32_t t) -> RefuteScratch::Range& {
+        if (S.has_range[t] != ep) {
+            S.has_range[t] = ep;
+            S.range_of[t] = (uint32_t)S.ranges.size();
+            S.range_terms.push_back(t);
+            S.ranges.emplace_back();
+            S.ranges.back().hi = ones(tape[t].width);
+        }
+        return S.ranges[S.range_of[t]];
     };
     // smt.py's ULE / UGE (bitvec_helper.py: Or(ULT(a, b), a == b)) read as BVULE / BVUGE
     auto cmp_of = [&](uint32_t n, Cmp& out) -> bool {
@@ -927,7 +961,7 @@ bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
         bool neg = false;
         uint32_t n = cj;
         if (x0.op == MH_OP_NOT) {
-            if (asserted.count(x0.a)) return true;
+            if (S.asserted[x0.a] == ep) return true;
             neg = true;
             n = x0.a;
         }
@@ -939,7 +973,7 @@ bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
         if (neg)  // not (t < c) is t >= c, ...; not (t == c) is t != c
             op = op == BVULT ? MH_OP_BVUGE : op == MH_OP_BVULE ? MH_OP_BVUGT
                : op == MH_OP_BVUGT ? MH_OP_BVULE : op == MH_OP_BVUGE ? BVULT : op;
-        Range& r = range(t);
+        RefuteScratch::Range& r = range(t);
         if (op == EQ && neg) {
             r.ne.push_back(k.c);
             continue;
@@ -959,9 +993,8 @@ bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
         }
         if (r.hi < r.lo) return true;
     }
-    for (const auto& kv : ranges) {  // a range pinned to one value that a disequality excludes
-        const Range& r = kv.second;
-        if (r.lo == r.hi)
+    for (const RefuteScratch::Range& r : S.ranges) {  // a range pinned to one value that a
+        if (r.lo == r.hi)                             // disequality excludes
             for (uint32_t ne : r.ne)
                 if (Q.qpool[tape[ne].imm0] == r.lo) return true;
     }
@@ -972,30 +1005,28 @@ bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
             lo = hi = Q.qpool[tape[t].imm0];
             return;
         }
-        auto it = ranges.find(t);
-        if (it != ranges.end()) {
-            lo = it->second.lo;
-            hi = it->second.hi;
+        if (S.has_range[t] == ep) {
+            lo = S.ranges[S.range_of[t]].lo;
+            hi = S.ranges[S.range_of[t]].hi;
             return;
         }
         lo = Big();
-        hi = Big();
-        for (uint32_t i = 0; i < tape[t].width && i < 32u * NL; ++i) hi.w[i / 32] |= 1u << (i % 32);
+        hi = ones(tape[t].width);
     };
     auto le = [](const Big& a, const Big& b) { return !(b < a); };
     // 1 = true under every value in the ranges, 0 = false under every one, -1 = either
-    std::function<int(uint32_t, int)> decide = [&](uint32_t n, int depth) -> int {
+    auto decide = [&](auto& self, uint32_t n, int depth) -> int {
         const mh_node& x = tape[n];
         if (depth > 8) return -1;
         switch (x.op) {
             case TRUE_: return 1;
             case FALSE_: return 0;
             case MH_OP_NOT: {
-                const int v = decide(x.a, depth + 1);
+                const int v = self(self, x.a, depth + 1);
                 return v < 0 ? -1 : 1 - v;
             }
             case MH_OP_OR: case AND: {
-                const int a = decide(x.a, depth + 1), b = decide(x.b, depth + 1);
+                const int a = self(self, x.a, depth + 1), b = self(self, x.b, depth + 1);
                 if (x.op == MH_OP_OR) return a == 1 || b == 1 ? 1 : (a == 0 && b == 0 ? 0 : -1);
                 return a == 0 || b == 0 ? 0 : (a == 1 && b == 1 ? 1 : -1);
             }
@@ -1026,7 +1057,7 @@ bool refuted(const Query& Q, const std::vector<uint32_t>& conj) {
         }
     };
     for (uint32_t cj : conj)
-        if (decide(cj, 0) == 0) return true;
+        if (decide(decide, cj, 0) == 0) return true;
     return false;
 }
 
