@@ -258,12 +258,38 @@ using Tables = std::vector<std::pair<std::string, std::vector<Big>>>;
 
 class Query {
 public:
-    // a fresh query: the per-query scratch starts a new epoch
-    explicit Query(mh_terms& t) : T(t) {
-        T.memo_lower.reset(T.nodes.size());
+    // a fresh query: the per-query scratch starts a new epoch (the lowering memo too, unless the
+    // caller may adopt the last query's lowering: adopt_lowering, or reset_lowering if not)
+    explicit Query(mh_terms& t, bool keep_lowering = false) : T(t) {
+        if (!keep_lowering) T.memo_lower.reset(T.nodes.size());
         T.seen.reset(T.nodes.size());
         T.local.reset(T.nodes.size());
         sync();
+    }
+    void reset_lowering() { T.memo_lower.reset(T.nodes.size()); }
+    // the lowering memo (T.memo_lower, kept) is valid for this query when its harvest equals the
+    // one the memo was made under: take over the nodes, constants and cell columns it refers to
+    bool same_harvest(const Query& o) const {
+        if (cells != o.cells || uf_cells != o.uf_cells || keccak.size() != o.keccak.size())
+            return false;
+        for (size_t i = 0; i < keccak.size(); ++i) {
+            const KeccakMap& a = keccak[i].second;
+            const KeccakMap& b = o.keccak[i].second;
+            if (keccak[i].first != o.keccak[i].first || !(a.base == b.base) ||
+                a.has_bound != b.has_bound || !(a.bound == b.bound) || a.pairs != b.pairs)
+                return false;
+        }
+        return true;
+    }
+    void adopt_lowering(Query& o) {
+        ov = std::move(o.ov);
+        ov_memo = std::move(o.ov_memo);
+        ov_vals = std::move(o.ov_vals);
+        ov_index = std::move(o.ov_index);
+        ov_cv = std::move(o.ov_cv);
+        ov_cv_vals = std::move(o.ov_cv_vals);
+        ccols = std::move(o.ccols);
+        cell_index = std::move(o.cell_index);
     }
     void sync() {  // the mirror may have grown since the query was made
         if (T.cv_state.size() < T.nodes.size()) T.cv_state.resize(T.nodes.size(), 0u);
@@ -1326,11 +1352,16 @@ struct Fingerprint {
 // afresh.  Either way the result equals the from-scratch one (tests/test_query_native.py).
 class QueryState {
 public:
-    explicit QueryState(mh_terms& t) : Q(t) {}
+    explicit QueryState(mh_terms& t, bool keep_lowering = false) : Q(t, keep_lowering) {}
 
-    void start(const uint32_t* rs, uint32_t n) {
+    // warm: the last query's state, whose lowering this one takes over when their harvests are
+    // equal (a JUMPI's second branch, svm.py:257-262: the same path with the other condition --
+    // only the new constraint is lowered afresh, the rest are memo hits)
+    void start(const uint32_t* rs, uint32_t n, QueryState* warm = nullptr) {
         roots.assign(rs, rs + n);
         Q.harvest(roots);
+        if (warm && Q.same_harvest(warm->Q)) Q.adopt_lowering(warm->Q);
+        else if (warm) Q.reset_lowering();
         for (uint32_t i = 0; i < n; ++i) {  // lower_query: the AND of the lowered roots
             const uint32_t x = lowered(roots[i]);
             root = i == 0 ? x : Q.add(AND, 0, root, x);
@@ -1650,7 +1681,14 @@ int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_
         // a child of the last query (its roots plus one) extends it when the harvest is unchanged
         const bool child = st && n_roots == st->roots.size() + 1 &&
                            std::equal(st->roots.begin(), st->roots.end(), roots);
-        if (!child || !st->extend(roots[n_roots - 1])) {
+        if (!child) {
+            // not a child of the last query: a fresh state, which takes over the last query's
+            // lowering when the harvests agree (start)
+            std::unique_ptr<QueryState> prev = std::move(t->last);
+            t->last.reset(new QueryState(*t, prev != nullptr));
+            t->last->start(roots, n_roots, prev.get());
+        } else if (!st->extend(roots[n_roots - 1])) {
+            // the new constraint changed the harvest (the last state has taken it in): afresh
             t->last.reset();  // a fresh query starts a new epoch of the scratch maps
             t->last.reset(new QueryState(*t));
             t->last->start(roots, n_roots);

@@ -475,6 +475,37 @@ def test_random_queries_match_python_stages(seed):
         check_query(ctx.b, nodes[:k], (seed, k))
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_random_queries_in_jumpi_order(seed):
+    """Both branches of every constraint, as LASER asks a JUMPI's two states (svm.py:257-262):
+    the path with the condition, then with its negation, and the walk goes on from the first --
+    so the second branch and the next query are not children of the last query and are built
+    afresh, taking over the last query's lowering when the harvests agree (query.cpp
+    QueryState::start).  Node for node the Python stages' result either way."""
+    import random
+
+    from mythril_amd.smt import Not
+
+    rng = random.Random(seed)
+    ctx, cs = _random_query(rng, 10)
+    cs = [c for c in cs if hasattr(c, "node")]
+    nodes = [c.node for c in cs]
+    for k in range(1, len(nodes) + 1):
+        check_query(ctx.b, nodes[:k], (seed, k, "taken"))
+        check_query(ctx.b, nodes[:k - 1] + [Not(cs[k - 1]).node], (seed, k, "other"))
+
+
+@pytest.mark.parametrize("shape", ["killbilly", "overflow", "ether_thief"])
+def test_grown_paths_in_jumpi_order(shape):
+    from mythril_amd.smt import Not
+
+    ctx, cs = grow(shape, 40)
+    nodes = [c.node for c in cs]
+    for k in range(1, len(nodes) + 1):
+        check_query(ctx.b, nodes[:k], (shape, k, "taken"))
+        check_query(ctx.b, nodes[:k - 1] + [Not(cs[k - 1]).node], (shape, k, "other"))
+
+
 def test_mirror_shared_by_threads():
     """Sieves of several threads over one builder take turns on its session: every result is the
     one a single thread gets."""
