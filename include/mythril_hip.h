@@ -385,6 +385,15 @@ int32_t mh_run_async(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape_first, uin
 int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const mh_assign* as,
                        uint64_t row_first, uint64_t row_count, uint32_t* out /* [8*row_count] */);
 
+/* Batched parity path (Model.eval, laser/smt/model.py:45-59, read in loops by the reference:
+ * calldata.py:240-245 evaluates one byte term per call): the root values of the `n` listed tapes
+ * at ONE row of `as`, out[8 * i + k] = limb k of tapes[i]'s root.  One kernel launch per
+ * register-class variant among the listed tapes (usually one), one copy back, one sync.       */
+int32_t mh_eval_values_many(mh_ctx* ctx, const mh_tapeset* ts, const uint32_t* tapes, uint32_t n,
+                            const mh_assign* as, uint64_t row, uint32_t* out /* [8*n] */);
+/* Kernel launches mh_eval_values_many has made on this context (a test / latency counter).     */
+int32_t mh_ctx_eval_launches(const mh_ctx* ctx, uint64_t* launches);
+
 /* ---- measurement ----------------------------------------------------------------------------- */
 /* ---- native-code path (no reference counterpart: replaces the interpreter for throughput runs)
  * mh_tapes_jit compiles every tape of the set that the JIT covers to gfx950 machine code -- one
@@ -463,8 +472,11 @@ int32_t mh_comm_destroy(mh_ctx* ctx);
  * interleaved, 29 v_mad_u64_u32 + v_addc carry count (product scanning), 30 v_cmp + v_cndmask;
  * mixed classes (independent): 31 v_mad_u64_u32 / v_add_u32 alternating, 32 v_addc_co_u32
  * chains / v_xor_b32 alternating, 33 two v_mad_u64_u32 per two v_add_u32; gfx950's
- * v_bitop3_b32: 34 alone (x ^ (~y & z)), 35 alternating with v_alignbit_b32.                    */
-#define MH_MB_NUM_KINDS 36
+ * v_bitop3_b32: 34 alone (x ^ (~y & z)), 35 alternating with v_alignbit_b32; round 6:
+ * 36 v_cmp_lt_u64 and 37 v_cmp_eq_u64 into SGPR pairs, 38 v_lshl_add_u64, 39 v_mul_lo_u32,
+ * 40 v_mul_hi_u32, 41 v_mul_u32_u24, 42 v_sub_co_u32_e64 into SGPR pairs, 43 v_cmp_lt_u32_e64,
+ * 44 a 256-bit `<` as 4 lt + 3 eq 64-bit compares with SALU folds (+1 filler compare).    */
+#define MH_MB_NUM_KINDS 45
 int32_t mh_microbench_issue(mh_ctx* ctx, uint32_t kind, uint32_t waves_per_simd,
                             double* lane_ops_per_s);
 /* Survivor-gather micro-benchmark (the memory side of the lane compaction costed in DESIGN.md

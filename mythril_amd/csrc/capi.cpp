@@ -85,6 +85,8 @@ struct mh_ctx {
     size_t masks_bytes = 0;
     // mh_tapes_compile_async: one worker thread, started on first use, joined by ctx_free
     AsyncCompile* acomp = nullptr;
+    // kernel launches of mh_eval_values_many (Model.eval batching is measured by it)
+    uint64_t eval_launches = 0;
 };
 
 // One compile at a time, handed to a worker thread that waits on a condition variable (a thread
@@ -1370,6 +1372,80 @@ int32_t mh_eval_values(mh_ctx* ctx, const mh_tapeset* ts, uint32_t tape, const m
     (void)hipFree(d);
     if (e != hipSuccess)
         return set_err(MH_E_DEVICE, std::string("mh_eval_values: ") + hipGetErrorString(e));
+    return MH_OK;
+}
+
+int32_t mh_eval_values_many(mh_ctx* ctx, const mh_tapeset* ts, const uint32_t* tapes,
+                            uint32_t n, const mh_assign* as, uint64_t row, uint32_t* out) {
+    if (int32_t r = check_run_args(ctx, ts, 0, 0, as, row, 1, MH_MODE_COUNT_ALL)) return r;
+    if (n == 0) return MH_OK;
+    if (!tapes || !out) return set_err(MH_E_INVALID, "null tapes / out");
+    uint32_t top = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (tapes[i] >= ts->n_tapes) return set_err(MH_E_INVALID, "tape id out of bounds");
+        top = std::max(top, tapes[i]);
+    }
+    if (int32_t r = use_device(ctx)) return r;
+    // one launch of the production sieve kernel in values mode per register-class variant: the
+    // listed tapes of a variant are its id list, their values land at [position][8] (one row)
+    std::vector<std::pair<uint32_t, uint32_t>> by_var;  // (variant, position in `tapes`)
+    by_var.reserve(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t v = mh::variant_of(ts->info[tapes[i]].n_regs, ts->info[tapes[i]].features);
+        if (!mh::variant_fits(v, as->stride)) return refuse_capacity(as->stride);
+        by_var.push_back({v, i});
+    }
+    std::stable_sort(by_var.begin(), by_var.end(),
+                     [](const auto& a, const auto& b) { return a.first < b.first; });
+    // device block: values [n][8], ids [n], first_hit / hit_count [top + 1] each (scratch: the
+    // kernel's count-mode bookkeeping, indexed by tape id)
+    const size_t n_words = (size_t)8 * n + n + 4 * ((size_t)top + 1) + 2;
+    std::vector<uint32_t> h(n + 4 * ((size_t)top + 1) + 2, 0u);
+    for (uint32_t i = 0; i < n; ++i) h[i] = tapes[by_var[i].second];
+    // the ctx's grow-only result buffer (stream-ordered after any earlier use of it)
+    void* dv = nullptr;
+    MH_HIP(ctx_dbuf(ctx, n_words * sizeof(uint32_t), &dv));
+    uint32_t* d = static_cast<uint32_t*>(dv);
+    uint32_t* d_ids = d + 8 * (size_t)n;
+    uint32_t* d_res = d_ids + n + ((n & 1) ? 1 : 0);  // 8-byte aligned
+    hipError_t e = hipMemcpyAsync(d_ids, h.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                  ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(d_res, 0xFF, 2 * ((size_t)top + 1) * sizeof(uint32_t), ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(d_res + 2 * ((size_t)top + 1), 0, 2 * ((size_t)top + 1) * sizeof(uint32_t),
+                           ctx->stream);
+    uint32_t launches = 0;
+    for (uint32_t i = 0; i < n && e == hipSuccess;) {
+        uint32_t j = i;
+        while (j < n && by_var[j].first == by_var[i].first) ++j;
+        mh::KParams p = make_params(ts, 0, as, row, 1, 0, MH_MODE_COUNT_ALL);
+        p.tape_ids = d_ids + i;
+        p.n_ids = j - i;
+        p.first_hit = reinterpret_cast<unsigned long long*>(d_res);
+        p.hit_count = reinterpret_cast<unsigned long long*>(d_res + 2 * ((size_t)top + 1));
+        p.values_out = d + 8 * (size_t)i;
+        e = mh::launch_sieve(p, by_var[i].first, ctx->stream);
+        ++launches;
+        i = j;
+    }
+    std::vector<uint32_t> vals((size_t)8 * n);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(vals.data(), d, vals.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess)
+        return set_err(MH_E_DEVICE, std::string("mh_eval_values_many: ") + hipGetErrorString(e));
+    for (uint32_t i = 0; i < n; ++i)
+        std::memcpy(out + 8 * (size_t)by_var[i].second, vals.data() + 8 * (size_t)i,
+                    8 * sizeof(uint32_t));
+    ctx->eval_launches += launches;
+    return MH_OK;
+}
+
+int32_t mh_ctx_eval_launches(const mh_ctx* ctx, uint64_t* launches) {
+    if (!ctx || !launches) return set_err(MH_E_INVALID, "null argument");
+    *launches = ctx->eval_launches;
     return MH_OK;
 }
 

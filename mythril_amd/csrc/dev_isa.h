@@ -32,6 +32,14 @@
 #pragma once
 #include <stdint.h>
 
+// the opcode helpers below are shared by the host (compiler, emulators) and the device's C++
+// step() path (exec.h; the MH_ASM_CORE=0 build)
+#if defined(__HIPCC__)
+#define MH_ISA_FN static inline __host__ __device__
+#else
+#define MH_ISA_FN static inline
+#endif
+
 #define MH_MAX_PRELOAD 4   // assignment columns kept resident in R0..R3 for the whole launch
 #define MH_NR_SMALL 7      // register-file sizes of the kernel variants (tapes bucketed by need);
 #define MH_NR_MID 9
@@ -95,7 +103,7 @@ enum mh_dop : uint8_t {
 static_assert(D_NUM_ASM <= D_FIRST_COMPLEX, "asm opcode space");
 
 // the base op of an X form (identity for every other op)
-static inline unsigned mh_base_op(unsigned op) {
+MH_ISA_FN unsigned mh_base_op(unsigned op) {
     if (op >= D_ADD_RX && op <= D_SGE_CX) return D_ADD_R + (op - D_ADD_RX);
     switch (op) {
         case D_MUL_RX: return D_MUL_R;
@@ -106,7 +114,7 @@ static inline unsigned mh_base_op(unsigned op) {
 }
 
 // the X form of a (final, R- or C-form) asm op, or 0 when it has none
-static inline unsigned mh_xform(unsigned op) {
+MH_ISA_FN unsigned mh_xform(unsigned op) {
     if (op >= D_ADD_R && op <= D_SGE_C) return D_ADD_RX + (op - D_ADD_R);
     switch (op) {
         case D_MUL_R: return D_MUL_RX;
@@ -117,14 +125,14 @@ static inline unsigned mh_xform(unsigned op) {
 }
 
 // ops whose result is a Bool (0/1 in limb 0)
-static inline bool mh_produces_bool(unsigned op) {
+MH_ISA_FN bool mh_produces_bool(unsigned op) {
     op = mh_base_op(op);
     return (op >= D_EQ_R && op <= D_SGE_C) || (op >= D_BAND && op <= D_FALSE) || op == D_BITE || op == D_BANDZ ||
            op == D_UADD_NOOVFL || op == D_UMUL_NOOVFL;
 }
 
 // *_R / *_C pairs (y from a register / inline constant): 1 = R form, 2 = C form, 0 = neither
-static inline int mh_pair_form(unsigned op) {
+MH_ISA_FN int mh_pair_form(unsigned op) {
     op = mh_base_op(op);
     if (op >= D_ADD_R && op <= D_SGE_C) return 1 + ((op - D_ADD_R) & 1);
     if (op == D_MUL_R || op == D_MUL_C) return 1 + (op - D_MUL_R);
@@ -133,7 +141,7 @@ static inline int mh_pair_form(unsigned op) {
 }
 
 // accumulator index (last register of the planes) of the kernel variant a tape needs
-static inline unsigned mh_nrx_of(unsigned n_regs) {
+MH_ISA_FN unsigned mh_nrx_of(unsigned n_regs) {
     return n_regs <= MH_NR_SMALL ? MH_NR_SMALL : n_regs <= MH_NR_MID ? MH_NR_MID : MH_NR_MAX;
 }
 static_assert(D_NUM_OPS <= 128, "opcode space");

@@ -169,8 +169,12 @@ __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, I
         const u32 w0 = __builtin_amdgcn_readlane(ic.w0, ip);
         const u32 w1 = __builtin_amdgcn_readlane(ic.w1, ip);
         const u32 op = w1 & 0xFFu;
+#if MH_ASM_CORE
         // D_BANDZ: the asm core left there because the conjunction is 0 in every lane (X = 0)
         if (op == D_END || op == D_BANDZ) break;
+#else
+        if (op == D_END) break;
+#endif
         if (op == D_WINDOW) {
             win += MH_WINDOW;
             const u32 j = win + (threadIdx.x & 63u);
@@ -213,6 +217,10 @@ __device__ __forceinline__ void exec_tape(DevMachine<NR>& m, const uint2* src, I
 #else
         m.ic = ic;
         ip += step<FEAT, true>(m, w0, w1, ip);
+        // D_BANDZ runs like D_BAND; the tape ends only when no lane's conjunction is left true
+        // (X = 0 in every lane, the root of every row the wave holds), as the asm core's exit
+        if (op == D_BANDZ && __builtin_amdgcn_ballot_w64((m.read0(m.nrx()) & 1u) != 0u) == 0ull)
+            break;
 #endif
     }
 }
@@ -548,6 +556,66 @@ __global__ void __launch_bounds__(kBlock) microbench_kernel(u32 iters, u32* sink
                                  "v_bitop3_b32 %2, %2, %8, %6 bitop3:0x96\n v_alignbit_b32 %3, %3, %7, 9\n")
                              : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
                              : "v"(y));
+            // round 6: 64-bit compares and the other candidates for the
+            // 4-cycle class -- v_cmp_{lt,eq}_u64 into SGPR pairs, v_lshl_add_u64, the 32-bit
+            // multiplies, a VOP3 v_sub_co into an SGPR pair, v_cmp_lt_u32 into an SGPR pair, and
+            // the lexicographic 256-bit `<` as 64-bit compares (4 lt + 3 eq + SALU folds)
+            if constexpr (KIND == 36 || KIND == 37) {
+                u64 m0 = ((u64)a1 << 32) | a0, m1 = ((u64)a3 << 32) | a2, m2 = ((u64)a5 << 32) | a4,
+                    m3 = ((u64)a7 << 32) | a6, yy = ((u64)y << 32) | (y ^ 0x9E3779B9u);
+                if constexpr (KIND == 36)
+                    asm volatile(MB8("v_cmp_lt_u64_e64 s[20:21], %0, %4\n v_cmp_lt_u64_e64 s[22:23], %1, %4\n"
+                                     "v_cmp_lt_u64_e64 s[24:25], %2, %4\n v_cmp_lt_u64_e64 s[26:27], %3, %4\n")
+                                 : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3) : "v"(yy)
+                                 : "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+                else
+                    asm volatile(MB8("v_cmp_eq_u64_e64 s[20:21], %0, %4\n v_cmp_eq_u64_e64 s[22:23], %1, %4\n"
+                                     "v_cmp_eq_u64_e64 s[24:25], %2, %4\n v_cmp_eq_u64_e64 s[26:27], %3, %4\n")
+                                 : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3) : "v"(yy)
+                                 : "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+                a0 ^= (u32)m0 ^ (u32)m1; a1 ^= (u32)m2 ^ (u32)m3;
+            }
+            if constexpr (KIND == 38) {
+                u64 m0 = ((u64)a1 << 32) | a0, m1 = ((u64)a3 << 32) | a2, m2 = ((u64)a5 << 32) | a4,
+                    m3 = ((u64)a7 << 32) | a6, yy = ((u64)y << 32) | (y ^ 0x9E3779B9u);
+                asm volatile(MB8("v_lshl_add_u64 %0, %0, 0, %4\n v_lshl_add_u64 %1, %1, 0, %4\n"
+                                 "v_lshl_add_u64 %2, %2, 0, %4\n v_lshl_add_u64 %3, %3, 0, %4\n")
+                             : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3) : "v"(yy));
+                a0 = (u32)m0; a1 = (u32)(m0 >> 32); a2 = (u32)m1; a3 = (u32)(m1 >> 32);
+                a4 = (u32)m2; a5 = (u32)(m2 >> 32); a6 = (u32)m3; a7 = (u32)(m3 >> 32);
+            }
+            if constexpr (KIND == 39) MB_ONE("v_mul_lo_u32");
+            if constexpr (KIND == 40) MB_ONE("v_mul_hi_u32");
+            if constexpr (KIND == 41) MB_ONE("v_mul_u32_u24");
+            if constexpr (KIND == 42)
+                asm volatile(MB8("v_sub_co_u32_e64 %0, s[20:21], %0, %8\n v_sub_co_u32_e64 %1, s[22:23], %1, %8\n"
+                                 "v_sub_co_u32_e64 %2, s[24:25], %2, %8\n v_sub_co_u32_e64 %3, s[26:27], %3, %8\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y) : "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+            if constexpr (KIND == 43)
+                asm volatile(MB8("v_cmp_lt_u32_e64 s[20:21], %0, %8\n v_cmp_lt_u32_e64 s[22:23], %1, %8\n"
+                                 "v_cmp_lt_u32_e64 s[24:25], %2, %8\n v_cmp_lt_u32_e64 s[26:27], %3, %8\n")
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                             : "v"(y) : "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+            if constexpr (KIND == 44) {
+                // a 256-bit unsigned `<` as 64-bit compares: lt3 | eq3 & (lt2 | eq2 & (lt1 | eq1 &
+                // lt0)), 7 VALU compares (+ 1 filler compare, so 4 of them are the 32 VALU of an
+                // iteration) and the folds on the scalar unit
+                u64 m0 = ((u64)a1 << 32) | a0, m1 = ((u64)a3 << 32) | a2, m2 = ((u64)a5 << 32) | a4,
+                    m3 = ((u64)a7 << 32) | a6, yy = ((u64)y << 32) | (y ^ 0x9E3779B9u);
+#define LT256 "v_cmp_lt_u64_e64 s[20:21], %0, %4\n v_cmp_lt_u64_e64 s[22:23], %1, %4\n" \
+              "v_cmp_eq_u64_e64 s[24:25], %1, %4\n v_cmp_lt_u64_e64 s[26:27], %2, %4\n" \
+              "s_and_b64 s[20:21], s[24:25], s[20:21]\n s_or_b64 s[20:21], s[22:23], s[20:21]\n" \
+              "v_cmp_eq_u64_e64 s[24:25], %2, %4\n v_cmp_lt_u64_e64 s[22:23], %3, %4\n" \
+              "s_and_b64 s[20:21], s[24:25], s[20:21]\n s_or_b64 s[20:21], s[26:27], s[20:21]\n" \
+              "v_cmp_eq_u64_e64 s[24:25], %3, %4\n v_cmp_eq_u64_e64 s[26:27], %0, %4\n" \
+              "s_and_b64 s[20:21], s[24:25], s[20:21]\n s_or_b64 s[20:21], s[22:23], s[20:21]\n"
+                asm volatile(LT256 LT256 LT256 LT256
+                             : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3) : "v"(yy)
+                             : "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+#undef LT256
+                a0 ^= (u32)m0 ^ (u32)m1; a1 ^= (u32)m2 ^ (u32)m3;
+            }
             // partial EXEC masks: does the SIMD skip lane groups that are all inactive?
             if constexpr (KIND >= 21 && KIND <= 24) {
                 constexpr uint64_t kExec = KIND == 21 || KIND == 22 ? 0x00000000FFFFFFFFull
@@ -691,7 +759,8 @@ hipError_t launch_microbench(uint32_t kind, uint32_t iters, uint32_t blocks, uin
         MB_CASE(15) MB_CASE(16) MB_CASE(17) MB_CASE(18) MB_CASE(19) MB_CASE(20)
         MB_CASE(21) MB_CASE(22) MB_CASE(23) MB_CASE(24) MB_CASE(25) MB_CASE(26) MB_CASE(27)
         MB_CASE(28) MB_CASE(29) MB_CASE(30) MB_CASE(31) MB_CASE(32) MB_CASE(33) MB_CASE(34)
-        MB_CASE(35)
+        MB_CASE(35) MB_CASE(36) MB_CASE(37) MB_CASE(38) MB_CASE(39) MB_CASE(40) MB_CASE(41)
+        MB_CASE(42) MB_CASE(43) MB_CASE(44)
 #undef MB_CASE
         default: return hipErrorInvalidValue;
     }

@@ -81,6 +81,8 @@ SIGNATURES = {
     "mh_microbench_gather": (C.c_int32, [C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_uint32, C.POINTER(C.c_double),
                                          C.POINTER(C.c_double), _u64p]),
+    "mh_eval_values_many": (C.c_int32, [_vp, _vp, _u32p, C.c_uint32, _vp, C.c_uint64, _u32p]),
+    "mh_ctx_eval_launches": (C.c_int32, [_vp, _u64p]),
     "mh_tapes_jit": (C.c_int32, [_vp, C.c_uint32, C.c_uint32]),
     "mh_tapes_jit_info": (C.c_int32, [_vp, _vp]),
     "mh_tapes_jit_code_id": (C.c_int32, [_vp, _u64p]),
@@ -140,7 +142,9 @@ MB_KINDS = ("add_co_chain", "mad_u64_u32", "add_u32", "xor_b32", "alignbit_b32",
             "xnor_b32", "and_b32", "or_b32", "not_b32", "xor_exec32", "alignbit_exec32",
             "xor_exec16", "xor_exec_alt", "dep_mad_u64_u32", "dep_add_u32", "dep_addc_vcc",
             "dep_mad_2chains", "dep_mad_carry", "dep_cmp_cndmask", "mix_mad_add", "mix_addc_xor",
-            "mix_mad2_add2", "bitop3_b32", "mix_bitop3_alignbit")
+            "mix_mad2_add2", "bitop3_b32", "mix_bitop3_alignbit", "cmp_lt_u64", "cmp_eq_u64",
+            "lshl_add_u64", "mul_lo_u32", "mul_hi_u32", "mul_u32_u24", "sub_co_e64_sgpr",
+            "cmp_lt_u32_e64", "lt256_via_u64")
 
 
 class NativeUnavailable(RuntimeError):
@@ -1052,6 +1056,23 @@ def eval_values(ctx: Context, tapes: CompiledTapes, tape: int, assign: Assignmen
     out = np.zeros((8, max(rc, 1)), dtype=np.uint32)
     _check(ctx.lib.mh_eval_values(ctx.h, tapes.h, tape, assign.h, row_first, rc, _ptr(out)))
     return out[:, :rc]
+
+
+def eval_values_many(ctx: Context, tapes: CompiledTapes, ids: Sequence[int], assign: Assignments,
+                     row: int = 0) -> np.ndarray:
+    """Root values of the tapes `ids` at one row (mh_eval_values_many): u32 [len(ids), 8]."""
+    ids_a = np.ascontiguousarray(ids, dtype=np.uint32)
+    out = np.zeros((max(len(ids_a), 1), 8), dtype=np.uint32)
+    _check(ctx.lib.mh_eval_values_many(ctx.h, tapes.h, _ptr(ids_a), len(ids_a), assign.h, row,
+                                       _ptr(out)))
+    return out[:len(ids_a)]
+
+
+def eval_launches(ctx: Context) -> int:
+    """Kernel launches mh_eval_values_many has made on `ctx`."""
+    v = C.c_uint64()
+    _check(ctx.lib.mh_ctx_eval_launches(ctx.h, C.byref(v)))
+    return int(v.value)
 
 
 def limbs_to_ints(arr: np.ndarray) -> Sequence[int]:

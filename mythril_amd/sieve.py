@@ -604,8 +604,9 @@ class Sieve:
                     for k in range(8):
                         soa[i, k, 0] = (v >> (32 * k)) & 0xFFFFFFFF
                 assign.upload(soa)
-                return [_limbs(native.eval_values(self.ctx, ct, i, assign, 0, 1)[:, 0])
-                        for i in range(len(terms))]
+                # every root in one batch (mh_eval_values_many: one launch per register class)
+                out = native.eval_values_many(self.ctx, ct, list(range(len(terms))), assign, 0)
+                return [_limbs(out[i]) for i in range(len(terms))]
             finally:
                 assign.close()
         finally:

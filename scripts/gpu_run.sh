@@ -4,6 +4,7 @@
 # steps (each under its own time limit, stopping at the first failure):
 #   native    tests/test_gpu_native.py (native code on the reference vectors, query shapes, 2^26)
 #   gpu       the whole -m gpu suite
+#   noasm     the C++ step() build of the interpreter against the oracle (one test)
 #   smoke     __graft_entry__.smoke()
 #   bench     default bench.py (N=1)
 #   miss      scripts/miss_cost.py (per-stage cost of sieve misses, JIT build vs interpreter)
@@ -26,6 +27,8 @@
 #   pprof4    pprofile for the default and variant libraries ($PV, default nowin) at first-round
 #             sizes $PFR (default 256 4096)
 #   bitop3    scripts/valu_peak.py for v_bitop3_b32 beside xor / alignbit / cndmask
+#   valu6     scripts/valu_peak.py for the round-6 candidates (64-bit compares, v_lshl_add_u64, the
+#             32-bit multiplies) beside the carry chains and v_mad_u64_u32
 #   hostprof  scripts/solve_profile.py (cProfile of LASER-order queries at 400 constraints)
 #   hiptrace  rocprofv3 HIP runtime + kernel trace of solve_profile.py (EtherThief-400)
 #   pprofile  rocprofv3 kernel trace + stats of path_scaling.py at 400 constraints
@@ -59,6 +62,7 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     native)   timeout -k 10 1000 $PYT tests/test_gpu_native.py > "$OUT/pytest_native.txt" 2>&1 ;;
+    noasm)    timeout -k 10 400 $PYT -m gpu tests/test_gpu_parity.py -k cpp_step_build > "$OUT/pytest_noasm.txt" 2>&1 ;;
     gpu)      timeout -k 10 1100 $PYT -m gpu tests > "$OUT/pytest_gpu.txt" 2>&1 ;;
     smoke)    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 ;;
     bench)    timeout -k 10 600 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.log" ;;
@@ -117,6 +121,9 @@ for step in "$@"; do
                 MYTHRIL_HIP_LIB=$lib SIEVE_FIRST_ROWS=$fr timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$tag" -o $tag -- \
                   python -u scripts/path_scaling.py 400 > "$OUT/$tag.jsonl" 2> "$OUT/$tag.log" || exit 1; done; done ;;
     bitop3)   timeout -k 10 300 python -u scripts/valu_peak.py bitop3_b32 mix_bitop3_alignbit xor_b32 alignbit_b32 cndmask_b32 > "$OUT/valu_bitop3.json" 2> "$OUT/valu_bitop3.log" ;;
+    valu6)    timeout -k 10 300 python -u scripts/valu_peak.py cmp_lt_u64 cmp_eq_u64 lshl_add_u64 mul_lo_u32 mul_hi_u32 \
+                mul_u32_u24 sub_co_e64_sgpr cmp_lt_u32_e64 lt256_via_u64 add_co_chain sub_co_vcc_chain mad_u64_u32 \
+                cmp_eq_e32 xor_b32 bitop3_b32 or3_b32 > "$OUT/valu6.json" 2> "$OUT/valu6.log" ;;
     hostprof) timeout -k 10 300 python -u scripts/solve_profile.py ether_thief 400 40 > "$OUT/solve_profile_et400.txt" 2>&1 && \
               timeout -k 10 300 python -u scripts/solve_profile.py killbilly 400 40 > "$OUT/solve_profile_kb400.txt" 2>&1 ;;
     hiptrace) timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --stats --output-format csv -d "$OUT/htrace" -o htrace -- \

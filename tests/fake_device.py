@@ -1,10 +1,10 @@
 """A CPU stand-in for the device side of mythril_amd.native, for tests of Sieve.solve's host logic
 without a GPU (test infrastructure only: the product path never imports this).
 
-``install(monkeypatch)`` replaces native.Context, native.run, native.run_rows, native.query_round
-and native.eval_values with restatements on the oracle: the guided generator (oracle/guided_gen.py, the restatement of
-mh_assign_generate_guided, pinned against the device by tests/test_gpu_frontend.py) and the tape
-evaluator (oracle/smt_eval.py).  FIRST_HIT is the smallest satisfying row per tape.  Slow (Python
+``install(monkeypatch)`` replaces native.Context, native.run, native.run_rows, native.query_round,
+native.eval_values and native.eval_values_many with restatements on the oracle: the guided
+generator (oracle/guided_gen.py, the restatement of mh_assign_generate_guided, pinned against the
+device by tests/test_gpu_frontend.py) and the tape evaluator (oracle/smt_eval.py).  FIRST_HIT is the smallest satisfying row per tape.  Slow (Python
 big-int evaluation): use small rounds, e.g. Sieve(rows=256).
 """
 import numpy as np
@@ -115,9 +115,23 @@ def fake_eval_values(ctx, tapes, tape, assign, row_first=0, row_count=None):
     return out[:, :rc]
 
 
+LAUNCHES = [0]  # batched evaluations (one per eval_values_many call: one variant stands in)
+
+
+def fake_eval_values_many(ctx, tapes, ids, assign, row=0):
+    LAUNCHES[0] += 1
+    out = np.zeros((max(len(ids), 1), 8), dtype=np.uint32)
+    for i, t in enumerate(ids):
+        v = int(E.evaluate(tapes.tapes[t], tapes.pool, assign.rows[row]))
+        for k in range(8):
+            out[i, k] = (v >> (32 * k)) & 0xFFFFFFFF
+    return out[:len(ids)]
+
+
 def install(monkeypatch):
     monkeypatch.setattr(native, "Context", FakeContext)
     monkeypatch.setattr(native, "run", fake_run)
     monkeypatch.setattr(native, "run_rows", fake_run_rows)
     monkeypatch.setattr(native, "query_round", fake_query_round)
     monkeypatch.setattr(native, "eval_values", fake_eval_values)
+    monkeypatch.setattr(native, "eval_values_many", fake_eval_values_many)

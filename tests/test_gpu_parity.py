@@ -818,3 +818,21 @@ def test_query_round_equals_generate_then_run_rows(gpu_ctx):
             guide.close()
     finally:
         s.close()
+
+
+def test_cpp_step_build_matches_oracle(gpu_ctx):
+    """the C++ step() build of the interpreter (`make noasm`, MH_ASM_CORE=0) runs
+    each short-circuit D_BANDZ and leaves a tape only when no lane's conjunction is left true,
+    so its counts, first witnesses and a LASER query's witness equal the oracle's (the check runs
+    in one child process with MYTHRIL_HIP_LIB naming that library: tests/noasm_check.py)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(HERE)
+    lib = os.path.join(root, "mythril_amd", "libmythril_hip_noasm.so")
+    assert os.path.exists(lib), "build it first: make -C mythril_amd/csrc noasm (build() does)"
+    env = dict(os.environ, MYTHRIL_HIP_LIB=lib)
+    r = subprocess.run([sys.executable, "-u", "-m", "tests.noasm_check"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "noasm ok" in r.stdout
