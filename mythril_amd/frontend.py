@@ -20,7 +20,9 @@ Mirrors mythril/support/model.py:15-62 line for line in behaviour —
 — with one change: when there is nothing to optimise (``minimize == maximize == ()``, the
 feasibility case of ``Constraints.is_possible`` and the detection modules), the
 query first goes to the sieve (sieve.py).  A witness comes back as a sieve ``Model``, re-verified
-by the configured verifier (z3 when the reference runs around this module, plugin.py).  A miss,
+by the configured verifier: under the plugin, z3 checks the query with every symbol pinned to the
+witness (plugin.witness_pins) and the caller gets z3's model in the reference's ``Model``
+(plugin.z3_verifier); with no verifier, the sieve ``Model`` itself.  A miss,
 an unsupported term, a device error or a failed verification hands the query, unchanged, to the
 fallback solver — the reference's own ``get_model`` when installed by the plugin.  With no
 fallback configured a miss is reported the way the reference reports a z3 ``unknown``:
@@ -44,9 +46,11 @@ log = logging.getLogger(__name__)
 _tls = threading.local()
 _config = {
     "fallback": None,   # callable(constraints, minimize, maximize, enforce_execution_time)
-    "verify": None,     # callable(constraints, model[, timeout_ms=...]) -> bool (z3 re-check);
-                        # timeout_ms (what is left of get_model's budget) is passed only to a
-                        # verifier that declares it (or **kwargs)
+    "verify": None,     # callable(constraints, model[, timeout_ms=...]) -> verdict (z3 re-check):
+                        # falsy rejects, True keeps the sieve Model, another object is the
+                        # model returned instead (z3_verifier: the reference's Model); timeout_ms
+                        # (what is left of get_model's budget) is passed only to a verifier that
+                        # declares it (or **kwargs)
     "to_terms": None,   # callable(constraints) -> (smt.Context, [Bool]) for foreign terms
     "log_writer": None,  # callable(constraints, minimize, maximize) -> SMT-LIB2 text (foreign)
     "fallback_logs": False,  # the fallback writes --solver-log files itself (the reference's)
@@ -91,10 +95,12 @@ def _takes_timeout(fn) -> bool:
     return any(p.name == "timeout_ms" or p.kind == p.VAR_KEYWORD for p in ps)
 
 
-def _verify(verify, constraints, m, left) -> bool:
+def _verify(verify, constraints, m, left):
+    """The verifier's verdict: falsy rejects; True accepts the sieve's Model; any other object
+    is the model to return instead (plugin.z3_verifier: the reference's Model of z3's check)."""
     if _takes_timeout(verify):
-        return bool(verify(constraints, m, timeout_ms=left))
-    return bool(verify(constraints, m))
+        return verify(constraints, m, timeout_ms=left)
+    return verify(constraints, m)
 
 
 def reset() -> None:
@@ -231,6 +237,8 @@ def sieve_model(constraints, timeout_ms: Optional[float] = None):
         if not ok:
             stats.sieve_rejected += 1
             return None
+        if ok is not True:
+            m = ok  # the verifier's own model (the reference's type)
     stats.sieve_hits += 1
     return m
 

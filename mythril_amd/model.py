@@ -18,10 +18,10 @@ terms wider than 256 bits (512-bit keccak inputs, the 257-bit no-overflow sums) 
 """
 from __future__ import annotations
 
-from typing import TYPE_CHECKING, List, Optional, Union
+from typing import TYPE_CHECKING, List, Optional, Sequence, Union
 
 from .lower import Schema
-from .tape import BOOL, Op, TapeError
+from .tape import ARITY, BOOL, Op, TapeError
 
 if TYPE_CHECKING:  # pragma: no cover
     from .sieve import Sieve
@@ -117,6 +117,8 @@ class Model:
         self.importer = importer
         self._own_importer = None
         self.raw = [self]
+        self._memo: dict = {}      # (node, model_completion) -> value (eval_many)
+        self._resident: dict = {}  # column tuple -> the witness row on the device
 
     # -- declarations -------------------------------------------------------------------------
     def decls(self) -> List[Decl]:
@@ -197,33 +199,168 @@ class Model:
         """model.py:45-59: the value of `expression` (this package's term or a reference z3
         term) under this model.  Without model_completion, a term reading a symbol the model
         does not interpret is returned unevaluated, as given (z3 behaviour); with it, such
-        symbols read 0."""
-        from .lower import LoweringUnsupported
+        symbols read 0.  Values are memoised per term; see ``eval_many`` for the batching."""
+        return self.eval_many([expression], model_completion)[0]
+
+    def eval_many(self, expressions: Sequence[object], model_completion: bool = False) -> list:
+        """The values of several terms: every term this model has not evaluated yet goes to the
+        device in ONE batch (one compile, the witness row uploaded once per column set and kept,
+        one ``mh_eval_values_many`` launch per register class).
+
+        The reference reads models one term at a time in loops -- ``calldata.concrete`` asks
+        ``eval(If(i < size, calldata[i], 0))`` for i = 0, 1, ... (calldata.py:234-245) -- so a
+        lone term that reads an array at a constant index is evaluated together with the same
+        term at the next ``SPECULATE`` indices (its constant index replaced; the terms are
+        hash-consed, so the reference's next term imports to exactly that node and is then a
+        memo hit).  A speculated term that cannot be evaluated is dropped silently."""
+        mc = bool(model_completion)
+        out: list = [None] * len(expressions)
+        pending: "dict[int, list]" = {}
+        for i, e in enumerate(expressions):
+            node, _ = self._term(e)
+            got = self._memo.get((node, mc))
+            if got is not None:
+                out[i] = e if got is _UNEVALUATED else got
+            else:
+                pending.setdefault(node, []).append(i)
+        if pending:
+            nodes = list(pending)
+            extra = self._speculate(nodes[0]) if len(nodes) == 1 and SPECULATE else []
+            vals = self._evaluate(nodes, extra, mc)
+            for n, v in vals.items():
+                self._memo[(n, mc)] = v
+            for n, pos in pending.items():
+                v = vals[n]
+                for i in pos:
+                    out[i] = expressions[i] if v is _UNEVALUATED else v
+        return out
+
+    def _evaluate(self, nodes: Sequence[int], extra: Sequence[int], mc: bool) -> dict:
+        """{node: value or _UNEVALUATED} of `nodes` (requested: a lowering failure with model
+        completion raises) and `extra` (speculated: failures are left out)."""
+        from copy import deepcopy
+
+        from .lower import Lowering, LoweringUnsupported, node_columns, var_names
 
         b = self.ctx.b
-        node, _ = self._term(expression)
-        try:
-            root, schema = lower_query_value(b, node, self.schema)
-        except LoweringUnsupported:
-            if not model_completion:  # e.g. a function the model does not interpret
-                return expression
-            raise
-        fresh = [n for n, c in schema.columns.items()
-                 if n not in self.values and c.kind == "var"]
-        if fresh and not model_completion:
-            return expression
-        width = b.widths[node]
+        schema = deepcopy(self.schema)
+        L = Lowering(b, schema)
+        res: dict = {}
+        roots: "list[tuple[int, int]]" = []  # (node, lowered root)
+        asked_set = set(nodes)
+        for n in list(nodes) + [x for x in extra if x not in asked_set]:
+            asked = n in asked_set
+            try:
+                roots.append((n, L.lower(n)))
+            except LoweringUnsupported:
+                if not asked:
+                    continue
+                if not mc:  # e.g. a function the model does not interpret
+                    res[n] = _UNEVALUATED
+                    continue
+                raise
+        names = var_names(b)
+        cols = node_columns(b, [r for _, r in roots])
+        todo: "list[tuple[int, int]]" = []
+        for n, r in roots:
+            if not mc and any(names[v] not in self.values and
+                              schema.columns.get(names[v]) is not None and
+                              schema.columns[names[v]].kind == "var" for v in cols[r]):
+                if n in asked_set:
+                    res[n] = _UNEVALUATED
+                continue
+            todo.append((n, r))
+        if not todo:
+            return res
         columns = list(schema.columns) or ["__ground__"]
         if columns == ["__ground__"]:
             b.var("__ground__", 1)
-        if width == BOOL or width <= SLICE:
-            v = self.sieve.eval_terms(b, [root], columns, self.values)[0]
-            return bool(v) if width == BOOL else BitVecValue(v, width)
-        # wider than the device's 256-bit operations: the lowered term rewritten as terms of its
-        # 256-bit slices (Slicer), every slice evaluated on the device, low first
-        roots = Slicer(b).slices(root)
-        parts = self.sieve.eval_terms(b, roots, columns, self.values)
-        return BitVecValue(sum(int(p) << (SLICE * i) for i, p in enumerate(parts)), width)
+        flat: "list[int]" = []
+        spans = []
+        for n, r in todo:
+            width = b.widths[n]
+            if width == BOOL or width <= SLICE:
+                spans.append((n, width, len(flat), 1))
+                flat.append(r)
+            else:
+                # wider than the device's 256-bit operations: the lowered term rewritten as
+                # terms of its 256-bit slices (Slicer), each evaluated on the device, low first
+                sl = Slicer(b).slices(r)
+                spans.append((n, width, len(flat), len(sl)))
+                flat.extend(sl)
+        vals = self.sieve.eval_terms(b, flat, columns, self.values, resident=self._resident)
+        for n, width, at, k in spans:
+            if width == BOOL:
+                res[n] = bool(vals[at])
+            elif k == 1:
+                res[n] = BitVecValue(vals[at], width)
+            else:
+                res[n] = BitVecValue(sum(int(p) << (SLICE * i)
+                                         for i, p in enumerate(vals[at:at + k])), width)
+        return res
+
+    def _speculate(self, node: int) -> "list[int]":
+        """The same term at the next SPECULATE values of its one constant array index (none
+        when the term reads no array at a constant index, reads several, or is large)."""
+        b = self.ctx.b
+        nodes = b.nodes
+        idx, seen, stack = set(), set(), [node]
+        while stack:
+            x = stack.pop()
+            if x in seen:
+                continue
+            seen.add(x)
+            if len(seen) > SPECULATE_WALK:
+                return []
+            op, _, a, bb, c = nodes[x][:5]
+            if op == Op.SELECT and nodes[bb][0] == Op.CONST:
+                idx.add(bb)
+            k = ARITY[Op(op)]
+            if k:
+                stack.extend((a, bb, c)[:k])
+        if len(idx) != 1:
+            return []
+        c = idx.pop()
+        v, w = b.const_value(c), b.widths[c]
+        out = []
+        for j in range(1, SPECULATE + 1):
+            if v + j >> w:
+                break
+            out.append(_substitute(b, node, c, b.const(v + j, w)))
+        return out
+
+
+_UNEVALUATED = object()  # memo marker: returned as the expression itself (no interpretation)
+SPECULATE = 127          # sibling terms evaluated with a lone array read at a constant index
+SPECULATE_WALK = 4096    # ... only for terms of at most this many nodes
+
+
+def _substitute(b, root: int, old: int, new: int) -> int:
+    """`root` with node `old` replaced by `new` (same sort), rebuilt through the builder's
+    hash-consing: the result is the node the same term written with `new` has."""
+    from .tape import F_ARRAY
+
+    nodes, flags = b.nodes, b.flags
+    memo = {old: new}
+    stack = [(root, False)]
+    while stack:
+        x, done = stack.pop()
+        if x in memo:
+            continue
+        op, w, a, bb, c, i0, i1 = nodes[x]
+        k = ARITY[Op(op)]
+        kids = (a, bb, c)[:k]
+        if not done:
+            stack.append((x, True))
+            stack.extend((y, False) for y in kids if y not in memo)
+            continue
+        new_kids = [memo.get(y, y) for y in kids]
+        if new_kids == list(kids):
+            memo[x] = x
+            continue
+        a2, b2, c2 = (new_kids + [a, bb, c][k:])[:3]
+        memo[x] = b._add(Op(op), w, a2, b2, c2, i0, i1, flags=flags[x] & F_ARRAY)
+    return memo[root]
 
 
 def lower_query_value(b, node: int, frozen: Schema):

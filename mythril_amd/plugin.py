@@ -111,34 +111,85 @@ def z3_log_writer(constraints, minimize, maximize) -> str:
     return s.sexpr()
 
 
-def z3_verifier(constraints, model, timeout_ms=None) -> bool:
-    """Re-verify a sieve witness with z3: the constraints plus the witness as equalities on every
-    scalar column must be SAT.  Runs only where z3 is importable.
+def witness_pins(raws, model, z3) -> list:
+    """Equalities that fix every uninterpreted symbol the query's z3 terms read to the sieve
+    witness's interpretation, so that z3's check of the query under them is an evaluation, not
+    a search ("witness as equalities, fully determined"):
 
-    The check runs under get_model's own budget (``timeout_ms`` = what is left of
-    ``min(args.solver_timeout, time_remaining - 500)``, support/model.py:26-31): array else-values
-    and keccak / UF interpretations stay free, so the check is a real solver call, and ``unknown``
-    (timeout) counts as a rejection — the query then goes to the fallback unchanged."""
-    import z3  # noqa: F401
+    * a scalar symbol (bit-vector or Bool constant): its column's value -- a symbol the witness
+      has no column for is one the lowered query does not read, and gets 0 (model completion);
+    * an array symbol: ``A == Store(...Store(K(dom, else), k1, v1)..., kn, vn)``, the z3 form of
+      the witness's table (its cells and else value, lower.py; model.Model.__getitem__);
+    * every application of an uninterpreted function -- keccak256_N, its inverse keccak256_N-1,
+      any other ``Function`` -- at the argument it has in the query: ``f(t) == v``, v the
+      witness's value of that application (``Model.eval_many``: one device batch for all).
 
-    from .support import args
+    ``raws`` are z3 ``ExprRef``s.  Walks the DAG once by AST id."""
+    scalars, arrays, apps = {}, {}, {}
+    seen, stack = set(), list(raws)
+    while stack:
+        t = stack.pop()
+        i = t.get_id()
+        if i in seen:
+            continue
+        seen.add(i)
+        if not z3.is_app(t):
+            continue
+        d = t.decl()
+        if d.kind() == z3.Z3_OP_UNINTERPRETED:
+            if d.arity() == 0:
+                (arrays if z3.is_array(t) else scalars)[d.name()] = t
+            else:
+                apps[i] = t
+        stack.extend(t.children())
+    pins = []
+    cols = model.schema.columns
+    for name, t in sorted(scalars.items()):
+        col = cols.get(name)
+        v = model.values.get(name, 0) if col is not None and col.kind == "var" else 0
+        pins.append(t == (z3.BoolVal(bool(v)) if z3.is_bool(t) else z3.BitVecVal(v, t.size())))
+    for name, t in sorted(arrays.items()):
+        srt = t.sort()
+        dom, rng = srt.domain(), srt.range()
+        cells = model.schema.cells.get(name, {})
+        else_v = model.values.get("%s[*]" % name, 0)
+        a = z3.K(dom, z3.BitVecVal(else_v, rng.size()))
+        for key, cname in sorted(cells.items()):
+            a = z3.Store(a, z3.BitVecVal(key, dom.size()),
+                         z3.BitVecVal(model.values.get(cname, else_v), rng.size()))
+        pins.append(t == a)
+    if apps:
+        ordered = [apps[i] for i in sorted(apps)]
+        for t, v in zip(ordered, model.eval_many(ordered, model_completion=True)):
+            pins.append(t == (z3.BoolVal(bool(v)) if z3.is_bool(t) else z3.BitVecVal(int(v), t.size())))
+    return pins
+
+
+def z3_verifier(constraints, model, timeout_ms=None):
+    """Re-verify a sieve witness with z3 and return the reference's model.
+
+    The constraints plus ``witness_pins`` (every scalar, array and function application fixed)
+    must be SAT; the result is then what the reference's get_model returns,
+    ``mythril.laser.smt.Model([solver.model()])`` (support/model.py:57-59, laser/smt/model.py:13-18;
+    its mirror ``support.RefModel`` when the reference is not importable).  None rejects the
+    witness: unsat, or ``unknown`` -- the check runs under get_model's own budget
+    (``timeout_ms`` = what is left of ``min(args.solver_timeout, time_remaining - 500)``,
+    support/model.py:26-31) -- and the query goes to the fallback unchanged."""
+    import z3
+
+    from .support import RefModel, args
 
     s = z3.Solver()
     budget = args.solver_timeout if timeout_ms is None else min(args.solver_timeout, timeout_ms)
     if budget <= 0:
-        return False
+        return None
     s.set("timeout", max(1, int(budget)))
-    s.add([getattr(c, "raw", c) for c in constraints])
-    arrays = model.ctx.b.symbols.arrays
-    for col in model.schema.columns.values():
-        v = model.values[col.name]
-        if col.kind == "var" and col.symbol != "__ground__":
-            s.add(z3.BitVec(col.symbol, col.width) == v)
-        elif col.kind == "cell" and col.symbol in arrays:
-            _, dom, rng = arrays[col.symbol]
-            a = z3.Array(col.symbol, z3.BitVecSort(dom), z3.BitVecSort(rng))
-            s.add(z3.Select(a, z3.BitVecVal(col.key, dom)) == v)
-    return s.check() == z3.sat
+    raws = [getattr(c, "raw", c) for c in constraints]
+    s.add(raws)
+    s.add(witness_pins(raws, model, z3))
+    if s.check() != z3.sat:
+        return None
+    return RefModel([s.model()])
 
 
 class SievePlugin(LaserPlugin):

@@ -574,10 +574,11 @@ class Sieve:
         return acc, defs
 
     def eval_terms(self, b: TapeBuilder, terms: Sequence[int], columns: Sequence[str],
-                   values: Dict[str, int]) -> List[int]:
+                   values: Dict[str, int], resident: Optional[dict] = None) -> List[int]:
         """The values of `terms` (bit-vector or Bool nodes over `columns`) under one assignment,
-        evaluated on the device (mh_eval_values over a one-row buffer)."""
-        return self.eval_tapeset(local_tapeset(b, terms, columns), columns, values)
+        evaluated on the device (mh_eval_values_many over a one-row buffer; `resident`, a dict
+        the caller keeps, holds that buffer per column tuple across calls)."""
+        return self.eval_tapeset(local_tapeset(b, terms, columns), columns, values, resident)
 
     def eval_definitions(self, b: TapeBuilder, defs, columns: Sequence[str],
                          values: Dict[str, int]) -> List[int]:
@@ -590,25 +591,31 @@ class Sieve:
             return self.eval_tapeset(ts, columns, values)
         return self.eval_terms(b, [t for _, t in defs], columns, values)
 
-    def eval_tapeset(self, ts: TapeSet, columns: Sequence[str],
-                     values: Dict[str, int]) -> List[int]:
+    def eval_tapeset(self, ts: TapeSet, columns: Sequence[str], values: Dict[str, int],
+                     resident: Optional[dict] = None) -> List[int]:
         """The root values of every tape of `ts` under one assignment of `columns`."""
         terms = ts.tapes
         ct = self.compile(ts)
         try:
-            assign = self.ctx.assignments(len(columns), 1)
-            try:
+            key = tuple(columns)
+            assign = resident.get(key) if resident is not None else None
+            if assign is None:
+                assign = self.ctx.assignments(len(columns), 1)
                 soa = np.zeros((len(columns), 8, 1), dtype=np.uint32)
                 for i, c in enumerate(columns):
                     v = values.get(c, 0)
                     for k in range(8):
                         soa[i, k, 0] = (v >> (32 * k)) & 0xFFFFFFFF
                 assign.upload(soa)
+                if resident is not None:
+                    resident[key] = assign
+            try:
                 # every root in one batch (mh_eval_values_many: one launch per register class)
                 out = native.eval_values_many(self.ctx, ct, list(range(len(terms))), assign, 0)
                 return [_limbs(out[i]) for i in range(len(terms))]
             finally:
-                assign.close()
+                if resident is None:
+                    assign.close()
         finally:
             ct.close()
 

@@ -3,6 +3,8 @@
 * ``UnsatError``        mythril/exceptions.py:16-20
 * ``args``              mythril/support/support_args.py:1-17 (solver_timeout 10000 ms, ...)
 * ``time_handler``      mythril/laser/ethereum/time_handler.py:5-18
+* ``RefModel``          mythril/laser/smt/model.py:6-59 (the Model get_model returns: a list of z3
+                        ModelRefs), used for a z3-verified sieve witness
 * ``SolverStatistics``  mythril/laser/smt/solver/solver_statistics.py:8-43, plus the sieve's own
                         counters (hits / misses / unsupported / errors / rejected, seconds), kept
                         beside z3's so wall-time splits stay comparable.
@@ -16,6 +18,7 @@ import time
 
 try:  # the reference, when it runs around this module
     from mythril.exceptions import UnsatError  # type: ignore
+    from mythril.laser.smt import Model as RefModel  # type: ignore
     from mythril.laser.ethereum.time_handler import time_handler  # type: ignore
     from mythril.laser.smt.solver.solver_statistics import \
         SolverStatistics as _RefStats  # type: ignore
@@ -25,6 +28,37 @@ try:  # the reference, when it runs around this module
 except Exception:  # z3 / mythril absent: standalone mirrors
     HAVE_MYTHRIL = False
     _RefStats = None
+
+    class RefModel:  # type: ignore[no-redef]
+        """laser/smt/model.py:6-59: wraps z3 ModelRefs; ``decls``, ``[item]`` and ``eval`` ask
+        them in order (the last one answers ``eval`` when no earlier one declares the term)."""
+
+        def __init__(self, models=None):
+            self.raw = models or []
+
+        def decls(self):
+            result = []
+            for internal_model in self.raw:
+                result.extend(internal_model.decls())
+            return result
+
+        def __getitem__(self, item):
+            for k, internal_model in enumerate(self.raw):
+                try:
+                    result = internal_model[item]
+                    if result is not None:
+                        return result
+                except IndexError:
+                    if k == len(self.raw) - 1:
+                        raise
+            return None
+
+        def eval(self, expression, model_completion: bool = False):
+            for k, internal_model in enumerate(self.raw):
+                relevant = expression.decl() in list(internal_model.decls())
+                if relevant or k == len(self.raw) - 1:
+                    return internal_model.eval(expression, model_completion)
+            return None
 
     class UnsatError(Exception):  # type: ignore[no-redef]
         """mythril/exceptions.py:16-20."""

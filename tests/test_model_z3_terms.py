@@ -263,3 +263,61 @@ def test_wide_terms_are_sliced_for_the_device():
             assert got == want, t.node
     with pytest.raises(smt.TapeError if hasattr(smt, "TapeError") else Exception):
         Slicer(b).slices((ZeroExt(256, x) * ZeroExt(256, y)).node)
+
+
+def calldata_query(size=100):
+    """A transaction whose calldata size is pinned (0x64 bytes), its dispatcher and argument
+    checks: the reference then reads the model byte by byte (calldata.py:234-245)."""
+    ref = smt.set_context(smt.Context())
+    cd = Calldata("1")
+    caller = symbol_factory.BitVecSym("sender_1", 256)
+    cs = [selector_is(cd, 0x9FA299CC), cd.size == symbol_factory.BitVecVal(size, 256),
+          sender_is_actor(caller), ULT(cd.word(4), symbol_factory.BitVecVal(1 << 160, 256))]
+    return ref, cd, cs
+
+
+def concrete_calldata(m, cd):
+    """SymbolicCalldata.concrete (calldata.py:234-245), term for term: the size, then one
+    ``eval(_load(i).raw, model_completion=True).as_long()`` per byte."""
+    n = m.eval(RefExpr(cd.size).raw, model_completion=True).as_long()
+    return [m.eval(RefExpr(cd.load(i)).raw, model_completion=True).as_long() for i in range(n)]
+
+
+def check_batched_calldata_reads(launches, size=100):
+    """The reference's byte loop over a sieve model reads `size` bytes in at most two device
+    launches (the size; then byte 0 with its speculated siblings), with the oracle's values."""
+    import time
+
+    from mythril_amd import native
+
+    ref, cd, cs = calldata_query(size)
+    m = frontend.get_model(tuple(RefExpr(c) for c in cs))
+    assert isinstance(m, Model), m
+    before = launches()
+    t0 = time.perf_counter()
+    got = concrete_calldata(m, cd)
+    dt = time.perf_counter() - t0
+    n_launch = launches() - before
+    assert len(got) == size
+    assert got == [oracle_value(ref, cd.load(i), m) for i in range(size)]
+    assert got[:4] == [0x9F, 0xA2, 0x99, 0xCC]
+    assert n_launch <= 2, n_launch
+    # a second read of the same model is all memo hits
+    before = launches()
+    assert concrete_calldata(m, cd) == got and launches() == before
+    return n_launch, dt
+
+
+def test_calldata_loop_is_batched_on_fake_device(monkeypatch, z3_world):
+    fake_device.install(monkeypatch)
+    frontend.configure(rows=256)
+    check_batched_calldata_reads(lambda: fake_device.LAUNCHES[0])
+
+
+@pytest.mark.gpu
+def test_calldata_loop_is_batched_on_gpu(gpu_ctx, z3_world):
+    from mythril_amd import native
+
+    frontend.configure(rows=256)
+    n, dt = check_batched_calldata_reads(lambda: native.eval_launches(frontend.sieve().ctx))
+    print("calldata.concrete: 100 bytes in %d launches, %.2f ms" % (n, 1e3 * dt))

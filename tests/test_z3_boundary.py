@@ -117,49 +117,136 @@ def _schema():
     return s
 
 
-def test_verifier_pins_the_witness_and_the_timeout(stub_z3):
-    """z3_verifier: the query's z3 terms (.raw) plus one equality per scalar column and per
-    array cell of the witness; timeout = min(solver_timeout, timeout_ms); sat -> accepted."""
+def _verifier_world(monkeypatch, rows=256):
+    """The AST z3 stand-in installed, the front end wired as SievePlugin.start wires it (z3
+    importer, z3_verifier, a recording fallback) over the CPU stand-in of the device; returns
+    (z3 module, [sieve Models handed to the verifier], [fallback calls])."""
+    from mythril_amd.smtlib import Z3Importer
+    from tests import fake_device, z3_ast
+
+    z3 = z3_ast.make_z3()
+    monkeypatch.setitem(sys.modules, "z3", z3)
+    fake_device.install(monkeypatch)
+    frontend.reset()
+    seen, fallback = [], []
+
+    def verify(constraints, model, timeout_ms=None):
+        seen.append(model)
+        return plugin.z3_verifier(constraints, model, timeout_ms=timeout_ms)
+
+    frontend.configure(to_terms=Z3Importer(), verify=verify, rows=rows,
+                       fallback=lambda *a: fallback.append(a) or "fallback")
+    return z3, seen, fallback
+
+
+@pytest.mark.parametrize("name", ["killbilly", "ether_thief", "keccak_mapping", "suicide_arg",
+                                  "k_storage", "balance"])
+def test_verifier_pins_every_symbol_and_returns_the_reference_model(monkeypatch, name):
+    """VERDICT r5 next 1 ("SAT from sieve => z3 re-verification, witness as
+    equalities, fully determined"): on LASER-shaped queries the verifier hands z3 the query plus
+    one equality per scalar symbol, one Store-chain over K(else) per array holding every cell of
+    the witness, and one equality per uninterpreted application -- keccak256_N, its inverse, any
+    function -- so no symbol the query reads is left free and z3's check is an evaluation; the
+    stand-in's check evaluates the constraints under exactly those pins (ORACLE) and finds them
+    true; get_model returns z3's model in the reference's Model type (support/model.py:57-59)."""
+    from mythril_amd.support import RefModel
+    from mythril_amd.tape import Op
+    from tests import z3_ast
+    from tests.laser_like import queries
+
+    z3, seen, fallback = _verifier_world(monkeypatch)
+    try:
+        qctx, qs = queries()
+        cs = dict(qs)[name]
+        m = frontend.get_model(tuple(z3_ast.Ref(c) for c in cs))
+        assert not fallback, "the sieve answered %s" % name
+        assert type(m) is RefModel and len(m.raw) == 1
+        (w,) = seen
+        checked = [s for s in z3.solvers if "timeout" in s.params]
+        assert len(checked) == 1
+        s = checked[0]
+        assert s.free == []
+        pins = {}
+        for p in s.pins:
+            pins.setdefault(qctx.b.nodes[p.lhs.node][0], []).append(p)
+        scalar = {p.lhs.decl().name(): p.rhs.v for p in pins.get(Op.VAR, [])}
+        arrays = {p.lhs.decl().name(): p.rhs for p in pins.get(Op.ARRAY, [])}
+        apps = pins.get(Op.UF, [])
+        for col in w.schema.columns.values():
+            if col.kind == "var" and col.symbol != "__ground__":
+                assert scalar[col.name] == w.values[col.name], col.name
+            elif col.kind == "cell":
+                assert arrays[col.symbol].table[col.key] == w.values[col.name], col.name
+            elif col.kind == "else":
+                assert arrays[col.symbol].dflt == w.values[col.name]
+            elif col.kind in ("ufcell", "ufelse"):
+                assert apps, col.name
+        for f in w.schema.keccak:
+            assert any(p.lhs.decl().name() == f for p in apps), f
+        # the reference reads the returned model with its own terms
+        for c in cs:
+            assert m.eval(z3_ast.Ref(c).raw, model_completion=True) is True
+        for d in m.decls():
+            assert m[d] is not None
+    finally:
+        frontend.reset()
+
+
+def test_verifier_timeout_unknown_and_unsat(monkeypatch):
+    """The check runs under min(args.solver_timeout, what is left of get_model's budget)
+    (support/model.py:26-31); unknown and unsat reject (the query goes to the fallback and
+    sieve_rejected counts it); a spent budget rejects without a solver call."""
+    from tests import z3_ast
+    from tests.laser_like import queries
+
     old = args.solver_timeout
     args.solver_timeout = 10000
+    z3, seen, fallback = _verifier_world(monkeypatch)
     try:
-        m = _model({"sender_1": 0xAFFE, "1_calldatasize": 36, "Storage[0]": 7, "__ground__": 0},
-                   _schema(), {"Storage": (0, 256, 256)})
-        cs = [RawBool("c1"), RawBool("c2")]
-        assert plugin.z3_verifier(cs, m, timeout_ms=2500.7) is True
-        (_, solver), (_, checked) = stub_z3.calls
-        assert checked is solver
-        assert solver.params == {"timeout": 2500}
-        a = solver.assertions
-        assert [x.what for x in a[:2]] == [("constraint", "c1"), ("constraint", "c2")]
-        eqs = {repr(x) for x in a[2:]}
-        assert repr(_Rec("==", _Rec("BitVec", "sender_1", 256), 0xAFFE)) in eqs
-        assert repr(_Rec("==", _Rec("BitVec", "1_calldatasize", 256), 36)) in eqs
-        sel = _Rec("Select", _Rec("Array", "Storage", _Rec("BitVecSort", 256),
-                                  _Rec("BitVecSort", 256)), _Rec("BitVecVal", 0, 256))
-        assert repr(_Rec("==", sel, 7)) in eqs
-        assert len(a) == 5  # the __ground__ column is not a symbol
-        # no budget passed: the solver timeout itself; a larger budget is capped by it
-        stub_z3.calls.clear()
-        plugin.z3_verifier(cs, m)
-        assert stub_z3.calls[0][1].params == {"timeout": 10000}
-        stub_z3.calls.clear()
-        plugin.z3_verifier(cs, m, timeout_ms=50000)
-        assert stub_z3.calls[0][1].params == {"timeout": 10000}
+        qctx, qs = queries()
+        cs = dict(qs)["selector"]
+        raws = tuple(z3_ast.Ref(c) for c in cs)
+        assert frontend.get_model(raws) != "fallback"
+        w = seen[-1]
+        for budget, want in ((2500.7, 2500), (None, 10000), (50000, 10000)):
+            z3.solvers.clear()
+            assert plugin.z3_verifier(raws, w, timeout_ms=budget) is not None
+            (s,) = [s for s in z3.solvers if "timeout" in s.params]
+            assert s.params == {"timeout": want}
+        z3.solvers.clear()
+        assert plugin.z3_verifier(raws, w, timeout_ms=0) is None
+        assert not [s for s in z3.solvers if "timeout" in s.params]
+        for verdict in (z3.unknown, z3.unsat):
+            monkeypatch.setattr(z3.Solver, "check", lambda self, v=verdict: v)
+            assert plugin.z3_verifier(raws, w, timeout_ms=100) is None
+        before = SolverStatistics().sieve_rejected
+        frontend.get_model.cache_clear()
+        assert frontend.get_model(raws) == "fallback"
+        assert SolverStatistics().sieve_rejected == before + 1
     finally:
         args.solver_timeout = old
+        frontend.reset()
 
 
-def test_verifier_rejects_unknown_and_a_spent_budget(stub_z3, monkeypatch):
-    m = _model({"sender_1": 1}, Schema())
-    monkeypatch.setattr(stub_z3.Solver, "check", lambda self: stub_z3.unknown)
-    assert plugin.z3_verifier([RawBool("c")], m, timeout_ms=100) is False
-    monkeypatch.setattr(stub_z3.Solver, "check", lambda self: stub_z3.unsat)
-    assert plugin.z3_verifier([RawBool("c")], m, timeout_ms=100) is False
-    # nothing left of the budget: rejected without a solver call
-    stub_z3.calls.clear()
-    assert plugin.z3_verifier([RawBool("c")], m, timeout_ms=0) is False
-    assert not [c for c in stub_z3.calls if c[0] == "check"]
+def test_pins_of_a_wrong_witness_are_unsat(monkeypatch):
+    """The pins are the witness, not a search space: a witness value changed after the sieve
+    found it makes z3's (the stand-in's) check unsat, so the verifier rejects it."""
+    from tests import z3_ast
+    from tests.laser_like import queries
+
+    z3, seen, fallback = _verifier_world(monkeypatch)
+    try:
+        qctx, qs = queries()
+        cs = dict(qs)["owner_check"]
+        raws = tuple(z3_ast.Ref(c) for c in cs)
+        assert frontend.get_model(raws) != "fallback"
+        w = seen[-1]
+        assert plugin.z3_verifier(raws, w) is not None
+        w.values["sender_1"] ^= 1
+        w._memo.clear()
+        assert plugin.z3_verifier(raws, w) is None
+    finally:
+        frontend.reset()
 
 
 def test_log_writer_prints_the_optimize_problem(stub_z3):
@@ -181,13 +268,19 @@ class _FakeSieve:
         return self.witness
 
 
-def test_plugin_start_wires_z3_and_unknown_goes_to_the_fallback(stub_z3, monkeypatch):
+def test_plugin_start_wires_z3_and_unknown_goes_to_the_fallback(monkeypatch):
     """SievePlugin.start with z3 importable: the verifier, the log writer and the term importer
     are the z3 ones.  A witness z3 cannot confirm (unknown) is rejected: the query goes, as it
-    came, to the reference's get_model, and sieve_rejected counts it."""
-    from mythril_amd.sieve import Witness
+    came, to the reference's get_model, and sieve_rejected counts it.  A confirmed one comes
+    back as z3's model in the reference's Model type, and the reference is not asked."""
     from mythril_amd.smtlib import Z3Importer
+    from mythril_amd.support import RefModel
+    from tests import fake_device, z3_ast
 
+    z3 = z3_ast.make_z3()
+    monkeypatch.setitem(sys.modules, "z3", z3)
+    fake_device.install(monkeypatch)
+    frontend.reset()
     calls = []
 
     def reference_get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True):
@@ -195,30 +288,29 @@ def test_plugin_start_wires_z3_and_unknown_goes_to_the_fallback(stub_z3, monkeyp
         return "z3 model"
 
     mod = types.SimpleNamespace(get_model=reference_get_model)
-    p = plugin.SievePlugin(modules=[mod])
+    p = plugin.SievePlugin(modules=[mod], rows=256)
     p.start()
     try:
         assert frontend._config["verify"] is plugin.z3_verifier
         assert frontend._config["log_writer"] is plugin.z3_log_writer
         assert isinstance(frontend._config["to_terms"], Z3Importer)
         assert frontend._config["fallback"] is reference_get_model
-        smt.set_context(smt.Context())
+        ref = smt.set_context(smt.Context())
         x = smt.symbol_factory.BitVecSym("x", 256)
-        schema = Schema()
-        schema.columns["x"] = Column("x", 256, "var", "x")
-        fake = _FakeSieve(Witness(schema, {"x": 3}, 0, 1))
-        monkeypatch.setattr(frontend, "sieve", lambda: fake)
-        monkeypatch.setattr(stub_z3.Solver, "check", lambda self: stub_z3.unknown)
+        monkeypatch.setattr(z3.Solver, "check", lambda self: z3.unknown)
         before = SolverStatistics().sieve_rejected
-        c = x == 3
+        c = z3_ast.Ref(x == smt.symbol_factory.BitVecVal(3, 256))
         assert mod.get_model((c,)) == "z3 model"
         assert calls == [(c,)]
         assert SolverStatistics().sieve_rejected == before + 1
-        # z3 confirms: the sieve's model is returned, the reference is not asked
-        monkeypatch.setattr(stub_z3.Solver, "check", lambda self: stub_z3.sat)
-        m = mod.get_model((x == 3, x != 4))
-        assert m != "z3 model" and m.values == {"x": 3}
+        monkeypatch.undo()
+        monkeypatch.setitem(sys.modules, "z3", z3)
+        fake_device.install(monkeypatch)
+        m = mod.get_model((c, z3_ast.Ref(x != smt.symbol_factory.BitVecVal(4, 256))))
+        assert type(m) is RefModel
+        assert m.eval(z3_ast.Ref(x).raw, model_completion=True).as_long() == 3
         assert len(calls) == 1
+        assert ref is not None
     finally:
         p.stop()
     assert mod.get_model is reference_get_model
