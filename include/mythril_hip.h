@@ -296,6 +296,9 @@ enum { MH_TABLE_CELLS = 0, MH_TABLE_UF_CELLS = 1, MH_TABLE_KECCAK = 2 };
                                    conjunct, a conjunct and its negation, a term pinned to an
                                    empty range by equalities / disequalities / unsigned bounds
                                    against constants): no witness exists                       */
+#define MH_QUERY_INCREMENTAL 4u /* diagnostic: built from the session's state (taken back to the
+                                   common prefix of the roots and extended by the rest) rather
+                                   than afresh; the result is the same either way               */
 #define MH_QUERY_KEY_LIMBS 36  /* limbs of a table entry / cell key (1152 bits; keccak arguments are
                                    up to 1088 bits wide)                                        */
 typedef struct {

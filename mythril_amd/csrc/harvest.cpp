@@ -287,12 +287,16 @@ struct Harvester {
     // (kind, node, value, mask) with values interned; hints by id (one per distinct hint)
     struct Key {
         uint32_t kind, n, v, m;
-        bool operator==(const Key& o) const { return kind == o.kind && n == o.n && v == o.v && m == o.m; }
+        uint32_t g = 0;  // the node's generation (set by memoised / memo_hints from gen[n])
+        bool operator==(const Key& o) const {
+            return kind == o.kind && n == o.n && v == o.v && m == o.m && g == o.g;
+        }
     };
     struct KeyHash {
         size_t operator()(const Key& k) const {
             uint64_t h = ((uint64_t)k.n << 32 | k.v) * 0x9E3779B97F4A7C15ull;
             h ^= ((uint64_t)k.m << 1 | k.kind) * 0xC2B2AE3D27D4EB4Full;
+            h ^= (uint64_t)k.g * 0x94D049BB133111EBull;
             return (size_t)(h ^ (h >> 31));
         }
     };
@@ -332,7 +336,7 @@ struct Harvester {
     std::map<int, std::vector<U>> consts_by_width;
     std::map<int, std::vector<uint32_t>> const_ids_by_width;  // their interned ids
     // eq_nodes per conjunct (a function of the tape prefix: kept across a session's queries)
-    std::unordered_map<uint32_t, std::vector<uint32_t>> eq_nodes_of;
+    std::unordered_map<uint64_t, std::vector<uint32_t>> eq_nodes_of;  // by nk(conjunct)
     // What a conjunct and an equality node contribute to a query, kept across a session's
     // queries (functions of the tape prefix, like the memo): the set pushed (null: none) and
     // the hint ids the inversions emit, replayed in order -- exactly what the memo's hits would
@@ -342,15 +346,33 @@ struct Harvester {
         std::shared_ptr<const Alts> set;
         std::vector<uint32_t> hints;
     };
-    std::unordered_map<uint32_t, Contribution> conj_done;
+    std::unordered_map<uint64_t, Contribution> conj_done;  // by nk(conjunct)
     struct EqPlan {
         bool skip = false;        // a Bool, a constant side, or both sides equal once stripped
         uint32_t x = 0, y = 0;
         std::vector<std::vector<Copy>> copies;  // copy alternatives (then no value pairs)
         std::unordered_map<uint32_t, Contribution> by_const;  // by the constant's interned id
     };
-    std::unordered_map<uint32_t, EqPlan> eq_plan;
-    std::vector<uint32_t> memo_hints(const Key& k) const {
+    std::unordered_map<uint64_t, EqPlan> eq_plan;  // by nk(equality node)
+    // Node generations: a session whose next tape shares only a prefix of p nodes with the last
+    // one (a JUMPI's other branch, the next state a BFS pops: the same path, another condition)
+    // keeps every memo of the nodes below p and gives the indices from p on a new generation,
+    // so entries of the nodes the new tape replaces are never found again (truncate)
+    std::vector<uint32_t> gen;
+    uint32_t cur_gen = 0;
+    uint64_t nk(uint32_t n) const { return (uint64_t)gen[n] << 32 | n; }
+    void truncate(uint32_t p, uint32_t pc) {
+        ++cur_gen;
+        nd.resize(p);
+        gen.resize(p);
+        cv_state.resize(p);
+        cv.resize(p);
+        pool.resize(pc);
+        last_conj.clear();  // its constants are recounted from the query's conjuncts
+        last_qc.clear();
+    }
+    std::vector<uint32_t> memo_hints(Key k) const {
+        k.g = gen[k.n];
         auto it = memo.find(k);
         if (it == memo.end()) return {};
         return std::vector<uint32_t>(it->second.hints.begin(), it->second.hints.end());
@@ -407,7 +429,8 @@ struct Harvester {
     }
 
     template <class F>
-    Res memoised(const Key& key, F compute) {
+    Res memoised(Key key, F compute) {
+        key.g = gen[key.n];
         auto it = memo.find(key);
         if (it == memo.end()) {
             cap.emplace_back();
@@ -537,9 +560,9 @@ struct Harvester {
         return none_();
     }
 
-    std::unordered_map<uint32_t, std::vector<std::pair<uint32_t, int>>> leaves_memo;
+    std::unordered_map<uint64_t, std::vector<std::pair<uint32_t, int>>> leaves_memo;
     const std::vector<std::pair<uint32_t, int>>& concat_leaves(uint32_t n) {
-        auto it = leaves_memo.find(n);
+        auto it = leaves_memo.find(nk(n));
         if (it != leaves_memo.end()) return it->second;
         std::vector<std::pair<uint32_t, int>> got;
         std::vector<std::pair<uint32_t, int>> st{{n, 0}};
@@ -553,7 +576,7 @@ struct Harvester {
                 got.push_back({x, lo});
             }
         }
-        return leaves_memo[n] = std::move(got);
+        return leaves_memo[nk(n)] = std::move(got);
     }
 
     Res invert_bool(uint32_t n, bool truth, int depth = 0) {
@@ -898,7 +921,7 @@ struct Harvester {
             if (c.set) sets.push_back({prob, c.set});
         };
         for (uint32_t cj : conj) {
-            auto cd = conj_done.find(cj);
+            auto cd = conj_done.find(nk(cj));
             if (cd != conj_done.end()) {
                 replay(cd->second, kProbDefault);
             } else {
@@ -911,14 +934,14 @@ struct Harvester {
                     c.set = std::make_shared<const Alts>(head(kept, kMaxAlts));
                     sets.push_back({kProbDefault, c.set});
                 }
-                conj_done.emplace(cj, std::move(c));
+                conj_done.emplace(nk(cj), std::move(c));
             }
-            auto eqn = eq_nodes_of.find(cj);
-            if (eqn == eq_nodes_of.end()) eqn = eq_nodes_of.emplace(cj, eq_nodes(cj)).first;
+            auto eqn = eq_nodes_of.find(nk(cj));
+            if (eqn == eq_nodes_of.end()) eqn = eq_nodes_of.emplace(nk(cj), eq_nodes(cj)).first;
             for (uint32_t n : eqn->second) {
                 if (seen_eq[n]) continue;
                 seen_eq[n] = 1;
-                auto pit = eq_plan.find(n);
+                auto pit = eq_plan.find(nk(n));
                 if (pit == eq_plan.end()) {
                     EqPlan pl;
                     uint32_t x = nd[n].a, y = nd[n].b;
@@ -931,7 +954,7 @@ struct Harvester {
                         pl.y = y;
                         if (!pl.skip) pl.copies = copy_alternatives(x, y);
                     }
-                    pit = eq_plan.emplace(n, std::move(pl)).first;
+                    pit = eq_plan.emplace(nk(n), std::move(pl)).first;
                 }
                 EqPlan& pl = pit->second;
                 if (pl.skip) continue;
@@ -1151,6 +1174,7 @@ int32_t harvest_into(Harvester& h, const mh_node* nodes, uint32_t n_nodes, const
                      mh_harvest** out, mh_guide* guide) {
     const uint32_t n0 = (uint32_t)h.nd.size();
     h.nd.resize(n_nodes);
+    h.gen.resize(n_nodes, h.cur_gen);
     for (uint32_t i = n0; i < n_nodes; ++i) {
         const mh_node& s = nodes[i];
         Node& d = h.nd[i];
@@ -1365,7 +1389,34 @@ extern "C" int32_t mh_guide_harvest_with(mh_harvester* s, const mh_node* nodes, 
                              memcmp(nodes, s->nodes.data(), pn * sizeof(mh_node)) == 0 &&
                              memcmp(consts, s->consts.data(), pc * 32) == 0 &&
                              memcmp(col_width, s->widths.data(), pw * sizeof(uint16_t)) == 0;
+        // otherwise the longest prefix of nodes the two tapes share whose constants and columns
+        // are in the prefixes of constants and column widths they share (the other branch of a
+        // JUMPI: the path's tape, then other nodes): kept when it is most of the new tape
+        uint32_t keep = 0, keep_c = 0;
+        if (!extends && s->h && s->arena.used() < kSessionArenaBytes) {
+            const size_t mn = std::min<size_t>(pn, n_nodes);
+            size_t p = 0;
+            while (p < mn && memcmp(&nodes[p], &s->nodes[p], sizeof(mh_node)) == 0) ++p;
+            const size_t mc = std::min<size_t>(pc, n_consts), mw = std::min<size_t>(pw, n_cols);
+            size_t qc = 0, qw = 0;
+            while (qc < mc && memcmp(consts + 8 * qc, s->consts.data() + 8 * qc, 32) == 0) ++qc;
+            while (qw < mw && col_width[qw] == s->widths[qw]) ++qw;
+            for (size_t i = 0; i < p; ++i)
+                if ((nodes[i].op == CONST && nodes[i].imm0 >= qc) ||
+                    (nodes[i].op == VAR && nodes[i].imm0 >= qw)) {
+                    p = i;
+                    break;
+                }
+            if (p >= 16 && 2 * p >= n_nodes) {
+                keep = (uint32_t)p;
+                keep_c = (uint32_t)qc;
+            }
+        }
         if (extends) {
+            s->h->begin_query();
+            ++s->reused;
+        } else if (keep) {
+            s->h->truncate(keep, keep_c);
             s->h->begin_query();
             ++s->reused;
         } else {

@@ -25,6 +25,7 @@
 // eliminate_definitions: variable == computed term) is flagged MH_QUERY_DEFINITIONS; the host
 // then takes its Python stages.  A session is used by one thread at a time (scratch is shared).
 #include <algorithm>
+#include <array>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -32,6 +33,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/mythril_hip.h"
@@ -204,6 +206,9 @@ struct Stamped {
         }
     }
     bool has(size_t i) const { return i < stamp.size() && stamp[i] == epoch; }
+    void unset(size_t i) {
+        if (i < stamp.size()) stamp[i] = 0u;  // epochs start at 1
+    }
     uint32_t get(size_t i) const { return val[i]; }
     void set(size_t i, uint32_t v) {
         if (i >= stamp.size()) {
@@ -244,13 +249,15 @@ struct KeccakMap {
     Big bound, base;
     bool has_bound = false;
     std::vector<std::pair<Big, Big>> pairs;  // (argument, hash); a later statement of a key wins
-    void put(const Big& arg, const Big& h) {
+    bool put(const Big& arg, const Big& h) {  // true: the table changed
         for (auto& p : pairs)
             if (p.first == arg) {
+                const bool changed = !(p.second == h);
                 p.second = h;
-                return;
+                return changed;
             }
         pairs.emplace_back(arg, h);
+        return true;
     }
 };
 
@@ -290,6 +297,25 @@ public:
         ov_cv_vals = std::move(o.ov_cv_vals);
         ccols = std::move(o.ccols);
         cell_index = std::move(o.cell_index);
+    }
+    // the harvest tables, copied whole (a state keeps one per depth at which its harvest grew)
+    struct HarvestCopy {
+        Tables cells, uf_cells;
+        std::unordered_map<std::string, size_t> cell_of, uf_of, kidx;
+        std::vector<std::pair<std::string, KeccakMap>> keccak;
+        uint64_t hver = 0;
+    };
+    HarvestCopy save_harvest() const {
+        return HarvestCopy{cells, uf_cells, cell_of, uf_of, kidx, keccak, hver};
+    }
+    void restore_harvest(const HarvestCopy& h) {
+        cells = h.cells;
+        uf_cells = h.uf_cells;
+        cell_of = h.cell_of;
+        uf_of = h.uf_of;
+        kidx = h.kidx;
+        keccak = h.keccak;
+        hver = h.hver;
     }
     void sync() {  // the mirror may have grown since the query was made
         if (T.cv_state.size() < T.nodes.size()) T.cv_state.resize(T.nodes.size(), 0u);
@@ -465,6 +491,14 @@ public:
                 if (!T.seen.has(kids[j]) && (nd(kids[j]).flags & F_HOST)) st.push_back(kids[j]);
         }
     }
+    // changes whenever the harvest does (a key, a keccak function, a pair or a bound added):
+    // start() finds the depth from which a state's prefixes all have its harvest
+    std::array<uint64_t, 4> harvest_sig() const {
+        uint64_t nc = 0, nu = 0;
+        for (const auto& kv : cells) nc += kv.second.size() + 1;
+        for (const auto& kv : uf_cells) nu += kv.second.size() + 1;
+        return {nc, nu, (uint64_t)keccak.size(), hver};
+    }
     void finish_harvest() {  // lower.py apply_harvest: sorted keys, the keccak bases
         for (Tables* tabs : {&cells, &uf_cells})
             for (auto& kv : *tabs) {
@@ -504,7 +538,7 @@ public:
                 const Big hv = *kv;
                 KeccakMap& km = keccak_map(fn_name(s[0]));
                 if (x.op == EQ) {
-                    if (const Big* arg = const_value(app.a)) km.put(*arg, hv);
+                    if (const Big* arg = const_value(app.a)) hver += km.put(*arg, hv);
                     continue;
                 }
                 // a lower bound on the application (f > k, f >= k, k < f, k <= f): the
@@ -524,6 +558,7 @@ public:
                 if (!km.has_bound || km.bound < lb) {
                     km.bound = lb;
                     km.has_bound = true;
+                    ++hver;
                 }
             }
         }
@@ -755,6 +790,7 @@ public:
         return n & OWN ? (uint32_t)local_own[n & ~OWN] : T.local.get(n);
     }
     void lset(uint32_t n, uint32_t v) {
+        local_log.push_back(n);  // undone by rollback (a sibling query takes the tape back)
         if (n & OWN) {
             if (local_own.size() <= (n & ~OWN)) local_own.resize(ov.size(), -1);
             local_own[n & ~OWN] = v;
@@ -814,6 +850,7 @@ public:
             cols.push_back(Column{name, name, x.width, MH_COL_VAR, false, Big()});
         }
         m.emplace(k, q);
+        map_log.push_back({cell ? 1u : 0u, k});
         return q;
     }
     uint32_t const_index(uint32_t n) {
@@ -824,7 +861,39 @@ public:
         const uint32_t q = (uint32_t)qpool.size();
         qpool.push_back(const_of(n));
         m.emplace(i0, q);
+        map_log.push_back({(n & OWN) && (i0 & OV_CONST) ? 3u : 2u, i0});
         return q;
+    }
+
+    // ---- checkpoints of the root tape: a query that is not a child of this one (a JUMPI's
+    // other branch, svm.py:257-262; the next state a BFS pops) takes the tape back to the common
+    // prefix of their roots and extends it from there.  The lowering overlay is not rolled back:
+    // it is a function of the harvest, which is the same at every depth of one state.
+    struct Mark {
+        size_t tape, cols, qpool, local_log, map_log;
+    };
+    Mark mark() const {
+        return Mark{tape.size(), cols.size(), qpool.size(), local_log.size(), map_log.size()};
+    }
+    void rollback(const Mark& m) {
+        for (size_t i = local_log.size(); i-- > m.local_log;) {
+            const uint32_t n = local_log[i];
+            if (n & OWN) local_own[n & ~OWN] = -1;
+            else T.local.unset(n);
+        }
+        local_log.resize(m.local_log);
+        for (size_t i = map_log.size(); i-- > m.map_log;) {
+            const auto& e = map_log[i];
+            (e.first == 0 ? var_cols : e.first == 1 ? cell_cols : e.first == 2 ? pool_consts
+                                                                                  : own_consts)
+                .erase(e.second);
+        }
+        map_log.resize(m.map_log);
+        for (size_t n = m.tape; n < tape.size(); ++n) tape_memo.erase(key_of(tape[n]));
+        tape.resize(m.tape);
+        has_col.resize(m.tape);
+        cols.resize(m.cols);
+        qpool.resize(m.qpool);
     }
 
     mh_terms& T;
@@ -838,6 +907,7 @@ public:
     Tables cells, uf_cells;
     std::unordered_map<std::string, size_t> cell_of, uf_of, kidx;
     std::vector<std::pair<std::string, KeccakMap>> keccak;
+    uint64_t hver = 0;          // keccak pairs / bounds changed (harvest_sig)
     std::vector<Column> ccols;  // every cell / else column lowering made
     std::unordered_map<std::string, uint32_t> cell_index;
     // the root tape
@@ -848,6 +918,10 @@ public:
     std::vector<Column> cols;  // query columns, in first-use order
     std::unordered_map<uint32_t, uint32_t> var_cols, cell_cols, pool_consts, own_consts;
     std::vector<Big> qpool;
+    // what linearise set since the state began (rollback's undo records): nodes given a tape
+    // index (OWN bit for the query's own), and (map, key) of new column / constant entries
+    std::vector<uint32_t> local_log;
+    std::vector<std::pair<uint32_t, uint32_t>> map_log;
 };
 
 }  // namespace
@@ -1354,33 +1428,41 @@ class QueryState {
 public:
     explicit QueryState(mh_terms& t, bool keep_lowering = false) : Q(t, keep_lowering) {}
 
-    // warm: the last query's state, whose lowering this one takes over when their harvests are
-    // equal (a JUMPI's second branch, svm.py:257-262: the same path with the other condition --
-    // only the new constraint is lowered afresh, the rest are memo hits)
+    // A fresh state for the query `rs` (n roots).  warm: the last query's state, whose lowering
+    // this one takes over when their harvests are equal (the same path with another condition:
+    // only what is new is lowered afresh, the rest are memo hits).
     void start(const uint32_t* rs, uint32_t n, QueryState* warm = nullptr) {
-        roots.assign(rs, rs + n);
-        Q.harvest(roots);
+        // the harvest root by root (the same tables as over all roots at once), a copy of the
+        // tables kept at every depth where they grew (rollback restores the prefix's harvest)
+        marks.clear();
+        snaps.clear();
+        snaps.push_back({0, Q.save_harvest()});
+        harvest_roots(rs, 0, n);
         if (warm && Q.same_harvest(warm->Q)) Q.adopt_lowering(warm->Q);
         else if (warm) Q.reset_lowering();
-        for (uint32_t i = 0; i < n; ++i) {  // lower_query: the AND of the lowered roots
-            const uint32_t x = lowered(roots[i]);
-            root = i == 0 ? x : Q.add(AND, 0, root, x);
+        roots.clear();
+        if (!n) {
+            root = Q.add(TRUE_, 0);
+            Q.linearise(root);
+            add_conjuncts(Q.lget(root));
+            return;
         }
-        if (!n) root = Q.add(TRUE_, 0);
-        Q.linearise(root);
-        add_conjuncts(Q.lget(root));
+        lower_roots(rs, 0, n);
     }
 
-    bool extend(uint32_t r) {  // false: r changes the harvest, build afresh
+    // The query `rs` (n roots) from this state: taken back to depth d (the length of the common
+    // prefix of their roots), the harvest of the prefix extended by the rest -- which must end
+    // where this state's harvest is, or the lowering memo would not hold (false: build afresh,
+    // the state is spent) -- then the rest lowered, linearised and grouped root by root.  A
+    // child of the last query is d = all its roots, a JUMPI's other branch d = all but one
+    // (svm.py:257-262), the next state a BFS pops d = where their paths parted (cli.py:417-419).
+    bool advance(const uint32_t* rs, uint32_t n, size_t d) {
         Q.sync();
         const Fingerprint before(Q);
-        Q.harvest({r});
+        rollback(d);
+        harvest_roots(rs, d, n);
         if (!before.same(Q)) return false;
-        const uint32_t x = lowered(r);
-        roots.push_back(r);
-        root = Q.add(AND, 0, root, x);
-        Q.linearise(root);
-        add_conjuncts(Q.lget(x));
+        lower_roots(rs, d, n);
         return true;
     }
 
@@ -1390,6 +1472,50 @@ public:
     std::vector<uint32_t> roots;
 
 private:
+    void harvest_roots(const uint32_t* rs, size_t from, size_t to) {
+        std::array<uint64_t, 4> sig = Q.harvest_sig();
+        for (size_t i = from; i < to; ++i) {
+            Q.harvest({rs[i]});
+            const std::array<uint64_t, 4> s2 = Q.harvest_sig();
+            if (s2 != sig) snaps.push_back({i + 1, Q.save_harvest()});
+            sig = s2;
+        }
+    }
+    void lower_roots(const uint32_t* rs, size_t from, size_t to) {
+        // lower_query: the AND of the lowered roots, linearised root by root (the tape of
+        // AND(x, y) is x's followed by y's new nodes), a checkpoint before every root
+        for (size_t i = from; i < to; ++i) {
+            marks.push_back(Mark{Q.mark(), root, defines, conj.size(), uf_log.size(),
+                                 owner_log.size()});
+            const uint32_t x = lowered(rs[i]);
+            roots.push_back(rs[i]);
+            root = i == 0 ? x : Q.add(AND, 0, root, x);
+            Q.linearise(root);
+            add_conjuncts(Q.lget(x));
+        }
+    }
+    // Back to depth d <= roots.size(): every root since undone (tape, columns, constants,
+    // conjuncts, union-find, owners; the harvest as it was after the first d roots).  The
+    // lowering overlay and memo stay: they hold for any query with this harvest.
+    void rollback(size_t d) {
+        if (d >= roots.size()) return;
+        const Mark m = marks.at(d);
+        for (size_t i = uf_log.size(); i-- > m.uf_log;) uf[uf_log[i].first] = uf_log[i].second;
+        uf_log.resize(m.uf_log);
+        for (size_t i = owner_log.size(); i-- > m.owner_log;)
+            owner[owner_log[i].first] = owner_log[i].second;
+        owner_log.resize(m.owner_log);
+        conj.resize(m.conj);
+        uf.resize(m.conj);
+        Q.rollback(m.q);
+        owner.resize(Q.tape.size(), -1);
+        root = m.root;
+        defines = m.defines;
+        roots.resize(d);
+        marks.resize(d);
+        while (snaps.size() > 1 && snaps.back().first > d) snaps.pop_back();
+        Q.restore_harvest(snaps.back().second);
+    }
     uint32_t lowered(uint32_t r) {
         const uint32_t x = Q.lower(r);
         if (Q.width(x) != 0 || (Q.nd(x).flags & F_ARRAY)) invalid("constraints must be Bool");
@@ -1412,9 +1538,10 @@ private:
                 if (!Q.has_col[n]) continue;
                 if (owner[n] >= 0) {
                     const uint32_t a = find((uint32_t)i), b = find((uint32_t)owner[n]);
-                    uf[std::max(a, b)] = std::min(a, b);  // the earlier conjunct stays the root
+                    set_uf(std::max(a, b), std::min(a, b));  // the earlier conjunct stays the root
                     continue;
                 }
+                owner_log.push_back({n, owner[n]});
                 owner[n] = (int32_t)i;
                 const mh_node& x = Q.tape[n];
                 const uint32_t kids[3] = {x.a, x.b, x.c};
@@ -1423,8 +1550,16 @@ private:
         }
     }
     uint32_t find(uint32_t x) {
-        while (uf[x] != x) x = uf[x] = uf[uf[x]];
+        while (uf[x] != x) {
+            set_uf(x, uf[uf[x]]);
+            x = uf[x];
+        }
         return x;
+    }
+    void set_uf(uint32_t i, uint32_t v) {  // every write logged: rollback restores them
+        if (uf[i] == v) return;
+        uf_log.push_back({i, uf[i]});
+        uf[i] = v;
     }
     bool emit_definitions(mh_query& q);
 
@@ -1433,15 +1568,35 @@ private:
     std::vector<int32_t> owner;   // per tape node: the first conjunct reaching it
     std::vector<uint32_t> uf;     // union-find over conj
     bool defines = false;
+    // checkpoints: marks[k] is the state at depth k (before root k); snaps the harvest tables
+    // after the first `first` roots, at 0 and at every depth where they grew
+    struct Mark {
+        Query::Mark q;
+        uint32_t root;
+        bool defines;
+        size_t conj, uf_log, owner_log;
+    };
+    std::vector<Mark> marks;
+    std::vector<std::pair<size_t, Query::HarvestCopy>> snaps;
+    std::vector<std::pair<uint32_t, uint32_t>> uf_log;   // (index, previous value)
+    std::vector<std::pair<uint32_t, int32_t>> owner_log;  // (tape node, previous owner)
 };
 
 void QueryState::emit(mh_query& q, uint32_t& flags) {
     const std::vector<mh_node>& tape = Q.tape;
     const uint32_t N = (uint32_t)tape.size();
     if (Q.lget(root) != N - 1) unsupported("the query's root is not the last node of its tape");
-    for (const Column& c : Q.cols)  // a variable named like a cell would make two columns one
-        if (c.kind == MH_COL_VAR && Q.cell_index.count(c.name))
-            unsupported("variable " + c.name + " is named like an array cell");
+    {
+        // a variable named like a cell of this query would make two columns one (the cell
+        // columns the lowering made for other queries of the state do not count)
+        std::unordered_set<std::string> cells;
+        for (const Column& c : Q.cols)
+            if (c.kind != MH_COL_VAR) cells.insert(c.name);
+        if (!cells.empty())
+            for (const Column& c : Q.cols)
+                if (c.kind == MH_COL_VAR && cells.count(c.name))
+                    unsupported("variable " + c.name + " is named like an array cell");
+    }
     if (refuted(Q, conj)) flags |= MH_QUERY_REFUTED;
     if (defines && emit_definitions(q)) {
         flags |= MH_QUERY_DEFINITIONS;
@@ -1678,20 +1833,27 @@ int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_
     uint32_t flags = 0;
     try {
         QueryState* st = t->last.get();
-        // a child of the last query (its roots plus one) extends it when the harvest is unchanged
-        const bool child = st && n_roots == st->roots.size() + 1 &&
-                           std::equal(st->roots.begin(), st->roots.end(), roots);
-        if (!child) {
-            // not a child of the last query: a fresh state, which takes over the last query's
-            // lowering when the harvests agree (start)
+        // The state keeps a checkpoint per root: a query sharing a prefix of d > 0 roots with it
+        // takes it back to depth d and extends it by the rest (QueryState::advance) -- a child
+        // of the last query, a JUMPI's other branch, the next state a BFS pops.  Otherwise, or
+        // when the rest changes the harvest, the query is built afresh, taking over the
+        // state's lowering when the harvests agree (start).
+        size_t d = 0;
+        if (st) {
+            const size_t m = std::min<size_t>(st->roots.size(), n_roots);
+            while (d < m && st->roots[d] == roots[d]) ++d;
+        }
+        if (st && d > 0 && st->advance(roots, n_roots, d)) {
+            flags |= MH_QUERY_INCREMENTAL;
+        } else if (st && d > 0) {
+            // the rest changed the harvest: afresh (a new epoch of the scratch maps)
+            t->last.reset();
+            t->last.reset(new QueryState(*t));
+            t->last->start(roots, n_roots);
+        } else {
             std::unique_ptr<QueryState> prev = std::move(t->last);
             t->last.reset(new QueryState(*t, prev != nullptr));
             t->last->start(roots, n_roots, prev.get());
-        } else if (!st->extend(roots[n_roots - 1])) {
-            // the new constraint changed the harvest (the last state has taken it in): afresh
-            t->last.reset();  // a fresh query starts a new epoch of the scratch maps
-            t->last.reset(new QueryState(*t));
-            t->last->start(roots, n_roots);
         }
         t->last->emit(*q, flags);
     } catch (const Fail& f) {

@@ -436,6 +436,7 @@ COLUMN_KINDS = ("var", "cell", "else", "ufcell", "ufelse")  # MH_COL_*
 TABLE_CELLS, TABLE_UF_CELLS, TABLE_KECCAK = 0, 1, 2
 QUERY_DEFINITIONS = 1
 QUERY_REFUTED = 2
+QUERY_INCREMENTAL = 4  # diagnostic: built from the session's state, not afresh
 QUERY_KEY_LIMBS = 36
 
 

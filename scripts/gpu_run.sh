@@ -17,6 +17,8 @@
 #   kbench    bench.py --variant keccak (config 4's kernel, 2^20 rows)
 #   kprofile  scripts/profile.sh <tag>_keccak --variant keccak
 #   paths     scripts/path_scaling.py (latency against path length, 25..400 constraints)
+#   bfs       scripts/bfs_order.py --solve and host-only (BFS / JUMPI order at 400 constraints)
+#   jumpi     scripts/jumpi_order.py (both branches of every JUMPI, 100 and 400 constraints)
 #   ibench    bench.py --engine interp (config 5 on the interpreter, one step)
 #   strong    bench.py --strong at N=1 (config 5 literally: 2^26 rows in total)
 #   import    scripts/import_cost.py (the z3 import stage per new constraint, C++ vs Python)
@@ -78,6 +80,9 @@ for step in "$@"; do
     kbench)   timeout -k 10 400 python -u bench.py --variant keccak --cpu-seconds 5 > "$OUT/bench_keccak.json" 2> "$OUT/bench_keccak.log" ;;
     kprofile) bash scripts/profile.sh "${TAG}_keccak" --variant keccak ;;
     paths)    timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" ;;
+    bfs)      timeout -k 10 600 python -u scripts/bfs_order.py --solve > "$OUT/bfs_order_solve.jsonl" 2> "$OUT/bfs_order_solve.log" && \
+              timeout -k 10 300 python -u scripts/bfs_order.py > "$OUT/bfs_order_host.jsonl" 2> "$OUT/bfs_order_host.log" ;;
+    jumpi)    timeout -k 10 600 python -u scripts/jumpi_order.py > "$OUT/jumpi_order.jsonl" 2> "$OUT/jumpi_order.log" ;;
     import)   timeout -k 10 300 python -u scripts/import_cost.py > "$OUT/import_cost.jsonl" 2> "$OUT/import_cost.log" ;;
     ibench)   timeout -k 10 600 python -u bench.py --engine interp --steps 1 --warmup 1 --no-companion --no-cpu-baseline > "$OUT/bench_interp.json" 2> "$OUT/bench_interp.log" ;;
     strong)   timeout -k 10 400 python -u bench.py --strong --no-companion --cpu-seconds 3 > "$OUT/bench_strong.json" 2> "$OUT/bench_strong.log" ;;

@@ -594,3 +594,114 @@ def test_definitions_are_solved_natively():
     cq = check_query(ctx.b, [nodes[0]], "one")
     assert cq.flags & native.QUERY_DEFINITIONS and len(cq.tapes) == 1
     assert int(cq.tapes[0]["op"][-1]) == int(Op.TRUE)
+
+
+@pytest.mark.parametrize("shape,k,seed", [("killbilly", 4, 0), ("overflow", 8, 1),
+                                          ("ether_thief", 4, 2), ("ether_thief", 8, 3)])
+def test_grown_paths_in_bfs_order(shape, k, seed):
+    """both branches of every JUMPI, the open states interleaved the way
+    LASER's BFS pops them (cli.py:417-419, svm.py:243-262; tests/bfs_order.py).  The session's
+    state is taken back to the common prefix of each query's roots and extended by the rest
+    (query.cpp mh_query_build): node for node the Python stages' result in that order, and past
+    the first queries every query is built from the state, none afresh."""
+    from mythril_amd.smt import Not
+    from tests.bfs_order import bfs_queries
+
+    from mythril_amd.lower import Lowering
+
+    ctx, cs = grow(shape, 30)
+    nodes = [c.node for c in cs]
+    negs = [Not(c).node for c in cs]
+    last_fp, fresh, dropped = None, [], set()
+    for i, roots in enumerate(bfs_queries(nodes, negs, 18, k, seed, dropped)):
+        cq = check_query(ctx.b, roots, (shape, k, i))
+        if cq is not None and cq.flags & native.QUERY_REFUTED:
+            dropped.add(tuple(roots))
+        fp = Lowering(ctx.b).collect(roots).fingerprint()
+        if cq is not None and i > 0 and not cq.flags & native.QUERY_INCREMENTAL:
+            fresh.append((i, fp != last_fp))
+        last_fp = fp
+    # afresh only where the query's harvest (constant keys, keccak pairs and bounds) is not the
+    # last query's: the lowering depends on it
+    assert all(changed for _, changed in fresh), fresh
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_queries_in_bfs_order(seed):
+    """The same over random array / function / keccak conjunctions (a new constraint may change
+    the harvest: that query is built afresh, still node for node the Python stages' result)."""
+    import random
+
+    from mythril_amd.smt import Not
+    from tests.bfs_order import bfs_queries
+
+    rng = random.Random(100 + seed)
+    ctx, cs = _random_query(rng, 10)
+    cs = [c for c in cs if hasattr(c, "node")]
+    nodes = [c.node for c in cs]
+    negs = [Not(c).node for c in cs]
+    dropped = set()
+    for i, roots in enumerate(bfs_queries(nodes, negs, 3, 4, seed, dropped)):
+        cq = check_query(ctx.b, roots, (seed, i))
+        if cq is not None and cq.flags & native.QUERY_REFUTED:
+            dropped.add(tuple(roots))
+
+
+@pytest.mark.parametrize("shape,k", [("killbilly", 4), ("ether_thief", 8), ("overflow", 4)])
+def test_guide_session_in_bfs_order(shape, k):
+    """The harvester session in BFS / JUMPI order: a tape that shares only a prefix with the
+    last one (the other branch: the path's tape, then other nodes) keeps the memo of the prefix
+    and gives the rest a new node generation (harvest.cpp Harvester::truncate) -- the arrays
+    are those of a fresh harvest on every query, and most queries reuse the session."""
+    import random
+
+    from mythril_amd.smt import Not
+    from tests.bfs_order import bfs_queries
+
+    ctx, cs = grow(shape, 40)
+    nodes = [c.node for c in cs]
+    negs = [Not(c).node for c in cs]
+    sess = native.GuideSession()
+    rng = random.Random(7)
+    m = native.TermMirror.of(ctx.b)
+    n, dropped = 0, set()
+    for i, roots in enumerate(bfs_queries(nodes, negs, 20, k, 3, dropped)):
+        cq = m.build(ctx.b, roots)
+        if cq.flags & native.QUERY_REFUTED:
+            dropped.add(tuple(roots))
+        parent = [(c, rng.getrandbits(int(cq.widths[c]))) for c in range(len(cq.names))
+                  if rng.random() < 0.3] if i % 3 == 0 else ()
+        want = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, parent)
+        got = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, parent, session=sess)
+        assert _guide_equal(got, want), (shape, k, i)
+        n += 1
+    reused, fresh, _ = sess.stats()
+    assert reused >= 0.9 * n, (reused, fresh, n)
+    sess.close()
+
+
+@pytest.mark.parametrize("family", ["random", "laser"])
+def test_guide_session_planted_paths_in_jumpi_order(family):
+    """Planted paths (keccak conditions, stores, wide equalities) with both branches of every
+    constraint asked: the session's arrays equal a fresh harvest's on every query."""
+    from mythril_amd.smt import Not
+    from tests.planted import planted_path
+
+    for seed in range(3):
+        ctx, cs, _, _ = planted_path(family, seed, 16)
+        nodes = [c.node for c in cs]
+        negs = [Not(c).node for c in cs]
+        sess = native.GuideSession()
+        m = native.TermMirror.of(ctx.b)
+        for kk in range(1, len(nodes) + 1):
+            for roots in (nodes[:kk], nodes[:kk - 1] + [negs[kk - 1]]):
+                try:
+                    cq = m.build(ctx.b, roots)
+                except native.Unsupported:
+                    continue
+                if cq.flags & native.QUERY_REFUTED:
+                    continue
+                want = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths)
+                got = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, session=sess)
+                assert _guide_equal(got, want), (family, seed, kk)
+        sess.close()

@@ -168,6 +168,26 @@ def workload(n_random=40):
         ctx, cs = _random_query(random.Random(seed), 3 + seed % 9)
         laser_order(ctx.b, [c.node for c in cs])
         done(ctx.b)
+    # BFS order with both branches of every JUMPI (the query compiler's rollback and replay,
+    # the harvester session's prefix truncation; tests/bfs_order.py)
+    from mythril_amd.smt import Not
+    from tests.bfs_order import bfs_queries
+
+    for shape, k in (("killbilly", 4), ("ether_thief", 8), ("overflow", 4)):
+        ctx, cs = grow(shape, 40)
+        nodes, negs = [c.node for c in cs], [Not(c).node for c in cs]
+        for roots in bfs_queries(nodes, negs, 20, k, k):
+            host_query(ctx.b, roots, guides, rng)
+        done(ctx.b)
+    for seed in range(min(n_random, 12)):
+        ctx, cs = _random_query(random.Random(500 + seed), 8)
+        cs = [c for c in cs if hasattr(c, "node")]
+        for roots in bfs_queries([c.node for c in cs], [Not(c).node for c in cs], 2, 4, seed):
+            try:
+                host_query(ctx.b, roots, guides, rng)
+            except native.Unsupported:
+                pass
+        done(ctx.b)
     guides.close()
     smtlib_workload()
 
