@@ -289,7 +289,10 @@ uint64_t mh_smtlib_size(const mh_smtlib* s);  /* nodes the session mirrors      
  * (the query goes to z3).  A session is used by one thread at a time.                            */
 typedef struct mh_terms mh_terms;
 typedef struct mh_query mh_query;
-enum { MH_COL_VAR = 0, MH_COL_CELL = 1, MH_COL_ELSE = 2, MH_COL_UFCELL = 3, MH_COL_UFELSE = 4 };
+/* column kinds; a read (MH_COL_READ / MH_COL_UFREAD: an array's / a tabled function's value at a
+ * symbolic index term, Ackermann's reduction) carries the index term's node id as its key      */
+enum { MH_COL_VAR = 0, MH_COL_CELL = 1, MH_COL_ELSE = 2, MH_COL_UFCELL = 3, MH_COL_UFELSE = 4,
+       MH_COL_READ = 5, MH_COL_UFREAD = 6 };
 enum { MH_TABLE_CELLS = 0, MH_TABLE_UF_CELLS = 1, MH_TABLE_KECCAK = 2 };
 #define MH_QUERY_DEFINITIONS 1u
 #define MH_QUERY_REFUTED 2u     /* the conjunction contradicts itself syntactically (a FALSE

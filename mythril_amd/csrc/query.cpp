@@ -297,6 +297,7 @@ public:
         ov_cv_vals = std::move(o.ov_cv_vals);
         ccols = std::move(o.ccols);
         cell_index = std::move(o.cell_index);
+        read_li = std::move(o.read_li);
     }
     // the harvest tables, copied whole (a state keeps one per depth at which its harvest grew)
     struct HarvestCopy {
@@ -566,14 +567,16 @@ public:
 
     // ---- pass 2: lower.py Lowering.lower / _rewrite -------------------------------------------
     uint32_t cell_column(const std::string& name, uint32_t w, uint32_t kind,
-                         const std::string& sym, const Big* key) {
+                         const std::string& sym, const Big* key, uint32_t li = UINT32_MAX) {
         auto it = cell_index.find(name);
         if (it == cell_index.end()) {
             it = cell_index.emplace(name, (uint32_t)ccols.size()).first;
             ccols.push_back(Column{name, sym, w, kind, key != nullptr, key ? *key : Big()});
+            read_li.push_back(li);  // a read's index term (the first lowering that made it)
         }
         return add(VAR, w, 0, 0, 0, CELL_COL | it->second);
     }
+    static bool read_kind(uint32_t k) { return k == MH_COL_READ || k == MH_COL_UFREAD; }
 
     void deps(uint32_t n, std::vector<uint32_t>& d) {  // Lowering._deps
         d.clear();
@@ -636,7 +639,7 @@ public:
 
     uint32_t rewrite(uint32_t n) {
         const mh_node x = nd(n);
-        if (x.op == SELECT) return select(x.a, low(x.b));
+        if (x.op == SELECT) return select(x.a, low(x.b), x.b);
         if (x.op == UF) return apply(n);
         const int k = arity(x.op);
         if (k == 0) return n;
@@ -716,27 +719,34 @@ public:
         return add(EXTRACT, hi - lo, piece, 0, 0, hi - 1, lo);
     }
 
-    uint32_t select(uint32_t arr, uint32_t idx) {  // Lowering._select
+    uint32_t select(uint32_t arr, uint32_t idx, uint32_t idx_orig) {  // Lowering._select
         const mh_node a = nd(arr);
         if (a.op == STORE) {
             const uint32_t key = low(a.b), val = low(a.c);
-            const uint32_t rest = select(a.a, idx);
+            const uint32_t rest = select(a.a, idx, idx_orig);
             return add(ITE, width(val), eq(idx, key), val, rest);
         }
         if (a.op == CONST_ARRAY) return low(a.a);
         const std::string& name = array_name(arr);
         auto it = cell_of.find(name);
         return table(name, a.width, idx, it == cell_of.end() ? nullptr : &cells[it->second].second,
-                     MH_COL_CELL, MH_COL_ELSE);
+                     MH_COL_CELL, MH_COL_ELSE, MH_COL_READ, idx_orig);
     }
+    // _table: a constant key's cell; any other constant key the else value; a symbolic index
+    // the cells' ite chain over its read column name[@idx_orig] (Ackermann's reduction)
     uint32_t table(const std::string& name, uint32_t rng, uint32_t idx,
-                   const std::vector<Big>* keys, uint32_t kcell, uint32_t kelse) {  // _table
+                   const std::vector<Big>* keys, uint32_t kcell, uint32_t kelse, uint32_t kread,
+                   uint32_t idx_orig) {
         const Big* kp = const_value(idx);
         const Big key = kp ? *kp : Big();
         if (kp && keys && std::binary_search(keys->begin(), keys->end(), key))
             return cell_column(name + "[" + key.hex() + "]", rng, kcell, name, &key);
-        uint32_t acc = cell_column(name + "[*]", rng, kelse, name, nullptr);
-        if (kp || !keys) return acc;  // a constant key outside the table reads the else value
+        if (kp) return cell_column(name + "[*]", rng, kelse, name, nullptr);
+        Big ik;
+        ik.w[0] = idx_orig;
+        uint32_t acc = cell_column(name + "[@" + std::to_string(idx_orig) + "]", rng, kread, name,
+                                   &ik, idx);
+        if (!keys) return acc;
         for (size_t i = keys->size(); i-- > 0;) {
             const Big k = (*keys)[i];
             const uint32_t cell = cell_column(name + "[" + k.hex() + "]", rng, kcell, name, &k);
@@ -776,7 +786,7 @@ public:
         }
         auto it = uf_of.find(f);
         return table(f, x.width, a, it == uf_of.end() ? nullptr : &uf_cells[it->second].second,
-                     MH_COL_UFCELL, MH_COL_UFELSE);
+                     MH_COL_UFCELL, MH_COL_UFELSE, MH_COL_UFREAD, x.a);
     }
 
     // ---- the root tape (sieve.py local_tapeset): VAR imm0 = query column, CONST imm0 = query
@@ -908,7 +918,8 @@ public:
     std::unordered_map<std::string, size_t> cell_of, uf_of, kidx;
     std::vector<std::pair<std::string, KeccakMap>> keccak;
     uint64_t hver = 0;          // keccak pairs / bounds changed (harvest_sig)
-    std::vector<Column> ccols;  // every cell / else column lowering made
+    std::vector<Column> ccols;  // every cell / else / read column lowering made
+    std::vector<uint32_t> read_li;  // per ccol: a read's lowered index term (else UINT32_MAX)
     std::unordered_map<std::string, uint32_t> cell_index;
     // the root tape
     std::vector<mh_node> tape;
@@ -1486,12 +1497,62 @@ private:
         // AND(x, y) is x's followed by y's new nodes), a checkpoint before every root
         for (size_t i = from; i < to; ++i) {
             marks.push_back(Mark{Q.mark(), root, defines, conj.size(), uf_log.size(),
-                                 owner_log.size()});
+                                 owner_log.size(), qreads.size()});
             const uint32_t x = lowered(rs[i]);
             roots.push_back(rs[i]);
             root = i == 0 ? x : Q.add(AND, 0, root, x);
             Q.linearise(root);
             add_conjuncts(Q.lget(x));
+            congruence(x);
+        }
+    }
+    // lower.py congruence: the read columns x reads first in this query (directly or in a read's
+    // index term), by (symbol, index term), each paired with every earlier read of its symbol:
+    // Or(Not(i == j), A[@i] == A[@j]) ANDed on as a conjunct of its own
+    void congruence(uint32_t x) {
+        std::vector<uint32_t> found, st{x};
+        std::unordered_set<uint32_t> vis, fs;
+        while (!st.empty()) {
+            const uint32_t n = st.back();
+            st.pop_back();
+            if (!vis.insert(n).second) continue;
+            const mh_node& v = Q.nd(n);
+            if (v.op == VAR && (n & OWN) && (v.imm0 & CELL_COL)) {
+                const uint32_t k = v.imm0 & ~CELL_COL;
+                if (Query::read_kind(Q.ccols.at(k).kind) && fs.insert(k).second) {
+                    found.push_back(k);
+                    st.push_back(Q.read_li.at(k));
+                }
+                continue;
+            }
+            const uint32_t kids[3] = {v.a, v.b, v.c};
+            for (int j = 0; j < arity(v.op); ++j) st.push_back(kids[j]);
+        }
+        std::vector<uint32_t> fresh;
+        for (uint32_t k : found)
+            if (!qseen.count(k)) fresh.push_back(k);
+        std::sort(fresh.begin(), fresh.end(), [&](uint32_t a, uint32_t b) {
+            const Column& ca = Q.ccols[a];
+            const Column& cb = Q.ccols[b];
+            if (ca.symbol != cb.symbol) return ca.symbol < cb.symbol;
+            return ca.key < cb.key;
+        });
+        for (uint32_t p : fresh) {
+            const Column& cp = Q.ccols[p];
+            for (size_t qi = 0; qi < qreads.size(); ++qi) {
+                const uint32_t q = qreads[qi];
+                const Column& cq = Q.ccols[q];
+                if (cq.symbol != cp.symbol || cq.kind != cp.kind) continue;
+                const uint32_t same = Q.eq(Q.read_li[q], Q.read_li[p]);
+                const uint32_t vq = Q.add(VAR, cq.width, 0, 0, 0, CELL_COL | q);
+                const uint32_t vp = Q.add(VAR, cp.width, 0, 0, 0, CELL_COL | p);
+                const uint32_t y = Q.add(MH_OP_OR, 0, Q.add(MH_OP_NOT, 0, same), Q.add(EQ, 0, vq, vp));
+                root = Q.add(AND, 0, root, y);
+                Q.linearise(root);
+                add_conjuncts(Q.lget(y));
+            }
+            qreads.push_back(p);
+            qseen.insert(p);
         }
     }
     // Back to depth d <= roots.size(): every root since undone (tape, columns, constants,
@@ -1507,6 +1568,10 @@ private:
         owner_log.resize(m.owner_log);
         conj.resize(m.conj);
         uf.resize(m.conj);
+        while (qreads.size() > m.qreads) {
+            qseen.erase(qreads.back());
+            qreads.pop_back();
+        }
         Q.rollback(m.q);
         owner.resize(Q.tape.size(), -1);
         root = m.root;
@@ -1574,9 +1639,11 @@ private:
         Query::Mark q;
         uint32_t root;
         bool defines;
-        size_t conj, uf_log, owner_log;
+        size_t conj, uf_log, owner_log, qreads;
     };
     std::vector<Mark> marks;
+    std::vector<uint32_t> qreads;        // read columns (ccol) in the order the query met them
+    std::unordered_set<uint32_t> qseen;
     std::vector<std::pair<size_t, Query::HarvestCopy>> snaps;
     std::vector<std::pair<uint32_t, uint32_t>> uf_log;   // (index, previous value)
     std::vector<std::pair<uint32_t, int32_t>> owner_log;  // (tape node, previous owner)

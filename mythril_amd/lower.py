@@ -7,11 +7,16 @@ The device evaluates bit-vector terms only, so a query is lowered, once per ``ge
 into a term over scalar *columns* whose every assignment denotes one complete z3-style model:
 
 * a free array ``A`` becomes a finite map over the constant keys the query reads (one *cell*
-  column per key) plus one *else* column: ``select(A, c)`` for a harvested constant ``c`` is
-  cell ``A[c]``; a symbolic index becomes ``ite(i == c1, A[c1], ite(i == c2, A[c2], ... A[*]))``.
-  That is exactly the shape of a z3 array model (``Store(...Store(K(else), c1, v1)..., ck, vk)``),
-  so a satisfying assignment is a model of the original query; ``store`` chains become ``ite``
-  over their keys and ``K(v)`` becomes ``v`` (array.py:16-63).
+  column per key) plus one *read* column per symbolic index term the query reads it at
+  (Ackermann's reduction, round 6): ``select(A, c)`` for a harvested constant ``c`` is cell
+  ``A[c]``; ``select(A, i)`` for a symbolic ``i`` is ``ite(i == c1, A[c1], ... ite(i == ck, A[ck],
+  A[@i]))``, and the query gains, after the constraint that first reads ``A[@j]``, one conjunct
+  ``Or(Not(i == j), A[@i] == A[@j])`` per earlier read ``A[@i]`` (congruence), so two reads at
+  unequal indices may differ.  A satisfying assignment is a model of the original query: ``A`` is
+  ``Store(...Store(K(else), c1, v1)..., i_val, A[@i]_val ...)`` (the reads at their indices'
+  values, where no cell is); ``store`` chains become ``ite`` over their keys and ``K(v)`` becomes
+  ``v`` (array.py:16-63).  A constant key outside the table -- only met by ``Model.eval`` of a
+  term the query did not state -- reads the reads at equal indices, else the *else* column.
 * a keccak function ``keccak256_N`` becomes ``ite(x == c_i, k_i, H(x))`` over the concrete pairs
   ``keccak256_N(c_i) == k_i`` the query states (keccak_function_manager.py:92-97,145-148), with
   ``H(x) = base + ((keccak256(x) >> 139) << 6)``: a function of the argument (so congruence
@@ -22,8 +27,8 @@ into a term over scalar *columns* whose every assignment denotes one complete z3
   rounded up to a multiple of 64 — the interval of ``_create_condition`` (:121-149) is
   ``PART = (2^256-1) // 10^40 > 2^123 + 64`` wide, so the interval and ``mod 64`` conditions hold
   by construction.  The hash runs on the device's Keccak-f[1600].
-* any other uninterpreted function is tabled like an array (cells over constant arguments plus
-  one else column).
+* any other uninterpreted function is tabled like an array (cells over constant arguments, a
+  read column per symbolic argument term with the same congruence conjuncts, function.py:7-25).
 
 Anything else array- or function-sorted (array equality, ``ite`` over arrays, an inverse applied
 to something other than its forward function) raises ``LoweringUnsupported``: the query goes to
@@ -58,9 +63,18 @@ class Column:
 
     name: str             # VAR name in the tape set
     width: int
-    kind: str             # "var" | "cell" | "else" | "ufcell" | "ufelse"
+    kind: str             # "var" | "cell" | "else" | "ufcell" | "ufelse" | "read" | "ufread"
     symbol: str           # variable / array / function name
-    key: Optional[int] = None
+    key: Optional[int] = None  # cells: the constant key; reads: the index term's node
+
+
+READ_KINDS = ("read", "ufread")
+
+
+def read_name(sym: str, index_node: int) -> str:
+    """The column of the value `sym` (a free array or a tabled function) has at the symbolic
+    index term `index_node` (the term as the query states it, before lowering)."""
+    return "%s[@%d]" % (sym, index_node)
 
 
 @dataclass
@@ -219,6 +233,8 @@ class Lowering:
         self.schema = frozen if frozen is not None else Schema()
         self.memo: Dict[int, int] = {}
         self.sym = b.symbols
+        # read column -> its lowered index term (the congruence conjuncts compare those)
+        self.read_index: Dict[str, int] = {}
         # rewrites that read the harvest's tables (a table lookup at a symbolic key, a keccak
         # application) depend on the fingerprint; every other rewrite is the same under any
         # harvest that contains the node's own (a constant key is in it): those are kept on the
@@ -516,21 +532,44 @@ class Lowering:
             return self.memo[b.nodes[arr][2]]
         name = self.sym.array_names[b.nodes[arr][5]]
         rng = b.widths[arr]
-        return self._table(name, rng, idx, self.schema.cells.get(name, {}), "cell", "else")
+        return self._table(name, rng, idx, self.schema.cells.get(name, {}), "cell", "else",
+                           "read", idx_orig)
 
     def _table(self, name: str, rng: int, idx: int, cells: Dict[int, str], kcell: str,
-               kelse: str) -> int:
+               kelse: str, kread: str, idx_orig: int) -> int:
         b = self.b
         key = b.const_value(idx)
         if key is not None and key in cells:
             return self._column(cells[key], rng, kcell, name, key)
-        acc = self._column(else_name(name), rng, kelse, name)
-        if key is not None:  # a constant key outside the table reads the else value
-            return acc
+        if key is not None:  # a constant key outside the table: the reads, else the else value
+            return self._fallback(name, rng, idx, kelse, kread)
+        rname = read_name(name, idx_orig)
+        if not self.frozen:
+            acc = self._column(rname, rng, kread, name, idx_orig)
+            self.read_index.setdefault(rname, idx)
+        elif rname in self.schema.columns:  # Model.eval of a read the query made
+            acc = self._column(rname, rng, kread, name, idx_orig)
+        else:  # Model.eval at another index: the model's value there
+            acc = self._fallback(name, rng, idx, kelse, kread)
         for ck in sorted(cells, reverse=True):
             cell = self._column(cells[ck], rng, kcell, name, ck)
             kn = b.const(ck, b.widths[idx])
             acc = b.op(Op.ITE, self.eq(idx, kn), cell, acc)
+        return acc
+
+    def _fallback(self, name: str, rng: int, idx: int, kelse: str, kread: str) -> int:
+        """The value at an index no cell holds: the read whose index equals it, else the else
+        column (with a frozen schema: the model's table; otherwise a query reads no such key)."""
+        b = self.b
+        acc = self._column(else_name(name), rng, kelse, name)
+        if not self.frozen:
+            return acc
+        reads = sorted((c for c in self.schema.columns.values()
+                        if c.kind == kread and c.symbol == name), key=lambda c: c.key)
+        for c in reversed(reads):
+            li = self.lower(c.key)
+            acc = b.op(Op.ITE, self.eq(idx, li), self._column(c.name, rng, kread, name, c.key),
+                       acc)
         return acc
 
     def _apply(self, n: int) -> int:
@@ -557,10 +596,40 @@ class Lowering:
                            b.const(km.pairs[arg], 256), acc)
             return acc
         cells = self.schema.uf_cells.get(fname, {})
-        return self._table(fname, w, x, cells, "ufcell", "ufelse")
+        return self._table(fname, w, x, cells, "ufcell", "ufelse", "ufread", a)
 
 
 MAX_LOWERINGS = 64  # pass-2 memos kept per builder, by harvest fingerprint (LRU)
+
+
+def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) -> List[int]:
+    """The conjuncts that keep the read columns functional (Ackermann's reduction): for every
+    read column the lowered constraint `x` reads first in its query (directly or in the index
+    term of a read it reads) -- ordered by (symbol, index term) -- and every read of the same
+    symbol before it (`reads`, in the order the query introduced them; updated here),
+    ``Or(Not(i == j), A[@i] == A[@j])``.  The native query
+    compiler makes the same conjuncts in the same order (csrc/query.cpp congruence)."""
+    names = var_names(b)
+    found, work = {}, [x]
+    while work:  # the reads under x, and under the index terms of those (A[B[i]])
+        t = work.pop()
+        for v in node_columns(b, [t])[t]:
+            col = L.schema.columns.get(names[v])
+            if col is not None and col.kind in READ_KINDS and col.name not in found:
+                found[col.name] = col
+                work.append(L.read_index[col.name])
+    new = sorted((c for c in found.values() if c.name not in seen),
+                 key=lambda c: (c.symbol, c.key))
+    out = []
+    for p in new:
+        for q in reads:
+            if q.symbol == p.symbol and q.kind == p.kind:
+                same = L.eq(L.read_index[q.name], L.read_index[p.name])
+                out.append(b.op(Op.OR, b.op(Op.NOT, same),
+                                b.op(Op.EQ, b.var(q.name, q.width), b.var(p.name, p.width))))
+        reads.append(p)
+        seen.add(p.name)
+    return out
 
 
 def lower_query(b: TapeBuilder, roots: Sequence[int],
@@ -596,7 +665,11 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
                 lows.popitem(last=False)
         else:
             lows.move_to_end(fp)
-        low = [L.lower(r) for r in roots]
+        low, reads, seen = [], [], set()
+        for r in roots:
+            x = L.lower(r)
+            low.append(x)
+            low.extend(congruence(b, L, x, reads, seen))
         cols = node_columns(b, low)
         used = frozenset().union(*(cols[r] for r in low)) if low else frozenset()
         schema = _schema_of(b, L, used)
@@ -609,7 +682,7 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
     for x in low[1:]:
         acc = b.op(Op.AND, acc, x)
     if frozen is None:
-        _remember_prefix(b, roots, h, fp, L, low, used, acc)
+        _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen)
     return acc, schema
 
 
@@ -625,6 +698,8 @@ class _Prefix:
     low: List[int]
     used: frozenset
     acc: int
+    reads: list = field(default_factory=list)   # read columns in introduction order
+    seen: set = field(default_factory=set)
 
 
 def _prefix_state(b: TapeBuilder, roots: Sequence[int]) -> Optional[_Prefix]:
@@ -632,9 +707,9 @@ def _prefix_state(b: TapeBuilder, roots: Sequence[int]) -> Optional[_Prefix]:
     return None if cache is None else cache.get(tuple(roots[:-1]))
 
 
-def _remember_prefix(b, roots, h, fp, L, low, used, acc) -> None:
+def _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen) -> None:
     cache = b.__dict__.setdefault("_lower_prefixes", OrderedDict())
-    cache[tuple(roots)] = _Prefix(h, fp, L, list(low), used, acc)
+    cache[tuple(roots)] = _Prefix(h, fp, L, list(low), used, acc, list(reads), set(seen))
     while len(cache) > PREFIX_STATES:
         cache.popitem(last=False)
 
@@ -662,10 +737,15 @@ def _lower_extend(b: TapeBuilder, roots: Sequence[int]) -> Tuple[int, "Schema"]:
     x = L.lower(new)
     if b.widths[x] != BOOL:
         raise TapeError("constraints must be Bool")
-    low = par.low + [x]
-    used = par.used | node_columns(b, [x])[x]
-    acc = b._add(Op.AND, BOOL, par.acc, x)
-    _remember_prefix(b, roots, h, fp, L, low, used, acc)
+    reads, seen = list(par.reads), set(par.seen)
+    added = [x] + congruence(b, L, x, reads, seen)
+    low = par.low + added
+    used = par.used
+    acc = par.acc
+    for y in added:
+        used = used | node_columns(b, [y])[y]
+        acc = b._add(Op.AND, BOOL, acc, y)
+    _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen)
     return acc, _schema_of(b, L, used)
 
 

@@ -155,18 +155,40 @@ class Model:
             if c.width == 1 and self._bool_symbol(name):
                 return bool(self.values[name])
             return BitVecValue(self.values[name], c.width)
-        cells = self.schema.cells.get(name) or self.schema.uf_cells.get(name)
-        els = [col for col in self.schema.columns.values()
-               if col.symbol == name and col.kind in ("else", "ufelse")]
-        if cells is not None or els:
-            cells = cells or {}
-            else_v = self.values.get(els[0].name, 0) if els else 0
-            return Interp(sorted((k, self.values.get(cname, else_v))
-                                 for k, cname in cells.items()), else_v)
+        got = self.table(name)
+        if got is not None:
+            return Interp(sorted(got[0].items()), got[1])
         km = self.schema.keccak.get(name)
         if km is not None:
             return Interp(sorted(km.pairs.items()), 0)
         return None
+
+    def table(self, name: str):
+        """({key: value}, else value) of array or tabled function `name` in this model, or None:
+        its cells, then its reads -- each at its index term's value under the witness (one
+        device batch), where no cell holds that key (lower.py: the read took the cell's branch
+        there) -- over the else value (model.py:34-51 reads z3's FuncInterp the same way)."""
+        from .lower import READ_KINDS
+
+        sc = self.schema
+        cells = sc.cells.get(name)
+        if cells is None:
+            cells = sc.uf_cells.get(name)
+        cols = [c for c in sc.columns.values() if c.symbol == name]
+        els = [c for c in cols if c.kind in ("else", "ufelse")]
+        reads = sorted((c for c in cols if c.kind in READ_KINDS), key=lambda c: c.key)
+        if cells is None and not els and not reads:
+            return None
+        cells = cells or {}
+        else_v = self.values.get(els[0].name, 0) if els else 0
+        tab = {k: self.values.get(cname, else_v) for k, cname in cells.items()}
+        if reads:
+            at = self._evaluate([c.key for c in reads], [], True)
+            for c in reads:
+                k = int(at[c.key])
+                if k not in cells:
+                    tab.setdefault(k, self.values.get(c.name, 0))
+        return tab, else_v
 
     def _bool_symbol(self, name: str) -> bool:
         """A 1-bit column made by BoolSym (a Bool symbol: z3 gives True / False)."""

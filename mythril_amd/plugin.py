@@ -119,7 +119,8 @@ def witness_pins(raws, model, z3) -> list:
     * a scalar symbol (bit-vector or Bool constant): its column's value -- a symbol the witness
       has no column for is one the lowered query does not read, and gets 0 (model completion);
     * an array symbol: ``A == Store(...Store(K(dom, else), k1, v1)..., kn, vn)``, the z3 form of
-      the witness's table (its cells and else value, lower.py; model.Model.__getitem__);
+      the witness's table (its cells, its reads at their indices' values and its else value,
+      lower.py; model.Model.table);
     * every application of an uninterpreted function -- keccak256_N, its inverse keccak256_N-1,
       any other ``Function`` -- at the argument it has in the query: ``f(t) == v``, v the
       witness's value of that application (``Model.eval_many``: one device batch for all).
@@ -151,12 +152,11 @@ def witness_pins(raws, model, z3) -> list:
     for name, t in sorted(arrays.items()):
         srt = t.sort()
         dom, rng = srt.domain(), srt.range()
-        cells = model.schema.cells.get(name, {})
-        else_v = model.values.get("%s[*]" % name, 0)
+        got = model.table(name)
+        tab, else_v = got if got is not None else ({}, 0)
         a = z3.K(dom, z3.BitVecVal(else_v, rng.size()))
-        for key, cname in sorted(cells.items()):
-            a = z3.Store(a, z3.BitVecVal(key, dom.size()),
-                         z3.BitVecVal(model.values.get(cname, else_v), rng.size()))
+        for key, v in sorted(tab.items()):
+            a = z3.Store(a, z3.BitVecVal(key, dom.size()), z3.BitVecVal(v, rng.size()))
         pins.append(t == a)
     if apps:
         ordered = [apps[i] for i in sorted(apps)]

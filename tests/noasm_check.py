@@ -61,7 +61,7 @@ def main() -> int:
         s.close()
     assert w is not None, "no witness for KillBilly's query"
     names = [n for n, _ in sorted(qctx.b.var_index.items(), key=lambda kv: kv[1])]
-    vars_, arrays, funcs = model_of(w.schema, w.values)
+    vars_, arrays, funcs = model_of(w.schema, w.values, qctx.b)
     tape = qctx.b.finish(And(*cs).node)
     assert evaluate_term(tape.nodes, qctx.b.pool.values, names, qctx.b.symbols.array_names,
                          qctx.b.symbols.function_names, vars_, arrays, funcs)

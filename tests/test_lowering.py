@@ -22,8 +22,28 @@ from oracle.term_eval import evaluate_term
 from tests.laser_like import PART, queries
 
 
-def model_of(schema, row):
-    """The z3-style model a row of columns denotes (restated from lower.py's docstring)."""
+def read_index_values(b, schema, row):
+    """{read column: the value of its index term under the row} (the lowered index, evaluated
+    by the ORACLE over the row's columns)."""
+    from copy import deepcopy
+
+    from mythril_amd.lower import READ_KINDS, Lowering
+
+    reads = [c for c in schema.columns.values() if c.kind in READ_KINDS]
+    if not reads:
+        return {}
+    L = Lowering(b, deepcopy(schema))
+    lowered = {c.name: L.lower(c.key) for c in reads}
+    names = [n for n, _ in sorted(b.var_index.items(), key=lambda kv: kv[1])]
+    assign = [row.get(n, 0) for n in names]
+    return {n: int(E.evaluate(b.finish(li).nodes, b.pool.values, assign))
+            for n, li in lowered.items()}
+
+
+def model_of(schema, row, b=None):
+    """The z3-style model a row of columns denotes (restated from lower.py's docstring).  A
+    query with read columns (symbolic-index selects, function applications at symbolic
+    arguments) needs the builder `b`: the reads sit at their index terms' values."""
     cols = schema.columns
     vars_ = {c.name: row[c.name] for c in cols.values() if c.kind == "var"}
     arrays = {}
@@ -32,6 +52,20 @@ def model_of(schema, row):
     for arr, cells in schema.cells.items():
         tab = {k: row.get(n, 0) for k, n in cells.items()}
         arrays[arr] = (tab, row.get("%s[*]" % arr, 0))
+    uf_tabs = {}
+    for f, cells in schema.uf_cells.items():
+        uf_tabs[f] = ({k: row.get(n, 0) for k, n in cells.items()}, row.get("%s[*]" % f, 0))
+    reads = sorted((c for c in cols.values() if c.kind in ("read", "ufread")),
+                   key=lambda c: (c.symbol, c.key))
+    if reads:
+        assert b is not None, "a model with read columns needs the builder"
+        at = read_index_values(b, schema, row)
+        for c in reads:
+            tabs = arrays if c.kind == "read" else uf_tabs
+            tab, dflt = tabs.setdefault(c.symbol, ({}, row.get("%s[*]" % c.symbol, 0)))
+            cells = (schema.cells if c.kind == "read" else schema.uf_cells).get(c.symbol, {})
+            if at[c.name] not in cells:  # a cell holds its key (the read took that branch)
+                tab.setdefault(at[c.name], row.get(c.name, 0))
     funcs = {}
     for f, km in schema.keccak.items():
         inv = {}
@@ -49,9 +83,7 @@ def model_of(schema, row):
 
         funcs[f] = fwd
         funcs[f + "-1"] = (lambda y, inv=inv: inv.get(y, 0))
-    for f, cells in schema.uf_cells.items():
-        tab = {k: row.get(n, 0) for k, n in cells.items()}
-        dflt = row.get("%s[*]" % f, 0)
+    for f, (tab, dflt) in uf_tabs.items():
         funcs[f] = (lambda x, tab=tab, dflt=dflt: tab.get(x, dflt))
     return vars_, arrays, funcs
 
@@ -90,11 +122,16 @@ def test_lowered_tape_matches_term_semantics(qi):
             row = {c.name: candidate_values(ctx, c.width, rng) for c in schema.columns.values()}
         assign = [row.get(n, 0) for n in var_names]
         low = E.evaluate(tape.nodes, ctx.b.pool.values, assign)
-        vars_, arrays, funcs = model_of(schema, row)
+        vars_, arrays, funcs = model_of(schema, row, ctx.b)
         want = evaluate_term(orig.nodes, ctx.b.pool.values, var_names,
                              ctx.b.symbols.array_names, ctx.b.symbols.function_names,
                              vars_, arrays, funcs)
-        assert bool(low) == bool(want), (name, trial, row)
+        if any(c.kind in ("read", "ufread") for c in schema.columns.values()):
+            # read columns: only rows that keep the reads functional (the congruence conjuncts)
+            # denote a model, so a witness is a model (sound); other rows may be false
+            assert not low or want, (name, trial, row)
+        else:
+            assert bool(low) == bool(want), (name, trial, row)
         outcomes.append(bool(low))
     if name == "unsat_actor":
         assert not any(outcomes)
@@ -123,7 +160,7 @@ def test_calldata_cells_and_else_columns():
     assert kinds == {"var", "cell"}
 
 
-def test_symbolic_index_reads_else_and_cells():
+def test_symbolic_index_reads_cells_then_its_read_column():
     from mythril_amd import smt
     from mythril_amd.smt import Array, symbol_factory
 
@@ -133,9 +170,49 @@ def test_symbolic_index_reads_else_and_cells():
     c1 = a[symbol_factory.BitVecVal(3, 256)] == symbol_factory.BitVecVal(9, 256)
     c2 = a[i] == symbol_factory.BitVecVal(5, 256)
     tape, schema = ctx.query(c1, c2)
-    assert set(schema.columns) == {"A[0x3]", "A[*]", "i"}
+    assert set(schema.columns) == {"A[0x3]", "A[@%d]" % i.node, "i"}
+    assert schema.columns["A[@%d]" % i.node].kind == "read"
     ops = [Op(int(o)) for o in tape.nodes["op"]]
     assert Op.ITE in ops
+
+
+def test_unequal_reads_at_symbolic_indices():
+    """A[i] != A[j] had no row (both read one else column); with read columns
+    and the congruence conjunct Or(Not(i == j), A[@i] == A[@j]) it does, and every row the
+    lowered query accepts is a model of the original (the ORACLE decides, reads at their
+    indices' values); i == j rows with unequal reads are rejected."""
+    from mythril_amd import smt
+    from mythril_amd.smt import Array, Function, Not, symbol_factory
+
+    ctx = smt.set_context(smt.Context())
+    a = Array("A", 256, 256)
+    f = Function("f", 256, 256)
+    i, j = symbol_factory.BitVecSym("i", 256), symbol_factory.BitVecSym("j", 256)
+    cs = [Not(a[i] == a[j]), f(i + j) == symbol_factory.BitVecVal(7, 256),
+          Not(f(i) == f(j)), a[symbol_factory.BitVecVal(1, 256)] == a[i]]
+    root, schema = lower_query(ctx.b, [c.node for c in cs])
+    kinds = sorted(c.kind for c in schema.columns.values())
+    assert kinds.count("read") == 2 and kinds.count("ufread") == 3, kinds
+    tape = ctx.b.finish(root)
+    orig = ctx.b.finish(And(*cs).node)
+    names = [n for n, _ in sorted(ctx.b.var_index.items(), key=lambda kv: kv[1])]
+    rng = random.Random(3)
+    hits = 0
+    for trial in range(400):
+        row = {c.name: rng.choice((0, 1, 2, rng.getrandbits(8))) for c in schema.columns.values()}
+        row["f[@%d]" % (i + j).node] = 7
+        if trial % 4 == 0:
+            row["j"] = row["i"]
+        assign = [row.get(n, 0) for n in names]
+        low = E.evaluate(tape.nodes, ctx.b.pool.values, assign)
+        vars_, arrays, funcs = model_of(schema, row, ctx.b)
+        want = evaluate_term(orig.nodes, ctx.b.pool.values, names, ctx.b.symbols.array_names,
+                             ctx.b.symbols.function_names, vars_, arrays, funcs)
+        assert not low or want, (trial, row)
+        hits += bool(low)
+        if row["i"] == row["j"]:
+            assert not low
+    assert hits > 0
 
 
 def test_inverse_of_something_else_is_unsupported():

@@ -136,7 +136,7 @@ def laser_query():
 def oracle_value(ref, expr, m):
     b = ref.b
     names = [n for n, _ in sorted(b.var_index.items(), key=lambda kv: kv[1])]
-    vars_, arrays, funcs = model_of(m.schema, m.values)
+    vars_, arrays, funcs = model_of(m.schema, m.values, m.ctx.b)
     tape = b.finish(expr.node)
     return evaluate_term(tape.nodes, b.pool.values, names, b.symbols.array_names,
                          b.symbols.function_names, vars_, arrays, funcs)

@@ -28,7 +28,7 @@ from tests.test_lowering import model_of
 
 def holds_original(ctx, cs, schema, values) -> bool:
     names = [n for n, _ in sorted(ctx.b.var_index.items(), key=lambda kv: kv[1])]
-    vars_, arrays, funcs = model_of(schema, values)
+    vars_, arrays, funcs = model_of(schema, values, ctx.b)
     tape = ctx.b.finish(And(*cs).node)
     return bool(evaluate_term(tape.nodes, ctx.b.pool.values, names, ctx.b.symbols.array_names,
                               ctx.b.symbols.function_names, vars_, arrays, funcs))
