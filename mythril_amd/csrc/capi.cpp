@@ -306,7 +306,24 @@ bool is_gfx950(int dev) {
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
 
+// The compile worker thread (mh_tapes_compile_async) sets this: its own calls into the ctx do not
+// wait for themselves.
+thread_local bool t_compile_worker = false;
+
+// Every entry point that uses a ctx's state (device buffers, the compiled-tape cache, the staging
+// buffer, the pool, the stream) passes here: while the ctx's worker thread runs a compile, the
+// call waits for that compile to finish (its result stays for mh_tapes_compile_wait), so no two
+// threads touch the ctx at once.  The host-only harvest the caller overlaps with the
+// compile never enters a ctx.
+void settle(const mh_ctx* ctx) {
+    AsyncCompile* a = ctx->acomp;
+    if (!a || t_compile_worker) return;
+    std::unique_lock<std::mutex> lk(a->m);
+    a->cv.wait(lk, [&] { return !a->job || a->done; });
+}
+
 int32_t use_device(const mh_ctx* ctx) {
+    settle(ctx);
     MH_HIP(hipSetDevice(ctx->device));
     return MH_OK;
 }
@@ -549,6 +566,7 @@ int32_t mh_ctx_destroy(mh_ctx* ctx) {
 
 int32_t mh_ctx_clear_cache(mh_ctx* ctx) {
     if (!ctx) return set_err(MH_E_INVALID, "null ctx");
+    settle(ctx);
     ctx->compile_cache.clear();
     ctx->compile_cache_words = 0;
     return MH_OK;
@@ -581,6 +599,7 @@ int32_t mh_tapes_compile_async(mh_ctx* ctx, const mh_node* nodes, const uint64_t
         if (!ctx->acomp) {
             AsyncCompile* a = new AsyncCompile();
             a->th = std::thread([ctx, a] {
+                t_compile_worker = true;
                 std::unique_lock<std::mutex> lk(a->m);
                 for (;;) {
                     a->cv.wait(lk, [&] { return a->stop || (a->job && !a->done); });
@@ -651,6 +670,7 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
     if (!ctx || !out || (!nodes && n_tapes) || !tape_offsets || (!consts && n_consts))
         return set_err(MH_E_INVALID, "null argument");
     *out = nullptr;
+    settle(ctx);  // the compile cache, staging buffer and pool are the ctx's
     std::vector<uint32_t> words, dconsts;
     mh::ConstIndex dindex;
     std::vector<mh_dev_tape> heads(n_tapes);
@@ -885,6 +905,7 @@ int32_t mh_tapes_compile(mh_ctx* ctx, const mh_node* nodes, const uint64_t* tape
 
 int32_t mh_tapes_destroy(mh_tapeset* ts) {
     if (!ts) return MH_OK;
+    settle(ts->ctx);
     (void)hipSetDevice(ts->ctx->device);
     // kernels of this set may still run on the ctx stream: finish them before the blocks go back
     if (ts->ctx->stream) (void)hipStreamSynchronize(ts->ctx->stream);
@@ -943,6 +964,7 @@ int32_t mh_assign_create(mh_ctx* ctx, uint32_t n_vars, uint64_t capacity, mh_ass
 
 int32_t mh_assign_destroy(mh_assign* as) {
     if (!as) return MH_OK;
+    settle(as->ctx);
     (void)hipSetDevice(as->ctx->device);
     if (as->staged_pending) (void)hipEventSynchronize(as->staged);
     if (as->staged) (void)hipEventDestroy(as->staged);

@@ -1319,13 +1319,15 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
                           uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                           ConstIndex& dconst_index,
                           std::vector<uint32_t>& words, CompiledTape& out, std::string& err,
-                          bool hold_vars);
+                          bool hold_vars, bool sc);
 
 }  // namespace
 
 // A tape that runs out of registers is retried without held columns (Lowering::hold_vars), then
 // with cheap shared sub-terms duplicated at their uses, widening what counts as cheap (8, 32, 256
-// nodes) -- each size first with held columns, then without.
+// nodes) -- each size first with held columns, then without; and each of those first with the
+// short-circuit order (short_circuit), then, if that runs out of registers, in the order as
+// lowered, whose live ranges may fit where the reordered ones do not.
 // The attempt that fitted the last tape compiled on this thread is tried first: a LASER query's
 // tapes grow by one conjunct per query (svm.py:257-262), and a long path's tape needs the same
 // rematerialisation as its parent's, so the attempts that ran out of registers for the parent are
@@ -1337,16 +1339,16 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
     static thread_local int hint = 0;  // index into the attempt list of the last success
     const bool hold = n_vars > MH_MAX_PRELOAD && !std::getenv("MH_NO_HOLD_VARS");
     static const uint32_t kSizes[4] = {0u, 8u, 32u, 256u};
-    std::vector<int> order;
-    for (int a = 0; a < 8; ++a)
-        if (!((a & 1) == 0 && !hold)) order.push_back(a);  // a = 2 * size index + (no hold)
+    std::vector<int> order;  // a = 4 * size index + 2 * (no hold) + (no short circuit)
+    for (int a = 0; a < 16; ++a)
+        if (!((a & 2) == 0 && !hold)) order.push_back(a);
     auto it = std::find(order.begin(), order.end(), hint);
     if (it != order.end()) std::rotate(order.begin(), it, it + 1);  // the hint first, then in order
     int32_t r = MH_E_UNSUPPORTED;
     const size_t words0 = words.size(), dconsts0 = dconsts.size();
     for (int a : order) {
-        const uint32_t sz = kSizes[a >> 1];
-        const bool h = (a & 1) == 0;
+        const uint32_t sz = kSizes[a >> 2];
+        const bool h = (a & 2) == 0, sc = (a & 1) == 0;
         std::vector<mh_node> t2;
         if (sz) t2 = rematerialize(nodes, n_nodes, sz);
         const mh_node* tn = sz ? t2.data() : nodes;
@@ -1359,7 +1361,7 @@ int32_t compile_tape(const mh_node* nodes, size_t n_nodes, const uint32_t* const
                 i = i->second >= dconsts0 / 8 ? dconst_index.erase(i) : std::next(i);
         }
         r = compile_tape_once(tn, nn, consts, n_consts, n_vars, dconsts, dconst_index, words, out,
-                              err, h);
+                              err, h, sc);
         out.n_nodes = (uint32_t)n_nodes;
         if (r != MH_E_UNSUPPORTED || err.find("register pressure") == std::string::npos) {
             if (r == MH_OK) hint = a;
@@ -1454,14 +1456,14 @@ int32_t compile_tape_once(const mh_node* nodes, size_t n_nodes, const uint32_t* 
                           uint32_t n_consts, uint32_t n_vars, std::vector<uint32_t>& dconsts,
                           ConstIndex& dconst_index,
                           std::vector<uint32_t>& words, CompiledTape& out, std::string& err,
-                          bool hold_vars) {
+                          bool hold_vars, bool sc) {
     SsaTape st;
     if (int32_t r = lower_tape_ssa(nodes, n_nodes, consts, n_consts, n_vars, dconsts,
                                    dconst_index, st, err, 0, false, hold_vars))
         return r;
     out.alg_ops = st.alg_ops;
     out.n_nodes = (uint32_t)n_nodes;
-    short_circuit(st);
+    if (sc) short_circuit(st);
     std::vector<VInsn>& code = st.code;
     const int n_pinned = st.n_pinned;
     int root_v = st.root;

@@ -469,11 +469,34 @@ public:
         std::vector<int64_t> st;
         for (uint32_t r : roots) {
             if (!(nd(r).flags & F_HOST)) continue;
+            polarity(r);
             T.seen.reset(T.nodes.size());
             st.assign(1, r);
             walk_host(st);
         }
         finish_harvest();
+    }
+    // lower.py _polarity: the host-only comparisons / equalities reached from the root through
+    // AND / OR / NOT only, 1 positive | 2 negative (NOT flips); absent = positive
+    std::unordered_map<uint32_t, uint8_t> pol;
+    void polarity(uint32_t r) {
+        pol.clear();
+        std::vector<std::pair<uint32_t, uint8_t>> st{{r, 0}};
+        std::unordered_set<uint64_t> vis;
+        while (!st.empty()) {
+            const auto [n, neg] = st.back();
+            st.pop_back();
+            if (!vis.insert((uint64_t)n << 1 | neg).second) continue;
+            const mh_node& x = nd(n);
+            if (x.op == AND || x.op == MH_OP_OR) {
+                for (uint32_t k : {x.a, x.b})
+                    if (nd(k).flags & F_HOST) st.push_back({k, neg});
+            } else if (x.op == MH_OP_NOT) {
+                if (nd(x.a).flags & F_HOST) st.push_back({x.a, (uint8_t)(neg ^ 1)});
+            } else {
+                pol[n] |= neg ? 2 : 1;
+            }
+        }
     }
     void walk_host(std::vector<int64_t>& st) {
         while (!st.empty()) {
@@ -530,6 +553,17 @@ public:
                 if (const Big* k = const_value(x.a)) keys.push_back(*k);
             }
         } else if (x.op == EQ || (x.op >= BVULT && x.op <= BVSGE)) {
+            uint8_t op = x.op;
+            auto pi = pol.find(n);
+            if (pi != pol.end() && pi->second == 2) {
+                // reached only under an odd number of NOTs: the negated comparison (ADVICE r5:
+                // Not(UGT(f(x), c)) is an upper bound); a disequality states no pair
+                if (op == EQ) return;
+                static const uint8_t neg_of[8] = {MH_OP_BVUGE, MH_OP_BVUGT, MH_OP_BVULE,
+                                                  MH_OP_BVULT, MH_OP_BVSGE, MH_OP_BVSGT,
+                                                  MH_OP_BVSLE, MH_OP_BVSLT};
+                op = neg_of[op - BVULT];
+            }
             const uint32_t sides[2][2] = {{x.a, x.b}, {x.b, x.a}};
             for (const auto& s : sides) {
                 const mh_node& app = nd(s[0]);
@@ -547,12 +581,12 @@ public:
                 // bound nothing here (lower.py Lowering.collect)
                 const bool left = &s == &sides[0];
                 bool lower = false, strict = false;
-                if (left && (x.op == MH_OP_BVUGT || x.op == MH_OP_BVUGE)) {
+                if (left && (op == MH_OP_BVUGT || op == MH_OP_BVUGE)) {
                     lower = true;
-                    strict = x.op == MH_OP_BVUGT;
-                } else if (!left && (x.op == BVULT || x.op == MH_OP_BVULE)) {
+                    strict = op == MH_OP_BVUGT;
+                } else if (!left && (op == BVULT || op == MH_OP_BVULE)) {
                     lower = true;
-                    strict = x.op == BVULT;
+                    strict = op == BVULT;
                 }
                 if (!lower) continue;
                 const Big lb = strict ? hv.plus(1) : hv;

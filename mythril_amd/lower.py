@@ -216,6 +216,34 @@ def _walk(b: TapeBuilder, roots: Iterable[int], host_only: bool = False) -> List
     return order
 
 
+_NEGATED = {Op.BVULT: Op.BVUGE, Op.BVULE: Op.BVUGT, Op.BVUGT: Op.BVULE, Op.BVUGE: Op.BVULT,
+            Op.BVSLT: Op.BVSGE, Op.BVSLE: Op.BVSGT, Op.BVSGT: Op.BVSLE, Op.BVSGE: Op.BVSLT}
+
+
+def _polarity(b: TapeBuilder, root: int) -> Dict[int, int]:
+    """{node: 1 positive | 2 negative} of the host-only comparisons and equalities reached from
+    Bool constraint `root` through AND / OR / NOT only (NOT flips); a node not in the map is
+    read as positive (csrc/query.cpp polarity)."""
+    nodes, fl = b.nodes, b.flags
+    pol: Dict[int, int] = {}
+    seen = set()
+    st = [(root, 0)] if fl[root] & F_HOST else []
+    while st:
+        n, neg = st.pop()
+        if (n, neg) in seen:
+            continue
+        seen.add((n, neg))
+        op, _, a, bb = nodes[n][:4]
+        if op in (Op.AND, Op.OR):
+            st += [(x, neg) for x in (a, bb) if fl[x] & F_HOST]
+        elif op == Op.NOT:
+            if fl[a] & F_HOST:
+                st.append((a, neg ^ 1))
+        else:
+            pol[n] = pol.get(n, 0) | (2 if neg else 1)
+    return pol
+
+
 def _arity(op: int) -> int:
     return ARITY[op]  # Op is an IntEnum: the int keys the table directly
 
@@ -249,12 +277,27 @@ class Lowering:
         self.apply_harvest(self.collect(roots))
 
     def collect(self, roots: Sequence[int]) -> "Harvest":
-        """The constant keys, keccak pairs and keccak bounds the terms under `roots` state."""
+        """The constant keys, keccak pairs and keccak bounds the terms under `roots` state (root
+        by root, as the native compiler harvests)."""
+        h = Harvest()
+        for r in roots:
+            h.merge(self._collect_one(r))
+        return h
+
+    def _collect_one(self, root: int) -> "Harvest":
         b = self.b
         h = Harvest()
+        pol = _polarity(b, root)
         # keys, keccak pairs and bounds all sit on host-only terms or their parents
-        for n in _walk(b, roots, host_only=True):
+        for n in _walk(b, [root], host_only=True):
             op, w, a, bb, c, i0, i1 = b.nodes[n]
+            if (op == Op.EQ or op in ORDERED) and pol.get(n, 1) == 2:
+                # reached only under an odd number of NOTs: the negated comparison states
+                # (ADVICE r5: Not(UGT(f(x), c)) is an upper bound, not a lower one) -- a
+                # disequality states no pair
+                if op == Op.EQ:
+                    continue
+                op = _NEGATED[op]
             if op == Op.SELECT:
                 base = self._array_base(a)
                 if base is not None:

@@ -860,6 +860,14 @@ class PendingCompile:
         return CompiledTapes(self.ctx, self.tapeset, _handle=h,
                              _timing=(self.flatten_s, secs.value))
 
+    def __del__(self):  # dropped without wait(): collect the compile (the worker still reads the
+        # input arrays this object holds) and free its tapes
+        if getattr(self, "args", None) is not None and getattr(self.ctx, "h", None):
+            try:
+                self.wait().close()
+            except Exception:  # noqa: BLE001 - interpreter shutdown, a failed compile
+                pass
+
 
 class CompiledTapes:
     """mh_tapeset: tapes lowered to device code, resident in HBM."""

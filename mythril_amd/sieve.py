@@ -728,11 +728,11 @@ class Sieve:
         columns, widths, schema, root_nodes, ts, group_cols, defs = host
         t_t = time.perf_counter()
         pending = None
-        if self.overlap and hasattr(self.ctx, "compile_async"):
-            pending = self.ctx.compile_async(ts)
-        col_index = {c: i for i, c in enumerate(columns)}
-        parent = self.witnesses.get(key[:-1]) if key else None
-        try:
+        try:  # from the compile's start: an error on this side still collects it
+            if self.overlap and hasattr(self.ctx, "compile_async"):
+                pending = self.ctx.compile_async(ts)
+            col_index = {c: i for i, c in enumerate(columns)}
+            parent = self.witnesses.get(key[:-1]) if key else None
             guide = native.harvest_guide(
                 root_nodes, ts.pool.to_array(), widths,
                 [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else (),

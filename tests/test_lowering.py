@@ -283,3 +283,44 @@ def test_finish_cache_is_bounded_by_nodes(monkeypatch):
     for c, (_, want) in zip(cs2[1:], tapes):
         acc2 = ctx2.b.op(Op.AND, acc2, c.node)
     assert ctx2.b.finish(acc2).nodes.tobytes() == tapes[-1][1]
+
+
+def test_negated_keccak_compare_is_not_a_lower_bound():
+    """Not(UGT(keccak(x), c)) -- a JUMPI's other branch over a hash -- states
+    keccak(x) <= c, an upper bound; the harvest used to read it as the lower bound c + 1, which
+    put the interval base above c so no row could satisfy it.  The base is the manager's lower
+    bound again (both harvesters: tests/test_query_native.py runs the same shapes natively), and
+    the lowered query has rows that are models of the original."""
+    from mythril_amd import smt
+    from mythril_amd.lower import keccak_base
+    from mythril_amd.smt import Not, UGT, symbol_factory
+    from tests.laser_like import KeccakManager
+
+    ctx = smt.set_context(smt.Context())
+    km = KeccakManager()
+    x = symbol_factory.BitVecSym("x", 256)
+    h, cond = km.create(x)
+    lo = km.hooks[256] * PART
+    c = symbol_factory.BitVecVal(lo + (1 << 124), 256)
+    cs = [cond, Not(UGT(h, c))]
+    root, schema = lower_query(ctx.b, [q.node for q in cs])
+    assert schema.keccak["keccak256_256"].base == keccak_base(lo)
+    from mythril_amd import native
+
+    cq = native.TermMirror.of(ctx.b).build(ctx.b, [q.node for q in cs])
+    kt = [items for k, n, items in cq.tables if k == native.TABLE_KECCAK]
+    assert kt and kt[0][0] == keccak_base(lo)
+    tape = ctx.b.finish(root)
+    orig = ctx.b.finish(And(*cs).node)
+    names = [n for n, _ in sorted(ctx.b.var_index.items(), key=lambda kv: kv[1])]
+    hits = 0
+    for v in range(64):
+        row = {"x": v}
+        assign = [row.get(n, 0) for n in names]
+        low = E.evaluate(tape.nodes, ctx.b.pool.values, assign)
+        vars_, arrays, funcs = model_of(schema, row, ctx.b)
+        want = evaluate_term(orig.nodes, ctx.b.pool.values, names, ctx.b.symbols.array_names,
+                             ctx.b.symbols.function_names, vars_, arrays, funcs)
+        assert bool(low) == bool(want)
+        hits += bool(low)
+    assert hits == 64
