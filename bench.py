@@ -175,30 +175,13 @@ def main() -> None:
     assign.generate(seed, index_base)
     fh = torch.empty(n_tapes, dtype=torch.int64, device=dev)
     hc = torch.empty(n_tapes, dtype=torch.int64, device=dev)
-    exchange = None
+    exchange, exchange_fallback = None, []
     if world > 1:
-        # the library's own RCCL communicator (mh_comm_init): rank 0's id reaches the others
-        # through torch.distributed; the per-step exchange then never leaves the C-ABI.  If any
-        # rank cannot open it, every rank uses torch.distributed's RCCL for the same MIN / SUM
-        # (shard.allreduce_results) instead.
-        box = [None]
-        if rank == 0:
-            try:
-                box = [native.comm_unique_id()]
-            except Exception as e:  # pragma: no cover - depends on the node's RCCL
-                log("[rank 0] mh_comm_unique_id failed: %s" % e)
-        dist.broadcast_object_list(box, src=0)
-        ok = 0
-        if box[0] is not None:
-            try:
-                ctx.comm_init(box[0], rank, world)
-                ok = 1
-            except Exception as e:  # pragma: no cover
-                log("[rank %d] mh_comm_init failed: %s" % (rank, e))
-        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        exchange = "library" if int(flag.item()) == 1 else "torch"
-        log("[rank %d] result exchange: %s" % (rank, exchange))
+        # the library's own RCCL communicator (mh_comm_init); if any rank cannot open it, every
+        # rank uses torch.distributed's RCCL for the same MIN / SUM, and the JSON line names why
+        exchange, exchange_fallback = shard.setup_exchange(ctx, rank, world, dev)
+        log("[rank %d] result exchange: %s%s" % (rank, exchange, "".join(
+            "\n  fallback: " + r for r in exchange_fallback)))
     torch.cuda.synchronize(dev)
     log("[rank %d] setup %.1fs: %d tapes, %d insns, %d rows, SURVEY op-table %.0f per row"
         % (rank, time.time() - t0, n_tapes, sum(i["n_insns"] for i in info), rows,
@@ -353,6 +336,8 @@ def main() -> None:
             "parallelism": "dp%d (row shards, all-reduce of per-tape results%s)"
                            % (world, "" if exchange is None else ", %s RCCL" % exchange),
         },
+        "exchange": exchange,
+        "exchange_fallback": "; ".join(exchange_fallback) or None,
         "per_gpu": value / world,
         "kernel_ms": kms,
         "tapes_with_witness": hits,

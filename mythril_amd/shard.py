@@ -44,3 +44,42 @@ def allreduce_results(first_hit, hit_count, group=None) -> None:
     dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
     dist.all_reduce(hit_count, op=dist.ReduceOp.SUM, group=group)
     first_hit.copy_(torch.where(f == INT64_MAX, torch.full_like(f, -1), f))
+
+
+def setup_exchange(ctx, rank: int, world: int, device=None):
+    """The per-step result exchange of a multi-rank sweep (bench.py): the library's own RCCL
+    communicator (``mh_comm_init``: rank 0's unique id reaches the others through
+    torch.distributed) when every rank can open it, else torch.distributed's all-reduce of the
+    same MIN / SUM (allreduce_results).  Returns (exchange, reasons): "library" or "torch", and
+    on the torch fallback the failure message of every rank that could not open the
+    communicator ("rank r: ..."), gathered to every rank -- bench.py puts them in its JSON line
+    (``exchange_fallback``), so a scaling number taken on the fallback says so.  `ctx` needs
+    ``comm_init(uid, rank, world)``; the unique id comes from ``native.comm_unique_id``."""
+    import torch
+    import torch.distributed as dist
+
+    from . import native
+
+    box, why = [None], None
+    if rank == 0:
+        try:
+            box = [native.comm_unique_id()]
+        except Exception as e:  # noqa: BLE001 - depends on the node's RCCL
+            why = "rank 0: mh_comm_unique_id: %s" % e
+    dist.broadcast_object_list(box, src=0)
+    if box[0] is not None:
+        try:
+            ctx.comm_init(box[0], rank, world)
+        except Exception as e:  # noqa: BLE001
+            why = "rank %d: mh_comm_init: %s" % (rank, e)
+    elif why is None:
+        why = "rank %d: no communicator id from rank 0" % rank
+    reasons = [None] * world
+    dist.all_gather_object(reasons, why)
+    failed = [r for r in reasons if r]
+    flag = torch.tensor([0 if failed else 1], dtype=torch.int32,
+                        device=device if device is not None else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return "library", []
+    return "torch", failed

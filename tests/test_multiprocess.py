@@ -130,3 +130,55 @@ def test_strong_shard_range_partitions_the_rows():
             assert max(n for _, n in parts) - min(n for _, n in parts) <= 1
     with pytest.raises(ValueError):
         shard.strong_shard_range(2, 2, 10)
+
+
+class _CommCtx:
+    """A ctx whose mh_comm_init fails on the ranks in `fail` (the library cannot open RCCL)."""
+
+    def __init__(self, rank, fail):
+        self.rank, self.fail, self.calls = rank, fail, []
+
+    def comm_init(self, uid, rank, world):
+        self.calls.append((uid, rank, world))
+        if rank in self.fail:
+            raise RuntimeError("ncclCommInitRank: unhandled system error (stand-in)")
+
+
+def _exchange_worker(rank, world, port, out, fail):
+    import torch.distributed as dist
+
+    from mythril_amd import native
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        native.comm_unique_id = lambda: b"uid-from-rank-0"  # rank 0 only asks
+        ctx = _CommCtx(rank, fail)
+        exchange, why = shard.setup_exchange(ctx, rank, world)
+        out[rank] = (exchange, why, ctx.calls)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", [(), (1,), (0, 1)])
+def test_exchange_fallback_is_reported(fail):
+    """bench.py's result exchange (shard.setup_exchange, world 2 over gloo):
+    every rank gets rank 0's communicator id; if any rank's mh_comm_init fails, EVERY rank falls
+    back to torch.distributed's all-reduce and every rank holds the reason of each failing rank
+    -- bench.py prints them in the JSON line (``exchange_fallback``), not only on stderr."""
+    world = 2
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_exchange_worker, args=(world, port, out, fail), nprocs=world, join=True)
+        res = dict(out)
+    for r in range(world):
+        exchange, why, calls = res[r]
+        assert calls == [(b"uid-from-rank-0", r, world)]
+        if fail:
+            assert exchange == "torch"
+            assert [w.split(":")[0] for w in why] == ["rank %d" % f for f in fail]
+            assert all("ncclCommInitRank" in w for w in why)
+        else:
+            assert exchange == "library" and why == []
