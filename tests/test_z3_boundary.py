@@ -368,3 +368,34 @@ def test_unusable_device_is_probed_once(monkeypatch):
         assert len(made) == 2
     finally:
         frontend.reset()
+
+
+def test_verifier_pins_reads_on_planted_random_paths(monkeypatch):
+    """The random planted family (free and K arrays, stores, selects at symbolic indices, a
+    tabled function at symbolic arguments, keccak with pairs and bounds): every witness the sieve
+    returns through get_model passes the fully determined check -- the arrays pinned as
+    Store chains holding the cells and the reads at their indices' values, every application
+    pinned -- and no symbol is left free."""
+    from tests import z3_ast
+    from tests.planted import planted_path
+
+    z3, seen, fallback = _verifier_world(monkeypatch)
+    rejected0 = SolverStatistics().sieve_rejected
+    try:
+        hits = 0
+        for seed in range(4):
+            ctx, cs, _, _ = planted_path("random", seed, 10)
+            for k in range(1, len(cs) + 1):
+                frontend.get_model.cache_clear()
+                before = len(seen)
+                m = frontend.get_model(tuple(z3_ast.Ref(c) for c in cs[:k]))
+                if m == "fallback":
+                    continue
+                hits += 1
+                assert len(seen) == before + 1
+                (s,) = [x for x in z3.solvers[-3:] if "timeout" in x.params][-1:]
+                assert s.free == [], (seed, k, s.free)
+        assert hits >= 8, hits
+        assert SolverStatistics().sieve_rejected == rejected0
+    finally:
+        frontend.reset()
