@@ -63,12 +63,13 @@ class Column:
 
     name: str             # VAR name in the tape set
     width: int
-    kind: str             # "var" | "cell" | "else" | "ufcell" | "ufelse" | "read" | "ufread"
+    kind: str             # "var" | "cell" | "else" | "ufcell" | "ufelse" | "read" | "ufread" |
+                          # "kread"
     symbol: str           # variable / array / function name
     key: Optional[int] = None  # cells: the constant key; reads: the index term's node
 
 
-READ_KINDS = ("read", "ufread")
+READ_KINDS = ("read", "ufread", "kread")
 
 
 def read_name(sym: str, index_node: int) -> str:
@@ -91,6 +92,8 @@ class Schema:
     uf_cells: Dict[str, Dict[int, str]] = field(default_factory=dict)
     keccak: Dict[str, KeccakMap] = field(default_factory=dict)
     columns: Dict[str, Column] = field(default_factory=dict)         # column name -> Column
+    # keccak applications as read columns (the second-chance lowering, Lowering keccak_reads)
+    keccak_reads: bool = False
 
 
 @dataclass
@@ -255,10 +258,12 @@ class Lowering:
     the schema read the else column, i.e. the value the model gives every other key — the
     behaviour ``Model.eval`` needs (mythril/laser/smt/model.py:45-59)."""
 
-    def __init__(self, b: TapeBuilder, frozen: Optional[Schema] = None):
+    def __init__(self, b: TapeBuilder, frozen: Optional[Schema] = None,
+                 keccak_reads: bool = False):
         self.b = b
         self.frozen = frozen is not None
-        self.schema = frozen if frozen is not None else Schema()
+        self.schema = frozen if frozen is not None else Schema(keccak_reads=keccak_reads)
+        self.keccak_reads = self.schema.keccak_reads
         self.memo: Dict[int, int] = {}
         self.sym = b.symbols
         # read column -> its lowered index term (the congruence conjuncts compare those)
@@ -497,6 +502,34 @@ class Lowering:
         args += [0] * (3 - k)
         return b._add(op, w, args[0], args[1], args[2], i0, i1)
 
+    def _keccak_read(self, fname: str, km: "KeccakMap", x: int, a_orig: int) -> int:
+        """The second-chance form of a keccak application (keccak_reads): the stated pairs'
+        ite chain over a read column of its own, ``ite(x == c_i, k_i, f[@a])`` -- free, kept a
+        function and injective by the conjuncts of ``congruence`` -- instead of the fixed
+        H(x).  With a frozen schema (Model.eval) a term the query did not apply f to reads the
+        reads at equal arguments, else H(x)."""
+        b = self.b
+        rname = read_name(fname, a_orig)
+        if not self.frozen:
+            acc = self._column(rname, 256, "kread", fname, a_orig)
+            self.read_index.setdefault(rname, x)
+        elif rname in self.schema.columns:
+            acc = self._column(rname, 256, "kread", fname, a_orig)
+        else:
+            h = b.op(Op.KECCAK, x)
+            h = b.op(Op.BVLSHR, h, b.const(KECCAK_SHIFT, 256))
+            h = b.op(Op.BVSHL, h, b.const(KECCAK_ALIGN, 256))
+            acc = b.op(Op.BVADD, h, b.const(km.base, 256)) if km.base else h
+            reads = sorted((c for c in self.schema.columns.values()
+                            if c.kind == "kread" and c.symbol == fname), key=lambda c: c.key)
+            for c in reversed(reads):
+                acc = b.op(Op.ITE, self.eq(x, self.lower(c.key)),
+                           self._column(c.name, 256, "kread", fname, c.key), acc)
+        for arg in sorted(km.pairs, reverse=True):
+            acc = b.op(Op.ITE, self.eq(x, b.const(arg, b.widths[x])),
+                       b.const(km.pairs[arg], 256), acc)
+        return acc
+
     # -- wide equalities: the device compares at most 256 bits ---------------------------------
     def _pieces(self, n: int) -> List[int]:
         """Leaves of the CONCAT tree of n, most significant first (ZEXT = zeros ++ x)."""
@@ -628,6 +661,10 @@ class Lowering:
                 if not self.frozen:
                     raise LoweringUnsupported("keccak function %s not harvested" % fname)
                 km = KeccakMap(0)
+            if w != 256:
+                raise LoweringUnsupported("keccak function %s has range %d" % (fname, w))
+            if self.keccak_reads:
+                return self._keccak_read(fname, km, x, a)
             h = b.op(Op.KECCAK, x)
             h = b.op(Op.BVLSHR, h, b.const(KECCAK_SHIFT, 256))
             h = b.op(Op.BVSHL, h, b.const(KECCAK_ALIGN, 256))
@@ -650,7 +687,9 @@ def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) ->
     read column the lowered constraint `x` reads first in its query (directly or in the index
     term of a read it reads) -- ordered by (symbol, index term) -- and every read of the same
     symbol before it (`reads`, in the order the query introduced them; updated here),
-    ``Or(Not(i == j), A[@i] == A[@j])``.  The native query
+    ``Or(Not(i == j), A[@i] == A[@j])``; keccak reads (the second-chance lowering) are also
+    injective: ``(i == j) == (f[@i] == f[@j])``, and ``Or(i == c, Not(f[@i] == k))`` for every
+    stated pair (c, k) -- the lowering maps ``f-1(f(x))`` to ``x``.  The native query
     compiler makes the same conjuncts in the same order (csrc/query.cpp congruence)."""
     names = var_names(b)
     found, work = {}, [x]
@@ -665,31 +704,44 @@ def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) ->
                  key=lambda c: (c.symbol, c.key))
     out = []
     for p in new:
+        rp = b.var(p.name, p.width)
         for q in reads:
             if q.symbol == p.symbol and q.kind == p.kind:
                 same = L.eq(L.read_index[q.name], L.read_index[p.name])
-                out.append(b.op(Op.OR, b.op(Op.NOT, same),
-                                b.op(Op.EQ, b.var(q.name, q.width), b.var(p.name, p.width))))
+                eqv = b.op(Op.EQ, b.var(q.name, q.width), rp)
+                if p.kind == "kread":  # a function and injective: (i == j) == (f_i == f_j)
+                    out.append(b.op(Op.EQ, same, eqv))
+                else:
+                    out.append(b.op(Op.OR, b.op(Op.NOT, same), eqv))
+        if p.kind == "kread":  # injective against the stated pairs too (the inverse reads them)
+            km = L.schema.keccak[p.symbol]
+            li = L.read_index[p.name]
+            for arg in sorted(km.pairs):
+                out.append(b.op(Op.OR, L.eq(li, b.const(arg, b.widths[li])),
+                                b.op(Op.NOT, b.op(Op.EQ, rp, b.const(km.pairs[arg], 256)))))
         reads.append(p)
         seen.add(p.name)
     return out
 
 
 def lower_query(b: TapeBuilder, roots: Sequence[int],
-                frozen: Optional[Schema] = None, _fresh_prefix: bool = False
-                ) -> Tuple[int, Schema]:
+                frozen: Optional[Schema] = None, _fresh_prefix: bool = False,
+                keccak_reads: bool = False) -> Tuple[int, Schema]:
     """Lower the conjunction of Bool `roots`: (root node of the column-only term, schema).
 
     Without ``frozen`` both passes are memoised on the builder: pass 1 per constraint
     (``Harvest``), pass 2 per harvest fingerprint (the rewrite of a node depends on nothing
     else), so a LASER query that adds one constraint to its parent's (svm.py:257-262) lowers only
-    that constraint.  The schema's columns are the ones the lowered term reads, in VAR order."""
+    that constraint.  The schema's columns are the ones the lowered term reads, in VAR order.
+    ``keccak_reads``: keccak applications as read columns (Lowering._keccak_read; the sieve's
+    second chance for a query its first lowering missed)."""
     if frozen is not None:
         L = Lowering(b, frozen)
         low = [L.lower(r) for r in roots]
         schema = L.schema
-    elif not _fresh_prefix and len(roots) > 1 and _prefix_state(b, roots) is not None:
-        return _lower_extend(b, roots)
+    elif not _fresh_prefix and len(roots) > 1 and \
+            _prefix_state(b, roots, keccak_reads) is not None:
+        return _lower_extend(b, roots, keccak_reads)
     else:
         per_root: Dict[int, Harvest] = _memo(b, "_harvest_of")
         h = Harvest()
@@ -700,14 +752,14 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
             h.merge(got)
         fp = h.fingerprint()
         lows = b.__dict__.setdefault("_lowerings", OrderedDict())
-        L = lows.get(fp)
+        L = lows.get((fp, keccak_reads))
         if L is None:
-            L = lows[fp] = Lowering(b)
+            L = lows[(fp, keccak_reads)] = Lowering(b, keccak_reads=keccak_reads)
             L.apply_harvest(h)
             if len(lows) > MAX_LOWERINGS:
                 lows.popitem(last=False)
         else:
-            lows.move_to_end(fp)
+            lows.move_to_end((fp, keccak_reads))
         low, reads, seen = [], [], set()
         for r in roots:
             x = L.lower(r)
@@ -725,7 +777,7 @@ def lower_query(b: TapeBuilder, roots: Sequence[int],
     for x in low[1:]:
         acc = b.op(Op.AND, acc, x)
     if frozen is None:
-        _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen)
+        _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen, keccak_reads)
     return acc, schema
 
 
@@ -745,25 +797,26 @@ class _Prefix:
     seen: set = field(default_factory=set)
 
 
-def _prefix_state(b: TapeBuilder, roots: Sequence[int]) -> Optional[_Prefix]:
+def _prefix_state(b: TapeBuilder, roots: Sequence[int], kr: bool = False) -> Optional[_Prefix]:
     cache = b.__dict__.get("_lower_prefixes")
-    return None if cache is None else cache.get(tuple(roots[:-1]))
+    return None if cache is None else cache.get((kr, tuple(roots[:-1])))
 
 
-def _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen) -> None:
+def _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen, kr=False) -> None:
     cache = b.__dict__.setdefault("_lower_prefixes", OrderedDict())
-    cache[tuple(roots)] = _Prefix(h, fp, L, list(low), used, acc, list(reads), set(seen))
+    cache[(kr, tuple(roots))] = _Prefix(h, fp, L, list(low), used, acc, list(reads), set(seen))
     while len(cache) > PREFIX_STATES:
         cache.popitem(last=False)
 
 
-def _lower_extend(b: TapeBuilder, roots: Sequence[int]) -> Tuple[int, "Schema"]:
+def _lower_extend(b: TapeBuilder, roots: Sequence[int], kr: bool = False
+                  ) -> Tuple[int, "Schema"]:
     """lower_query of `roots` from the lowered state of ``roots[:-1]`` (svm.py:257-262: every new
     state's query is its parent's plus one constraint): the new constraint's harvest is merged
     into the parent's; an unchanged fingerprint keeps the parent's lowering and its lowered
     conjuncts, so only the new constraint is lowered and ANDed on.  The result is lower_query's
     from scratch (tests/test_lowering.py compares them)."""
-    par = _prefix_state(b, roots)
+    par = _prefix_state(b, roots, kr)
     new = roots[-1]
     per_root: Dict[int, Harvest] = _memo(b, "_harvest_of")
     hn = per_root.get(new)
@@ -775,7 +828,7 @@ def _lower_extend(b: TapeBuilder, roots: Sequence[int]) -> Tuple[int, "Schema"]:
     h.merge(hn)
     fp = h.fingerprint()
     if fp != par.fp:  # new keys / keccak pairs: every constraint's rewrite may change
-        return lower_query(b, list(roots[:-1]) + [new], _fresh_prefix=True)
+        return lower_query(b, list(roots[:-1]) + [new], _fresh_prefix=True, keccak_reads=kr)
     L = par.lowering
     x = L.lower(new)
     if b.widths[x] != BOOL:
@@ -788,7 +841,7 @@ def _lower_extend(b: TapeBuilder, roots: Sequence[int]) -> Tuple[int, "Schema"]:
     for y in added:
         used = used | node_columns(b, [y])[y]
         acc = b._add(Op.AND, BOOL, acc, y)
-    _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen)
+    _remember_prefix(b, roots, h, fp, L, low, used, acc, reads, seen, kr)
     return acc, _schema_of(b, L, used)
 
 
@@ -811,4 +864,4 @@ def _schema_of(b: TapeBuilder, L: "Lowering", used: frozenset) -> "Schema":
             # compiler refuses the same, csrc/query.cpp QueryState::emit)
             raise LoweringUnsupported("variable %s is named like an array cell" % name)
         cols[name] = col
-    return Schema(full.cells, full.uf_cells, full.keccak, cols)
+    return Schema(full.cells, full.uf_cells, full.keccak, cols, full.keccak_reads)

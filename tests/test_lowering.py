@@ -55,12 +55,18 @@ def model_of(schema, row, b=None):
     uf_tabs = {}
     for f, cells in schema.uf_cells.items():
         uf_tabs[f] = ({k: row.get(n, 0) for k, n in cells.items()}, row.get("%s[*]" % f, 0))
-    reads = sorted((c for c in cols.values() if c.kind in ("read", "ufread")),
+    reads = sorted((c for c in cols.values() if c.kind in ("read", "ufread", "kread")),
                    key=lambda c: (c.symbol, c.key))
+    kread_pts = {}
     if reads:
         assert b is not None, "a model with read columns needs the builder"
         at = read_index_values(b, schema, row)
         for c in reads:
+            if c.kind == "kread":  # keccak reads (second-chance lowering): f at the argument
+                pairs = schema.keccak[c.symbol].pairs
+                if at[c.name] not in pairs:
+                    kread_pts.setdefault(c.symbol, {}).setdefault(at[c.name], row.get(c.name, 0))
+                continue
             tabs = arrays if c.kind == "read" else uf_tabs
             tab, dflt = tabs.setdefault(c.symbol, ({}, row.get("%s[*]" % c.symbol, 0)))
             cells = (schema.cells if c.kind == "read" else schema.uf_cells).get(c.symbol, {})
@@ -72,9 +78,12 @@ def model_of(schema, row, b=None):
 
         # the argument width is bound per function (a late-bound closure variable would give
         # every keccak function the last one's width)
-        def fwd(x, km=km, inv=inv, nbytes=int(f.split("_")[1]) // 8):
+        def fwd(x, km=km, inv=inv, nbytes=int(f.split("_")[1]) // 8,
+                pts=kread_pts.get(f, {})):
             if x in km.pairs:
                 y = km.pairs[x]
+            elif x in pts:
+                y = pts[x]
             else:
                 h = int.from_bytes(keccak256(x.to_bytes(nbytes, "big")), "big")
                 y = (km.base + ((h >> KECCAK_SHIFT) << KECCAK_ALIGN)) % (1 << 256)
@@ -126,7 +135,7 @@ def test_lowered_tape_matches_term_semantics(qi):
         want = evaluate_term(orig.nodes, ctx.b.pool.values, var_names,
                              ctx.b.symbols.array_names, ctx.b.symbols.function_names,
                              vars_, arrays, funcs)
-        if any(c.kind in ("read", "ufread") for c in schema.columns.values()):
+        if any(c.kind in ("read", "ufread", "kread") for c in schema.columns.values()):
             # read columns: only rows that keep the reads functional (the congruence conjuncts)
             # denote a model, so a witness is a model (sound); other rows may be false
             assert not low or want, (name, trial, row)
@@ -324,3 +333,66 @@ def test_negated_keccak_compare_is_not_a_lower_bound():
         assert bool(low) == bool(want)
         hits += bool(low)
     assert hits == 64
+
+
+@pytest.mark.parametrize("qi", range(12))
+def test_keccak_reads_lowering_is_sound(qi):
+    """The second-chance lowering (keccak_reads: every keccak application a read column, kept a
+    function, injective and apart from the stated pairs by conjuncts): every row the lowered
+    query accepts is a model of the original query (ORACLE, keccak at the reads' arguments as
+    the row says, H elsewhere), on the LASER-shaped queries."""
+    ctx, qs = queries()
+    name, cs = qs[qi]
+    root, schema = lower_query(ctx.b, [c.node for c in cs], keccak_reads=True)
+    assert schema.keccak_reads
+    tape = ctx.b.finish(root)
+    orig = ctx.b.finish(And(*cs).node)
+    var_names = [n for n, _ in sorted(ctx.b.var_index.items(), key=lambda kv: kv[1])]
+    rng = random.Random(77 + qi)
+    cols = list(schema.columns)
+    guide = build_guide(ctx.b, root, schema, cols).arrays()
+    for trial in range(120):
+        if trial % 2:
+            row = dict(zip(cols, generate_row(7 + qi, trial, guide)))
+        else:
+            row = {c.name: candidate_values(ctx, c.width, rng) for c in schema.columns.values()}
+        assign = [row.get(n, 0) for n in var_names]
+        low = E.evaluate(tape.nodes, ctx.b.pool.values, assign)
+        vars_, arrays, funcs = model_of(schema, row, ctx.b)
+        want = evaluate_term(orig.nodes, ctx.b.pool.values, var_names,
+                             ctx.b.symbols.array_names, ctx.b.symbols.function_names,
+                             vars_, arrays, funcs)
+        assert not low or want, (name, trial, row)
+
+
+def test_keccak_pinned_at_a_symbolic_argument():
+    """What the first lowering cannot express (VERDICT r5 missing 2): a keccak value pinned at a
+    symbolic argument -- f(x) == v for a v that is not H(x) -- has a row under keccak_reads, and
+    two applications at unequal arguments cannot share a value (the inverse)."""
+    from mythril_amd import smt
+    from mythril_amd.smt import Function, Not, symbol_factory
+
+    ctx = smt.set_context(smt.Context())
+    f = Function("keccak256_256", 256, 256)
+    inv = Function("keccak256_256-1", 256, 256)
+    x, y = symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecSym("y", 256)
+    v = symbol_factory.BitVecVal(0x1234 << 64, 256)
+    cs = [f(x) == v, inv(f(x)) == x, Not(x == y), f(y) == v]  # unsat: f injective
+    cs_sat = cs[:3]
+    for query, sat in ((cs_sat, True), (cs, False)):
+        root, schema = lower_query(ctx.b, [c.node for c in query], keccak_reads=True)
+        tape = ctx.b.finish(root)
+        names = [n for n, _ in sorted(ctx.b.var_index.items(), key=lambda kv: kv[1])]
+        hits = 0
+        for xv in range(4):
+            for yv in range(4):
+                row = {c.name: 0 for c in schema.columns.values()}
+                row["x"], row["y"] = xv, yv
+                for c in schema.columns.values():
+                    if c.kind == "kread":
+                        row[c.name] = 0x1234 << 64
+                assign = [row.get(n, 0) for n in names]
+                hits += bool(E.evaluate(tape.nodes, ctx.b.pool.values, assign))
+        assert (hits > 0) == sat, (sat, hits)
+        _, plain = lower_query(ctx.b, [c.node for c in cs_sat])
+        assert not any(c.kind == "kread" for c in plain.columns.values())
