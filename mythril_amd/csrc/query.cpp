@@ -234,6 +234,7 @@ struct mh_terms {
     std::vector<Big> cv_vals;
     Stamped memo_lower, seen, local;  // per-query scratch (mirrored node ids)
     std::unique_ptr<class QueryState> last;  // the last query, kept for a child that extends it
+    uint32_t options = 0;                     // MH_TERMS_*
 };
 
 namespace {
@@ -610,7 +611,9 @@ public:
         }
         return add(VAR, w, 0, 0, 0, CELL_COL | it->second);
     }
-    static bool read_kind(uint32_t k) { return k == MH_COL_READ || k == MH_COL_UFREAD; }
+    static bool read_kind(uint32_t k) {
+        return k == MH_COL_READ || k == MH_COL_UFREAD || k == MH_COL_KREAD;
+    }
 
     void deps(uint32_t n, std::vector<uint32_t>& d) {  // Lowering._deps
         d.clear();
@@ -798,15 +801,27 @@ public:
             auto it = kidx.find(f);
             if (it == kidx.end()) unsupported("keccak function " + f + " not harvested");
             const KeccakMap km = keccak[it->second].second;
-            Big s1, s2;
-            s1.w[0] = KECCAK_SHIFT;
-            s2.w[0] = KECCAK_ALIGN;
-            uint32_t h = add(KECCAK, 256, a);
-            h = add(BVLSHR, 256, h, konst(s1, 256));
-            h = add(BVSHL, 256, h, konst(s2, 256));
-            uint32_t acc = km.base.zero() ? h : add(BVADD, 256, h, konst(km.base, 256));
             if (x.width != 256)
                 unsupported("keccak function " + f + " has range " + std::to_string(x.width));
+            uint32_t acc;
+            if (T.options & MH_TERMS_KECCAK_READS) {  // Lowering._keccak_read: f[@a], free
+                Big ik;
+                ik.w[0] = x.a;
+                const Big* cx = const_value(a);
+                if (cx)  // a stated pair's hash, else a read no pair's ite chain can take
+                    for (const auto& pr : km.pairs)
+                        if (pr.first == *cx) return konst(pr.second, 256);
+                acc = cell_column(f + "[@" + std::to_string(x.a) + "]", 256, MH_COL_KREAD, f, &ik, a);
+                if (cx) return acc;
+            } else {
+                Big s1, s2;
+                s1.w[0] = KECCAK_SHIFT;
+                s2.w[0] = KECCAK_ALIGN;
+                uint32_t h = add(KECCAK, 256, a);
+                h = add(BVLSHR, 256, h, konst(s1, 256));
+                h = add(BVSHL, 256, h, konst(s2, 256));
+                acc = km.base.zero() ? h : add(BVADD, 256, h, konst(km.base, 256));
+            }
             std::vector<std::pair<Big, Big>> pairs = km.pairs;
             std::sort(pairs.begin(), pairs.end(),
                       [](const std::pair<Big, Big>& p, const std::pair<Big, Big>& q) {
@@ -1577,17 +1592,42 @@ private:
                 const uint32_t q = qreads[qi];
                 const Column& cq = Q.ccols[q];
                 if (cq.symbol != cp.symbol || cq.kind != cp.kind) continue;
-                const uint32_t same = Q.eq(Q.read_li[q], Q.read_li[p]);
                 const uint32_t vq = Q.add(VAR, cq.width, 0, 0, 0, CELL_COL | q);
                 const uint32_t vp = Q.add(VAR, cp.width, 0, 0, 0, CELL_COL | p);
-                const uint32_t y = Q.add(MH_OP_OR, 0, Q.add(MH_OP_NOT, 0, same), Q.add(EQ, 0, vq, vp));
-                root = Q.add(AND, 0, root, y);
-                Q.linearise(root);
-                add_conjuncts(Q.lget(y));
+                const uint32_t eqv = Q.add(EQ, 0, vq, vp);
+                const Big* cq_ = Q.const_value(Q.read_li[q]);
+                const Big* cp_ = Q.const_value(Q.read_li[p]);
+                if (cp.kind == MH_COL_KREAD && cq_ && cp_) {  // both at constant arguments
+                    conjoin(*cq_ == *cp_ ? eqv : Q.add(MH_OP_NOT, 0, eqv));
+                    continue;
+                }
+                const uint32_t same = Q.eq(Q.read_li[q], Q.read_li[p]);
+                conjoin(Q.add(MH_OP_OR, 0, Q.add(MH_OP_NOT, 0, same), eqv));
+                if (cp.kind == MH_COL_KREAD)  // injective too: Or(i == j, Not(f_i == f_j))
+                    conjoin(Q.add(MH_OP_OR, 0, same, Q.add(MH_OP_NOT, 0, eqv)));
+            }
+            if (cp.kind == MH_COL_KREAD) {  // apart from the stated pairs (the inverse reads them)
+                const uint32_t li = Q.read_li[p];
+                const uint32_t vp = Q.add(VAR, cp.width, 0, 0, 0, CELL_COL | p);
+                std::vector<std::pair<Big, Big>> pairs = Q.keccak.at(Q.kidx.at(cp.symbol)).second.pairs;
+                std::sort(pairs.begin(), pairs.end(),
+                          [](const std::pair<Big, Big>& u, const std::pair<Big, Big>& v) {
+                              return u.first < v.first;
+                          });
+                const bool lc = Q.const_value(li) != nullptr;  // no pair's argument
+                for (const auto& pr : pairs) {
+                    const uint32_t ne = Q.add(MH_OP_NOT, 0, Q.add(EQ, 0, vp, Q.konst(pr.second, 256)));
+                    conjoin(lc ? ne : Q.add(MH_OP_OR, 0, Q.eq(li, Q.konst(pr.first, Q.width(li))), ne));
+                }
             }
             qreads.push_back(p);
             qseen.insert(p);
         }
+    }
+    void conjoin(uint32_t y) {  // one more conjunct of its own
+        root = Q.add(AND, 0, root, y);
+        Q.linearise(root);
+        add_conjuncts(Q.lget(y));
     }
     // Back to depth d <= roots.size(): every root since undone (tape, columns, constants,
     // conjuncts, union-find, owners; the harvest as it was after the first d roots).  The
@@ -1849,6 +1889,14 @@ int32_t mh_terms_create(mh_terms** out) {
 int32_t mh_terms_destroy(mh_terms* t) {
     if (!t) return mh_detail_set_err(MH_E_INVALID, "null terms");
     delete t;
+    return MH_OK;
+}
+
+int32_t mh_terms_set_options(mh_terms* t, uint32_t options) {
+    if (!t) return mh_detail_set_err(MH_E_INVALID, "null terms");
+    if (options & ~MH_TERMS_KECCAK_READS) return mh_detail_set_err(MH_E_INVALID, "unknown option");
+    t->options = options;
+    t->last.reset();
     return MH_OK;
 }
 

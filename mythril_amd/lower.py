@@ -509,7 +509,14 @@ class Lowering:
         H(x).  With a frozen schema (Model.eval) a term the query did not apply f to reads the
         reads at equal arguments, else H(x)."""
         b = self.b
+        cx = b.const_value(x)
+        if cx is not None and cx in km.pairs:  # a stated pair: its hash
+            return b.const(km.pairs[cx], 256)
         rname = read_name(fname, a_orig)
+        if cx is not None and (not self.frozen or rname in self.schema.columns):
+            if not self.frozen:
+                self.read_index.setdefault(rname, x)
+            return self._column(rname, 256, "kread", fname, a_orig)  # no pair's argument
         if not self.frozen:
             acc = self._column(rname, 256, "kread", fname, a_orig)
             self.read_index.setdefault(rname, x)
@@ -688,10 +695,11 @@ def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) ->
     term of a read it reads) -- ordered by (symbol, index term) -- and every read of the same
     symbol before it (`reads`, in the order the query introduced them; updated here),
     ``Or(Not(i == j), A[@i] == A[@j])``; keccak reads (the second-chance lowering) are also
-    injective: ``(i == j) == (f[@i] == f[@j])``, and ``Or(i == c, Not(f[@i] == k))`` for every
-    stated pair (c, k) -- the lowering maps ``f-1(f(x))`` to ``x``.  The native query
+    injective: ``Or(i == j, Not(f[@i] == f[@j]))`` after it, and ``Or(i == c,
+    Not(f[@i] == k))`` for every stated pair (c, k) -- the lowering maps ``f-1(f(x))`` to ``x``.  The native query
     compiler makes the same conjuncts in the same order (csrc/query.cpp congruence)."""
     names = var_names(b)
+    cv = b.const_value
     found, work = {}, [x]
     while work:  # the reads under x, and under the index terms of those (A[B[i]])
         t = work.pop()
@@ -707,18 +715,24 @@ def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) ->
         rp = b.var(p.name, p.width)
         for q in reads:
             if q.symbol == p.symbol and q.kind == p.kind:
-                same = L.eq(L.read_index[q.name], L.read_index[p.name])
+                iq, ip = L.read_index[q.name], L.read_index[p.name]
                 eqv = b.op(Op.EQ, b.var(q.name, q.width), rp)
-                if p.kind == "kread":  # a function and injective: (i == j) == (f_i == f_j)
-                    out.append(b.op(Op.EQ, same, eqv))
-                else:
-                    out.append(b.op(Op.OR, b.op(Op.NOT, same), eqv))
+                if p.kind == "kread" and cv(iq) is not None and cv(ip) is not None:
+                    # two keccak reads at constant arguments: equal values, or unequal ones
+                    out.append(eqv if cv(iq) == cv(ip) else b.op(Op.NOT, eqv))
+                    continue
+                same = L.eq(iq, ip)
+                out.append(b.op(Op.OR, b.op(Op.NOT, same), eqv))
+                if p.kind == "kread":  # injective too: Or(i == j, Not(f_i == f_j))
+                    out.append(b.op(Op.OR, same, b.op(Op.NOT, eqv)))
         if p.kind == "kread":  # injective against the stated pairs too (the inverse reads them)
             km = L.schema.keccak[p.symbol]
             li = L.read_index[p.name]
             for arg in sorted(km.pairs):
-                out.append(b.op(Op.OR, L.eq(li, b.const(arg, b.widths[li])),
-                                b.op(Op.NOT, b.op(Op.EQ, rp, b.const(km.pairs[arg], 256)))))
+                ne = b.op(Op.NOT, b.op(Op.EQ, rp, b.const(km.pairs[arg], 256)))
+                # a constant argument is no pair's (those lower to the pair's hash)
+                out.append(ne if cv(li) is not None else
+                           b.op(Op.OR, L.eq(li, b.const(arg, b.widths[li])), ne))
         reads.append(p)
         seen.add(p.name)
     return out

@@ -156,11 +156,13 @@ class Model:
                 return bool(self.values[name])
             return BitVecValue(self.values[name], c.width)
         got = self.table(name)
+        km = self.schema.keccak.get(name)
+        if km is not None:  # the stated pairs over its reads (keccak_reads: lower.py)
+            tab = dict(got[0]) if got is not None else {}
+            tab.update(km.pairs)
+            return Interp(sorted(tab.items()), 0)
         if got is not None:
             return Interp(sorted(got[0].items()), got[1])
-        km = self.schema.keccak.get(name)
-        if km is not None:
-            return Interp(sorted(km.pairs.items()), 0)
         return None
 
     def table(self, name: str):

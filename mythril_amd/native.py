@@ -113,6 +113,7 @@ SIGNATURES = {
     "mh_smtlib_size": (C.c_uint64, [_vp]),
     "mh_terms_create": (C.c_int32, [C.POINTER(_vp)]),
     "mh_terms_destroy": (C.c_int32, [_vp]),
+    "mh_terms_set_options": (C.c_int32, [_vp, C.c_uint32]),
     "mh_terms_append": (C.c_int32, [_vp, _vp, C.c_uint64, _u32p, C.c_uint64, C.c_char_p,
                                     C.c_uint64, C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64]),
     "mh_terms_sizes": (C.c_int32, [_vp, _u64p]),
@@ -432,7 +433,8 @@ QUERY_COLUMN_DTYPE = np.dtype([("name_off", "<u4"), ("name_len", "<u4"), ("symbo
 QUERY_TABLE_DTYPE = np.dtype([("kind", "<u4"), ("name_off", "<u4"), ("name_len", "<u4"),
                               ("limb_off", "<u4"), ("n_items", "<u4"), ("pad", "<u4")])
 assert QUERY_COLUMN_DTYPE.itemsize == 32 and QUERY_TABLE_DTYPE.itemsize == 24
-COLUMN_KINDS = ("var", "cell", "else", "ufcell", "ufelse", "read", "ufread")  # MH_COL_*
+COLUMN_KINDS = ("var", "cell", "else", "ufcell", "ufelse", "read", "ufread", "kread")  # MH_COL_*
+TERMS_KECCAK_READS = 1  # mh_terms_set_options
 TABLE_CELLS, TABLE_UF_CELLS, TABLE_KECCAK = 0, 1, 2
 QUERY_DEFINITIONS = 1
 QUERY_REFUTED = 2
@@ -530,25 +532,31 @@ def _ints(rows: np.ndarray) -> List[int]:
 class TermMirror:
     """An mh_terms session mirroring one TapeBuilder (tape.py): each sync hands the library the
     nodes, constants and names the builder made since the last one; build() compiles a query
-    (mh_query_build).  One per builder, kept on it (``TermMirror.of``)."""
+    (mh_query_build).  One per builder and lowering mode, kept on it (``TermMirror.of``);
+    ``keccak_reads``: keccak applications as read columns (MH_TERMS_KECCAK_READS, lower_query's
+    keyword of that name)."""
 
-    def __init__(self):
+    def __init__(self, keccak_reads: bool = False):
         import threading
 
         self.lib = load()
         h = C.c_void_p()
         _check(self.lib.mh_terms_create(C.byref(h)))
         self.h = h
+        self.keccak_reads = keccak_reads
+        if keccak_reads:
+            _check(self.lib.mh_terms_set_options(h, TERMS_KECCAK_READS))
         self.n = [0, 0, 0, 0, 0]  # nodes, constants, variables, arrays, functions sent
         # one session per builder, used by one thread at a time (query.cpp keeps scratch and the
         # last query's state on it): sieves of several threads over one builder take turns
         self.lock = threading.Lock()
 
     @classmethod
-    def of(cls, b) -> "TermMirror":
-        m = b.__dict__.get("_term_mirror")
+    def of(cls, b, keccak_reads: bool = False) -> "TermMirror":
+        attr = "_term_mirror_kr" if keccak_reads else "_term_mirror"
+        m = b.__dict__.get(attr)
         if m is None:  # setdefault: two threads racing here end up with the same session
-            m = b.__dict__.setdefault("_term_mirror", cls())
+            m = b.__dict__.setdefault(attr, cls(keccak_reads))
         return m
 
     def close(self) -> None:
@@ -838,13 +846,16 @@ class PendingCompile:
 
         self.ctx, self.tapeset = ctx, tapeset
         t0 = time.perf_counter()
-        self.args = _compile_args(tapeset)
-        nodes, offs, consts = self.args
+        args = _compile_args(tapeset)
+        nodes, offs, consts = args
         self.t1 = time.perf_counter()
         self.flatten_s = self.t1 - t0
         _check(ctx.lib.mh_tapes_compile_async(
             ctx.h, nodes.ctypes.data_as(C.c_void_p), _ptr(offs, C.c_uint64), len(tapeset.tapes),
             _ptr(consts), len(tapeset.pool.values), tapeset.n_vars))
+        # held from here on, and only once the compile is queued: a refused call (another
+        # compile pending) leaves nothing for __del__ to collect -- it would take the other's
+        self.args = args
 
     def wait(self) -> "CompiledTapes":
         import time

@@ -8,7 +8,8 @@ sieve could have answered and z3 must.  Per query: the outcome (a hit in the fir
 or only in the second, 2^16-row round; a miss; a refutation -- a soundness failure, since M is a
 model; an unsupported shape), the wall time, and for a hit that the witness is a model of the
 original query (oracle/term_eval.py).  One JSON line per family with the recall overall, per
-round, per shape class of the query's newest constraint, latency percentiles; with --extended,
+round, per shape class of the query's newest constraint, latency percentiles, the hits of the
+keccak second chance (SIEVE_KECCAK2=0 turns it off); with --extended,
 the misses are asked again of a sieve with 2^20-row second rounds (how many more rows would
 recover).
 
@@ -70,6 +71,8 @@ def run_family(s, family, n_paths, path_len, big=None, check=True, feedback=Fals
     times = defaultdict(list)
     bad, missed = [], []
     learnt0 = s.stats.extra.get("learnt", 0)
+    k2t0 = s.stats.extra.get("keccak2_tries", 0)
+    k2hits = 0
     for seed in range(n_paths):
         ctx, cs, m, kinds = planted_path(family, seed, path_len)
         nodes = [c.node for c in cs]
@@ -81,6 +84,7 @@ def run_family(s, family, n_paths, path_len, big=None, check=True, feedback=Fals
                 dt = (time.perf_counter() - t0) * 1e3
                 if w is not None:
                     kind = "hit_r%d" % w.rounds
+                    k2hits += bool(getattr(w.schema, "keccak_reads", False))
                     if check and not holds_original(ctx, cs[:k], w.schema, w.values):
                         bad.append((seed, k))
                 elif s.stats.extra.get("refuted", 0) > r0:
@@ -110,6 +114,9 @@ def run_family(s, family, n_paths, path_len, big=None, check=True, feedback=Fals
         "unsupported": outcomes["unsupported"], "error": outcomes["error"],
         "invalid_witnesses": len(bad),
         "second_round": s.second_round,
+        # hits of the keccak second chance (keccak applications as read columns, Sieve.solve)
+        "keccak_second_chance": s.keccak_second_chance, "keccak2_hits": k2hits,
+        "keccak2_tries": s.stats.extra.get("keccak2_tries", 0) - k2t0,
         "feedback": feedback, "learnt": s.stats.extra.get("learnt", 0) - learnt0,
         "first_round_progress": dict(progress),
         "by_newest_constraint": {
@@ -146,7 +153,9 @@ def main():
 
         fake_device.install(pytest.MonkeyPatch())
     policy = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--round2=")), None)
-    s = Sieve(rows=256, second_round=policy) if fake else Sieve(second_round=policy)
+    # the stand-in is slow: a budget that does not cut its rounds short
+    s = (Sieve(rows=256, second_round=policy, budget_s=60.0) if fake
+         else Sieve(second_round=policy))
     big = None
     if "--extended" in sys.argv:
         big = Sieve(rows=1 << 20)

@@ -4,6 +4,8 @@ import ctypes as C
 import os
 import re
 
+import pytest
+
 from mythril_amd import native
 from oracle import smt_eval
 
@@ -78,3 +80,23 @@ def test_async_compile_argument_validation_without_device():
     assert lib.mh_tapes_compile_async(None, None, None, 0, None, 0, 0) == native.MH_E_INVALID
     assert lib.mh_tapes_compile_wait(None, C.byref(h), None) == native.MH_E_INVALID
     assert b"null" in lib.mh_last_error()
+
+
+def test_refused_async_compile_leaves_the_pending_one(monkeypatch):
+    """A compile_async the library refuses (another compile pending on the ctx) must not collect
+    the pending compile when its PendingCompile is dropped (it used to: __del__ waited on the
+    ctx and took the other compile's result, r06b GPU suite)."""
+    import gc
+    import types
+
+    from mythril_amd import synth
+
+    waits = []
+    lib = types.SimpleNamespace(
+        mh_tapes_compile_async=lambda *a: native.MH_E_INVALID,
+        mh_tapes_compile_wait=lambda *a: waits.append(a) or native.MH_OK)
+    ctx = types.SimpleNamespace(lib=lib, h=C.c_void_p(1))
+    with pytest.raises(native.SieveError):
+        native.PendingCompile(ctx, synth.generate(2))
+    gc.collect()
+    assert waits == []

@@ -38,10 +38,10 @@ def _values(rows):
     return native._ints(rows)
 
 
-def python_stages(b, roots):
+def python_stages(b, roots, keccak_reads=False):
     """The Python host stages of Sieve._host_python: lowering, definitions (solved for and
     substituted away, Sieve.solve_definitions), groups, the root tape."""
-    root, schema = lower_query(b, roots)
+    root, schema = lower_query(b, roots, keccak_reads=keccak_reads)
     cols = list(schema.columns) or ["__ground__"]
     rest, defs = eliminate_definitions(b, Sieve.conjuncts(b, root), schema)
     if defs:
@@ -54,14 +54,14 @@ def python_stages(b, roots):
     return root, schema, cols, groups, names, ts, defs
 
 
-def check_query(b, roots, label):
+def check_query(b, roots, label, keccak_reads=False):
     try:
-        root, schema, cols, groups, names, ts, defs = python_stages(b, roots)
+        root, schema, cols, groups, names, ts, defs = python_stages(b, roots, keccak_reads)
     except LoweringUnsupported:
         with pytest.raises(native.Unsupported):
-            native.TermMirror.of(b).build(b, roots)
+            native.TermMirror.of(b, keccak_reads).build(b, roots)
         return None
-    cq = native.TermMirror.of(b).build(b, roots)
+    cq = native.TermMirror.of(b, keccak_reads).build(b, roots)
     # columns
     got = {n: (w, k, s, key) for n, w, k, s, key in cq.columns}
     want = {c.name: (c.width, c.kind, c.symbol, c.key) for c in schema.columns.values()}
@@ -705,3 +705,66 @@ def test_guide_session_planted_paths_in_jumpi_order(family):
                 got = native.harvest_guide(cq.tapes[0], cq.consts, cq.widths, session=sess)
                 assert _guide_equal(got, want), (family, seed, kk)
         sess.close()
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_keccak_reads_match_python_stages(seed):
+    _kreads_parity(seed)
+
+
+def _kreads_parity(seed):
+    """The second-chance lowering (MH_TERMS_KECCAK_READS / lower_query(keccak_reads=True)): keccak
+    applications as read columns with the injectivity and pair conjuncts -- node for node the
+    Python stages' result, in LASER order and both branches of every constraint (JUMPI order),
+    on a session of its own beside the default one (whose results are unchanged)."""
+    import random
+
+    from mythril_amd.smt import Not
+
+    rng = random.Random(500 + seed)
+    ctx, cs = _random_query(rng, 10)
+    cs = [c for c in cs if hasattr(c, "node")]
+    nodes = [c.node for c in cs]
+    kreads = 0
+    for k in range(1, len(nodes) + 1):
+        cq = check_query(ctx.b, nodes[:k], (seed, k, "taken"), keccak_reads=True)
+        kreads += cq is not None and any(c[2] == "kread" for c in cq.columns)
+        check_query(ctx.b, nodes[:k], (seed, k, "default"))
+        check_query(ctx.b, nodes[:k - 1] + [Not(cs[k - 1]).node], (seed, k, "other"),
+                    keccak_reads=True)
+    return kreads
+
+
+def test_keccak_reads_are_made():
+    """The random family does apply keccak at symbolic arguments (the parity above is not
+    vacuous), and the LASER-shaped queries and grown paths match in that mode too."""
+    assert sum(_kreads_parity(s) for s in range(6)) > 0
+    ctx, qs = laser_like.queries()
+    for name, cs in qs:
+        nodes = [c.node for c in cs]
+        for k in range(1, len(nodes) + 1):
+            check_query(ctx.b, nodes[:k], (name, k), keccak_reads=True)
+    for shape in ("killbilly", "overflow", "ether_thief"):
+        ctx, cs = grow(shape, 25)
+        nodes = [c.node for c in cs]
+        for k in (1, 12, 25):
+            check_query(ctx.b, nodes[:k], (shape, k), keccak_reads=True)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_keccak_reads_in_bfs_order(seed):
+    import random
+
+    from mythril_amd.smt import Not
+    from tests.bfs_order import bfs_queries
+
+    rng = random.Random(700 + seed)
+    ctx, cs = _random_query(rng, 10)
+    cs = [c for c in cs if hasattr(c, "node")]
+    nodes = [c.node for c in cs]
+    negs = [Not(c).node for c in cs]
+    dropped = set()
+    for i, roots in enumerate(bfs_queries(nodes, negs, 3, 4, seed, dropped)):
+        cq = check_query(ctx.b, roots, (seed, i), keccak_reads=True)
+        if cq is not None and cq.flags & native.QUERY_REFUTED:
+            dropped.add(tuple(roots))
