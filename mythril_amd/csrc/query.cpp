@@ -767,23 +767,24 @@ public:
         const std::string& name = array_name(arr);
         auto it = cell_of.find(name);
         return table(name, a.width, idx, it == cell_of.end() ? nullptr : &cells[it->second].second,
-                     MH_COL_CELL, MH_COL_ELSE, MH_COL_READ, idx_orig);
+                     MH_COL_CELL, MH_COL_READ, idx_orig);
     }
-    // _table: a constant key's cell; any other constant key the else value; a symbolic index
-    // the cells' ite chain over its read column name[@idx_orig] (Ackermann's reduction)
+    // _table: a constant key's cell; any other index the cells' ite chain over its read column
+    // name[@idx_orig] (Ackermann's reduction)
     uint32_t table(const std::string& name, uint32_t rng, uint32_t idx,
-                   const std::vector<Big>* keys, uint32_t kcell, uint32_t kelse, uint32_t kread,
+                   const std::vector<Big>* keys, uint32_t kcell, uint32_t kread,
                    uint32_t idx_orig) {
         const Big* kp = const_value(idx);
         const Big key = kp ? *kp : Big();
         if (kp && keys && std::binary_search(keys->begin(), keys->end(), key))
             return cell_column(name + "[" + key.hex() + "]", rng, kcell, name, &key);
-        if (kp) return cell_column(name + "[*]", rng, kelse, name, nullptr);
         Big ik;
         ik.w[0] = idx_orig;
         uint32_t acc = cell_column(name + "[@" + std::to_string(idx_orig) + "]", rng, kread, name,
                                    &ik, idx);
-        if (!keys) return acc;
+        // an index that lowers to a constant no harvest saw: a read of its own (an else value
+        // there would let a read at an equal index take another value)
+        if (kp || !keys) return acc;
         for (size_t i = keys->size(); i-- > 0;) {
             const Big k = (*keys)[i];
             const uint32_t cell = cell_column(name + "[" + k.hex() + "]", rng, kcell, name, &k);
@@ -835,7 +836,7 @@ public:
         }
         auto it = uf_of.find(f);
         return table(f, x.width, a, it == uf_of.end() ? nullptr : &uf_cells[it->second].second,
-                     MH_COL_UFCELL, MH_COL_UFELSE, MH_COL_UFREAD, x.a);
+                     MH_COL_UFCELL, MH_COL_UFREAD, x.a);
     }
 
     // ---- the root tape (sieve.py local_tapeset): VAR imm0 = query column, CONST imm0 = query

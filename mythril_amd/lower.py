@@ -624,9 +624,17 @@ class Lowering:
         key = b.const_value(idx)
         if key is not None and key in cells:
             return self._column(cells[key], rng, kcell, name, key)
-        if key is not None:  # a constant key outside the table: the reads, else the else value
-            return self._fallback(name, rng, idx, kelse, kread)
         rname = read_name(name, idx_orig)
+        if key is not None and (self.frozen and rname not in self.schema.columns):
+            # Model.eval at a constant key outside the table: the reads, else the else value
+            return self._fallback(name, rng, idx, kelse, kread)
+        if key is not None:
+            # an index that lowers to a constant no harvest saw (select(K(7), i) as a key): a
+            # read of its own -- the else column would let a read at an equal index take another
+            # value there (kept apart by congruence like any two reads)
+            if not self.frozen:
+                self.read_index.setdefault(rname, idx)
+            return self._column(rname, rng, kread, name, idx_orig)
         if not self.frozen:
             acc = self._column(rname, rng, kread, name, idx_orig)
             self.read_index.setdefault(rname, idx)

@@ -36,6 +36,7 @@
 #   pprofile  rocprofv3 kernel trace + stats of path_scaling.py at 400 constraints
 #   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
 #   recall    scripts/planted_recall.py (recall on planted-SAT paths, per round and shape class)
+#   cdreads   scripts/calldata_reads.py (the reference's calldata byte loop over a sieve model)
 #   recall0   planted_recall without the keccak second chance (SIEVE_KECCAK2=0), no extended pass
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
 #             (SIEVE_ROUND2=progress) and never run (recall only)
@@ -95,6 +96,7 @@ for step in "$@"; do
     recall)   timeout -k 10 900 python -u scripts/planted_recall.py 100 24 --extended > "$OUT/planted_recall.jsonl" 2> "$OUT/planted_recall.log" ;;
     occupancy) MH_JIT_PAD_VGPR=168 timeout -k 10 400 python -u bench.py --no-companion --no-cpu-baseline --steps 2 > "$OUT/bench_vgpr168.json" 2> "$OUT/bench_vgpr168.log" && \
               MH_JIT_PAD_VGPR=256 timeout -k 10 400 python -u bench.py --no-companion --no-cpu-baseline --steps 2 > "$OUT/bench_vgpr256.json" 2> "$OUT/bench_vgpr256.log" ;;
+    cdreads)  timeout -k 10 300 python -u scripts/calldata_reads.py > "$OUT/calldata_reads.json" 2> "$OUT/calldata_reads.log" ;;
     recall0)  SIEVE_KECCAK2=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_nok2.jsonl" 2> "$OUT/planted_recall_nok2.log" ;;
     round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
               timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \
