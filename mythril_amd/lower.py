@@ -15,8 +15,10 @@ into a term over scalar *columns* whose every assignment denotes one complete z3
   unequal indices may differ.  A satisfying assignment is a model of the original query: ``A`` is
   ``Store(...Store(K(else), c1, v1)..., i_val, A[@i]_val ...)`` (the reads at their indices'
   values, where no cell is); ``store`` chains become ``ite`` over their keys and ``K(v)`` becomes
-  ``v`` (array.py:16-63).  A constant key outside the table -- only met by ``Model.eval`` of a
-  term the query did not state -- reads the reads at equal indices, else the *else* column.
+  ``v`` (array.py:16-63).  An index that lowers to a constant the harvest did not see
+  (``select(A, select(K(7), i))``) is a read of its own, kept apart like any two reads.  A
+  constant key outside the table in ``Model.eval`` of a term the query did not state reads the
+  reads at equal indices, else the array's *else* value (0: no lowered query reads it).
 * a keccak function ``keccak256_N`` becomes ``ite(x == c_i, k_i, H(x))`` over the concrete pairs
   ``keccak256_N(c_i) == k_i`` the query states (keccak_function_manager.py:92-97,145-148), with
   ``H(x) = base + ((keccak256(x) >> 139) << 6)``: a function of the argument (so congruence
@@ -26,7 +28,11 @@ into a term over scalar *columns* whose every assignment denotes one complete z3
   function's values (``ULE(lo, f(x))`` of the manager's condition, ``UGT(f(x), c)``, ...),
   rounded up to a multiple of 64 — the interval of ``_create_condition`` (:121-149) is
   ``PART = (2^256-1) // 10^40 > 2^123 + 64`` wide, so the interval and ``mod 64`` conditions hold
-  by construction.  The hash runs on the device's Keccak-f[1600].
+  by construction.  The hash runs on the device's Keccak-f[1600].  The second-chance lowering
+  (``keccak_reads``; Sieve.solve after a miss whose unsolved groups read H) gives every
+  application at an argument no stated pair has a *kread* column instead of H, kept a function
+  (congruence) and injective (``Or(i == j, Not(f[@i] == f[@j]))`` and ``Or(i == c, Not(f[@i] ==
+  k))`` per stated pair): a path that pins a keccak value elsewhere than H has rows then.
 * any other uninterpreted function is tabled like an array (cells over constant arguments, a
   read column per symbolic argument term with the same congruence conjuncts, function.py:7-25).
 

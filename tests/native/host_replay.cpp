@@ -104,6 +104,13 @@ int main(int argc, char** argv) {
             terms.erase(it);
             break;
         }
+        case 'O': {
+            auto it = terms.find(sid);
+            const uint32_t opts = r.get<uint32_t>();
+            if (it == terms.end() || !r.ok || mh_terms_set_options(it->second, opts) != MH_OK)
+                return fail("terms_set_options");
+            break;
+        }
         case 'A': {
             auto it = terms.find(sid);
             if (it == terms.end()) return fail("append: unknown session");

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Record the host-only native calls of the query path (test infrastructure): every
-mh_terms_create / mh_terms_append / mh_query_build / mh_terms_destroy, mh_harvester_create /
+mh_terms_create / mh_terms_set_options / mh_terms_append / mh_query_build / mh_terms_destroy,
+mh_harvester_create /
 mh_guide_harvest_with / mh_guide_harvest / mh_harvester_destroy and mh_smtlib_create / read /
 commit / rollback / destroy the Python side makes, with the bytes of their arguments (and the
 read's return code), into a file that tests/native/host_replay.cpp replays against a build of
@@ -9,7 +10,8 @@ csrc/query.cpp + harvest.cpp + smtlib.cpp under AddressSanitizer / UBSan
 
 The workload is the query path's host half without a device: the LASER-shaped queries of
 tests/laser_like.py and tests/laser_paths.py in LASER order (each prefix a query, svm.py:257-262),
-their UNSAT variants, and random conjunctions (tests/test_query_native._random_query), each
+their UNSAT variants, random conjunctions (tests/test_query_native._random_query) in LASER, BFS
+and JUMPI order, and planted random paths with keccak applications as read columns, each
 compiled by the native query compiler and, when not refuted, harvested by a guide session; and
 the z3-printed text of every LASER-shaped query read constraint by constraint into one SMT-LIB
 session (tests/z3_style.py), plus malformed texts the reader must refuse.
@@ -57,6 +59,10 @@ class Recorder:
         r = self.lib.mh_terms_create(pp)
         self._w(b"C", self._handle(pp))
         return r
+
+    def mh_terms_set_options(self, h, options):
+        self._w(b"O", h.value or 0, struct.pack("<I", options))
+        return self.lib.mh_terms_set_options(h, options)
 
     def mh_terms_destroy(self, h):
         self._w(b"D", h.value or 0)
@@ -124,9 +130,9 @@ class Recorder:
         return self.lib.mh_smtlib_rollback(h)
 
 
-def host_query(b, roots, guides, rng):
+def host_query(b, roots, guides, rng, keccak_reads=False):
     """The host half of Sieve.solve for one query: native compile, then the guide harvest."""
-    cq = native.TermMirror.of(b).build(b, roots)
+    cq = native.TermMirror.of(b, keccak_reads).build(b, roots)
     if cq.flags & (native.QUERY_REFUTED | native.QUERY_DEFINITIONS):
         return
     parent = []
@@ -149,10 +155,11 @@ def workload(n_random=40):
         for k in range(1, len(nodes) + 1):  # every prefix, parents first
             host_query(b, nodes[:k], guides, rng)
 
-    def done(b):  # the builder's session ends inside the recording
-        m = b.__dict__.pop("_term_mirror", None)
-        if m is not None:
-            m.close()
+    def done(b):  # the builder's sessions end inside the recording
+        for attr in ("_term_mirror", "_term_mirror_kr"):
+            m = b.__dict__.pop(attr, None)
+            if m is not None:
+                m.close()
 
     for make in (queries, hard_queries):
         ctx, qs = make()
@@ -187,6 +194,28 @@ def workload(n_random=40):
                 host_query(ctx.b, roots, guides, rng)
             except native.Unsupported:
                 pass
+        done(ctx.b)
+    # the keccak second chance (MH_TERMS_KECCAK_READS): planted random paths in LASER order and
+    # the random conjunctions in JUMPI order, on a session of that mode beside the default one
+    from tests.planted import planted_path
+
+    for seed in range(min(n_random, 8)):
+        ctx, cs, _, _ = planted_path("random", seed, 12)
+        nodes = [c.node for c in cs]
+        for k in range(1, len(nodes) + 1):
+            host_query(ctx.b, nodes[:k], guides, rng)
+            host_query(ctx.b, nodes[:k], guides, rng, keccak_reads=True)
+        done(ctx.b)
+    for seed in range(min(n_random, 8)):
+        ctx, cs = _random_query(random.Random(900 + seed), 8)
+        cs = [c for c in cs if hasattr(c, "node")]
+        for k in range(1, len(cs) + 1):
+            for roots in ([c.node for c in cs[:k]],
+                          [c.node for c in cs[:k - 1]] + [Not(cs[k - 1]).node]):
+                try:
+                    host_query(ctx.b, roots, guides, rng, keccak_reads=True)
+                except native.Unsupported:
+                    pass
         done(ctx.b)
     guides.close()
     smtlib_workload()
