@@ -341,6 +341,10 @@ typedef struct {
                                          n_defs tapes are their terms, the root and group tapes
                                          come first (n_tapes - n_defs of them)                     */
     const uint32_t* def_cols;         /* [n_defs]: the column each definition tape's value gives   */
+    uint32_t parent_len;              /* nodes of the root tape that are the tape of the query
+                                         without its last root (it is linearised root by root, so
+                                         they come first; 0 with one root or definitions): the
+                                         nodes at or past it are the newest root's conjuncts    */
 } mh_query_info;
 int32_t mh_terms_create(mh_terms** out);
 int32_t mh_terms_destroy(mh_terms* t);

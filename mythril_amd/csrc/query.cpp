@@ -996,6 +996,7 @@ struct mh_query {
     std::vector<uint32_t> key_limbs, group_cols, group_off, table_limbs;
     std::vector<mh_query_table> tables;
     std::vector<uint32_t> def_cols;  // the column each definition tape (the last ones) gives
+    uint32_t parent_len = 0;         // root tape nodes of the query without its last root
 };
 
 namespace {
@@ -1743,6 +1744,8 @@ void QueryState::emit(mh_query& q, uint32_t& flags) {
     if (defines && emit_definitions(q)) {
         flags |= MH_QUERY_DEFINITIONS;
     } else {
+        // the root tape lists the query without its last root first (linearised root by root)
+        if (roots.size() >= 2) q.parent_len = Q.lget(marks.back().root) + 1;
         std::vector<std::vector<uint32_t>> gconj;  // conjunct tape nodes per group, path order
         std::unordered_map<int64_t, uint32_t> gid;
         std::vector<uint32_t> group_of(conj.size(), UINT32_MAX);  // by union-find root
@@ -2039,6 +2042,7 @@ int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_
     info->n_table_entries = (uint32_t)(r->table_limbs.size() / NL);
     info->n_defs = (uint32_t)r->def_cols.size();
     info->def_cols = r->def_cols.data();
+    info->parent_len = r->parent_len;
     *out = r;
     return MH_OK;
 }

@@ -460,6 +460,9 @@ class Sieve:
         if keccak_second_chance is None:
             keccak_second_chance = os.environ.get("SIEVE_KECCAK2", "1") != "0"
         self.keccak_second_chance = keccak_second_chance
+        # the second round of a query whose parent has a witness: the parent's witness under
+        # the newest root's conjuncts (SIEVE_INCREMENTAL=0: the 2^16-row full-guide round)
+        self.incremental_round = os.environ.get("SIEVE_INCREMENTAL", "1") != "0"
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)
         self.last_rounds: Dict[str, int] = {}
         self.seed = seed
@@ -470,7 +473,8 @@ class Sieve:
         self.max_witnesses = 1 << 14
         # the last query this sieve missed after a device round, (key, schema): a model the
         # fallback then finds for it is learnt as its witness (learn)
-        self.last_miss: Optional[Tuple[tuple, Schema]] = None
+        # (key, schema[, the keccak second chance's schema])
+        self.last_miss: Optional[tuple] = None
         # the tape compile runs on the context's worker thread (mh_tapes_compile_async) while
         # this one harvests the guide: the harvest is host-only, both only read the query's
         # tapes, and the round needs both (SIEVE_OVERLAP=0: one after the other)
@@ -511,19 +515,24 @@ class Sieve:
         around it as around a witness of the sieve's own (svm.py:257-262: the children of a state
         z3 found feasible are asked next).  Without it one miss leaves every later query of the
         path without parent-guided rows.  ``value_of(column)`` is the model's value of a column
-        (lower.Column: a variable, an array cell or a function cell), None where the model does
-        not fix it.  Returns the number of columns learnt."""
+        (lower.Column: a variable, an array or function cell, a read at its index term), None
+        where the model does not fix it.  Returns the number of columns learnt."""
         lm, self.last_miss = self.last_miss, None
         if not key or lm is None or lm[0] != key:
             return 0
         values: Dict[str, int] = {}
-        for name, col in lm[1].columns.items():
-            try:
-                v = value_of(col)
-            except Exception:  # noqa: BLE001 - a column the model cannot evaluate stays free
-                v = None
-            if v is not None:
-                values[name] = int(v) & ((1 << col.width) - 1)
+        # the columns of both lowerings the miss tried (the keccak second chance's reads too:
+        # a child's second chance is then generated around the model's keccak values)
+        for sc in lm[1:]:
+            for name, col in sc.columns.items():
+                if name in values:
+                    continue
+                try:
+                    v = value_of(col)
+                except Exception:  # noqa: BLE001 - a column the model cannot evaluate stays free
+                    v = None
+                if v is not None:
+                    values[name] = int(v) & ((1 << col.width) - 1)
         if values:
             self._store(key, values)
             self.stats.extra["learnt"] = self.stats.extra.get("learnt", 0) + 1
@@ -668,7 +677,8 @@ class Sieve:
         ts.flat = (cq.nodes[cq.tape_off[k]:cq.tape_off[-1]], off - off[0], cq.consts)
         if len(cq.groups) > 1:
             st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
-        return columns, cq.widths, NativeSchema(cq, keccak_reads), tapes[0], ts, cq.groups, defs
+        return (columns, cq.widths, NativeSchema(cq, keccak_reads), tapes[0], ts, cq.groups, defs,
+                0 if defs else cq.parent_len)
 
     def _host_python(self, b: TapeBuilder, roots: Sequence[int], keccak_reads: bool = False):
         """The host stages in Python: lower_query, definitions, buckets, local tapes."""
@@ -702,7 +712,7 @@ class Sieve:
             st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
         st.add("tapes", time.perf_counter() - t_l)
         widths = [schema.columns[c].width for c in columns]
-        return columns, widths, schema, root_nodes, ts, group_cols, defs
+        return columns, widths, schema, root_nodes, ts, group_cols, defs, 0
 
     @classmethod
     def buckets(cls, b: TapeBuilder, root: int) -> List[Tuple[List[int], set]]:
@@ -734,18 +744,20 @@ class Sieve:
             return None
         st = self.stats
         w, schema, kec = self._attempt(b, roots, key, budget, t0, False)
+        schema2 = None
         if (w is None and kec and self.keccak_second_chance
                 and time.perf_counter() - t0 < budget):
             st.extra["keccak2_tries"] = st.extra.get("keccak2_tries", 0) + 1
             first = self.last_rounds
-            w, _, _ = self._attempt(b, roots, key, budget, t0, True)
+            w, schema2, _ = self._attempt(b, roots, key, budget, t0, True)
             self.last_rounds = dict(first, keccak2=int(w is not None))
             if w is not None:
                 st.extra["keccak2_hits"] = st.extra.get("keccak2_hits", 0) + 1
         if w is None:
             self.stats.misses += 1
-            if schema is not REFUTED:
-                self.last_miss = (key, schema) if key else None
+            if schema is not REFUTED and key:
+                self.last_miss = ((key, schema) if schema2 is None or schema2 is REFUTED
+                                  else (key, schema, schema2))
             return None
         if key:
             self.remember(key, w)
@@ -772,7 +784,7 @@ class Sieve:
             return None, REFUTED, False
         if host is None:
             host = self._host_python(b, roots, keccak_reads)
-        columns, widths, schema, root_nodes, ts, group_cols, defs = host
+        columns, widths, schema, root_nodes, ts, group_cols, defs, parent_len = host
         t_t = time.perf_counter()
         pending = None
         try:  # from the compile's start: an error on this side still collects it
@@ -811,6 +823,7 @@ class Sieve:
             guide.close()
             raise
         t_c = time.perf_counter()
+        round_guide = guide  # the incremental round's own guide replaces it (closed below)
         ft, nt = getattr(ct, "timing", (0.0, 0.0))
         st.add("compile_flatten", ft)
         st.add("compile_native", nt)
@@ -820,11 +833,16 @@ class Sieve:
             solved = [False] * len(group_cols)
             first_index = None
             offset = (1 << 23) if keccak_reads else 0
+            # the incremental round: the parent's witness under the newest root's conjuncts'
+            # sets only (the parent's conjuncts hold there already), instead of the 2^16-row
+            # round of the full guide -- a child whose own conjunct the full guide's rows keep
+            # breaking while they break the parent's
+            inc_ok = bool(parent) and parent_len > 0 and self.incremental_round
             launches = [self.first_rows]
             if self.max_rounds > 1:
-                launches.append((self.max_rounds - 1) * self.rows)
+                launches.append(self.first_rows if inc_ok else (self.max_rounds - 1) * self.rows)
             self.last_rounds = {"groups": len(group_cols), "r1_solved": 0, "rounds": 0}
-            if keccak_reads:  # the second chance: one first round
+            if keccak_reads and not inc_ok:  # the second chance: one first round
                 launches = launches[:1]
             for rnd, n in enumerate(launches):
                 if rnd == 1:
@@ -835,6 +853,18 @@ class Sieve:
                         self.stats.extra["round2_skipped"] = \
                             self.stats.extra.get("round2_skipped", 0) + 1
                         break
+                    if inc_ok:
+                        ti = time.perf_counter()
+                        inc = newest_tape(root_nodes, parent_len)
+                        if inc is None:
+                            break
+                        round_guide = native.harvest_guide(
+                            inc, ts.pool.to_array(), widths,
+                            [(col_index[k], v) for k, v in parent.items() if k in col_index],
+                            keep=True)
+                        st.add("guide", time.perf_counter() - ti)
+                        st.extra["inc_rounds"] = st.extra.get("inc_rounds", 0) + 1
+                        self.last_rounds["incremental"] = 1
                 self.last_rounds["rounds"] = rnd + 1
                 base = (self.stats.queries << 24) + offset
                 offset += n
@@ -844,8 +874,8 @@ class Sieve:
                 g1 = len(solved) - solved[::-1].index(False)
                 # generator, run, and the first witnesses with their rows' columns in one call and
                 # one copy back (mh_query_round)
-                fh, _, wrows = native.query_round(self.ctx, ct, assign, guide, self.seed, base, n,
-                                                  len(columns), tape_first=g0,
+                fh, _, wrows = native.query_round(self.ctx, ct, assign, round_guide, self.seed,
+                                                  base, n, len(columns), tape_first=g0,
                                                   tape_count=g1 - g0,
                                                   mode=native.MODE_FIRST_HIT)
                 tr = time.perf_counter()
@@ -871,6 +901,8 @@ class Sieve:
                         for (c, _), v in zip(defs, got):
                             values[c] = v
                         st.add("definitions", time.perf_counter() - td)
+                    if rnd and inc_ok:
+                        st.extra["inc_hits"] = st.extra.get("inc_hits", 0) + 1
                     return Witness(schema, values, first_index, rnd + 1), schema, False
                 if time.perf_counter() - t0 > budget:
                     break
@@ -880,7 +912,71 @@ class Sieve:
         finally:
             ct.close()
             guide.close()
+            if round_guide is not guide:
+                round_guide.close()
             self.stats.device_s += time.perf_counter() - t1
+
+
+def newest_tape(nodes: np.ndarray, parent_len: int) -> Optional[np.ndarray]:
+    """The conjunction of the conjuncts a query's root tape adds to its parent's: the tape of
+    ``AND(...AND(parent, c1)..., ck)`` lists the parent's root tape first (linearised root by
+    root, query.cpp), ending in the parent's root at ``parent_len - 1``; the right operands of
+    the AND chain above it are the new conjuncts (the newest constraint's lowering and its
+    congruence conjuncts).  Their AND, re-linearised over the same columns and constants;
+    None when there is none.  The guide harvested from it (the parent's witness under the newest
+    conjuncts' sets only) is Sieve.solve's incremental round."""
+    n = len(nodes)
+    if parent_len <= 0 or parent_len >= n:
+        return None
+    op, a, bb, cc = nodes["op"], nodes["a"], nodes["b"], nodes["c"]
+    AND = int(Op.AND)
+    # down the root's AND chain to the parent's root (the last prefix node): the right operands
+    # on the way are the new conjuncts (a hash-consed one may be a node of the prefix), each
+    # flattened into its AND leaves
+    tops, x = [], n - 1
+    while x >= parent_len and op[x] == AND:
+        tops.append(int(bb[x]))
+        x = int(a[x])
+    if x != parent_len - 1 or not tops:
+        return None
+    leaves = []
+    for top in reversed(tops):
+        stack = [top]
+        while stack:
+            y = stack.pop()
+            if op[y] == AND:
+                stack += [int(bb[y]), int(a[y])]
+            else:
+                leaves.append(y)
+    from .tape import ARITY
+
+    ar = {int(o): ARITY[o] for o in Op}
+    remap: Dict[int, int] = {}
+    out: List[np.void] = []
+    for leaf in leaves:
+        st = [(leaf, False)]
+        while st:
+            x, done = st.pop()
+            if x in remap:
+                continue
+            k = ar[int(op[x])]
+            kids = (int(a[x]), int(bb[x]), int(cc[x]))[:k]
+            if not done:
+                st.append((x, True))
+                st += [(y, False) for y in reversed(kids) if y not in remap]
+                continue
+            y = nodes[x].copy()
+            for f, kid in zip(("a", "b", "c"), kids):
+                y[f] = remap[kid]
+            remap[x] = len(out)
+            out.append(y)
+    acc = remap[leaves[0]]
+    for leaf in leaves[1:]:
+        y = np.zeros((), dtype=nodes.dtype)
+        y["op"], y["a"], y["b"] = AND, acc, remap[leaf]
+        acc = len(out)
+        out.append(y)
+    return np.array(out, dtype=nodes.dtype)
 
 
 def _reads_keccak(nodes) -> bool:

@@ -37,6 +37,9 @@
 #   gather    scripts/gather_bench.py (survivor reload cost of lane compaction, SoA vs row-major)
 #   recall    scripts/planted_recall.py (recall on planted-SAT paths, per round and shape class)
 #   cdreads   scripts/calldata_reads.py (the reference's calldata byte loop over a sieve model)
+#   misses    scripts/recall_misses.py (first misses of the random family: search or lowering)
+#   feedback  planted_recall with every miss answered by the planted model, learnt (--feedback)
+#   recalli   planted_recall without the incremental second round (SIEVE_INCREMENTAL=0)
 #   recall0   planted_recall without the keccak second chance (SIEVE_KECCAK2=0), no extended pass
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
 #             (SIEVE_ROUND2=progress) and never run (recall only)
@@ -97,6 +100,9 @@ for step in "$@"; do
     occupancy) MH_JIT_PAD_VGPR=168 timeout -k 10 400 python -u bench.py --no-companion --no-cpu-baseline --steps 2 > "$OUT/bench_vgpr168.json" 2> "$OUT/bench_vgpr168.log" && \
               MH_JIT_PAD_VGPR=256 timeout -k 10 400 python -u bench.py --no-companion --no-cpu-baseline --steps 2 > "$OUT/bench_vgpr256.json" 2> "$OUT/bench_vgpr256.log" ;;
     cdreads)  timeout -k 10 300 python -u scripts/calldata_reads.py > "$OUT/calldata_reads.json" 2> "$OUT/calldata_reads.log" ;;
+    misses)   timeout -k 10 600 python -u scripts/recall_misses.py 100 24 > "$OUT/recall_misses.json" 2> "$OUT/recall_misses.log" ;;
+    feedback) timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --feedback > "$OUT/planted_recall_feedback.jsonl" 2> "$OUT/planted_recall_feedback.log" ;;
+    recalli)  SIEVE_INCREMENTAL=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_noinc.jsonl" 2> "$OUT/planted_recall_noinc.log" ;;
     recall0)  SIEVE_KECCAK2=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_nok2.jsonl" 2> "$OUT/planted_recall_nok2.log" ;;
     round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
               timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \

@@ -48,8 +48,17 @@ def _pct(v):
             "p99": round(float(np.percentile(a, 99)), 3), "max": round(float(a.max()), 3)}
 
 
-def planted_value(m):
-    """value_of(column) for Sieve.learn under the planted model M."""
+def planted_value(m, ctx=None):
+    """value_of(column) for Sieve.learn under the planted model M (a read column at its index
+    term's value under M, given the term context)."""
+    def at(node):
+        b = ctx.b
+        names = [n for n, _ in sorted(b.var_index.items(), key=lambda kv: kv[1])]
+        from oracle.term_eval import evaluate_term
+
+        return evaluate_term(b.finish(node).nodes, b.pool.values, names, b.symbols.array_names,
+                             b.symbols.function_names, m.vars, m.arrays, m.funcs)
+
     def value_of(col):
         if col.kind == "var":
             return m.vars.get(col.symbol)
@@ -58,6 +67,11 @@ def planted_value(m):
             return els if col.kind == "else" else table.get(col.key, els)
         if col.kind == "ufcell" and col.symbol in m.funcs:
             return m.funcs[col.symbol](col.key)
+        if ctx is not None and col.kind == "read" and col.symbol in m.arrays:
+            table, els = m.arrays[col.symbol]
+            return table.get(at(col.key), els)
+        if ctx is not None and col.kind in ("ufread", "kread") and col.symbol in m.funcs:
+            return m.funcs[col.symbol](at(col.key))
         return None
     return value_of
 
@@ -93,7 +107,7 @@ def run_family(s, family, n_paths, path_len, big=None, check=True, feedback=Fals
                     kind = "miss"
                     missed.append((seed, k))
                     if feedback:
-                        s.learn(tuple(nodes[:k]), planted_value(m))
+                        s.learn(tuple(nodes[:k]), planted_value(m, ctx))
             except Exception as e:  # noqa: BLE001 - the front end falls back on any error
                 dt = (time.perf_counter() - t0) * 1e3
                 kind = "unsupported" if "Unsupported" in type(e).__name__ else "error"

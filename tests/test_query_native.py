@@ -768,3 +768,41 @@ def test_keccak_reads_in_bfs_order(seed):
         cq = check_query(ctx.b, roots, (seed, i), keccak_reads=True)
         if cq is not None and cq.flags & native.QUERY_REFUTED:
             dropped.add(tuple(roots))
+
+
+@pytest.mark.parametrize("shape,k,seed", [("killbilly", 4, 0), ("ether_thief", 8, 3)])
+def test_parent_len_splits_the_root_tape(shape, k, seed):
+    """mh_query_info.parent_len: the root tape's first parent_len nodes are the tape of the query
+    without its last root (linearised root by root), so the root is that prefix's root AND the
+    newest root's conjuncts (sieve.newest_tape) -- on every row, in LASER, JUMPI and BFS order
+    (random rows, the ORACLE evaluating all three tapes)."""
+    import random
+
+    from mythril_amd.sieve import newest_tape
+    from mythril_amd.smt import Not
+    from oracle import smt_eval as E
+    from tests.bfs_order import bfs_queries
+
+    ctx, cs = grow(shape, 30)
+    nodes = [c.node for c in cs]
+    negs = [Not(c).node for c in cs]
+    m = native.TermMirror.of(ctx.b)
+    rng = random.Random(seed)
+    split = 0
+    for roots in bfs_queries(nodes, negs, 18, k, seed, set()):
+        cq = m.build(ctx.b, roots)
+        if cq.flags & native.QUERY_DEFINITIONS or len(roots) < 2:
+            assert cq.parent_len == 0
+            continue
+        t = cq.tapes[0]
+        p = cq.parent_len
+        assert 0 < p < len(t)
+        inc = newest_tape(t, p)
+        assert inc is not None
+        split += 1
+        consts = native._ints(cq.consts)
+        for _ in range(4):
+            row = [rng.getrandbits(int(w)) for w in cq.widths]
+            whole = E.evaluate(t, consts, row)
+            assert whole == (E.evaluate(t[:p], consts, row) and E.evaluate(inc, consts, row))
+    assert split > 10
