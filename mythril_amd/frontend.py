@@ -221,6 +221,7 @@ def sieve_model(constraints, timeout_ms: Optional[float] = None):
     if w is None:
         stats.sieve_misses += 1
         _tls.miss_key = key  # the fallback's model of this query is learnt (learn_from_fallback)
+        _tls.miss_ctx = ctx
         return None
     conv = _config["to_terms"]  # reads reference terms for Model.eval / Model[decl]
     m = Model(s, ctx, w.schema, w.values, w.index,
@@ -283,27 +284,41 @@ def z3_column_reader(model, z3):
     ``raw`` z3 ModelRefs) or a z3 ModelRef -- for Sieve.learn: a variable's value, an array cell
     ``Select(A, key)``, a function cell ``f(key)``, each evaluated with model completion; None
     for the else columns (any value completes a model) and for symbols the model does not
-    declare."""
+    declare.  ``value_of.value_at(column, index)`` reads a read column (``Select(A, i)``,
+    ``f(i)``, keccak included) at its index term's value, which Sieve.learn computes."""
     models = list(getattr(model, "raw", None) or [model])
     decls = {}
     for zm in models:
         for d in zm.decls():
             decls.setdefault(d.name(), (zm, d))
 
-    def value_of(col):
+    def at(col, key):
         hit = decls.get(col.symbol)
-        if hit is None or col.kind not in ("var", "cell", "ufcell"):
+        if hit is None:
             return None
         zm, d = hit
         if col.kind == "var":
             v = zm.eval(d(), model_completion=True)
-        elif col.kind == "cell":
-            v = zm.eval(z3.Select(d(), z3.BitVecVal(col.key, d.range().domain().size())),
+        elif col.kind in ("cell", "read"):
+            v = zm.eval(z3.Select(d(), z3.BitVecVal(key, d.range().domain().size())),
                         model_completion=True)
         else:
-            v = zm.eval(d(z3.BitVecVal(col.key, d.domain(0).size())), model_completion=True)
+            v = zm.eval(d(z3.BitVecVal(key, d.domain(0).size())), model_completion=True)
         return v.as_long() if z3.is_bv_value(v) else None
 
+    def value_of(col):
+        if col.kind not in ("var", "cell", "ufcell"):
+            return None
+        return at(col, col.key)
+
+    def value_at(col, index):
+        """A read column (an array's, a tabled function's or a keccak function's value at a
+        symbolic index term) at that term's value ``index`` (Sieve.learn computes it)."""
+        if col.kind not in ("read", "ufread", "kread"):
+            return None
+        return at(col, index)
+
+    value_of.value_at = value_at
     return value_of
 
 
@@ -319,6 +334,7 @@ def learn_from_fallback(model) -> None:
     try:
         import z3
 
-        s.learn(key, z3_column_reader(model, z3))
+        reader = z3_column_reader(model, z3)
+        s.learn(key, reader, ctx=getattr(_tls, "miss_ctx", None), value_at=reader.value_at)
     except Exception as e:  # noqa: BLE001 - learning never changes the answer
         log.debug("fallback model not learnt: %s", e)

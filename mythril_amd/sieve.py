@@ -509,14 +509,18 @@ class Sieve:
         while len(self.witnesses) > self.max_witnesses:
             self.witnesses.popitem(last=False)
 
-    def learn(self, key: tuple, value_of: Callable[[Column], Optional[int]]) -> int:
+    def learn(self, key: tuple, value_of: Callable[[Column], Optional[int]], ctx=None,
+              value_at: Optional[Callable[[Column, int], Optional[int]]] = None) -> int:
         """A model the fallback found for the query this sieve missed last (the same ``key``)
         becomes that query's remembered witness, so the query's LASER children are generated
         around it as around a witness of the sieve's own (svm.py:257-262: the children of a state
         z3 found feasible are asked next).  Without it one miss leaves every later query of the
         path without parent-guided rows.  ``value_of(column)`` is the model's value of a column
-        (lower.Column: a variable, an array or function cell, a read at its index term), None
-        where the model does not fix it.  Returns the number of columns learnt."""
+        (lower.Column: a variable, an array or function cell), None where the model does not fix
+        it.  With the query's term context ``ctx`` and ``value_at(column, index)``, the read
+        columns (arrays, functions and keccak at symbolic index terms) are learnt too: their index
+        terms are evaluated on the device over what was learnt so far (a read inside an index term
+        is learnt on the next pass).  Returns the number of columns learnt."""
         lm, self.last_miss = self.last_miss, None
         if not key or lm is None or lm[0] != key:
             return 0
@@ -533,10 +537,45 @@ class Sieve:
                     v = None
                 if v is not None:
                     values[name] = int(v) & ((1 << col.width) - 1)
+        if ctx is not None and value_at is not None:
+            self._learn_reads(lm[1:], values, ctx, value_at)
         if values:
             self._store(key, values)
             self.stats.extra["learnt"] = self.stats.extra.get("learnt", 0) + 1
         return len(values)
+
+    def _learn_reads(self, schemas, values: Dict[str, int], ctx, value_at) -> None:
+        """Sieve.learn's read columns: each index term evaluated over the values learnt so far
+        (Model._evaluate, one device batch per pass), the model's value there; three passes at
+        most (a read whose index reads another read)."""
+        from .lower import READ_KINDS
+        from .model import Model
+
+        for sc in schemas:
+            reads = [c for c in sc.columns.values() if c.kind in READ_KINDS]
+            for _ in range(3):
+                todo = [c for c in reads if c.name not in values]
+                if not todo:
+                    break
+                try:
+                    at = Model(self, ctx, sc, dict(values), 0)._evaluate(
+                        [c.key for c in todo], [], True)
+                except Exception:  # noqa: BLE001 - learning is best effort
+                    return
+                got = 0
+                for c in todo:
+                    idx = at.get(c.key)
+                    if not isinstance(idx, int):
+                        continue
+                    try:
+                        v = value_at(c, idx)
+                    except Exception:  # noqa: BLE001
+                        v = None
+                    if v is not None:
+                        values[c.name] = int(v) & ((1 << c.width) - 1)
+                        got += 1
+                if not got:
+                    break
 
     def compile(self, ts: TapeSet) -> native.CompiledTapes:
         """Compile a query's tapes; a tape that runs out of registers is retried with cheap

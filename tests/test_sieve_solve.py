@@ -414,3 +414,47 @@ def test_divergent_keccak_case_is_answered(monkeypatch, native_query):
         assert m.values.get("N1", 0) == 100
     finally:
         frontend.reset()
+
+
+def test_fallback_model_learns_read_columns(monkeypatch):
+    """The fallback's model is learnt over read columns too (frontend.z3_column_reader.value_at;
+    Sieve.learn evaluates each read's index term on the device over what it learnt first): the
+    child of a missed query that reads an array at a symbolic index is answered from it."""
+    import random
+    import sys
+
+    from mythril_amd import smt
+    from mythril_amd.smt import Array, symbol_factory
+
+    fake_device.install(monkeypatch)
+    monkeypatch.setitem(sys.modules, "z3", _Z3)
+    rng = random.Random(78)
+    x0, y0 = rng.getrandbits(256) | 1, rng.getrandbits(256) | 1
+    k = (x0 * y0) % (1 << 256)
+    frontend.reset()
+    try:
+        frontend.configure(rows=256)
+        smt.set_context(smt.Context())
+        x, y, z = (symbol_factory.BitVecSym(n, 256) for n in "xyz")
+        a = Array("A", 256, 8)
+        c1 = x * y == symbol_factory.BitVecVal(k, 256)
+        c2 = a[x + symbol_factory.BitVecVal(1, 256)] == symbol_factory.BitVecVal(0x5A, 8)
+        c3 = z == symbol_factory.BitVecVal(7, 256)
+        calls = []
+
+        def fallback(cs, mn, mx, enf):
+            calls.append(len(cs))
+            return _Model({"x": x0, "y": y0, "z": 0}, {"A": {(x0 + 1) % (1 << 256): 0x5A}})
+
+        frontend.configure(fallback=fallback)
+        assert frontend.get_model((c1, c2)) is not None and calls == [2]  # the sieve missed
+        s = frontend.sieve()
+        key = tuple(c.node for c in (c1, c2))
+        learnt = s.witnesses[key]
+        reads = [n for n in learnt if n.startswith("A[@")]
+        assert reads and all(learnt[n] == 0x5A for n in reads), learnt
+        m = frontend.get_model((c1, c2, c3))
+        assert isinstance(m, Model) and calls == [2], "the child was not answered"
+        assert (m.values["x"], m.values["y"], m.values["z"]) == (x0, y0, 7)
+    finally:
+        frontend.reset()
