@@ -13,8 +13,11 @@ from scripts.planted_recall import run_family
 pytestmark = pytest.mark.gpu
 
 # measured on MI355X on this workload (20 paths x 16 constraint attempts, seeds 0..19):
-# LASER 1.000 (326 queries), random 0.653 (455; profiles/r05d/pytest_recall.txt)
-FLOOR = {"laser": 0.99, "random": 0.60}
+# LASER 1.000 (326 queries), random 0.653 (455; profiles/r05d/pytest_recall.txt); round 6 (read
+# columns, the keccak second chance, the incremental second round): random 0.723, 0.925 with
+# the fallback's models learnt (profiles/r06h/pytest_recall.txt)
+FLOOR = {"laser": 0.99, "random": 0.70}
+FLOOR_LEARNT = 0.90
 
 
 @pytest.mark.parametrize("family", ["laser", "random"])
@@ -48,3 +51,4 @@ def test_learnt_fallback_models_do_not_lower_recall(gpu_ctx):
     assert fed["refuted"] == 0 and fed["invalid_witnesses"] == 0 and fed["error"] == 0, fed
     assert 0 < fed["learnt"] <= fed["miss"]
     assert fed["recall"] >= base["recall"], (base, fed)
+    assert fed["recall"] >= FLOOR_LEARNT, fed
