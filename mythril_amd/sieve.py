@@ -34,7 +34,7 @@ import numpy as np
 
 from . import native
 from .lower import Column, KeccakMap, Schema, cell_name, lower_query, node_columns
-from .tape import NODE_DTYPE, Op, Tape, TapeBuilder, TapeSet
+from .tape import NODE_DTYPE, Op, Tape, TapeBuilder, TapeError, TapeSet
 
 
 @dataclass
@@ -788,7 +788,7 @@ class Sieve:
                 and time.perf_counter() - t0 < budget):
             st.extra["keccak2_tries"] = st.extra.get("keccak2_tries", 0) + 1
             first = self.last_rounds
-            w, schema2, _ = self._attempt(b, roots, key, budget, t0, True)
+            w, schema2, _ = self._attempt(b, roots, key, budget, t0, True, base_schema=schema)
             self.last_rounds = dict(first, keccak2=int(w is not None))
             if w is not None:
                 st.extra["keccak2_hits"] = st.extra.get("keccak2_hits", 0) + 1
@@ -811,10 +811,40 @@ class Sieve:
             self.guides_kr = native.GuideSession()
         return self.guides_kr
 
+    def _parent_kreads(self, b: TapeBuilder, schema: Schema, base_schema: Schema,
+                       parent: Dict[str, int]) -> Dict[str, int]:
+        """The parent's witness with the keccak read columns of `schema` (the second chance's
+        lowering) it lacks -- a witness of the default lowering has none -- at the values the
+        default lowering gives those applications under it (the stated pair or H(x),
+        `base_schema`; one device batch).  The incremental round's parent rows then satisfy
+        the parent's keccak conjuncts too."""
+        from copy import deepcopy
+
+        from .lower import Lowering, LoweringUnsupported
+
+        need = [c for c in schema.columns.values()
+                if c.kind == "kread" and c.name not in parent]
+        if not need:
+            return parent
+        try:
+            sc = deepcopy(base_schema)
+            L = Lowering(b, sc)
+            terms = [L.lower(b.apply(c.symbol, b.widths[c.key], 256, c.key)) for c in need]
+            vals = self.eval_terms(b, terms, list(sc.columns) or ["__ground__"], parent)
+        except (LoweringUnsupported, native.Unsupported, TapeError):
+            return parent
+        out = dict(parent)
+        for c, v in zip(need, vals):
+            out[c.name] = v
+        self.stats.extra["parent_kreads"] = self.stats.extra.get("parent_kreads", 0) + 1
+        return out
+
     def _attempt(self, b: TapeBuilder, roots: Sequence[int], key: Optional[tuple],
-                 budget: float, t0: float, keccak_reads: bool):
+                 budget: float, t0: float, keccak_reads: bool,
+                 base_schema: Optional[Schema] = None):
         """One lowering of the query and its rounds: (witness or None, schema or REFUTED,
-        whether a group left unsolved reads a keccak application)."""
+        whether a group left unsolved reads a keccak application).  ``base_schema``: the
+        default lowering's schema, for the second chance's incremental round."""
         st = self.stats
         th = time.perf_counter()
         host = self._host_native(b, roots, keccak_reads) if self.native_query else None
@@ -897,9 +927,13 @@ class Sieve:
                         inc = newest_tape(root_nodes, parent_len)
                         if inc is None:
                             break
+                        pv = parent
+                        if keccak_reads and base_schema is not None \
+                                and base_schema is not REFUTED:
+                            pv = self._parent_kreads(b, schema, base_schema, parent)
                         round_guide = native.harvest_guide(
                             inc, ts.pool.to_array(), widths,
-                            [(col_index[k], v) for k, v in parent.items() if k in col_index],
+                            [(col_index[k], v) for k, v in pv.items() if k in col_index],
                             keep=True)
                         st.add("guide", time.perf_counter() - ti)
                         st.extra["inc_rounds"] = st.extra.get("inc_rounds", 0) + 1
