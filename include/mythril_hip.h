@@ -345,6 +345,10 @@ typedef struct {
                                          without its last root (it is linearised root by root, so
                                          they come first; 0 with one root or definitions): the
                                          nodes at or past it are the newest root's conjuncts    */
+    const uint32_t* root_ends;        /* [n_root_ends]: entry d - 1 = nodes of the root tape that are
+                                         the tape of the first d roots (d < n_roots; none with
+                                         definitions); the last entry is parent_len               */
+    uint32_t n_root_ends;
 } mh_query_info;
 int32_t mh_terms_create(mh_terms** out);
 int32_t mh_terms_destroy(mh_terms* t);

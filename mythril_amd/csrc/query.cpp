@@ -997,6 +997,7 @@ struct mh_query {
     std::vector<mh_query_table> tables;
     std::vector<uint32_t> def_cols;  // the column each definition tape (the last ones) gives
     uint32_t parent_len = 0;         // root tape nodes of the query without its last root
+    std::vector<uint32_t> root_ends;  // [d - 1]: root tape nodes of its first d roots
 };
 
 namespace {
@@ -1745,7 +1746,8 @@ void QueryState::emit(mh_query& q, uint32_t& flags) {
         flags |= MH_QUERY_DEFINITIONS;
     } else {
         // the root tape lists the query without its last root first (linearised root by root)
-        if (roots.size() >= 2) q.parent_len = Q.lget(marks.back().root) + 1;
+        for (size_t d = 1; d < roots.size(); ++d) q.root_ends.push_back(Q.lget(marks[d].root) + 1);
+        if (roots.size() >= 2) q.parent_len = q.root_ends.back();
         std::vector<std::vector<uint32_t>> gconj;  // conjunct tape nodes per group, path order
         std::unordered_map<int64_t, uint32_t> gid;
         std::vector<uint32_t> group_of(conj.size(), UINT32_MAX);  // by union-find root
@@ -2043,6 +2045,8 @@ int32_t mh_query_build(mh_terms* t, const uint32_t* roots, uint32_t n_roots, mh_
     info->n_defs = (uint32_t)r->def_cols.size();
     info->def_cols = r->def_cols.data();
     info->parent_len = r->parent_len;
+    info->root_ends = r->root_ends.data();
+    info->n_root_ends = (uint32_t)r->root_ends.size();
     *out = r;
     return MH_OK;
 }

@@ -451,7 +451,8 @@ class QueryInfo(C.Structure):
                 ("n_tapes", C.c_uint32), ("n_consts", C.c_uint32), ("n_columns", C.c_uint32),
                 ("names_len", C.c_uint32), ("n_groups", C.c_uint32), ("n_tables", C.c_uint32),
                 ("flags", C.c_uint32), ("n_keys", C.c_uint32), ("n_table_entries", C.c_uint32),
-                ("n_defs", C.c_uint32), ("def_cols", _u32p), ("parent_len", C.c_uint32)]
+                ("n_defs", C.c_uint32), ("def_cols", _u32p), ("parent_len", C.c_uint32),
+                ("root_ends", _u32p), ("n_root_ends", C.c_uint32)]
 
 
 class CompiledQuery:
@@ -462,7 +463,7 @@ class CompiledQuery:
     when a model is evaluated, mythril/laser/smt/model.py:45-59)."""
 
     __slots__ = ("tapes", "consts", "names", "widths", "groups", "flags", "nodes", "tape_off",
-                 "defs", "def_tapes", "parent_len", "_raw", "_columns", "_tables")
+                 "defs", "def_tapes", "parent_len", "root_ends", "_raw", "_columns", "_tables")
 
     def __init__(self, info: QueryInfo):
         def raw(p, nbytes):
@@ -491,6 +492,9 @@ class CompiledQuery:
         self.groups = [gcols[goff[g]:goff[g + 1]] for g in range(ng)]
         self.flags = int(info.flags)
         self.parent_len = int(info.parent_len)  # root-tape nodes of the query minus its last root
+        # root_ends[d - 1]: root-tape nodes of the query's first d roots
+        self.root_ends = np.frombuffer(raw(info.root_ends, 4 * info.n_root_ends),
+                                       dtype=np.uint32).tolist()
         kb = 4 * QUERY_KEY_LIMBS
         self._raw = (names, cols, raw(info.key_limbs, kb * info.n_keys),
                      raw(info.tables, 24 * info.n_tables),

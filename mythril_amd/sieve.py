@@ -463,6 +463,7 @@ class Sieve:
         # the second round of a query whose parent has a witness: the parent's witness under
         # the newest root's conjuncts (SIEVE_INCREMENTAL=0: the 2^16-row full-guide round)
         self.incremental_round = os.environ.get("SIEVE_INCREMENTAL", "1") != "0"
+        self.inc_rows = int(os.environ.get("SIEVE_INC_ROWS", "4096"))  # its rows
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)
         self.last_rounds: Dict[str, int] = {}
         self.seed = seed
@@ -717,7 +718,7 @@ class Sieve:
         if len(cq.groups) > 1:
             st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
         return (columns, cq.widths, NativeSchema(cq, keccak_reads), tapes[0], ts, cq.groups, defs,
-                0 if defs else cq.parent_len)
+                [] if defs else cq.root_ends)
 
     def _host_python(self, b: TapeBuilder, roots: Sequence[int], keccak_reads: bool = False):
         """The host stages in Python: lower_query, definitions, buckets, local tapes."""
@@ -751,7 +752,7 @@ class Sieve:
             st.extra["bucketed"] = st.extra.get("bucketed", 0) + 1
         st.add("tapes", time.perf_counter() - t_l)
         widths = [schema.columns[c].width for c in columns]
-        return columns, widths, schema, root_nodes, ts, group_cols, defs, 0
+        return columns, widths, schema, root_nodes, ts, group_cols, defs, []
 
     @classmethod
     def buckets(cls, b: TapeBuilder, root: int) -> List[Tuple[List[int], set]]:
@@ -811,6 +812,20 @@ class Sieve:
             self.guides_kr = native.GuideSession()
         return self.guides_kr
 
+    ANCESTORS = 8  # how far up a path Sieve._ancestor looks for a witness
+
+    def _ancestor(self, key: Optional[tuple], root_ends: Sequence[int]):
+        """(witness, root-tape nodes of its query) of the nearest of the query's last ANCESTORS
+        prefixes that has a witness -- the parent, or past a missed parent the state above it
+        (its children are then searched around the last model the path had) -- or (None, 0)."""
+        if not key:
+            return None, 0
+        for j in range(len(key) - 1, max(len(key) - 1 - self.ANCESTORS, 0), -1):
+            w = self.witnesses.get(key[:j])
+            if w is not None:
+                return w, (root_ends[j - 1] if j - 1 < len(root_ends) else 0)
+        return None, 0
+
     def _parent_kreads(self, b: TapeBuilder, schema: Schema, base_schema: Schema,
                        parent: Dict[str, int]) -> Dict[str, int]:
         """The parent's witness with the keccak read columns of `schema` (the second chance's
@@ -853,14 +868,14 @@ class Sieve:
             return None, REFUTED, False
         if host is None:
             host = self._host_python(b, roots, keccak_reads)
-        columns, widths, schema, root_nodes, ts, group_cols, defs, parent_len = host
+        columns, widths, schema, root_nodes, ts, group_cols, defs, root_ends = host
         t_t = time.perf_counter()
         pending = None
         try:  # from the compile's start: an error on this side still collects it
             if self.overlap and hasattr(self.ctx, "compile_async"):
                 pending = self.ctx.compile_async(ts)
             col_index = {c: i for i, c in enumerate(columns)}
-            parent = self.witnesses.get(key[:-1]) if key else None
+            parent, parent_len = self._ancestor(key, root_ends)
             guide = native.harvest_guide(
                 root_nodes, ts.pool.to_array(), widths,
                 [(col_index[k], v) for k, v in parent.items() if k in col_index] if parent else (),
@@ -909,7 +924,8 @@ class Sieve:
             inc_ok = bool(parent) and parent_len > 0 and self.incremental_round
             launches = [self.first_rows]
             if self.max_rounds > 1:
-                launches.append(self.first_rows if inc_ok else (self.max_rounds - 1) * self.rows)
+                launches.append(min(self.inc_rows, self.rows) if inc_ok
+                                else (self.max_rounds - 1) * self.rows)
             self.last_rounds = {"groups": len(group_cols), "r1_solved": 0, "rounds": 0}
             if keccak_reads and not inc_ok:  # the second chance: one first round
                 launches = launches[:1]
@@ -991,7 +1007,7 @@ class Sieve:
 
 
 def newest_tape(nodes: np.ndarray, parent_len: int) -> Optional[np.ndarray]:
-    """The conjunction of the conjuncts a query's root tape adds to its parent's: the tape of
+    """The conjunction of the conjuncts a query's root tape adds to an ancestor's: the tape of
     ``AND(...AND(parent, c1)..., ck)`` lists the parent's root tape first (linearised root by
     root, query.cpp), ending in the parent's root at ``parent_len - 1``; the right operands of
     the AND chain above it are the new conjuncts (the newest constraint's lowering and its

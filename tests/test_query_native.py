@@ -797,6 +797,11 @@ def test_parent_len_splits_the_root_tape(shape, k, seed):
         t = cq.tapes[0]
         p = cq.parent_len
         assert 0 < p < len(t)
+        ends = cq.root_ends
+        assert len(ends) == len(roots) - 1 and ends[-1] == p and ends == sorted(ends)
+        d = rng.randrange(1, len(roots))  # an ancestor's prefix splits the tape the same way
+        anc = newest_tape(t, ends[d - 1])
+        assert anc is not None
         inc = newest_tape(t, p)
         assert inc is not None
         split += 1
@@ -805,4 +810,6 @@ def test_parent_len_splits_the_root_tape(shape, k, seed):
             row = [rng.getrandbits(int(w)) for w in cq.widths]
             whole = E.evaluate(t, consts, row)
             assert whole == (E.evaluate(t[:p], consts, row) and E.evaluate(inc, consts, row))
+            e = ends[d - 1]
+            assert whole == (E.evaluate(t[:e], consts, row) and E.evaluate(anc, consts, row))
     assert split > 10
