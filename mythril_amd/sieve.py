@@ -812,7 +812,11 @@ class Sieve:
             self.guides_kr = native.GuideSession()
         return self.guides_kr
 
-    ANCESTORS = 8  # how far up a path Sieve._ancestor looks for a witness
+    # how far up a path Sieve._ancestor looks for a witness: 1, the parent.  Looking 8 up (past a
+    # missed parent) answered 13 instead of 8 queries after a miss on the planted random family
+    # (recall 0.651 either way) and took its misses from 1.32 to 2.24 ms (p50; profiles/r06l):
+    # under the plugin a missed parent has the fallback's model learnt anyway
+    ANCESTORS = int(os.environ.get("SIEVE_ANCESTORS", "1"))
 
     def _ancestor(self, key: Optional[tuple], root_ends: Sequence[int]):
         """(witness, root-tape nodes of its query) of the nearest of the query's last ANCESTORS
