@@ -399,3 +399,30 @@ def test_verifier_pins_reads_on_planted_random_paths(monkeypatch):
         assert SolverStatistics().sieve_rejected == rejected0
     finally:
         frontend.reset()
+
+
+def test_verifier_checks_a_keccak_second_chance_witness(monkeypatch):
+    """keccak_tests.py:23-26 (reference_cases.DIVERGENT) answered by the keccak second chance:
+    the verifier pins keccak256_256 at N1's value to the read column's value (not H), the
+    manager's inverse at that hash back to N1, and z3's evaluation says sat -- the reference's
+    Model comes back, nothing is left free."""
+    from mythril_amd.support import RefModel
+    from tests import z3_ast
+    from tests.reference_cases import BY_NAME
+
+    from mythril_amd.support import args
+
+    z3, seen, fallback = _verifier_world(monkeypatch)
+    # the CPU stand-in is slow: no round cut short by the sieve's or get_model's budget
+    monkeypatch.setattr(args, "solver_timeout", 600000)
+    try:
+        frontend.configure(budget_s=600.0, rows=256)
+        ctx, cs = BY_NAME["keccak_basic_val8_100_sym_N1"].build()
+        m = frontend.get_model(tuple(z3_ast.Ref(c) for c in cs))
+        assert not fallback and len(seen) == 1
+        assert seen[0].schema.keccak_reads
+        assert isinstance(m, RefModel) or type(m).__name__ == "Model", type(m)
+        (s,) = [x for x in z3.solvers if "timeout" in x.params][-1:]
+        assert s.free == [] and s.check() == "sat"
+    finally:
+        frontend.reset()
