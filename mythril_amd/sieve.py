@@ -464,6 +464,7 @@ class Sieve:
         # the newest root's conjuncts (SIEVE_INCREMENTAL=0: the 2^16-row full-guide round)
         self.incremental_round = os.environ.get("SIEVE_INCREMENTAL", "1") != "0"
         self.inc_rows = int(os.environ.get("SIEVE_INC_ROWS", "4096"))  # its rows
+        self.inc_hops = int(os.environ.get("SIEVE_INC_HOPS", "0"))  # newest_tape(hops)
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)
         self.last_rounds: Dict[str, int] = {}
         self.seed = seed
@@ -944,7 +945,7 @@ class Sieve:
                         break
                     if inc_ok:
                         ti = time.perf_counter()
-                        inc = newest_tape(root_nodes, parent_len)
+                        inc = newest_tape(root_nodes, parent_len, self.inc_hops)
                         if inc is None:
                             break
                         pv = parent
@@ -1010,14 +1011,16 @@ class Sieve:
             self.stats.device_s += time.perf_counter() - t1
 
 
-def newest_tape(nodes: np.ndarray, parent_len: int) -> Optional[np.ndarray]:
+def newest_tape(nodes: np.ndarray, parent_len: int, hops: int = 0) -> Optional[np.ndarray]:
     """The conjunction of the conjuncts a query's root tape adds to an ancestor's: the tape of
     ``AND(...AND(parent, c1)..., ck)`` lists the parent's root tape first (linearised root by
     root, query.cpp), ending in the parent's root at ``parent_len - 1``; the right operands of
     the AND chain above it are the new conjuncts (the newest constraint's lowering and its
     congruence conjuncts).  Their AND, re-linearised over the same columns and constants;
     None when there is none.  The guide harvested from it (the parent's witness under the newest
-    conjuncts' sets only) is Sieve.solve's incremental round."""
+    conjuncts' sets only) is Sieve.solve's incremental round.  ``hops`` = 1 puts the parent's
+    conjuncts that read a column a new conjunct reads in front of them (their sets re-satisfy
+    what the new conjuncts' sets break; measured, SIEVE_INC_HOPS)."""
     n = len(nodes)
     if parent_len <= 0 or parent_len >= n:
         return None
@@ -1041,6 +1044,8 @@ def newest_tape(nodes: np.ndarray, parent_len: int) -> Optional[np.ndarray]:
                 stack += [int(bb[y]), int(a[y])]
             else:
                 leaves.append(y)
+    if hops:
+        leaves = _column_neighbours(nodes, parent_len - 1, leaves) + leaves
     from .tape import ARITY
 
     ar = {int(o): ARITY[o] for o in Op}
@@ -1070,6 +1075,41 @@ def newest_tape(nodes: np.ndarray, parent_len: int) -> Optional[np.ndarray]:
         acc = len(out)
         out.append(y)
     return np.array(out, dtype=nodes.dtype)
+
+
+def _column_neighbours(nodes: np.ndarray, parent_root: int, leaves: List[int]) -> List[int]:
+    """The AND leaves under `parent_root` that read a column one of `leaves` reads."""
+    op, a, bb, cc, i0 = nodes["op"], nodes["a"], nodes["b"], nodes["c"], nodes["imm0"]
+    from .tape import ARITY
+
+    ar = {int(o): ARITY[o] for o in Op}
+    VAR, AND = int(Op.VAR), int(Op.AND)
+
+    def cols(root: int) -> set:
+        out, seen, st = set(), set(), [root]
+        while st:
+            x = st.pop()
+            if x in seen:
+                continue
+            seen.add(x)
+            o = int(op[x])
+            if o == VAR:
+                out.add(int(i0[x]))
+                continue
+            st += [int(y) for y in (a[x], bb[x], cc[x])[:ar[o]]]
+        return out
+
+    want = set()
+    for leaf in leaves:
+        want |= cols(leaf)
+    pl, st = [], [parent_root]
+    while st:
+        y = st.pop()
+        if int(op[y]) == AND:
+            st += [int(bb[y]), int(a[y])]
+        else:
+            pl.append(y)
+    return [y for y in pl if cols(y) & want]
 
 
 def _reads_keccak(nodes) -> bool:

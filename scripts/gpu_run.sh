@@ -42,6 +42,7 @@
 #   recalli   planted_recall without the incremental second round (SIEVE_INCREMENTAL=0)
 #   grecall   tests/test_gpu_recall.py with its printed numbers (-s)
 #   incrows   planted_recall with 16384 / 65536-row incremental rounds (SIEVE_INC_ROWS)
+#   inchops   planted_recall with the parent's column-sharing conjuncts in the incremental guide
 #   recall0   planted_recall without the keccak second chance (SIEVE_KECCAK2=0), no extended pass
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
 #             (SIEVE_ROUND2=progress) and never run (recall only)
@@ -107,6 +108,7 @@ for step in "$@"; do
     recalli)  SIEVE_INCREMENTAL=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_noinc.jsonl" 2> "$OUT/planted_recall_noinc.log" ;;
     grecall)  timeout -k 10 600 python -u -m pytest -x -v -s --timeout 500 --timeout-method thread -m gpu tests/test_gpu_recall.py > "$OUT/pytest_recall.txt" 2>&1 ;;
     incrows)  for r in 16384 65536; do SIEVE_INC_ROWS=$r timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_inc$r.jsonl" 2> "$OUT/planted_recall_inc$r.log" || exit 1; done ;;
+    inchops)  SIEVE_INC_HOPS=1 timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_hops1.jsonl" 2> "$OUT/planted_recall_hops1.log" ;;
     recall0)  SIEVE_KECCAK2=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_nok2.jsonl" 2> "$OUT/planted_recall_nok2.log" ;;
     round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
               timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \

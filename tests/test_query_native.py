@@ -804,12 +804,15 @@ def test_parent_len_splits_the_root_tape(shape, k, seed):
         assert anc is not None
         inc = newest_tape(t, p)
         assert inc is not None
+        hop = newest_tape(t, p, 1)  # plus the parent's conjuncts sharing a column: still implied
+        assert hop is not None and len(hop) >= len(inc)
         split += 1
         consts = native._ints(cq.consts)
         for _ in range(4):
             row = [rng.getrandbits(int(w)) for w in cq.widths]
             whole = E.evaluate(t, consts, row)
             assert whole == (E.evaluate(t[:p], consts, row) and E.evaluate(inc, consts, row))
+            assert not whole or E.evaluate(hop, consts, row)
             e = ends[d - 1]
             assert whole == (E.evaluate(t[:e], consts, row) and E.evaluate(anc, consts, row))
     assert split > 10
