@@ -710,8 +710,9 @@ def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) ->
     symbol before it (`reads`, in the order the query introduced them; updated here),
     ``Or(Not(i == j), A[@i] == A[@j])``; keccak reads (the second-chance lowering) are also
     injective: ``Or(i == j, Not(f[@i] == f[@j]))`` after it, and ``Or(i == c,
-    Not(f[@i] == k))`` for every stated pair (c, k) -- the lowering maps ``f-1(f(x))`` to ``x``.  The native query
-    compiler makes the same conjuncts in the same order (csrc/query.cpp congruence)."""
+    Not(f[@i] == k))`` for every stated pair (c, k) -- the lowering maps ``f-1(f(x))`` to ``x``.
+    The native query compiler makes the same conjuncts in the same order (csrc/query.cpp
+    congruence)."""
     names = var_names(b)
     cv = b.const_value
     found, work = {}, [x]

@@ -161,7 +161,8 @@ def witness_pins(raws, model, z3) -> list:
     if apps:
         ordered = [apps[i] for i in sorted(apps)]
         for t, v in zip(ordered, model.eval_many(ordered, model_completion=True)):
-            pins.append(t == (z3.BoolVal(bool(v)) if z3.is_bool(t) else z3.BitVecVal(int(v), t.size())))
+            pins.append(t == (z3.BoolVal(bool(v)) if z3.is_bool(t)
+                              else z3.BitVecVal(int(v), t.size())))
     return pins
 
 
