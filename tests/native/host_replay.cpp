@@ -160,6 +160,16 @@ int main(int argc, char** argv) {
                 if ((uint64_t)c.name_off + c.name_len > info.names_len) return fail("column name range");
             }
             sum = mix(sum, &info.flags, sizeof info.flags);
+            // the root boundaries: one per proper prefix, ascending, inside the root tape
+            sum = mix(sum, info.root_ends, (size_t)info.n_root_ends * 4);
+            const uint64_t root_len = info.n_tapes ? info.tape_off[1] : 0;
+            for (uint32_t i = 0; i < info.n_root_ends; ++i)
+                if (info.root_ends[i] == 0 || info.root_ends[i] >= root_len ||
+                    (i && info.root_ends[i] < info.root_ends[i - 1]))
+                    return fail("root_ends");
+            if (info.n_root_ends && info.parent_len != info.root_ends[info.n_root_ends - 1])
+                return fail("parent_len");
+            if (info.n_root_ends && info.n_root_ends + 1 != n) return fail("n_root_ends");
             if (mh_query_free(q) != MH_OK) return fail("query_free");
             break;
         }
