@@ -291,10 +291,9 @@ typedef struct mh_terms mh_terms;
 typedef struct mh_query mh_query;
 /* column kinds; a read (MH_COL_READ / MH_COL_UFREAD: an array's / a tabled function's value at a
  * symbolic index term, Ackermann's reduction; MH_COL_KREAD: a keccak application's value, made
- * only under MH_TERMS_KECCAK_READS, with its 8-bit selector MH_COL_KSEL: 1 switches the value in,
- * else the application is H(x)) carries the index term's node id as its key                    */
+ * only under MH_TERMS_KECCAK_READS) carries the index term's node id as its key                 */
 enum { MH_COL_VAR = 0, MH_COL_CELL = 1, MH_COL_ELSE = 2, MH_COL_UFCELL = 3, MH_COL_UFELSE = 4,
-       MH_COL_READ = 5, MH_COL_UFREAD = 6, MH_COL_KREAD = 7, MH_COL_KSEL = 8 };
+       MH_COL_READ = 5, MH_COL_UFREAD = 6, MH_COL_KREAD = 7 };
 enum { MH_TABLE_CELLS = 0, MH_TABLE_UF_CELLS = 1, MH_TABLE_KECCAK = 2 };
 #define MH_QUERY_DEFINITIONS 1u
 #define MH_QUERY_REFUTED 2u     /* the conjunction contradicts itself syntactically (a FALSE
@@ -354,11 +353,10 @@ typedef struct {
 int32_t mh_terms_create(mh_terms** out);
 int32_t mh_terms_destroy(mh_terms* t);
 /* Session options (lower.py lower_query's keyword arguments; the session's query state is dropped).
- * MH_TERMS_KECCAK_READS: every keccak256_N application is ite(sel == 1, value, H(x)) over columns
- * of its own (MH_COL_KREAD value, MH_COL_KSEL selector) under the stated pairs' ite chain instead
- * of the fixed H(x) = base + ((keccak(x) >> 139) << 6), kept a function and injective by
- * conjuncts (lower.py Lowering._keccak_read / congruence): the sieve's second chance for a query
- * whose keccak values the query pins elsewhere than H.
+ * MH_TERMS_KECCAK_READS: every keccak256_N application is a read column of its own (MH_COL_KREAD)
+ * under the stated pairs' ite chain instead of the fixed H(x) = base + ((keccak(x) >> 139) << 6),
+ * kept a function and injective by conjuncts (lower.py Lowering._keccak_read / congruence): the
+ * sieve's second chance for a query whose keccak values the query pins elsewhere than H.
  * Replaces the reference's keccak_function_manager.py:80-113 hash model for that query.        */
 #define MH_TERMS_KECCAK_READS 1u
 int32_t mh_terms_set_options(mh_terms* t, uint32_t options);

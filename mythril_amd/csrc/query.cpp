@@ -299,7 +299,6 @@ public:
         ccols = std::move(o.ccols);
         cell_index = std::move(o.cell_index);
         read_li = std::move(o.read_li);
-        kterm = std::move(o.kterm);
     }
     // the harvest tables, copied whole (a state keeps one per depth at which its harvest grew)
     struct HarvestCopy {
@@ -609,7 +608,6 @@ public:
             it = cell_index.emplace(name, (uint32_t)ccols.size()).first;
             ccols.push_back(Column{name, sym, w, kind, key != nullptr, key ? *key : Big()});
             read_li.push_back(li);  // a read's index term (the first lowering that made it)
-            kterm.push_back(UINT32_MAX);  // a keccak read's value term (kread_value)
         }
         return add(VAR, w, 0, 0, 0, CELL_COL | it->second);
     }
@@ -795,30 +793,6 @@ public:
         }
         return acc;
     }
-    uint32_t hash_of(const KeccakMap& km, uint32_t a) {  // Lowering._h
-        Big s1, s2;
-        s1.w[0] = KECCAK_SHIFT;
-        s2.w[0] = KECCAK_ALIGN;
-        uint32_t h = add(KECCAK, 256, a);
-        h = add(BVLSHR, 256, h, konst(s1, 256));
-        h = add(BVSHL, 256, h, konst(s2, 256));
-        return km.base.zero() ? h : add(BVADD, 256, h, konst(km.base, 256));
-    }
-    // Lowering._kread_value: the read's value column switched in by its 8-bit selector, else H
-    uint32_t kread_value(const std::string& f, const KeccakMap& km, uint32_t a, uint32_t a_orig) {
-        const std::string idx = std::to_string(a_orig);
-        auto it = cell_index.find(f + "[@" + idx + "]");
-        if (it != cell_index.end() && kterm.at(it->second) != UINT32_MAX) return kterm[it->second];
-        Big ik, one;
-        ik.w[0] = a_orig;
-        one.w[0] = 1;
-        const uint32_t h = hash_of(km, a);
-        const uint32_t v = cell_column(f + "[@" + idx + "]", 256, MH_COL_KREAD, f, &ik, a);
-        const uint32_t o = cell_column(f + "[?" + idx + "]", 8, MH_COL_KSEL, f, &ik);
-        const uint32_t acc = add(ITE, 256, add(EQ, 0, o, konst(one, 8)), v, h);
-        kterm.at(cell_index.at(f + "[@" + idx + "]")) = acc;
-        return acc;
-    }
     uint32_t apply(uint32_t n) {  // Lowering._apply
         const mh_node x = nd(n);
         const std::string& f = fn_name(n);
@@ -831,16 +805,23 @@ public:
             if (x.width != 256)
                 unsupported("keccak function " + f + " has range " + std::to_string(x.width));
             uint32_t acc;
-            if (T.options & MH_TERMS_KECCAK_READS) {
-                // Lowering._keccak_read: ite(f[?a] == 1, f[@a], H(a)) under the pairs' chain
+            if (T.options & MH_TERMS_KECCAK_READS) {  // Lowering._keccak_read: f[@a], free
+                Big ik;
+                ik.w[0] = x.a;
                 const Big* cx = const_value(a);
-                if (cx)  // a stated pair's hash
+                if (cx)  // a stated pair's hash, else a read no pair's ite chain can take
                     for (const auto& pr : km.pairs)
                         if (pr.first == *cx) return konst(pr.second, 256);
-                acc = kread_value(f, km, a, x.a);
-                if (cx) return acc;  // no pair's argument
+                acc = cell_column(f + "[@" + std::to_string(x.a) + "]", 256, MH_COL_KREAD, f, &ik, a);
+                if (cx) return acc;
             } else {
-                acc = hash_of(km, a);
+                Big s1, s2;
+                s1.w[0] = KECCAK_SHIFT;
+                s2.w[0] = KECCAK_ALIGN;
+                uint32_t h = add(KECCAK, 256, a);
+                h = add(BVLSHR, 256, h, konst(s1, 256));
+                h = add(BVSHL, 256, h, konst(s2, 256));
+                acc = km.base.zero() ? h : add(BVADD, 256, h, konst(km.base, 256));
             }
             std::vector<std::pair<Big, Big>> pairs = km.pairs;
             std::sort(pairs.begin(), pairs.end(),
@@ -988,7 +969,6 @@ public:
     std::vector<std::pair<std::string, KeccakMap>> keccak;
     uint64_t hver = 0;          // keccak pairs / bounds changed (harvest_sig)
     std::vector<Column> ccols;  // every cell / else / read column lowering made
-    std::vector<uint32_t> kterm;  // per ccol: a keccak read's value term, else UINT32_MAX
     std::vector<uint32_t> read_li;  // per ccol: a read's lowered index term (else UINT32_MAX)
     std::unordered_map<std::string, uint32_t> cell_index;
     // the root tape
@@ -1615,9 +1595,8 @@ private:
                 const uint32_t q = qreads[qi];
                 const Column& cq = Q.ccols[q];
                 if (cq.symbol != cp.symbol || cq.kind != cp.kind) continue;
-                const bool kr = cp.kind == MH_COL_KREAD;  // the reads' values: selector over H
-                const uint32_t vq = kr ? Q.kterm.at(q) : Q.add(VAR, cq.width, 0, 0, 0, CELL_COL | q);
-                const uint32_t vp = kr ? Q.kterm.at(p) : Q.add(VAR, cp.width, 0, 0, 0, CELL_COL | p);
+                const uint32_t vq = Q.add(VAR, cq.width, 0, 0, 0, CELL_COL | q);
+                const uint32_t vp = Q.add(VAR, cp.width, 0, 0, 0, CELL_COL | p);
                 const uint32_t eqv = Q.add(EQ, 0, vq, vp);
                 const Big* cq_ = Q.const_value(Q.read_li[q]);
                 const Big* cp_ = Q.const_value(Q.read_li[p]);
@@ -1632,7 +1611,7 @@ private:
             }
             if (cp.kind == MH_COL_KREAD) {  // apart from the stated pairs (the inverse reads them)
                 const uint32_t li = Q.read_li[p];
-                const uint32_t vp = Q.kterm.at(p);
+                const uint32_t vp = Q.add(VAR, cp.width, 0, 0, 0, CELL_COL | p);
                 std::vector<std::pair<Big, Big>> pairs = Q.keccak.at(Q.kidx.at(cp.symbol)).second.pairs;
                 std::sort(pairs.begin(), pairs.end(),
                           [](const std::pair<Big, Big>& u, const std::pair<Big, Big>& v) {

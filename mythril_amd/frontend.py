@@ -307,8 +307,6 @@ def z3_column_reader(model, z3):
         return v.as_long() if z3.is_bv_value(v) else None
 
     def value_of(col):
-        if col.kind == "ksel":  # a keccak read's selector: its value column holds z3's value
-            return 1 if col.symbol in decls else None
         if col.kind not in ("var", "cell", "ufcell"):
             return None
         return at(col, col.key)

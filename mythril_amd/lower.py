@@ -70,17 +70,12 @@ class Column:
     name: str             # VAR name in the tape set
     width: int
     kind: str             # "var" | "cell" | "else" | "ufcell" | "ufelse" | "read" | "ufread" |
-                          # "kread" | "ksel"
+                          # "kread"
     symbol: str           # variable / array / function name
     key: Optional[int] = None  # cells: the constant key; reads: the index term's node
 
 
 READ_KINDS = ("read", "ufread", "kread")
-
-
-def ksel_name(sym: str, index_node: int) -> str:
-    """The 8-bit selector column of a keccak read: 1 switches the read's value column in."""
-    return "%s[?%d]" % (sym, index_node)
 
 
 def read_name(sym: str, index_node: int) -> str:
@@ -275,7 +270,6 @@ class Lowering:
         self.frozen = frozen is not None
         self.schema = frozen if frozen is not None else Schema(keccak_reads=keccak_reads)
         self.keccak_reads = self.schema.keccak_reads
-        self.kterm: Dict[str, int] = {}  # keccak read column -> its value term (_keccak_read)
         self.memo: Dict[int, int] = {}
         self.sym = b.symbols
         # read column -> its lowered index term (the congruence conjuncts compare those)
@@ -516,58 +510,38 @@ class Lowering:
 
     def _keccak_read(self, fname: str, km: "KeccakMap", x: int, a_orig: int) -> int:
         """The second-chance form of a keccak application (keccak_reads): the stated pairs'
-        ite chain over ``ite(f[?a] == 1, f[@a], H(x))`` -- a value column of its own that an
-        8-bit selector column switches in, else the default lowering's H(x) (so an application
-        nobody pins keeps a value that follows its argument, is injective and lies in the
-        interval by construction) -- kept a function and injective by the conjuncts of
-        ``congruence`` over those terms.  With a frozen schema (Model.eval) a term the query did
-        not apply f to reads the reads at equal arguments, else H(x)."""
+        ite chain over a read column of its own, ``ite(x == c_i, k_i, f[@a])`` -- free, kept a
+        function and injective by the conjuncts of ``congruence`` -- instead of the fixed
+        H(x).  With a frozen schema (Model.eval) a term the query did not apply f to reads the
+        reads at equal arguments, else H(x)."""
         b = self.b
         cx = b.const_value(x)
         if cx is not None and cx in km.pairs:  # a stated pair: its hash
             return b.const(km.pairs[cx], 256)
         rname = read_name(fname, a_orig)
-        if not self.frozen or rname in self.schema.columns:
+        if cx is not None and (not self.frozen or rname in self.schema.columns):
             if not self.frozen:
                 self.read_index.setdefault(rname, x)
-            acc = self._kread_value(fname, km, x, a_orig)
-            if cx is not None:  # no pair's argument
-                return acc
+            return self._column(rname, 256, "kread", fname, a_orig)  # no pair's argument
+        if not self.frozen:
+            acc = self._column(rname, 256, "kread", fname, a_orig)
+            self.read_index.setdefault(rname, x)
+        elif rname in self.schema.columns:
+            acc = self._column(rname, 256, "kread", fname, a_orig)
         else:
-            acc = self._h(km, x)
+            h = b.op(Op.KECCAK, x)
+            h = b.op(Op.BVLSHR, h, b.const(KECCAK_SHIFT, 256))
+            h = b.op(Op.BVSHL, h, b.const(KECCAK_ALIGN, 256))
+            acc = b.op(Op.BVADD, h, b.const(km.base, 256)) if km.base else h
             reads = sorted((c for c in self.schema.columns.values()
                             if c.kind == "kread" and c.symbol == fname), key=lambda c: c.key)
             for c in reversed(reads):
-                acc = b.op(Op.ITE, self.eq(x, self.lower(c.key)), self.kread_term(c), acc)
+                acc = b.op(Op.ITE, self.eq(x, self.lower(c.key)),
+                           self._column(c.name, 256, "kread", fname, c.key), acc)
         for arg in sorted(km.pairs, reverse=True):
             acc = b.op(Op.ITE, self.eq(x, b.const(arg, b.widths[x])),
                        b.const(km.pairs[arg], 256), acc)
         return acc
-
-    def _h(self, km: "KeccakMap", x: int) -> int:
-        """H(x) = base + ((keccak(x) >> 139) << 6)."""
-        b = self.b
-        h = b.op(Op.KECCAK, x)
-        h = b.op(Op.BVLSHR, h, b.const(KECCAK_SHIFT, 256))
-        h = b.op(Op.BVSHL, h, b.const(KECCAK_ALIGN, 256))
-        return b.op(Op.BVADD, h, b.const(km.base, 256)) if km.base else h
-
-    def _kread_value(self, fname: str, km: "KeccakMap", x: int, a_orig: int) -> int:
-        """``ite(f[?a] == 1, f[@a], H(x))``, made once per read column (kterm)."""
-        rname = read_name(fname, a_orig)
-        acc = self.kterm.get(rname)
-        if acc is None:
-            b = self.b
-            h = self._h(km, x)
-            v = self._column(rname, 256, "kread", fname, a_orig)
-            o = self._column(ksel_name(fname, a_orig), 8, "ksel", fname, a_orig)
-            acc = self.kterm[rname] = b.op(Op.ITE, b.op(Op.EQ, o, b.const(1, 8)), v, h)
-        return acc
-
-    def kread_term(self, c: Column) -> int:
-        """The value term of keccak read column `c` (its selector over H at its argument)."""
-        km = self.schema.keccak.get(c.symbol) or KeccakMap(0)
-        return self._kread_value(c.symbol, km, self.lower(c.key), c.key)
 
     # -- wide equalities: the device compares at most 256 bits ---------------------------------
     def _pieces(self, n: int) -> List[int]:
@@ -757,10 +731,7 @@ def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) ->
         for q in reads:
             if q.symbol == p.symbol and q.kind == p.kind:
                 iq, ip = L.read_index[q.name], L.read_index[p.name]
-                if p.kind == "kread":  # the reads' values: selector over H
-                    eqv = b.op(Op.EQ, L.kterm[q.name], L.kterm[p.name])
-                else:
-                    eqv = b.op(Op.EQ, b.var(q.name, q.width), rp)
+                eqv = b.op(Op.EQ, b.var(q.name, q.width), rp)
                 if p.kind == "kread" and cv(iq) is not None and cv(ip) is not None:
                     # two keccak reads at constant arguments: equal values, or unequal ones
                     out.append(eqv if cv(iq) == cv(ip) else b.op(Op.NOT, eqv))
@@ -772,9 +743,8 @@ def congruence(b: TapeBuilder, L: "Lowering", x: int, reads: list, seen: set) ->
         if p.kind == "kread":  # injective against the stated pairs too (the inverse reads them)
             km = L.schema.keccak[p.symbol]
             li = L.read_index[p.name]
-            rv = L.kterm[p.name]
             for arg in sorted(km.pairs):
-                ne = b.op(Op.NOT, b.op(Op.EQ, rv, b.const(km.pairs[arg], 256)))
+                ne = b.op(Op.NOT, b.op(Op.EQ, rp, b.const(km.pairs[arg], 256)))
                 # a constant argument is no pair's (those lower to the pair's hash)
                 out.append(ne if cv(li) is not None else
                            b.op(Op.OR, L.eq(li, b.const(arg, b.widths[li])), ne))

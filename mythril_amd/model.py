@@ -131,8 +131,7 @@ class Model:
                 continue
             seen.add(c.symbol)
             out.append(Decl(c.symbol, "var" if c.kind == "var" else
-                            "function" if c.kind.startswith("uf") or c.kind in ("kread", "ksel")
-                            else "array"))
+                            "function" if c.kind.startswith("uf") else "array"))
         for f in self.schema.keccak:
             if f not in seen:
                 seen.add(f)
@@ -186,17 +185,11 @@ class Model:
         else_v = self.values.get(els[0].name, 0) if els else 0
         tab = {k: self.values.get(cname, else_v) for k, cname in cells.items()}
         if reads:
-            # a keccak read's value is its selector over H at its argument (lower.py): the
-            # application itself, evaluated with the rest
-            b = self.ctx.b
-            apps = {c.name: b.apply(c.symbol, b.widths[c.key], c.width, c.key)
-                    for c in reads if c.kind == "kread"}
-            at = self._evaluate([c.key for c in reads], list(apps.values()), True)
+            at = self._evaluate([c.key for c in reads], [], True)
             for c in reads:
                 k = int(at[c.key])
                 if k not in cells:
-                    v = at.get(apps[c.name]) if c.name in apps else self.values.get(c.name, 0)
-                    tab.setdefault(k, int(v) if isinstance(v, int) else 0)
+                    tab.setdefault(k, self.values.get(c.name, 0))
         return tab, else_v
 
     def _bool_symbol(self, name: str) -> bool:

@@ -433,8 +433,7 @@ QUERY_COLUMN_DTYPE = np.dtype([("name_off", "<u4"), ("name_len", "<u4"), ("symbo
 QUERY_TABLE_DTYPE = np.dtype([("kind", "<u4"), ("name_off", "<u4"), ("name_len", "<u4"),
                               ("limb_off", "<u4"), ("n_items", "<u4"), ("pad", "<u4")])
 assert QUERY_COLUMN_DTYPE.itemsize == 32 and QUERY_TABLE_DTYPE.itemsize == 24
-COLUMN_KINDS = ("var", "cell", "else", "ufcell", "ufelse", "read", "ufread", "kread",
-                "ksel")  # MH_COL_*
+COLUMN_KINDS = ("var", "cell", "else", "ufcell", "ufelse", "read", "ufread", "kread")  # MH_COL_*
 TERMS_KECCAK_READS = 1  # mh_terms_set_options
 TABLE_CELLS, TABLE_UF_CELLS, TABLE_KECCAK = 0, 1, 2
 QUERY_DEFINITIONS = 1

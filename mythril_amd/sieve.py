@@ -833,16 +833,29 @@ class Sieve:
 
     def _parent_kreads(self, b: TapeBuilder, schema: Schema, base_schema: Schema,
                        parent: Dict[str, int]) -> Dict[str, int]:
-        """The parent's witness with the keccak read selectors of `schema` (the second chance's
-        lowering) it lacks -- a witness of the default lowering has none -- at 0: each
-        application then takes H at its argument, the value the default lowering gave it, and
-        follows the argument wherever the incremental round moves it."""
-        need = [c for c in schema.columns.values() if c.kind == "ksel" and c.name not in parent]
+        """The parent's witness with the keccak read columns of `schema` (the second chance's
+        lowering) it lacks -- a witness of the default lowering has none -- at the values the
+        default lowering gives those applications under it (the stated pair or H(x),
+        `base_schema`; one device batch).  The incremental round's parent rows then satisfy
+        the parent's keccak conjuncts too."""
+        from copy import deepcopy
+
+        from .lower import Lowering, LoweringUnsupported
+
+        need = [c for c in schema.columns.values()
+                if c.kind == "kread" and c.name not in parent]
         if not need:
             return parent
+        try:
+            sc = deepcopy(base_schema)
+            L = Lowering(b, sc)
+            terms = [L.lower(b.apply(c.symbol, b.widths[c.key], 256, c.key)) for c in need]
+            vals = self.eval_terms(b, terms, list(sc.columns) or ["__ground__"], parent)
+        except (LoweringUnsupported, native.Unsupported, TapeError):
+            return parent
         out = dict(parent)
-        for c in need:
-            out[c.name] = 0
+        for c, v in zip(need, vals):
+            out[c.name] = v
         self.stats.extra["parent_kreads"] = self.stats.extra.get("parent_kreads", 0) + 1
         return out
 

@@ -70,8 +70,6 @@ def planted_value(m, ctx=None):
         if ctx is not None and col.kind == "read" and col.symbol in m.arrays:
             table, els = m.arrays[col.symbol]
             return table.get(at(col.key), els)
-        if col.kind == "ksel" and col.symbol in m.funcs:  # the value column holds M's value
-            return 1
         if ctx is not None and col.kind in ("ufread", "kread") and col.symbol in m.funcs:
             return m.funcs[col.symbol](at(col.key))
         return None

@@ -62,11 +62,9 @@ def model_of(schema, row, b=None):
         assert b is not None, "a model with read columns needs the builder"
         at = read_index_values(b, schema, row)
         for c in reads:
-            if c.kind == "kread":  # keccak reads (second-chance lowering): f at the argument,
-                # the value column where the selector switches it in, else H there
+            if c.kind == "kread":  # keccak reads (second-chance lowering): f at the argument
                 pairs = schema.keccak[c.symbol].pairs
-                sel = row.get("%s[?%d]" % (c.symbol, c.key), 0)
-                if at[c.name] not in pairs and sel == 1:
+                if at[c.name] not in pairs:
                     kread_pts.setdefault(c.symbol, {}).setdefault(at[c.name], row.get(c.name, 0))
                 continue
             tabs = arrays if c.kind == "read" else uf_tabs
@@ -393,8 +391,6 @@ def test_keccak_pinned_at_a_symbolic_argument():
                 for c in schema.columns.values():
                     if c.kind == "kread":
                         row[c.name] = 0x1234 << 64
-                    elif c.kind == "ksel":
-                        row[c.name] = 1
                 assign = [row.get(n, 0) for n in names]
                 hits += bool(E.evaluate(tape.nodes, ctx.b.pool.values, assign))
         assert (hits > 0) == sat, (sat, hits)
