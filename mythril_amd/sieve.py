@@ -33,7 +33,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import native
-from .lower import Column, KeccakMap, Schema, cell_name, lower_query, node_columns
+from .lower import (Column, KeccakMap, LoweringUnsupported, Schema, cell_name, lower_query,
+                    node_columns)
 from .tape import NODE_DTYPE, Op, Tape, TapeBuilder, TapeError, TapeSet
 
 
@@ -790,7 +791,14 @@ class Sieve:
                 and time.perf_counter() - t0 < budget):
             st.extra["keccak2_tries"] = st.extra.get("keccak2_tries", 0) + 1
             first = self.last_rounds
-            w, schema2, _ = self._attempt(b, roots, key, budget, t0, True, base_schema=schema)
+            try:
+                w, schema2, _ = self._attempt(b, roots, key, budget, t0, True,
+                                              base_schema=schema)
+            except (LoweringUnsupported, native.Unsupported):
+                # a shape the second lowering cannot take (register pressure of its larger
+                # tapes, ...): the first attempt's miss stands
+                st.extra["keccak2_unsupported"] = st.extra.get("keccak2_unsupported", 0) + 1
+                w = None
             self.last_rounds = dict(first, keccak2=int(w is not None))
             if w is not None:
                 st.extra["keccak2_hits"] = st.extra.get("keccak2_hits", 0) + 1

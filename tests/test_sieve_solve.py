@@ -6,7 +6,7 @@ reference's own outcome cases (tests/reference_cases.py) through frontend.get_mo
 """
 import pytest
 
-from mythril_amd import frontend
+from mythril_amd import frontend, native
 from mythril_amd.model import Model
 from mythril_amd.sieve import Sieve
 from tests import fake_device
@@ -458,3 +458,22 @@ def test_fallback_model_learns_read_columns(monkeypatch):
         assert (m.values["x"], m.values["y"], m.values["z"]) == (x0, y0, 7)
     finally:
         frontend.reset()
+
+
+def test_second_chance_that_cannot_lower_leaves_the_miss(monkeypatch):
+    """A second-chance lowering the compiler refuses (register pressure of its larger tapes)
+    leaves the first attempt's miss: solve returns None instead of raising, counted."""
+    fake_device.install(monkeypatch)
+    ctx, cs = _pinned_keccak_query()
+    nodes = [c.node for c in cs]
+    s = Sieve(rows=256, budget_s=60.0)
+    real = s._attempt
+
+    def attempt(*a, **k):
+        if a[5]:  # keccak_reads
+            raise native.Unsupported(-3, "register pressure")
+        return real(*a, **k)
+
+    monkeypatch.setattr(s, "_attempt", attempt)
+    assert s.solve(ctx.b, nodes) is None
+    assert s.stats.extra["keccak2_unsupported"] == 1 and s.stats.misses == 1
