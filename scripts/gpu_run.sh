@@ -43,6 +43,8 @@
 #   grecall   tests/test_gpu_recall.py with its printed numbers (-s)
 #   incrows   planted_recall with 16384 / 65536-row incremental rounds (SIEVE_INC_ROWS)
 #   inchops   planted_recall with the parent's column-sharing conjuncts in the incremental guide
+#   inc16k    planted_recall, path_scaling and sieve_queries with 16384-row incremental rounds,
+#             then path_scaling and sieve_queries at the default on the same box
 #   recall0   planted_recall without the keccak second chance (SIEVE_KECCAK2=0), no extended pass
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
 #             (SIEVE_ROUND2=progress) and never run (recall only)
@@ -109,6 +111,11 @@ for step in "$@"; do
     grecall)  timeout -k 10 600 python -u -m pytest -x -v -s --timeout 500 --timeout-method thread -m gpu tests/test_gpu_recall.py > "$OUT/pytest_recall.txt" 2>&1 ;;
     incrows)  for r in 16384 65536; do SIEVE_INC_ROWS=$r timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_inc$r.jsonl" 2> "$OUT/planted_recall_inc$r.log" || exit 1; done ;;
     inchops)  SIEVE_INC_HOPS=1 timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_hops1.jsonl" 2> "$OUT/planted_recall_hops1.log" ;;
+    inc16k)   SIEVE_INC_ROWS=16384 timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_inc16k.jsonl" 2> "$OUT/planted_recall_inc16k.log" && \
+              SIEVE_INC_ROWS=16384 timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_inc16k.jsonl" 2> "$OUT/path_scaling_inc16k.log" && \
+              SIEVE_INC_ROWS=16384 SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_inc16k.jsonl" 2> "$OUT/sieve_queries_inc16k.log" && \
+              timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" && \
+              SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries.jsonl" 2> "$OUT/sieve_queries.log" ;;
     recall0)  SIEVE_KECCAK2=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_nok2.jsonl" 2> "$OUT/planted_recall_nok2.log" ;;
     round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
               timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \
