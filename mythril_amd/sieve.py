@@ -464,7 +464,10 @@ class Sieve:
         # the second round of a query whose parent has a witness: the parent's witness under
         # the newest root's conjuncts (SIEVE_INCREMENTAL=0: the 2^16-row full-guide round)
         self.incremental_round = os.environ.get("SIEVE_INCREMENTAL", "1") != "0"
-        self.inc_rows = int(os.environ.get("SIEVE_INC_ROWS", "4096"))  # its rows
+        # its rows: 16384 (256 one-wave workgroups, one per CU: a round's latency-bound cost
+        # barely moves) answered 1.5 points more of the random family than 4096, LASER-shaped
+        # latency unchanged (profiles/r06s)
+        self.inc_rows = int(os.environ.get("SIEVE_INC_ROWS", "16384"))
         self.inc_hops = int(os.environ.get("SIEVE_INC_HOPS", "0"))  # newest_tape(hops)
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)
         self.last_rounds: Dict[str, int] = {}
