@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 # measured on MI355X on this workload (20 paths x 16 constraint attempts, seeds 0..19):
 # LASER 1.000 (326 queries), random 0.653 (455; profiles/r05d/pytest_recall.txt); round 6 (read
 # columns, the keccak second chance, the incremental second round): random 0.723, 0.925 with
-# the fallback's models learnt (profiles/r06h/pytest_recall.txt)
+# the fallback's models learnt (profiles/r06h/pytest_recall.txt); final build 0.758 / 0.947
+# (profiles/r06t/pytest_recall.txt)
 FLOOR = {"laser": 0.99, "random": 0.70}
 FLOOR_LEARNT = 0.90
 
