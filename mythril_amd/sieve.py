@@ -469,6 +469,8 @@ class Sieve:
         # latency unchanged (profiles/r06s)
         self.inc_rows = int(os.environ.get("SIEVE_INC_ROWS", "16384"))
         self.inc_hops = int(os.environ.get("SIEVE_INC_HOPS", "0"))  # newest_tape(hops)
+        # after the incremental round, the 2^16-row round of the full guide (SIEVE_ROUND3=1)
+        self.round3 = os.environ.get("SIEVE_ROUND3", "0") == "1"
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)
         self.last_rounds: Dict[str, int] = {}
         self.seed = seed
@@ -924,6 +926,7 @@ class Sieve:
             raise
         t_c = time.perf_counter()
         round_guide = guide  # the incremental round's own guide replaces it (closed below)
+        inc_guide = None
         ft, nt = getattr(ct, "timing", (0.0, 0.0))
         st.add("compile_flatten", ft)
         st.add("compile_native", nt)
@@ -945,7 +948,11 @@ class Sieve:
             self.last_rounds = {"groups": len(group_cols), "r1_solved": 0, "rounds": 0}
             if keccak_reads and not inc_ok:  # the second chance: one first round
                 launches = launches[:1]
+            if inc_ok and self.round3 and self.max_rounds > 1 and not keccak_reads:
+                launches.append((self.max_rounds - 1) * self.rows)  # then the full guide's
             for rnd, n in enumerate(launches):
+                if rnd == 2:
+                    round_guide = guide
                 if rnd == 1:
                     k = sum(solved)
                     self.last_rounds["r1_solved"] = k
@@ -963,7 +970,7 @@ class Sieve:
                         if keccak_reads and base_schema is not None \
                                 and base_schema is not REFUTED:
                             pv = self._parent_kreads(b, schema, base_schema, parent)
-                        round_guide = native.harvest_guide(
+                        round_guide = inc_guide = native.harvest_guide(
                             inc, ts.pool.to_array(), widths,
                             [(col_index[k], v) for k, v in pv.items() if k in col_index],
                             keep=True)
@@ -1017,8 +1024,8 @@ class Sieve:
         finally:
             ct.close()
             guide.close()
-            if round_guide is not guide:
-                round_guide.close()
+            if inc_guide is not None:
+                inc_guide.close()
             self.stats.device_s += time.perf_counter() - t1
 
 

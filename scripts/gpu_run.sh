@@ -45,6 +45,8 @@
 #   inchops   planted_recall with the parent's column-sharing conjuncts in the incremental guide
 #   inc16k    planted_recall, path_scaling and sieve_queries with 16384-row incremental rounds,
 #             then path_scaling and sieve_queries at the default on the same box
+#   round3    planted_recall and path_scaling with a third round (the full guide's 2^16 rows after
+#             the incremental round, SIEVE_ROUND3=1), then path_scaling at the default
 #   recall0   planted_recall without the keccak second chance (SIEVE_KECCAK2=0), no extended pass
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
 #             (SIEVE_ROUND2=progress) and never run (recall only)
@@ -116,6 +118,9 @@ for step in "$@"; do
               SIEVE_INC_ROWS=16384 SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries_inc16k.jsonl" 2> "$OUT/sieve_queries_inc16k.log" && \
               timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" && \
               SIEVE_QUERY_REPS=9 timeout -k 10 300 python -u scripts/sieve_queries.py > "$OUT/sieve_queries.jsonl" 2> "$OUT/sieve_queries.log" ;;
+    round3)   SIEVE_ROUND3=1 timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_r3.jsonl" 2> "$OUT/planted_recall_r3.log" && \
+              SIEVE_ROUND3=1 timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_r3.jsonl" 2> "$OUT/path_scaling_r3.log" && \
+              timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" ;;
     recall0)  SIEVE_KECCAK2=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_nok2.jsonl" 2> "$OUT/planted_recall_nok2.log" ;;
     round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
               timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \
