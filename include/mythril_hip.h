@@ -204,6 +204,16 @@ int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, const uint32_t*
                          uint32_t n_consts, const uint16_t* col_width, uint32_t n_cols,
                          const uint32_t* parent_cols, const uint32_t* parent_vals,
                          uint32_t n_parent, mh_harvest** out, mh_guide* guide);
+/* mh_guide_harvest for the incremental round (sieve.newest_tape: the conjuncts a query adds to its
+ * parent's): an operand every column of which the parent witness fixes, built from the bit-layout
+ * and linear ops, counts as known beside constants when the other side of an arithmetic op, an
+ * equality or a comparison is solved for -- so `x + y == k` proposes x = k - y(parent) where the
+ * plain harvest proposes nothing.  Stateless; the same arrays as candidates.build_guide(...,
+ * parent_eval=True).                                                                           */
+int32_t mh_guide_harvest_inc(const mh_node* nodes, uint32_t n_nodes, const uint32_t* consts,
+                             uint32_t n_consts, const uint16_t* col_width, uint32_t n_cols,
+                             const uint32_t* parent_cols, const uint32_t* parent_vals,
+                             uint32_t n_parent, mh_harvest** out, mh_guide* guide);
 int32_t mh_harvest_free(mh_harvest* h);
 /* The same harvest by a session kept across a path's queries: when the tape, the constants and
  * the column widths extend the last call's (a LASER child whose new constraint left its parent's

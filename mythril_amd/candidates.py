@@ -177,8 +177,14 @@ def _prune_hints(hints: List[Tuple[int, List[Alt]]]) -> List[Tuple[int, List[Alt
 
 
 class Harvester:
-    def __init__(self, b: TapeBuilder, schema: Schema, columns: Sequence[str]):
+    def __init__(self, b: TapeBuilder, schema: Schema, columns: Sequence[str],
+                 parent_eval: bool = False):
         self.b = b
+        # parent_eval (mh_guide_harvest_inc): operands the parent witness fixes count as known
+        # (_pick); set from harvest()'s parent, with a memo of this harvest's own
+        self.parent_eval = parent_eval
+        self._parent: Optional[Dict[str, int]] = None
+        self._pv: Dict[int, Optional[int]] = {}
         self.schema = schema
         self.columns = list(columns)
         # every VAR under a lowered query is one of its columns
@@ -187,12 +193,95 @@ class Harvester:
         self.sets: List[Tuple[int, List[Alt]]] = []
         # inversions by (node, value, mask) / (node, truth), with the hints each produced
         # (transitively), so a memo hit replays them exactly as a fresh inversion would
-        self._inv_memo: Dict[tuple, tuple] = _memo(b, "_guide_inv")
+        self._inv_memo: Dict[tuple, tuple] = {} if parent_eval else _memo(b, "_guide_inv")
         self._cap: List[list] = []
         self._consts_by_width: Dict[int, List[int]] = {}
         self.hints: List[Tuple[int, List[Alt]]] = []
         self.copy_sets: List[List[List[Copy]]] = []
         self._hint_keys = set()
+
+    def _pick(self, a: int, bb: int, a_first: bool = False) -> Optional[Tuple[int, int]]:
+        """(the operand to solve for, the other side's value): a constant first (a before b
+        with `a_first`, else b before a), then with ``parent_eval`` a side the parent witness
+        fixes, b before a (csrc/harvest.cpp Harvester::pick)."""
+        cv = self.b.const_value
+        if a_first and cv(a) is not None:
+            return bb, cv(a)
+        if cv(bb) is not None:
+            return a, cv(bb)
+        if cv(a) is not None:
+            return bb, cv(a)
+        if self._parent is not None:
+            pb = self._parent_value(bb)
+            if pb is not None:
+                return a, pb
+            pa = self._parent_value(a)
+            if pa is not None:
+                return bb, pa
+        return None
+
+    def _parent_value(self, root: int) -> Optional[int]:
+        """The value of term `root` under the parent witness, when every column it reads has
+        a parent value and every op is a bit-layout or linear one; else None (memoised)."""
+        b, memo = self.b, self._pv
+        if root in memo:
+            return memo[root]
+        st = [(root, False)]
+        un = (Op.BVNOT, Op.BVNEG, Op.ZEXT, Op.EXTRACT)
+        bin_ = (Op.BVADD, Op.BVSUB, Op.BVXOR, Op.BVAND, Op.BVOR, Op.BVMUL, Op.CONCAT)
+        while st:
+            n, done = st.pop()
+            if n in memo:
+                continue
+            op, w, a, bb, _, i0, i1 = b.nodes[n]
+            c = b.const_value(n)
+            if c is not None:
+                memo[n] = c
+                continue
+            if op == Op.VAR:
+                name = self.col_of_var.get(i0)
+                v = self._parent.get(name) if name is not None else None
+                memo[n] = None if v is None else v & _mask(w)
+                continue
+            if op not in un and op not in bin_:
+                memo[n] = None
+                continue
+            if not done:
+                st.append((n, True))
+                st.append((a, False))
+                if op in bin_:
+                    st.append((bb, False))
+                continue
+            va = memo.get(a)
+            vb = memo.get(bb) if op in bin_ else 0
+            if va is None or vb is None:
+                memo[n] = None
+                continue
+            m = _mask(w)
+            if op == Op.BVNOT:
+                v = ~va & m
+            elif op == Op.BVNEG:
+                v = -va & m
+            elif op == Op.ZEXT:
+                v = va
+            elif op == Op.EXTRACT:
+                v = (va >> i1) & m
+            elif op == Op.BVADD:
+                v = (va + vb) & m
+            elif op == Op.BVSUB:
+                v = (va - vb) & m
+            elif op == Op.BVXOR:
+                v = va ^ vb
+            elif op == Op.BVAND:
+                v = va & vb
+            elif op == Op.BVOR:
+                v = va | vb
+            elif op == Op.BVMUL:
+                v = (va * vb) & m
+            else:  # CONCAT
+                v = (va << b.widths[bb]) | vb
+            memo[n] = v
+        return memo[root]
 
     def _memoised(self, key: tuple, compute):
         got = self._inv_memo.get(key)
@@ -278,13 +367,10 @@ class Harvester:
             return None
         m = _mask(w)
         if op in (Op.BVADD, Op.BVSUB, Op.BVXOR, Op.BVMUL):
-            ka, kb = b.const_value(a), b.const_value(bb)
-            if kb is not None:
-                x, k = a, kb
-            elif ka is not None:
-                x, k = bb, ka
-            else:
+            got = self._pick(a, bb)
+            if got is None:
                 return None
+            x, k = got
             if op == Op.BVADD:
                 t = value - k
             elif op == Op.BVSUB:
@@ -345,10 +431,10 @@ class Harvester:
         if op == Op.EQ:
             if b.widths[a] == BOOL:
                 return None
-            ka, kb = b.const_value(a), b.const_value(bb)
-            t, k = (a, kb) if kb is not None else (bb, ka)
-            if k is None:
+            got = self._pick(a, bb)
+            if got is None:
                 return None
+            t, k = got
             if truth:
                 return self.invert_bits(t, k, _mask(b.widths[t]))
             return [{}]  # t != K: almost every value satisfies it
@@ -370,12 +456,11 @@ class Harvester:
             return out[:MAX_ALTS] if out else None
         if op in (Op.BVULT, Op.BVULE, Op.BVUGT, Op.BVUGE, Op.BVSLT, Op.BVSLE, Op.BVSGT,
                   Op.BVSGE):
-            ka, kb = b.const_value(a), b.const_value(bb)
-            if ka is None and kb is None:
+            got = self._pick(a, bb, a_first=True)
+            if got is None:
                 return None
             wt = b.widths[a]
-            t = bb if ka is not None else a
-            k = ka if ka is not None else kb
+            t, k = got
             out = []
             for v in self._boundary(Op(op), k, t == a, truth, wt):
                 r = self.invert_bits(t, v, _mask(wt))
@@ -520,6 +605,8 @@ class Harvester:
                 got = consts_of[conj] = frozenset(got)
             qc |= got
         alt = {k: v for k, v in parent.items() if k in self.pools} if parent else {}
+        if self.parent_eval:
+            self._parent = alt
         if alt:
             self.sets.append((PROB_PARENT, [alt]))
         seen_eq = set()
@@ -704,5 +791,5 @@ class Harvester:
 
 
 def build_guide(b: TapeBuilder, root: int, schema: Schema, columns: Sequence[str],
-                parent: Optional[Alt] = None) -> Guide:
-    return Harvester(b, schema, columns).harvest(root, parent)
+                parent: Optional[Alt] = None, parent_eval: bool = False) -> Guide:
+    return Harvester(b, schema, columns, parent_eval).harvest(root, parent)

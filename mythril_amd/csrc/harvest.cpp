@@ -37,7 +37,8 @@ constexpr uint32_t kCopyFlag = 0x80000000u;
 enum : uint8_t {
     CONST = MH_OP_CONST, VAR = MH_OP_VAR, TRUE_ = MH_OP_TRUE, FALSE_ = MH_OP_FALSE,
     BVADD = MH_OP_BVADD, BVSUB = MH_OP_BVSUB, BVMUL = MH_OP_BVMUL, BVNEG = MH_OP_BVNEG,
-    BVNOT = MH_OP_BVNOT, BVAND = MH_OP_BVAND, BVXOR = MH_OP_BVXOR, BVSHL = MH_OP_BVSHL,
+    BVNOT = MH_OP_BVNOT, BVAND = MH_OP_BVAND, BVOR = MH_OP_BVOR, BVXOR = MH_OP_BVXOR,
+    BVSHL = MH_OP_BVSHL,
     BVLSHR = MH_OP_BVLSHR, EQ = MH_OP_EQ, BVULT = MH_OP_BVULT, BVULE = MH_OP_BVULE,
     BVUGT = MH_OP_BVUGT, BVUGE = MH_OP_BVUGE, BVSLT = MH_OP_BVSLT, BVSLE = MH_OP_BVSLE,
     BVSGT = MH_OP_BVSGT, BVSGE = MH_OP_BVSGE, AND = MH_OP_AND, OR = MH_OP_OR, NOT = MH_OP_NOT,
@@ -400,6 +401,89 @@ struct Harvester {
             default: return 2;
         }
     }
+    // mh_guide_harvest_inc: an operand whose value the parent witness fixes (every column it
+    // reads has a parent value, every op is one of the bit-layout / linear ops below) counts as
+    // known when the other side of an arithmetic op, an equality or a comparison must be
+    // solved for -- the incremental round's guide then moves one side and keeps the other where
+    // the parent had it (candidates.Harvester parent_eval, the same rule)
+    bool peval = false;
+    std::unordered_map<uint32_t, U> parent_of;  // column -> parent value
+    std::vector<uint8_t> pv_state;                // 0 unknown, 1 known, 2 not
+    std::vector<U> pv;
+    const U* parent_value(uint32_t root) {
+        if (!peval) return nullptr;
+        if (pv_state.size() < nd.size()) {
+            pv_state.resize(nd.size(), 0);
+            pv.resize(nd.size());
+        }
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        while (!st.empty()) {
+            const auto [n, done] = st.back();
+            st.pop_back();
+            if (pv_state[n]) continue;
+            const Node x = nd[n];
+            if (const U* c = const_value(n)) {
+                pv[n] = *c;
+                pv_state[n] = 1;
+                continue;
+            }
+            const bool un = x.op == BVNOT || x.op == BVNEG || x.op == ZEXT || x.op == EXTRACT;
+            const bool bin = x.op == BVADD || x.op == BVSUB || x.op == BVXOR || x.op == BVAND ||
+                             x.op == BVOR || x.op == BVMUL || x.op == CONCAT;
+            if (x.op == VAR) {
+                auto it = x.imm0 < n_cols ? parent_of.find(x.imm0) : parent_of.end();
+                pv_state[n] = it == parent_of.end() ? 2 : 1;
+                if (it != parent_of.end()) pv[n] = it->second & mask(x.width);
+                continue;
+            }
+            if (!un && !bin) {
+                pv_state[n] = 2;
+                continue;
+            }
+            if (!done) {
+                st.push_back({n, true});
+                st.push_back({x.a, false});
+                if (bin) st.push_back({x.b, false});
+                continue;
+            }
+            if (pv_state[x.a] != 1 || (bin && pv_state[x.b] != 1)) {
+                pv_state[n] = 2;
+                continue;
+            }
+            const U& a = pv[x.a];
+            const U m = mask(x.width);
+            U v;
+            switch (x.op) {
+                case BVNOT: v = ~a & m; break;
+                case BVNEG: v = neg(a) & m; break;
+                case ZEXT: v = a; break;
+                case EXTRACT: v = shr(a, (int)x.imm1) & m; break;
+                case BVADD: v = (a + pv[x.b]) & m; break;
+                case BVSUB: v = (a - pv[x.b]) & m; break;
+                case BVXOR: v = (a ^ pv[x.b]) & m; break;
+                case BVAND: v = a & pv[x.b]; break;
+                case BVOR: v = a | pv[x.b]; break;
+                case BVMUL: v = (a * pv[x.b]) & m; break;
+                default: v = shl(a, nd[x.b].width) | pv[x.b]; break;  // CONCAT
+            }
+            pv[n] = v;
+            pv_state[n] = 1;
+        }
+        return pv_state[root] == 1 ? &pv[root] : nullptr;
+    }
+    // the operand to solve for and the other side's value: a constant first (either side), then
+    // (peval) a side the parent fixes, b before a
+    // (a_first: a constant a before a constant b, the comparisons' order)
+    bool pick(uint32_t a, uint32_t b, uint32_t& t, U& k, bool a_first = false) {
+        if (a_first)
+            if (const U* ka = const_value(a)) { t = b; k = *ka; return true; }
+        if (const U* kb = const_value(b)) { t = a; k = *kb; return true; }
+        if (const U* ka = const_value(a)) { t = b; k = *ka; return true; }
+        if (const U* pb = parent_value(b)) { t = a; k = *pb; return true; }
+        if (const U* pa = parent_value(a)) { t = b; k = *pa; return true; }
+        return false;
+    }
+
     const U* const_value(uint32_t n) {
         if (cv_state[n] == 0) {
             const Node& x = nd[n];
@@ -538,13 +622,9 @@ struct Harvester {
         if (!full) return none_();
         const U m = mask(x.width);
         if (x.op == BVADD || x.op == BVSUB || x.op == BVXOR || x.op == BVMUL) {
-            const U* ka = const_value(x.a);
-            const U* kb = const_value(x.b);
             uint32_t t;
             U k;
-            if (kb) { t = x.a; k = *kb; }
-            else if (ka) { t = x.b; k = *ka; }
-            else return none_();
+            if (!pick(x.a, x.b, t, k)) return none_();
             U v;
             if (x.op == BVADD) v = value - k;
             else if (x.op == BVSUB) v = t == x.a ? value + k : k - value;
@@ -600,13 +680,10 @@ struct Harvester {
         }
         if (x.op == EQ) {
             if (nd[x.a].width == 0) return none_();
-            const U* ka = const_value(x.a);
-            const U* kb = const_value(x.b);
             uint32_t t;
-            const U* k;
-            if (kb) { t = x.a; k = kb; } else { t = x.b; k = ka; }
-            if (!k) return none_();
-            if (truth) return invert_bits(t, *k, mask(nd[t].width));
+            U k;
+            if (!pick(x.a, x.b, t, k)) return none_();
+            if (truth) return invert_bits(t, k, mask(nd[t].width));
             return one_empty();
         }
         if (x.op == ADD_NOOVFL_U || x.op == MUL_NOOVFL_U || x.op == SUB_NOUDFL_U) {
@@ -633,12 +710,10 @@ struct Harvester {
             return of(head(out, kMaxAlts));
         }
         if (x.op >= BVULT && x.op <= BVSGE) {
-            const U* ka = const_value(x.a);
-            const U* kb = const_value(x.b);
-            if (!ka && !kb) return none_();
             const int wt = nd[x.a].width;
-            const uint32_t t = ka ? x.b : x.a;
-            const U k = ka ? *ka : *kb;
+            uint32_t t;
+            U k;
+            if (!pick(x.a, x.b, t, k, true)) return none_();
             Alts out;
             for (const U& v : boundary(x.op, k, t == x.a, truth, wt)) {
                 Res r = invert_bits(t, v, mask(wt));
@@ -1208,6 +1283,11 @@ int32_t harvest_into(Harvester& h, const mh_node* nodes, uint32_t n_nodes, const
         V v;
         for (int k = 0; k < 8; ++k) v.w[k] = parent_vals[8ull * i + k];
         parent.push_back({parent_cols[i], v});
+        if (h.peval) {  // a later pair of one column wins, as in the parent set
+            U u = U::of(0);
+            for (int k = 0; k < 8; ++k) u.w[k] = v.w[k];
+            h.parent_of[parent_cols[i]] = u;
+        }
     }
     std::vector<std::vector<V>> pools;
     std::vector<std::pair<int, const Alts*>> sets;
@@ -1340,6 +1420,32 @@ extern "C" int32_t mh_guide_harvest(const mh_node* nodes, uint32_t n_nodes, cons
             ~ArenaReset() { g_arena.reset(); }
         } arena_reset;
         Harvester h;
+        return harvest_into(h, nodes, n_nodes, consts, n_consts, col_width, n_cols, parent_cols,
+                            parent_vals, n_parent, out, guide);
+    } catch (const std::bad_alloc&) {
+        return mh_detail_set_err(MH_E_NOMEM, "host allocation failed");
+    }
+}
+
+// mh_guide_harvest with the parent witness fixing what it can evaluate (Harvester::peval): the
+// incremental round's guide (sieve.newest_tape), stateless like mh_guide_harvest.
+extern "C" int32_t mh_guide_harvest_inc(const mh_node* nodes, uint32_t n_nodes,
+                                        const uint32_t* consts, uint32_t n_consts,
+                                        const uint16_t* col_width, uint32_t n_cols,
+                                        const uint32_t* parent_cols, const uint32_t* parent_vals,
+                                        uint32_t n_parent, mh_harvest** out, mh_guide* guide) {
+    if (!out || !guide) return mh_detail_set_err(MH_E_INVALID, "null out pointer");
+    *out = nullptr;
+    if (!check_args(nodes, n_nodes, consts, n_consts, col_width, n_cols, parent_cols, parent_vals,
+                    n_parent))
+        return mh_detail_set_err(MH_E_INVALID, "null or empty argument");
+    try {
+        UseArena use(&g_arena);
+        struct ArenaReset {
+            ~ArenaReset() { g_arena.reset(); }
+        } arena_reset;
+        Harvester h;
+        h.peval = true;
         return harvest_into(h, nodes, n_nodes, consts, n_consts, col_width, n_cols, parent_cols,
                             parent_vals, n_parent, out, guide);
     } catch (const std::bad_alloc&) {

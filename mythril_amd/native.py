@@ -98,6 +98,9 @@ SIGNATURES = {
     "mh_ctx_kernel_time": (C.c_int32, [_vp, C.POINTER(C.c_double), _u64p]),
     "mh_guide_harvest": (C.c_int32, [_vp, C.c_uint32, _u32p, C.c_uint32, C.POINTER(C.c_uint16),
                                      C.c_uint32, _u32p, _u32p, C.c_uint32, C.POINTER(_vp), _vp]),
+    "mh_guide_harvest_inc": (C.c_int32, [_vp, C.c_uint32, _u32p, C.c_uint32,
+                                         C.POINTER(C.c_uint16), C.c_uint32, _u32p, _u32p,
+                                         C.c_uint32, C.POINTER(_vp), _vp]),
     "mh_harvest_free": (C.c_int32, [_vp]),
     "mh_harvester_create": (C.c_int32, [C.POINTER(_vp)]),
     "mh_harvester_destroy": (C.c_int32, [_vp]),
@@ -259,7 +262,7 @@ class GuideHandle:
 
 def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
                   parent: Sequence[Tuple[int, int]] = (), session: "Optional[GuideSession]" = None,
-                  keep: bool = False):
+                  keep: bool = False, parent_eval: bool = False):
     """mh_guide_harvest: the guide of one lowered query tape (root last, VAR imm0 = column,
     CONST imm0 = row of `consts`), as the arrays candidates.Guide.arrays() gives -- the same
     values (tests/test_harvest.py).  `parent` = the parent witness as (column, value) pairs in
@@ -278,7 +281,11 @@ def harvest_guide(nodes: np.ndarray, consts: np.ndarray, widths: Sequence[int],
     args = (nodes.ctypes.data, len(nodes), _ptr(consts), len(consts),
             w.ctypes.data_as(C.POINTER(C.c_uint16)), len(w), _ptr(pc), _ptr(pv), len(pc),
             C.byref(h), C.byref(g))
-    if session is None:
+    if parent_eval:  # mh_guide_harvest_inc: operands the parent fixes count as known
+        if session is not None:
+            raise ValueError("parent_eval harvests are stateless")
+        _check(lib.mh_guide_harvest_inc(*args))
+    elif session is None:
         _check(lib.mh_guide_harvest(*args))
     else:
         _check(lib.mh_guide_harvest_with(session.h, *args))

@@ -469,6 +469,9 @@ class Sieve:
         # latency unchanged (profiles/r06s)
         self.inc_rows = int(os.environ.get("SIEVE_INC_ROWS", "16384"))
         self.inc_hops = int(os.environ.get("SIEVE_INC_HOPS", "0"))  # newest_tape(hops)
+        # its guide solves for one side of x op y == k with the other at the parent's value
+        # (mh_guide_harvest_inc; SIEVE_INC_PEVAL=0: the plain harvest)
+        self.inc_parent_eval = os.environ.get("SIEVE_INC_PEVAL", "1") != "0"
         # after the incremental round, the 2^16-row round of the full guide (SIEVE_ROUND3=1)
         self.round3 = os.environ.get("SIEVE_ROUND3", "0") == "1"
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)
@@ -973,7 +976,7 @@ class Sieve:
                         round_guide = inc_guide = native.harvest_guide(
                             inc, ts.pool.to_array(), widths,
                             [(col_index[k], v) for k, v in pv.items() if k in col_index],
-                            keep=True)
+                            keep=True, parent_eval=self.inc_parent_eval)
                         st.add("guide", time.perf_counter() - ti)
                         st.extra["inc_rounds"] = st.extra.get("inc_rounds", 0) + 1
                         self.last_rounds["incremental"] = 1

@@ -187,7 +187,8 @@ int main(int argc, char** argv) {
             break;
         }
         case 'G':
-        case 'g': {
+        case 'g':
+        case 'i': {
             const uint32_t nn = r.get<uint32_t>();
             auto nodes = copy_of<mh_node>(r.take((size_t)nn * sizeof(mh_node)), nn);
             const uint32_t nc = r.get<uint32_t>();
@@ -206,6 +207,9 @@ int main(int argc, char** argv) {
                 if (it == harvesters.end()) return fail("guide: unknown session");
                 rc = mh_guide_harvest_with(it->second, nodes.data(), nn, consts.data(), nc,
                                            widths.data(), ncol, pcols.data(), pvals.data(), np, &h, &g);
+            } else if (kind == 'i') {  // the incremental round's parent-evaluating harvest
+                rc = mh_guide_harvest_inc(nodes.data(), nn, consts.data(), nc, widths.data(), ncol,
+                                          pcols.data(), pvals.data(), np, &h, &g);
             } else {
                 rc = mh_guide_harvest(nodes.data(), nn, consts.data(), nc, widths.data(), ncol,
                                       pcols.data(), pvals.data(), np, &h, &g);

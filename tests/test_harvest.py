@@ -39,17 +39,18 @@ def _parent_of(cols, widths, salt: str):
     return out
 
 
-def _compare(b, roots, parent=None):
+def _compare(b, roots, parent=None, parent_eval=False):
     root, schema = lower_query(b, roots)
     cols = list(schema.columns)
     if not cols:
         return 0
     widths = [schema.columns[c].width for c in cols]
-    want = build_guide(b, root, schema, cols, parent).arrays()
+    want = build_guide(b, root, schema, cols, parent, parent_eval=parent_eval).arrays()
     ts = local_tapeset(b, [root], cols)
     index = {c: i for i, c in enumerate(cols)}
     par = [(index[k], v) for k, v in (parent or {}).items() if k in index]
-    got = native.harvest_guide(ts.tapes[0].nodes, ts.pool.to_array(), widths, par)
+    got = native.harvest_guide(ts.tapes[0].nodes, ts.pool.to_array(), widths, par,
+                               parent_eval=parent_eval)
     for k in KEYS:
         assert got[k].dtype == want[k].dtype, k
         assert got[k].shape == want[k].shape, (k, got[k].shape, want[k].shape)
@@ -253,3 +254,46 @@ def test_interval_sets_propose_values_inside_every_bound():
     vals = sorted(a["9_calldatasize"] for a in last)
     assert vals == sorted(_interval_values(68, 4999)) and all(68 <= v <= 4999 for v in vals)
     _compare(ctx.b, [c.node for c in cs])
+
+
+def test_parent_eval_harvest_matches_python():
+    """mh_guide_harvest_inc (the incremental round's guide: operands the parent witness fixes
+    count as known) gives candidates.build_guide(parent_eval=True)'s arrays, on the LASER-shaped
+    queries and on planted random paths with their planted models as parents -- and there it
+    proposes alternatives the plain harvest cannot (x + y == k solved for x at y's parent value)."""
+    _lib_or_skip()
+    from tests.planted import planted_path
+
+    ctx, qs = laser_like.queries()
+    for name, cs in qs:
+        root, schema = lower_query(ctx.b, [c.node for c in cs])
+        cols = list(schema.columns)
+        widths = [schema.columns[c].width for c in cols]
+        _compare(ctx.b, [c.node for c in cs], _parent_of(cols, widths, name + "p"), True)
+    more = 0
+    for seed in range(6):
+        pctx, pcs, m, _ = planted_path("random", seed, 12)
+        nodes = [c.node for c in pcs]
+        for k in range(2, len(nodes) + 1, 3):
+            root, schema = lower_query(pctx.b, nodes[:k])
+            parent = {c: v for c, v in m.vars.items() if c in schema.columns}
+            a = _compare(pctx.b, nodes[:k], parent, True)
+            more += a > _compare(pctx.b, nodes[:k], parent, False)
+    assert more > 0
+
+
+def test_parent_eval_solves_a_sum_for_one_side():
+    from mythril_amd import smt
+    from mythril_amd.smt import symbol_factory as sf
+
+    _lib_or_skip()
+    ctx = smt.set_context(smt.Context())
+    x, y = sf.BitVecSym("x", 256), sf.BitVecSym("y", 256)
+    c = x + y == sf.BitVecVal(1000, 256)
+    root, schema = lower_query(ctx.b, [c.node])
+    cols = list(schema.columns)
+    plain = build_guide(ctx.b, root, schema, cols, {"y": 58}).arrays()
+    inc = build_guide(ctx.b, root, schema, cols, {"y": 58}, parent_eval=True).arrays()
+    vals = {int(v[0]) for v in inc["entry_val"]}
+    assert 942 in vals and 942 not in {int(v[0]) for v in plain["entry_val"]}
+    _compare(ctx.b, [c.node], {"y": 58}, True)

@@ -103,6 +103,10 @@ class Recorder:
         self._guide(b"G", s.value or 0, args)
         return self.lib.mh_guide_harvest_with(s, *args)
 
+    def mh_guide_harvest_inc(self, *args):
+        self._guide(b"i", 0, args)
+        return self.lib.mh_guide_harvest_inc(*args)
+
     def mh_guide_harvest(self, *args):
         self._guide(b"g", 0, args)
         return self.lib.mh_guide_harvest(*args)
@@ -199,12 +203,21 @@ def workload(n_random=40):
     # the random conjunctions in JUMPI order, on a session of that mode beside the default one
     from tests.planted import planted_path
 
+    from mythril_amd.sieve import newest_tape
+
     for seed in range(min(n_random, 8)):
-        ctx, cs, _, _ = planted_path("random", seed, 12)
+        ctx, cs, m, _ = planted_path("random", seed, 12)
         nodes = [c.node for c in cs]
         for k in range(1, len(nodes) + 1):
             host_query(ctx.b, nodes[:k], guides, rng)
             host_query(ctx.b, nodes[:k], guides, rng, keccak_reads=True)
+            # the incremental round's guide: the newest root's conjuncts, the planted model's
+            # values as the parent (mh_guide_harvest_inc)
+            cq = native.TermMirror.of(ctx.b).build(ctx.b, nodes[:k])
+            inc = newest_tape(cq.tapes[0], cq.parent_len) if cq.parent_len else None
+            if inc is not None:
+                par = [(i, m.vars[c]) for i, c in enumerate(cq.names) if c in m.vars]
+                native.harvest_guide(inc, cq.consts, cq.widths, par, parent_eval=True)
         done(ctx.b)
     for seed in range(min(n_random, 8)):
         ctx, cs = _random_query(random.Random(900 + seed), 8)
