@@ -47,6 +47,7 @@
 #             then path_scaling and sieve_queries at the default on the same box
 #   round3    planted_recall and path_scaling with a third round (the full guide's 2^16 rows after
 #             the incremental round, SIEVE_ROUND3=1), then path_scaling at the default
+#   peval     planted_recall without the parent-evaluating incremental guide (SIEVE_INC_PEVAL=0)
 #   recall0   planted_recall without the keccak second chance (SIEVE_KECCAK2=0), no extended pass
 #   round2    planted_recall and path_scaling with the second round gated on first-round progress
 #             (SIEVE_ROUND2=progress) and never run (recall only)
@@ -121,6 +122,7 @@ for step in "$@"; do
     round3)   SIEVE_ROUND3=1 timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_r3.jsonl" 2> "$OUT/planted_recall_r3.log" && \
               SIEVE_ROUND3=1 timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling_r3.jsonl" 2> "$OUT/path_scaling_r3.log" && \
               timeout -k 10 600 python -u scripts/path_scaling.py > "$OUT/path_scaling.jsonl" 2> "$OUT/path_scaling.log" ;;
+    peval)    SIEVE_INC_PEVAL=0 timeout -k 10 600 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_nopeval.jsonl" 2> "$OUT/planted_recall_nopeval.log" ;;
     recall0)  SIEVE_KECCAK2=0 timeout -k 10 900 python -u scripts/planted_recall.py 100 24 > "$OUT/planted_recall_nok2.jsonl" 2> "$OUT/planted_recall_nok2.log" ;;
     round2)   timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=progress > "$OUT/planted_recall_progress.jsonl" 2> "$OUT/planted_recall_progress.log" && \
               timeout -k 10 600 python -u scripts/planted_recall.py 100 24 --round2=never > "$OUT/planted_recall_never.jsonl" 2> "$OUT/planted_recall_never.log" && \
