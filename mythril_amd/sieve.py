@@ -469,9 +469,11 @@ class Sieve:
         # latency unchanged (profiles/r06s)
         self.inc_rows = int(os.environ.get("SIEVE_INC_ROWS", "16384"))
         self.inc_hops = int(os.environ.get("SIEVE_INC_HOPS", "0"))  # newest_tape(hops)
-        # its guide solves for one side of x op y == k with the other at the parent's value
-        # (mh_guide_harvest_inc; SIEVE_INC_PEVAL=0: the plain harvest)
-        self.inc_parent_eval = os.environ.get("SIEVE_INC_PEVAL", "1") != "0"
+        # its guide solving for one side of x op y == k with the other at the parent's value
+        # (mh_guide_harvest_inc, SIEVE_INC_PEVAL=1): measured, not kept -- random recall 0.6686
+        # -> 0.6625, learnt 0.9183 -> 0.9107 (profiles/r06v): its extra sets override the
+        # parent's values in more rows than they complete
+        self.inc_parent_eval = os.environ.get("SIEVE_INC_PEVAL", "0") == "1"
         # after the incremental round, the 2^16-row round of the full guide (SIEVE_ROUND3=1)
         self.round3 = os.environ.get("SIEVE_ROUND3", "0") == "1"
         # the last solve's rounds (diagnostics: scripts/planted_recall.py)
