@@ -33,6 +33,18 @@ def test_library_exports_every_symbol():
         assert C.cast(getattr(lib, name), C.c_void_p).value
 
 
+def test_noasm_library_is_current():
+    """The C++ step() build (libmythril_hip_noasm.so, tests/noasm_check.py on the GPU) exports the
+    same ABI: a stale copy failed the GPU suite once (r06w), so `make` now builds both."""
+    path = os.path.join(os.path.dirname(os.path.abspath(native.__file__)),
+                        "libmythril_hip_noasm.so")
+    if not os.path.exists(path):
+        pytest.skip("noasm library not built")
+    lib = C.CDLL(path)
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+
+
 def test_version_and_errors_without_device():
     assert native.version() == (0, 1, 0)
     assert native.device_count() == 0 or native.device_count() >= 1
